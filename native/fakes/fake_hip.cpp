@@ -1,0 +1,248 @@
+// Fake HIP runtime (SONAME libamdhip64.so.7, symbol versions copied from the
+// real library at build time) for CPU-only tests of the enforcement library.
+//
+// Device memory is a bump allocator over a fake address space (nothing is
+// actually allocated, so a 288 GB device costs no host RAM).  Like the real
+// CLR, the first API call creates one HSA queue per device through
+// hsa_queue_create — resolved through the global scope, i.e. through the
+// preloaded libvgpu.so hook, exactly as in a PyTorch process.
+//
+// Fixture env: VGPU_FAKE_GPUS (1), VGPU_FAKE_MEM (bytes, default 288 GiB),
+// VGPU_FAKE_CUS (256).
+#include <hip/hip_runtime_api.h>
+#include <dlfcn.h>
+#include <hsa/hsa.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <map>
+#include <mutex>
+#include <vector>
+
+namespace {
+
+struct Dev {
+  uint64_t total = 0;
+  uint64_t used = 0;
+  hsa_queue_t* queue = nullptr;
+};
+
+std::mutex g_mu;
+std::vector<Dev> g_devs;
+std::map<uintptr_t, std::pair<int, uint64_t>> g_allocs;  // ptr -> (dev, size)
+uintptr_t g_next = 0x7f0000000000ull;
+thread_local int tl_dev = 0;
+std::atomic<uint64_t> g_launches{0};
+std::atomic<uint64_t> g_launch_blocks{0};
+std::atomic<uint64_t> g_graph_launches{0};
+bool g_inited = false;
+
+int env_int(const char* n, int d) {
+  const char* v = getenv(n);
+  return v && *v ? atoi(v) : d;
+}
+
+hsa_status_t pick_gpu(hsa_agent_t a, void* data) {
+  auto* v = (std::vector<hsa_agent_t>*)data;
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS &&
+      t == HSA_DEVICE_TYPE_GPU)
+    v->push_back(a);
+  return HSA_STATUS_SUCCESS;
+}
+
+void init_locked() {
+  if (g_inited) return;
+  g_inited = true;
+  int n = env_int("VGPU_FAKE_GPUS", 1);
+  const char* m = getenv("VGPU_FAKE_MEM");
+  uint64_t mem = m ? strtoull(m, nullptr, 10) : (288ull << 30);
+  g_devs.assign(n, Dev{});
+  std::vector<hsa_agent_t> gpus;
+  hsa_iterate_agents(pick_gpu, &gpus);
+  for (int i = 0; i < n; ++i) {
+    g_devs[i].total = mem;
+    if (i < (int)gpus.size())
+      hsa_queue_create(gpus[i], 4096, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, 0, 0,
+                       &g_devs[i].queue);
+  }
+}
+
+void init() {
+  std::lock_guard<std::mutex> g(g_mu);
+  init_locked();
+}
+
+hipError_t dev_alloc(void** p, size_t size, int dev) {
+  std::lock_guard<std::mutex> g(g_mu);
+  init_locked();
+  if (dev < 0 || dev >= (int)g_devs.size()) return hipErrorInvalidDevice;
+  if (g_devs[dev].used + size > g_devs[dev].total) return hipErrorOutOfMemory;
+  g_devs[dev].used += size;
+  uintptr_t a = g_next;
+  g_next += ((size + 4095) / 4096) * 4096 + 4096;
+  g_allocs[a] = {dev, size};
+  *p = (void*)a;
+  return hipSuccess;
+}
+
+hipError_t dev_free(void* p) {
+  if (!p) return hipSuccess;
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_allocs.find((uintptr_t)p);
+  if (it == g_allocs.end()) return hipErrorInvalidValue;
+  g_devs[it->second.first].used -= it->second.second;
+  g_allocs.erase(it);
+  return hipSuccess;
+}
+
+void count_launch(uint64_t blocks) {
+  init();
+  g_launches.fetch_add(1);
+  g_launch_blocks.fetch_add(blocks);
+}
+
+}  // namespace
+
+extern "C" {
+
+hipError_t hipInit(unsigned int) { init(); return hipSuccess; }
+hipError_t hipSetDevice(int d) {
+  init();
+  if (d < 0 || d >= (int)g_devs.size()) return hipErrorInvalidDevice;
+  tl_dev = d;
+  return hipSuccess;
+}
+hipError_t hipGetDevice(int* d) { *d = tl_dev; return hipSuccess; }
+hipError_t hipGetDeviceCount(int* n) { init(); *n = (int)g_devs.size(); return hipSuccess; }
+hipError_t hipGetLastError() { return hipSuccess; }
+hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipDeviceSynchronize() { return hipSuccess; }
+
+hipError_t hipMalloc(void** p, size_t size) { return dev_alloc(p, size, tl_dev); }
+hipError_t hipExtMallocWithFlags(void** p, size_t size, unsigned int) { return dev_alloc(p, size, tl_dev); }
+hipError_t hipMallocAsync(void** p, size_t size, hipStream_t) { return dev_alloc(p, size, tl_dev); }
+hipError_t hipMallocFromPoolAsync(void** p, size_t size, hipMemPool_t, hipStream_t) {
+  return dev_alloc(p, size, tl_dev);
+}
+hipError_t hipMallocManaged(void** p, size_t size, unsigned int) { return dev_alloc(p, size, tl_dev); }
+hipError_t hipMallocPitch(void** p, size_t* pitch, size_t w, size_t h) {
+  *pitch = ((w + 511) / 512) * 512;
+  return dev_alloc(p, *pitch * h, tl_dev);
+}
+hipError_t hipFree(void* p) { return dev_free(p); }
+hipError_t hipFreeAsync(void* p, hipStream_t) { return dev_free(p); }
+
+hipError_t hipHostMalloc(void** p, size_t size, unsigned int) {
+  // Host memory: a fake address too (tests allocate hundreds of GB virtually).
+  std::lock_guard<std::mutex> g(g_mu);
+  uintptr_t a = g_next | (1ull << 46);
+  g_next += ((size + 4095) / 4096) * 4096 + 4096;
+  *p = (void*)a;
+  return hipSuccess;
+}
+hipError_t hipHostFree(void*) { return hipSuccess; }
+
+hipError_t hipMemCreate(hipMemGenericAllocationHandle_t* h, size_t size,
+                        const hipMemAllocationProp* prop, unsigned long long) {
+  void* p = nullptr;
+  hipError_t rc = dev_alloc(&p, size, prop ? prop->location.id : tl_dev);
+  *h = (hipMemGenericAllocationHandle_t)p;
+  return rc;
+}
+hipError_t hipMemRelease(hipMemGenericAllocationHandle_t h) { return dev_free((void*)h); }
+
+hipError_t hipMemGetInfo(size_t* f, size_t* t) {
+  std::lock_guard<std::mutex> g(g_mu);
+  init_locked();
+  Dev& d = g_devs[tl_dev];
+  *f = d.total - d.used;
+  *t = d.total;
+  return hipSuccess;
+}
+hipError_t hipDeviceTotalMem(size_t* b, hipDevice_t dev) {
+  init();
+  *b = g_devs[dev].total;
+  return hipSuccess;
+}
+hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_tR0600* p, int dev) {
+  init();
+  memset(p, 0, sizeof(*p));
+  snprintf(p->name, sizeof(p->name), "AMD Instinct MI355X (fake)");
+  snprintf(p->gcnArchName, sizeof(p->gcnArchName), "gfx950:sramecc+:xnack-");
+  p->totalGlobalMem = g_devs[dev].total;
+  p->multiProcessorCount = env_int("VGPU_FAKE_CUS", 256);
+  p->warpSize = 64;
+  return hipSuccess;
+}
+hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t a, int) {
+  init();
+  if (a == hipDeviceAttributeMultiprocessorCount) { *v = env_int("VGPU_FAKE_CUS", 256); return hipSuccess; }
+  *v = 0;
+  return hipSuccess;
+}
+hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int* n, const void*, int, size_t) {
+  *n = 8;
+  return hipSuccess;
+}
+
+hipError_t hipLaunchKernel(const void*, dim3 g, dim3, void**, size_t, hipStream_t) {
+  count_launch((uint64_t)g.x * g.y * g.z);
+  return hipSuccess;
+}
+hipError_t hipExtLaunchKernel(const void*, dim3 g, dim3, void**, size_t, hipStream_t, hipEvent_t,
+                              hipEvent_t, int) {
+  count_launch((uint64_t)g.x * g.y * g.z);
+  return hipSuccess;
+}
+hipError_t hipModuleLaunchKernel(hipFunction_t, unsigned gx, unsigned gy, unsigned gz, unsigned,
+                                 unsigned, unsigned, unsigned, hipStream_t, void**, void**) {
+  count_launch((uint64_t)gx * gy * gz);
+  return hipSuccess;
+}
+hipError_t hipExtModuleLaunchKernel(hipFunction_t, uint32_t gx, uint32_t gy, uint32_t gz,
+                                    uint32_t lx, uint32_t ly, uint32_t lz, size_t, hipStream_t,
+                                    void**, void**, hipEvent_t, hipEvent_t, uint32_t) {
+  count_launch((uint64_t)(gx / (lx ? lx : 1)) * (gy / (ly ? ly : 1)) * (gz / (lz ? lz : 1)));
+  return hipSuccess;
+}
+hipError_t hipLaunchCooperativeKernel(const void*, dim3 g, dim3, void**, unsigned int, hipStream_t) {
+  count_launch((uint64_t)g.x * g.y * g.z);
+  return hipSuccess;
+}
+hipError_t hipModuleLaunchCooperativeKernel(hipFunction_t, unsigned gx, unsigned gy, unsigned gz,
+                                            unsigned, unsigned, unsigned, unsigned, hipStream_t,
+                                            void**) {
+  count_launch((uint64_t)gx * gy * gz);
+  return hipSuccess;
+}
+hipError_t hipLaunchKernelExC(const hipLaunchConfig_t* c, const void*, void**) {
+  count_launch((uint64_t)c->gridDim.x * c->gridDim.y * c->gridDim.z);
+  return hipSuccess;
+}
+hipError_t hipGraphLaunch(hipGraphExec_t, hipStream_t) {
+  init();
+  g_graph_launches.fetch_add(1);
+  g_launches.fetch_add(1);
+  return hipSuccess;
+}
+hipError_t hipGetProcAddress(const char* sym, void** pfn, int, uint64_t,
+                             hipDriverProcAddressQueryResult* st) {
+  // Answer from this library only (the real runtime returns its own entry points).
+  static void* self = dlopen("libamdhip64.so.7", RTLD_NOLOAD | RTLD_LAZY);
+  *pfn = self ? dlsym(self, sym) : nullptr;
+  if (st) *st = *pfn ? HIP_GET_PROC_ADDRESS_SUCCESS : HIP_GET_PROC_ADDRESS_SYMBOL_NOT_FOUND;
+  return *pfn ? hipSuccess : hipErrorNotFound;
+}
+
+// ---- test introspection ----
+uint64_t fake_hip_launches() { return g_launches.load(); }
+uint64_t fake_hip_launch_blocks() { return g_launch_blocks.load(); }
+uint64_t fake_hip_physical_used(int dev) {
+  std::lock_guard<std::mutex> g(g_mu);
+  return dev < (int)g_devs.size() ? g_devs[dev].used : 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,145 @@
+// C ABI exported for Python (ctypes): the node monitor attaches to container
+// regions through these entry points so every structural write happens under
+// the same robust lock the shim uses (the reference monitor writes the mmap
+// with no lock at all: cmd/vGPUmonitor/feedback.go:208,231,244).
+#include <signal.h>
+
+#include "common.h"
+#include "state.h"
+
+using namespace vgpu;
+
+extern "C" {
+
+__attribute__((visibility("default"))) void vgpu_region_layout(vgpu_region_layout_t* out) {
+  region_fill_layout(out);
+}
+
+__attribute__((visibility("default"))) uint32_t vgpu_region_version() { return VGPU_REGION_VERSION; }
+
+// Create (or attach to and refresh) a region using the limits in the current
+// environment.  Returns the mapping or NULL.
+__attribute__((visibility("default"))) void* vgpu_region_create(const char* path) {
+  DeviceLimits lim = limits_from_env();
+  int fd = -1;
+  void* r = region_map(path, &lim, &fd);
+  if (fd >= 0) close(fd);  // the mapping stays valid after close
+  return r;
+}
+
+// Attach to an existing, initialised region without modifying it.
+__attribute__((visibility("default"))) void* vgpu_region_attach(const char* path) {
+  int fd = -1;
+  void* r = region_map(path, nullptr, &fd);
+  if (fd >= 0) close(fd);
+  return r;
+}
+
+__attribute__((visibility("default"))) void vgpu_region_detach(void* r) {
+  region_unmap((vgpu_shared_region_t*)r, -1);
+}
+
+__attribute__((visibility("default"))) int vgpu_region_lock(void* r) {
+  return region_lock((vgpu_shared_region_t*)r);
+}
+
+__attribute__((visibility("default"))) void vgpu_region_unlock(void* r) {
+  region_unlock((vgpu_shared_region_t*)r);
+}
+
+__attribute__((visibility("default"))) int vgpu_region_purge(void* r, int host_ns) {
+  return region_purge_dead((vgpu_shared_region_t*)r, host_ns != 0);
+}
+
+__attribute__((visibility("default"))) int vgpu_region_claim(void* r, int pid, int host_pid, int prio) {
+  return region_claim_slot((vgpu_shared_region_t*)r, pid, host_pid, prio);
+}
+
+__attribute__((visibility("default"))) void vgpu_region_release(void* r, int slot) {
+  region_release_slot((vgpu_shared_region_t*)r, slot);
+}
+
+__attribute__((visibility("default"))) uint64_t vgpu_region_device_used(void* r, int dev) {
+  return region_device_used((vgpu_shared_region_t*)r, dev);
+}
+
+// Feedback words (monitor → shim).  Negative values are left unchanged.
+__attribute__((visibility("default"))) void vgpu_region_set_feedback(void* rp, int recent_kernel,
+                                                                     int utilization_switch,
+                                                                     int set_recent) {
+  auto* r = (vgpu_shared_region_t*)rp;
+  if (set_recent) __atomic_store_n(&r->recent_kernel, recent_kernel, __ATOMIC_RELAXED);
+  if (utilization_switch >= 0)
+    __atomic_store_n(&r->utilization_switch, utilization_switch, __ATOMIC_RELAXED);
+  __atomic_fetch_add(&r->monitor_seq, 1, __ATOMIC_RELAXED);
+}
+
+// Decrement recent_kernel if positive; returns the new value.
+__attribute__((visibility("default"))) int vgpu_region_decay_recent(void* rp) {
+  auto* r = (vgpu_shared_region_t*)rp;
+  int cur = __atomic_load_n(&r->recent_kernel, __ATOMIC_RELAXED);
+  while (cur > 0 && !__atomic_compare_exchange_n(&r->recent_kernel, &cur, cur - 1, true,
+                                                  __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+  }
+  return cur > 0 ? cur - 1 : cur;
+}
+
+// Elastic CU resizing: install a new mask for `dev` (words little-endian).
+__attribute__((visibility("default"))) int vgpu_region_set_cu_mask(void* rp, int dev,
+                                                                   const uint64_t* words) {
+  auto* r = (vgpu_shared_region_t*)rp;
+  if (dev < 0 || dev >= VGPU_MAX_DEVICES) return -1;
+  if (region_lock(r) != 0) return -1;
+  for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w)
+    __atomic_store_n(&r->dev[dev].cu_mask[w], words[w], __ATOMIC_RELAXED);
+  region_unlock(r);
+  return 0;
+}
+
+// Signal every live process of the region (suspend_all / resume_all analogue).
+__attribute__((visibility("default"))) int vgpu_region_signal_all(void* rp, int sig, int host_ns) {
+  auto* r = (vgpu_shared_region_t*)rp;
+  int n = 0;
+  if (region_lock(r) != 0) return -1;
+  for (int i = 0; i < VGPU_MAX_PROCS; ++i) {
+    const vgpu_proc_slot_t& s = r->procs[i];
+    if (s.status == VGPU_PROC_FREE) continue;
+    int pid = host_ns ? s.host_pid : s.pid;
+    if (pid > 0 && kill(pid, sig) == 0) ++n;
+  }
+  region_unlock(r);
+  return n;
+}
+
+__attribute__((visibility("default"))) uint64_t vgpu_parse_mem(const char* s) { return parse_mem(s); }
+
+__attribute__((visibility("default"))) int vgpu_parse_cu_mask(const char* s, uint64_t* out, int words) {
+  return parse_cu_mask(s, out, words);
+}
+
+// In-process introspection for tests running under the preload.
+__attribute__((visibility("default"))) void* vgpu_self_region() {
+  ensure_init();
+  return st().region;
+}
+__attribute__((visibility("default"))) int vgpu_self_slot() {
+  ensure_init();
+  return st().slot;
+}
+__attribute__((visibility("default"))) int vgpu_self_enabled() {
+  ensure_init();
+  return st().enabled ? 1 : 0;
+}
+__attribute__((visibility("default"))) int vgpu_self_reserve(int dev, uint64_t size) {
+  ensure_init();
+  return mem_reserve(dev, size, kDeviceBuf) ? 1 : 0;
+}
+__attribute__((visibility("default"))) void vgpu_self_unreserve(int dev, uint64_t size) {
+  mem_unreserve(dev, size, kDeviceBuf);
+}
+__attribute__((visibility("default"))) void vgpu_self_on_launch(int dev, uint64_t wg) {
+  ensure_init();
+  limiter_on_launch(dev, wg);
+}
+
+}  // extern "C"

@@ -1,0 +1,359 @@
+// HIP runtime interposers (LD_PRELOAD / /etc/ld.so.preload).
+//
+// Reference parity: the CUDA driver hooks in libvgpu.so
+// cover every allocation path (cuMemAlloc_v2, cuMemAllocManaged,
+// cuMemAllocPitch_v2, cuMemAllocAsync, cuMemAllocFromPoolAsync, cuMemCreate,
+// cuMemFree_v2), the memory info queries (cuMemGetInfo_v2, cuDeviceTotalMem_v2,
+// cuDeviceGetAttribute) and the launch paths (cuLaunchKernel,
+// cuLaunchCooperativeKernel).  The HIP surface below is the one PyTorch-ROCm,
+// MIOpen, rocBLAS, hipBLASLt and RCCL actually import (nm -D of torch/lib).
+//
+// Every hook: (1) lazily initialises, (2) passes straight through when
+// control is disabled, (3) keeps the fast path to a couple of relaxed atomics.
+#include <algorithm>
+
+#include "common.h"
+#include "real.h"
+#include "state.h"
+
+using namespace vgpu;
+
+namespace {
+
+inline int cur_dev() { return tl_device; }
+
+inline uint64_t blocks3(unsigned x, unsigned y, unsigned z) {
+  return (uint64_t)(x ? x : 1) * (y ? y : 1) * (z ? z : 1);
+}
+
+// Shared allocation path: reserve → real alloc → record (or unreserve).
+template <class F>
+hipError_t charged_alloc(void** ptr, size_t size, int kind, F&& real_alloc) {
+  ensure_init();
+  State& s = st();
+  if (!s.enabled || size == 0) return real_alloc();
+  suspend_gate();
+  int dev = cur_dev();
+  charge_context(dev);
+  if (!mem_reserve(dev, size, kind)) return hipErrorOutOfMemory;
+  hipError_t rc = real_alloc();
+  if (rc == hipErrorOutOfMemory && kind == kDeviceBuf && s.region && s.region->oversubscribe) {
+    // Virtual device memory: HBM is physically exhausted but the container's
+    // (scaled) limit still has room — back the allocation with pinned,
+    // device-mapped host memory.  The pager (vgpu/ops/pager.py) migrates hot
+    // chunks back into HBM.
+    (void)REAL_HIP(hipGetLastError)();
+    mem_unreserve(dev, size, kind);
+    mem_reserve(dev, size, kHostSpill);
+    rc = REAL_HIP(hipHostMalloc)(ptr, size, hipHostMallocDefault);
+    if (rc == hipSuccess) {
+      ledger_add(*ptr, size, dev, kHostSpill);
+      VLOG_INFO("device %d: %zu bytes oversubscribed to host memory at %p", dev, size, *ptr);
+      return rc;
+    }
+    mem_unreserve(dev, size, kHostSpill);
+    return hipErrorOutOfMemory;
+  }
+  if (rc != hipSuccess) {
+    mem_unreserve(dev, size, kind);
+    return rc;
+  }
+  ledger_add(*ptr, size, dev, kind);
+  return rc;
+}
+
+bool uncharge(void* p, Alloc* a) {
+  if (!p) return false;
+  if (!ledger_take(p, a)) return false;
+  mem_unreserve(a->dev, a->size, a->kind);
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+__attribute__((visibility("default"))) hipError_t hipSetDevice(int deviceId) {
+  hipError_t rc = REAL_HIP(hipSetDevice)(deviceId);
+  if (rc == hipSuccess) tl_device = deviceId;
+  return rc;
+}
+
+// ---- allocation ------------------------------------------------------------------
+__attribute__((visibility("default"))) hipError_t hipMalloc(void** ptr, size_t size) {
+  return charged_alloc(ptr, size, kDeviceBuf, [&] { return REAL_HIP(hipMalloc)(ptr, size); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipExtMallocWithFlags(void** ptr, size_t size,
+                                                                        unsigned int flags) {
+  return charged_alloc(ptr, size, kDeviceBuf,
+                       [&] { return REAL_HIP(hipExtMallocWithFlags)(ptr, size, flags); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipMallocAsync(void** ptr, size_t size,
+                                                                 hipStream_t stream) {
+  return charged_alloc(ptr, size, kDeviceBuf,
+                       [&] { return REAL_HIP(hipMallocAsync)(ptr, size, stream); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipMallocFromPoolAsync(void** ptr, size_t size,
+                                                                         hipMemPool_t pool,
+                                                                         hipStream_t stream) {
+  return charged_alloc(ptr, size, kDeviceBuf, [&] {
+    return REAL_HIP(hipMallocFromPoolAsync)(ptr, size, pool, stream);
+  });
+}
+
+__attribute__((visibility("default"))) hipError_t hipMallocManaged(void** ptr, size_t size,
+                                                                   unsigned int flags) {
+  return charged_alloc(ptr, size, kManaged,
+                       [&] { return REAL_HIP(hipMallocManaged)(ptr, size, flags); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipMallocPitch(void** ptr, size_t* pitch,
+                                                                 size_t width, size_t height) {
+  // Pitch is chosen by the runtime; charge the conservative upper bound
+  // (width rounded to 256 B rows) then correct to the real pitch.
+  size_t est = ((width + 255) / 256) * 256 * height;
+  hipError_t rc = charged_alloc(ptr, est, kDeviceBuf,
+                                [&] { return REAL_HIP(hipMallocPitch)(ptr, pitch, width, height); });
+  if (rc == hipSuccess && pitch && *pitch * height != est) {
+    Alloc a;
+    if (ledger_take(*ptr, &a)) {
+      mem_unreserve(a.dev, a.size, a.kind);
+      size_t real = *pitch * height;
+      mem_reserve(a.dev, real, a.kind);  // may exceed by < one row per call; accepted
+      ledger_add(*ptr, real, a.dev, a.kind);
+    }
+  }
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipFree(void* ptr) {
+  ensure_init();
+  Alloc a;
+  if (uncharge(ptr, &a) && a.kind == kHostSpill) return REAL_HIP(hipHostFree)(ptr);
+  return REAL_HIP(hipFree)(ptr);
+}
+
+__attribute__((visibility("default"))) hipError_t hipFreeAsync(void* ptr, hipStream_t stream) {
+  ensure_init();
+  Alloc a;
+  if (uncharge(ptr, &a) && a.kind == kHostSpill) {
+    (void)REAL_HIP(hipStreamSynchronize)(stream);
+    return REAL_HIP(hipHostFree)(ptr);
+  }
+  return REAL_HIP(hipFreeAsync)(ptr, stream);
+}
+
+// Virtual memory management (PyTorch expandable segments): charge physical
+// handles, not VA reservations.
+__attribute__((visibility("default"))) hipError_t hipMemCreate(
+    hipMemGenericAllocationHandle_t* handle, size_t size, const hipMemAllocationProp* prop,
+    unsigned long long flags) {
+  ensure_init();
+  State& s = st();
+  if (!s.enabled || !prop || prop->location.type != hipMemLocationTypeDevice)
+    return REAL_HIP(hipMemCreate)(handle, size, prop, flags);
+  int dev = prop->location.id;
+  charge_context(dev);
+  if (!mem_reserve(dev, size, kVmmHandle)) return hipErrorOutOfMemory;
+  hipError_t rc = REAL_HIP(hipMemCreate)(handle, size, prop, flags);
+  if (rc != hipSuccess) {
+    mem_unreserve(dev, size, kVmmHandle);
+    return rc;
+  }
+  ledger_add((void*)*handle, size, dev, kVmmHandle);
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemRelease(
+    hipMemGenericAllocationHandle_t handle) {
+  ensure_init();
+  Alloc a;
+  uncharge((void*)handle, &a);
+  return REAL_HIP(hipMemRelease)(handle);
+}
+
+// ---- memory info ---------------------------------------------------------------
+__attribute__((visibility("default"))) hipError_t hipMemGetInfo(size_t* free_b, size_t* total_b) {
+  ensure_init();
+  hipError_t rc = REAL_HIP(hipMemGetInfo)(free_b, total_b);
+  if (rc != hipSuccess) return rc;
+  int dev = cur_dev();
+  uint64_t lim = mem_limit(dev);
+  if (lim == 0) return rc;
+  State& s = st();
+  uint64_t used = mem_used(dev);
+  uint64_t vfree = used >= lim ? 0 : lim - used;
+  bool over = s.region && s.region->oversubscribe;
+  if (free_b) *free_b = over ? vfree : std::min<uint64_t>(vfree, *free_b);
+  if (total_b) *total_b = over ? lim : std::min<uint64_t>(lim, *total_b);
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipDeviceTotalMem(size_t* bytes, hipDevice_t device) {
+  ensure_init();
+  hipError_t rc = REAL_HIP(hipDeviceTotalMem)(bytes, device);
+  if (rc != hipSuccess || !bytes) return rc;
+  uint64_t lim = mem_limit(device);
+  State& s = st();
+  if (lim) *bytes = (s.region && s.region->oversubscribe) ? lim : std::min<uint64_t>(lim, *bytes);
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipGetDevicePropertiesR0600(
+    hipDeviceProp_tR0600* prop, int device) {
+  ensure_init();
+  hipError_t rc = REAL_HIP(hipGetDevicePropertiesR0600)(prop, device);
+  if (rc != hipSuccess || !prop) return rc;
+  State& s = st();
+  uint64_t lim = mem_limit(device);
+  if (lim)
+    prop->totalGlobalMem = (s.region && s.region->oversubscribe)
+                               ? lim
+                               : std::min<uint64_t>(lim, prop->totalGlobalMem);
+  if (s.enabled && s.report_masked_cus)
+    prop->multiProcessorCount = cu_count_masked(device, prop->multiProcessorCount);
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipDeviceGetAttribute(int* pi,
+                                                                        hipDeviceAttribute_t attr,
+                                                                        int device) {
+  ensure_init();
+  hipError_t rc = REAL_HIP(hipDeviceGetAttribute)(pi, attr, device);
+  if (rc != hipSuccess || !pi) return rc;
+  State& s = st();
+  if (s.enabled && s.report_masked_cus && attr == hipDeviceAttributeMultiprocessorCount)
+    *pi = cu_count_masked(device, *pi);
+  return rc;
+}
+
+// ---- dispatch -----------------------------------------------------------------------
+__attribute__((visibility("default"))) hipError_t hipLaunchKernel(const void* f, dim3 grid, dim3 block,
+                                                                  void** args, size_t shmem,
+                                                                  hipStream_t stream) {
+  ensure_init();
+  limiter_on_launch(cur_dev(), blocks3(grid.x, grid.y, grid.z));
+  return REAL_HIP(hipLaunchKernel)(f, grid, block, args, shmem, stream);
+}
+
+__attribute__((visibility("default"))) hipError_t hipExtLaunchKernel(const void* f, dim3 grid,
+                                                                     dim3 block, void** args,
+                                                                     size_t shmem, hipStream_t stream,
+                                                                     hipEvent_t start, hipEvent_t stop,
+                                                                     int flags) {
+  ensure_init();
+  limiter_on_launch(cur_dev(), blocks3(grid.x, grid.y, grid.z));
+  return REAL_HIP(hipExtLaunchKernel)(f, grid, block, args, shmem, stream, start, stop, flags);
+}
+
+__attribute__((visibility("default"))) hipError_t hipModuleLaunchKernel(
+    hipFunction_t f, unsigned int gx, unsigned int gy, unsigned int gz, unsigned int bx,
+    unsigned int by, unsigned int bz, unsigned int shmem, hipStream_t stream, void** params,
+    void** extra) {
+  ensure_init();
+  limiter_on_launch(cur_dev(), blocks3(gx, gy, gz));
+  return REAL_HIP(hipModuleLaunchKernel)(f, gx, gy, gz, bx, by, bz, shmem, stream, params, extra);
+}
+
+__attribute__((visibility("default"))) hipError_t hipExtModuleLaunchKernel(
+    hipFunction_t f, uint32_t gwx, uint32_t gwy, uint32_t gwz, uint32_t lwx, uint32_t lwy,
+    uint32_t lwz, size_t shmem, hipStream_t stream, void** params, void** extra, hipEvent_t start,
+    hipEvent_t stop, uint32_t flags) {
+  ensure_init();
+  // Global work size is in work-items here.
+  auto nb = [](uint32_t g, uint32_t l) { return l ? (g + l - 1) / l : g; };
+  limiter_on_launch(cur_dev(), blocks3(nb(gwx, lwx), nb(gwy, lwy), nb(gwz, lwz)));
+  return REAL_HIP(hipExtModuleLaunchKernel)(f, gwx, gwy, gwz, lwx, lwy, lwz, shmem, stream, params,
+                                            extra, start, stop, flags);
+}
+
+static hipError_t cooperative_guard(const void* f, dim3 grid, dim3 block, size_t shmem) {
+  // A cooperative grid sized for all 256 CUs cannot be co-resident on a
+  // masked subset; refuse it (as the runtime would for an oversized grid)
+  // instead of deadlocking at the first grid barrier.
+  State& s = st();
+  if (!s.enabled) return hipSuccess;
+  int dev = cur_dev();
+  int phys = 0;
+  if (REAL_HIP(hipDeviceGetAttribute)(&phys, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return hipSuccess;
+  int cus = cu_count_masked(dev, phys);
+  if (cus >= phys) return hipSuccess;
+  int per = 0;
+  if (f && REAL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor)(
+               &per, f, (int)(block.x * block.y * block.z), shmem) != hipSuccess)
+    return hipSuccess;
+  uint64_t nblk = blocks3(grid.x, grid.y, grid.z);
+  if (per > 0 && nblk > (uint64_t)per * cus) {
+    VLOG_WARN("cooperative launch of %llu blocks exceeds %d masked CUs x %d blocks/CU",
+              (unsigned long long)nblk, cus, per);
+    return hipErrorCooperativeLaunchTooLarge;
+  }
+  return hipSuccess;
+}
+
+__attribute__((visibility("default"))) hipError_t hipLaunchCooperativeKernel(const void* f, dim3 grid,
+                                                                             dim3 block, void** params,
+                                                                             unsigned int shmem,
+                                                                             hipStream_t stream) {
+  ensure_init();
+  hipError_t g = cooperative_guard(f, grid, block, shmem);
+  if (g != hipSuccess) return g;
+  limiter_on_launch(cur_dev(), blocks3(grid.x, grid.y, grid.z));
+  return REAL_HIP(hipLaunchCooperativeKernel)(f, grid, block, params, shmem, stream);
+}
+
+__attribute__((visibility("default"))) hipError_t hipModuleLaunchCooperativeKernel(
+    hipFunction_t f, unsigned int gx, unsigned int gy, unsigned int gz, unsigned int bx,
+    unsigned int by, unsigned int bz, unsigned int shmem, hipStream_t stream, void** params) {
+  ensure_init();
+  limiter_on_launch(cur_dev(), blocks3(gx, gy, gz));
+  return REAL_HIP(hipModuleLaunchCooperativeKernel)(f, gx, gy, gz, bx, by, bz, shmem, stream, params);
+}
+
+__attribute__((visibility("default"))) hipError_t hipLaunchKernelExC(const hipLaunchConfig_t* cfg,
+                                                                     const void* f, void** args) {
+  ensure_init();
+  if (cfg) limiter_on_launch(cur_dev(), blocks3(cfg->gridDim.x, cfg->gridDim.y, cfg->gridDim.z));
+  return REAL_HIP(hipLaunchKernelExC)(cfg, f, args);
+}
+
+__attribute__((visibility("default"))) hipError_t hipGraphLaunch(hipGraphExec_t exec, hipStream_t stream) {
+  ensure_init();
+  static uint64_t graph_tokens = [] {
+    const char* v = getenv("VGPU_GRAPH_LAUNCH_TOKENS");
+    return v ? strtoull(v, nullptr, 10) : 4096ull;
+  }();
+  limiter_on_launch(cur_dev(), graph_tokens);
+  return REAL_HIP(hipGraphLaunch)(exec, stream);
+}
+
+// hipGetProcAddress must hand out our hooks too, or a runtime-resolved call
+// would bypass the ledger.
+__attribute__((visibility("default"))) hipError_t hipGetProcAddress(const char* symbol, void** pfn,
+                                                                    int hipVersion, uint64_t flags,
+                                                                    hipDriverProcAddressQueryResult* status) {
+  hipError_t rc = REAL_HIP(hipGetProcAddress)(symbol, pfn, hipVersion, flags, status);
+  if (rc != hipSuccess || !symbol || !pfn || !*pfn) return rc;
+  static const char* hooked[] = {
+      "hipSetDevice", "hipMalloc", "hipExtMallocWithFlags", "hipMallocAsync",
+      "hipMallocFromPoolAsync", "hipMallocManaged", "hipMallocPitch", "hipFree", "hipFreeAsync",
+      "hipMemCreate", "hipMemRelease", "hipMemGetInfo", "hipDeviceTotalMem",
+      "hipGetDevicePropertiesR0600", "hipDeviceGetAttribute", "hipLaunchKernel",
+      "hipExtLaunchKernel", "hipModuleLaunchKernel", "hipExtModuleLaunchKernel",
+      "hipLaunchCooperativeKernel", "hipModuleLaunchCooperativeKernel", "hipLaunchKernelExC",
+      "hipGraphLaunch", nullptr};
+  for (const char** h = hooked; *h; ++h) {
+    if (!strcmp(symbol, *h)) {
+      void* self = dlsym(RTLD_DEFAULT, symbol);
+      if (self) *pfn = self;
+      break;
+    }
+  }
+  return rc;
+}
+
+}  // extern "C"

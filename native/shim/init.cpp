@@ -1,0 +1,125 @@
+// Lazy initialisation, fork handling, exit cleanup and suspend/resume signals.
+//
+// Reference behaviour: libvgpu.so cuInit → pthread_once(preInit) → postInit
+// (allocator_init, set_task_pid, init_utilization_watcher), exit_handler, and
+// SIGUSR2/SIGUSR1 → sig_swap_stub / sig_restore_stub.
+#include <signal.h>
+
+#include "common.h"
+#include "state.h"
+
+namespace vgpu {
+
+static State* g_state = nullptr;
+static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+
+State& st() {
+  if (__builtin_expect(g_state == nullptr, 0)) {
+    // Leaked on purpose: hooks may run during static destruction.
+    static State* s = new State();
+    g_state = s;
+  }
+  return *g_state;
+}
+
+static void on_exit_release() {
+  State& s = st();
+  if (s.region && s.slot >= 0) {
+    region_release_slot(s.region, s.slot);
+    s.slot = -1;
+  }
+}
+
+static void sig_suspend(int) {
+  State& s = st();
+  s.suspended.store(1, std::memory_order_relaxed);
+  if (vgpu_proc_slot_t* sl = my_slot())
+    __atomic_store_n(&sl->status, VGPU_PROC_SUSPENDED, __ATOMIC_RELAXED);
+}
+
+static void sig_resume(int) {
+  State& s = st();
+  s.suspended.store(0, std::memory_order_relaxed);
+  if (vgpu_proc_slot_t* sl = my_slot())
+    __atomic_store_n(&sl->status, VGPU_PROC_RUNNING, __ATOMIC_RELAXED);
+}
+
+static void install_signal(int sig, void (*fn)(int)) {
+  struct sigaction old;
+  if (sigaction(sig, nullptr, &old) == 0 && old.sa_handler != SIG_DFL && old.sa_handler != SIG_IGN)
+    return;  // the application owns this signal; leave it alone
+  struct sigaction sa;
+  memset(&sa, 0, sizeof sa);
+  sa.sa_handler = fn;
+  sa.sa_flags = SA_RESTART;
+  sigaction(sig, &sa, nullptr);
+}
+
+static void atfork_child() {
+  // The child inherits the parent's mapping but not its slot; it claims its
+  // own slot lazily on first use.
+  State& s = st();
+  s.slot = -1;
+  s.pid = getpid();
+  if (s.region) {
+    s.slot = region_claim_slot(s.region, s.pid, host_pid_of_self(), s.lim.priority);
+  }
+  {
+    std::lock_guard<std::mutex> g(s.ledger_mu);
+    s.ledger.clear();
+  }
+  for (auto& t : s.dev_touched) t.store(0);
+}
+
+static void do_init() {
+  State& s = st();
+  s.pid = getpid();
+  bool disabled = env_bool(env_first("VGPU_DISABLE_CONTROL", "CUDA_DISABLE_CONTROL"), false);
+  s.lim = limits_from_env();
+  s.report_masked_cus = env_bool(env_first("VGPU_REPORT_MASKED_CUS"), false);
+  s.active_oom_killer = env_bool(env_first("ACTIVE_OOM_KILLER"), false);
+  s.context_charge = parse_mem(env_first("VGPU_CONTEXT_CHARGE"));
+  s.enabled = !disabled;
+  if (!s.enabled) {
+    VLOG_INFO("vgpu control disabled by environment");
+    s.init_done.store(1, std::memory_order_release);
+    return;
+  }
+  const char* path = env_first("VGPU_SHARED_REGION", "CUDA_DEVICE_MEMORY_SHARED_CACHE");
+  s.region = region_map(path, &s.lim, &s.region_fd);
+  if (!s.region && path) {
+    VLOG_WARN("falling back to a private region (could not map %s)", path);
+    s.region = region_map(nullptr, &s.lim, &s.region_fd);
+  }
+  if (s.region) {
+    s.slot = region_claim_slot(s.region, s.pid, host_pid_of_self(), s.lim.priority);
+    if (s.slot < 0) VLOG_ERR("no free process slot in the shared region");
+  }
+  install_signal(SIGUSR2, sig_suspend);
+  install_signal(SIGUSR1, sig_resume);
+  atexit(on_exit_release);
+  pthread_atfork(nullptr, nullptr, atfork_child);
+  for (int i = 0; i < s.lim.num_devices; ++i) {
+    if (s.lim.mem_limit[i] || s.lim.cu_limit[i])
+      VLOG_INFO("device %d: memory limit %llu MiB, cu limit %u%%", i,
+                (unsigned long long)(s.lim.mem_limit[i] >> 20), s.lim.cu_limit[i]);
+  }
+  limiter_start();
+  s.init_done.store(1, std::memory_order_release);
+}
+
+void ensure_init() {
+  if (__builtin_expect(st().init_done.load(std::memory_order_acquire), 1)) return;
+  pthread_once(&g_once, do_init);
+}
+
+void suspend_gate() {
+  State& s = st();
+  if (__builtin_expect(!s.suspended.load(std::memory_order_relaxed), 1)) return;
+  uint64_t t0 = mono_ns();
+  while (s.suspended.load(std::memory_order_relaxed)) sleep_ns(1000000);  // 1 ms
+  if (vgpu_proc_slot_t* sl = my_slot())
+    __atomic_fetch_add(&sl->throttle_wait_ns, mono_ns() - t0, __ATOMIC_RELAXED);
+}
+
+}  // namespace vgpu

@@ -1,0 +1,122 @@
+// Allocation ledger + container-wide HBM cap.
+//
+// Reference behaviour: lib/nvidia/libvgpu.so allocator.c — allocate_raw →
+// add_chunk → oom_check (limit vs Σ shared-region usage, purging exited
+// processes via rm_quitted_process) → add_gpu_device_memory_usage; free_raw →
+// remove_chunk.  "Device %d OOM %lu / %lu" log line.
+//
+// Here: the charge is RESERVED in the shared region under the robust lock
+// before the real allocator runs (so two processes racing for the last bytes
+// cannot both win), and released if the real call fails.
+#include <signal.h>
+
+#include "common.h"
+#include "state.h"
+
+namespace vgpu {
+
+uint64_t mem_limit(int dev) {
+  State& s = st();
+  if (!s.enabled || dev < 0 || dev >= VGPU_MAX_DEVICES) return 0;
+  if (s.region) return s.region->dev[dev].mem_limit;
+  return s.lim.mem_limit[dev];
+}
+
+uint64_t mem_used(int dev) {
+  State& s = st();
+  if (!s.region || dev < 0 || dev >= VGPU_MAX_DEVICES) return 0;
+  return region_device_used(s.region, dev) + region_device_host_used(s.region, dev);
+}
+
+static void add_usage(vgpu_dev_usage_t& u, uint64_t size, int kind, bool add) {
+  auto op = [&](uint64_t* f) {
+    if (add) __atomic_fetch_add(f, size, __ATOMIC_RELAXED);
+    else __atomic_fetch_sub(f, size, __ATOMIC_RELAXED);
+  };
+  switch (kind) {
+    case kHostSpill:
+      op(&u.host_bytes);
+      return;
+    case kModule:
+      op(&u.module_bytes);
+      break;
+    default:
+      op(&u.buffer_bytes);
+      break;
+  }
+  op(&u.total_bytes);
+  if (add) {
+    uint64_t t = __atomic_load_n(&u.total_bytes, __ATOMIC_RELAXED);
+    uint64_t pk = __atomic_load_n(&u.peak_bytes, __ATOMIC_RELAXED);
+    while (t > pk && !__atomic_compare_exchange_n(&u.peak_bytes, &pk, t, true, __ATOMIC_RELAXED,
+                                                  __ATOMIC_RELAXED)) {
+    }
+  }
+}
+
+bool mem_reserve(int dev, uint64_t size, int kind) {
+  State& s = st();
+  vgpu_proc_slot_t* sl = my_slot();
+  if (!s.enabled || !sl || dev < 0 || dev >= VGPU_MAX_DEVICES) return true;
+  uint64_t limit = s.region->dev[dev].mem_limit;
+  if (limit == 0) {  // unlimited: account only
+    add_usage(sl->used[dev], size, kind, true);
+    return true;
+  }
+  if (region_lock(s.region) != 0) return true;
+  uint64_t used = region_device_used(s.region, dev) + region_device_host_used(s.region, dev);
+  if (used + size > limit) {
+    region_purge_dead_locked(s.region, false);
+    used = region_device_used(s.region, dev) + region_device_host_used(s.region, dev);
+  }
+  bool ok = used + size <= limit;
+  if (ok) add_usage(sl->used[dev], size, kind, true);
+  else __atomic_fetch_add(&sl->oom_events, 1, __ATOMIC_RELAXED);
+  region_unlock(s.region);
+  if (!ok) {
+    VLOG_WARN("Device %d OOM %llu / %llu (request %llu bytes)", dev,
+              (unsigned long long)(used + size), (unsigned long long)limit,
+              (unsigned long long)size);
+    if (s.active_oom_killer) {
+      VLOG_ERR("ACTIVE_OOM_KILLER: terminating pid %d", s.pid);
+      kill(s.pid, SIGKILL);
+    }
+  }
+  return ok;
+}
+
+void mem_unreserve(int dev, uint64_t size, int kind) {
+  State& s = st();
+  vgpu_proc_slot_t* sl = my_slot();
+  if (!s.enabled || !sl || dev < 0 || dev >= VGPU_MAX_DEVICES) return;
+  add_usage(sl->used[dev], size, kind, false);
+}
+
+void ledger_add(void* p, uint64_t size, int dev, int kind) {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.ledger_mu);
+  s.ledger[(uintptr_t)p] = Alloc{size, dev, kind};
+}
+
+bool ledger_take(void* p, Alloc* out) {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.ledger_mu);
+  auto it = s.ledger.find((uintptr_t)p);
+  if (it == s.ledger.end()) return false;
+  *out = it->second;
+  s.ledger.erase(it);
+  return true;
+}
+
+void charge_context(int dev) {
+  State& s = st();
+  if (!s.enabled || dev < 0 || dev >= VGPU_MAX_DEVICES || s.context_charge == 0) return;
+  int expected = 0;
+  if (!s.dev_touched[dev].compare_exchange_strong(expected, 1)) return;
+  if (vgpu_proc_slot_t* sl = my_slot()) {
+    __atomic_fetch_add(&sl->used[dev].context_bytes, s.context_charge, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&sl->used[dev].total_bytes, s.context_charge, __ATOMIC_RELAXED);
+  }
+}
+
+}  // namespace vgpu

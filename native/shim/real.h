@@ -1,0 +1,85 @@
+// Resolution of the real HIP / HSA entry points behind our interposers.
+//
+// The shim never links libamdhip64 / libhsa-runtime64: a PyTorch-ROCm process
+// ships its own copies under torch/lib (SONAME libamdhip64.so.7,
+// libhsa-runtime64.so.1) and a second runtime in the process would be fatal.
+// We look the already-loaded library up by SONAME with RTLD_NOLOAD and only
+// fall back to RTLD_NEXT / a plain dlopen for non-PyTorch programs.
+#pragma once
+
+#include <dlfcn.h>
+
+#include <hip/hip_runtime_api.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
+namespace vgpu {
+
+void* hip_lib_handle();
+void* hsa_lib_handle();
+void* resolve_real(void* handle, const char* name);
+
+}  // namespace vgpu
+
+// Signatures of the HIP entry points we call through (the HIP header adds C++
+// template overloads for several of them, so decltype(&fn) is ambiguous).
+namespace vgpu {
+namespace fnt {
+using hipSetDevice = hipError_t (*)(int);
+using hipMalloc = hipError_t (*)(void**, size_t);
+using hipExtMallocWithFlags = hipError_t (*)(void**, size_t, unsigned int);
+using hipMallocAsync = hipError_t (*)(void**, size_t, hipStream_t);
+using hipMallocFromPoolAsync = hipError_t (*)(void**, size_t, hipMemPool_t, hipStream_t);
+using hipMallocManaged = hipError_t (*)(void**, size_t, unsigned int);
+using hipMallocPitch = hipError_t (*)(void**, size_t*, size_t, size_t);
+using hipHostMalloc = hipError_t (*)(void**, size_t, unsigned int);
+using hipHostFree = hipError_t (*)(void*);
+using hipFree = hipError_t (*)(void*);
+using hipFreeAsync = hipError_t (*)(void*, hipStream_t);
+using hipMemCreate = hipError_t (*)(hipMemGenericAllocationHandle_t*, size_t,
+                                    const hipMemAllocationProp*, unsigned long long);
+using hipMemRelease = hipError_t (*)(hipMemGenericAllocationHandle_t);
+using hipMemGetInfo = hipError_t (*)(size_t*, size_t*);
+using hipDeviceTotalMem = hipError_t (*)(size_t*, hipDevice_t);
+using hipGetDevicePropertiesR0600 = hipError_t (*)(hipDeviceProp_tR0600*, int);
+using hipDeviceGetAttribute = hipError_t (*)(int*, hipDeviceAttribute_t, int);
+using hipGetLastError = hipError_t (*)();
+using hipStreamSynchronize = hipError_t (*)(hipStream_t);
+using hipLaunchKernel = hipError_t (*)(const void*, dim3, dim3, void**, size_t, hipStream_t);
+using hipExtLaunchKernel = hipError_t (*)(const void*, dim3, dim3, void**, size_t, hipStream_t,
+                                          hipEvent_t, hipEvent_t, int);
+using hipModuleLaunchKernel = hipError_t (*)(hipFunction_t, unsigned int, unsigned int,
+                                             unsigned int, unsigned int, unsigned int,
+                                             unsigned int, unsigned int, hipStream_t, void**,
+                                             void**);
+using hipExtModuleLaunchKernel = hipError_t (*)(hipFunction_t, uint32_t, uint32_t, uint32_t,
+                                                uint32_t, uint32_t, uint32_t, size_t,
+                                                hipStream_t, void**, void**, hipEvent_t,
+                                                hipEvent_t, uint32_t);
+using hipLaunchCooperativeKernel = hipError_t (*)(const void*, dim3, dim3, void**, unsigned int,
+                                                  hipStream_t);
+using hipModuleLaunchCooperativeKernel = hipError_t (*)(hipFunction_t, unsigned int, unsigned int,
+                                                        unsigned int, unsigned int, unsigned int,
+                                                        unsigned int, unsigned int, hipStream_t,
+                                                        void**);
+using hipLaunchKernelExC = hipError_t (*)(const hipLaunchConfig_t*, const void*, void**);
+using hipGraphLaunch = hipError_t (*)(hipGraphExec_t, hipStream_t);
+using hipOccupancyMaxActiveBlocksPerMultiprocessor = hipError_t (*)(int*, const void*, int, size_t);
+using hipGetProcAddress = hipError_t (*)(const char*, void**, int, uint64_t,
+                                         hipDriverProcAddressQueryResult*);
+}  // namespace fnt
+}  // namespace vgpu
+
+#define VGPU_REAL_IMPL(lib, T, name)                                              \
+  ([]() -> T {                                                                    \
+    static T p = nullptr;                                                         \
+    T v = __atomic_load_n(&p, __ATOMIC_ACQUIRE);                                  \
+    if (!v) {                                                                     \
+      v = (T)::vgpu::resolve_real(::vgpu::lib(), name);                           \
+      __atomic_store_n(&p, v, __ATOMIC_RELEASE);                                  \
+    }                                                                             \
+    return v;                                                                     \
+  }())
+// REAL_HIP(hipMalloc)(args...) calls the next definition of hipMalloc.
+#define REAL_HIP(fn) VGPU_REAL_IMPL(hip_lib_handle, ::vgpu::fnt::fn, #fn)
+#define REAL_HSA(fn) VGPU_REAL_IMPL(hsa_lib_handle, decltype(&::fn), #fn)

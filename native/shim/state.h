@@ -1,0 +1,88 @@
+// Process-global state of the enforcement library.
+//
+// Reference behaviour (what, not how): lib/nvidia/libvgpu.so keeps a
+// per-process view of the shared region, its slot, the allocation chunk list
+// (allocator.c: add_chunk/remove_chunk/oom_check), the utilization watcher
+// thread and the suspend status.
+#pragma once
+
+#include <pthread.h>
+
+#include <atomic>
+#include <mutex>
+#include <unordered_map>
+
+#include "region.h"
+
+namespace vgpu {
+
+enum AllocKind : int {
+  kDeviceBuf = 0,   // HBM buffer (hipMalloc, hipMallocAsync, hipExtMallocWithFlags, ...)
+  kHostSpill = 1,   // oversubscribed allocation backed by pinned host memory
+  kManaged = 2,     // hipMallocManaged
+  kVmmHandle = 3,   // hipMemCreate physical handle
+  kModule = 4,      // code object bytes
+};
+
+struct Alloc {
+  uint64_t size;
+  int dev;
+  int kind;
+};
+
+struct State {
+  std::atomic<int> init_done{0};
+  bool enabled = false;           // VGPU_DISABLE_CONTROL unset and limits present
+  DeviceLimits lim;
+  vgpu_shared_region_t* region = nullptr;
+  int region_fd = -1;
+  int slot = -1;
+  int pid = 0;
+  bool report_masked_cus = false;
+  bool active_oom_killer = false;
+  uint64_t context_charge = 0;    // bytes charged per device at first use
+
+  std::mutex ledger_mu;
+  std::unordered_map<uintptr_t, Alloc> ledger;
+
+  std::atomic<int> suspended{0};
+  std::atomic<int> dev_touched[VGPU_MAX_DEVICES] = {};
+};
+
+State& st();
+
+// Lazily initialise (pthread_once).  Cheap after the first call.
+void ensure_init();
+
+inline vgpu_proc_slot_t* my_slot() {
+  State& s = st();
+  if (!s.region || s.slot < 0) return nullptr;
+  return &s.region->procs[s.slot];
+}
+
+// Memory accounting ---------------------------------------------------------
+// Reserve `size` bytes of HBM charge on `dev` for this process.  Returns false
+// (and counts an OOM event) when the container limit would be exceeded.
+bool mem_reserve(int dev, uint64_t size, int kind);
+void mem_unreserve(int dev, uint64_t size, int kind);
+void ledger_add(void* p, uint64_t size, int dev, int kind);
+bool ledger_take(void* p, Alloc* out);
+uint64_t mem_limit(int dev);          // 0 = unlimited
+uint64_t mem_used(int dev);           // container-wide HBM + host charge
+void charge_context(int dev);         // first-touch context charge
+
+// Compute limiting ------------------------------------------------------------
+void limiter_start();
+// Called on every dispatch with the number of workgroups it launches.
+void limiter_on_launch(int dev, uint64_t workgroups);
+void suspend_gate();
+int cu_count_masked(int dev, int physical);
+
+// CU masks on HSA queues ---------------------------------------------------------
+void cumask_on_queue_created(void* agent_handle_ptr, void* queue);
+void cumask_on_queue_destroyed(void* queue);
+int cumask_reapply_all();
+
+extern thread_local int tl_device;
+
+}  // namespace vgpu

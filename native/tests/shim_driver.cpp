@@ -1,0 +1,196 @@
+// Scenario driver for the enforcement library on the fake HIP/HSA runtimes.
+// Run as:  LD_PRELOAD=libvgpu.so LD_LIBRARY_PATH=<fakes> shim_driver <scenario> [args]
+// Prints "key=value" lines that tests/test_shim_native.py parses.
+//
+// It links the fake libamdhip64.so.7 exactly the way libc10_hip.so links the
+// real one, so every hip* call below goes through the preloaded interposer.
+#include <dlfcn.h>
+#include <hip/hip_runtime_api.h>
+#include <signal.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "vgpu/shared_region.h"
+
+extern "C" int fake_hsa_queue_count();
+extern "C" int fake_hsa_queue_mask(int idx, uint32_t* out, int max_words, uint64_t* agent);
+extern "C" uint64_t fake_hip_launches();
+extern "C" uint64_t fake_hip_physical_used(int dev);
+
+template <class T>
+static T sym(const char* name) {
+  return (T)dlsym(RTLD_DEFAULT, name);
+}
+
+static void print_region(int dev) {
+  auto self_region = sym<void* (*)()>("vgpu_self_region");
+  auto self_slot = sym<int (*)()>("vgpu_self_slot");
+  auto used = sym<uint64_t (*)(void*, int)>("vgpu_region_device_used");
+  if (!self_region) {
+    printf("shim_loaded=0\n");
+    return;
+  }
+  auto* r = (vgpu_shared_region_t*)self_region();
+  int slot = self_slot();
+  printf("shim_loaded=1\nslot=%d\n", slot);
+  if (!r) return;
+  printf("region_used=%llu\n", (unsigned long long)used(r, dev));
+  printf("proc_num=%d\n", r->proc_num);
+  if (slot >= 0) {
+    printf("slot_launches=%llu\n", (unsigned long long)r->procs[slot].launches);
+    printf("slot_oom=%llu\n", (unsigned long long)r->procs[slot].oom_events);
+    printf("slot_host_bytes=%llu\n", (unsigned long long)r->procs[slot].used[dev].host_bytes);
+    printf("slot_peak=%llu\n", (unsigned long long)r->procs[slot].used[dev].peak_bytes);
+  }
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    fprintf(stderr, "usage: shim_driver <scenario> ...\n");
+    return 2;
+  }
+  std::string sc = argv[1];
+  int dev = argc > 3 && sc == "fill" ? 0 : 0;
+  if (getenv("DRIVER_DEVICE")) dev = atoi(getenv("DRIVER_DEVICE"));
+  if (hipSetDevice(dev) != hipSuccess) {
+    printf("error=set_device\n");
+    return 1;
+  }
+
+  if (sc == "meminfo") {
+    size_t f = 0, t = 0;
+    hipMemGetInfo(&f, &t);
+    printf("free=%zu\ntotal=%zu\n", f, t);
+    hipDeviceProp_tR0600 p;
+    hipGetDevicePropertiesR0600(&p, dev);
+    printf("prop_total=%zu\nprop_cus=%d\n", p.totalGlobalMem, p.multiProcessorCount);
+    size_t dt = 0;
+    hipDeviceTotalMem(&dt, dev);
+    printf("device_total=%zu\n", dt);
+    int cus = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    printf("attr_cus=%d\n", cus);
+    print_region(dev);
+    return 0;
+  }
+
+  if (sc == "fill") {
+    size_t chunk = argc > 2 ? strtoull(argv[2], nullptr, 10) : (1ull << 30);
+    std::vector<void*> ptrs;
+    hipError_t last = hipSuccess;
+    for (int i = 0; i < 100000; ++i) {
+      void* p = nullptr;
+      last = hipMalloc(&p, chunk);
+      if (last != hipSuccess) break;
+      ptrs.push_back(p);
+    }
+    printf("allocated=%zu\nlast_error=%d\n", ptrs.size(), (int)last);
+    size_t f = 0, t = 0;
+    hipMemGetInfo(&f, &t);
+    printf("free_at_full=%zu\n", f);
+    print_region(dev);
+    for (void* p : ptrs) hipFree(p);
+    auto used = sym<uint64_t (*)(void*, int)>("vgpu_region_device_used");
+    auto self_region = sym<void* (*)()>("vgpu_self_region");
+    if (used && self_region) printf("region_used_after_free=%llu\n",
+                                    (unsigned long long)used(self_region(), dev));
+    printf("physical_used_after_free=%llu\n", (unsigned long long)fake_hip_physical_used(dev));
+    return 0;
+  }
+
+  if (sc == "spill") {
+    // Oversubscription: allocate `n` chunks; report how many landed in host memory.
+    size_t chunk = argc > 2 ? strtoull(argv[2], nullptr, 10) : (1ull << 30);
+    int n = argc > 3 ? atoi(argv[3]) : 10;
+    std::vector<void*> ptrs;
+    int fails = 0;
+    for (int i = 0; i < n; ++i) {
+      void* p = nullptr;
+      if (hipMalloc(&p, chunk) == hipSuccess) ptrs.push_back(p);
+      else ++fails;
+    }
+    printf("allocated=%zu\nfailed=%d\nphysical_used=%llu\n", ptrs.size(), fails,
+           (unsigned long long)fake_hip_physical_used(dev));
+    print_region(dev);
+    for (void* p : ptrs) hipFree(p);
+    return 0;
+  }
+
+  if (sc == "masks") {
+    void* p = nullptr;
+    hipMalloc(&p, 4096);  // forces runtime init (queue creation)
+    int n = fake_hsa_queue_count();
+    printf("queues=%d\n", n);
+    for (int q = 0; q < n; ++q) {
+      uint32_t m[8] = {};
+      uint64_t agent = 0;
+      int words = fake_hsa_queue_mask(q, m, 8, &agent);
+      printf("queue%d_agent=%llu\nqueue%d_words=%d\nqueue%d_mask=", q, (unsigned long long)agent, q,
+             words, q);
+      for (int w = words - 1; w >= 0; --w) printf("%08x", m[w]);
+      printf("\n");
+    }
+    hipFree(p);
+    return 0;
+  }
+
+  if (sc == "launch") {
+    int n = argc > 2 ? atoi(argv[2]) : 100;
+    unsigned grid = argc > 3 ? (unsigned)atoi(argv[3]) : 1024;
+    for (int i = 0; i < n; ++i) hipLaunchKernel((const void*)&main, dim3(grid), dim3(256), nullptr, 0, nullptr);
+    hipModuleLaunchKernel(nullptr, grid, 1, 1, 256, 1, 1, 0, nullptr, nullptr, nullptr);
+    hipGraphLaunch(nullptr, nullptr);
+    printf("fake_launches=%llu\n", (unsigned long long)fake_hip_launches());
+    print_region(dev);
+    return 0;
+  }
+
+  if (sc == "hold") {
+    // Allocate `bytes`, print, then sleep (multi-process cap tests).
+    size_t bytes = argc > 2 ? strtoull(argv[2], nullptr, 10) : (1ull << 30);
+    double secs = argc > 3 ? atof(argv[3]) : 2.0;
+    void* p = nullptr;
+    hipError_t rc = hipMalloc(&p, bytes);
+    printf("hold_rc=%d\n", (int)rc);
+    fflush(stdout);
+    usleep((useconds_t)(secs * 1e6));
+    if (rc == hipSuccess && !getenv("DRIVER_LEAK")) hipFree(p);
+    return 0;
+  }
+
+  if (sc == "throttle") {
+    // Launch for `secs` seconds; report launches/s (temporal limiter tests).
+    double secs = argc > 2 ? atof(argv[2]) : 1.0;
+    unsigned grid = argc > 3 ? (unsigned)atoi(argv[3]) : 256;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    uint64_t n = 0;
+    for (;;) {
+      hipLaunchKernel((const void*)&main, dim3(grid), dim3(256), nullptr, 0, nullptr);
+      ++n;
+      clock_gettime(CLOCK_MONOTONIC, &t1);
+      double el = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+      if (el >= secs) break;
+    }
+    printf("launches=%llu\n", (unsigned long long)n);
+    print_region(dev);
+    return 0;
+  }
+
+  if (sc == "proc_addr") {
+    void* fn = nullptr;
+    hipGetProcAddress("hipMalloc", &fn, 700, 0, nullptr);
+    void* self = dlsym(RTLD_DEFAULT, "hipMalloc");
+    printf("proc_addr_is_hook=%d\n", fn == self ? 1 : 0);
+    return 0;
+  }
+
+  fprintf(stderr, "unknown scenario %s\n", sc.c_str());
+  return 2;
+}
