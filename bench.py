@@ -1,0 +1,164 @@
+#!/usr/bin/env python3
+"""Headline benchmark: aggregate ai-benchmark-equivalent throughput of N vGPU
+pods sharing each MI355X, plus VRAM-cap accuracy (BASELINE.json metric).
+
+Default config = BASELINE.json config 2: every GPU is split 2 ways, each pod
+``amd.com/gpumem=144000`` (MiB) and ``amd.com/gpucores=50``, running ResNet-V2-50
+bf16 inference at the reference's ai-benchmark shape (test 1.1: batch 50,
+346x346; reference README.md:244).  Weights are random-init and inputs
+synthetic.  Every pod runs under the in-container enforcement library
+(LD_PRELOAD libvgpu.so) with its own shared region, HBM cap and XCD-balanced
+CU mask — exactly what the device plugin's Allocate hands a container.
+
+Launch: ``python bench.py --gpus N --steps K --warmup W`` (N>1 under
+torch.distributed.run, one rank per GPU).  Each rank spawns its pods BEFORE
+touching the GPU itself (it never does), runs W untimed warmup steps in every
+pod, then a cross-rank barrier, then exactly K timed steps in every pod
+concurrently (each pod synchronizes its device before reporting ready and after
+its last step).  The rank measures the wall time from GO to the last DONE;
+the job's ms_per_step is the MAX over ranks, and `value` is total images over
+all pods on all GPUs divided by that wall time (weak scaling: per-GPU work is
+fixed as N grows).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+METRIC = "aggregate ai-benchmark score, N pods sharing 1 MI355X; VRAM-cap accuracy"
+BASELINE_VGPU_R50_INF = 141.2  # images/s, ResNet-V2-50 inference, vGPU-device-plugin
+
+
+def log(msg: str) -> None:
+    sys.stderr.write(f"[bench {time.strftime('%H:%M:%S')}] {msg}\n")
+    sys.stderr.flush()
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--pods", type=int, default=2, help="vGPU pods sharing each GPU")
+    ap.add_argument("--workload", default="1.1", help="ai-benchmark test id (vgpu.models.WORKLOADS)")
+    ap.add_argument("--gpumem", type=int, default=144000, help="per-pod amd.com/gpumem (MiB)")
+    ap.add_argument("--gpucores", type=int, default=50, help="per-pod amd.com/gpucores (%%)")
+    ap.add_argument("--no-shim", action="store_true", help="run pods without enforcement")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--find", action="store_true", help="MIOpen find (cudnn.benchmark) in warmup")
+    ap.add_argument("--no-cap-probe", action="store_true")
+    ap.add_argument("--ready-timeout", type=float, default=1500.0)
+    args = ap.parse_args(argv)
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        log(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}")
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from vgpu.native import ensure_built
+    from vgpu.bench.launch import PodSpec, launch_pods, visible_device_for
+    from vgpu.models import WORKLOADS
+
+    if not args.no_shim:
+        ensure_built(kernels=False)
+    w = WORKLOADS[args.workload]
+
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pg = dist
+
+    device = visible_device_for(local_rank)
+    specs = [PodSpec(workload=args.workload, mem_mib=args.gpumem, cores=args.gpucores)
+             for _ in range(args.pods)]
+    log(f"rank {rank}/{world}: launching {args.pods} pods of {w.name} (test {w.test_id}) on device {device}")
+    pods = launch_pods(specs, device, steps=args.steps, warmup=args.warmup, shim=not args.no_shim,
+                       graph=not args.no_graph, cap_probe=not args.no_cap_probe, find=args.find)
+    try:
+        for p in pods:
+            p.ready = p.read_tagged("READY", args.ready_timeout, progress=log)
+            log(f"pod {p.idx} ready: {json.dumps(p.ready)}")
+        if pg:
+            pg.barrier()
+        for p in pods:
+            p.send("GO")
+        for p in pods:
+            p.done = p.read_tagged("DONE", 600.0 + 60.0 * args.steps, progress=log)
+        # Timed window: first pod's post-sync start → last pod's post-sync end
+        # (CLOCK_MONOTONIC is node-wide, so pod timestamps are comparable).
+        t_end = max(p.done["t1"] for p in pods)
+        t_start = min(p.done["t0"] for p in pods)
+        wall = t_end - t_start
+        for p in pods:
+            p.proc.wait(timeout=120)
+    finally:
+        for p in pods:
+            if p.proc.poll() is None:
+                p.proc.kill()
+
+    samples = sum(p.done["samples"] for p in pods)
+    ms_step = 1e3 * wall / args.steps
+    cap = []
+    for p in pods:
+        d = p.done
+        if "reserved_at_oom" in d:
+            limit = args.gpumem * (1 << 20)
+            cap.append({"pod": p.idx, "limit": limit, "reported_total": d["mem_total_reported"],
+                        "reserved_at_oom": d["reserved_at_oom"],
+                        "accuracy": d["reserved_at_oom"] / limit,
+                        "violation": d["reserved_at_oom"] > limit})
+    if pg:
+        import torch
+        t = torch.tensor([ms_step, float(samples)], dtype=torch.float64)
+        mx = t.clone()
+        pg.all_reduce(mx, op=pg.ReduceOp.MAX)
+        sm = t.clone()
+        pg.all_reduce(sm, op=pg.ReduceOp.SUM)
+        ms_step = float(mx[0])
+        samples = float(sm[1])
+    value = samples / (ms_step * args.steps / 1e3)
+    if rank == 0:
+        per_gpu = value / world
+        res = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_VGPU_R50_INF, 2) if args.workload == "1.1" else None,
+            "dtype": "bf16",
+            "data": "synthetic inputs, random-init weights",
+            "config": {
+                "model": f"{w.name} (ai-benchmark test {w.test_id}, {'training' if w.train else 'inference'})",
+                "global_batch": w.batch * args.pods * world,
+                "seq_len": w.shape[-1],
+                "parallelism": f"vgpu: {args.pods} pods/GPU x {world} GPU(s)",
+                "pods_per_gpu": args.pods,
+                "gpumem_mib": args.gpumem,
+                "gpucores": args.gpucores,
+                "enforcement": "none" if args.no_shim else "libvgpu.so (HBM cap + XCD-balanced CU mask)",
+                "hipgraph": not args.no_graph,
+            },
+            "per_gpu_images_s": round(per_gpu, 2),
+            "per_pod_images_s": [round(p.done["throughput"], 2) for p in pods],
+            "vram_cap": cap,
+        }
+        print(json.dumps(res), flush=True)
+    if pg:
+        pg.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -45,12 +45,15 @@ static void add_usage(vgpu_dev_usage_t& u, uint64_t size, int kind, bool add) {
       break;
   }
   op(&u.total_bytes);
-  if (add) {
-    uint64_t t = __atomic_load_n(&u.total_bytes, __ATOMIC_RELAXED);
-    uint64_t pk = __atomic_load_n(&u.peak_bytes, __ATOMIC_RELAXED);
-    while (t > pk && !__atomic_compare_exchange_n(&u.peak_bytes, &pk, t, true, __ATOMIC_RELAXED,
-                                                  __ATOMIC_RELAXED)) {
-    }
+}
+
+// High-water mark; called only once an allocation has really succeeded (a
+// reservation that the runtime then refuses must not move the peak).
+static void note_peak(vgpu_dev_usage_t& u) {
+  uint64_t t = __atomic_load_n(&u.total_bytes, __ATOMIC_RELAXED);
+  uint64_t pk = __atomic_load_n(&u.peak_bytes, __ATOMIC_RELAXED);
+  while (t > pk && !__atomic_compare_exchange_n(&u.peak_bytes, &pk, t, true, __ATOMIC_RELAXED,
+                                                __ATOMIC_RELAXED)) {
   }
 }
 
@@ -94,8 +97,12 @@ void mem_unreserve(int dev, uint64_t size, int kind) {
 
 void ledger_add(void* p, uint64_t size, int dev, int kind) {
   State& s = st();
-  std::lock_guard<std::mutex> g(s.ledger_mu);
-  s.ledger[(uintptr_t)p] = Alloc{size, dev, kind};
+  {
+    std::lock_guard<std::mutex> g(s.ledger_mu);
+    s.ledger[(uintptr_t)p] = Alloc{size, dev, kind};
+  }
+  vgpu_proc_slot_t* sl = my_slot();
+  if (sl && dev >= 0 && dev < VGPU_MAX_DEVICES) note_peak(sl->used[dev]);
 }
 
 bool ledger_take(void* p, Alloc* out) {

@@ -1,0 +1,185 @@
+"""CPU tests of the in-container enforcement library (native/shim) against
+the fixture-driven fake HIP / HSA runtimes (the reference
+has no harness for libvgpu.so at all; its only native-boundary test is the
+fake libcndev pattern, pkg/device-plugin/mlu/cndev/bindings_test.go:27-103).
+"""
+import os
+import subprocess
+import time
+
+import pytest
+
+from vgpu.native import FAKES_DIR, shim_path
+
+GiB = 1 << 30
+
+
+def run(scenario, *args, env=None, preload=True, timeout=60):
+    e = {k: v for k, v in os.environ.items() if not k.startswith(("VGPU_", "CUDA_", "HIP_"))}
+    e["LD_LIBRARY_PATH"] = str(FAKES_DIR)
+    if preload:
+        e["LD_PRELOAD"] = str(shim_path())
+    e.update(env or {})
+    r = subprocess.run([str(FAKES_DIR / "shim_driver"), scenario, *map(str, args)], env=e,
+                       capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr
+    out = {}
+    for line in r.stdout.splitlines():
+        if "=" in line:
+            k, v = line.split("=", 1)
+            out[k] = v
+    out["_stderr"] = r.stderr
+    return out
+
+
+def test_passthrough_without_preload(native_build):
+    o = run("meminfo", preload=False)
+    assert o["shim_loaded"] == "0"
+    assert int(o["total"]) == 288 * GiB
+
+
+def test_meminfo_reports_cap(native_build):
+    o = run("meminfo", env={"VGPU_DEVICE_MEMORY_LIMIT_0": "144000m"})
+    cap = 144000 << 20
+    assert int(o["total"]) == cap
+    assert int(o["free"]) == cap
+    assert int(o["prop_total"]) == cap
+    assert int(o["device_total"]) == cap
+    assert int(o["prop_cus"]) == 256  # masked CU reporting is opt-in
+
+
+def test_legacy_cuda_env_names_accepted(native_build):
+    o = run("meminfo", env={"CUDA_DEVICE_MEMORY_LIMIT_0": "2048m"})
+    assert int(o["total"]) == 2048 << 20
+
+
+def test_oom_exactly_at_cap(native_build):
+    o = run("fill", GiB, env={"VGPU_DEVICE_MEMORY_LIMIT_0": "10g"})
+    assert o["allocated"] == "10"
+    assert o["last_error"] == "2"  # hipErrorOutOfMemory
+    assert int(o["free_at_full"]) == 0
+    assert int(o["region_used"]) == 10 * GiB
+    assert o["slot_oom"] == "1"
+    assert int(o["region_used_after_free"]) == 0
+    assert int(o["physical_used_after_free"]) == 0
+
+
+def test_uncapped_accounts_without_refusing(native_build):
+    o = run("fill", 64 * GiB, env={"VGPU_DEVICE_MEMORY_LIMIT_1": "1g"})
+    # device 0 has no limit → physical exhaustion (288 GiB / 64 GiB = 4)
+    assert o["allocated"] == "4"
+    assert int(o["slot_peak"]) == 256 * GiB
+
+
+def test_disable_control_env(native_build):
+    o = run("meminfo", env={"VGPU_DEVICE_MEMORY_LIMIT_0": "1g", "VGPU_DISABLE_CONTROL": "true"})
+    assert int(o["total"]) == 288 * GiB
+
+
+def test_cu_mask_from_limit_is_xcd_balanced(native_build):
+    o = run("masks", env={"VGPU_DEVICE_CU_LIMIT_0": "50"})
+    assert o["queues"] == "1"
+    mask = int(o["queue0_mask"], 16)
+    assert bin(mask).count("1") == 128
+    from vgpu.device.cualloc import MI355X
+    assert MI355X.per_xcd_counts(mask) == [16] * 8
+
+
+def test_cu_mask_explicit(native_build):
+    m = (0xFF << 64) | 0xFF
+    o = run("masks", env={"VGPU_CU_MASK_0": hex(m)})
+    assert int(o["queue0_mask"], 16) == m
+
+
+def test_cu_mask_rounds_up_to_granules(native_build):
+    o = run("masks", env={"VGPU_DEVICE_CU_LIMIT_0": "30"})
+    mask = int(o["queue0_mask"], 16)
+    # 30% of 256 = 76.8 → 77 → 80 (10 granules of 8)
+    assert bin(mask).count("1") == 80
+
+
+def test_cu_policy_disable_means_no_mask(native_build):
+    o = run("masks", env={"VGPU_DEVICE_CU_LIMIT_0": "50", "GPU_CORE_UTILIZATION_POLICY": "disable"})
+    assert o["queue0_words"] == "0"
+
+
+def test_cu_mask_respects_visible_devices(native_build):
+    # Two fake GPUs; the container sees only physical GPU 1 as device 0.
+    o = run("masks", env={"VGPU_FAKE_GPUS": "2", "HIP_VISIBLE_DEVICES": "1",
+                          "VGPU_DEVICE_CU_LIMIT_0": "25"})
+    assert o["queues"] == "2"
+    by_agent = {o[f"queue{i}_agent"]: o[f"queue{i}_mask"] for i in range(2)}
+    assert int(by_agent["101"], 16).bit_count() == 64
+    assert by_agent["100"] == ""  # not our device: untouched
+
+
+def test_launch_counting(native_build):
+    o = run("launch", 50, env={"VGPU_DEVICE_MEMORY_LIMIT_0": "1g"})
+    assert o["fake_launches"] == "52"
+    assert o["slot_launches"] == "52"
+
+
+def test_get_proc_address_returns_hook(native_build):
+    o = run("proc_addr", env={"VGPU_DEVICE_MEMORY_LIMIT_0": "1g"})
+    assert o["proc_addr_is_hook"] == "1"
+
+
+def test_oversubscribe_spills_to_host(native_build):
+    # physical 8 GiB, virtual cap 20 GiB: 8 chunks in HBM, the rest in host memory
+    o = run("spill", GiB, 16, env={"VGPU_FAKE_MEM": str(8 * GiB), "VGPU_DEVICE_MEMORY_LIMIT_0": "20g",
+                                   "VGPU_OVERSUBSCRIBE": "true"})
+    assert o["allocated"] == "16" and o["failed"] == "0"
+    assert int(o["physical_used"]) == 8 * GiB
+    assert int(o["slot_host_bytes"]) == 8 * GiB
+
+
+def test_oversubscribe_still_capped(native_build):
+    o = run("spill", GiB, 30, env={"VGPU_FAKE_MEM": str(8 * GiB), "VGPU_DEVICE_MEMORY_LIMIT_0": "20g",
+                                   "VGPU_OVERSUBSCRIBE": "true"})
+    assert o["allocated"] == "20" and o["failed"] == "10"
+
+
+def test_shared_region_cap_across_processes(native_build, tmp_path):
+    """Two processes of one container share the cap through the region file."""
+    region = tmp_path / "r.cache"
+    env = {"VGPU_DEVICE_MEMORY_LIMIT_0": "10g", "VGPU_SHARED_REGION": str(region)}
+    e = {k: v for k, v in os.environ.items() if not k.startswith(("VGPU_", "HIP_"))}
+    e.update(env)
+    e["LD_LIBRARY_PATH"] = str(FAKES_DIR)
+    e["LD_PRELOAD"] = str(shim_path())
+    holder = subprocess.Popen([str(FAKES_DIR / "shim_driver"), "hold", str(6 * GiB), "5"], env=e,
+                              stdout=subprocess.PIPE, text=True)
+    assert holder.stdout.readline().strip() == "hold_rc=0"
+    o = run("fill", GiB, env=env)
+    holder.wait(timeout=30)
+    assert o["allocated"] == "4"  # 10 GiB cap − 6 GiB held by the other process
+
+
+def test_dead_process_charge_is_purged(native_build, tmp_path):
+    region = tmp_path / "r.cache"
+    env = {"VGPU_DEVICE_MEMORY_LIMIT_0": "10g", "VGPU_SHARED_REGION": str(region),
+           "DRIVER_LEAK": "1"}
+    e = {k: v for k, v in os.environ.items() if not k.startswith(("VGPU_", "HIP_"))}
+    e.update(env)
+    e["LD_LIBRARY_PATH"] = str(FAKES_DIR)
+    e["LD_PRELOAD"] = str(shim_path())
+    holder = subprocess.Popen([str(FAKES_DIR / "shim_driver"), "hold", str(8 * GiB), "30"], env=e,
+                              stdout=subprocess.PIPE, text=True)
+    assert holder.stdout.readline().strip() == "hold_rc=0"
+    holder.kill()  # SIGKILL: no exit handler runs, its slot still holds 8 GiB
+    holder.wait()
+    o = run("fill", GiB, env={k: v for k, v in env.items() if k != "DRIVER_LEAK"})
+    assert o["allocated"] == "10"
+
+
+def test_temporal_limiter_throttles_when_forced(native_build, tmp_path):
+    """GPU_CORE_UTILIZATION_POLICY=force + a (fake) utilization signal above the
+    limit must cut the dispatch rate."""
+    util = tmp_path / "util"
+    util.write_text("0 100\n")
+    base = {"VGPU_DEVICE_CU_LIMIT_0": "25", "VGPU_FAKE_UTIL_FILE": str(util),
+            "GPU_CORE_UTILIZATION_POLICY": "force", "VGPU_LIMITER_TICK_MS": "5"}
+    free = run("throttle", 1.5, 64, env={"VGPU_DEVICE_MEMORY_LIMIT_0": "1g"})
+    thr = run("throttle", 1.5, 64, env=base)
+    n_free, n_thr = int(free["launches"]), int(thr["launches"])
+    assert n_thr < n_free * 0.5, (n_free, n_thr)

@@ -1,0 +1,131 @@
+"""Node-local pod launcher: emulates the device plugin's ``Allocate`` for N pods
+sharing one physical GPU, without Kubernetes.
+
+Each pod gets exactly what a scheduled container would get: its own shared
+region file, VGPU_DEVICE_MEMORY_LIMIT_0 / VGPU_DEVICE_CU_LIMIT_0, an
+XCD-balanced CU mask from the same allocator the device plugin uses, and
+LD_PRELOAD of libvgpu.so.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+
+from vgpu.api.env import DeviceGrant, container_env
+from vgpu.device.cualloc import MI355X, alloc_cu_mask
+from vgpu.native import preload_env, shim_path
+
+REPO = Path(__file__).resolve().parents[2]
+
+
+@dataclass
+class PodSpec:
+    workload: str = "1.1"
+    mem_mib: int = 144000
+    cores: int = 50
+    priority: int | None = None
+    extra_env: dict = field(default_factory=dict)
+
+
+def visible_device_for(local_rank: int) -> str:
+    """Device id (in the parent's visible-device numbering) for one rank."""
+    lst = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+    if lst:
+        ids = [s for s in lst.split(",") if s.strip()]
+        return ids[local_rank % len(ids)].strip()
+    return str(local_rank)
+
+
+class Pod:
+    def __init__(self, idx: int, proc: subprocess.Popen, region: str, env: dict):
+        self.idx = idx
+        self.proc = proc
+        self.region = region
+        self.env = env
+        self.ready: dict | None = None
+        self.done: dict | None = None
+
+    def read_tagged(self, tag: str, timeout: float, progress=None) -> dict:
+        """Read stdout lines until `TAG {json}`; raises on EOF or timeout."""
+        import selectors
+        sel = selectors.DefaultSelector()
+        sel.register(self.proc.stdout, selectors.EVENT_READ)
+        deadline = time.monotonic() + timeout
+        last_note = time.monotonic()
+        while True:
+            left = deadline - time.monotonic()
+            if left <= 0:
+                raise TimeoutError(f"pod {self.idx}: no {tag} within {timeout:.0f}s")
+            if not sel.select(timeout=min(left, 30.0)):
+                if progress and time.monotonic() - last_note > 55:
+                    progress(f"pod {self.idx}: waiting for {tag} ...")
+                    last_note = time.monotonic()
+                continue
+            line = self.proc.stdout.readline()
+            if not line:
+                rc = self.proc.wait()
+                raise RuntimeError(f"pod {self.idx} exited (rc={rc}) before {tag}")
+            if line.startswith(tag + " "):
+                return json.loads(line[len(tag) + 1:])
+            sys.stderr.write(f"[pod{self.idx}] {line}")
+
+    def send(self, msg: str) -> None:
+        self.proc.stdin.write(msg + "\n")
+        self.proc.stdin.flush()
+
+
+def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, shim: bool = True,
+                graph: bool = True, cap_probe: bool = False, find: bool = False,
+                workdir: str | None = None, oversubscribe: bool = False) -> list[Pod]:
+    """Start one process per pod on physical device `device`."""
+    workdir = workdir or tempfile.mkdtemp(prefix="vgpu-pods-")
+    used = 0
+    pods = []
+    for i, sp in enumerate(specs):
+        mask = 0
+        if sp.cores and sp.cores < 100:
+            m = alloc_cu_mask(used, sp.cores, MI355X)
+            if m is not None:
+                mask = m
+                used |= m
+        region = str(Path(workdir) / f"pod{i}" / "vgpu.cache")
+        Path(region).parent.mkdir(parents=True, exist_ok=True)
+        grant = DeviceGrant(uuid=f"GPU-{device}", index=int(device) if device.isdigit() else 0,
+                            mem_mib=sp.mem_mib, cores=sp.cores, cu_mask=mask)
+        cenv = container_env([grant], region, priority=sp.priority, oversubscribe=oversubscribe,
+                             visible_var=ENV_PLACEHOLDER)
+        cenv.pop(ENV_PLACEHOLDER, None)
+        env = dict(os.environ)
+        env["HIP_VISIBLE_DEVICES"] = device
+        env.pop("CUDA_VISIBLE_DEVICES", None)
+        env["PYTHONPATH"] = str(REPO) + os.pathsep + env.get("PYTHONPATH", "")
+        env.setdefault("MIOPEN_LOG_LEVEL", "3")
+        if shim:
+            env.update(cenv)
+            env = preload_env(env)
+        env.update(sp.extra_env)
+        cmd = [sys.executable, "-u", "-m", "vgpu.bench.pod", "--workload", sp.workload,
+               "--steps", str(steps), "--warmup", str(warmup), "--pod-index", str(i)]
+        if graph:
+            cmd.append("--graph")
+        if cap_probe:
+            cmd.append("--cap-probe")
+        if find:
+            cmd.append("--find")
+        proc = subprocess.Popen(cmd, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                                text=True, bufsize=1, cwd=str(REPO))
+        pods.append(Pod(i, proc, region, {k: v for k, v in cenv.items()}))
+    return pods
+
+
+ENV_PLACEHOLDER = "__VGPU_UNUSED_VISIBLE__"
+
+
+def shim_available() -> bool:
+    return shim_path().exists()

@@ -1,0 +1,151 @@
+"""One benchmark "pod": an ai-benchmark-equivalent workload running on one
+(v)GPU under the enforcement library, driven by a launcher over stdin/stdout.
+
+Protocol (one JSON object per line on stdout, prefixed):
+    READY {...}   after the untimed warmup and a device synchronize
+    <- "GO"       read from stdin
+    DONE {...}    after exactly `steps` steps and a device synchronize
+Optional post-timing probe (--cap-probe): allocate 1 GiB blocks until the
+vGPU cap refuses, report how close to the cap that got (VRAM-cap accuracy).
+
+Run standalone for debugging:  python -m vgpu.bench.pod --workload 1.1 --steps 5 --no-wait
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+
+def emit(tag: str, obj: dict) -> None:
+    sys.stdout.write(f"{tag} {json.dumps(obj)}\n")
+    sys.stdout.flush()
+
+
+def build(args):
+    import torch
+    from vgpu.models import WORKLOADS
+
+    w = WORKLOADS[args.workload]
+    torch.manual_seed(1234 + args.pod_index)
+    torch.backends.cudnn.benchmark = args.find
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    model = w.builder().to(dev)
+    dtype = torch.bfloat16
+    if w.kind == "image":
+        model = model.to(memory_format=torch.channels_last)
+    model = model.to(dtype)
+    x = w.make_input(dev, dtype)
+    if w.train:
+        model.train()
+        opt = torch.optim.SGD(model.parameters(), lr=1e-3, momentum=0.9)
+        ncls = 21 if w.name == "deeplab" else (2 if w.name == "lstm" else 1000)
+        if w.name == "deeplab":
+            target = torch.randint(0, ncls, (w.batch, *w.shape[1:]), device=dev)
+        else:
+            target = torch.randint(0, ncls, (w.batch,), device=dev)
+        lossf = torch.nn.CrossEntropyLoss()
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            out = model(x)
+            loss = lossf(out.float(), target)
+            loss.backward()
+            opt.step()
+            return loss
+    else:
+        model.eval()
+        if hasattr(model, "fuse_for_inference"):
+            model.fuse_for_inference()
+
+        @torch.inference_mode()
+        def step():
+            return model(x)
+
+    graph = None
+    if args.graph and not w.train:
+        # Warm up on a side stream, then capture one step into a hipGraph:
+        # replays cost one launch instead of hundreds (launch-bound at b≤50).
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                step()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.inference_mode(), torch.cuda.graph(graph):
+            model(x)
+
+        def step():  # noqa: F811
+            graph.replay()
+    return w, step
+
+
+def cap_probe() -> dict:
+    import torch
+    free, total = torch.cuda.mem_get_info()
+    torch.cuda.empty_cache()
+    blocks = []
+    gib = 1 << 30
+    try:
+        while True:
+            blocks.append(torch.empty(gib, dtype=torch.uint8, device="cuda"))
+    except torch.OutOfMemoryError:
+        pass
+    allocated_probe = len(blocks) * gib
+    reserved = torch.cuda.memory_reserved()
+    del blocks
+    torch.cuda.empty_cache()
+    return {"mem_total_reported": total, "probe_bytes": allocated_probe,
+            "reserved_at_oom": reserved}
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="1.1")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--pod-index", type=int, default=0)
+    ap.add_argument("--graph", action="store_true")
+    ap.add_argument("--find", action="store_true", help="cudnn.benchmark (MIOpen find) in warmup")
+    ap.add_argument("--cap-probe", action="store_true")
+    ap.add_argument("--no-wait", action="store_true", help="do not wait for GO on stdin")
+    args = ap.parse_args(argv)
+
+    import torch
+    t_init = time.time()
+    w, step = build(args)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    free, total = torch.cuda.mem_get_info()
+    props = torch.cuda.get_device_properties(0)
+    emit("READY", {"pod": args.pod_index, "init_s": time.time() - t_init, "mem_free": free,
+                   "mem_total": total, "prop_total": props.total_memory,
+                   "cus": props.multi_processor_count, "pid": os.getpid(),
+                   "allocated": torch.cuda.memory_allocated()})
+    if not args.no_wait:
+        line = sys.stdin.readline()
+        if line.strip() != "GO":
+            return 3
+    torch.cuda.synchronize()
+    t0 = time.monotonic()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.monotonic()
+    res = {"pod": args.pod_index, "t0": t0, "t1": t1, "steps": args.steps,
+           "samples": args.steps * w.batch, "ms_per_step": 1e3 * (t1 - t0) / max(args.steps, 1),
+           "throughput": args.steps * w.batch / max(t1 - t0, 1e-9)}
+    if args.cap_probe:
+        res.update(cap_probe())
+    emit("DONE", res)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

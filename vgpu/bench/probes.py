@@ -1,0 +1,87 @@
+"""Device-side probes run inside a (capped) vGPU process; each prints one JSON
+line.  Used by the GPU tests and by the accuracy benchmarks.
+
+  python -m vgpu.bench.probes census [blocks] [spin_ticks]
+      which physical CUs (XCD, SE, SH, CU) the process's workgroups ran on
+  python -m vgpu.bench.probes busy [blocks] [iters] [reps]
+      wall time of a fixed amount of VALU work (compute-share accuracy)
+  python -m vgpu.bench.probes cap [chunk_mib]
+      reported total + how many bytes torch could allocate before OOM
+"""
+from __future__ import annotations
+
+import json
+import sys
+import time
+
+
+def census(blocks: int = 4096, spin: int = 200000) -> dict:
+    import torch
+    from vgpu.ops import kernels as K
+    K.census(64, 100)  # warm the code object
+    torch.cuda.synchronize()
+    xh, ticks = K.census(blocks, spin)
+    torch.cuda.synchronize()
+    xcc = xh[:, 0].cpu()
+    f = K.decode_hw_id(xh[:, 1].cpu())
+    tuples = set(zip(xcc.tolist(), f["se"].tolist(), f["sh"].tolist(), f["cu"].tolist()))
+    per_xcc: dict[int, int] = {}
+    for x, *_ in tuples:
+        per_xcc[x] = per_xcc.get(x, 0) + 1
+    per_se: dict[str, int] = {}
+    for x, se, sh, cu in tuples:
+        k = f"{x}.{se}"
+        per_se[k] = per_se.get(k, 0) + 1
+    return {"distinct_cus": len(tuples), "per_xcc": {str(k): v for k, v in sorted(per_xcc.items())},
+            "per_se": per_se, "blocks": blocks,
+            "cus_prop": torch.cuda.get_device_properties(0).multi_processor_count}
+
+
+def busy(blocks: int = 8192, iters: int = 20000, reps: int = 5) -> dict:
+    import torch
+    from vgpu.ops import kernels as K
+    K.busy(blocks, 100)
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        K.busy(blocks, iters)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    return {"blocks": blocks, "iters": iters, "times": times, "median_s": sorted(times)[len(times) // 2]}
+
+
+def cap(chunk_mib: int = 1024) -> dict:
+    import torch
+    free, total = torch.cuda.mem_get_info()
+    props = torch.cuda.get_device_properties(0)
+    blocks = []
+    try:
+        while True:
+            blocks.append(torch.empty(chunk_mib << 20, dtype=torch.uint8, device="cuda"))
+    except torch.OutOfMemoryError:
+        pass
+    res = {"free": free, "total": total, "prop_total": props.total_memory,
+           "allocated": len(blocks) * (chunk_mib << 20), "reserved": torch.cuda.memory_reserved()}
+    # touch everything: prove the bytes are real
+    from vgpu.ops import kernels as K
+    errs = 0
+    for i, b in enumerate(blocks):
+        K.fill_pattern(b, i + 1)
+    for i, b in enumerate(blocks):
+        errs += K.verify_pattern(b, i + 1)
+    res["verify_errors"] = errs
+    return res
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    cmd = argv.pop(0) if argv else "census"
+    nums = [int(a) for a in argv]
+    out = {"census": census, "busy": busy, "cap": cap}[cmd](*nums)
+    print("PROBE " + json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

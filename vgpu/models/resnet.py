@@ -1,0 +1,104 @@
+"""ResNet-V2 (pre-activation) — the ai-benchmark ResNet-V2-50 / ResNet-V2-152
+workloads the reference publishes numbers for (BASELINE.md rows 1.x / 2.x;
+reference README.md:244-247: ResNet-V2-50 b=50 346² inference, b=20 346²
+training; ResNet-V2-152 b=10 256²).
+
+Random init, NCHW module layout run in channels_last memory format so MIOpen
+picks its NHWC (CK) kernels on gfx950.  `fuse_for_inference()` folds every
+BatchNorm that directly follows a convolution into that convolution's weights,
+leaving only the block-entry pre-activation BNs (which sit after a residual
+add and cannot be folded).
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+
+class PreActBottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin: int, width: int, stride: int):
+        super().__init__()
+        cout = width * self.expansion
+        self.bn_in = nn.BatchNorm2d(cin)
+        self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
+        self.shortcut = None
+        if stride != 1 or cin != cout:
+            self.shortcut = nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+        self.fused = False
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        pre = F.relu(self.bn_in(x))
+        sc = self.shortcut(pre) if self.shortcut is not None else x
+        if self.fused:
+            y = F.relu(self.conv1(pre))
+            y = F.relu(self.conv2(y))
+        else:
+            y = F.relu(self.bn1(self.conv1(pre)))
+            y = F.relu(self.bn2(self.conv2(y)))
+        return self.conv3(y) + sc
+
+
+def _fold_bn(conv: nn.Conv2d, bn: nn.BatchNorm2d) -> nn.Conv2d:
+    w = conv.weight.detach()
+    scale = bn.weight.detach() / torch.sqrt(bn.running_var + bn.eps)
+    new = nn.Conv2d(conv.in_channels, conv.out_channels, conv.kernel_size, conv.stride,
+                    conv.padding, conv.dilation, conv.groups, bias=True)
+    new.weight.data = (w * scale.reshape(-1, 1, 1, 1)).to(w.dtype)
+    b = conv.bias.detach() if conv.bias is not None else torch.zeros_like(bn.running_mean)
+    new.bias.data = ((b - bn.running_mean) * scale + bn.bias.detach()).to(w.dtype)
+    return new.to(w.device)
+
+
+class ResNetV2(nn.Module):
+    def __init__(self, layers: list[int], num_classes: int = 1000):
+        super().__init__()
+        self.stem = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.pool = nn.MaxPool2d(3, stride=2, padding=1)
+        blocks = []
+        cin = 64
+        for i, (n, width) in enumerate(zip(layers, (64, 128, 256, 512))):
+            for j in range(n):
+                stride = 2 if (j == 0 and i > 0) else 1
+                blocks.append(PreActBottleneck(cin, width, stride))
+                cin = width * PreActBottleneck.expansion
+        self.blocks = nn.Sequential(*blocks)
+        self.bn_out = nn.BatchNorm2d(cin)
+        self.fc = nn.Linear(cin, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.pool(self.stem(x))
+        x = self.blocks(x)
+        x = F.relu(self.bn_out(x))
+        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        return self.fc(x)
+
+    @torch.no_grad()
+    def fuse_for_inference(self) -> "ResNetV2":
+        for b in self.blocks:
+            b.conv1 = _fold_bn(b.conv1, b.bn1)
+            b.conv2 = _fold_bn(b.conv2, b.bn2)
+            b.bn1 = nn.Identity()
+            b.bn2 = nn.Identity()
+            b.fused = True
+        return self
+
+
+def resnet_v2_50(num_classes: int = 1000) -> ResNetV2:
+    return ResNetV2([3, 4, 6, 3], num_classes)
+
+
+def resnet_v2_152(num_classes: int = 1000) -> ResNetV2:
+    return ResNetV2([3, 8, 36, 3], num_classes)

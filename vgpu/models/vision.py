@@ -1,0 +1,133 @@
+"""VGG-16 and DeepLab-v3 (MobileNet-V2 backbone + ASPP) for the
+ai-benchmark-equivalent suite (reference
+README.md:248-251: VGG-16 b=20 224² inference / b=2 training, DeepLab b=2 512²
+inference / b=1 384² training).
+
+The reference measured TF-1 ai-benchmark graphs whose exact DeepLab variant
+is not recorded in the repository, so the DeepLab here is architecture-
+equivalent (parity unpinned); all weights are random-init.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+
+class VGG16(nn.Module):
+    cfg = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512, "M"]
+
+    def __init__(self, num_classes: int = 1000):
+        super().__init__()
+        layers: list[nn.Module] = []
+        cin = 3
+        for v in self.cfg:
+            if v == "M":
+                layers.append(nn.MaxPool2d(2, 2))
+            else:
+                layers += [nn.Conv2d(cin, v, 3, padding=1), nn.ReLU(inplace=True)]
+                cin = v
+        self.features = nn.Sequential(*layers)
+        self.pool = nn.AdaptiveAvgPool2d((7, 7))
+        self.classifier = nn.Sequential(
+            nn.Linear(512 * 7 * 7, 4096), nn.ReLU(inplace=True),
+            nn.Linear(4096, 4096), nn.ReLU(inplace=True),
+            nn.Linear(4096, num_classes))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.pool(self.features(x))
+        return self.classifier(torch.flatten(x, 1))
+
+
+def _conv_bn(cin: int, cout: int, k: int, stride: int = 1, groups: int = 1, dilation: int = 1,
+             act: bool = True) -> nn.Sequential:
+    pad = dilation * (k - 1) // 2
+    mods: list[nn.Module] = [nn.Conv2d(cin, cout, k, stride, pad, dilation=dilation, groups=groups,
+                                       bias=False), nn.BatchNorm2d(cout)]
+    if act:
+        mods.append(nn.ReLU6(inplace=True))
+    return nn.Sequential(*mods)
+
+
+class InvertedResidual(nn.Module):
+    def __init__(self, cin: int, cout: int, stride: int, expand: int, dilation: int = 1):
+        super().__init__()
+        hid = cin * expand
+        self.use_res = stride == 1 and cin == cout
+        layers: list[nn.Module] = []
+        if expand != 1:
+            layers.append(_conv_bn(cin, hid, 1))
+        layers += [_conv_bn(hid, hid, 3, stride, groups=hid, dilation=dilation),
+                   _conv_bn(hid, cout, 1, act=False)]
+        self.body = nn.Sequential(*layers)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        y = self.body(x)
+        return x + y if self.use_res else y
+
+
+class MobileNetV2Backbone(nn.Module):
+    # (expand, channels, repeats, stride) — output stride 16 with dilation in the last stages
+    settings = [(1, 16, 1, 1), (6, 24, 2, 2), (6, 32, 3, 2), (6, 64, 4, 2), (6, 96, 3, 1),
+                (6, 160, 3, 1), (6, 320, 1, 1)]
+
+    def __init__(self):
+        super().__init__()
+        layers: list[nn.Module] = [_conv_bn(3, 32, 3, 2)]
+        cin = 32
+        dilation = 1
+        for i, (t, c, n, s) in enumerate(self.settings):
+            if i >= 5:
+                dilation = 2
+            for j in range(n):
+                layers.append(InvertedResidual(cin, c, s if j == 0 else 1, t, dilation if j else 1))
+                cin = c
+        self.features = nn.Sequential(*layers)
+        self.out_channels = cin
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.features(x)
+
+
+class ASPP(nn.Module):
+    def __init__(self, cin: int, cout: int = 256, rates=(6, 12, 18)):
+        super().__init__()
+        self.branches = nn.ModuleList([_conv_bn(cin, cout, 1)] +
+                                      [_conv_bn(cin, cout, 3, dilation=r) for r in rates])
+        self.image_pool = nn.Sequential(nn.AdaptiveAvgPool2d(1), nn.Conv2d(cin, cout, 1, bias=False),
+                                        nn.ReLU(inplace=True))
+        self.project = _conv_bn(cout * (len(rates) + 2), cout, 1)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        h, w = x.shape[-2:]
+        feats = [b(x) for b in self.branches]
+        feats.append(F.interpolate(self.image_pool(x), size=(h, w), mode="bilinear",
+                                   align_corners=False))
+        return self.project(torch.cat(feats, dim=1))
+
+
+class DeepLabV3(nn.Module):
+    def __init__(self, num_classes: int = 21):
+        super().__init__()
+        self.backbone = MobileNetV2Backbone()
+        self.aspp = ASPP(self.backbone.out_channels)
+        self.head = nn.Conv2d(256, num_classes, 1)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        h, w = x.shape[-2:]
+        y = self.head(self.aspp(self.backbone(x)))
+        return F.interpolate(y, size=(h, w), mode="bilinear", align_corners=False)
+
+
+class LSTMSentiment(nn.Module):
+    """ai-benchmark "LSTM-Sentiment": 1024-token sequences of 300-d embeddings
+    (reference README.md:252-253: inference b=100, training b=10)."""
+
+    def __init__(self, emb: int = 300, hidden: int = 128, layers: int = 2, num_classes: int = 2):
+        super().__init__()
+        self.lstm = nn.LSTM(emb, hidden, num_layers=layers, batch_first=True)
+        self.fc = nn.Linear(hidden, num_classes)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        y, _ = self.lstm(x)
+        return self.fc(y[:, -1])

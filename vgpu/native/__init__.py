@@ -1,0 +1,120 @@
+"""Locating and loading the in-tree native artefacts (vgpu/_lib).
+
+The kernels library must be loaded AFTER torch so that its NEEDED
+libamdhip64.so.7 binds to the HIP runtime PyTorch already loaded (same SONAME)
+instead of pulling in a second runtime.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+LIB_DIR = Path(__file__).resolve().parents[1] / "_lib"
+FAKES_DIR = LIB_DIR / "fakes"
+
+
+class NativeMissing(RuntimeError):
+    pass
+
+
+def lib_path(name: str) -> Path:
+    return LIB_DIR / name
+
+
+def shim_path() -> Path:
+    return lib_path("libvgpu.so")
+
+
+def ensure_built(kernels: bool = True) -> None:
+    """Build whatever is missing (hipcc/g++ are in the image on the GPU box too)."""
+    need = not shim_path().exists() or (kernels and not lib_path("libvgpu_kernels.so").exists())
+    if need:
+        from . import build
+        build.build_all(kernels=kernels)
+
+
+_kernels = None
+_capi = None
+
+
+def load_kernels() -> ctypes.CDLL:
+    """Load libvgpu_kernels.so; raises NativeMissing (never falls back)."""
+    global _kernels
+    if _kernels is not None:
+        return _kernels
+    import torch  # noqa: F401  (must precede: bind to torch's HIP runtime)
+    p = lib_path("libvgpu_kernels.so")
+    if not p.exists():
+        raise NativeMissing(f"{p} not built: run `python -m vgpu.native.build kernels`")
+    lib = ctypes.CDLL(str(p), mode=ctypes.RTLD_GLOBAL)
+    vp, u32, u64, i64p = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p
+    lib.vgpu_census.argtypes = [vp, u32, u64, vp, vp]
+    lib.vgpu_busy.argtypes = [vp, u32, u32, vp]
+    lib.vgpu_gather_pages.argtypes = [vp, vp, i64p, u64, u64, vp]
+    lib.vgpu_scatter_pages.argtypes = [vp, vp, i64p, u64, u64, vp]
+    lib.vgpu_fill_pattern.argtypes = [vp, u64, u32, vp]
+    lib.vgpu_verify_pattern.argtypes = [vp, u64, u32, vp, vp]
+    for f in ("vgpu_census", "vgpu_busy", "vgpu_gather_pages", "vgpu_scatter_pages",
+              "vgpu_fill_pattern", "vgpu_verify_pattern", "vgpu_kernels_abi_version"):
+        getattr(lib, f).restype = ctypes.c_int
+    _kernels = lib
+    return lib
+
+
+class RegionLayout(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "region_size", "proc_slot_size", "dev_usage_size", "device_cfg_size", "off_lock",
+        "off_num_devices", "off_recent_kernel", "off_dev", "off_procs", "mutex_size")]
+
+
+def load_capi() -> ctypes.CDLL:
+    """libvgpu.so's C ABI (region attach/lock/feedback) for the node monitor and tests.
+    Loading it into a process without HIP is harmless: hooks stay dormant."""
+    global _capi
+    if _capi is not None:
+        return _capi
+    p = shim_path()
+    if not p.exists():
+        raise NativeMissing(f"{p} not built: run `python -m vgpu.native.build shim`")
+    lib = ctypes.CDLL(str(p))
+    vp, ci, cu64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64
+    lib.vgpu_region_layout.argtypes = [ctypes.POINTER(RegionLayout)]
+    lib.vgpu_region_create.argtypes = [ctypes.c_char_p]
+    lib.vgpu_region_create.restype = vp
+    lib.vgpu_region_attach.argtypes = [ctypes.c_char_p]
+    lib.vgpu_region_attach.restype = vp
+    lib.vgpu_region_detach.argtypes = [vp]
+    lib.vgpu_region_lock.argtypes = [vp]
+    lib.vgpu_region_unlock.argtypes = [vp]
+    lib.vgpu_region_purge.argtypes = [vp, ci]
+    lib.vgpu_region_claim.argtypes = [vp, ci, ci, ci]
+    lib.vgpu_region_release.argtypes = [vp, ci]
+    lib.vgpu_region_device_used.argtypes = [vp, ci]
+    lib.vgpu_region_device_used.restype = cu64
+    lib.vgpu_region_set_feedback.argtypes = [vp, ci, ci, ci]
+    lib.vgpu_region_decay_recent.argtypes = [vp]
+    lib.vgpu_region_set_cu_mask.argtypes = [vp, ci, ctypes.POINTER(ctypes.c_uint64)]
+    lib.vgpu_region_signal_all.argtypes = [vp, ci, ci]
+    lib.vgpu_parse_mem.argtypes = [ctypes.c_char_p]
+    lib.vgpu_parse_mem.restype = cu64
+    lib.vgpu_parse_cu_mask.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64), ci]
+    _capi = lib
+    return lib
+
+
+def region_layout() -> dict[str, int]:
+    lib = load_capi()
+    lay = RegionLayout()
+    lib.vgpu_region_layout(ctypes.byref(lay))
+    return {n: getattr(lay, n) for n, _ in RegionLayout._fields_}
+
+
+def preload_env(base: dict[str, str] | None = None) -> dict[str, str]:
+    """Environment for a child process running under the enforcement library."""
+    env = dict(os.environ if base is None else base)
+    cur = env.get("LD_PRELOAD", "")
+    sp = str(shim_path())
+    if sp not in cur.split():
+        env["LD_PRELOAD"] = (sp + " " + cur).strip()
+    return env
