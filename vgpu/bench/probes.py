@@ -63,6 +63,10 @@ def cap(chunk_mib: int = 1024) -> dict:
         pass
     res = {"free": free, "total": total, "prop_total": props.total_memory,
            "allocated": len(blocks) * (chunk_mib << 20), "reserved": torch.cuda.memory_reserved()}
+    # release one chunk so the verification's own small buffers fit under the cap
+    if blocks:
+        blocks.pop()
+        torch.cuda.empty_cache()
     # touch everything: prove the bytes are real
     from vgpu.ops import kernels as K
     errs = 0
