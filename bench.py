@@ -48,7 +48,11 @@ def main(argv=None) -> int:
     ap.add_argument("--gpucores", type=int, default=50, help="per-pod amd.com/gpucores (%%)")
     ap.add_argument("--no-shim", action="store_true", help="run pods without enforcement")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--find", action="store_true", help="MIOpen find (cudnn.benchmark) in warmup")
+    ap.add_argument("--no-find", action="store_true",
+                    help="skip MIOpen find (cudnn.benchmark) during the untimed warmup")
+    ap.add_argument("--no-fused", action="store_true", help="plain PyTorch epilogues")
+    ap.add_argument("--hw-queues", type=int, default=1,
+                    help="GPU_MAX_HW_QUEUES per pod (vGPU HW-queue budget; 0 = runtime default)")
     ap.add_argument("--no-cap-probe", action="store_true")
     ap.add_argument("--ready-timeout", type=float, default=1500.0)
     args = ap.parse_args(argv)
@@ -65,7 +69,7 @@ def main(argv=None) -> int:
     from vgpu.models import WORKLOADS
 
     if not args.no_shim:
-        ensure_built(kernels=False)
+        ensure_built(kernels=True)
     w = WORKLOADS[args.workload]
 
     pg = None
@@ -80,7 +84,9 @@ def main(argv=None) -> int:
              for _ in range(args.pods)]
     log(f"rank {rank}/{world}: launching {args.pods} pods of {w.name} (test {w.test_id}) on device {device}")
     pods = launch_pods(specs, device, steps=args.steps, warmup=args.warmup, shim=not args.no_shim,
-                       graph=not args.no_graph, cap_probe=not args.no_cap_probe, find=args.find)
+                       graph=not args.no_graph, cap_probe=not args.no_cap_probe,
+                       find=not args.no_find, hw_queues=args.hw_queues or None,
+                       fused=not args.no_fused)
     try:
         for p in pods:
             p.ready = p.read_tagged("READY", args.ready_timeout, progress=log)
@@ -149,6 +155,9 @@ def main(argv=None) -> int:
                 "gpucores": args.gpucores,
                 "enforcement": "none" if args.no_shim else "libvgpu.so (HBM cap + XCD-balanced CU mask)",
                 "hipgraph": not args.no_graph,
+                "miopen_find": not args.no_find,
+                "fused_epilogues": not args.no_fused,
+                "hw_queues_per_pod": args.hw_queues,
             },
             "per_gpu_images_s": round(per_gpu, 2),
             "per_pod_images_s": [round(p.done["throughput"], 2) for p in pods],

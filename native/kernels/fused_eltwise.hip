@@ -1,0 +1,180 @@
+// Fused NHWC bf16 epilogue kernels for the ai-benchmark CNN workloads on MI355X.
+//
+// Why: with BatchNorm folded into the convolution weights, a pre-activation
+// ResNet bottleneck still needs bias → ReLU after conv1 and conv2 and
+// residual-add → BN → ReLU after conv3.  As separate PyTorch / MIOpen ops that
+// is 7 full passes over the activation per block (MIOpen's bias kernel alone
+// costs ~4x the 1x1 convolution it follows on gfx950, measured in
+// vgpu/bench/convbench.py).  These kernels do it in 3 passes:
+//
+//   bias_act:             x <- act(x + bias[c])                      (in place)
+//   scale_shift_act:      y <- act(x * scale[c] + shift[c])
+//   add_scale_shift_act:  s <- a + b ; y <- act(s * scale[c] + shift[c])  (dual output)
+//
+// Memory-bound: 16 B per lane per access (8 bf16), fp32 math, per-channel
+// parameters read through the vector L1 (tiny, shared by every row), grid
+// capped at 256 CUs x 8 workgroups with a grid-stride loop.  Requires C % 8 == 0
+// and 16-B aligned tensors (checked on the host).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define VGPU_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxGrid = 256 * 8;
+
+struct alignas(16) bf16x8 {
+  uint16_t v[8];
+};
+
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  // v_cvt_pk_bf16_f32 on gfx950 (round-to-nearest-even, NaN-preserving)
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+template <int kAct>
+__device__ __forceinline__ float act(float x) {
+  if constexpr (kAct == 1) return fmaxf(x, 0.0f);
+  if constexpr (kAct == 2) return fminf(fmaxf(x, 0.0f), 6.0f);
+  return x;
+}
+
+__device__ __forceinline__ void load8(const float* __restrict__ p, float (&o)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+  o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+
+// Channel-group index tracked incrementally: one 64-bit modulo per thread,
+// then a compare-and-subtract per grid-stride step.
+#define VGPU_GRID_LOOP(i, ci, nvec, cvec)                                          \
+  const uint64_t stride_ = (uint64_t)gridDim.x * kThreads;                         \
+  const uint32_t cstep_ = (uint32_t)(stride_ % (cvec));                            \
+  uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;                      \
+  uint32_t ci = (uint32_t)(i % (cvec));                                            \
+  for (; i < (nvec); i += stride_, ci = (ci + cstep_ >= (cvec)) ? ci + cstep_ - (cvec) : ci + cstep_)
+
+template <int kAct>
+__global__ void __launch_bounds__(kThreads) bias_act_kernel(bf16x8* __restrict__ x,
+                                                            const float* __restrict__ bias,
+                                                            uint64_t nvec, uint32_t cvec) {
+  VGPU_GRID_LOOP(i, ci, nvec, cvec) {
+    bf16x8 v = x[i];
+    float bb[8];
+    load8(bias + ci * 8, bb);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v.v[k] = f2bf(act<kAct>(bf2f(v.v[k]) + bb[k]));
+    x[i] = v;
+  }
+}
+
+template <int kAct>
+__global__ void __launch_bounds__(kThreads) scale_shift_act_kernel(
+    const bf16x8* __restrict__ x, bf16x8* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, uint64_t nvec, uint32_t cvec) {
+  VGPU_GRID_LOOP(i, ci, nvec, cvec) {
+    const bf16x8 v = x[i];
+    float sc[8], sh[8];
+    load8(scale + ci * 8, sc);
+    load8(shift + ci * 8, sh);
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.v[k] = f2bf(act<kAct>(bf2f(v.v[k]) * sc[k] + sh[k]));
+    y[i] = o;
+  }
+}
+
+template <int kAct>
+__global__ void __launch_bounds__(kThreads) add_scale_shift_act_kernel(
+    const bf16x8* __restrict__ a, const bf16x8* __restrict__ b, bf16x8* __restrict__ s_out,
+    bf16x8* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
+    uint64_t nvec, uint32_t cvec) {
+  VGPU_GRID_LOOP(i, ci, nvec, cvec) {
+    const bf16x8 va = a[i];
+    const bf16x8 vb = b[i];
+    float sc[8], sh[8];
+    load8(scale + ci * 8, sc);
+    load8(shift + ci * 8, sh);
+    bf16x8 s, o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      // the residual stream is stored in bf16: round the sum once, and derive
+      // the activation from the rounded value (what an unfused graph computes)
+      const uint16_t sk = f2bf(bf2f(va.v[k]) + bf2f(vb.v[k]));
+      s.v[k] = sk;
+      o.v[k] = f2bf(act<kAct>(bf2f(sk) * sc[k] + sh[k]));
+    }
+    s_out[i] = s;
+    y[i] = o;
+  }
+}
+
+inline unsigned grid_for(uint64_t nvec) {
+  uint64_t g = (nvec + kThreads - 1) / kThreads;
+  if (g < 1) g = 1;
+  if (g > kMaxGrid) g = kMaxGrid;
+  return (unsigned)g;
+}
+
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+// act: 0 = identity, 1 = relu, 2 = relu6.  n = total elements, c = channels.
+VGPU_API int vgpu_bias_act_nhwc(void* x, const float* bias, uint64_t n, uint32_t c, int act,
+                                void* stream) {
+  if (c % 8 || n % c || !aligned16(x) || !aligned16(bias)) return (int)hipErrorInvalidValue;
+  const uint64_t nvec = n / 8;
+  const uint32_t cvec = c / 8;
+  auto* xv = (bf16x8*)x;
+  switch (act) {
+    case 0: hipLaunchKernelGGL(bias_act_kernel<0>, dim3(grid_for(nvec)), dim3(kThreads), 0, (hipStream_t)stream, xv, bias, nvec, cvec); break;
+    case 1: hipLaunchKernelGGL(bias_act_kernel<1>, dim3(grid_for(nvec)), dim3(kThreads), 0, (hipStream_t)stream, xv, bias, nvec, cvec); break;
+    case 2: hipLaunchKernelGGL(bias_act_kernel<2>, dim3(grid_for(nvec)), dim3(kThreads), 0, (hipStream_t)stream, xv, bias, nvec, cvec); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+VGPU_API int vgpu_scale_shift_act_nhwc(const void* x, void* y, const float* scale, const float* shift,
+                                       uint64_t n, uint32_t c, int act, void* stream) {
+  if (c % 8 || n % c || !aligned16(x) || !aligned16(y) || !aligned16(scale) || !aligned16(shift)) return (int)hipErrorInvalidValue;
+  const uint64_t nvec = n / 8;
+  const uint32_t cvec = c / 8;
+  auto* xv = (const bf16x8*)x;
+  auto* yv = (bf16x8*)y;
+  switch (act) {
+    case 0: hipLaunchKernelGGL(scale_shift_act_kernel<0>, dim3(grid_for(nvec)), dim3(kThreads), 0, (hipStream_t)stream, xv, yv, scale, shift, nvec, cvec); break;
+    case 1: hipLaunchKernelGGL(scale_shift_act_kernel<1>, dim3(grid_for(nvec)), dim3(kThreads), 0, (hipStream_t)stream, xv, yv, scale, shift, nvec, cvec); break;
+    case 2: hipLaunchKernelGGL(scale_shift_act_kernel<2>, dim3(grid_for(nvec)), dim3(kThreads), 0, (hipStream_t)stream, xv, yv, scale, shift, nvec, cvec); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+VGPU_API int vgpu_add_scale_shift_act_nhwc(const void* a, const void* b, void* s_out, void* y,
+                                           const float* scale, const float* shift, uint64_t n,
+                                           uint32_t c, int act, void* stream) {
+  if (c % 8 || n % c || !aligned16(a) || !aligned16(b) || !aligned16(s_out) || !aligned16(y) ||
+      !aligned16(scale) || !aligned16(shift))
+    return (int)hipErrorInvalidValue;
+  const uint64_t nvec = n / 8;
+  const uint32_t cvec = c / 8;
+  auto* av = (const bf16x8*)a;
+  auto* bv = (const bf16x8*)b;
+  auto* sv = (bf16x8*)s_out;
+  auto* yv = (bf16x8*)y;
+  switch (act) {
+    case 0: hipLaunchKernelGGL(add_scale_shift_act_kernel<0>, dim3(grid_for(nvec)), dim3(kThreads), 0, (hipStream_t)stream, av, bv, sv, yv, scale, shift, nvec, cvec); break;
+    case 1: hipLaunchKernelGGL(add_scale_shift_act_kernel<1>, dim3(grid_for(nvec)), dim3(kThreads), 0, (hipStream_t)stream, av, bv, sv, yv, scale, shift, nvec, cvec); break;
+    case 2: hipLaunchKernelGGL(add_scale_shift_act_kernel<2>, dim3(grid_for(nvec)), dim3(kThreads), 0, (hipStream_t)stream, av, bv, sv, yv, scale, shift, nvec, cvec); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}

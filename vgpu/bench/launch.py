@@ -82,7 +82,8 @@ class Pod:
 
 def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, shim: bool = True,
                 graph: bool = True, cap_probe: bool = False, find: bool = False,
-                workdir: str | None = None, oversubscribe: bool = False) -> list[Pod]:
+                workdir: str | None = None, oversubscribe: bool = False,
+                hw_queues: int | None = None, fused: bool = True) -> list[Pod]:
     """Start one process per pod on physical device `device`."""
     workdir = workdir or tempfile.mkdtemp(prefix="vgpu-pods-")
     used = 0
@@ -106,6 +107,9 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
         env.pop("CUDA_VISIBLE_DEVICES", None)
         env["PYTHONPATH"] = str(REPO) + os.pathsep + env.get("PYTHONPATH", "")
         env.setdefault("MIOPEN_LOG_LEVEL", "3")
+        if hw_queues:
+            # HW-queue budget of a fractional vGPU (see vgpu/deviceplugin/allocate.py)
+            env["GPU_MAX_HW_QUEUES"] = str(hw_queues)
         if shim:
             env.update(cenv)
             env = preload_env(env)
@@ -118,6 +122,8 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
             cmd.append("--cap-probe")
         if find:
             cmd.append("--find")
+        if not fused:
+            cmd.append("--no-fused")
         proc = subprocess.Popen(cmd, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                 text=True, bufsize=1, cwd=str(REPO))
         pods.append(Pod(i, proc, region, {k: v for k, v in cenv.items()}))

@@ -58,7 +58,10 @@ def build(args):
             return loss
     else:
         model.eval()
-        if hasattr(model, "fuse_for_inference"):
+        from vgpu.models.resnet import FusedResNetV2Inference, ResNetV2
+        if isinstance(model, ResNetV2) and not args.no_fused:
+            model = FusedResNetV2Inference(model)
+        elif hasattr(model, "fuse_for_inference"):
             model.fuse_for_inference()
 
         @torch.inference_mode()
@@ -113,6 +116,7 @@ def main(argv=None) -> int:
     ap.add_argument("--graph", action="store_true")
     ap.add_argument("--find", action="store_true", help="cudnn.benchmark (MIOpen find) in warmup")
     ap.add_argument("--cap-probe", action="store_true")
+    ap.add_argument("--no-fused", action="store_true", help="plain PyTorch epilogues (no HIP fusion)")
     ap.add_argument("--no-wait", action="store_true", help="do not wait for GO on stdin")
     args = ap.parse_args(argv)
 

@@ -96,6 +96,67 @@ class ResNetV2(nn.Module):
         return self
 
 
+class FusedResNetV2Inference(nn.Module):
+    """Inference runner for a ResNetV2 with every BN folded and every
+    bias / ReLU / residual-add / pre-activation BN done by the fused NHWC HIP
+    epilogues (vgpu.ops.fused): 3 activation passes per bottleneck instead of 7,
+    and no MIOpen bias kernels (convolutions run bias-free).
+
+    Numerically equivalent to `ResNetV2.eval()` up to bf16 rounding of the
+    folded weights (tests/test_gpu_fused.py).
+    """
+
+    def __init__(self, m: ResNetV2):
+        super().__init__()
+        from vgpu.ops.fused import bn_scale_shift
+        m = m.eval()
+        dt = m.stem.weight.dtype
+        cl = torch.channels_last
+
+        def fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
+            scale = bn.weight.float() / torch.sqrt(bn.running_var.float() + bn.eps)
+            w = (conv.weight.float() * scale.reshape(-1, 1, 1, 1)).to(dt).contiguous(memory_format=cl)
+            b = (bn.bias.float() - bn.running_mean.float() * scale).contiguous()
+            return w, b
+
+        with torch.no_grad():
+            self.stem_w = m.stem.weight.detach().contiguous(memory_format=cl)
+            self.blocks = []
+            for blk in m.blocks:
+                w1, b1 = fold(blk.conv1, blk.bn1)
+                w2, b2 = fold(blk.conv2, blk.bn2)
+                self.blocks.append({
+                    "in": bn_scale_shift(blk.bn_in),
+                    "w1": w1, "b1": b1, "w2": w2, "b2": b2,
+                    "stride": blk.conv2.stride[0],
+                    "w3": blk.conv3.weight.detach().contiguous(memory_format=cl),
+                    "sc": None if blk.shortcut is None else
+                    (blk.shortcut.weight.detach().contiguous(memory_format=cl), blk.shortcut.stride[0]),
+                })
+            self.out_ss = bn_scale_shift(m.bn_out)
+            self.fc = m.fc
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        from vgpu.ops.fused import add_scale_shift_act, bias_act_, scale_shift_act
+        x = F.max_pool2d(F.conv2d(x, self.stem_w, stride=2, padding=3), 3, 2, 1)
+        x = x.contiguous(memory_format=torch.channels_last)
+        pre = scale_shift_act(x, *self.blocks[0]["in"])
+        n = len(self.blocks)
+        for i, b in enumerate(self.blocks):
+            if b["sc"] is None:
+                sc = x
+            else:
+                sc = F.conv2d(pre, b["sc"][0], stride=b["sc"][1])
+            h = bias_act_(F.conv2d(pre, b["w1"]), b["b1"])
+            h = bias_act_(F.conv2d(h, b["w2"], stride=b["stride"], padding=1), b["b2"])
+            h = F.conv2d(h, b["w3"])
+            nss = self.blocks[i + 1]["in"] if i + 1 < n else self.out_ss
+            x, pre = add_scale_shift_act(h, sc, *nss)
+        pooled = pre.mean(dim=(2, 3))
+        return self.fc(pooled)
+
+
 def resnet_v2_50(num_classes: int = 1000) -> ResNetV2:
     return ResNetV2([3, 4, 6, 3], num_classes)
 

@@ -55,8 +55,12 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_scatter_pages.argtypes = [vp, vp, i64p, u64, u64, vp]
     lib.vgpu_fill_pattern.argtypes = [vp, u64, u32, vp]
     lib.vgpu_verify_pattern.argtypes = [vp, u64, u32, vp, vp]
+    lib.vgpu_bias_act_nhwc.argtypes = [vp, vp, u64, u32, ctypes.c_int, vp]
+    lib.vgpu_scale_shift_act_nhwc.argtypes = [vp, vp, vp, vp, u64, u32, ctypes.c_int, vp]
+    lib.vgpu_add_scale_shift_act_nhwc.argtypes = [vp, vp, vp, vp, vp, vp, u64, u32, ctypes.c_int, vp]
     for f in ("vgpu_census", "vgpu_busy", "vgpu_gather_pages", "vgpu_scatter_pages",
-              "vgpu_fill_pattern", "vgpu_verify_pattern", "vgpu_kernels_abi_version"):
+              "vgpu_fill_pattern", "vgpu_verify_pattern", "vgpu_kernels_abi_version",
+              "vgpu_bias_act_nhwc", "vgpu_scale_shift_act_nhwc", "vgpu_add_scale_shift_act_nhwc"):
         getattr(lib, f).restype = ctypes.c_int
     _kernels = lib
     return lib
