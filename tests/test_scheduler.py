@@ -1,0 +1,392 @@
+"""Scheduler extender: scoring semantics, webhook, node lock, handshake and
+end-to-end Filter/Bind against the in-process fake API server (the reference
+leaves all of this untested — SURVEY.md §4)."""
+import base64
+import datetime as dt
+import json
+import threading
+
+import pytest
+
+from vgpu import config
+from vgpu.api import resources as R
+from vgpu.api.codec import NODE_REGISTER_EXT, decode_pod_devices, encode_node_devices, encode_node_devices_ext
+from vgpu.api.resources import ContainerDeviceRequest, DeviceInfo, DeviceUsage
+from vgpu.device.base import init_default_devices, resource_reqs
+from vgpu.k8s.client import KubeClient
+from vgpu.k8s.fakeapi import FakeApiServer
+from vgpu.k8s.nodelock import NodeLockError, lock_node, release_node_lock
+from vgpu.scheduler.core import HANDSHAKE_TIME_FMT, Scheduler
+from vgpu.scheduler.score import NodeUsage, calc_score, fit_in_certain_device, FitError, pick_node
+from vgpu.scheduler.webhook import handle_admission
+
+MIB_288G = 294912
+
+
+@pytest.fixture(autouse=True)
+def _devices():
+    init_default_devices(fake=True)
+    saved = config.SCHEDULER
+    config.SCHEDULER = config.SchedulerConfig()
+    yield
+    config.SCHEDULER = saved
+
+
+def usage(n, count=10, mem=MIB_288G, core=100, numa=None, hive=""):
+    return [DeviceUsage(id=f"GPU-{i}", index=i, used=0, count=count, usedmem=0, totalmem=mem,
+                        usedcores=0, totalcore=core, type="AMD-MI355X",
+                        numa=(numa[i] if numa else 0), health=True, xgmi_hive=hive) for i in range(n)]
+
+
+def req(n=1, mem=0, pct=101, cores=0):
+    return ContainerDeviceRequest(nums=n, type="AMD", memreq=mem, mem_percentage=pct, coresreq=cores)
+
+
+def pod(name, n=1, mem=None, pct=None, cores=None, prio=None, annos=None, ctrs=1, uid=None):
+    lim = {R.RESOURCE_COUNT: str(n)}
+    if mem is not None:
+        lim[R.RESOURCE_MEM] = str(mem)
+    if pct is not None:
+        lim[R.RESOURCE_MEM_PERCENTAGE] = str(pct)
+    if cores is not None:
+        lim[R.RESOURCE_CORES] = str(cores)
+    if prio is not None:
+        lim[R.RESOURCE_PRIORITY] = str(prio)
+    return {"apiVersion": "v1", "kind": "Pod",
+            "metadata": {"name": name, "namespace": "default", "uid": uid or f"uid-{name}",
+                         "annotations": dict(annos or {})},
+            "spec": {"containers": [{"name": f"c{i}", "image": "x", "resources": {"limits": dict(lim)}}
+                                    for i in range(ctrs)]}}
+
+
+# ---- request parsing -------------------------------------------------------------------
+def test_request_defaults_full_device_memory():
+    r = resource_reqs(pod("a"))[0][0]
+    assert r.nums == 1 and r.mem_percentage == 100 and r.memreq == 0 and r.coresreq == 0
+
+
+def test_request_default_mem_flag():
+    config.SCHEDULER.default_mem = 5000
+    r = resource_reqs(pod("a"))[0][0]
+    assert r.memreq == 5000 and r.mem_percentage == R.MEM_PERCENT_UNSET
+
+
+def test_request_hygon_aliases():
+    p = {"metadata": {"name": "h", "uid": "h"}, "spec": {"containers": [{"resources": {"limits": {
+        "hygon.com/dcunum": "1", "hygon.com/dcumem": "2000", "hygon.com/dcucores": "30"}}}]}}
+    r = resource_reqs(p)[0][0]
+    assert (r.nums, r.memreq, r.coresreq) == (1, 2000, 30)
+
+
+def test_request_quantities():
+    r = resource_reqs(pod("a", n=2, mem="144000", cores="50"))[0][0]
+    assert (r.nums, r.memreq, r.coresreq) == (2, 144000, 50)
+
+
+# ---- scoring semantics -------------------------------------------------------------------
+def test_spread_within_node():
+    node = NodeUsage(usage(2))
+    node.devices[0].used = 1
+    ok, devs = fit_in_certain_device(node, req(), {})
+    assert ok and devs[0].uuid == "GPU-1"  # most free first
+
+
+def test_exclusive_cores_100_needs_unused_device():
+    node = NodeUsage(usage(1))
+    node.devices[0].used = 1
+    assert not fit_in_certain_device(node, req(cores=100), {})[0]
+
+
+def test_cores0_cannot_land_on_full_device():
+    node = NodeUsage(usage(1))
+    node.devices[0].usedcores = 100
+    node.devices[0].used = 1
+    assert not fit_in_certain_device(node, req(cores=0), {})[0]
+
+
+def test_cores_over_100_is_error():
+    with pytest.raises(FitError):
+        fit_in_certain_device(NodeUsage(usage(1)), req(cores=150), {})
+
+
+def test_mem_percentage():
+    node = NodeUsage(usage(1, mem=1000))
+    node.devices[0].usedmem = 600
+    assert not fit_in_certain_device(node, req(pct=50), {})[0]
+    assert fit_in_certain_device(node, req(pct=40), {})[0]
+
+
+def test_type_allow_deny():
+    node = NodeUsage(usage(1))
+    assert not fit_in_certain_device(node, req(), {R.ANN_USE_GPUTYPE: "MI300X"})[0]
+    assert fit_in_certain_device(node, req(), {R.ANN_USE_GPUTYPE: "mi300x,MI355"})[0]
+    assert not fit_in_certain_device(node, req(), {R.ANN_NOUSE_GPUTYPE: "mi355x"})[0]
+
+
+def test_numa_bind_keeps_one_numa():
+    node = NodeUsage(usage(4, numa=[0, 0, 1, 1]))
+    node.devices[3].used = 10  # numa 1 has only one free device
+    node.devices.sort(key=lambda d: (d.numa, d.count - d.used))
+    ok, devs = fit_in_certain_device(node, req(n=2), {R.ANN_NUMA_BIND: "true"})
+    assert ok and {d.uuid for d in devs} == {"GPU-0", "GPU-1"}
+
+
+def test_xgmi_bind():
+    devs = usage(4)
+    devs[0].xgmi_hive = devs[1].xgmi_hive = "h0"
+    devs[2].xgmi_hive = devs[3].xgmi_hive = "h1"
+    devs[3].used = 10
+    node = NodeUsage(devs)
+    ok, got = fit_in_certain_device(node, req(n=2), {R.ANN_XGMI_BIND: "true"})
+    assert ok and {d.uuid for d in got} == {"GPU-0", "GPU-1"}
+
+
+def test_node_score_packs_across_nodes():
+    # score = Σcount/Σfree of the chosen devices + (ndev − nreq): a node whose
+    # best device is already shared scores higher (reference score.go:180)
+    a, b = NodeUsage(usage(2)), NodeUsage(usage(2))
+    a.devices[0].used = 5
+    a.devices[1].used = 5
+    scores = calc_score({"a": a, "b": b}, [[req()]], {})
+    assert pick_node(scores).node_id == "a"
+
+
+# ---- webhook ------------------------------------------------------------------------------
+def _review(p):
+    return {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
+            "request": {"uid": "u1", "object": p}}
+
+
+def _apply(p, patch):
+    import copy
+    out = copy.deepcopy(p)
+    for op in patch:
+        parts = [x.replace("~1", "/").replace("~0", "~") for x in op["path"].split("/")[1:]]
+        cur = out
+        for k in parts[:-1]:
+            cur = cur[int(k)] if isinstance(cur, list) else cur[k]
+        last = parts[-1]
+        if op["op"] in ("add", "replace"):
+            if isinstance(cur, list):
+                cur[int(last)] = op["value"]
+            else:
+                cur[last] = op["value"]
+        elif op["op"] == "remove":
+            del cur[last]
+    return out
+
+
+def test_webhook_sets_scheduler_and_priority():
+    p = pod("w", prio=0)
+    r = handle_admission(_review(p), scheduler_name="vgpu-scheduler")["response"]
+    assert r["allowed"] and r["patchType"] == "JSONPatch"
+    new = _apply(p, json.loads(base64.b64decode(r["patch"])))
+    assert new["spec"]["schedulerName"] == "vgpu-scheduler"
+    assert {"name": "VGPU_TASK_PRIORITY", "value": "0"} in new["spec"]["containers"][0]["env"]
+
+
+def test_webhook_skips_privileged_and_plain():
+    p = pod("w")
+    p["spec"]["containers"][0]["securityContext"] = {"privileged": True}
+    r = handle_admission(_review(p))["response"]
+    assert r["allowed"] and "patch" not in r
+    plain = {"metadata": {"name": "x"}, "spec": {"containers": [{"name": "c"}]}}
+    assert "patch" not in handle_admission(_review(plain))["response"]
+
+
+def test_webhook_denies_empty_pod():
+    r = handle_admission(_review({"metadata": {"name": "x"}, "spec": {"containers": []}}))["response"]
+    assert not r["allowed"]
+
+
+# ---- fake API server fixtures -------------------------------------------------------------------
+@pytest.fixture
+def api():
+    srv = FakeApiServer()
+    url = srv.start()
+    yield srv, KubeClient(url)
+    srv.stop()
+
+
+def register_node(srv, name, devs, hs=None):
+    annos = {R.NODE_REGISTER: encode_node_devices(devs), NODE_REGISTER_EXT: encode_node_devices_ext(devs),
+             R.NODE_HANDSHAKE: hs or ("Reported " + dt.datetime.now().strftime(HANDSHAKE_TIME_FMT))}
+    srv.add_node(name, annotations=annos)
+
+
+def mi355x_devs(n=8, split=4, hive="hive0"):
+    return [DeviceInfo(id=f"{hive}-GPU-{i}", count=split, devmem=MIB_288G, devcore=100,
+                       type="AMD-MI355X", numa=i // 4, health=True, cus=256, xgmi_hive=hive, index=i)
+            for i in range(n)]
+
+
+def test_nodelock(api):
+    srv, c = api
+    srv.add_node("n1")
+    lock_node(c, "n1")
+    with pytest.raises(NodeLockError):
+        lock_node(c, "n1")
+    # expired lock is broken
+    later = dt.datetime.now(dt.timezone.utc) + dt.timedelta(seconds=R.NODE_LOCK_EXPIRE_S + 5)
+    lock_node(c, "n1", now=later)
+    release_node_lock(c, "n1")
+    assert R.NODE_LOCK not in c.get_node("n1")["metadata"]["annotations"]
+
+
+def test_nodelock_concurrent_only_one_wins(api):
+    srv, c = api
+    srv.add_node("n1")
+    wins, errs = [], []
+
+    def go():
+        try:
+            lock_node(c, "n1")
+            wins.append(1)
+        except NodeLockError:
+            errs.append(1)
+
+    ts = [threading.Thread(target=go) for _ in range(8)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert len(wins) == 1 and len(errs) == 7
+
+
+def test_handshake_state_machine(api):
+    srv, c = api
+    register_node(srv, "n1", mi355x_devs(2))
+    s = Scheduler(c)
+    s.register_from_node_annotations_once()
+    assert len(s.list_nodes()["n1"].devices) == 2
+    hs = c.get_node("n1")["metadata"]["annotations"][R.NODE_HANDSHAKE]
+    assert hs.startswith(R.HANDSHAKE_REQUESTING)
+    # plugin never answers: after the timeout the devices are dropped
+    s._now = lambda: dt.datetime.now() + dt.timedelta(seconds=120)
+    s.register_from_node_annotations_once()
+    assert "n1" not in s.list_nodes()
+    assert c.get_node("n1")["metadata"]["annotations"][R.NODE_HANDSHAKE].startswith(R.HANDSHAKE_DELETED)
+    # plugin reports again → back
+    s._now = dt.datetime.now
+    c.patch_node_annotations("n1", {R.NODE_HANDSHAKE: "Reported " + dt.datetime.now().strftime(HANDSHAKE_TIME_FMT)})
+    s.register_from_node_annotations_once()
+    assert len(s.list_nodes()["n1"].devices) == 2
+
+
+def schedule(s, c, srv, p, nodes):
+    srv.add_pod(p)
+    res = s.filter({"Pod": c.get_pod("default", p["metadata"]["name"]), "NodeNames": nodes})
+    return res
+
+
+def test_config1_eight_pods_on_four_fake_vgpus(api):
+    """BASELINE.json config 1: bin-pack 8 pods onto 4 fake vGPUs (2 devices × split 2)."""
+    srv, c = api
+    devs = [DeviceInfo(id=f"FAKE-{i}", count=2, devmem=16000, devcore=100, type="FAKE-vgpu")
+            for i in range(2)]
+    srv.add_node("cpu-node", annotations={"4pd.io/node-fake-register": encode_node_devices(devs),
+                                          "4pd.io/node-handshake-fake": "Reported now"})
+    s = Scheduler(c)
+    s.register_from_node_annotations_once()
+    placed = []
+    for i in range(8):
+        p = {"metadata": {"name": f"p{i}", "namespace": "default", "uid": f"u{i}"},
+             "spec": {"containers": [{"name": "c", "resources": {"limits": {"fake.com/vgpu": "1",
+                                                                         "fake.com/vgpumem": "4000"}}}]}}
+        r = schedule(s, c, srv, p, ["cpu-node"])
+        placed.append(bool(r["nodenames"]))
+    assert placed == [True] * 4 + [False] * 4
+    usage, _ = s.nodes_usage(None)
+    assert sorted(d.used for d in usage["cpu-node"].devices) == [2, 2]
+
+
+def test_config4_32_mixed_pods_on_8xmi355x(api):
+    """BASELINE.json config 4: 32 pods with mixed gpumem on one 8×MI355X node (split 4)."""
+    srv, c = api
+    register_node(srv, "mi355x-0", mi355x_devs(8, split=4))
+    s = Scheduler(c)
+    s.register_from_node_annotations_once()
+    mems = [120000, 70000, 36000, 18000] * 8
+    ok = 0
+    for i, m in enumerate(mems):
+        r = schedule(s, c, srv, pod(f"p{i}", mem=m, cores=25, uid=f"u{i}"), ["mi355x-0"])
+        ok += bool(r["nodenames"])
+    assert ok == 32
+    usage, _ = s.nodes_usage(None)
+    for d in usage["mi355x-0"].devices:
+        assert d.used == 4 and d.usedcores == 100 and d.usedmem <= d.totalmem
+    # a 33rd pod does not fit anywhere (all slots used)
+    r = schedule(s, c, srv, pod("extra", mem=1000, uid="ux"), ["mi355x-0"])
+    assert r["nodenames"] == []
+
+
+def test_filter_bind_roundtrip_and_restart_recovery(api):
+    srv, c = api
+    register_node(srv, "n1", mi355x_devs(2, split=2))
+    register_node(srv, "n2", mi355x_devs(2, split=2, hive="hive1"))
+    s = Scheduler(c)
+    s.register_from_node_annotations_once()
+    r = schedule(s, c, srv, pod("a", mem=144000, cores=50), ["n1", "n2"])
+    node = r["nodenames"][0]
+    p = c.get_pod("default", "a")
+    annos = p["metadata"]["annotations"]
+    assert annos[R.ASSIGNED_NODE] == node
+    assert annos[R.ASSIGNED_IDS] == annos[R.ASSIGNED_IDS_TO_ALLOCATE]
+    cd = decode_pod_devices(annos[R.ASSIGNED_IDS])[0][0]
+    assert (cd.usedmem, cd.usedcores) == (144000, 50)
+    b = s.bind({"podName": "a", "podNamespace": "default", "podUID": "uid-a", "node": node})
+    assert b["error"] == ""
+    p = c.get_pod("default", "a")
+    assert p["spec"]["nodeName"] == node
+    assert p["metadata"]["annotations"][R.BIND_PHASE] == R.BIND_ALLOCATING
+    assert R.NODE_LOCK in c.get_node(node)["metadata"]["annotations"]
+    # second bind to the locked node fails cleanly (reference ignores this error)
+    schedule(s, c, srv, pod("b", mem=1000), [node])
+    b2 = s.bind({"podName": "b", "podNamespace": "default", "podUID": "uid-b", "node": node})
+    assert "lock" in b2["error"]
+    # restart: a fresh scheduler rebuilds the ledger from annotations
+    s2 = Scheduler(c)
+    s2.register_from_node_annotations_once()
+    s2.resync_pods()
+    usage, _ = s2.nodes_usage(None)
+    assert sum(d.used for d in usage[node].devices) == 2
+
+
+def test_filter_api_failure_does_not_leak_ledger(api):
+    srv, c = api
+    register_node(srv, "n1", mi355x_devs(1))
+    s = Scheduler(c)
+    s.register_from_node_annotations_once()
+    srv.add_pod(pod("a"))
+    srv.inject("PATCH", r"/pods/a$", 500)
+    r = s.filter({"pod": c.get_pod("default", "a"), "nodenames": ["n1"]})
+    assert r["nodenames"] == [] and "patch pod failed" in r["error"]
+    assert s.scheduled_pods() == {}
+
+
+def test_http_routes_and_metrics(api):
+    import urllib.request
+    from prometheus_client import CollectorRegistry, generate_latest
+    from vgpu.scheduler.metrics import SchedulerCollector
+    from vgpu.scheduler.routes import serve
+    srv, c = api
+    register_node(srv, "n1", mi355x_devs(2))
+    s = Scheduler(c)
+    s.register_from_node_annotations_once()
+    http = serve(s, "127.0.0.1:0", background=True)
+    base = f"http://127.0.0.1:{http.server_address[1]}"
+    srv.add_pod(pod("a", mem=1000, cores=10))
+
+    def post(path, obj):
+        rq = urllib.request.Request(base + path, data=json.dumps(obj).encode(), method="POST",
+                                    headers={"Content-Type": "application/json"})
+        return json.loads(urllib.request.urlopen(rq).read())
+
+    r = post("/filter", {"Pod": c.get_pod("default", "a"), "NodeNames": ["n1"]})
+    assert r["nodenames"] == ["n1"]
+    r = post("/webhook", _review(pod("w")))
+    assert r["response"]["allowed"]
+    reg = CollectorRegistry()
+    reg.register(SchedulerCollector(s))
+    text = generate_latest(reg).decode()
+    assert 'GPUDeviceSharedNum{deviceidx=' in text and "vGPUPodsDeviceAllocated" in text
+    assert "nodeGPUOverview" in text
+    http.shutdown()

@@ -1,0 +1,110 @@
+"""Typed configuration shared by the extender, device plugin and monitor.
+
+Reference knobs: pkg/scheduler/config/config.go:19-24 (HttpBind,
+SchedulerName, DefaultMem, DefaultCores), pkg/util/types.go:85-117
+(DeviceSplitCount, DeviceMemoryScaling, DeviceCoresScaling, DisableCoreLimit,
+per-node DevicePluginConfigs JSON), cmd/device-plugin/nvidia/vgpucfg.go:15-133
+(flags + /config/config.json per-node overrides), docs/config.md:1-45.
+
+Precedence (lowest → highest): defaults, environment (VGPU_*), CLI flags,
+per-node JSON override (device plugin only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+from dataclasses import asdict, dataclass, field, fields
+
+
+@dataclass
+class SchedulerConfig:
+    http_bind: str = "127.0.0.1:8080"
+    cert_file: str = ""
+    key_file: str = ""
+    scheduler_name: str = "vgpu-scheduler"
+    default_mem: int = 0          # MiB; 0 → 100% of the device when nothing is requested
+    default_cores: int = 0        # percent
+    metrics_bind: str = ":9395"
+    node_scheduler_policy: str = "binpack"   # binpack | spread (across nodes)
+    gpu_scheduler_policy: str = "spread"     # spread | binpack (across devices of a node)
+    xgmi_weight: float = 1.0                 # weight of the xGMI-locality term for multi-GPU pods
+    register_interval_s: float = 15.0
+    handshake_timeout_s: float = 60.0
+
+
+@dataclass
+class NodeOverride:
+    name: str = ""
+    devicesplitcount: int | None = None
+    devicememoryscaling: float | None = None
+    devicecorescaling: float | None = None
+
+
+@dataclass
+class DevicePluginConfig:
+    node_name: str = ""
+    resource_name: str = "amd.com/gpu"
+    device_split_count: int = 10          # chart default (values.yaml:89-94); CLI default 2 in the reference
+    device_memory_scaling: float = 1.0    # >1 enables virtual device memory (oversubscription)
+    device_cores_scaling: float = 1.0
+    disable_core_limit: bool = False
+    hw_queues_per_vgpu: int = 1           # GPU_MAX_HW_QUEUES for fractional vGPUs (0 = runtime default)
+    partition_mode: str = ""             # SPX|DPX|QPX|CPX expected compute partition ("" = as found)
+    config_file: str = "/config/config.json"
+    socket_dir: str = "/var/lib/kubelet/device-plugins"
+    host_lib_dir: str = "/usr/local/vgpu"
+    register_interval_s: float = 30.0
+    backend: str = "auto"                  # auto | amdsmi | sysfs | fake:<json>
+    overrides: list = field(default_factory=list)
+
+    def apply_node_overrides(self) -> None:
+        """Per-node JSON (reference vgpucfg.go:81-107): {"nodeconfig":[{"name":...}]}"""
+        p = self.config_file
+        if not p or not os.path.exists(p):
+            return
+        try:
+            cfg = json.load(open(p))
+        except (OSError, ValueError):
+            return
+        for n in cfg.get("nodeconfig", []):
+            if n.get("name") != self.node_name:
+                continue
+            if n.get("devicesplitcount") is not None:
+                self.device_split_count = int(n["devicesplitcount"])
+            if n.get("devicememoryscaling") is not None:
+                self.device_memory_scaling = float(n["devicememoryscaling"])
+            if n.get("devicecorescaling") is not None:
+                self.device_cores_scaling = float(n["devicecorescaling"])
+
+
+def add_dataclass_args(ap: argparse.ArgumentParser, cls, prefix: str = "") -> None:
+    """One --flag per field (dashes), defaulting to VGPU_<FIELD> env or the dataclass default."""
+    inst = cls()
+    for f in fields(cls):
+        if f.name in ("overrides",):
+            continue
+        flag = "--" + prefix + f.name.replace("_", "-")
+        env = os.environ.get("VGPU_" + f.name.upper())
+        default = getattr(inst, f.name)
+        typ = type(default) if default is not None else str
+        if typ is bool:
+            dv = default if env is None else env.lower() in ("1", "true", "yes", "on")
+            ap.add_argument(flag, dest=f.name, type=lambda s: s.lower() in ("1", "true", "yes", "on"),
+                            default=dv, nargs="?", const=True)
+        else:
+            dv = default if env is None else typ(env)
+            ap.add_argument(flag, dest=f.name, type=typ, default=dv)
+
+
+def from_namespace(cls, ns: argparse.Namespace):
+    kw = {f.name: getattr(ns, f.name) for f in fields(cls) if hasattr(ns, f.name)}
+    return cls(**kw)
+
+
+# Process-global scheduler config (the reference keeps package-level globals).
+SCHEDULER = SchedulerConfig()
+
+
+def to_dict(cfg) -> dict:
+    return asdict(cfg)
