@@ -1,0 +1,272 @@
+"""Device plugin: discovery through libvgpu_smi (fake amdsmi fixture and a fake
+KFD sysfs tree), node registration, and the kubelet gRPC surface end to end with
+a fake kubelet + fake API server + the real scheduler extender."""
+import json
+import os
+import threading
+from concurrent import futures
+
+import grpc
+import pytest
+
+from vgpu import config
+from vgpu.api import resources as R
+from vgpu.api.codec import decode_node_devices
+from vgpu.config import DevicePluginConfig
+from vgpu.device.base import init_default_devices
+from vgpu.device.cualloc import MI355X, parse_mask
+from vgpu.deviceplugin import api
+from vgpu.deviceplugin.custate import CUMaskState
+from vgpu.deviceplugin.discovery import (EVT_POST_RESET, EVT_PRE_RESET, LINK_XGMI, SmiBackend,
+                                         StaticBackend, mi355x_node)
+from vgpu.deviceplugin.register import register_once
+from vgpu.deviceplugin.server import VGPUDevicePlugin
+from vgpu.k8s.client import KubeClient
+from vgpu.k8s.fakeapi import FakeApiServer
+from vgpu.native import FAKES_DIR
+from vgpu.scheduler.core import Scheduler
+
+from test_scheduler import pod as mkpod
+
+
+# ---- discovery ------------------------------------------------------------------------
+def _smi_subprocess(env, code):
+    import subprocess
+    import sys
+    e = dict(os.environ)
+    e.update(env)
+    r = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, timeout=60,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+DISCOVER = ("import json; from vgpu.deviceplugin.discovery import SmiBackend; b=SmiBackend('{mode}');"
+            "d=b.devices(); print(json.dumps({{'backend': b.name, 'devs': [x.__dict__ for x in d],"
+            "'link': b.link(0, 1) if len(d) > 1 else None, 'procs': [p.__dict__ for p in b.processes(0)],"
+            "'events': b.events(10)}}))")
+
+
+def test_discovery_fake_amdsmi(native_build, tmp_path):
+    fx = {"gpus": [{"uuid": f"GPU-{i}", "bdf": f"0000:{5 + i:02x}:00.0", "name": "AMD Instinct MI355X",
+                    "vram": 309220868096, "cus": 256, "numa": i // 2, "render": 128 + i, "card": i,
+                    "hive": 77, "partition": "SPX", "mem_partition": "NPS1", "gfx": 30,
+                    "processes": [{"pid": 42, "vram": 1 << 30, "cu": 64}] if i == 0 else []}
+                   for i in range(4)],
+          "link": "xgmi", "events": [{"gpu": 1, "type": 3, "message": "reset"}]}
+    f = tmp_path / "fx.json"
+    f.write_text(json.dumps(fx))
+    out = _smi_subprocess({"VGPU_AMDSMI_LIB": str(FAKES_DIR / "libamd_smi.so"),
+                           "VGPU_FAKE_AMDSMI_JSON": str(f)}, DISCOVER.format(mode="amdsmi"))
+    assert out["backend"] == "amdsmi"
+    devs = out["devs"]
+    assert len(devs) == 4
+    assert devs[2]["numa"] == 1 and devs[3]["render_minor"] == 131 and devs[0]["bdf"] == "0000:05:00.0"
+    assert devs[0]["vram_total"] == 309220868096 and devs[0]["cus"] == 256 and devs[0]["gfx_activity"] == 30
+    assert out["link"][1] == LINK_XGMI
+    assert out["procs"] == [{"pid": 42, "vram_bytes": 1 << 30, "cu_occupancy": 64, "gfx_ns": 0}]
+    assert out["events"] == [[1, 3, "reset"]]
+
+
+def make_sysfs(root, n=2):
+    for i in range(n + 1):  # node 0 = CPU
+        nd = root / f"sys/class/kfd/kfd/topology/nodes/{i}"
+        nd.mkdir(parents=True)
+        if i == 0:
+            (nd / "gpu_id").write_text("0\n")
+            (nd / "properties").write_text("cpu_cores_count 64\nsimd_count 0\n")
+            continue
+        (nd / "gpu_id").write_text(f"{4000 + i}\n")
+        loc = (0x10 * i) << 8
+        (nd / "properties").write_text(
+            f"simd_count 1024\nsimd_per_cu 4\nnum_xcc 8\nvendor_id 4098\ndevice_id 30115\n"
+            f"drm_render_minor {127 + i}\nhive_id 555\nunique_id {0xabc0 + i}\nlocation_id {loc}\ndomain 0\n")
+        mb = nd / "mem_banks/0"
+        mb.mkdir(parents=True)
+        (mb / "properties").write_text(f"heap_type 1\nsize_in_bytes {288 << 30}\n")
+        il = nd / "io_links/0"
+        il.mkdir(parents=True)
+        other = 2 if i == 1 else 1
+        (il / "properties").write_text(f"type 11\nnode_from {i}\nnode_to {other}\nweight 15\n")
+        pci = root / f"sys/bus/pci/devices/0000:{0x10 * i:02x}:00.0"
+        pci.mkdir(parents=True)
+        (pci / "numa_node").write_text(f"{i - 1}\n")
+        (pci / "current_compute_partition").write_text("SPX\n")
+        (pci / "current_memory_partition").write_text("NPS1\n")
+        (pci / "product_name").write_text("AMD Instinct MI355X\n")
+        (pci / "mem_info_vram_used").write_text("1048576\n")
+
+
+def test_discovery_sysfs(native_build, tmp_path):
+    make_sysfs(tmp_path)
+    out = _smi_subprocess({"VGPU_SYSFS_ROOT": str(tmp_path)}, DISCOVER.format(mode="sysfs"))
+    assert out["backend"] == "sysfs"
+    d0, d1 = out["devs"]
+    assert d0["cus"] == 256 and d0["num_xcc"] == 8 and d0["vram_total"] == 288 << 30
+    assert d0["uuid"] == f"GPU-{0xabc1:016x}" and d1["numa"] == 1 and d1["render_minor"] == 129
+    assert d0["bdf"] == "0000:10:00.0" and d0["vram_used"] == 1048576
+    assert out["link"][1] == LINK_XGMI
+
+
+# ---- CU-mask state ------------------------------------------------------------------------
+def test_cumask_state_disjoint_and_gc(tmp_path):
+    st = CUMaskState(str(tmp_path))
+    a = st.allocate("uid1_c", [("GPU-0", 50)])["GPU-0"]
+    b = st.allocate("uid2_c", [("GPU-0", 50)])["GPU-0"]
+    assert a and b and a & b == 0 and MI355X.per_xcd_counts(a) == [16] * 8
+    assert st.allocate("uid3_c", [("GPU-0", 25)])["GPU-0"] == 0  # device fully partitioned
+    assert st.allocate("uid4_c", [("GPU-1", 100)])["GPU-1"] == 0  # exclusive: no mask
+    assert st.used("GPU-0") == a | b
+    removed = st.gc({"uid2"}, grace_s=0)
+    assert "uid1_c" in removed and st.used("GPU-0") == b
+
+
+# ---- end to end ------------------------------------------------------------------------------
+class FakeKubelet:
+    def __init__(self, sock):
+        self.registrations = []
+        self.srv = grpc.server(futures.ThreadPoolExecutor(max_workers=2))
+        self.srv.add_generic_rpc_handlers((api.service_handler("Registration", self),))
+        self.srv.add_insecure_port(api.unix_target(sock))
+        self.srv.start()
+
+    def Register(self, request, context):
+        self.registrations.append(request)
+        return api.Empty()
+
+
+@pytest.fixture
+def cluster(tmp_path):
+    init_default_devices()
+    config.SCHEDULER = config.SchedulerConfig()
+    srv = FakeApiServer()
+    url = srv.start()
+    client = KubeClient(url)
+    sockdir = tmp_path / "dp"
+    sockdir.mkdir()
+    kubelet = FakeKubelet(str(sockdir / "kubelet.sock"))
+    cfg = DevicePluginConfig(node_name="n1", device_split_count=4, socket_dir=str(sockdir),
+                             host_lib_dir=str(tmp_path / "host"), config_file="")
+    srv.add_node("n1")
+    backend = StaticBackend(mi355x_node(8))
+    plugin = VGPUDevicePlugin(cfg, backend, client, "n1")
+    plugin.start()
+    register_once(client, "n1", plugin.devices, cfg)
+    sched = Scheduler(client)
+    sched.register_from_node_annotations_once()
+    ch = grpc.insecure_channel(api.unix_target(plugin.socket_path))
+    stub = api.Stub(ch, "DevicePlugin")
+    yield dict(srv=srv, client=client, plugin=plugin, sched=sched, stub=stub, kubelet=kubelet,
+               backend=backend, cfg=cfg)
+    ch.close()
+    plugin.stop()
+    kubelet.srv.stop(0)
+    srv.stop()
+
+
+def test_registration_and_list(cluster):
+    reg = cluster["kubelet"].registrations
+    assert len(reg) == 1 and reg[0].resource_name == "amd.com/gpu" and reg[0].version == "v1beta1"
+    assert reg[0].options.get_preferred_allocation_available
+    first = next(iter(cluster["stub"].ListAndWatch(api.Empty(), timeout=5)))
+    assert len(first.devices) == 8 * 4
+    assert all(d.health == api.HEALTHY for d in first.devices)
+    node = cluster["client"].get_node("n1")
+    devs = decode_node_devices(node["metadata"]["annotations"][R.NODE_REGISTER])
+    assert len(devs) == 8 and devs[0].count == 4 and devs[0].devmem == 294912 and devs[0].type == "AMD-MI355X"
+    assert {d.numa for d in devs} == {0, 1}
+
+
+def schedule_and_allocate(c, name, mem, cores, n=1):
+    p = mkpod(name, n=n, mem=mem, cores=cores, uid=f"uid-{name}")
+    c["srv"].add_pod(p)
+    r = c["sched"].filter({"pod": c["client"].get_pod("default", name), "nodenames": ["n1"]})
+    assert r["nodenames"] == ["n1"], r
+    assert c["sched"].bind({"podName": name, "podNamespace": "default", "podUID": f"uid-{name}",
+                            "node": "n1"})["error"] == ""
+    lw = next(iter(c["stub"].ListAndWatch(api.Empty(), timeout=5)))
+    ids = [d.ID for d in lw.devices]
+    pref = c["stub"].GetPreferredAllocation(api.PreferredAllocationRequest(container_requests=[
+        dict(available_deviceIDs=ids, allocation_size=n)]), timeout=5)
+    chosen = list(pref.container_responses[0].deviceIDs)
+    resp = c["stub"].Allocate(api.AllocateRequest(container_requests=[dict(devices_ids=chosen)]), timeout=10)
+    return chosen, resp.container_responses[0]
+
+
+def test_allocate_two_pods_share_one_gpu(cluster):
+    c = cluster
+    c["sched"].cfg.gpu_scheduler_policy = "binpack"
+    config.SCHEDULER.gpu_scheduler_policy = "binpack"
+    ch1, r1 = schedule_and_allocate(c, "a", 144000, 50)
+    ch2, r2 = schedule_and_allocate(c, "b", 144000, 50)
+    # binpack: same physical GPU; preferred allocation steered kubelet to it
+    assert ch1[0].rsplit("-", 1)[0] == ch2[0].rsplit("-", 1)[0]
+    for r in (r1, r2):
+        e = dict(r.envs)
+        assert e["VGPU_DEVICE_MEMORY_LIMIT_0"] == "144000m" and e["VGPU_DEVICE_CU_LIMIT_0"] == "50"
+        assert e["VGPU_SHARED_REGION"] == "/var/run/vgpu/vgpu.cache"
+        assert e["GPU_MAX_HW_QUEUES"] == "1"
+        paths = {m.container_path for m in r.mounts}
+        assert {"/usr/local/vgpu/libvgpu.so", "/var/run/vgpu", "/tmp/vgpulock", "/etc/ld.so.preload"} <= paths
+        devs = {d.container_path for d in r.devices}
+        assert "/dev/kfd" in devs and any(p.startswith("/dev/dri/renderD") for p in devs)
+    m1, m2 = parse_mask(dict(r1.envs)["VGPU_CU_MASK_0"]), parse_mask(dict(r2.envs)["VGPU_CU_MASK_0"])
+    assert m1 & m2 == 0 and bin(m1).count("1") == 128 and bin(m2).count("1") == 128
+    for name in ("a", "b"):
+        a = c["client"].get_pod("default", name)["metadata"]["annotations"]
+        assert a[R.BIND_PHASE] == R.BIND_SUCCESS
+        assert a[R.ASSIGNED_IDS_TO_ALLOCATE] == ""
+    assert R.NODE_LOCK not in c["client"].get_node("n1")["metadata"]["annotations"]
+
+
+def test_allocate_multi_gpu_prefers_one_numa(cluster):
+    c = cluster
+    chosen, r = schedule_and_allocate(c, "big", 0, 100, n=4)
+    e = dict(r.envs)
+    assert sorted(k for k in e if k.startswith("VGPU_DEVICE_MEMORY_LIMIT_")) == \
+        [f"VGPU_DEVICE_MEMORY_LIMIT_{i}" for i in range(4)]
+    assert "VGPU_DEVICE_CU_LIMIT_0" not in e and "GPU_MAX_HW_QUEUES" not in e
+    renders = [d.container_path for d in r.devices if "renderD" in d.container_path]
+    assert len(renders) == 4
+    by_render = {f"/dev/dri/renderD{d.render_minor}": d for d in c["plugin"].devices}
+    assert len({by_render[p].numa for p in renders}) == 1  # one NUMA node, one xGMI hive
+    # container ordinal i follows physical (KFD) order
+    uuids = [e[f"VGPU_DEVICE_UUID_{i}"] for i in range(4)]
+    idx = [next(d.index for d in c["plugin"].devices if d.uuid == u) for u in uuids]
+    assert idx == sorted(idx)
+
+
+def test_allocate_without_pending_pod_fails(cluster):
+    with pytest.raises(grpc.RpcError) as ei:
+        cluster["stub"].Allocate(api.AllocateRequest(container_requests=[dict(devices_ids=["x-0"])]), timeout=5)
+    assert ei.value.code() in (grpc.StatusCode.INVALID_ARGUMENT, grpc.StatusCode.UNKNOWN)
+
+
+def test_allocate_count_mismatch_marks_failed(cluster):
+    c = cluster
+    p = mkpod("m", n=1, mem=1000, cores=10, uid="uid-m")
+    c["srv"].add_pod(p)
+    c["sched"].filter({"pod": c["client"].get_pod("default", "m"), "nodenames": ["n1"]})
+    c["sched"].bind({"podName": "m", "podNamespace": "default", "podUID": "uid-m", "node": "n1"})
+    ids = [d.ID for d in next(iter(c["stub"].ListAndWatch(api.Empty(), timeout=5))).devices][:2]
+    with pytest.raises(grpc.RpcError):
+        c["stub"].Allocate(api.AllocateRequest(container_requests=[dict(devices_ids=ids)]), timeout=5)
+    assert c["client"].get_pod("default", "m")["metadata"]["annotations"][R.BIND_PHASE] == R.BIND_FAILED
+    assert R.NODE_LOCK not in c["client"].get_node("n1")["metadata"]["annotations"]
+
+
+def test_health_reset_and_recovery(cluster):
+    c = cluster
+    stream = c["stub"].ListAndWatch(api.Empty(), timeout=10)
+    first = next(stream)
+    assert all(d.health == api.HEALTHY for d in first.devices)
+    c["backend"].pending_events.append((2, EVT_PRE_RESET, "mode1 reset"))
+    c["plugin"].health_step(10)
+    upd = next(stream)
+    bad = {d.ID.rsplit("-", 1)[0] for d in upd.devices if d.health == api.UNHEALTHY}
+    assert bad == {c["plugin"].devices[2].uuid}
+    c["backend"].pending_events.append((2, EVT_POST_RESET, "done"))
+    c["plugin"].health_step(10)
+    upd = next(stream)
+    assert all(d.health == api.HEALTHY for d in upd.devices)
+    stream.cancel()

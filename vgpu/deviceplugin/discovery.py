@@ -1,0 +1,202 @@
+"""Device discovery for the node agents: ctypes over libvgpu_smi.so (amdsmi or
+KFD sysfs), plus a static backend for tests / fixtures.
+
+Reference equivalents: NVML enumeration in the NVIDIA plugin
+(pkg/device-plugin/nvidiadevice/nvinternal/rm/nvml_devices.go:48-168,
+plugin/register.go:55-100 incl. NUMA from `nvidia-smi topo -m`), Hygon's
+`hy-smi` scraping + libdrm_amdgpu cgo (pkg/device-plugin/hygon/dcu/server.go:50-175,
+amdgpu/amdgpu.go) and hwloc NUMA lookup (hygon/dcu/hwloc/hwloc.go:69-97).
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+from dataclasses import asdict, dataclass, field
+
+from vgpu.native import LIB_DIR, NativeMissing
+
+STR = 64
+
+
+class _SmiDevice(ctypes.Structure):
+    _fields_ = [("uuid", ctypes.c_char * STR), ("bdf", ctypes.c_char * STR), ("name", ctypes.c_char * STR),
+                ("compute_partition", ctypes.c_char * 16), ("memory_partition", ctypes.c_char * 16),
+                ("vram_total", ctypes.c_uint64), ("vram_used", ctypes.c_uint64),
+                ("xgmi_hive", ctypes.c_uint64), ("device_id", ctypes.c_uint64),
+                ("vendor_id", ctypes.c_uint32), ("cus", ctypes.c_uint32), ("num_xcc", ctypes.c_uint32),
+                ("numa_node", ctypes.c_int32), ("render_minor", ctypes.c_uint32), ("card", ctypes.c_uint32),
+                ("kfd_gpu_id", ctypes.c_uint32), ("index", ctypes.c_uint32), ("health", ctypes.c_uint32),
+                ("gfx_activity", ctypes.c_uint32), ("umc_activity", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32 * 7)]
+
+
+class _SmiProc(ctypes.Structure):
+    _fields_ = [("pid", ctypes.c_uint32), ("cu_occupancy", ctypes.c_uint32),
+                ("vram_bytes", ctypes.c_uint64), ("gfx_ns", ctypes.c_uint64)]
+
+
+class _SmiEvent(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("type", ctypes.c_int32), ("message", ctypes.c_char * (STR * 2))]
+
+
+# AMDSMI_EVT_NOTIF_* values we act on
+EVT_VMFAULT, EVT_THERMAL, EVT_PRE_RESET, EVT_POST_RESET = 1, 2, 3, 4
+LINK_UNKNOWN, LINK_PCIE, LINK_XGMI = 0, 1, 2
+
+
+@dataclass
+class Device:
+    uuid: str
+    index: int
+    bdf: str = ""
+    name: str = "AMD Instinct MI355X"
+    vram_total: int = 288 << 30
+    vram_used: int = 0
+    cus: int = 256
+    num_xcc: int = 8
+    numa: int = 0
+    render_minor: int = 128
+    card: int = 0
+    kfd_gpu_id: int = 0
+    xgmi_hive: int = 0
+    compute_partition: str = "SPX"
+    memory_partition: str = "NPS1"
+    health: bool = True
+    gfx_activity: int = 0
+    umc_activity: int = 0
+    vendor_id: int = 0x1002
+
+    @property
+    def model(self) -> str:
+        """Short model for the device type string, e.g. 'MI355X'."""
+        for tok in self.name.replace("(", " ").split():
+            if tok.upper().startswith("MI") and any(c.isdigit() for c in tok):
+                return tok.upper()
+        return self.name.split()[-1] if self.name else "GPU"
+
+    @property
+    def type(self) -> str:
+        t = f"AMD-{self.model}"
+        if self.compute_partition and self.compute_partition.upper() != "SPX":
+            t += f"-{self.compute_partition.upper()}"
+        return t
+
+
+@dataclass
+class Proc:
+    pid: int
+    vram_bytes: int
+    cu_occupancy: int = 0
+    gfx_ns: int = 0
+
+
+class Backend:
+    name = "base"
+
+    def devices(self) -> list[Device]:
+        raise NotImplementedError
+
+    def link(self, a: int, b: int) -> tuple[int, int]:
+        return 0, LINK_UNKNOWN
+
+    def processes(self, index: int) -> list[Proc]:
+        return []
+
+    def events(self, timeout_ms: int = 1000) -> list[tuple[int, int, str]]:
+        return []
+
+
+class SmiBackend(Backend):
+    def __init__(self, mode: str = "auto"):
+        p = LIB_DIR / "libvgpu_smi.so"
+        if not p.exists():
+            raise NativeMissing(f"{p} not built")
+        lib = ctypes.CDLL(str(p))
+        lib.vgpu_smi_open.argtypes = [ctypes.c_char_p]
+        lib.vgpu_smi_get.argtypes = [ctypes.c_int, ctypes.POINTER(_SmiDevice)]
+        lib.vgpu_smi_link.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.POINTER(ctypes.c_int32)]
+        lib.vgpu_smi_processes.argtypes = [ctypes.c_int, ctypes.POINTER(_SmiProc), ctypes.c_int]
+        lib.vgpu_smi_events.argtypes = [ctypes.POINTER(_SmiEvent), ctypes.c_int, ctypes.c_int]
+        lib.vgpu_smi_backend.restype = ctypes.c_char_p
+        self.lib = lib
+        n = lib.vgpu_smi_open(mode.encode())
+        if n < 0:
+            raise RuntimeError(f"vgpu_smi_open({mode}) failed")
+        self.count = n
+        self.name = lib.vgpu_smi_backend().decode()
+
+    def devices(self) -> list[Device]:
+        out = []
+        for i in range(self.lib.vgpu_smi_count()):
+            d = _SmiDevice()
+            if self.lib.vgpu_smi_get(i, ctypes.byref(d)) != 0:
+                continue
+            out.append(Device(
+                uuid=d.uuid.decode() or f"GPU-{i}", index=i, bdf=d.bdf.decode(), name=d.name.decode(),
+                vram_total=d.vram_total, vram_used=d.vram_used, cus=d.cus or 256,
+                num_xcc=d.num_xcc or 8, numa=max(d.numa_node, 0), render_minor=d.render_minor,
+                card=d.card, kfd_gpu_id=d.kfd_gpu_id, xgmi_hive=d.xgmi_hive,
+                compute_partition=d.compute_partition.decode() or "SPX",
+                memory_partition=d.memory_partition.decode() or "NPS1", health=bool(d.health),
+                gfx_activity=d.gfx_activity, umc_activity=d.umc_activity, vendor_id=d.vendor_id))
+        return out
+
+    def link(self, a: int, b: int) -> tuple[int, int]:
+        hops, t = ctypes.c_uint64(0), ctypes.c_int32(0)
+        self.lib.vgpu_smi_link(a, b, ctypes.byref(hops), ctypes.byref(t))
+        return hops.value, t.value
+
+    def processes(self, index: int) -> list[Proc]:
+        buf = (_SmiProc * 256)()
+        n = self.lib.vgpu_smi_processes(index, buf, 256)
+        return [Proc(buf[i].pid, buf[i].vram_bytes, buf[i].cu_occupancy, buf[i].gfx_ns)
+                for i in range(max(n, 0))]
+
+    def events(self, timeout_ms: int = 1000) -> list[tuple[int, int, str]]:
+        buf = (_SmiEvent * 32)()
+        n = self.lib.vgpu_smi_events(buf, 32, timeout_ms)
+        return [(buf[i].device, buf[i].type, buf[i].message.decode(errors="replace")) for i in range(n)]
+
+
+class StaticBackend(Backend):
+    """Fixed device list (tests, dry runs, `--backend fake:<file.json>`)."""
+    name = "static"
+
+    def __init__(self, devices: list[Device], xgmi: bool = True, procs: dict | None = None):
+        self._devs = devices
+        self.xgmi = xgmi
+        self._procs = procs or {}
+        self.pending_events: list[tuple[int, int, str]] = []
+
+    def devices(self) -> list[Device]:
+        return [Device(**asdict(d)) for d in self._devs]
+
+    def link(self, a: int, b: int) -> tuple[int, int]:
+        da, db = self._devs[a], self._devs[b]
+        if self.xgmi and da.xgmi_hive == db.xgmi_hive:
+            return 1, LINK_XGMI
+        return 2, LINK_PCIE
+
+    def processes(self, index: int) -> list[Proc]:
+        return list(self._procs.get(index, []))
+
+    def events(self, timeout_ms: int = 1000) -> list[tuple[int, int, str]]:
+        ev, self.pending_events = self.pending_events, []
+        return ev
+
+
+def mi355x_node(n: int = 8, hive: int = 0x1111) -> list[Device]:
+    """A synthetic 8 × MI355X node (one xGMI hive, two NUMA nodes)."""
+    return [Device(uuid=f"GPU-{hive:x}-{i:02d}", index=i, bdf=f"0000:{0x05 + 0x10 * i:02x}:00.0",
+                   numa=i // 4, render_minor=128 + i, card=i, kfd_gpu_id=1000 + i, xgmi_hive=hive)
+            for i in range(n)]
+
+
+def load_backend(spec: str = "auto") -> Backend:
+    if spec.startswith("fake:"):
+        data = json.load(open(spec[5:]))
+        return StaticBackend([Device(**d) for d in data["devices"]], xgmi=data.get("xgmi", True))
+    if spec == "synthetic":
+        return StaticBackend(mi355x_node())
+    return SmiBackend(spec)

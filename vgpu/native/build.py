@@ -200,7 +200,7 @@ def build_fakes(force: bool = False) -> dict[str, Path]:
     drv_src = NATIVE / "tests" / "shim_driver.cpp"
     drv = FAKES_OUT / "shim_driver"
     if force or not _stamp(drv, [drv_src, hip_src, hsa_src] + _headers()):
-        _run([CXX, *COMMON, drv_src, "-o", drv, f"-L{FAKES_OUT}", "-l:libamdhip64.so.7",
+        _run([CXX, *COMMON, "-Wno-unused-result", drv_src, "-o", drv, f"-L{FAKES_OUT}", "-l:libamdhip64.so.7",
               "-l:libhsa-runtime64.so.1", f"-Wl,-rpath,{FAKES_OUT}", "-ldl", "-lpthread"])
         _mark(drv, [drv_src, hip_src, hsa_src] + _headers())
     res["driver"] = drv
