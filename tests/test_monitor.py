@@ -1,0 +1,120 @@
+"""Node monitor: region layout mirror, priority feedback, path discovery/GC,
+metrics, and the shim obeying the monitor's blocking word."""
+import os
+import subprocess
+import time
+
+import pytest
+
+from vgpu.api import resources as R
+from vgpu.k8s.client import KubeClient
+from vgpu.k8s.fakeapi import FakeApiServer
+from vgpu.monitor.feedback import observe
+from vgpu.monitor.metrics import MonitorCollector
+from vgpu.monitor.pathmonitor import PathMonitor
+from vgpu.monitor.region import AttachedRegion, check_layout
+from vgpu.native import FAKES_DIR, shim_path
+
+GiB = 1 << 30
+
+
+def make_region(path, monkeypatch, uuid="GPU-0", limit="8g", prio=1, cu=0):
+    for k in list(os.environ):
+        if k.startswith("VGPU_"):
+            monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("VGPU_DEVICE_MEMORY_LIMIT_0", limit)
+    monkeypatch.setenv("VGPU_DEVICE_UUID_0", uuid)
+    monkeypatch.setenv("VGPU_TASK_PRIORITY", str(prio))
+    if cu:
+        monkeypatch.setenv("VGPU_DEVICE_CU_LIMIT_0", str(cu))
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    return AttachedRegion(str(path), create=True)
+
+
+def test_layout_matches_c(native_build):
+    check_layout()
+
+
+def test_region_roundtrip(native_build, tmp_path, monkeypatch):
+    r = make_region(tmp_path / "a" / "vgpu.cache", monkeypatch, cu=50)
+    devs = r.devices()
+    assert devs[0].uuid == "GPU-0" and devs[0].mem_limit == 8 * GiB and devs[0].cu_limit == 50
+    assert r.priority == 1
+    r.set_cu_mask(0, 0xFF)
+    assert r.devices()[0].cu_mask == 0xFF
+    r.close()
+
+
+def test_feedback_blocks_low_priority(native_build, tmp_path, monkeypatch):
+    hi = make_region(tmp_path / "hi" / "vgpu.cache", monkeypatch, prio=0)
+    lo = make_region(tmp_path / "lo" / "vgpu.cache", monkeypatch, prio=1)
+    other = make_region(tmp_path / "ot" / "vgpu.cache", monkeypatch, uuid="GPU-1", prio=1)
+    for r in (hi, lo, other):
+        r.set_recent_kernel(2)
+    observe({"hi": hi, "lo": lo, "ot": other})
+    assert lo.recent_kernel == -1          # high-priority task active on GPU-0
+    assert hi.recent_kernel == 1 and hi.utilization_switch == 0
+    assert lo.utilization_switch == 1
+    assert other.recent_kernel == 1 and other.utilization_switch == 0  # alone on GPU-1
+    # the high-priority task goes idle: two passes later the low one is released
+    observe({"hi": hi, "lo": lo, "ot": other})
+    observe({"hi": hi, "lo": lo, "ot": other})
+    assert lo.recent_kernel == 0
+    for r in (hi, lo, other):
+        r.close()
+
+
+def test_shim_obeys_blocking_word(native_build, tmp_path, monkeypatch):
+    path = tmp_path / "c" / "vgpu.cache"
+    r = make_region(path, monkeypatch, limit="1g")
+    r.set_recent_kernel(-1)
+    env = {k: v for k, v in os.environ.items() if not k.startswith("HIP_")}
+    env.update({"LD_PRELOAD": str(shim_path()), "LD_LIBRARY_PATH": str(FAKES_DIR),
+                "VGPU_SHARED_REGION": str(path)})
+    p = subprocess.Popen([str(FAKES_DIR / "shim_driver"), "launch", "5"], env=env, stdout=subprocess.PIPE,
+                         text=True)
+    time.sleep(1.0)
+    assert p.poll() is None  # held back by the monitor
+    r.set_recent_kernel(0)
+    out, _ = p.communicate(timeout=20)
+    assert "fake_launches=7" in out
+    assert r.recent_kernel == 2
+    r.close()
+
+
+def test_pathmonitor_discovery_gc_and_metrics(native_build, tmp_path, monkeypatch):
+    from prometheus_client import CollectorRegistry, generate_latest
+    srv = FakeApiServer()
+    c = KubeClient(srv.start())
+    srv.add_node("n1")
+    srv.add_pod({"metadata": {"name": "p", "namespace": "ns1", "uid": "uidA"},
+                 "spec": {"nodeName": "n1", "containers": [{"name": "main"}]}})
+    cdir = tmp_path / "containers"
+    ra = make_region(cdir / "uidA_main" / "vgpu.cache", monkeypatch, uuid="GPU-7", limit="4g")
+    rb = make_region(cdir / "uidGone_x" / "vgpu.cache", monkeypatch)
+    # a live process of container A holds 1 GiB
+    env = {k: v for k, v in os.environ.items() if not k.startswith("HIP_")}
+    env.update({"LD_PRELOAD": str(shim_path()), "LD_LIBRARY_PATH": str(FAKES_DIR),
+                "VGPU_SHARED_REGION": str(cdir / "uidA_main" / "vgpu.cache"),
+                "VGPU_DEVICE_MEMORY_LIMIT_0": "4g", "VGPU_DEVICE_UUID_0": "GPU-7"})
+    holder = subprocess.Popen([str(FAKES_DIR / "shim_driver"), "hold", str(GiB), "5"], env=env,
+                              stdout=subprocess.PIPE, text=True)
+    assert holder.stdout.readline().strip() == "hold_rc=0"
+    pm = PathMonitor(str(cdir), c, "n1")
+    t0 = time.time()
+    regs = pm.scan(now=t0)
+    assert set(regs) == {"uidA_main", "uidGone_x"}
+    assert regs["uidA_main"].pod_name == "p" and regs["uidA_main"].namespace == "ns1"
+    reg = CollectorRegistry()
+    reg.register(MonitorCollector(pm))
+    text = generate_latest(reg).decode()
+    line = [l for l in text.splitlines() if l.startswith("vGPU_device_memory_usage_in_bytes{") and "GPU-7" in l]
+    assert line and float(line[0].split()[-1]) == GiB
+    assert 'vGPU_device_memory_limit_in_bytes{ctrname="main",deviceuuid="GPU-7"' in text
+    holder.wait(timeout=20)
+    # GC after the grace period removes the dead pod's directory
+    regs = pm.scan(now=t0 + 400)
+    assert set(regs) == {"uidA_main"} and not (cdir / "uidGone_x").exists()
+    ra.close()
+    rb.close()
+    srv.stop()
