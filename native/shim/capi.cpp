@@ -137,6 +137,23 @@ __attribute__((visibility("default"))) int vgpu_self_reserve(int dev, uint64_t s
 __attribute__((visibility("default"))) void vgpu_self_unreserve(int dev, uint64_t size) {
   mem_unreserve(dev, size, kDeviceBuf);
 }
+// Pager accounting (vgpu/ops/pager.py): HBM<->host bytes moved by this process.
+__attribute__((visibility("default"))) void vgpu_self_add_swap(int dev, uint64_t in_bytes,
+                                                               uint64_t out_bytes) {
+  ensure_init();
+  vgpu_proc_slot_t* sl = my_slot();
+  if (!sl || dev < 0 || dev >= VGPU_MAX_DEVICES) return;
+  __atomic_fetch_add(&sl->used[dev].swap_in_bytes, in_bytes, __ATOMIC_RELAXED);
+  __atomic_fetch_add(&sl->used[dev].swap_out_bytes, out_bytes, __ATOMIC_RELAXED);
+}
+
+__attribute__((visibility("default"))) uint64_t vgpu_self_host_bytes(int dev) {
+  ensure_init();
+  vgpu_proc_slot_t* sl = my_slot();
+  if (!sl || dev < 0 || dev >= VGPU_MAX_DEVICES) return 0;
+  return __atomic_load_n(&sl->used[dev].host_bytes, __ATOMIC_RELAXED);
+}
+
 __attribute__((visibility("default"))) void vgpu_self_on_launch(int dev, uint64_t wg) {
   ensure_init();
   limiter_on_launch(dev, wg);

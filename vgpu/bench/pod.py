@@ -79,12 +79,18 @@ def build(args):
                 step()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.inference_mode(), torch.cuda.graph(graph):
-            model(x)
+        try:
+            graph = torch.cuda.CUDAGraph()
+            with torch.inference_mode(), torch.cuda.graph(graph):
+                model(x)
+        except Exception as e:  # e.g. an op without capture support: run eagerly
+            sys.stderr.write(f"[pod {args.pod_index}] hipGraph capture failed ({e}); running eagerly\n")
+            torch.cuda.synchronize()
+            return w, step
 
-        def step():  # noqa: F811
+        def replay():
             graph.replay()
+        return w, replay
     return w, step
 
 

@@ -1,0 +1,73 @@
+"""ai-benchmark-equivalent suite on one MI355X: every test id the reference
+publishes (BASELINE.md rows 1.1–5.2) in three scenarios, mirroring the
+reference's comparison (README.md:234-257):
+
+  exclusive   — one pod, whole GPU, no enforcement library
+  vgpu        — `--pods` pods sharing the GPU (default 2 × gpucores=50, gpumem=144000)
+  vgpu-cu25   — 4 pods × gpucores=25 (BASELINE.json config 3 for the training tests)
+
+Prints one JSON line per (test, scenario) and a markdown table at the end.
+    python -m vgpu.bench.suite [--tests 1.1,1.2,...] [--steps 20]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+SCENARIOS = {
+    "exclusive": ["--pods", "1", "--no-shim", "--gpucores", "100", "--gpumem", "0"],
+    "vgpu": ["--pods", "2", "--gpucores", "50", "--gpumem", "144000"],
+    "vgpu-cu25": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000"],
+}
+
+
+def run(test: str, scen: str, steps: int, warmup: int, timeout: int) -> dict:
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--workload", test, "--steps", str(steps),
+           "--warmup", str(warmup), "--no-cap-probe", *SCENARIOS[scen]]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=REPO)
+    except subprocess.TimeoutExpired:
+        return {"test": test, "scenario": scen, "error": "timeout"}
+    js = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    if r.returncode != 0 or not js:
+        return {"test": test, "scenario": scen, "error": r.stderr[-1500:]}
+    d = json.loads(js[-1])
+    return {"test": test, "scenario": scen, "images_s": d["value"], "per_pod": d["per_pod_images_s"],
+            "ms_per_step": d["ms_per_step"]}
+
+
+def main(argv=None) -> int:
+    from vgpu.models import WORKLOADS
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tests", default=",".join(WORKLOADS))
+    ap.add_argument("--scenarios", default="exclusive,vgpu,vgpu-cu25")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--timeout", type=int, default=900)
+    a = ap.parse_args(argv)
+    rows = []
+    for t in a.tests.split(","):
+        for s in a.scenarios.split(","):
+            res = run(t, s, a.steps, a.warmup, a.timeout)
+            print("SUITE " + json.dumps(res), flush=True)
+            rows.append(res)
+    print("\n| test | workload | " + " | ".join(a.scenarios.split(",")) + " | reference 2xV100 (excl / vGPU) |")
+    print("|---|---|" + "---|" * len(a.scenarios.split(",")) + "---|")
+    for t in a.tests.split(","):
+        w = WORKLOADS[t]
+        cells = []
+        for s in a.scenarios.split(","):
+            r = next((x for x in rows if x["test"] == t and x["scenario"] == s), {})
+            cells.append(f"{r.get('images_s', 'err')}")
+        print(f"| {t} | {w.name} {'train' if w.train else 'inf'} b={w.batch} | " + " | ".join(cells)
+              + f" | {w.baseline_exclusive} / {w.baseline_vgpu} |")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
