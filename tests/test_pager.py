@@ -58,6 +58,30 @@ def test_streamed_llama_matches_resident_cpu():
     assert sm.pager.stats.evictions == cfg.layers - 1
 
 
+def test_streamed_llama_pins_prefix_cpu():
+    """Cyclic layer scans thrash LRU; the runner pins a prefix and streams the rest."""
+    from vgpu.models.llama import Llama, LlamaConfig
+    from vgpu.models.streamed import StreamedLlama
+    torch.manual_seed(0)
+    cfg = LlamaConfig.tiny()
+    cfg.layers = 6
+    m = Llama(cfg).eval()
+    tokens = torch.randint(0, cfg.vocab, (1, 4))
+    with torch.inference_mode():
+        ref = m(tokens)
+    lb = sum(p.numel() * 4 for p in m.layers[0].parameters())
+    sm = StreamedLlama(m, budget_bytes=4 * lb, device="cpu", lookahead=1)
+    assert sm.n_resident() == 2
+    for _ in range(3):
+        torch.testing.assert_close(sm(tokens), ref)
+    # token 1 loads all 6 layers, tokens 2-3 stream only the 4 non-resident ones
+    assert sm.pager.stats.swap_in_bytes == (6 + 4 + 4) * lb
+    sm.policy = "lru"
+    s0 = sm.pager.stats.swap_in_bytes
+    sm(tokens)
+    assert sm.pager.stats.swap_in_bytes - s0 >= 4 * lb
+
+
 @pytest.mark.gpu
 def test_streamed_llama_matches_resident(gpu_build):
     from vgpu.models.llama import Llama, LlamaConfig

@@ -95,20 +95,38 @@ class StreamedLlama:
         self.template = tmpl.to_empty(device=self.device)
         return self
 
+    def n_resident(self) -> int:
+        """Layers kept permanently in HBM.  A decoder scans its layers cyclically,
+        which is LRU's worst case (every layer misses once the model exceeds the
+        budget), so the pager pins a prefix of the layers and streams only the
+        rest through a ring of `lookahead + 1` slots."""
+        if getattr(self, "policy", "pin-prefix") == "lru":
+            return 0
+        slots = self.pager.budget // max(self.layer_bytes(), 1)
+        if slots >= self.n:
+            return self.n
+        return max(0, min(self.n, slots - (self.lookahead + 1)))
+
     @torch.inference_mode()
     def forward(self, tokens: torch.Tensor, kv_caches=None, pos: int = 0) -> torch.Tensor:
         cos, sin = self.model.rope(self.device)
         x = self.embed(tokens)
-        self.pager.prefetch([f"L{j}" for j in range(min(self.lookahead, self.n))])
+        n_res = self.n_resident()
+        # the ring fills while the resident prefix computes
+        first = n_res if n_res < self.n else 0
+        self.pager.prefetch([f"L{j}" for j in range(first, min(first + self.lookahead, self.n))])
         for i in range(self.n):
-            ahead = [f"L{j}" for j in range(i + 1, min(i + 1 + self.lookahead, self.n))]
-            self.pager.pin(f"L{i}")
-            flat = self.pager.get(f"L{i}")
-            self.pager.prefetch(ahead)
+            name = f"L{i}"
+            self.pager.pin(name)
+            flat = self.pager.get(name)
+            if i + 1 >= n_res:
+                lo = max(i + 1, n_res)
+                self.pager.prefetch([f"L{j}" for j in range(lo, min(i + 1 + self.lookahead, self.n))])
             params = self.layout.views(flat)
             kv = kv_caches[i] if kv_caches is not None else None
             x = functional_call(self.template, params, (x, cos, sin, kv, pos))
-            self.pager.unpin(f"L{i}")
+            if i >= n_res:
+                self.pager.unpin(name)
         return self.head(self.norm(x[:, -1:]))
 
     __call__ = forward
