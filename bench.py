@@ -55,7 +55,13 @@ def main(argv=None) -> int:
                     help="GPU_MAX_HW_QUEUES per pod (vGPU HW-queue budget; 0 = runtime default)")
     ap.add_argument("--no-cap-probe", action="store_true")
     ap.add_argument("--ready-timeout", type=float, default=1500.0)
+    ap.add_argument("--cpu-smoke", action="store_true",
+                    help="rehearse the multi-rank orchestration on CPU (tests; not a measurement)")
     args = ap.parse_args(argv)
+    if args.cpu_smoke:
+        os.environ["VGPU_BENCH_CPU"] = "1"
+        args.no_shim = True
+        args.no_cap_probe = True
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -12,6 +12,7 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <string>
 #include <thread>
 #include <vector>
@@ -179,6 +180,34 @@ int main(int argc, char** argv) {
       if (el >= secs) break;
     }
     printf("launches=%llu\n", (unsigned long long)n);
+    print_region(dev);
+    return 0;
+  }
+
+  if (sc == "threads") {
+    // Concurrent alloc/free/launch from many threads (race-detector target).
+    int nthreads = argc > 2 ? atoi(argv[2]) : 8;
+    int iters = argc > 3 ? atoi(argv[3]) : 200;
+    std::vector<std::thread> ts;
+    std::atomic<int> fails{0};
+    for (int t = 0; t < nthreads; ++t) {
+      ts.emplace_back([&, t] {
+        hipSetDevice(0);
+        for (int i = 0; i < iters; ++i) {
+          void* p = nullptr;
+          if (hipMalloc(&p, (size_t)(1 + (i + t) % 7) << 20) != hipSuccess) {
+            fails.fetch_add(1);
+            continue;
+          }
+          hipLaunchKernel((const void*)&main, dim3(64), dim3(256), nullptr, 0, nullptr);
+          size_t f = 0, tot = 0;
+          hipMemGetInfo(&f, &tot);
+          hipFree(p);
+        }
+      });
+    }
+    for (auto& th : ts) th.join();
+    printf("thread_fails=%d\n", fails.load());
     print_region(dev);
     return 0;
   }

@@ -1,0 +1,44 @@
+"""bench.py's multi-rank orchestration rehearsed on CPU (gloo, world_size 2,
+two pods per rank): the driver runs the real thing on an 8-GPU node, so the
+rank/pod protocol, barrier and MAX/SUM reductions must be right by construction.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_bench_single_rank_cpu():
+    r = subprocess.run([sys.executable, "bench.py", "--cpu-smoke", "--steps", "3", "--warmup", "1",
+                        "--pods", "2"], cwd=REPO, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["value"] > 0
+    assert len(d["per_pod_images_s"]) == 2
+
+
+def test_bench_two_ranks_gloo_cpu():
+    port = _free_port()
+    env = dict(os.environ)
+    env.pop("HIP_VISIBLE_DEVICES", None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--steps", "3", "--warmup", "1", "--pods", "2", "--cpu-smoke"],
+                       cwd=REPO, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1  # only rank 0 prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 50 * 2 * 2
+    assert d["scaling"] == "weak" and d["ms_per_step"] > 0

@@ -128,30 +128,47 @@ def main(argv=None) -> int:
 
     import torch
     t_init = time.time()
-    w, step = build(args)
+    cpu = os.environ.get("VGPU_BENCH_CPU") == "1"
+    if cpu:
+        # orchestration rehearsal on a CPU-only host (tests): same protocol, tiny work
+        from types import SimpleNamespace
+        w = SimpleNamespace(batch=4)
+        a = torch.randn(256, 256)
+
+        def step():
+            return a @ a
+
+        def sync():
+            pass
+    else:
+        w, step = build(args)
+        sync = torch.cuda.synchronize
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    free, total = torch.cuda.mem_get_info()
-    props = torch.cuda.get_device_properties(0)
-    emit("READY", {"pod": args.pod_index, "init_s": time.time() - t_init, "mem_free": free,
-                   "mem_total": total, "prop_total": props.total_memory,
-                   "cus": props.multi_processor_count, "pid": os.getpid(),
-                   "allocated": torch.cuda.memory_allocated()})
+    sync()
+    if cpu:
+        emit("READY", {"pod": args.pod_index, "init_s": time.time() - t_init, "pid": os.getpid()})
+    else:
+        free, total = torch.cuda.mem_get_info()
+        props = torch.cuda.get_device_properties(0)
+        emit("READY", {"pod": args.pod_index, "init_s": time.time() - t_init, "mem_free": free,
+                       "mem_total": total, "prop_total": props.total_memory,
+                       "cus": props.multi_processor_count, "pid": os.getpid(),
+                       "allocated": torch.cuda.memory_allocated()})
     if not args.no_wait:
         line = sys.stdin.readline()
         if line.strip() != "GO":
             return 3
-    torch.cuda.synchronize()
+    sync()
     t0 = time.monotonic()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     t1 = time.monotonic()
     res = {"pod": args.pod_index, "t0": t0, "t1": t1, "steps": args.steps,
            "samples": args.steps * w.batch, "ms_per_step": 1e3 * (t1 - t0) / max(args.steps, 1),
            "throughput": args.steps * w.batch / max(t1 - t0, 1e-9)}
-    if args.cap_probe:
+    if args.cap_probe and not cpu:
         res.update(cap_probe())
     emit("DONE", res)
     return 0

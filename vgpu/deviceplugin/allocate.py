@@ -34,6 +34,8 @@ from vgpu.k8s import objects as O
 from vgpu.k8s.client import ApiError, KubeClient
 from vgpu.k8s.nodelock import release_node_lock
 
+from vgpu.device.cualloc import CULayout
+
 from .custate import CUMaskState
 from .discovery import Device
 
@@ -139,7 +141,10 @@ def build_container_grant(cfg: DevicePluginConfig, pod: dict, ctr_idx: int, devr
     for d in ordered:
         if d.uuid not in devices:
             raise AllocateError(f"unknown device {d.uuid}")
-    masks = {} if cfg.disable_core_limit else cu_state.allocate(key, [(d.uuid, d.usedcores) for d in ordered])
+    layouts = {d.uuid: CULayout(total_cus=devices[d.uuid].cus or 256,
+                                num_xcc=max(devices[d.uuid].num_xcc or 1, 1)) for d in ordered}
+    masks = {} if cfg.disable_core_limit else cu_state.allocate(
+        key, [(d.uuid, d.usedcores) for d in ordered], layouts)
     g = ContainerGrant()
     env_names = _ctr_env_names(pod, ctr_idx)
     fractional = False

@@ -47,9 +47,13 @@ class CUMaskState:
             m |= g.get(uuid, 0)
         return m
 
-    def allocate(self, container_key: str, requests: list[tuple[str, int]]) -> dict[str, int]:
+    def allocate(self, container_key: str, requests: list[tuple[str, int]],
+                 layouts: dict[str, CULayout] | None = None) -> dict[str, int]:
         """requests: [(device uuid, cores %)] → {uuid: mask} (0 = no spatial mask:
-        exclusive, best-effort, or not enough free granules → temporal limiting)."""
+        exclusive, best-effort, or not enough free granules → temporal limiting).
+        `layouts` gives each device's CU/XCD geometry (a CPX compute partition
+        is one XCD of 32 CUs; SPX is 8 × 32)."""
+        layouts = layouts or {}
         with self._lock:
             grants = self._grants()
             grants.pop(container_key, None)  # re-allocation of the same container
@@ -62,7 +66,7 @@ class CUMaskState:
                 for g in grants.values():
                     used |= g.get(uuid, 0)
                 used |= res.get(uuid, 0)
-                m = alloc_cu_mask(used, cores, self.layout)
+                m = alloc_cu_mask(used, cores, layouts.get(uuid, self.layout))
                 res[uuid] = m or 0
             d = self.dir / container_key
             d.mkdir(parents=True, exist_ok=True)
