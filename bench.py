@@ -51,6 +51,8 @@ def main(argv=None) -> int:
     ap.add_argument("--no-find", action="store_true",
                     help="skip MIOpen find (cudnn.benchmark) during the untimed warmup")
     ap.add_argument("--no-fused", action="store_true", help="plain PyTorch epilogues")
+    ap.add_argument("--conv", choices=("native", "miopen"), default="native",
+                    help="ResNet convolutions: fused MFMA implicit-GEMM kernels or MIOpen")
     ap.add_argument("--hw-queues", type=int, default=1,
                     help="GPU_MAX_HW_QUEUES per pod (vGPU HW-queue budget; 0 = runtime default)")
     ap.add_argument("--no-cap-probe", action="store_true")
@@ -92,7 +94,7 @@ def main(argv=None) -> int:
     pods = launch_pods(specs, device, steps=args.steps, warmup=args.warmup, shim=not args.no_shim,
                        graph=not args.no_graph, cap_probe=not args.no_cap_probe,
                        find=not args.no_find, hw_queues=args.hw_queues or None,
-                       fused=not args.no_fused)
+                       fused=not args.no_fused, conv=args.conv)
     try:
         for p in pods:
             p.ready = p.read_tagged("READY", args.ready_timeout, progress=log)
@@ -163,6 +165,7 @@ def main(argv=None) -> int:
                 "hipgraph": not args.no_graph,
                 "miopen_find": not args.no_find,
                 "fused_epilogues": not args.no_fused,
+                "conv": args.conv,
                 "hw_queues_per_pod": args.hw_queues,
             },
             "per_gpu_images_s": round(per_gpu, 2),

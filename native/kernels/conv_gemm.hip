@@ -1,0 +1,473 @@
+// Implicit-GEMM NHWC bf16 convolution on gfx950 MFMA with fused prologue and
+// epilogue — the hot op of the ai-benchmark CNN workloads (ResNet-V2-50/152).
+//
+// Why a hand-written conv: on MI355X a pre-activation bottleneck is HBM-bound,
+// not MFMA-bound (stage 1 at b=50 346²: 12 GFLOP per 1x1 conv against ~240 MB of
+// activation traffic).  MIOpen convolutions cannot take a prologue or a
+// residual, so a bottleneck costs 7 passes over the 4×-wide activation.  Here
+//
+//   y = act( conv(pro(x), w) + bias[co] + residual )       pro(x) = relu(x*s[c] + t[c])
+//
+// is one kernel: the block-entry BN+ReLU is applied while the input tile is
+// staged into LDS (so the pre-activation is never written), conv bias + ReLU
+// (BN folded into the weights) and the residual add are applied while the
+// output tile leaves.  Per bottleneck the wide activation is read twice and
+// written once instead of read 4× and written 3×.
+//
+// GEMM view: M = N*OH*OW output pixels, N = Cout, K = KS*KS*C with k ordered
+// (kh, kw, c) — exactly PyTorch's channels_last weight [Cout][KS][KS][C].  A
+// 64-wide K tile is one filter tap × 64 input channels, i.e. 128 contiguous
+// bytes of one input pixel (or zeros for padding), so the implicit im2col is a
+// per-row base pointer + tap offset.  Requires C % 64 == 0, Cout % 64 == 0.
+//
+// Tiling for CDNA4: 256 threads = 4 wave64s in 2×2, workgroup tile BM=128 ×
+// BN∈{64,128}, BK=64, mfma_f32_16x16x32_bf16 (lane l holds A[l&15][8(l>>4)..+7]
+// and B[8(l>>4)..+7][l&15]).  Two LDS stages with register prefetch: the global
+// loads of tile t+1 are in flight while tile t is multiplied.  LDS rows are
+// 128 B with a 16-B-slot XOR swizzle (slot ^ row&7) so every ds_read_b128 lane
+// group hits 16 distinct slots (conflict-free).  The epilogue stages the fp32
+// accumulator tile through LDS (row pad 4 floats: conflict-free ds_write_b32)
+// so bias/residual/store are 16-B coalesced per lane.  Workgroups are numbered
+// XCD-aware (bijective remap) so the N-tiles sharing an A panel run on one
+// XCD's L2.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define VGPU_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+// Native 16-B vector (HIP's u32x4 is a class; copies of it go through memcpy
+// and defeat register promotion of the staging arrays).
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+
+constexpr int kThreads = 256;
+constexpr int BK = 64;
+
+struct ConvArgs {
+  const uint16_t* x;     // [N][H][W][C]
+  const uint16_t* w;     // [Cout][KS][KS][C]
+  uint16_t* y;           // [N][OH][OW][Cout]
+  const uint16_t* res;   // [N][OH][OW][Cout] or nullptr
+  const float* bias;     // [Cout] or nullptr
+  const float* pscale;   // [C] prologue scale (PRO only)
+  const float* pshift;   // [C] prologue shift
+  int N, H, W, C, Cout, OH, OW, stride, pad;
+  int M, K, ktiles, cblocks, nM, nN, nwg, act;
+};
+
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+__device__ __forceinline__ void unpack8(const u32x4 v, float (&f)[8]) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+__device__ __forceinline__ u32x4 pack8(const float (&f)[8]) {
+  return u32x4{pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7])};
+}
+
+__device__ __forceinline__ int swz(int row, int slot) { return row * 128 + (((slot ^ (row & 7))) << 4); }
+
+__device__ __forceinline__ void tile_origin(const ConvArgs& a, int tile, int bm, int bn, int& m0,
+                                            int& n0) {
+  // XCD-aware bijective numbering: tiles that run on one XCD (tile % 8 — the grid
+  // stride is a multiple of 8) get consecutive ids, so the N-tiles sharing an A
+  // panel meet in that XCD's L2.
+  const int xcd = tile & 7, q = a.nwg >> 3, r8 = a.nwg & 7;
+  const int id = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (tile >> 3);
+  const int mi = id / a.nN;
+  m0 = mi * bm;
+  n0 = (id - mi * a.nN) * bn;
+}
+
+// Persistent: workgroup b processes tiles b, b+G, b+2G, ... as one flattened
+// sequence of K steps, so the global loads of the next step — including the
+// first step of the next tile, and that tile's residual — are in flight while
+// the current step is multiplied and the current tile's epilogue runs.
+template <int KS, int BM, int BN, bool PRO>
+__global__ void __launch_bounds__(kThreads, 2) conv_gemm_kernel(const ConvArgs a) {
+  constexpr int AR = BM * 8 / kThreads;  // 16-B A chunks per thread per K step
+  constexpr int BR = BN * 8 / kThreads;
+  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int CS = BN + 4;  // epilogue fp32 row stride (pad: conflict-free ds_write_b32)
+  constexpr int PIPE = 2 * STAGE, EPI = BM * CS * 4;
+  constexpr int CPR = BN / 8, RSTEP = kThreads / CPR, RROWS = BM / RSTEP;
+  __shared__ __attribute__((aligned(16))) char smem[PIPE > EPI ? PIPE : EPI];
+
+  const int G = gridDim.x;
+  int tile = blockIdx.x;
+  if (tile >= a.nwg) return;
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int slot = t & 7, r0 = t >> 3;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int chunk = t % CPR, rfirst = t / CPR;
+  const bool has_res = a.res != nullptr;
+
+  int m0, n0;
+  tile_origin(a, tile, BM, BN, m0, n0);
+  int em0 = m0, en0 = n0;  // tile owned by the accumulators (epilogue)
+
+  int64_t abase[AR];
+  int aih[AR], aiw[AR];
+  bool aok[AR];
+#define VGPU_SETUP_ROWS()                                                                    \
+  _Pragma("unroll") for (int i = 0; i < AR; ++i) {                                           \
+    const int m = m0 + r0 + 32 * i;                                                         \
+    aok[i] = m < a.M;                                                                       \
+    const int mm = aok[i] ? m : 0;                                                          \
+    const int ow = mm % a.OW, t2 = mm / a.OW, oh = t2 % a.OH, n = t2 / a.OH;               \
+    aih[i] = oh * a.stride - a.pad;                                                         \
+    aiw[i] = ow * a.stride - a.pad;                                                         \
+    abase[i] = ((int64_t)(n * a.H + aih[i]) * a.W + aiw[i]) * a.C;                          \
+  }
+  u32x4 resA[RROWS], resB[RROWS];
+#define VGPU_LOAD_RES(dst)                                                                   \
+  _Pragma("unroll") for (int i = 0; i < RROWS; ++i) {                                        \
+    const int m = m0 + rfirst + RSTEP * i;                                                  \
+    dst[i] = m < a.M ? *reinterpret_cast<const u32x4*>(a.res + (int64_t)m * a.Cout + n0 + chunk * 8) \
+                     : u32x4{0u, 0u, 0u, 0u};                                               \
+  }
+
+  u32x4 ra[AR], rb[BR];
+  bool rv[AR];
+  // Global → registers for K step ktl of the tile at (m0, n0): implicit im2col
+  // with zero padding for A, a weight panel for B.
+#define VGPU_LOAD_TILE(kt_)                                                                  \
+  {                                                                                          \
+    const int ktl = (kt_);                                                                   \
+    const int tap = ktl / a.cblocks, cb = ktl - tap * a.cblocks;                             \
+    const int kh = tap / KS, kw = tap - kh * KS;                                             \
+    const int64_t toff = (int64_t)(kh * a.W + kw) * a.C + cb * BK + slot * 8;                \
+    _Pragma("unroll") for (int i = 0; i < AR; ++i) {                                         \
+      bool v = aok[i];                                                                       \
+      if (KS != 1 || a.pad != 0) {                                                           \
+        const int ih = aih[i] + kh, iw = aiw[i] + kw;                                        \
+        v = v && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;               \
+      }                                                                                      \
+      rv[i] = v;                                                                             \
+      ra[i] = v ? *reinterpret_cast<const u32x4*>(a.x + abase[i] + toff) : u32x4{0u, 0u, 0u, 0u}; \
+    }                                                                                        \
+    const uint16_t* wp = a.w + (int64_t)(n0 + r0) * a.K + (int64_t)ktl * BK + slot * 8;      \
+    _Pragma("unroll") for (int i = 0; i < BR; ++i)                                           \
+      rb[i] = *reinterpret_cast<const u32x4*>(wp + (int64_t)(32 * i) * a.K);                 \
+  }
+  // Registers → LDS stage st_, applying the prologue to real (non-padding) pixels.
+#define VGPU_STORE_TILE(kt_, st_)                                                            \
+  {                                                                                          \
+    char* sA = smem + (st_) * STAGE;                                                         \
+    char* sB = sA + A_BYTES;                                                                 \
+    if constexpr (PRO) {                                                                     \
+      const int c = ((kt_) % a.cblocks) * BK + slot * 8;                                     \
+      const float4 s0 = *reinterpret_cast<const float4*>(a.pscale + c);                     \
+      const float4 s1 = *reinterpret_cast<const float4*>(a.pscale + c + 4);                  \
+      const float4 h0 = *reinterpret_cast<const float4*>(a.pshift + c);                     \
+      const float4 h1 = *reinterpret_cast<const float4*>(a.pshift + c + 4);                  \
+      const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};                  \
+      const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};                  \
+      _Pragma("unroll") for (int i = 0; i < AR; ++i) {                                       \
+        if (rv[i]) {                                                                         \
+          float e[8];                                                                        \
+          unpack8(ra[i], e);                                                                 \
+          _Pragma("unroll") for (int j = 0; j < 8; ++j) e[j] = fmaxf(e[j] * sc[j] + sh[j], 0.0f); \
+          ra[i] = pack8(e);                                                                  \
+        }                                                                                    \
+      }                                                                                      \
+    }                                                                                        \
+    _Pragma("unroll") for (int i = 0; i < AR; ++i)                                           \
+      *reinterpret_cast<u32x4*>(sA + swz(r0 + 32 * i, slot)) = ra[i];                        \
+    _Pragma("unroll") for (int i = 0; i < BR; ++i)                                           \
+      *reinterpret_cast<u32x4*>(sB + swz(r0 + 32 * i, slot)) = rb[i];                        \
+  }
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  VGPU_SETUP_ROWS()
+  if (has_res) VGPU_LOAD_RES(resA)
+  VGPU_LOAD_TILE(0)
+  VGPU_STORE_TILE(0, 0)
+  __syncthreads();
+
+  int kt = 0, st = 0;
+  for (;;) {
+    int nkt = kt + 1, ntile = tile;
+    if (nkt == a.ktiles) {
+      nkt = 0;
+      ntile = tile + G;
+    }
+    const bool has_next = ntile < a.nwg;
+    if (has_next) {
+      if (nkt == 0) {
+        tile_origin(a, ntile, BM, BN, m0, n0);
+        VGPU_SETUP_ROWS()
+        if (has_res) VGPU_LOAD_RES(resB)
+      }
+      VGPU_LOAD_TILE(nkt)
+    }
+
+    {  // MFMA over the staged K step
+      const char* sA = smem + st * STAGE;
+      const char* sB = sA + A_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[i] = *reinterpret_cast<const bf16x8_t*>(sA + swz(wm * WTM + i * 16 + fr, kk * 4 + fk));
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(wn * WTN + j * 16 + fr, kk * 4 + fk));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+
+    if (nkt == 0) {
+      // Tile done. Epilogue: accumulators → LDS (fp32) → 16-B coalesced
+      // bias + residual + act + store.  The next tile's first step waits in registers.
+      __syncthreads();
+      float* sC = reinterpret_cast<float*>(smem);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            sC[(wm * WTM + i * 16 + fk * 4 + e) * CS + wn * WTN + j * 16 + fr] = acc[i][j][e];
+          acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        }
+      __syncthreads();
+      const int col = en0 + chunk * 8;
+      float bb[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bb[j] = 0.0f;
+      if (a.bias) {
+        const float4 b0 = *reinterpret_cast<const float4*>(a.bias + col);
+        const float4 b1 = *reinterpret_cast<const float4*>(a.bias + col + 4);
+        bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
+        bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+      }
+#pragma unroll
+      for (int i = 0; i < RROWS; ++i) {
+        const int r = rfirst + RSTEP * i, m = em0 + r;
+        if (m < a.M) {
+          const float4 c0 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8);
+          const float4 c1 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8 + 4);
+          float v[8] = {c0.x + bb[0], c0.y + bb[1], c0.z + bb[2], c0.w + bb[3],
+                        c1.x + bb[4], c1.y + bb[5], c1.z + bb[6], c1.w + bb[7]};
+          if (has_res) {
+            float re[8];
+            unpack8(resA[i], re);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] += re[j];
+          }
+          if (a.act) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);
+          }
+          *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = pack8(v);
+        }
+      }
+      if (has_res) {
+#pragma unroll
+        for (int i = 0; i < RROWS; ++i) resA[i] = resB[i];
+      }
+      em0 = m0;
+      en0 = n0;
+      __syncthreads();  // staging reads done before the pipeline reuses LDS
+    }
+    if (!has_next) break;
+    VGPU_STORE_TILE(nkt, st ^ 1)
+    __syncthreads();
+    st ^= 1;
+    kt = nkt;
+    tile = ntile;
+  }
+}
+
+#undef VGPU_SETUP_ROWS
+#undef VGPU_LOAD_RES
+#undef VGPU_LOAD_TILE
+#undef VGPU_STORE_TILE
+
+template <int KS, int BM, int BN, bool PRO>
+hipError_t launch(ConvArgs a, hipStream_t s) {
+  static int occ = 0;  // resident workgroups per CU (LDS / VGPR bound); one value per instantiation
+  if (occ == 0) {
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, conv_gemm_kernel<KS, BM, BN, PRO>, kThreads,
+                                                     0) != hipSuccess || o < 1)
+      o = 1;
+    occ = o;
+  }
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    cus = 256;
+  a.nM = (a.M + BM - 1) / BM;
+  a.nN = a.Cout / BN;
+  a.nwg = a.nM * a.nN;
+  int grid = cus * occ;
+  grid = grid < 8 ? 8 : grid & ~7;  // multiple of 8: a workgroup keeps its XCD's tiles
+  if (a.nwg <= grid) grid = a.nwg;
+  hipLaunchKernelGGL((conv_gemm_kernel<KS, BM, BN, PRO>), dim3(grid), dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int KS, int BM>
+hipError_t dispatch_bn(const ConvArgs& a, bool pro, hipStream_t s) {
+  if (a.Cout % 128 == 0)
+    return pro ? launch<KS, BM, 128, true>(a, s) : launch<KS, BM, 128, false>(a, s);
+  return pro ? launch<KS, BM, 64, true>(a, s) : launch<KS, BM, 64, false>(a, s);
+}
+
+// ---- NHWC 3x3/s2/p1 max pool and fused BN+ReLU+global-average pool -----------
+__global__ void __launch_bounds__(kThreads) maxpool3s2_kernel(const u32x4* __restrict__ x,
+                                                              u32x4* __restrict__ y, int N, int H,
+                                                              int W, int cv, int OH, int OW) {
+  const int64_t total = (int64_t)N * OH * OW * cv;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * kThreads) {
+    const int c = (int)(i % cv);
+    int64_t p = i / cv;
+    const int ow = (int)(p % OW);
+    p /= OW;
+    const int oh = (int)(p % OH);
+    const int n = (int)(p / OH);
+    float m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+#pragma unroll
+    for (int dh = 0; dh < 3; ++dh) {
+      const int ih = oh * 2 - 1 + dh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+#pragma unroll
+      for (int dw = 0; dw < 3; ++dw) {
+        const int iw = ow * 2 - 1 + dw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        float e[8];
+        unpack8(x[(((int64_t)n * H + ih) * W + iw) * cv + c], e);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], e[j]);
+      }
+    }
+    y[i] = pack8(m);
+  }
+}
+
+// out[n][c] = mean_hw relu(x[n,h,w,c]*s[c] + t[c]); grid (N, ceil(cv/64)), 4 waves split pixels.
+__global__ void __launch_bounds__(kThreads) ssr_mean_kernel(const u32x4* __restrict__ x,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ shift,
+                                                            u32x4* __restrict__ y, int HW, int cv) {
+  __shared__ float part[4][64][8];
+  const int n = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + lane;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c < cv) {
+    float sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sc[j] = scale[c * 8 + j]; sh[j] = shift[c * 8 + j]; }
+    for (int p = wave; p < HW; p += 4) {
+      float e[8];
+      unpack8(x[((int64_t)n * HW + p) * cv + c], e);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += fmaxf(e[j] * sc[j] + sh[j], 0.0f);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[wave][lane][j] = acc[j];
+  __syncthreads();
+  if (wave == 0 && c < cv) {
+    const float inv = 1.0f / (float)HW;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      o[j] = (part[0][lane][j] + part[1][lane][j] + part[2][lane][j] + part[3][lane][j]) * inv;
+    y[(int64_t)n * cv + c] = pack8(o);
+  }
+}
+
+}  // namespace
+
+// Returns 0, a hipError_t, or -1 for an unsupported shape (checked before any launch).
+VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void* res,
+                              const float* bias, const float* pscale, const float* pshift, int N,
+                              int H, int W, int C, int Cout, int KS, int stride, int pad, int act,
+                              hipStream_t s) {
+  if (C % 64 || Cout % 64 || (KS != 1 && KS != 3) || stride < 1 || pad < 0 || N < 1) return -1;
+  if ((pscale == nullptr) != (pshift == nullptr)) return -1;
+  ConvArgs a{};
+  a.x = static_cast<const uint16_t*>(x);
+  a.w = static_cast<const uint16_t*>(w);
+  a.y = static_cast<uint16_t*>(y);
+  a.res = static_cast<const uint16_t*>(res);
+  a.bias = bias;
+  a.pscale = pscale;
+  a.pshift = pshift;
+  a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.stride = stride; a.pad = pad;
+  a.OH = (H + 2 * pad - KS) / stride + 1;
+  a.OW = (W + 2 * pad - KS) / stride + 1;
+  if (a.OH < 1 || a.OW < 1) return -1;
+  const int64_t M = (int64_t)N * a.OH * a.OW;
+  if (M > (int64_t)1 << 30) return -1;
+  a.M = (int)M;
+  a.K = KS * KS * C;
+  a.cblocks = C / 64;
+  a.ktiles = KS * KS * a.cblocks;
+  a.act = act != 0;
+  const bool pro = pscale != nullptr;
+  // Small-M layers (late stages) use 64-row tiles so the grid still fills the chip.
+  const int bn = (Cout % 128 == 0) ? 128 : 64;
+  const int64_t tiles128 = (int64_t)((a.M + 127) / 128) * (Cout / bn);
+  const bool small = tiles128 < 512;
+  hipError_t e;
+  if (KS == 1)
+    e = small ? dispatch_bn<1, 64>(a, pro, s) : dispatch_bn<1, 128>(a, pro, s);
+  else
+    e = small ? dispatch_bn<3, 64>(a, pro, s) : dispatch_bn<3, 128>(a, pro, s);
+  return (int)e;
+}
+
+VGPU_API int vgpu_maxpool3s2_nhwc(const void* x, void* y, int N, int H, int W, int C,
+                                  hipStream_t s) {
+  if (C % 8) return -1;
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  const int64_t total = (int64_t)N * OH * OW * (C / 8);
+  const int grid = (int)((total + kThreads - 1) / kThreads < 256 * 16 ? (total + kThreads - 1) / kThreads
+                                                                       : 256 * 16);
+  hipLaunchKernelGGL(maxpool3s2_kernel, dim3(grid), dim3(kThreads), 0, s,
+                     static_cast<const u32x4*>(x), static_cast<u32x4*>(y), N, H, W, C / 8, OH, OW);
+  return (int)hipGetLastError();
+}
+
+VGPU_API int vgpu_scale_shift_relu_mean_nhwc(const void* x, const float* scale, const float* shift,
+                                             void* y, int N, int HW, int C, hipStream_t s) {
+  if (C % 8) return -1;
+  const int cv = C / 8;
+  hipLaunchKernelGGL(ssr_mean_kernel, dim3(N, (cv + 63) / 64), dim3(kThreads), 0, s,
+                     static_cast<const u32x4*>(x), scale, shift, static_cast<u32x4*>(y), HW, cv);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,105 @@
+"""MFMA implicit-GEMM convolution (native/kernels/conv_gemm.hip), stem max-pool and
+the fused BN+ReLU+mean against plain-PyTorch fp32 references; the native ResNet
+runner against the module."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last
+
+
+@pytest.fixture(scope="module")
+def C(gpu_build):
+    from vgpu.ops import conv
+    return conv
+
+
+def _t(shape, seed, scale=1.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(shape, generator=g) * scale).to(torch.bfloat16).cuda().contiguous(memory_format=CL)
+
+
+def _f(shape, seed, lo=-0.5, hi=0.5):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.rand(shape, generator=g) * (hi - lo) + lo).cuda().contiguous()
+
+
+CASES = [
+    # n, c, h, w, cout, ks, stride, pad, bias, act, pro, res
+    (2, 64, 9, 11, 64, 1, 1, 0, False, "none", False, False),
+    (2, 256, 9, 11, 64, 1, 1, 0, True, "relu", True, False),     # conv1: BN+ReLU prologue
+    (2, 64, 9, 11, 256, 1, 1, 0, False, "none", False, True),    # conv3: residual
+    (3, 256, 13, 13, 512, 1, 2, 0, False, "none", True, False),  # strided projection shortcut
+    (2, 64, 9, 11, 64, 3, 1, 1, True, "relu", False, False),     # conv2
+    (2, 128, 15, 15, 128, 3, 2, 1, True, "relu", False, False),  # strided conv2
+    (1, 192, 7, 5, 320, 3, 1, 1, True, "none", True, True),      # everything, odd sizes
+    (5, 512, 6, 6, 2048, 1, 1, 0, False, "none", False, True),   # stage-4 conv3, M % 128 != 0
+    (1, 2048, 3, 3, 512, 1, 1, 0, True, "relu", True, False),    # deep K
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c[:8])))
+def test_conv_matches_fp32(C, case):
+    n, c, h, w, cout, ks, stride, pad, has_bias, act, has_pro, has_res = case
+    x = _t((n, c, h, w), 1)
+    wt = _t((cout, c, ks, ks), 2, scale=(2.0 / (c * ks * ks)) ** 0.5)
+    bias = _f((cout,), 3) if has_bias else None
+    pro = (_f((c,), 4, 0.5, 1.5), _f((c,), 5)) if has_pro else None
+    oh, ow = C.out_hw(h, w, ks, stride, pad)
+    res = _t((n, cout, oh, ow), 6) if has_res else None
+    got = C.conv2d(x, wt, bias, stride=stride, padding=pad, act=act, pro=pro, residual=res)
+    ref = C.conv2d_ref(x, wt, bias, stride=stride, padding=pad, act=act, pro=pro, residual=res)
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=CL)
+    torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+def test_conv_asymmetric_exact(C):
+    """Integer data (exact in bf16/fp32): catches any row/col or k-order swap."""
+    n, c, h, w, cout = 1, 64, 4, 5, 128
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = torch.randint(-2, 3, (n, c, h, w), generator=g).to(torch.bfloat16).cuda().contiguous(memory_format=CL)
+    wt = torch.randint(-2, 3, (cout, c, 3, 3), generator=g).to(torch.bfloat16).cuda().contiguous(memory_format=CL)
+    got = C.conv2d(x, wt, stride=1, padding=1)
+    ref = C.conv2d_ref(x, wt, stride=1, padding=1)
+    assert torch.equal(got.float(), ref)
+
+
+def test_conv_rejects_unsupported(C):
+    x = _t((1, 3, 8, 8), 0)
+    with pytest.raises(ValueError):
+        C.conv2d(x, _t((64, 3, 7, 7), 1))
+    with pytest.raises(ValueError):
+        C.conv2d(_t((1, 64, 8, 8), 0).contiguous(), _t((64, 64, 1, 1), 1).contiguous())
+
+
+def test_maxpool(C):
+    x = _t((2, 64, 13, 12), 7)
+    torch.testing.assert_close(C.maxpool3s2(x).float(), C.maxpool3s2_ref(x), atol=0, rtol=0)
+
+
+def test_scale_shift_relu_mean(C):
+    x = _t((3, 2048, 5, 7), 8)
+    s, b = _f((2048,), 9, 0.5, 1.5), _f((2048,), 10)
+    torch.testing.assert_close(C.scale_shift_relu_mean(x, s, b).float(),
+                               C.scale_shift_relu_mean_ref(x, s, b), atol=1e-2, rtol=1e-2)
+
+
+def test_native_resnet_matches_module(gpu_build):
+    from vgpu.models.resnet import FusedResNetV2Inference, resnet_v2_50
+    torch.manual_seed(0)
+    m = resnet_v2_50().cuda().eval()
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_mean.uniform_(-0.1, 0.1)
+            mod.running_var.uniform_(0.5, 1.5)
+            mod.weight.data.uniform_(0.5, 1.5)
+            mod.bias.data.uniform_(-0.1, 0.1)
+    x = torch.randn(2, 3, 128, 128, device="cuda")
+    with torch.no_grad():
+        ref = m.float()(x.contiguous(memory_format=CL))
+    mb = m.to(torch.bfloat16).to(memory_format=CL)
+    fm = FusedResNetV2Inference(mb, conv="native")
+    got = fm(x.to(torch.bfloat16).contiguous(memory_format=CL)).float()
+    rel = (got - ref).norm() / ref.norm()
+    assert rel < 0.05, float(rel)

@@ -1,0 +1,92 @@
+"""Per-layer timing of the MFMA implicit-GEMM convolution against MIOpen on the
+ResNet-V2-50 layer shapes of ai-benchmark test 1.1 (b=50, 346²).
+
+    python -m vgpu.bench.convnative [--batch 50 --size 346 --iters 20]
+
+Prints one JSON line per layer: native µs (with its fused prologue/epilogue),
+MIOpen µs (bare convolution after find), TFLOP/s, and the native kernel's
+effective HBM bandwidth (compulsory bytes / time).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+
+
+def layer_shapes(batch: int, size: int):
+    """(name, n, c, h, w, cout, ks, stride, pad, bias/act, prologue, residual) of every
+    distinct convolution after the stem."""
+    h = ((size + 6 - 7) // 2 + 1 + 2 - 3) // 2 + 1
+    cin = 64
+    out = []
+    for i, (n_blocks, width) in enumerate(zip((3, 4, 6, 3), (64, 128, 256, 512))):
+        for j in range(min(n_blocks, 2)):
+            stride = 2 if (j == 0 and i > 0) else 1
+            cout = width * 4
+            tag = f"s{i + 1}b{j + 1}"
+            oh = (h + 2 - 3) // stride + 1
+            if j == 0:
+                out.append((f"{tag}.sc", batch, cin, h, h, cout, 1, stride, 0, False, True, False))
+            out.append((f"{tag}.conv1", batch, cin, h, h, width, 1, 1, 0, True, True, False))
+            out.append((f"{tag}.conv2", batch, width, h, h, width, 3, stride, 1, True, False, False))
+            out.append((f"{tag}.conv3", batch, width, oh, oh, cout, 1, 1, 0, False, False, True))
+            h, cin = oh, cout
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=50)
+    ap.add_argument("--size", type=int, default=346)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--no-miopen", action="store_true")
+    args = ap.parse_args(argv)
+
+    import torch
+    import torch.nn.functional as F
+    from vgpu.ops import conv as C
+    torch.backends.cudnn.benchmark = True
+    cl = torch.channels_last
+    dev = "cuda"
+
+    def timeit(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / args.iters
+
+    tot_n = tot_m = 0.0
+    for name, n, c, h, w, cout, ks, stride, pad, ba, pro, res in layer_shapes(args.batch, args.size):
+        x = torch.randn(n, c, h, w, device=dev, dtype=torch.bfloat16).contiguous(memory_format=cl)
+        wt = (torch.randn(cout, c, ks, ks, device=dev) * (2 / (c * ks * ks)) ** 0.5).to(
+            torch.bfloat16).contiguous(memory_format=cl)
+        oh, ow = C.out_hw(h, w, ks, stride, pad)
+        bias = torch.zeros(cout, device=dev) if ba else None
+        pp = (torch.ones(c, device=dev), torch.zeros(c, device=dev)) if pro else None
+        r = torch.randn(n, cout, oh, ow, device=dev, dtype=torch.bfloat16).contiguous(memory_format=cl) if res else None
+        y = torch.empty(n, cout, oh, ow, device=dev, dtype=torch.bfloat16).contiguous(memory_format=cl)
+        t_nat = timeit(lambda: C.conv2d(x, wt, bias, stride=stride, padding=pad,
+                                        act="relu" if ba else "none", pro=pp, residual=r, out=y))
+        t_mio = None if args.no_miopen else timeit(lambda: F.conv2d(x, wt, stride=stride, padding=pad))
+        flop = 2.0 * n * oh * ow * cout * c * ks * ks
+        in_bytes = x.numel() * 2 if (ks == 1 and stride == 1) or ks == 3 else n * oh * ow * c * 2
+        nbytes = in_bytes + wt.numel() * 2 + y.numel() * 2 * (2 if res else 1)
+        tot_n += t_nat
+        tot_m += t_mio or 0.0
+        print(json.dumps({"layer": name, "M": n * oh * ow, "K": c * ks * ks, "N": cout,
+                          "native_us": round(t_nat, 1),
+                          "miopen_us": None if t_mio is None else round(t_mio, 1),
+                          "native_tflops": round(flop / t_nat / 1e6, 1),
+                          "native_tbps": round(nbytes / t_nat / 1e6, 2)}), flush=True)
+    print(json.dumps({"total_native_us": round(tot_n, 1), "total_miopen_us": round(tot_m, 1)}))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -83,7 +83,8 @@ class Pod:
 def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, shim: bool = True,
                 graph: bool = True, cap_probe: bool = False, find: bool = False,
                 workdir: str | None = None, oversubscribe: bool = False,
-                hw_queues: int | None = None, fused: bool = True) -> list[Pod]:
+                hw_queues: int | None = None, fused: bool = True,
+                conv: str = "native") -> list[Pod]:
     """Start one process per pod on physical device `device`."""
     workdir = workdir or tempfile.mkdtemp(prefix="vgpu-pods-")
     used = 0
@@ -124,6 +125,7 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
             cmd.append("--find")
         if not fused:
             cmd.append("--no-fused")
+        cmd += ["--conv", conv]
         proc = subprocess.Popen(cmd, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                 text=True, bufsize=1, cwd=str(REPO))
         pods.append(Pod(i, proc, region, {k: v for k, v in cenv.items()}))

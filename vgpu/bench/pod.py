@@ -60,7 +60,7 @@ def build(args):
         model.eval()
         from vgpu.models.resnet import FusedResNetV2Inference, ResNetV2
         if isinstance(model, ResNetV2) and not args.no_fused:
-            model = FusedResNetV2Inference(model)
+            model = FusedResNetV2Inference(model, conv=getattr(args, "conv", "native"))
         elif hasattr(model, "fuse_for_inference"):
             model.fuse_for_inference()
 
@@ -123,6 +123,8 @@ def main(argv=None) -> int:
     ap.add_argument("--find", action="store_true", help="cudnn.benchmark (MIOpen find) in warmup")
     ap.add_argument("--cap-probe", action="store_true")
     ap.add_argument("--no-fused", action="store_true", help="plain PyTorch epilogues (no HIP fusion)")
+    ap.add_argument("--conv", choices=("native", "miopen"), default="native",
+                    help="ResNet convolutions: fused MFMA kernels (native) or MIOpen + fused epilogues")
     ap.add_argument("--no-wait", action="store_true", help="do not wait for GO on stdin")
     args = ap.parse_args(argv)
 

@@ -97,17 +97,28 @@ class ResNetV2(nn.Module):
 
 
 class FusedResNetV2Inference(nn.Module):
-    """Inference runner for a ResNetV2 with every BN folded and every
-    bias / ReLU / residual-add / pre-activation BN done by the fused NHWC HIP
-    epilogues (vgpu.ops.fused): 3 activation passes per bottleneck instead of 7,
-    and no MIOpen bias kernels (convolutions run bias-free).
+    """Inference runner for a ResNetV2 with every BN folded.
 
-    Numerically equivalent to `ResNetV2.eval()` up to bf16 rounding of the
-    folded weights (tests/test_gpu_fused.py).
+    conv="native" (default): every convolution after the stem is the MFMA
+    implicit-GEMM kernel of native/kernels/conv_gemm.hip with its neighbours
+    fused in — the block-entry BN+ReLU as the prologue of conv1 and of the
+    projection shortcut, folded-BN bias + ReLU as the epilogue of conv1/conv2,
+    the residual add as the epilogue of conv3 — so a bottleneck is 3 (or 4)
+    kernels and the pre-activation tensor is never materialised.  The stem
+    max-pool and the final BN+ReLU+global-mean are hand-written kernels too.
+
+    conv="miopen": MIOpen convolutions + the fused NHWC epilogues of
+    vgpu.ops.fused (3 activation passes per bottleneck instead of 7).
+
+    Both are numerically equivalent to `ResNetV2.eval()` up to bf16 rounding
+    (tests/test_gpu_fused.py, tests/test_gpu_conv.py).
     """
 
-    def __init__(self, m: ResNetV2):
+    def __init__(self, m: ResNetV2, conv: str = "native"):
         super().__init__()
+        if conv not in ("native", "miopen"):
+            raise ValueError(conv)
+        self.conv = conv
         from vgpu.ops.fused import bn_scale_shift
         m = m.eval()
         dt = m.stem.weight.dtype
@@ -138,6 +149,26 @@ class FusedResNetV2Inference(nn.Module):
 
     @torch.no_grad()
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.conv == "native":
+            return self._forward_native(x)
+        return self._forward_miopen(x)
+
+    def _forward_native(self, x: torch.Tensor) -> torch.Tensor:
+        from vgpu.ops import conv as C
+        x = F.conv2d(x, self.stem_w, stride=2, padding=3)  # C=3: MIOpen
+        x = C.maxpool3s2(x.contiguous(memory_format=torch.channels_last))
+        for b in self.blocks:
+            pro = b["in"]
+            if b["sc"] is None:
+                sc = x
+            else:
+                sc = C.conv2d(x, b["sc"][0], stride=b["sc"][1], pro=pro)
+            h = C.conv2d(x, b["w1"], b["b1"], act="relu", pro=pro)
+            h = C.conv2d(h, b["w2"], b["b2"], stride=b["stride"], padding=1, act="relu")
+            x = C.conv2d(h, b["w3"], residual=sc)
+        return self.fc(C.scale_shift_relu_mean(x, *self.out_ss))
+
+    def _forward_miopen(self, x: torch.Tensor) -> torch.Tensor:
         from vgpu.ops.fused import add_scale_shift_act, bias_act_, scale_shift_act
         x = F.max_pool2d(F.conv2d(x, self.stem_w, stride=2, padding=3), 3, 2, 1)
         x = x.contiguous(memory_format=torch.channels_last)

@@ -1,0 +1,130 @@
+"""MFMA implicit-GEMM NHWC convolution with fused prologue / epilogue
+(native/kernels/conv_gemm.hip) and its fp32 PyTorch reference.
+
+    y = act(conv(pro(x), w) + bias + residual),   pro(x) = relu(x * scale[c] + shift[c])
+
+Tensors: bf16, NCHW-shaped, channels_last memory.  Supported: 1x1 and 3x3
+filters, any stride / padding, C % 64 == 0 and Cout % 64 == 0 (every
+convolution of ResNet-V2 after the stem).  No silent fallback: unsupported
+shapes raise, a missing extension raises NativeMissing.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.nn.functional as F
+
+from vgpu.native import load_kernels
+
+_CL = torch.channels_last
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t: torch.Tensor | None):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _nhwc(t: torch.Tensor, name: str) -> None:
+    if t.dtype != torch.bfloat16 or not t.is_cuda or t.dim() != 4:
+        raise TypeError(f"{name}: expected a 4-D bf16 CUDA tensor")
+    if not t.is_contiguous(memory_format=_CL):
+        raise ValueError(f"{name}: expected channels_last memory format")
+
+
+def supported(c: int, cout: int, ks: int) -> bool:
+    return c % 64 == 0 and cout % 64 == 0 and ks in (1, 3)
+
+
+def out_hw(h: int, w: int, ks: int, stride: int, pad: int) -> tuple[int, int]:
+    return (h + 2 * pad - ks) // stride + 1, (w + 2 * pad - ks) // stride + 1
+
+
+def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *,
+           stride: int = 1, padding: int = 0, act: str = "none",
+           pro: tuple[torch.Tensor, torch.Tensor] | None = None,
+           residual: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """x [N,C,H,W] bf16 channels_last; w [Cout,C,k,k] bf16 channels_last;
+    bias fp32 [Cout]; pro = (scale, shift) fp32 [C] (BN+ReLU on the input);
+    residual [N,Cout,OH,OW] bf16 channels_last; act 'none' | 'relu'."""
+    _nhwc(x, "x")
+    _nhwc(w, "w")
+    n, c, h, wd = x.shape
+    cout, cw, ks, ks2 = w.shape
+    if cw != c or ks != ks2 or not supported(c, cout, ks):
+        raise ValueError(f"unsupported conv: x {tuple(x.shape)} w {tuple(w.shape)}")
+    oh, ow = out_hw(h, wd, ks, stride, padding)
+    if act not in ("none", "relu"):
+        raise ValueError(act)
+    for p in ((bias,) + (pro if pro is not None else ())):
+        if p is not None and (p.dtype != torch.float32 or not p.is_contiguous() or not p.is_cuda):
+            raise TypeError("bias / prologue parameters must be contiguous fp32 CUDA tensors")
+    if bias is not None and bias.numel() != cout:
+        raise ValueError("bias size")
+    if pro is not None and (pro[0].numel() != c or pro[1].numel() != c):
+        raise ValueError("prologue size")
+    if residual is not None:
+        _nhwc(residual, "residual")
+        if tuple(residual.shape) != (n, cout, oh, ow):
+            raise ValueError("residual shape")
+    if out is None:
+        out = torch.empty((n, cout, oh, ow), dtype=x.dtype, device=x.device, memory_format=_CL)
+    else:
+        _nhwc(out, "out")
+    rc = load_kernels().vgpu_conv2d_nhwc(
+        _ptr(x), _ptr(w), _ptr(out), _ptr(residual), _ptr(bias),
+        _ptr(pro[0] if pro else None), _ptr(pro[1] if pro else None),
+        n, h, wd, c, cout, ks, stride, padding, 1 if act == "relu" else 0, _stream())
+    if rc != 0:
+        raise RuntimeError(f"vgpu_conv2d_nhwc: error {rc}")
+    return out
+
+
+def maxpool3s2(x: torch.Tensor) -> torch.Tensor:
+    """3x3 / stride 2 / pad 1 max pool, NHWC bf16 (the ResNet stem pool)."""
+    _nhwc(x, "x")
+    n, c, h, w = x.shape
+    oh, ow = out_hw(h, w, 3, 2, 1)
+    out = torch.empty((n, c, oh, ow), dtype=x.dtype, device=x.device, memory_format=_CL)
+    rc = load_kernels().vgpu_maxpool3s2_nhwc(_ptr(x), _ptr(out), n, h, w, c, _stream())
+    if rc != 0:
+        raise RuntimeError(f"vgpu_maxpool3s2_nhwc: error {rc}")
+    return out
+
+
+def scale_shift_relu_mean(x: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor) -> torch.Tensor:
+    """mean over H,W of relu(x*scale[c] + shift[c]) → [N, C] bf16 (final BN+ReLU+pool)."""
+    _nhwc(x, "x")
+    n, c, h, w = x.shape
+    out = torch.empty((n, c), dtype=x.dtype, device=x.device)
+    rc = load_kernels().vgpu_scale_shift_relu_mean_nhwc(_ptr(x), _ptr(scale), _ptr(shift), _ptr(out),
+                                                       n, h * w, c, _stream())
+    if rc != 0:
+        raise RuntimeError(f"vgpu_scale_shift_relu_mean_nhwc: error {rc}")
+    return out
+
+
+# ---- fp32 references -----------------------------------------------------------------
+def conv2d_ref(x, w, bias=None, *, stride=1, padding=0, act="none", pro=None, residual=None):
+    xf = x.float()
+    if pro is not None:
+        xf = (xf * pro[0].view(1, -1, 1, 1) + pro[1].view(1, -1, 1, 1)).clamp_min(0)
+        xf = xf.to(x.dtype).float()  # the kernel stages the prologue output as bf16
+    y = F.conv2d(xf, w.float(), None if bias is None else bias.float(), stride=stride, padding=padding)
+    if residual is not None:
+        y = y + residual.float()
+    if act == "relu":
+        y = y.clamp_min(0)
+    return y
+
+
+def maxpool3s2_ref(x):
+    return F.max_pool2d(x.float(), 3, 2, 1)
+
+
+def scale_shift_relu_mean_ref(x, scale, shift):
+    y = (x.float() * scale.view(1, -1, 1, 1) + shift.view(1, -1, 1, 1)).clamp_min(0)
+    return y.mean(dim=(2, 3))
