@@ -56,6 +56,7 @@ struct ConvArgs {
   const float* pshift;   // [C] prologue shift
   int N, H, W, C, Cout, OH, OW, stride, pad;
   int M, K, ktiles, cblocks, nM, nN, nwg, act;
+  uint32_t x_bytes, y_bytes;  // buffer-resource extents (< 2^31: the host splits the batch)
 };
 
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
@@ -91,11 +92,20 @@ __device__ __forceinline__ void tile_origin(const ConvArgs& a, int tile, int bm,
   n0 = (id - mi * a.nN) * bn;
 }
 
+constexpr uint32_t kOOB = 0x80000000u;  // buffer offset past num_records: loads return 0
+
 // Persistent: workgroup b processes tiles b, b+G, b+2G, ... as one flattened
 // sequence of K steps, so the global loads of the next step — including the
-// first step of the next tile, and that tile's residual — are in flight while
-// the current step is multiplied and the current tile's epilogue runs.
-template <int KS, int BM, int BN, bool PRO>
+// first step of the next tile — are in flight while the current step is
+// multiplied and the current tile's epilogue runs.
+//
+// Every global load in the loop is unconditional: activations and the residual
+// go through buffer loads whose out-of-range offset (kOOB) returns zeros, which
+// gives the conv zero padding and the M tail for free and keeps hipcc from
+// branching around loads (a branch around a load makes it wait vmcnt(0) and
+// de-pipelines the loop).  The residual of a tile is fetched in its last K step,
+// issued before that step's A/B prefetch so the epilogue waits only for it.
+template <int KS, int BM, int BN, bool PRO, bool RES>
 __global__ void __launch_bounds__(kThreads, 2) conv_gemm_kernel(const ConvArgs a) {
   constexpr int AR = BM * 8 / kThreads;  // 16-B A chunks per thread per K step
   constexpr int BR = BN * 8 / kThreads;
@@ -117,14 +127,16 @@ __global__ void __launch_bounds__(kThreads, 2) conv_gemm_kernel(const ConvArgs a
   const int slot = t & 7, r0 = t >> 3;
   const int fr = lane & 15, fk = lane >> 4;
   const int chunk = t % CPR, rfirst = t / CPR;
-  const bool has_res = a.res != nullptr;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.x), 0, a.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(RES ? a.res : a.x), 0, RES ? a.y_bytes : 0u, 0x00020000);
 
-  int m0, n0;
+  int m0, n0;  // tile whose A/B are being loaded
   tile_origin(a, tile, BM, BN, m0, n0);
   int em0 = m0, en0 = n0;  // tile owned by the accumulators (epilogue)
 
-  int64_t abase[AR];
-  int aih[AR], aiw[AR];
+  int abase[AR], aih[AR], aiw[AR];  // byte offset of the window origin, origin row/col
   bool aok[AR];
 #define VGPU_SETUP_ROWS()                                                                    \
   _Pragma("unroll") for (int i = 0; i < AR; ++i) {                                           \
@@ -134,41 +146,45 @@ __global__ void __launch_bounds__(kThreads, 2) conv_gemm_kernel(const ConvArgs a
     const int ow = mm % a.OW, t2 = mm / a.OW, oh = t2 % a.OH, n = t2 / a.OH;               \
     aih[i] = oh * a.stride - a.pad;                                                         \
     aiw[i] = ow * a.stride - a.pad;                                                         \
-    abase[i] = ((int64_t)(n * a.H + aih[i]) * a.W + aiw[i]) * a.C;                          \
-  }
-  u32x4 resA[RROWS], resB[RROWS];
-#define VGPU_LOAD_RES(dst)                                                                   \
-  _Pragma("unroll") for (int i = 0; i < RROWS; ++i) {                                        \
-    const int m = m0 + rfirst + RSTEP * i;                                                  \
-    dst[i] = m < a.M ? *reinterpret_cast<const u32x4*>(a.res + (int64_t)m * a.Cout + n0 + chunk * 8) \
-                     : u32x4{0u, 0u, 0u, 0u};                                               \
+    abase[i] = ((n * a.H + aih[i]) * a.W + aiw[i]) * a.C * 2;                               \
   }
 
-  u32x4 ra[AR], rb[BR];
-  bool rv[AR];
+  // Two register sets (A/B chunks + validity + K step): the loads of step s+2
+  // are issued while step s is multiplied and step s+1 waits in the other set.
+  u32x4 ra0[AR], rb0[BR], ra1[AR], rb1[BR], res[RROWS];
+  bool rv0[AR], rv1[AR];
+  int kt0 = 0, kt1 = 0;
   // Global → registers for K step ktl of the tile at (m0, n0): implicit im2col
-  // with zero padding for A, a weight panel for B.
-#define VGPU_LOAD_TILE(kt_)                                                                  \
+  // (zero padding via out-of-range buffer offsets) for A, a weight panel for B.
+#define VGPU_LOAD_TILE(kt_, RA, RB, RV)                                                      \
   {                                                                                          \
     const int ktl = (kt_);                                                                   \
     const int tap = ktl / a.cblocks, cb = ktl - tap * a.cblocks;                             \
     const int kh = tap / KS, kw = tap - kh * KS;                                             \
-    const int64_t toff = (int64_t)(kh * a.W + kw) * a.C + cb * BK + slot * 8;                \
+    const int toff = ((kh * a.W + kw) * a.C + cb * BK + slot * 8) * 2;                       \
     _Pragma("unroll") for (int i = 0; i < AR; ++i) {                                         \
       bool v = aok[i];                                                                       \
       if (KS != 1 || a.pad != 0) {                                                           \
         const int ih = aih[i] + kh, iw = aiw[i] + kw;                                        \
         v = v && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;               \
       }                                                                                      \
-      rv[i] = v;                                                                             \
-      ra[i] = v ? *reinterpret_cast<const u32x4*>(a.x + abase[i] + toff) : u32x4{0u, 0u, 0u, 0u}; \
+      RV[i] = v;                                                                             \
+      RA[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, v ? (uint32_t)(abase[i] + toff) : kOOB, 0, 0); \
     }                                                                                        \
     const uint16_t* wp = a.w + (int64_t)(n0 + r0) * a.K + (int64_t)ktl * BK + slot * 8;      \
     _Pragma("unroll") for (int i = 0; i < BR; ++i)                                           \
-      rb[i] = *reinterpret_cast<const u32x4*>(wp + (int64_t)(32 * i) * a.K);                 \
+      RB[i] = *reinterpret_cast<const u32x4*>(wp + (int64_t)(32 * i) * a.K);                 \
+  }
+  // Residual rows of the epilogue tile; real loads only when `last` (else kOOB: no traffic).
+#define VGPU_LOAD_RES(last_)                                                                 \
+  _Pragma("unroll") for (int i = 0; i < RROWS; ++i) {                                        \
+    const int m = em0 + rfirst + RSTEP * i;                                                 \
+    const bool v = (last_) && m < a.M;                                                      \
+    res[i] = __builtin_amdgcn_raw_buffer_load_b128(                                         \
+        rr, v ? (uint32_t)(((int64_t)m * a.Cout + en0 + chunk * 8) * 2) : kOOB, 0, 0);      \
   }
   // Registers → LDS stage st_, applying the prologue to real (non-padding) pixels.
-#define VGPU_STORE_TILE(kt_, st_)                                                            \
+#define VGPU_STORE_TILE(kt_, st_, RA, RB, RV)                                                \
   {                                                                                          \
     char* sA = smem + (st_) * STAGE;                                                         \
     char* sB = sA + A_BYTES;                                                                 \
@@ -181,18 +197,32 @@ __global__ void __launch_bounds__(kThreads, 2) conv_gemm_kernel(const ConvArgs a
       const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};                  \
       const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};                  \
       _Pragma("unroll") for (int i = 0; i < AR; ++i) {                                       \
-        if (rv[i]) {                                                                         \
-          float e[8];                                                                        \
-          unpack8(ra[i], e);                                                                 \
-          _Pragma("unroll") for (int j = 0; j < 8; ++j) e[j] = fmaxf(e[j] * sc[j] + sh[j], 0.0f); \
-          ra[i] = pack8(e);                                                                  \
+        float e[8];                                                                          \
+        unpack8(RA[i], e);                                                                   \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                      \
+          const float f = fmaxf(e[j] * sc[j] + sh[j], 0.0f);                                 \
+          e[j] = RV[i] ? f : 0.0f;                                                           \
         }                                                                                    \
+        RA[i] = pack8(e);                                                                    \
       }                                                                                      \
     }                                                                                        \
     _Pragma("unroll") for (int i = 0; i < AR; ++i)                                           \
-      *reinterpret_cast<u32x4*>(sA + swz(r0 + 32 * i, slot)) = ra[i];                        \
+      *reinterpret_cast<u32x4*>(sA + swz(r0 + 32 * i, slot)) = RA[i];                        \
     _Pragma("unroll") for (int i = 0; i < BR; ++i)                                           \
-      *reinterpret_cast<u32x4*>(sB + swz(r0 + 32 * i, slot)) = rb[i];                        \
+      *reinterpret_cast<u32x4*>(sB + swz(r0 + 32 * i, slot)) = RB[i];                        \
+  }
+  // Load cursor: the next (tile, K step) to fetch; entering a tile sets up its rows.
+  int ltile = tile, lkt = 0;
+#define VGPU_ADVANCE_LOAD()                                                                  \
+  {                                                                                          \
+    if (++lkt == a.ktiles) {                                                                 \
+      lkt = 0;                                                                               \
+      ltile += G;                                                                            \
+      if (ltile < a.nwg) {                                                                   \
+        tile_origin(a, ltile, BM, BN, m0, n0);                                               \
+        VGPU_SETUP_ROWS()                                                                    \
+      }                                                                                      \
+    }                                                                                        \
   }
 
   f32x4_t acc[TM][TN];
@@ -202,108 +232,93 @@ __global__ void __launch_bounds__(kThreads, 2) conv_gemm_kernel(const ConvArgs a
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   VGPU_SETUP_ROWS()
-  if (has_res) VGPU_LOAD_RES(resA)
-  VGPU_LOAD_TILE(0)
-  VGPU_STORE_TILE(0, 0)
+  VGPU_LOAD_TILE(0, ra0, rb0, rv0)
+  VGPU_STORE_TILE(0, 0, ra0, rb0, rv0)
+  VGPU_ADVANCE_LOAD()
+  kt1 = lkt;
+  VGPU_LOAD_TILE(ltile < a.nwg ? lkt : 0, ra1, rb1, rv1)
+  VGPU_ADVANCE_LOAD()
   __syncthreads();
 
-  int kt = 0, st = 0;
+  int ckt = 0, st = 0;  // compute cursor: K step of `tile` staged in LDS stage st
+  // One step: prefetch step s+2 into set F, multiply step s, epilogue at a tile
+  // end, then stage step s+1 (set I) for the next iteration.
+#define VGPU_STEP(RAF, RBF, RVF, KTF, RAI, RBI, RVI, KTI)                                     \
+  {                                                                                          \
+    const bool last = ckt + 1 == a.ktiles;                                                   \
+    if constexpr (RES) VGPU_LOAD_RES(last)                                                   \
+    KTF = lkt;                                                                               \
+    VGPU_LOAD_TILE(ltile < a.nwg ? lkt : 0, RAF, RBF, RVF)                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                       \
+    {                                                                                        \
+      const char* sA = smem + st * STAGE;                                                    \
+      const char* sB = sA + A_BYTES;                                                         \
+      _Pragma("unroll") for (int kk = 0; kk < 2; ++kk) {                                     \
+        bf16x8_t af[TM], bfr[TN];                                                            \
+        _Pragma("unroll") for (int i = 0; i < TM; ++i)                                       \
+          af[i] = *reinterpret_cast<const bf16x8_t*>(sA + swz(wm * WTM + i * 16 + fr, kk * 4 + fk)); \
+        _Pragma("unroll") for (int j = 0; j < TN; ++j)                                       \
+          bfr[j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(wn * WTN + j * 16 + fr, kk * 4 + fk)); \
+        _Pragma("unroll") for (int i = 0; i < TM; ++i)                                       \
+          _Pragma("unroll") for (int j = 0; j < TN; ++j)                                     \
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0); \
+      }                                                                                      \
+    }                                                                                        \
+    if (last) VGPU_EPILOGUE()                                                                \
+    if (++ckt == a.ktiles) {                                                                 \
+      ckt = 0;                                                                               \
+      tile += G;                                                                             \
+      if (tile >= a.nwg) break;                                                              \
+      tile_origin(a, tile, BM, BN, em0, en0);                                                \
+    }                                                                                        \
+    st ^= 1;                                                                                 \
+    VGPU_STORE_TILE(KTI, st, RAI, RBI, RVI)                                                  \
+    __syncthreads();                                                                         \
+    VGPU_ADVANCE_LOAD()                                                                      \
+  }
+  // Accumulators → LDS (fp32) → 16-B coalesced bias + residual + act + store.
+#define VGPU_EPILOGUE()                                                                      \
+  {                                                                                          \
+    __syncthreads();                                                                         \
+    float* sC = reinterpret_cast<float*>(smem);                                              \
+    _Pragma("unroll") for (int i = 0; i < TM; ++i)                                           \
+      _Pragma("unroll") for (int j = 0; j < TN; ++j) {                                       \
+        _Pragma("unroll") for (int e = 0; e < 4; ++e)                                        \
+          sC[(wm * WTM + i * 16 + fk * 4 + e) * CS + wn * WTN + j * 16 + fr] = acc[i][j][e]; \
+        acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};                                             \
+      }                                                                                      \
+    __syncthreads();                                                                         \
+    const int col = en0 + chunk * 8;                                                         \
+    float bb[8];                                                                             \
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) bb[j] = 0.0f;                              \
+    if (a.bias) {                                                                            \
+      const float4 b0 = *reinterpret_cast<const float4*>(a.bias + col);                      \
+      const float4 b1 = *reinterpret_cast<const float4*>(a.bias + col + 4);                  \
+      bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;                                \
+      bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;                                \
+    }                                                                                        \
+    _Pragma("unroll") for (int i = 0; i < RROWS; ++i) {                                      \
+      const int r = rfirst + RSTEP * i, m = em0 + r;                                         \
+      const float4 c0 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8);           \
+      const float4 c1 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8 + 4);       \
+      float v[8] = {c0.x + bb[0], c0.y + bb[1], c0.z + bb[2], c0.w + bb[3],                  \
+                    c1.x + bb[4], c1.y + bb[5], c1.z + bb[6], c1.w + bb[7]};                 \
+      if constexpr (RES) {                                                                   \
+        float re[8];                                                                         \
+        unpack8(res[i], re);                                                                 \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) v[j] += re[j];                         \
+      }                                                                                      \
+      if (a.act) {                                                                           \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);              \
+      }                                                                                      \
+      if (m < a.M) *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = pack8(v);    \
+    }                                                                                        \
+    __syncthreads(); /* staging reads done before the pipeline reuses LDS */                 \
+  }
+
   for (;;) {
-    int nkt = kt + 1, ntile = tile;
-    if (nkt == a.ktiles) {
-      nkt = 0;
-      ntile = tile + G;
-    }
-    const bool has_next = ntile < a.nwg;
-    if (has_next) {
-      if (nkt == 0) {
-        tile_origin(a, ntile, BM, BN, m0, n0);
-        VGPU_SETUP_ROWS()
-        if (has_res) VGPU_LOAD_RES(resB)
-      }
-      VGPU_LOAD_TILE(nkt)
-    }
-
-    {  // MFMA over the staged K step
-      const char* sA = smem + st * STAGE;
-      const char* sB = sA + A_BYTES;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8_t af[TM], bfr[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          af[i] = *reinterpret_cast<const bf16x8_t*>(sA + swz(wm * WTM + i * 16 + fr, kk * 4 + fk));
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          bfr[j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(wn * WTN + j * 16 + fr, kk * 4 + fk));
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      }
-    }
-
-    if (nkt == 0) {
-      // Tile done. Epilogue: accumulators → LDS (fp32) → 16-B coalesced
-      // bias + residual + act + store.  The next tile's first step waits in registers.
-      __syncthreads();
-      float* sC = reinterpret_cast<float*>(smem);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            sC[(wm * WTM + i * 16 + fk * 4 + e) * CS + wn * WTN + j * 16 + fr] = acc[i][j][e];
-          acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        }
-      __syncthreads();
-      const int col = en0 + chunk * 8;
-      float bb[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) bb[j] = 0.0f;
-      if (a.bias) {
-        const float4 b0 = *reinterpret_cast<const float4*>(a.bias + col);
-        const float4 b1 = *reinterpret_cast<const float4*>(a.bias + col + 4);
-        bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
-        bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
-      }
-#pragma unroll
-      for (int i = 0; i < RROWS; ++i) {
-        const int r = rfirst + RSTEP * i, m = em0 + r;
-        if (m < a.M) {
-          const float4 c0 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8);
-          const float4 c1 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8 + 4);
-          float v[8] = {c0.x + bb[0], c0.y + bb[1], c0.z + bb[2], c0.w + bb[3],
-                        c1.x + bb[4], c1.y + bb[5], c1.z + bb[6], c1.w + bb[7]};
-          if (has_res) {
-            float re[8];
-            unpack8(resA[i], re);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] += re[j];
-          }
-          if (a.act) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);
-          }
-          *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = pack8(v);
-        }
-      }
-      if (has_res) {
-#pragma unroll
-        for (int i = 0; i < RROWS; ++i) resA[i] = resB[i];
-      }
-      em0 = m0;
-      en0 = n0;
-      __syncthreads();  // staging reads done before the pipeline reuses LDS
-    }
-    if (!has_next) break;
-    VGPU_STORE_TILE(nkt, st ^ 1)
-    __syncthreads();
-    st ^= 1;
-    kt = nkt;
-    tile = ntile;
+    VGPU_STEP(ra0, rb0, rv0, kt0, ra1, rb1, rv1, kt1)
+    VGPU_STEP(ra1, rb1, rv1, kt1, ra0, rb0, rv0, kt0)
   }
 }
 
@@ -311,14 +326,17 @@ __global__ void __launch_bounds__(kThreads, 2) conv_gemm_kernel(const ConvArgs a
 #undef VGPU_LOAD_RES
 #undef VGPU_LOAD_TILE
 #undef VGPU_STORE_TILE
+#undef VGPU_ADVANCE_LOAD
+#undef VGPU_STEP
+#undef VGPU_EPILOGUE
 
-template <int KS, int BM, int BN, bool PRO>
+template <int KS, int BM, int BN, bool PRO, bool RES>
 hipError_t launch(ConvArgs a, hipStream_t s) {
   static int occ = 0;  // resident workgroups per CU (LDS / VGPR bound); one value per instantiation
   if (occ == 0) {
     int o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, conv_gemm_kernel<KS, BM, BN, PRO>, kThreads,
-                                                     0) != hipSuccess || o < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, conv_gemm_kernel<KS, BM, BN, PRO, RES>,
+                                                     kThreads, 0) != hipSuccess || o < 1)
       o = 1;
     occ = o;
   }
@@ -332,21 +350,27 @@ hipError_t launch(ConvArgs a, hipStream_t s) {
   int grid = cus * occ;
   grid = grid < 8 ? 8 : grid & ~7;  // multiple of 8: a workgroup keeps its XCD's tiles
   if (a.nwg <= grid) grid = a.nwg;
-  hipLaunchKernelGGL((conv_gemm_kernel<KS, BM, BN, PRO>), dim3(grid), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL((conv_gemm_kernel<KS, BM, BN, PRO, RES>), dim3(grid), dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 
+template <int KS, int BM, int BN>
+hipError_t dispatch_pr(const ConvArgs& a, bool pro, bool res, hipStream_t s) {
+  if (pro) return res ? launch<KS, BM, BN, true, true>(a, s) : launch<KS, BM, BN, true, false>(a, s);
+  return res ? launch<KS, BM, BN, false, true>(a, s) : launch<KS, BM, BN, false, false>(a, s);
+}
+
 template <int KS, int BM>
-hipError_t dispatch_bn(const ConvArgs& a, bool pro, hipStream_t s) {
-  if (a.Cout % 128 == 0)
-    return pro ? launch<KS, BM, 128, true>(a, s) : launch<KS, BM, 128, false>(a, s);
-  return pro ? launch<KS, BM, 64, true>(a, s) : launch<KS, BM, 64, false>(a, s);
+hipError_t dispatch_bn(const ConvArgs& a, bool pro, bool res, hipStream_t s) {
+  if (a.Cout % 128 == 0) return dispatch_pr<KS, BM, 128>(a, pro, res, s);
+  return dispatch_pr<KS, BM, 64>(a, pro, res, s);
 }
 
 // ---- NHWC 3x3/s2/p1 max pool and fused BN+ReLU+global-average pool -----------
-__global__ void __launch_bounds__(kThreads) maxpool3s2_kernel(const u32x4* __restrict__ x,
-                                                              u32x4* __restrict__ y, int N, int H,
-                                                              int W, int cv, int OH, int OW) {
+__global__ void __launch_bounds__(kThreads) maxpool_kernel(const u32x4* __restrict__ x,
+                                                          u32x4* __restrict__ y, int N, int H, int W,
+                                                          int cv, int OH, int OW, int k, int stride,
+                                                          int pad) {
   const int64_t total = (int64_t)N * OH * OW * cv;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * kThreads) {
@@ -359,13 +383,11 @@ __global__ void __launch_bounds__(kThreads) maxpool3s2_kernel(const u32x4* __res
     float m[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
-#pragma unroll
-    for (int dh = 0; dh < 3; ++dh) {
-      const int ih = oh * 2 - 1 + dh;
+    for (int dh = 0; dh < k; ++dh) {
+      const int ih = oh * stride - pad + dh;
       if ((unsigned)ih >= (unsigned)H) continue;
-#pragma unroll
-      for (int dw = 0; dw < 3; ++dw) {
-        const int iw = ow * 2 - 1 + dw;
+      for (int dw = 0; dw < k; ++dw) {
+        const int iw = ow * stride - pad + dw;
         if ((unsigned)iw >= (unsigned)W) continue;
         float e[8];
         unpack8(x[(((int64_t)n * H + ih) * W + iw) * cv + c], e);
@@ -431,35 +453,51 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
   a.OH = (H + 2 * pad - KS) / stride + 1;
   a.OW = (W + 2 * pad - KS) / stride + 1;
   if (a.OH < 1 || a.OW < 1) return -1;
-  const int64_t M = (int64_t)N * a.OH * a.OW;
-  if (M > (int64_t)1 << 30) return -1;
-  a.M = (int)M;
   a.K = KS * KS * C;
   a.cblocks = C / 64;
   a.ktiles = KS * KS * a.cblocks;
   a.act = act != 0;
-  const bool pro = pscale != nullptr;
-  // Small-M layers (late stages) use 64-row tiles so the grid still fills the chip.
+  const bool pro = pscale != nullptr, has_res = res != nullptr;
+  // Buffer offsets are 32-bit: run the batch in slices whose activations stay < 2 GiB.
+  const int64_t xi = (int64_t)H * W * C * 2, yi = (int64_t)a.OH * a.OW * Cout * 2;
+  const int64_t lim = ((int64_t)1 << 31) - 1;
+  const int64_t per = lim / (xi > yi ? xi : yi);
+  if (per < 1) return -1;
   const int bn = (Cout % 128 == 0) ? 128 : 64;
-  const int64_t tiles128 = (int64_t)((a.M + 127) / 128) * (Cout / bn);
-  const bool small = tiles128 < 512;
-  hipError_t e;
-  if (KS == 1)
-    e = small ? dispatch_bn<1, 64>(a, pro, s) : dispatch_bn<1, 128>(a, pro, s);
-  else
-    e = small ? dispatch_bn<3, 64>(a, pro, s) : dispatch_bn<3, 128>(a, pro, s);
-  return (int)e;
+  for (int n0 = 0; n0 < N; n0 += (int)per) {
+    const int nb = (int)((N - n0) < per ? (N - n0) : per);
+    ConvArgs c = a;
+    c.N = nb;
+    c.x = a.x + (int64_t)n0 * (xi / 2);
+    c.y = a.y + (int64_t)n0 * (yi / 2);
+    if (has_res) c.res = a.res + (int64_t)n0 * (yi / 2);
+    c.x_bytes = (uint32_t)(nb * xi);
+    c.y_bytes = (uint32_t)(nb * yi);
+    c.M = nb * a.OH * a.OW;
+    // Small-M layers (late stages) use 64-row tiles so the grid still fills the chip.
+    const int64_t tiles128 = (int64_t)((c.M + 127) / 128) * (Cout / bn);
+    const bool small = tiles128 < 512;
+    hipError_t e;
+    if (KS == 1)
+      e = small ? dispatch_bn<1, 64>(c, pro, has_res, s) : dispatch_bn<1, 128>(c, pro, has_res, s);
+    else
+      e = small ? dispatch_bn<3, 64>(c, pro, has_res, s) : dispatch_bn<3, 128>(c, pro, has_res, s);
+    if (e != hipSuccess) return (int)e;
+  }
+  return 0;
 }
 
-VGPU_API int vgpu_maxpool3s2_nhwc(const void* x, void* y, int N, int H, int W, int C,
-                                  hipStream_t s) {
-  if (C % 8) return -1;
-  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+// NHWC bf16 max pool (k×k window, stride, symmetric zero-excluded padding), 16 B per lane.
+VGPU_API int vgpu_maxpool_nhwc(const void* x, void* y, int N, int H, int W, int C, int k, int stride,
+                               int pad, hipStream_t s) {
+  if (C % 8 || k < 1 || stride < 1 || pad < 0 || 2 * pad >= k + 1) return -1;
+  const int OH = (H + 2 * pad - k) / stride + 1, OW = (W + 2 * pad - k) / stride + 1;
+  if (OH < 1 || OW < 1) return -1;
   const int64_t total = (int64_t)N * OH * OW * (C / 8);
-  const int grid = (int)((total + kThreads - 1) / kThreads < 256 * 16 ? (total + kThreads - 1) / kThreads
-                                                                       : 256 * 16);
-  hipLaunchKernelGGL(maxpool3s2_kernel, dim3(grid), dim3(kThreads), 0, s,
-                     static_cast<const u32x4*>(x), static_cast<u32x4*>(y), N, H, W, C / 8, OH, OW);
+  const int64_t want = (total + kThreads - 1) / kThreads;
+  const int grid = (int)(want < 256 * 16 ? want : 256 * 16);
+  hipLaunchKernelGGL(maxpool_kernel, dim3(grid), dim3(kThreads), 0, s, static_cast<const u32x4*>(x),
+                     static_cast<u32x4*>(y), N, H, W, C / 8, OH, OW, k, stride, pad);
   return (int)hipGetLastError();
 }
 

@@ -73,9 +73,10 @@ def test_conv_rejects_unsupported(C):
         C.conv2d(_t((1, 64, 8, 8), 0).contiguous(), _t((64, 64, 1, 1), 1).contiguous())
 
 
-def test_maxpool(C):
+@pytest.mark.parametrize("kpad", [(3, 2, 1), (2, 2, 0), (3, 1, 1)])
+def test_maxpool(C, kpad):
     x = _t((2, 64, 13, 12), 7)
-    torch.testing.assert_close(C.maxpool3s2(x).float(), C.maxpool3s2_ref(x), atol=0, rtol=0)
+    torch.testing.assert_close(C.maxpool(x, *kpad).float(), C.maxpool_ref(x, *kpad), atol=0, rtol=0)
 
 
 def test_scale_shift_relu_mean(C):
@@ -101,5 +102,18 @@ def test_native_resnet_matches_module(gpu_build):
     mb = m.to(torch.bfloat16).to(memory_format=CL)
     fm = FusedResNetV2Inference(mb, conv="native")
     got = fm(x.to(torch.bfloat16).contiguous(memory_format=CL)).float()
+    rel = (got - ref).norm() / ref.norm()
+    assert rel < 0.05, float(rel)
+
+
+def test_native_vgg_matches_module(gpu_build):
+    from vgpu.models.vision import VGG16, NativeVGG16Inference
+    torch.manual_seed(0)
+    m = VGG16().cuda().eval()
+    x = torch.randn(2, 3, 64, 64, device="cuda")
+    with torch.no_grad():
+        ref = m.float()(x.contiguous(memory_format=CL))
+    mb = m.to(torch.bfloat16).to(memory_format=CL)
+    got = NativeVGG16Inference(mb)(x.to(torch.bfloat16)).float()
     rel = (got - ref).norm() / ref.norm()
     assert rel < 0.05, float(rel)

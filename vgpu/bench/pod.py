@@ -59,8 +59,12 @@ def build(args):
     else:
         model.eval()
         from vgpu.models.resnet import FusedResNetV2Inference, ResNetV2
+        from vgpu.models.vision import VGG16, NativeVGG16Inference
+        conv = getattr(args, "conv", "native")
         if isinstance(model, ResNetV2) and not args.no_fused:
-            model = FusedResNetV2Inference(model, conv=getattr(args, "conv", "native"))
+            model = FusedResNetV2Inference(model, conv=conv)
+        elif isinstance(model, VGG16) and not args.no_fused and conv == "native":
+            model = NativeVGG16Inference(model)
         elif hasattr(model, "fuse_for_inference"):
             model.fuse_for_inference()
 

@@ -39,6 +39,49 @@ class VGG16(nn.Module):
         return self.classifier(torch.flatten(x, 1))
 
 
+class NativeVGG16Inference(nn.Module):
+    """VGG-16 inference on the hand-written gfx950 kernels: every 3x3 convolution
+    with C % 64 == 0 is the MFMA implicit-GEMM conv of native/kernels/conv_gemm.hip
+    with bias + ReLU fused into its epilogue (one pass per layer instead of
+    conv → bias → ReLU), max-pools are the NHWC pool kernel.  The 3-channel
+    first layer stays on MIOpen.  Matches `VGG16.eval()` up to bf16 rounding
+    (tests/test_gpu_conv.py)."""
+
+    def __init__(self, m: VGG16):
+        super().__init__()
+        from vgpu.ops.conv import supported
+        cl = torch.channels_last
+        self.ops: list[tuple] = []
+        with torch.no_grad():
+            for mod in m.features:
+                if isinstance(mod, nn.Conv2d):
+                    w = mod.weight.detach().contiguous(memory_format=cl)
+                    native = supported(mod.in_channels, mod.out_channels, mod.kernel_size[0])
+                    b = mod.bias.detach().float().contiguous() if native else mod.bias.detach()
+                    self.ops.append(("conv", w, b, native))
+                elif isinstance(mod, nn.MaxPool2d):
+                    self.ops.append(("pool", mod.kernel_size, mod.stride))
+        self.pool = m.pool
+        self.classifier = m.classifier
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        from vgpu.ops import conv as C
+        x = x.contiguous(memory_format=torch.channels_last)
+        for op in self.ops:
+            if op[0] == "conv":
+                _, w, b, native = op
+                if native:
+                    x = C.conv2d(x, w, b, padding=1, act="relu")
+                else:
+                    x = F.relu(F.conv2d(x, w, b, padding=1)).contiguous(memory_format=torch.channels_last)
+            else:
+                x = C.maxpool(x, op[1], op[2], 0)
+        if x.shape[-2:] != (7, 7):
+            x = self.pool(x)
+        return self.classifier(torch.flatten(x, 1))
+
+
 def _conv_bn(cin: int, cout: int, k: int, stride: int = 1, groups: int = 1, dilation: int = 1,
              act: bool = True) -> nn.Sequential:
     pad = dilation * (k - 1) // 2

@@ -60,12 +60,12 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_add_scale_shift_act_nhwc.argtypes = [vp, vp, vp, vp, vp, vp, u64, u32, ctypes.c_int, vp]
     ci = ctypes.c_int
     lib.vgpu_conv2d_nhwc.argtypes = [vp, vp, vp, vp, vp, vp, vp] + [ci] * 9 + [vp]
-    lib.vgpu_maxpool3s2_nhwc.argtypes = [vp, vp, ci, ci, ci, ci, vp]
+    lib.vgpu_maxpool_nhwc.argtypes = [vp, vp] + [ci] * 7 + [vp]
     lib.vgpu_scale_shift_relu_mean_nhwc.argtypes = [vp, vp, vp, vp, ci, ci, ci, vp]
     for f in ("vgpu_census", "vgpu_busy", "vgpu_gather_pages", "vgpu_scatter_pages",
               "vgpu_fill_pattern", "vgpu_verify_pattern", "vgpu_kernels_abi_version",
               "vgpu_bias_act_nhwc", "vgpu_scale_shift_act_nhwc", "vgpu_add_scale_shift_act_nhwc",
-              "vgpu_conv2d_nhwc", "vgpu_maxpool3s2_nhwc", "vgpu_scale_shift_relu_mean_nhwc"):
+              "vgpu_conv2d_nhwc", "vgpu_maxpool_nhwc", "vgpu_scale_shift_relu_mean_nhwc"):
         getattr(lib, f).restype = ctypes.c_int
     _kernels = lib
     return lib

@@ -83,16 +83,20 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
     return out
 
 
-def maxpool3s2(x: torch.Tensor) -> torch.Tensor:
-    """3x3 / stride 2 / pad 1 max pool, NHWC bf16 (the ResNet stem pool)."""
+def maxpool(x: torch.Tensor, k: int, stride: int, pad: int = 0) -> torch.Tensor:
+    """k×k max pool, NHWC bf16 (ResNet stem: 3/2/1; VGG: 2/2/0)."""
     _nhwc(x, "x")
     n, c, h, w = x.shape
-    oh, ow = out_hw(h, w, 3, 2, 1)
+    oh, ow = out_hw(h, w, k, stride, pad)
     out = torch.empty((n, c, oh, ow), dtype=x.dtype, device=x.device, memory_format=_CL)
-    rc = load_kernels().vgpu_maxpool3s2_nhwc(_ptr(x), _ptr(out), n, h, w, c, _stream())
+    rc = load_kernels().vgpu_maxpool_nhwc(_ptr(x), _ptr(out), n, h, w, c, k, stride, pad, _stream())
     if rc != 0:
-        raise RuntimeError(f"vgpu_maxpool3s2_nhwc: error {rc}")
+        raise RuntimeError(f"vgpu_maxpool_nhwc: error {rc}")
     return out
+
+
+def maxpool3s2(x: torch.Tensor) -> torch.Tensor:
+    return maxpool(x, 3, 2, 1)
 
 
 def scale_shift_relu_mean(x: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor) -> torch.Tensor:
@@ -121,8 +125,8 @@ def conv2d_ref(x, w, bias=None, *, stride=1, padding=0, act="none", pro=None, re
     return y
 
 
-def maxpool3s2_ref(x):
-    return F.max_pool2d(x.float(), 3, 2, 1)
+def maxpool_ref(x, k, stride, pad=0):
+    return F.max_pool2d(x.float(), k, stride, pad)
 
 
 def scale_shift_relu_mean_ref(x, scale, shift):
