@@ -125,6 +125,25 @@ amdsmi_status_t amdsmi_get_gpu_memory_usage(amdsmi_processor_handle h, amdsmi_me
   return AMDSMI_STATUS_SUCCESS;
 }
 
+amdsmi_status_t amdsmi_get_gpu_vram_usage(amdsmi_processor_handle h, amdsmi_vram_usage_t* info) {
+  auto* g = gpu(h);
+  if (!g) return AMDSMI_STATUS_INVAL;
+  memset(info, 0, sizeof(*info));
+  info->vram_total = (uint32_t)((uint64_t)(*g)["vram"].num(288.0 * (1ull << 30)) >> 20);
+  info->vram_used = (uint32_t)((uint64_t)(*g)["vram_used"].num(0) >> 20);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_vram_info(amdsmi_processor_handle h, amdsmi_vram_info_t* info) {
+  auto* g = gpu(h);
+  if (!g) return AMDSMI_STATUS_INVAL;
+  memset(info, 0, sizeof(*info));
+  info->vram_type = AMDSMI_VRAM_TYPE_HBM3E;
+  info->vram_size = (uint64_t)(*g)["vram"].num(288.0 * (1ull << 30)) >> 20;
+  info->vram_bit_width = 8192;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
 amdsmi_status_t amdsmi_get_gpu_topo_numa_affinity(amdsmi_processor_handle h, int32_t* numa) {
   auto* g = gpu(h);
   if (!g) return AMDSMI_STATUS_INVAL;

@@ -7,11 +7,17 @@
 // hsa_queue_create — resolved through the global scope, i.e. through the
 // preloaded libvgpu.so hook, exactly as in a PyTorch process.
 //
+// Device buffers come from the GPU agent's HSA memory pool
+// (hsa_amd_memory_pool_allocate through the global scope, as CLR does), and
+// VGPU_FAKE_RUNTIME_ALLOC bytes per device are allocated at init the way CLR
+// allocates its device kernarg / staging pools outside any hipMalloc.
+//
 // Fixture env: VGPU_FAKE_GPUS (1), VGPU_FAKE_MEM (bytes, default 288 GiB),
-// VGPU_FAKE_CUS (256).
+// VGPU_FAKE_CUS (256), VGPU_FAKE_RUNTIME_ALLOC (bytes, default 0).
 #include <hip/hip_runtime_api.h>
 #include <dlfcn.h>
 #include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -27,6 +33,8 @@ struct Dev {
   uint64_t total = 0;
   uint64_t used = 0;
   hsa_queue_t* queue = nullptr;
+  hsa_amd_memory_pool_t pool{0};
+  void* runtime_buf = nullptr;
 };
 
 std::mutex g_mu;
@@ -53,20 +61,34 @@ hsa_status_t pick_gpu(hsa_agent_t a, void* data) {
   return HSA_STATUS_SUCCESS;
 }
 
+hsa_status_t first_pool(hsa_amd_memory_pool_t p, void* data) {
+  *(hsa_amd_memory_pool_t*)data = p;
+  return HSA_STATUS_SUCCESS;
+}
+
 void init_locked() {
   if (g_inited) return;
   g_inited = true;
+  hsa_init();
   int n = env_int("VGPU_FAKE_GPUS", 1);
   const char* m = getenv("VGPU_FAKE_MEM");
   uint64_t mem = m ? strtoull(m, nullptr, 10) : (288ull << 30);
+  const char* ra = getenv("VGPU_FAKE_RUNTIME_ALLOC");
+  uint64_t runtime_alloc = ra ? strtoull(ra, nullptr, 10) : 0;
   g_devs.assign(n, Dev{});
   std::vector<hsa_agent_t> gpus;
   hsa_iterate_agents(pick_gpu, &gpus);
   for (int i = 0; i < n; ++i) {
     g_devs[i].total = mem;
-    if (i < (int)gpus.size())
+    if (i < (int)gpus.size()) {
       hsa_queue_create(gpus[i], 4096, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, 0, 0,
                        &g_devs[i].queue);
+      hsa_amd_agent_iterate_memory_pools(gpus[i], first_pool, &g_devs[i].pool);
+      if (runtime_alloc &&
+          hsa_amd_memory_pool_allocate(g_devs[i].pool, runtime_alloc, 0, &g_devs[i].runtime_buf) ==
+              HSA_STATUS_SUCCESS)
+        g_devs[i].used += runtime_alloc;
+    }
   }
 }
 
@@ -80,9 +102,11 @@ hipError_t dev_alloc(void** p, size_t size, int dev) {
   init_locked();
   if (dev < 0 || dev >= (int)g_devs.size()) return hipErrorInvalidDevice;
   if (g_devs[dev].used + size > g_devs[dev].total) return hipErrorOutOfMemory;
+  void* hp = nullptr;
+  if (hsa_amd_memory_pool_allocate(g_devs[dev].pool, size, 0, &hp) != HSA_STATUS_SUCCESS || !hp)
+    return hipErrorOutOfMemory;
   g_devs[dev].used += size;
-  uintptr_t a = g_next;
-  g_next += ((size + 4095) / 4096) * 4096 + 4096;
+  uintptr_t a = (uintptr_t)hp;
   g_allocs[a] = {dev, size};
   *p = (void*)a;
   return hipSuccess;
@@ -95,6 +119,7 @@ hipError_t dev_free(void* p) {
   if (it == g_allocs.end()) return hipErrorInvalidValue;
   g_devs[it->second.first].used -= it->second.second;
   g_allocs.erase(it);
+  hsa_amd_memory_pool_free(p);
   return hipSuccess;
 }
 

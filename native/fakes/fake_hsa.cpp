@@ -5,10 +5,22 @@
 //
 // Built as libhsa-runtime64.so.1 (SONAME) with the ROCR_1 symbol version.
 // Fixture: VGPU_FAKE_GPUS (default 1), VGPU_FAKE_CUS (256), VGPU_FAKE_XCC (8).
+//
+// Like ROCr, every exported queue / pool entry point dispatches through an
+// HsaApiTable, and hsa_init() hands that table to the OnLoad() of every
+// library named in HSA_TOOLS_LIB — the tools-library interception path of
+// the enforcement library (native/shim/hooks_hsa.cpp).
+#include <dlfcn.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
+#define AMD_INTERNAL_BUILD 1
+#include <hsa/hsa_api_trace.h>
+#undef AMD_INTERNAL_BUILD
 #include <stdlib.h>
 #include <string.h>
+
+#include <map>
+#include <string>
 
 #include <mutex>
 #include <vector>
@@ -31,11 +43,64 @@ int env_int(const char* n, int d) {
   return v && *v ? atoi(v) : d;
 }
 
+// Pools: CPU agent (handle 1) owns pool 2; GPU agent 100+i owns pool 200+i.
+std::map<uintptr_t, std::pair<uint64_t, uint64_t>> g_pool_allocs;  // ptr -> (pool, size)
+std::map<uint64_t, uint64_t> g_pool_used;
+uintptr_t g_pool_next = 0x600000000000ull;
+
+hsa_status_t impl_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32_t type,
+                               void (*callback)(hsa_status_t, hsa_queue_t*, void*), void* data,
+                               uint32_t priv, uint32_t group, hsa_queue_t** queue);
+hsa_status_t impl_queue_destroy(hsa_queue_t* q);
+hsa_status_t impl_cu_set_mask(const hsa_queue_t* q, uint32_t bits, const uint32_t* mask);
+hsa_status_t impl_pool_allocate(hsa_amd_memory_pool_t pool, size_t size, uint32_t flags, void** ptr);
+hsa_status_t impl_pool_free(void* ptr);
+
+CoreApiTable g_core;
+AmdExtTable g_ext;
+HsaApiTable g_api;
+std::once_flag g_table_once;
+int g_tools_loaded = 0;
+
+void setup_table() {
+  std::call_once(g_table_once, [] {
+    memset(&g_core, 0, sizeof g_core);
+    memset(&g_ext, 0, sizeof g_ext);
+    memset(&g_api, 0, sizeof g_api);
+    g_core.hsa_queue_create_fn = impl_queue_create;
+    g_core.hsa_queue_destroy_fn = impl_queue_destroy;
+    g_ext.hsa_amd_queue_cu_set_mask_fn = impl_cu_set_mask;
+    g_ext.hsa_amd_memory_pool_allocate_fn = impl_pool_allocate;
+    g_ext.hsa_amd_memory_pool_free_fn = impl_pool_free;
+    g_api.core_ = &g_core;
+    g_api.amd_ext_ = &g_ext;
+    const char* tools = getenv("HSA_TOOLS_LIB");
+    if (!tools || !*tools) return;
+    std::string all(tools);
+    size_t pos = 0;
+    while (pos <= all.size()) {
+      size_t end = all.find_first_of(" :", pos);
+      if (end == std::string::npos) end = all.size();
+      std::string lib = all.substr(pos, end - pos);
+      pos = end + 1;
+      if (lib.empty()) continue;
+      void* h = dlopen(lib.c_str(), RTLD_NOW);
+      if (!h) continue;
+      typedef bool (*onload_t)(void*, uint64_t, uint64_t, const char* const*);
+      auto fn = (onload_t)dlsym(h, "OnLoad");
+      if (fn && fn(&g_api, 1, 0, nullptr)) ++g_tools_loaded;
+    }
+  });
+}
+
 }  // namespace
 
 extern "C" {
 
-hsa_status_t hsa_init() { return HSA_STATUS_SUCCESS; }
+hsa_status_t hsa_init() {
+  setup_table();
+  return HSA_STATUS_SUCCESS;
+}
 hsa_status_t hsa_shut_down() { return HSA_STATUS_SUCCESS; }
 
 hsa_status_t hsa_iterate_agents(hsa_status_t (*cb)(hsa_agent_t, void*), void* data) {
@@ -72,9 +137,82 @@ hsa_status_t hsa_agent_get_info(hsa_agent_t agent, hsa_agent_info_t attr, void* 
   }
 }
 
+hsa_status_t hsa_amd_agent_iterate_memory_pools(hsa_agent_t agent,
+                                                hsa_status_t (*cb)(hsa_amd_memory_pool_t, void*),
+                                                void* data) {
+  hsa_amd_memory_pool_t p{agent.handle >= 100 ? 200 + (agent.handle - 100) : 2};
+  return cb(p, data);
+}
+
+hsa_status_t hsa_amd_memory_pool_get_info(hsa_amd_memory_pool_t pool,
+                                          hsa_amd_memory_pool_info_t attr, void* value) {
+  if (attr == HSA_AMD_MEMORY_POOL_INFO_SEGMENT) {
+    *(hsa_amd_segment_t*)value = HSA_AMD_SEGMENT_GLOBAL;
+    return HSA_STATUS_SUCCESS;
+  }
+  return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+}
+
+// Exported entry points dispatch through the API table, as ROCr's do.
 hsa_status_t hsa_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32_t type,
                               void (*callback)(hsa_status_t, hsa_queue_t*, void*), void* data,
                               uint32_t priv, uint32_t group, hsa_queue_t** queue) {
+  setup_table();
+  return g_core.hsa_queue_create_fn(agent, size, type, callback, data, priv, group, queue);
+}
+hsa_status_t hsa_queue_destroy(hsa_queue_t* q) {
+  setup_table();
+  return g_core.hsa_queue_destroy_fn(q);
+}
+hsa_status_t hsa_amd_queue_cu_set_mask(const hsa_queue_t* q, uint32_t bits, const uint32_t* mask) {
+  setup_table();
+  return g_ext.hsa_amd_queue_cu_set_mask_fn(q, bits, mask);
+}
+hsa_status_t hsa_amd_memory_pool_allocate(hsa_amd_memory_pool_t pool, size_t size, uint32_t flags,
+                                          void** ptr) {
+  setup_table();
+  return g_ext.hsa_amd_memory_pool_allocate_fn(pool, size, flags, ptr);
+}
+hsa_status_t hsa_amd_memory_pool_free(void* ptr) {
+  setup_table();
+  return g_ext.hsa_amd_memory_pool_free_fn(ptr);
+}
+
+// ---- test introspection ----
+uint64_t fake_hsa_pool_used(int dev) {
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_pool_used.find(200 + (uint64_t)dev);
+  return it == g_pool_used.end() ? 0 : it->second;
+}
+int fake_hsa_tools_loaded() { return g_tools_loaded; }
+
+}  // extern "C"
+
+namespace {
+
+hsa_status_t impl_pool_allocate(hsa_amd_memory_pool_t pool, size_t size, uint32_t, void** ptr) {
+  if (!ptr || size == 0) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> g(g_mu);
+  uintptr_t a = g_pool_next;
+  g_pool_next += ((size + 4095) / 4096) * 4096 + 4096;
+  g_pool_allocs[a] = {pool.handle, size};
+  g_pool_used[pool.handle] += size;
+  *ptr = (void*)a;
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t impl_pool_free(void* ptr) {
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_pool_allocs.find((uintptr_t)ptr);
+  if (it == g_pool_allocs.end()) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  g_pool_used[it->second.first] -= it->second.second;
+  g_pool_allocs.erase(it);
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t impl_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32_t type,
+                               void (*callback)(hsa_status_t, hsa_queue_t*, void*), void* data,
+                               uint32_t priv, uint32_t group, hsa_queue_t** queue) {
   auto* fq = new FakeQueue();
   memset(fq, 0, sizeof(*fq));
   fq->agent = agent.handle;
@@ -86,14 +224,14 @@ hsa_status_t hsa_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32
   return HSA_STATUS_SUCCESS;
 }
 
-hsa_status_t hsa_queue_destroy(hsa_queue_t* q) {
+hsa_status_t impl_queue_destroy(hsa_queue_t* q) {
   std::lock_guard<std::mutex> g(g_mu);
   for (auto* fq : g_queues)
     if (&fq->q == q) fq->alive = 0;
   return HSA_STATUS_SUCCESS;
 }
 
-hsa_status_t hsa_amd_queue_cu_set_mask(const hsa_queue_t* q, uint32_t bits, const uint32_t* mask) {
+hsa_status_t impl_cu_set_mask(const hsa_queue_t* q, uint32_t bits, const uint32_t* mask) {
   if (bits % 32) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
   if (bits && !mask) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> g(g_mu);
@@ -107,7 +245,10 @@ hsa_status_t hsa_amd_queue_cu_set_mask(const hsa_queue_t* q, uint32_t bits, cons
   return HSA_STATUS_ERROR_INVALID_QUEUE;
 }
 
-// ---- test introspection ----
+}  // namespace
+
+extern "C" {
+
 int fake_hsa_queue_count() {
   std::lock_guard<std::mutex> g(g_mu);
   return (int)g_queues.size();

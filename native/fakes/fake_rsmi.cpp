@@ -1,0 +1,30 @@
+// Minimal fake librocm_smi64.so.1 (memory queries only) for CPU tests of the
+// rocm-smi virtualisation in the enforcement library (native/shim/hooks_rsmi.cpp).
+// Every device reports VGPU_FAKE_MEM bytes of VRAM (default 288 GiB) and
+// VGPU_FAKE_RSMI_USED bytes in use.
+#include <rocm_smi/rocm_smi.h>
+#include <stdlib.h>
+
+static uint64_t env_u64(const char* n, uint64_t d) {
+  const char* v = getenv(n);
+  return v && *v ? strtoull(v, nullptr, 10) : d;
+}
+
+extern "C" {
+
+rsmi_status_t rsmi_init(uint64_t) { return RSMI_STATUS_SUCCESS; }
+rsmi_status_t rsmi_shut_down(void) { return RSMI_STATUS_SUCCESS; }
+rsmi_status_t rsmi_num_monitor_devices(uint32_t* n) {
+  *n = (uint32_t)env_u64("VGPU_FAKE_GPUS", 1);
+  return RSMI_STATUS_SUCCESS;
+}
+rsmi_status_t rsmi_dev_memory_total_get(uint32_t, rsmi_memory_type_t, uint64_t* total) {
+  *total = env_u64("VGPU_FAKE_MEM", 288ull << 30);
+  return RSMI_STATUS_SUCCESS;
+}
+rsmi_status_t rsmi_dev_memory_usage_get(uint32_t, rsmi_memory_type_t, uint64_t* used) {
+  *used = env_u64("VGPU_FAKE_RSMI_USED", 1ull << 30);
+  return RSMI_STATUS_SUCCESS;
+}
+
+}  // extern "C"

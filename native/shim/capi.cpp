@@ -154,6 +154,21 @@ __attribute__((visibility("default"))) uint64_t vgpu_self_host_bytes(int dev) {
   return __atomic_load_n(&sl->used[dev].host_bytes, __ATOMIC_RELAXED);
 }
 
+// 1 when ROCr handed us its API table (HSA_TOOLS_LIB=libvgpu.so), else 0.
+__attribute__((visibility("default"))) int vgpu_self_hsa_table_mode() { return hsa_table_mode() ? 1 : 0; }
+
+// This process's charge on `dev` by class: 0 context/runtime, 1 module, 2 buffer, 3 host, 4 total.
+__attribute__((visibility("default"))) uint64_t vgpu_self_usage(int dev, int which) {
+  ensure_init();
+  vgpu_proc_slot_t* sl = my_slot();
+  if (!sl || dev < 0 || dev >= VGPU_MAX_DEVICES) return 0;
+  const vgpu_dev_usage_t& u = sl->used[dev];
+  const uint64_t* f[] = {&u.context_bytes, &u.module_bytes, &u.buffer_bytes, &u.host_bytes,
+                         &u.total_bytes};
+  if (which < 0 || which > 4) return 0;
+  return __atomic_load_n(f[which], __ATOMIC_RELAXED);
+}
+
 __attribute__((visibility("default"))) void vgpu_self_on_launch(int dev, uint64_t wg) {
   ensure_init();
   limiter_on_launch(dev, wg);

@@ -136,7 +136,7 @@ static void apply_mask(hsa_queue_t* q, int dev, const AgentInfo& ai) {
     words32[2 * w] = (uint32_t)(m[w] & 0xffffffffu);
     words32[2 * w + 1] = (uint32_t)(m[w] >> 32);
   }
-  hsa_status_t rc = REAL_HSA(hsa_amd_queue_cu_set_mask)(q, bits, words32);
+  hsa_status_t rc = real_cu_set_mask(q, bits, words32);
   if (rc != HSA_STATUS_SUCCESS && (int)rc != (int)HSA_STATUS_CU_MASK_REDUCED) {
     VLOG_WARN("hsa_amd_queue_cu_set_mask failed on device %d: %d", dev, (int)rc);
   } else {
@@ -179,7 +179,7 @@ int cumask_reapply_all() {
     if (mask_for_device(q.second, *a, m)) {
       apply_mask(q.first, q.second, *a);
     } else {
-      REAL_HSA(hsa_amd_queue_cu_set_mask)(q.first, 0, nullptr);  // all CUs
+      real_cu_set_mask(q.first, 0, nullptr);  // all CUs
     }
     ++n;
   }
@@ -228,6 +228,39 @@ uint32_t cumask_driver_uid(int dev) {
   std::lock_guard<std::mutex> g(g_mu);
   AgentInfo* a = agent_for_hip_index(dev);
   return a ? a->driver_uid : 0;
+}
+
+// Device-memory pools (GLOBAL segment) of every container-visible GPU agent,
+// for the HSA pool-allocation accounting in hooks_hsa.cpp.
+static std::vector<std::pair<uint64_t, int>> g_pools;  // pool handle, hip device
+static bool g_pools_ready = false;
+
+static hsa_status_t collect_pool(hsa_amd_memory_pool_t pool, void* data) {
+  auto* out = static_cast<std::vector<uint64_t>*>(data);
+  hsa_amd_segment_t seg;
+  if (REAL_HSA(hsa_amd_memory_pool_get_info)(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) ==
+          HSA_STATUS_SUCCESS &&
+      seg == HSA_AMD_SEGMENT_GLOBAL)
+    out->push_back(pool.handle);
+  return HSA_STATUS_SUCCESS;
+}
+
+int cumask_hip_index_for_pool(uint64_t pool_handle) {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (!g_pools_ready) {
+    ensure_agents_locked();
+    if (!g_agents_ready) return -1;
+    for (auto& a : g_agents) {
+      if (a.hip_index < 0) continue;
+      std::vector<uint64_t> pools;
+      REAL_HSA(hsa_amd_agent_iterate_memory_pools)(a.agent, collect_pool, &pools);
+      for (uint64_t p : pools) g_pools.push_back({p, a.hip_index});
+    }
+    g_pools_ready = true;
+  }
+  for (auto& e : g_pools)
+    if (e.first == pool_handle) return e.second;
+  return -1;
 }
 
 int cu_count_masked(int dev, int physical) {

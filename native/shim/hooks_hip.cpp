@@ -22,6 +22,12 @@ namespace {
 
 inline int cur_dev() { return tl_device; }
 
+// Marks the real runtime call of an allocation hook (see tl_in_hip_alloc).
+struct InHipAlloc {
+  InHipAlloc() { ++tl_in_hip_alloc; }
+  ~InHipAlloc() { --tl_in_hip_alloc; }
+};
+
 inline uint64_t blocks3(unsigned x, unsigned y, unsigned z) {
   return (uint64_t)(x ? x : 1) * (y ? y : 1) * (z ? z : 1);
 }
@@ -31,6 +37,7 @@ template <class F>
 hipError_t charged_alloc(void** ptr, size_t size, int kind, F&& real_alloc) {
   ensure_init();
   State& s = st();
+  InHipAlloc in_alloc;
   if (!s.enabled || size == 0) return real_alloc();
   suspend_gate();
   int dev = cur_dev();
@@ -153,6 +160,7 @@ __attribute__((visibility("default"))) hipError_t hipMemCreate(
     unsigned long long flags) {
   ensure_init();
   State& s = st();
+  InHipAlloc in_alloc;
   if (!s.enabled || !prop || prop->location.type != hipMemLocationTypeDevice)
     return REAL_HIP(hipMemCreate)(handle, size, prop, flags);
   int dev = prop->location.id;
@@ -338,21 +346,7 @@ __attribute__((visibility("default"))) hipError_t hipGetProcAddress(const char* 
                                                                     hipDriverProcAddressQueryResult* status) {
   hipError_t rc = REAL_HIP(hipGetProcAddress)(symbol, pfn, hipVersion, flags, status);
   if (rc != hipSuccess || !symbol || !pfn || !*pfn) return rc;
-  static const char* hooked[] = {
-      "hipSetDevice", "hipMalloc", "hipExtMallocWithFlags", "hipMallocAsync",
-      "hipMallocFromPoolAsync", "hipMallocManaged", "hipMallocPitch", "hipFree", "hipFreeAsync",
-      "hipMemCreate", "hipMemRelease", "hipMemGetInfo", "hipDeviceTotalMem",
-      "hipGetDevicePropertiesR0600", "hipDeviceGetAttribute", "hipLaunchKernel",
-      "hipExtLaunchKernel", "hipModuleLaunchKernel", "hipExtModuleLaunchKernel",
-      "hipLaunchCooperativeKernel", "hipModuleLaunchCooperativeKernel", "hipLaunchKernelExC",
-      "hipGraphLaunch", nullptr};
-  for (const char** h = hooked; *h; ++h) {
-    if (!strcmp(symbol, *h)) {
-      void* self = dlsym(RTLD_DEFAULT, symbol);
-      if (self) *pfn = self;
-      break;
-    }
-  }
+  if (void* mine = own_hook(symbol)) *pfn = mine;
   return rc;
 }
 

@@ -1,17 +1,123 @@
 // ROCr (HSA) interposers: catch every hardware queue the process creates so the
-// container's CU mask is applied before the first dispatch, and keep the
-// application from widening it.
+// container's CU mask is applied before the first dispatch (and keep the
+// application from widening it), and charge device-memory pool allocations
+// that bypass the HIP allocation hooks (runtime kernarg / staging buffers,
+// direct HSA users) to the container.
 //
-// This has no reference counterpart (CUDA offers no per-stream SM mask); it is
-// the MI355X replacement for the time-sliced SM limiter (SURVEY.md §2.6 E1f,
-// §7.2 step 3(a)).
+// The CU-mask half has no reference counterpart (CUDA offers no per-stream SM
+// mask); it is the MI355X replacement for the time-sliced SM limiter
+// (SURVEY.md §2.6 E1f, §7.2 step 3(a)).  The pool half is the HSA-level
+// accounting of SURVEY.md §7.4 item 1 (reference: allocator.c tracks context /
+// module / buffer bytes separately, E1d).
+//
+// Two ways in, one implementation:
+//  * LD_PRELOAD / ld.so.preload: the exported hsa_* below interpose on the
+//    HIP runtime's PLT calls into libhsa-runtime64.
+//  * HSA_TOOLS_LIB=libvgpu.so: ROCr calls OnLoad() with its API table before
+//    the first queue exists, and we swap the table entries.  Every caller —
+//    including code that resolved hsa_* by hand — dispatches through that
+//    table (the rocprofiler mechanism; SURVEY.md §2.6 E1a "HSA tools-lib
+//    OnLoad").  Once the table is patched the PLT interposers pass through,
+//    so nothing is applied or charged twice.
+// The installed header picks its sibling includes by this macro.
+#define AMD_INTERNAL_BUILD 1
+#include <hsa/hsa_api_trace.h>
+#undef AMD_INTERNAL_BUILD
+
 #include "common.h"
 #include "real.h"
 #include "state.h"
 
 namespace vgpu {
 bool cumask_intersect(const hsa_queue_t* q, uint32_t* bits, const uint32_t* in, uint32_t* out);
+int cumask_hip_index_for_pool(uint64_t pool_handle);
+
+namespace {
+
+struct HsaTable {
+  decltype(&::hsa_queue_create) queue_create = nullptr;
+  decltype(&::hsa_queue_destroy) queue_destroy = nullptr;
+  decltype(&::hsa_amd_queue_cu_set_mask) cu_set_mask = nullptr;
+  decltype(&::hsa_amd_memory_pool_allocate) pool_allocate = nullptr;
+  decltype(&::hsa_amd_memory_pool_free) pool_free = nullptr;
+};
+HsaTable g_orig;                    // ROCr's entries, saved by OnLoad
+std::atomic<bool> g_table_mode{false};
+
+hsa_status_t queue_create_impl(decltype(&::hsa_queue_create) real, hsa_agent_t agent, uint32_t size,
+                               hsa_queue_type32_t type,
+                               void (*callback)(hsa_status_t, hsa_queue_t*, void*), void* data,
+                               uint32_t private_segment_size, uint32_t group_segment_size,
+                               hsa_queue_t** queue) {
+  ensure_init();
+  hsa_status_t rc = real(agent, size, type, callback, data, private_segment_size,
+                         group_segment_size, queue);
+  if (rc == HSA_STATUS_SUCCESS && queue && *queue) cumask_on_queue_created(&agent, *queue);
+  return rc;
 }
+
+hsa_status_t cu_set_mask_impl(decltype(&::hsa_amd_queue_cu_set_mask) real, const hsa_queue_t* queue,
+                              uint32_t num_cu_mask_count, const uint32_t* cu_mask) {
+  ensure_init();
+  uint32_t bits = num_cu_mask_count;
+  uint32_t merged[VGPU_CU_MASK_WORDS * 2] = {};
+  if (num_cu_mask_count <= VGPU_CU_MASK_WORDS * 64 &&
+      cumask_intersect(queue, &bits, cu_mask, merged))
+    return real(queue, bits, merged);
+  return real(queue, num_cu_mask_count, cu_mask);
+}
+
+hsa_status_t pool_allocate_impl(decltype(&::hsa_amd_memory_pool_allocate) real,
+                                hsa_amd_memory_pool_t pool, size_t size, uint32_t flags,
+                                void** ptr) {
+  hsa_status_t rc = real(pool, size, flags, ptr);
+  // Allocations made inside a HIP allocation hook are already charged there.
+  if (rc != HSA_STATUS_SUCCESS || !ptr || !*ptr || tl_in_hip_alloc || size == 0) return rc;
+  ensure_init();
+  if (!st().enabled) return rc;
+  int dev = cumask_hip_index_for_pool(pool.handle);
+  if (dev < 0) return rc;  // system (host) pool or a device outside the container
+  mem_charge_nofail(dev, size, kRuntime);
+  ledger_add(*ptr, size, dev, kRuntime);
+  return rc;
+}
+
+hsa_status_t pool_free_impl(decltype(&::hsa_amd_memory_pool_free) real, void* ptr) {
+  Alloc a;
+  if (ptr && ledger_take_if(ptr, kRuntime, &a)) mem_unreserve(a.dev, a.size, a.kind);
+  return real(ptr);
+}
+
+// Table entries (HSA_TOOLS_LIB mode).
+hsa_status_t tab_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32_t type,
+                              void (*cb)(hsa_status_t, hsa_queue_t*, void*), void* data,
+                              uint32_t priv, uint32_t group, hsa_queue_t** queue) {
+  return queue_create_impl(g_orig.queue_create, agent, size, type, cb, data, priv, group, queue);
+}
+hsa_status_t tab_queue_destroy(hsa_queue_t* queue) {
+  cumask_on_queue_destroyed(queue);
+  return g_orig.queue_destroy(queue);
+}
+hsa_status_t tab_cu_set_mask(const hsa_queue_t* q, uint32_t n, const uint32_t* m) {
+  return cu_set_mask_impl(g_orig.cu_set_mask, q, n, m);
+}
+hsa_status_t tab_pool_allocate(hsa_amd_memory_pool_t pool, size_t size, uint32_t flags, void** ptr) {
+  return pool_allocate_impl(g_orig.pool_allocate, pool, size, flags, ptr);
+}
+hsa_status_t tab_pool_free(void* ptr) { return pool_free_impl(g_orig.pool_free, ptr); }
+
+}  // namespace
+
+bool hsa_table_mode() { return g_table_mode.load(std::memory_order_acquire); }
+
+// The runtime's own cu_set_mask, for the shim's internal use: in table mode the
+// exported symbol would come back through tab_cu_set_mask (and its lock).
+hsa_status_t real_cu_set_mask(const hsa_queue_t* q, uint32_t bits, const uint32_t* mask) {
+  if (hsa_table_mode()) return g_orig.cu_set_mask(q, bits, mask);
+  return REAL_HSA(hsa_amd_queue_cu_set_mask)(q, bits, mask);
+}
+
+}  // namespace vgpu
 
 using namespace vgpu;
 
@@ -21,27 +127,60 @@ __attribute__((visibility("default"))) hsa_status_t hsa_queue_create(
     hsa_agent_t agent, uint32_t size, hsa_queue_type32_t type,
     void (*callback)(hsa_status_t status, hsa_queue_t* source, void* data), void* data,
     uint32_t private_segment_size, uint32_t group_segment_size, hsa_queue_t** queue) {
-  ensure_init();
-  hsa_status_t rc = REAL_HSA(hsa_queue_create)(agent, size, type, callback, data,
-                                               private_segment_size, group_segment_size, queue);
-  if (rc == HSA_STATUS_SUCCESS && queue && *queue) cumask_on_queue_created(&agent, *queue);
-  return rc;
+  if (hsa_table_mode())
+    return REAL_HSA(hsa_queue_create)(agent, size, type, callback, data, private_segment_size,
+                                      group_segment_size, queue);
+  return queue_create_impl(REAL_HSA(hsa_queue_create), agent, size, type, callback, data,
+                           private_segment_size, group_segment_size, queue);
 }
 
 __attribute__((visibility("default"))) hsa_status_t hsa_queue_destroy(hsa_queue_t* queue) {
-  cumask_on_queue_destroyed(queue);
+  if (!hsa_table_mode()) cumask_on_queue_destroyed(queue);
   return REAL_HSA(hsa_queue_destroy)(queue);
 }
 
 __attribute__((visibility("default"))) hsa_status_t hsa_amd_queue_cu_set_mask(
     const hsa_queue_t* queue, uint32_t num_cu_mask_count, const uint32_t* cu_mask) {
-  ensure_init();
-  uint32_t bits = num_cu_mask_count;
-  uint32_t merged[VGPU_CU_MASK_WORDS * 2] = {};
-  if (num_cu_mask_count <= VGPU_CU_MASK_WORDS * 64 &&
-      cumask_intersect(queue, &bits, cu_mask, merged))
-    return REAL_HSA(hsa_amd_queue_cu_set_mask)(queue, bits, merged);
-  return REAL_HSA(hsa_amd_queue_cu_set_mask)(queue, num_cu_mask_count, cu_mask);
+  if (hsa_table_mode()) return REAL_HSA(hsa_amd_queue_cu_set_mask)(queue, num_cu_mask_count, cu_mask);
+  return cu_set_mask_impl(REAL_HSA(hsa_amd_queue_cu_set_mask), queue, num_cu_mask_count, cu_mask);
 }
+
+__attribute__((visibility("default"))) hsa_status_t hsa_amd_memory_pool_allocate(
+    hsa_amd_memory_pool_t pool, size_t size, uint32_t flags, void** ptr) {
+  if (hsa_table_mode()) return REAL_HSA(hsa_amd_memory_pool_allocate)(pool, size, flags, ptr);
+  return pool_allocate_impl(REAL_HSA(hsa_amd_memory_pool_allocate), pool, size, flags, ptr);
+}
+
+__attribute__((visibility("default"))) hsa_status_t hsa_amd_memory_pool_free(void* ptr) {
+  if (hsa_table_mode()) return REAL_HSA(hsa_amd_memory_pool_free)(ptr);
+  return pool_free_impl(REAL_HSA(hsa_amd_memory_pool_free), ptr);
+}
+
+// ROCr tools-library entry (HSA_TOOLS_LIB).  Runs inside hsa_init, before any
+// queue or pool allocation of the process.
+__attribute__((visibility("default"))) bool OnLoad(void* api_table, uint64_t runtime_version,
+                                                   uint64_t failed_tool_count,
+                                                   const char* const* failed_tool_names) {
+  auto* t = static_cast<HsaApiTable*>(api_table);
+  if (!t || !t->core_ || !t->amd_ext_) return true;
+  g_orig.queue_create = t->core_->hsa_queue_create_fn;
+  g_orig.queue_destroy = t->core_->hsa_queue_destroy_fn;
+  g_orig.cu_set_mask = t->amd_ext_->hsa_amd_queue_cu_set_mask_fn;
+  g_orig.pool_allocate = t->amd_ext_->hsa_amd_memory_pool_allocate_fn;
+  g_orig.pool_free = t->amd_ext_->hsa_amd_memory_pool_free_fn;
+  if (!g_orig.queue_create || !g_orig.queue_destroy || !g_orig.cu_set_mask ||
+      !g_orig.pool_allocate || !g_orig.pool_free)
+    return true;  // unknown table layout: stay on the PLT interposers
+  t->core_->hsa_queue_create_fn = tab_queue_create;
+  t->core_->hsa_queue_destroy_fn = tab_queue_destroy;
+  t->amd_ext_->hsa_amd_queue_cu_set_mask_fn = tab_cu_set_mask;
+  t->amd_ext_->hsa_amd_memory_pool_allocate_fn = tab_pool_allocate;
+  t->amd_ext_->hsa_amd_memory_pool_free_fn = tab_pool_free;
+  g_table_mode.store(true, std::memory_order_release);
+  VLOG_INFO("HSA API table intercepted (runtime %llu)", (unsigned long long)runtime_version);
+  return true;
+}
+
+__attribute__((visibility("default"))) void OnUnload() {}
 
 }  // extern "C"

@@ -26,6 +26,7 @@
 namespace vgpu {
 
 thread_local int tl_device = 0;
+thread_local int tl_in_hip_alloc = 0;
 
 struct DevLimiter {
   std::atomic<int64_t> tokens{0};

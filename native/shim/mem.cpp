@@ -40,6 +40,9 @@ static void add_usage(vgpu_dev_usage_t& u, uint64_t size, int kind, bool add) {
     case kModule:
       op(&u.module_bytes);
       break;
+    case kRuntime:
+      op(&u.context_bytes);
+      break;
     default:
       op(&u.buffer_bytes);
       break;
@@ -103,6 +106,23 @@ void ledger_add(void* p, uint64_t size, int dev, int kind) {
   }
   vgpu_proc_slot_t* sl = my_slot();
   if (sl && dev >= 0 && dev < VGPU_MAX_DEVICES) note_peak(sl->used[dev]);
+}
+
+bool ledger_take_if(void* p, int kind, Alloc* out) {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.ledger_mu);
+  auto it = s.ledger.find((uintptr_t)p);
+  if (it == s.ledger.end() || it->second.kind != kind) return false;
+  *out = it->second;
+  s.ledger.erase(it);
+  return true;
+}
+
+void mem_charge_nofail(int dev, uint64_t size, int kind) {
+  State& s = st();
+  vgpu_proc_slot_t* sl = my_slot();
+  if (!s.enabled || !sl || dev < 0 || dev >= VGPU_MAX_DEVICES) return;
+  add_usage(sl->used[dev], size, kind, true);
 }
 
 bool ledger_take(void* p, Alloc* out) {

@@ -44,14 +44,39 @@ void* hsa_lib_handle() {
   return v;
 }
 
+void* amdsmi_lib_handle() {
+  static void* h = nullptr;
+  void* v = __atomic_load_n(&h, __ATOMIC_ACQUIRE);
+  if (v) return v;
+  // Only ever called from a hook the application reached, i.e. once the
+  // application has loaded the library itself.
+  static const char* names[] = {"libamd_smi.so.26", "libamd_smi.so.25", "libamd_smi.so.24",
+                                "libamd_smi.so", nullptr};
+  v = open_noload(names);
+  if (!v) v = RTLD_NEXT;
+  __atomic_store_n(&h, v, __ATOMIC_RELEASE);
+  return v;
+}
+
+void* rsmi_lib_handle() {
+  static void* h = nullptr;
+  void* v = __atomic_load_n(&h, __ATOMIC_ACQUIRE);
+  if (v) return v;
+  static const char* names[] = {"librocm_smi64.so.1", "librocm_smi64.so", nullptr};
+  v = open_noload(names);
+  if (!v) v = RTLD_NEXT;
+  __atomic_store_n(&h, v, __ATOMIC_RELEASE);
+  return v;
+}
+
 void* resolve_real(void* handle, const char* name) {
-  void* p = dlsym(handle, name);
-  if (!p && handle != RTLD_NEXT) p = dlsym(RTLD_NEXT, name);
+  void* p = real_dlsym(handle, name);
+  if (!p && handle != RTLD_NEXT) p = real_dlsym(RTLD_NEXT, name);
   // Never resolve to ourselves (would recurse forever).
   Dl_info self_info, sym_info;
   if (p && dladdr((void*)&resolve_real, &self_info) && dladdr(p, &sym_info) &&
       self_info.dli_fbase == sym_info.dli_fbase) {
-    p = dlsym(RTLD_NEXT, name);
+    p = real_dlsym(RTLD_NEXT, name);
   }
   if (!p) VLOG_ERR("cannot resolve real %s: %s", name, dlerror());
   return p;

@@ -18,6 +18,12 @@ namespace vgpu {
 void* hip_lib_handle();
 void* hsa_lib_handle();
 void* resolve_real(void* handle, const char* name);
+// glibc's dlsym (the exported `dlsym` of this library is an interposer, dlsym.cpp).
+void* real_dlsym(void* handle, const char* name);
+// This library's own definition of a hooked entry point, or nullptr.
+void* own_hook(const char* name);
+void* amdsmi_lib_handle();
+void* rsmi_lib_handle();
 
 }  // namespace vgpu
 

@@ -17,12 +17,31 @@
 #include <thread>
 #include <vector>
 
+#include <amd_smi/amdsmi.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <rocm_smi/rocm_smi.h>
+
 #include "vgpu/shared_region.h"
 
 extern "C" int fake_hsa_queue_count();
 extern "C" int fake_hsa_queue_mask(int idx, uint32_t* out, int max_words, uint64_t* agent);
 extern "C" uint64_t fake_hip_launches();
 extern "C" uint64_t fake_hip_physical_used(int dev);
+extern "C" uint64_t fake_hsa_pool_used(int dev);
+extern "C" int fake_hsa_tools_loaded();
+
+static hsa_status_t gpu_agent_cb(hsa_agent_t a, void* data) {
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS &&
+      t == HSA_DEVICE_TYPE_GPU && ((hsa_agent_t*)data)->handle == 0)
+    *(hsa_agent_t*)data = a;
+  return HSA_STATUS_SUCCESS;
+}
+static hsa_status_t pool_cb(hsa_amd_memory_pool_t p, void* data) {
+  *(hsa_amd_memory_pool_t*)data = p;
+  return HSA_STATUS_SUCCESS;
+}
 
 template <class T>
 static T sym(const char* name) {
@@ -149,6 +168,81 @@ int main(int argc, char** argv) {
     hipGraphLaunch(nullptr, nullptr);
     printf("fake_launches=%llu\n", (unsigned long long)fake_hip_launches());
     print_region(dev);
+    return 0;
+  }
+
+  if (sc == "pool") {
+    // HSA-level accounting: runtime-internal pool allocations are charged to
+    // the context class; a hipMalloc (which reaches the same pool inside the
+    // runtime) is charged once, to the buffer class.
+    auto usage = sym<uint64_t (*)(int, int)>("vgpu_self_usage");
+    auto table = sym<int (*)()>("vgpu_self_hsa_table_mode");
+    printf("table_mode=%d\ntools_loaded=%d\n", table ? table() : -1, fake_hsa_tools_loaded());
+    printf("ctx0=%llu\nbuf0=%llu\n", (unsigned long long)usage(dev, 0), (unsigned long long)usage(dev, 2));
+    void* p = nullptr;
+    hipMalloc(&p, 1ull << 30);
+    printf("ctx1=%llu\nbuf1=%llu\n", (unsigned long long)usage(dev, 0), (unsigned long long)usage(dev, 2));
+    hsa_agent_t gpu{0};
+    hsa_iterate_agents(gpu_agent_cb, &gpu);
+    hsa_amd_memory_pool_t pool{0};
+    hsa_amd_agent_iterate_memory_pools(gpu, pool_cb, &pool);
+    void* q = nullptr;
+    hsa_amd_memory_pool_allocate(pool, 256ull << 20, 0, &q);
+    printf("ctx2=%llu\n", (unsigned long long)usage(dev, 0));
+    hsa_amd_memory_pool_free(q);
+    printf("ctx3=%llu\n", (unsigned long long)usage(dev, 0));
+    hipFree(p);
+    printf("buf4=%llu\npool_used=%llu\n", (unsigned long long)usage(dev, 2),
+           (unsigned long long)fake_hsa_pool_used(dev));
+    print_region(dev);
+    return 0;
+  }
+
+  if (sc == "smi") {
+    // amdsmi / rocm-smi through dlopen handles (the ctypes path of amd-smi and
+    // torch): the dlsym interposer must hand out the virtualising hooks.
+    void* h = dlopen("libamd_smi.so", RTLD_NOW);
+    printf("amdsmi_loaded=%d\n", h ? 1 : 0);
+    if (h) {
+      auto init = (amdsmi_status_t(*)(uint64_t))dlsym(h, "amdsmi_init");
+      auto socks = (amdsmi_status_t(*)(uint32_t*, amdsmi_socket_handle*))dlsym(h, "amdsmi_get_socket_handles");
+      auto procs = (amdsmi_status_t(*)(amdsmi_socket_handle, uint32_t*, amdsmi_processor_handle*))dlsym(
+          h, "amdsmi_get_processor_handles");
+      auto total = (amdsmi_status_t(*)(amdsmi_processor_handle, amdsmi_memory_type_t, uint64_t*))dlsym(
+          h, "amdsmi_get_gpu_memory_total");
+      auto used = (amdsmi_status_t(*)(amdsmi_processor_handle, amdsmi_memory_type_t, uint64_t*))dlsym(
+          h, "amdsmi_get_gpu_memory_usage");
+      auto vram = (amdsmi_status_t(*)(amdsmi_processor_handle, amdsmi_vram_usage_t*))dlsym(
+          h, "amdsmi_get_gpu_vram_usage");
+      printf("interposed=%d\n", (void*)total == dlsym(RTLD_DEFAULT, "amdsmi_get_gpu_memory_total") ? 1 : 0);
+      init(0);
+      uint32_t ns = 1;
+      amdsmi_socket_handle sh;
+      socks(&ns, &sh);
+      uint32_t np = 4;
+      amdsmi_processor_handle ph[4];
+      procs(sh, &np, ph);
+      uint64_t t = 0, u = 0, g = 0;
+      total(ph[dev], AMDSMI_MEM_TYPE_VRAM, &t);
+      used(ph[dev], AMDSMI_MEM_TYPE_VRAM, &u);
+      total(ph[dev], AMDSMI_MEM_TYPE_GTT, &g);
+      amdsmi_vram_usage_t vu{};
+      vram(ph[dev], &vu);
+      printf("smi_total=%llu\nsmi_used=%llu\nsmi_gtt_total=%llu\nsmi_vram_total_mb=%u\nsmi_vram_used_mb=%u\n",
+             (unsigned long long)t, (unsigned long long)u, (unsigned long long)g, vu.vram_total,
+             vu.vram_used);
+    }
+    void* r = dlopen("librocm_smi64.so.1", RTLD_NOW);
+    if (r) {
+      auto rt = (rsmi_status_t(*)(uint32_t, rsmi_memory_type_t, uint64_t*))dlsym(r, "rsmi_dev_memory_total_get");
+      auto ru = (rsmi_status_t(*)(uint32_t, rsmi_memory_type_t, uint64_t*))dlsym(r, "rsmi_dev_memory_usage_get");
+      uint64_t t = 0, u = 0;
+      rt((uint32_t)dev, RSMI_MEM_TYPE_VRAM, &t);
+      ru((uint32_t)dev, RSMI_MEM_TYPE_VRAM, &u);
+      printf("rsmi_total=%llu\nrsmi_used=%llu\n", (unsigned long long)t, (unsigned long long)u);
+    }
+    // RTLD_NEXT keeps its caller-relative meaning through the interposer.
+    printf("next_ok=%d\n", dlsym(RTLD_NEXT, "getpid") == dlsym(RTLD_DEFAULT, "getpid") ? 1 : 0);
     return 0;
   }
 

@@ -1,0 +1,35 @@
+#!/bin/bash
+# One GPU-box session: GPU tests, smoke, flagship bench, per-layer conv bench and a
+# rocprofv3 kernel trace of the flagship.  Every GPU step has its own time limit;
+# the script stops at the first fault/abort/timeout.  .so files are built here
+# (CPU container) and travel with the tree.
+set -u
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+OUT=gpurun_out
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(date +%T))"
+  tail -n ${TAILN:-6} "$OUT/$name.log" | cut -c1-600
+  return $rc
+}
+ok_or_testfail() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+IFS=, read -ra STAGES <<< "${1:-tests,smoke,bench,conv,prof}"
+for s in "${STAGES[@]}"; do
+  case $s in
+    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider
+           rc=$?; ok_or_testfail $rc || exit $rc ;;
+    smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
+    bench) step bench 900 python bench.py || exit 1
+           grep '^{' "$OUT/bench.log" | tail -1 > "$OUT/bench.json" ;;
+    excl)  step bench_excl 600 python bench.py --pods 1 --gpucores 100 --gpumem 0 --no-cap-probe || exit 1 ;;
+    conv)  step convnative 600 python -m vgpu.bench.convnative || exit 1 ;;
+    prof)  step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_native/%pid%" -o run -- python3 bench.py --steps 20 --warmup 5 --no-cap-probe || exit 1 ;;
+    *) step "$s" 900 bash -c "$s" || exit 1 ;;
+  esac
+done
+exit 0

@@ -78,3 +78,47 @@ def test_compute_share_accuracy(gpu_build):
     print("busy full/half/quarter", full, half, quarter)
     assert 1.7 < half / full < 2.3
     assert 3.4 < quarter / full < 4.6
+
+
+def test_runtime_pool_memory_accounted(gpu_build):
+    # HSA pool allocations the runtime makes outside hipMalloc are charged to
+    # the context class; the classes add up to the total the cap is checked on.
+    res = probe(["cap", 1024], {"VGPU_DEVICE_MEMORY_LIMIT_0": "8192m"})
+    sh = res["shim"]
+    print("shim charge by class:", sh)
+    assert sh["hsa_table_mode"] == 0
+    assert sh["context"] + sh["module"] + sh["buffer"] == sh["total"]
+    assert sh["total"] <= 8192 << 20
+    assert sh["context"] < 2 * GiB
+
+
+def test_amdsmi_reports_cap(gpu_build):
+    res = probe(["smi", 1024], {"VGPU_DEVICE_MEMORY_LIMIT_0": "8192m"})
+    if "error" in res:
+        pytest.skip(f"amdsmi unavailable on this host: {res['error']}")
+    cap = 8192 << 20
+    assert res["total"] == cap and res["torch_total"] == cap
+    assert res["vram_total_mb"] == 8192
+    assert GiB <= res["used"] <= cap                   # the container's usage, not the device's
+    assert res["vram_used_mb"] == res["used"] >> 20
+
+
+def test_amdsmi_uncapped_passthrough(gpu_build):
+    res = probe(["smi", 64], {})
+    if "error" in res:
+        pytest.skip(f"amdsmi unavailable on this host: {res['error']}")
+    assert res["total"] > 250 * GiB
+
+
+def test_hsa_tools_lib_mode_masks_and_cap(gpu_build):
+    # HSA_TOOLS_LIB=libvgpu.so: ROCr hands the shim its API table in hsa_init;
+    # masks and the cap hold with the PLT interposers stepping aside.
+    from vgpu.native import shim_path
+    env = {"VGPU_DEVICE_CU_LIMIT_0": "25", "HSA_TOOLS_LIB": str(shim_path())}
+    res = probe(["census", 4096, 200000], env)
+    assert res["shim"]["hsa_table_mode"] == 1, res
+    assert res["distinct_cus"] == 64, res
+    res = probe(["cap", 1024], {"VGPU_DEVICE_MEMORY_LIMIT_0": "8192m",
+                                "HSA_TOOLS_LIB": str(shim_path())})
+    assert res["shim"]["hsa_table_mode"] == 1
+    assert res["total"] == 8192 << 20 and res["reserved"] <= 8192 << 20

@@ -1,0 +1,98 @@
+"""CPU tests of the interposition paths added around the HIP hooks (fake
+runtimes, no GPU):
+
+* HSA memory-pool accounting — runtime-internal device allocations are
+  charged to the container once (reference allocator.c
+  tracks context/module/buffer bytes separately, §2.6 E1d).
+* HSA tools-library mode — ROCr's OnLoad(api_table) hands us the table
+  (SURVEY.md §2.6 E1a), and the PLT interposers step aside (nothing twice).
+* amdsmi / rocm-smi virtualisation through dlopen handles (the `dlsym`
+  override; reference nvmlDeviceGetMemoryInfo hooks, §2.6 E1c).
+"""
+import json
+
+from vgpu.native import shim_path
+
+from test_shim_native import GiB, run
+
+MiB = 1 << 20
+
+
+def test_runtime_pool_allocations_charged_once(native_build):
+    o = run("pool", env={"VGPU_DEVICE_MEMORY_LIMIT_0": "16g",
+                         "VGPU_FAKE_RUNTIME_ALLOC": str(64 * MiB)})
+    assert o["table_mode"] == "0"
+    assert int(o["ctx0"]) == 64 * MiB           # CLR's init-time pool allocation
+    assert int(o["buf0"]) == 0
+    assert int(o["buf1"]) == GiB                # hipMalloc: buffer class only ...
+    assert int(o["ctx1"]) == 64 * MiB           # ... not again at the pool level
+    assert int(o["ctx2"]) == 64 * MiB + 256 * MiB
+    assert int(o["ctx3"]) == 64 * MiB
+    assert int(o["buf4"]) == 0
+    assert int(o["pool_used"]) == 64 * MiB      # the fake runtime really freed the rest
+
+
+def test_runtime_charge_counts_against_cap(native_build):
+    # 1 GiB of runtime-internal memory leaves room for 9 of 10 1-GiB buffers.
+    o = run("fill", GiB, env={"VGPU_DEVICE_MEMORY_LIMIT_0": "10g",
+                              "VGPU_FAKE_RUNTIME_ALLOC": str(GiB)})
+    assert o["allocated"] == "9"
+    assert int(o["region_used"]) == 10 * GiB
+
+
+def test_hsa_tools_lib_table_mode(native_build):
+    env = {"VGPU_DEVICE_MEMORY_LIMIT_0": "16g", "VGPU_FAKE_RUNTIME_ALLOC": str(64 * MiB),
+           "HSA_TOOLS_LIB": str(shim_path())}
+    o = run("pool", env=env)
+    assert o["tools_loaded"] == "1"
+    assert o["table_mode"] == "1"
+    assert int(o["ctx1"]) == 64 * MiB and int(o["buf1"]) == GiB
+    assert int(o["ctx2"]) == 64 * MiB + 256 * MiB
+    assert int(o["ctx3"]) == 64 * MiB
+
+
+def test_hsa_tools_lib_applies_cu_mask_once(native_build):
+    env = {"VGPU_DEVICE_CU_LIMIT_0": "25", "HSA_TOOLS_LIB": str(shim_path())}
+    o = run("masks", env=env)
+    assert o["queues"] == "1"
+    assert o["queue0_words"] == "8"
+    # 25 % of 256 CUs = 64 → the 64 low logical bits (8 per XCD)
+    assert o["queue0_mask"].lower().endswith("ffffffffffffffff")
+    assert int(o["queue0_mask"], 16).bit_count() == 64
+
+
+def test_tools_lib_without_preload(native_build):
+    # HSA_TOOLS_LIB alone (no LD_PRELOAD): the table path still enforces masks.
+    env = {"VGPU_DEVICE_CU_LIMIT_0": "50", "HSA_TOOLS_LIB": str(shim_path())}
+    o = run("masks", env=env, preload=False)
+    assert int(o["queue0_mask"], 16).bit_count() == 128
+
+
+def _smi_fixture(tmp_path):
+    f = tmp_path / "smi.json"
+    f.write_text(json.dumps({"gpus": [{"uuid": "GPU-0", "vram": 288 * GiB, "vram_used": 5 * GiB}]}))
+    return str(f)
+
+
+def test_amdsmi_and_rsmi_report_the_cap(native_build, tmp_path):
+    env = {"VGPU_DEVICE_MEMORY_LIMIT_0": "144000m", "VGPU_FAKE_AMDSMI_JSON": _smi_fixture(tmp_path),
+           "VGPU_FAKE_RUNTIME_ALLOC": str(512 * MiB)}
+    o = run("smi", env=env)
+    cap = 144000 * MiB
+    assert o["amdsmi_loaded"] == "1"
+    assert o["interposed"] == "1"               # dlsym(handle) → our hook
+    assert int(o["smi_total"]) == cap
+    assert int(o["smi_used"]) == 512 * MiB      # container usage, not the device's 5 GiB
+    assert int(o["smi_vram_total_mb"]) == 144000
+    assert int(o["smi_vram_used_mb"]) == 512
+    assert int(o["smi_gtt_total"]) != cap       # non-VRAM types pass through
+    assert int(o["rsmi_total"]) == cap
+    assert int(o["rsmi_used"]) == 512 * MiB
+    assert o["next_ok"] == "1"
+
+
+def test_smi_passthrough_without_limit(native_build, tmp_path):
+    o = run("smi", env={"VGPU_FAKE_AMDSMI_JSON": _smi_fixture(tmp_path)})
+    assert o["interposed"] == "1"
+    assert int(o["rsmi_total"]) == 288 * GiB
+    assert int(o["rsmi_used"]) == GiB           # fake's own number

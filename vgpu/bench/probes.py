@@ -7,12 +7,54 @@ line.  Used by the GPU tests and by the accuracy benchmarks.
       wall time of a fixed amount of VALU work (compute-share accuracy)
   python -m vgpu.bench.probes cap [chunk_mib]
       reported total + how many bytes torch could allocate before OOM
+  python -m vgpu.bench.probes smi [alloc_mib]
+      what amdsmi (python bindings over libamd_smi, the amd-smi CLI's path)
+      reports for VRAM total / used after torch allocates alloc_mib
+Every probe also reports the enforcement library's own view ("shim") when
+the library is loaded in the process.
 """
 from __future__ import annotations
 
 import json
 import sys
 import time
+
+
+def shim_stats(dev: int = 0) -> dict | None:
+    """Per-class charge of this process and the HSA interception mode, read
+    through the preloaded enforcement library's C ABI (None when not loaded)."""
+    import ctypes
+    try:
+        lib = ctypes.CDLL(None)
+        fn = lib.vgpu_self_usage
+    except (OSError, AttributeError):
+        return None
+    fn.restype = ctypes.c_uint64
+    fn.argtypes = [ctypes.c_int, ctypes.c_int]
+    names = ("context", "module", "buffer", "host", "total")
+    out = {k: int(fn(dev, i)) for i, k in enumerate(names)}
+    out["hsa_table_mode"] = int(lib.vgpu_self_hsa_table_mode())
+    return out
+
+
+def smi(alloc_mib: int = 1024) -> dict:
+    import torch
+    x = torch.empty(alloc_mib << 20, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    try:
+        import amdsmi
+        amdsmi.amdsmi_init()
+    except Exception as e:  # no amdsmi bindings / no access on this host
+        return {"error": repr(e)}
+    h = amdsmi.amdsmi_get_processor_handles()[0]
+    vu = amdsmi.amdsmi_get_gpu_vram_usage(h)
+    res = {"total": int(amdsmi.amdsmi_get_gpu_memory_total(h, amdsmi.AmdSmiMemoryType.VRAM)),
+           "used": int(amdsmi.amdsmi_get_gpu_memory_usage(h, amdsmi.AmdSmiMemoryType.VRAM)),
+           "vram_total_mb": int(vu["vram_total"]), "vram_used_mb": int(vu["vram_used"]),
+           "torch_total": int(torch.cuda.mem_get_info()[1])}
+    amdsmi.amdsmi_shut_down()
+    del x
+    return res
 
 
 def census(blocks: int = 4096, spin: int = 200000) -> dict:
@@ -82,7 +124,8 @@ def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     cmd = argv.pop(0) if argv else "census"
     nums = [int(a) for a in argv]
-    out = {"census": census, "busy": busy, "cap": cap}[cmd](*nums)
+    out = {"census": census, "busy": busy, "cap": cap, "smi": smi}[cmd](*nums)
+    out["shim"] = shim_stats()
     print("PROBE " + json.dumps(out), flush=True)
     return 0
 

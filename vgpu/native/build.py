@@ -169,7 +169,7 @@ def build_fakes(force: bool = False) -> dict[str, Path]:
     hsa = FAKES_OUT / "libhsa-runtime64.so.1"
     if force or not _stamp(hsa, [hsa_src]):
         vs = FAKES_OUT / "hsa.map"
-        vs.write_text(_version_script(hsa_src, "ROCR_1", {}, "fake_hsa_queue_count; fake_hsa_queue_mask;"))
+        vs.write_text(_version_script(hsa_src, "ROCR_1", {}, "fake_hsa_queue_count; fake_hsa_queue_mask; fake_hsa_pool_used; fake_hsa_tools_loaded;"))
         _run([CXX, *COMMON, hsa_src, "-o", hsa, "-shared", "-Wl,-soname,libhsa-runtime64.so.1",
               f"-Wl,--version-script={vs}", "-lpthread"])
         _mark(hsa, [hsa_src])
@@ -196,6 +196,14 @@ def build_fakes(force: bool = False) -> dict[str, Path]:
                   "-lpthread"])
             _mark(smi, [smi_src])
         res["smi"] = smi
+
+    rsmi_src = NATIVE / "fakes" / "fake_rsmi.cpp"
+    if rsmi_src.exists():
+        rsmi = FAKES_OUT / "librocm_smi64.so.1"
+        if force or not _stamp(rsmi, [rsmi_src]):
+            _run([CXX, *COMMON, rsmi_src, "-o", rsmi, "-shared", "-Wl,-soname,librocm_smi64.so.1"])
+            _mark(rsmi, [rsmi_src])
+        res["rsmi"] = rsmi
 
     drv_src = NATIVE / "tests" / "shim_driver.cpp"
     drv = FAKES_OUT / "shim_driver"
