@@ -21,6 +21,10 @@
 #include <link.h>
 #include <pthread.h>
 
+#include <mutex>
+#include <string>
+#include <unordered_map>
+
 #include "common.h"
 
 typedef void* (*dlsym_fn)(void*, const char*);
@@ -119,6 +123,29 @@ void* own_hook(const char* name) {
   return p;
 }
 
+// What the application's own lookup would have returned, per hooked name
+// (handle-specific lookups only): the smi hooks call exactly that function,
+// not whichever copy of the library a by-name lookup finds first (PyTorch
+// ships its own librocm_smi64 / libamd_smi beside the system ones).
+static std::mutex g_rec_mu;
+static std::unordered_map<std::string, void*> g_recorded;
+
+static void record_real(const char* name, void* p) {
+  std::lock_guard<std::mutex> g(g_rec_mu);
+  g_recorded[name] = p;
+}
+
+void* recorded_real(const char* name) {
+  std::lock_guard<std::mutex> g(g_rec_mu);
+  auto it = g_recorded.find(name);
+  return it == g_recorded.end() ? nullptr : it->second;
+}
+
+bool is_own_address(void* p) {
+  Dl_info di;
+  return p && dladdr(p, &di) && di.dli_fbase == self_base();
+}
+
 }  // namespace vgpu
 
 extern "C" void* vgpu_dlsym_hook(void* handle, const char* name) {
@@ -127,6 +154,7 @@ extern "C" void* vgpu_dlsym_hook(void* handle, const char* name) {
   void* mine = vgpu::own_hook(name);
   if (mine && mine != p) {
     VLOG_DEBUG("dlsym(%p, %s) -> interposer", handle, name);
+    vgpu::record_real(name, p);
     return mine;
   }
   return p;

@@ -11,7 +11,8 @@
 
 using namespace vgpu;
 
-#define REAL_RSMI(name) VGPU_REAL_IMPL(rsmi_lib_handle, decltype(&::name), #name)
+#define REAL_RSMI(name) \
+  ((decltype(&::name))smi_real(#name, __builtin_return_address(0), rsmi_lib_handle))
 
 static bool rsmi_vram(rsmi_memory_type_t t) {
   return t == RSMI_MEM_TYPE_VRAM || t == RSMI_MEM_TYPE_VIS_VRAM;

@@ -28,7 +28,8 @@ using namespace vgpu;
 
 namespace {
 
-#define REAL_SMI(name) VGPU_REAL_IMPL(amdsmi_lib_handle, decltype(&::name), #name)
+#define REAL_SMI(name) \
+  ((decltype(&::name))smi_real(#name, __builtin_return_address(0), amdsmi_lib_handle))
 
 std::mutex g_mu;
 std::vector<amdsmi_processor_handle> g_gpus;

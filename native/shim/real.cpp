@@ -62,11 +62,32 @@ void* rsmi_lib_handle() {
   static void* h = nullptr;
   void* v = __atomic_load_n(&h, __ATOMIC_ACQUIRE);
   if (v) return v;
+  // libamd_smi bundles rocm-smi and calls its rsmi_* entry points through the
+  // GOT — i.e. through our interposers — even when librocm_smi64 is not loaded.
   static const char* names[] = {"librocm_smi64.so.1", "librocm_smi64.so", nullptr};
   v = open_noload(names);
+  if (!v && amdsmi_lib_handle() != RTLD_NEXT) v = amdsmi_lib_handle();
   if (!v) v = RTLD_NEXT;
   __atomic_store_n(&h, v, __ATOMIC_RELEASE);
   return v;
+}
+
+void* smi_real(const char* name, void* ret_addr, void* (*fallback_handle)()) {
+  // 1. A call from inside an smi library (libamd_smi calling its bundled
+  //    rsmi_* through the GOT): that library's own definition.
+  Dl_info di;
+  if (ret_addr && dladdr(ret_addr, &di) && di.dli_fname && strstr(di.dli_fname, "smi") &&
+      !is_own_address(ret_addr)) {
+    if (void* h = dlopen(di.dli_fname, RTLD_NOLOAD | RTLD_LAZY)) {
+      void* p = real_dlsym(h, name);
+      dlclose(h);
+      if (p && !is_own_address(p)) return p;
+    }
+  }
+  // 2. The definition the application's dlsym(handle, name) found.
+  if (void* p = recorded_real(name)) return p;
+  // 3. By library name.
+  return resolve_real(fallback_handle(), name);
 }
 
 void* resolve_real(void* handle, const char* name) {

@@ -23,6 +23,10 @@ void* real_dlsym(void* handle, const char* name);
 // This library's own definition of a hooked entry point, or nullptr.
 void* own_hook(const char* name);
 void* amdsmi_lib_handle();
+void* recorded_real(const char* name);
+bool is_own_address(void* p);
+// The real smi entry point for a hook called from `ret_addr` (see real.cpp).
+void* smi_real(const char* name, void* ret_addr, void* (*fallback_handle)());
 void* rsmi_lib_handle();
 
 }  // namespace vgpu

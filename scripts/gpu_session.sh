@@ -18,6 +18,7 @@ step() {  # step <name> <seconds> <cmd...>
   return $rc
 }
 ok_or_testfail() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+n=0
 IFS=, read -ra STAGES <<< "${1:-tests,smoke,bench,conv,prof}"
 for s in "${STAGES[@]}"; do
   case $s in
@@ -29,7 +30,9 @@ for s in "${STAGES[@]}"; do
     excl)  step bench_excl 600 python bench.py --pods 1 --gpucores 100 --gpumem 0 --no-cap-probe || exit 1 ;;
     conv)  step convnative 600 python -m vgpu.bench.convnative || exit 1 ;;
     prof)  step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_native/%pid%" -o run -- python3 bench.py --steps 20 --warmup 5 --no-cap-probe || exit 1 ;;
-    *) step "$s" 900 bash -c "$s" || exit 1 ;;
+    shim) step pytest_shim 900 python -u -m pytest tests/test_gpu_shim.py -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider
+          rc=$?; ok_or_testfail $rc || exit $rc ;;
+    *) n=$((n+1)); step "cmd$n" 900 bash -c "$s" || exit 1 ;;
   esac
 done
 exit 0

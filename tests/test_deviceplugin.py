@@ -236,6 +236,18 @@ def test_allocate_multi_gpu_prefers_one_numa(cluster):
     assert idx == sorted(idx)
 
 
+def test_allocate_hsa_tools_intercept_knob(cluster):
+    c = cluster
+    _, r = schedule_and_allocate(c, "plain", 1000, 25)
+    assert "HSA_TOOLS_LIB" not in dict(r.envs)
+    c["cfg"].hsa_tools_intercept = True
+    try:
+        _, r = schedule_and_allocate(c, "tools", 1000, 25)
+    finally:
+        c["cfg"].hsa_tools_intercept = False
+    assert dict(r.envs)["HSA_TOOLS_LIB"] == "/usr/local/vgpu/libvgpu.so"
+
+
 def test_allocate_without_pending_pod_fails(cluster):
     with pytest.raises(grpc.RpcError) as ei:
         cluster["stub"].Allocate(api.AllocateRequest(container_requests=[dict(devices_ids=["x-0"])]), timeout=5)

@@ -47,11 +47,23 @@ def smi(alloc_mib: int = 1024) -> dict:
     except Exception as e:  # no amdsmi bindings / no access on this host
         return {"error": repr(e)}
     h = amdsmi.amdsmi_get_processor_handles()[0]
-    vu = amdsmi.amdsmi_get_gpu_vram_usage(h)
-    res = {"total": int(amdsmi.amdsmi_get_gpu_memory_total(h, amdsmi.AmdSmiMemoryType.VRAM)),
-           "used": int(amdsmi.amdsmi_get_gpu_memory_usage(h, amdsmi.AmdSmiMemoryType.VRAM)),
-           "vram_total_mb": int(vu["vram_total"]), "vram_used_mb": int(vu["vram_used"]),
-           "torch_total": int(torch.cuda.mem_get_info()[1])}
+    res: dict = {"torch_total": int(torch.cuda.mem_get_info()[1])}
+    calls = {
+        "total": lambda: int(amdsmi.amdsmi_get_gpu_memory_total(h, amdsmi.AmdSmiMemoryType.VRAM)),
+        "used": lambda: int(amdsmi.amdsmi_get_gpu_memory_usage(h, amdsmi.AmdSmiMemoryType.VRAM)),
+        "vram_usage": lambda: amdsmi.amdsmi_get_gpu_vram_usage(h),
+        "vram_info": lambda: int(amdsmi.amdsmi_get_gpu_vram_info(h)["vram_size"]),
+    }
+    for k, fn in calls.items():
+        try:
+            v = fn()
+        except Exception as e:  # not every query is supported on every host/partition mode
+            res.setdefault("errors", {})[k] = repr(e)[:200]
+            continue
+        if k == "vram_usage":
+            res["vram_total_mb"], res["vram_used_mb"] = int(v["vram_total"]), int(v["vram_used"])
+        else:
+            res[k] = v
     amdsmi.amdsmi_shut_down()
     del x
     return res

@@ -50,6 +50,7 @@ class DevicePluginConfig:
     device_cores_scaling: float = 1.0
     disable_core_limit: bool = False
     hw_queues_per_vgpu: int = 1           # GPU_MAX_HW_QUEUES for fractional vGPUs (0 = runtime default)
+    hsa_tools_intercept: bool = False     # also hand the shim ROCr's API table (HSA_TOOLS_LIB)
     partition_mode: str = ""             # SPX|DPX|QPX|CPX expected compute partition ("" = as found)
     config_file: str = "/config/config.json"
     socket_dir: str = "/var/lib/kubelet/device-plugins"

@@ -168,6 +168,10 @@ def build_container_grant(cfg: DevicePluginConfig, pod: dict, ctr_idx: int, devr
     if fractional and cfg.hw_queues_per_vgpu and "GPU_MAX_HW_QUEUES" not in env_names:
         g.envs["GPU_MAX_HW_QUEUES"] = str(cfg.hw_queues_per_vgpu)
     g.envs[ENV_SHARED_REGION] = f"{CONTAINER_CACHE_DIR}/vgpu.cache"
+    if cfg.hsa_tools_intercept and "HSA_TOOLS_LIB" not in env_names:
+        # ROCr hands the shim its API table in hsa_init: queue and pool calls
+        # are enforced even for code that resolved hsa_* by hand.
+        g.envs["HSA_TOOLS_LIB"] = f"{CONTAINER_LIB_DIR}/{SHIM_NAME}"
     if cfg.device_memory_scaling > 1:
         g.envs[ENV_OVERSUBSCRIBE] = "true"
     if cfg.disable_core_limit:
