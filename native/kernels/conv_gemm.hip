@@ -32,6 +32,7 @@
 // XCD's L2.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #define VGPU_API extern "C" __attribute__((visibility("default")))
 
@@ -330,6 +331,283 @@ __global__ void __launch_bounds__(kThreads, 2) conv_gemm_kernel(const ConvArgs a
 #undef VGPU_STEP
 #undef VGPU_EPILOGUE
 
+// ---- LDS-DMA variant (no prologue): A and B tiles go HBM → LDS with
+// buffer_load_dword×4 … lds, bypassing the VGPR → ds_write_b128 path.
+//
+// Why: with register staging a 128×128×64 step writes 32 KB into LDS through
+// ds_write_b128 (≈79 B/clk/CU) and reads 64 KB back (256 B/clk/CU): ≈670 LDS
+// cycles against 512 MFMA cycles per block-step, i.e. LDS-bound at 2 blocks/CU.
+// The DMA writes at the LDS array rate, so the same step costs ≈384 LDS cycles.
+//
+// The LDS image is the same XOR-swizzled [row][128 B] layout as the register
+// path; a DMA lands lane-linearly (wave base + 16·lane), so each lane fetches
+// the LOGICAL chunk (lane&7) ^ (row&7) of its row — the swizzle is applied to
+// the global source address.  Zero padding / M tail: out-of-range buffer
+// offsets load zeros into LDS.  Two stages, one DMA step in flight: wait for
+// the current stage with a counted vmcnt (the next stage stays in flight),
+// raw s_barrier (a __syncthreads() would drain the DMA with vmcnt(0)).
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+constexpr int vmcnt_imm(int n) {  // s_waitcnt vmcnt(n), expcnt/lgkmcnt untouched (gfx9 encoding)
+  return (n & 15) | (((n >> 4) & 3) << 14) | (7 << 4) | (15 << 8);
+}
+constexpr int kLgkm0 = 15 | (3 << 14) | (7 << 4);  // s_waitcnt lgkmcnt(0) only
+
+// PRO (block-entry BN+ReLU on the input, 1x1 / pad 0 only, so no padded
+// pixel exists that the prologue would turn non-zero): the raw input is DMA'd
+// like any other, and the per-channel affine + ReLU is applied to each A
+// fragment in registers between its ds_read and its MFMA.  The block's BN
+// scale/shift (C ≤ 2048 floats each) sit in LDS behind the two stages.
+//
+// CSM = 16: a narrow-input conv (the ResNet stem after space-to-depth: C = 16,
+// 4x4 taps) — a 64-wide K step then spans 64/C taps, so each lane derives its
+// own tap from its chunk.
+template <int KS, int BM, int BN, bool PRO, bool RES, int CSM = 0>
+__global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a) {
+  static_assert(!PRO || KS == 1, "the in-register prologue needs a padding-free conv");
+  static_assert(CSM == 0 || (!PRO && 64 % CSM == 0 && CSM % 8 == 0), "narrow-C variant");
+  constexpr int AR = BM / 32, BR = BN / 32;  // DMA instructions per thread per K step
+  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int CS = BN + 4;
+  constexpr int PIPE = 2 * STAGE;
+  constexpr int HROWS = BM / 2, EPI = HROWS * CS * 4;  // epilogue staged in two row halves
+  constexpr int BODY = PIPE > EPI ? PIPE : EPI;
+  constexpr int PARAMS = PRO ? 2048 * 2 * 4 : 0;     // scale[C] then shift[C]
+  constexpr int CPR = BN / 8, RSTEP = kThreads / CPR, RROWS = HROWS / RSTEP;
+  __shared__ __attribute__((aligned(16))) char smem[BODY + PARAMS];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int lrow = t >> 3, lchunk = (t & 7) ^ (lrow & 7);
+  const int chunk = t % CPR, rfirst = t / CPR;
+  int m0, n0;
+  tile_origin(a, blockIdx.x, BM, BN, m0, n0);
+
+  float* sPar = reinterpret_cast<float*>(smem + BODY);
+  if constexpr (PRO) {  // before the first DMA: no ordinary load shares the pipeline with it
+    for (int c = t * 4; c < a.C; c += kThreads * 4) {
+      *reinterpret_cast<float4*>(sPar + c) = *reinterpret_cast<const float4*>(a.pscale + c);
+      *reinterpret_cast<float4*>(sPar + a.C + c) = *reinterpret_cast<const float4*>(a.pshift + c);
+    }
+  }
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.x), 0, a.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.w), 0, (uint32_t)((int64_t)a.Cout * a.K * 2), 0x00020000);
+
+  int abase[AR], aih[AR], aiw[AR];
+  bool aok[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int m = m0 + lrow + 32 * i;
+    aok[i] = m < a.M;
+    const int mm = aok[i] ? m : 0;
+    const int ow = mm % a.OW, t2 = mm / a.OW, oh = t2 % a.OH, n = t2 / a.OH;
+    aih[i] = oh * a.stride - a.pad;
+    aiw[i] = ow * a.stride - a.pad;
+    abase[i] = ((n * a.H + aih[i]) * a.W + aiw[i]) * a.C * 2;
+  }
+  const uint32_t boff = (uint32_t)(((n0 + lrow) * a.K + lchunk * 8) * 2);
+
+  auto issue = [&](int kt, int st) {
+    char* sA = smem + st * STAGE;
+    char* sB = sA + A_BYTES;
+    int kh, kw, toff;
+    if constexpr (CSM != 0) {  // per-lane tap: k = kt*64 + lchunk*8 = tap*CSM + c
+      const int k = kt * BK + lchunk * 8, tap = k / CSM, c = k % CSM;
+      kh = tap / KS;
+      kw = tap % KS;
+      toff = ((kh * a.W + kw) * CSM + c) * 2;
+    } else {
+      const int tap = kt / a.cblocks, cb = kt - tap * a.cblocks;
+      kh = tap / KS;
+      kw = tap - kh * KS;
+      toff = ((kh * a.W + kw) * a.C + cb * BK + lchunk * 8) * 2;
+    }
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      bool v = aok[i];
+      if (KS != 1 || a.pad != 0) {
+        const int ih = aih[i] + kh, iw = aiw[i] + kw;
+        v = v && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          xr, (lds_void_t*)(sA + (32 * i + wave * 8) * 128), 16,
+          v ? (uint32_t)(abase[i] + toff) : kOOB, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          wr, (lds_void_t*)(sB + (32 * i + wave * 8) * 128), 16,
+          boff + (uint32_t)((32 * i * a.K + kt * BK) * 2), 0, 0, 0);
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  if constexpr (PRO) __syncthreads();  // parameters visible (no DMA in flight yet)
+  issue(0, 0);
+  for (int kt = 0; kt < a.ktiles; ++kt) {
+    const int st = kt & 1;
+    if (kt + 1 < a.ktiles) {
+      issue(kt + 1, st ^ 1);
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR + BR));
+    } else {
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+    }
+    __builtin_amdgcn_s_barrier();
+    const char* sA = smem + st * STAGE;
+    const char* sB = sA + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8_t*>(sA + swz(wm * WTM + i * 16 + fr, kk * 4 + fk));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(wn * WTN + j * 16 + fr, kk * 4 + fk));
+      if constexpr (PRO) {
+        // channels of this lane's 8 k-elements: cb*64 + kk*32 + fk*8 + (0..7)
+        const int c = (kt % a.cblocks) * BK + kk * 32 + fk * 8;
+        const float4 s0 = *reinterpret_cast<const float4*>(sPar + c);
+        const float4 s1 = *reinterpret_cast<const float4*>(sPar + c + 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(sPar + a.C + c);
+        const float4 h1 = *reinterpret_cast<const float4*>(sPar + a.C + c + 4);
+        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          float e[8];
+          unpack8(__builtin_bit_cast(u32x4, af[i]), e);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) e[j] = fmaxf(e[j] * sc[j] + sh[j], 0.0f);
+          af[i] = __builtin_bit_cast(bf16x8_t, pack8(e));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    // Stage st fully read (this wave's ds_reads retired) before any wave refills it.
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // Epilogue, one row half at a time: accumulators → LDS (fp32) → 16-B
+  // coalesced bias + residual + act + store.  The residual loads of a half
+  // overlap its accumulator staging.
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(RES ? a.res : a.x), 0, RES ? a.y_bytes : 0u, 0x00020000);
+  const int col = n0 + chunk * 8;
+  float bb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bb[j] = 0.0f;
+  if (a.bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(a.bias + col);
+    const float4 b1 = *reinterpret_cast<const float4*>(a.bias + col + 4);
+    bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
+    bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+  }
+  float* sC = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    u32x4 res[RROWS];
+    if constexpr (RES) {
+#pragma unroll
+      for (int i = 0; i < RROWS; ++i) {
+        const int m = m0 + h * HROWS + rfirst + RSTEP * i;
+        res[i] = __builtin_amdgcn_raw_buffer_load_b128(
+            rr, m < a.M ? (uint32_t)(((int64_t)m * a.Cout + col) * 2) : kOOB, 0, 0);
+      }
+    }
+    if (wm == h) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            sC[(i * 16 + fk * 4 + e) * CS + wn * WTN + j * 16 + fr] = acc[i][j][e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RROWS; ++i) {
+      const int r = rfirst + RSTEP * i, m = m0 + h * HROWS + r;
+      const float4 c0 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8);
+      const float4 c1 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8 + 4);
+      float v[8] = {c0.x + bb[0], c0.y + bb[1], c0.z + bb[2], c0.w + bb[3],
+                    c1.x + bb[4], c1.y + bb[5], c1.z + bb[6], c1.w + bb[7]};
+      if constexpr (RES) {
+        float re[8];
+        unpack8(res[i], re);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += re[j];
+      }
+      if (a.act) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);
+      }
+      if (m < a.M) *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = pack8(v);
+    }
+    if (h == 0) __syncthreads();  // half 0 read out before half 1 is staged
+  }
+}
+
+template <int KS, int BM, int BN, bool PRO, bool RES, int CSM = 0>
+hipError_t launch_glds(ConvArgs a, hipStream_t s) {
+  a.nM = (a.M + BM - 1) / BM;
+  a.nN = a.Cout / BN;
+  a.nwg = a.nM * a.nN;
+  hipLaunchKernelGGL((conv_glds_kernel<KS, BM, BN, PRO, RES, CSM>), dim3(a.nwg), dim3(kThreads), 0, s,
+                     a);
+  return hipGetLastError();
+}
+
+template <int KS, int BM, int BN, bool PRO>
+hipError_t dispatch_glds_r(const ConvArgs& a, bool res, hipStream_t s) {
+  return res ? launch_glds<KS, BM, BN, PRO, true>(a, s) : launch_glds<KS, BM, BN, PRO, false>(a, s);
+}
+
+template <int KS, int BM>
+hipError_t dispatch_glds(const ConvArgs& a, bool pro, bool res, hipStream_t s) {
+  if constexpr (KS == 1) {
+    if (pro)
+      return a.Cout % 128 == 0 ? dispatch_glds_r<1, BM, 128, true>(a, res, s)
+                               : dispatch_glds_r<1, BM, 64, true>(a, res, s);
+  }
+  return a.Cout % 128 == 0 ? dispatch_glds_r<KS, BM, 128, false>(a, res, s)
+                           : dispatch_glds_r<KS, BM, 64, false>(a, res, s);
+}
+
+bool glds_pro_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* v = getenv("VGPU_CONV_GLDS_PRO");
+    on = (v && v[0] == '1') ? 1 : 0;
+  }
+  return on == 1;
+}
+
+bool glds_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* v = getenv("VGPU_CONV_GLDS");
+    on = (v && (v[0] == '0' || v[0] == 'n' || v[0] == 'f')) ? 0 : 1;
+  }
+  return on == 1;
+}
+
 template <int KS, int BM, int BN, bool PRO, bool RES>
 hipError_t launch(ConvArgs a, hipStream_t s) {
   static int occ = 0;  // resident workgroups per CU (LDS / VGPR bound); one value per instantiation
@@ -432,14 +710,69 @@ __global__ void __launch_bounds__(kThreads) ssr_mean_kernel(const u32x4* __restr
   }
 }
 
+// ---- ResNet stem space-to-depth: x [N][H][W][3] → X [N][HS][WS][16] ------------
+// X[n][i][j][b*6 + b'*3 + c] = x[n][2i+b-pad][2j+b'-pad][c] (zero outside; channels
+// 12..15 zero), so the 7x7/s2 stem becomes a 4x4/s1 conv with C = 16 (16-B
+// aligned taps for the LDS-DMA conv).  One thread per X pixel, 2×16-B stores.
+__global__ void __launch_bounds__(kThreads) s2d_stem_kernel(const uint16_t* __restrict__ x,
+                                                            u32x4* __restrict__ X, int N, int H,
+                                                            int W, int HS, int WS, int pad) {
+  const int64_t total = (int64_t)N * HS * WS;
+  for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < total;
+       p += (int64_t)gridDim.x * kThreads) {
+    const int j = (int)(p % WS);
+    const int64_t t2 = p / WS;
+    const int i = (int)(t2 % HS);
+    const int n = (int)(t2 / HS);
+    uint16_t v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = 0;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int r = 2 * i + b - pad;
+      if ((unsigned)r >= (unsigned)H) continue;
+#pragma unroll
+      for (int b2 = 0; b2 < 2; ++b2) {
+        const int c0 = 2 * j + b2 - pad;
+        if ((unsigned)c0 >= (unsigned)W) continue;
+        const uint16_t* src = x + (((int64_t)n * H + r) * W + c0) * 3;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[b * 6 + b2 * 3 + c] = src[c];
+      }
+    }
+    u32x4 lo, hi;
+    lo.x = v[0] | ((uint32_t)v[1] << 16); lo.y = v[2] | ((uint32_t)v[3] << 16);
+    lo.z = v[4] | ((uint32_t)v[5] << 16); lo.w = v[6] | ((uint32_t)v[7] << 16);
+    hi.x = v[8] | ((uint32_t)v[9] << 16); hi.y = v[10] | ((uint32_t)v[11] << 16);
+    hi.z = 0; hi.w = 0;
+    X[2 * p] = lo;
+    X[2 * p + 1] = hi;
+  }
+}
+
 }  // namespace
+
+VGPU_API int vgpu_stem_space_to_depth(const void* x, void* X, int N, int H, int W, int pad, int HS,
+                                      int WS, hipStream_t s) {
+  if (N < 1 || H < 1 || W < 1 || HS < 1 || WS < 1 || pad < 0) return -1;
+  const int64_t total = (int64_t)N * HS * WS;
+  const int64_t want = (total + kThreads - 1) / kThreads;
+  const int grid = (int)(want < 256 * 32 ? want : 256 * 32);
+  hipLaunchKernelGGL(s2d_stem_kernel, dim3(grid), dim3(kThreads), 0, s,
+                     static_cast<const uint16_t*>(x), static_cast<u32x4*>(X), N, H, W, HS, WS, pad);
+  return (int)hipGetLastError();
+}
 
 // Returns 0, a hipError_t, or -1 for an unsupported shape (checked before any launch).
 VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void* res,
                               const float* bias, const float* pscale, const float* pshift, int N,
                               int H, int W, int C, int Cout, int KS, int stride, int pad, int act,
                               hipStream_t s) {
-  if (C % 64 || Cout % 64 || (KS != 1 && KS != 3) || stride < 1 || pad < 0 || N < 1) return -1;
+  // C % 64 == 0 with 1x1 / 3x3 filters, or the narrow stem form (C = 16, 4x4,
+  // stride 1, no prologue: a 7x7/s2 conv on a space-to-depth input).
+  const bool narrow = C == 16 && KS == 4 && stride == 1 && pscale == nullptr;
+  if (!narrow && (C % 64 || (KS != 1 && KS != 3))) return -1;
+  if (Cout % 64 || stride < 1 || pad < 0 || N < 1) return -1;
   if ((pscale == nullptr) != (pshift == nullptr)) return -1;
   ConvArgs a{};
   a.x = static_cast<const uint16_t*>(x);
@@ -455,7 +788,7 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
   if (a.OH < 1 || a.OW < 1) return -1;
   a.K = KS * KS * C;
   a.cblocks = C / 64;
-  a.ktiles = KS * KS * a.cblocks;
+  a.ktiles = a.K / 64;
   a.act = act != 0;
   const bool pro = pscale != nullptr, has_res = res != nullptr;
   // Buffer offsets are 32-bit: run the batch in slices whose activations stay < 2 GiB.
@@ -478,7 +811,17 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
     const int64_t tiles128 = (int64_t)((c.M + 127) / 128) * (Cout / bn);
     const bool small = tiles128 < 512;
     hipError_t e;
-    if (KS == 1)
+    // LDS-DMA kernels for everything except a prologue on a padded conv
+    // (padding must stay zero AFTER the prologue).
+    // (The in-register prologue variant measured slower than the register
+    // path on every ResNet-50 shape — VALU-bound — so it is opt-in.)
+    const bool glds = glds_enabled() && (!pro || (glds_pro_enabled() && KS == 1 && pad == 0 && C <= 2048));
+    if (narrow)
+      e = small ? launch_glds<4, 64, 64, false, false, 16>(c, s) : launch_glds<4, 128, 64, false, false, 16>(c, s);
+    else if (glds)
+      e = KS == 1 ? (small ? dispatch_glds<1, 64>(c, pro, has_res, s) : dispatch_glds<1, 128>(c, pro, has_res, s))
+                  : (small ? dispatch_glds<3, 64>(c, pro, has_res, s) : dispatch_glds<3, 128>(c, pro, has_res, s));
+    else if (KS == 1)
       e = small ? dispatch_bn<1, 64>(c, pro, has_res, s) : dispatch_bn<1, 128>(c, pro, has_res, s);
     else
       e = small ? dispatch_bn<3, 64>(c, pro, has_res, s) : dispatch_bn<3, 128>(c, pro, has_res, s);

@@ -36,6 +36,9 @@ CASES = [
     (1, 192, 7, 5, 320, 3, 1, 1, True, "none", True, True),      # everything, odd sizes
     (5, 512, 6, 6, 2048, 1, 1, 0, False, "none", False, True),   # stage-4 conv3, M % 128 != 0
     (1, 2048, 3, 3, 512, 1, 1, 0, True, "relu", True, False),    # deep K
+    (16, 64, 64, 64, 256, 3, 1, 1, True, "relu", False, False),  # BM=128 LDS-DMA 3x3 tiles
+    (16, 64, 64, 63, 64, 3, 1, 1, False, "none", False, True),   # BM=128 x BN=64, ragged M
+    (16, 64, 64, 64, 256, 1, 1, 0, False, "none", False, True),  # BM=128 1x1 + residual
 ]
 
 
@@ -117,3 +120,14 @@ def test_native_vgg_matches_module(gpu_build):
     got = NativeVGG16Inference(mb)(x.to(torch.bfloat16)).float()
     rel = (got - ref).norm() / ref.norm()
     assert rel < 0.05, float(rel)
+
+
+@pytest.mark.parametrize("hw", [(346, 346), (64, 61), (9, 10)])
+def test_stem_space_to_depth_conv(C, hw):
+    h, w = hw
+    x = _t((2, 3, h, w), 11)
+    wt = _t((64, 3, 7, 7), 12, scale=(2.0 / 147) ** 0.5)
+    got = C.stem_conv(x, C.stem_weight_s2d(wt))
+    ref = torch.nn.functional.conv2d(x.float(), wt.float(), stride=2, padding=3)
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=CL)
+    torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)

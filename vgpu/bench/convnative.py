@@ -62,6 +62,27 @@ def main(argv=None) -> int:
         return e0.elapsed_time(e1) * 1e3 / args.iters
 
     tot_n = tot_m = 0.0
+    # stem: space-to-depth + 4x4 narrow-C MFMA conv vs MIOpen's 7x7/s2 on C=3
+    xs = torch.randn(args.batch, 3, args.size, args.size, device=dev, dtype=torch.bfloat16).contiguous(
+        memory_format=cl)
+    ws = (torch.randn(64, 3, 7, 7, device=dev) * (2 / 147) ** 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+    ws2d = C.stem_weight_s2d(ws)
+    t_nat = timeit(lambda: C.stem_conv(xs, ws2d))
+    t_mio = None if args.no_miopen else timeit(lambda: F.conv2d(xs, ws, stride=2, padding=3))
+    oh = (args.size + 6 - 7) // 2 + 1
+    flop = 2.0 * args.batch * oh * oh * 64 * 147
+    tot_n += t_nat
+    tot_m += t_mio or 0.0
+    print(json.dumps({"layer": "stem", "M": args.batch * oh * oh, "K": 147, "N": 64,
+                      "native_us": round(t_nat, 1), "miopen_us": None if t_mio is None else round(t_mio, 1),
+                      "native_tflops": round(flop / t_nat / 1e6, 1),
+                      "native_tbps": round((xs.numel() * 2 + args.batch * oh * oh * 64 * 2) / t_nat / 1e6, 2)}),
+          flush=True)
+    y0 = C.stem_conv(xs, ws2d)
+    t_pool = timeit(lambda: C.maxpool3s2(y0))
+    print(json.dumps({"layer": "stem.maxpool", "native_us": round(t_pool, 1),
+                      "native_tbps": round((y0.numel() * 2 * 1.25) / t_pool / 1e6, 2)}), flush=True)
+    tot_n += t_pool
     for name, n, c, h, w, cout, ks, stride, pad, ba, pro, res in layer_shapes(args.batch, args.size):
         x = torch.randn(n, c, h, w, device=dev, dtype=torch.bfloat16).contiguous(memory_format=cl)
         wt = (torch.randn(cout, c, ks, ks, device=dev) * (2 / (c * ks * ks)) ** 0.5).to(

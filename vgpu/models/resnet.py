@@ -105,6 +105,7 @@ class FusedResNetV2Inference(nn.Module):
     projection shortcut, folded-BN bias + ReLU as the epilogue of conv1/conv2,
     the residual add as the epilogue of conv3 — so a bottleneck is 3 (or 4)
     kernels and the pre-activation tensor is never materialised.  The stem
+    7x7/s2 stem runs as space-to-depth + a 4x4 narrow-C MFMA conv; its
     max-pool and the final BN+ReLU+global-mean are hand-written kernels too.
 
     conv="miopen": MIOpen convolutions + the fused NHWC epilogues of
@@ -132,6 +133,9 @@ class FusedResNetV2Inference(nn.Module):
 
         with torch.no_grad():
             self.stem_w = m.stem.weight.detach().contiguous(memory_format=cl)
+            if conv == "native":
+                from vgpu.ops.conv import stem_weight_s2d
+                self.stem_w_s2d = stem_weight_s2d(self.stem_w)
             self.blocks = []
             for blk in m.blocks:
                 w1, b1 = fold(blk.conv1, blk.bn1)
@@ -155,8 +159,8 @@ class FusedResNetV2Inference(nn.Module):
 
     def _forward_native(self, x: torch.Tensor) -> torch.Tensor:
         from vgpu.ops import conv as C
-        x = F.conv2d(x, self.stem_w, stride=2, padding=3)  # C=3: MIOpen
-        x = C.maxpool3s2(x.contiguous(memory_format=torch.channels_last))
+        x = C.stem_conv(x.contiguous(memory_format=torch.channels_last), self.stem_w_s2d)
+        x = C.maxpool3s2(x)
         for b in self.blocks:
             pro = b["in"]
             if b["sc"] is None:

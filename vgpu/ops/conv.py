@@ -5,7 +5,8 @@
 
 Tensors: bf16, NCHW-shaped, channels_last memory.  Supported: 1x1 and 3x3
 filters, any stride / padding, C % 64 == 0 and Cout % 64 == 0 (every
-convolution of ResNet-V2 after the stem).  No silent fallback: unsupported
+convolution of ResNet-V2 after the stem), plus the narrow 4x4 C=16 form the
+stem takes after space-to-depth (stem_conv).  No silent fallback: unsupported
 shapes raise, a missing extension raises NativeMissing.
 """
 from __future__ import annotations
@@ -36,7 +37,7 @@ def _nhwc(t: torch.Tensor, name: str) -> None:
 
 
 def supported(c: int, cout: int, ks: int) -> bool:
-    return c % 64 == 0 and cout % 64 == 0 and ks in (1, 3)
+    return cout % 64 == 0 and ((c % 64 == 0 and ks in (1, 3)) or (c == 16 and ks == 4))
 
 
 def out_hw(h: int, w: int, ks: int, stride: int, pad: int) -> tuple[int, int]:
@@ -81,6 +82,54 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
     if rc != 0:
         raise RuntimeError(f"vgpu_conv2d_nhwc: error {rc}")
     return out
+
+
+# ---- ResNet stem as a space-to-depth conv ------------------------------------------
+# conv7x7/s2/p3 over C=3 == conv4x4/s1/p0 over X = s2d(pad(x)) with C = 12 (→16):
+#   out[oh,ow] = Σ_{a,a',b,b',c} X[oh+a, ow+a', (b,b',c)] · W8[c, 2a+b, 2a'+b']
+# (W8 = the 7x7 filter zero-padded to 8x8).  The MFMA conv then sees 16-B-aligned
+# taps instead of 6-byte pixels.
+
+def stem_s2d_shape(h: int, w: int, k: int = 7, stride: int = 2, pad: int = 3) -> tuple[int, int, int, int]:
+    """(OH, OW, HS, WS) of a k×k/stride-2 stem and its space-to-depth input."""
+    if stride != 2 or k % 2 != 1:
+        raise ValueError("space-to-depth stem needs an odd kernel with stride 2")
+    oh, ow = out_hw(h, w, k, stride, pad)
+    kk = (k + 1) // 2
+    return oh, ow, oh + kk - 1, ow + kk - 1
+
+
+def stem_weight_s2d(w: torch.Tensor) -> torch.Tensor:
+    """[Cout,3,k,k] (k odd) → [Cout,16,(k+1)/2,(k+1)/2] bf16 channels_last."""
+    cout, c, k, _ = w.shape
+    if c != 3 or k % 2 != 1:
+        raise ValueError("stem weight must be [Cout,3,k,k] with k odd")
+    kk = (k + 1) // 2
+    w8 = torch.zeros(cout, c, 2 * kk, 2 * kk, dtype=torch.float32, device=w.device)
+    w8[:, :, :k, :k] = w.float()
+    # (o, c, a, b, a', b') → (o, a, a', b, b', c)
+    t = w8.view(cout, c, kk, 2, kk, 2).permute(0, 2, 4, 3, 5, 1).reshape(cout, kk, kk, 4 * c)
+    t = F.pad(t, (0, 16 - 4 * c))
+    return t.to(w.dtype).permute(0, 3, 1, 2).contiguous(memory_format=_CL)
+
+
+def stem_space_to_depth(x: torch.Tensor, k: int = 7, pad: int = 3) -> torch.Tensor:
+    """x [N,3,H,W] bf16 channels_last → X [N,16,HS,WS] bf16 channels_last."""
+    _nhwc(x, "x")
+    n, c, h, w = x.shape
+    if c != 3:
+        raise ValueError("stem input must have 3 channels")
+    _, _, hs, ws = stem_s2d_shape(h, w, k, 2, pad)
+    out = torch.empty((n, 16, hs, ws), dtype=x.dtype, device=x.device, memory_format=_CL)
+    rc = load_kernels().vgpu_stem_space_to_depth(_ptr(x), _ptr(out), n, h, w, pad, hs, ws, _stream())
+    if rc != 0:
+        raise RuntimeError(f"vgpu_stem_space_to_depth: error {rc}")
+    return out
+
+
+def stem_conv(x: torch.Tensor, w_s2d: torch.Tensor, k: int = 7, pad: int = 3) -> torch.Tensor:
+    """7x7/s2 stem on the MFMA conv: space-to-depth + 4x4/s1 narrow-C conv."""
+    return conv2d(stem_space_to_depth(x, k, pad), w_s2d)
 
 
 def maxpool(x: torch.Tensor, k: int, stride: int, pad: int = 0) -> torch.Tensor:
