@@ -353,6 +353,90 @@ constexpr int vmcnt_imm(int n) {  // s_waitcnt vmcnt(n), expcnt/lgkmcnt untouche
 }
 constexpr int kLgkm0 = 15 | (3 << 14) | (7 << 4);  // s_waitcnt lgkmcnt(0) only
 
+// Epilogue, one row half at a time: accumulators → LDS (fp32) → 16-B
+// coalesced bias + residual + act + store.  The residual loads of a half
+// overlap its accumulator staging.  Needs (BM/2)·(BN+4)·4 bytes of LDS and a
+// block-wide barrier behind the last read of the pipeline stages.
+template <int BM, int BN>
+struct EpiShape {
+  static constexpr int HROWS = BM / 2, CPR = BN / 8, RSTEP = kThreads / CPR, RROWS = HROWS / RSTEP;
+};
+
+// Residual rows this thread adds in the epilogue (both halves), issued early —
+// before the first DMA of the K loop — so their latency hides behind the loop.
+template <int BM, int BN>
+__device__ __forceinline__ void load_residual(const ConvArgs& a, int m0, int n0,
+                                              u32x4 (&res)[2][EpiShape<BM, BN>::RROWS]) {
+  using E = EpiShape<BM, BN>;
+  const int t = threadIdx.x, chunk = t % E::CPR, rfirst = t / E::CPR;
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.res), 0, a.y_bytes, 0x00020000);
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < E::RROWS; ++i) {
+      const int m = m0 + h * E::HROWS + rfirst + E::RSTEP * i;
+      res[h][i] = __builtin_amdgcn_raw_buffer_load_b128(
+          rr, m < a.M ? (uint32_t)(((int64_t)m * a.Cout + n0 + chunk * 8) * 2) : kOOB, 0, 0);
+    }
+}
+
+template <int BM, int BN, bool RES>
+__device__ __forceinline__ void epilogue_halves(const ConvArgs& a, f32x4_t (&acc)[BM / 32][BN / 32],
+                                                int m0, int n0, char* smem,
+                                                const u32x4 (&res)[2][EpiShape<BM, BN>::RROWS]) {
+  constexpr int WTM = BM / 2, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
+  constexpr int CS = BN + 4, HROWS = BM / 2;
+  constexpr int CPR = BN / 8, RSTEP = kThreads / CPR, RROWS = HROWS / RSTEP;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fk = lane >> 4;
+  const int chunk = t % CPR, rfirst = t / CPR;
+  const int col = n0 + chunk * 8;
+  float bb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bb[j] = 0.0f;
+  if (a.bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(a.bias + col);
+    const float4 b1 = *reinterpret_cast<const float4*>(a.bias + col + 4);
+    bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
+    bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+  }
+  float* sC = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (wm == h) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            sC[(i * 16 + fk * 4 + e) * CS + wn * WTN + j * 16 + fr] = acc[i][j][e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RROWS; ++i) {
+      const int r = rfirst + RSTEP * i, m = m0 + h * HROWS + r;
+      const float4 c0 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8);
+      const float4 c1 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8 + 4);
+      float v[8] = {c0.x + bb[0], c0.y + bb[1], c0.z + bb[2], c0.w + bb[3],
+                    c1.x + bb[4], c1.y + bb[5], c1.z + bb[6], c1.w + bb[7]};
+      if constexpr (RES) {
+        float re[8];
+        unpack8(res[h][i], re);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += re[j];
+      }
+      if (a.act) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);
+      }
+      if (m < a.M) *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = pack8(v);
+    }
+    if (h == 0) __syncthreads();  // half 0 read out before half 1 is staged
+  }
+}
+
 // PRO (block-entry BN+ReLU on the input, 1x1 / pad 0 only, so no padded
 // pixel exists that the prologue would turn non-zero): the raw input is DMA'd
 // like any other, and the per-channel affine + ReLU is applied to each A
@@ -431,11 +515,9 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
     }
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
-      bool v = aok[i];
-      if (KS != 1 || a.pad != 0) {
-        const int ih = aih[i] + kh, iw = aiw[i] + kw;
-        v = v && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      }
+      // Bitwise (not short-circuit) validity: no exec-mask branch around the load.
+      const int ih = aih[i] + kh, iw = aiw[i] + kw;
+      const bool v = aok[i] & ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           xr, (lds_void_t*)(sA + (32 * i + wave * 8) * 128), 16,
           v ? (uint32_t)(abase[i] + toff) : kOOB, 0, 0, 0);
@@ -454,6 +536,14 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   if constexpr (PRO) __syncthreads();  // parameters visible (no DMA in flight yet)
+  // Short K loops (stage-1 1x1 convs: one K step) fetch the residual up front,
+  // so its latency overlaps the A/B DMA; longer loops fetch it after the loop
+  // (measured: early fetch costs 5-20 % on K ≥ 4 steps).
+  u32x4 res[2][EpiShape<BM, BN>::RROWS];
+  const bool early_res = RES && a.ktiles <= 1;
+  if constexpr (RES) {
+    if (early_res) load_residual<BM, BN>(a, m0, n0, res);
+  }
   issue(0, 0);
   for (int kt = 0; kt < a.ktiles; ++kt) {
     const int st = kt & 1;
@@ -503,65 +593,10 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     __builtin_amdgcn_s_barrier();
   }
-
-  // Epilogue, one row half at a time: accumulators → LDS (fp32) → 16-B
-  // coalesced bias + residual + act + store.  The residual loads of a half
-  // overlap its accumulator staging.
-  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(RES ? a.res : a.x), 0, RES ? a.y_bytes : 0u, 0x00020000);
-  const int col = n0 + chunk * 8;
-  float bb[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bb[j] = 0.0f;
-  if (a.bias) {
-    const float4 b0 = *reinterpret_cast<const float4*>(a.bias + col);
-    const float4 b1 = *reinterpret_cast<const float4*>(a.bias + col + 4);
-    bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
-    bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+  if constexpr (RES) {
+    if (!early_res) load_residual<BM, BN>(a, m0, n0, res);
   }
-  float* sC = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    u32x4 res[RROWS];
-    if constexpr (RES) {
-#pragma unroll
-      for (int i = 0; i < RROWS; ++i) {
-        const int m = m0 + h * HROWS + rfirst + RSTEP * i;
-        res[i] = __builtin_amdgcn_raw_buffer_load_b128(
-            rr, m < a.M ? (uint32_t)(((int64_t)m * a.Cout + col) * 2) : kOOB, 0, 0);
-      }
-    }
-    if (wm == h) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            sC[(i * 16 + fk * 4 + e) * CS + wn * WTN + j * 16 + fr] = acc[i][j][e];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < RROWS; ++i) {
-      const int r = rfirst + RSTEP * i, m = m0 + h * HROWS + r;
-      const float4 c0 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8);
-      const float4 c1 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8 + 4);
-      float v[8] = {c0.x + bb[0], c0.y + bb[1], c0.z + bb[2], c0.w + bb[3],
-                    c1.x + bb[4], c1.y + bb[5], c1.z + bb[6], c1.w + bb[7]};
-      if constexpr (RES) {
-        float re[8];
-        unpack8(res[i], re);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] += re[j];
-      }
-      if (a.act) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);
-      }
-      if (m < a.M) *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = pack8(v);
-    }
-    if (h == 0) __syncthreads();  // half 0 read out before half 1 is staged
-  }
+  epilogue_halves<BM, BN, RES>(a, acc, m0, n0, smem, res);
 }
 
 template <int KS, int BM, int BN, bool PRO, bool RES, int CSM = 0>
@@ -588,6 +623,195 @@ hipError_t dispatch_glds(const ConvArgs& a, bool pro, bool res, hipStream_t s) {
   }
   return a.Cout % 128 == 0 ? dispatch_glds_r<KS, BM, 128, false>(a, res, s)
                            : dispatch_glds_r<KS, BM, 64, false>(a, res, s);
+}
+
+// ---- Prologue convs (block-entry BN+ReLU on the input): A through registers,
+// B through LDS-DMA.
+//
+// The prologue must touch every A element once, so A keeps the register path
+// (global → VGPR → affine+ReLU → ds_write, zero padding re-applied after the
+// prologue).  The weights need no transform and go HBM → LDS by DMA, which
+// halves the ds_write_b128 traffic that bounds the all-register kernel.
+// Per K step kt:  DMA B(kt+1) into the idle stage; load A(kt+2) into the free
+// register set; MFMA on stage kt; prologue + ds_write of A(kt+1) into the idle
+// stage; vmcnt(AR) (= B(kt+1) landed, A(kt+2) still in flight); barrier.
+template <int KS, int BM, int BN, bool RES>
+__global__ void __launch_bounds__(kThreads, 2) conv_pro_kernel(const ConvArgs a) {
+  constexpr int AR = BM / 32, BR = BN / 32;
+  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int PIPE = 2 * STAGE, EPI = (BM / 2) * (BN + 4) * 4;
+  constexpr int BODY = PIPE > EPI ? PIPE : EPI;
+  // BN scale/shift of the input channels live in LDS (C ≤ 2048): reading them
+  // with ordinary global loads inside the loop would make hipcc wait vmcnt(0)
+  // behind the weight DMA.
+  __shared__ __attribute__((aligned(16))) char smem[BODY + 2048 * 2 * 4];
+  float* sPar = reinterpret_cast<float*>(smem + BODY);
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int slot = t & 7, r0 = t >> 3;
+  const int lchunk = slot ^ (r0 & 7);  // DMA source chunk (swizzle on the source)
+  int m0, n0;
+  tile_origin(a, blockIdx.x, BM, BN, m0, n0);
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.x), 0, a.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.w), 0, (uint32_t)((int64_t)a.Cout * a.K * 2), 0x00020000);
+
+  int abase[AR], aih[AR], aiw[AR];
+  bool aok[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int m = m0 + r0 + 32 * i;
+    aok[i] = m < a.M;
+    const int mm = aok[i] ? m : 0;
+    const int ow = mm % a.OW, t2 = mm / a.OW, oh = t2 % a.OH, n = t2 / a.OH;
+    aih[i] = oh * a.stride - a.pad;
+    aiw[i] = ow * a.stride - a.pad;
+    abase[i] = ((n * a.H + aih[i]) * a.W + aiw[i]) * a.C * 2;
+  }
+  const uint32_t boff = (uint32_t)(((n0 + r0) * a.K + lchunk * 8) * 2);
+  for (int c = t * 4; c < a.C; c += kThreads * 4) {
+    *reinterpret_cast<float4*>(sPar + c) = *reinterpret_cast<const float4*>(a.pscale + c);
+    *reinterpret_cast<float4*>(sPar + a.C + c) = *reinterpret_cast<const float4*>(a.pshift + c);
+  }
+  __syncthreads();
+
+  auto issue_b = [&](int kt, int st) {
+    char* sB = smem + st * STAGE + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          wr, (lds_void_t*)(sB + (32 * i + wave * 8) * 128), 16,
+          boff + (uint32_t)((32 * i * a.K + kt * BK) * 2), 0, 0, 0);
+  };
+  auto load_a = [&](int kt, u32x4 (&ra)[AR], bool (&rv)[AR]) {
+    const int tap = kt / a.cblocks, cb = kt - tap * a.cblocks;
+    const int kh = tap / KS, kw = tap - kh * KS;
+    const int toff = ((kh * a.W + kw) * a.C + cb * BK + slot * 8) * 2;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      // Bitwise (not short-circuit) validity: no exec-mask branch around the load.
+      const int ih = aih[i] + kh, iw = aiw[i] + kw;
+      const bool v = aok[i] & ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
+      rv[i] = v;
+      ra[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, v ? (uint32_t)(abase[i] + toff) : kOOB, 0, 0);
+    }
+  };
+  auto store_a = [&](int kt, int st, u32x4 (&ra)[AR], const bool (&rv)[AR]) {
+    char* sA = smem + st * STAGE;
+    const int c = (kt % a.cblocks) * BK + slot * 8;
+    const float4 s0 = *reinterpret_cast<const float4*>(sPar + c);
+    const float4 s1 = *reinterpret_cast<const float4*>(sPar + c + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(sPar + a.C + c);
+    const float4 h1 = *reinterpret_cast<const float4*>(sPar + a.C + c + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      float e[8];
+      unpack8(ra[i], e);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = fmaxf(e[j] * sc[j] + sh[j], 0.0f);
+        e[j] = rv[i] ? f : 0.0f;  // padding / M tail stay zero after the prologue
+      }
+      *reinterpret_cast<u32x4*>(sA + swz(r0 + 32 * i, slot)) = pack8(e);
+    }
+  };
+  auto compute = [&](int st, f32x4_t (&acc)[TM][TN]) {
+    const char* sA = smem + st * STAGE;
+    const char* sB = sA + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8_t*>(sA + swz(wm * WTM + i * 16 + fr, kk * 4 + fk));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(wn * WTN + j * 16 + fr, kk * 4 + fk));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ra0[AR], ra1[AR];
+  bool rv0[AR], rv1[AR];
+  const int nk = a.ktiles;
+  u32x4 res[2][EpiShape<BM, BN>::RROWS];
+  load_a(0, ra0, rv0);
+  issue_b(0, 0);
+  store_a(0, 0, ra0, rv0);
+  load_a(nk > 1 ? 1 : 0, ra1, rv1);
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR));
+  __builtin_amdgcn_s_waitcnt(kLgkm0);
+  __builtin_amdgcn_s_barrier();
+  // Unrolled by two so the register sets stay static: step kt stores set
+  // (kt+1)&1 and refills set kt&1 with A(kt+2).
+  // Branch-free body: past the last K step the loads re-fetch the last tile into
+  // the idle stage (never read) — a branch around a load would make hipcc wait
+  // vmcnt(0) there and de-pipeline the loop.
+  auto step = [&](int kt, u32x4 (&rn)[AR], bool (&vn)[AR], u32x4 (&rs)[AR], bool (&vs)[AR]) {
+    const int st = kt & 1;
+    const int k1 = kt + 1 < nk ? kt + 1 : nk - 1, k2 = kt + 2 < nk ? kt + 2 : nk - 1;
+    issue_b(k1, st ^ 1);
+    load_a(k2, rn, vn);
+    compute(st, acc);
+    store_a(k1, st ^ 1, rs, vs);
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR));
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    __builtin_amdgcn_s_barrier();
+  };
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    step(kt, ra0, rv0, ra1, rv1);
+    step(kt + 1, ra1, rv1, ra0, rv0);
+  }
+  if (kt < nk) step(kt, ra0, rv0, ra1, rv1);
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // the trailing dummy loads, before LDS reuse
+  __syncthreads();
+  if constexpr (RES) load_residual<BM, BN>(a, m0, n0, res);
+  epilogue_halves<BM, BN, RES>(a, acc, m0, n0, smem, res);
+}
+
+template <int KS, int BM, int BN, bool RES>
+hipError_t launch_pro(ConvArgs a, hipStream_t s) {
+  a.nM = (a.M + BM - 1) / BM;
+  a.nN = a.Cout / BN;
+  a.nwg = a.nM * a.nN;
+  hipLaunchKernelGGL((conv_pro_kernel<KS, BM, BN, RES>), dim3(a.nwg), dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int KS, int BM>
+hipError_t dispatch_pro(const ConvArgs& a, bool res, hipStream_t s) {
+  if (a.Cout % 128 == 0)
+    return res ? launch_pro<KS, BM, 128, true>(a, s) : launch_pro<KS, BM, 128, false>(a, s);
+  return res ? launch_pro<KS, BM, 64, true>(a, s) : launch_pro<KS, BM, 64, false>(a, s);
+}
+
+bool pro_dma_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* v = getenv("VGPU_CONV_PRO_DMA");
+    on = (v && (v[0] == '0' || v[0] == 'n' || v[0] == 'f')) ? 0 : 1;
+  }
+  return on == 1;
 }
 
 bool glds_pro_enabled() {
@@ -818,6 +1042,11 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
     const bool glds = glds_enabled() && (!pro || (glds_pro_enabled() && KS == 1 && pad == 0 && C <= 2048));
     if (narrow)
       e = small ? launch_glds<4, 64, 64, false, false, 16>(c, s) : launch_glds<4, 128, 64, false, false, 16>(c, s);
+    // Short K (≤ 2 steps) or 64-wide outputs: the persistent register kernel,
+    // which overlaps the next tile's loads with this tile's epilogue, wins there.
+    else if (pro && !glds && pro_dma_enabled() && C <= 2048 && a.ktiles > 2 && Cout > 64)
+      e = KS == 1 ? (small ? dispatch_pro<1, 64>(c, has_res, s) : dispatch_pro<1, 128>(c, has_res, s))
+                  : (small ? dispatch_pro<3, 64>(c, has_res, s) : dispatch_pro<3, 128>(c, has_res, s));
     else if (glds)
       e = KS == 1 ? (small ? dispatch_glds<1, 64>(c, pro, has_res, s) : dispatch_glds<1, 128>(c, pro, has_res, s))
                   : (small ? dispatch_glds<3, 64>(c, pro, has_res, s) : dispatch_glds<3, 128>(c, pro, has_res, s));
