@@ -40,6 +40,8 @@ def main(argv=None) -> int:
     ap.add_argument("--size", type=int, default=346)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-miopen", action="store_true")
+    ap.add_argument("--only", default="", help="comma-separated layer names (profiling)")
+    ap.add_argument("--no-stem", action="store_true")
     args = ap.parse_args(argv)
 
     import torch
@@ -62,6 +64,10 @@ def main(argv=None) -> int:
         return e0.elapsed_time(e1) * 1e3 / args.iters
 
     tot_n = tot_m = 0.0
+    only = set(filter(None, args.only.split(",")))
+    if args.no_stem or only:
+        layers = [l for l in layer_shapes(args.batch, args.size) if not only or l[0] in only]
+        return _run_layers(args, layers, timeit, C, F, cl, dev)
     # stem: space-to-depth + 4x4 narrow-C MFMA conv vs MIOpen's 7x7/s2 on C=3
     xs = torch.randn(args.batch, 3, args.size, args.size, device=dev, dtype=torch.bfloat16).contiguous(
         memory_format=cl)
@@ -83,7 +89,12 @@ def main(argv=None) -> int:
     print(json.dumps({"layer": "stem.maxpool", "native_us": round(t_pool, 1),
                       "native_tbps": round((y0.numel() * 2 * 1.25) / t_pool / 1e6, 2)}), flush=True)
     tot_n += t_pool
-    for name, n, c, h, w, cout, ks, stride, pad, ba, pro, res in layer_shapes(args.batch, args.size):
+    return _run_layers(args, layer_shapes(args.batch, args.size), timeit, C, F, cl, dev, tot_n, tot_m)
+
+
+def _run_layers(args, layers, timeit, C, F, cl, dev, tot_n=0.0, tot_m=0.0) -> int:
+    import torch
+    for name, n, c, h, w, cout, ks, stride, pad, ba, pro, res in layers:
         x = torch.randn(n, c, h, w, device=dev, dtype=torch.bfloat16).contiguous(memory_format=cl)
         wt = (torch.randn(cout, c, ks, ks, device=dev) * (2 / (c * ks * ks)) ** 0.5).to(
             torch.bfloat16).contiguous(memory_format=cl)
