@@ -16,7 +16,9 @@ partially used together (leave whole GPUs free).
 """
 from __future__ import annotations
 
+import ctypes
 import itertools
+import os
 
 from .discovery import LINK_XGMI, Backend, Device
 
@@ -40,10 +42,51 @@ def score_set(idx: tuple[int, ...], devs: list[Device], links: list[list[int]], 
     return (xgmi_pairs, -hives, -numas, busy, tuple(-i for i in idx))
 
 
+_NATIVE = None
+
+
+def _native():
+    """vgpu_topo_preferred from libvgpu_smi.so (native/smi/topo.cpp), or None."""
+    global _NATIVE
+    if _NATIVE is None:
+        _NATIVE = False
+        if os.environ.get("VGPU_TOPO_NATIVE", "1") != "0":
+            from vgpu.native import lib_path
+            p = lib_path("libvgpu_smi.so")
+            if p.exists():
+                fn = ctypes.CDLL(str(p)).vgpu_topo_preferred
+                fn.restype = ctypes.c_int
+                _NATIVE = fn
+    return _NATIVE or None
+
+
 def preferred(available: list[int], must: list[int], size: int, devs: list[Device],
               links: list[list[int]], used: dict[int, int] | None = None, limit: int = 20000) -> list[int]:
     """Pick `size` device positions from `available` (positions into `devs`),
-    always including `must`.  Exhaustive for the ≤8-GPU node, capped otherwise."""
+    always including `must`.  Runs the native solver (native/smi/topo.cpp) when
+    libvgpu_smi is built; preferred_py below is its executable specification."""
+    fn = _native()
+    if fn is None:
+        return preferred_py(available, must, size, devs, links, used, limit)
+    used = used or {}
+    n = len(devs)
+    I = ctypes.c_int
+    arr = lambda xs: (I * max(1, len(xs)))(*xs)  # noqa: E731
+    flat = [links[a][b] for a in range(n) for b in range(n)]
+    out = (I * max(1, size + len(must) + len(available)))()
+    dense = lambda vals: [sorted(set(vals)).index(v) for v in vals]  # noqa: E731  (64-bit hive ids)
+    k = fn(I(n), arr(flat), arr(dense([d.numa for d in devs])), arr(dense([d.xgmi_hive for d in devs])),
+           arr([used.get(i, 0) for i in range(n)]), arr(list(available)), I(len(available)),
+           arr(list(must)), I(len(must)), I(size), ctypes.c_longlong(limit), out)
+    if k < 0:
+        raise ValueError("vgpu_topo_preferred: bad arguments")
+    return list(out[:k])
+
+
+def preferred_py(available: list[int], must: list[int], size: int, devs: list[Device],
+                 links: list[list[int]], used: dict[int, int] | None = None, limit: int = 20000) -> list[int]:
+    """Reference implementation of `preferred` (exhaustive for the ≤8-GPU node,
+    capped otherwise)."""
     used = used or {}
     must = [m for m in must if m in available]
     rest = [a for a in available if a not in must]
