@@ -446,7 +446,12 @@ __device__ __forceinline__ void epilogue_halves(const ConvArgs& a, f32x4_t (&acc
 // CSM = 16: a narrow-input conv (the ResNet stem after space-to-depth: C = 16,
 // 4x4 taps) — a 64-wide K step then spans 64/C taps, so each lane derives its
 // own tap from its chunk.
-template <int KS, int BM, int BN, bool PRO, bool RES, int CSM = 0>
+// NS = LDS stages: the DMA runs NS-1 K steps ahead of the MFMA.  With NS = 2
+// a step's DMA has one step of MFMA (~0.2 µs) to cover an HBM round trip
+// (≈1-2 µs), so every step waits; NS = 3 gives it two, and needs one barrier
+// per step (the barrier after the wait both publishes stage kt and retires
+// the reads of stage kt-1, which the next DMA overwrites).
+template <int KS, int BM, int BN, bool PRO, bool RES, int CSM = 0, int NS = 2>
 __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a) {
   static_assert(!PRO || KS == 1, "the in-register prologue needs a padding-free conv");
   static_assert(CSM == 0 || (!PRO && 64 % CSM == 0 && CSM % 8 == 0), "narrow-C variant");
@@ -456,7 +461,7 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int CS = BN + 4;
-  constexpr int PIPE = 2 * STAGE;
+  constexpr int PIPE = NS * STAGE;
   constexpr int HROWS = BM / 2, EPI = HROWS * CS * 4;  // epilogue staged in two row halves
   constexpr int BODY = PIPE > EPI ? PIPE : EPI;
   constexpr int PARAMS = PRO ? 2048 * 2 * 4 : 0;     // scale[C] then shift[C]
@@ -544,16 +549,33 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
   if constexpr (RES) {
     if (early_res) load_residual<BM, BN>(a, m0, n0, res);
   }
-  issue(0, 0);
+  if constexpr (NS == 2) {
+    issue(0, 0);
+  } else {
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p) issue(p < a.ktiles ? p : a.ktiles - 1, p);
+  }
   for (int kt = 0; kt < a.ktiles; ++kt) {
-    const int st = kt & 1;
-    if (kt + 1 < a.ktiles) {
-      issue(kt + 1, st ^ 1);
-      __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR + BR));
+    int st;
+    if constexpr (NS == 2) {
+      st = kt & 1;
+      if (kt + 1 < a.ktiles) {
+        issue(kt + 1, st ^ 1);
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR + BR));
+      } else {
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+      }
+      __builtin_amdgcn_s_barrier();
     } else {
-      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+      st = kt % NS;
+      // Steps kt .. kt+NS-2 are in flight; retire step kt.
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm((NS - 2) * (AR + BR)));
+      __builtin_amdgcn_s_barrier();
+      // Past the end the DMA re-fetches the last step into a stage nobody reads
+      // again (it is (kt-1) % NS): the loop stays branch-free around loads.
+      const int kn = kt + NS - 1;
+      issue(kn < a.ktiles ? kn : a.ktiles - 1, kn % NS);
     }
-    __builtin_amdgcn_s_barrier();
     const char* sA = smem + st * STAGE;
     const char* sB = sA + A_BYTES;
 #pragma unroll
@@ -589,7 +611,14 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    // Stage st fully read (this wave's ds_reads retired) before any wave refills it.
+    if constexpr (NS == 2) {
+      // Stage st fully read (this wave's ds_reads retired) before any wave refills it.
+      __builtin_amdgcn_s_waitcnt(kLgkm0);
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  if constexpr (NS > 2) {  // drain the dummy DMAs and all reads before the epilogue reuses LDS
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     __builtin_amdgcn_s_barrier();
   }
@@ -599,13 +628,32 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
   epilogue_halves<BM, BN, RES>(a, acc, m0, n0, smem, res);
 }
 
+int g_forced_stages = -1;  // vgpu_conv_set_stages (A/B benchmarking); -1 = env / default
+
+int glds_stages(int bm, int bn, int ktiles) {
+  if (g_forced_stages < 0) {
+    const char* v = getenv("VGPU_CONV_STAGES");
+    g_forced_stages = v ? atoi(v) : 0;
+  }
+  if (g_forced_stages == 2 || g_forced_stages == 3) return g_forced_stages;
+  // Default 2: on every ResNet-50 shape the 3-stage ring measured slower
+  // (profiles/conv_stages_r1.md) — the second block per CU already covers the
+  // DMA latency, and the third stage costs it LDS.
+  (void)bm; (void)bn; (void)ktiles;
+  return 2;
+}
+
 template <int KS, int BM, int BN, bool PRO, bool RES, int CSM = 0>
 hipError_t launch_glds(ConvArgs a, hipStream_t s) {
   a.nM = (a.M + BM - 1) / BM;
   a.nN = a.Cout / BN;
   a.nwg = a.nM * a.nN;
-  hipLaunchKernelGGL((conv_glds_kernel<KS, BM, BN, PRO, RES, CSM>), dim3(a.nwg), dim3(kThreads), 0, s,
-                     a);
+  if (!PRO && glds_stages(BM, BN, a.ktiles) == 3)
+    hipLaunchKernelGGL((conv_glds_kernel<KS, BM, BN, PRO, RES, CSM, 3>), dim3(a.nwg), dim3(kThreads),
+                       0, s, a);
+  else
+    hipLaunchKernelGGL((conv_glds_kernel<KS, BM, BN, PRO, RES, CSM, 2>), dim3(a.nwg), dim3(kThreads),
+                       0, s, a);
   return hipGetLastError();
 }
 
@@ -986,6 +1034,9 @@ VGPU_API int vgpu_stem_space_to_depth(const void* x, void* X, int N, int H, int 
                      static_cast<const uint16_t*>(x), static_cast<u32x4*>(X), N, H, W, HS, WS, pad);
   return (int)hipGetLastError();
 }
+
+// Benchmark knob: LDS stages of the DMA conv (2 or 3; 0 = default).
+VGPU_API void vgpu_conv_set_stages(int n) { g_forced_stages = n; }
 
 // Returns 0, a hipError_t, or -1 for an unsupported shape (checked before any launch).
 VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void* res,
