@@ -628,7 +628,8 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
   epilogue_halves<BM, BN, RES>(a, acc, m0, n0, smem, res);
 }
 
-int g_forced_stages = -1;  // vgpu_conv_set_stages (A/B benchmarking); -1 = env / default
+int g_forced_stages = -1;
+int g_forced_bm = 0;  // vgpu_conv_set_tile_m (A/B benchmarking); 0 = heuristic  // vgpu_conv_set_stages (A/B benchmarking); -1 = env / default
 
 int glds_stages(int bm, int bn, int ktiles) {
   if (g_forced_stages < 0) {
@@ -1037,6 +1038,8 @@ VGPU_API int vgpu_stem_space_to_depth(const void* x, void* X, int N, int H, int 
 
 // Benchmark knob: LDS stages of the DMA conv (2 or 3; 0 = default).
 VGPU_API void vgpu_conv_set_stages(int n) { g_forced_stages = n; }
+// Benchmark knob: force 64- or 128-row tiles (0 = heuristic).
+VGPU_API void vgpu_conv_set_tile_m(int bm) { g_forced_bm = bm; }
 
 // Returns 0, a hipError_t, or -1 for an unsupported shape (checked before any launch).
 VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void* res,
@@ -1084,7 +1087,13 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
     c.M = nb * a.OH * a.OW;
     // Small-M layers (late stages) use 64-row tiles so the grid still fills the chip.
     const int64_t tiles128 = (int64_t)((c.M + 127) / 128) * (Cout / bn);
-    const bool small = tiles128 < 512;
+    bool small = tiles128 < 512;
+    // Non-prologue 1x1 convs (conv3 + residual) are DMA/HBM-bound: 64-row tiles
+    // (48 KB LDS → 3 blocks per CU) beat 128-row tiles on every ResNet-50 shape
+    // (profiles/conv_tiles_r1.md).
+    if (!pro && KS == 1) small = true;
+    if (g_forced_bm == 64) small = true;
+    if (g_forced_bm == 128) small = false;
     hipError_t e;
     // LDS-DMA kernels for everything except a prologue on a padded conv
     // (padding must stay zero AFTER the prologue).

@@ -42,6 +42,8 @@ def main(argv=None) -> int:
     ap.add_argument("--no-miopen", action="store_true")
     ap.add_argument("--only", default="", help="comma-separated layer names (profiling)")
     ap.add_argument("--no-stem", action="store_true")
+    ap.add_argument("--ab-tile", action="store_true",
+                    help="per layer, interleaved: 64-row vs 128-row tiles")
     ap.add_argument("--ab-stages", action="store_true",
                     help="per layer, interleaved: 2-stage vs 3-stage LDS-DMA ring (in place of MIOpen)")
     args = ap.parse_args(argv)
@@ -121,6 +123,19 @@ def _run_layers(args, layers, timeit, C, F, cl, dev, tot_n=0.0, tot_m=0.0) -> in
             lib.vgpu_conv_set_stages(0)
             print(json.dumps({"layer": name, "stages2_us": round(t2, 1), "stages3_us": round(t3, 1)}),
                   flush=True)
+        if args.ab_tile:
+            from vgpu.native import load_kernels
+            lib = load_kernels()
+            run = lambda: C.conv2d(x, wt, bias, stride=stride, padding=pad,  # noqa: E731
+                                   act="relu" if ba else "none", pro=pp, residual=r, out=y)
+            t64 = t128 = 0.0
+            for _ in range(3):
+                lib.vgpu_conv_set_tile_m(64)
+                t64 += timeit(run) / 3
+                lib.vgpu_conv_set_tile_m(128)
+                t128 += timeit(run) / 3
+            lib.vgpu_conv_set_tile_m(0)
+            print(json.dumps({"layer": name, "bm64_us": round(t64, 1), "bm128_us": round(t128, 1)}), flush=True)
         t_mio = None if args.no_miopen else timeit(lambda: F.conv2d(x, wt, stride=stride, padding=pad))
         flop = 2.0 * n * oh * ow * cout * c * ks * ks
         in_bytes = x.numel() * 2 if (ks == 1 and stride == 1) or ks == 3 else n * oh * ow * c * 2
