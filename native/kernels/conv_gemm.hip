@@ -854,6 +854,191 @@ hipError_t dispatch_pro(const ConvArgs& a, bool res, hipStream_t s) {
   return res ? launch_pro<KS, BM, 64, true>(a, s) : launch_pro<KS, BM, 64, false>(a, s);
 }
 
+// ---- Fused bottleneck tail: conv2 (3x3, W→W, bias+ReLU) → conv3 (1x1, W→4W)
+// + residual, one kernel per row tile.
+//
+// The conv2 output tile (BM rows × all W channels) never leaves the CU: its
+// bias+ReLU'd bf16 values are written straight into LDS in the swizzled A-tile
+// layout and become conv3's A operand; conv3 then sweeps its 4W outputs in
+// 128-wide chunks whose weight panels are DMA'd into the (now idle) conv2
+// pipeline stages.  Per bottleneck this removes the write and the re-read of
+// the conv2 activation and one kernel boundary (stage 1 at b=50, 346²: 96 MB
+// of HBM traffic per block).  Numerics equal the unfused pair (the conv2
+// output is rounded to bf16 exactly where the unfused kernel stores it).
+//
+// Phase 1 is the LDS-DMA conv loop with the transposed MFMA (mfma(B, A)) so a
+// lane holds 4 consecutive conv2 channels of one row: one 8-byte ds_write per
+// 16×16 subtile lands them in the conv3 A image.
+template <int BM, int W>
+__global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, const ConvArgs b) {
+  constexpr int KCH = W / 64;                // conv3 K chunks (64 channels each)
+  constexpr int AR = BM / 32, BR = W / 32;   // phase-1 DMA instructions per thread per step
+  constexpr int WTM = BM / 2, WTN = W / 2;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int A_BYTES = BM * 128, B_BYTES = W * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int BN2 = 128, TN2 = 4;           // conv3 output chunk; 64 columns per wave
+  constexpr int B2_BYTES = BN2 * 128 * KCH;
+  constexpr int EPI = (BM / 2) * (BN2 + 4) * 4;
+  constexpr int P1 = 2 * STAGE, P2 = B2_BYTES + EPI;
+  constexpr int P = P1 > P2 ? P1 : P2;
+  constexpr int A2_BYTES = BM * 128 * KCH;
+  __shared__ __attribute__((aligned(16))) char smem[P + A2_BYTES];
+  char* sA2 = smem + P;
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int lrow = t >> 3, lchunk = (t & 7) ^ (lrow & 7);
+  int m0, n0;
+  tile_origin(a, blockIdx.x, BM, W, m0, n0);  // n0 == 0: one tile spans all of conv2's W outputs
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.x), 0, a.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.w), 0, (uint32_t)((int64_t)a.Cout * a.K * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t w3r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(b.w), 0, (uint32_t)((int64_t)b.Cout * b.K * 2), 0x00020000);
+
+  int abase[AR], aih[AR], aiw[AR];
+  bool aok[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int m = m0 + lrow + 32 * i;
+    aok[i] = m < a.M;
+    const int mm = aok[i] ? m : 0;
+    const int ow = mm % a.OW, t2 = mm / a.OW, oh = t2 % a.OH, n = t2 / a.OH;
+    aih[i] = oh * a.stride - a.pad;
+    aiw[i] = ow * a.stride - a.pad;
+    abase[i] = ((n * a.H + aih[i]) * a.W + aiw[i]) * a.C * 2;
+  }
+  const uint32_t boff = (uint32_t)((lrow * a.K + lchunk * 8) * 2);
+
+  auto issue = [&](int kt, int st) {
+    char* sA = smem + st * STAGE;
+    char* sB = sA + A_BYTES;
+    const int tap = kt / a.cblocks, cb = kt - tap * a.cblocks;
+    const int kh = tap / 3, kw = tap - kh * 3;
+    const int toff = ((kh * a.W + kw) * a.C + cb * BK + lchunk * 8) * 2;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int ih = aih[i] + kh, iw = aiw[i] + kw;
+      const bool v = aok[i] & ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          xr, (lds_void_t*)(sA + (32 * i + wave * 8) * 128), 16,
+          v ? (uint32_t)(abase[i] + toff) : kOOB, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          wr, (lds_void_t*)(sB + (32 * i + wave * 8) * 128), 16,
+          boff + (uint32_t)((32 * i * a.K + kt * BK) * 2), 0, 0, 0);
+  };
+
+  // ---- phase 1: conv2 --------------------------------------------------------------
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  issue(0, 0);
+  for (int kt = 0; kt < a.ktiles; ++kt) {
+    const int st = kt & 1;
+    if (kt + 1 < a.ktiles) {
+      issue(kt + 1, st ^ 1);
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR + BR));
+    } else {
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+    }
+    __builtin_amdgcn_s_barrier();
+    const char* sA = smem + st * STAGE;
+    const char* sB = sA + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8_t*>(sA + swz(wm * WTM + i * 16 + fr, kk * 4 + fk));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(wn * WTN + j * 16 + fr, kk * 4 + fk));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // conv2 bias + ReLU → bf16 → conv3's A image: lane (fr, fk) of subtile (i, j)
+  // holds row i*16+fr (+wave offset), channels j*16+fk*4 .. +3.
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int c = wn * WTN + j * 16 + fk * 4;
+    const float4 bb = *reinterpret_cast<const float4*>(a.bias + c);
+    const int panel = c >> 6, cc = c & 63;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int r = wm * WTM + i * 16 + fr;
+      const float v0 = fmaxf(acc[i][j][0] + bb.x, 0.f), v1 = fmaxf(acc[i][j][1] + bb.y, 0.f);
+      const float v2 = fmaxf(acc[i][j][2] + bb.z, 0.f), v3 = fmaxf(acc[i][j][3] + bb.w, 0.f);
+      *reinterpret_cast<uint2*>(sA2 + panel * (BM * 128) + swz(r, cc >> 3) + (cc & 7) * 2) =
+          uint2{pack2(v0, v1), pack2(v2, v3)};
+    }
+  }
+
+  // ---- phase 2: conv3 over 128-wide output chunks --------------------------------
+  constexpr int WTM2 = BM / 2, TM2 = WTM2 / 16;
+  char* sB2 = smem;
+  const int nchunks = b.Cout / BN2;
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int c0 = ch * BN2;
+#pragma unroll
+    for (int kc = 0; kc < KCH; ++kc)
+#pragma unroll
+      for (int i = 0; i < BN2 / 32; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            w3r, (lds_void_t*)(sB2 + kc * (BN2 * 128) + (32 * i + wave * 8) * 128), 16,
+            (uint32_t)(((c0 + lrow + 32 * i) * b.K + kc * 64 + lchunk * 8) * 2), 0, 0, 0);
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+    __syncthreads();  // B2 landed; A2 written (first chunk); previous chunk's staging read out
+    f32x4_t acc2[TM2][TN2];
+#pragma unroll
+    for (int i = 0; i < TM2; ++i)
+#pragma unroll
+      for (int j = 0; j < TN2; ++j) acc2[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < KCH; ++kc) {
+      const char* pA = sA2 + kc * (BM * 128);
+      const char* pB = sB2 + kc * (BN2 * 128);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8_t af[TM2], bfr[TN2];
+#pragma unroll
+        for (int i = 0; i < TM2; ++i)
+          af[i] = *reinterpret_cast<const bf16x8_t*>(pA + swz(wm * WTM2 + i * 16 + fr, kk * 4 + fk));
+#pragma unroll
+        for (int j = 0; j < TN2; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8_t*>(pB + swz(wn * 64 + j * 16 + fr, kk * 4 + fk));
+#pragma unroll
+        for (int i = 0; i < TM2; ++i)
+#pragma unroll
+          for (int j = 0; j < TN2; ++j)
+            acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc2[i][j], 0, 0, 0);
+      }
+    }
+    // B2 reads must finish before the next chunk's DMA overwrites the panel;
+    // the staging area of the epilogue does not overlap it.
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    __builtin_amdgcn_s_barrier();
+    u32x4 res[2][EpiShape<BM, BN2>::RROWS];
+    load_residual<BM, BN2>(b, m0, c0, res);
+    epilogue_halves<BM, BN2, true>(b, acc2, m0, c0, smem + B2_BYTES, res);
+  }
+}
+
 bool pro_dma_enabled() {
   static int on = -1;
   if (on < 0) {
@@ -1040,6 +1225,58 @@ VGPU_API int vgpu_stem_space_to_depth(const void* x, void* X, int N, int H, int 
 VGPU_API void vgpu_conv_set_stages(int n) { g_forced_stages = n; }
 // Benchmark knob: force 64- or 128-row tiles (0 = heuristic).
 VGPU_API void vgpu_conv_set_tile_m(int bm) { g_forced_bm = bm; }
+
+// Fused conv2 (3x3, pad 1, stride s, C = W → W, bias + ReLU) + conv3 (1x1,
+// W → 4W) + residual.  W ∈ {64, 128}.  Returns 0, a hipError_t, or -1.
+VGPU_API int vgpu_conv23_nhwc(const void* x, const void* w2, const float* b2, const void* w3,
+                              const void* res, void* y, int N, int H, int W, int C, int stride,
+                              hipStream_t s) {
+  if ((C != 64 && C != 128) || stride < 1 || N < 1 || !b2 || !res) return -1;
+  ConvArgs a{};
+  a.x = static_cast<const uint16_t*>(x);
+  a.w = static_cast<const uint16_t*>(w2);
+  a.bias = b2;
+  a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = C; a.stride = stride; a.pad = 1;
+  a.OH = (H + 2 - 3) / stride + 1;
+  a.OW = (W + 2 - 3) / stride + 1;
+  if (a.OH < 1 || a.OW < 1) return -1;
+  a.K = 9 * C;
+  a.cblocks = C / 64;
+  a.ktiles = a.K / 64;
+  a.act = 1;
+  ConvArgs b{};
+  b.w = static_cast<const uint16_t*>(w3);
+  b.y = static_cast<uint16_t*>(y);
+  b.res = static_cast<const uint16_t*>(res);
+  b.Cout = 4 * C;
+  b.K = C;
+  const int64_t xi = (int64_t)H * W * C * 2, yi = (int64_t)a.OH * a.OW * b.Cout * 2;
+  const int64_t lim = ((int64_t)1 << 31) - 1;
+  const int64_t per = lim / (xi > yi ? xi : yi);
+  if (per < 1) return -1;
+  for (int n0 = 0; n0 < N; n0 += (int)per) {
+    const int nb = (int)((N - n0) < per ? (N - n0) : per);
+    ConvArgs c = a, d = b;
+    c.N = nb;
+    c.x = a.x + (int64_t)n0 * (xi / 2);
+    c.x_bytes = (uint32_t)(nb * xi);
+    c.M = nb * a.OH * a.OW;
+    d.M = c.M;
+    d.y = b.y + (int64_t)n0 * (yi / 2);
+    d.res = b.res + (int64_t)n0 * (yi / 2);
+    d.y_bytes = (uint32_t)(nb * yi);
+    if (C == 64) {
+      c.nM = (c.M + 127) / 128; c.nN = 1; c.nwg = c.nM;
+      hipLaunchKernelGGL((conv23_kernel<128, 64>), dim3(c.nwg), dim3(kThreads), 0, s, c, d);
+    } else {
+      c.nM = (c.M + 63) / 64; c.nN = 1; c.nwg = c.nM;
+      hipLaunchKernelGGL((conv23_kernel<64, 128>), dim3(c.nwg), dim3(kThreads), 0, s, c, d);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return 0;
+}
 
 // Returns 0, a hipError_t, or -1 for an unsupported shape (checked before any launch).
 VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void* res,

@@ -131,3 +131,24 @@ def test_stem_space_to_depth_conv(C, hw):
     ref = torch.nn.functional.conv2d(x.float(), wt.float(), stride=2, padding=3)
     assert got.shape == ref.shape and got.is_contiguous(memory_format=CL)
     torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("case", [(2, 64, 19, 17, 1), (2, 128, 21, 19, 2), (3, 128, 9, 9, 1),
+                                  (4, 64, 64, 64, 1)])
+def test_conv23_matches_unfused(C, case):
+    n, c, h, w, stride = case
+    x = _t((n, c, h, w), 21)
+    w2 = _t((c, c, 3, 3), 22, scale=(2.0 / (9 * c)) ** 0.5)
+    b2 = _f((c,), 23)
+    w3 = _t((4 * c, c, 1, 1), 24, scale=(2.0 / c) ** 0.5)
+    oh, ow = C.out_hw(h, w, 3, stride, 1)
+    res = _t((n, 4 * c, oh, ow), 25)
+    got = C.conv23(x, w2, b2, w3, res, stride=stride)
+    h2 = C.conv2d_ref(x, w2, b2, stride=stride, padding=1, act="relu").to(torch.bfloat16)
+    ref = C.conv2d_ref(h2.contiguous(memory_format=CL), w3, residual=res)
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=CL)
+    torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
+    # and bit-for-bit against the unfused native pair
+    h2n = C.conv2d(x, w2, b2, stride=stride, padding=1, act="relu")
+    unf = C.conv2d(h2n, w3, residual=res)
+    torch.testing.assert_close(got, unf, atol=0, rtol=0)

@@ -42,6 +42,8 @@ def main(argv=None) -> int:
     ap.add_argument("--no-miopen", action="store_true")
     ap.add_argument("--only", default="", help="comma-separated layer names (profiling)")
     ap.add_argument("--no-stem", action="store_true")
+    ap.add_argument("--ab-tail", action="store_true",
+                    help="bottleneck tail conv2+conv3: fused kernel vs the two kernels (stages 1-2)")
     ap.add_argument("--ab-tile", action="store_true",
                     help="per layer, interleaved: 64-row vs 128-row tiles")
     ap.add_argument("--ab-stages", action="store_true",
@@ -68,6 +70,8 @@ def main(argv=None) -> int:
         return e0.elapsed_time(e1) * 1e3 / args.iters
 
     tot_n = tot_m = 0.0
+    if args.ab_tail:
+        return _ab_tail(args, timeit, C, cl, dev)
     only = set(filter(None, args.only.split(",")))
     if args.no_stem or only:
         layers = [l for l in layer_shapes(args.batch, args.size) if not only or l[0] in only]
@@ -94,6 +98,30 @@ def main(argv=None) -> int:
                       "native_tbps": round((y0.numel() * 2 * 1.25) / t_pool / 1e6, 2)}), flush=True)
     tot_n += t_pool
     return _run_layers(args, layer_shapes(args.batch, args.size), timeit, C, F, cl, dev, tot_n, tot_m)
+
+
+def _ab_tail(args, timeit, C, cl, dev) -> int:
+    import torch
+    h1 = ((args.size + 6 - 7) // 2 + 1 + 2 - 3) // 2 + 1
+    for name, c, h, stride in (("s1.tail", 64, h1, 1), ("s2b1.tail", 128, h1, 2),
+                               ("s2.tail", 128, (h1 - 1) // 2 + 1, 1)):
+        n = args.batch
+        x = torch.randn(n, c, h, h, device=dev, dtype=torch.bfloat16).contiguous(memory_format=cl)
+        w2 = (torch.randn(c, c, 3, 3, device=dev) * (2 / (9 * c)) ** 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+        b2 = torch.zeros(c, device=dev)
+        w3 = (torch.randn(4 * c, c, 1, 1, device=dev) * (2 / c) ** 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+        oh = (h - 1) // stride + 1
+        r = torch.randn(n, 4 * c, oh, oh, device=dev, dtype=torch.bfloat16).contiguous(memory_format=cl)
+        y = torch.empty_like(r)
+        two = lambda: C.conv2d(C.conv2d(x, w2, b2, stride=stride, padding=1, act="relu"), w3,  # noqa: E731
+                               residual=r, out=y)
+        one = lambda: C.conv23(x, w2, b2, w3, r, stride=stride, out=y)  # noqa: E731
+        tf = tu = 0.0
+        for _ in range(3):
+            tu += timeit(two) / 3
+            tf += timeit(one) / 3
+        print(json.dumps({"layer": name, "unfused_us": round(tu, 1), "fused_us": round(tf, 1)}), flush=True)
+    return 0
 
 
 def _run_layers(args, layers, timeit, C, F, cl, dev, tot_n=0.0, tot_m=0.0) -> int:

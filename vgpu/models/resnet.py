@@ -120,6 +120,9 @@ class FusedResNetV2Inference(nn.Module):
         if conv not in ("native", "miopen"):
             raise ValueError(conv)
         self.conv = conv
+        # conv2+conv3 fusion (VGPU_FUSE_TAIL=0 disables, for A/B)
+        import os
+        self.fuse_tail = os.environ.get("VGPU_FUSE_TAIL", "1") != "0"
         from vgpu.ops.fused import bn_scale_shift
         m = m.eval()
         dt = m.stem.weight.dtype
@@ -168,8 +171,12 @@ class FusedResNetV2Inference(nn.Module):
             else:
                 sc = C.conv2d(x, b["sc"][0], stride=b["sc"][1], pro=pro)
             h = C.conv2d(x, b["w1"], b["b1"], act="relu", pro=pro)
-            h = C.conv2d(h, b["w2"], b["b2"], stride=b["stride"], padding=1, act="relu")
-            x = C.conv2d(h, b["w3"], residual=sc)
+            if self.fuse_tail and C.conv23_supported(h.shape[1]):
+                # conv2 + conv3 + residual in one kernel (stages 1-2)
+                x = C.conv23(h, b["w2"], b["b2"], b["w3"], sc, stride=b["stride"])
+            else:
+                h = C.conv2d(h, b["w2"], b["b2"], stride=b["stride"], padding=1, act="relu")
+                x = C.conv2d(h, b["w3"], residual=sc)
         return self.fc(C.scale_shift_relu_mean(x, *self.out_ss))
 
     def _forward_miopen(self, x: torch.Tensor) -> torch.Tensor:

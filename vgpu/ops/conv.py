@@ -84,6 +84,39 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
     return out
 
 
+def conv23(x: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor, w3: torch.Tensor,
+           residual: torch.Tensor, *, stride: int = 1, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Fused bottleneck tail: y = conv1x1(relu(conv3x3(x, w2, stride, pad 1) + b2), w3) + residual.
+
+    x [N,W,H,Wd] with W ∈ {64, 128}; w2 [W,W,3,3]; b2 fp32 [W]; w3 [4W,W,1,1];
+    residual [N,4W,OH,OW].  The conv2 activation stays on-chip (native/kernels/conv_gemm.hip,
+    conv23_kernel); numerics equal conv2d(conv2d(...)) with the bf16 intermediate."""
+    _nhwc(x, "x")
+    _nhwc(w2, "w2")
+    _nhwc(w3, "w3")
+    _nhwc(residual, "residual")
+    n, c, h, wd = x.shape
+    if c not in (64, 128) or tuple(w2.shape) != (c, c, 3, 3) or tuple(w3.shape) != (4 * c, c, 1, 1):
+        raise ValueError(f"unsupported fused conv2+conv3: x {tuple(x.shape)} w2 {tuple(w2.shape)} "
+                         f"w3 {tuple(w3.shape)}")
+    if b2.dtype != torch.float32 or not b2.is_contiguous() or b2.numel() != c:
+        raise TypeError("b2 must be a contiguous fp32 tensor of size C")
+    oh, ow = out_hw(h, wd, 3, stride, 1)
+    if tuple(residual.shape) != (n, 4 * c, oh, ow):
+        raise ValueError("residual shape")
+    if out is None:
+        out = torch.empty((n, 4 * c, oh, ow), dtype=x.dtype, device=x.device, memory_format=_CL)
+    rc = load_kernels().vgpu_conv23_nhwc(_ptr(x), _ptr(w2), _ptr(b2), _ptr(w3), _ptr(residual), _ptr(out),
+                                         n, h, wd, c, stride, _stream())
+    if rc != 0:
+        raise RuntimeError(f"vgpu_conv23_nhwc: error {rc}")
+    return out
+
+
+def conv23_supported(c: int) -> bool:
+    return c in (64, 128)
+
+
 # ---- ResNet stem as a space-to-depth conv ------------------------------------------
 # conv7x7/s2/p3 over C=3 == conv4x4/s1/p0 over X = s2d(pad(x)) with C = 12 (→16):
 #   out[oh,ow] = Σ_{a,a',b,b',c} X[oh+a, ow+a', (b,b',c)] · W8[c, 2a+b, 2a'+b']
