@@ -142,6 +142,9 @@ static void apply_mask(hsa_queue_t* q, int dev, const AgentInfo& ai) {
   } else {
     VLOG_INFO("device %d queue %p: CU mask %s", dev, (void*)q,
               format_cu_mask(m, VGPU_CU_MASK_WORDS).c_str());
+    int n = 0;
+    for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) n += __builtin_popcountll(m[w]);
+    trace_emit(VGPU_EV_QUEUE, dev, (uint64_t)(uintptr_t)q, (uint64_t)n);
   }
 }
 

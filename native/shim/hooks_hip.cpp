@@ -243,7 +243,7 @@ __attribute__((visibility("default"))) hipError_t hipLaunchKernel(const void* f,
                                                                   void** args, size_t shmem,
                                                                   hipStream_t stream) {
   ensure_init();
-  limiter_on_launch(cur_dev(), blocks3(grid.x, grid.y, grid.z));
+  limiter_on_launch(cur_dev(), blocks3(grid.x, grid.y, grid.z), f);
   return REAL_HIP(hipLaunchKernel)(f, grid, block, args, shmem, stream);
 }
 
@@ -253,7 +253,7 @@ __attribute__((visibility("default"))) hipError_t hipExtLaunchKernel(const void*
                                                                      hipEvent_t start, hipEvent_t stop,
                                                                      int flags) {
   ensure_init();
-  limiter_on_launch(cur_dev(), blocks3(grid.x, grid.y, grid.z));
+  limiter_on_launch(cur_dev(), blocks3(grid.x, grid.y, grid.z), f);
   return REAL_HIP(hipExtLaunchKernel)(f, grid, block, args, shmem, stream, start, stop, flags);
 }
 
@@ -310,7 +310,7 @@ __attribute__((visibility("default"))) hipError_t hipLaunchCooperativeKernel(con
   ensure_init();
   hipError_t g = cooperative_guard(f, grid, block, shmem);
   if (g != hipSuccess) return g;
-  limiter_on_launch(cur_dev(), blocks3(grid.x, grid.y, grid.z));
+  limiter_on_launch(cur_dev(), blocks3(grid.x, grid.y, grid.z), f);
   return REAL_HIP(hipLaunchCooperativeKernel)(f, grid, block, params, shmem, stream);
 }
 
@@ -325,7 +325,7 @@ __attribute__((visibility("default"))) hipError_t hipModuleLaunchCooperativeKern
 __attribute__((visibility("default"))) hipError_t hipLaunchKernelExC(const hipLaunchConfig_t* cfg,
                                                                      const void* f, void** args) {
   ensure_init();
-  if (cfg) limiter_on_launch(cur_dev(), blocks3(cfg->gridDim.x, cfg->gridDim.y, cfg->gridDim.z));
+  if (cfg) limiter_on_launch(cur_dev(), blocks3(cfg->gridDim.x, cfg->gridDim.y, cfg->gridDim.z), f);
   return REAL_HIP(hipLaunchKernelExC)(cfg, f, args);
 }
 

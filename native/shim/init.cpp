@@ -69,6 +69,7 @@ static void atfork_child() {
     s.ledger.clear();
   }
   for (auto& t : s.dev_touched) t.store(0);
+  trace_after_fork();
 }
 
 static void do_init() {
@@ -95,6 +96,7 @@ static void do_init() {
     s.slot = region_claim_slot(s.region, s.pid, host_pid_of_self(), s.lim.priority);
     if (s.slot < 0) VLOG_ERR("no free process slot in the shared region");
   }
+  trace_open();
   install_signal(SIGUSR2, sig_suspend);
   install_signal(SIGUSR1, sig_resume);
   atexit(on_exit_release);
@@ -118,8 +120,10 @@ void suspend_gate() {
   if (__builtin_expect(!s.suspended.load(std::memory_order_relaxed), 1)) return;
   uint64_t t0 = mono_ns();
   while (s.suspended.load(std::memory_order_relaxed)) sleep_ns(1000000);  // 1 ms
+  const uint64_t waited = mono_ns() - t0;
   if (vgpu_proc_slot_t* sl = my_slot())
-    __atomic_fetch_add(&sl->throttle_wait_ns, mono_ns() - t0, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&sl->throttle_wait_ns, waited, __ATOMIC_RELAXED);
+  trace_emit(VGPU_EV_SUSPEND, -1, waited, 0);
 }
 
 }  // namespace vgpu

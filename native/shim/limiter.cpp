@@ -16,7 +16,10 @@
 // tracks the limit (multiplicative controller), rather than a fixed
 // SM²-proportional step.
 #include <dirent.h>
+#include <dlfcn.h>
 #include <math.h>
+
+#include <unordered_map>
 
 #include <thread>
 
@@ -220,19 +223,48 @@ static void priority_gate(vgpu_shared_region_t* r) {
   }
   uint64_t t0 = mono_ns();
   while (__atomic_load_n(&r->recent_kernel, __ATOMIC_RELAXED) < 0) sleep_ns(1000000);
+  const uint64_t waited = mono_ns() - t0;
   if (vgpu_proc_slot_t* sl = my_slot())
-    __atomic_fetch_add(&sl->throttle_wait_ns, mono_ns() - t0, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&sl->throttle_wait_ns, waited, __ATOMIC_RELAXED);
+  trace_emit(VGPU_EV_PRIORITY_BLOCK, -1, waited, 0);
   __atomic_store_n(&r->recent_kernel, 2, __ATOMIC_RELAXED);
 }
 
-void limiter_on_launch(int dev, uint64_t wg) {
+// Collective kernels (RCCL) are exempt from the temporal limiter: every rank's
+// kernel must be resident for a collective to progress, so throttling one
+// rank's launches stalls the others (distributed backend row;
+// §7.4 item 8).  A kernel is RCCL's when its host stub lives in librccl (or a
+// library matching VGPU_THROTTLE_EXEMPT).  Decided once per function pointer.
+static bool exempt_kernel(const void* fn) {
+  if (!fn) return false;
+  static std::mutex mu;
+  static std::unordered_map<const void*, bool> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(fn);
+  if (it != cache.end()) return it->second;
+  bool ex = false;
+  Dl_info di;
+  if (dladdr(fn, &di) && di.dli_fname) {
+    const char* extra = env_first("VGPU_THROTTLE_EXEMPT");
+    ex = strstr(di.dli_fname, "rccl") || strstr(di.dli_fname, "nccl") ||
+         (extra && *extra && strstr(di.dli_fname, extra));
+  }
+  cache.emplace(fn, ex);
+  return ex;
+}
+
+void limiter_on_launch(int dev, uint64_t wg, const void* fn) {
   State& s = st();
   if (!s.enabled) return;
   suspend_gate();
   vgpu_proc_slot_t* sl = my_slot();
   if (s.region) priority_gate(s.region);
   if (sl) __atomic_fetch_add(&sl->launches, 1, __ATOMIC_RELAXED);
-  if (__builtin_expect(!g_throttle_any.load(std::memory_order_relaxed), 1)) return;
+  const bool throttling = g_throttle_any.load(std::memory_order_relaxed) != 0;
+  if (__builtin_expect(!throttling && !trace_on(), 1)) return;
+  const bool exempt = throttling && exempt_kernel(fn);
+  trace_emit(VGPU_EV_LAUNCH, dev, wg, exempt ? 1 : 0);
+  if (!throttling || exempt) return;
   if (dev < 0 || dev >= VGPU_MAX_DEVICES) return;
   DevLimiter& L = g_lim[dev];
   if (!L.active) return;
@@ -255,7 +287,11 @@ void limiter_on_launch(int dev, uint64_t wg) {
     sleep_ns(500000);  // 0.5 ms
     cur = L.tokens.load(std::memory_order_relaxed);
   }
-  if (t0 && sl) __atomic_fetch_add(&sl->throttle_wait_ns, mono_ns() - t0, __ATOMIC_RELAXED);
+  if (t0) {
+    const uint64_t waited = mono_ns() - t0;
+    if (sl) __atomic_fetch_add(&sl->throttle_wait_ns, waited, __ATOMIC_RELAXED);
+    trace_emit(VGPU_EV_THROTTLE, dev, waited, wg);
+  }
 }
 
 }  // namespace vgpu

@@ -80,6 +80,7 @@ bool mem_reserve(int dev, uint64_t size, int kind) {
   else __atomic_fetch_add(&sl->oom_events, 1, __ATOMIC_RELAXED);
   region_unlock(s.region);
   if (!ok) {
+    trace_emit(VGPU_EV_OOM, dev, size, limit);
     VLOG_WARN("Device %d OOM %llu / %llu (request %llu bytes)", dev,
               (unsigned long long)(used + size), (unsigned long long)limit,
               (unsigned long long)size);
@@ -100,6 +101,7 @@ void mem_unreserve(int dev, uint64_t size, int kind) {
 
 void ledger_add(void* p, uint64_t size, int dev, int kind) {
   State& s = st();
+  trace_emit(VGPU_EV_ALLOC, dev, size, (uint64_t)kind);
   {
     std::lock_guard<std::mutex> g(s.ledger_mu);
     s.ledger[(uintptr_t)p] = Alloc{size, dev, kind};
@@ -115,6 +117,7 @@ bool ledger_take_if(void* p, int kind, Alloc* out) {
   if (it == s.ledger.end() || it->second.kind != kind) return false;
   *out = it->second;
   s.ledger.erase(it);
+  trace_emit(VGPU_EV_FREE, out->dev, out->size, (uint64_t)out->kind);
   return true;
 }
 
@@ -127,11 +130,14 @@ void mem_charge_nofail(int dev, uint64_t size, int kind) {
 
 bool ledger_take(void* p, Alloc* out) {
   State& s = st();
-  std::lock_guard<std::mutex> g(s.ledger_mu);
-  auto it = s.ledger.find((uintptr_t)p);
-  if (it == s.ledger.end()) return false;
-  *out = it->second;
-  s.ledger.erase(it);
+  {
+    std::lock_guard<std::mutex> g(s.ledger_mu);
+    auto it = s.ledger.find((uintptr_t)p);
+    if (it == s.ledger.end()) return false;
+    *out = it->second;
+    s.ledger.erase(it);
+  }
+  trace_emit(VGPU_EV_FREE, out->dev, out->size, (uint64_t)out->kind);
   return true;
 }
 

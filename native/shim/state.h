@@ -15,6 +15,7 @@
 #include <hsa/hsa.h>
 
 #include "region.h"
+#include "vgpu/trace.h"
 
 namespace vgpu {
 
@@ -81,7 +82,8 @@ void charge_context(int dev);         // first-touch context charge
 // Compute limiting ------------------------------------------------------------
 void limiter_start();
 // Called on every dispatch with the number of workgroups it launches.
-void limiter_on_launch(int dev, uint64_t workgroups);
+// `fn` = the kernel's host stub when known (RCCL kernels are exempt from throttling).
+void limiter_on_launch(int dev, uint64_t workgroups, const void* fn = nullptr);
 void suspend_gate();
 int cu_count_masked(int dev, int physical);
 
@@ -89,6 +91,12 @@ int cu_count_masked(int dev, int physical);
 void cumask_on_queue_created(void* agent_handle_ptr, void* queue);
 void cumask_on_queue_destroyed(void* queue);
 int cumask_reapply_all();
+
+// Event trace (trace.cpp; VGPU_TRACE=<dir>) -----------------------------------------
+void trace_open();
+void trace_after_fork();
+bool trace_on();
+void trace_emit(uint32_t type, int dev, uint64_t a, uint64_t b);
 
 extern thread_local int tl_device;
 // Non-zero while a HIP allocation hook is inside the real runtime call: the

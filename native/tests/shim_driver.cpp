@@ -259,15 +259,25 @@ int main(int argc, char** argv) {
     return 0;
   }
 
-  if (sc == "throttle") {
+  if (sc == "throttle" || sc == "throttle_rccl") {
     // Launch for `secs` seconds; report launches/s (temporal limiter tests).
+    // throttle_rccl launches a kernel whose host stub lives in an "rccl" library.
     double secs = argc > 2 ? atof(argv[2]) : 1.0;
     unsigned grid = argc > 3 ? (unsigned)atoi(argv[3]) : 256;
+    const void* fn = (const void*)&main;
+    if (sc == "throttle_rccl") {
+      void* h = dlopen("librccl_fake.so", RTLD_NOW);
+      fn = h ? dlsym(h, "rccl_fake_kernel_stub") : nullptr;
+      if (!fn) {
+        printf("error=no_rccl_fake\n");
+        return 1;
+      }
+    }
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     uint64_t n = 0;
     for (;;) {
-      hipLaunchKernel((const void*)&main, dim3(grid), dim3(256), nullptr, 0, nullptr);
+      hipLaunchKernel(fn, dim3(grid), dim3(256), nullptr, 0, nullptr);
       ++n;
       clock_gettime(CLOCK_MONOTONIC, &t1);
       double el = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);

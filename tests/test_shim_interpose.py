@@ -96,3 +96,35 @@ def test_smi_passthrough_without_limit(native_build, tmp_path):
     assert o["interposed"] == "1"
     assert int(o["rsmi_total"]) == 288 * GiB
     assert int(o["rsmi_used"]) == GiB           # fake's own number
+
+
+def test_event_trace_records_allocs_oom_and_launches(native_build, tmp_path):
+    from vgpu.monitor import trace
+    o = run("fill", GiB, env={"VGPU_DEVICE_MEMORY_LIMIT_0": "4g", "VGPU_TRACE": str(tmp_path)})
+    assert o["allocated"] == "4"
+    (f,) = list(tmp_path.glob("vgpu-trace-*.bin"))
+    h, ev = trace.read(str(f))
+    s = trace.summarize(ev)
+    assert s["events"]["alloc"] == 4 and s["events"]["free"] == 4 and s["events"]["oom"] == 1
+    assert s["alloc_bytes"] == s["free_bytes"] == 4 * GiB
+    assert s["events"].get("queue", 0) == 0  # no CU limit → no mask
+    assert all(a["t_ns"] <= b["t_ns"] for a, b in zip(ev, ev[1:]))
+
+
+def test_event_trace_launches_and_masked_queue(native_build, tmp_path):
+    from vgpu.monitor import trace
+    run("launch", 50, 1024, env={"VGPU_DEVICE_CU_LIMIT_0": "25", "VGPU_TRACE": str(tmp_path)})
+    (f,) = list(tmp_path.glob("vgpu-trace-*.bin"))
+    _, ev = trace.read(str(f))
+    s = trace.summarize(ev)
+    assert s["events"]["launch"] >= 50 and s["launch_workgroups"] >= 50 * 1024
+    q = [e for e in ev if e["type"] == "queue"]
+    assert q and q[0]["b"] == 64
+
+
+def test_event_trace_ring_wraps(native_build, tmp_path):
+    from vgpu.monitor import trace
+    run("launch", 500, 8, env={"VGPU_TRACE": str(tmp_path), "VGPU_TRACE_EVENTS": "64"})
+    (f,) = list(tmp_path.glob("vgpu-trace-*.bin"))
+    h, ev = trace.read(str(f))
+    assert h.head > 500 and len(ev) == 64

@@ -183,3 +183,16 @@ def test_temporal_limiter_throttles_when_forced(native_build, tmp_path):
     thr = run("throttle", 1.5, 64, env=base)
     n_free, n_thr = int(free["launches"]), int(thr["launches"])
     assert n_thr < n_free * 0.5, (n_free, n_thr)
+
+
+def test_rccl_kernels_exempt_from_temporal_limiter(native_build, tmp_path):
+    """Collective kernels must not be throttled (every rank's kernel has to be
+    resident for a collective to progress): a kernel stub from an rccl library
+    launches at the unthrottled rate while ordinary kernels are cut."""
+    util = tmp_path / "util"
+    util.write_text("0 100\n")
+    base = {"VGPU_DEVICE_CU_LIMIT_0": "25", "VGPU_FAKE_UTIL_FILE": str(util),
+            "GPU_CORE_UTILIZATION_POLICY": "force", "VGPU_LIMITER_TICK_MS": "5"}
+    thr = run("throttle", 1.0, 64, env=base)
+    rccl = run("throttle_rccl", 1.0, 64, env=base)
+    assert int(rccl["launches"]) > 3 * int(thr["launches"]), (rccl["launches"], thr["launches"])

@@ -205,6 +205,14 @@ def build_fakes(force: bool = False) -> dict[str, Path]:
             _mark(rsmi, [rsmi_src])
         res["rsmi"] = rsmi
 
+    rccl_src = NATIVE / "fakes" / "fake_rccl.cpp"
+    if rccl_src.exists():
+        rccl = FAKES_OUT / "librccl_fake.so"
+        if force or not _stamp(rccl, [rccl_src]):
+            _run([CXX, *COMMON, rccl_src, "-o", rccl, "-shared"])
+            _mark(rccl, [rccl_src])
+        res["rccl"] = rccl
+
     drv_src = NATIVE / "tests" / "shim_driver.cpp"
     drv = FAKES_OUT / "shim_driver"
     if force or not _stamp(drv, [drv_src, hip_src, hsa_src] + _headers()):
