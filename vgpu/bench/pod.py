@@ -56,6 +56,15 @@ def build(args):
             loss.backward()
             opt.step()
             return loss
+
+        def train_graph_body():
+            # Whole-step capture (forward, backward, optimizer): the gradients
+            # are allocated inside the graph's pool on capture and rewritten in
+            # place on every replay (PyTorch "whole network capture").
+            out = model(x)
+            loss = lossf(out.float(), target)
+            loss.backward()
+            opt.step()
     else:
         model.eval()
         from vgpu.models.resnet import FusedResNetV2Inference, ResNetV2
@@ -73,6 +82,27 @@ def build(args):
             return model(x)
 
     graph = None
+    if args.graph and w.train and getattr(args, "train_graph", True):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(3):  # MIOpen find + momentum buffers before capture
+                step()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        try:
+            graph = torch.cuda.CUDAGraph()
+            opt.zero_grad(set_to_none=True)
+            with torch.cuda.graph(graph):
+                train_graph_body()
+        except Exception as e:  # an op without capture support (e.g. some RNN paths): eager
+            sys.stderr.write(f"[pod {args.pod_index}] training hipGraph capture failed ({e}); eager\n")
+            torch.cuda.synchronize()
+            return w, step
+
+        def replay_train():
+            graph.replay()
+        return w, replay_train
     if args.graph and not w.train:
         # Warm up on a side stream, then capture one step into a hipGraph:
         # replays cost one launch instead of hundreds (launch-bound at b≤50).
@@ -124,6 +154,8 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--pod-index", type=int, default=0)
     ap.add_argument("--graph", action="store_true")
+    ap.add_argument("--no-train-graph", dest="train_graph", action="store_false",
+                    help="run training steps eagerly even with --graph")
     ap.add_argument("--find", action="store_true", help="cudnn.benchmark (MIOpen find) in warmup")
     ap.add_argument("--cap-probe", action="store_true")
     ap.add_argument("--no-fused", action="store_true", help="plain PyTorch epilogues (no HIP fusion)")
