@@ -1,0 +1,425 @@
+// Training-mode BatchNorm (+ ReLU / ReLU6) for NHWC bf16 activations on MI355X.
+//
+// Why: a ResNet-V2-50 training step (ai-benchmark 1.2, b=20 346²) spent 53% of
+// its steady-state GPU time in PyTorch's channels-last BatchNorm reductions
+// (batch_norm_collect_statistics + batch_norm_backward_reduce, ~110 µs each per
+// layer; profiles/rocprof_train_r1.md).  These kernels are bandwidth-shaped:
+//
+//   forward:  reduce  (shifted sums of x per channel, fp32 per block)
+//             finalize (fp64 merge of the block partials -> mean / invstd,
+//                      running-stat update, folded scale/shift)
+//             apply   y = act(x * s[c] + t[c])
+//   backward: reduce  (Σ dz, Σ dz·x̂ with dz = dy · act'(x * s + t))
+//             finalize (dβ, dγ, folded dx coefficients)
+//             apply   dx = s·dz + cc·x + b          (one pass, no dz tensor)
+//
+// The reduction grid is ≈2048 workgroups (8 per CU) of 256 threads; a thread
+// owns 8 channels (one 16-B load per row) and walks rows with 4 loads in
+// flight, all addresses clamped in range so the loop has no exec branches.
+// Variance uses sums shifted by the first row's value (one shift for every
+// block, so partials merge by plain addition) and an fp64 merge: no E[x²]-E[x]²
+// cancellation at 600k rows/channel.
+//
+// Parameters (γ, β, running stats, dγ, dβ) are fp32 or bf16 (a model cast with
+// .to(bfloat16)); the saved mean / invstd are always fp32.  Requires C % 8 == 0
+// and 16-B aligned tensors (checked on the host).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#define VGPU_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kUnroll = 4;           // rows in flight per thread
+constexpr int kMaxChunk = 512;       // channels per reduction workgroup
+constexpr int kTargetBlocks = 2048;  // reduction grid ≈ 8 workgroups per CU
+constexpr int kFinC = 16;            // finalize: channels per workgroup
+constexpr int kFinG = 32;            //           partial groups per workgroup
+constexpr int kMaxGrid = 256 * 8;
+
+struct alignas(16) bf16x8 {
+  uint16_t v[8];
+};
+
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+// Parameter access: P = float or uint16_t (bf16 bits); a null pointer reads as dflt.
+__device__ __forceinline__ float ldp(const float* p, int i, float dflt) { return p ? p[i] : dflt; }
+__device__ __forceinline__ float ldp(const uint16_t* p, int i, float dflt) { return p ? bf2f(p[i]) : dflt; }
+__device__ __forceinline__ void stp(float* p, int i, float v) { p[i] = v; }
+__device__ __forceinline__ void stp(uint16_t* p, int i, float v) { p[i] = f2bf(v); }
+
+template <int kAct>
+__device__ __forceinline__ float act_fwd(float z) {
+  if constexpr (kAct == 1) return fmaxf(z, 0.0f);
+  if constexpr (kAct == 2) return fminf(fmaxf(z, 0.0f), 6.0f);
+  return z;
+}
+
+// d act / dz as PyTorch defines it (threshold_backward / hardtanh_backward).
+template <int kAct>
+__device__ __forceinline__ float act_grad(float z) {
+  if constexpr (kAct == 1) return z > 0.0f ? 1.0f : 0.0f;
+  if constexpr (kAct == 2) return (z > 0.0f && z < 6.0f) ? 1.0f : 0.0f;
+  return 1.0f;
+}
+
+__device__ __forceinline__ void load8(const float* __restrict__ p, float (&o)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+  o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+
+// Per-channel reduction.  Grid (G, ceil(C / chunk)); a workgroup reduces
+// `rows_per_block` rows of one channel chunk into partial[blockIdx.x][c].
+//   kMode 0: (Σ (x - x₀), Σ (x - x₀)²)         x₀ = row 0 (the shift)
+//   kMode 1: (Σ dz, Σ dz · x̂)                   dz = dy · act'(x·s + t)
+template <int kMode, int kAct, typename P>
+__global__ void __launch_bounds__(kThreads) bn_reduce_kernel(
+    const bf16x8* __restrict__ x, const bf16x8* __restrict__ dy, const P* __restrict__ gamma,
+    const P* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ invstd,
+    float2* __restrict__ partial, int64_t M, int C, int chunk, int rows_per_block) {
+  __shared__ float2 red[kThreads * 8];
+  const int tpr = chunk >> 3;  // threads per row
+  const int rpb = kThreads / tpr;
+  const int tid = threadIdx.x;
+  const int cg = tid % tpr, ro = tid / tpr;
+  const int c0 = blockIdx.y * chunk + cg * 8;
+  const bool live = ro < rpb && c0 < C;
+  const int cvec = C >> 3;
+  const int cv = live ? c0 >> 3 : 0;
+
+  float k0[8], k1[8], k2[8], k3[8];
+  if constexpr (kMode == 0) {
+    const bf16x8 v = x[cv];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) k0[j] = bf2f(v.v[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = live ? c0 + j : 0;
+      const float is = invstd[c];
+      const float s = ldp(gamma, c, 1.0f) * is;
+      k0[j] = s;
+      k1[j] = ldp(beta, c, 0.0f) - mean[c] * s;
+      k2[j] = mean[c];
+      k3[j] = is;
+    }
+  }
+
+  float a1[8], a2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a1[j] = a2[j] = 0.0f;
+
+  const int64_t rbase = (int64_t)blockIdx.x * rows_per_block + ro;
+  for (int k = 0; k < rows_per_block; k += rpb * kUnroll) {
+    bf16x8 v[kUnroll], g[kUnroll];
+    float ok[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int64_t r = rbase + k + u * rpb;
+      const bool in = live & (r < M);
+      ok[u] = in ? 1.0f : 0.0f;
+      const int64_t idx = in ? r * cvec + cv : 0;  // clamped: always a valid address
+      v[u] = x[idx];
+      if constexpr (kMode == 1) g[u] = dy[idx];
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xf = bf2f(v[u].v[j]);
+        if constexpr (kMode == 0) {
+          const float d = (xf - k0[j]) * ok[u];
+          a1[j] += d;
+          a2[j] = fmaf(d, d, a2[j]);
+        } else {
+          const float dz = bf2f(g[u].v[j]) * act_grad<kAct>(fmaf(xf, k0[j], k1[j])) * ok[u];
+          a1[j] += dz;
+          a2[j] = fmaf(dz, (xf - k2[j]) * k3[j], a2[j]);
+        }
+      }
+    }
+  }
+
+  if (ro < rpb) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[ro * chunk + cg * 8 + j] = make_float2(a1[j], a2[j]);
+  }
+  __syncthreads();
+  for (int t = tid; t < chunk; t += kThreads) {
+    const int c = blockIdx.y * chunk + t;
+    if (c >= C) break;
+    float s1 = 0.0f, s2 = 0.0f;
+    for (int q = 0; q < rpb; ++q) {
+      const float2 p = red[q * chunk + t];
+      s1 += p.x;
+      s2 += p.y;
+    }
+    partial[(int64_t)blockIdx.x * C + c] = make_float2(s1, s2);
+  }
+}
+
+// fp64 merge of the G block partials of kFinC channels (kFinG groups of rows
+// summed in parallel, then across groups in LDS).  Valid in threads grp == 0.
+__device__ __forceinline__ void merge_partials(const float2* __restrict__ partial, int64_t G, int C,
+                                               int c, int cl, int grp, double& s1, double& s2) {
+  __shared__ double r1[kFinG][kFinC], r2[kFinG][kFinC];
+  s1 = 0.0;
+  s2 = 0.0;
+  if (c < C)
+    for (int64_t g = grp; g < G; g += kFinG) {
+      const float2 p = partial[g * C + c];
+      s1 += p.x;
+      s2 += p.y;
+    }
+  r1[grp][cl] = s1;
+  r2[grp][cl] = s2;
+  __syncthreads();
+  if (grp == 0)
+    for (int q = 1; q < kFinG; ++q) {
+      s1 += r1[q][cl];
+      s2 += r2[q][cl];
+    }
+}
+
+template <typename P>
+__global__ void __launch_bounds__(kFinC * kFinG) bn_fwd_finalize_kernel(
+    const float2* __restrict__ partial, int64_t G, const uint16_t* __restrict__ x,
+    const P* __restrict__ gamma, const P* __restrict__ beta, P* __restrict__ run_mean,
+    P* __restrict__ run_var, float* __restrict__ mean, float* __restrict__ invstd,
+    float* __restrict__ coef, int64_t M, int C, float eps, float momentum) {
+  const int cl = threadIdx.x % kFinC, grp = threadIdx.x / kFinC;
+  const int c = blockIdx.x * kFinC + cl;
+  double s1, s2;
+  merge_partials(partial, G, C, c, cl, grp, s1, s2);
+  if (grp != 0 || c >= C) return;
+  const double n = (double)M;
+  const double m1 = s1 / n;
+  double var = s2 / n - m1 * m1;
+  if (var < 0.0) var = 0.0;
+  const double mu = (double)bf2f(x[c]) + m1;
+  const float is = (float)(1.0 / sqrt(var + (double)eps));
+  mean[c] = (float)mu;
+  invstd[c] = is;
+  const float s = ldp(gamma, c, 1.0f) * is;
+  coef[c] = s;
+  coef[C + c] = ldp(beta, c, 0.0f) - (float)mu * s;
+  if (run_mean) {
+    const float unbiased = (float)(M > 1 ? var * n / (n - 1.0) : var);
+    stp(run_mean, c, (1.0f - momentum) * ldp(run_mean, c, 0.0f) + momentum * (float)mu);
+    stp(run_var, c, (1.0f - momentum) * ldp(run_var, c, 0.0f) + momentum * unbiased);
+  }
+}
+
+// dβ = Σ dz, dγ = Σ dz·x̂; dx = s·(dz - dβ/M - x̂·dγ/M) folded to s·dz + cc·x + b.
+template <typename P>
+__global__ void __launch_bounds__(kFinC * kFinG) bn_bwd_finalize_kernel(
+    const float2* __restrict__ partial, int64_t G, const P* __restrict__ gamma,
+    const P* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ invstd,
+    P* __restrict__ dgamma, P* __restrict__ dbeta, float* __restrict__ coef, int64_t M, int C) {
+  const int cl = threadIdx.x % kFinC, grp = threadIdx.x / kFinC;
+  const int c = blockIdx.x * kFinC + cl;
+  double s1, s2;
+  merge_partials(partial, G, C, c, cl, grp, s1, s2);
+  if (grp != 0 || c >= C) return;
+  const float db = (float)s1, dg = (float)s2;
+  if (dgamma) stp(dgamma, c, dg);
+  if (dbeta) stp(dbeta, c, db);
+  const float is = invstd[c], mu = mean[c];
+  const float s = ldp(gamma, c, 1.0f) * is;
+  const float inv_m = (float)(1.0 / (double)M);
+  const float cc = -s * is * dg * inv_m;
+  coef[c] = s;
+  coef[C + c] = ldp(beta, c, 0.0f) - mu * s;
+  coef[2 * C + c] = cc;
+  coef[3 * C + c] = -s * db * inv_m - mu * cc;
+}
+
+#define VGPU_BN_GRID_LOOP(i, ci, nvec, cvec)                                       \
+  const uint64_t stride_ = (uint64_t)gridDim.x * kThreads;                         \
+  const uint32_t cstep_ = (uint32_t)(stride_ % (cvec));                            \
+  uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;                      \
+  uint32_t ci = (uint32_t)(i % (cvec));                                            \
+  for (; i < (nvec); i += stride_, ci = (ci + cstep_ >= (cvec)) ? ci + cstep_ - (cvec) : ci + cstep_)
+
+template <int kAct>
+__global__ void __launch_bounds__(kThreads) bn_apply_kernel(const bf16x8* __restrict__ x,
+                                                            bf16x8* __restrict__ y,
+                                                            const float* __restrict__ coef,
+                                                            uint64_t nvec, uint32_t cvec) {
+  const float* sc = coef;
+  const float* sh = coef + cvec * 8;
+  VGPU_BN_GRID_LOOP(i, ci, nvec, cvec) {
+    const bf16x8 v = x[i];
+    float s[8], t[8];
+    load8(sc + ci * 8, s);
+    load8(sh + ci * 8, t);
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.v[k] = f2bf(act_fwd<kAct>(fmaf(bf2f(v.v[k]), s[k], t[k])));
+    y[i] = o;
+  }
+}
+
+template <int kAct>
+__global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const bf16x8* __restrict__ dy,
+                                                                const bf16x8* __restrict__ x,
+                                                                bf16x8* __restrict__ dx,
+                                                                const float* __restrict__ coef,
+                                                                uint64_t nvec, uint32_t cvec) {
+  const uint32_t C = cvec * 8;
+  VGPU_BN_GRID_LOOP(i, ci, nvec, cvec) {
+    const bf16x8 v = x[i];
+    const bf16x8 g = dy[i];
+    float s[8], t[8], cc[8], b[8];
+    load8(coef + ci * 8, s);
+    load8(coef + C + ci * 8, t);
+    load8(coef + 2 * C + ci * 8, cc);
+    load8(coef + 3 * C + ci * 8, b);
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float xf = bf2f(v.v[k]);
+      const float dz = bf2f(g.v[k]) * act_grad<kAct>(fmaf(xf, s[k], t[k]));
+      o.v[k] = f2bf(fmaf(s[k], dz, fmaf(cc[k], xf, b[k])));
+    }
+    dx[i] = o;
+  }
+}
+
+struct Plan {
+  int chunk, nchunks, rpb, rows_per_block;
+  int64_t G;
+};
+
+Plan make_plan(int64_t M, int C) {
+  Plan p;
+  p.chunk = C <= kMaxChunk ? C : kMaxChunk;
+  p.nchunks = (C + p.chunk - 1) / p.chunk;
+  p.rpb = kThreads / (p.chunk / 8);
+  int64_t target = kTargetBlocks / p.nchunks;
+  if (target < 1) target = 1;
+  int64_t iters = (M + p.rpb * target - 1) / (p.rpb * target);
+  iters = (iters + kUnroll - 1) / kUnroll * kUnroll;
+  p.rows_per_block = (int)(p.rpb * iters);
+  p.G = (M + p.rows_per_block - 1) / p.rows_per_block;
+  return p;
+}
+
+inline unsigned grid_for(uint64_t nvec) {
+  uint64_t g = (nvec + kThreads - 1) / kThreads;
+  if (g < 1) g = 1;
+  if (g > kMaxGrid) g = kMaxGrid;
+  return (unsigned)g;
+}
+
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+inline bool shape_ok(int64_t M, int C) { return M >= 1 && C >= 8 && C % 8 == 0 && M <= (int64_t)1 << 40; }
+
+template <typename P>
+int fwd_train(const void* x, void* y, const void* gamma, const void* beta, void* run_mean, void* run_var,
+              float* mean, float* invstd, float* ws, int64_t M, int C, float eps, float momentum, int act,
+              hipStream_t s) {
+  const Plan p = make_plan(M, C);
+  auto* partial = reinterpret_cast<float2*>(ws);
+  float* coef = ws + 2 * p.G * C;
+  const auto* xv = static_cast<const bf16x8*>(x);
+  hipLaunchKernelGGL((bn_reduce_kernel<0, 0, P>), dim3((unsigned)p.G, p.nchunks), dim3(kThreads), 0, s, xv,
+                     nullptr, nullptr, nullptr, nullptr, nullptr, partial, M, C, p.chunk, p.rows_per_block);
+  hipLaunchKernelGGL((bn_fwd_finalize_kernel<P>), dim3((C + kFinC - 1) / kFinC), dim3(kFinC * kFinG), 0, s,
+                     partial, p.G, static_cast<const uint16_t*>(x), static_cast<const P*>(gamma),
+                     static_cast<const P*>(beta), static_cast<P*>(run_mean), static_cast<P*>(run_var), mean,
+                     invstd, coef, M, C, eps, momentum);
+  const uint64_t nvec = (uint64_t)M * (C / 8);
+  auto* yv = static_cast<bf16x8*>(y);
+  switch (act) {
+    case 0: hipLaunchKernelGGL(bn_apply_kernel<0>, dim3(grid_for(nvec)), dim3(kThreads), 0, s, xv, yv, coef, nvec, C / 8); break;
+    case 1: hipLaunchKernelGGL(bn_apply_kernel<1>, dim3(grid_for(nvec)), dim3(kThreads), 0, s, xv, yv, coef, nvec, C / 8); break;
+    case 2: hipLaunchKernelGGL(bn_apply_kernel<2>, dim3(grid_for(nvec)), dim3(kThreads), 0, s, xv, yv, coef, nvec, C / 8); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+template <int kAct, typename P>
+void bwd_launch(const bf16x8* dyv, const bf16x8* xv, bf16x8* dxv, const P* gamma, const P* beta,
+                const float* mean, const float* invstd, P* dgamma, P* dbeta, float* ws, int64_t M, int C,
+                hipStream_t s) {
+  const Plan p = make_plan(M, C);
+  auto* partial = reinterpret_cast<float2*>(ws);
+  float* coef = ws + 2 * p.G * C;
+  hipLaunchKernelGGL((bn_reduce_kernel<1, kAct, P>), dim3((unsigned)p.G, p.nchunks), dim3(kThreads), 0, s,
+                     xv, dyv, gamma, beta, mean, invstd, partial, M, C, p.chunk, p.rows_per_block);
+  hipLaunchKernelGGL((bn_bwd_finalize_kernel<P>), dim3((C + kFinC - 1) / kFinC), dim3(kFinC * kFinG), 0, s,
+                     partial, p.G, gamma, beta, mean, invstd, dgamma, dbeta, coef, M, C);
+  const uint64_t nvec = (uint64_t)M * (C / 8);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<kAct>, dim3(grid_for(nvec)), dim3(kThreads), 0, s, dyv, xv, dxv,
+                     coef, nvec, C / 8);
+}
+
+template <typename P>
+int bwd(const void* dy, const void* x, void* dx, const void* gamma, const void* beta, const float* mean,
+        const float* invstd, void* dgamma, void* dbeta, float* ws, int64_t M, int C, int act, hipStream_t s) {
+  const auto* dyv = static_cast<const bf16x8*>(dy);
+  const auto* xv = static_cast<const bf16x8*>(x);
+  auto* dxv = static_cast<bf16x8*>(dx);
+  const auto* g = static_cast<const P*>(gamma);
+  const auto* b = static_cast<const P*>(beta);
+  auto* dg = static_cast<P*>(dgamma);
+  auto* db = static_cast<P*>(dbeta);
+  switch (act) {
+    case 0: bwd_launch<0, P>(dyv, xv, dxv, g, b, mean, invstd, dg, db, ws, M, C, s); break;
+    case 1: bwd_launch<1, P>(dyv, xv, dxv, g, b, mean, invstd, dg, db, ws, M, C, s); break;
+    case 2: bwd_launch<2, P>(dyv, xv, dxv, g, b, mean, invstd, dg, db, ws, M, C, s); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// fp32 workspace elements vgpu_bn_act_fwd_train / vgpu_bn_act_bwd need for
+// M = N·H·W rows of C channels (block partials + folded coefficients).
+VGPU_API int64_t vgpu_bn_workspace(int64_t M, int C) {
+  if (!shape_ok(M, C)) return -1;
+  return 2 * make_plan(M, C).G * C + 4 * (int64_t)C;
+}
+
+// y = act(batchnorm_train(x)); saves mean / invstd (fp32 [C]); updates the
+// running stats (unbiased variance, PyTorch momentum convention) when given.
+// gamma / beta / running stats: fp32, or bf16 when param_bf16; any may be null
+// (affine=False, track_running_stats=False).  act: 0 none, 1 relu, 2 relu6.
+VGPU_API int vgpu_bn_act_fwd_train(const void* x, void* y, const void* gamma, const void* beta, void* run_mean,
+                                   void* run_var, float* mean, float* invstd, float* ws, int64_t M, int C,
+                                   float eps, float momentum, int act, int param_bf16, void* stream) {
+  if (!shape_ok(M, C) || !aligned16(x) || !aligned16(y) || !aligned16(ws) || !mean || !invstd ||
+      (!run_mean) != (!run_var))
+    return (int)hipErrorInvalidValue;
+  auto s = (hipStream_t)stream;
+  if (param_bf16)
+    return fwd_train<uint16_t>(x, y, gamma, beta, run_mean, run_var, mean, invstd, ws, M, C, eps, momentum, act, s);
+  return fwd_train<float>(x, y, gamma, beta, run_mean, run_var, mean, invstd, ws, M, C, eps, momentum, act, s);
+}
+
+// dx, dgamma, dbeta of y = act(batchnorm_train(x)) given dy and the saved
+// mean / invstd.  dgamma / dbeta may be null.
+VGPU_API int vgpu_bn_act_bwd(const void* dy, const void* x, void* dx, const void* gamma, const void* beta,
+                             const float* mean, const float* invstd, void* dgamma, void* dbeta, float* ws,
+                             int64_t M, int C, int act, int param_bf16, void* stream) {
+  if (!shape_ok(M, C) || !aligned16(dy) || !aligned16(x) || !aligned16(dx) || !aligned16(ws) || !mean ||
+      !invstd)
+    return (int)hipErrorInvalidValue;
+  auto s = (hipStream_t)stream;
+  if (param_bf16) return bwd<uint16_t>(dy, x, dx, gamma, beta, mean, invstd, dgamma, dbeta, ws, M, C, act, s);
+  return bwd<float>(dy, x, dx, gamma, beta, mean, invstd, dgamma, dbeta, ws, M, C, act, s);
+}

@@ -22,7 +22,10 @@ def family(name: str) -> str:
     if m:
         ks, bm, bn, pro = m.groups()
         return f"vgpu conv_gemm {ks}x{ks} BM{bm} BN{bn}{' +prologue' if pro == '1' else ''}"
-    for key, fam in (("maxpool_kernel", "vgpu maxpool"), ("ssr_mean", "vgpu BN+ReLU+mean"),
+    for key, fam in (("bn_reduce_kernelILi0", "vgpu BN fwd reduce"), ("bn_reduce_kernelILi1", "vgpu BN bwd reduce"),
+                     ("bn_fwd_finalize", "vgpu BN finalize"), ("bn_bwd_finalize", "vgpu BN finalize"),
+                     ("bn_bwd_apply", "vgpu BN bwd apply"), ("bn_apply_kernel", "vgpu BN+act apply"),
+                     ("maxpool_kernel", "vgpu maxpool"), ("ssr_mean", "vgpu BN+ReLU+mean"),
                      ("add_scale_shift", "vgpu add+BN+ReLU"), ("bias_act", "vgpu bias+act"),
                      ("scale_shift_act", "vgpu BN+act"), ("igemm", "MIOpen igemm conv"),
                      ("kernel_grouped_conv", "MIOpen CK grouped conv"), ("Cijk", "hipBLASLt/Tensile GEMM"),
@@ -37,6 +40,7 @@ def main() -> int:
     ap.add_argument("dir")
     ap.add_argument("--tail", type=float, default=0.5)
     ap.add_argument("--step-dispatches", type=int, default=0, help="print the last N dispatches")
+    ap.add_argument("--last", type=int, default=0, help="aggregate only the last N dispatches")
     args = ap.parse_args()
     files = sorted(glob.glob(os.path.join(args.dir, "**", "*kernel_trace.csv"), recursive=True))
     for f in files:
@@ -44,7 +48,7 @@ def main() -> int:
         if not rows:
             continue
         rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-        tail = rows[int(len(rows) * (1 - args.tail)):]
+        tail = rows[-args.last:] if args.last else rows[int(len(rows) * (1 - args.tail)):]
         busy = collections.Counter()
         count = collections.Counter()
         for r in tail:

@@ -1,0 +1,133 @@
+"""Training-mode BatchNorm + activation (native/kernels/bn_nhwc.hip) against the
+plain-PyTorch fp32 reference: forward output, saved statistics / running-stat
+update, dx / dγ / dβ, hipGraph capture, and a whole ResNet-V2 training forward
+with the native path against the same model on PyTorch's BatchNorm."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last
+
+
+@pytest.fixture(scope="module")
+def B(gpu_build):
+    from vgpu.ops import bn
+    return bn
+
+
+def _x(shape, seed, offset=0.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(shape, generator=g) + offset).to(torch.bfloat16).cuda().contiguous(memory_format=CL)
+
+
+def _close_most(a, b, atol, rtol, frac=1e-4):
+    """allclose on all but `frac` of the elements (a ReLU mask may flip where
+    the pre-activation rounds to ±0 differently), and a bounded worst case."""
+    a, b = a.float(), b.float()
+    bad = ((a - b).abs() > atol + rtol * b.abs()).float().mean().item()
+    assert bad <= frac, f"{bad:.2e} of elements out of tolerance (max err {(a - b).abs().max().item():.3g})"
+
+
+CASES = [
+    # n, c, h, w, act, param dtype, input offset
+    (2, 64, 9, 11, "relu", torch.float32, 0.0),
+    (4, 256, 17, 13, "relu", torch.bfloat16, 0.0),
+    (1, 2048, 3, 3, "none", torch.float32, 0.0),
+    (3, 960, 5, 7, "relu6", torch.float32, 0.0),      # partial last channel chunk
+    (2, 96, 7, 7, "relu6", torch.bfloat16, 0.0),      # threads-per-row not a power of two
+    (20, 64, 87, 87, "relu", torch.float32, 0.0),     # ResNet-V2-50 b=20 stage-1 size
+    (8, 128, 33, 33, "relu", torch.float32, 50.0),    # large mean: shifted-sum variance
+]
+
+
+@pytest.mark.parametrize("n,c,h,w,act,pdt,off", CASES)
+def test_bn_act_train_matches_fp32_reference(B, n, c, h, w, act, pdt, off):
+    x = _x((n, c, h, w), 1, off)
+    g = torch.Generator(device="cpu").manual_seed(2)
+    weight = (torch.rand(c, generator=g) + 0.5).to(pdt).cuda()
+    bias = (torch.rand(c, generator=g) - 0.5).to(pdt).cuda()
+    rm = (torch.rand(c, generator=g) - 0.5).to(pdt).cuda()
+    rv = (torch.rand(c, generator=g) + 0.5).to(pdt).cuda()
+    rm_ref, rv_ref = rm.float().clone(), rv.float().clone()
+
+    w_n = weight.clone().requires_grad_()
+    b_n = bias.clone().requires_grad_()
+    x_n = x.clone().requires_grad_()
+    y = B._BNActFn.apply(x_n, w_n, b_n, rm, rv, 0.1, 1e-5, B.ACT[act])
+
+    x_r = x.float().requires_grad_()
+    w_r = weight.float().requires_grad_()
+    b_r = bias.float().requires_grad_()
+    y_r = B.bn_act_reference(x_r, w_r, b_r, rm_ref, rv_ref, 0.1, 1e-5, act)
+
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=CL)
+    _close_most(y, y_r, atol=3e-2, rtol=1e-2)
+    ptol = 1e-2 if pdt == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(rm.float(), rm_ref, atol=ptol, rtol=ptol)
+    torch.testing.assert_close(rv.float(), rv_ref, atol=ptol, rtol=ptol)
+
+    dy = _x((n, c, h, w), 3)
+    y.backward(dy)
+    y_r.backward(dy.float())
+    scale = x_r.grad.abs().max().item()
+    _close_most(x_n.grad, x_r.grad, atol=2e-2 * scale, rtol=2e-2)
+    # dγ, dβ are sums over N·H·W rows: compare against their own magnitude
+    for got, ref in ((w_n.grad, w_r.grad), (b_n.grad, b_r.grad)):
+        assert got.dtype == pdt
+        tol = (2e-2 if pdt == torch.bfloat16 else 2e-3) * ref.abs().max().item() + 1e-3
+        torch.testing.assert_close(got.float(), ref, atol=tol, rtol=2e-2)
+
+
+def test_bn_act_module_entry_updates_counters(B):
+    bn = torch.nn.BatchNorm2d(64).cuda().train()
+    x = _x((2, 64, 8, 8), 4)
+    ref = torch.nn.BatchNorm2d(64).cuda().train()
+    y = B.bn_act(x, bn, "relu")
+    y_r = torch.relu(ref(x.float()))
+    assert int(bn.num_batches_tracked) == 1
+    _close_most(y, y_r, atol=3e-2, rtol=1e-2)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(bn.running_var, ref.running_var, atol=1e-4, rtol=1e-4)
+    bn.eval()  # eval: running statistics via PyTorch
+    torch.testing.assert_close(B.bn_act(x, bn, "relu").float(), torch.relu(bn(x)).float())
+
+
+def test_bn_act_graph_capture_replays(B):
+    bn = torch.nn.BatchNorm2d(128).cuda().to(torch.bfloat16).train()
+    x = _x((4, 128, 16, 16), 5).requires_grad_()
+    dy = _x((4, 128, 16, 16), 6)
+
+    def body():
+        y = B.bn_act(x, bn, "relu")
+        y.backward(dy)
+        return y
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        body()
+    torch.cuda.current_stream().wait_stream(s)
+    x.grad = None
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        y_g = body()
+    graph.replay()
+    torch.cuda.synchronize()
+    gx = x.grad.clone()
+    x.grad = None
+    y_e = body()
+    torch.testing.assert_close(y_g, y_e)
+    torch.testing.assert_close(gx, x.grad)
+
+
+def test_resnet_training_forward_native_bn_matches_torch_bn(B, monkeypatch):
+    from vgpu.models.resnet import resnet_v2_50
+    torch.manual_seed(0)
+    m = resnet_v2_50().cuda().to(memory_format=CL).to(torch.bfloat16).train()
+    x = _x((4, 3, 96, 96), 7)
+    out_n = m(x).float()
+    monkeypatch.setattr(B, "native_eligible", lambda *a: False)
+    out_t = m(x).float()
+    cos = torch.nn.functional.cosine_similarity(out_n.flatten(), out_t.flatten(), dim=0).item()
+    assert cos > 0.99, cos

@@ -1,0 +1,40 @@
+"""Model definitions on the CPU: the BN+activation entry point keeps the
+module semantics off the native path, and every ai-benchmark workload builds
+and runs a (shrunken) forward/backward."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+
+def test_bn_act_cpu_fallback_matches_module():
+    from vgpu.ops.bn import bn_act, native_eligible
+    bn = torch.nn.BatchNorm2d(16).train()
+    ref = torch.nn.BatchNorm2d(16).train()
+    x = torch.randn(2, 16, 5, 5)
+    assert not native_eligible(x, bn)
+    for act, f in (("relu", F.relu), ("relu6", F.relu6), ("none", lambda t: t)):
+        torch.testing.assert_close(bn_act(x, bn, act), f(ref(x)))
+    torch.testing.assert_close(bn.running_mean, ref.running_mean)
+    assert int(bn.num_batches_tracked) == int(ref.num_batches_tracked) == 3
+    with pytest.raises(ValueError):
+        bn_act(x, bn, "gelu")
+
+
+def test_conv_bn_act_keeps_sequential_layout():
+    from vgpu.models.vision import _conv_bn
+    m = _conv_bn(8, 16, 3)
+    assert [k for k in m.state_dict()][:2] == ["0.weight", "1.weight"]
+    x = torch.randn(1, 8, 6, 6)
+    torch.testing.assert_close(m(x), F.relu6(m[1](m[0](x))))
+    m2 = _conv_bn(8, 16, 1, act=False).eval()
+    torch.testing.assert_close(m2(x), m2[1](m2[0](x)))
+
+
+def test_resnet_v2_training_step_cpu():
+    from vgpu.models.resnet import ResNetV2
+    m = ResNetV2([1, 1, 1, 1], num_classes=10).train()
+    x = torch.randn(2, 3, 64, 64)
+    loss = F.cross_entropy(m(x), torch.tensor([1, 2]))
+    loss.backward()
+    assert all(p.grad is not None for p in m.parameters())
+    assert int(m.blocks[0].bn_in.num_batches_tracked) == 1

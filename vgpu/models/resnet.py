@@ -15,6 +15,8 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
+from vgpu.ops.bn import bn_act
+
 
 class PreActBottleneck(nn.Module):
     expansion = 4
@@ -34,14 +36,14 @@ class PreActBottleneck(nn.Module):
         self.fused = False
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        pre = F.relu(self.bn_in(x))
+        pre = bn_act(x, self.bn_in)
         sc = self.shortcut(pre) if self.shortcut is not None else x
         if self.fused:
             y = F.relu(self.conv1(pre))
             y = F.relu(self.conv2(y))
         else:
-            y = F.relu(self.bn1(self.conv1(pre)))
-            y = F.relu(self.bn2(self.conv2(y)))
+            y = bn_act(self.conv1(pre), self.bn1)
+            y = bn_act(self.conv2(y), self.bn2)
         return self.conv3(y) + sc
 
 
@@ -81,7 +83,7 @@ class ResNetV2(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = self.pool(self.stem(x))
         x = self.blocks(x)
-        x = F.relu(self.bn_out(x))
+        x = bn_act(x, self.bn_out)
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)
 

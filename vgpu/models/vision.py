@@ -13,6 +13,8 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
+from vgpu.ops.bn import bn_act
+
 
 class VGG16(nn.Module):
     cfg = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512, "M"]
@@ -82,6 +84,14 @@ class NativeVGG16Inference(nn.Module):
         return self.classifier(torch.flatten(x, 1))
 
 
+class ConvBNAct(nn.Sequential):
+    """conv → BatchNorm → (ReLU6); the BN + activation pair runs as one native
+    training kernel pair (vgpu.ops.bn) on bf16 channels_last tensors."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return bn_act(self[0](x), self[1], "relu6" if len(self) > 2 else "none")
+
+
 def _conv_bn(cin: int, cout: int, k: int, stride: int = 1, groups: int = 1, dilation: int = 1,
              act: bool = True) -> nn.Sequential:
     pad = dilation * (k - 1) // 2
@@ -89,7 +99,7 @@ def _conv_bn(cin: int, cout: int, k: int, stride: int = 1, groups: int = 1, dila
                                        bias=False), nn.BatchNorm2d(cout)]
     if act:
         mods.append(nn.ReLU6(inplace=True))
-    return nn.Sequential(*mods)
+    return ConvBNAct(*mods)
 
 
 class InvertedResidual(nn.Module):

@@ -62,7 +62,12 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_conv2d_nhwc.argtypes = [vp, vp, vp, vp, vp, vp, vp] + [ci] * 9 + [vp]
     lib.vgpu_maxpool_nhwc.argtypes = [vp, vp] + [ci] * 7 + [vp]
     lib.vgpu_scale_shift_relu_mean_nhwc.argtypes = [vp, vp, vp, vp, ci, ci, ci, vp]
-    for f in ("vgpu_census", "vgpu_busy", "vgpu_gather_pages", "vgpu_scatter_pages",
+    i64, cf = ctypes.c_int64, ctypes.c_float
+    lib.vgpu_bn_workspace.argtypes = [i64, ci]
+    lib.vgpu_bn_workspace.restype = i64
+    lib.vgpu_bn_act_fwd_train.argtypes = [vp] * 9 + [i64, ci, cf, cf, ci, ci, vp]
+    lib.vgpu_bn_act_bwd.argtypes = [vp] * 10 + [i64, ci, ci, ci, vp]
+    for f in ("vgpu_bn_act_fwd_train", "vgpu_bn_act_bwd","vgpu_census", "vgpu_busy", "vgpu_gather_pages", "vgpu_scatter_pages",
               "vgpu_fill_pattern", "vgpu_verify_pattern", "vgpu_kernels_abi_version",
               "vgpu_bias_act_nhwc", "vgpu_scale_shift_act_nhwc", "vgpu_add_scale_shift_act_nhwc",
               "vgpu_conv2d_nhwc", "vgpu_maxpool_nhwc", "vgpu_scale_shift_relu_mean_nhwc"):
