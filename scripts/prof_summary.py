@@ -22,8 +22,10 @@ def family(name: str) -> str:
     if m:
         ks, bm, bn, pro = m.groups()
         return f"vgpu conv_gemm {ks}x{ks} BM{bm} BN{bn}{' +prologue' if pro == '1' else ''}"
-    for key, fam in (("bn_reduce_kernelILi0", "vgpu BN fwd reduce"), ("bn_reduce_kernelILi1", "vgpu BN bwd reduce"),
-                     ("bn_fwd_finalize", "vgpu BN finalize"), ("bn_bwd_finalize", "vgpu BN finalize"),
+    m = re.search(r"bn_reduce_kernel(?:ILi|<)(\d)", name)
+    if m:
+        return "vgpu BN " + ("fwd" if m.group(1) == "0" else "bwd") + " reduce"
+    for key, fam in (("bn_fwd_finalize", "vgpu BN finalize"), ("bn_bwd_finalize", "vgpu BN finalize"),
                      ("bn_bwd_apply", "vgpu BN bwd apply"), ("bn_apply_kernel", "vgpu BN+act apply"),
                      ("maxpool_kernel", "vgpu maxpool"), ("ssr_mean", "vgpu BN+ReLU+mean"),
                      ("add_scale_shift", "vgpu add+BN+ReLU"), ("bias_act", "vgpu bias+act"),
@@ -41,6 +43,8 @@ def main() -> int:
     ap.add_argument("--tail", type=float, default=0.5)
     ap.add_argument("--step-dispatches", type=int, default=0, help="print the last N dispatches")
     ap.add_argument("--last", type=int, default=0, help="aggregate only the last N dispatches")
+    ap.add_argument("--last-ms", type=float, default=0.0,
+                    help="aggregate only dispatches starting in the last T ms of the trace (steady state)")
     args = ap.parse_args()
     files = sorted(glob.glob(os.path.join(args.dir, "**", "*kernel_trace.csv"), recursive=True))
     for f in files:
@@ -49,6 +53,9 @@ def main() -> int:
             continue
         rows.sort(key=lambda r: int(r["Start_Timestamp"]))
         tail = rows[-args.last:] if args.last else rows[int(len(rows) * (1 - args.tail)):]
+        if args.last_ms:
+            t_end = int(rows[-1]["End_Timestamp"])
+            tail = [r for r in rows if int(r["Start_Timestamp"]) >= t_end - args.last_ms * 1e6]
         busy = collections.Counter()
         count = collections.Counter()
         for r in tail:

@@ -118,3 +118,22 @@ def test_pathmonitor_discovery_gc_and_metrics(native_build, tmp_path, monkeypatc
     ra.close()
     rb.close()
     srv.stop()
+
+
+def test_dashboard_queries_exported_series():
+    """docs/gpu-dashboard.json is generated (scripts/gen_dashboard.py) and only
+    queries series the scheduler / monitor collectors export."""
+    import json
+    import pathlib
+    import re
+    import runpy
+    root = pathlib.Path(__file__).resolve().parents[1]
+    gen = runpy.run_path(str(root / "scripts" / "gen_dashboard.py"))
+    assert json.loads((root / "docs" / "gpu-dashboard.json").read_text()) == gen["dashboard"]()
+    src = (root / "vgpu" / "monitor" / "metrics.py").read_text() + (root / "vgpu" / "scheduler" / "metrics.py").read_text()
+    exported = set(re.findall(r'MetricFamily\(\s*"([A-Za-z_]+)"', src))
+    for p in gen["dashboard"]()["panels"]:
+        for t in p["targets"]:
+            names = set(re.findall(r"[A-Za-z_][A-Za-z_]+", t["expr"])) - {"sum", "by", "rate", "increase", "m",
+                                                                        "nodeid", "deviceidx"}
+            assert names and names <= exported, (t["expr"], names - exported)

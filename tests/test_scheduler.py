@@ -390,3 +390,32 @@ def test_http_routes_and_metrics(api):
     assert 'GPUDeviceSharedNum{deviceidx=' in text and "vGPUPodsDeviceAllocated" in text
     assert "nodeGPUOverview" in text
     http.shutdown()
+
+
+def test_every_example_pod_schedules_on_an_mi355x_node():
+    """examples/*.yaml: each request form the docs show is accepted by the
+    request parser and finds a placement on an 8 x MI355X node (SPX, two NUMA
+    nodes, one xGMI hive), a node whose GPUs run in CPX mode, or a node whose
+    plugin registers 1.5x HBM (deviceMemoryScaling > 1: virtual device memory)."""
+    import copy
+    import os
+    import yaml
+    ex = os.path.join(os.path.dirname(__file__), "..", "examples")
+    spx = usage(8, numa=[0, 0, 0, 0, 1, 1, 1, 1], hive="h0")
+    cpx = usage(8, mem=MIB_288G // 8)
+    for d in cpx:
+        d.type = "AMD-MI355X-CPX"
+    placed = {}
+    for f in sorted(os.listdir(ex)):
+        for p in yaml.safe_load_all(open(os.path.join(ex, f))):
+            reqs = resource_reqs(p)
+            assert any(reqs), f
+            annos = p["metadata"].get("annotations") or {}
+            nodes = {"spx": NodeUsage(copy.deepcopy(spx)), "cpx": NodeUsage(copy.deepcopy(cpx)),
+                     "vmem": NodeUsage(usage(8, mem=MIB_288G * 3 // 2))}
+            best = pick_node(calc_score(nodes, reqs, annos))
+            assert best is not None, f
+            placed[f] = best.node_id
+    assert placed["compute-partition.yaml"] == "cpx"
+    assert placed["specify-card-type-not-use.yaml"] != "cpx"
+    assert placed["virtual-memory.yaml"] == "vmem"
