@@ -13,7 +13,7 @@
 //             finalize (dβ, dγ, folded dx coefficients)
 //             apply   dx = s·dz + cc·x + b          (one pass, no dz tensor)
 //
-// The reduction grid is ≈2048 workgroups (8 per CU) of 256 threads; a thread
+// The reduction grid is ≈1024 workgroups (4 per CU) of 256 threads; a thread
 // owns 8 channels (one 16-B load per row) and walks rows with 4 loads in
 // flight, all addresses clamped in range so the loop has no exec branches.
 // Variance uses sums shifted by the first row's value (one shift for every
@@ -34,9 +34,9 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kUnroll = 4;           // rows in flight per thread
 constexpr int kMaxChunk = 512;       // channels per reduction workgroup
-constexpr int kTargetBlocks = 2048;  // reduction grid ≈ 8 workgroups per CU
-constexpr int kFinC = 16;            // finalize: channels per workgroup
-constexpr int kFinG = 32;            //           partial groups per workgroup
+constexpr int kTargetBlocks = 1024;  // reduction grid ≈ 4 workgroups per CU
+constexpr int kFinC = 8;             // finalize: channels per workgroup
+constexpr int kFinG = 64;            //           partial groups per workgroup (tree-merged)
 constexpr int kMaxGrid = 256 * 8;
 
 struct alignas(16) bf16x8 {
@@ -168,27 +168,33 @@ __global__ void __launch_bounds__(kThreads) bn_reduce_kernel(
   }
 }
 
-// fp64 merge of the G block partials of kFinC channels (kFinG groups of rows
-// summed in parallel, then across groups in LDS).  Valid in threads grp == 0.
+// fp64 merge of the G block partials of kFinC channels: kFinG groups of
+// partials summed in parallel, then a log2(kFinG)-step tree in LDS (a serial
+// merge here made the finalize a 10 µs latency chain).  Valid in grp == 0.
 __device__ __forceinline__ void merge_partials(const float2* __restrict__ partial, int64_t G, int C,
                                                int c, int cl, int grp, double& s1, double& s2) {
   __shared__ double r1[kFinG][kFinC], r2[kFinG][kFinC];
   s1 = 0.0;
   s2 = 0.0;
-  if (c < C)
+  if (c < C) {
+#pragma unroll 4
     for (int64_t g = grp; g < G; g += kFinG) {
       const float2 p = partial[g * C + c];
       s1 += p.x;
       s2 += p.y;
     }
+  }
   r1[grp][cl] = s1;
   r2[grp][cl] = s2;
   __syncthreads();
-  if (grp == 0)
-    for (int q = 1; q < kFinG; ++q) {
-      s1 += r1[q][cl];
-      s2 += r2[q][cl];
+#pragma unroll
+  for (int h = kFinG / 2; h > 0; h >>= 1) {
+    if (grp < h) {
+      r1[grp][cl] = s1 = s1 + r1[grp + h][cl];
+      r2[grp][cl] = s2 = s2 + r2[grp + h][cl];
     }
+    __syncthreads();
+  }
 }
 
 template <typename P>

@@ -121,13 +121,50 @@ def test_bn_act_graph_capture_replays(B):
     torch.testing.assert_close(gx, x.grad)
 
 
-def test_resnet_training_forward_native_bn_matches_torch_bn(B, monkeypatch):
-    from vgpu.models.resnet import resnet_v2_50
+def test_resnet_training_step_native_matches_pytorch(B, monkeypatch):
+    """ResNet-V2 training forward + backward (one bottleneck per stage, so bf16
+    gradients stay well above rounding noise; at 50 layers and random init both
+    bf16 paths are ~95% off fp32 for most tensors) with native BN and convs
+    against an fp32 copy of the same model: logits, and every parameter
+    gradient no further from fp32 than PyTorch's own bf16 path (BN + MIOpen)."""
+    import copy
+    from vgpu.models.resnet import ResNetV2
+    from vgpu.ops import conv as C
     torch.manual_seed(0)
-    m = resnet_v2_50().cuda().to(memory_format=CL).to(torch.bfloat16).train()
+    m32 = ResNetV2([1, 1, 1, 1]).cuda().to(memory_format=CL).train()
+    m = copy.deepcopy(m32).to(torch.bfloat16)
     x = _x((4, 3, 96, 96), 7)
-    out_n = m(x).float()
+    tgt = torch.arange(4, device="cuda")
+
+    def run(model, inp):
+        model.zero_grad(set_to_none=True)
+        out = model(inp).float()
+        torch.nn.functional.cross_entropy(out, tgt).backward()
+        return out.detach(), {k: p.grad.detach().float().clone() for k, p in model.named_parameters()}
+
+    out_n, g_n = run(m, x)
+    out_f, g_f = run(m32, x.float())
     monkeypatch.setattr(B, "native_eligible", lambda *a: False)
-    out_t = m(x).float()
-    cos = torch.nn.functional.cosine_similarity(out_n.flatten(), out_t.flatten(), dim=0).item()
-    assert cos > 0.99, cos
+    monkeypatch.setattr(C, "train_eligible", lambda *a: False)
+    out_t, g_t = run(m, x)
+    cos = lambda a, b: torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()  # noqa: E731
+    assert cos(out_n, out_f) > 0.99 and cos(out_t, out_f) > 0.99
+    # Early-layer BN gradients are sums with heavy cancellation: in bf16 both
+    # paths sit far from fp32 there (cosine 0.3-0.7 for PyTorch's own path), so
+    # compare error norms against PyTorch's, and demand tight agreement only
+    # where PyTorch's bf16 gradient is itself well conditioned.
+    bad, rows = [], []
+    for k in g_f:
+        nf = g_f[k].norm()
+        if nf == 0:
+            continue
+        en, et = ((g_n[k] - g_f[k]).norm() / nf).item(), ((g_t[k] - g_f[k]).norm() / nf).item()
+        cn, ct = cos(g_n[k], g_f[k]), cos(g_t[k], g_f[k])
+        rows.append((k, round(en, 3), round(et, 3)))
+        if en > 1.5 * et + 0.02 or (ct > 0.99 and cn < 0.98):
+            bad.append((k, round(en, 3), round(et, 3), round(cn, 3), round(ct, 3)))
+    en_all = sorted(r[1] for r in rows)
+    et_all = sorted(r[2] for r in rows)
+    print("median rel err native %.3f pytorch %.3f; max native %.3f pytorch %.3f"
+          % (en_all[len(en_all) // 2], et_all[len(et_all) // 2], en_all[-1], et_all[-1]))
+    assert not bad, bad

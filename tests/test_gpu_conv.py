@@ -152,3 +152,38 @@ def test_conv23_matches_unfused(C, case):
     h2n = C.conv2d(x, w2, b2, stride=stride, padding=1, act="relu")
     unf = C.conv2d(h2n, w3, residual=res)
     torch.testing.assert_close(got, unf, atol=0, rtol=0)
+
+
+TRAIN_CASES = [
+    # n, c, h, w, cout, ks, stride, pad, residual
+    (2, 64, 12, 10, 256, 1, 1, 0, True),     # conv3 + residual
+    (2, 256, 12, 10, 64, 1, 1, 0, False),    # conv1
+    (2, 64, 12, 10, 64, 3, 1, 1, False),     # conv2
+    (2, 128, 12, 10, 128, 3, 2, 1, False),   # strided conv2: MIOpen gradients
+    (2, 256, 12, 10, 512, 1, 2, 0, False),   # projection shortcut
+]
+
+
+@pytest.mark.parametrize("n,c,h,w,cout,ks,stride,pad,res", TRAIN_CASES)
+def test_conv_train_fwd_bwd_matches_fp32(C, n, c, h, w, cout, ks, stride, pad, res):
+    conv = torch.nn.Conv2d(c, cout, ks, stride=stride, padding=pad, bias=False).cuda().to(torch.bfloat16)
+    conv = conv.to(memory_format=CL)
+    assert C.train_eligible(_t((n, c, h, w), 1), conv)
+    x = _t((n, c, h, w), 1).requires_grad_()
+    oh, ow = C.out_hw(h, w, ks, stride, pad)
+    r = _t((n, cout, oh, ow), 2).requires_grad_() if res else None
+    y = C.conv_train(x, conv, residual=r)
+    xr = x.detach().float().requires_grad_()
+    wr = conv.weight.detach().float().requires_grad_()
+    rr = r.detach().float().requires_grad_() if res else None
+    yr = torch.nn.functional.conv2d(xr, wr, stride=stride, padding=pad)
+    if res:
+        yr = yr + rr
+    assert y.is_contiguous(memory_format=CL)
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
+    dy = _t((n, cout, oh, ow), 3)
+    y.backward(dy)
+    yr.backward(dy.float())
+    for got, ref in ((x.grad, xr.grad), (conv.weight.grad, wr.grad)) + (((r.grad, rr.grad),) if res else ()):
+        scale = ref.abs().max().item()
+        torch.testing.assert_close(got.float(), ref, atol=2e-2 * scale, rtol=2e-2)

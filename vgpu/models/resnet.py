@@ -16,6 +16,7 @@ from torch import nn
 import torch.nn.functional as F
 
 from vgpu.ops.bn import bn_act
+from vgpu.ops.conv import conv_train
 
 
 class PreActBottleneck(nn.Module):
@@ -37,14 +38,17 @@ class PreActBottleneck(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         pre = bn_act(x, self.bn_in)
-        sc = self.shortcut(pre) if self.shortcut is not None else x
         if self.fused:
+            sc = self.shortcut(pre) if self.shortcut is not None else x
             y = F.relu(self.conv1(pre))
             y = F.relu(self.conv2(y))
-        else:
-            y = bn_act(self.conv1(pre), self.bn1)
-            y = bn_act(self.conv2(y), self.bn2)
-        return self.conv3(y) + sc
+            return self.conv3(y) + sc
+        # training / unfused: MFMA convs (residual add in conv3's epilogue) and
+        # native BN+ReLU on bf16 channels_last CUDA tensors, PyTorch elsewhere
+        sc = conv_train(pre, self.shortcut) if self.shortcut is not None else x
+        y = bn_act(conv_train(pre, self.conv1), self.bn1)
+        y = bn_act(conv_train(y, self.conv2), self.bn2)
+        return conv_train(y, self.conv3, residual=sc)
 
 
 def _fold_bn(conv: nn.Conv2d, bn: nn.BatchNorm2d) -> nn.Conv2d:

@@ -12,6 +12,7 @@ shapes raise, a missing extension raises NativeMissing.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.nn.functional as F
@@ -191,6 +192,69 @@ def scale_shift_relu_mean(x: torch.Tensor, scale: torch.Tensor, shift: torch.Ten
     if rc != 0:
         raise RuntimeError(f"vgpu_scale_shift_relu_mean_nhwc: error {rc}")
     return out
+
+
+# ---- training: native forward / data gradient, MIOpen weight gradient -------------------
+# VGPU_NATIVE_CONV_TRAIN=0 keeps every training convolution on MIOpen (A/B).
+_TRAIN_NATIVE = os.environ.get("VGPU_NATIVE_CONV_TRAIN", "1") != "0"
+
+
+class _ConvTrainFn(torch.autograd.Function):
+    """y = conv(x, w) (+ residual) on the MFMA kernel; backward: dx on the same
+    kernel (stride 1: the data gradient is a stride-1 convolution of dy with the
+    transposed, spatially flipped filter and padding k-1-p), dw from MIOpen.
+    Per-layer timings that motivated the split: profiles/convtrain_r1.md."""
+
+    @staticmethod
+    def forward(ctx, x, w, residual, stride: int, padding: int):
+        y = conv2d(x, w, stride=stride, padding=padding, residual=residual)
+        ctx.save_for_backward(x, w)
+        ctx.stride, ctx.padding = stride, padding
+        ctx.has_res = residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=_CL)
+        s, p = ctx.stride, ctx.padding
+        need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        common = ([0], [s, s], [p, p], [1, 1], False, [0, 0], 1)
+        bw = torch.ops.aten.convolution_backward
+        dx = dw = None
+        if s == 1:
+            if need_dx:
+                ks = w.shape[2]
+                wt = w.transpose(0, 1)
+                if ks > 1:
+                    wt = wt.flip(2, 3)
+                dx = conv2d(dy, wt.contiguous(memory_format=_CL), stride=1, padding=ks - 1 - p)
+            if need_dw:
+                dw = bw(dy, x, w, *common, [False, True, False])[1]
+        elif need_dx or need_dw:
+            dx, dw, _ = bw(dy, x, w, *common, [need_dx, need_dw, False])
+        dres = dy if ctx.has_res and ctx.needs_input_grad[2] else None
+        return dx, dw, dres, None, None
+
+
+def train_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
+    w = conv.weight
+    return (_TRAIN_NATIVE and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and x.dim() == 4 and x.is_contiguous(memory_format=_CL) and w.is_contiguous(memory_format=_CL)
+            and conv.bias is None and conv.groups == 1 and conv.dilation == (1, 1)
+            and conv.kernel_size[0] == conv.kernel_size[1] and conv.stride[0] == conv.stride[1]
+            and conv.padding[0] == conv.padding[1] and isinstance(conv.padding[0], int)
+            and supported(conv.in_channels, conv.out_channels, conv.kernel_size[0])
+            and conv.kernel_size[0] in (1, 3))
+
+
+def conv_train(x: torch.Tensor, conv: torch.nn.Conv2d, residual: torch.Tensor | None = None) -> torch.Tensor:
+    """conv(x) (+ residual) with the module's semantics; bf16 channels_last CUDA
+    tensors of supported shapes run natively, anything else through the module."""
+    if not train_eligible(x, conv) or (residual is not None and not residual.is_contiguous(memory_format=_CL)):
+        y = conv(x)
+        return y if residual is None else y + residual
+    return _ConvTrainFn.apply(x, conv.weight, residual, conv.stride[0], conv.padding[0])
 
 
 # ---- fp32 references -----------------------------------------------------------------
