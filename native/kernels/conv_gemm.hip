@@ -352,6 +352,46 @@ constexpr int vmcnt_imm(int n) {  // s_waitcnt vmcnt(n), expcnt/lgkmcnt untouche
   return (n & 15) | (((n >> 4) & 3) << 14) | (7 << 4) | (15 << 8);
 }
 constexpr int kLgkm0 = 15 | (3 << 14) | (7 << 4);  // s_waitcnt lgkmcnt(0) only
+constexpr int lgkm_imm(int n) { return kLgkm0 | ((n & 15) << 8); }  // s_waitcnt lgkmcnt(n) only
+
+// One 64-wide K step of a wave's TM x TN grid of 16x16 sub-tiles from a
+// swizzled LDS stage (rows of 128 B): fragment reads software-pipelined — the
+// second 32-wide half's ds_reads are issued behind the wait for the first half
+// and land while the first half multiplies.  (With LDS DMA in flight hipcc only
+// emits full lgkmcnt drains, so the overlap comes from issue order.)
+// SWAP: acc += B·A (transposed output tile, conv23's first GEMM).
+template <int TM, int TN, bool SWAP = false>
+__device__ __forceinline__ void mma_k64(const char* sA, const char* sB, int arow, int brow, int fr, int fk,
+                                        f32x4_t (&acc)[TM][TN]) {
+  bf16x8_t af[2][TM], bfr[2][TN];
+  auto rd = [&](int kk) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+      af[kk][i] = *reinterpret_cast<const bf16x8_t*>(sA + swz(arow + i * 16 + fr, kk * 4 + fk));
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      bfr[kk][j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(brow + j * 16 + fr, kk * 4 + fk));
+  };
+  auto mm = [&](int kk) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = SWAP ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[kk][j], af[kk][i], acc[i][j], 0, 0, 0)
+                         : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+  };
+  rd(0);
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(kLgkm0);
+  __builtin_amdgcn_sched_barrier(0);
+  rd(1);
+  __builtin_amdgcn_sched_barrier(0);
+  mm(0);
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(kLgkm0);
+  __builtin_amdgcn_sched_barrier(0);
+  mm(1);
+}
 
 // Epilogue, one row half at a time: accumulators → LDS (fp32) → 16-B
 // coalesced bias + residual + act + store.  The residual loads of a half
@@ -952,22 +992,7 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
     }
     __builtin_amdgcn_s_barrier();
     const char* sA = smem + st * STAGE;
-    const char* sB = sA + A_BYTES;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8_t af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8_t*>(sA + swz(wm * WTM + i * 16 + fr, kk * 4 + fk));
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(wn * WTN + j * 16 + fr, kk * 4 + fk));
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    }
+    mma_k64<TM, TN, true>(sA, sA + A_BYTES, wm * WTM, wn * WTN, fr, fk, acc);
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     __builtin_amdgcn_s_barrier();
   }
@@ -1013,21 +1038,7 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
     for (int kc = 0; kc < KCH; ++kc) {
       const char* pA = sA2 + kc * (BM * 128);
       const char* pB = sB2 + kc * (BN2 * 128);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8_t af[TM2], bfr[TN2];
-#pragma unroll
-        for (int i = 0; i < TM2; ++i)
-          af[i] = *reinterpret_cast<const bf16x8_t*>(pA + swz(wm * WTM2 + i * 16 + fr, kk * 4 + fk));
-#pragma unroll
-        for (int j = 0; j < TN2; ++j)
-          bfr[j] = *reinterpret_cast<const bf16x8_t*>(pB + swz(wn * 64 + j * 16 + fr, kk * 4 + fk));
-#pragma unroll
-        for (int i = 0; i < TM2; ++i)
-#pragma unroll
-          for (int j = 0; j < TN2; ++j)
-            acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc2[i][j], 0, 0, 0);
-      }
+      mma_k64<TM2, TN2>(pA, pB, wm * WTM2, wn * 64, fr, fk, acc2);
     }
     // B2 reads must finish before the next chunk's DMA overwrites the panel;
     // the staging area of the epilogue does not overlap it.
