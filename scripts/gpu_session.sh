@@ -19,7 +19,13 @@ step() {  # step <name> <seconds> <cmd...>
 }
 ok_or_testfail() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 n=0
-IFS=, read -ra STAGES <<< "${1:-tests,smoke,bench,conv,prof}"
+# Stages are comma-separated; an argument containing newlines is split on
+# newlines instead (custom commands that need commas of their own).
+if [[ "${1:-}" == *$'\n'* ]]; then
+  mapfile -t STAGES <<< "$1"
+else
+  IFS=, read -ra STAGES <<< "${1:-tests,smoke,bench,conv,prof}"
+fi
 for s in "${STAGES[@]}"; do
   case $s in
     tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider
