@@ -247,11 +247,70 @@ hipError_t hipLaunchKernelExC(const hipLaunchConfig_t* c, const void*, void**) {
   count_launch((uint64_t)c->gridDim.x * c->gridDim.y * c->gridDim.z);
   return hipSuccess;
 }
+// Minimal graphs: a graph is a list of kernel nodes (grid sizes) and child
+// graphs, enough for the shim's node walk; an exec remembers its graph.
+struct FakeNode {
+  hipGraphNodeType type;
+  dim3 grid;
+  hipGraph_t child;
+};
+struct FakeGraph {
+  std::vector<FakeNode*> nodes;
+};
+hipError_t hipGraphGetNodes(hipGraph_t g, hipGraphNode_t* nodes, size_t* n) {
+  auto* fg = reinterpret_cast<FakeGraph*>(g);
+  if (!fg || !n) return hipErrorInvalidValue;
+  if (nodes)
+    for (size_t i = 0; i < *n && i < fg->nodes.size(); ++i) nodes[i] = reinterpret_cast<hipGraphNode_t>(fg->nodes[i]);
+  *n = fg->nodes.size();
+  return hipSuccess;
+}
+hipError_t hipGraphNodeGetType(hipGraphNode_t node, hipGraphNodeType* t) {
+  *t = reinterpret_cast<FakeNode*>(node)->type;
+  return hipSuccess;
+}
+hipError_t hipGraphKernelNodeGetParams(hipGraphNode_t node, hipKernelNodeParams* p) {
+  auto* fn = reinterpret_cast<FakeNode*>(node);
+  if (fn->type != hipGraphNodeTypeKernel) return hipErrorInvalidValue;
+  *p = hipKernelNodeParams{};
+  p->gridDim = fn->grid;
+  p->blockDim = dim3(256, 1, 1);
+  return hipSuccess;
+}
+hipError_t hipGraphChildGraphNodeGetGraph(hipGraphNode_t node, hipGraph_t* g) {
+  *g = reinterpret_cast<FakeNode*>(node)->child;
+  return hipSuccess;
+}
+hipError_t hipGraphInstantiateWithFlags(hipGraphExec_t* e, hipGraph_t g, unsigned long long) {
+  *e = reinterpret_cast<hipGraphExec_t>(new hipGraph_t(g));
+  return hipSuccess;
+}
+hipError_t hipGraphInstantiate(hipGraphExec_t* e, hipGraph_t g, hipGraphNode_t*, char*, size_t) {
+  return hipGraphInstantiateWithFlags(e, g, 0);
+}
+hipError_t hipGraphExecDestroy(hipGraphExec_t e) {
+  delete reinterpret_cast<hipGraph_t*>(e);
+  return hipSuccess;
+}
 hipError_t hipGraphLaunch(hipGraphExec_t, hipStream_t) {
   init();
   g_graph_launches.fetch_add(1);
   g_launches.fetch_add(1);
   return hipSuccess;
+}
+// Test helper: a graph of kernel nodes with grids (grids[i], 2, 1) plus, when
+// child_grid > 0, one child graph holding a kernel node of grid child_grid.
+hipGraph_t fake_hip_graph_create(const unsigned* grids, int n, unsigned child_grid) {
+  auto* g = new FakeGraph;
+  for (int i = 0; i < n; ++i) g->nodes.push_back(new FakeNode{hipGraphNodeTypeKernel, dim3(grids[i], 2, 1), nullptr});
+  if (child_grid) {
+    auto* c = new FakeGraph;
+    c->nodes.push_back(new FakeNode{hipGraphNodeTypeKernel, dim3(child_grid, 1, 1), nullptr});
+    g->nodes.push_back(new FakeNode{hipGraphNodeTypeGraph, dim3(1, 1, 1), reinterpret_cast<hipGraph_t>(c)});
+  }
+  // a memcpy-like node the walk must ignore
+  g->nodes.push_back(new FakeNode{hipGraphNodeTypeMemset, dim3(99999, 1, 1), nullptr});
+  return reinterpret_cast<hipGraph_t>(g);
 }
 hipError_t hipGetProcAddress(const char* sym, void** pfn, int, uint64_t,
                              hipDriverProcAddressQueryResult* st) {

@@ -11,6 +11,9 @@
 // Every hook: (1) lazily initialises, (2) passes straight through when
 // control is disabled, (3) keeps the fast path to a couple of relaxed atomics.
 #include <algorithm>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
 
 #include "common.h"
 #include "real.h"
@@ -30,6 +33,53 @@ struct InHipAlloc {
 
 inline uint64_t blocks3(unsigned x, unsigned y, unsigned z) {
   return (uint64_t)(x ? x : 1) * (y ? y : 1) * (z ? z : 1);
+}
+
+// Workgroups per launch of each executable graph (kernel nodes, recursively).
+std::mutex g_graph_mu;
+std::unordered_map<const void*, uint64_t> g_graph_wg;
+
+uint64_t graph_workgroups(hipGraph_t g, int depth) {
+  auto get_nodes = REAL_HIP(hipGraphGetNodes);
+  auto get_type = REAL_HIP(hipGraphNodeGetType);
+  auto get_kernel = REAL_HIP(hipGraphKernelNodeGetParams);
+  auto get_child = REAL_HIP(hipGraphChildGraphNodeGetGraph);
+  if (!g || depth > 8 || !get_nodes || !get_type || !get_kernel) return 0;
+  size_t n = 0;
+  if (get_nodes(g, nullptr, &n) != hipSuccess || n == 0) return 0;
+  std::vector<hipGraphNode_t> nodes(n);
+  if (get_nodes(g, nodes.data(), &n) != hipSuccess) return 0;
+  uint64_t wg = 0;
+  for (size_t i = 0; i < n; ++i) {
+    hipGraphNodeType t;
+    if (get_type(nodes[i], &t) != hipSuccess) continue;
+    if (t == hipGraphNodeTypeKernel) {
+      hipKernelNodeParams kp{};
+      if (get_kernel(nodes[i], &kp) == hipSuccess) wg += blocks3(kp.gridDim.x, kp.gridDim.y, kp.gridDim.z);
+    } else if (t == hipGraphNodeTypeGraph && get_child) {
+      hipGraph_t child = nullptr;
+      if (get_child(nodes[i], &child) == hipSuccess) wg += graph_workgroups(child, depth + 1);
+    }
+  }
+  return wg;
+}
+
+void graph_exec_record(hipGraphExec_t exec, hipGraph_t graph) {
+  if (!exec || !st().enabled) return;
+  const uint64_t wg = graph_workgroups(graph, 0);
+  std::lock_guard<std::mutex> l(g_graph_mu);
+  g_graph_wg[exec] = wg;
+}
+
+void graph_exec_forget(hipGraphExec_t exec) {
+  std::lock_guard<std::mutex> l(g_graph_mu);
+  g_graph_wg.erase(exec);
+}
+
+uint64_t graph_exec_workgroups(hipGraphExec_t exec) {
+  std::lock_guard<std::mutex> l(g_graph_mu);
+  auto it = g_graph_wg.find(exec);
+  return it == g_graph_wg.end() ? 0 : it->second;
 }
 
 // Shared allocation path: reserve → real alloc → record (or unreserve).
@@ -329,14 +379,52 @@ __attribute__((visibility("default"))) hipError_t hipLaunchKernelExC(const hipLa
   return REAL_HIP(hipLaunchKernelExC)(cfg, f, args);
 }
 
+// Graphs: a hipGraphLaunch bypasses every per-kernel hook, so each executable
+// graph is charged the workgroups of all its kernel nodes (child graphs
+// included), counted once when it is instantiated — the reference charges
+// `grids` per cuLaunchKernel and has no graph path.
+// Graphs the walk cannot see (instantiated before the shim, or updated in
+// place) fall back to VGPU_GRAPH_LAUNCH_TOKENS.
 __attribute__((visibility("default"))) hipError_t hipGraphLaunch(hipGraphExec_t exec, hipStream_t stream) {
   ensure_init();
-  static uint64_t graph_tokens = [] {
+  static uint64_t fallback_tokens = [] {
     const char* v = getenv("VGPU_GRAPH_LAUNCH_TOKENS");
     return v ? strtoull(v, nullptr, 10) : 4096ull;
   }();
-  limiter_on_launch(cur_dev(), graph_tokens);
+  uint64_t wg = graph_exec_workgroups(exec);
+  limiter_on_launch(cur_dev(), wg ? wg : fallback_tokens);
   return REAL_HIP(hipGraphLaunch)(exec, stream);
+}
+
+__attribute__((visibility("default"))) hipError_t hipGraphInstantiate(hipGraphExec_t* pExec, hipGraph_t graph,
+                                                                      hipGraphNode_t* pErrorNode,
+                                                                      char* pLogBuffer, size_t bufferSize) {
+  ensure_init();
+  hipError_t rc = REAL_HIP(hipGraphInstantiate)(pExec, graph, pErrorNode, pLogBuffer, bufferSize);
+  if (rc == hipSuccess && pExec) graph_exec_record(*pExec, graph);
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipGraphInstantiateWithFlags(hipGraphExec_t* pExec,
+                                                                               hipGraph_t graph,
+                                                                               unsigned long long flags) {
+  ensure_init();
+  hipError_t rc = REAL_HIP(hipGraphInstantiateWithFlags)(pExec, graph, flags);
+  if (rc == hipSuccess && pExec) graph_exec_record(*pExec, graph);
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipGraphInstantiateWithParams(
+    hipGraphExec_t* pExec, hipGraph_t graph, hipGraphInstantiateParams* params) {
+  ensure_init();
+  hipError_t rc = REAL_HIP(hipGraphInstantiateWithParams)(pExec, graph, params);
+  if (rc == hipSuccess && pExec) graph_exec_record(*pExec, graph);
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipGraphExecDestroy(hipGraphExec_t exec) {
+  graph_exec_forget(exec);
+  return REAL_HIP(hipGraphExecDestroy)(exec);
 }
 
 // hipGetProcAddress must hand out our hooks too, or a runtime-resolved call

@@ -74,6 +74,14 @@ using hipModuleLaunchCooperativeKernel = hipError_t (*)(hipFunction_t, unsigned 
                                                         void**);
 using hipLaunchKernelExC = hipError_t (*)(const hipLaunchConfig_t*, const void*, void**);
 using hipGraphLaunch = hipError_t (*)(hipGraphExec_t, hipStream_t);
+using hipGraphInstantiate = hipError_t (*)(hipGraphExec_t*, hipGraph_t, hipGraphNode_t*, char*, size_t);
+using hipGraphInstantiateWithFlags = hipError_t (*)(hipGraphExec_t*, hipGraph_t, unsigned long long);
+using hipGraphInstantiateWithParams = hipError_t (*)(hipGraphExec_t*, hipGraph_t, hipGraphInstantiateParams*);
+using hipGraphExecDestroy = hipError_t (*)(hipGraphExec_t);
+using hipGraphGetNodes = hipError_t (*)(hipGraph_t, hipGraphNode_t*, size_t*);
+using hipGraphNodeGetType = hipError_t (*)(hipGraphNode_t, hipGraphNodeType*);
+using hipGraphKernelNodeGetParams = hipError_t (*)(hipGraphNode_t, hipKernelNodeParams*);
+using hipGraphChildGraphNodeGetGraph = hipError_t (*)(hipGraphNode_t, hipGraph_t*);
 using hipOccupancyMaxActiveBlocksPerMultiprocessor = hipError_t (*)(int*, const void*, int, size_t);
 using hipGetProcAddress = hipError_t (*)(const char*, void**, int, uint64_t,
                                          hipDriverProcAddressQueryResult*);

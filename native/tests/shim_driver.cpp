@@ -30,6 +30,7 @@ extern "C" uint64_t fake_hip_launches();
 extern "C" uint64_t fake_hip_physical_used(int dev);
 extern "C" uint64_t fake_hsa_pool_used(int dev);
 extern "C" int fake_hsa_tools_loaded();
+extern "C" hipGraph_t fake_hip_graph_create(const unsigned* grids, int n, unsigned child_grid);
 
 static hsa_status_t gpu_agent_cb(hsa_agent_t a, void* data) {
   hsa_device_type_t t;
@@ -157,6 +158,23 @@ int main(int argc, char** argv) {
       printf("\n");
     }
     hipFree(p);
+    return 0;
+  }
+
+  if (sc == "graph") {
+    // kernel nodes (100,2,1) + (300,2,1) + child (50): 850 workgroups per launch
+    const unsigned grids[2] = {100, 300};
+    hipGraph_t g = fake_hip_graph_create(grids, 2, 50);
+    hipGraphExec_t e1 = nullptr, e2 = nullptr;
+    hipGraphInstantiateWithFlags(&e1, g, 0);
+    hipGraphInstantiate(&e2, g, nullptr, nullptr, 0);
+    int n = argc > 2 ? atoi(argv[2]) : 3;
+    for (int i = 0; i < n; ++i) hipGraphLaunch(e1, nullptr);
+    hipGraphLaunch(e2, nullptr);
+    hipGraphExecDestroy(e1);
+    hipGraphLaunch(e1, nullptr);  // destroyed (or unknown) exec: fallback charge
+    printf("fake_launches=%llu\n", (unsigned long long)fake_hip_launches());
+    print_region(dev);
     return 0;
   }
 

@@ -122,3 +122,15 @@ def test_hsa_tools_lib_mode_masks_and_cap(gpu_build):
                                 "HSA_TOOLS_LIB": str(shim_path())})
     assert res["shim"]["hsa_table_mode"] == 1
     assert res["total"] == 8192 << 20 and res["reserved"] <= 8192 << 20
+
+
+def test_graph_replay_charged_by_kernel_nodes(gpu_build, tmp_path):
+    """A captured hipGraph's replay is charged the workgroups of its kernel
+    nodes (the two busy kernels), not a flat per-launch guess."""
+    from vgpu.monitor import trace
+    probe(["graph", 1000, 3000], {"VGPU_DEVICE_CU_LIMIT_0": "50", "VGPU_TRACE": str(tmp_path),
+                                  "VGPU_GRAPH_LAUNCH_TOKENS": "1"})
+    files = list(tmp_path.glob("vgpu-trace-*.bin"))
+    ev = [e for f in files for e in trace.read(str(f))[1] if e["type"] == "launch"]
+    graph_launches = [e["a"] for e in ev if e["a"] >= 4000]
+    assert len(graph_launches) == 2 and all(a == 4000 for a in graph_launches), [e["a"] for e in ev][-10:]

@@ -128,3 +128,17 @@ def test_event_trace_ring_wraps(native_build, tmp_path):
     (f,) = list(tmp_path.glob("vgpu-trace-*.bin"))
     h, ev = trace.read(str(f))
     assert h.head > 500 and len(ev) == 64
+
+
+def test_graph_launch_charged_by_kernel_nodes(native_build, tmp_path):
+    """hipGraphLaunch is charged the workgroups of the executable graph's
+    kernel nodes (child graphs included, other node types ignored), recorded
+    at instantiation; an unknown exec falls back to VGPU_GRAPH_LAUNCH_TOKENS."""
+    from vgpu.monitor import trace
+    o = run("graph", 3, env={"VGPU_TRACE": str(tmp_path), "VGPU_GRAPH_LAUNCH_TOKENS": "7"})
+    assert o["fake_launches"] == "5"
+    (f,) = list(tmp_path.glob("vgpu-trace-*.bin"))
+    _, ev = trace.read(str(f))
+    wg = [e["a"] for e in ev if e["type"] == "launch"]
+    # 2 kernel nodes (100x2, 300x2) + child (50) = 850 per launch; e1 x3, e2 x1, destroyed e1 x1
+    assert wg == [850, 850, 850, 850, 7]

@@ -7,6 +7,9 @@ line.  Used by the GPU tests and by the accuracy benchmarks.
       wall time of a fixed amount of VALU work (compute-share accuracy)
   python -m vgpu.bench.probes cap [chunk_mib]
       reported total + how many bytes torch could allocate before OOM
+  python -m vgpu.bench.probes graph [blocks_a] [blocks_b]
+      capture two busy kernels into a hipGraph and replay it (the library
+      charges a graph launch by its kernel nodes' workgroups; see VGPU_TRACE)
   python -m vgpu.bench.probes smi [alloc_mib]
       what amdsmi (python bindings over libamd_smi, the amd-smi CLI's path)
       reports for VRAM total / used after torch allocates alloc_mib
@@ -132,11 +135,28 @@ def cap(chunk_mib: int = 1024) -> dict:
     return res
 
 
+def graph(blocks_a: int = 1000, blocks_b: int = 3000) -> dict:
+    import torch
+    from vgpu.ops import kernels as K
+    K.busy(blocks_a, 10)  # load the module / warm up outside the capture
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            K.busy(blocks_a, 10)
+            K.busy(blocks_b, 10)
+    for _ in range(2):
+        g.replay()
+    torch.cuda.synchronize()
+    return {"blocks": [blocks_a, blocks_b], "replays": 2}
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     cmd = argv.pop(0) if argv else "census"
     nums = [int(a) for a in argv]
-    out = {"census": census, "busy": busy, "cap": cap, "smi": smi}[cmd](*nums)
+    out = {"census": census, "busy": busy, "cap": cap, "smi": smi, "graph": graph}[cmd](*nums)
     out["shim"] = shim_stats()
     print("PROBE " + json.dumps(out), flush=True)
     return 0
