@@ -894,6 +894,67 @@ hipError_t dispatch_pro(const ConvArgs& a, bool res, hipStream_t s) {
   return res ? launch_pro<KS, BM, 64, true>(a, s) : launch_pro<KS, BM, 64, false>(a, s);
 }
 
+// epilogue_halves for a conv3 chunk whose output also feeds the next block's
+// conv1: besides storing y = acc + residual (bf16), each thread keeps
+// p = relu(bf16(y) * s[c] + t[c]) (the next block-entry BN+ReLU, rounded to
+// bf16 exactly as conv_pro's prologue stages it) for its rows in registers.
+template <int BM, int BN>
+__device__ __forceinline__ void epilogue_halves_next(const ConvArgs& a, f32x4_t (&acc)[BM / 32][BN / 32],
+                                                     int m0, int n0, char* smem,
+                                                     const u32x4 (&res)[2][EpiShape<BM, BN>::RROWS],
+                                                     const float* __restrict__ ps, const float* __restrict__ pt,
+                                                     u32x4 (&pv)[2][EpiShape<BM, BN>::RROWS]) {
+  constexpr int WTM = BM / 2, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
+  constexpr int CS = BN + 4, HROWS = BM / 2;
+  constexpr int CPR = BN / 8, RSTEP = kThreads / CPR, RROWS = HROWS / RSTEP;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fk = lane >> 4;
+  const int chunk = t % CPR, rfirst = t / CPR;
+  const int col = n0 + chunk * 8;
+  float sc[8], sh[8];
+  {
+    const float4 s0 = *reinterpret_cast<const float4*>(ps + col);
+    const float4 s1 = *reinterpret_cast<const float4*>(ps + col + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(pt + col);
+    const float4 h1 = *reinterpret_cast<const float4*>(pt + col + 4);
+    sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+    sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w; sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+  }
+  float* sC = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (wm == h) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            sC[(i * 16 + fk * 4 + e) * CS + wn * WTN + j * 16 + fr] = acc[i][j][e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RROWS; ++i) {
+      const int r = rfirst + RSTEP * i, m = m0 + h * HROWS + r;
+      const float4 c0 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8);
+      const float4 c1 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8 + 4);
+      float v[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      float re[8];
+      unpack8(res[h][i], re);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += re[j];
+      const u32x4 yv = pack8(v);
+      if (m < a.M) *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = yv;
+      float q[8];
+      unpack8(yv, q);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[j] = fmaxf(q[j] * sc[j] + sh[j], 0.0f);
+      pv[h][i] = pack8(q);
+    }
+    __syncthreads();  // this half read out before the next staging / the A3 image reuses it
+  }
+}
+
 // ---- Fused bottleneck tail: conv2 (3x3, W→W, bias+ReLU) → conv3 (1x1, W→4W)
 // + residual, one kernel per row tile.
 //
@@ -909,8 +970,17 @@ hipError_t dispatch_pro(const ConvArgs& a, bool res, hipStream_t s) {
 // Phase 1 is the LDS-DMA conv loop with the transposed MFMA (mfma(B, A)) so a
 // lane holds 4 consecutive conv2 channels of one row: one 8-byte ds_write per
 // 16×16 subtile lands them in the conv3 A image.
-template <int BM, int W>
-__global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, const ConvArgs b) {
+// NEXT: also the NEXT block's conv1 (1x1, 4W→W, BN+ReLU prologue, bias+ReLU
+// epilogue; ConvArgs c) on the conv3 output while it is on chip: after each
+// 128-channel conv3 chunk, its BN+ReLU'd bf16 values become a K chunk of conv1's
+// A operand (an image in the epilogue staging area) and the matching 128-row K
+// chunk of conv1's weights is DMA'd into the conv3 panel slot, so h1 of the next
+// block accumulates in registers across the chunks.  Saves the next block's
+// re-read of the 4W-wide activation (stage 1 at b=50: 194 MB per block).
+// Numerics equal conv23 + conv_pro (same bf16 roundings, same K order).
+template <int BM, int W, bool NEXT = false>
+__global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, const ConvArgs b,
+                                                             const ConvArgs c) {
   constexpr int KCH = W / 64;                // conv3 K chunks (64 channels each)
   constexpr int AR = BM / 32, BR = W / 32;   // phase-1 DMA instructions per thread per step
   constexpr int WTM = BM / 2, WTN = W / 2;
@@ -1018,6 +1088,18 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
   constexpr int WTM2 = BM / 2, TM2 = WTM2 / 16;
   char* sB2 = smem;
   const int nchunks = b.Cout / BN2;
+  // phase 3 (NEXT): conv1 of the next block, W outputs per row, K = 4W
+  constexpr int TM3 = BM / 32, TN3 = W / 32;
+  f32x4_t acc3[TM3][TN3];
+  if constexpr (NEXT) {
+#pragma unroll
+    for (int i = 0; i < TM3; ++i)
+#pragma unroll
+      for (int j = 0; j < TN3; ++j) acc3[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  const __amdgpu_buffer_rsrc_t w1r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(NEXT ? c.w : b.w), 0, NEXT ? (uint32_t)((int64_t)c.Cout * c.K * 2) : 0u,
+      0x00020000);
   for (int ch = 0; ch < nchunks; ++ch) {
     const int c0 = ch * BN2;
 #pragma unroll
@@ -1045,8 +1127,49 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     __builtin_amdgcn_s_barrier();
     u32x4 res[2][EpiShape<BM, BN2>::RROWS];
-    load_residual<BM, BN2>(b, m0, c0, res);
-    epilogue_halves<BM, BN2, true>(b, acc2, m0, c0, smem + B2_BYTES, res);
+    if constexpr (!NEXT) {
+      load_residual<BM, BN2>(b, m0, c0, res);
+      epilogue_halves<BM, BN2, true>(b, acc2, m0, c0, smem + B2_BYTES, res);
+    } else {
+      // conv1's weight K chunk [W rows][c0 .. c0+127] into the (now idle) B2
+      // slot, in flight behind the epilogue: two 64-wide K panels of W rows.
+#pragma unroll
+      for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+        for (int i = 0; i < W / 32; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              w1r, (lds_void_t*)(sB2 + kc * (W * 128) + (32 * i + wave * 8) * 128), 16,
+              (uint32_t)(((lrow + 32 * i) * c.K + c0 + kc * 64 + lchunk * 8) * 2), 0, 0, 0);
+      load_residual<BM, BN2>(b, m0, c0, res);
+      u32x4 pv[2][EpiShape<BM, BN2>::RROWS];
+      char* sE = smem + B2_BYTES;
+      epilogue_halves_next<BM, BN2>(b, acc2, m0, c0, sE, res, c.pscale, c.pshift, pv);
+      // A3 image (BM rows x 128 channels = two 64-wide swizzled panels) in the
+      // staging area, which the epilogue has finished reading.
+      {
+        using E = EpiShape<BM, BN2>;
+        const int chunk = t % E::CPR, rfirst = t / E::CPR;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int i = 0; i < E::RROWS; ++i) {
+            const int r = h * E::HROWS + rfirst + E::RSTEP * i;
+            *reinterpret_cast<u32x4*>(sE + (chunk >> 3) * (BM * 128) + swz(r, chunk & 7)) = pv[h][i];
+          }
+      }
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+      __syncthreads();  // A3 written, conv1 weight chunk landed
+#pragma unroll
+      for (int kc = 0; kc < 2; ++kc)
+        mma_k64<TM3, TN3>(sE + kc * (BM * 128), sB2 + kc * (W * 128), wm * (BM / 2), wn * (W / 2), fr, fk,
+                          acc3);
+      __builtin_amdgcn_s_waitcnt(kLgkm0);
+      __builtin_amdgcn_s_barrier();  // A3 / weight chunk read before the next chunk reuses them
+    }
+  }
+  if constexpr (NEXT) {
+    u32x4 none[2][EpiShape<BM, W>::RROWS];
+    epilogue_halves<BM, W, false>(c, acc3, m0, 0, smem, none);
   }
 }
 
@@ -1238,11 +1361,14 @@ VGPU_API void vgpu_conv_set_stages(int n) { g_forced_stages = n; }
 VGPU_API void vgpu_conv_set_tile_m(int bm) { g_forced_bm = bm; }
 
 // Fused conv2 (3x3, pad 1, stride s, C = W → W, bias + ReLU) + conv3 (1x1,
-// W → 4W) + residual.  W ∈ {64, 128}.  Returns 0, a hipError_t, or -1.
-VGPU_API int vgpu_conv23_nhwc(const void* x, const void* w2, const float* b2, const void* w3,
-                              const void* res, void* y, int N, int H, int W, int C, int stride,
-                              hipStream_t s) {
+// W → 4W) + residual; with w1n, also the next block's conv1 (1x1, 4W → W,
+// prologue relu(y*ps + pt), bias b1n + ReLU) into h1n.  W ∈ {64, 128}.
+static int conv23_impl(const void* x, const void* w2, const float* b2, const void* w3, const void* res,
+                       void* y, const void* w1n, const float* b1n, const float* psn, const float* ptn,
+                       void* h1n, int N, int H, int W, int C, int stride, hipStream_t s) {
   if ((C != 64 && C != 128) || stride < 1 || N < 1 || !b2 || !res) return -1;
+  const bool next = w1n != nullptr;
+  if (next && (!b1n || !psn || !ptn || !h1n)) return -1;
   ConvArgs a{};
   a.x = static_cast<const uint16_t*>(x);
   a.w = static_cast<const uint16_t*>(w2);
@@ -1261,13 +1387,25 @@ VGPU_API int vgpu_conv23_nhwc(const void* x, const void* w2, const float* b2, co
   b.res = static_cast<const uint16_t*>(res);
   b.Cout = 4 * C;
   b.K = C;
+  ConvArgs cn{};
+  if (next) {
+    cn.w = static_cast<const uint16_t*>(w1n);
+    cn.y = static_cast<uint16_t*>(h1n);
+    cn.bias = b1n;
+    cn.pscale = psn;
+    cn.pshift = ptn;
+    cn.Cout = C;
+    cn.K = 4 * C;
+    cn.act = 1;
+  }
   const int64_t xi = (int64_t)H * W * C * 2, yi = (int64_t)a.OH * a.OW * b.Cout * 2;
+  const int64_t hi = (int64_t)a.OH * a.OW * C * 2;
   const int64_t lim = ((int64_t)1 << 31) - 1;
   const int64_t per = lim / (xi > yi ? xi : yi);
   if (per < 1) return -1;
   for (int n0 = 0; n0 < N; n0 += (int)per) {
     const int nb = (int)((N - n0) < per ? (N - n0) : per);
-    ConvArgs c = a, d = b;
+    ConvArgs c = a, d = b, e = cn;
     c.N = nb;
     c.x = a.x + (int64_t)n0 * (xi / 2);
     c.x_bytes = (uint32_t)(nb * xi);
@@ -1276,17 +1414,45 @@ VGPU_API int vgpu_conv23_nhwc(const void* x, const void* w2, const float* b2, co
     d.y = b.y + (int64_t)n0 * (yi / 2);
     d.res = b.res + (int64_t)n0 * (yi / 2);
     d.y_bytes = (uint32_t)(nb * yi);
-    if (C == 64) {
-      c.nM = (c.M + 127) / 128; c.nN = 1; c.nwg = c.nM;
-      hipLaunchKernelGGL((conv23_kernel<128, 64>), dim3(c.nwg), dim3(kThreads), 0, s, c, d);
-    } else {
-      c.nM = (c.M + 63) / 64; c.nN = 1; c.nwg = c.nM;
-      hipLaunchKernelGGL((conv23_kernel<64, 128>), dim3(c.nwg), dim3(kThreads), 0, s, c, d);
+    if (next) {
+      e.M = c.M;
+      e.y = cn.y + (int64_t)n0 * (hi / 2);
+      e.y_bytes = (uint32_t)(nb * hi);
     }
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return (int)e;
+    const int bm = C == 64 ? 128 : 64;
+    c.nM = (c.M + bm - 1) / bm; c.nN = 1; c.nwg = c.nM;
+    if (C == 64) {
+      if (next)
+        hipLaunchKernelGGL((conv23_kernel<128, 64, true>), dim3(c.nwg), dim3(kThreads), 0, s, c, d, e);
+      else
+        hipLaunchKernelGGL((conv23_kernel<128, 64>), dim3(c.nwg), dim3(kThreads), 0, s, c, d, e);
+    } else {
+      if (next)
+        hipLaunchKernelGGL((conv23_kernel<64, 128, true>), dim3(c.nwg), dim3(kThreads), 0, s, c, d, e);
+      else
+        hipLaunchKernelGGL((conv23_kernel<64, 128>), dim3(c.nwg), dim3(kThreads), 0, s, c, d, e);
+    }
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return (int)err;
   }
   return 0;
+}
+
+VGPU_API int vgpu_conv23_nhwc(const void* x, const void* w2, const float* b2, const void* w3,
+                              const void* res, void* y, int N, int H, int W, int C, int stride,
+                              hipStream_t s) {
+  return conv23_impl(x, w2, b2, w3, res, y, nullptr, nullptr, nullptr, nullptr, nullptr, N, H, W, C, stride, s);
+}
+
+// conv23 + the next (identity-shortcut) block's conv1 in one kernel: y is the
+// next block's input x (still stored: it is that block's residual), h1n its
+// conv1 output.  Same constraints as vgpu_conv23_nhwc; b1n/psn/ptn fp32.
+VGPU_API int vgpu_conv231_nhwc(const void* x, const void* w2, const float* b2, const void* w3,
+                               const void* res, void* y, const void* w1n, const float* b1n,
+                               const float* psn, const float* ptn, void* h1n, int N, int H, int W,
+                               int C, int stride, hipStream_t s) {
+  if (!w1n) return -1;
+  return conv23_impl(x, w2, b2, w3, res, y, w1n, b1n, psn, ptn, h1n, N, H, W, C, stride, s);
 }
 
 // Returns 0, a hipError_t, or -1 for an unsupported shape (checked before any launch).

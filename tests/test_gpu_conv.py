@@ -154,6 +154,32 @@ def test_conv23_matches_unfused(C, case):
     torch.testing.assert_close(got, unf, atol=0, rtol=0)
 
 
+@pytest.mark.parametrize("case", [(2, 64, 19, 17, 1), (2, 128, 21, 19, 2), (3, 128, 9, 9, 1),
+                                  (4, 64, 64, 64, 1), (1, 64, 7, 5, 1)])
+def test_conv231_matches_conv23_then_conv1(C, case):
+    """Tail + next block's BN+ReLU+conv1 in one kernel: bit-for-bit equal to
+    conv23 followed by the prologue conv1 (same roundings, same K order)."""
+    n, c, h, w, stride = case
+    x = _t((n, c, h, w), 31)
+    w2 = _t((c, c, 3, 3), 32, scale=(2.0 / (9 * c)) ** 0.5)
+    b2 = _f((c,), 33)
+    w3 = _t((4 * c, c, 1, 1), 34, scale=(2.0 / c) ** 0.5)
+    w1n = _t((c, 4 * c, 1, 1), 35, scale=(2.0 / (4 * c)) ** 0.5)
+    b1n = _f((c,), 36)
+    pro = (_f((4 * c,), 37, 0.5, 1.5), _f((4 * c,), 38))
+    oh, ow = C.out_hw(h, w, 3, stride, 1)
+    res = _t((n, 4 * c, oh, ow), 39)
+    y, h1 = C.conv231(x, w2, b2, w3, res, w1n, b1n, pro, stride=stride)
+    y_ref = C.conv23(x, w2, b2, w3, res, stride=stride)
+    h1_ref = C.conv2d(y_ref, w1n, b1n, act="relu", pro=pro)
+    assert y.is_contiguous(memory_format=CL) and h1.is_contiguous(memory_format=CL)
+    torch.testing.assert_close(y, y_ref, atol=0, rtol=0)
+    torch.testing.assert_close(h1, h1_ref, atol=0, rtol=0)
+    # and against fp32
+    ref = C.conv2d_ref(y_ref, w1n, b1n, act="relu", pro=pro)
+    torch.testing.assert_close(h1.float(), ref, atol=3e-2, rtol=2e-2)
+
+
 TRAIN_CASES = [
     # n, c, h, w, cout, ks, stride, pad, residual
     (2, 64, 12, 10, 256, 1, 1, 0, True),     # conv3 + residual

@@ -129,6 +129,8 @@ class FusedResNetV2Inference(nn.Module):
         # conv2+conv3 fusion (VGPU_FUSE_TAIL=0 disables, for A/B)
         import os
         self.fuse_tail = os.environ.get("VGPU_FUSE_TAIL", "1") != "0"
+        # ... and the next identity block's conv1 into that tail (VGPU_FUSE_NEXT=0 disables)
+        self.fuse_next = self.fuse_tail and os.environ.get("VGPU_FUSE_NEXT", "1") != "0"
         from vgpu.ops.fused import bn_scale_shift
         m = m.eval()
         dt = m.stem.weight.dtype
@@ -170,14 +172,22 @@ class FusedResNetV2Inference(nn.Module):
         from vgpu.ops import conv as C
         x = C.stem_conv(x.contiguous(memory_format=torch.channels_last), self.stem_w_s2d)
         x = C.maxpool3s2(x)
-        for b in self.blocks:
+        h_next = None
+        for i, b in enumerate(self.blocks):
             pro = b["in"]
             if b["sc"] is None:
                 sc = x
             else:
                 sc = C.conv2d(x, b["sc"][0], stride=b["sc"][1], pro=pro)
-            h = C.conv2d(x, b["w1"], b["b1"], act="relu", pro=pro)
-            if self.fuse_tail and C.conv23_supported(h.shape[1]):
+            h = h_next if h_next is not None else C.conv2d(x, b["w1"], b["b1"], act="relu", pro=pro)
+            h_next = None
+            nb = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
+            if (self.fuse_next and nb is not None and nb["sc"] is None
+                    and C.conv23_supported(h.shape[1])):
+                # conv2 + conv3 + residual + the next block's BN+ReLU+conv1 (stages 1-2)
+                x, h_next = C.conv231(h, b["w2"], b["b2"], b["w3"], sc, nb["w1"], nb["b1"], nb["in"],
+                                      stride=b["stride"])
+            elif self.fuse_tail and C.conv23_supported(h.shape[1]):
                 # conv2 + conv3 + residual in one kernel (stages 1-2)
                 x = C.conv23(h, b["w2"], b["b2"], b["w3"], sc, stride=b["stride"])
             else:

@@ -114,6 +114,36 @@ def conv23(x: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor, w3: torch.Tensor
     return out
 
 
+def conv231(x: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor, w3: torch.Tensor,
+            residual: torch.Tensor, w1n: torch.Tensor, b1n: torch.Tensor,
+            pro_n: tuple[torch.Tensor, torch.Tensor], *, stride: int = 1) -> tuple[torch.Tensor, torch.Tensor]:
+    """conv23 plus the next identity-shortcut block's conv1 in one kernel:
+    y = conv23(x, ...) (the next block's input, still stored as its residual) and
+    h1n = relu(conv1x1(relu(y*s + t), w1n) + b1n) with (s, t) = pro_n.  Numerics
+    equal conv23 followed by conv2d(y, w1n, b1n, act='relu', pro=pro_n)."""
+    _nhwc(x, "x")
+    for t, nm in ((w2, "w2"), (w3, "w3"), (residual, "residual"), (w1n, "w1n")):
+        _nhwc(t, nm)
+    n, c, h, wd = x.shape
+    if (c not in (64, 128) or tuple(w2.shape) != (c, c, 3, 3) or tuple(w3.shape) != (4 * c, c, 1, 1)
+            or tuple(w1n.shape) != (c, 4 * c, 1, 1)):
+        raise ValueError(f"unsupported fused tail + next conv1: x {tuple(x.shape)} w1n {tuple(w1n.shape)}")
+    for p_, nm, size in ((b2, "b2", c), (b1n, "b1n", c), (pro_n[0], "scale", 4 * c), (pro_n[1], "shift", 4 * c)):
+        if p_.dtype != torch.float32 or not p_.is_contiguous() or p_.numel() != size:
+            raise TypeError(f"{nm} must be a contiguous fp32 tensor of size {size}")
+    oh, ow = out_hw(h, wd, 3, stride, 1)
+    if tuple(residual.shape) != (n, 4 * c, oh, ow):
+        raise ValueError("residual shape")
+    y = torch.empty((n, 4 * c, oh, ow), dtype=x.dtype, device=x.device, memory_format=_CL)
+    h1 = torch.empty((n, c, oh, ow), dtype=x.dtype, device=x.device, memory_format=_CL)
+    rc = load_kernels().vgpu_conv231_nhwc(_ptr(x), _ptr(w2), _ptr(b2), _ptr(w3), _ptr(residual), _ptr(y),
+                                          _ptr(w1n), _ptr(b1n), _ptr(pro_n[0]), _ptr(pro_n[1]), _ptr(h1),
+                                          n, h, wd, c, stride, _stream())
+    if rc != 0:
+        raise RuntimeError(f"vgpu_conv231_nhwc: error {rc}")
+    return y, h1
+
+
 def conv23_supported(c: int) -> bool:
     return c in (64, 128)
 
