@@ -134,3 +134,26 @@ def test_graph_replay_charged_by_kernel_nodes(gpu_build, tmp_path):
     ev = [e for f in files for e in trace.read(str(f))[1] if e["type"] == "launch"]
     graph_launches = [e["a"] for e in ev if e["a"] >= 4000]
     assert len(graph_launches) == 2 and all(a == 4000 for a in graph_launches), [e["a"] for e in ev][-10:]
+
+
+def test_ddp_over_rccl_under_the_shim(gpu_build):
+    """A data-parallel training step (vgpu.parallel.ddp, backend nccl = RCCL)
+    runs inside a capped vGPU process: RCCL initialises and all-reduces with
+    the enforcement library loaded (its kernels are limiter-exempt)."""
+    import socket
+    from vgpu.native import preload_env
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = preload_env(dict(os.environ))
+    env.update({"VGPU_DEVICE_MEMORY_LIMIT_0": "64g", "VGPU_DEVICE_CU_LIMIT_0": "50",
+                "PYTHONPATH": REPO + os.pathsep + env.get("PYTHONPATH", "")})
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                        "--master-addr=127.0.0.1", f"--master-port={port}", "-m", "vgpu.parallel.ddp",
+                        "--workload", "1.2", "--steps", "3", "--warmup", "2", "--batch", "4", "--size", "128"],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    print(res)
+    assert res["backend"] == "nccl" and res["value"] > 0 and res["final_loss"] == res["final_loss"]

@@ -57,17 +57,10 @@ def main(argv=None) -> int:
     cl = torch.channels_last
     dev = "cuda"
 
+    from vgpu.utils.timing import cuda_time_us
+
     def timeit(fn):
-        for _ in range(3):
-            fn()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(args.iters):
-            fn()
-        e1.record()
-        torch.cuda.synchronize()
-        return e0.elapsed_time(e1) * 1e3 / args.iters
+        return cuda_time_us(fn, args.iters)
 
     tot_n = tot_m = 0.0
     if args.ab_tail:

@@ -1,1 +1,1 @@
-"""vgpu.utils."""
+"""vgpu.utils: small shared helpers (GPU timing for the kernel benchmarks)."""
