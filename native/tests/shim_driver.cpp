@@ -161,6 +161,35 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (sc == "suspend") {
+    // SIGUSR2 suspends: allocation and launch paths wait until SIGUSR1.
+    void* p0 = nullptr;
+    hipMalloc(&p0, 1 << 20);
+    auto self_region = sym<void* (*)()>("vgpu_self_region");
+    auto self_slot = sym<int (*)()>("vgpu_self_slot");
+    auto* r = self_region ? (vgpu_shared_region_t*)self_region() : nullptr;
+    const int slot = self_slot ? self_slot() : -1;
+    raise(SIGUSR2);
+    if (r && slot >= 0) printf("status_suspended=%d\n", r->procs[slot].status);
+    std::atomic<int> alloc_done{0}, launch_done{0};
+    std::thread ta([&] { void* p = nullptr; hipMalloc(&p, 1 << 20); alloc_done = 1; });
+    std::thread tl([&] {
+      hipLaunchKernel((const void*)&main, dim3(64), dim3(256), nullptr, 0, nullptr);
+      launch_done = 1;
+    });
+    usleep(300000);
+    printf("alloc_done_while_suspended=%d\nlaunch_done_while_suspended=%d\n", alloc_done.load(),
+           launch_done.load());
+    raise(SIGUSR1);
+    ta.join();
+    tl.join();
+    printf("alloc_done=%d\nlaunch_done=%d\n", alloc_done.load(), launch_done.load());
+    if (r && slot >= 0)
+      printf("status_resumed=%d\nwait_ns=%llu\n", r->procs[slot].status,
+             (unsigned long long)r->procs[slot].throttle_wait_ns);
+    return 0;
+  }
+
   if (sc == "graph") {
     // kernel nodes (100,2,1) + (300,2,1) + child (50): 850 workgroups per launch
     const unsigned grids[2] = {100, 300};

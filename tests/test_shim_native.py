@@ -196,3 +196,15 @@ def test_rccl_kernels_exempt_from_temporal_limiter(native_build, tmp_path):
     thr = run("throttle", 1.0, 64, env=base)
     rccl = run("throttle_rccl", 1.0, 64, env=base)
     assert int(rccl["launches"]) > 3 * int(thr["launches"]), (rccl["launches"], thr["launches"])
+
+
+def test_suspend_resume_signals_gate_alloc_and_launch(native_build):
+    """SIGUSR2 suspends the container process (allocations and launches wait,
+    slot status SUSPENDED), SIGUSR1 resumes it (reference sig_swap_stub /
+    sig_restore_stub); the wait is accounted."""
+    o = run("suspend", env={"VGPU_DEVICE_MEMORY_LIMIT_0": "8g"})
+    assert o["status_suspended"] == "2"
+    assert o["alloc_done_while_suspended"] == "0" and o["launch_done_while_suspended"] == "0"
+    assert o["alloc_done"] == "1" and o["launch_done"] == "1"
+    assert o["status_resumed"] == "1"
+    assert int(o["wait_ns"]) >= 250_000_000
