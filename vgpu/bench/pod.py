@@ -116,6 +116,9 @@ def build(args):
                 step()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        split = max(1, int(os.environ.get("VGPU_POD_SPLIT", "1")))
+        if split > 1:
+            return w, split_replay(model, x, split)
         try:
             graph = torch.cuda.CUDAGraph()
             with torch.inference_mode(), torch.cuda.graph(graph):
@@ -129,6 +132,40 @@ def build(args):
             graph.replay()
         return w, replay
     return w, step
+
+
+def split_replay(model, x, split: int):
+    """The batch as `split` micro-batches, one hipGraph each, replayed on their
+    own streams so the kernels of different micro-batches can co-reside on the
+    pod's CUs (fills tile-quantisation tails, hides per-kernel latency).  Same
+    work per step; VGPU_POD_SPLIT selects it (A/B knob)."""
+    import torch
+    cur = torch.cuda.current_stream()
+    chunks = x.chunk(split)
+    streams = [torch.cuda.Stream() for _ in chunks]
+    with torch.inference_mode():
+        for st, xc in zip(streams, chunks):  # warm the micro-batch shape eagerly
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                model(xc)
+    torch.cuda.synchronize()
+    graphs = []
+    for st, xc in zip(streams, chunks):
+        g = torch.cuda.CUDAGraph()
+        with torch.inference_mode(), torch.cuda.graph(g, stream=st):
+            model(xc)
+        graphs.append(g)
+    torch.cuda.synchronize()
+
+    def replay():
+        cur = torch.cuda.current_stream()
+        for st, g in zip(streams, graphs):
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                g.replay()
+        for st in streams:
+            cur.wait_stream(st)
+    return replay
 
 
 def cap_probe() -> dict:
