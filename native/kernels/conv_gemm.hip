@@ -32,6 +32,7 @@
 // XCD's L2.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 
 #define VGPU_API extern "C" __attribute__((visibility("default")))
@@ -1191,6 +1192,45 @@ bool glds_pro_enabled() {
   return on == 1;
 }
 
+// CUs this process can occupy on the current device — the grid-fill term of
+// the tile choice.  A vGPU pod owns an XCD-balanced CU mask of
+// VGPU_DEVICE_CU_LIMIT_<i> % of the device (the enforcement library's env
+// contract), so a 50 % pod has 128 CUs to fill, not 256.  VGPU_CONV_CUS
+// overrides (A/B).  Cached per device.
+int conv_cus() {
+  static int forced = -1;
+  static int cached[16] = {};
+  if (forced < 0) {
+    const char* v = getenv("VGPU_CONV_CUS");
+    forced = v ? atoi(v) : 0;
+  }
+  if (forced > 0) return forced;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+  if (cached[dev]) return cached[dev];
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  const char* masked = getenv("VGPU_REPORT_MASKED_CUS");  // the runtime already reports the mask
+  char name[40];
+  snprintf(name, sizeof name, "VGPU_DEVICE_CU_LIMIT_%d", dev);
+  const char* lim = getenv(name);
+  const int pct = lim ? atoi(lim) : 0;
+  if (!(masked && masked[0] == '1') && pct > 0 && pct < 100) cus = (cus * pct + 99) / 100;
+  cached[dev] = cus > 0 ? cus : 1;
+  return cached[dev];
+}
+
+// A/B knob: 128-row tiles for non-prologue 1x1 convs too (VGPU_CONV_1X1_BIG=1).
+bool conv_1x1_big() {
+  static int on = -1;
+  if (on < 0) {
+    const char* v = getenv("VGPU_CONV_1X1_BIG");
+    on = (v && v[0] == '1') ? 1 : 0;
+  }
+  return on == 1;
+}
+
 bool glds_enabled() {
   static int on = -1;
   if (on < 0) {
@@ -1499,13 +1539,16 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
     c.x_bytes = (uint32_t)(nb * xi);
     c.y_bytes = (uint32_t)(nb * yi);
     c.M = nb * a.OH * a.OW;
-    // Small-M layers (late stages) use 64-row tiles so the grid still fills the chip.
+    // Small-M layers use 64-row tiles so the grid still fills the CUs this
+    // process owns: 128-row tiles fetch fewer bytes per FLOP, but below ~1.5
+    // workgroups per CU the kernel is latency-bound (profiles/conv_cus_r1.md:
+    // exclusive 256 CUs and 50 % pods of 128 CUs agree with this threshold).
     const int64_t tiles128 = (int64_t)((c.M + 127) / 128) * (Cout / bn);
-    bool small = tiles128 < 512;
+    bool small = tiles128 < (int64_t)conv_cus() * 3 / 2;
     // Non-prologue 1x1 convs (conv3 + residual) are DMA/HBM-bound: 64-row tiles
     // (48 KB LDS → 3 blocks per CU) beat 128-row tiles on every ResNet-50 shape
     // (profiles/conv_tiles_r1.md).
-    if (!pro && KS == 1) small = true;
+    if (!pro && KS == 1) small = !conv_1x1_big();
     if (g_forced_bm == 64) small = true;
     if (g_forced_bm == 128) small = false;
     hipError_t e;
