@@ -213,3 +213,30 @@ def test_conv_train_fwd_bwd_matches_fp32(C, n, c, h, w, cout, ks, stride, pad, r
     for got, ref in ((x.grad, xr.grad), (conv.weight.grad, wr.grad)) + (((r.grad, rr.grad),) if res else ()):
         scale = ref.abs().max().item()
         torch.testing.assert_close(got.float(), ref, atol=2e-2 * scale, rtol=2e-2)
+
+
+WGRAD_CASES = [
+    # n, c, h, w, cout, ks, stride, pad — covers the 4 tile shapes, split-K, padding taps, strides
+    (2, 64, 12, 10, 64, 3, 1, 1),       # BM=64 x BN=64
+    (2, 128, 12, 10, 128, 3, 2, 1),     # BM=128 x BN=128, strided
+    (4, 64, 33, 31, 256, 1, 1, 0),      # BM=128 x BN=64, ragged pixel tail
+    (3, 256, 13, 13, 64, 1, 2, 0),      # BM=64 x BN=128, strided 1x1
+    (20, 64, 87, 87, 64, 3, 1, 1),      # ResNet-V2-50 stage-1 conv2 at ai-benchmark 1.2 (b=20, 346²)
+    (20, 256, 87, 87, 64, 1, 1, 0),     # stage-1 conv1: 1024 splits
+    (3, 64, 9, 9, 64, 1, 1, 0),         # one split, odd step count
+    (2, 512, 11, 11, 512, 3, 1, 1),     # deep columns, few pixels
+]
+
+
+@pytest.mark.parametrize("n,c,h,w,cout,ks,stride,pad", WGRAD_CASES)
+def test_conv_wgrad_matches_fp32(C, n, c, h, w, cout, ks, stride, pad):
+    x = _t((n, c, h, w), 11)
+    oh, ow = C.out_hw(h, w, ks, stride, pad)
+    dy = _t((n, cout, oh, ow), 12)
+    dw = C.conv2d_wgrad(dy, x, ks, stride=stride, padding=pad)
+    assert dw.shape == (cout, c, ks, ks) and dw.is_contiguous(memory_format=CL)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (cout, c, ks, ks), dy.float(), stride=stride, padding=pad)
+    scale = ref.abs().max().item()
+    torch.testing.assert_close(dw.float(), ref, atol=1e-2 * scale, rtol=1e-2)
+    # deterministic: split-K partials are reduced in a fixed order
+    assert torch.equal(dw, C.conv2d_wgrad(dy, x, ks, stride=stride, padding=pad))

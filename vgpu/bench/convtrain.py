@@ -7,7 +7,9 @@ backward-weight against the native candidates.
 Native candidates per layer (stride-1 only for the data gradient):
   fwd    native MFMA implicit GEMM (vgpu.ops.conv.conv2d)
   dgrad  the same kernel on dy with the transposed (and, for 3x3, flipped) filter
-  wgrad  1x1: one GEMM dW = dyᵀ·x (hipBLASLt through torch.mm)
+  wgrad  native MFMA weight gradient (vgpu.ops.conv.conv2d_wgrad: transposed LDS
+         reads, split-K over pixels); the earlier 1x1-as-hipBLASLt-GEMM candidate
+         (dW = dyᵀ·x) measured 3.4x slower than MIOpen (profiles/convtrain_r1.md)
 One JSON line per layer plus a total line.
 """
 from __future__ import annotations
@@ -58,15 +60,12 @@ def main(argv=None) -> int:
             ref = bw(dy, x, wt, *common, [True, False, False])[0]
             got = C.conv2d(dy, wt_t, stride=1, padding=ks - 1 - pad)
             r["dgrad_err"] = ((got.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
-        if ks == 1:
-            xs = x if stride == 1 else x[:, :, ::stride, ::stride]
-
-            def wg():
-                xm = xs.permute(0, 2, 3, 1).reshape(-1, c)
-                return torch.mm(dy.permute(0, 2, 3, 1).reshape(-1, cout).t(), xm)
-            r["mm_wgrad"] = timeit(wg)
+        r["nat_wgrad"] = timeit(lambda: C.conv2d_wgrad(dy, x, ks, stride=stride, padding=pad))
+        ref = bw(dy, x, wt, *common, [False, True, False])[1]
+        got = C.conv2d_wgrad(dy, x, ks, stride=stride, padding=pad)
+        r["wgrad_err"] = ((got.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
         for k, v in list(r.items()):
-            if k.startswith(("mio_", "nat_", "mm_")):
+            if k.startswith(("mio_", "nat_")):
                 r[k] = round(v, 1)
                 tot[k] = tot.get(k, 0.0) + v
         print(json.dumps(r), flush=True)

@@ -67,6 +67,10 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_bn_workspace.restype = i64
     lib.vgpu_bn_act_fwd_train.argtypes = [vp] * 9 + [i64, ci, cf, cf, ci, ci, vp]
     lib.vgpu_bn_act_bwd.argtypes = [vp] * 10 + [i64, ci, ci, ci, vp]
+    lib.vgpu_conv_wgrad_workspace.argtypes = [ci] * 8
+    lib.vgpu_conv_wgrad_workspace.restype = i64
+    lib.vgpu_conv_wgrad_nhwc.argtypes = [vp] * 4 + [i64] + [ci] * 8 + [vp]
+    lib.vgpu_conv_wgrad_nhwc.restype = ci
     for f in ("vgpu_bn_act_fwd_train", "vgpu_bn_act_bwd","vgpu_census", "vgpu_busy", "vgpu_gather_pages", "vgpu_scatter_pages",
               "vgpu_fill_pattern", "vgpu_verify_pattern", "vgpu_kernels_abi_version",
               "vgpu_bias_act_nhwc", "vgpu_scale_shift_act_nhwc", "vgpu_add_scale_shift_act_nhwc",

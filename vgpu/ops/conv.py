@@ -229,10 +229,51 @@ def scale_shift_relu_mean(x: torch.Tensor, scale: torch.Tensor, shift: torch.Ten
 _TRAIN_NATIVE = os.environ.get("VGPU_NATIVE_CONV_TRAIN", "1") != "0"
 
 
+def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, ks: int, *, stride: int = 1,
+                 padding: int = 0) -> torch.Tensor:
+    """Weight gradient of y = conv2d(x, w, stride, padding) for a [Cout, C, ks, ks]
+    channels_last bf16 weight, on the MFMA kernel (native/kernels/conv_wgrad.hip:
+    split-K over output pixels, fp32 partials, deterministic reduce).
+    dy [N,Cout,OH,OW] and x [N,C,H,W] bf16 channels_last; C, Cout multiples of 64."""
+    _nhwc(dy, "dy")
+    _nhwc(x, "x")
+    n, c, h, wd = x.shape
+    cout = dy.shape[1]
+    if c % 64 or cout % 64 or dy.shape[0] != n or tuple(dy.shape[2:]) != out_hw(h, wd, ks, stride, padding):
+        raise ValueError(f"unsupported wgrad: dy {tuple(dy.shape)} x {tuple(x.shape)} ks {ks}")
+    lib = load_kernels()
+    need = lib.vgpu_conv_wgrad_workspace(n, h, wd, c, cout, ks, stride, padding)
+    if need < 0:
+        raise ValueError("unsupported wgrad shape")
+    ws = torch.empty(max(need // 4, 1), dtype=torch.float32, device=x.device)
+    dw = torch.empty((cout, c, ks, ks), dtype=x.dtype, device=x.device, memory_format=_CL)
+    rc = lib.vgpu_conv_wgrad_nhwc(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), need, n, h, wd, c, cout,
+                                  ks, stride, padding, _stream())
+    if rc != 0:
+        raise RuntimeError(f"vgpu_conv_wgrad_nhwc: error {rc}")
+    return dw
+
+
+# Weight gradient in training: the native kernel where it measured ahead of
+# MIOpen (1x1 convolutions over ≥ 32k output pixels — few output tiles, a long
+# pixel reduction: ResNet stages 1-2 at ai-benchmark sizes; profiles/wgrad_r1.md),
+# MIOpen elsewhere.  VGPU_CONV_WGRAD=0: always MIOpen; =all: always native.
+_WGRAD_MODE = os.environ.get("VGPU_CONV_WGRAD", "auto")
+
+
+def _wgrad_native(dy: torch.Tensor, ks: int) -> bool:
+    if _WGRAD_MODE == "0":
+        return False
+    if _WGRAD_MODE == "all":
+        return True
+    return ks == 1 and dy.shape[0] * dy.shape[2] * dy.shape[3] >= 32768
+
+
 class _ConvTrainFn(torch.autograd.Function):
     """y = conv(x, w) (+ residual) on the MFMA kernel; backward: dx on the same
     kernel (stride 1: the data gradient is a stride-1 convolution of dy with the
-    transposed, spatially flipped filter and padding k-1-p), dw from MIOpen.
+    transposed, spatially flipped filter and padding k-1-p), dw on the native
+    weight-gradient kernel where it wins (_wgrad_native), else MIOpen.
     Per-layer timings that motivated the split: profiles/convtrain_r1.md."""
 
     @staticmethod
@@ -252,6 +293,7 @@ class _ConvTrainFn(torch.autograd.Function):
         common = ([0], [s, s], [p, p], [1, 1], False, [0, 0], 1)
         bw = torch.ops.aten.convolution_backward
         dx = dw = None
+        native_dw = need_dw and _wgrad_native(dy, w.shape[2])
         if s == 1:
             if need_dx:
                 ks = w.shape[2]
@@ -259,10 +301,12 @@ class _ConvTrainFn(torch.autograd.Function):
                 if ks > 1:
                     wt = wt.flip(2, 3)
                 dx = conv2d(dy, wt.contiguous(memory_format=_CL), stride=1, padding=ks - 1 - p)
-            if need_dw:
-                dw = bw(dy, x, w, *common, [False, True, False])[1]
-        elif need_dx or need_dw:
-            dx, dw, _ = bw(dy, x, w, *common, [need_dx, need_dw, False])
+        elif need_dx:
+            dx, dw, _ = bw(dy, x, w, *common, [True, need_dw and not native_dw, False])
+        if native_dw:
+            dw = conv2d_wgrad(dy, x, w.shape[2], stride=s, padding=p)
+        elif need_dw and dw is None:
+            dw = bw(dy, x, w, *common, [False, True, False])[1]
         dres = dy if ctx.has_res and ctx.needs_input_grad[2] else None
         return dx, dw, dres, None, None
 
