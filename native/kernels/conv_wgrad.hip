@@ -25,6 +25,7 @@
 // prefetch two steps ahead, double-buffered LDS, one barrier per step.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #define VGPU_API extern "C" __attribute__((visibility("default")))
 
@@ -35,6 +36,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) char lds_char;  // 32-bit LDS addressing
 
 constexpr int kThreads = 256;
 constexpr int KP = 32;                     // pixels per K step (one MFMA depth)
@@ -47,6 +49,7 @@ struct WgradArgs {
   uint16_t* dw;        // [Cout][Ktot] bf16 (written directly when splits == 1)
   int N, H, W, C, Cout, OH, OW, KS, stride, pad;
   int P, Ktot, cblocks, steps, splits;
+  int nseg;            // 3x3 tap-fused path: 32-pixel segments per output row
   uint32_t dy_bytes, x_bytes;
 };
 
@@ -58,9 +61,9 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 // Two transposed 4-pixel reads → the 8 k-values (pixels 8g..8g+7) of one
 // MFMA operand row (channel base + lane&15).  `tile` is a [KP][RS/2] bf16 image.
 template <int RS>
-__device__ __forceinline__ bf16x8_t tr_operand(const char* tile, int base_ch, int lane) {
+__device__ __forceinline__ bf16x8_t tr_operand(const lds_char* tile, int base_ch, int lane) {
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const char* a0 = tile + (8 * g + q) * RS + (base_ch + 4 * p) * 2;
+  const lds_char* a0 = tile + (8 * g + q) * RS + (base_ch + 4 * p) * 2;
   const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
   const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * RS));
   const s16x4 v[2] = {lo, hi};
@@ -139,8 +142,8 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(const WgradArgs a) {
   // Two register sets in flight: the loads of step s+2 are issued while step
   // s is multiplied, so each step's global latency is covered by two steps.
   auto mma = [&](int st) {
-    const char* sA = smem + st * STAGE;
-    const char* sB = sA + A_BYTES;
+    const lds_char* sA = (const lds_char*)smem + st * STAGE;
+    const lds_char* sB = sA + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < KP / 32; ++kk) {  // 32 pixels per MFMA depth
       bf16x8_t af[TM], bf[TN];
@@ -237,6 +240,159 @@ __global__ void __launch_bounds__(kThreads) wgrad_reduce_kernel(const float* __r
   }
 }
 
+// 3x3 (pad 1) weight gradient with the nine taps fused: a K step is one
+// 32-pixel segment of one output row; the block stages that segment of dy once
+// and the x halo the nine taps need (3 input rows × (32·S + 2) columns) once,
+// and feeds each tap's B operand from the same halo through per-lane row
+// addresses of the transposing read (pixel j of tap (kh, kw) is halo row
+// kh·HC + j·S + kw).  Versus nine independent GEMMs: dy is read once instead of
+// nine times and x ≈ 3× instead of 9×, and each barrier covers 36 MFMAs per
+// wave instead of 4.
+template <int STRIDE>
+__device__ __forceinline__ bf16x8_t tr_halo(const lds_char* halo, int kh, int kw, int base_ch, int lane) {
+  constexpr int HC = 32 * STRIDE + 2, RS = 128;
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const lds_char* a0 = halo + (kh * HC + (8 * g + q) * STRIDE + kw) * RS + (base_ch + 4 * p) * 2;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * STRIDE * RS));
+  const s16x4 v[2] = {lo, hi};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+template <int STRIDE>
+__global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(const WgradArgs a) {
+  constexpr int RS = 128;                          // LDS row: 64 bf16 channels
+  constexpr int HC = 32 * STRIDE + 2, HROWS = 3 * HC;
+  constexpr int LX = (HROWS * 8 + kThreads - 1) / kThreads;
+  // halo image padded to LX·256 chunks: every thread's LDS store is in bounds
+  // (no branch around it; the pad rows hold zeros and are never read)
+  constexpr int DY_BYTES = KP * RS, STAGE = DY_BYTES + LX * kThreads * 16;
+  constexpr int TM = 2, TN = 2;                    // 64x64 tile, 2x2 waves of 32x32
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int cb = blockIdx.x, m0 = blockIdx.y * 64, split = blockIdx.z;
+  const int step0 = split * a.steps;
+  const int per_img = a.OH * a.nseg;
+  const int total = a.N * per_img;
+
+  const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.dy), 0, a.dy_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.x), 0, a.x_bytes, 0x00020000);
+
+  u32x4 rd0, rd1, rx0[LX], rx1[LX];
+  auto load = [&](int step, u32x4& rd, u32x4 (&rx)[LX]) {
+    const int seg = step0 + step;
+    const bool vs = seg < total;
+    const int n = seg / per_img, rem = seg - n * per_img, oh = rem / a.nseg;
+    const int ow0 = (rem - oh * a.nseg) * 32;
+    {
+      const int r = t >> 3, ch = t & 7, ow = ow0 + r;
+      const bool ok = vs & (ow < a.OW);
+      rd = __builtin_amdgcn_raw_buffer_load_b128(
+          dyr, ok ? (uint32_t)(((((int64_t)n * a.OH + oh) * a.OW + ow) * a.Cout + m0 + ch * 8) * 2) : kOOB,
+          0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < LX; ++i) {
+      const int idx = t + i * kThreads, hr = idx >> 3, ch = idx & 7;
+      const int kh = hr / HC, col = hr - kh * HC;
+      const int ih = oh * STRIDE - a.pad + kh, iw = ow0 * STRIDE - a.pad + col;
+      const bool ok = vs & (idx < HROWS * 8) & ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
+      rx[i] = __builtin_amdgcn_raw_buffer_load_b128(
+          xr, ok ? (uint32_t)(((((int64_t)n * a.H + ih) * a.W + iw) * a.C + cb * 64 + ch * 8) * 2) : kOOB,
+          0, 0);
+    }
+  };
+  auto store = [&](int st, const u32x4& rd, const u32x4 (&rx)[LX]) {
+    char* sD = smem + st * STAGE;
+    char* sX = sD + DY_BYTES;
+    *reinterpret_cast<u32x4*>(sD + (t >> 3) * RS + (t & 7) * 16) = rd;
+#pragma unroll
+    for (int i = 0; i < LX; ++i) {
+      const int idx = t + i * kThreads;
+      *reinterpret_cast<u32x4*>(sX + (idx >> 3) * RS + (idx & 7) * 16) = rx[i];
+    }
+  };
+
+  f32x4_t acc[9][TM][TN];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[k][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto mma = [&](int st) {
+    const lds_char* sD = (const lds_char*)smem + st * STAGE;
+    const lds_char* sX = sD + DY_BYTES;
+    bf16x8_t af[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = tr_operand<RS>(sD, wm * 32 + i * 16, lane);
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        bf16x8_t bf[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bf[j] = tr_halo<STRIDE>(sX, kh, kw, wn * 32 + j * 16, lane);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[kh * 3 + kw][i][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[kh * 3 + kw][i][j], 0, 0, 0);
+        // keep one tap's operands live at a time (unbounded hoisting of the 36
+        // transposed reads spills the 144 accumulator registers)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+  };
+
+  const int nsteps = min(a.steps, total - step0);
+  if (nsteps > 0) load(0, rd0, rx0);
+  if (nsteps > 1) load(1, rd1, rx1);
+  for (int s = 0; s < nsteps; s += 2) {
+    store(0, rd0, rx0);
+    __syncthreads();
+    if (s + 2 < nsteps) load(s + 2, rd0, rx0);
+    mma(0);
+    if (s + 1 >= nsteps) break;
+    store(1, rd1, rx1);
+    __syncthreads();
+    if (s + 3 < nsteps) load(s + 3, rd1, rx1);
+    mma(1);
+  }
+
+  // One uniform branch, then straight-line stores.
+  const int64_t lane_off = (int64_t)(m0 + wm * 32 + fk * 4) * a.Ktot + cb * 64 + wn * 32 + fr;
+  if (a.splits == 1) {
+    uint16_t* out = a.dw + lane_off;
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            out[(i * 16 + e) * a.Ktot + k * a.C + j * 16] = f2bf(acc[k][i][j][e]);
+  } else {
+    float* out = a.ws + (int64_t)split * a.Cout * a.Ktot + lane_off;
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            out[(i * 16 + e) * a.Ktot + k * a.C + j * 16] = acc[k][i][j][e];
+  }
+}
+
 template <int BM, int BN>
 hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((wgrad_kernel<BM, BN>), dim3(a.Ktot / BN, a.Cout / BM, a.splits), dim3(kThreads),
@@ -247,14 +403,24 @@ hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s) {
 }  // namespace
 
 namespace {
+int g_wgrad3 = -1;  // VGPU_CONV_WGRAD3=0 disables the tap-fused 3x3 path (A/B)
+bool wgrad3_eligible(int KS, int stride, int pad) {
+  if (g_wgrad3 < 0) {
+    const char* v = getenv("VGPU_CONV_WGRAD3");
+    g_wgrad3 = (v && v[0] == '0') ? 0 : 1;
+  }
+  return g_wgrad3 == 1 && KS == 3 && pad == 1 && (stride == 1 || stride == 2);
+}
+
 // Split-K factor for a shape; -1 = unsupported.
 int64_t wgrad_splits(int N, int H, int W, int C, int Cout, int KS, int stride, int pad) {
   const int OH = (H + 2 * pad - KS) / stride + 1, OW = (W + 2 * pad - KS) / stride + 1;
   if (OH < 1 || OW < 1 || C % 64 || Cout % 64) return -1;
   const int64_t P = (int64_t)N * OH * OW;
-  const int bm = Cout % 128 == 0 ? 128 : 64, bn = C % 128 == 0 ? 128 : 64;
-  const int64_t tiles = (int64_t)(KS * KS * C / bn) * (Cout / bm);
-  const int64_t steps_total = (P + KP - 1) / KP;
+  const bool fused3 = wgrad3_eligible(KS, stride, pad);
+  const int bm = fused3 ? 64 : Cout % 128 == 0 ? 128 : 64, bn = fused3 ? 64 : C % 128 == 0 ? 128 : 64;
+  const int64_t tiles = fused3 ? (int64_t)(C / 64) * (Cout / 64) : (int64_t)(KS * KS * C / bn) * (Cout / bm);
+  const int64_t steps_total = fused3 ? (int64_t)N * OH * ((OW + 31) / 32) : (P + KP - 1) / KP;
   // Split count from a small cost model (µs): the K loop of a split is
   // latency-bound (t_step per step plus ≈ 3 µs fixed), splits run
   // `slots` at a time (resident workgroups: 4 waves each, occupancy per tile
@@ -262,10 +428,11 @@ int64_t wgrad_splits(int N, int H, int W, int C, int Cout, int KS, int stride, i
   // tile written and re-read in fp32 at ≈ 4 TB/s.  Few output tiles over many
   // pixels (stage 1) want hundreds of splits; big tiles over few pixels
   // (stage 4) want 1-2, or the workspace traffic dominates.
-  const int occ = (bm == 128 && bn == 128) ? 2 : (bm == 128 || bn == 128) ? 4 : 7;
+  const int occ = fused3 ? 1 : (bm == 128 && bn == 128) ? 2 : (bm == 128 || bn == 128) ? 4 : 7;
   const double slots = occ * 256.0, tile_bytes = (double)Cout * KS * KS * C * 4;
-  // µs per K step: latency plus the step's bytes (KP·(BM+BN)·2) at a CU's fill rate
-  const double t_step = 0.4 + KP * (bm + bn) * 2 / 16384.0 * 0.6;
+  // µs per K step: latency plus the step's bytes (KP·(BM+BN)·2) at a CU's fill
+  // rate; the fused 3x3 step carries nine taps' MFMAs
+  const double t_step = fused3 ? 0.8 + 0.4 * stride : 0.4 + KP * (bm + bn) * 2 / 16384.0 * 0.6;
   int64_t splits = 1;
   double best = 1e30;
   for (int64_t sp = 1; sp <= 1024 && sp <= (steps_total + 3) / 4; sp *= 2) {
@@ -316,13 +483,23 @@ VGPU_API int vgpu_conv_wgrad_nhwc(const void* dy, const void* x, void* dw, void*
   if (sp < 1 || ws_bytes < (sp == 1 ? 0 : sp * Cout * (int64_t)a.Ktot * 4)) return -1;
   a.splits = (int)sp;
   a.dw = static_cast<uint16_t*>(dw);
-  const int64_t steps_total = (P + KP - 1) / KP;
-  a.steps = (int)((steps_total + a.splits - 1) / a.splits);
   hipError_t e;
-  if (bm == 128 && bn == 128) e = launch_wgrad<128, 128>(a, s);
-  else if (bm == 128) e = launch_wgrad<128, 64>(a, s);
-  else if (bn == 128) e = launch_wgrad<64, 128>(a, s);
-  else e = launch_wgrad<64, 64>(a, s);
+  if (wgrad3_eligible(KS, stride, pad)) {
+    a.nseg = (a.OW + 31) / 32;
+    const int64_t steps_total = (int64_t)N * a.OH * a.nseg;
+    a.steps = (int)((steps_total + a.splits - 1) / a.splits);
+    const dim3 grid(C / 64, Cout / 64, a.splits);
+    if (stride == 1) hipLaunchKernelGGL((wgrad3_kernel<1>), grid, dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((wgrad3_kernel<2>), grid, dim3(kThreads), 0, s, a);
+    e = hipGetLastError();
+  } else {
+    const int64_t steps_total = (P + KP - 1) / KP;
+    a.steps = (int)((steps_total + a.splits - 1) / a.splits);
+    if (bm == 128 && bn == 128) e = launch_wgrad<128, 128>(a, s);
+    else if (bm == 128) e = launch_wgrad<128, 64>(a, s);
+    else if (bn == 128) e = launch_wgrad<64, 128>(a, s);
+    else e = launch_wgrad<64, 64>(a, s);
+  }
   if (e != hipSuccess) return (int)e;
   if (a.splits == 1) return 0;  // the K loop wrote bf16 directly
   const int64_t n4 = (int64_t)Cout * a.Ktot / 4;

@@ -17,7 +17,7 @@ run() {
   return $rc
 }
 T="python bench.py --workload 1.2 --steps 20 --warmup 5 --no-cap-probe --pods 1 --gpucores 100 --gpumem 0"
-for r in 1 2 3; do
+for r in 1 2; do
   run nat_$r $T || exit 1
   VGPU_CONV_WGRAD=0 run mio_$r $T || exit 1
   VGPU_CONV_WGRAD=all run all_$r $T || exit 1

@@ -222,9 +222,11 @@ WGRAD_CASES = [
     (4, 64, 33, 31, 256, 1, 1, 0),      # BM=128 x BN=64, ragged pixel tail
     (3, 256, 13, 13, 64, 1, 2, 0),      # BM=64 x BN=128, strided 1x1
     (20, 64, 87, 87, 64, 3, 1, 1),      # ResNet-V2-50 stage-1 conv2 at ai-benchmark 1.2 (b=20, 346²)
-    (20, 256, 87, 87, 64, 1, 1, 0),     # stage-1 conv1: 1024 splits
+    (20, 256, 87, 87, 64, 1, 1, 0),     # stage-1 conv1: hundreds of splits
     (3, 64, 9, 9, 64, 1, 1, 0),         # one split, odd step count
     (2, 512, 11, 11, 512, 3, 1, 1),     # deep columns, few pixels
+    (2, 128, 40, 37, 192, 3, 1, 1),     # tap-fused 3x3: ragged 32-pixel row segments
+    (2, 64, 33, 35, 128, 3, 2, 1),      # tap-fused 3x3, stride 2, odd sizes
 ]
 
 

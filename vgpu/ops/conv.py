@@ -255,18 +255,20 @@ def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, ks: int, *, stride: int = 1,
 
 
 # Weight gradient in training: the native kernel where it measured ahead of
-# MIOpen (1x1 convolutions over ≥ 32k output pixels — few output tiles, a long
-# pixel reduction: ResNet stages 1-2 at ai-benchmark sizes; profiles/wgrad_r1.md),
+# MIOpen — few output tiles over a long pixel reduction: 1x1 convolutions over
+# ≥ 32k output pixels (ResNet stages 1-2 at ai-benchmark sizes) and stride-1
+# 3x3 over ≥ 64k (stage 1, on the tap-fused kernel); profiles/wgrad_r1.md.
 # MIOpen elsewhere.  VGPU_CONV_WGRAD=0: always MIOpen; =all: always native.
 _WGRAD_MODE = os.environ.get("VGPU_CONV_WGRAD", "auto")
 
 
-def _wgrad_native(dy: torch.Tensor, ks: int) -> bool:
+def _wgrad_native(dy: torch.Tensor, ks: int, stride: int) -> bool:
     if _WGRAD_MODE == "0":
         return False
     if _WGRAD_MODE == "all":
         return True
-    return ks == 1 and dy.shape[0] * dy.shape[2] * dy.shape[3] >= 32768
+    pixels = dy.shape[0] * dy.shape[2] * dy.shape[3]
+    return (ks == 1 and pixels >= 32768) or (ks == 3 and stride == 1 and pixels >= 65536)
 
 
 class _ConvTrainFn(torch.autograd.Function):
@@ -293,7 +295,7 @@ class _ConvTrainFn(torch.autograd.Function):
         common = ([0], [s, s], [p, p], [1, 1], False, [0, 0], 1)
         bw = torch.ops.aten.convolution_backward
         dx = dw = None
-        native_dw = need_dw and _wgrad_native(dy, w.shape[2])
+        native_dw = need_dw and _wgrad_native(dy, w.shape[2], s)
         if s == 1:
             if need_dx:
                 ks = w.shape[2]
