@@ -276,16 +276,21 @@ __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const bf16x8* __rest
   }
 }
 
-template <int kAct>
+// kAdd: dx += add (a second gradient of x, e.g. the identity shortcut's),
+// summed in fp32 before the one bf16 rounding — replaces an autograd add pass.
+template <int kAct, bool kAdd>
 __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const bf16x8* __restrict__ dy,
                                                                 const bf16x8* __restrict__ x,
                                                                 bf16x8* __restrict__ dx,
                                                                 const float* __restrict__ coef,
+                                                                const bf16x8* __restrict__ add,
                                                                 uint64_t nvec, uint32_t cvec) {
   const uint32_t C = cvec * 8;
   VGPU_BN_GRID_LOOP(i, ci, nvec, cvec) {
     const bf16x8 v = x[i];
     const bf16x8 g = dy[i];
+    bf16x8 r;
+    if constexpr (kAdd) r = add[i];
     float s[8], t[8], cc[8], b[8];
     load8(coef + ci * 8, s);
     load8(coef + C + ci * 8, t);
@@ -296,7 +301,9 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const bf16x8* __
     for (int k = 0; k < 8; ++k) {
       const float xf = bf2f(v.v[k]);
       const float dz = bf2f(g.v[k]) * act_grad<kAct>(fmaf(xf, s[k], t[k]));
-      o.v[k] = f2bf(fmaf(s[k], dz, fmaf(cc[k], xf, b[k])));
+      float d = fmaf(s[k], dz, fmaf(cc[k], xf, b[k]));
+      if constexpr (kAdd) d += bf2f(r.v[k]);
+      o.v[k] = f2bf(d);
     }
     dx[i] = o;
   }
@@ -360,7 +367,7 @@ int fwd_train(const void* x, void* y, const void* gamma, const void* beta, void*
 template <int kAct, typename P>
 void bwd_launch(const bf16x8* dyv, const bf16x8* xv, bf16x8* dxv, const P* gamma, const P* beta,
                 const float* mean, const float* invstd, P* dgamma, P* dbeta, float* ws, int64_t M, int C,
-                hipStream_t s) {
+                const bf16x8* addv, hipStream_t s) {
   const Plan p = make_plan(M, C);
   auto* partial = reinterpret_cast<float2*>(ws);
   float* coef = ws + 2 * p.G * C;
@@ -369,13 +376,19 @@ void bwd_launch(const bf16x8* dyv, const bf16x8* xv, bf16x8* dxv, const P* gamma
   hipLaunchKernelGGL((bn_bwd_finalize_kernel<P>), dim3((C + kFinC - 1) / kFinC), dim3(kFinC * kFinG), 0, s,
                      partial, p.G, gamma, beta, mean, invstd, dgamma, dbeta, coef, M, C);
   const uint64_t nvec = (uint64_t)M * (C / 8);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel<kAct>, dim3(grid_for(nvec)), dim3(kThreads), 0, s, dyv, xv, dxv,
-                     coef, nvec, C / 8);
+  if (addv)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<kAct, true>), dim3(grid_for(nvec)), dim3(kThreads), 0, s, dyv, xv,
+                       dxv, coef, addv, nvec, C / 8);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<kAct, false>), dim3(grid_for(nvec)), dim3(kThreads), 0, s, dyv, xv,
+                       dxv, coef, addv, nvec, C / 8);
 }
 
 template <typename P>
 int bwd(const void* dy, const void* x, void* dx, const void* gamma, const void* beta, const float* mean,
-        const float* invstd, void* dgamma, void* dbeta, float* ws, int64_t M, int C, int act, hipStream_t s) {
+        const float* invstd, void* dgamma, void* dbeta, float* ws, int64_t M, int C, int act, const void* add,
+        hipStream_t s) {
+  const auto* addv = static_cast<const bf16x8*>(add);
   const auto* dyv = static_cast<const bf16x8*>(dy);
   const auto* xv = static_cast<const bf16x8*>(x);
   auto* dxv = static_cast<bf16x8*>(dx);
@@ -384,9 +397,9 @@ int bwd(const void* dy, const void* x, void* dx, const void* gamma, const void* 
   auto* dg = static_cast<P*>(dgamma);
   auto* db = static_cast<P*>(dbeta);
   switch (act) {
-    case 0: bwd_launch<0, P>(dyv, xv, dxv, g, b, mean, invstd, dg, db, ws, M, C, s); break;
-    case 1: bwd_launch<1, P>(dyv, xv, dxv, g, b, mean, invstd, dg, db, ws, M, C, s); break;
-    case 2: bwd_launch<2, P>(dyv, xv, dxv, g, b, mean, invstd, dg, db, ws, M, C, s); break;
+    case 0: bwd_launch<0, P>(dyv, xv, dxv, g, b, mean, invstd, dg, db, ws, M, C, addv, s); break;
+    case 1: bwd_launch<1, P>(dyv, xv, dxv, g, b, mean, invstd, dg, db, ws, M, C, addv, s); break;
+    case 2: bwd_launch<2, P>(dyv, xv, dxv, g, b, mean, invstd, dg, db, ws, M, C, addv, s); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
@@ -419,13 +432,21 @@ VGPU_API int vgpu_bn_act_fwd_train(const void* x, void* y, const void* gamma, co
 
 // dx, dgamma, dbeta of y = act(batchnorm_train(x)) given dy and the saved
 // mean / invstd.  dgamma / dbeta may be null.
+// `add` (nullable, bf16 like dx): a second gradient of x summed into dx.
+VGPU_API int vgpu_bn_act_bwd_add(const void* dy, const void* x, void* dx, const void* gamma, const void* beta,
+                                 const float* mean, const float* invstd, void* dgamma, void* dbeta, float* ws,
+                                 int64_t M, int C, int act, int param_bf16, const void* add, void* stream) {
+  if (!shape_ok(M, C) || !aligned16(dy) || !aligned16(x) || !aligned16(dx) || !aligned16(ws) || !mean ||
+      !invstd || (add && !aligned16(add)))
+    return (int)hipErrorInvalidValue;
+  auto s = (hipStream_t)stream;
+  if (param_bf16) return bwd<uint16_t>(dy, x, dx, gamma, beta, mean, invstd, dgamma, dbeta, ws, M, C, act, add, s);
+  return bwd<float>(dy, x, dx, gamma, beta, mean, invstd, dgamma, dbeta, ws, M, C, act, add, s);
+}
+
 VGPU_API int vgpu_bn_act_bwd(const void* dy, const void* x, void* dx, const void* gamma, const void* beta,
                              const float* mean, const float* invstd, void* dgamma, void* dbeta, float* ws,
                              int64_t M, int C, int act, int param_bf16, void* stream) {
-  if (!shape_ok(M, C) || !aligned16(dy) || !aligned16(x) || !aligned16(dx) || !aligned16(ws) || !mean ||
-      !invstd)
-    return (int)hipErrorInvalidValue;
-  auto s = (hipStream_t)stream;
-  if (param_bf16) return bwd<uint16_t>(dy, x, dx, gamma, beta, mean, invstd, dgamma, dbeta, ws, M, C, act, s);
-  return bwd<float>(dy, x, dx, gamma, beta, mean, invstd, dgamma, dbeta, ws, M, C, act, s);
+  return vgpu_bn_act_bwd_add(dy, x, dx, gamma, beta, mean, invstd, dgamma, dbeta, ws, M, C, act, param_bf16,
+                             nullptr, stream);
 }

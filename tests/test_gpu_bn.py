@@ -168,3 +168,48 @@ def test_resnet_training_step_native_matches_pytorch(B, monkeypatch):
     print("median rel err native %.3f pytorch %.3f; max native %.3f pytorch %.3f"
           % (en_all[len(en_all) // 2], et_all[len(et_all) // 2], en_all[-1], et_all[-1]))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("act", ["relu", "none"])
+def test_bn_act_res_sums_shortcut_gradient(B, act):
+    """bn_act_res: (act(bn(x)), x) with the shortcut's gradient summed into the
+    BN backward's dx in-kernel — equals bn_act + autograd's separate add."""
+    import copy
+    from torch import nn
+    bn = nn.BatchNorm2d(256).cuda().to(torch.bfloat16).train()
+    bn2 = copy.deepcopy(bn)
+    x = _x((4, 256, 17, 13), 21).requires_grad_()
+    y, xr = B.bn_act_res(x, bn, act)
+    assert torch.equal(xr, x.detach())
+    gy, gr = _x(tuple(y.shape), 22), _x(tuple(x.shape), 23)
+    torch.autograd.backward([y, xr], [gy, gr])
+    x2 = x.detach().clone().requires_grad_()
+    y2 = B.bn_act(x2, bn2, act)
+    torch.testing.assert_close(y, y2)
+    torch.autograd.backward([y2, x2 * 1], [gy, gr])
+    _close_most(x.grad, x2.grad, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(bn.weight.grad, bn2.weight.grad)
+    assert int(bn.num_batches_tracked) == int(bn2.num_batches_tracked) == 1
+
+
+def test_resnet_identity_blocks_fused_shortcut_gradient(B, monkeypatch):
+    """A ResNet-V2 with identity blocks: the training step with the fused
+    shortcut gradient matches the same native model with autograd's add."""
+    import copy
+    from vgpu.models import resnet as R
+    torch.manual_seed(0)
+    m = R.ResNetV2([2, 1, 1, 1]).cuda().to(memory_format=CL).to(torch.bfloat16).train()
+    m2 = copy.deepcopy(m)
+    x = _x((2, 3, 64, 64), 9)
+
+    def grads(model):
+        model.zero_grad(set_to_none=True)
+        model(x).float().logsumexp(-1).sum().backward()
+        return {k: p.grad.float().clone() for k, p in model.named_parameters()}
+
+    g = grads(m)
+    monkeypatch.setattr(R, "bn_act_res", lambda x_, bn, act="relu": (B.bn_act(x_, bn, act), x_))
+    g2 = grads(m2)
+    for k in g:
+        cos = torch.nn.functional.cosine_similarity(g[k].flatten(), g2[k].flatten(), dim=0).item()
+        assert cos > 0.999, (k, cos)

@@ -38,3 +38,21 @@ def test_resnet_v2_training_step_cpu():
     loss.backward()
     assert all(p.grad is not None for p in m.parameters())
     assert int(m.blocks[0].bn_in.num_batches_tracked) == 1
+
+
+def test_batched_step_counters_match_per_layer_updates():
+    """num_batches_tracked deferred to one multi-tensor add per forward: same
+    values as the per-layer update, nested blocks flush once."""
+    import torch
+    from torch import nn
+    from vgpu.ops import bn as B
+
+    mods = [nn.BatchNorm2d(8) for _ in range(3)]
+    with B.batched_step_counters():
+        for m in mods:
+            B._counters.pending.append(m.num_batches_tracked)
+        with B.batched_step_counters():
+            B._counters.pending.append(mods[0].num_batches_tracked)
+        assert all(int(m.num_batches_tracked) == 0 for m in mods)  # deferred
+    assert [int(m.num_batches_tracked) for m in mods] == [2, 1, 1]
+    assert getattr(B._counters, "pending", None) is None

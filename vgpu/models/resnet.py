@@ -15,7 +15,7 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
-from vgpu.ops.bn import bn_act
+from vgpu.ops.bn import batched_step_counters, bn_act, bn_act_res
 from vgpu.ops.conv import conv_train
 
 
@@ -37,7 +37,11 @@ class PreActBottleneck(nn.Module):
         self.fused = False
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        pre = bn_act(x, self.bn_in)
+        if self.shortcut is None and not self.fused and torch.is_grad_enabled():
+            # identity shortcut: its gradient is summed into bn_in's backward
+            pre, x = bn_act_res(x, self.bn_in)
+        else:
+            pre = bn_act(x, self.bn_in)
         if self.fused:
             sc = self.shortcut(pre) if self.shortcut is not None else x
             y = F.relu(self.conv1(pre))
@@ -85,9 +89,10 @@ class ResNetV2(nn.Module):
                 nn.init.zeros_(m.bias)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.pool(self.stem(x))
-        x = self.blocks(x)
-        x = bn_act(x, self.bn_out)
+        with batched_step_counters():
+            x = self.pool(self.stem(x))
+            x = self.blocks(x)
+            x = bn_act(x, self.bn_out)
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)
 

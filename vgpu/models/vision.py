@@ -13,7 +13,7 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
-from vgpu.ops.bn import bn_act
+from vgpu.ops.bn import batched_step_counters, bn_act
 
 
 class VGG16(nn.Module):
@@ -168,7 +168,8 @@ class DeepLabV3(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         h, w = x.shape[-2:]
-        y = self.head(self.aspp(self.backbone(x)))
+        with batched_step_counters():
+            y = self.head(self.aspp(self.backbone(x)))
         return F.interpolate(y, size=(h, w), mode="bilinear", align_corners=False)
 
 

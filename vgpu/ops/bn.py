@@ -17,8 +17,10 @@ numerics reference (tests/test_gpu_bn.py).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
+import threading
 
 import torch
 import torch.nn.functional as F
@@ -59,7 +61,8 @@ def _workspace(lib, m: int, c: int, device) -> torch.Tensor:
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum: float, eps: float, act: int):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum: float, eps: float, act: int,
+                res_out: bool = False):
         lib = load_kernels()
         n, c, h, w = x.shape
         m = n * h * w
@@ -76,10 +79,15 @@ class _BNActFn(torch.autograd.Function):
         ctx.save_for_backward(x, weight, bias, mean, invstd)
         ctx.act = act
         ctx.pb = pb
+        if res_out:
+            # x again, as an output of this node: the gradient it receives (an
+            # identity shortcut's) is summed into dx by the backward kernel
+            # instead of by a separate autograd add pass over the activation.
+            return y, x.view_as(x)
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dres=None):
         x, weight, bias, mean, invstd = ctx.saved_tensors
         lib = load_kernels()
         dy = dy.contiguous(memory_format=_CL)
@@ -88,12 +96,15 @@ class _BNActFn(torch.autograd.Function):
         dx = torch.empty_like(x, memory_format=_CL)
         dw = torch.empty_like(weight) if weight is not None and ctx.needs_input_grad[1] else None
         db = torch.empty_like(bias) if bias is not None and ctx.needs_input_grad[2] else None
-        rc = lib.vgpu_bn_act_bwd(
+        if dres is not None:
+            dres = dres.contiguous(memory_format=_CL)
+        rc = lib.vgpu_bn_act_bwd_add(
             _ptr(dy), _ptr(x), _ptr(dx), _ptr(weight), _ptr(bias), _ptr(mean), _ptr(invstd),
-            _ptr(dw), _ptr(db), _ptr(_workspace(lib, m, c, x.device)), m, c, ctx.act, ctx.pb, _stream())
+            _ptr(dw), _ptr(db), _ptr(_workspace(lib, m, c, x.device)), m, c, ctx.act, ctx.pb, _ptr(dres),
+            _stream())
         if rc != 0:
             raise RuntimeError(f"vgpu_bn_act_bwd: hipError {rc}")
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
 def native_eligible(x: torch.Tensor, bn: nn.BatchNorm2d) -> bool:
@@ -112,6 +123,28 @@ def _act(y: torch.Tensor, act: str) -> torch.Tensor:
     return y
 
 
+_counters = threading.local()
+
+
+@contextlib.contextmanager
+def batched_step_counters():
+    """Defer every native BN's `num_batches_tracked += 1` inside the block to one
+    multi-tensor add at exit: one kernel per forward instead of one per layer
+    (a ResNet-V2-50 training step launched 41 of them, 190 µs of a 7.8 ms step).
+    Same counter values as the module's own update; nests (the outermost block
+    flushes)."""
+    outer = getattr(_counters, "pending", None)
+    if outer is None:
+        _counters.pending = []
+    try:
+        yield
+    finally:
+        if outer is None:
+            pend, _counters.pending = _counters.pending, None
+            if pend:
+                torch._foreach_add_(pend, 1)
+
+
 def bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, act: str = "relu") -> torch.Tensor:
     """act(bn(x)) with the module's own semantics (training statistics and
     running-stat update in train mode, running stats in eval mode)."""
@@ -121,10 +154,35 @@ def bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, act: str = "relu") -> torch.Tens
         return _act(bn(x), act)
     track = bn.track_running_stats and bn.running_mean is not None
     if track:
-        bn.num_batches_tracked.add_(1)
+        pend = getattr(_counters, "pending", None)
+        if pend is not None:
+            pend.append(bn.num_batches_tracked)
+        else:
+            bn.num_batches_tracked.add_(1)
     return _BNActFn.apply(x, bn.weight, bn.bias, bn.running_mean if track else None,
                           bn.running_var if track else None, bn.momentum if track else 0.0,
                           bn.eps, ACT[act])
+
+
+def bn_act_res(x: torch.Tensor, bn: nn.BatchNorm2d, act: str = "relu") -> tuple[torch.Tensor, torch.Tensor]:
+    """(act(bn(x)), x) for a pre-activation block whose identity shortcut is x
+    itself: use the returned x as the shortcut, and its gradient is added into
+    the BN backward's dx in the same kernel (no separate add over x).  Same
+    values as (bn_act(x, bn, act), x)."""
+    if act not in ACT:
+        raise ValueError(act)
+    if not native_eligible(x, bn):
+        return _act(bn(x), act), x
+    track = bn.track_running_stats and bn.running_mean is not None
+    if track:
+        pend = getattr(_counters, "pending", None)
+        if pend is not None:
+            pend.append(bn.num_batches_tracked)
+        else:
+            bn.num_batches_tracked.add_(1)
+    return _BNActFn.apply(x, bn.weight, bn.bias, bn.running_mean if track else None,
+                          bn.running_var if track else None, bn.momentum if track else 0.0,
+                          bn.eps, ACT[act], True)
 
 
 def bn_act_reference(x: torch.Tensor, weight, bias, running_mean, running_var, momentum: float,
