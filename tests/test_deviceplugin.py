@@ -282,3 +282,39 @@ def test_health_reset_and_recovery(cluster):
     upd = next(stream)
     assert all(d.health == api.HEALTHY for d in upd.devices)
     stream.cancel()
+
+
+def test_cdi_spec(tmp_path):
+    """N10: CDI spec — /dev/kfd shared, per-GPU render + card nodes, an 'all'
+    device, atomic write; qualified names are kind=uuid."""
+    import json
+    from vgpu.deviceplugin import cdi
+    from vgpu.deviceplugin.discovery import Device
+    devs = [Device(uuid=f"GPU-{i}", index=i, render_minor=128 + 8 * i, card=i) for i in range(2)]
+    path = cdi.write_spec(devs, str(tmp_path / "cdi"))
+    spec = json.load(open(path))
+    assert spec["kind"] == "amd.com/gpu" and spec["cdiVersion"] == cdi.CDI_VERSION
+    assert spec["containerEdits"]["deviceNodes"] == [{"path": "/dev/kfd", "permissions": "rw"}]
+    by_name = {d["name"]: d["containerEdits"]["deviceNodes"] for d in spec["devices"]}
+    assert [n["path"] for n in by_name["GPU-1"]] == ["/dev/dri/renderD136", "/dev/dri/card1"]
+    assert [n["path"] for n in by_name["all"]] == ["/dev/dri/renderD128", "/dev/dri/renderD136"]
+    assert not os.path.exists(path + ".tmp")
+    assert cdi.device_names(["GPU-0"]) == ["amd.com/gpu=GPU-0"]
+
+
+def test_allocate_cdi_strategies(cluster):
+    """device-list-strategy: cdi-cri returns CDI names instead of device nodes,
+    cdi-annotations puts them in the container annotation."""
+    from vgpu.deviceplugin.allocate import CDI_ANNOTATION
+    c = cluster
+    c["cfg"].device_list_strategy = "cdi-cri"
+    _, r = schedule_and_allocate(c, "cri", 1000, 25)
+    assert len(r.devices) == 0
+    names = [d.name for d in r.cdi_devices]
+    assert len(names) == 1 and names[0].startswith("amd.com/gpu=")
+    assert dict(r.envs)["VGPU_DEVICE_MEMORY_LIMIT_0"] == "1000m"
+    c["cfg"].device_list_strategy = "cdi-annotations"
+    _, r = schedule_and_allocate(c, "ann", 1000, 25)
+    assert len(r.devices) == 0 and len(r.cdi_devices) == 0
+    assert dict(r.annotations)[CDI_ANNOTATION].startswith("amd.com/gpu=")
+    c["cfg"].device_list_strategy = "envvar"

@@ -137,3 +137,35 @@ def test_dashboard_queries_exported_series():
             names = set(re.findall(r"[A-Za-z_][A-Za-z_]+", t["expr"])) - {"sum", "by", "rate", "increase", "m",
                                                                         "nodeid", "deviceidx"}
             assert names and names <= exported, (t["expr"], names - exported)
+
+
+def test_nodeinfo_endpoint(native_build, tmp_path, monkeypatch):
+    """V6: the reference's NodeVGPUInfo gRPC is unimplemented; ours serves the
+    same per-container view as JSON over HTTP."""
+    import json
+    import urllib.request
+    from vgpu.monitor.__main__ import serve_nodeinfo
+    srv = FakeApiServer()
+    c = KubeClient(srv.start())
+    srv.add_node("n1")
+    srv.add_pod({"metadata": {"name": "p", "namespace": "ns1", "uid": "uidA"},
+                 "spec": {"nodeName": "n1", "containers": [{"name": "main"}]}})
+    cdir = tmp_path / "containers"
+    ra = make_region(cdir / "uidA_main" / "vgpu.cache", monkeypatch, uuid="GPU-3", limit="2g", prio=0)
+    pm = PathMonitor(str(cdir), c, "n1")
+    pm.scan()
+    http = serve_nodeinfo(pm, 0, host="127.0.0.1")
+    try:
+        base = f"http://127.0.0.1:{http.server_address[1]}"
+        info = json.loads(urllib.request.urlopen(base + "/nodeinfo", timeout=10).read())
+        assert set(info) == {"uidA_main"}
+        e = info["uidA_main"]
+        assert (e["pod"], e["namespace"], e["container"], e["priority"]) == ("p", "ns1", "main", 0)
+        assert [d["uuid"] for d in e["devices"]] == ["GPU-3"]
+        assert json.loads(urllib.request.urlopen(base + "/healthz", timeout=10).read()) == {"status": "ok"}
+        with pytest.raises(urllib.error.HTTPError):
+            urllib.request.urlopen(base + "/other", timeout=10)
+    finally:
+        http.shutdown()
+        ra.close()
+        srv.stop()

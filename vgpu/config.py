@@ -52,6 +52,8 @@ class DevicePluginConfig:
     hw_queues_per_vgpu: int = 1           # GPU_MAX_HW_QUEUES for fractional vGPUs (0 = runtime default)
     hsa_tools_intercept: bool = False     # also hand the shim ROCr's API table (HSA_TOOLS_LIB)
     partition_mode: str = ""             # SPX|DPX|QPX|CPX expected compute partition ("" = as found)
+    device_list_strategy: str = "envvar"  # envvar (device nodes in the response) | cdi-annotations | cdi-cri
+    cdi_dir: str = "/var/run/cdi"
     config_file: str = "/config/config.json"
     socket_dir: str = "/var/lib/kubelet/device-plugins"
     host_lib_dir: str = "/usr/local/vgpu"

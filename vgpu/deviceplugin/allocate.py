@@ -36,6 +36,7 @@ from vgpu.k8s.nodelock import release_node_lock
 
 from vgpu.device.cualloc import CULayout
 
+from .cdi import device_names as cdi_device_names
 from .custate import CUMaskState
 from .discovery import Device
 
@@ -56,6 +57,10 @@ class ContainerGrant:
     mounts: list = field(default_factory=list)     # (container_path, host_path, read_only)
     devices: list = field(default_factory=list)    # (container_path, host_path, permissions)
     annotations: dict = field(default_factory=dict)
+    cdi_devices: list = field(default_factory=list)  # fully-qualified CDI names (cdi-cri strategy)
+
+
+CDI_ANNOTATION = "cdi.k8s.io/amd-vgpu"
 
 
 def get_pending_pod(client: KubeClient, node: str) -> dict | None:
@@ -183,6 +188,15 @@ def build_container_grant(cfg: DevicePluginConfig, pod: dict, ctr_idx: int, devr
     if ENV_DISABLE_CONTROL not in env_names and "CUDA_DISABLE_CONTROL" not in env_names:
         g.mounts.append(("/etc/ld.so.preload", f"{cfg.host_lib_dir}/{PRELOAD_FILE}", True))
     g.annotations["amd.com/vgpu-devices"] = ",".join(d.uuid for d in ordered)
+    if cfg.device_list_strategy in ("cdi-annotations", "cdi-cri"):
+        # Device nodes come from the CDI spec the plugin wrote at start
+        # (reference nvinternal/plugin/server.go:322-344 + cdi/cdi.go).
+        g.devices = []
+        names = cdi_device_names([d.uuid for d in ordered])
+        if cfg.device_list_strategy == "cdi-annotations":
+            g.annotations[CDI_ANNOTATION] = ",".join(names)
+        else:
+            g.cdi_devices = names
     return g
 
 

@@ -31,6 +31,7 @@ from vgpu.k8s.client import KubeClient
 
 from . import api
 from .allocate import AllocateError, allocate, get_pending_pod, next_device_request
+from . import cdi
 from .custate import CUMaskState
 from .discovery import EVT_POST_RESET, EVT_PRE_RESET, Backend, Device
 from .topology import link_matrix, preferred
@@ -179,6 +180,8 @@ class VGPUDevicePlugin:
                 cr.devices.add(container_path=cp, host_path=hp, permissions=perm)
             for k, v in g.annotations.items():
                 cr.annotations[k] = v
+            for name in g.cdi_devices:
+                cr.cdi_devices.add(name=name)
         return resp
 
     def PreStartContainer(self, request, context):
@@ -209,6 +212,8 @@ class VGPUDevicePlugin:
                 options=api.DevicePluginOptions(get_preferred_allocation_available=True)), timeout=5)
 
     def start(self) -> None:
+        if self.cfg.device_list_strategy.startswith("cdi"):
+            cdi.write_spec(self.devices, self.cfg.cdi_dir)
         self.serve()
         self.register()
         threading.Thread(target=self._health_loop, daemon=True, name="vgpu-health").start()

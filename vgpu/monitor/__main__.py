@@ -34,7 +34,7 @@ def node_info(pm: PathMonitor) -> dict:
             for key, cr in pm.regions.items()}
 
 
-def serve_nodeinfo(pm: PathMonitor, port: int) -> None:
+def serve_nodeinfo(pm: PathMonitor, port: int, host: str = "0.0.0.0") -> ThreadingHTTPServer:
     class H(BaseHTTPRequestHandler):
         def log_message(self, *a):
             pass
@@ -51,8 +51,9 @@ def serve_nodeinfo(pm: PathMonitor, port: int) -> None:
             self.end_headers()
             self.wfile.write(raw)
 
-    srv = ThreadingHTTPServer(("0.0.0.0", port), H)
+    srv = ThreadingHTTPServer((host, port), H)
     threading.Thread(target=srv.serve_forever, daemon=True).start()
+    return srv
 
 
 def main(argv=None) -> int:
