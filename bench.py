@@ -55,6 +55,8 @@ def main(argv=None) -> int:
                     help="ResNet convolutions: fused MFMA implicit-GEMM kernels or MIOpen")
     ap.add_argument("--hw-queues", type=int, default=1,
                     help="GPU_MAX_HW_QUEUES per pod (vGPU HW-queue budget; 0 = runtime default)")
+    ap.add_argument("--cu-share", choices=("mask", "temporal", "group2", "group2i"), default="mask",
+                    help="compute-share enforcement of fractional pods (vgpu.bench.launch.launch_pods)")
     ap.add_argument("--no-cap-probe", action="store_true")
     ap.add_argument("--ready-timeout", type=float, default=1500.0)
     ap.add_argument("--cpu-smoke", action="store_true",
@@ -94,7 +96,7 @@ def main(argv=None) -> int:
     pods = launch_pods(specs, device, steps=args.steps, warmup=args.warmup, shim=not args.no_shim,
                        graph=not args.no_graph, cap_probe=not args.no_cap_probe,
                        find=not args.no_find, hw_queues=args.hw_queues or None,
-                       fused=not args.no_fused, conv=args.conv)
+                       fused=not args.no_fused, conv=args.conv, cu_share=args.cu_share)
     try:
         for p in pods:
             p.ready = p.read_tagged("READY", args.ready_timeout, progress=log)
@@ -167,6 +169,7 @@ def main(argv=None) -> int:
                 "fused_epilogues": not args.no_fused,
                 "conv": args.conv,
                 "hw_queues_per_pod": args.hw_queues,
+                "cu_share": args.cu_share,
             },
             "per_gpu_images_s": round(per_gpu, 2),
             "per_pod_images_s": [round(p.done["throughput"], 2) for p in pods],

@@ -1276,36 +1276,53 @@ hipError_t dispatch_bn(const ConvArgs& a, bool pro, bool res, hipStream_t s) {
   return dispatch_pr<KS, BM, 64>(a, pro, res, s);
 }
 
-// ---- NHWC 3x3/s2/p1 max pool and fused BN+ReLU+global-average pool -----------
+// ---- NHWC k x k max pool and fused BN+ReLU+global-average pool ----------------
+// One block per output row (grid OH x N): 32-bit index math only (the earlier
+// flat-index version spent its time in 64-bit div/mod — it ran ALU-bound, twice
+// as slow on half the CUs); K = 3 unrolls the window so all 9 16-B loads of an
+// interior output are in flight together.  Row/column reuse is caught by L1/L2.
+template <int K>
 __global__ void __launch_bounds__(kThreads) maxpool_kernel(const u32x4* __restrict__ x,
-                                                          u32x4* __restrict__ y, int N, int H, int W,
+                                                          u32x4* __restrict__ y, int H, int W,
                                                           int cv, int OH, int OW, int k, int stride,
                                                           int pad) {
-  const int64_t total = (int64_t)N * OH * OW * cv;
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * kThreads) {
-    const int c = (int)(i % cv);
-    int64_t p = i / cv;
-    const int ow = (int)(p % OW);
-    p /= OW;
-    const int oh = (int)(p % OH);
-    const int n = (int)(p / OH);
+  const int oh = blockIdx.x, n = blockIdx.y;
+  if (K) k = K;
+  const u32x4* __restrict__ xn = x + (int64_t)n * H * W * cv;
+  u32x4* __restrict__ yr = y + ((int64_t)n * OH + oh) * OW * cv;
+  const int h0 = oh * stride - pad;
+  const int hlo = h0 > 0 ? h0 : 0, hhi = h0 + k < H ? h0 + k : H;
+  const int row = OW * cv;
+  for (int i = threadIdx.x; i < row; i += kThreads) {
+    const int ow = (int)((unsigned)i / (unsigned)cv), c = i - ow * cv;
+    const int w0 = ow * stride - pad;
     float m[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
-    for (int dh = 0; dh < k; ++dh) {
-      const int ih = oh * stride - pad + dh;
-      if ((unsigned)ih >= (unsigned)H) continue;
-      for (int dw = 0; dw < k; ++dw) {
-        const int iw = ow * stride - pad + dw;
-        if ((unsigned)iw >= (unsigned)W) continue;
+    if (K && hlo == h0 && hhi == h0 + K && w0 >= 0 && w0 + K <= W) {
+      u32x4 v[K ? K * K : 1];
+#pragma unroll
+      for (int dh = 0; dh < K; ++dh)
+#pragma unroll
+        for (int dw = 0; dw < K; ++dw) v[dh * K + dw] = xn[((h0 + dh) * W + w0 + dw) * cv + c];
+#pragma unroll
+      for (int t = 0; t < K * K; ++t) {
         float e[8];
-        unpack8(x[(((int64_t)n * H + ih) * W + iw) * cv + c], e);
+        unpack8(v[t], e);
 #pragma unroll
         for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], e[j]);
       }
+    } else {
+      const int wlo = w0 > 0 ? w0 : 0, whi = w0 + k < W ? w0 + k : W;
+      for (int ih = hlo; ih < hhi; ++ih)
+        for (int iw = wlo; iw < whi; ++iw) {
+          float e[8];
+          unpack8(xn[(ih * W + iw) * cv + c], e);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], e[j]);
+        }
     }
-    y[i] = pack8(m);
+    yr[i] = pack8(m);
   }
 }
 
@@ -1345,53 +1362,51 @@ __global__ void __launch_bounds__(kThreads) ssr_mean_kernel(const u32x4* __restr
 // ---- ResNet stem space-to-depth: x [N][H][W][3] → X [N][HS][WS][16] ------------
 // X[n][i][j][b*6 + b'*3 + c] = x[n][2i+b-pad][2j+b'-pad][c] (zero outside; channels
 // 12..15 zero), so the 7x7/s2 stem becomes a 4x4/s1 conv with C = 16 (16-B
-// aligned taps for the LDS-DMA conv).  One thread per X pixel, 2×16-B stores.
+// aligned taps for the LDS-DMA conv).  Grid (ceil(HS*WS/256), N): one thread per
+// X pixel of image blockIdx.y, 32-bit index math (one 32-bit divide per pixel),
+// 2 x 16-B stores.  (An LDS-staged row version measured slower: 174-pixel blocks
+// with a barrier do too little work each.)
 __global__ void __launch_bounds__(kThreads) s2d_stem_kernel(const uint16_t* __restrict__ x,
-                                                            u32x4* __restrict__ X, int N, int H,
-                                                            int W, int HS, int WS, int pad) {
-  const int64_t total = (int64_t)N * HS * WS;
-  for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < total;
-       p += (int64_t)gridDim.x * kThreads) {
-    const int j = (int)(p % WS);
-    const int64_t t2 = p / WS;
-    const int i = (int)(t2 % HS);
-    const int n = (int)(t2 / HS);
-    uint16_t v[16];
+                                                            u32x4* __restrict__ X, int H, int W,
+                                                            int HS, int WS, int pad) {
+  const int n = blockIdx.y;
+  const int p = blockIdx.x * kThreads + threadIdx.x;
+  if (p >= HS * WS) return;
+  const int i = (int)((unsigned)p / (unsigned)WS), j = p - i * WS;
+  const uint16_t* __restrict__ xn = x + (int64_t)n * H * W * 3;
+  uint32_t v[12];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = 0;
+  for (int b = 0; b < 2; ++b) {
+    const int r = 2 * i + b - pad;
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int r = 2 * i + b - pad;
-      if ((unsigned)r >= (unsigned)H) continue;
+    for (int b2 = 0; b2 < 2; ++b2) {
+      const int c0 = 2 * j + b2 - pad;
+      const bool ok = (unsigned)r < (unsigned)H && (unsigned)c0 < (unsigned)W;
+      const uint16_t* src = xn + (ok ? (r * W + c0) * 3 : 0);
 #pragma unroll
-      for (int b2 = 0; b2 < 2; ++b2) {
-        const int c0 = 2 * j + b2 - pad;
-        if ((unsigned)c0 >= (unsigned)W) continue;
-        const uint16_t* src = x + (((int64_t)n * H + r) * W + c0) * 3;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) v[b * 6 + b2 * 3 + c] = src[c];
-      }
+      for (int c = 0; c < 3; ++c) v[b * 6 + b2 * 3 + c] = ok ? (uint32_t)src[c] : 0u;
     }
-    u32x4 lo, hi;
-    lo.x = v[0] | ((uint32_t)v[1] << 16); lo.y = v[2] | ((uint32_t)v[3] << 16);
-    lo.z = v[4] | ((uint32_t)v[5] << 16); lo.w = v[6] | ((uint32_t)v[7] << 16);
-    hi.x = v[8] | ((uint32_t)v[9] << 16); hi.y = v[10] | ((uint32_t)v[11] << 16);
-    hi.z = 0; hi.w = 0;
-    X[2 * p] = lo;
-    X[2 * p + 1] = hi;
   }
+  u32x4 lo, hi;
+  lo.x = v[0] | (v[1] << 16); lo.y = v[2] | (v[3] << 16);
+  lo.z = v[4] | (v[5] << 16); lo.w = v[6] | (v[7] << 16);
+  hi.x = v[8] | (v[9] << 16); hi.y = v[10] | (v[11] << 16);
+  hi.z = 0; hi.w = 0;
+  u32x4* __restrict__ Xp = X + ((int64_t)n * HS * WS + p) * 2;
+  Xp[0] = lo;
+  Xp[1] = hi;
 }
 
 }  // namespace
 
 VGPU_API int vgpu_stem_space_to_depth(const void* x, void* X, int N, int H, int W, int pad, int HS,
                                       int WS, hipStream_t s) {
-  if (N < 1 || H < 1 || W < 1 || HS < 1 || WS < 1 || pad < 0) return -1;
-  const int64_t total = (int64_t)N * HS * WS;
-  const int64_t want = (total + kThreads - 1) / kThreads;
-  const int grid = (int)(want < 256 * 32 ? want : 256 * 32);
-  hipLaunchKernelGGL(s2d_stem_kernel, dim3(grid), dim3(kThreads), 0, s,
-                     static_cast<const uint16_t*>(x), static_cast<u32x4*>(X), N, H, W, HS, WS, pad);
+  if (N < 1 || N > 65535 || H < 1 || W < 1 || HS < 1 || WS < 1 || pad < 0) return -1;
+  if ((int64_t)H * W * 3 >= ((int64_t)1 << 31) || (int64_t)HS * WS >= ((int64_t)1 << 31) - kThreads)
+    return -1;  // per-image offsets are 32-bit in the kernel
+  const int blocks = (HS * WS + kThreads - 1) / kThreads;
+  hipLaunchKernelGGL(s2d_stem_kernel, dim3(blocks, N), dim3(kThreads), 0, s,
+                     static_cast<const uint16_t*>(x), static_cast<u32x4*>(X), H, W, HS, WS, pad);
   return (int)hipGetLastError();
 }
 
@@ -1579,14 +1594,14 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
 // NHWC bf16 max pool (k×k window, stride, symmetric zero-excluded padding), 16 B per lane.
 VGPU_API int vgpu_maxpool_nhwc(const void* x, void* y, int N, int H, int W, int C, int k, int stride,
                                int pad, hipStream_t s) {
-  if (C % 8 || k < 1 || stride < 1 || pad < 0 || 2 * pad >= k + 1) return -1;
+  if (C % 8 || k < 1 || stride < 1 || pad < 0 || 2 * pad >= k + 1 || N < 1 || N > 65535) return -1;
   const int OH = (H + 2 * pad - k) / stride + 1, OW = (W + 2 * pad - k) / stride + 1;
   if (OH < 1 || OW < 1) return -1;
-  const int64_t total = (int64_t)N * OH * OW * (C / 8);
-  const int64_t want = (total + kThreads - 1) / kThreads;
-  const int grid = (int)(want < 256 * 16 ? want : 256 * 16);
-  hipLaunchKernelGGL(maxpool_kernel, dim3(grid), dim3(kThreads), 0, s, static_cast<const u32x4*>(x),
-                     static_cast<u32x4*>(y), N, H, W, C / 8, OH, OW, k, stride, pad);
+  if ((int64_t)H * W * (C / 8) >= ((int64_t)1 << 31) || (int64_t)OW * (C / 8) >= ((int64_t)1 << 31))
+    return -1;  // per-image offsets are 32-bit in the kernel
+  auto kern = k == 3 ? maxpool_kernel<3> : maxpool_kernel<0>;
+  hipLaunchKernelGGL(kern, dim3(OH, N), dim3(kThreads), 0, s, static_cast<const u32x4*>(x),
+                     static_cast<u32x4*>(y), H, W, C / 8, OH, OW, k, stride, pad);
   return (int)hipGetLastError();
 }
 

@@ -53,3 +53,23 @@ def test_parse_mask():
     assert parse_mask("0xff00") == 0xFF00
     assert parse_mask("ff,00") == 0xFF00
     assert parse_mask("") == 0
+
+
+def test_se_packed_order_gives_whole_shader_engines():
+    """VGPU_CU_PACK=se: a 25 % pod owns one SE on every XCD (local CUs j with
+    j % 4 == se), a 50 % pod two; masks stay disjoint and XCD-balanced."""
+    from vgpu.device.cualloc import MI355X, alloc_cu_mask, granule_order, popcount
+    order = granule_order(MI355X, "se")
+    assert sorted(order) == list(range(32)) and order[:8] == list(range(0, 32, 4))
+    used = 0
+    for se in range(4):
+        m = alloc_cu_mask(used, 25, MI355X, "se")
+        assert popcount(m) == 64 and MI355X.per_xcd_counts(m) == [8] * 8
+        local = {bit // 8 for bit in range(256) if m >> bit & 1}
+        assert {j % 4 for j in local} == {se}
+        used |= m
+    assert alloc_cu_mask(used, 25, MI355X, "se") is None
+    assert granule_order(MI355X, "spread") == list(range(32))
+    import pytest
+    with pytest.raises(ValueError):
+        granule_order(MI355X, "bogus")

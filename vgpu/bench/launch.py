@@ -84,14 +84,32 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
                 graph: bool = True, cap_probe: bool = False, find: bool = False,
                 workdir: str | None = None, oversubscribe: bool = False,
                 hw_queues: int | None = None, fused: bool = True,
-                conv: str = "native") -> list[Pod]:
-    """Start one process per pod on physical device `device`."""
+                conv: str = "native", cu_share: str = "mask") -> list[Pod]:
+    """Start one process per pod on physical device `device`.
+
+    cu_share: how a fractional pod's compute share is enforced —
+      mask      one XCD-balanced CU mask per pod (device-plugin default);
+      temporal  no mask, the shim's dispatch token bucket (VGPU_CU_MASK_FROM_LIMIT=false);
+      group2    pods 2k and 2k+1 share one mask sized for both (A/B tool);
+      group2i   pods k and k+n/2 share one mask (A/B tool)."""
     workdir = workdir or tempfile.mkdtemp(prefix="vgpu-pods-")
     used = 0
     pods = []
+    group_masks: dict[int, int] = {}
     for i, sp in enumerate(specs):
         mask = 0
-        if sp.cores and sp.cores < 100:
+        extra = {}
+        if sp.cores and sp.cores < 100 and cu_share == "temporal":
+            extra["VGPU_CU_MASK_FROM_LIMIT"] = "false"
+        elif sp.cores and sp.cores < 100 and cu_share in ("group2", "group2i"):
+            g = i // 2 if cu_share == "group2" else i % max(1, (len(specs) + 1) // 2)
+            if g not in group_masks:
+                m = alloc_cu_mask(used, min(100, 2 * sp.cores), MI355X)
+                if m is not None:
+                    group_masks[g] = m
+                    used |= m
+            mask = group_masks.get(g, 0)
+        elif sp.cores and sp.cores < 100:
             m = alloc_cu_mask(used, sp.cores, MI355X)
             if m is not None:
                 mask = m
@@ -114,6 +132,7 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
         if shim:
             env.update(cenv)
             env = preload_env(env)
+        env.update(extra)
         env.update(sp.extra_env)
         cmd = [sys.executable, "-u", "-m", "vgpu.bench.pod", "--workload", sp.workload,
                "--steps", str(steps), "--warmup", str(warmup), "--pod-index", str(i)]

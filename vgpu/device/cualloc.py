@@ -15,6 +15,7 @@ engines (local CU j → SE j % 4), so low granules are also SE-balanced.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 
@@ -23,6 +24,7 @@ class CULayout:
     total_cus: int = 256
     num_xcc: int = 8
     interleaved: bool = True   # bit i -> XCD i % num_xcc (gfx950); False: blocked
+    num_se: int = 4            # shader engines per XCD (local CU j -> SE j % num_se)
 
     @property
     def granules(self) -> int:
@@ -66,15 +68,34 @@ def popcount(m: int) -> int:
     return bin(m).count("1")
 
 
-def alloc_cu_mask(used: int, pct: int, layout: CULayout = MI355X) -> int | None:
+PACKINGS = ("spread", "se")
+
+
+def granule_order(layout: CULayout, pack: str | None = None) -> list[int]:
+    """Order in which free granules are taken.
+
+    spread: 0, 1, 2, ... — a pod's CUs are spread over every shader engine.
+    se:     all granules of SE 0, then SE 1, ... — a pod owns whole shader
+            engines where its share allows, so no two pods feed the same SE's
+            workgroup dispatcher."""
+    pack = pack or os.environ.get("VGPU_CU_PACK", "spread")
+    if pack not in PACKINGS:
+        raise ValueError(f"unknown CU packing {pack!r} (one of {PACKINGS})")
+    if pack == "se" and layout.num_se > 1 and layout.granules % layout.num_se == 0:
+        return [g for se in range(layout.num_se) for g in range(se, layout.granules, layout.num_se)]
+    return list(range(layout.granules))
+
+
+def alloc_cu_mask(used: int, pct: int, layout: CULayout = MI355X, pack: str | None = None) -> int | None:
     """Allocate an XCD-balanced mask for `pct` percent of the device's CUs from
-    the granules not set in `used`.  Returns None when not enough free granules
-    remain (the caller then falls back to sharing + temporal limiting)."""
+    the granules not set in `used` (taken in `granule_order`).  Returns None when
+    not enough free granules remain (the caller then falls back to sharing +
+    temporal limiting)."""
     need = layout.cus_for_percent(pct) // layout.num_xcc
     if need == 0:
         return 0
     mask = 0
-    for g in range(layout.granules):
+    for g in granule_order(layout, pack):
         gm = layout.granule_mask(g)
         if used & gm:
             continue
