@@ -37,6 +37,20 @@ def log(msg: str) -> None:
     sys.stderr.flush()
 
 
+def enforcement_label(args) -> str:
+    """What actually enforced the pods' compute share in this run."""
+    if args.no_shim:
+        return "none"
+    if args.gpucores <= 0 or args.gpucores >= 100:
+        return "libvgpu.so (HBM cap; whole GPU, no compute limit)"
+    return {
+        "mask": "libvgpu.so (HBM cap + XCD-balanced CU mask per pod)",
+        "temporal": "libvgpu.so (HBM cap + GPU-time token bucket, fair-share board; no CU mask)",
+        "group2": "libvgpu.so (HBM cap + one CU mask per pod pair 2k,2k+1)",
+        "group2i": "libvgpu.so (HBM cap + one CU mask per pod pair k,k+n/2)",
+    }[args.cu_share]
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -163,7 +177,8 @@ def main(argv=None) -> int:
                 "pods_per_gpu": args.pods,
                 "gpumem_mib": args.gpumem,
                 "gpucores": args.gpucores,
-                "enforcement": "none" if args.no_shim else "libvgpu.so (HBM cap + XCD-balanced CU mask)",
+                "enforcement": enforcement_label(args),
+                "cu_pack": os.environ.get("VGPU_CU_PACK", "spread"),
                 "hipgraph": not args.no_graph,
                 "miopen_find": not args.no_find,
                 "fused_epilogues": not args.no_fused,
@@ -173,6 +188,7 @@ def main(argv=None) -> int:
             },
             "per_gpu_images_s": round(per_gpu, 2),
             "per_pod_images_s": [round(p.done["throughput"], 2) for p in pods],
+            "per_pod_cu_mask_bits": [p.mask_bits for p in pods],
             "vram_cap": cap,
         }
         print(json.dumps(res), flush=True)

@@ -18,9 +18,13 @@
 #include <dlfcn.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
+#include <fcntl.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/file.h>
+#include <time.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <map>
@@ -51,6 +55,75 @@ int env_int(const char* n, int d) {
   const char* v = getenv(n);
   return v && *v ? atoi(v) : d;
 }
+
+// ---- fake GPU timeline -------------------------------------------------------
+// VGPU_FAKE_KERNEL_US > 0 gives every launch that much GPU time.  Launches run
+// in FIFO order on one timeline: per process, or — with VGPU_FAKE_GPU_TIMELINE
+// naming a file — shared by every process using that file (time-sharing one
+// device).  Events complete when the process's last launch before the record
+// has finished.
+uint64_t now_ns() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + ts.tv_nsec;
+}
+std::mutex g_tl_mu;
+uint64_t g_busy_until = 0;   // private timeline
+uint64_t g_my_last_end = 0;  // end of this process's latest launch
+std::atomic<uint64_t> g_exec_ns{0};
+
+void sleep_until(uint64_t t) {
+  for (uint64_t n = now_ns(); n < t; n = now_ns()) {
+    struct timespec ts{0, (long)std::min<uint64_t>(t - n, 1000000)};
+    nanosleep(&ts, nullptr);
+  }
+}
+
+void timeline_launch() {
+  static const int us = env_int("VGPU_FAKE_KERNEL_US", 0);
+  if (us <= 0) return;
+  const uint64_t dur = (uint64_t)us * 1000;
+  // A full AQL queue blocks the submitter: keep at most ~20 ms queued.
+  uint64_t last;
+  {
+    std::lock_guard<std::mutex> g(g_tl_mu);
+    last = g_my_last_end;
+  }
+  if (last > 20000000ull) sleep_until(last - 20000000ull);
+  std::lock_guard<std::mutex> g(g_tl_mu);
+  const uint64_t now = now_ns();
+  static const char* shared = getenv("VGPU_FAKE_GPU_TIMELINE");
+  if (shared && *shared) {
+    int fd = open(shared, O_RDWR | O_CREAT, 0666);
+    if (fd >= 0) {
+      flock(fd, LOCK_EX);
+      uint64_t until = 0;
+      if (pread(fd, &until, sizeof until, 0) != sizeof until) until = 0;
+      const uint64_t start = until > now ? until : now;
+      until = start + dur;
+      if (pwrite(fd, &until, sizeof until, 0) != sizeof until) {}
+      flock(fd, LOCK_UN);
+      close(fd);
+      g_my_last_end = until;
+      g_exec_ns.fetch_add(dur);
+      return;
+    }
+  }
+  const uint64_t start = g_busy_until > now ? g_busy_until : now;
+  g_busy_until = start + dur;
+  g_my_last_end = g_busy_until;
+  g_exec_ns.fetch_add(dur);
+}
+
+uint64_t timeline_last_end() {
+  std::lock_guard<std::mutex> g(g_tl_mu);
+  return g_my_last_end;
+}
+
+
+struct FakeEvent {
+  uint64_t at = 0;
+};
 
 hsa_status_t pick_gpu(hsa_agent_t a, void* data) {
   auto* v = (std::vector<hsa_agent_t>*)data;
@@ -127,6 +200,7 @@ void count_launch(uint64_t blocks) {
   init();
   g_launches.fetch_add(1);
   g_launch_blocks.fetch_add(blocks);
+  timeline_launch();
 }
 
 }  // namespace
@@ -143,8 +217,41 @@ hipError_t hipSetDevice(int d) {
 hipError_t hipGetDevice(int* d) { *d = tl_dev; return hipSuccess; }
 hipError_t hipGetDeviceCount(int* n) { init(); *n = (int)g_devs.size(); return hipSuccess; }
 hipError_t hipGetLastError() { return hipSuccess; }
-hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
-hipError_t hipDeviceSynchronize() { return hipSuccess; }
+hipError_t hipStreamSynchronize(hipStream_t) { sleep_until(timeline_last_end()); return hipSuccess; }
+hipError_t hipDeviceSynchronize() { sleep_until(timeline_last_end()); return hipSuccess; }
+hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) {
+  *e = reinterpret_cast<hipEvent_t>(new FakeEvent);
+  return hipSuccess;
+}
+hipError_t hipEventCreate(hipEvent_t* e) { return hipEventCreateWithFlags(e, 0); }
+hipError_t hipEventRecord(hipEvent_t e, hipStream_t) {
+  if (!e) return hipErrorInvalidHandle;
+  reinterpret_cast<FakeEvent*>(e)->at = timeline_last_end();
+  return hipSuccess;
+}
+hipError_t hipEventQuery(hipEvent_t e) {
+  if (!e) return hipErrorInvalidHandle;
+  return now_ns() >= reinterpret_cast<FakeEvent*>(e)->at ? hipSuccess : hipErrorNotReady;
+}
+hipError_t hipEventSynchronize(hipEvent_t e) {
+  if (!e) return hipErrorInvalidHandle;
+  sleep_until(reinterpret_cast<FakeEvent*>(e)->at);
+  return hipSuccess;
+}
+hipError_t hipEventDestroy(hipEvent_t e) {
+  delete reinterpret_cast<FakeEvent*>(e);
+  return hipSuccess;
+}
+hipError_t hipStreamIsCapturing(hipStream_t, hipStreamCaptureStatus* st) {
+  if (st) *st = hipStreamCaptureStatusNone;
+  return hipSuccess;
+}
+hipError_t hipThreadExchangeStreamCaptureMode(hipStreamCaptureMode*) { return hipSuccess; }
+hipError_t hipStreamBeginCapture(hipStream_t, hipStreamCaptureMode) { return hipSuccess; }
+hipError_t hipStreamEndCapture(hipStream_t, hipGraph_t* g) {
+  if (g) *g = nullptr;
+  return hipSuccess;
+}
 
 hipError_t hipMalloc(void** p, size_t size) { return dev_alloc(p, size, tl_dev); }
 hipError_t hipExtMallocWithFlags(void** p, size_t size, unsigned int) { return dev_alloc(p, size, tl_dev); }
@@ -296,6 +403,7 @@ hipError_t hipGraphLaunch(hipGraphExec_t, hipStream_t) {
   init();
   g_graph_launches.fetch_add(1);
   g_launches.fetch_add(1);
+  timeline_launch();
   return hipSuccess;
 }
 // Test helper: a graph of kernel nodes with grids (grids[i], 2, 1) plus, when
@@ -323,6 +431,7 @@ hipError_t hipGetProcAddress(const char* sym, void** pfn, int, uint64_t,
 
 // ---- test introspection ----
 uint64_t fake_hip_launches() { return g_launches.load(); }
+uint64_t fake_hip_exec_ns() { return g_exec_ns.load(); }
 uint64_t fake_hip_launch_blocks() { return g_launch_blocks.load(); }
 uint64_t fake_hip_physical_used(int dev) {
   std::lock_guard<std::mutex> g(g_mu);

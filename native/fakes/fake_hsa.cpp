@@ -11,6 +11,11 @@
 // library named in HSA_TOOLS_LIB — the tools-library interception path of
 // the enforcement library (native/shim/hooks_hsa.cpp).
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #define AMD_INTERNAL_BUILD 1
@@ -93,12 +98,53 @@ void setup_table() {
   });
 }
 
+// Fake KFD driver: opening VGPU_FAKE_KFD_DEV creates this process's entry in
+// the KFD proc directory (VGPU_KFD_PROC_DIR) named by VGPU_FAKE_HOST_PID, the
+// way amdgpu's kfd_open() creates /sys/class/kfd/kfd/proc/<host pid> inside
+// the open() call.  VGPU_FAKE_KFD_NOISE=<pid> adds an unrelated process's
+// entry in the same instant (an ambiguous diff).
+int fake_kfd_open(const char* path, int flags, mode_t mode) {
+  typedef int (*open_t)(const char*, int, ...);
+  static open_t real = (open_t)dlsym(RTLD_NEXT, "open");
+  const char* dev = getenv("VGPU_FAKE_KFD_DEV");
+  if (dev && *dev && path && !strcmp(path, dev)) {
+    const char* dir = getenv("VGPU_KFD_PROC_DIR");
+    const char* hp = getenv("VGPU_FAKE_HOST_PID");
+    char p[512];
+    if (dir && hp) {
+      snprintf(p, sizeof p, "%s/%s", dir, hp);
+      mkdir(p, 0755);
+    }
+    const char* noise = getenv("VGPU_FAKE_KFD_NOISE");
+    if (dir && noise && *noise) {
+      snprintf(p, sizeof p, "%s/%s", dir, noise);
+      mkdir(p, 0755);
+    }
+  }
+  return real(path, flags, mode);
+}
+
 }  // namespace
 
 extern "C" {
 
+int open(const char* path, int flags, ...) {
+  mode_t mode = 0;
+  if (flags & O_CREAT) {
+    va_list ap;
+    va_start(ap, flags);
+    mode = (mode_t)va_arg(ap, int);
+    va_end(ap);
+  }
+  return fake_kfd_open(path, flags, mode);
+}
+
 hsa_status_t hsa_init() {
   setup_table();
+  // ROCr opens the KFD character device first thing in hsa_init.
+  const char* dev = getenv("VGPU_FAKE_KFD_DEV");
+  static int kfd_fd = -1;
+  if (dev && *dev && kfd_fd < 0) kfd_fd = open(dev, O_RDWR | O_CLOEXEC);
   return HSA_STATUS_SUCCESS;
 }
 hsa_status_t hsa_shut_down() { return HSA_STATUS_SUCCESS; }

@@ -1,0 +1,69 @@
+/*
+ * vgpu share board — one small mmap'd file per physical GPU in the node-wide
+ * lock directory (/tmp/vgpulock, mounted into every vGPU container by the
+ * device plugin's Allocate; reference: the "unified lock" directory,
+ * pkg/device-plugin/nvidiadevice/nvinternal/plugin/server.go:357-369).
+ *
+ * It lets the temporal limiters of different pods on the same GPU charge
+ * each other FAIR-SHARE GPU time instead of wall-clock busy time: while k
+ * processes have work outstanding on the GPU, each is charged 1/k of the
+ * elapsed time (processor-sharing virtual time, as in GPS/WFQ).  A pod alone
+ * on the GPU is charged its full busy time; four busy pods are charged a
+ * quarter each, so four 25 % pods run unthrottled at the GPU's full aggregate
+ * rate while a lone 25 % pod is held to a quarter of the GPU.
+ *
+ * The reference's equivalent signal is NVML's per-process SM utilization
+ * (libvgpu.so utilization_watcher / get_used_gpu_utilization, SURVEY.md §2.6
+ * E1f); ROCm has no per-process busy-time counter for KFD user queues.
+ *
+ * Layout rules as in shared_region.h: fixed size, no pointers, robust
+ * process-shared mutex, monitor-readable.
+ */
+#ifndef VGPU_BOARD_H_
+#define VGPU_BOARD_H_
+
+#include <pthread.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VGPU_BOARD_MAGIC 0x56424F44u /* "VBOD" */
+#define VGPU_BOARD_VERSION 1u
+#define VGPU_BOARD_SLOTS 128
+#define VGPU_BOARD_STALE_NS 500000000ull /* a slot without heartbeat for 0.5 s is inactive */
+
+typedef struct vgpu_board_slot {
+  int32_t pid;                   /* pid inside the owner's container (0 = free) */
+  int32_t host_pid;              /* host pid when known                         */
+  volatile int32_t active;       /* 1 while the owner has work outstanding       */
+  int32_t limit_pct;             /* the owner's compute limit (informational)    */
+  volatile uint64_t heartbeat_ns;/* CLOCK_MONOTONIC, refreshed by the owner      */
+  volatile uint64_t charged_ns;  /* fair-share GPU time charged so far           */
+  volatile uint64_t busy_ns;     /* wall time with work outstanding so far       */
+  double v_mark;                 /* board virtual time at the last charge        */
+  uint64_t claim_ns;             /* CLOCK_MONOTONIC of the claim                 */
+} vgpu_board_slot_t;
+
+typedef struct vgpu_board {
+  uint32_t magic;
+  uint32_t version;
+  uint32_t struct_size;
+  volatile int32_t initialized;
+  union {
+    pthread_mutex_t m; /* PTHREAD_PROCESS_SHARED + ROBUST */
+    uint8_t raw[64];
+  } lock;
+  double v;               /* virtual time (ns): advances at 1/max(1, n_active) */
+  uint64_t last_ns;       /* CLOCK_MONOTONIC of the last advance              */
+  int32_t n_active;       /* live active slots at the last advance            */
+  int32_t reserved;
+  vgpu_board_slot_t slot[VGPU_BOARD_SLOTS];
+} vgpu_board_t;
+
+#ifdef __cplusplus
+}  // extern "C"
+#endif
+
+#endif  // VGPU_BOARD_H_

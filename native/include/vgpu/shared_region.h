@@ -35,11 +35,17 @@ extern "C" {
 #endif
 
 #define VGPU_REGION_MAGIC 0x56475055u /* "VGPU" */
-#define VGPU_REGION_VERSION 2u
+#define VGPU_REGION_VERSION 3u
 #define VGPU_MAX_DEVICES 16
 #define VGPU_MAX_PROCS 1024
 #define VGPU_UUID_LEN 64
 #define VGPU_CU_MASK_WORDS 4 /* 4 x 64 bit = 256 CUs (MI355X: 8 XCD x 32 CU) */
+
+/* how a slot's host_pid was obtained */
+#define VGPU_HOSTPID_UNVERIFIED 0 /* getpid()/NSpid: equals the host pid only outside a pid namespace */
+#define VGPU_HOSTPID_KFD_DIFF 1   /* KFD proc-dir diff around our first /dev/kfd open (hostpid.cpp) */
+#define VGPU_HOSTPID_MONITOR 2    /* node monitor (hostPID) matched NSpid + cgroup (vgpu/monitor/pids.py) */
+#define VGPU_HOSTPID_HOST_NS 3    /* process runs in the host pid namespace */
 
 /* process slot status */
 #define VGPU_PROC_FREE 0
@@ -63,6 +69,8 @@ typedef struct vgpu_proc_slot {
   int32_t host_pid;  /* pid in the host pid namespace (/proc/self/status NSpid) */
   int32_t status;    /* VGPU_PROC_*                                          */
   int32_t priority;  /* 0 = high, 1 = low                                    */
+  int32_t host_pid_src; /* VGPU_HOSTPID_*                                    */
+  int32_t reserved0;
   uint64_t start_ns; /* CLOCK_MONOTONIC at slot claim                        */
   uint64_t launches; /* kernel dispatches observed                           */
   uint64_t throttle_wait_ns; /* time spent blocked in the dispatch limiter   */
@@ -78,6 +86,12 @@ typedef struct vgpu_device_cfg {
   uint32_t cu_limit;        /* percent of the device's CUs, 0 or >=100 = unlimited */
   uint32_t cu_total;        /* CUs on the physical device                    */
   uint64_t cu_mask[VGPU_CU_MASK_WORDS]; /* HSA logical CU mask; all-zero = no mask */
+  /* Utilization of this container on the device as measured by the node
+   * monitor (hostPID view of KFD cu_occupancy), consumed by the temporal
+   * limiter when the shim has no verified host pid of its own. */
+  volatile uint32_t busy_permille;      /* 0..1000 of the device's CUs            */
+  uint32_t reserved1;
+  volatile uint64_t busy_ns;            /* CLOCK_MONOTONIC of the sample; 0 = none */
 } vgpu_device_cfg_t;
 
 typedef struct vgpu_shared_region {

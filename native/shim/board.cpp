@@ -1,0 +1,171 @@
+// Node-wide per-GPU share board (include/vgpu/board.h): fair-share charging of
+// GPU time between the pods that time-share one physical device.
+#include "board.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <sys/file.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+
+#include "common.h"
+#include "state.h"
+
+namespace vgpu {
+
+static_assert(sizeof(pthread_mutex_t) <= 64, "mutex must fit its 64-byte slot");
+
+namespace {
+
+void init_board(vgpu_board_t* b) {
+  memset(b, 0, sizeof(*b));
+  b->magic = VGPU_BOARD_MAGIC;
+  b->version = VGPU_BOARD_VERSION;
+  b->struct_size = (uint32_t)sizeof(*b);
+  pthread_mutexattr_t a;
+  pthread_mutexattr_init(&a);
+  pthread_mutexattr_setpshared(&a, PTHREAD_PROCESS_SHARED);
+  pthread_mutexattr_setrobust(&a, PTHREAD_MUTEX_ROBUST);
+  pthread_mutex_init(&b->lock.m, &a);
+  pthread_mutexattr_destroy(&a);
+  b->last_ns = mono_ns();
+  __atomic_store_n(&b->initialized, 1, __ATOMIC_RELEASE);
+}
+
+bool lock(vgpu_board_t* b) {
+  int rc = pthread_mutex_lock(&b->lock.m);
+  if (rc == EOWNERDEAD) {
+    pthread_mutex_consistent(&b->lock.m);
+    rc = 0;
+  }
+  return rc == 0;
+}
+
+void unlock(vgpu_board_t* b) { pthread_mutex_unlock(&b->lock.m); }
+
+bool live(const vgpu_board_slot_t& s, uint64_t now) {
+  return s.pid != 0 && s.active && now - s.heartbeat_ns < VGPU_BOARD_STALE_NS;
+}
+
+// Advance virtual time to `now` at the rate set by the active count of the
+// previous interval, then recount (caller holds the lock).
+void advance(vgpu_board_t* b, uint64_t now) {
+  if (now > b->last_ns) {
+    const int n = b->n_active > 1 ? b->n_active : 1;
+    b->v += (double)(now - b->last_ns) / n;
+    b->last_ns = now;
+  }
+  int n = 0;
+  for (int i = 0; i < VGPU_BOARD_SLOTS; ++i) n += live(b->slot[i], now);
+  b->n_active = n;
+}
+
+}  // namespace
+
+vgpu_board_t* board_map(const char* path) {
+  const size_t sz = sizeof(vgpu_board_t);
+  int fd = open(path, O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+  if (fd < 0) {
+    VLOG_WARN("cannot open share board %s: %s", path, strerror(errno));
+    return nullptr;
+  }
+  flock(fd, LOCK_EX);
+  struct stat stt;
+  fstat(fd, &stt);
+  const bool fresh = (size_t)stt.st_size < sz;
+  if (fresh && ftruncate(fd, (off_t)sz) != 0) {
+    flock(fd, LOCK_UN);
+    close(fd);
+    return nullptr;
+  }
+  void* p = mmap(nullptr, sz, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  if (p == MAP_FAILED) {
+    flock(fd, LOCK_UN);
+    close(fd);
+    return nullptr;
+  }
+  auto* b = (vgpu_board_t*)p;
+  if (fresh || b->magic != VGPU_BOARD_MAGIC || b->version != VGPU_BOARD_VERSION ||
+      b->struct_size != sz || !b->initialized)
+    init_board(b);
+  flock(fd, LOCK_UN);
+  close(fd);
+  return b;
+}
+
+int board_claim(vgpu_board_t* b, int pid, int host_pid, int limit_pct) {
+  if (!b || !lock(b)) return -1;
+  const uint64_t now = mono_ns();
+  int got = -1;
+  for (int i = 0; i < VGPU_BOARD_SLOTS && got < 0; ++i) {
+    vgpu_board_slot_t& s = b->slot[i];
+    // free, or abandoned (no heartbeat for 10 x the stale interval)
+    if (s.pid == 0 || now - s.heartbeat_ns > 10 * VGPU_BOARD_STALE_NS) got = i;
+  }
+  if (got >= 0) {
+    vgpu_board_slot_t& s = b->slot[got];
+    memset(&s, 0, sizeof(s));
+    s.pid = pid;
+    s.host_pid = host_pid;
+    s.limit_pct = limit_pct;
+    s.heartbeat_ns = now;
+    s.claim_ns = now;
+  }
+  unlock(b);
+  return got;
+}
+
+void board_release(vgpu_board_t* b, int slot) {
+  if (!b || slot < 0 || !lock(b)) return;
+  advance(b, mono_ns());
+  memset(&b->slot[slot], 0, sizeof(b->slot[slot]));
+  advance(b, mono_ns());
+  unlock(b);
+}
+
+void board_heartbeat(vgpu_board_t* b, int slot) {
+  if (b && slot >= 0) __atomic_store_n(&b->slot[slot].heartbeat_ns, mono_ns(), __ATOMIC_RELAXED);
+}
+
+// Work became outstanding: start accruing fair-share time from now.
+void board_enter(vgpu_board_t* b, int slot) {
+  if (!b || slot < 0 || !lock(b)) return;
+  const uint64_t now = mono_ns();
+  advance(b, now);
+  vgpu_board_slot_t& s = b->slot[slot];
+  s.heartbeat_ns = now;
+  s.active = 1;
+  s.v_mark = b->v;
+  advance(b, now);  // recount with us included
+  unlock(b);
+}
+
+// Fair-share ns accrued since the last charge; `leave` ends the activity.
+uint64_t board_charge(vgpu_board_t* b, int slot, uint64_t wall_ns, bool leave) {
+  if (!b || slot < 0 || !lock(b)) return wall_ns;
+  const uint64_t now = mono_ns();
+  advance(b, now);
+  vgpu_board_slot_t& s = b->slot[slot];
+  double c = s.active ? b->v - s.v_mark : 0.0;
+  if (c < 0) c = 0;
+  s.v_mark = b->v;
+  s.charged_ns += (uint64_t)c;
+  s.busy_ns += wall_ns;
+  s.heartbeat_ns = now;
+  if (leave) {
+    s.active = 0;
+    advance(b, now);
+  }
+  unlock(b);
+  return (uint64_t)c;
+}
+
+int board_active_count(vgpu_board_t* b) {
+  if (!b) return 0;
+  const uint64_t now = mono_ns();
+  int n = 0;
+  for (int i = 0; i < VGPU_BOARD_SLOTS; ++i) n += live(b->slot[i], now);
+  return n;
+}
+
+}  // namespace vgpu

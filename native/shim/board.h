@@ -1,0 +1,17 @@
+// Share-board API (board.cpp; layout in include/vgpu/board.h).
+#pragma once
+
+#include "vgpu/board.h"
+
+namespace vgpu {
+
+vgpu_board_t* board_map(const char* path);  // create or attach; nullptr on failure
+int board_claim(vgpu_board_t* b, int pid, int host_pid, int limit_pct);
+void board_release(vgpu_board_t* b, int slot);
+void board_heartbeat(vgpu_board_t* b, int slot);
+void board_enter(vgpu_board_t* b, int slot);
+// Fair-share GPU ns accrued since the previous charge (wall_ns when there is no board).
+uint64_t board_charge(vgpu_board_t* b, int slot, uint64_t wall_ns, bool leave);
+int board_active_count(vgpu_board_t* b);
+
+}  // namespace vgpu

@@ -104,6 +104,7 @@ __attribute__((visibility("default"))) int vgpu_region_signal_all(void* rp, int 
   for (int i = 0; i < VGPU_MAX_PROCS; ++i) {
     const vgpu_proc_slot_t& s = r->procs[i];
     if (s.status == VGPU_PROC_FREE) continue;
+    if (host_ns && s.host_pid_src == VGPU_HOSTPID_UNVERIFIED) continue;
     int pid = host_ns ? s.host_pid : s.pid;
     if (pid > 0 && kill(pid, sig) == 0) ++n;
   }
@@ -167,6 +168,12 @@ __attribute__((visibility("default"))) uint64_t vgpu_self_usage(int dev, int whi
                          &u.total_bytes};
   if (which < 0 || which > 4) return 0;
   return __atomic_load_n(f[which], __ATOMIC_RELAXED);
+}
+
+// Temporal limiter: fair-share GPU ns charged and wall ns busy on `dev` so far.
+__attribute__((visibility("default"))) void vgpu_self_gpu_time(int dev, uint64_t* charged,
+                                                               uint64_t* busy) {
+  limiter_stats(dev, charged, busy);
 }
 
 __attribute__((visibility("default"))) void vgpu_self_on_launch(int dev, uint64_t wg) {

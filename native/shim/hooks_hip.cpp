@@ -293,8 +293,11 @@ __attribute__((visibility("default"))) hipError_t hipLaunchKernel(const void* f,
                                                                   void** args, size_t shmem,
                                                                   hipStream_t stream) {
   ensure_init();
-  limiter_on_launch(cur_dev(), blocks3(grid.x, grid.y, grid.z), f);
-  return REAL_HIP(hipLaunchKernel)(f, grid, block, args, shmem, stream);
+  const int dev = cur_dev();
+  const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
+  hipError_t rc = REAL_HIP(hipLaunchKernel)(f, grid, block, args, shmem, stream);
+  if (track && rc == hipSuccess) limiter_track(dev, stream);
+  return rc;
 }
 
 __attribute__((visibility("default"))) hipError_t hipExtLaunchKernel(const void* f, dim3 grid,
@@ -303,8 +306,11 @@ __attribute__((visibility("default"))) hipError_t hipExtLaunchKernel(const void*
                                                                      hipEvent_t start, hipEvent_t stop,
                                                                      int flags) {
   ensure_init();
-  limiter_on_launch(cur_dev(), blocks3(grid.x, grid.y, grid.z), f);
-  return REAL_HIP(hipExtLaunchKernel)(f, grid, block, args, shmem, stream, start, stop, flags);
+  const int dev = cur_dev();
+  const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
+  hipError_t rc = REAL_HIP(hipExtLaunchKernel)(f, grid, block, args, shmem, stream, start, stop, flags);
+  if (track && rc == hipSuccess) limiter_track(dev, stream);
+  return rc;
 }
 
 __attribute__((visibility("default"))) hipError_t hipModuleLaunchKernel(
@@ -312,8 +318,11 @@ __attribute__((visibility("default"))) hipError_t hipModuleLaunchKernel(
     unsigned int by, unsigned int bz, unsigned int shmem, hipStream_t stream, void** params,
     void** extra) {
   ensure_init();
-  limiter_on_launch(cur_dev(), blocks3(gx, gy, gz));
-  return REAL_HIP(hipModuleLaunchKernel)(f, gx, gy, gz, bx, by, bz, shmem, stream, params, extra);
+  const int dev = cur_dev();
+  const bool track = limiter_on_launch(dev, blocks3(gx, gy, gz));
+  hipError_t rc = REAL_HIP(hipModuleLaunchKernel)(f, gx, gy, gz, bx, by, bz, shmem, stream, params, extra);
+  if (track && rc == hipSuccess) limiter_track(dev, stream);
+  return rc;
 }
 
 __attribute__((visibility("default"))) hipError_t hipExtModuleLaunchKernel(
@@ -323,9 +332,12 @@ __attribute__((visibility("default"))) hipError_t hipExtModuleLaunchKernel(
   ensure_init();
   // Global work size is in work-items here.
   auto nb = [](uint32_t g, uint32_t l) { return l ? (g + l - 1) / l : g; };
-  limiter_on_launch(cur_dev(), blocks3(nb(gwx, lwx), nb(gwy, lwy), nb(gwz, lwz)));
-  return REAL_HIP(hipExtModuleLaunchKernel)(f, gwx, gwy, gwz, lwx, lwy, lwz, shmem, stream, params,
-                                            extra, start, stop, flags);
+  const int dev = cur_dev();
+  const bool track = limiter_on_launch(dev, blocks3(nb(gwx, lwx), nb(gwy, lwy), nb(gwz, lwz)));
+  hipError_t rc = REAL_HIP(hipExtModuleLaunchKernel)(f, gwx, gwy, gwz, lwx, lwy, lwz, shmem, stream,
+                                                     params, extra, start, stop, flags);
+  if (track && rc == hipSuccess) limiter_track(dev, stream);
+  return rc;
 }
 
 static hipError_t cooperative_guard(const void* f, dim3 grid, dim3 block, size_t shmem) {
@@ -360,23 +372,32 @@ __attribute__((visibility("default"))) hipError_t hipLaunchCooperativeKernel(con
   ensure_init();
   hipError_t g = cooperative_guard(f, grid, block, shmem);
   if (g != hipSuccess) return g;
-  limiter_on_launch(cur_dev(), blocks3(grid.x, grid.y, grid.z), f);
-  return REAL_HIP(hipLaunchCooperativeKernel)(f, grid, block, params, shmem, stream);
+  const int dev = cur_dev();
+  const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
+  hipError_t rc = REAL_HIP(hipLaunchCooperativeKernel)(f, grid, block, params, shmem, stream);
+  if (track && rc == hipSuccess) limiter_track(dev, stream);
+  return rc;
 }
 
 __attribute__((visibility("default"))) hipError_t hipModuleLaunchCooperativeKernel(
     hipFunction_t f, unsigned int gx, unsigned int gy, unsigned int gz, unsigned int bx,
     unsigned int by, unsigned int bz, unsigned int shmem, hipStream_t stream, void** params) {
   ensure_init();
-  limiter_on_launch(cur_dev(), blocks3(gx, gy, gz));
-  return REAL_HIP(hipModuleLaunchCooperativeKernel)(f, gx, gy, gz, bx, by, bz, shmem, stream, params);
+  const int dev = cur_dev();
+  const bool track = limiter_on_launch(dev, blocks3(gx, gy, gz));
+  hipError_t rc = REAL_HIP(hipModuleLaunchCooperativeKernel)(f, gx, gy, gz, bx, by, bz, shmem, stream, params);
+  if (track && rc == hipSuccess) limiter_track(dev, stream);
+  return rc;
 }
 
 __attribute__((visibility("default"))) hipError_t hipLaunchKernelExC(const hipLaunchConfig_t* cfg,
                                                                      const void* f, void** args) {
   ensure_init();
-  if (cfg) limiter_on_launch(cur_dev(), blocks3(cfg->gridDim.x, cfg->gridDim.y, cfg->gridDim.z), f);
-  return REAL_HIP(hipLaunchKernelExC)(cfg, f, args);
+  const int dev = cur_dev();
+  const bool track = cfg && limiter_on_launch(dev, blocks3(cfg->gridDim.x, cfg->gridDim.y, cfg->gridDim.z), f);
+  hipError_t rc = REAL_HIP(hipLaunchKernelExC)(cfg, f, args);
+  if (track && rc == hipSuccess) limiter_track(dev, cfg->stream);
+  return rc;
 }
 
 // Graphs: a hipGraphLaunch bypasses every per-kernel hook, so each executable
@@ -392,8 +413,11 @@ __attribute__((visibility("default"))) hipError_t hipGraphLaunch(hipGraphExec_t 
     return v ? strtoull(v, nullptr, 10) : 4096ull;
   }();
   uint64_t wg = graph_exec_workgroups(exec);
-  limiter_on_launch(cur_dev(), wg ? wg : fallback_tokens);
-  return REAL_HIP(hipGraphLaunch)(exec, stream);
+  const int dev = cur_dev();
+  const bool track = limiter_on_launch(dev, wg ? wg : fallback_tokens);
+  hipError_t rc = REAL_HIP(hipGraphLaunch)(exec, stream);
+  if (track && rc == hipSuccess) limiter_track(dev, stream);
+  return rc;
 }
 
 __attribute__((visibility("default"))) hipError_t hipGraphInstantiate(hipGraphExec_t* pExec, hipGraph_t graph,
@@ -425,6 +449,34 @@ __attribute__((visibility("default"))) hipError_t hipGraphInstantiateWithParams(
 __attribute__((visibility("default"))) hipError_t hipGraphExecDestroy(hipGraphExec_t exec) {
   graph_exec_forget(exec);
   return REAL_HIP(hipGraphExecDestroy)(exec);
+}
+
+// Stream capture bracketing (see g_open_captures).  A capture that ends in
+// another thread or never ends only delays marker polling, never correctness.
+__attribute__((visibility("default"))) hipError_t hipStreamBeginCapture(hipStream_t stream,
+                                                                        hipStreamCaptureMode mode) {
+  g_open_captures.fetch_add(1);
+  hipError_t rc = REAL_HIP(hipStreamBeginCapture)(stream, mode);
+  if (rc != hipSuccess) g_open_captures.fetch_sub(1);
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipStreamBeginCaptureToGraph(
+    hipStream_t stream, hipGraph_t graph, const hipGraphNode_t* deps, const hipGraphEdgeData* data,
+    size_t n, hipStreamCaptureMode mode) {
+  g_open_captures.fetch_add(1);
+  hipError_t rc = REAL_HIP(hipStreamBeginCaptureToGraph)(stream, graph, deps, data, n, mode);
+  if (rc != hipSuccess) g_open_captures.fetch_sub(1);
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipStreamEndCapture(hipStream_t stream,
+                                                                      hipGraph_t* graph) {
+  hipError_t rc = REAL_HIP(hipStreamEndCapture)(stream, graph);
+  int cur = g_open_captures.load();
+  while (cur > 0 && !g_open_captures.compare_exchange_weak(cur, cur - 1)) {
+  }
+  return rc;
 }
 
 // hipGetProcAddress must hand out our hooks too, or a runtime-resolved call

@@ -23,6 +23,7 @@ State& st() {
 }
 
 static void on_exit_release() {
+  limiter_stop();
   State& s = st();
   if (s.region && s.slot >= 0) {
     region_release_slot(s.region, s.slot);
@@ -61,8 +62,11 @@ static void atfork_child() {
   State& s = st();
   s.slot = -1;
   s.pid = getpid();
+  hostpid_after_fork();
+  limiter_after_fork();
   if (s.region) {
-    s.slot = region_claim_slot(s.region, s.pid, host_pid_of_self(), s.lim.priority);
+    s.slot = region_claim_slot(s.region, s.pid, self_host_pid(nullptr), s.lim.priority);
+    hostpid_publish();
   }
   {
     std::lock_guard<std::mutex> g(s.ledger_mu);
@@ -93,8 +97,9 @@ static void do_init() {
     s.region = region_map(nullptr, &s.lim, &s.region_fd);
   }
   if (s.region) {
-    s.slot = region_claim_slot(s.region, s.pid, host_pid_of_self(), s.lim.priority);
+    s.slot = region_claim_slot(s.region, s.pid, self_host_pid(nullptr), s.lim.priority);
     if (s.slot < 0) VLOG_ERR("no free process slot in the shared region");
+    hostpid_publish();
   }
   trace_open();
   install_signal(SIGUSR2, sig_suspend);

@@ -1,113 +1,135 @@
 // Compute-share enforcement on the dispatch path.
 //
 // Reference behaviour: libvgpu.so's
-// `utilization_watcher` thread samples per-process SM utilization every 120 ms
-// and feeds a global token counter; `rate_limiter(grids, blocks)` runs on
-// every cuLaunchKernel: it blocks while the monitor has set recent_kernel < 0
-// (priority preemption), sets recent_kernel = 2, returns when the limit is 0 or
-// >= 100 or utilizationSwitch == 0, and otherwise CAS-decrements the counter
-// by `grids`, sleeping while it is negative.
+// `utilization_watcher` thread samples per-process SM utilization
+// (nvmlDeviceGetProcessUtilization) every 120 ms and feeds a global token
+// counter; `rate_limiter(grids, blocks)` runs on every cuLaunchKernel: it
+// blocks while the monitor has set recent_kernel < 0 (priority preemption),
+// sets recent_kernel = 2, returns when the limit is 0 or >= 100 or
+// utilizationSwitch == 0, and otherwise CAS-decrements the counter by `grids`,
+// sleeping while it is negative.
 //
-// MI355X design: the PRIMARY mechanism is spatial (XCD-balanced CU masks on
-// every HSA queue, cumask.cpp) which is exact and costs nothing per dispatch.
-// This temporal limiter only engages when a mask cannot express the share
-// (GPU_CORE_UTILIZATION_POLICY=force, or no mask) — it is a workgroup-rate
-// token bucket whose refill rate is adapted so that the sampled utilization
-// tracks the limit (multiplicative controller), rather than a fixed
-// SM²-proportional step.
-#include <dirent.h>
+// MI355X design.  The PRIMARY mechanism is spatial (XCD-balanced CU masks on
+// every HSA queue, cumask.cpp): exact and free per dispatch.  This temporal
+// limiter engages when a mask cannot express the share
+// (GPU_CORE_UTILIZATION_POLICY=force, VGPU_CU_MASK_FROM_LIMIT=false, or more
+// sharers than a GPU has good mask slots for).  ROCm has no per-process
+// busy-time counter for KFD user queues (KFD's cu_occupancy is an occupancy
+// snapshot, not time), so the limiter measures the GPU time of its OWN work:
+//
+//   * after every tracked launch (kernel, module kernel, graph) the hook
+//     records a timing-free marker event on the launch's stream;
+//   * the limiter thread polls the oldest markers (hipEventQuery, 100 µs) and
+//     turns "this process had work outstanding on the device from t0 to t1"
+//     into a charge.  With a share board (board.cpp; node-wide, one per GPU)
+//     the charge is the processor-sharing virtual time of the interval — each
+//     of k concurrently busy pods pays 1/k of the wall time — otherwise it is
+//     the wall time itself;
+//   * a token bucket in GPU-nanoseconds refills at limit% of wall time, and
+//     the launch hook blocks while the bucket, minus the estimated cost of the
+//     work already in flight, is negative.
+//
+// The charge is for time actually spent on the GPU, so it is exact for a
+// graph replay as for a stream of tiny kernels, needs no host-PID mapping,
+// and converges on hardware without calibration.
 #include <dlfcn.h>
 #include <math.h>
+#include <sys/stat.h>
 
-#include <unordered_map>
-
+#include <condition_variable>
+#include <deque>
 #include <thread>
+#include <unordered_map>
+#include <vector>
 
+#include "board.h"
 #include "common.h"
+#include "real.h"
 #include "state.h"
 
 namespace vgpu {
 
 thread_local int tl_device = 0;
 thread_local int tl_in_hip_alloc = 0;
+std::atomic<int> g_open_captures{0};
 
-struct DevLimiter {
-  std::atomic<int64_t> tokens{0};
-  std::atomic<uint64_t> launched{0};  // workgroups launched (for rate estimation)
-  std::atomic<uint64_t> waited{0};    // launches that had to wait
-  double rate = 0;                    // workgroups / second
-  double cap = 0;                     // bucket depth (workgroups)
-  int active = 0;                     // temporal throttling enabled for this device
-  double util_acc = 0;
-  int util_n = 0;
-};
-
-static DevLimiter g_lim[VGPU_MAX_DEVICES];
-static std::atomic<int> g_throttle_any{0};
-static std::atomic<int> g_watcher_running{0};
-
-// Utilization sampling -------------------------------------------------------------
-// Returns percent busy of device `dev` attributable to this container, or -1.
 extern int cumask_device_cus(int dev);        // CUs available to us (mask or physical)
 extern uint32_t cumask_driver_uid(int dev);   // KFD gpu_id of device, 0 = unknown
 
-static double sample_fake(int dev) {
-  const char* f = getenv("VGPU_FAKE_UTIL_FILE");
-  if (!f) return -1;
-  FILE* fp = fopen(f, "r");
-  if (!fp) return -1;
-  int d;
-  double u;
-  double out = -1;
-  while (fscanf(fp, "%d %lf", &d, &u) == 2)
-    if (d == dev) out = u;
-  fclose(fp);
-  return out;
+namespace {
+
+struct Marker {
+  hipEvent_t ev;
+  uint64_t submit_ns;
+};
+
+struct DevLimiter {
+  int active = 0;             // temporal limiting configured for this device
+  double frac = 0;            // limit / 100
+  std::atomic<int64_t> tokens{0};  // fair-share GPU ns we may still spend
+  int64_t cap = 0;            // bucket depth (ns)
+  int64_t quantum = 0;        // an overdrawn bucket must refill this far before launches resume
+  std::atomic<int> hold{0};   // 1 while waiting for the quantum
+  std::atomic<int> outstanding{0};
+  std::atomic<int64_t> ema_charge{0};  // ns per completed marker
+  std::mutex mu;              // guards streams / free_ev / act_mark_ns / board
+  std::unordered_map<hipStream_t, std::deque<Marker>> streams;
+  std::vector<hipEvent_t> free_ev;
+  uint64_t act_mark_ns = 0;   // start of the not-yet-charged busy interval
+  uint64_t last_poll_ns = 0;  // previous poll that found work still in flight
+  vgpu_board_t* board = nullptr;
+  int board_slot = -1;
+  bool board_tried = false;
+  // window statistics (limiter thread only)
+  uint64_t win_charge = 0, win_busy = 0, win_start = 0;
+  std::atomic<uint64_t> charged_total{0}, busy_total{0};
+};
+
+DevLimiter g_lim[VGPU_MAX_DEVICES];
+std::atomic<int> g_throttle_any{0};
+std::atomic<int> g_thread_running{0};
+std::atomic<int> g_shutdown{0};
+std::atomic<int> g_thread_alive{0};
+std::mutex g_cv_mu;
+std::condition_variable g_cv;
+
+const char* lock_dir() {
+  const char* d = env_first("VGPU_LOCK_DIR");
+  return d && *d ? d : "/tmp/vgpulock";
 }
 
-static double sample_kfd(int dev) {
+// Board of the physical GPU behind logical device `dev` (lazy; caller holds L.mu).
+void attach_board(int dev, DevLimiter& L) {
+  if (L.board_tried) return;
+  L.board_tried = true;
+  if (!env_bool(env_first("VGPU_SHARE_BOARD"), true)) return;
   State& s = st();
-  if (!s.region) return -1;
-  uint32_t uid = cumask_driver_uid(dev);
-  int cus = cumask_device_cus(dev);
-  if (cus <= 0) return -1;
-  double busy = 0;
-  bool any = false;
-  for (int i = 0; i < VGPU_MAX_PROCS; ++i) {
-    const vgpu_proc_slot_t& sl = s.region->procs[i];
-    if (sl.status == VGPU_PROC_FREE) continue;
-    int pid = sl.host_pid > 0 ? sl.host_pid : sl.pid;
-    char dir[128];
-    snprintf(dir, sizeof dir, "/sys/class/kfd/kfd/proc/%d", pid);
-    DIR* d = opendir(dir);
-    if (!d) continue;
-    struct dirent* e;
-    while ((e = readdir(d))) {
-      if (strncmp(e->d_name, "stats_", 6)) continue;
-      if (uid && (uint32_t)strtoul(e->d_name + 6, nullptr, 10) != uid) continue;
-      char path[512];
-      snprintf(path, sizeof path, "%s/%s/cu_occupancy", dir, e->d_name);
-      FILE* fp = fopen(path, "r");
-      if (!fp) continue;
-      int v = 0;
-      if (fscanf(fp, "%d", &v) == 1) { busy += v; any = true; }
-      fclose(fp);
-    }
-    closedir(d);
+  char key[VGPU_UUID_LEN + 16] = {};
+  if (s.region && s.region->dev[dev].uuid[0])
+    snprintf(key, sizeof key, "%s", s.region->dev[dev].uuid);
+  else if (uint32_t uid = cumask_driver_uid(dev))
+    snprintf(key, sizeof key, "kfd-%u", uid);
+  else
+    return;
+  for (char* p = key; *p; ++p)
+    if (*p == '/') *p = '_';
+  struct stat stt;
+  if (stat(lock_dir(), &stt) != 0 || !S_ISDIR(stt.st_mode)) return;
+  char path[640];
+  snprintf(path, sizeof path, "%s/%s.board", lock_dir(), key);
+  L.board = board_map(path);
+  if (!L.board) return;
+  L.board_slot = board_claim(L.board, getpid(), self_host_pid(nullptr), (int)lround(L.frac * 100));
+  if (L.board_slot < 0) {
+    VLOG_WARN("share board %s is full; charging wall time", path);
+    L.board = nullptr;
+    return;
   }
-  if (!any) return -1;
-  double u = 100.0 * busy / cus;
-  return u > 100 ? 100 : u;
-}
-
-static double sample_util(int dev) {
-  double u = sample_fake(dev);
-  if (u >= 0) return u;
-  return sample_kfd(dev);
+  VLOG_INFO("device %d: fair-share board %s slot %d", dev, path, L.board_slot);
 }
 
 // Decide per device whether temporal throttling applies.
-static void configure() {
+void configure() {
   State& s = st();
   int any = 0;
   for (int d = 0; d < VGPU_MAX_DEVICES; ++d) {
@@ -119,31 +141,132 @@ static void configure() {
     // A CU mask already enforces the share spatially; temporal limiting on top
     // of it only when explicitly forced.
     if (has_mask && s.lim.core_policy != 1) want = false;
-    if (!has_mask && s.lim.core_policy == 0 &&
-        env_bool(env_first("VGPU_CU_MASK_FROM_LIMIT"), true))
+    if (!has_mask && s.lim.core_policy == 0 && env_bool(env_first("VGPU_CU_MASK_FROM_LIMIT"), true))
       want = false;  // cumask.cpp derives a balanced mask from the limit
-    g_lim[d].active = want;
+    DevLimiter& L = g_lim[d];
+    if (want && !L.active) {
+      L.frac = lim / 100.0;
+      const double burst_ms = env_first("VGPU_LIMITER_BURST_MS") ? atof(env_first("VGPU_LIMITER_BURST_MS")) : 50.0;
+      L.cap = (int64_t)(L.frac * burst_ms * 1e6);
+      // Time-slice quantum: a throttled pod runs in slices of ~quantum_ms of
+      // wall time (at its share) instead of one launch per refill, so the
+      // per-slice costs (clock ramp after idle, pipeline fill) are amortised.
+      const double q_ms = env_first("VGPU_LIMITER_QUANTUM_MS") ? atof(env_first("VGPU_LIMITER_QUANTUM_MS")) : 200.0;
+      L.quantum = (int64_t)(L.frac * q_ms * 1e6);
+      if (L.cap < L.quantum) L.cap = L.quantum;
+      L.tokens.store(L.cap);
+      L.win_start = mono_ns();
+    }
+    L.active = want;
     any |= want;
   }
   g_throttle_any.store(any, std::memory_order_release);
 }
 
-static void watcher_main() {
-  const uint64_t tick_ns =
-      (uint64_t)(1e6 * (getenv("VGPU_LIMITER_TICK_MS") ? atof(getenv("VGPU_LIMITER_TICK_MS")) : 10.0));
-  const uint64_t window_ns = 120000000ull;  // 120 ms control window (reference cadence)
-  uint64_t last = mono_ns(), last_ctl = last;
-  uint64_t seen_seq = 0;
+// Poll the oldest markers of every stream of `dev`; charge completed intervals.
+bool reap(int dev, DevLimiter& L, uint64_t now_hint) {
+  if (L.outstanding.load(std::memory_order_relaxed) == 0) return false;
+  if (g_open_captures.load(std::memory_order_acquire) > 0) return true;  // poll after the capture
+  auto query = REAL_HIP(hipEventQuery);
+  std::lock_guard<std::mutex> g(L.mu);
+  int done = 0;
+  for (auto it = L.streams.begin(); it != L.streams.end();) {
+    auto& q = it->second;
+    while (!q.empty()) {
+      hipError_t rc = query(q.front().ev);
+      if (rc == hipErrorNotReady || rc == hipErrorStreamCaptureUnsupported ||
+          rc == hipErrorStreamCaptureImplicit)
+        break;
+      L.free_ev.push_back(q.front().ev);  // complete (or invalid: never wait on it again)
+      q.pop_front();
+      ++done;
+    }
+    if (q.empty())
+      it = L.streams.erase(it);
+    else
+      ++it;
+  }
+  const uint64_t polled = mono_ns();
+  if (!done) {
+    L.last_poll_ns = polled;
+    return true;
+  }
+  // The completion happened between the previous poll and this one.
+  uint64_t now = L.last_poll_ns > L.act_mark_ns ? (L.last_poll_ns + polled) / 2 : polled;
+  if (now < L.act_mark_ns) now = L.act_mark_ns;
+  L.last_poll_ns = polled;
+  const int left = L.outstanding.fetch_sub(done) - done;
+  const uint64_t wall = now > L.act_mark_ns ? now - L.act_mark_ns : 0;
+  L.act_mark_ns = now;
+  const uint64_t charge = L.board ? board_charge(L.board, L.board_slot, wall, left == 0) : wall;
+  L.tokens.fetch_sub((int64_t)charge, std::memory_order_relaxed);
+  const int64_t per = (int64_t)(charge / done);
+  const int64_t old = L.ema_charge.load(std::memory_order_relaxed);
+  L.ema_charge.store(old ? (old * 3 + per) / 4 : per, std::memory_order_relaxed);
+  L.win_charge += charge;
+  L.win_busy += wall;
+  L.charged_total.fetch_add(charge, std::memory_order_relaxed);
+  L.busy_total.fetch_add(wall, std::memory_order_relaxed);
+  trace_emit(VGPU_EV_GPU_TIME, dev, charge, wall);
+  (void)now_hint;
+  return left > 0;
+}
+
+void limiter_main() {
+  g_thread_alive.store(1);
+  // Our polling must not be refused (or break) an application's graph capture
+  // in hipStreamCaptureModeGlobal on another thread.
+  if (auto xm = REAL_HIP(hipThreadExchangeStreamCaptureMode)) {
+    hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
+    (void)xm(&m);
+  }
+  uint64_t last = mono_ns(), last_mask = last;
   uint64_t mask_sig = 0;
   State& s = st();
-  for (;;) {
-    sleep_ns(tick_ns);
-    uint64_t now = mono_ns();
-    double dt = (now - last) * 1e-9;
+  while (!g_shutdown.load(std::memory_order_relaxed)) {
+    bool busy = false;
+    if (g_throttle_any.load(std::memory_order_relaxed))
+      for (int d = 0; d < VGPU_MAX_DEVICES; ++d)
+        if (g_lim[d].active) busy |= reap(d, g_lim[d], 0);
+    if (busy) {
+      sleep_ns(100000);  // 100 µs: completion-time resolution while work is in flight
+    } else {
+      std::unique_lock<std::mutex> lk(g_cv_mu);
+      g_cv.wait_for(lk, std::chrono::milliseconds(2));
+    }
+    const uint64_t now = mono_ns();
+    const double dt = (double)(now - last);
     last = now;
+    for (int d = 0; d < VGPU_MAX_DEVICES; ++d) {
+      DevLimiter& L = g_lim[d];
+      if (!L.active) continue;
+      const int64_t add = (int64_t)(L.frac * dt);
+      int64_t cur = L.tokens.load(std::memory_order_relaxed), nv;
+      do {
+        nv = cur + add;
+        if (nv > L.cap) nv = L.cap;
+      } while (!L.tokens.compare_exchange_weak(cur, nv, std::memory_order_relaxed));
+      if (L.board) board_heartbeat(L.board, L.board_slot);
+      // Publish this process's fair-share utilization of the last ~120 ms window
+      // (the reference watcher's cadence) for the monitor's metrics.
+      if (now - L.win_start >= 120000000ull) {
+        const double win = (double)(now - L.win_start);
+        if (s.region) {
+          __atomic_store_n(&s.region->dev[d].busy_permille,
+                           (uint32_t)fmin(1000.0, 1000.0 * L.win_charge / win), __ATOMIC_RELAXED);
+          __atomic_store_n(&s.region->dev[d].busy_ns, now, __ATOMIC_RELEASE);
+        }
+        VLOG_DEBUG("limiter dev %d: charged %.1f%% busy %.1f%% of %.0f ms (target %.0f%%, tokens %.2f ms)",
+                   d, 100.0 * L.win_charge / win, 100.0 * L.win_busy / win, win / 1e6, 100 * L.frac,
+                   L.tokens.load() / 1e6);
+        L.win_charge = L.win_busy = 0;
+        L.win_start = now;
+      }
+    }
     // Re-apply CU masks when the region's masks change (elastic resizing by
     // the node monitor / device plugin).
-    if (s.region) {
+    if (s.region && now - last_mask >= 10000000ull) {
+      last_mask = now;
       uint64_t sig = 1469598103934665603ull;
       for (int d = 0; d < VGPU_MAX_DEVICES; ++d)
         for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w)
@@ -154,67 +277,12 @@ static void watcher_main() {
         mask_sig = sig;
         configure();
       }
-      (void)seen_seq;
-    }
-    if (!g_throttle_any.load(std::memory_order_relaxed)) continue;
-    for (int d = 0; d < VGPU_MAX_DEVICES; ++d) {
-      DevLimiter& L = g_lim[d];
-      if (!L.active) continue;
-      if (L.rate > 0) {
-        int64_t add = (int64_t)(L.rate * dt);
-        int64_t cur = L.tokens.load(std::memory_order_relaxed);
-        int64_t nv;
-        do {
-          nv = cur + add;
-          if (nv > (int64_t)L.cap) nv = (int64_t)L.cap;
-        } while (!L.tokens.compare_exchange_weak(cur, nv, std::memory_order_relaxed));
-      }
-      double u = sample_util(d);
-      if (u >= 0) { L.util_acc += u; L.util_n++; }
-    }
-    if (now - last_ctl < window_ns) continue;
-    double wdt = (now - last_ctl) * 1e-9;
-    last_ctl = now;
-    for (int d = 0; d < VGPU_MAX_DEVICES; ++d) {
-      DevLimiter& L = g_lim[d];
-      if (!L.active) continue;
-      uint32_t lim = s.region ? s.region->dev[d].cu_limit : s.lim.cu_limit[d];
-      uint64_t launched = L.launched.exchange(0);
-      uint64_t waited = L.waited.exchange(0);
-      double obs_rate = launched / wdt;
-      if (L.util_n == 0) continue;  // no utilization signal: keep the current rate
-      double u = L.util_acc / L.util_n;
-      L.util_acc = 0;
-      L.util_n = 0;
-      double target = (double)lim;
-      if (L.rate <= 0) {
-        // First window: calibrate from what the application actually issued.
-        L.rate = obs_rate > 0 ? obs_rate * fmin(1.0, target / fmax(u, 1.0)) : 0;
-      } else {
-        double ratio = (target + 1.0) / (u + 1.0);
-        ratio = fmax(0.5, fmin(2.0, ratio));
-        // Only grow the grant when the application was actually held back.
-        if (ratio > 1.0 && waited == 0) ratio = 1.0;
-        L.rate = fmax(L.rate * ratio, 64.0);
-      }
-      L.cap = fmax(L.rate * 0.05, 1024.0);  // 50 ms of burst
-      VLOG_DEBUG("limiter dev %d: util %.1f%% target %u%% rate %.0f wg/s (obs %.0f)", d, u, lim,
-                 L.rate, obs_rate);
     }
   }
+  g_thread_alive.store(0);
 }
 
-void limiter_start() {
-  configure();
-  int expected = 0;
-  if (!g_watcher_running.compare_exchange_strong(expected, 1)) return;
-  State& s = st();
-  bool need = g_throttle_any.load() || (s.region && s.region->num_devices > 0);
-  if (!need) return;
-  std::thread(watcher_main).detach();
-}
-
-static void priority_gate(vgpu_shared_region_t* r) {
+void priority_gate(vgpu_shared_region_t* r) {
   // Monitor preemption: a higher-priority task is active on the device.
   if (__builtin_expect(__atomic_load_n(&r->recent_kernel, __ATOMIC_RELAXED) >= 0, 1)) {
     if (__atomic_load_n(&r->recent_kernel, __ATOMIC_RELAXED) != 2)
@@ -235,7 +303,7 @@ static void priority_gate(vgpu_shared_region_t* r) {
 // rank's launches stalls the others (distributed backend row;
 // §7.4 item 8).  A kernel is RCCL's when its host stub lives in librccl (or a
 // library matching VGPU_THROTTLE_EXEMPT).  Decided once per function pointer.
-static bool exempt_kernel(const void* fn) {
+bool exempt_kernel(const void* fn) {
   if (!fn) return false;
   static std::mutex mu;
   static std::unordered_map<const void*, bool> cache;
@@ -253,45 +321,130 @@ static bool exempt_kernel(const void* fn) {
   return ex;
 }
 
-void limiter_on_launch(int dev, uint64_t wg, const void* fn) {
+}  // namespace
+
+void limiter_start() {
+  configure();
+  int expected = 0;
+  if (!g_thread_running.compare_exchange_strong(expected, 1)) return;
   State& s = st();
-  if (!s.enabled) return;
+  bool need = g_throttle_any.load() || (s.region && s.region->num_devices > 0);
+  if (!need) return;
+  std::thread(limiter_main).detach();
+}
+
+void limiter_stop() {
+  g_shutdown.store(1);
+  g_cv.notify_all();
+  for (int i = 0; i < 200 && g_thread_alive.load(); ++i) sleep_ns(1000000);
+  for (auto& L : g_lim)
+    if (L.board) {
+      board_release(L.board, L.board_slot);
+      L.board = nullptr;
+    }
+}
+
+void limiter_after_fork() {
+  // The child has no limiter thread and no live markers of its own.
+  g_thread_running.store(0);
+  g_thread_alive.store(0);
+  for (auto& L : g_lim) {
+    L.streams.clear();
+    L.free_ev.clear();
+    L.outstanding.store(0);
+    L.board = nullptr;
+    L.board_slot = -1;
+    L.board_tried = false;
+  }
+}
+
+bool limiter_on_launch(int dev, uint64_t wg, const void* fn) {
+  State& s = st();
+  if (!s.enabled) return false;
   suspend_gate();
   vgpu_proc_slot_t* sl = my_slot();
   if (s.region) priority_gate(s.region);
-  if (sl) __atomic_fetch_add(&sl->launches, 1, __ATOMIC_RELAXED);
+  if (sl) {
+    __atomic_fetch_add(&sl->launches, 1, __ATOMIC_RELAXED);
+    __atomic_store_n(&sl->last_launch_ns, mono_ns(), __ATOMIC_RELAXED);
+  }
   const bool throttling = g_throttle_any.load(std::memory_order_relaxed) != 0;
-  if (__builtin_expect(!throttling && !trace_on(), 1)) return;
+  if (__builtin_expect(!throttling && !trace_on(), 1)) return false;
   const bool exempt = throttling && exempt_kernel(fn);
   trace_emit(VGPU_EV_LAUNCH, dev, wg, exempt ? 1 : 0);
-  if (!throttling || exempt) return;
-  if (dev < 0 || dev >= VGPU_MAX_DEVICES) return;
+  if (!throttling || exempt) return false;
+  if (dev < 0 || dev >= VGPU_MAX_DEVICES) return false;
   DevLimiter& L = g_lim[dev];
-  if (!L.active) return;
-  L.launched.fetch_add(wg, std::memory_order_relaxed);
+  if (!L.active) return false;
   if (s.region && s.lim.core_policy != 1 &&
       __atomic_load_n(&s.region->utilization_switch, __ATOMIC_RELAXED) == 0)
-    return;  // monitor says no contention: run unthrottled
-  if (L.rate <= 0) return;  // not calibrated yet
-  int64_t cur = L.tokens.load(std::memory_order_relaxed);
+    return false;  // monitor says no contention: run unthrottled
+  // Wait while the bucket cannot pay for the work already in flight; once
+  // overdrawn, hold until it has refilled by a whole quantum.
   uint64_t t0 = 0;
   for (;;) {
-    if (cur > 0) {
-      if (L.tokens.compare_exchange_weak(cur, cur - (int64_t)wg, std::memory_order_relaxed)) break;
-      continue;
+    // Until the first marker completes, assume 1 ms per launch in flight.
+    int64_t per = L.ema_charge.load(std::memory_order_relaxed);
+    if (per <= 0) per = 1000000;
+    const int64_t pending = (int64_t)L.outstanding.load(std::memory_order_relaxed) * per;
+    const int64_t avail = L.tokens.load(std::memory_order_relaxed) - pending;
+    if (L.hold.load(std::memory_order_relaxed)) {
+      if (avail >= L.quantum) {
+        L.hold.store(0, std::memory_order_relaxed);
+        break;
+      }
+    } else if (avail >= 0) {
+      break;
+    } else {
+      L.hold.store(1, std::memory_order_relaxed);
     }
-    if (!t0) {
-      t0 = mono_ns();
-      L.waited.fetch_add(1, std::memory_order_relaxed);
-    }
-    sleep_ns(500000);  // 0.5 ms
-    cur = L.tokens.load(std::memory_order_relaxed);
+    if (!t0) t0 = mono_ns();
+    sleep_ns(200000);  // 0.2 ms
+    if (g_shutdown.load(std::memory_order_relaxed)) break;
   }
   if (t0) {
     const uint64_t waited = mono_ns() - t0;
     if (sl) __atomic_fetch_add(&sl->throttle_wait_ns, waited, __ATOMIC_RELAXED);
     trace_emit(VGPU_EV_THROTTLE, dev, waited, wg);
   }
+  return true;
+}
+
+void limiter_track(int dev, hipStream_t stream) {
+  if (dev < 0 || dev >= VGPU_MAX_DEVICES) return;
+  DevLimiter& L = g_lim[dev];
+  if (g_open_captures.load(std::memory_order_acquire) > 0) return;  // no HIP calls mid-capture
+  auto is_cap = REAL_HIP(hipStreamIsCapturing);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (is_cap && is_cap(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return;
+  std::unique_lock<std::mutex> g(L.mu);
+  hipEvent_t ev = nullptr;
+  if (!L.free_ev.empty()) {
+    ev = L.free_ev.back();
+    L.free_ev.pop_back();
+  } else if (REAL_HIP(hipEventCreateWithFlags)(&ev, hipEventDisableTiming) != hipSuccess) {
+    return;
+  }
+  if (REAL_HIP(hipEventRecord)(ev, stream) != hipSuccess) {
+    L.free_ev.push_back(ev);
+    return;
+  }
+  const uint64_t now = mono_ns();
+  L.streams[stream].push_back({ev, now});
+  if (L.outstanding.fetch_add(1) == 0) {
+    attach_board(dev, L);
+    L.act_mark_ns = now;
+    if (L.board) board_enter(L.board, L.board_slot);
+  }
+  g.unlock();
+  g_cv.notify_one();
+}
+
+// Fair-share GPU ns charged / wall ns busy so far on `dev` (tests, metrics).
+void limiter_stats(int dev, uint64_t* charged, uint64_t* busy) {
+  if (dev < 0 || dev >= VGPU_MAX_DEVICES) return;
+  if (charged) *charged = g_lim[dev].charged_total.load();
+  if (busy) *busy = g_lim[dev].busy_total.load();
 }
 
 }  // namespace vgpu

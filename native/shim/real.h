@@ -83,6 +83,16 @@ using hipGraphNodeGetType = hipError_t (*)(hipGraphNode_t, hipGraphNodeType*);
 using hipGraphKernelNodeGetParams = hipError_t (*)(hipGraphNode_t, hipKernelNodeParams*);
 using hipGraphChildGraphNodeGetGraph = hipError_t (*)(hipGraphNode_t, hipGraph_t*);
 using hipOccupancyMaxActiveBlocksPerMultiprocessor = hipError_t (*)(int*, const void*, int, size_t);
+using hipEventCreateWithFlags = hipError_t (*)(hipEvent_t*, unsigned);
+using hipEventRecord = hipError_t (*)(hipEvent_t, hipStream_t);
+using hipEventQuery = hipError_t (*)(hipEvent_t);
+using hipEventDestroy = hipError_t (*)(hipEvent_t);
+using hipStreamIsCapturing = hipError_t (*)(hipStream_t, hipStreamCaptureStatus*);
+using hipThreadExchangeStreamCaptureMode = hipError_t (*)(hipStreamCaptureMode*);
+using hipStreamBeginCapture = hipError_t (*)(hipStream_t, hipStreamCaptureMode);
+using hipStreamBeginCaptureToGraph = hipError_t (*)(hipStream_t, hipGraph_t, const hipGraphNode_t*,
+                                                    const hipGraphEdgeData*, size_t, hipStreamCaptureMode);
+using hipStreamEndCapture = hipError_t (*)(hipStream_t, hipGraph_t*);
 using hipGetProcAddress = hipError_t (*)(const char*, void**, int, uint64_t,
                                          hipDriverProcAddressQueryResult*);
 }  // namespace fnt

@@ -183,6 +183,9 @@ int region_purge_dead_locked(vgpu_shared_region_t* r, bool host_ns) {
   for (int i = 0; i < VGPU_MAX_PROCS; ++i) {
     vgpu_proc_slot_t& s = r->procs[i];
     if (s.status == VGPU_PROC_FREE) continue;
+    // A host-side caller cannot judge a slot whose host pid was never
+    // verified (it is a container pid, meaningless in the host namespace).
+    if (host_ns && s.host_pid_src == VGPU_HOSTPID_UNVERIFIED) { ++live; continue; }
     int pid = host_ns ? s.host_pid : s.pid;
     if (!pid_alive(pid)) {
       VLOG_INFO("purging slot %d of exited pid %d", i, pid);
@@ -227,6 +230,7 @@ int region_claim_slot(vgpu_shared_region_t* r, int pid, int host_pid, int priori
     if (found < 0) memset(&s, 0, sizeof(s));  // stale pid reuse: fresh counters
     s.pid = pid;
     s.host_pid = host_pid;
+    s.host_pid_src = VGPU_HOSTPID_UNVERIFIED;
     s.priority = priority;
     s.start_ns = mono_ns();
     __atomic_store_n(&s.status, VGPU_PROC_RUNNING, __ATOMIC_RELEASE);

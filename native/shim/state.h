@@ -12,6 +12,7 @@
 #include <mutex>
 #include <unordered_map>
 
+#include <hip/hip_runtime_api.h>
 #include <hsa/hsa.h>
 
 #include "region.h"
@@ -81,9 +82,20 @@ void charge_context(int dev);         // first-touch context charge
 
 // Compute limiting ------------------------------------------------------------
 void limiter_start();
-// Called on every dispatch with the number of workgroups it launches.
-// `fn` = the kernel's host stub when known (RCCL kernels are exempt from throttling).
-void limiter_on_launch(int dev, uint64_t workgroups, const void* fn = nullptr);
+void limiter_stop();        // exit: stop the limiter thread, release the share board
+void limiter_after_fork();
+// Called before every dispatch with the number of workgroups it launches;
+// blocks while the temporal limiter's bucket is overdrawn.  `fn` = the
+// kernel's host stub when known (RCCL kernels are exempt from throttling).
+// Returns true when the launch must be tracked: call limiter_track after a
+// successful launch on `stream`.
+bool limiter_on_launch(int dev, uint64_t workgroups, const void* fn = nullptr);
+void limiter_track(int dev, hipStream_t stream);
+// Stream captures in progress anywhere in the process: the limiter thread makes
+// no HIP call while one is open (an event query can invalidate a global-mode
+// capture on another thread).
+extern std::atomic<int> g_open_captures;
+void limiter_stats(int dev, uint64_t* charged_ns, uint64_t* busy_ns);
 void suspend_gate();
 int cu_count_masked(int dev, int physical);
 
@@ -102,6 +114,14 @@ extern thread_local int tl_device;
 // Non-zero while a HIP allocation hook is inside the real runtime call: the
 // HSA pool interposer must not charge the same bytes again.
 extern thread_local int tl_in_hip_alloc;
+
+// Host-PID resolution (hostpid.cpp) ---------------------------------------------------
+const char* kfd_proc_dir();               // VGPU_KFD_PROC_DIR | /sys/class/kfd/kfd/proc
+bool pid_ns_is_host();
+int hostpid_resolved(int* src);           // KFD-diff result, 0 = none yet
+int self_host_pid(int* src);              // best current answer + VGPU_HOSTPID_* source
+void hostpid_publish();                   // write it into this process's slot
+void hostpid_after_fork();
 
 // HSA API table mode (HSA_TOOLS_LIB OnLoad took over the hsa_* hooks).
 bool hsa_table_mode();

@@ -41,7 +41,7 @@ void trace_open() {
   h->capacity = cap;
   h->head = 0;
   h->pid = getpid();
-  h->host_pid = host_pid_of_self();
+  h->host_pid = self_host_pid(nullptr);
   h->start_ns = mono_ns();
   g_ev = reinterpret_cast<vgpu_trace_event_t*>(h + 1);
   __atomic_store_n(&g_hdr, h, __ATOMIC_RELEASE);

@@ -10,6 +10,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -27,6 +28,7 @@
 extern "C" int fake_hsa_queue_count();
 extern "C" int fake_hsa_queue_mask(int idx, uint32_t* out, int max_words, uint64_t* agent);
 extern "C" uint64_t fake_hip_launches();
+extern "C" uint64_t fake_hip_exec_ns();
 extern "C" uint64_t fake_hip_physical_used(int dev);
 extern "C" uint64_t fake_hsa_pool_used(int dev);
 extern "C" int fake_hsa_tools_loaded();
@@ -82,6 +84,60 @@ int main(int argc, char** argv) {
   if (hipSetDevice(dev) != hipSuccess) {
     printf("error=set_device\n");
     return 1;
+  }
+
+  if (sc == "duty") {
+    // Launch back-to-back for `secs` of wall time (the fake timeline gives each
+    // launch VGPU_FAKE_KERNEL_US of GPU time); report GPU time executed / wall.
+    double secs = argc > 2 ? atof(argv[2]) : 1.0;
+    const bool graphs = argc > 3 && !strcmp(argv[3], "graph");
+    hipGraphExec_t ge = nullptr;
+    if (graphs) {
+      unsigned grids[1] = {64};
+      hipGraphInstantiateWithFlags(&ge, fake_hip_graph_create(grids, 1, 0), 0);
+    }
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    const uint64_t e0 = fake_hip_exec_ns();
+    uint64_t n = 0;
+    for (;;) {
+      clock_gettime(CLOCK_MONOTONIC, &b);
+      double el = (b.tv_sec - a.tv_sec) + 1e-9 * (b.tv_nsec - a.tv_nsec);
+      if (el >= secs) break;
+      if (graphs)
+        hipGraphLaunch(ge, nullptr);
+      else
+        hipLaunchKernel((const void*)&main, dim3(64), dim3(256), nullptr, 0, nullptr);
+      ++n;
+    }
+    hipDeviceSynchronize();
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    double wall = (b.tv_sec - a.tv_sec) + 1e-9 * (b.tv_nsec - a.tv_nsec);
+    printf("launches=%llu\nexec_s=%.6f\nwall_s=%.6f\n", (unsigned long long)n,
+           (fake_hip_exec_ns() - e0) * 1e-9, wall);
+    auto gt = sym<void (*)(int, uint64_t*, uint64_t*)>("vgpu_self_gpu_time");
+    uint64_t charged = 0, busy = 0;
+    if (gt) gt(dev, &charged, &busy);
+    printf("charged_s=%.6f\nbusy_s=%.6f\n", charged * 1e-9, busy * 1e-9);
+    print_region(dev);
+    return 0;
+  }
+
+  if (sc == "hostpid") {
+    // hipSetDevice above initialised the runtime (fake hsa_init opened the fake KFD).
+    auto hp = sym<int (*)(int*)>("vgpu_self_host_pid");
+    auto self_region = sym<void* (*)()>("vgpu_self_region");
+    auto self_slot = sym<int (*)()>("vgpu_self_slot");
+    int src = -1;
+    const int h = hp ? hp(&src) : -1;
+    printf("host_pid=%d\nhost_src=%d\n", h, src);
+    if (self_region && self_slot && self_slot() >= 0) {
+      auto* r = (vgpu_shared_region_t*)self_region();
+      printf("slot_host_pid=%d\nslot_host_src=%d\n", r->procs[self_slot()].host_pid,
+             r->procs[self_slot()].host_pid_src);
+    }
+    printf("pid=%d\n", (int)getpid());
+    return 0;
   }
 
   if (sc == "meminfo") {

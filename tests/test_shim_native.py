@@ -208,3 +208,111 @@ def test_suspend_resume_signals_gate_alloc_and_launch(native_build):
     assert o["alloc_done"] == "1" and o["launch_done"] == "1"
     assert o["status_resumed"] == "1"
     assert int(o["wait_ns"]) >= 250_000_000
+
+
+def _kfd_env(tmp_path, host_pid, noise=None, lock=True):
+    proc = tmp_path / "kfdproc"
+    proc.mkdir()
+    (proc / "4242").mkdir()  # some other process already on the GPU
+    dev = tmp_path / "kfd"
+    dev.write_text("")
+    env = {"VGPU_DEVICE_MEMORY_LIMIT_0": "8g", "VGPU_KFD_DEV": str(dev), "VGPU_FAKE_KFD_DEV": str(dev),
+           "VGPU_KFD_PROC_DIR": str(proc), "VGPU_FAKE_HOST_PID": str(host_pid),
+           "VGPU_SHARED_REGION": str(tmp_path / "r.cache")}
+    if noise:
+        env["VGPU_FAKE_KFD_NOISE"] = str(noise)
+    if lock:
+        (tmp_path / "vgpulock").mkdir()
+        env["VGPU_LOCK_DIR"] = str(tmp_path / "vgpulock")
+    return env
+
+
+def test_host_pid_from_kfd_diff(native_build, tmp_path):
+    """reference set_task_pid: the new KFD process entry around our first
+    /dev/kfd open is our host pid, and it lands in the slot as verified."""
+    o = run("hostpid", env=_kfd_env(tmp_path, 777001))
+    assert o["host_pid"] == "777001"
+    assert o["host_src"] == "1"  # VGPU_HOSTPID_KFD_DIFF
+    assert o["slot_host_pid"] == "777001" and o["slot_host_src"] == "1"
+    assert (tmp_path / "vgpulock" / "lock").exists()  # the node-wide unified lock was taken
+
+
+def test_host_pid_ambiguous_diff_left_unverified(native_build, tmp_path):
+    o = run("hostpid", env=_kfd_env(tmp_path, 777002, noise=777003))
+    assert o["host_pid"] == "0"
+    assert o["slot_host_src"] in ("0", "3")  # unverified (or host namespace on a bare host)
+    assert "host pid unresolved: 2 new KFD" in o["_stderr"]
+
+
+def test_host_pid_without_lock_dir_still_resolves(native_build, tmp_path):
+    o = run("hostpid", env=_kfd_env(tmp_path, 777004, lock=False))
+    assert o["host_pid"] == "777004"
+
+
+# ---- temporal limiter: GPU-time token bucket + fair-share board ---------------------------
+def _duty(o):
+    return float(o["exec_s"]) / float(o["wall_s"])
+
+
+@pytest.mark.parametrize("limit", [25, 50])
+def test_temporal_limit_holds_gpu_time_share(native_build, limit):
+    """A lone pod with a 25 % / 50 % temporal limit gets that share of GPU time
+    (fake timeline: every launch is 500 µs of GPU work)."""
+    o = run("duty", 2, env={"VGPU_DEVICE_CU_LIMIT_0": str(limit), "VGPU_CU_MASK_FROM_LIMIT": "false",
+                            "VGPU_FAKE_KERNEL_US": "500"}, timeout=60)
+    assert abs(_duty(o) - limit / 100) < 0.04, o
+    assert abs(float(o["charged_s"]) / float(o["wall_s"]) - limit / 100) < 0.04
+
+
+def test_temporal_limit_graph_launches(native_build):
+    """Graph replays are charged by their measured GPU time too."""
+    o = run("duty", 2, "graph", env={"VGPU_DEVICE_CU_LIMIT_0": "25", "VGPU_CU_MASK_FROM_LIMIT": "false",
+                                     "VGPU_FAKE_KERNEL_US": "2000"}, timeout=60)
+    assert abs(_duty(o) - 0.25) < 0.05, o
+
+
+def test_unlimited_runs_flat_out(native_build):
+    o = run("duty", 1, env={"VGPU_FAKE_KERNEL_US": "500"}, timeout=60)
+    assert _duty(o) > 0.95
+
+
+def _pair(tmp_path, limit, board):
+    lock = tmp_path / "lock"
+    lock.mkdir(exist_ok=True)
+    env = {"VGPU_DEVICE_CU_LIMIT_0": str(limit), "VGPU_CU_MASK_FROM_LIMIT": "false",
+           "VGPU_FAKE_KERNEL_US": "500", "VGPU_FAKE_GPU_TIMELINE": str(tmp_path / "timeline"),
+           "VGPU_LOCK_DIR": str(lock), "VGPU_DEVICE_UUID_0": "GPU-test",
+           "VGPU_SHARE_BOARD": "true" if board else "false"}
+    e = {k: v for k, v in os.environ.items() if not k.startswith(("VGPU_", "CUDA_", "HIP_"))}
+    e.update({"LD_LIBRARY_PATH": str(FAKES_DIR), "LD_PRELOAD": str(shim_path())}, **env)
+    procs = [subprocess.Popen([str(FAKES_DIR / "shim_driver"), "duty", "2"], env=e, stdout=subprocess.PIPE,
+                              text=True) for _ in range(2)]
+    outs = []
+    for p in procs:
+        out, _ = p.communicate(timeout=60)
+        assert p.returncode == 0
+        outs.append(dict(l.split("=", 1) for l in out.splitlines() if "=" in l))
+    return outs
+
+
+def test_fair_share_board_two_pods_use_whole_gpu(native_build, tmp_path):
+    """Two 50 % pods time-sharing one device: charged 1/2 of the wall time each
+    while both are busy, so neither is throttled and the device stays full."""
+    a, b = _pair(tmp_path, 50, board=True)
+    agg = _duty(a) + _duty(b)
+    assert agg > 0.9, (a, b)
+    assert abs(_duty(a) - 0.5) < 0.075 and abs(_duty(b) - 0.5) < 0.075
+    assert (tmp_path / "lock" / "GPU-test.board").exists()
+
+
+def test_without_board_sharers_are_overcharged(native_build, tmp_path):
+    """Control: charging wall-clock busy time (no board) bills each pod for the
+    time it waits behind the other; the board bills only its fair share."""
+    (tmp_path / "a").mkdir()
+    (tmp_path / "b").mkdir()
+    for o in _pair(tmp_path / "a", 80, board=False):
+        assert float(o["charged_s"]) > 1.25 * float(o["exec_s"]), o
+    pair = _pair(tmp_path / "b", 80, board=True)
+    for o in pair:
+        assert 0.8 < float(o["charged_s"]) / float(o["exec_s"]) < 1.2, o
+    assert sum(_duty(o) for o in pair) > 0.9

@@ -28,6 +28,9 @@ ENV_DISABLE_CONTROL = "VGPU_DISABLE_CONTROL"
 ENV_LOG_LEVEL = "VGPU_LOG_LEVEL"
 ENV_VISIBLE = "ROCR_VISIBLE_DEVICES"
 ENV_HIP_VISIBLE = "HIP_VISIBLE_DEVICES"
+# Node-wide lock directory (unified lock + per-GPU share boards); defaults to
+# HOST_LOCK_DIR, which Allocate mounts into the container at the same path.
+ENV_LOCK_DIR = "VGPU_LOCK_DIR"
 
 # Host paths (same layout as the reference: server.go:347,354-369)
 HOST_LIB_DIR = "/usr/local/vgpu"
@@ -54,7 +57,7 @@ class DeviceGrant:
 def container_env(grants: list[DeviceGrant], region_path: str | None, *,
                   oversubscribe: bool = False, priority: int | None = None,
                   core_policy: str | None = None, disable_core_limit: bool = False,
-                  visible_var: str = ENV_VISIBLE) -> dict[str, str]:
+                  visible_var: str = ENV_VISIBLE, lock_dir: str | None = None) -> dict[str, str]:
     """Env vars for one container. Device ordinal i inside the container is
     grants[i] (ROCm honours ROCR_VISIBLE_DEVICES natively)."""
     env: dict[str, str] = {}
@@ -70,6 +73,8 @@ def container_env(grants: list[DeviceGrant], region_path: str | None, *,
         env[ENV_UUID.format(i=i)] = g.uuid
     if region_path:
         env[ENV_SHARED_REGION] = region_path
+    if lock_dir:
+        env[ENV_LOCK_DIR] = lock_dir
     if oversubscribe:
         env[ENV_OVERSUBSCRIBE] = "true"
     if priority is not None:

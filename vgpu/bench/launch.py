@@ -50,6 +50,7 @@ class Pod:
         self.env = env
         self.ready: dict | None = None
         self.done: dict | None = None
+        self.mask_bits = 0  # CUs in the pod's mask (0 = no mask)
 
     def read_tagged(self, tag: str, timeout: float, progress=None) -> dict:
         """Read stdout lines until `TAG {json}`; raises on EOF or timeout."""
@@ -89,10 +90,15 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
 
     cu_share: how a fractional pod's compute share is enforced —
       mask      one XCD-balanced CU mask per pod (device-plugin default);
-      temporal  no mask, the shim's dispatch token bucket (VGPU_CU_MASK_FROM_LIMIT=false);
+      temporal  no mask, the shim's GPU-time token bucket with fair-share charging
+                through the GPU's share board (VGPU_CU_MASK_FROM_LIMIT=false);
       group2    pods 2k and 2k+1 share one mask sized for both (A/B tool);
       group2i   pods k and k+n/2 share one mask (A/B tool)."""
     workdir = workdir or tempfile.mkdtemp(prefix="vgpu-pods-")
+    # Node-wide lock directory shared by the pods of this node (the device
+    # plugin mounts the host's /tmp/vgpulock into every vGPU container).
+    lock_dir = str(Path(workdir) / "vgpulock")
+    Path(lock_dir).mkdir(parents=True, exist_ok=True)
     used = 0
     pods = []
     group_masks: dict[int, int] = {}
@@ -105,10 +111,11 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
             g = i // 2 if cu_share == "group2" else i % max(1, (len(specs) + 1) // 2)
             if g not in group_masks:
                 m = alloc_cu_mask(used, min(100, 2 * sp.cores), MI355X)
-                if m is not None:
-                    group_masks[g] = m
-                    used |= m
-            mask = group_masks.get(g, 0)
+                if m is None:
+                    raise RuntimeError(f"{cu_share}: no CUs left for the mask of pod group {g}")
+                group_masks[g] = m
+                used |= m
+            mask = group_masks[g]
         elif sp.cores and sp.cores < 100:
             m = alloc_cu_mask(used, sp.cores, MI355X)
             if m is not None:
@@ -119,7 +126,7 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
         grant = DeviceGrant(uuid=f"GPU-{device}", index=int(device) if device.isdigit() else 0,
                             mem_mib=sp.mem_mib, cores=sp.cores, cu_mask=mask)
         cenv = container_env([grant], region, priority=sp.priority, oversubscribe=oversubscribe,
-                             visible_var=ENV_PLACEHOLDER)
+                             visible_var=ENV_PLACEHOLDER, lock_dir=lock_dir)
         cenv.pop(ENV_PLACEHOLDER, None)
         env = dict(os.environ)
         env["HIP_VISIBLE_DEVICES"] = device
@@ -147,7 +154,9 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
         cmd += ["--conv", conv]
         proc = subprocess.Popen(cmd, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                 text=True, bufsize=1, cwd=str(REPO))
-        pods.append(Pod(i, proc, region, {k: v for k, v in cenv.items()}))
+        pod = Pod(i, proc, region, {k: v for k, v in cenv.items()})
+        pod.mask_bits = bin(mask).count("1")
+        pods.append(pod)
     return pods
 
 

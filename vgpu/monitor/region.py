@@ -19,8 +19,10 @@ MAX_PROCS = 1024
 UUID_LEN = 64
 CU_WORDS = 4
 MAGIC = 0x56475055
-VERSION = 2
+VERSION = 3
 PROC_FREE, PROC_RUNNING, PROC_SUSPENDED = 0, 1, 2
+# slot.host_pid_src (how the host pid was obtained)
+HOSTPID_UNVERIFIED, HOSTPID_KFD_DIFF, HOSTPID_MONITOR, HOSTPID_HOST_NS = 0, 1, 2, 3
 
 
 class DevUsage(ctypes.Structure):
@@ -31,7 +33,8 @@ class DevUsage(ctypes.Structure):
 
 class ProcSlot(ctypes.Structure):
     _fields_ = [("pid", ctypes.c_int32), ("host_pid", ctypes.c_int32), ("status", ctypes.c_int32),
-                ("priority", ctypes.c_int32), ("start_ns", ctypes.c_uint64), ("launches", ctypes.c_uint64),
+                ("priority", ctypes.c_int32), ("host_pid_src", ctypes.c_int32), ("reserved0", ctypes.c_int32),
+                ("start_ns", ctypes.c_uint64), ("launches", ctypes.c_uint64),
                 ("throttle_wait_ns", ctypes.c_uint64), ("oom_events", ctypes.c_uint64),
                 ("last_launch_ns", ctypes.c_uint64), ("used", DevUsage * MAX_DEVICES)]
 
@@ -39,7 +42,8 @@ class ProcSlot(ctypes.Structure):
 class DeviceCfg(ctypes.Structure):
     _fields_ = [("uuid", ctypes.c_char * UUID_LEN), ("mem_limit", ctypes.c_uint64),
                 ("mem_physical", ctypes.c_uint64), ("cu_limit", ctypes.c_uint32),
-                ("cu_total", ctypes.c_uint32), ("cu_mask", ctypes.c_uint64 * CU_WORDS)]
+                ("cu_total", ctypes.c_uint32), ("cu_mask", ctypes.c_uint64 * CU_WORDS),
+                ("busy_permille", ctypes.c_uint32), ("reserved1", ctypes.c_uint32), ("busy_ns", ctypes.c_uint64)]
 
 
 class Region(ctypes.Structure):
