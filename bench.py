@@ -43,12 +43,12 @@ def enforcement_label(args) -> str:
         return "none"
     if args.gpucores <= 0 or args.gpucores >= 100:
         return "libvgpu.so (HBM cap; whole GPU, no compute limit)"
-    return {
-        "mask": "libvgpu.so (HBM cap + XCD-balanced CU mask per pod)",
-        "temporal": "libvgpu.so (HBM cap + GPU-time token bucket, fair-share board; no CU mask)",
-        "group2": "libvgpu.so (HBM cap + one CU mask per pod pair 2k,2k+1)",
-        "group2i": "libvgpu.so (HBM cap + one CU mask per pod pair k,k+n/2)",
-    }[args.cu_share]
+    if args.cu_share == "group2":
+        return "libvgpu.so (HBM cap + one CU mask per pod pair 2k,2k+1)"
+    if args.cu_share == "group2i":
+        return "libvgpu.so (HBM cap + one CU mask per pod pair k,k+n/2)"
+    return (f"device-plugin Allocate (cu_share={args.cu_share}) + libvgpu.so: HBM cap, "
+            "per-pod XCD-balanced CU masks and/or GPU-time limiter with fair-share board")
 
 
 def main(argv=None) -> int:
@@ -69,8 +69,9 @@ def main(argv=None) -> int:
                     help="ResNet convolutions: fused MFMA implicit-GEMM kernels or MIOpen")
     ap.add_argument("--hw-queues", type=int, default=1,
                     help="GPU_MAX_HW_QUEUES per pod (vGPU HW-queue budget; 0 = runtime default)")
-    ap.add_argument("--cu-share", choices=("mask", "temporal", "group2", "group2i"), default="mask",
-                    help="compute-share enforcement of fractional pods (vgpu.bench.launch.launch_pods)")
+    ap.add_argument("--cu-share", choices=("hybrid", "mask", "temporal", "group2", "group2i"), default="hybrid",
+                    help="compute-share policy of fractional pods: the device plugin's "
+                         "(hybrid|mask|temporal, vgpu/deviceplugin/custate.py) or an A/B tool")
     ap.add_argument("--no-cap-probe", action="store_true")
     ap.add_argument("--ready-timeout", type=float, default=1500.0)
     ap.add_argument("--cpu-smoke", action="store_true",
@@ -189,6 +190,7 @@ def main(argv=None) -> int:
             "per_gpu_images_s": round(per_gpu, 2),
             "per_pod_images_s": [round(p.done["throughput"], 2) for p in pods],
             "per_pod_cu_mask_bits": [p.mask_bits for p in pods],
+            "per_pod_share": [p.share for p in pods],
             "vram_cap": cap,
         }
         print(json.dumps(res), flush=True)

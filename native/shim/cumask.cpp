@@ -227,6 +227,13 @@ int cumask_device_cus(int dev) {
   return (int)a->cus;
 }
 
+int cumask_device_physical_cus(int dev) {
+  std::lock_guard<std::mutex> g(g_mu);
+  ensure_agents_locked();
+  AgentInfo* a = agent_for_hip_index(dev);
+  return a ? (int)a->cus : -1;
+}
+
 uint32_t cumask_driver_uid(int dev) {
   std::lock_guard<std::mutex> g(g_mu);
   AgentInfo* a = agent_for_hip_index(dev);

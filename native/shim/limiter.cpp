@@ -34,6 +34,7 @@
 // and converges on hardware without calibration.
 #include <dlfcn.h>
 #include <math.h>
+#include <strings.h>
 #include <sys/stat.h>
 
 #include <condition_variable>
@@ -55,6 +56,7 @@ std::atomic<int> g_open_captures{0};
 
 extern int cumask_device_cus(int dev);        // CUs available to us (mask or physical)
 extern uint32_t cumask_driver_uid(int dev);   // KFD gpu_id of device, 0 = unknown
+extern int cumask_device_physical_cus(int dev);
 
 namespace {
 
@@ -65,7 +67,8 @@ struct Marker {
 
 struct DevLimiter {
   int active = 0;             // temporal limiting configured for this device
-  double frac = 0;            // limit / 100
+  double frac = 0;            // share of the time this process may have work on the device
+  std::atomic<int> pool_scale_pending{0};  // frac still to be scaled by device CUs / pool CUs
   std::atomic<int64_t> tokens{0};  // fair-share GPU ns we may still spend
   int64_t cap = 0;            // bucket depth (ns)
   int64_t quantum = 0;        // an overdrawn bucket must refill this far before launches resume
@@ -128,6 +131,27 @@ void attach_board(int dev, DevLimiter& L) {
   VLOG_INFO("device %d: fair-share board %s slot %d", dev, path, L.board_slot);
 }
 
+// A pool member's limit is a share of the whole device, but its work only
+// runs on the pool's CUs: a 25 % vGPU on a 128-CU pool of a 256-CU device may
+// keep the pool busy 50 % of the time.  Needs the HSA agents (first launch).
+void apply_pool_scale(int dev, DevLimiter& L) {
+  int expected = 1;
+  if (!L.pool_scale_pending.compare_exchange_strong(expected, 0)) return;
+  State& s = st();
+  int pool = 0;
+  for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w)
+    pool += __builtin_popcountll(__atomic_load_n(&s.region->dev[dev].cu_mask[w], __ATOMIC_RELAXED));
+  const int phys = cumask_device_physical_cus(dev);
+  if (pool <= 0 || phys <= 0 || pool >= phys) return;
+  const double f = fmin(1.0, L.frac * phys / pool);
+  VLOG_INFO("device %d: pool of %d/%d CUs, time share %.0f%% -> %.0f%%", dev, pool, phys, 100 * L.frac, 100 * f);
+  const double r = f / L.frac;
+  L.frac = f;
+  L.cap = (int64_t)(L.cap * r);
+  L.quantum = (int64_t)(L.quantum * r);
+  L.tokens.store(L.cap);
+}
+
 // Decide per device whether temporal throttling applies.
 void configure() {
   State& s = st();
@@ -137,15 +161,22 @@ void configure() {
     bool has_mask = false;
     if (s.region)
       for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) has_mask |= s.region->dev[d].cu_mask[w] != 0;
+    const char* share = env_first("VGPU_CU_SHARE");
+    // VGPU_CU_SHARE=temporal (device plugin, pool member): the share is
+    // enforced in time; a mask, if any, is the pool of CUs the pool members share.
+    const bool temporal_share = share && !strcasecmp(share, "temporal");
     bool want = lim > 0 && lim < 100 && s.lim.core_policy != 2;
-    // A CU mask already enforces the share spatially; temporal limiting on top
-    // of it only when explicitly forced.
-    if (has_mask && s.lim.core_policy != 1) want = false;
-    if (!has_mask && s.lim.core_policy == 0 && env_bool(env_first("VGPU_CU_MASK_FROM_LIMIT"), true))
-      want = false;  // cumask.cpp derives a balanced mask from the limit
+    if (!temporal_share) {
+      // A CU mask already enforces the share spatially; temporal limiting on
+      // top of it only when explicitly forced.
+      if (has_mask && s.lim.core_policy != 1) want = false;
+      if (!has_mask && s.lim.core_policy == 0 && env_bool(env_first("VGPU_CU_MASK_FROM_LIMIT"), true))
+        want = false;  // cumask.cpp derives a balanced mask from the limit
+    }
     DevLimiter& L = g_lim[d];
     if (want && !L.active) {
       L.frac = lim / 100.0;
+      L.pool_scale_pending.store(temporal_share && has_mask ? 1 : 0);
       const double burst_ms = env_first("VGPU_LIMITER_BURST_MS") ? atof(env_first("VGPU_LIMITER_BURST_MS")) : 50.0;
       L.cap = (int64_t)(L.frac * burst_ms * 1e6);
       // Time-slice quantum: a throttled pod runs in slices of ~quantum_ms of
@@ -376,6 +407,7 @@ bool limiter_on_launch(int dev, uint64_t wg, const void* fn) {
   if (dev < 0 || dev >= VGPU_MAX_DEVICES) return false;
   DevLimiter& L = g_lim[dev];
   if (!L.active) return false;
+  if (__builtin_expect(L.pool_scale_pending.load(std::memory_order_relaxed), 0)) apply_pool_scale(dev, L);
   if (s.region && s.lim.core_policy != 1 &&
       __atomic_load_n(&s.region->utilization_switch, __ATOMIC_RELAXED) == 0)
     return false;  // monitor says no contention: run unthrottled

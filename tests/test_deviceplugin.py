@@ -110,15 +110,47 @@ def test_discovery_sysfs(native_build, tmp_path):
 
 # ---- CU-mask state ------------------------------------------------------------------------
 def test_cumask_state_disjoint_and_gc(tmp_path):
-    st = CUMaskState(str(tmp_path))
+    st = CUMaskState(str(tmp_path), policy="mask")
     a = st.allocate("uid1_c", [("GPU-0", 50)])["GPU-0"]
     b = st.allocate("uid2_c", [("GPU-0", 50)])["GPU-0"]
-    assert a and b and a & b == 0 and MI355X.per_xcd_counts(a) == [16] * 8
-    assert st.allocate("uid3_c", [("GPU-0", 25)])["GPU-0"] == 0  # device fully partitioned
-    assert st.allocate("uid4_c", [("GPU-1", 100)])["GPU-1"] == 0  # exclusive: no mask
-    assert st.used("GPU-0") == a | b
+    assert a.mask and b.mask and a.mask & b.mask == 0 and MI355X.per_xcd_counts(a.mask) == [16] * 8
+    c = st.allocate("uid3_c", [("GPU-0", 25)])["GPU-0"]
+    assert c.temporal and c.mask == 0  # device fully partitioned: temporal pool (no CUs left to pin)
+    e = st.allocate("uid4_c", [("GPU-1", 100)])["GPU-1"]
+    assert e.mask == 0 and not e.temporal  # exclusive: no mask, no limiter
+    assert st.used("GPU-0") == a.mask | b.mask
     removed = st.gc({"uid2"}, grace_s=0)
-    assert "uid1_c" in removed and st.used("GPU-0") == b
+    assert "uid1_c" in removed and st.used("GPU-0") == b.mask
+
+
+def test_cumask_state_hybrid_policy_pools_after_two_masks(tmp_path):
+    """hybrid: two masked pods per GPU, later fractional pods share the rest in time."""
+    st = CUMaskState(str(tmp_path), policy="hybrid", max_mask_slots=2)
+    g = [st.allocate(f"u{i}_c", [("GPU-0", 25)])["GPU-0"] for i in range(4)]
+    assert [x.mode for x in g] == ["mask", "mask", "pool", "pool"]
+    assert g[0].mask & g[1].mask == 0 and bin(g[0].mask).count("1") == 64
+    pool = ((1 << 256) - 1) & ~(g[0].mask | g[1].mask)
+    assert g[2].mask == pool and g[3].mask == pool and bin(pool).count("1") == 128
+    assert st.pool_members("GPU-0") == 2
+    # a freed mask slot goes to the next pod, outside the pool's CUs
+    st.gc({"u0", "u2", "u3"}, grace_s=0)
+    n = st.allocate("u4_c", [("GPU-0", 25)])["GPU-0"]
+    assert n.mode == "mask" and n.mask & pool == 0 and n.mask & g[0].mask == 0
+
+
+def test_cumask_state_temporal_policy_never_masks(tmp_path):
+    st = CUMaskState(str(tmp_path), policy="temporal")
+    for i in range(3):
+        sg = st.allocate(f"u{i}_c", [("GPU-0", 25)])["GPU-0"]
+        assert sg.temporal and sg.mask == 0
+    assert st.used("GPU-0") == 0
+
+
+def test_cumask_state_reads_round1_grant_format(tmp_path):
+    (tmp_path / "old_c").mkdir()
+    (tmp_path / "old_c" / "grant.json").write_text(json.dumps({"GPU-0": "0xff"}))
+    st = CUMaskState(str(tmp_path))
+    assert st.used("GPU-0") == 0xFF
 
 
 # ---- end to end ------------------------------------------------------------------------------

@@ -316,3 +316,20 @@ def test_without_board_sharers_are_overcharged(native_build, tmp_path):
     for o in pair:
         assert 0.8 < float(o["charged_s"]) / float(o["exec_s"]) < 1.2, o
     assert sum(_duty(o) for o in pair) > 0.9
+
+
+def test_pool_member_time_share_scaled_to_pool(native_build):
+    """A 25 % vGPU in a 128-CU pool (device plugin hybrid policy) may keep the
+    pool busy half of the time: its work never reaches the other 128 CUs."""
+    pool = hex(int("ff" * 16, 16))  # 128 low CUs
+    o = run("duty", 2, env={"VGPU_DEVICE_CU_LIMIT_0": "25", "VGPU_CU_MASK_0": pool, "VGPU_CU_SHARE": "temporal",
+                            "VGPU_CU_MASK_FROM_LIMIT": "false", "VGPU_FAKE_KERNEL_US": "500",
+                            "VGPU_LOG_LEVEL": "3"}, timeout=60)
+    assert abs(_duty(o) - 0.5) < 0.05, o
+    assert "pool of 128/256 CUs, time share 25% -> 50%" in o["_stderr"]
+
+
+def test_masked_pod_without_temporal_share_is_not_throttled(native_build):
+    o = run("duty", 1, env={"VGPU_DEVICE_CU_LIMIT_0": "25", "VGPU_CU_MASK_0": hex((1 << 64) - 1),
+                            "VGPU_FAKE_KERNEL_US": "500"}, timeout=60)
+    assert _duty(o) > 0.95

@@ -18,6 +18,9 @@ from dataclasses import dataclass
 ENV_MEM_LIMIT = "VGPU_DEVICE_MEMORY_LIMIT_{i}"
 ENV_CU_LIMIT = "VGPU_DEVICE_CU_LIMIT_{i}"
 ENV_CU_MASK = "VGPU_CU_MASK_{i}"
+# "temporal": the container's compute share is enforced in time (GPU-time limiter);
+# a VGPU_CU_MASK_<i> given with it is the shared pool the container runs on.
+ENV_CU_SHARE = "VGPU_CU_SHARE"
 ENV_UUID = "VGPU_DEVICE_UUID_{i}"
 ENV_SHARED_REGION = "VGPU_SHARED_REGION"
 ENV_OVERSUBSCRIBE = "VGPU_OVERSUBSCRIBE"

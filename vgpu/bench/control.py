@@ -1,0 +1,148 @@
+"""Admit benchmark pods through the real control plane.
+
+Every pod goes through the same path as in a cluster:
+* the mutating webhook;
+* the scheduler extender (`Scheduler.filter` + `bind`: scoring, node lock,
+  annotations);
+* the device plugin's `allocate` (compute-share policy, CU masks, HBM caps, env
+  contract, mounts).
+
+The API server is the in-process fake. The node is this machine, with the one
+physical GPU the pods share. The returned environments are what kubelet would
+hand the containers. Container mount paths are rewritten to the host paths
+behind them, so the pod processes run on the host.
+
+Reference flow: pkg/scheduler/scheduler.go:312-402 (Filter/Bind),
+pkg/device-plugin/nvidiadevice/nvinternal/plugin/server.go:280-403 (Allocate).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from pathlib import Path
+
+from vgpu import config
+from vgpu.api import resources as R
+from vgpu.config import DevicePluginConfig, SchedulerConfig
+from vgpu.device.base import init_default_devices
+from vgpu.deviceplugin.allocate import ContainerGrant, allocate
+from vgpu.deviceplugin.custate import CUMaskState
+from vgpu.deviceplugin.discovery import Device
+from vgpu.deviceplugin.register import register_once
+from vgpu.k8s.client import KubeClient
+from vgpu.k8s.fakeapi import FakeApiServer
+from vgpu.scheduler.core import Scheduler
+from vgpu.scheduler.webhook import handle_admission
+
+NODE = "bench-node"
+
+
+@dataclass
+class AdmittedPod:
+    name: str
+    env: dict = field(default_factory=dict)       # container env, host paths
+    grant: ContainerGrant | None = None
+    cu_mask_bits: int = 0
+    share: str = "none"                           # mask | temporal | none
+
+
+def _pod(name: str, mem_mib: int, cores: int, priority: int | None) -> dict:
+    lim = {R.RESOURCE_COUNT: "1"}
+    if mem_mib:
+        lim[R.RESOURCE_MEM] = str(mem_mib)
+    if cores:
+        lim[R.RESOURCE_CORES] = str(cores)
+    if priority is not None:
+        lim[R.RESOURCE_PRIORITY] = str(priority)
+    return {"apiVersion": "v1", "kind": "Pod",
+            "metadata": {"name": name, "namespace": "bench", "uid": f"uid-{name}", "annotations": {}},
+            "spec": {"containers": [{"name": "main", "image": "bench", "resources": {"limits": lim}}]}}
+
+
+def _host_path(value: str, mounts: list) -> str:
+    for cpath, hpath, _ in sorted(mounts, key=lambda m: -len(m[0])):
+        if value == cpath or value.startswith(cpath.rstrip("/") + "/"):
+            return hpath + value[len(cpath):]
+    return value
+
+
+def admit_pods(specs: list, device_index: int, workdir: str, *, policy: str = "hybrid",
+               max_mask_slots: int = 2, memory_scaling: float = 1.0,
+               device: Device | None = None) -> list[AdmittedPod]:
+    """Admit `specs` (vgpu.bench.launch.PodSpec) onto one physical GPU."""
+    init_default_devices()
+    config.SCHEDULER = SchedulerConfig(gpu_scheduler_policy="binpack")
+    work = Path(workdir)
+    host_lib = work / "host"
+    lock = work / "vgpulock"
+    lock.mkdir(parents=True, exist_ok=True)
+    cfg = DevicePluginConfig(node_name=NODE, device_split_count=max(10, len(specs)), config_file="",
+                             host_lib_dir=str(host_lib), host_lock_dir=str(lock), cu_share=policy,
+                             max_mask_slots=max_mask_slots, device_memory_scaling=memory_scaling)
+    dev = device or Device(uuid=f"GPU-bench-{device_index}", index=device_index,
+                           render_minor=128 + device_index, card=device_index)
+    srv = FakeApiServer()
+    url = srv.start()
+    try:
+        client = KubeClient(url)
+        srv.add_node(NODE)
+        register_once(client, NODE, [dev], cfg)
+        sched = Scheduler(client)
+        sched.register_from_node_annotations_once()
+        cu_state = CUMaskState(str(host_lib / "containers"), policy=policy, max_mask_slots=max_mask_slots)
+        out = []
+        for i, sp in enumerate(specs):
+            name = f"pod{i}"
+            pod = _pod(name, sp.mem_mib, sp.cores, sp.priority)
+            review = handle_admission({"request": {"uid": name, "object": pod}})
+            if not review["response"]["allowed"]:
+                raise RuntimeError(f"webhook refused {name}: {review}")
+            srv.add_pod(pod)
+            r = sched.filter({"pod": client.get_pod("bench", name), "nodenames": [NODE]})
+            if r.get("nodenames") != [NODE]:
+                raise RuntimeError(f"scheduler could not place {name}: {r}")
+            b = sched.bind({"podName": name, "podNamespace": "bench", "podUID": f"uid-{name}", "node": NODE})
+            if b.get("error"):
+                raise RuntimeError(f"bind {name}: {b['error']}")
+            grant = allocate(client, cfg, R.VENDOR, [[f"{dev.uuid}-{i}"]], {dev.uuid: dev}, cu_state, NODE)[0]
+            env = {k: _host_path(v, grant.mounts) for k, v in grant.envs.items()}
+            env["VGPU_LOCK_DIR"] = str(lock)
+            # the per-container cache dir is a host directory the plugin mounts
+            region = Path(env.get("VGPU_SHARED_REGION", str(work / name / "vgpu.cache")))
+            region.parent.mkdir(parents=True, exist_ok=True)
+            mask = env.get("VGPU_CU_MASK_0", "0x0")
+            share = "temporal" if env.get("VGPU_CU_SHARE") == "temporal" else (
+                "mask" if int(mask, 16) else "none")
+            out.append(AdmittedPod(name, env, grant, bin(int(mask, 16)).count("1"), share))
+        return out
+    finally:
+        srv.stop()
+
+
+def container_visible_env(device_index: int) -> dict:
+    """Device selection for a host process standing in for the container (the
+    container would only see its own render node)."""
+    return {"HIP_VISIBLE_DEVICES": str(device_index), "ROCR_VISIBLE_DEVICES": None}
+
+
+def apply_env(base: dict, env: dict) -> dict:
+    out = dict(base)
+    for k, v in env.items():
+        if v is None:
+            out.pop(k, None)
+        else:
+            out[k] = v
+    return out
+
+
+__all__ = ["admit_pods", "AdmittedPod", "apply_env", "container_visible_env", "NODE"]
+
+if __name__ == "__main__":  # pragma: no cover - manual inspection
+    import json
+    import tempfile
+    from vgpu.bench.launch import PodSpec
+    pods = admit_pods([PodSpec(cores=25, mem_mib=72000)] * 4, 0, tempfile.mkdtemp())
+    print(json.dumps([{"name": p.name, "share": p.share, "cus": p.cu_mask_bits,
+                       "env": {k: v for k, v in p.env.items() if k.startswith(("VGPU", "GPU"))}}
+                      for p in pods], indent=1), flush=True)
+    os._exit(0)

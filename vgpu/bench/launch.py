@@ -1,10 +1,10 @@
-"""Node-local pod launcher: emulates the device plugin's ``Allocate`` for N pods
-sharing one physical GPU, without Kubernetes.
+"""Node-local pod launcher: N pods sharing one physical GPU.
 
-Each pod gets exactly what a scheduled container would get: its own shared
-region file, VGPU_DEVICE_MEMORY_LIMIT_0 / VGPU_DEVICE_CU_LIMIT_0, an
-XCD-balanced CU mask from the same allocator the device plugin uses, and
-LD_PRELOAD of libvgpu.so.
+Pods are admitted through the real control plane (vgpu.bench.control: webhook,
+scheduler filter/bind, device plugin Allocate against an in-process API
+server).  Each one runs with the env Allocate returned: its own shared region,
+HBM cap, compute limit, CU mask or pool membership.  LD_PRELOAD of libvgpu.so
+stands in for the /etc/ld.so.preload mount.
 """
 from __future__ import annotations
 
@@ -51,6 +51,7 @@ class Pod:
         self.ready: dict | None = None
         self.done: dict | None = None
         self.mask_bits = 0  # CUs in the pod's mask (0 = no mask)
+        self.share = "none"  # mask | temporal | none (how its compute share is enforced)
 
     def read_tagged(self, tag: str, timeout: float, progress=None) -> dict:
         """Read stdout lines until `TAG {json}`; raises on EOF or timeout."""
@@ -85,49 +86,55 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
                 graph: bool = True, cap_probe: bool = False, find: bool = False,
                 workdir: str | None = None, oversubscribe: bool = False,
                 hw_queues: int | None = None, fused: bool = True,
-                conv: str = "native", cu_share: str = "mask") -> list[Pod]:
+                conv: str = "native", cu_share: str = "hybrid", memory_scaling: float = 1.0) -> list[Pod]:
     """Start one process per pod on physical device `device`.
 
-    cu_share: how a fractional pod's compute share is enforced —
-      mask      one XCD-balanced CU mask per pod (device-plugin default);
-      temporal  no mask, the shim's GPU-time token bucket with fair-share charging
-                through the GPU's share board (VGPU_CU_MASK_FROM_LIMIT=false);
-      group2    pods 2k and 2k+1 share one mask sized for both (A/B tool);
-      group2i   pods k and k+n/2 share one mask (A/B tool)."""
+    cu_share: how a fractional pod's compute share is enforced.
+      hybrid, mask, temporal: the device plugin's share policy
+        (vgpu/deviceplugin/custate.py).  Pods are admitted through the real
+        control plane (webhook → scheduler filter/bind → device plugin
+        Allocate, vgpu.bench.control) and run with exactly the env Allocate
+        returns.
+      group2, group2i: A/B tools outside the plugin.  Pods 2k and 2k+1
+        (group2i: k and k+n/2) share one mask sized for both."""
     workdir = workdir or tempfile.mkdtemp(prefix="vgpu-pods-")
     # Node-wide lock directory shared by the pods of this node (the device
     # plugin mounts the host's /tmp/vgpulock into every vGPU container).
     lock_dir = str(Path(workdir) / "vgpulock")
     Path(lock_dir).mkdir(parents=True, exist_ok=True)
+    admitted = None
+    if shim and cu_share in ("hybrid", "mask", "temporal"):
+        from vgpu.bench.control import admit_pods
+        admitted = admit_pods(specs, int(device) if device.isdigit() else 0, workdir, policy=cu_share,
+                              memory_scaling=max(memory_scaling, 2.0 if oversubscribe else 1.0))
     used = 0
     pods = []
     group_masks: dict[int, int] = {}
     for i, sp in enumerate(specs):
         mask = 0
-        extra = {}
-        if sp.cores and sp.cores < 100 and cu_share == "temporal":
-            extra["VGPU_CU_MASK_FROM_LIMIT"] = "false"
-        elif sp.cores and sp.cores < 100 and cu_share in ("group2", "group2i"):
-            g = i // 2 if cu_share == "group2" else i % max(1, (len(specs) + 1) // 2)
-            if g not in group_masks:
-                m = alloc_cu_mask(used, min(100, 2 * sp.cores), MI355X)
-                if m is None:
-                    raise RuntimeError(f"{cu_share}: no CUs left for the mask of pod group {g}")
-                group_masks[g] = m
-                used |= m
-            mask = group_masks[g]
-        elif sp.cores and sp.cores < 100:
-            m = alloc_cu_mask(used, sp.cores, MI355X)
-            if m is not None:
-                mask = m
-                used |= m
-        region = str(Path(workdir) / f"pod{i}" / "vgpu.cache")
-        Path(region).parent.mkdir(parents=True, exist_ok=True)
-        grant = DeviceGrant(uuid=f"GPU-{device}", index=int(device) if device.isdigit() else 0,
-                            mem_mib=sp.mem_mib, cores=sp.cores, cu_mask=mask)
-        cenv = container_env([grant], region, priority=sp.priority, oversubscribe=oversubscribe,
-                             visible_var=ENV_PLACEHOLDER, lock_dir=lock_dir)
-        cenv.pop(ENV_PLACEHOLDER, None)
+        if admitted is not None:
+            cenv = dict(admitted[i].env)
+            mask_bits = admitted[i].cu_mask_bits
+        else:
+            if sp.cores and sp.cores < 100 and cu_share in ("group2", "group2i"):
+                g = i // 2 if cu_share == "group2" else i % max(1, (len(specs) + 1) // 2)
+                if g not in group_masks:
+                    m = alloc_cu_mask(used, min(100, 2 * sp.cores), MI355X)
+                    if m is None:
+                        raise RuntimeError(f"{cu_share}: no CUs left for the mask of pod group {g}")
+                    group_masks[g] = m
+                    used |= m
+                mask = group_masks[g]
+            region = str(Path(workdir) / f"pod{i}" / "vgpu.cache")
+            Path(region).parent.mkdir(parents=True, exist_ok=True)
+            grant = DeviceGrant(uuid=f"GPU-{device}", index=int(device) if device.isdigit() else 0,
+                                mem_mib=sp.mem_mib, cores=sp.cores, cu_mask=mask)
+            cenv = container_env([grant], region, priority=sp.priority, oversubscribe=oversubscribe,
+                                 visible_var=ENV_PLACEHOLDER, lock_dir=lock_dir)
+            cenv.pop(ENV_PLACEHOLDER, None)
+            mask_bits = bin(mask).count("1")
+        if sp.priority is not None:
+            cenv.setdefault("VGPU_TASK_PRIORITY", str(sp.priority))
         env = dict(os.environ)
         env["HIP_VISIBLE_DEVICES"] = device
         env.pop("CUDA_VISIBLE_DEVICES", None)
@@ -139,7 +146,6 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
         if shim:
             env.update(cenv)
             env = preload_env(env)
-        env.update(extra)
         env.update(sp.extra_env)
         cmd = [sys.executable, "-u", "-m", "vgpu.bench.pod", "--workload", sp.workload,
                "--steps", str(steps), "--warmup", str(warmup), "--pod-index", str(i)]
@@ -154,8 +160,9 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
         cmd += ["--conv", conv]
         proc = subprocess.Popen(cmd, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                 text=True, bufsize=1, cwd=str(REPO))
-        pod = Pod(i, proc, region, {k: v for k, v in cenv.items()})
-        pod.mask_bits = bin(mask).count("1")
+        pod = Pod(i, proc, cenv.get("VGPU_SHARED_REGION", ""), {k: v for k, v in cenv.items()})
+        pod.mask_bits = mask_bits
+        pod.share = admitted[i].share if admitted is not None else cu_share
         pods.append(pod)
     return pods
 

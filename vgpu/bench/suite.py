@@ -2,9 +2,12 @@
 publishes (BASELINE.md rows 1.1–5.2) in three scenarios, mirroring the
 reference's comparison (README.md:234-257):
 
-  exclusive   — one pod, whole GPU, no enforcement library
-  vgpu        — `--pods` pods sharing the GPU (default 2 × gpucores=50, gpumem=144000)
-  vgpu-cu25   — 4 pods × gpucores=25 (BASELINE.json config 3 for the training tests)
+  exclusive          — one pod, whole GPU, no enforcement library
+  vgpu               — 2 pods × gpucores=50, gpumem=144000 (BASELINE.json config 2)
+  vgpu-cu25          — 4 pods × gpucores=25 (BASELINE.json config 3), device-plugin
+                       default share policy (hybrid: 2 CU masks + a temporal pool)
+  vgpu-cu25-temporal — the same 4 pods, all under the GPU-time limiter
+  vgpu-cu25-mask     — the same 4 pods, one CU mask each
 
 Prints one JSON line per (test, scenario) and a markdown table at the end.
     python -m vgpu.bench.suite [--tests 1.1,1.2,...] [--steps 20]
@@ -23,6 +26,8 @@ SCENARIOS = {
     "exclusive": ["--pods", "1", "--no-shim", "--gpucores", "100", "--gpumem", "0"],
     "vgpu": ["--pods", "2", "--gpucores", "50", "--gpumem", "144000"],
     "vgpu-cu25": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000"],
+    "vgpu-cu25-temporal": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "temporal"],
+    "vgpu-cu25-mask": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "mask"],
 }
 
 
@@ -38,7 +43,7 @@ def run(test: str, scen: str, steps: int, warmup: int, timeout: int) -> dict:
         return {"test": test, "scenario": scen, "error": r.stderr[-1500:]}
     d = json.loads(js[-1])
     return {"test": test, "scenario": scen, "images_s": d["value"], "per_pod": d["per_pod_images_s"],
-            "ms_per_step": d["ms_per_step"]}
+            "ms_per_step": d["ms_per_step"], "share": d.get("per_pod_share")}
 
 
 def main(argv=None) -> int:

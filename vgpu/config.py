@@ -52,6 +52,14 @@ class DevicePluginConfig:
     hw_queues_per_vgpu: int = 1           # GPU_MAX_HW_QUEUES for fractional vGPUs (0 = runtime default)
     hsa_tools_intercept: bool = False     # also hand the shim ROCr's API table (HSA_TOOLS_LIB)
     partition_mode: str = ""             # SPX|DPX|QPX|CPX expected compute partition ("" = as found)
+    # How a fractional vGPU's compute share is enforced (vgpu/deviceplugin/custate.py):
+    #   mask      an XCD-balanced CU mask per container (temporal only when no granules are free)
+    #   temporal  no per-container mask: the shim's GPU-time limiter with fair-share charging
+    #   hybrid    CU masks for the first `max_mask_slots` fractional containers of a GPU, the
+    #             rest share the remaining CUs (one pool mask) under the temporal limiter
+    cu_share: str = "hybrid"
+    max_mask_slots: int = 2
+    host_lock_dir: str = "/tmp/vgpulock"  # node-wide unified lock + per-GPU share boards
     device_list_strategy: str = "envvar"  # envvar (device nodes in the response) | cdi-annotations | cdi-cri
     cdi_dir: str = "/var/run/cdi"
     config_file: str = "/config/config.json"

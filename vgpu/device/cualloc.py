@@ -71,6 +71,19 @@ def popcount(m: int) -> int:
 PACKINGS = ("spread", "se")
 
 
+def resolve_packing(pack: str | None = None, layout: CULayout = MI355X) -> str:
+    """Validate a packing name (default: VGPU_CU_PACK, else "spread") and return
+    the packing that takes effect on `layout`.  "se" needs whole SE groups of
+    granules and degrades to "spread" otherwise.  Callers resolve this once at
+    start-up, so a bad value fails there and not inside Allocate."""
+    pack = pack or os.environ.get("VGPU_CU_PACK", "spread")
+    if pack not in PACKINGS:
+        raise ValueError(f"unknown CU packing {pack!r} (one of {PACKINGS})")
+    if pack == "se" and not (layout.num_se > 1 and layout.granules % layout.num_se == 0):
+        return "spread"
+    return pack
+
+
 def granule_order(layout: CULayout, pack: str | None = None) -> list[int]:
     """Order in which free granules are taken.
 
@@ -78,10 +91,7 @@ def granule_order(layout: CULayout, pack: str | None = None) -> list[int]:
     se:     all granules of SE 0, then SE 1, ... — a pod owns whole shader
             engines where its share allows, so no two pods feed the same SE's
             workgroup dispatcher."""
-    pack = pack or os.environ.get("VGPU_CU_PACK", "spread")
-    if pack not in PACKINGS:
-        raise ValueError(f"unknown CU packing {pack!r} (one of {PACKINGS})")
-    if pack == "se" and layout.num_se > 1 and layout.granules % layout.num_se == 0:
+    if resolve_packing(pack, layout) == "se":
         return [g for se in range(layout.num_se) for g in range(se, layout.granules, layout.num_se)]
     return list(range(layout.granules))
 

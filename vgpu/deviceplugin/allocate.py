@@ -25,7 +25,7 @@ from dataclasses import dataclass, field
 
 from vgpu.api import resources as R
 from vgpu.api.codec import decode_pod_devices, encode_pod_devices
-from vgpu.api.env import (ENV_CU_LIMIT, ENV_CU_MASK, ENV_CORE_POLICY, ENV_DISABLE_CONTROL, ENV_MEM_LIMIT,
+from vgpu.api.env import (ENV_CU_LIMIT, ENV_CU_MASK, ENV_CU_SHARE, ENV_CORE_POLICY, ENV_DISABLE_CONTROL, ENV_MEM_LIMIT,
                           ENV_OVERSUBSCRIBE, ENV_SHARED_REGION, ENV_UUID, PRELOAD_FILE, SHIM_NAME,
                           format_mask)
 from vgpu.api.resources import ContainerDevice
@@ -148,11 +148,12 @@ def build_container_grant(cfg: DevicePluginConfig, pod: dict, ctr_idx: int, devr
             raise AllocateError(f"unknown device {d.uuid}")
     layouts = {d.uuid: CULayout(total_cus=devices[d.uuid].cus or 256,
                                 num_xcc=max(devices[d.uuid].num_xcc or 1, 1)) for d in ordered}
-    masks = {} if cfg.disable_core_limit else cu_state.allocate(
+    shares = {} if cfg.disable_core_limit else cu_state.allocate(
         key, [(d.uuid, d.usedcores) for d in ordered], layouts)
     g = ContainerGrant()
     env_names = _ctr_env_names(pod, ctr_idx)
     fractional = False
+    temporal = False
     for i, d in enumerate(ordered):
         dev = devices[d.uuid]
         g.envs[ENV_MEM_LIMIT.format(i=i)] = f"{d.usedmem}m"
@@ -160,16 +161,19 @@ def build_container_grant(cfg: DevicePluginConfig, pod: dict, ctr_idx: int, devr
         if 0 < d.usedcores < 100 and not cfg.disable_core_limit:
             fractional = True
             g.envs[ENV_CU_LIMIT.format(i=i)] = str(d.usedcores)
-            m = masks.get(d.uuid, 0)
-            if m:
-                g.envs[ENV_CU_MASK.format(i=i)] = format_mask(m)
+            sg = shares.get(d.uuid)
+            if sg and sg.mask:
+                g.envs[ENV_CU_MASK.format(i=i)] = format_mask(sg.mask)
+            temporal |= bool(sg and sg.temporal)
         g.devices.append((f"/dev/dri/renderD{dev.render_minor}", f"/dev/dri/renderD{dev.render_minor}", "rw"))
         g.devices.append((f"/dev/dri/card{dev.card}", f"/dev/dri/card{dev.card}", "rw"))
     g.devices.insert(0, ("/dev/kfd", "/dev/kfd", "rw"))
-    if fractional and any(masks.get(d.uuid, 0) == 0 and 0 < d.usedcores < 100 for d in ordered):
-        # no free XCD-balanced granules: fall back to the temporal limiter
+    if temporal:
+        # Pool member: shares the device's unmasked CUs with the other pool
+        # members under the shim's GPU-time limiter (fair-share board in the
+        # node-wide lock dir); no mask is derived from the limit.
+        g.envs[ENV_CU_SHARE] = "temporal"
         g.envs["VGPU_CU_MASK_FROM_LIMIT"] = "false"
-        g.envs.setdefault(ENV_CORE_POLICY, "force")
     if fractional and cfg.hw_queues_per_vgpu and "GPU_MAX_HW_QUEUES" not in env_names:
         g.envs["GPU_MAX_HW_QUEUES"] = str(cfg.hw_queues_per_vgpu)
     g.envs[ENV_SHARED_REGION] = f"{CONTAINER_CACHE_DIR}/vgpu.cache"
@@ -184,7 +188,7 @@ def build_container_grant(cfg: DevicePluginConfig, pod: dict, ctr_idx: int, devr
     host_cache = f"{cfg.host_lib_dir}/containers/{key}"
     g.mounts.append((f"{CONTAINER_LIB_DIR}/{SHIM_NAME}", f"{cfg.host_lib_dir}/{SHIM_NAME}", True))
     g.mounts.append((CONTAINER_CACHE_DIR, host_cache, False))
-    g.mounts.append((CONTAINER_LOCK_DIR, CONTAINER_LOCK_DIR, False))
+    g.mounts.append((CONTAINER_LOCK_DIR, cfg.host_lock_dir, False))
     if ENV_DISABLE_CONTROL not in env_names and "CUDA_DISABLE_CONTROL" not in env_names:
         g.mounts.append(("/etc/ld.so.preload", f"{cfg.host_lib_dir}/{PRELOAD_FILE}", True))
     g.annotations["amd.com/vgpu-devices"] = ",".join(d.uuid for d in ordered)

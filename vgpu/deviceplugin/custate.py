@@ -1,34 +1,82 @@
-"""Node-local CU-mask occupancy, persisted next to each container's shared
-region so it survives device-plugin restarts.
+"""Node-local compute-share state: which containers hold a CU mask on which
+device, persisted next to each container's shared region so it survives
+device-plugin restarts.
 
 Reference analogue: the Hygon plugin rebuilds its CU-mask occupancy from
 per-container directory names and garbage-collects dead pods
-(pkg/device-plugin/hygon/dcu/server.go:258-336, RefreshContainerDevices).
-Here each container dir holds `grant.json` ({device uuid: mask hex}); the
-occupancy of a device is the OR over live containers.
+(pkg/device-plugin/hygon/dcu/server.go:258-336, RefreshContainerDevices); its
+allocator takes free CU bits greedily (corealloc.go:60-77).
+
+Each container dir holds `grant.json`: {device uuid: {"mask": hex, "mode":
+"mask"|"pool"}} (a bare hex string is read as mode "mask", the round-1 format).
+
+Share policies (DevicePluginConfig.cu_share; measurements in
+profiles/sharing_4way_r1.md and profiles/temporal_r2.md):
+
+* ``mask``: every fractional container gets its own XCD-balanced CU mask.
+  When no granules are free, the container gets the pool instead.
+* ``temporal``: no per-container masks. Every fractional container is a pool
+  member: the shim's GPU-time limiter, charged through the per-GPU fair-share
+  board. On MI355X, 4 x 25 % temporal pods run at 1.04-1.06 x the exclusive
+  GPU, against 0.65 x with four masks.
+* ``hybrid`` (default): the first ``max_mask_slots`` fractional containers on a
+  GPU get masks, which is exact isolation. With two or fewer masked pods on a
+  GPU, masks still beat the exclusive GPU. Later containers join the pool.
+
+The pool of a device is every CU not held by a masked container; pool members
+share it in time. The shim scales a pool member's time limit by
+(device CUs / pool CUs).
 """
 from __future__ import annotations
 
 import json
+import logging
 import os
 import shutil
 import threading
 import time
+from dataclasses import dataclass
 from pathlib import Path
 
-from vgpu.device.cualloc import MI355X, CULayout, alloc_cu_mask
+from vgpu.device.cualloc import MI355X, CULayout, alloc_cu_mask, resolve_packing
+
+log = logging.getLogger("vgpu.deviceplugin.custate")
 
 GRANT_FILE = "grant.json"
+MODE_MASK = "mask"
+MODE_POOL = "pool"
+POLICIES = ("mask", "temporal", "hybrid")
+
+
+@dataclass
+class ShareGrant:
+    mask: int = 0          # CU mask handed to the container (0 = all CUs / none)
+    mode: str = MODE_MASK  # MODE_MASK: exclusive CUs; MODE_POOL: shared CUs + temporal limiter
+
+    @property
+    def temporal(self) -> bool:
+        return self.mode == MODE_POOL
 
 
 class CUMaskState:
-    def __init__(self, containers_dir: str, layout: CULayout = MI355X):
+    def __init__(self, containers_dir: str, layout: CULayout = MI355X, policy: str = "hybrid",
+                 max_mask_slots: int = 2, pack: str | None = None):
+        if policy not in POLICIES:
+            raise ValueError(f"cu_share policy must be one of {POLICIES}, got {policy!r}")
+        # CU packing order (VGPU_CU_PACK), validated once here rather than per Allocate.
+        self.pack = resolve_packing(pack, layout)
+        requested = pack or os.environ.get("VGPU_CU_PACK", "spread")
+        if requested != self.pack:
+            log.warning("CU packing %r does not fit the %d-CU layout; using %r", requested,
+                        layout.total_cus, self.pack)
         self.dir = Path(containers_dir)
         self.layout = layout
+        self.policy = policy
+        self.max_mask_slots = max(0, int(max_mask_slots))
         self._lock = threading.Lock()
 
-    def _grants(self) -> dict[str, dict[str, int]]:
-        out = {}
+    def _grants(self) -> dict[str, dict[str, ShareGrant]]:
+        out: dict[str, dict[str, ShareGrant]] = {}
         if not self.dir.exists():
             return out
         for d in self.dir.iterdir():
@@ -36,42 +84,66 @@ class CUMaskState:
             if not g.exists():
                 continue
             try:
-                out[d.name] = {k: int(v, 16) for k, v in json.loads(g.read_text()).items()}
-            except (OSError, ValueError):
+                raw = json.loads(g.read_text())
+                out[d.name] = {k: (ShareGrant(int(v, 16), MODE_MASK) if isinstance(v, str)
+                                   else ShareGrant(int(v.get("mask", "0x0"), 16), v.get("mode", MODE_MASK)))
+                               for k, v in raw.items()}
+            except (OSError, ValueError, AttributeError):
                 continue
         return out
 
     def used(self, uuid: str) -> int:
+        """CUs of `uuid` held exclusively by masked containers."""
         m = 0
         for g in self._grants().values():
-            m |= g.get(uuid, 0)
+            sg = g.get(uuid)
+            if sg and sg.mode == MODE_MASK:
+                m |= sg.mask
         return m
 
+    def pool_members(self, uuid: str) -> int:
+        return sum(1 for g in self._grants().values() if uuid in g and g[uuid].mode == MODE_POOL)
+
     def allocate(self, container_key: str, requests: list[tuple[str, int]],
-                 layouts: dict[str, CULayout] | None = None) -> dict[str, int]:
-        """requests: [(device uuid, cores %)] → {uuid: mask} (0 = no spatial mask:
-        exclusive, best-effort, or not enough free granules → temporal limiting).
-        `layouts` gives each device's CU/XCD geometry (a CPX compute partition
-        is one XCD of 32 CUs; SPX is 8 × 32)."""
+                 layouts: dict[str, CULayout] | None = None) -> dict[str, ShareGrant]:
+        """requests: [(device uuid, cores %)] → {uuid: ShareGrant}.  Whole-device
+        and best-effort requests (cores 0 or >= 100) get ShareGrant(0, "mask"):
+        no mask, no limiter.  `layouts` gives each device's CU/XCD geometry (a CPX
+        compute partition is one XCD of 32 CUs; SPX is 8 × 32)."""
         layouts = layouts or {}
         with self._lock:
             grants = self._grants()
             grants.pop(container_key, None)  # re-allocation of the same container
-            res: dict[str, int] = {}
+            res: dict[str, ShareGrant] = {}
             for uuid, cores in requests:
                 if cores <= 0 or cores >= 100:
-                    res[uuid] = 0
+                    res[uuid] = ShareGrant(0, MODE_MASK)
                     continue
-                used = 0
-                for g in grants.values():
-                    used |= g.get(uuid, 0)
-                used |= res.get(uuid, 0)
-                m = alloc_cu_mask(used, cores, layouts.get(uuid, self.layout))
-                res[uuid] = m or 0
+                lay = layouts.get(uuid, self.layout)
+                full = (1 << lay.total_cus) - 1
+                masked = 0      # CUs held by masked containers
+                occupied = 0    # CUs of any grant (pool masks included)
+                n_masked = 0
+                for g in list(grants.values()) + [res]:
+                    sg = g.get(uuid)
+                    if not sg:
+                        continue
+                    occupied |= sg.mask
+                    if sg.mode == MODE_MASK and sg.mask:
+                        masked |= sg.mask
+                        n_masked += 1
+                want_mask = self.policy == "mask" or (self.policy == "hybrid" and n_masked < self.max_mask_slots)
+                m = alloc_cu_mask(occupied, cores, lay, resolve_packing(self.pack, lay)) if want_mask else None
+                if m:
+                    res[uuid] = ShareGrant(m, MODE_MASK)
+                else:
+                    pool = full & ~masked
+                    res[uuid] = ShareGrant(0 if pool == full else pool, MODE_POOL)
             d = self.dir / container_key
             d.mkdir(parents=True, exist_ok=True)
             tmp = d / (GRANT_FILE + ".tmp")
-            tmp.write_text(json.dumps({k: hex(v) for k, v in res.items() if v}))
+            tmp.write_text(json.dumps({k: {"mask": hex(v.mask), "mode": v.mode} for k, v in res.items()
+                                       if v.mask or v.mode == MODE_POOL}))
             os.replace(tmp, d / GRANT_FILE)
             return res
 

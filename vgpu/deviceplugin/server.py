@@ -60,7 +60,10 @@ class VGPUDevicePlugin:
         self.devices = backend.devices()
         self.by_uuid = {d.uuid: d for d in self.devices}
         self.health: dict[str, bool] = {d.uuid: d.health for d in self.devices}
-        self.cu_state = CUMaskState(os.path.join(cfg.host_lib_dir, "containers"))
+        self.cu_state = CUMaskState(os.path.join(cfg.host_lib_dir, "containers"), policy=cfg.cu_share,
+                                    max_mask_slots=cfg.max_mask_slots)
+        log.info("compute share policy %s (max %d masked vGPUs per GPU), CU packing %s", cfg.cu_share,
+                 cfg.max_mask_slots, self.cu_state.pack)
         self._links = None
         self._server: grpc.Server | None = None
         self._watchers: list[queue.Queue] = []
