@@ -247,6 +247,87 @@ hipError_t hipStreamIsCapturing(hipStream_t, hipStreamCaptureStatus* st) {
   return hipSuccess;
 }
 hipError_t hipThreadExchangeStreamCaptureMode(hipStreamCaptureMode*) { return hipSuccess; }
+
+// Arrays / 3D / mipmaps: device memory from the pool like any buffer (the
+// real runtime sizes image rows at a 256-byte pitch).
+static size_t fake_array_bytes(size_t elem, size_t w, size_t h, size_t d) {
+  return ((w ? w : 1) * elem + 255) / 256 * 256 * (h ? h : 1) * (d ? d : 1);
+}
+hipError_t hipMalloc3D(hipPitchedPtr* pp, hipExtent e) {
+  void* p = nullptr;
+  hipError_t rc = dev_alloc(&p, fake_array_bytes(1, e.width, e.height, e.depth), tl_dev);
+  if (rc == hipSuccess) *pp = hipPitchedPtr{p, (e.width + 255) / 256 * 256, e.width, e.height};
+  return rc;
+}
+hipError_t hipMallocArray(hipArray_t* a, const hipChannelFormatDesc* d, size_t w, size_t h, unsigned int) {
+  size_t elem = d ? (size_t)(d->x + d->y + d->z + d->w + 7) / 8 : 4;
+  return dev_alloc((void**)a, fake_array_bytes(elem, w, h, 1), tl_dev);
+}
+hipError_t hipArray3DCreate(hipArray_t* a, const HIP_ARRAY3D_DESCRIPTOR* d) {
+  return dev_alloc((void**)a, fake_array_bytes(4 * d->NumChannels, d->Width, d->Height, d->Depth), tl_dev);
+}
+hipError_t hipArrayCreate(hipArray_t* a, const HIP_ARRAY_DESCRIPTOR* d) {
+  return dev_alloc((void**)a, fake_array_bytes(4 * d->NumChannels, d->Width, d->Height, 1), tl_dev);
+}
+hipError_t hipFreeArray(hipArray_t a) { return dev_free((void*)a); }
+hipError_t hipArrayDestroy(hipArray_t a) { return dev_free((void*)a); }
+// Code objects: the loaded image occupies device memory of its own size.
+hipError_t hipModuleLoadData(hipModule_t* m, const void* image) {
+  size_t n = 0;
+  const unsigned char* p = (const unsigned char*)image;
+  if (p && p[0] == 0x7f && p[1] == 'E') {
+    uint64_t shoff;
+    uint16_t shentsize, shnum;
+    memcpy(&shoff, p + 0x28, 8);
+    memcpy(&shentsize, p + 0x3a, 2);
+    memcpy(&shnum, p + 0x3c, 2);
+    n = shoff + (size_t)shentsize * shnum;
+  }
+  return dev_alloc((void**)m, n ? n : 4096, tl_dev);
+}
+hipError_t hipModuleUnload(hipModule_t m) { return dev_free((void*)m); }
+// IPC: a handle carries (address, size); opening it maps the exporter's
+// buffer at a new address without allocating device memory.
+std::map<uintptr_t, size_t> g_imports;
+uintptr_t g_import_next = 0x7e0000000000ull;
+hipError_t hipIpcGetMemHandle(hipIpcMemHandle_t* h, void* p) {
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_allocs.find((uintptr_t)p);
+  if (it == g_allocs.end()) return hipErrorInvalidValue;
+  memset(h, 0, sizeof *h);
+  uint64_t a = (uint64_t)(uintptr_t)p, sz = it->second.second;
+  memcpy(h->reserved, &a, 8);
+  memcpy(h->reserved + 8, &sz, 8);
+  return hipSuccess;
+}
+hipError_t hipIpcOpenMemHandle(void** p, hipIpcMemHandle_t h, unsigned int) {
+  std::lock_guard<std::mutex> g(g_mu);
+  uint64_t sz;
+  memcpy(&sz, h.reserved + 8, 8);
+  uintptr_t a = g_import_next;
+  g_import_next += (sz + (1 << 21)) & ~((uintptr_t)(1 << 21) - 1);
+  g_imports[a] = sz;
+  *p = (void*)a;
+  return hipSuccess;
+}
+hipError_t hipIpcCloseMemHandle(void* p) {
+  std::lock_guard<std::mutex> g(g_mu);
+  return g_imports.erase((uintptr_t)p) ? hipSuccess : hipErrorInvalidValue;
+}
+hipError_t hipMemGetAddressRange(hipDeviceptr_t* base, size_t* size, hipDeviceptr_t p) {
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_allocs.find((uintptr_t)p);
+  if (it != g_allocs.end()) {
+    *base = p;
+    *size = it->second.second;
+    return hipSuccess;
+  }
+  auto jt = g_imports.find((uintptr_t)p);
+  if (jt == g_imports.end()) return hipErrorInvalidValue;
+  *base = p;
+  *size = jt->second;
+  return hipSuccess;
+}
 hipError_t hipStreamBeginCapture(hipStream_t, hipStreamCaptureMode) { return hipSuccess; }
 hipError_t hipStreamEndCapture(hipStream_t, hipGraph_t* g) {
   if (g) *g = nullptr;

@@ -170,6 +170,12 @@ __attribute__((visibility("default"))) uint64_t vgpu_self_usage(int dev, int whi
   return __atomic_load_n(f[which], __ATOMIC_RELAXED);
 }
 
+// Bytes of other processes' buffers this process has mapped via hipIpcOpenMemHandle.
+__attribute__((visibility("default"))) int64_t vgpu_self_ipc_imported(int dev) {
+  if (dev < 0 || dev >= VGPU_MAX_DEVICES) return 0;
+  return st().ipc_imported[dev].load();
+}
+
 // Temporal limiter: fair-share GPU ns charged and wall ns busy on `dev` so far.
 __attribute__((visibility("default"))) void vgpu_self_gpu_time(int dev, uint64_t* charged,
                                                                uint64_t* busy) {

@@ -12,6 +12,7 @@
 // control is disabled, (3) keeps the fast path to a couple of relaxed atomics.
 #include <algorithm>
 #include <mutex>
+#include <shared_mutex>
 #include <unordered_map>
 #include <vector>
 
@@ -455,7 +456,10 @@ __attribute__((visibility("default"))) hipError_t hipGraphExecDestroy(hipGraphEx
 // another thread or never ends only delays marker polling, never correctness.
 __attribute__((visibility("default"))) hipError_t hipStreamBeginCapture(hipStream_t stream,
                                                                         hipStreamCaptureMode mode) {
-  g_open_captures.fetch_add(1);
+  {
+    std::unique_lock<std::shared_mutex> g(g_capture_mu);  // no limiter marker in flight past here
+    g_open_captures.fetch_add(1);
+  }
   hipError_t rc = REAL_HIP(hipStreamBeginCapture)(stream, mode);
   if (rc != hipSuccess) g_open_captures.fetch_sub(1);
   return rc;
@@ -464,7 +468,10 @@ __attribute__((visibility("default"))) hipError_t hipStreamBeginCapture(hipStrea
 __attribute__((visibility("default"))) hipError_t hipStreamBeginCaptureToGraph(
     hipStream_t stream, hipGraph_t graph, const hipGraphNode_t* deps, const hipGraphEdgeData* data,
     size_t n, hipStreamCaptureMode mode) {
-  g_open_captures.fetch_add(1);
+  {
+    std::unique_lock<std::shared_mutex> g(g_capture_mu);
+    g_open_captures.fetch_add(1);
+  }
   hipError_t rc = REAL_HIP(hipStreamBeginCaptureToGraph)(stream, graph, deps, data, n, mode);
   if (rc != hipSuccess) g_open_captures.fetch_sub(1);
   return rc;

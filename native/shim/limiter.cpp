@@ -39,6 +39,7 @@
 
 #include <condition_variable>
 #include <deque>
+#include <shared_mutex>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -53,6 +54,7 @@ namespace vgpu {
 thread_local int tl_device = 0;
 thread_local int tl_in_hip_alloc = 0;
 std::atomic<int> g_open_captures{0};
+std::shared_mutex g_capture_mu;
 
 extern int cumask_device_cus(int dev);        // CUs available to us (mask or physical)
 extern uint32_t cumask_driver_uid(int dev);   // KFD gpu_id of device, 0 = unknown
@@ -63,6 +65,19 @@ namespace {
 struct Marker {
   hipEvent_t ev;
   uint64_t submit_ns;
+  uint32_t launches;  // launches this marker covers (since the previous one on its stream)
+};
+
+// Per-stream marker state.  A launch records a marker only when the stream
+// has none in flight or the last one is older than the marking interval; the
+// launches in between are "dirty" and the limiter thread covers them with a
+// marker of its own once the older markers have completed, so no GPU time
+// goes uncharged while the per-launch cost stays a few hundred nanoseconds.
+struct StreamTrack {
+  std::deque<Marker> q;
+  uint64_t last_mark_ns = 0;
+  uint32_t unmarked = 0;  // launches since the last marker
+  bool dirty = false;
 };
 
 struct DevLimiter {
@@ -73,10 +88,11 @@ struct DevLimiter {
   int64_t cap = 0;            // bucket depth (ns)
   int64_t quantum = 0;        // an overdrawn bucket must refill this far before launches resume
   std::atomic<int> hold{0};   // 1 while waiting for the quantum
-  std::atomic<int> outstanding{0};
-  std::atomic<int64_t> ema_charge{0};  // ns per completed marker
+  std::atomic<int> outstanding{0};     // markers in flight
+  std::atomic<int64_t> inflight{0};    // tracked launches not yet charged
+  std::atomic<int64_t> ema_charge{0};  // charged ns per launch
   std::mutex mu;              // guards streams / free_ev / act_mark_ns / board
-  std::unordered_map<hipStream_t, std::deque<Marker>> streams;
+  std::unordered_map<hipStream_t, StreamTrack> streams;
   std::vector<hipEvent_t> free_ev;
   uint64_t act_mark_ns = 0;   // start of the not-yet-charged busy interval
   uint64_t last_poll_ns = 0;  // previous poll that found work still in flight
@@ -194,6 +210,32 @@ void configure() {
   g_throttle_any.store(any, std::memory_order_release);
 }
 
+// Record one marker on `stream` (caller holds L.mu).  From the limiter thread
+// the record is made under the capture guard: a capture that begins on the
+// stream must not swallow our event.  Returns 1 when a marker was recorded.
+int record_marker(DevLimiter& L, hipStream_t stream, StreamTrack& t, bool from_app) {
+  std::shared_lock<std::shared_mutex> cap(g_capture_mu, std::defer_lock);
+  if (!from_app) cap.lock();
+  if (g_open_captures.load(std::memory_order_acquire) > 0) return 0;
+  hipEvent_t ev = nullptr;
+  if (!L.free_ev.empty()) {
+    ev = L.free_ev.back();
+    L.free_ev.pop_back();
+  } else if (REAL_HIP(hipEventCreateWithFlags)(&ev, hipEventDisableTiming) != hipSuccess) {
+    return 0;
+  }
+  if (REAL_HIP(hipEventRecord)(ev, stream) != hipSuccess) {
+    L.free_ev.push_back(ev);
+    return 0;
+  }
+  const uint64_t now = mono_ns();
+  t.q.push_back({ev, now, t.unmarked});
+  t.unmarked = 0;
+  t.last_mark_ns = now;
+  t.dirty = false;
+  return 1;
+}
+
 // Poll the oldest markers of every stream of `dev`; charge completed intervals.
 bool reap(int dev, DevLimiter& L, uint64_t now_hint) {
   if (L.outstanding.load(std::memory_order_relaxed) == 0) return false;
@@ -201,22 +243,29 @@ bool reap(int dev, DevLimiter& L, uint64_t now_hint) {
   auto query = REAL_HIP(hipEventQuery);
   std::lock_guard<std::mutex> g(L.mu);
   int done = 0;
+  int added = 0;
+  int64_t covered = 0;
   for (auto it = L.streams.begin(); it != L.streams.end();) {
-    auto& q = it->second;
+    StreamTrack& t = it->second;
+    auto& q = t.q;
     while (!q.empty()) {
       hipError_t rc = query(q.front().ev);
       if (rc == hipErrorNotReady || rc == hipErrorStreamCaptureUnsupported ||
           rc == hipErrorStreamCaptureImplicit)
         break;
       L.free_ev.push_back(q.front().ev);  // complete (or invalid: never wait on it again)
+      covered += q.front().launches;
       q.pop_front();
       ++done;
     }
-    if (q.empty())
+    // Launches since the last marker are still uncovered: cover them now.
+    if (q.empty() && t.dirty) added += record_marker(L, it->first, t, /*from_app=*/false);
+    if (q.empty() && !t.dirty)
       it = L.streams.erase(it);
     else
       ++it;
   }
+  if (added) L.outstanding.fetch_add(added);
   const uint64_t polled = mono_ns();
   if (!done) {
     L.last_poll_ns = polled;
@@ -226,12 +275,13 @@ bool reap(int dev, DevLimiter& L, uint64_t now_hint) {
   uint64_t now = L.last_poll_ns > L.act_mark_ns ? (L.last_poll_ns + polled) / 2 : polled;
   if (now < L.act_mark_ns) now = L.act_mark_ns;
   L.last_poll_ns = polled;
-  const int left = L.outstanding.fetch_sub(done) - done;
+  const int left = L.outstanding.fetch_sub(done) - done;  // includes markers added above
   const uint64_t wall = now > L.act_mark_ns ? now - L.act_mark_ns : 0;
   L.act_mark_ns = now;
   const uint64_t charge = L.board ? board_charge(L.board, L.board_slot, wall, left == 0) : wall;
   L.tokens.fetch_sub((int64_t)charge, std::memory_order_relaxed);
-  const int64_t per = (int64_t)(charge / done);
+  L.inflight.fetch_sub(covered, std::memory_order_relaxed);
+  const int64_t per = covered > 0 ? (int64_t)(charge / covered) : (int64_t)charge;
   const int64_t old = L.ema_charge.load(std::memory_order_relaxed);
   L.ema_charge.store(old ? (old * 3 + per) / 4 : per, std::memory_order_relaxed);
   L.win_charge += charge;
@@ -383,6 +433,7 @@ void limiter_after_fork() {
     L.streams.clear();
     L.free_ev.clear();
     L.outstanding.store(0);
+    L.inflight.store(0);
     L.board = nullptr;
     L.board_slot = -1;
     L.board_tried = false;
@@ -418,7 +469,7 @@ bool limiter_on_launch(int dev, uint64_t wg, const void* fn) {
     // Until the first marker completes, assume 1 ms per launch in flight.
     int64_t per = L.ema_charge.load(std::memory_order_relaxed);
     if (per <= 0) per = 1000000;
-    const int64_t pending = (int64_t)L.outstanding.load(std::memory_order_relaxed) * per;
+    const int64_t pending = L.inflight.load(std::memory_order_relaxed) * per;
     const int64_t avail = L.tokens.load(std::memory_order_relaxed) - pending;
     if (L.hold.load(std::memory_order_relaxed)) {
       if (avail >= L.quantum) {
@@ -446,23 +497,28 @@ void limiter_track(int dev, hipStream_t stream) {
   if (dev < 0 || dev >= VGPU_MAX_DEVICES) return;
   DevLimiter& L = g_lim[dev];
   if (g_open_captures.load(std::memory_order_acquire) > 0) return;  // no HIP calls mid-capture
+  static const uint64_t interval_ns = [] {
+    const char* v = env_first("VGPU_LIMITER_MARK_US");
+    return (uint64_t)((v ? atof(v) : 500.0) * 1000.0);
+  }();
+  std::unique_lock<std::mutex> g(L.mu);
+  StreamTrack& t = L.streams[stream];
+  const uint64_t now = mono_ns();
+  t.unmarked++;
+  L.inflight.fetch_add(1, std::memory_order_relaxed);
+  if (!t.q.empty() && now - t.last_mark_ns < interval_ns) {
+    t.dirty = true;  // covered by the next marker (ours or the limiter thread's)
+    return;
+  }
   auto is_cap = REAL_HIP(hipStreamIsCapturing);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (is_cap && is_cap(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return;
-  std::unique_lock<std::mutex> g(L.mu);
-  hipEvent_t ev = nullptr;
-  if (!L.free_ev.empty()) {
-    ev = L.free_ev.back();
-    L.free_ev.pop_back();
-  } else if (REAL_HIP(hipEventCreateWithFlags)(&ev, hipEventDisableTiming) != hipSuccess) {
+  if ((is_cap && is_cap(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) ||
+      !record_marker(L, stream, t, /*from_app=*/true)) {
+    // captured (not executed now) or no marker possible: not tracked
+    t.unmarked--;
+    L.inflight.fetch_sub(1, std::memory_order_relaxed);
     return;
   }
-  if (REAL_HIP(hipEventRecord)(ev, stream) != hipSuccess) {
-    L.free_ev.push_back(ev);
-    return;
-  }
-  const uint64_t now = mono_ns();
-  L.streams[stream].push_back({ev, now});
   if (L.outstanding.fetch_add(1) == 0) {
     attach_board(dev, L);
     L.act_mark_ns = now;

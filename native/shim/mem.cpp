@@ -34,6 +34,8 @@ static void add_usage(vgpu_dev_usage_t& u, uint64_t size, int kind, bool add) {
     else __atomic_fetch_sub(f, size, __ATOMIC_RELAXED);
   };
   switch (kind) {
+    case kIpcImport:
+      return;  // another process's buffer: charged to its exporter only
     case kHostSpill:
       op(&u.host_bytes);
       return;
@@ -99,6 +101,11 @@ void mem_unreserve(int dev, uint64_t size, int kind) {
   add_usage(sl->used[dev], size, kind, false);
 }
 
+void ipc_import_account(int dev, int64_t delta) {
+  if (dev < 0 || dev >= VGPU_MAX_DEVICES) return;
+  st().ipc_imported[dev].fetch_add(delta, std::memory_order_relaxed);
+}
+
 void ledger_add(void* p, uint64_t size, int dev, int kind) {
   State& s = st();
   trace_emit(VGPU_EV_ALLOC, dev, size, (uint64_t)kind);
@@ -133,7 +140,8 @@ bool ledger_take(void* p, Alloc* out) {
   {
     std::lock_guard<std::mutex> g(s.ledger_mu);
     auto it = s.ledger.find((uintptr_t)p);
-    if (it == s.ledger.end()) return false;
+    // An IPC mapping is released only by hipIpcCloseMemHandle (ledger_take_if).
+    if (it == s.ledger.end() || it->second.kind == kIpcImport) return false;
     *out = it->second;
     s.ledger.erase(it);
   }

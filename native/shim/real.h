@@ -93,6 +93,25 @@ using hipStreamBeginCapture = hipError_t (*)(hipStream_t, hipStreamCaptureMode);
 using hipStreamBeginCaptureToGraph = hipError_t (*)(hipStream_t, hipGraph_t, const hipGraphNode_t*,
                                                     const hipGraphEdgeData*, size_t, hipStreamCaptureMode);
 using hipStreamEndCapture = hipError_t (*)(hipStream_t, hipGraph_t*);
+using hipMalloc3D = hipError_t (*)(hipPitchedPtr*, hipExtent);
+using hipMallocArray = hipError_t (*)(hipArray_t*, const hipChannelFormatDesc*, size_t, size_t, unsigned int);
+using hipMalloc3DArray = hipError_t (*)(hipArray_t*, const hipChannelFormatDesc*, hipExtent, unsigned int);
+using hipArrayCreate = hipError_t (*)(hipArray_t*, const HIP_ARRAY_DESCRIPTOR*);
+using hipArray3DCreate = hipError_t (*)(hipArray_t*, const HIP_ARRAY3D_DESCRIPTOR*);
+using hipMipmappedArrayCreate = hipError_t (*)(hipMipmappedArray_t*, HIP_ARRAY3D_DESCRIPTOR*, unsigned int);
+using hipMallocMipmappedArray = hipError_t (*)(hipMipmappedArray_t*, const hipChannelFormatDesc*, hipExtent,
+                                               unsigned int, unsigned int);
+using hipFreeArray = hipError_t (*)(hipArray_t);
+using hipArrayDestroy = hipError_t (*)(hipArray_t);
+using hipFreeMipmappedArray = hipError_t (*)(hipMipmappedArray_t);
+using hipMipmappedArrayDestroy = hipError_t (*)(hipMipmappedArray_t);
+using hipModuleLoad = hipError_t (*)(hipModule_t*, const char*);
+using hipModuleLoadData = hipError_t (*)(hipModule_t*, const void*);
+using hipModuleLoadDataEx = hipError_t (*)(hipModule_t*, const void*, unsigned int, hipJitOption*, void**);
+using hipModuleUnload = hipError_t (*)(hipModule_t);
+using hipIpcOpenMemHandle = hipError_t (*)(void**, hipIpcMemHandle_t, unsigned int);
+using hipIpcCloseMemHandle = hipError_t (*)(void*);
+using hipMemGetAddressRange = hipError_t (*)(hipDeviceptr_t*, size_t*, hipDeviceptr_t);
 using hipGetProcAddress = hipError_t (*)(const char*, void**, int, uint64_t,
                                          hipDriverProcAddressQueryResult*);
 }  // namespace fnt

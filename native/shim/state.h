@@ -10,6 +10,7 @@
 
 #include <atomic>
 #include <mutex>
+#include <shared_mutex>
 #include <unordered_map>
 
 #include <hip/hip_runtime_api.h>
@@ -27,6 +28,7 @@ enum AllocKind : int {
   kVmmHandle = 3,   // hipMemCreate physical handle
   kModule = 4,      // code object bytes
   kRuntime = 5,     // HSA pool allocations made outside the HIP hooks (runtime-internal)
+  kIpcImport = 6,   // another process's buffer mapped through hipIpcOpenMemHandle (charged 0)
 };
 
 struct Alloc {
@@ -51,6 +53,7 @@ struct State {
   std::unordered_map<uintptr_t, Alloc> ledger;
 
   std::atomic<int> suspended{0};
+  std::atomic<int64_t> ipc_imported[VGPU_MAX_DEVICES] = {};  // bytes mapped from other processes
   std::atomic<int> dev_touched[VGPU_MAX_DEVICES] = {};
 };
 
@@ -77,6 +80,7 @@ bool ledger_take_if(void* p, int kind, Alloc* out);  // only an entry of that ki
 // cannot be refused): it still counts against the next hipMalloc.
 void mem_charge_nofail(int dev, uint64_t size, int kind);
 uint64_t mem_limit(int dev);          // 0 = unlimited
+void ipc_import_account(int dev, int64_t delta);
 uint64_t mem_used(int dev);           // container-wide HBM + host charge
 void charge_context(int dev);         // first-touch context charge
 
@@ -95,6 +99,7 @@ void limiter_track(int dev, hipStream_t stream);
 // no HIP call while one is open (an event query can invalidate a global-mode
 // capture on another thread).
 extern std::atomic<int> g_open_captures;
+extern std::shared_mutex g_capture_mu;  // writers: capture begin; readers: limiter-thread markers
 void limiter_stats(int dev, uint64_t* charged_ns, uint64_t* busy_ns);
 void suspend_gate();
 int cu_count_masked(int dev, int physical);

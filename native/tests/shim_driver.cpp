@@ -123,6 +123,84 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (sc == "arrays") {
+    // Array / 3D / module allocations under the cap (reference cuArrayCreate_v2,
+    // cuArray3DCreate_v2, cuModuleLoad*): refusable past it, charged by class.
+    auto usage = sym<uint64_t (*)(int, int)>("vgpu_self_usage");
+    hipPitchedPtr a{}, b{};
+    hipExtent e{6ull << 30, 1, 1};  // 6 GiB of bytes in one row
+    printf("malloc3d_a=%d\n", (int)hipMalloc3D(&a, e));
+    printf("malloc3d_b=%d\n", (int)hipMalloc3D(&b, e));  // 12 GiB > 8 GiB cap
+    hipChannelFormatDesc fd{32, 0, 0, 0, hipChannelFormatKindFloat};
+    hipArray_t arr = nullptr, arr2 = nullptr;
+    printf("array_a=%d\n", (int)hipMallocArray(&arr, &fd, 16384, 16384, 0));   // 1 GiB
+    printf("array_b=%d\n", (int)hipMallocArray(&arr2, &fd, 32768, 32768, 0));  // 4 GiB: refused
+    HIP_ARRAY3D_DESCRIPTOR d3{1024, 1024, 512, HIP_AD_FORMAT_FLOAT, 1, 0};      // 2 GiB: refused
+    hipArray_t arr3 = nullptr;
+    printf("array3d=%d\n", (int)hipArray3DCreate(&arr3, &d3));
+    static unsigned char elf[4096] = {0x7f, 'E', 'L', 'F', 2};
+    uint64_t shoff = 3000;
+    uint16_t shentsize = 64, shnum = 8;  // 3000 + 512 = 3512 bytes
+    memcpy(elf + 0x28, &shoff, 8);
+    memcpy(elf + 0x3a, &shentsize, 2);
+    memcpy(elf + 0x3c, &shnum, 2);
+    hipModule_t mod = nullptr;
+    printf("module=%d\n", (int)hipModuleLoadData(&mod, elf));
+    printf("ctx=%llu\nmodule_bytes=%llu\nbuffer_bytes=%llu\ntotal_bytes=%llu\n",
+           (unsigned long long)usage(dev, 0), (unsigned long long)usage(dev, 1),
+           (unsigned long long)usage(dev, 2), (unsigned long long)usage(dev, 4));
+    hipModuleUnload(mod);
+    hipFreeArray(arr);
+    hipFree(a.ptr);
+    printf("after_free_total=%llu\nphysical_after=%llu\n", (unsigned long long)usage(dev, 4),
+           (unsigned long long)fake_hip_physical_used(dev));
+    return 0;
+  }
+
+  if (sc == "ipc_export" || sc == "ipc_import") {
+    // Two processes of one container: the exporter's buffer is charged once.
+    auto usage = sym<uint64_t (*)(int, int)>("vgpu_self_usage");
+    auto imported = sym<int64_t (*)(int)>("vgpu_self_ipc_imported");
+    auto used = sym<uint64_t (*)(void*, int)>("vgpu_region_device_used");
+    auto self_region = sym<void* (*)()>("vgpu_self_region");
+    const char* path = argv[2];
+    if (sc == "ipc_export") {
+      void* p = nullptr;
+      hipMalloc(&p, 1ull << 30);
+      hipIpcMemHandle_t h;
+      hipIpcGetMemHandle(&h, p);
+      FILE* f = fopen(path, "wb");
+      fwrite(&h, sizeof h, 1, f);
+      fclose(f);
+      printf("exported=1\nbuffer=%llu\n", (unsigned long long)usage(dev, 2));
+      fflush(stdout);
+      // hold the buffer until the importer is done (it removes the file)
+      for (int i = 0; i < 2000 && access(path, F_OK) == 0; ++i) usleep(5000);
+      printf("region_used_while_imported=%s\n", getenv("IPC_SEEN") ? getenv("IPC_SEEN") : "");
+      return 0;
+    }
+    hipIpcMemHandle_t h;
+    for (int i = 0; i < 2000; ++i) {
+      FILE* f = fopen(path, "rb");
+      if (f && fread(&h, sizeof h, 1, f) == 1) {
+        fclose(f);
+        break;
+      }
+      if (f) fclose(f);
+      usleep(5000);
+    }
+    void* q = nullptr;
+    printf("open=%d\n", (int)hipIpcOpenMemHandle(&q, h, hipIpcMemLazyEnablePeerAccess));
+    printf("imported=%lld\nbuffer=%llu\nregion_used=%llu\n", (long long)imported(dev),
+           (unsigned long long)usage(dev, 2), (unsigned long long)used(self_region(), dev));
+    hipFree(q);  // misuse: must not uncharge anything
+    printf("buffer_after_free=%llu\n", (unsigned long long)usage(dev, 2));
+    const int crc = (int)hipIpcCloseMemHandle(q);
+    printf("close=%d\nimported_after=%lld\n", crc, (long long)imported(dev));
+    remove(path);
+    return 0;
+  }
+
   if (sc == "hostpid") {
     // hipSetDevice above initialised the runtime (fake hsa_init opened the fake KFD).
     auto hp = sym<int (*)(int*)>("vgpu_self_host_pid");
@@ -291,9 +369,14 @@ int main(int argc, char** argv) {
     hsa_amd_agent_iterate_memory_pools(gpu, pool_cb, &pool);
     void* q = nullptr;
     hsa_amd_memory_pool_allocate(pool, 256ull << 20, 0, &q);
-    printf("ctx2=%llu\n", (unsigned long long)usage(dev, 0));
+    printf("ctx2=%llu\nbuf2=%llu\n", (unsigned long long)usage(dev, 0), (unsigned long long)usage(dev, 2));
     hsa_amd_memory_pool_free(q);
-    printf("ctx3=%llu\n", (unsigned long long)usage(dev, 0));
+    printf("ctx3=%llu\nbuf3=%llu\n", (unsigned long long)usage(dev, 0), (unsigned long long)usage(dev, 2));
+    // A direct HSA user is refused past the cap, like hipMalloc.
+    void* big = nullptr;
+    hsa_status_t brc = hsa_amd_memory_pool_allocate(pool, 64ull << 30, 0, &big);
+    printf("big_rc=%d\n", (int)brc);
+    if (brc == HSA_STATUS_SUCCESS) hsa_amd_memory_pool_free(big);
     hipFree(p);
     printf("buf4=%llu\npool_used=%llu\n", (unsigned long long)usage(dev, 2),
            (unsigned long long)fake_hsa_pool_used(dev));

@@ -157,3 +157,21 @@ def test_ddp_over_rccl_under_the_shim(gpu_build):
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     print(res)
     assert res["backend"] == "nccl" and res["value"] > 0 and res["final_loss"] == res["final_loss"]
+
+
+def test_array_3d_module_allocations_capped(gpu_build):
+    """under an 8 GiB cap, hipMalloc3D and hipMallocArray past
+    the cap fail, a hipModuleLoadData is charged to the module class, and the
+    classes still add up to the total (reference cuArrayCreate_v2 /
+    cuArray3DCreate_v2 / cuModuleLoad* hooks)."""
+    res = probe(["arrays", 8192], {"VGPU_DEVICE_MEMORY_LIMIT_0": "8192m"})
+    OOM, UNSUPPORTED = 2, 801  # gfx950 has no image arrays: hipErrorNotSupported from the runtime
+    assert res["malloc3d_a"] == 0 and res["malloc3d_b"] == OOM, res
+    assert res["array_a"] in (0, UNSUPPORTED), res
+    assert res["array_b"] == OOM and res["array3d"] == OOM, res  # refused by the cap before the runtime
+    assert res["module"] == 0
+    u = res["usage"]
+    assert u["module"] > 0, u
+    assert u["buffer"] >= (6 << 30) + ((256 << 20) if res["array_a"] == 0 else 0), u
+    assert u["context"] + u["module"] + u["buffer"] == u["total"], u
+    assert res["usage_after_free"]["module"] == 0 and res["usage_after_free"]["buffer"] < u["buffer"]

@@ -26,10 +26,12 @@ def test_runtime_pool_allocations_charged_once(native_build):
     assert int(o["buf0"]) == 0
     assert int(o["buf1"]) == GiB                # hipMalloc: buffer class only ...
     assert int(o["ctx1"]) == 64 * MiB           # ... not again at the pool level
-    assert int(o["ctx2"]) == 64 * MiB + 256 * MiB
-    assert int(o["ctx3"]) == 64 * MiB
+    # the driver itself calling HSA is an application allocation: buffer class
+    assert int(o["ctx2"]) == 64 * MiB and int(o["buf2"]) == GiB + 256 * MiB
+    assert int(o["ctx3"]) == 64 * MiB and int(o["buf3"]) == GiB
     assert int(o["buf4"]) == 0
     assert int(o["pool_used"]) == 64 * MiB      # the fake runtime really freed the rest
+    assert o["big_rc"] == str(0x1008)           # HSA_STATUS_ERROR_OUT_OF_RESOURCES past the 16 GiB cap
 
 
 def test_runtime_charge_counts_against_cap(native_build):
@@ -47,8 +49,10 @@ def test_hsa_tools_lib_table_mode(native_build):
     assert o["tools_loaded"] == "1"
     assert o["table_mode"] == "1"
     assert int(o["ctx1"]) == 64 * MiB and int(o["buf1"]) == GiB
-    assert int(o["ctx2"]) == 64 * MiB + 256 * MiB
+    # the caller is recovered through the PLT hop even though the table entry runs the hook
+    assert int(o["ctx2"]) == 64 * MiB and int(o["buf2"]) == GiB + 256 * MiB
     assert int(o["ctx3"]) == 64 * MiB
+    assert o["big_rc"] == str(0x1008)
 
 
 def test_hsa_tools_lib_applies_cu_mask_once(native_build):

@@ -333,3 +333,41 @@ def test_masked_pod_without_temporal_share_is_not_throttled(native_build):
     o = run("duty", 1, env={"VGPU_DEVICE_CU_LIMIT_0": "25", "VGPU_CU_MASK_0": hex((1 << 64) - 1),
                             "VGPU_FAKE_KERNEL_US": "500"}, timeout=60)
     assert _duty(o) > 0.95
+
+
+# ---- cap-refusable array / 3D / module allocations, IPC --------------------------------------
+def test_array_and_3d_allocations_refused_past_cap(native_build):
+    """reference cuArrayCreate_v2 / cuArray3DCreate_v2 / cuModuleLoad* hooks: under an
+    8 GiB cap hipMalloc3D and array creation past the cap fail, module bytes are
+    charged to their own class, and the classes add up to the total."""
+    o = run("arrays", env={"VGPU_DEVICE_MEMORY_LIMIT_0": "8g"})
+    assert o["malloc3d_a"] == "0" and o["malloc3d_b"] == "2"  # hipErrorOutOfMemory
+    assert o["array_a"] == "0" and o["array_b"] == "2" and o["array3d"] == "2"
+    assert o["module"] == "0" and int(o["module_bytes"]) == 3512
+    assert int(o["buffer_bytes"]) == 6 * GiB + GiB
+    assert int(o["total_bytes"]) == int(o["ctx"]) + int(o["module_bytes"]) + int(o["buffer_bytes"])
+    assert int(o["after_free_total"]) == int(o["ctx"])
+    assert int(o["physical_after"]) == 0
+
+
+def test_ipc_import_is_charged_to_the_exporter_only(native_build, tmp_path):
+    """RCCL-style IPC between two processes of one container: the imported
+    buffer is not charged again (reference cuIpcOpenMemHandle_v2 pass-through)."""
+    e = {k: v for k, v in os.environ.items() if not k.startswith(("VGPU_", "CUDA_", "HIP_"))}
+    e.update(LD_LIBRARY_PATH=str(FAKES_DIR), LD_PRELOAD=str(shim_path()),
+             VGPU_DEVICE_MEMORY_LIMIT_0="16g", VGPU_SHARED_REGION=str(tmp_path / "r.cache"))
+    h = str(tmp_path / "handle")
+    exp = subprocess.Popen([str(FAKES_DIR / "shim_driver"), "ipc_export", h], env=e, stdout=subprocess.PIPE,
+                           text=True)
+    imp = subprocess.run([str(FAKES_DIR / "shim_driver"), "ipc_import", h], env=e, capture_output=True,
+                         text=True, timeout=60)
+    out_e, _ = exp.communicate(timeout=60)
+    assert imp.returncode == 0 and exp.returncode == 0, imp.stderr
+    o = dict(l.split("=", 1) for l in imp.stdout.splitlines() if "=" in l)
+    x = dict(l.split("=", 1) for l in out_e.splitlines() if "=" in l)
+    assert x["buffer"] == str(GiB)
+    assert o["open"] == "0" and o["imported"] == str(GiB)
+    assert o["buffer"] == "0"                   # importer charged nothing
+    assert o["region_used"] == str(GiB)         # container total: the buffer once
+    assert o["buffer_after_free"] == "0"        # a stray hipFree of the mapping uncharges nothing
+    assert o["close"] == "0" and o["imported_after"] == "0"

@@ -10,6 +10,9 @@ line.  Used by the GPU tests and by the accuracy benchmarks.
   python -m vgpu.bench.probes graph [blocks_a] [blocks_b]
       capture two busy kernels into a hipGraph and replay it (the library
       charges a graph launch by its kernel nodes' workgroups; see VGPU_TRACE)
+  python -m vgpu.bench.probes arrays [cap_mib]
+      hipMalloc3D / hipMallocArray / hipArray3DCreate past the cap, and
+      hipModuleLoadData of a gfx950 code object (module charge class)
   python -m vgpu.bench.probes smi [alloc_mib]
       what amdsmi (python bindings over libamd_smi, the amd-smi CLI's path)
       reports for VRAM total / used after torch allocates alloc_mib
@@ -152,11 +155,68 @@ def graph(blocks_a: int = 1000, blocks_b: int = 3000) -> dict:
     return {"blocks": [blocks_a, blocks_b], "replays": 2}
 
 
+def arrays(cap_mib: int = 8192) -> dict:
+    """Array-class allocations through the real HIP runtime (ctypes): under a
+    cap of `cap_mib`, the second 6 GiB hipMalloc3D and a 4 GiB hipMallocArray
+    must fail; a code object must land in the module class."""
+    import ctypes
+    from pathlib import Path
+    import torch
+    torch.cuda.init()
+    hip = ctypes.CDLL("libamdhip64.so")  # the runtime torch already loaded
+
+    class Extent(ctypes.Structure):
+        _fields_ = [("width", ctypes.c_size_t), ("height", ctypes.c_size_t), ("depth", ctypes.c_size_t)]
+
+    class Pitched(ctypes.Structure):
+        _fields_ = [("ptr", ctypes.c_void_p), ("pitch", ctypes.c_size_t), ("xsize", ctypes.c_size_t),
+                    ("ysize", ctypes.c_size_t)]
+
+    class ChanDesc(ctypes.Structure):
+        _fields_ = [("x", ctypes.c_int), ("y", ctypes.c_int), ("z", ctypes.c_int), ("w", ctypes.c_int),
+                    ("f", ctypes.c_int)]
+
+    class Arr3D(ctypes.Structure):
+        _fields_ = [("Width", ctypes.c_size_t), ("Height", ctypes.c_size_t), ("Depth", ctypes.c_size_t),
+                    ("Format", ctypes.c_int), ("NumChannels", ctypes.c_uint), ("Flags", ctypes.c_uint)]
+
+    hip.hipMalloc3D.argtypes = [ctypes.POINTER(Pitched), Extent]
+    res: dict = {}
+    a, b = Pitched(), Pitched()
+    six = Extent(6 << 30, 1, 1)
+    res["malloc3d_a"] = hip.hipMalloc3D(ctypes.byref(a), six)
+    res["malloc3d_b"] = hip.hipMalloc3D(ctypes.byref(b), six)
+    hip.hipGetLastError()
+    fd = ChanDesc(32, 0, 0, 0, 2)  # hipChannelFormatKindFloat
+    arr, arr2, arr3 = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    hip.hipMallocArray.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ChanDesc), ctypes.c_size_t,
+                                   ctypes.c_size_t, ctypes.c_uint]
+    res["array_a"] = hip.hipMallocArray(ctypes.byref(arr), ctypes.byref(fd), 8192, 8192, 0)    # 256 MiB
+    res["array_b"] = hip.hipMallocArray(ctypes.byref(arr2), ctypes.byref(fd), 32768, 32768, 0)  # 4 GiB
+    hip.hipGetLastError()
+    d3 = Arr3D(1024, 1024, 1024, 0x20, 1, 0)  # HIP_AD_FORMAT_FLOAT: 4 GiB
+    res["array3d"] = hip.hipArray3DCreate(ctypes.byref(arr3), ctypes.byref(d3))
+    hip.hipGetLastError()
+    image = (Path(__file__).resolve().parents[1] / "_lib" / "module_probe.hsaco").read_bytes()
+    mod = ctypes.c_void_p()
+    buf = ctypes.create_string_buffer(image, len(image))
+    res["module"] = hip.hipModuleLoadData(ctypes.byref(mod), buf)
+    res["image_bytes"] = len(image)
+    res["usage"] = shim_stats()
+    hip.hipModuleUnload(mod)
+    if res["array_a"] == 0:
+        hip.hipFreeArray(arr)
+    if res["malloc3d_a"] == 0:
+        hip.hipFree(ctypes.c_void_p(a.ptr))
+    res["usage_after_free"] = shim_stats()
+    return res
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     cmd = argv.pop(0) if argv else "census"
     nums = [int(a) for a in argv]
-    out = {"census": census, "busy": busy, "cap": cap, "smi": smi, "graph": graph}[cmd](*nums)
+    out = {"census": census, "busy": busy, "cap": cap, "smi": smi, "graph": graph, "arrays": arrays}[cmd](*nums)
     out["shim"] = shim_stats()
     print("PROBE " + json.dumps(out), flush=True)
     return 0

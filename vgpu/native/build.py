@@ -117,6 +117,19 @@ def build_kernels(force: bool = False) -> Path:
     return target
 
 
+def build_probe_module(force: bool = False) -> Path:
+    """hipcc --genco: a raw gfx950 code object (not a shared library) for the
+    module-charging probe (hipModuleLoadData)."""
+    OUT.mkdir(parents=True, exist_ok=True)
+    target = OUT / "module_probe.hsaco"
+    src = NATIVE / "probes" / "module_probe.hip"
+    if not force and _stamp(target, [src], ARCH):
+        return target
+    _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "--genco", src, "-o", target])
+    _mark(target, [src], ARCH)
+    return target
+
+
 def _hip_versions() -> dict[str, str]:
     """symbol -> version node of the real libamdhip64 (for the fake's version script)."""
     out: dict[str, str] = {}
@@ -235,6 +248,7 @@ def build_all(sanitize: str | None = None, kernels: bool = True) -> dict[str, Pa
         out["shim_" + sanitize] = build_shim(sanitize)
     if kernels and have_hipcc() and any((NATIVE / "kernels").glob("*.hip")):
         out["kernels"] = build_kernels()
+        out["probe_module"] = build_probe_module()
     return out
 
 
