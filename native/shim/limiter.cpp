@@ -68,11 +68,14 @@ struct Marker {
   uint32_t launches;  // launches this marker covers (since the previous one on its stream)
 };
 
-// Per-stream marker state.  A launch records a marker only when the stream
-// has none in flight or the last one is older than the marking interval; the
-// launches in between are "dirty" and the limiter thread covers them with a
-// marker of its own once the older markers have completed, so no GPU time
-// goes uncharged while the per-launch cost stays a few hundred nanoseconds.
+// Per-stream marker state.  By default every tracked launch records a marker.
+// With VGPU_LIMITER_MARK_US > 0 a launch records one only when the stream has
+// none in flight or the last one is older than that interval; the launches in
+// between are "dirty" and the limiter thread covers them with a marker of its
+// own once the older markers have completed (no GPU time goes uncharged).
+// Measured on MI355X (4 x 25 % temporal pods, profiles/temporal_r2.md) the
+// sparse mode is slower: an event recorded from the limiter thread on the
+// application's stream costs more than the per-launch record it saves.
 struct StreamTrack {
   std::deque<Marker> q;
   uint64_t last_mark_ns = 0;
@@ -499,7 +502,7 @@ void limiter_track(int dev, hipStream_t stream) {
   if (g_open_captures.load(std::memory_order_acquire) > 0) return;  // no HIP calls mid-capture
   static const uint64_t interval_ns = [] {
     const char* v = env_first("VGPU_LIMITER_MARK_US");
-    return (uint64_t)((v ? atof(v) : 500.0) * 1000.0);
+    return (uint64_t)((v ? atof(v) : 0.0) * 1000.0);
   }();
   std::unique_lock<std::mutex> g(L.mu);
   StreamTrack& t = L.streams[stream];
