@@ -101,6 +101,19 @@ def build_smi(force: bool = False) -> Path:
     return target
 
 
+def build_sched(force: bool = False) -> Path:
+    """libvgpu_sched.so: the scheduler extender's native scoring core."""
+    OUT.mkdir(parents=True, exist_ok=True)
+    target = OUT / "libvgpu_sched.so"
+    srcs = sorted((NATIVE / "sched").glob("*.cpp"))
+    if not force and _stamp(target, srcs):
+        return target
+    _run([CXX, "-std=c++17", "-O3", "-fPIC", "-Wall", "-fvisibility=hidden", *srcs, "-o", target, "-shared",
+          "-Wl,--no-undefined"])
+    _mark(target, srcs)
+    return target
+
+
 def build_kernels(force: bool = False) -> Path:
     """hipcc --offload-arch=gfx950 → libvgpu_kernels.so (links libamdhip64.so.7,
     which resolves to the already-loaded PyTorch runtime in a torch process)."""
@@ -241,7 +254,7 @@ def have_hipcc() -> bool:
 
 
 def build_all(sanitize: str | None = None, kernels: bool = True) -> dict[str, Path]:
-    out = {"shim": build_shim(), "fakes": build_fakes()}
+    out = {"shim": build_shim(), "fakes": build_fakes(), "sched": build_sched()}
     if (NATIVE / "smi").exists() and any((NATIVE / "smi").glob("*.cpp")):
         out["smi"] = build_smi()
     if sanitize:
@@ -269,6 +282,8 @@ def main(argv: list[str] | None = None) -> int:
             build_kernels(a.force)
         elif t == "smi":
             build_smi(a.force)
+        elif t == "sched":
+            build_sched(a.force)
         elif t == "clean":
             shutil.rmtree(OUT, ignore_errors=True)
         else:

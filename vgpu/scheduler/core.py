@@ -34,7 +34,8 @@ from vgpu.k8s import objects as O
 from vgpu.k8s.client import ApiError, KubeClient
 from vgpu.k8s.nodelock import NodeLockError, lock_node
 
-from .score import FitError, NodeUsage, calc_score, pick_node
+from . import native as N
+from .score import FitError, NodeUsage, calc_score, check_type, pick_node
 
 log = logging.getLogger("vgpu.scheduler")
 
@@ -68,15 +69,25 @@ class Scheduler:
         self.overview: dict[str, NodeUsage] = {}
         self._stop = threading.Event()
         self.filter_latency_s: list[float] = []
+        # Flat per-device state for the native scorer, kept current on pod
+        # add/remove and rebuilt when the node registry changes.
+        self._flat: N.FlatState | None = None
 
     # ---- pod ledger (C4) ----------------------------------------------------------------
     def add_pod(self, pod: dict, node_id: str, devices: list[list[ContainerDevice]]) -> None:
         with self._lock:
+            old = self.pods.get(O.uid(pod))
             self.pods[O.uid(pod)] = PodInfo(O.namespace(pod), O.name(pod), O.uid(pod), node_id, devices)
+            if self._flat is not None:
+                if old is not None:
+                    self._flat.apply(old.node_id, old.devices, -1)
+                self._flat.apply(node_id, devices, +1)
 
     def del_pod(self, pod: dict) -> None:
         with self._lock:
-            self.pods.pop(O.uid(pod), None)
+            old = self.pods.pop(O.uid(pod), None)
+            if old is not None and self._flat is not None:
+                self._flat.apply(old.node_id, old.devices, -1)
 
     def scheduled_pods(self) -> dict[str, PodInfo]:
         with self._lock:
@@ -107,11 +118,14 @@ class Scheduler:
         with self._lock:
             for uid in list(self.pods):
                 if uid not in seen:
-                    self.pods.pop(uid)
+                    old = self.pods.pop(uid)
+                    if self._flat is not None:
+                        self._flat.apply(old.node_id, old.devices, -1)
 
     # ---- node registry (C3) ---------------------------------------------------------------
     def add_node(self, node_id: str, info: NodeInfo) -> None:
         with self._lock:
+            self._flat = None
             cur = self.nodes.get(node_id)
             if cur is None:
                 self.nodes[node_id] = copy.deepcopy(info)
@@ -121,6 +135,7 @@ class Scheduler:
 
     def rm_node_devices(self, node_id: str, info: NodeInfo) -> None:
         with self._lock:
+            self._flat = None
             cur = self.nodes.get(node_id)
             if cur is None:
                 return
@@ -187,6 +202,7 @@ class Scheduler:
                         log.error("patch node %s failed: %s", name, e)
                 info = NodeInfo(id=name)
                 with self._lock:
+                    self._flat = None  # device attributes may change below
                     cur = self.nodes.get(name)
                     for i, d in enumerate(devs):
                         if not d.index:
@@ -282,15 +298,21 @@ class Scheduler:
             return {"nodenames": node_names, "failedNodes": {}, "error": ""}
         annos = O.annotations(pod)
         self.del_pod(pod)  # re-scheduling is idempotent
-        usage, failed = self.nodes_usage(node_names)
-        try:
-            scores = calc_score(usage, nums, annos)
-        except FitError as e:
-            return {"nodenames": [], "failedNodes": failed, "error": str(e)}
-        best = pick_node(scores)
+        if N.load_lib() is not None:
+            best, failed = self._filter_native(node_names, nums, annos)
+            if isinstance(best, str):
+                return {"nodenames": [], "failedNodes": failed, "error": best}
+        else:
+            usage, failed = self.nodes_usage(node_names)
+            try:
+                scores = calc_score(usage, nums, annos)
+            except FitError as e:
+                return {"nodenames": [], "failedNodes": failed, "error": str(e)}
+            best = pick_node(scores)
+            if best is None:
+                for nid in usage:
+                    failed.setdefault(nid, "no device fits the request")
         if best is None:
-            for nid in usage:
-                failed.setdefault(nid, "no device fits the request")
             return {"nodenames": [], "failedNodes": failed, "error": ""}
         enc = encode_pod_devices(best.devices)
         patch = {R.ASSIGNED_NODE: best.node_id, R.ASSIGNED_TIME: str(int(time.time())),
@@ -303,6 +325,24 @@ class Scheduler:
             return {"nodenames": [], "failedNodes": failed, "error": f"patch pod failed: {e}"}
         log.info("schedule %s/%s to %s %s", O.namespace(pod), O.name(pod), best.node_id, enc)
         return {"nodenames": [best.node_id], "failedNodes": failed, "error": ""}
+
+    def _filter_native(self, node_names, nums, annos):
+        """Score on the flat device state (native/sched/score.cpp).  Returns
+        (NodeScore | None | error string, failed nodes)."""
+        from vgpu.device.amd import assert_xgmi
+        from .score import NodeScore
+        with self._lock:
+            if self._flat is None:
+                self._flat = N.FlatState(self.nodes, self.pods)
+            res, failed = self._flat.filter(
+                node_names, nums, check_type, annos, assert_xgmi(annos), config.SCHEDULER.xgmi_weight,
+                binpack_devices=config.SCHEDULER.gpu_scheduler_policy != "spread",
+                spread_nodes=config.SCHEDULER.node_scheduler_policy == "spread")
+        if res.error:
+            return res.error, failed
+        if res.node is None:
+            return None, failed
+        return NodeScore(node_id=res.node, score=res.score, devices=res.devices), failed
 
     def bind(self, args: dict) -> dict:
         ns = _ci(args, "podNamespace")
