@@ -507,3 +507,68 @@ def test_filter_scales_to_1000_nodes():
     assert r.returncode == 0, r.stderr
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["median_ms"] < 20 and res["p90_ms"] < 20, res
+
+
+# ---- watch-based pod informer ---------------------------------------------------------------
+def _wait(pred, timeout=5.0):
+    import time
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < timeout:
+        if pred():
+            return time.monotonic() - t0
+        time.sleep(0.01)
+    raise AssertionError("condition not met in time")
+
+
+def test_informer_frees_deleted_pod_slot_within_a_second(api):
+    """reference scheduler.go:72-129 (informer delete handler): once a pod is
+    deleted, its exclusive GPU can be handed out again right away."""
+    srv, c = api
+    register_node(srv, "n1", mi355x_devs(1, split=2))
+    s = Scheduler(c)
+    s.register_from_node_annotations_once()
+    import threading as th
+    t = th.Thread(target=s.run_informer, kwargs={"watch_timeout_s": 5}, daemon=True)
+    t.start()
+    try:
+        assert s.informer_synced.wait(5)
+        r = schedule(s, c, srv, pod("a", mem=1000, cores=100, uid="ua"), ["n1"])
+        assert r["nodenames"] == ["n1"]
+        assert schedule(s, c, srv, pod("b", mem=1000, cores=100, uid="ub"), ["n1"])["nodenames"] == []
+        c.delete_pod("default", "a")
+        dt_s = _wait(lambda: "ua" not in s.scheduled_pods())
+        assert dt_s < 1.0, dt_s
+        s.del_pod(c.get_pod("default", "b"))
+        assert s.filter({"pod": c.get_pod("default", "b"), "nodenames": ["n1"]})["nodenames"] == ["n1"]
+    finally:
+        s.stop()
+
+
+def test_informer_relists_after_410_gone(api):
+    srv, c = api
+    register_node(srv, "n1", mi355x_devs(2, split=2))
+    s = Scheduler(c)
+    s.register_from_node_annotations_once()
+    import threading as th
+    th.Thread(target=s.run_informer, kwargs={"watch_timeout_s": 2}, daemon=True).start()
+    try:
+        assert s.informer_synced.wait(5)
+        r = schedule(s, c, srv, pod("a", mem=1000, cores=10, uid="ua"), ["n1"])
+        assert r["nodenames"] == ["n1"]
+        srv.compact()        # history gone: the next resume gets 410 and must relist
+        _wait(lambda: s.informer_relists >= 1, timeout=8)
+        c.delete_pod("default", "a")
+        _wait(lambda: "ua" not in s.scheduled_pods(), timeout=3)
+    finally:
+        s.stop()
+
+
+def test_watch_stream_events(api):
+    srv, c = api
+    items, rv = c.list_pods_rv()
+    assert items == []
+    srv.add_pod(pod("w", uid="uw"))
+    c.patch_pod_annotations("default", "w", {"x": "1"})
+    c.delete_pod("default", "w")
+    evs = [(t, o["metadata"].get("name")) for t, o in c.watch_pods(rv, timeout_s=1) if t != "BOOKMARK"]
+    assert evs == [("ADDED", "w"), ("MODIFIED", "w"), ("DELETED", "w")]

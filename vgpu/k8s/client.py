@@ -147,6 +147,44 @@ class KubeClient:
         path = f"/api/v1/namespaces/{namespace}/pods" if namespace else "/api/v1/pods"
         return self.request("GET", path, query=q or None).get("items", [])
 
+    def list_pods_rv(self, field_selector: str | None = None) -> tuple[list[dict], str]:
+        """LIST all pods; returns (items, list resourceVersion) to start a watch from."""
+        q = {"fieldSelector": field_selector} if field_selector else None
+        r = self.request("GET", "/api/v1/pods", query=q)
+        return r.get("items", []), (r.get("metadata") or {}).get("resourceVersion", "0")
+
+    def watch_pods(self, resource_version: str, timeout_s: float = 60.0,
+                   field_selector: str | None = None):
+        """WATCH pods from `resource_version`: yields (type, object) for ADDED /
+        MODIFIED / DELETED / BOOKMARK events until the server ends the stream.
+        An ERROR event (e.g. 410 Gone: the version was compacted) raises
+        ApiError with its code; the caller relists."""
+        q = {"watch": "1", "resourceVersion": resource_version, "allowWatchBookmarks": "true",
+             "timeoutSeconds": str(int(timeout_s))}
+        if field_selector:
+            q["fieldSelector"] = field_selector
+        url = self.server + "/api/v1/pods?" + urllib.parse.urlencode(q)
+        req = urllib.request.Request(url, method="GET")
+        req.add_header("Accept", "application/json")
+        if self.token:
+            req.add_header("Authorization", f"Bearer {self.token}")
+        try:
+            resp = urllib.request.urlopen(req, timeout=timeout_s + 10, context=self._ctx)
+        except urllib.error.HTTPError as e:
+            raise ApiError(e.code, e.read().decode(errors="replace")) from None
+        except urllib.error.URLError as e:
+            raise ApiError(0, str(e.reason)) from None
+        with resp:
+            for line in resp:
+                line = line.strip()
+                if not line:
+                    continue
+                ev = json.loads(line)
+                if ev.get("type") == "ERROR":
+                    st = ev.get("object") or {}
+                    raise ApiError(int(st.get("code") or 500), st.get("message", ""))
+                yield ev.get("type"), ev.get("object") or {}
+
     def patch_pod_annotations(self, ns: str, name: str, annos: dict) -> dict:
         return self.request("PATCH", f"/api/v1/namespaces/{ns}/pods/{name}",
                             {"metadata": {"annotations": annos}},

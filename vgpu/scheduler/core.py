@@ -11,9 +11,11 @@ Differences:
   * every shared map is accessed under one lock and readers get copies (the
     reference's ListNodes / GetScheduledPods return live maps unlocked);
   * Bind fails the binding when the node lock cannot be taken;
-  * the pod informer is a resync loop over a `spec.nodeName`-filtered LIST plus
-    direct updates from Filter/Bind (no watch needed for correctness: the
-    annotations are the source of truth, so a restart rebuilds the ledger).
+  * the pod informer is LIST + WATCH (resourceVersion, bookmarks, relist on
+    410 Gone or any stream error; reference: client-go informer with
+    add/update/delete handlers, scheduler.go:72-129), so a deleted pod frees
+    its vGPU slot as soon as the delete event arrives.  The annotations stay
+    the source of truth: a restart (or a relist) rebuilds the ledger.
 """
 from __future__ import annotations
 
@@ -72,6 +74,9 @@ class Scheduler:
         # Flat per-device state for the native scorer, kept current on pod
         # add/remove and rebuilt when the node registry changes.
         self._flat: N.FlatState | None = None
+        self.informer_synced = threading.Event()
+        self.informer_events = 0
+        self.informer_relists = 0
 
     # ---- pod ledger (C4) ----------------------------------------------------------------
     def add_pod(self, pod: dict, node_id: str, devices: list[list[ContainerDevice]]) -> None:
@@ -107,9 +112,10 @@ class Scheduler:
             return
         self.add_pod(pod, node_id, decode_pod_devices(ids))
 
-    def resync_pods(self) -> None:
-        """Rebuild the ledger from pod annotations (restart recovery)."""
-        pods = self.client.list_pods()
+    def resync_pods(self, pods: list[dict] | None = None) -> None:
+        """Rebuild the ledger from pod annotations (restart recovery / relist)."""
+        if pods is None:
+            pods = self.client.list_pods()
         seen = set()
         for p in pods:
             if R.ASSIGNED_NODE in O.annotations(p):
@@ -227,16 +233,36 @@ class Scheduler:
                     log.error("registration pass failed: %s", e)
                 self._stop.wait(self.cfg.register_interval_s)
 
-        def sync():
-            while not self._stop.is_set():
-                try:
-                    self.resync_pods()
-                except Exception as e:
-                    log.error("pod resync failed: %s", e)
-                self._stop.wait(30.0)
-
         threading.Thread(target=reg, daemon=True, name="vgpu-register").start()
-        threading.Thread(target=sync, daemon=True, name="vgpu-podsync").start()
+        threading.Thread(target=self.run_informer, daemon=True, name="vgpu-informer").start()
+
+    def run_informer(self, watch_timeout_s: float = 300.0) -> None:
+        """Pod informer: LIST (ledger rebuilt from annotations) then WATCH from
+        the list's resourceVersion; relist after 410 Gone or a broken stream."""
+        backoff = 0.5
+        while not self._stop.is_set():
+            try:
+                items, rv = self.client.list_pods_rv()
+                self.resync_pods(items)
+                self.informer_synced.set()
+                backoff = 0.5
+                while not self._stop.is_set():
+                    for typ, obj in self.client.watch_pods(rv, timeout_s=watch_timeout_s):
+                        rv = (obj.get("metadata") or {}).get("resourceVersion", rv)
+                        if typ == "BOOKMARK":
+                            continue
+                        if R.ASSIGNED_NODE in O.annotations(obj) or typ == "DELETED":
+                            self.on_pod(obj, deleted=typ == "DELETED")
+                        self.informer_events += 1
+                        if self._stop.is_set():
+                            break
+            except Exception as e:  # 410 Gone, connection loss, decode errors: relist
+                if self._stop.is_set():
+                    break
+                log.warning("pod informer: %s; relisting", e)
+                self.informer_relists += 1
+                self._stop.wait(backoff)
+                backoff = min(backoff * 2, 10.0)
 
     def stop(self) -> None:
         self._stop.set()
