@@ -72,6 +72,8 @@ def main(argv=None) -> int:
     ap.add_argument("--cu-share", choices=("hybrid", "mask", "temporal", "group2", "group2i"), default="hybrid",
                     help="compute-share policy of fractional pods: the device plugin's "
                          "(hybrid|mask|temporal, vgpu/deviceplugin/custate.py) or an A/B tool")
+    ap.add_argument("--core-policy", choices=("default", "force", "disable"), default="default",
+                    help="GPU_CORE_UTILIZATION_POLICY of the pods (reference docs/config.md:34-38)")
     ap.add_argument("--no-cap-probe", action="store_true")
     ap.add_argument("--ready-timeout", type=float, default=1500.0)
     ap.add_argument("--cpu-smoke", action="store_true",
@@ -105,7 +107,8 @@ def main(argv=None) -> int:
         pg = dist
 
     device = visible_device_for(local_rank)
-    specs = [PodSpec(workload=args.workload, mem_mib=args.gpumem, cores=args.gpucores)
+    pol_env = {} if args.core_policy == "default" else {"GPU_CORE_UTILIZATION_POLICY": args.core_policy}
+    specs = [PodSpec(workload=args.workload, mem_mib=args.gpumem, cores=args.gpucores, extra_env=dict(pol_env))
              for _ in range(args.pods)]
     log(f"rank {rank}/{world}: launching {args.pods} pods of {w.name} (test {w.test_id}) on device {device}")
     pods = launch_pods(specs, device, steps=args.steps, warmup=args.warmup, shim=not args.no_shim,
@@ -186,6 +189,7 @@ def main(argv=None) -> int:
                 "conv": args.conv,
                 "hw_queues_per_pod": args.hw_queues,
                 "cu_share": args.cu_share,
+                "core_policy": args.core_policy,
             },
             "per_gpu_images_s": round(per_gpu, 2),
             "per_pod_images_s": [round(p.done["throughput"], 2) for p in pods],

@@ -8,6 +8,10 @@
 //           "mem_partition":"NPS1","gfx":0,"umc":0,"vendor":4098,
 //           "processes":[{"pid":1,"vram":N,"cu":N,"gfx_ns":N}]}],
 //  "link":"xgmi"|"pcie", "events":[{"gpu":0,"type":3,"message":".."}]}
+// Telemetry ($VGPU_FAKE_AMDSMI_TELEMETRY, re-read on every call so a test can
+// inject ECC errors while the plugin runs):
+// {"0": {"ecc_ue":N,"ecc_ce":N,"power":W,"temp_edge":C,"temp_hotspot":C,"temp_mem":C,
+//        "xgmi_read_kb":N,"xgmi_write_kb":N}}
 #include <amd_smi/amdsmi.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -37,9 +41,60 @@ const minijson::Value* gpu(amdsmi_processor_handle h) {
 
 void copy_str(char* dst, size_t n, const std::string& s) { snprintf(dst, n, "%s", s.c_str()); }
 
+minijson::Value telemetry(amdsmi_processor_handle h) {
+  minijson::Value v;
+  const char* p = getenv("VGPU_FAKE_AMDSMI_TELEMETRY");
+  if (!p) return v;
+  std::ifstream f(p);
+  if (!f) return v;
+  std::stringstream ss;
+  ss << f.rdbuf();
+  minijson::Value all;
+  if (!minijson::parse(ss.str(), all)) return v;
+  return all[std::to_string(idx(h))];
+}
+
 }  // namespace
 
 extern "C" {
+
+amdsmi_status_t amdsmi_get_gpu_total_ecc_count(amdsmi_processor_handle h, amdsmi_error_count_t* ec) {
+  if (!gpu(h)) return AMDSMI_STATUS_INVAL;
+  auto t = telemetry(h);
+  memset(ec, 0, sizeof(*ec));
+  ec->uncorrectable_count = (uint64_t)t["ecc_ue"].num(0);
+  ec->correctable_count = (uint64_t)t["ecc_ce"].num(0);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_power_info(amdsmi_processor_handle h, amdsmi_power_info_t* info) {
+  if (!gpu(h)) return AMDSMI_STATUS_INVAL;
+  auto t = telemetry(h);
+  memset(info, 0, sizeof(*info));
+  info->current_socket_power = (uint32_t)t["power"].num(0);
+  info->socket_power = info->current_socket_power;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_temp_metric(amdsmi_processor_handle h, amdsmi_temperature_type_t type,
+                                       amdsmi_temperature_metric_t, int64_t* out) {
+  if (!gpu(h)) return AMDSMI_STATUS_INVAL;
+  auto t = telemetry(h);
+  const char* key = type == AMDSMI_TEMPERATURE_TYPE_EDGE ? "temp_edge"
+                    : type == AMDSMI_TEMPERATURE_TYPE_HOTSPOT ? "temp_hotspot" : "temp_mem";
+  *out = (int64_t)t[key].num(0);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_metrics_info(amdsmi_processor_handle h, amdsmi_gpu_metrics_t* m) {
+  if (!gpu(h)) return AMDSMI_STATUS_INVAL;
+  auto t = telemetry(h);
+  memset(m, 0xff, sizeof(*m));  // "not supported" sentinel for every field we do not fill
+  for (int l = 0; l < AMDSMI_MAX_NUM_XGMI_LINKS; ++l) m->xgmi_read_data_acc[l] = m->xgmi_write_data_acc[l] = 0;
+  m->xgmi_read_data_acc[0] = (uint64_t)t["xgmi_read_kb"].num(0);
+  m->xgmi_write_data_acc[0] = (uint64_t)t["xgmi_write_kb"].num(0);
+  return AMDSMI_STATUS_SUCCESS;
+}
 
 amdsmi_status_t amdsmi_init(uint64_t) {
   const char* p = getenv("VGPU_FAKE_AMDSMI_JSON");

@@ -58,6 +58,28 @@ typedef struct vgpu_smi_event {
   char message[VGPU_SMI_STR * 2];
 } vgpu_smi_event_t;
 
+/* Health / host telemetry of one device (amdsmi: total ECC counts, power
+ * info, temperature metrics, gpu_metrics xGMI accumulators; sysfs: RAS
+ * *_err_count files and hwmon). Fields the backend cannot read stay 0. */
+typedef struct vgpu_smi_telemetry {
+  uint64_t ecc_correctable;
+  uint64_t ecc_uncorrectable;
+  uint64_t ecc_deferred;
+  uint64_t xgmi_read_kb;   /* accumulated over all links */
+  uint64_t xgmi_write_kb;
+  uint32_t power_w;
+  int32_t temp_edge_c;
+  int32_t temp_hotspot_c;
+  int32_t temp_mem_c;
+  uint32_t valid;          /* bit 0 ecc, 1 power, 2 temperature, 3 xgmi */
+  uint32_t reserved[7];
+} vgpu_smi_telemetry_t;
+
+#define VGPU_TELEM_ECC 1u
+#define VGPU_TELEM_POWER 2u
+#define VGPU_TELEM_TEMP 4u
+#define VGPU_TELEM_XGMI 8u
+
 /* link types */
 #define VGPU_LINK_UNKNOWN 0
 #define VGPU_LINK_PCIE 1
@@ -70,6 +92,7 @@ int vgpu_smi_get(int index, vgpu_smi_device_t* out);
 int vgpu_smi_link(int a, int b, uint64_t* hops, int32_t* type);
 int vgpu_smi_processes(int index, vgpu_smi_proc_t* out, int max);
 int vgpu_smi_events(vgpu_smi_event_t* out, int max, int timeout_ms);
+int vgpu_smi_telemetry(int index, vgpu_smi_telemetry_t* out);
 void vgpu_smi_close(void);
 
 #ifdef __cplusplus

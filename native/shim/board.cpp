@@ -160,6 +160,22 @@ uint64_t board_charge(vgpu_board_t* b, int slot, uint64_t wall_ns, bool leave) {
   return (uint64_t)c;
 }
 
+// Weighted fair share of `slot` among the slots with work outstanding, counting
+// `slot` itself as active: limit_pct(self) / Σ limit_pct(active).  Racy reads
+// of other slots are fine: the limiter integrates this over time.
+double board_entitlement(vgpu_board_t* b, int slot) {
+  if (!b || slot < 0) return 1.0;
+  const uint64_t now = mono_ns();
+  const double self_w = b->slot[slot].limit_pct > 0 ? b->slot[slot].limit_pct : 1;
+  double sum = self_w;
+  for (int i = 0; i < VGPU_BOARD_SLOTS; ++i) {
+    if (i == slot) continue;
+    const vgpu_board_slot_t& s = b->slot[i];
+    if (live(s, now)) sum += s.limit_pct > 0 ? s.limit_pct : 1;
+  }
+  return self_w / sum;
+}
+
 int board_active_count(vgpu_board_t* b) {
   if (!b) return 0;
   const uint64_t now = mono_ns();

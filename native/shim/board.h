@@ -13,5 +13,6 @@ void board_enter(vgpu_board_t* b, int slot);
 // Fair-share GPU ns accrued since the previous charge (wall_ns when there is no board).
 uint64_t board_charge(vgpu_board_t* b, int slot, uint64_t wall_ns, bool leave);
 int board_active_count(vgpu_board_t* b);
+double board_entitlement(vgpu_board_t* b, int slot);  // weighted fair share among active slots
 
 }  // namespace vgpu

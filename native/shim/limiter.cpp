@@ -324,7 +324,14 @@ void limiter_main() {
     for (int d = 0; d < VGPU_MAX_DEVICES; ++d) {
       DevLimiter& L = g_lim[d];
       if (!L.active) continue;
-      const int64_t add = (int64_t)(L.frac * dt);
+      // Credit rate.  force: the hard cap (limit % of wall time).  default:
+      // work-conserving weighted fair share among the pods of this GPU that
+      // have work outstanding (board entitlement) -- a pod alone is not held
+      // back, k equal pods get 1/k each, a 25 % and a 75 % pod get 1:3 --
+      // the reference's "throttle only under contention" made proportional.
+      double rate = L.frac;
+      if (s.lim.core_policy != 1 && L.board) rate = fmax(L.frac, board_entitlement(L.board, L.board_slot));
+      const int64_t add = (int64_t)(rate * dt);
       int64_t cur = L.tokens.load(std::memory_order_relaxed), nv;
       do {
         nv = cur + add;
@@ -465,6 +472,9 @@ bool limiter_on_launch(int dev, uint64_t wg, const void* fn) {
   if (s.region && s.lim.core_policy != 1 &&
       __atomic_load_n(&s.region->utilization_switch, __ATOMIC_RELAXED) == 0)
     return false;  // monitor says no contention: run unthrottled
+  // VGPU_LIMITER_DRYRUN=1: measure and charge, never wait (diagnostics).
+  static const bool dryrun = env_bool(env_first("VGPU_LIMITER_DRYRUN"), false);
+  if (dryrun) return true;
   // Wait while the bucket cannot pay for the work already in flight; once
   // overdrawn, hold until it has refilled by a whole quantum.
   uint64_t t0 = 0;

@@ -51,6 +51,10 @@ struct AmdSmi {
   F(amdsmi_init_gpu_event_notification);
   F(amdsmi_set_gpu_event_notification_mask);
   F(amdsmi_get_gpu_event_notification);
+  F(amdsmi_get_gpu_total_ecc_count);
+  F(amdsmi_get_power_info);
+  F(amdsmi_get_temp_metric);
+  F(amdsmi_get_gpu_metrics_info);
 #undef F
   std::vector<amdsmi_processor_handle> gpus;
   bool events_on = false;
@@ -75,6 +79,8 @@ struct AmdSmi {
     L(amdsmi_get_gpu_enumeration_info); L(amdsmi_get_xgmi_info);
     L(amdsmi_init_gpu_event_notification); L(amdsmi_set_gpu_event_notification_mask);
     L(amdsmi_get_gpu_event_notification);
+    L(amdsmi_get_gpu_total_ecc_count); L(amdsmi_get_power_info); L(amdsmi_get_temp_metric);
+    L(amdsmi_get_gpu_metrics_info);
 #undef L
     if (!amdsmi_init || !amdsmi_get_socket_handles || !amdsmi_get_processor_handles) return false;
     if (amdsmi_init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) return false;
@@ -96,6 +102,54 @@ struct AmdSmi {
       }
     }
     return true;
+  }
+
+  void telemetry(int i, vgpu_smi_telemetry_t* t) {
+    amdsmi_processor_handle p = gpus[i];
+    memset(t, 0, sizeof(*t));
+    amdsmi_error_count_t ec;
+    if (amdsmi_get_gpu_total_ecc_count && amdsmi_get_gpu_total_ecc_count(p, &ec) == AMDSMI_STATUS_SUCCESS) {
+      t->ecc_correctable = ec.correctable_count;
+      t->ecc_uncorrectable = ec.uncorrectable_count;
+      t->ecc_deferred = ec.deferred_count;
+      t->valid |= VGPU_TELEM_ECC;
+    }
+    amdsmi_power_info_t pw;
+    if (amdsmi_get_power_info && amdsmi_get_power_info(p, &pw) == AMDSMI_STATUS_SUCCESS) {
+      uint32_t w = pw.current_socket_power;
+      if (w == 0 || w == 0xFFFFu || w == 0xFFFFFFFFu) w = pw.average_socket_power;
+      if (w == 0xFFFFu || w == 0xFFFFFFFFu) w = 0;
+      t->power_w = w;
+      t->valid |= VGPU_TELEM_POWER;
+    }
+    if (amdsmi_get_temp_metric) {
+      int64_t v = 0;
+      bool any = false;
+      if (amdsmi_get_temp_metric(p, AMDSMI_TEMPERATURE_TYPE_EDGE, AMDSMI_TEMP_CURRENT, &v) == AMDSMI_STATUS_SUCCESS) {
+        t->temp_edge_c = (int32_t)v;
+        any = true;
+      }
+      if (amdsmi_get_temp_metric(p, AMDSMI_TEMPERATURE_TYPE_HOTSPOT, AMDSMI_TEMP_CURRENT, &v) == AMDSMI_STATUS_SUCCESS) {
+        t->temp_hotspot_c = (int32_t)v;
+        any = true;
+      }
+      if (amdsmi_get_temp_metric(p, AMDSMI_TEMPERATURE_TYPE_VRAM, AMDSMI_TEMP_CURRENT, &v) == AMDSMI_STATUS_SUCCESS) {
+        t->temp_mem_c = (int32_t)v;
+        any = true;
+      }
+      if (any) t->valid |= VGPU_TELEM_TEMP;
+    }
+    if (amdsmi_get_gpu_metrics_info) {
+      amdsmi_gpu_metrics_t* m = new amdsmi_gpu_metrics_t;
+      if (amdsmi_get_gpu_metrics_info(p, m) == AMDSMI_STATUS_SUCCESS) {
+        for (int l = 0; l < AMDSMI_MAX_NUM_XGMI_LINKS; ++l) {
+          if (m->xgmi_read_data_acc[l] != UINT64_MAX) t->xgmi_read_kb += m->xgmi_read_data_acc[l];
+          if (m->xgmi_write_data_acc[l] != UINT64_MAX) t->xgmi_write_kb += m->xgmi_write_data_acc[l];
+        }
+        t->valid |= VGPU_TELEM_XGMI;
+      }
+      delete m;
+    }
   }
 
   void fill(int i, vgpu_smi_device_t* d) {
@@ -393,6 +447,65 @@ __attribute__((visibility("default"))) int vgpu_smi_processes(int i, vgpu_smi_pr
   }
   closedir(d);
   return k;
+}
+
+namespace {
+
+// sysfs telemetry: RAS error counters ("ue: N" / "ce: N" per block in
+// <pci>/ras/*_err_count) and the first hwmon's power / temperature.
+void sysfs_telemetry(const SysfsDev& s, vgpu_smi_telemetry_t* t) {
+  std::string ras = s.pci_dir + "/ras";
+  if (DIR* d = opendir(ras.c_str())) {
+    while (struct dirent* e = readdir(d)) {
+      std::string n = e->d_name;
+      if (n.size() < 10 || n.compare(n.size() - 10, 10, "_err_count") != 0) continue;
+      std::string body;
+      if (!read_file(ras + "/" + n, body)) continue;
+      unsigned long long ue = 0, ce = 0;
+      const char* u = strstr(body.c_str(), "ue:");
+      const char* c = strstr(body.c_str(), "ce:");
+      if (u) ue = strtoull(u + 3, nullptr, 10);
+      if (c) ce = strtoull(c + 3, nullptr, 10);
+      t->ecc_uncorrectable += ue;
+      t->ecc_correctable += ce;
+      t->valid |= VGPU_TELEM_ECC;
+    }
+    closedir(d);
+  }
+  std::string hw = s.pci_dir + "/hwmon";
+  if (DIR* d = opendir(hw.c_str())) {
+    while (struct dirent* e = readdir(d)) {
+      if (strncmp(e->d_name, "hwmon", 5)) continue;
+      std::string base = hw + "/" + e->d_name, v;
+      if (read_file(base + "/power1_average", v) || read_file(base + "/power1_input", v)) {
+        t->power_w = (uint32_t)(strtoull(v.c_str(), nullptr, 10) / 1000000ull);  // microwatts
+        t->valid |= VGPU_TELEM_POWER;
+      }
+      if (read_file(base + "/temp1_input", v)) {
+        t->temp_edge_c = (int32_t)(atoll(v.c_str()) / 1000);  // millidegrees
+        t->valid |= VGPU_TELEM_TEMP;
+      }
+      if (read_file(base + "/temp2_input", v)) t->temp_hotspot_c = (int32_t)(atoll(v.c_str()) / 1000);
+      if (read_file(base + "/temp3_input", v)) t->temp_mem_c = (int32_t)(atoll(v.c_str()) / 1000);
+      break;
+    }
+    closedir(d);
+  }
+}
+
+}  // namespace
+
+__attribute__((visibility("default"))) int vgpu_smi_telemetry(int i, vgpu_smi_telemetry_t* out) {
+  std::lock_guard<std::mutex> g(g_mu);
+  memset(out, 0, sizeof(*out));
+  if (g_smi) {
+    if (i < 0 || i >= (int)g_smi->gpus.size()) return -1;
+    g_smi->telemetry(i, out);
+    return 0;
+  }
+  if (i < 0 || i >= (int)g_sysfs.size()) return -1;
+  sysfs_telemetry(g_sysfs[i], out);
+  return 0;
 }
 
 __attribute__((visibility("default"))) int vgpu_smi_events(vgpu_smi_event_t* out, int max, int timeout_ms) {

@@ -95,6 +95,15 @@ def make_sysfs(root, n=2):
         (pci / "current_memory_partition").write_text("NPS1\n")
         (pci / "product_name").write_text("AMD Instinct MI355X\n")
         (pci / "mem_info_vram_used").write_text("1048576\n")
+        ras = pci / "ras"
+        ras.mkdir()
+        (ras / "umc_err_count").write_text(f"ue: {i}\nce: {10 * i}\n")
+        (ras / "gfx_err_count").write_text("ue: 0\nce: 1\n")
+        hw = pci / "hwmon/hwmon3"
+        hw.mkdir(parents=True)
+        (hw / "power1_average").write_text(f"{(700 + i) * 1000000}\n")
+        (hw / "temp1_input").write_text("51000\n")
+        (hw / "temp2_input").write_text("73500\n")
 
 
 def test_discovery_sysfs(native_build, tmp_path):
@@ -350,3 +359,66 @@ def test_allocate_cdi_strategies(cluster):
     assert len(r.devices) == 0 and len(r.cdi_devices) == 0
     assert dict(r.annotations)[CDI_ANNOTATION].startswith("amd.com/gpu=")
     c["cfg"].device_list_strategy = "envvar"
+
+
+# ---- health: ECC / VM fault / thermal + host telemetry ------------------------------------
+TELEM = ("import json; from vgpu.deviceplugin.discovery import SmiBackend; b=SmiBackend('{mode}');"
+         "print(json.dumps([b.telemetry(i).__dict__ for i in range(len(b.devices()))]))")
+
+
+def test_telemetry_fake_amdsmi(native_build, tmp_path):
+    fx = {"gpus": [{"uuid": f"GPU-{i}", "hive": 1} for i in range(2)], "link": "xgmi"}
+    (tmp_path / "fx.json").write_text(json.dumps(fx))
+    (tmp_path / "t.json").write_text(json.dumps({"1": {"ecc_ue": 3, "ecc_ce": 40, "power": 1120, "temp_edge": 55,
+                                                       "temp_hotspot": 81, "temp_mem": 70,
+                                                       "xgmi_read_kb": 5, "xgmi_write_kb": 7}}))
+    out = _smi_subprocess({"VGPU_AMDSMI_LIB": str(FAKES_DIR / "libamd_smi.so"),
+                           "VGPU_FAKE_AMDSMI_JSON": str(tmp_path / "fx.json"),
+                           "VGPU_FAKE_AMDSMI_TELEMETRY": str(tmp_path / "t.json")}, TELEM.format(mode="amdsmi"))
+    t0, t1 = out
+    assert t0["ecc_uncorrectable"] == 0 and t0["valid"] & 1
+    assert (t1["ecc_uncorrectable"], t1["ecc_correctable"], t1["power_w"]) == (3, 40, 1120)
+    assert (t1["temp_edge_c"], t1["temp_hotspot_c"], t1["temp_mem_c"]) == (55, 81, 70)
+    assert (t1["xgmi_read_bytes"], t1["xgmi_write_bytes"]) == (5 * 1024, 7 * 1024)
+
+
+def test_telemetry_sysfs_ras_and_hwmon(native_build, tmp_path):
+    make_sysfs(tmp_path, 2)
+    out = _smi_subprocess({"VGPU_SYSFS_ROOT": str(tmp_path)}, TELEM.format(mode="sysfs"))
+    assert [t["ecc_uncorrectable"] for t in out] == [1, 2]
+    assert [t["ecc_correctable"] for t in out] == [11, 21]
+    assert [t["power_w"] for t in out] == [701, 702]
+    assert out[0]["temp_edge_c"] == 51 and out[0]["temp_hotspot_c"] == 73
+
+
+def test_health_uncorrectable_ecc_then_reset_recovers(cluster):
+    """reference rm/health.go:42-189 (ECC events → unhealthy); the reference
+    never recovers (server.go:253 FIXME) — here a GPU reset clears it."""
+    from vgpu.deviceplugin.discovery import EVT_THERMAL, EVT_VMFAULT, Telemetry
+    c = cluster
+    plugin, backend = c["plugin"], c["backend"]
+    stream = c["stub"].ListAndWatch(api.Empty(), timeout=10)
+    next(stream)
+    backend.telemetry_by_index = {i: Telemetry(ecc_uncorrectable=5, valid=1) for i in range(8)}
+    plugin.health_step(10)  # baseline: pre-existing errors do not count
+    assert all(plugin.health.values())
+    backend.telemetry_by_index[3] = Telemetry(ecc_uncorrectable=7, valid=1)
+    plugin.health_step(10)
+    upd = next(stream)
+    bad = {d.ID.rsplit("-", 1)[0] for d in upd.devices if d.health == api.UNHEALTHY}
+    assert bad == {plugin.devices[3].uuid}
+    # application faults and throttling are counted, device health unchanged
+    backend.pending_events += [(1, EVT_VMFAULT, "page fault"), (1, EVT_THERMAL, "hot")]
+    plugin.health_step(10)
+    assert plugin.vm_faults[plugin.devices[1].uuid] == 1 and plugin.thermal_events[plugin.devices[1].uuid] == 1
+    assert plugin.health[plugin.devices[1].uuid]
+    # reset: pre → still unhealthy, post → healthy with a new ECC baseline
+    backend.pending_events.append((3, EVT_PRE_RESET, "mode1"))
+    plugin.health_step(10)
+    backend.pending_events.append((3, EVT_POST_RESET, "done"))
+    plugin.health_step(10)
+    assert plugin.health[plugin.devices[3].uuid]
+    upd = next(stream)
+    while any(d.health == api.UNHEALTHY for d in upd.devices):
+        upd = next(stream)
+    stream.cancel()

@@ -4,8 +4,10 @@ inference, hipGraph replays), run through bench.py's pod launcher.
 
 Reference semantics: libvgpu.so `rate_limiter` / `utilization_watcher`
  hold a pod to its gpucores share of the GPU; VERDICT r1
-asks for a lone 25 % pod at 22-28 % of exclusive and 4 x 25 % pods at
->= 0.85 x exclusive with per-pod shares within +-15 % of 25 %.
+asks for a lone 25 % pod at 22-28 % of exclusive (policy force: the cap holds
+without contention) and 4 x 25 % pods at >= 0.85 x exclusive with per-pod
+shares within +-15 % of 25 % (default policy: weighted fair share under
+contention, work-conserving).
 """
 import json
 import os
@@ -36,7 +38,8 @@ def exclusive(gpu_build):
 
 
 def test_lone_quarter_pod_gets_a_quarter(exclusive):
-    d = bench("--pods", "1", "--gpucores", "25", "--cu-share", "temporal")
+    """GPU_CORE_UTILIZATION_POLICY=force: the hard cap even without contention."""
+    d = bench("--pods", "1", "--gpucores", "25", "--cu-share", "temporal", "--core-policy", "force")
     share = d["value"] / exclusive
     assert 0.22 <= share <= 0.28, share
 

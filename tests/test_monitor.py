@@ -169,3 +169,27 @@ def test_nodeinfo_endpoint(native_build, tmp_path, monkeypatch):
         http.shutdown()
         ra.close()
         srv.stop()
+
+
+def test_host_telemetry_metrics():
+    """V5 host series (reference HostGPUMemoryUsage / HostCoreUtilization,
+    cmd/vGPUmonitor/metrics.go:113-129) plus MI355X power, temperature, ECC
+    and xGMI traffic."""
+    from prometheus_client import CollectorRegistry, generate_latest
+    from vgpu.deviceplugin.discovery import StaticBackend, Telemetry, mi355x_node
+
+    class NoRegions:
+        regions = {}
+
+    be = StaticBackend(mi355x_node(2))
+    be.telemetry_by_index = {0: Telemetry(ecc_correctable=4, ecc_uncorrectable=1, xgmi_read_bytes=1 << 30,
+                                          xgmi_write_bytes=2 << 30, power_w=1050, temp_edge_c=50,
+                                          temp_hotspot_c=80, temp_mem_c=70, valid=15)}
+    reg = CollectorRegistry()
+    reg.register(MonitorCollector(NoRegions(), be))
+    text = generate_latest(reg).decode()
+    assert 'HostGPUPowerWatts{deviceidx="0",deviceuuid="GPU-1111-00"} 1050.0' in text
+    assert 'HostGPUTemperatureCelsius{deviceidx="0",deviceuuid="GPU-1111-00",sensor="hotspot"} 80.0' in text
+    assert 'HostGPUECCErrors_total{deviceidx="0",deviceuuid="GPU-1111-00",type="uncorrectable"} 1.0' in text
+    assert 'HostXGMIReadBytes_total{deviceidx="0",deviceuuid="GPU-1111-00"} 1.073741824e+09' in text
+    assert 'GPU-1111-01"} 1050' not in text  # device 1 reports no telemetry

@@ -259,7 +259,7 @@ def test_temporal_limit_holds_gpu_time_share(native_build, limit):
     """A lone pod with a 25 % / 50 % temporal limit gets that share of GPU time
     (fake timeline: every launch is 500 µs of GPU work)."""
     o = run("duty", 2, env={"VGPU_DEVICE_CU_LIMIT_0": str(limit), "VGPU_CU_MASK_FROM_LIMIT": "false",
-                            "VGPU_FAKE_KERNEL_US": "500"}, timeout=60)
+                            "GPU_CORE_UTILIZATION_POLICY": "force", "VGPU_FAKE_KERNEL_US": "500"}, timeout=60)
     assert abs(_duty(o) - limit / 100) < 0.04, o
     assert abs(float(o["charged_s"]) / float(o["wall_s"]) - limit / 100) < 0.04
 
@@ -267,7 +267,8 @@ def test_temporal_limit_holds_gpu_time_share(native_build, limit):
 def test_temporal_limit_graph_launches(native_build):
     """Graph replays are charged by their measured GPU time too."""
     o = run("duty", 2, "graph", env={"VGPU_DEVICE_CU_LIMIT_0": "25", "VGPU_CU_MASK_FROM_LIMIT": "false",
-                                     "VGPU_FAKE_KERNEL_US": "2000"}, timeout=60)
+                                     "GPU_CORE_UTILIZATION_POLICY": "force", "VGPU_FAKE_KERNEL_US": "2000"},
+            timeout=60)
     assert abs(_duty(o) - 0.25) < 0.05, o
 
 
@@ -276,10 +277,11 @@ def test_unlimited_runs_flat_out(native_build):
     assert _duty(o) > 0.95
 
 
-def _pair(tmp_path, limit, board):
+def _pair(tmp_path, limit, board, policy="force"):
     lock = tmp_path / "lock"
     lock.mkdir(exist_ok=True)
     env = {"VGPU_DEVICE_CU_LIMIT_0": str(limit), "VGPU_CU_MASK_FROM_LIMIT": "false",
+           "GPU_CORE_UTILIZATION_POLICY": policy,
            "VGPU_FAKE_KERNEL_US": "500", "VGPU_FAKE_GPU_TIMELINE": str(tmp_path / "timeline"),
            "VGPU_LOCK_DIR": str(lock), "VGPU_DEVICE_UUID_0": "GPU-test",
            "VGPU_SHARE_BOARD": "true" if board else "false"}
@@ -324,7 +326,7 @@ def test_pool_member_time_share_scaled_to_pool(native_build):
     pool = hex(int("ff" * 16, 16))  # 128 low CUs
     o = run("duty", 2, env={"VGPU_DEVICE_CU_LIMIT_0": "25", "VGPU_CU_MASK_0": pool, "VGPU_CU_SHARE": "temporal",
                             "VGPU_CU_MASK_FROM_LIMIT": "false", "VGPU_FAKE_KERNEL_US": "500",
-                            "VGPU_LOG_LEVEL": "3"}, timeout=60)
+                            "GPU_CORE_UTILIZATION_POLICY": "force", "VGPU_LOG_LEVEL": "3"}, timeout=60)
     assert abs(_duty(o) - 0.5) < 0.05, o
     assert "pool of 128/256 CUs, time share 25% -> 50%" in o["_stderr"]
 
@@ -371,3 +373,25 @@ def test_ipc_import_is_charged_to_the_exporter_only(native_build, tmp_path):
     assert o["region_used"] == str(GiB)         # container total: the buffer once
     assert o["buffer_after_free"] == "0"        # a stray hipFree of the mapping uncharges nothing
     assert o["close"] == "0" and o["imported_after"] == "0"
+
+
+def test_default_policy_is_work_conserving(native_build, tmp_path):
+    """Default policy (reference: throttle only under contention): two 25 % pods
+    that both keep the device busy split it evenly instead of idling half of it;
+    with GPU_CORE_UTILIZATION_POLICY=force each is held to its 25 %."""
+    (tmp_path / "d").mkdir()
+    (tmp_path / "f").mkdir()
+    soft = _pair(tmp_path / "d", 25, board=True, policy="default")
+    hard = _pair(tmp_path / "f", 25, board=True, policy="force")
+    assert sum(_duty(o) for o in soft) > 0.9, soft
+    for o in hard:
+        assert abs(_duty(o) - 0.25) < 0.05, o
+
+
+def test_default_policy_lone_pod_unthrottled(native_build, tmp_path):
+    lock = tmp_path / "lock"
+    lock.mkdir()
+    o = run("duty", 1, env={"VGPU_DEVICE_CU_LIMIT_0": "25", "VGPU_CU_MASK_FROM_LIMIT": "false",
+                            "VGPU_FAKE_KERNEL_US": "500", "VGPU_LOCK_DIR": str(lock),
+                            "VGPU_DEVICE_UUID_0": "GPU-solo"}, timeout=60)
+    assert _duty(o) > 0.9, o

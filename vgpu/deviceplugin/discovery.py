@@ -35,6 +35,32 @@ class _SmiProc(ctypes.Structure):
                 ("vram_bytes", ctypes.c_uint64), ("gfx_ns", ctypes.c_uint64)]
 
 
+class _SmiTelemetry(ctypes.Structure):
+    _fields_ = [("ecc_correctable", ctypes.c_uint64), ("ecc_uncorrectable", ctypes.c_uint64),
+                ("ecc_deferred", ctypes.c_uint64), ("xgmi_read_kb", ctypes.c_uint64),
+                ("xgmi_write_kb", ctypes.c_uint64), ("power_w", ctypes.c_uint32),
+                ("temp_edge_c", ctypes.c_int32), ("temp_hotspot_c", ctypes.c_int32),
+                ("temp_mem_c", ctypes.c_int32), ("valid", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 7)]
+
+
+TELEM_ECC, TELEM_POWER, TELEM_TEMP, TELEM_XGMI = 1, 2, 4, 8
+
+
+@dataclass
+class Telemetry:
+    """Health / host counters of one device (native vgpu_smi_telemetry)."""
+    ecc_correctable: int = 0
+    ecc_uncorrectable: int = 0
+    ecc_deferred: int = 0
+    xgmi_read_bytes: int = 0
+    xgmi_write_bytes: int = 0
+    power_w: int = 0
+    temp_edge_c: int = 0
+    temp_hotspot_c: int = 0
+    temp_mem_c: int = 0
+    valid: int = 0
+
+
 class _SmiEvent(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("type", ctypes.c_int32), ("message", ctypes.c_char * (STR * 2))]
 
@@ -105,6 +131,9 @@ class Backend:
     def events(self, timeout_ms: int = 1000) -> list[tuple[int, int, str]]:
         return []
 
+    def telemetry(self, index: int) -> Telemetry | None:
+        return None
+
 
 class SmiBackend(Backend):
     def __init__(self, mode: str = "auto"):
@@ -119,6 +148,7 @@ class SmiBackend(Backend):
         lib.vgpu_smi_processes.argtypes = [ctypes.c_int, ctypes.POINTER(_SmiProc), ctypes.c_int]
         lib.vgpu_smi_events.argtypes = [ctypes.POINTER(_SmiEvent), ctypes.c_int, ctypes.c_int]
         lib.vgpu_smi_backend.restype = ctypes.c_char_p
+        lib.vgpu_smi_telemetry.argtypes = [ctypes.c_int, ctypes.POINTER(_SmiTelemetry)]
         self.lib = lib
         n = lib.vgpu_smi_open(mode.encode())
         if n < 0:
@@ -153,6 +183,14 @@ class SmiBackend(Backend):
         return [Proc(buf[i].pid, buf[i].vram_bytes, buf[i].cu_occupancy, buf[i].gfx_ns)
                 for i in range(max(n, 0))]
 
+    def telemetry(self, index: int) -> Telemetry | None:
+        t = _SmiTelemetry()
+        if self.lib.vgpu_smi_telemetry(index, ctypes.byref(t)) != 0:
+            return None
+        return Telemetry(t.ecc_correctable, t.ecc_uncorrectable, t.ecc_deferred, t.xgmi_read_kb * 1024,
+                         t.xgmi_write_kb * 1024, t.power_w, t.temp_edge_c, t.temp_hotspot_c, t.temp_mem_c,
+                         t.valid)
+
     def events(self, timeout_ms: int = 1000) -> list[tuple[int, int, str]]:
         buf = (_SmiEvent * 32)()
         n = self.lib.vgpu_smi_events(buf, 32, timeout_ms)
@@ -168,6 +206,7 @@ class StaticBackend(Backend):
         self.xgmi = xgmi
         self._procs = procs or {}
         self.pending_events: list[tuple[int, int, str]] = []
+        self.telemetry_by_index: dict[int, Telemetry] = {}
 
     def devices(self) -> list[Device]:
         return [Device(**asdict(d)) for d in self._devs]
@@ -184,6 +223,9 @@ class StaticBackend(Backend):
     def events(self, timeout_ms: int = 1000) -> list[tuple[int, int, str]]:
         ev, self.pending_events = self.pending_events, []
         return ev
+
+    def telemetry(self, index: int) -> Telemetry | None:
+        return self.telemetry_by_index.get(index)
 
 
 def mi355x_node(n: int = 8, hive: int = 0x1111) -> list[Device]:

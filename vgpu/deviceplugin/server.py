@@ -33,7 +33,8 @@ from . import api
 from .allocate import AllocateError, allocate, get_pending_pod, next_device_request
 from . import cdi
 from .custate import CUMaskState
-from .discovery import EVT_POST_RESET, EVT_PRE_RESET, Backend, Device
+from .discovery import (EVT_POST_RESET, EVT_PRE_RESET, EVT_THERMAL, EVT_VMFAULT, TELEM_ECC, Backend,
+                        Device)
 from .topology import link_matrix, preferred
 
 log = logging.getLogger("vgpu.deviceplugin")
@@ -60,6 +61,9 @@ class VGPUDevicePlugin:
         self.devices = backend.devices()
         self.by_uuid = {d.uuid: d for d in self.devices}
         self.health: dict[str, bool] = {d.uuid: d.health for d in self.devices}
+        self._ecc_baseline: dict[str, int] = {}   # uncorrectable ECC count at the last healthy point
+        self.vm_faults: dict[str, int] = {}
+        self.thermal_events: dict[str, int] = {}
         self.cu_state = CUMaskState(os.path.join(cfg.host_lib_dir, "containers"), policy=cfg.cu_share,
                                     max_mask_slots=cfg.max_mask_slots)
         log.info("compute share policy %s (max %d masked vGPUs per GPU), CU packing %s", cfg.cu_share,
@@ -242,8 +246,15 @@ class VGPUDevicePlugin:
 
     # ---- health ---------------------------------------------------------------------------------
     def health_step(self, timeout_ms: int = 1000) -> None:
-        """One poll: device events (reset → unhealthy, post-reset → healthy) and
-        the device list itself (a vanished device → unhealthy)."""
+        """One poll (reference rm/health.go:42-189: XID/ECC event set):
+        * device events: reset → unhealthy, post-reset → healthy again (the
+          reference has no recovery path, server.go:253 FIXME); VM faults and
+          thermal throttling are counted and logged but leave the device
+          healthy (an application fault, like the XIDs 13/31/43/45/68 the
+          reference skips);
+        * uncorrectable ECC: any increase of the device's RAS uncorrectable
+          count since the last healthy baseline → unhealthy until a reset;
+        * the device list itself: a vanished device → unhealthy."""
         if os.environ.get("DP_DISABLE_HEALTHCHECKS", "").lower() in ("all", "true", "1"):
             return
         for dev, typ, msg in self.backend.events(timeout_ms):
@@ -253,7 +264,22 @@ class VGPUDevicePlugin:
             if typ == EVT_PRE_RESET:
                 self.set_health(uuid, False, f"GPU reset: {msg}")
             elif typ == EVT_POST_RESET:
+                self._ecc_baseline.pop(uuid, None)  # counters restart with the device
                 self.set_health(uuid, True, f"GPU reset done: {msg}")
+            elif typ == EVT_VMFAULT:
+                self.vm_faults[uuid] = self.vm_faults.get(uuid, 0) + 1
+                log.warning("device %s: VM fault (%s); device stays healthy", uuid, msg)
+            elif typ == EVT_THERMAL:
+                self.thermal_events[uuid] = self.thermal_events.get(uuid, 0) + 1
+                log.warning("device %s: thermal throttling (%s)", uuid, msg)
+        for d in self.devices:
+            t = self.backend.telemetry(d.index)
+            if t is None or not t.valid & TELEM_ECC:
+                continue
+            base = self._ecc_baseline.setdefault(d.uuid, t.ecc_uncorrectable)
+            if t.ecc_uncorrectable > base and self.health.get(d.uuid, True):
+                self.set_health(d.uuid, False,
+                                f"uncorrectable ECC errors: {t.ecc_uncorrectable - base} new")
         present = {d.uuid: d for d in self.backend.devices()}
         for d in self.devices:
             if d.uuid not in present:

@@ -85,6 +85,8 @@ class DeviceView:
     buffer: int
     swap_in: int
     swap_out: int
+    busy_permille: int = 0   # fair-share GPU time of the last limiter window (shim-published)
+    busy_ns: int = 0
 
 
 class AttachedRegion:
@@ -122,7 +124,7 @@ class AttachedRegion:
             out.append(DeviceView(i, d.uuid.decode(errors="replace"), d.mem_limit, d.cu_limit, mask,
                                   agg["total_bytes"], agg["host_bytes"], agg["context_bytes"],
                                   agg["module_bytes"], agg["buffer_bytes"], agg["swap_in_bytes"],
-                                  agg["swap_out_bytes"]))
+                                  agg["swap_out_bytes"], d.busy_permille, d.busy_ns))
         return out
 
     @property
