@@ -27,4 +27,21 @@ rsmi_status_t rsmi_dev_memory_usage_get(uint32_t, rsmi_memory_type_t, uint64_t* 
   return RSMI_STATUS_SUCCESS;
 }
 
+// VGPU_FAKE_RSMI_PIDS="pid,pid,..": compute processes on the "node".
+rsmi_status_t rsmi_compute_process_info_get(rsmi_process_info_t* procs, uint32_t* num) {
+  const char* v = getenv("VGPU_FAKE_RSMI_PIDS");
+  uint32_t n = 0;
+  for (const char* p = v; p && *p;) {
+    char* end;
+    unsigned long pid = strtoul(p, &end, 10);
+    if (end == p) break;
+    if (procs && n < *num) procs[n] = rsmi_process_info_t{(uint32_t)pid, 0, 1ull << 20, 0, 0};
+    ++n;
+    p = *end ? end + 1 : end;
+  }
+  const bool small = procs && n > *num;
+  *num = n;
+  return small ? RSMI_STATUS_INSUFFICIENT_SIZE : RSMI_STATUS_SUCCESS;
+}
+
 }  // extern "C"

@@ -4,6 +4,7 @@
 #include <rocm_smi/rocm_smi.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "common.h"
 #include "real.h"
@@ -44,6 +45,31 @@ __attribute__((visibility("default"))) rsmi_status_t rsmi_dev_memory_usage_get(
     *used = std::min<uint64_t>(u, lim);
   }
   return rc;
+}
+
+// Compute processes on the node (KFD), filtered to this container's own.
+__attribute__((visibility("default"))) rsmi_status_t rsmi_compute_process_info_get(
+    rsmi_process_info_t* procs, uint32_t* num_items) {
+  auto real = REAL_RSMI(rsmi_compute_process_info_get);
+  ensure_init();
+  if (!st().enabled || !num_items) return real(procs, num_items);
+  uint32_t n = 0;
+  rsmi_status_t rc = real(nullptr, &n);
+  if (rc != RSMI_STATUS_SUCCESS && rc != RSMI_STATUS_INSUFFICIENT_SIZE) return rc;
+  std::vector<rsmi_process_info_t> all(n + 16);
+  uint32_t got = (uint32_t)all.size();
+  rc = real(all.data(), &got);
+  if (rc != RSMI_STATUS_SUCCESS && rc != RSMI_STATUS_INSUFFICIENT_SIZE) return rc;
+  const std::vector<int> mine = container_host_pids();
+  const uint32_t cap = procs ? *num_items : 0;
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < got && i < all.size(); ++i) {
+    if (std::find(mine.begin(), mine.end(), (int)all[i].process_id) == mine.end()) continue;
+    if (k < cap) procs[k] = all[i];
+    ++k;
+  }
+  *num_items = k;
+  return procs && k > cap ? RSMI_STATUS_INSUFFICIENT_SIZE : RSMI_STATUS_SUCCESS;
 }
 
 }  // extern "C"

@@ -11,6 +11,11 @@
 // ctypes through a dlopen handle reach these via the dlsym interposer
 // (dlsym.cpp).
 //
+// Process lists (reference: NVML process-list virtualisation, §2.6 E1c) are
+// filtered to this container's processes: the host pids of its region's slots
+// as resolved by hostpid.cpp.  A process whose host pid is unknown is hidden
+// rather than guessed.
+//
 // Device index: the limit arrays are indexed by the container's visible device
 // ordinal.  Inside a pod only the allocated GPUs' render nodes exist, and
 // amdsmi / rocm-smi enumerate them in the same (KFD node) order HIP does.
@@ -113,6 +118,31 @@ __attribute__((visibility("default"))) amdsmi_status_t amdsmi_get_gpu_vram_usage
     info->vram_used = (uint32_t)(std::min<uint64_t>(hbm_used(dev), lim) >> 20);
   }
   return rc;
+}
+
+__attribute__((visibility("default"))) amdsmi_status_t amdsmi_get_gpu_process_list(
+    amdsmi_processor_handle h, uint32_t* max, amdsmi_proc_info_t* list) {
+  auto real = REAL_SMI(amdsmi_get_gpu_process_list);
+  ensure_init();
+  if (!st().enabled || !max) return real(h, max, list);
+  // Fetch the whole device list, then keep only our own processes.
+  uint32_t n = 0;
+  amdsmi_status_t rc = real(h, &n, nullptr);
+  if (rc != AMDSMI_STATUS_SUCCESS && rc != AMDSMI_STATUS_OUT_OF_RESOURCES) return rc;
+  std::vector<amdsmi_proc_info_t> all(n + 16);
+  uint32_t got = (uint32_t)all.size();
+  rc = real(h, &got, all.data());
+  if (rc != AMDSMI_STATUS_SUCCESS) return rc;
+  const std::vector<int> mine = container_host_pids();
+  uint32_t k = 0;
+  const uint32_t cap = list ? *max : 0;
+  for (uint32_t i = 0; i < got && i < all.size(); ++i) {
+    if (std::find(mine.begin(), mine.end(), (int)all[i].pid) == mine.end()) continue;
+    if (k < cap) list[k] = all[i];
+    ++k;
+  }
+  *max = k;
+  return AMDSMI_STATUS_SUCCESS;
 }
 
 __attribute__((visibility("default"))) amdsmi_status_t amdsmi_get_gpu_vram_info(

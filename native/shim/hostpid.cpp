@@ -224,6 +224,19 @@ void hostpid_publish() {
   __atomic_store_n(&sl->host_pid_src, src, __ATOMIC_RELEASE);
 }
 
+std::vector<int> container_host_pids() {
+  std::vector<int> out;
+  State& s = st();
+  if (!s.region) return out;
+  for (int i = 0; i < VGPU_MAX_PROCS; ++i) {
+    const vgpu_proc_slot_t& sl = s.region->procs[i];
+    if (__atomic_load_n(&sl.status, __ATOMIC_ACQUIRE) == VGPU_PROC_FREE) continue;
+    if (__atomic_load_n(&sl.host_pid_src, __ATOMIC_ACQUIRE) == VGPU_HOSTPID_UNVERIFIED) continue;
+    out.push_back(sl.host_pid);
+  }
+  return out;
+}
+
 void hostpid_after_fork() {
   g_phase.store(0);
   g_host_pid.store(0);

@@ -12,6 +12,7 @@
 #include <mutex>
 #include <shared_mutex>
 #include <unordered_map>
+#include <vector>
 
 #include <hip/hip_runtime_api.h>
 #include <hsa/hsa.h>
@@ -127,6 +128,9 @@ int hostpid_resolved(int* src);           // KFD-diff result, 0 = none yet
 int self_host_pid(int* src);              // best current answer + VGPU_HOSTPID_* source
 void hostpid_publish();                   // write it into this process's slot
 void hostpid_after_fork();
+// Host pids of this container's live processes that are known for sure
+// (KFD diff, monitor or host namespace); used to filter smi process lists.
+std::vector<int> container_host_pids();
 
 // HSA API table mode (HSA_TOOLS_LIB OnLoad took over the hsa_* hooks).
 bool hsa_table_mode();

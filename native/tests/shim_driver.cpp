@@ -417,6 +417,14 @@ int main(int argc, char** argv) {
       printf("smi_total=%llu\nsmi_used=%llu\nsmi_gtt_total=%llu\nsmi_vram_total_mb=%u\nsmi_vram_used_mb=%u\n",
              (unsigned long long)t, (unsigned long long)u, (unsigned long long)g, vu.vram_total,
              vu.vram_used);
+      auto plist = (amdsmi_status_t(*)(amdsmi_processor_handle, uint32_t*, amdsmi_proc_info_t*))dlsym(
+          h, "amdsmi_get_gpu_process_list");
+      amdsmi_proc_info_t pl[16];
+      uint32_t pn = 16;
+      plist(ph[dev], &pn, pl);
+      printf("smi_procs=");
+      for (uint32_t i = 0; i < pn; ++i) printf("%s%u", i ? "," : "", (unsigned)pl[i].pid);
+      printf("\n");
     }
     void* r = dlopen("librocm_smi64.so.1", RTLD_NOW);
     if (r) {
@@ -426,6 +434,14 @@ int main(int argc, char** argv) {
       rt((uint32_t)dev, RSMI_MEM_TYPE_VRAM, &t);
       ru((uint32_t)dev, RSMI_MEM_TYPE_VRAM, &u);
       printf("rsmi_total=%llu\nrsmi_used=%llu\n", (unsigned long long)t, (unsigned long long)u);
+      auto rp = (rsmi_status_t(*)(rsmi_process_info_t*, uint32_t*))dlsym(r, "rsmi_compute_process_info_get");
+      rsmi_process_info_t rl[16];
+      uint32_t rn = 16;
+      if (rp && rp(rl, &rn) == RSMI_STATUS_SUCCESS) {
+        printf("rsmi_procs=");
+        for (uint32_t i = 0; i < rn; ++i) printf("%s%u", i ? "," : "", (unsigned)rl[i].process_id);
+        printf("\n");
+      }
     }
     // RTLD_NEXT keeps its caller-relative meaning through the interposer.
     printf("next_ok=%d\n", dlsym(RTLD_NEXT, "getpid") == dlsym(RTLD_DEFAULT, "getpid") ? 1 : 0);

@@ -146,3 +146,25 @@ def test_graph_launch_charged_by_kernel_nodes(native_build, tmp_path):
     wg = [e["a"] for e in ev if e["type"] == "launch"]
     # 2 kernel nodes (100x2, 300x2) + child (50) = 850 per launch; e1 x3, e2 x1, destroyed e1 x1
     assert wg == [850, 850, 850, 850, 7]
+
+
+def test_smi_process_lists_show_only_the_container(native_build, tmp_path):
+    """E1c process-list virtualisation: amd-smi / rocm-smi inside a pod list only
+    the pod's own processes (host pids resolved by the KFD diff)."""
+    from test_shim_native import _kfd_env
+    env = _kfd_env(tmp_path, 777100)
+    f = tmp_path / "smi.json"
+    f.write_text(json.dumps({"gpus": [{"uuid": "GPU-0", "processes": [
+        {"pid": 4242, "vram": GiB}, {"pid": 777100, "vram": GiB}, {"pid": 5151, "vram": GiB}]}]}))
+    env.update({"VGPU_FAKE_AMDSMI_JSON": str(f), "VGPU_FAKE_RSMI_PIDS": "4242,777100,5151"})
+    o = run("smi", env=env)
+    assert o["smi_procs"] == "777100"
+    assert o["rsmi_procs"] == "777100"
+
+
+def test_smi_process_lists_pass_through_without_control(native_build, tmp_path):
+    f = tmp_path / "smi.json"
+    f.write_text(json.dumps({"gpus": [{"uuid": "GPU-0", "processes": [{"pid": 4242}, {"pid": 5151}]}]}))
+    o = run("smi", env={"VGPU_FAKE_AMDSMI_JSON": str(f), "VGPU_FAKE_RSMI_PIDS": "4242,5151",
+                        "VGPU_DISABLE_CONTROL": "true"})
+    assert o["smi_procs"] == "4242,5151" and o["rsmi_procs"] == "4242,5151"

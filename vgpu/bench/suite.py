@@ -28,6 +28,8 @@ SCENARIOS = {
     "vgpu-cu25": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000"],
     "vgpu-cu25-temporal": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "temporal"],
     "vgpu-cu25-mask": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "mask"],
+    "vgpu-cu25-temporal-q0": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "temporal",
+                              "--hw-queues", "0"],
 }
 
 
