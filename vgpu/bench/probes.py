@@ -212,11 +212,30 @@ def arrays(cap_mib: int = 8192) -> dict:
     return res
 
 
+def progress(seconds: int = 10, blocks: int = 256, iters: int = 2000) -> dict:
+    """Launch small busy kernels back to back for `seconds`, printing
+    `PROGRESS <launches> <t>` lines (priority-feedback tests watch them)."""
+    import torch
+    from vgpu.ops import kernels as K
+    torch.cuda.init()
+    t0 = time.time()
+    n = 0
+    while time.time() - t0 < seconds:
+        K.busy(blocks, iters)
+        n += 1
+        if n % 8 == 0:
+            torch.cuda.synchronize()
+            print(f"PROGRESS {n} {time.time():.3f}", flush=True)
+    torch.cuda.synchronize()
+    return {"launches": n}
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     cmd = argv.pop(0) if argv else "census"
     nums = [int(a) for a in argv]
-    out = {"census": census, "busy": busy, "cap": cap, "smi": smi, "graph": graph, "arrays": arrays}[cmd](*nums)
+    out = {"census": census, "busy": busy, "cap": cap, "smi": smi, "graph": graph, "arrays": arrays,
+           "progress": progress}[cmd](*nums)
     out["shim"] = shim_stats()
     print("PROBE " + json.dumps(out), flush=True)
     return 0
