@@ -82,6 +82,16 @@ def test_maxpool(C, kpad):
     torch.testing.assert_close(C.maxpool(x, *kpad).float(), C.maxpool_ref(x, *kpad), atol=0, rtol=0)
 
 
+@pytest.mark.parametrize("shape", [(2, 64, 112, 112), (1, 64, 173, 173)])
+def test_maxpool_stem_shape(C, shape):
+    """The ResNet stem pooling shape: a row (OW x C = 56 x 64 = 3 584 values)
+    is far wider than the kernel's 256 threads, so the strided row loop and
+    the mix of the K=3 fast path and the edge path inside one row run
+    (ADVICE r1).  Bit-exact against the reference."""
+    x = _t(shape, 17)
+    torch.testing.assert_close(C.maxpool(x, 3, 2, 1).float(), C.maxpool_ref(x, 3, 2, 1), atol=0, rtol=0)
+
+
 def test_scale_shift_relu_mean(C):
     x = _t((3, 2048, 5, 7), 8)
     s, b = _f((2048,), 9, 0.5, 1.5), _f((2048,), 10)
