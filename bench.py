@@ -137,6 +137,15 @@ def main(argv=None) -> int:
             if p.proc.poll() is None:
                 p.proc.kill()
 
+    # Where every rank's pods ran (device, vGPU uuid, shared region): gathered
+    # to rank 0 so a multi-GPU run shows its placement and region isolation.
+    placement = [{"rank": rank, "local_rank": local_rank, "device": device,
+                  "uuids": [p.env.get("VGPU_DEVICE_UUID_0", "") for p in pods],
+                  "regions": [p.region for p in pods], "shares": [p.share for p in pods]}]
+    if pg:
+        gathered = [None] * world
+        pg.all_gather_object(gathered, placement[0])
+        placement = gathered
     samples = sum(p.done["samples"] for p in pods)
     ms_step = 1e3 * wall / args.steps
     cap = []
@@ -196,6 +205,7 @@ def main(argv=None) -> int:
             "per_pod_cu_mask_bits": [p.mask_bits for p in pods],
             "per_pod_share": [p.share for p in pods],
             "vram_cap": cap,
+            "placement": placement,
         }
         print(json.dumps(res), flush=True)
     if pg:

@@ -42,3 +42,27 @@ def test_bench_two_ranks_gloo_cpu():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 50 * 2 * 2
     assert d["scaling"] == "weak" and d["ms_per_step"] > 0
+
+
+def test_bench_eight_ranks_gloo_cpu_placement():
+    """Rehearsal of the driver's 8-GPU run on CPU: one rank per GPU (gloo),
+    each rank's pod admitted through the control plane onto its own device,
+    distinct shared regions (no cross-rank accounting), one JSON line."""
+    port = _free_port()
+    env = dict(os.environ)
+    env["HIP_VISIBLE_DEVICES"] = ",".join(str(i) for i in range(8))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "8",
+                        "--steps", "2", "--warmup", "1", "--pods", "1", "--cpu-smoke"],
+                       cwd=REPO, capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8
+    pl = sorted(d["placement"], key=lambda x: x["rank"])
+    assert [x["rank"] for x in pl] == list(range(8))
+    assert [x["device"] for x in pl] == [str(i) for i in range(8)]
+    assert [x["uuids"] for x in pl] == [[f"GPU-bench-{i}"] for i in range(8)]
+    regions = [reg for x in pl for reg in x["regions"]]
+    assert len(set(regions)) == 8 and all(regions)
