@@ -66,16 +66,16 @@ acc_dev = Access(Loc(DEV, 0), 3)
 
 def verify(ptr, seed):
     err = torch.zeros(1, dtype=torch.int64, device="cuda")
-    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    K.vgpu_verify_pattern(ctypes.c_void_p(ptr), ctypes.c_uint64(size), ctypes.c_uint64(seed),
-                          ctypes.c_void_p(err.data_ptr()), s)
+    s = torch.cuda.current_stream().cuda_stream
+    K.vgpu_verify_pattern(ptr, size, seed,
+                          err.data_ptr(), s)
     torch.cuda.synchronize()
     return int(err.item())
 
 
 def fill(ptr, seed):
-    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    K.vgpu_fill_pattern(ctypes.c_void_p(ptr), ctypes.c_uint64(size), ctypes.c_uint64(seed), s)
+    s = torch.cuda.current_stream().cuda_stream
+    K.vgpu_fill_pattern(ptr, size, seed, s)
     torch.cuda.synchronize()
 
 

@@ -422,3 +422,28 @@ def test_health_uncorrectable_ecc_then_reset_recovers(cluster):
     while any(d.health == api.UNHEALTHY for d in upd.devices):
         upd = next(stream)
     stream.cancel()
+
+
+def test_partition_mode_mismatch_is_unhealthy_until_restored():
+    """--partition-mode pins the expected compute partition: a device found in
+    another mode is advertised unhealthy, and healthy again once it is back."""
+    from vgpu.config import DevicePluginConfig
+    from vgpu.deviceplugin.discovery import StaticBackend, mi355x_node
+    from vgpu.deviceplugin.server import VGPUDevicePlugin
+    devs = mi355x_node(2)
+    devs[1].compute_partition = "CPX"
+    backend = StaticBackend(devs)
+    cfg = DevicePluginConfig(node_name="n1", partition_mode="SPX", host_lib_dir="/tmp/vgpu-pm-test")
+    plugin = VGPUDevicePlugin(cfg, backend, None, "n1")
+    assert plugin.health == {devs[0].uuid: True, devs[1].uuid: False}
+    plugin.health_step(1)
+    assert not plugin.health[devs[1].uuid]
+    backend._devs[1].compute_partition = "SPX"
+    plugin.health_step(1)
+    assert plugin.health[devs[1].uuid]
+    backend._devs[0].compute_partition = "DPX"
+    plugin.health_step(1)
+    assert not plugin.health[devs[0].uuid] and plugin.health[devs[1].uuid]
+    # no expectation configured: any mode is fine
+    cfg2 = DevicePluginConfig(node_name="n1", host_lib_dir="/tmp/vgpu-pm-test")
+    assert all(VGPUDevicePlugin(cfg2, backend, None, "n1").health.values())

@@ -4,6 +4,7 @@ reference's comparison (README.md:234-257):
 
   exclusive          — one pod, whole GPU, no enforcement library
   vgpu               — 2 pods × gpucores=50, gpumem=144000 (BASELINE.json config 2)
+  vgpu-temporal      — the same 2 pods in the GPU's temporal pool (no CU masks)
   vgpu-cu25          — 4 pods × gpucores=25 (BASELINE.json config 3), device-plugin
                        default share policy (hybrid: 2 CU masks + a temporal pool)
   vgpu-cu25-temporal — the same 4 pods, all under the GPU-time limiter
@@ -25,6 +26,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 SCENARIOS = {
     "exclusive": ["--pods", "1", "--no-shim", "--gpucores", "100", "--gpumem", "0"],
     "vgpu": ["--pods", "2", "--gpucores", "50", "--gpumem", "144000"],
+    "vgpu-temporal": ["--pods", "2", "--gpucores", "50", "--gpumem", "144000", "--cu-share", "temporal"],
     "vgpu-cu25": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000"],
     "vgpu-cu25-temporal": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "temporal"],
     "vgpu-cu25-mask": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "mask"],

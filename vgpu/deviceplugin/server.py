@@ -60,7 +60,12 @@ class VGPUDevicePlugin:
         self.socket_path = os.path.join(cfg.socket_dir, socket_name)
         self.devices = backend.devices()
         self.by_uuid = {d.uuid: d for d in self.devices}
-        self.health: dict[str, bool] = {d.uuid: d.health for d in self.devices}
+        self.health: dict[str, bool] = {d.uuid: d.health and not self._partition_mismatch(d)
+                                        for d in self.devices}
+        for d in self.devices:
+            if self._partition_mismatch(d):
+                log.warning("device %s is in compute partition %s, expected %s: advertised unhealthy",
+                            d.uuid, d.compute_partition, cfg.partition_mode)
         self._ecc_baseline: dict[str, int] = {}   # uncorrectable ECC count at the last healthy point
         self.vm_faults: dict[str, int] = {}
         self.thermal_events: dict[str, int] = {}
@@ -85,6 +90,15 @@ class VGPUDevicePlugin:
                 dv.topology.nodes.add(ID=max(d.numa, 0))
                 out.append(dv)
         return out
+
+    def _partition_mismatch(self, d) -> bool:
+        """--partition-mode pins the compute partition (SPX/DPX/QPX/CPX) this node is
+        expected to run in; a device found in another mode (re-partitioned under a
+        running plugin, or a node prepared with the wrong amd-smi profile) would
+        hand out vGPUs sized for the wrong CU/HBM share, so it is advertised
+        unhealthy until it is back in the expected mode."""
+        want = (self.cfg.partition_mode or "").upper()
+        return bool(want) and (d.compute_partition or "SPX").upper() != want
 
     def set_health(self, uuid: str, healthy: bool, reason: str = "") -> None:
         with self._lock:
@@ -265,7 +279,8 @@ class VGPUDevicePlugin:
                 self.set_health(uuid, False, f"GPU reset: {msg}")
             elif typ == EVT_POST_RESET:
                 self._ecc_baseline.pop(uuid, None)  # counters restart with the device
-                self.set_health(uuid, True, f"GPU reset done: {msg}")
+                if not self._partition_mismatch(self.devices[dev]):
+                    self.set_health(uuid, True, f"GPU reset done: {msg}")
             elif typ == EVT_VMFAULT:
                 self.vm_faults[uuid] = self.vm_faults.get(uuid, 0) + 1
                 log.warning("device %s: VM fault (%s); device stays healthy", uuid, msg)
@@ -286,6 +301,14 @@ class VGPUDevicePlugin:
                 self.set_health(d.uuid, False, "device disappeared")
             elif not present[d.uuid].health:
                 self.set_health(d.uuid, False, "driver reports unhealthy")
+            elif self.cfg.partition_mode:
+                pd = present[d.uuid]
+                was_bad, d.compute_partition = self._partition_mismatch(d), pd.compute_partition
+                if self._partition_mismatch(d):
+                    self.set_health(d.uuid, False, f"compute partition {d.compute_partition}, "
+                                    f"expected {self.cfg.partition_mode}")
+                elif was_bad:
+                    self.set_health(d.uuid, True, f"compute partition {d.compute_partition} restored")
 
     def _health_loop(self) -> None:
         while not self._stop.is_set():
