@@ -26,6 +26,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <map>
 #include <mutex>
@@ -340,12 +341,41 @@ hipError_t hipMallocAsync(void** p, size_t size, hipStream_t) { return dev_alloc
 hipError_t hipMallocFromPoolAsync(void** p, size_t size, hipMemPool_t, hipStream_t) {
   return dev_alloc(p, size, tl_dev);
 }
-hipError_t hipMallocManaged(void** p, size_t size, unsigned int) { return dev_alloc(p, size, tl_dev); }
+// Managed (KFD SVM) ranges start host-resident and take no VRAM until the
+// fake HSA's hsa_amd_svm_prefetch_async moves them (fake_hip_svm_move).
+struct Managed {
+  int dev;
+  uint64_t size;
+  uint64_t gpu_bytes;
+};
+std::map<uintptr_t, Managed> g_managed;
+hipError_t hipMallocManaged(void** p, size_t size, unsigned int) {
+  std::lock_guard<std::mutex> g(g_mu);
+  init_locked();
+  uintptr_t a = g_next | (1ull << 45);
+  g_next += ((size + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1)) + (2u << 20);
+  g_managed[a] = Managed{tl_dev, size, 0};
+  *p = (void*)a;
+  return hipSuccess;
+}
+hipError_t hipMemAdvise(const void*, size_t, hipMemoryAdvise, int) { return hipSuccess; }
+hipError_t hipDeviceGetPCIBusId(char*, int, int) { return hipErrorNotSupported; }  // no sysfs behind a fake
 hipError_t hipMallocPitch(void** p, size_t* pitch, size_t w, size_t h) {
   *pitch = ((w + 511) / 512) * 512;
   return dev_alloc(p, *pitch * h, tl_dev);
 }
-hipError_t hipFree(void* p) { return dev_free(p); }
+hipError_t hipFree(void* p) {
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    auto it = g_managed.find((uintptr_t)p);
+    if (it != g_managed.end()) {
+      g_devs[it->second.dev].used -= it->second.gpu_bytes;
+      g_managed.erase(it);
+      return hipSuccess;
+    }
+  }
+  return dev_free(p);
+}
 hipError_t hipFreeAsync(void* p, hipStream_t) { return dev_free(p); }
 
 hipError_t hipHostMalloc(void** p, size_t size, unsigned int) {
@@ -371,7 +401,11 @@ hipError_t hipMemGetInfo(size_t* f, size_t* t) {
   std::lock_guard<std::mutex> g(g_mu);
   init_locked();
   Dev& d = g_devs[tl_dev];
-  *f = d.total - d.used;
+  // Like ROCm: VRAM that SVM migrations took is not subtracted.
+  uint64_t svm = 0;
+  for (auto& m : g_managed)
+    if (m.second.dev == tl_dev) svm += m.second.gpu_bytes;
+  *f = d.total - d.used + svm;
   *t = d.total;
   return hipSuccess;
 }
@@ -517,6 +551,33 @@ uint64_t fake_hip_launch_blocks() { return g_launch_blocks.load(); }
 uint64_t fake_hip_physical_used(int dev) {
   std::lock_guard<std::mutex> g(g_mu);
   return dev < (int)g_devs.size() ? g_devs[dev].used : 0;
+}
+// KFD SVM migration of [p, p+n) of a managed range: to HBM only if it fits
+// (KFD leaves pages in system memory otherwise, and still reports success).
+int fake_hip_svm_move(const void* p, uint64_t n, int to_gpu) {
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_managed.upper_bound((uintptr_t)p);
+  if (it == g_managed.begin()) return -1;
+  --it;
+  Managed& m = it->second;
+  if ((uintptr_t)p >= it->first + m.size) return -1;
+  Dev& d = g_devs[m.dev];
+  if (to_gpu) {
+    uint64_t add = std::min<uint64_t>(n, m.size - m.gpu_bytes);
+    if (d.used + add > d.total) return 0;
+    m.gpu_bytes += add;
+    d.used += add;
+  } else {
+    uint64_t sub = std::min<uint64_t>(n, m.gpu_bytes);
+    m.gpu_bytes -= sub;
+    d.used -= sub;
+  }
+  return 1;
+}
+uint64_t fake_hip_managed_gpu_bytes(const void* p) {
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_managed.find((uintptr_t)p);
+  return it == g_managed.end() ? 0 : it->second.gpu_bytes;
 }
 
 }  // extern "C"

@@ -224,6 +224,34 @@ hsa_status_t hsa_amd_memory_pool_free(void* ptr) {
   return g_ext.hsa_amd_memory_pool_free_fn(ptr);
 }
 
+// Signals: a heap word; every fake asynchronous operation completes before it returns.
+hsa_status_t hsa_signal_create(hsa_signal_value_t initial, uint32_t, const hsa_agent_t*, hsa_signal_t* sig) {
+  sig->handle = (uint64_t)(uintptr_t)new int64_t(initial);
+  return HSA_STATUS_SUCCESS;
+}
+hsa_status_t hsa_signal_destroy(hsa_signal_t sig) {
+  delete (int64_t*)(uintptr_t)sig.handle;
+  return HSA_STATUS_SUCCESS;
+}
+hsa_signal_value_t hsa_signal_wait_scacquire(hsa_signal_t sig, hsa_signal_condition_t, hsa_signal_value_t,
+                                             uint64_t, hsa_wait_state_t) {
+  return *(int64_t*)(uintptr_t)sig.handle;
+}
+// KFD SVM: attributes are accepted; a prefetch moves the fake HIP's managed
+// range bookkeeping (VRAM use) at VGPU_FAKE_SVM_GBPS (default: instantly).
+hsa_status_t hsa_amd_svm_attributes_set(void*, size_t, hsa_amd_svm_attribute_pair_t*, size_t) {
+  return HSA_STATUS_SUCCESS;
+}
+hsa_status_t hsa_amd_svm_prefetch_async(void* ptr, size_t size, hsa_agent_t agent, uint32_t, const hsa_signal_t*,
+                                        hsa_signal_t done) {
+  typedef int (*move_t)(const void*, uint64_t, int);
+  static move_t move = (move_t)dlsym(RTLD_DEFAULT, "fake_hip_svm_move");
+  if (!move || move(ptr, size, agent.handle >= 100 ? 1 : 0) < 0) return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  if (int gbps = env_int("VGPU_FAKE_SVM_GBPS", 0)) usleep((useconds_t)(size / (gbps * 1000.0)));
+  if (done.handle) --*(int64_t*)(uintptr_t)done.handle;
+  return HSA_STATUS_SUCCESS;
+}
+
 // ---- test introspection ----
 uint64_t fake_hsa_pool_used(int dev) {
   std::lock_guard<std::mutex> g(g_mu);

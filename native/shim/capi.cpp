@@ -148,6 +148,13 @@ __attribute__((visibility("default"))) void vgpu_self_add_swap(int dev, uint64_t
   __atomic_fetch_add(&sl->used[dev].swap_out_bytes, out_bytes, __ATOMIC_RELAXED);
 }
 
+// Virtual device memory pager counters: bytes promoted / demoted, migrations,
+// bytes of spilled ranges now resident in HBM, spilled ranges alive.
+__attribute__((visibility("default"))) void vgpu_self_vmem_stats(uint64_t out[5]) {
+  ensure_init();
+  vmem_stats(&out[0], &out[1], &out[2], &out[3], &out[4]);
+}
+
 __attribute__((visibility("default"))) uint64_t vgpu_self_host_bytes(int dev) {
   ensure_init();
   vgpu_proc_slot_t* sl = my_slot();

@@ -234,6 +234,32 @@ int cumask_device_physical_cus(int dev) {
   return a ? (int)a->cus : -1;
 }
 
+bool hsa_gpu_agent(int dev, hsa_agent_t* out) {
+  std::lock_guard<std::mutex> g(g_mu);
+  ensure_agents_locked();
+  AgentInfo* a = agent_for_hip_index(dev);
+  if (!a) return false;
+  *out = a->agent;
+  return true;
+}
+
+bool hsa_cpu_agent(hsa_agent_t* out) {
+  static hsa_agent_t cpu{0};
+  static std::once_flag once;
+  std::call_once(once, [] {
+    REAL_HSA(hsa_iterate_agents)([](hsa_agent_t a, void* d) {
+      hsa_device_type_t t;
+      if (REAL_HSA(hsa_agent_get_info)(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+        *(hsa_agent_t*)d = a;
+        return HSA_STATUS_INFO_BREAK;
+      }
+      return HSA_STATUS_SUCCESS;
+    }, &cpu);
+  });
+  *out = cpu;
+  return cpu.handle != 0;
+}
+
 uint32_t cumask_driver_uid(int dev) {
   std::lock_guard<std::mutex> g(g_mu);
   AgentInfo* a = agent_for_hip_index(dev);

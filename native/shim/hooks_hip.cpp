@@ -94,19 +94,31 @@ hipError_t charged_alloc(void** ptr, size_t size, int kind, F&& real_alloc) {
   int dev = cur_dev();
   charge_context(dev);
   if (!mem_reserve(dev, size, kind)) return hipErrorOutOfMemory;
-  hipError_t rc = real_alloc();
-  if (rc == hipErrorOutOfMemory && kind == kDeviceBuf && s.region && s.region->oversubscribe) {
+  const bool over = kind == kDeviceBuf && s.region && s.region->oversubscribe;
+  hipError_t rc = over && vmem_should_spill(dev, size) ? hipErrorOutOfMemory : real_alloc();
+  if (rc == hipErrorOutOfMemory && over) {
     // Virtual device memory: HBM is physically exhausted but the container's
-    // (scaled) limit still has room — back the allocation with pinned,
-    // device-mapped host memory.  The pager (vgpu/ops/pager.py) migrates hot
-    // chunks back into HBM.
+    // (scaled) limit still has room.  First give back HBM that ranges promoted
+    // by the pager hold but no longer use (vmem.cpp), then spill the new
+    // allocation to a managed range the pager promotes once it is in use
+    // (VGPU_VMEM_MIGRATE=0: pinned zero-copy host memory, never promoted).
     (void)REAL_HIP(hipGetLastError)();
+    if (vmem_make_room(dev, size) && !vmem_should_spill(dev, size)) {
+      rc = real_alloc();
+      if (rc == hipSuccess) {
+        ledger_add(*ptr, size, dev, kind);
+        return rc;
+      }
+      (void)REAL_HIP(hipGetLastError)();
+    }
     mem_unreserve(dev, size, kind);
     mem_reserve(dev, size, kHostSpill);
-    rc = REAL_HIP(hipHostMalloc)(ptr, size, hipHostMallocDefault);
+    rc = vmem_enabled() ? vmem_alloc_overflow(ptr, size, dev)
+                        : REAL_HIP(hipHostMalloc)(ptr, size, hipHostMallocDefault);
     if (rc == hipSuccess) {
       ledger_add(*ptr, size, dev, kHostSpill);
-      VLOG_INFO("device %d: %zu bytes oversubscribed to host memory at %p", dev, size, *ptr);
+      VLOG_INFO("device %d: %zu bytes oversubscribed to host memory at %p%s", dev, size, *ptr,
+                vmem_enabled() ? " (managed, migrates on use)" : "");
       return rc;
     }
     mem_unreserve(dev, size, kHostSpill);
@@ -187,10 +199,17 @@ __attribute__((visibility("default"))) hipError_t hipMallocPitch(void** ptr, siz
   return rc;
 }
 
+// Spilled allocations: a managed range (vmem.cpp) is freed by hipFree, a
+// zero-copy one by hipHostFree.
+static hipError_t free_spilled(void* ptr) {
+  if (vmem_release(ptr)) return REAL_HIP(hipFree)(ptr);
+  return REAL_HIP(hipHostFree)(ptr);
+}
+
 __attribute__((visibility("default"))) hipError_t hipFree(void* ptr) {
   ensure_init();
   Alloc a;
-  if (uncharge(ptr, &a) && a.kind == kHostSpill) return REAL_HIP(hipHostFree)(ptr);
+  if (uncharge(ptr, &a) && a.kind == kHostSpill) return free_spilled(ptr);
   return REAL_HIP(hipFree)(ptr);
 }
 
@@ -199,7 +218,7 @@ __attribute__((visibility("default"))) hipError_t hipFreeAsync(void* ptr, hipStr
   Alloc a;
   if (uncharge(ptr, &a) && a.kind == kHostSpill) {
     (void)REAL_HIP(hipStreamSynchronize)(stream);
-    return REAL_HIP(hipHostFree)(ptr);
+    return free_spilled(ptr);
   }
   return REAL_HIP(hipFreeAsync)(ptr, stream);
 }
@@ -296,6 +315,7 @@ __attribute__((visibility("default"))) hipError_t hipLaunchKernel(const void* f,
   ensure_init();
   const int dev = cur_dev();
   const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
+  vmem_scan_args(args);
   hipError_t rc = REAL_HIP(hipLaunchKernel)(f, grid, block, args, shmem, stream);
   if (track && rc == hipSuccess) limiter_track(dev, stream);
   return rc;
@@ -309,6 +329,7 @@ __attribute__((visibility("default"))) hipError_t hipExtLaunchKernel(const void*
   ensure_init();
   const int dev = cur_dev();
   const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
+  vmem_scan_args(args);
   hipError_t rc = REAL_HIP(hipExtLaunchKernel)(f, grid, block, args, shmem, stream, start, stop, flags);
   if (track && rc == hipSuccess) limiter_track(dev, stream);
   return rc;
@@ -321,6 +342,8 @@ __attribute__((visibility("default"))) hipError_t hipModuleLaunchKernel(
   ensure_init();
   const int dev = cur_dev();
   const bool track = limiter_on_launch(dev, blocks3(gx, gy, gz));
+  if (extra) vmem_scan_extra(extra);
+  else vmem_scan_args(params);
   hipError_t rc = REAL_HIP(hipModuleLaunchKernel)(f, gx, gy, gz, bx, by, bz, shmem, stream, params, extra);
   if (track && rc == hipSuccess) limiter_track(dev, stream);
   return rc;
@@ -335,6 +358,8 @@ __attribute__((visibility("default"))) hipError_t hipExtModuleLaunchKernel(
   auto nb = [](uint32_t g, uint32_t l) { return l ? (g + l - 1) / l : g; };
   const int dev = cur_dev();
   const bool track = limiter_on_launch(dev, blocks3(nb(gwx, lwx), nb(gwy, lwy), nb(gwz, lwz)));
+  if (extra) vmem_scan_extra(extra);
+  else vmem_scan_args(params);
   hipError_t rc = REAL_HIP(hipExtModuleLaunchKernel)(f, gwx, gwy, gwz, lwx, lwy, lwz, shmem, stream,
                                                      params, extra, start, stop, flags);
   if (track && rc == hipSuccess) limiter_track(dev, stream);
@@ -375,6 +400,7 @@ __attribute__((visibility("default"))) hipError_t hipLaunchCooperativeKernel(con
   if (g != hipSuccess) return g;
   const int dev = cur_dev();
   const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
+  vmem_scan_args(params);
   hipError_t rc = REAL_HIP(hipLaunchCooperativeKernel)(f, grid, block, params, shmem, stream);
   if (track && rc == hipSuccess) limiter_track(dev, stream);
   return rc;
@@ -386,6 +412,7 @@ __attribute__((visibility("default"))) hipError_t hipModuleLaunchCooperativeKern
   ensure_init();
   const int dev = cur_dev();
   const bool track = limiter_on_launch(dev, blocks3(gx, gy, gz));
+  vmem_scan_args(params);
   hipError_t rc = REAL_HIP(hipModuleLaunchCooperativeKernel)(f, gx, gy, gz, bx, by, bz, shmem, stream, params);
   if (track && rc == hipSuccess) limiter_track(dev, stream);
   return rc;
@@ -396,6 +423,7 @@ __attribute__((visibility("default"))) hipError_t hipLaunchKernelExC(const hipLa
   ensure_init();
   const int dev = cur_dev();
   const bool track = cfg && limiter_on_launch(dev, blocks3(cfg->gridDim.x, cfg->gridDim.y, cfg->gridDim.z), f);
+  vmem_scan_args(args);
   hipError_t rc = REAL_HIP(hipLaunchKernelExC)(cfg, f, args);
   if (track && rc == hipSuccess) limiter_track(dev, cfg->stream);
   return rc;

@@ -24,6 +24,7 @@ State& st() {
 
 static void on_exit_release() {
   limiter_stop();
+  vmem_stop();
   State& s = st();
   if (s.region && s.slot >= 0) {
     region_release_slot(s.region, s.slot);
@@ -64,6 +65,7 @@ static void atfork_child() {
   s.pid = getpid();
   hostpid_after_fork();
   limiter_after_fork();
+  vmem_after_fork();
   if (s.region) {
     s.slot = region_claim_slot(s.region, s.pid, self_host_pid(nullptr), s.lim.priority);
     hostpid_publish();

@@ -111,6 +111,8 @@ using hipModuleLoadDataEx = hipError_t (*)(hipModule_t*, const void*, unsigned i
 using hipModuleUnload = hipError_t (*)(hipModule_t);
 using hipIpcOpenMemHandle = hipError_t (*)(void**, hipIpcMemHandle_t, unsigned int);
 using hipIpcCloseMemHandle = hipError_t (*)(void*);
+using hipDeviceGetPCIBusId = hipError_t (*)(char*, int, int);
+using hipMemAdvise = hipError_t (*)(const void*, size_t, hipMemoryAdvise, int);
 using hipMemGetAddressRange = hipError_t (*)(hipDeviceptr_t*, size_t*, hipDeviceptr_t);
 using hipGetProcAddress = hipError_t (*)(const char*, void**, int, uint64_t,
                                          hipDriverProcAddressQueryResult*);

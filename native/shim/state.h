@@ -102,6 +102,23 @@ void limiter_track(int dev, hipStream_t stream);
 extern std::atomic<int> g_open_captures;
 extern std::shared_mutex g_capture_mu;  // writers: capture begin; readers: limiter-thread markers
 void limiter_stats(int dev, uint64_t* charged_ns, uint64_t* busy_ns);
+
+// HSA agents behind HIP device ordinals (cumask.cpp).
+bool hsa_gpu_agent(int dev, hsa_agent_t* out);
+bool hsa_cpu_agent(hsa_agent_t* out);
+
+// Transparent virtual device memory (vmem.cpp).
+bool vmem_enabled();
+bool vmem_should_spill(int dev, uint64_t size);  // physical HBM (minus a runtime reserve) cannot take `size`
+hipError_t vmem_alloc_overflow(void** ptr, size_t size, int dev);
+bool vmem_owns(void* p);
+bool vmem_release(void* p);                 // forget a range before the real free; false if not ours
+bool vmem_make_room(int dev, uint64_t need); // demote cold promoted ranges; true if `need` now fits
+void vmem_scan_args(void** args);           // HIP-Clang stub argument array
+void vmem_scan_extra(void** extra);         // HIP_LAUNCH_PARAM_BUFFER_* kernarg blob
+void vmem_stats(uint64_t* in_bytes, uint64_t* out_bytes, uint64_t* moves, uint64_t* gpu_bytes, uint64_t* ranges);
+void vmem_stop();
+void vmem_after_fork();
 void suspend_gate();
 int cu_count_masked(int dev, int physical);
 

@@ -1,0 +1,509 @@
+// Transparent virtual device memory (VGPU_OVERSUBSCRIBE=true).
+//
+// Reference: the NVIDIA libvgpu.so backs an oversubscribed pod with
+// cuMemAllocManaged (README.md:283-287,
+// pkg/device-plugin/nvidiadevice/nvinternal/plugin/server.go:348-350) and
+// leaves page migration to the UVM driver's fault handler.  MI355X runs with
+// XNACK off, so there are no recoverable GPU page faults: nothing migrates
+// unless somebody asks.  This module is that somebody.
+//
+// Measured on MI355X (native/probes/svm_probe.hip, profiles/vmem_r2.md):
+// host-located VMM handles are refused (hipMemCreate -> invalid value), so a
+// VA-stable HBM <-> host swap has exactly one vehicle, a KFD SVM range
+// (hipMallocManaged).  The GPU reads one in place from host memory at the
+// zero-copy rate (55 GB/s) and at HBM speed (5.3 TB/s) once it lives in
+// VRAM; hsa_amd_svm_prefetch_async moves it at ~6 GB/s up / ~10 GB/s down
+// (hipMemPrefetchAsync goes through a slower path: 1.3-2 GB/s), with the
+// process's queues paused by KFD during the move, so it is always safe.
+//
+// Design:
+//   * an allocation that no longer fits in physical HBM (the real allocator
+//     says out-of-memory, the container cap still has room) becomes a
+//     coarse-grained managed range that starts host-resident;
+//   * every kernel launch scans its argument blob for pointers into those
+//     ranges (the HIP-Clang stub's argument array lives in the caller's
+//     frame; module launches carry a sized kernarg buffer) and stamps the
+//     range's last-use tick — no metadata, no device-side cost, and a missed
+//     or spurious hit only costs performance, never correctness;
+//   * a pager thread promotes recently used host-resident ranges into HBM
+//     while physical HBM has room (beyond VGPU_VMEM_HEADROOM_MB), and demotes
+//     ranges it promoted earlier that went cold when a hotter one is waiting
+//     or when a new allocation needs the room;
+//   * charges never change (the cap counts HBM + host), only where they are
+//     booked: host_bytes <-> buffer/total bytes, plus swap_in/swap_out bytes
+//     and VGPU_EV_MIGRATE trace events.
+// VGPU_VMEM_MIGRATE=0 keeps the round-1 behaviour (pinned zero-copy spill).
+#include <pthread.h>
+
+#include <new>
+
+#include <algorithm>
+#include <cctype>
+#include <cstdio>
+#include <string>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <shared_mutex>
+#include <thread>
+#include <vector>
+
+#include "common.h"
+#include "real.h"
+#include "state.h"
+
+namespace vgpu {
+
+namespace {
+
+struct VRange {
+  uintptr_t base;
+  uint64_t size;
+  int dev;
+  uint64_t gpu_bytes;                      // promoted prefix [base, base + gpu_bytes)
+  std::atomic<uint64_t> last_use{0};       // pager tick of the latest launch that named it
+  std::atomic<uint32_t> uses{0};           // launches that named it (halved every second)
+  bool pager_owned_gpu = false;            // promoted by the pager (so it may demote it)
+  VRange(uintptr_t b, uint64_t s, int d) : base(b), size(s), dev(d), gpu_bytes(0) {}
+};
+
+std::shared_mutex g_tab_mu;                // guards g_tab's shape (launch hooks take it shared)
+std::vector<VRange*> g_tab;                // sorted by base
+std::atomic<int> g_count{0};
+std::mutex g_move_mu;                      // one migration or free at a time
+std::atomic<uint64_t> g_tick{1};
+std::atomic<uint64_t> g_in_bytes{0}, g_out_bytes{0}, g_moves{0};
+
+std::mutex g_thr_mu;
+std::condition_variable g_thr_cv;
+bool g_thr_run = false;          // guarded by g_thr_mu
+std::atomic<int> g_thr_alive{0};
+
+struct Knobs {
+  bool on = true;
+  uint64_t headroom = 2ull << 30;
+  int tick_ms = 50;
+  uint64_t hot_ticks = 20;   // used within the last second -> promote
+  uint64_t cold_ticks = 40;  // unused for two seconds -> may be demoted
+  uint64_t piece = 1ull << 30;
+};
+
+const Knobs& knobs() {
+  static Knobs k = [] {
+    Knobs v;
+    v.on = env_bool(env_first("VGPU_VMEM_MIGRATE"), true);
+    if (const char* e = env_first("VGPU_VMEM_HEADROOM_MB")) v.headroom = strtoull(e, nullptr, 10) << 20;
+    if (const char* e = env_first("VGPU_VMEM_TICK_MS")) v.tick_ms = std::max(1, atoi(e));
+    if (const char* e = env_first("VGPU_VMEM_HOT_MS")) v.hot_ticks = std::max<uint64_t>(1, strtoull(e, nullptr, 10) / v.tick_ms);
+    if (const char* e = env_first("VGPU_VMEM_COLD_MS"))
+      v.cold_ticks = std::max<uint64_t>(1, strtoull(e, nullptr, 10) / v.tick_ms);
+    if (const char* e = env_first("VGPU_VMEM_PIECE_MB")) v.piece = std::max<uint64_t>(2, strtoull(e, nullptr, 10)) << 20;
+    return v;
+  }();
+  return k;
+}
+
+VRange* find_locked(uintptr_t p) {
+  auto it = std::upper_bound(g_tab.begin(), g_tab.end(), p, [](uintptr_t v, const VRange* r) { return v < r->base; });
+  if (it == g_tab.begin()) return nullptr;
+  VRange* r = *(it - 1);
+  return p < r->base + r->size ? r : nullptr;
+}
+
+inline void touch_word(uintptr_t w, uint64_t tick) {
+  if (w < g_tab.front()->base || w >= g_tab.back()->base + g_tab.back()->size) return;
+  if (VRange* r = find_locked(w)) {
+    if (r->last_use.load(std::memory_order_relaxed) != tick) r->last_use.store(tick, std::memory_order_relaxed);
+    r->uses.fetch_add(1, std::memory_order_relaxed);
+  }
+}
+
+void scan_words_locked(const unsigned char* p, size_t n, uint64_t tick) {
+  for (size_t off = 0; off + sizeof(uintptr_t) <= n; off += 4) {  // kernargs are 4-byte aligned at least
+    uintptr_t w;
+    memcpy(&w, p + off, sizeof w);
+    touch_word(w, tick);
+  }
+}
+
+// Bounds of the calling thread's stack: [frame of the scanner, top of stack).
+uintptr_t stack_top() {
+  static thread_local uintptr_t top = 0;
+  if (!top) {
+    pthread_attr_t a;
+    void* lo = nullptr;
+    size_t sz = 0;
+    if (pthread_getattr_np(pthread_self(), &a) == 0) {
+      pthread_attr_getstack(&a, &lo, &sz);
+      pthread_attr_destroy(&a);
+    }
+    top = lo ? (uintptr_t)lo + sz : 1;
+  }
+  return top;
+}
+
+// ---- accounting ----------------------------------------------------------------------
+void book_move(int dev, uint64_t bytes, bool to_gpu) {
+  vgpu_proc_slot_t* sl = my_slot();
+  if (!sl || dev < 0 || dev >= VGPU_MAX_DEVICES || !bytes) return;
+  vgpu_dev_usage_t& u = sl->used[dev];
+  if (to_gpu) {
+    __atomic_fetch_sub(&u.host_bytes, bytes, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&u.buffer_bytes, bytes, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&u.total_bytes, bytes, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&u.swap_in_bytes, bytes, __ATOMIC_RELAXED);
+  } else {
+    __atomic_fetch_sub(&u.buffer_bytes, bytes, __ATOMIC_RELAXED);
+    __atomic_fetch_sub(&u.total_bytes, bytes, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&u.host_bytes, bytes, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&u.swap_out_bytes, bytes, __ATOMIC_RELAXED);
+  }
+}
+
+// ---- migration --------------------------------------------------------------------------
+bool prefetch(uintptr_t p, uint64_t n, int dev, bool to_gpu) {
+  hsa_agent_t agent;
+  if (!(to_gpu ? hsa_gpu_agent(dev, &agent) : hsa_cpu_agent(&agent))) return false;
+  hsa_signal_t sig;
+  if (REAL_HSA(hsa_signal_create)(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) return false;
+  hsa_status_t st = REAL_HSA(hsa_amd_svm_prefetch_async)((void*)p, n, agent, 0, nullptr, sig);
+  bool ok = st == HSA_STATUS_SUCCESS;
+  if (ok) {
+    hsa_signal_value_t v = REAL_HSA(hsa_signal_wait_scacquire)(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                                               HSA_WAIT_STATE_BLOCKED);
+    ok = v == 0;
+  }
+  REAL_HSA(hsa_signal_destroy)(sig);
+  if (!ok) VLOG_WARN("vmem: prefetch of %llu bytes at %p to %s failed (status %d)", (unsigned long long)n, (void*)p,
+                     to_gpu ? "HBM" : "host", (int)st);
+  return ok;
+}
+
+// Bytes of spilled ranges the pager has moved into HBM on `dev`.
+uint64_t promoted_bytes(int dev) {
+  uint64_t n = 0;
+  std::shared_lock<std::shared_mutex> g(g_tab_mu);
+  for (VRange* r : g_tab)
+    if (r->dev == dev) n += r->gpu_bytes;
+  return n;
+}
+
+// amdgpu's own VRAM counters (/sys/bus/pci/devices/<bdf>/mem_info_vram_*):
+// they count every VRAM buffer, SVM migrations included.  0 when unreadable.
+uint64_t sysfs_vram_free(int dev) {
+  static std::mutex mu;
+  static std::string dirs[VGPU_MAX_DEVICES];
+  static bool tried[VGPU_MAX_DEVICES] = {};
+  if (dev < 0 || dev >= VGPU_MAX_DEVICES) return 0;
+  std::string dir;
+  {
+    std::lock_guard<std::mutex> l(mu);
+    if (!tried[dev]) {
+      tried[dev] = true;
+      char bus[64] = {0};
+      if (REAL_HIP(hipDeviceGetPCIBusId)(bus, sizeof bus, dev) == hipSuccess) {
+        for (char* c = bus; *c; ++c) *c = (char)tolower(*c);
+        dirs[dev] = std::string("/sys/bus/pci/devices/") + bus;
+      }
+    }
+    dir = dirs[dev];
+  }
+  if (dir.empty()) return 0;
+  auto rd = [](const std::string& p) -> uint64_t {
+    FILE* f = fopen(p.c_str(), "r");
+    if (!f) return 0;
+    unsigned long long v = 0;
+    if (fscanf(f, "%llu", &v) != 1) v = 0;
+    fclose(f);
+    return v;
+  };
+  uint64_t total = rd(dir + "/mem_info_vram_total"), used = rd(dir + "/mem_info_vram_used");
+  return total > used ? total - used : (total ? 1 : 0);
+}
+
+// Physical free HBM of `dev` as the pager must see it.  hipMemGetInfo does
+// not count VRAM that KFD SVM migrations took (measured: free unchanged after
+// a 4 GiB prefetch into HBM), and a migration into a full device stalls the
+// process while KFD evicts its own buffers, so the promoted bytes are taken
+// off it and amdgpu's VRAM counters have the last word when readable.
+uint64_t hbm_free(int dev) {
+  size_t f = 0, t = 0;
+  const int cur = tl_device;
+  if (cur != dev) (void)REAL_HIP(hipSetDevice)(dev);
+  hipError_t rc = REAL_HIP(hipMemGetInfo)(&f, &t);
+  if (cur != dev && cur >= 0) (void)REAL_HIP(hipSetDevice)(cur);
+  if (rc != hipSuccess) return 0;
+  const uint64_t mine = promoted_bytes(dev);
+  uint64_t free_b = f > mine ? f - mine : 0;
+  if (uint64_t sys = sysfs_vram_free(dev)) free_b = std::min(free_b, sys);
+  return free_b;
+}
+
+// Move the whole range back to host memory.  Caller holds g_move_mu.
+bool demote_locked(VRange* r) {
+  if (!r->gpu_bytes) return true;
+  uint64_t n = r->gpu_bytes;
+  auto t0 = std::chrono::steady_clock::now();
+  if (!prefetch(r->base, n, r->dev, false)) return false;
+  uint64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+  r->gpu_bytes = 0;
+  r->pager_owned_gpu = false;
+  book_move(r->dev, n, false);
+  g_out_bytes.fetch_add(n);
+  g_moves.fetch_add(1);
+  trace_emit(VGPU_EV_MIGRATE, r->dev, n, ns << 1);
+  VLOG_INFO("vmem: demoted %llu bytes at %p in %.3f s", (unsigned long long)n, (void*)r->base, ns / 1e9);
+  return true;
+}
+
+// Promote the next piece of `r`.  Caller holds g_move_mu.  False when there is no room.
+bool promote_piece_locked(VRange* r) {
+  const Knobs& k = knobs();
+  uint64_t n = std::min<uint64_t>(k.piece, r->size - r->gpu_bytes);
+  if (!n) return false;
+  if (hbm_free(r->dev) < n + k.headroom) return false;  // make_room_locked ran first
+  auto t0 = std::chrono::steady_clock::now();
+  if (!prefetch(r->base + r->gpu_bytes, n, r->dev, true)) return false;
+  uint64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+  r->gpu_bytes += n;
+  r->pager_owned_gpu = true;
+  book_move(r->dev, n, true);
+  g_in_bytes.fetch_add(n);
+  g_moves.fetch_add(1);
+  trace_emit(VGPU_EV_MIGRATE, r->dev, n, (ns << 1) | 1);
+  VLOG_INFO("vmem: promoted %llu bytes at %p in %.3f s", (unsigned long long)n, (void*)(r->base + r->gpu_bytes - n),
+            ns / 1e9);
+  return true;
+}
+
+// Demote cold promoted ranges of `dev` (oldest first, never `keep`) until
+// `need` bytes of HBM are free beyond the headroom.  Caller holds g_move_mu.
+bool make_room_locked(int dev, uint64_t need, const VRange* keep, uint64_t newer_than) {
+  const Knobs& k = knobs();
+  if (hbm_free(dev) >= need + k.headroom) return true;
+  std::vector<VRange*> cold;
+  {
+    std::shared_lock<std::shared_mutex> g(g_tab_mu);
+    for (VRange* r : g_tab)
+      if (r != keep && r->dev == dev && r->gpu_bytes && r->last_use.load() < newer_than) cold.push_back(r);
+  }
+  std::sort(cold.begin(), cold.end(), [](VRange* a, VRange* b) { return a->last_use.load() < b->last_use.load(); });
+  for (VRange* r : cold) {
+    if (hbm_free(dev) >= need + k.headroom) break;
+    demote_locked(r);
+  }
+  return hbm_free(dev) >= need + k.headroom;
+}
+
+void pager_step() {
+  const Knobs& k = knobs();
+  const uint64_t tick = g_tick.fetch_add(1) + 1;
+  if (tick % (1000 / k.tick_ms + 1) == 0) {
+    std::shared_lock<std::shared_mutex> g(g_tab_mu);
+    for (VRange* r : g_tab) r->uses.store(r->uses.load() / 2);
+  }
+  std::vector<VRange*> hot;
+  {
+    std::shared_lock<std::shared_mutex> g(g_tab_mu);
+    for (VRange* r : g_tab)
+      if (r->gpu_bytes < r->size && r->last_use.load() + k.hot_ticks >= tick && r->last_use.load()) hot.push_back(r);
+  }
+  if (hot.empty()) return;
+  std::sort(hot.begin(), hot.end(), [](VRange* a, VRange* b) { return a->uses.load() > b->uses.load(); });
+  for (VRange* r : hot) {
+    std::lock_guard<std::mutex> m(g_move_mu);
+    {  // freed meanwhile?
+      std::shared_lock<std::shared_mutex> g(g_tab_mu);
+      if (std::find(g_tab.begin(), g_tab.end(), r) == g_tab.end()) continue;
+    }
+    const uint64_t stale = tick > k.cold_ticks ? tick - k.cold_ticks : 0;
+    while (r->gpu_bytes < r->size) {
+      uint64_t n = std::min<uint64_t>(k.piece, r->size - r->gpu_bytes);
+      if (!make_room_locked(r->dev, n, r, stale)) break;
+      if (!promote_piece_locked(r)) break;
+    }
+  }
+}
+
+void pager_main() {
+  pthread_setname_np(pthread_self(), "vgpu-vmem");
+  tl_device = -1;
+  // HIP calls from this thread must not invalidate another thread's stream capture.
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  (void)REAL_HIP(hipThreadExchangeStreamCaptureMode)(&mode);
+  const Knobs& k = knobs();
+  std::unique_lock<std::mutex> l(g_thr_mu);
+  while (g_thr_run) {
+    g_thr_cv.wait_for(l, std::chrono::milliseconds(k.tick_ms));
+    if (!g_thr_run) break;
+    l.unlock();
+    if (g_count.load() > 0) pager_step();
+    l.lock();
+  }
+  g_thr_alive.store(0);
+}
+
+void ensure_pager() {
+  std::lock_guard<std::mutex> l(g_thr_mu);
+  if (g_thr_run) return;
+  g_thr_run = true;
+  g_thr_alive.store(1);
+  std::thread(pager_main).detach();
+}
+
+}  // namespace
+
+// Oversubscribed pods spill before the device is physically full: the HIP
+// runtime and ROCr still need HBM of their own after the application's last
+// buffer (code objects loaded lazily at a kernel's first launch, scratch,
+// kernarg pools) and fail with hipErrorNoBinaryForGpu / out-of-resources
+// when it is gone.  VGPU_VMEM_RESERVE_MB (default 1024) stays free.
+bool vmem_should_spill(int dev, uint64_t size) {
+  static const uint64_t reserve = [] {
+    const char* e = env_first("VGPU_VMEM_RESERVE_MB");
+    return (e ? strtoull(e, nullptr, 10) : 1024ull) << 20;
+  }();
+  return hbm_free(dev) < size + reserve;
+}
+
+bool vmem_enabled() {
+  State& s = st();
+  return s.enabled && s.region && s.region->oversubscribe && knobs().on;
+}
+
+hipError_t vmem_alloc_overflow(void** ptr, size_t size, int dev) {
+  if (!vmem_enabled()) return hipErrorNotSupported;
+  hipError_t rc = REAL_HIP(hipMallocManaged)(ptr, size, hipMemAttachGlobal);
+  if (rc != hipSuccess) return rc;
+  // Coarse-grained: coherent at kernel boundaries like hipMalloc memory, so
+  // the GPU caches it (fine-grained managed memory bypasses them).
+  (void)REAL_HIP(hipMemAdvise)(*ptr, size, hipMemAdviseSetCoarseGrain, dev);
+  (void)REAL_HIP(hipGetLastError)();
+  auto* r = new VRange((uintptr_t)*ptr, size, dev);
+  r->last_use.store(g_tick.load());  // allocated now: in use now
+  {
+    std::unique_lock<std::shared_mutex> g(g_tab_mu);
+    g_tab.insert(std::upper_bound(g_tab.begin(), g_tab.end(), r,
+                                  [](const VRange* a, const VRange* b) { return a->base < b->base; }),
+                 r);
+    g_count.store((int)g_tab.size());
+  }
+  ensure_pager();
+  return hipSuccess;
+}
+
+bool vmem_owns(void* p) {
+  if (g_count.load(std::memory_order_relaxed) == 0) return false;
+  std::shared_lock<std::shared_mutex> g(g_tab_mu);
+  VRange* r = find_locked((uintptr_t)p);
+  return r && r->base == (uintptr_t)p;
+}
+
+bool vmem_release(void* p) {
+  if (!vmem_owns(p)) return false;
+  std::lock_guard<std::mutex> m(g_move_mu);
+  VRange* r = nullptr;
+  {
+    std::unique_lock<std::shared_mutex> g(g_tab_mu);
+    auto it = std::find_if(g_tab.begin(), g_tab.end(), [&](VRange* x) { return x->base == (uintptr_t)p; });
+    if (it == g_tab.end()) return false;
+    r = *it;
+    g_tab.erase(it);
+    g_count.store((int)g_tab.size());
+  }
+  // the ledger books the whole allocation as host bytes: book the HBM part back first
+  if (r->gpu_bytes) {
+    vgpu_proc_slot_t* sl = my_slot();
+    if (sl && r->dev >= 0 && r->dev < VGPU_MAX_DEVICES) {
+      vgpu_dev_usage_t& u = sl->used[r->dev];
+      __atomic_fetch_sub(&u.buffer_bytes, r->gpu_bytes, __ATOMIC_RELAXED);
+      __atomic_fetch_sub(&u.total_bytes, r->gpu_bytes, __ATOMIC_RELAXED);
+      __atomic_fetch_add(&u.host_bytes, r->gpu_bytes, __ATOMIC_RELAXED);
+    }
+  }
+  delete r;
+  return true;
+}
+
+bool vmem_make_room(int dev, uint64_t need) {
+  if (g_count.load(std::memory_order_relaxed) == 0) return false;
+  std::lock_guard<std::mutex> m(g_move_mu);
+  const Knobs& k = knobs();
+  const uint64_t tick = g_tick.load();
+  return make_room_locked(dev, need, nullptr, tick > k.cold_ticks ? tick - k.cold_ticks : 0);
+}
+
+void vmem_scan_args(void** args) {
+  if (g_count.load(std::memory_order_relaxed) == 0 || !args) return;
+  const uintptr_t lo = (uintptr_t)__builtin_frame_address(0);
+  const uintptr_t hi = stack_top();
+  if ((uintptr_t)args < lo || (uintptr_t)args >= hi) return;  // not a stub frame: nothing safe to read
+  uintptr_t a[64];
+  int n = 0;
+  for (int i = 0; i < 64; ++i) {
+    if ((uintptr_t)(args + i) + sizeof(void*) > hi) break;
+    uintptr_t e = (uintptr_t)args[i];
+    if (e < lo || e + sizeof(uint32_t) > hi) break;
+    a[n++] = e;
+  }
+  if (!n) return;
+  std::sort(a, a + n);
+  const uint64_t tick = g_tick.load(std::memory_order_relaxed);
+  std::shared_lock<std::shared_mutex> g(g_tab_mu);
+  if (g_tab.empty()) return;
+  for (int i = 0; i < n; ++i) {
+    uintptr_t end = i + 1 < n ? a[i + 1] : a[i] + 1024;  // the last argument: a bounded look
+    end = std::min<uintptr_t>({end, a[i] + 4096, hi});
+    if (end > a[i]) scan_words_locked((const unsigned char*)a[i], end - a[i], tick);
+  }
+}
+
+void vmem_scan_extra(void** extra) {
+  if (g_count.load(std::memory_order_relaxed) == 0 || !extra) return;
+  const void* buf = nullptr;
+  size_t n = 0;
+  for (int i = 0; i < 8 && extra[i] != HIP_LAUNCH_PARAM_END; i += 2) {
+    if (extra[i] == HIP_LAUNCH_PARAM_BUFFER_POINTER) buf = extra[i + 1];
+    else if (extra[i] == HIP_LAUNCH_PARAM_BUFFER_SIZE && extra[i + 1]) n = *(size_t*)extra[i + 1];
+  }
+  if (!buf || !n) return;
+  const uint64_t tick = g_tick.load(std::memory_order_relaxed);
+  std::shared_lock<std::shared_mutex> g(g_tab_mu);
+  if (!g_tab.empty()) scan_words_locked((const unsigned char*)buf, std::min<size_t>(n, 4096), tick);
+}
+
+void vmem_stats(uint64_t* in_bytes, uint64_t* out_bytes, uint64_t* moves, uint64_t* gpu_bytes,
+                uint64_t* ranges) {
+  *in_bytes = g_in_bytes.load();
+  *out_bytes = g_out_bytes.load();
+  *moves = g_moves.load();
+  uint64_t gb = 0;
+  std::shared_lock<std::shared_mutex> g(g_tab_mu);
+  for (VRange* r : g_tab) gb += r->gpu_bytes;
+  *gpu_bytes = gb;
+  *ranges = g_tab.size();
+}
+
+void vmem_stop() {
+  {
+    std::lock_guard<std::mutex> l(g_thr_mu);
+    if (!g_thr_run) return;
+    g_thr_run = false;
+  }
+  g_thr_cv.notify_all();
+  // let a migration in flight finish before the runtime is torn down
+  for (int i = 0; i < 500 && g_thr_alive.load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+}
+
+void vmem_after_fork() {
+  // The pager thread does not exist in the child.  Mutexes may have been held
+  // by it at fork time: re-create them.
+  new (&g_thr_mu) std::mutex();
+  new (&g_move_mu) std::mutex();
+  new (&g_tab_mu) std::shared_mutex();
+  g_thr_run = false;
+  g_thr_alive.store(0);
+}
+
+}  // namespace vgpu

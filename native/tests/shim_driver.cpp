@@ -32,6 +32,7 @@ extern "C" uint64_t fake_hip_exec_ns();
 extern "C" uint64_t fake_hip_physical_used(int dev);
 extern "C" uint64_t fake_hsa_pool_used(int dev);
 extern "C" int fake_hsa_tools_loaded();
+extern "C" uint64_t fake_hip_managed_gpu_bytes(const void* p);
 extern "C" hipGraph_t fake_hip_graph_create(const unsigned* grids, int n, unsigned child_grid);
 
 static hsa_status_t gpu_agent_cb(hsa_agent_t a, void* data) {
@@ -256,6 +257,66 @@ int main(int argc, char** argv) {
     if (used && self_region) printf("region_used_after_free=%llu\n",
                                     (unsigned long long)used(self_region(), dev));
     printf("physical_used_after_free=%llu\n", (unsigned long long)fake_hip_physical_used(dev));
+    return 0;
+  }
+
+  if (sc == "vmem") {
+    // Transparent virtual device memory on an 8 GiB fake device, 32 GiB cap:
+    // a spilled range is promoted once it is in use and HBM has room, and
+    // demoted again when it went cold and a new allocation needs HBM.
+    const size_t G = 1ull << 30;
+    auto vstats = sym<void (*)(uint64_t*)>("vgpu_self_vmem_stats");
+    auto self_region = sym<void* (*)()>("vgpu_self_region");
+    auto self_slot = sym<int (*)()>("vgpu_self_slot");
+    auto slot_u = [&]() -> vgpu_dev_usage_t& {
+      return ((vgpu_shared_region_t*)self_region())->procs[self_slot()].used[dev];
+    };
+    struct Functor {  // a PyTorch-style by-value argument that carries the pointer inside
+      int n;
+      float alpha;
+      void* data[2];
+    };
+    auto launch_with = [&](void* p, int ms) {
+      for (int t = 0; t < ms; t += 5) {
+        int n = 1 << 20;
+        Functor fn{n, 1.f, {nullptr, (char*)p + 4096}};
+        void* args[] = {&n, &fn};
+        hipLaunchKernel((const void*)0x1, dim3(64), dim3(256), args, 0, nullptr);
+        usleep(5000);
+      }
+    };
+    void *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr;
+    int ra = hipMalloc(&a, 6 * G);
+    int rb = hipMalloc(&b, 4 * G);
+    printf("alloc_a=%d\nalloc_b=%d\nb_gpu_after_alloc=%llu\nhost_after_spill=%llu\n", ra, rb,
+           (unsigned long long)fake_hip_managed_gpu_bytes(b), (unsigned long long)slot_u().host_bytes);
+    launch_with(b, 300);  // hot, but a holds the HBM
+    printf("b_gpu_while_full=%llu\n", (unsigned long long)fake_hip_managed_gpu_bytes(b));
+    hipFree(a);
+    launch_with(b, 400);  // room now: promoted
+    uint64_t v[5];
+    vstats(v);
+    printf("b_gpu_after_room=%llu\nhost_after_promote=%llu\nbuffer_after_promote=%llu\nswap_in=%llu\n"
+           "vmem_in=%llu\nphysical_used=%llu\n",
+           (unsigned long long)fake_hip_managed_gpu_bytes(b), (unsigned long long)slot_u().host_bytes,
+           (unsigned long long)slot_u().buffer_bytes, (unsigned long long)slot_u().swap_in_bytes,
+           (unsigned long long)v[0], (unsigned long long)fake_hip_physical_used(dev));
+    usleep(400000);  // b goes cold
+    int rc_ = hipMalloc(&c, 3 * G);
+    int rd = hipMalloc(&d, 2 * G);  // needs b's HBM back
+    vstats(v);
+    printf("alloc_c=%d\nalloc_d=%d\nb_gpu_after_demote=%llu\nhost_after_demote=%llu\nswap_out=%llu\n"
+           "vmem_out=%llu\nvmem_ranges=%llu\n",
+           rc_, rd, (unsigned long long)fake_hip_managed_gpu_bytes(b), (unsigned long long)slot_u().host_bytes,
+           (unsigned long long)slot_u().swap_out_bytes, (unsigned long long)v[1], (unsigned long long)v[4]);
+    hipFree(b);
+    hipFree(c);
+    hipFree(d);
+    vstats(v);
+    printf("final_total=%llu\nfinal_host=%llu\nfinal_buffer=%llu\nfinal_ranges=%llu\nfinal_physical=%llu\n",
+           (unsigned long long)slot_u().total_bytes, (unsigned long long)slot_u().host_bytes,
+           (unsigned long long)slot_u().buffer_bytes, (unsigned long long)v[4],
+           (unsigned long long)fake_hip_physical_used(dev));
     return 0;
   }
 

@@ -175,3 +175,19 @@ def test_array_3d_module_allocations_capped(gpu_build):
     assert u["buffer"] >= (6 << 30) + ((256 << 20) if res["array_a"] == 0 else 0), u
     assert u["context"] + u["module"] + u["buffer"] == u["total"], u
     assert res["usage_after_free"]["module"] == 0 and res["usage_after_free"]["buffer"] < u["buffer"]
+
+
+def test_vmem_spill_promoted_transparently(gpu_build):
+    """an allocation that spilled past physical HBM is a
+    managed range; once HBM frees up, the pager moves it into HBM on its own
+    (the probe only launches kernels on it) — data intact, read bandwidth from
+    the zero-copy rate to HBM rate, charges balanced."""
+    GiB_ = 1 << 30
+    res = probe(["vmem", 4, 30], {"VGPU_DEVICE_MEMORY_LIMIT_0": "400000m", "VGPU_OVERSUBSCRIBE": "true"},
+                timeout=300)
+    assert res["host_bytes"] == 4 * GiB_ and res["after_spill"]["ranges"] == 1
+    assert res["in_place_errors"] == 0 and res["promoted_errors"] == 0
+    assert res["after_room"]["spill_in_hbm"] == 4 * GiB_ and res["after_room"]["swap_in"] >= 4 * GiB_
+    assert res["host_bytes_after"] == 0
+    assert res["in_place_GBps"] < 200 and res["promoted_GBps"] > 1000, res
+    assert res["final"]["ranges"] == 0

@@ -125,12 +125,47 @@ def test_get_proc_address_returns_hook(native_build):
 
 
 def test_oversubscribe_spills_to_host(native_build):
-    # physical 8 GiB, virtual cap 20 GiB: 8 chunks in HBM, the rest in host memory
+    # physical 8 GiB, virtual cap 20 GiB: 7 chunks in HBM (1 GiB stays free for
+    # the runtime's own allocations, VGPU_VMEM_RESERVE_MB), the rest in host memory
     o = run("spill", GiB, 16, env={"VGPU_FAKE_MEM": str(8 * GiB), "VGPU_DEVICE_MEMORY_LIMIT_0": "20g",
                                    "VGPU_OVERSUBSCRIBE": "true"})
     assert o["allocated"] == "16" and o["failed"] == "0"
-    assert int(o["physical_used"]) == 8 * GiB
-    assert int(o["slot_host_bytes"]) == 8 * GiB
+    assert int(o["physical_used"]) == 7 * GiB
+    assert int(o["slot_host_bytes"]) == 9 * GiB
+
+
+VMEM_ENV = {"VGPU_FAKE_MEM": str(8 * GiB), "VGPU_DEVICE_MEMORY_LIMIT_0": "32g", "VGPU_OVERSUBSCRIBE": "true",
+            "VGPU_VMEM_HEADROOM_MB": "0", "VGPU_VMEM_TICK_MS": "10", "VGPU_VMEM_HOT_MS": "100",
+            "VGPU_VMEM_COLD_MS": "200", "VGPU_VMEM_RESERVE_MB": "0"}
+
+
+def test_vmem_promotes_used_spill_and_demotes_it_when_cold(native_build):
+    """Transparent virtual device memory: a spilled
+    allocation is a managed range; launches that pass a pointer into it (here
+    inside a by-value struct argument) make the pager move it into HBM once HBM
+    has room, and a later allocation that needs HBM demotes it after it went
+    cold.  Charges stay balanced at every step."""
+    o = run("vmem", env=VMEM_ENV)
+    assert o["alloc_a"] == "0" and o["alloc_b"] == "0"
+    assert o["b_gpu_after_alloc"] == "0" and int(o["host_after_spill"]) == 4 * GiB
+    assert int(o["b_gpu_while_full"]) == 2 * GiB  # the 2 GiB of HBM that 6 GiB of plain buffers left
+    assert int(o["b_gpu_after_room"]) == 4 * GiB
+    assert int(o["host_after_promote"]) == 0 and int(o["buffer_after_promote"]) == 4 * GiB
+    assert int(o["swap_in"]) == 4 * GiB == int(o["vmem_in"])
+    assert int(o["physical_used"]) == 4 * GiB
+    assert o["alloc_c"] == "0" and o["alloc_d"] == "0"
+    assert o["b_gpu_after_demote"] == "0" and int(o["host_after_demote"]) == 4 * GiB
+    assert int(o["swap_out"]) == 4 * GiB == int(o["vmem_out"])
+    assert o["vmem_ranges"] == "1"
+    assert (o["final_total"], o["final_host"], o["final_buffer"], o["final_ranges"], o["final_physical"]) == \
+        ("0", "0", "0", "0", "0")
+
+
+def test_vmem_off_keeps_zero_copy_spill(native_build):
+    o = run("vmem", env={**VMEM_ENV, "VGPU_VMEM_MIGRATE": "0"})
+    assert o["alloc_b"] == "0" and int(o["host_after_spill"]) == 4 * GiB
+    assert o["b_gpu_after_room"] == "0" and int(o["host_after_promote"]) == 4 * GiB
+    assert o["final_total"] == "0" and o["final_host"] == "0"
 
 
 def test_oversubscribe_still_capped(native_build):

@@ -230,12 +230,84 @@ def progress(seconds: int = 10, blocks: int = 256, iters: int = 2000) -> dict:
     return {"launches": n}
 
 
+def vmem(block_gib: int = 4, wait_s: int = 20) -> dict:
+    """Transparent migration on the device (oversubscribed pod): fill HBM with
+    plain blocks until one spills, use the spilled block from kernels (read
+    bandwidth in place), free two plain blocks, keep using the spilled block
+    until the shim's pager has moved it into HBM, then read it again."""
+    import ctypes
+
+    import torch
+    from vgpu.ops import kernels as K
+    lib = ctypes.CDLL(None)
+    host_bytes = lib.vgpu_self_host_bytes
+    host_bytes.restype = ctypes.c_uint64
+
+    def vstats():
+        v = (ctypes.c_uint64 * 5)()
+        lib.vgpu_self_vmem_stats(v)
+        return {"swap_in": v[0], "swap_out": v[1], "moves": v[2], "spill_in_hbm": v[3], "ranges": v[4]}
+
+    def read_gbps(t, seed, reps=3):
+        K.verify_pattern(t, seed)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        errs = 0
+        for _ in range(reps):
+            errs += K.verify_pattern(t, seed)
+        torch.cuda.synchronize()
+        return round(reps * t.numel() / (time.time() - t0) / 1e9, 1), errs
+
+    import faulthandler
+    faulthandler.dump_traceback_later(30, repeat=True)
+
+    def note(msg):
+        print(f"VMEM_PROBE {time.time():.3f} {msg} {vstats()}", file=sys.stderr, flush=True)
+
+    n = block_gib << 30
+    blocks = []
+    while True:
+        blocks.append(torch.empty(n, dtype=torch.uint8, device="cuda"))
+        if host_bytes(0):
+            break
+        if len(blocks) > 400:
+            return {"error": "no spill"}
+    spilled = blocks.pop()
+    note(f"spilled after {len(blocks)} plain blocks")
+    res = {"plain_blocks": len(blocks), "host_bytes": host_bytes(0), "after_spill": vstats()}
+    K.fill_pattern(spilled, 42)
+    torch.cuda.synchronize()
+    res["in_place_GBps"], res["in_place_errors"] = read_gbps(spilled, 42, 2)
+    res["after_use_full"] = vstats()
+    note("used in place")
+    del blocks[-2:]
+    torch.cuda.empty_cache()
+    note("freed two blocks")
+    t0 = time.time()
+    while time.time() - t0 < wait_s:
+        K.verify_pattern(spilled, 42)
+        torch.cuda.synchronize()
+        if vstats()["spill_in_hbm"] >= spilled.numel():
+            break
+        time.sleep(0.05)
+    res["promote_wait_s"] = round(time.time() - t0, 2)
+    note("promoted")
+    faulthandler.cancel_dump_traceback_later()
+    res["after_room"] = vstats()
+    res["promoted_GBps"], res["promoted_errors"] = read_gbps(spilled, 42)
+    res["host_bytes_after"] = host_bytes(0)
+    del spilled, blocks
+    torch.cuda.empty_cache()
+    res["final"] = vstats()
+    return res
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     cmd = argv.pop(0) if argv else "census"
     nums = [int(a) for a in argv]
     out = {"census": census, "busy": busy, "cap": cap, "smi": smi, "graph": graph, "arrays": arrays,
-           "progress": progress}[cmd](*nums)
+           "progress": progress, "vmem": vmem}[cmd](*nums)
     out["shim"] = shim_stats()
     print("PROBE " + json.dumps(out), flush=True)
     return 0

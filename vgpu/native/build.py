@@ -195,7 +195,7 @@ def build_fakes(force: bool = False) -> dict[str, Path]:
     hsa = FAKES_OUT / "libhsa-runtime64.so.1"
     if force or not _stamp(hsa, [hsa_src]):
         vs = FAKES_OUT / "hsa.map"
-        vs.write_text(_version_script(hsa_src, "ROCR_1", {}, "fake_hsa_queue_count; fake_hsa_queue_mask; fake_hsa_pool_used; fake_hsa_tools_loaded; open;"))
+        vs.write_text(_version_script(hsa_src, "ROCR_1", {}, "fake_hsa_queue_count; fake_hsa_queue_mask; fake_hsa_pool_used; fake_hsa_tools_loaded; open; hsa_signal_wait_scacquire;"))
         _run([CXX, *COMMON, hsa_src, "-o", hsa, "-shared", "-Wl,-soname,libhsa-runtime64.so.1",
               f"-Wl,--version-script={vs}", "-lpthread"])
         _mark(hsa, [hsa_src])
@@ -207,7 +207,7 @@ def build_fakes(force: bool = False) -> dict[str, Path]:
         vs = FAKES_OUT / "hip.map"
         vs.write_text(_version_script(
             hip_src, "hip_4.2", versions,
-            "fake_hip_launches; fake_hip_launch_blocks; fake_hip_physical_used; fake_hip_graph_create; fake_hip_exec_ns;"))
+            "fake_hip_launches; fake_hip_launch_blocks; fake_hip_physical_used; fake_hip_graph_create; fake_hip_exec_ns; fake_hip_svm_move; fake_hip_managed_gpu_bytes;"))
         _run([CXX, *COMMON, hip_src, "-o", hip, "-shared", "-Wl,-soname,libamdhip64.so.7",
               f"-Wl,--version-script={vs}", f"-L{FAKES_OUT}", "-l:libhsa-runtime64.so.1",
               f"-Wl,-rpath,{FAKES_OUT}", "-ldl", "-lpthread"])
