@@ -311,6 +311,7 @@ void pager_step() {
   }
   if (hot.empty()) return;
   std::sort(hot.begin(), hot.end(), [](VRange* a, VRange* b) { return a->uses.load() > b->uses.load(); });
+  uint64_t waiting = 0;
   for (VRange* r : hot) {
     std::lock_guard<std::mutex> m(g_move_mu);
     {  // freed meanwhile?
@@ -320,9 +321,17 @@ void pager_step() {
     const uint64_t stale = tick > k.cold_ticks ? tick - k.cold_ticks : 0;
     while (r->gpu_bytes < r->size) {
       uint64_t n = std::min<uint64_t>(k.piece, r->size - r->gpu_bytes);
-      if (!make_room_locked(r->dev, n, r, stale)) break;
-      if (!promote_piece_locked(r)) break;
+      if (!make_room_locked(r->dev, n, r, stale) || !promote_piece_locked(r)) {
+        waiting += r->size - r->gpu_bytes;
+        break;
+      }
     }
+  }
+  static uint64_t last_note = 0;
+  if (waiting && tick - last_note >= 1000 / (uint64_t)k.tick_ms) {
+    last_note = tick;
+    VLOG_INFO("vmem: %llu bytes of used spilled ranges wait for HBM (free for the pager %llu)",
+              (unsigned long long)waiting, (unsigned long long)hbm_free(hot.front()->dev));
   }
 }
 

@@ -202,11 +202,14 @@ def part_c(leave_gib: float, tokens: int, ctx: int, windows: int, migrate: bool)
     held = nb.stdout.readline().split()
     env = preload_env()
     env.update({"VGPU_DEVICE_MEMORY_LIMIT_0": "400000m", "VGPU_OVERSUBSCRIBE": "true", "PYTHONPATH": repo,
+                "VGPU_LOG_LEVEL": env.get("VGPU_LOG_LEVEL", "3"),
                 "VGPU_VMEM_MIGRATE": "1" if migrate else "0"})
-    if os.environ.get("VGPU_TRACE"):
+    if os.environ.get("VGPU_TRACE") and migrate:
         env["VGPU_TRACE"] = os.environ["VGPU_TRACE"]
+        env.setdefault("VGPU_TRACE_EVENTS", "1000000")
     import tempfile
-    errf = tempfile.TemporaryFile(mode="w+")
+    errf = tempfile.NamedTemporaryFile(mode="w+", prefix="vmem_c_", suffix=".log",
+                                       dir=os.environ.get("VGPU_VMEM_LOG_DIR") or None, delete=False)
     pod = subprocess.Popen([sys.executable, "-m", "vgpu.bench.vmem", "--child-c", "--tokens", str(tokens),
                             "--ctx", str(ctx), "--windows", str(windows)], env=env, stdin=subprocess.PIPE,
                            stdout=subprocess.PIPE, stderr=errf, text=True)
@@ -253,6 +256,7 @@ def main(argv=None) -> int:
     ap.add_argument("--part-c", action="store_true", help="only part C (transparent migration A/B)")
     ap.add_argument("--leave-gib", type=float, default=8.0)
     ap.add_argument("--windows", type=int, default=6)
+    ap.add_argument("--modes", default="pager,zero_copy")
     ap.add_argument("--skip-a", action="store_true")
     ap.add_argument("--skip-b", action="store_true")
     a = ap.parse_args(argv)
@@ -265,9 +269,9 @@ def main(argv=None) -> int:
     if a.part_c:
         out = {"config": "amd.com/gpumem=400000 (MiB), VGPU_OVERSUBSCRIBE=true, Llama-3-8B bf16 decode, "
                          f"neighbour holds all but {a.leave_gib} GiB of HBM during load"}
-        for migrate in (True, False):
-            out["pager" if migrate else "zero_copy"] = part_c(a.leave_gib, a.tokens, a.ctx, a.windows, migrate)
-            print("VMEM_C_RUN " + json.dumps(out["pager" if migrate else "zero_copy"]), flush=True)
+        for mode in a.modes.split(","):
+            out[mode] = part_c(a.leave_gib, a.tokens, a.ctx, a.windows, mode == "pager")
+            print("VMEM_C_RUN " + json.dumps(out[mode]), flush=True)
         print(json.dumps(out), flush=True)
         return 0
     out = {"config": "amd.com/gpumem=400000 (MiB) on one MI355X, VGPU_OVERSUBSCRIBE=true"}

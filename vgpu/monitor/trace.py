@@ -18,7 +18,7 @@ import os
 
 MAGIC = 0x56545243
 TYPES = {1: "alloc", 2: "free", 3: "oom", 4: "launch", 5: "throttle", 6: "suspend",
-         7: "priority_block", 8: "queue", 9: "gpu_time"}
+         7: "priority_block", 8: "queue", 9: "gpu_time", 10: "migrate"}
 
 
 class Event(ctypes.Structure):
@@ -68,6 +68,16 @@ def summarize(events: list[dict]) -> dict:
     s["exempt_launches"] = sum(1 for e in events if e["type"] == "launch" and e["b"])
     s["throttle_wait_ms"] = sum(e["a"] for e in events if e["type"] == "throttle") / 1e6
     s["blocked_ms"] = sum(e["a"] for e in events if e["type"] in ("suspend", "priority_block")) / 1e6
+    mig = [e for e in events if e["type"] == "migrate"]
+    if mig:  # b = (ns << 1) | to_hbm
+        up = [e for e in mig if e["b"] & 1]
+        down = [e for e in mig if not e["b"] & 1]
+        s["migrate_to_hbm_bytes"] = sum(e["a"] for e in up)
+        s["migrate_to_host_bytes"] = sum(e["a"] for e in down)
+        busy = sum(e["b"] >> 1 for e in mig)
+        s["migrate_busy_ms"] = busy / 1e6
+        s["migrate_GBps"] = round(sum(e["a"] for e in mig) / busy, 2) if busy else None
+        s["migrate_window_ms"] = [mig[0]["t_ns"] / 1e6, (mig[-1]["t_ns"]) / 1e6]
     return s
 
 
