@@ -253,6 +253,15 @@ def test_allocate_two_pods_share_one_gpu(cluster):
         assert "/dev/kfd" in devs and any(p.startswith("/dev/dri/renderD") for p in devs)
     m1, m2 = parse_mask(dict(r1.envs)["VGPU_CU_MASK_0"]), parse_mask(dict(r2.envs)["VGPU_CU_MASK_0"])
     assert m1 & m2 == 0 and bin(m1).count("1") == 128 and bin(m2).count("1") == 128
+    # the same masks for ROCr's own queues (HSA_CU_MASK list syntax)
+    for r, m in ((r1, m1), (r2, m2)):
+        dev, _, spec = dict(r.envs)["HSA_CU_MASK"].partition(":")
+        bits = 0
+        for part in spec.split(","):
+            lo, _, hi = part.partition("-")
+            for b in range(int(lo), int(hi or lo) + 1):
+                bits |= 1 << b
+        assert dev == "0" and bits == m
     for name in ("a", "b"):
         a = c["client"].get_pod("default", name)["metadata"]["annotations"]
         assert a[R.BIND_PHASE] == R.BIND_SUCCESS
@@ -422,6 +431,13 @@ def test_health_uncorrectable_ecc_then_reset_recovers(cluster):
     while any(d.health == api.UNHEALTHY for d in upd.devices):
         upd = next(stream)
     stream.cancel()
+
+
+def test_mask_ranges_syntax():
+    from vgpu.deviceplugin.allocate import mask_ranges
+    assert mask_ranges(0b1110011) == "0-1,4-6"
+    assert mask_ranges(1 << 255) == "255"
+    assert mask_ranges((1 << 256) - 1) == "0-255"
 
 
 def test_partition_mode_mismatch_is_unhealthy_until_restored():

@@ -191,3 +191,17 @@ def test_vmem_spill_promoted_transparently(gpu_build):
     assert res["host_bytes_after"] == 0
     assert res["in_place_GBps"] < 200 and res["promoted_GBps"] > 1000, res
     assert res["final"]["ranges"] == 0
+
+
+def test_rocr_cu_mask_env_matches_shim_masks(gpu_build):
+    """Allocate also sets HSA_CU_MASK so ROCr masks the
+    queues the shim never sees (its internal blit queue).  Same logical bits:
+    a process with only HSA_CU_MASK (no shim) lands on exactly the CUs the
+    shim's mask gives, XCD-balanced."""
+    from vgpu.deviceplugin.allocate import mask_ranges
+    from vgpu.device.cualloc import MI355X, alloc_cu_mask
+    m = alloc_cu_mask(0, 25, MI355X)
+    env_only = probe(["census", 4096, 200000], {"HSA_CU_MASK": f"0:{mask_ranges(m)}"}, preload=False)
+    shim = probe(["census", 4096, 200000], {"VGPU_CU_MASK_0": hex(m)})
+    assert env_only["distinct_cus"] == 64 == shim["distinct_cus"], (env_only, shim)
+    assert env_only["per_xcc"] == shim["per_xcc"]

@@ -115,6 +115,11 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
         if admitted is not None:
             cenv = dict(admitted[i].env)
             mask_bits = admitted[i].cu_mask_bits
+            if "HSA_CU_MASK" in cenv and device.isdigit():
+                # In a pod ROCr enumerates only the container's GPUs (index 0 here);
+                # a bench pod sees the whole node, so name the physical ordinal.
+                cenv["HSA_CU_MASK"] = ";".join(f"{device}:{e.partition(':')[2]}"
+                                               for e in cenv["HSA_CU_MASK"].split(";"))
         else:
             if sp.cores and sp.cores < 100 and cu_share in ("group2", "group2i"):
                 g = i // 2 if cu_share == "group2" else i % max(1, (len(specs) + 1) // 2)

@@ -59,6 +59,7 @@ class DevicePluginConfig:
     #             rest share the remaining CUs (one pool mask) under the temporal limiter
     cu_share: str = "hybrid"
     max_mask_slots: int = 2
+    rocr_cu_mask: bool = True             # also hand the masks to ROCr (HSA_CU_MASK: internal queues too)
     host_lock_dir: str = "/tmp/vgpulock"  # node-wide unified lock + per-GPU share boards
     device_list_strategy: str = "envvar"  # envvar (device nodes in the response) | cdi-annotations | cdi-cri
     cdi_dir: str = "/var/run/cdi"

@@ -137,6 +137,19 @@ def _ctr_env_names(pod: dict, idx: int) -> set[str]:
     return {e.get("name") for e in ctrs[idx].get("env") or []}
 
 
+def mask_ranges(mask: int) -> str:
+    """CU bit set → ROCr HSA_CU_MASK list syntax, e.g. 0b1110011 → '0-1,4-6'."""
+    out, bit = [], 0
+    while mask >> bit:
+        if mask >> bit & 1:
+            start = bit
+            while mask >> (bit + 1) & 1:
+                bit += 1
+            out.append(str(start) if start == bit else f"{start}-{bit}")
+        bit += 1
+    return ",".join(out)
+
+
 def build_container_grant(cfg: DevicePluginConfig, pod: dict, ctr_idx: int, devreq: list[ContainerDevice],
                           devices: dict[str, Device], cu_state: CUMaskState) -> ContainerGrant:
     ctrs = O.containers(pod)
@@ -154,6 +167,7 @@ def build_container_grant(cfg: DevicePluginConfig, pod: dict, ctr_idx: int, devr
     env_names = _ctr_env_names(pod, ctr_idx)
     fractional = False
     temporal = False
+    rocr_masks: list[str] = []
     for i, d in enumerate(ordered):
         dev = devices[d.uuid]
         g.envs[ENV_MEM_LIMIT.format(i=i)] = f"{d.usedmem}m"
@@ -164,6 +178,7 @@ def build_container_grant(cfg: DevicePluginConfig, pod: dict, ctr_idx: int, devr
             sg = shares.get(d.uuid)
             if sg and sg.mask:
                 g.envs[ENV_CU_MASK.format(i=i)] = format_mask(sg.mask)
+                rocr_masks.append(f"{i}:{mask_ranges(sg.mask)}")
             temporal |= bool(sg and sg.temporal)
         g.devices.append((f"/dev/dri/renderD{dev.render_minor}", f"/dev/dri/renderD{dev.render_minor}", "rw"))
         g.devices.append((f"/dev/dri/card{dev.card}", f"/dev/dri/card{dev.card}", "rw"))
@@ -174,6 +189,12 @@ def build_container_grant(cfg: DevicePluginConfig, pod: dict, ctr_idx: int, devr
         # node-wide lock dir); no mask is derived from the limit.
         g.envs[ENV_CU_SHARE] = "temporal"
         g.envs["VGPU_CU_MASK_FROM_LIMIT"] = "false"
+    if rocr_masks and cfg.rocr_cu_mask and "HSA_CU_MASK" not in env_names:
+        # ROCr applies HSA_CU_MASK to every AQL queue it creates, its internal
+        # blit/utility queue included — the one queue the shim's
+        # hsa_queue_create hook never sees.  Same logical CU bits as the shim's
+        # hsa_amd_queue_cu_set_mask (tests/test_gpu_shim.py census).
+        g.envs["HSA_CU_MASK"] = ";".join(rocr_masks)
     if fractional and cfg.hw_queues_per_vgpu and "GPU_MAX_HW_QUEUES" not in env_names:
         g.envs["GPU_MAX_HW_QUEUES"] = str(cfg.hw_queues_per_vgpu)
     g.envs[ENV_SHARED_REGION] = f"{CONTAINER_CACHE_DIR}/vgpu.cache"
