@@ -669,6 +669,153 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
   epilogue_halves<BM, BN, RES>(a, acc, m0, n0, smem, res);
 }
 
+// ---- 256x256 tile for large 1x1 / stride-1 convs without a prologue ----------
+// A plain GEMM y[M][Cout] = x[M][C] · W[Cout][C]ᵀ (+bias, +residual, act) whose
+// two operands are both K-contiguous.  The 128x128 kernels above spend two
+// workgroup barriers and 64 KB of LDS fragment reads per 2.1 MFLOP K step
+// (≈800 TFLOP/s on 65536x1024x1024, profiles/gemm_ceiling_r1.md).  Here one
+// workgroup of 8 waves (2 M x 4 N, wave tile 128x64) owns a 256x256 output
+// tile: a K step is 8.4 MFLOP — 64 MFMAs per wave — against the same two
+// barriers, and each wave reads 24 KB of fragments for 4x the work of a
+// 64x64 wave tile (LDS traffic per FLOP -33 %).  Two 64 KB LDS stages are
+// filled by LDS-DMA one K step ahead (one workgroup per CU: 128 KB of 160).
+// The epilogue goes through a per-wave LDS slab in four 32-row quarters so
+// every store is a 16-B bf16x8 and the bias is loaded once per lane.
+constexpr int kBigThreads = 512;
+
+template <bool RES>
+__global__ void __launch_bounds__(kBigThreads, 1) conv_big_kernel(const ConvArgs a) {
+  constexpr int BM = 256, BN = 256;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  constexpr int TM = 8, TN = 4;              // 16x16 sub-tiles per wave: 128 x 64
+  constexpr int CS = 64 + 4;                  // epilogue slab row stride (floats)
+  constexpr int SLAB = 32 * CS * 4;           // 32 rows of one wave's 64 columns
+  static_assert(8 * SLAB <= 2 * STAGE, "epilogue slabs fit in the pipeline stages");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int lrow = t >> 3, lchunk = (t & 7) ^ (lrow & 7);  // DMA row 0..63 of a 64-row group
+  int m0, n0;
+  tile_origin(a, blockIdx.x, BM, BN, m0, n0);
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.x), 0, a.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.w), 0, (uint32_t)((int64_t)a.Cout * a.K * 2), 0x00020000);
+  uint32_t aoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + lrow + 64 * i;
+    aoff[i] = m < a.M ? (uint32_t)(((int64_t)m * a.K + lchunk * 8) * 2) : kOOB;
+  }
+  const uint32_t boff = (uint32_t)(((n0 + lrow) * a.K + lchunk * 8) * 2);
+
+  auto issue = [&](int kt, int st) {
+    char* sA = smem + st * STAGE;
+    char* sB = sA + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void_t*)(sA + (64 * i + wave * 8) * 128), 16,
+                                               aoff[i] == kOOB ? kOOB : aoff[i] + (uint32_t)kt * 128, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void_t*)(sB + (64 * i + wave * 8) * 128), 16,
+                                               boff + (uint32_t)((64 * i * a.K + kt * BK) * 2), 0, 0, 0);
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  issue(0, 0);
+  for (int kt = 0; kt < a.ktiles; ++kt) {
+    const int st = kt & 1;
+    if (kt + 1 < a.ktiles) {
+      issue(kt + 1, st ^ 1);
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(8));  // this thread's 8 DMAs of stage st retired
+    } else {
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+    }
+    __builtin_amdgcn_s_barrier();
+    const char* sA = smem + st * STAGE;
+    __builtin_amdgcn_s_setprio(1);
+    mma_k64<TM, TN>(sA, sA + A_BYTES, wm * 128, wn * 64, fr, fk, acc);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_waitcnt(kLgkm0);  // stage st read out before anyone refills it
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // Epilogue: per wave, 4 quarters of 32 rows x 64 columns through its own slab.
+  float* sC = reinterpret_cast<float*>(smem + wave * SLAB);
+  const int ecol = (lane & 7) * 8, erow = lane >> 3;  // lane: 8 columns of rows erow + 8r
+  const int col = n0 + wn * 64 + ecol;
+  float bb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bb[j] = 0.0f;
+  if (a.bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(a.bias + col);
+    const float4 b1 = *reinterpret_cast<const float4*>(a.bias + col + 4);
+    bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
+    bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+  }
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.res), 0, a.y_bytes, 0x00020000);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    u32x4 res[4];
+    if constexpr (RES) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 128 + q * 32 + erow + 8 * r;
+        res[r] = __builtin_amdgcn_raw_buffer_load_b128(
+            rr, m < a.M ? (uint32_t)(((int64_t)m * a.Cout + col) * 2) : kOOB, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sC[(ii * 16 + fk * 4 + e) * CS + j * 16 + fr] = acc[2 * q + ii][j][e];
+    __builtin_amdgcn_s_waitcnt(kLgkm0);  // one wave owns the slab: no workgroup barrier
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = erow + 8 * r, m = m0 + wm * 128 + q * 32 + row;
+      const float4 c0 = *reinterpret_cast<const float4*>(sC + row * CS + ecol);
+      const float4 c1 = *reinterpret_cast<const float4*>(sC + row * CS + ecol + 4);
+      float v[8] = {c0.x + bb[0], c0.y + bb[1], c0.z + bb[2], c0.w + bb[3],
+                    c1.x + bb[4], c1.y + bb[5], c1.z + bb[6], c1.w + bb[7]};
+      if constexpr (RES) {
+        float re[8];
+        unpack8(res[r], re);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += re[j];
+      }
+      if (a.act) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);
+      }
+      if (m < a.M) *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = pack8(v);
+    }
+    __builtin_amdgcn_s_waitcnt(kLgkm0);  // slab read out before the next quarter overwrites it
+  }
+}
+
+template <bool RES>
+hipError_t launch_big(ConvArgs a, hipStream_t s) {
+  a.nM = (a.M + 255) / 256;
+  a.nN = a.Cout / 256;
+  a.nwg = a.nM * a.nN;
+  hipLaunchKernelGGL((conv_big_kernel<RES>), dim3(a.nwg), dim3(kBigThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+int g_forced_big = -1;  // vgpu_conv_set_big: -1 = env VGPU_CONV_BIG / heuristic, 0 = off, 1 = whenever eligible
+
 int g_forced_stages = -1;
 int g_forced_bm = 0;  // vgpu_conv_set_tile_m (A/B benchmarking); 0 = heuristic  // vgpu_conv_set_stages (A/B benchmarking); -1 = env / default
 
@@ -1414,6 +1561,7 @@ VGPU_API int vgpu_stem_space_to_depth(const void* x, void* X, int N, int H, int 
 VGPU_API void vgpu_conv_set_stages(int n) { g_forced_stages = n; }
 // Benchmark knob: force 64- or 128-row tiles (0 = heuristic).
 VGPU_API void vgpu_conv_set_tile_m(int bm) { g_forced_bm = bm; }
+VGPU_API void vgpu_conv_set_big(int mode) { g_forced_big = mode; }  // -1 env/heuristic, 0 off, 1 when eligible
 
 // Fused conv2 (3x3, pad 1, stride s, C = W → W, bias + ReLU) + conv3 (1x1,
 // W → 4W) + residual; with w1n, also the next block's conv1 (1x1, 4W → W,
@@ -1572,7 +1720,18 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
     // (The in-register prologue variant measured slower than the register
     // path on every ResNet-50 shape — VALU-bound — so it is opt-in.)
     const bool glds = glds_enabled() && (!pro || (glds_pro_enabled() && KS == 1 && pad == 0 && C <= 2048));
-    if (narrow)
+    // 256x256 tiles: 1x1 / stride 1 / no prologue, Cout % 256 == 0, and enough
+    // tiles to give every CU this process owns at least one.
+    if (g_forced_big < 0) {
+      const char* v = getenv("VGPU_CONV_BIG");
+      g_forced_big = v ? (v[0] == '1' ? 1 : (v[0] == '0' ? 0 : 2)) : 2;
+    }
+    const bool big_ok = !narrow && !pro && KS == 1 && stride == 1 && pad == 0 && Cout % 256 == 0;
+    const int64_t tiles256 = (int64_t)((c.M + 255) / 256) * (Cout / 256);
+    const bool big = big_ok && (g_forced_big == 1 || (g_forced_big == 2 && tiles256 >= (int64_t)conv_cus()));
+    if (big)
+      e = has_res ? launch_big<true>(c, s) : launch_big<false>(c, s);
+    else if (narrow)
       e = small ? launch_glds<4, 64, 64, false, false, 16>(c, s) : launch_glds<4, 128, 64, false, false, 16>(c, s);
     // Short K (≤ 2 steps) or 64-wide outputs: the persistent register kernel,
     // which overlaps the next tile's loads with this tile's epilogue, wins there.

@@ -57,6 +57,32 @@ def test_conv_matches_fp32(C, case):
     torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
 
 
+BIG_CASES = [
+    # 256x256-tile kernel (1x1, stride 1, no prologue, Cout % 256 == 0), forced on
+    (4, 256, 32, 33, 512, True, "relu", True),    # M = 4224: ragged last M tile, bias+act+residual
+    (2, 1024, 16, 16, 256, False, "none", False),  # deep K (16 steps), one N tile
+    (1, 64, 7, 9, 768, True, "none", True),        # M = 63 < one tile, three N tiles
+]
+
+
+@pytest.mark.parametrize("case", BIG_CASES, ids=lambda c: "x".join(map(str, c[:5])))
+def test_conv_big_tile_matches_fp32(C, case):
+    from vgpu.native import load_kernels
+    n, c, h, w, cout, has_bias, act, has_res = case
+    x = _t((n, c, h, w), 11)
+    wt = _t((cout, c, 1, 1), 12, scale=(2.0 / c) ** 0.5)
+    bias = _f((cout,), 13) if has_bias else None
+    res = _t((n, cout, h, w), 14) if has_res else None
+    lib = load_kernels()
+    lib.vgpu_conv_set_big(1)
+    try:
+        got = C.conv2d(x, wt, bias, act=act, residual=res)
+    finally:
+        lib.vgpu_conv_set_big(-1)
+    ref = C.conv2d_ref(x, wt, bias, act=act, residual=res)
+    torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
+
+
 def test_conv_asymmetric_exact(C):
     """Integer data (exact in bf16/fp32): catches any row/col or k-order swap."""
     n, c, h, w, cout = 1, 64, 4, 5, 128
