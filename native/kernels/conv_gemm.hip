@@ -682,14 +682,26 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
 // The epilogue goes through a per-wave LDS slab in four 32-row quarters so
 // every store is a 16-B bf16x8 and the bias is loaded once per lane.
 constexpr int kBigThreads = 512;
+int conv_cus();
 
+
+// Ping-pong schedule: the two waves that share a SIMD (one from each M half of
+// the workgroup, wm = 0 / 1) run half a K step apart.  A K step is two phases
+// per wave — R: the 24 ds_read_b128 of all its A/B fragments, M: its 64 MFMAs
+// — and the wm = 1 group starts one phase late, so in every phase one wave
+// of a SIMD multiplies while the other fills its registers from LDS (the
+// fragment reads no longer stall the MFMA pipe at the top of each step).  One
+// workgroup barrier per phase.  Stage k % 2 holds K step k: group 0 reads it
+// in phase 2k, group 1 in phase 2k+1; the DMA of step k+2 into the same stage
+// is issued at the start of phase 2k+2 and waited for (vmcnt(0)) at the end of
+// phase 2k+3, before the barrier that publishes it to phase 2k+4.
 template <bool RES>
 __global__ void __launch_bounds__(kBigThreads, 1) conv_big_kernel(const ConvArgs a) {
   constexpr int BM = 256, BN = 256;
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
   constexpr int TM = 8, TN = 4;              // 16x16 sub-tiles per wave: 128 x 64
   constexpr int CS = 64 + 4;                  // epilogue slab row stride (floats)
-  constexpr int SLAB = 32 * CS * 4;           // 32 rows of one wave's 64 columns
+  constexpr int SLAB = 16 * CS * 4;           // 16 rows of one wave's 64 columns
   static_assert(8 * SLAB <= 2 * STAGE, "epilogue slabs fit in the pipeline stages");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
@@ -711,9 +723,8 @@ __global__ void __launch_bounds__(kBigThreads, 1) conv_big_kernel(const ConvArgs
     aoff[i] = m < a.M ? (uint32_t)(((int64_t)m * a.K + lchunk * 8) * 2) : kOOB;
   }
   const uint32_t boff = (uint32_t)(((n0 + lrow) * a.K + lchunk * 8) * 2);
-
-  auto issue = [&](int kt, int st) {
-    char* sA = smem + st * STAGE;
+  auto issue = [&](int kt) {
+    char* sA = smem + (kt & 1) * STAGE;
     char* sB = sA + A_BYTES;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -730,28 +741,54 @@ __global__ void __launch_bounds__(kBigThreads, 1) conv_big_kernel(const ConvArgs
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  bf16x8_t af[2][TM], bfr[2][TN];
 
-  issue(0, 0);
-  for (int kt = 0; kt < a.ktiles; ++kt) {
-    const int st = kt & 1;
-    if (kt + 1 < a.ktiles) {
-      issue(kt + 1, st ^ 1);
-      __builtin_amdgcn_s_waitcnt(vmcnt_imm(8));  // this thread's 8 DMAs of stage st retired
-    } else {
-      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+  const int K = a.ktiles;
+  issue(0);
+  if (K > 1) {
+    issue(1);
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(8));
+  } else {
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+  }
+  __builtin_amdgcn_s_barrier();
+  const int arow = wm * 128, brow = wn * 64;
+  for (int p = 0; p <= 2 * K; ++p) {
+    if (!(p & 1) && p >= 2 && p / 2 + 1 < K) issue(p / 2 + 1);
+    const int q = p - wm;
+    if (q >= 0 && q < 2 * K) {
+      if (!(q & 1)) {  // R: all fragments of step q/2
+        const char* sA = smem + ((q >> 1) & 1) * STAGE;
+        const char* sB = sA + A_BYTES;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            af[kk][i] = *reinterpret_cast<const bf16x8_t*>(sA + swz(arow + i * 16 + fr, kk * 4 + fk));
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            bfr[kk][j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(brow + j * 16 + fr, kk * 4 + fk));
+        }
+      } else {  // M: 64 MFMAs
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
     }
-    __builtin_amdgcn_s_barrier();
-    const char* sA = smem + st * STAGE;
-    __builtin_amdgcn_s_setprio(1);
-    mma_k64<TM, TN>(sA, sA + A_BYTES, wm * 128, wn * 64, fr, fk, acc);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_waitcnt(kLgkm0);  // stage st read out before anyone refills it
+    if ((p & 1) && (p >> 1) + 1 < K) __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // step p/2+1 landed
+    __builtin_amdgcn_s_waitcnt(kLgkm0);  // this phase's fragment reads retired
     __builtin_amdgcn_s_barrier();
   }
 
-  // Epilogue: per wave, 4 quarters of 32 rows x 64 columns through its own slab.
+  // Epilogue: per wave, eight 16-row passes through its own slab.
   float* sC = reinterpret_cast<float*>(smem + wave * SLAB);
-  const int ecol = (lane & 7) * 8, erow = lane >> 3;  // lane: 8 columns of rows erow + 8r
+  const int ecol = (lane & 7) * 8, erow = lane >> 3;
   const int col = n0 + wn * 64 + ecol;
   float bb[8];
 #pragma unroll
@@ -765,26 +802,24 @@ __global__ void __launch_bounds__(kBigThreads, 1) conv_big_kernel(const ConvArgs
   const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(a.res), 0, a.y_bytes, 0x00020000);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    u32x4 res[4];
+  for (int i = 0; i < TM; ++i) {
+    u32x4 res[2];
     if constexpr (RES) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 128 + q * 32 + erow + 8 * r;
+      for (int r = 0; r < 2; ++r) {
+        const int m = m0 + wm * 128 + i * 16 + erow + 8 * r;
         res[r] = __builtin_amdgcn_raw_buffer_load_b128(
             rr, m < a.M ? (uint32_t)(((int64_t)m * a.Cout + col) * 2) : kOOB, 0, 0);
       }
     }
 #pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sC[(ii * 16 + fk * 4 + e) * CS + j * 16 + fr] = acc[2 * q + ii][j][e];
+      for (int e = 0; e < 4; ++e) sC[(fk * 4 + e) * CS + j * 16 + fr] = acc[i][j][e];
     __builtin_amdgcn_s_waitcnt(kLgkm0);  // one wave owns the slab: no workgroup barrier
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = erow + 8 * r, m = m0 + wm * 128 + q * 32 + row;
+    for (int r = 0; r < 2; ++r) {
+      const int row = erow + 8 * r, m = m0 + wm * 128 + i * 16 + row;
       const float4 c0 = *reinterpret_cast<const float4*>(sC + row * CS + ecol);
       const float4 c1 = *reinterpret_cast<const float4*>(sC + row * CS + ecol + 4);
       float v[8] = {c0.x + bb[0], c0.y + bb[1], c0.z + bb[2], c0.w + bb[3],
@@ -801,7 +836,7 @@ __global__ void __launch_bounds__(kBigThreads, 1) conv_big_kernel(const ConvArgs
       }
       if (m < a.M) *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = pack8(v);
     }
-    __builtin_amdgcn_s_waitcnt(kLgkm0);  // slab read out before the next quarter overwrites it
+    __builtin_amdgcn_s_waitcnt(kLgkm0);  // slab read out before the next pass overwrites it
   }
 }
 
