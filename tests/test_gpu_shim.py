@@ -187,7 +187,8 @@ def test_vmem_spill_promoted_transparently(gpu_build):
                 timeout=300)
     assert res["host_bytes"] == 4 * GiB_ and res["after_spill"]["ranges"] == 1
     assert res["in_place_errors"] == 0 and res["promoted_errors"] == 0
-    assert res["after_room"]["spill_in_hbm"] == 4 * GiB_ and res["after_room"]["swap_in"] >= 4 * GiB_
+    # (small runtime buffers allocated while HBM was full may have spilled and been promoted too)
+    assert res["after_room"]["spill_in_hbm"] >= 4 * GiB_ and res["after_room"]["swap_in"] >= 4 * GiB_
     assert res["host_bytes_after"] == 0
     assert res["in_place_GBps"] < 200 and res["promoted_GBps"] > 1000, res
     assert res["final"]["ranges"] == 0
