@@ -685,30 +685,38 @@ constexpr int kBigThreads = 512;
 int conv_cus();
 
 
-// Ping-pong schedule: the two waves that share a SIMD (one from each M half of
-// the workgroup, wm = 0 / 1) run half a K step apart.  A K step is two phases
-// per wave — R: the 24 ds_read_b128 of all its A/B fragments, M: its 64 MFMAs
-// — and the wm = 1 group starts one phase late, so in every phase one wave
-// of a SIMD multiplies while the other fills its registers from LDS (the
-// fragment reads no longer stall the MFMA pipe at the top of each step).  One
-// workgroup barrier per phase.  Stage k % 2 holds K step k: group 0 reads it
-// in phase 2k, group 1 in phase 2k+1; the DMA of step k+2 into the same stage
-// is issued at the start of phase 2k+2 and waited for (vmcnt(0)) at the end of
-// phase 2k+3, before the barrier that publishes it to phase 2k+4.
-template <bool RES>
+// K steps of 32 (BK32) in an NS-deep ring of 32 KB LDS stages (NS = 4: 128 KB),
+// so the DMA of step k+NS-1 is issued while step k is multiplied: three steps
+// (1.5 64-deep steps) of lead instead of one, and the wait before the single
+// barrier per step is a counted vmcnt that leaves NS-2 steps in flight across
+// it.  Fragments are double-buffered in registers: the MFMAs of step k are
+// split around the barrier that publishes step k+1, and the reads of step k+1
+// are issued behind that barrier under the second half of step k's MFMAs.
+//
+// LDS image: rows of 64 B (32 bf16), 16-B slots; logical slot f of row r sits
+// in physical slot f ^ g((r>>2)&3), g = {0,2,3,1}: the four 16-lane groups of
+// a ds_read_b128 (lanes {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) then hit
+// 16 distinct bank quads — conflict-free.  The DMA lands lane-linearly (16
+// rows per wave instruction), so each lane fetches the logical slot that its
+// physical slot holds.
+__device__ __forceinline__ int swz_g(int q) { return (q >> 1) | (((q ^ (q >> 1)) & 1) << 1); }
+__device__ __forceinline__ int swz32(int row, int slot) {
+  return row * 64 + ((slot ^ swz_g((row >> 2) & 3)) << 4);
+}
+
+template <bool RES, int NS = 4>
 __global__ void __launch_bounds__(kBigThreads, 1) conv_big_kernel(const ConvArgs a) {
   constexpr int BM = 256, BN = 256;
-  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64, STAGE = A_BYTES + B_BYTES;  // 32 KB
   constexpr int TM = 8, TN = 4;              // 16x16 sub-tiles per wave: 128 x 64
   constexpr int CS = 64 + 4;                  // epilogue slab row stride (floats)
   constexpr int SLAB = 16 * CS * 4;           // 16 rows of one wave's 64 columns
-  static_assert(8 * SLAB <= 2 * STAGE, "epilogue slabs fit in the pipeline stages");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  static_assert(8 * SLAB <= NS * STAGE, "epilogue slabs fit in the pipeline stages");
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int fr = lane & 15, fk = lane >> 4;
-  const int lrow = t >> 3, lchunk = (t & 7) ^ (lrow & 7);  // DMA row 0..63 of a 64-row group
   int m0, n0;
   tile_origin(a, blockIdx.x, BM, BN, m0, n0);
 
@@ -716,24 +724,27 @@ __global__ void __launch_bounds__(kBigThreads, 1) conv_big_kernel(const ConvArgs
       const_cast<uint16_t*>(a.x), 0, a.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(a.w), 0, (uint32_t)((int64_t)a.Cout * a.K * 2), 0x00020000);
-  uint32_t aoff[4];
+  // DMA: wave instruction i (0,1) fills rows 32*wave + 16*i + (lane>>2) of the A and B images.
+  const int drow = lane >> 2, dslot = (lane & 3) ^ swz_g((lane >> 4) & 3);
+  uint32_t aoff[2], boff[2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + lrow + 64 * i;
-    aoff[i] = m < a.M ? (uint32_t)(((int64_t)m * a.K + lchunk * 8) * 2) : kOOB;
+  for (int i = 0; i < 2; ++i) {
+    const int r = 32 * wave + 16 * i + drow, m = m0 + r;
+    aoff[i] = m < a.M ? (uint32_t)(((int64_t)m * a.K + dslot * 8) * 2) : kOOB;
+    boff[i] = (uint32_t)(((int64_t)(n0 + r) * a.K + dslot * 8) * 2);
   }
-  const uint32_t boff = (uint32_t)(((n0 + lrow) * a.K + lchunk * 8) * 2);
+  const int ks = a.K / 32;
   auto issue = [&](int kt) {
-    char* sA = smem + (kt & 1) * STAGE;
+    const int kc = kt < ks ? kt : ks - 1;  // past the end: refetch the last step into a stage nobody reads again
+    char* sA = smem + (kt % NS) * STAGE;
     char* sB = sA + A_BYTES;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void_t*)(sA + (64 * i + wave * 8) * 128), 16,
-                                               aoff[i] == kOOB ? kOOB : aoff[i] + (uint32_t)kt * 128, 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void_t*)(sB + (64 * i + wave * 8) * 128), 16,
-                                               boff + (uint32_t)((64 * i * a.K + kt * BK) * 2), 0, 0, 0);
+    for (int i = 0; i < 2; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void_t*)(sA + (32 * wave + 16 * i) * 64), 16,
+                                               aoff[i] == kOOB ? kOOB : aoff[i] + (uint32_t)kc * 64, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void_t*)(sB + (32 * wave + 16 * i) * 64), 16,
+                                               boff[i] + (uint32_t)kc * 64, 0, 0, 0);
+    }
   };
 
   f32x4_t acc[TM][TN];
@@ -741,50 +752,61 @@ __global__ void __launch_bounds__(kBigThreads, 1) conv_big_kernel(const ConvArgs
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  bf16x8_t af[2][TM], bfr[2][TN];
-
-  const int K = a.ktiles;
-  issue(0);
-  if (K > 1) {
-    issue(1);
-    __builtin_amdgcn_s_waitcnt(vmcnt_imm(8));
-  } else {
-    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-  }
-  __builtin_amdgcn_s_barrier();
-  const int arow = wm * 128, brow = wn * 64;
-  for (int p = 0; p <= 2 * K; ++p) {
-    if (!(p & 1) && p >= 2 && p / 2 + 1 < K) issue(p / 2 + 1);
-    const int q = p - wm;
-    if (q >= 0 && q < 2 * K) {
-      if (!(q & 1)) {  // R: all fragments of step q/2
-        const char* sA = smem + ((q >> 1) & 1) * STAGE;
-        const char* sB = sA + A_BYTES;
+  // One rolling set of A fragments (rows 0-3 of step k+1 replace rows 0-3 of
+  // step k once the first MFMA half has used them) and two B sets.
+  bf16x8_t af[TM], bfr[2][TN];
+  const int arow = wm * 128 + fr, brow = wn * 64 + fr;
+  auto read_a = [&](int kt, int i0, int i1) {
+    const char* sA = smem + (kt % NS) * STAGE;
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
+    for (int i = i0; i < i1; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(sA + swz32(arow + i * 16, fk));
+  };
+  auto read_b = [&](int kt, bf16x8_t (&b)[TN]) {
+    const char* sB = smem + (kt % NS) * STAGE + A_BYTES;
 #pragma unroll
-          for (int i = 0; i < TM; ++i)
-            af[kk][i] = *reinterpret_cast<const bf16x8_t*>(sA + swz(arow + i * 16 + fr, kk * 4 + fk));
+    for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const bf16x8_t*>(sB + swz32(brow + j * 16, fk));
+  };
+  auto mfma_rows = [&](const bf16x8_t (&b)[TN], int i0, int i1) {
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            bfr[kk][j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(brow + j * 16 + fr, kk * 4 + fk));
-        }
-      } else {  // M: 64 MFMAs
-        __builtin_amdgcn_s_setprio(1);
+    for (int i = i0; i < i1; ++i)
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
-    }
-    if ((p & 1) && (p >> 1) + 1 < K) __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // step p/2+1 landed
-    __builtin_amdgcn_s_waitcnt(kLgkm0);  // this phase's fragment reads retired
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], b[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // One K step: A rows 4-7 of step kt load under the first MFMA half; the
+  // barrier publishing step kt+1 sits between the halves; step kt+1's A rows
+  // 0-3 and B load under the second half.
+  auto kstep = [&](int kt, bf16x8_t (&bc)[TN], bf16x8_t (&bn)[TN]) {
+    issue(kt + NS - 1);  // into the stage of step kt-1, read out before the last barrier
+    read_a(kt, TM / 2, TM);
+    mfma_rows(bc, 0, TM / 2);
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm((NS - 2) * 4));  // step kt+1 landed
+    __builtin_amdgcn_s_waitcnt(kLgkm0);                   // every read of step kt retired
     __builtin_amdgcn_s_barrier();
+    if (kt + 1 < ks) {
+      read_a(kt + 1, 0, TM / 2);
+      read_b(kt + 1, bn);
+    }
+    mfma_rows(bc, TM / 2, TM);
+  };
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) issue(s);
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm((NS - 2) * 4));  // step 0 landed (this thread's DMAs)
+  __builtin_amdgcn_s_barrier();
+  read_a(0, 0, TM / 2);
+  read_b(0, bfr[0]);
+  int kt = 0;
+  for (; kt + 1 < ks; kt += 2) {
+    kstep(kt, bfr[0], bfr[1]);
+    kstep(kt + 1, bfr[1], bfr[0]);
   }
+  if (kt < ks) kstep(kt, bfr[0], bfr[1]);
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // refetches past the end
+  __builtin_amdgcn_s_waitcnt(kLgkm0);
+  __builtin_amdgcn_s_barrier();
 
   // Epilogue: per wave, eight 16-row passes through its own slab.
   float* sC = reinterpret_cast<float*>(smem + wave * SLAB);
@@ -845,7 +867,7 @@ hipError_t launch_big(ConvArgs a, hipStream_t s) {
   a.nM = (a.M + 255) / 256;
   a.nN = a.Cout / 256;
   a.nwg = a.nM * a.nN;
-  hipLaunchKernelGGL((conv_big_kernel<RES>), dim3(a.nwg), dim3(kBigThreads), 0, s, a);
+  hipLaunchKernelGGL((conv_big_kernel<RES, 4>), dim3(a.nwg), dim3(kBigThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1761,7 +1783,7 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
       const char* v = getenv("VGPU_CONV_BIG");
       g_forced_big = v ? (v[0] == '1' ? 1 : (v[0] == '0' ? 0 : 2)) : 2;
     }
-    const bool big_ok = !narrow && !pro && KS == 1 && stride == 1 && pad == 0 && Cout % 256 == 0;
+    const bool big_ok = !narrow && !pro && KS == 1 && stride == 1 && pad == 0 && Cout % 256 == 0 && C >= 128;
     const int64_t tiles256 = (int64_t)((c.M + 255) / 256) * (Cout / 256);
     const bool big = big_ok && (g_forced_big == 1 || (g_forced_big == 2 && tiles256 >= (int64_t)conv_cus()));
     if (big)

@@ -61,7 +61,9 @@ BIG_CASES = [
     # 256x256-tile kernel (1x1, stride 1, no prologue, Cout % 256 == 0), forced on
     (4, 256, 32, 33, 512, True, "relu", True),    # M = 4224: ragged last M tile, bias+act+residual
     (2, 1024, 16, 16, 256, False, "none", False),  # deep K (16 steps), one N tile
-    (1, 64, 7, 9, 768, True, "none", True),        # M = 63 < one tile, three N tiles
+    (1, 128, 7, 9, 768, True, "none", True),       # M = 63 < one tile, three N tiles
+    (16, 128, 64, 64, 512, True, "relu", True),    # 512 tiles: each workgroup walks several (persistent ring)
+    (9, 192, 33, 35, 256, False, "none", False),   # K = 192 (6 steps of 32), ragged M across tiles
 ]
 
 
