@@ -1777,15 +1777,19 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
     // (The in-register prologue variant measured slower than the register
     // path on every ResNet-50 shape — VALU-bound — so it is opt-in.)
     const bool glds = glds_enabled() && (!pro || (glds_pro_enabled() && KS == 1 && pad == 0 && C <= 2048));
-    // 256x256 tiles: 1x1 / stride 1 / no prologue, Cout % 256 == 0, and enough
-    // tiles to give every CU this process owns at least one.
+    // 256x256 tiles: 1x1 / stride 1 / no prologue, Cout % 256 == 0, deep K
+    // (≥ 1024: below it these layers are HBM-bound and the 64-row tiles at 3
+    // blocks per CU win — the ResNet-50 flagship measured 1 % slower with the
+    // big tile on its K = 128-512 conv3 layers), and enough tiles to give every
+    // CU this process owns at least one.
     if (g_forced_big < 0) {
       const char* v = getenv("VGPU_CONV_BIG");
       g_forced_big = v ? (v[0] == '1' ? 1 : (v[0] == '0' ? 0 : 2)) : 2;
     }
     const bool big_ok = !narrow && !pro && KS == 1 && stride == 1 && pad == 0 && Cout % 256 == 0 && C >= 128;
     const int64_t tiles256 = (int64_t)((c.M + 255) / 256) * (Cout / 256);
-    const bool big = big_ok && (g_forced_big == 1 || (g_forced_big == 2 && tiles256 >= (int64_t)conv_cus()));
+    const bool big = big_ok && (g_forced_big == 1 ||
+                                (g_forced_big == 2 && C >= 1024 && tiles256 >= (int64_t)conv_cus()));
     if (big)
       e = has_res ? launch_big<true>(c, s) : launch_big<false>(c, s);
     else if (narrow)
