@@ -206,3 +206,42 @@ def test_rocr_cu_mask_env_matches_shim_masks(gpu_build):
     shim = probe(["census", 4096, 200000], {"VGPU_CU_MASK_0": hex(m)})
     assert env_only["distinct_cus"] == 64 == shim["distinct_cus"], (env_only, shim)
     assert env_only["per_xcc"] == shim["per_xcc"]
+
+
+def test_two_processes_race_for_the_last_bytes(gpu_build, tmp_path):
+    """two processes of one container (one shared region,
+    an 8 GiB cap) allocate 256 MiB chunks at the same time until refused.  The
+    reservation is taken under the region's robust lock before the real
+    allocation, so together they never exceed the cap, and the loser of the
+    last chunk is refused rather than overcommitted."""
+    from vgpu.native import preload_env
+    env = preload_env(dict(os.environ))
+    env.update({"VGPU_DEVICE_MEMORY_LIMIT_0": "8192m", "VGPU_SHARED_REGION": str(tmp_path / "vgpu.cache"),
+                "PYTHONPATH": REPO + os.pathsep + env.get("PYTHONPATH", "")})
+    procs = [subprocess.Popen([sys.executable, "-m", "vgpu.bench.probes", "capheld", "256"], env=env, cwd=REPO,
+                              stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True) for _ in range(2)]
+    try:
+        for p in procs:
+            assert p.stdout.readline().startswith("READY")
+        for p in procs:
+            p.stdin.write("go\n")
+            p.stdin.flush()
+        held = []
+        for p in procs:
+            line = p.stdout.readline()
+            assert line.startswith("HELD "), line
+            held.append(int(line.split()[1]))
+    finally:
+        for p in procs:
+            try:
+                p.stdin.write("\n")
+                p.stdin.flush()
+            except OSError:
+                pass
+        for p in procs:
+            p.wait(timeout=120)
+    cap = 8192 << 20
+    print("held", held)
+    assert sum(held) <= cap
+    assert sum(held) >= cap - 4 * (256 << 20)  # runtime context charges + one chunk each
+    assert min(held) > 0  # both ran concurrently

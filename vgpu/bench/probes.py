@@ -230,6 +230,30 @@ def progress(seconds: int = 10, blocks: int = 256, iters: int = 2000) -> dict:
     return {"launches": n}
 
 
+def capheld(chunk_mib: int = 256) -> dict:
+    """Allocate chunks until the cap refuses one, print `HELD <bytes>`, and keep
+    them until a line arrives on stdin (two of these race for one region)."""
+    import torch
+    torch.cuda.init()
+    torch.empty(1, device="cuda")
+    print("READY", flush=True)
+    sys.stdin.readline()  # start line: both processes allocate at the same time
+    n = chunk_mib << 20
+    held = []
+    while True:
+        try:
+            held.append(torch.empty(n, dtype=torch.uint8, device="cuda"))
+        except torch.OutOfMemoryError:
+            break
+        if len(held) > 4096:
+            break
+        time.sleep(0.005)  # interleave with the other process
+    torch.cuda.synchronize()
+    print(f"HELD {len(held) * n}", flush=True)
+    sys.stdin.readline()
+    return {"held": len(held) * n, "usage": shim_stats()}
+
+
 def vmem(block_gib: int = 4, wait_s: int = 20) -> dict:
     """Transparent migration on the device (oversubscribed pod): fill HBM with
     plain blocks until one spills, use the spilled block from kernels (read
@@ -307,7 +331,7 @@ def main(argv=None) -> int:
     cmd = argv.pop(0) if argv else "census"
     nums = [int(a) for a in argv]
     out = {"census": census, "busy": busy, "cap": cap, "smi": smi, "graph": graph, "arrays": arrays,
-           "progress": progress, "vmem": vmem}[cmd](*nums)
+           "progress": progress, "vmem": vmem, "capheld": capheld}[cmd](*nums)
     out["shim"] = shim_stats()
     print("PROBE " + json.dumps(out), flush=True)
     return 0
