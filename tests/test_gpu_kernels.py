@@ -60,3 +60,22 @@ def test_census_reports_valid_ids(K):
     torch.cuda.synchronize()
     assert int(xh[:, 0].max()) <= 7
     assert bool((ticks >= 1000).all())
+
+
+@pytest.mark.parametrize("b,t,e,layers", [(37, 64, 300, 2), (100, 48, 128, 1)])
+def test_fused_lstm_matches_fp32(gpu_build, b, t, e, layers):
+    """native/kernels/lstm.hip (+ input-projection GEMM) against torch.nn.LSTM in
+    fp32 on the same bf16-rounded weights and inputs; B = 37 leaves a partial
+    16-row slice."""
+    import torch
+    from vgpu.ops import lstm as fused
+    torch.manual_seed(0)
+    ref = torch.nn.LSTM(e, 128, num_layers=layers, batch_first=True).cuda()
+    with torch.no_grad():
+        for p in ref.parameters():
+            p.copy_((p * 2.0).to(torch.bfloat16).float())
+    x = (torch.randn(b, t, e, device="cuda") * 0.5).to(torch.bfloat16)
+    with torch.no_grad():
+        want = ref(x.float())[0][:, -1]
+        got = fused.lstm_last_hidden(ref.to(torch.bfloat16), x).float()
+    torch.testing.assert_close(got, want, atol=3e-2, rtol=3e-2)

@@ -62,6 +62,8 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_conv2d_nhwc.argtypes = [vp, vp, vp, vp, vp, vp, vp] + [ci] * 9 + [vp]
     lib.vgpu_maxpool_nhwc.argtypes = [vp, vp] + [ci] * 7 + [vp]
     lib.vgpu_conv_set_big.argtypes = [ci]
+    lib.vgpu_lstm_recurrence.argtypes = [vp, vp, vp, vp, ci, ci, ci, vp]
+    lib.vgpu_lstm_recurrence.restype = ci
     lib.vgpu_scale_shift_relu_mean_nhwc.argtypes = [vp, vp, vp, vp, ci, ci, ci, vp]
     i64, cf = ctypes.c_int64, ctypes.c_float
     lib.vgpu_bn_workspace.argtypes = [i64, ci]
