@@ -43,10 +43,14 @@ __device__ __forceinline__ float tanh_f(float x) { return 2.0f / (1.0f + __expf(
 
 // xp: [T][B][4H] bf16 (biases folded in); whh: [4H][H] bf16 (PyTorch weight_hh_l*);
 // y: [B][T][H] bf16 or nullptr; hlast: [B][H] bf16 or nullptr.
+// Training: gates (activated, bf16 [T][B][4H]) and cells (fp32 [T][B][H]) are
+// also written for the backward kernel.
 __global__ void __launch_bounds__(256, 1) lstm_recurrence_kernel(const uint16_t* __restrict__ xp,
                                                                  const uint16_t* __restrict__ whh,
                                                                  uint16_t* __restrict__ y,
-                                                                 uint16_t* __restrict__ hlast, int B, int T) {
+                                                                 uint16_t* __restrict__ hlast,
+                                                                 uint16_t* __restrict__ gates_out,
+                                                                 float* __restrict__ cells_out, int B, int T) {
   __shared__ __attribute__((aligned(16))) uint16_t sh[kRows * kHStride];   // h_{t-1}, bf16
   __shared__ __attribute__((aligned(16))) float sg[4 * kRows * kH];          // activated gates
 
@@ -122,6 +126,20 @@ __global__ void __launch_bounds__(256, 1) lstm_recurrence_kernel(const uint16_t*
                        (uint32_t)hv[4] | ((uint32_t)hv[5] << 16), (uint32_t)hv[6] | ((uint32_t)hv[7] << 16)};
     *reinterpret_cast<u32x4*>(sh + cm * kHStride + cn) = packed;
     const int row = b0 + cm;
+    if (row < B && gates_out) {
+      const float* gsrc[4] = {gi, gf, gg, go};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint32_t pk[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pk[q] = (uint32_t)f2bf(gsrc[k][2 * q]) | ((uint32_t)f2bf(gsrc[k][2 * q + 1]) << 16);
+        *reinterpret_cast<u32x4*>(gates_out + ((size_t)t * B + row) * (4 * kH) + k * kH + cn) =
+            u32x4{pk[0], pk[1], pk[2], pk[3]};
+      }
+      float* cd = cells_out + ((size_t)t * B + row) * kH + cn;
+      *reinterpret_cast<float4*>(cd) = float4{c[0], c[1], c[2], c[3]};
+      *reinterpret_cast<float4*>(cd + 4) = float4{c[4], c[5], c[6], c[7]};
+    }
     if (row < B) {
       if (y) *reinterpret_cast<u32x4*>(y + ((size_t)row * T + t) * kH + cn) = packed;
       if (hlast && t == T - 1) *reinterpret_cast<u32x4*>(hlast + (size_t)row * kH + cn) = packed;
@@ -130,7 +148,118 @@ __global__ void __launch_bounds__(256, 1) lstm_recurrence_kernel(const uint16_t*
   }
 }
 
+// Backward through time of one layer.  dgates_t (pre-activation) from the saved
+// activated gates and cells, dh_t = dY_t + dh_next, and
+//   dh_next = dgates_t · W_hh          (16 x 512) · (512 x 128) on MFMA
+// with wave w owning hidden columns [32w, 32w+32) and its W_hh slice (k = all
+// 512 gate rows) as B fragments in registers.  dgates go to global (bf16
+// [T][B][4H]) for the weight-gradient GEMMs done outside.
+constexpr int kGStride = 4 * kH + 8;  // dgates rows in LDS: 1040 B
+
+__global__ void __launch_bounds__(256, 1) lstm_backward_kernel(const uint16_t* __restrict__ gates,
+                                                               const float* __restrict__ cells,
+                                                               const uint16_t* __restrict__ dy,
+                                                               const uint16_t* __restrict__ whh,
+                                                               uint16_t* __restrict__ dgates, int B, int T) {
+  __shared__ __attribute__((aligned(16))) uint16_t sdg[kRows * kGStride];  // dgates_t, bf16
+  __shared__ __attribute__((aligned(16))) float sdh[kRows * kH];            // dh_next, fp32
+
+  const int t_ = threadIdx.x, lane = t_ & 63, w = t_ >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int b0 = blockIdx.x * kRows;
+  // B operand: B[k][n] = W_hh[k][n], k = gate row (0..511), n = hidden column of this wave's tiles.
+  bf16x8_t wf[2][16];
+#pragma unroll
+  for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      uint16_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = whh[(size_t)(ks * 32 + fk * 8 + j) * kH + w * 32 + jn * 16 + fr];
+      wf[jn][ks] = __builtin_bit_cast(bf16x8_t, u32x4{(uint32_t)v[0] | ((uint32_t)v[1] << 16),
+                                                       (uint32_t)v[2] | ((uint32_t)v[3] << 16),
+                                                       (uint32_t)v[4] | ((uint32_t)v[5] << 16),
+                                                       (uint32_t)v[6] | ((uint32_t)v[7] << 16)});
+    }
+  for (int i = t_; i < kRows * kH; i += 256) sdh[i] = 0.0f;
+  const int cm = t_ >> 4, cn = (t_ & 15) * 8;  // this thread's 8 cells
+  const int row = b0 + cm;
+  const bool live = row < B;
+  float dcn[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dcn[q] = 0.0f;
+  __syncthreads();
+
+  for (int t = T - 1; t >= 0; --t) {
+    float dg_i[8], dg_f[8], dg_g[8], dg_o[8];
+    if (live) {
+      const uint16_t* gp = gates + ((size_t)t * B + row) * (4 * kH) + cn;
+      const float* cp = cells + ((size_t)t * B + row) * kH + cn;
+      const float* cpp = t > 0 ? cells + ((size_t)(t - 1) * B + row) * kH + cn : nullptr;
+      const uint16_t* dyp = dy + ((size_t)row * T + t) * kH + cn;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float i = bf2f(gp[q]), f = bf2f(gp[kH + q]), g = bf2f(gp[2 * kH + q]), o = bf2f(gp[3 * kH + q]);
+        const float c = cp[q], cprev = cpp ? cpp[q] : 0.0f;
+        const float dh = bf2f(dyp[q]) + sdh[cm * kH + cn + q];
+        const float tc = tanh_f(c);
+        const float dc = dh * o * (1.0f - tc * tc) + dcn[q];
+        dg_o[q] = dh * tc * o * (1.0f - o);
+        dg_i[q] = dc * g * i * (1.0f - i);
+        dg_g[q] = dc * i * (1.0f - g * g);
+        dg_f[q] = dc * cprev * f * (1.0f - f);
+        dcn[q] = dc * f;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) dg_i[q] = dg_f[q] = dg_g[q] = dg_o[q] = 0.0f;
+    }
+    const float* dsrc[4] = {dg_i, dg_f, dg_g, dg_o};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t pk[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pk[q] = (uint32_t)f2bf(dsrc[k][2 * q]) | ((uint32_t)f2bf(dsrc[k][2 * q + 1]) << 16);
+      const u32x4 v{pk[0], pk[1], pk[2], pk[3]};
+      *reinterpret_cast<u32x4*>(sdg + cm * kGStride + k * kH + cn) = v;
+      if (live) *reinterpret_cast<u32x4*>(dgates + ((size_t)t * B + row) * (4 * kH) + k * kH + cn) = v;
+    }
+    __syncthreads();  // dgates_t complete; every read of dh_next done
+    f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(sdg + fr * kGStride + ks * 32 + fk * 8);
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn) acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[jn][ks], acc[jn], 0, 0, 0);
+    }
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sdh[(fk * 4 + e) * kH + w * 32 + jn * 16 + fr] = acc[jn][e];
+    __syncthreads();  // dh_next published; dgates buffer free
+  }
+}
+
 }  // namespace
+
+VGPU_API int vgpu_lstm_forward_train(const void* xp, const void* whh, void* y, void* gates, void* cells, int B,
+                                     int T, int H, hipStream_t s) {
+  if (H != kH || B < 1 || T < 1 || !gates || !cells) return -1;
+  hipLaunchKernelGGL(lstm_recurrence_kernel, dim3((B + kRows - 1) / kRows), dim3(256), 0, s,
+                     static_cast<const uint16_t*>(xp), static_cast<const uint16_t*>(whh), static_cast<uint16_t*>(y),
+                     static_cast<uint16_t*>(nullptr), static_cast<uint16_t*>(gates), static_cast<float*>(cells), B, T);
+  return (int)hipGetLastError();
+}
+
+VGPU_API int vgpu_lstm_backward(const void* gates, const void* cells, const void* dy, const void* whh, void* dgates,
+                                int B, int T, int H, hipStream_t s) {
+  if (H != kH || B < 1 || T < 1) return -1;
+  hipLaunchKernelGGL(lstm_backward_kernel, dim3((B + kRows - 1) / kRows), dim3(256), 0, s,
+                     static_cast<const uint16_t*>(gates), static_cast<const float*>(cells),
+                     static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(whh),
+                     static_cast<uint16_t*>(dgates), B, T);
+  return (int)hipGetLastError();
+}
 
 // Returns 0, or -1 for an unsupported shape (hidden size must be 128).
 VGPU_API int vgpu_lstm_recurrence(const void* xp, const void* whh, void* y, void* hlast, int B, int T, int H,
@@ -138,7 +267,7 @@ VGPU_API int vgpu_lstm_recurrence(const void* xp, const void* whh, void* y, void
   if (H != kH || B < 1 || T < 1) return -1;
   const int grid = (B + kRows - 1) / kRows;
   hipLaunchKernelGGL(lstm_recurrence_kernel, dim3(grid), dim3(256), 0, s, static_cast<const uint16_t*>(xp),
-                     static_cast<const uint16_t*>(whh), static_cast<uint16_t*>(y), static_cast<uint16_t*>(hlast), B,
-                     T);
+                     static_cast<const uint16_t*>(whh), static_cast<uint16_t*>(y), static_cast<uint16_t*>(hlast),
+                     static_cast<uint16_t*>(nullptr), static_cast<float*>(nullptr), B, T);
   return (int)hipGetLastError();
 }

@@ -79,3 +79,33 @@ def test_fused_lstm_matches_fp32(gpu_build, b, t, e, layers):
         want = ref(x.float())[0][:, -1]
         got = fused.lstm_last_hidden(ref.to(torch.bfloat16), x).float()
     torch.testing.assert_close(got, want, atol=3e-2, rtol=3e-2)
+
+
+def test_fused_lstm_training_grads_match_fp32(gpu_build):
+    """Forward + backward-through-time kernels (LSTMLayerFn) against
+    torch.nn.LSTM in fp32 on the same bf16-rounded weights: the loss, every
+    weight / bias gradient, and the input gradient of a 2-layer stack."""
+    import torch
+    from vgpu.ops import lstm as fused
+    torch.manual_seed(1)
+    b, t, e = 10, 40, 300
+    ref = torch.nn.LSTM(e, 128, num_layers=2, batch_first=True).cuda()
+    with torch.no_grad():
+        for p in ref.parameters():
+            p.copy_((p * 2.0).to(torch.bfloat16).float())
+    x = (torch.randn(b, t, e, device="cuda") * 0.5).to(torch.bfloat16)
+    head = torch.randn(128, device="cuda")
+    xr = x.float().requires_grad_(True)
+    (ref(xr)[0][:, -1] @ head).sum().backward()
+    mod = torch.nn.LSTM(e, 128, num_layers=2, batch_first=True).cuda().to(torch.bfloat16)
+    with torch.no_grad():
+        for p, q in zip(mod.parameters(), ref.parameters()):
+            p.copy_(q.to(torch.bfloat16))
+    xb = x.clone().requires_grad_(True)
+    (fused.lstm_forward_train(mod, xb)[:, -1].float() @ head).sum().backward()
+    for (name, p), q in zip(mod.named_parameters(), ref.parameters()):
+        scale = q.grad.abs().max().item() + 1e-6
+        err = (p.grad.float() - q.grad).abs().max().item() / scale
+        assert err < 0.05, (name, err)
+    err = (xb.grad.float() - xr.grad).abs().max().item() / (xr.grad.abs().max().item() + 1e-6)
+    assert err < 0.05, ("x", err)

@@ -186,5 +186,7 @@ class LSTMSentiment(nn.Module):
         from vgpu.ops import lstm as fused
         if not self.training and fused.supported(self.lstm, x):
             return self.fc(fused.lstm_last_hidden(self.lstm, x))  # native recurrence kernel
+        if self.training and fused.supported(self.lstm, x, training=True):
+            return self.fc(fused.lstm_forward_train(self.lstm, x)[:, -1])  # native forward + backward kernels
         y, _ = self.lstm(x)
         return self.fc(y[:, -1])

@@ -64,6 +64,10 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_conv_set_big.argtypes = [ci]
     lib.vgpu_lstm_recurrence.argtypes = [vp, vp, vp, vp, ci, ci, ci, vp]
     lib.vgpu_lstm_recurrence.restype = ci
+    lib.vgpu_lstm_forward_train.argtypes = [vp] * 5 + [ci, ci, ci, vp]
+    lib.vgpu_lstm_forward_train.restype = ci
+    lib.vgpu_lstm_backward.argtypes = [vp] * 5 + [ci, ci, ci, vp]
+    lib.vgpu_lstm_backward.restype = ci
     lib.vgpu_scale_shift_relu_mean_nhwc.argtypes = [vp, vp, vp, vp, ci, ci, ci, vp]
     i64, cf = ctypes.c_int64, ctypes.c_float
     lib.vgpu_bn_workspace.argtypes = [i64, ci]
