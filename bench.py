@@ -69,7 +69,7 @@ def main(argv=None) -> int:
                     help="ResNet convolutions: fused MFMA implicit-GEMM kernels or MIOpen")
     ap.add_argument("--hw-queues", type=int, default=1,
                     help="GPU_MAX_HW_QUEUES per pod (vGPU HW-queue budget; 0 = runtime default)")
-    ap.add_argument("--cu-share", choices=("hybrid", "mask", "temporal", "group2", "group2i"), default="hybrid",
+    ap.add_argument("--cu-share", choices=("hybrid", "mask", "temporal", "group2", "group2i"), default="temporal",
                     help="compute-share policy of fractional pods: the device plugin's "
                          "(hybrid|mask|temporal, vgpu/deviceplugin/custate.py) or an A/B tool")
     ap.add_argument("--core-policy", choices=("default", "force", "disable"), default="default",

@@ -43,7 +43,7 @@ def test_cpx_partition_layout():
 
 
 def test_state_uses_per_device_layout(tmp_path):
-    st = CUMaskState(str(tmp_path))
+    st = CUMaskState(str(tmp_path), policy="mask")
     got = st.allocate("u_c", [("CPX-0", 50), ("SPX-0", 50)],
                       {"CPX-0": CULayout(32, 1), "SPX-0": MI355X})
     assert popcount(got["CPX-0"].mask) == 16 and popcount(got["SPX-0"].mask) == 128

@@ -187,7 +187,7 @@ def cluster(tmp_path):
     sockdir.mkdir()
     kubelet = FakeKubelet(str(sockdir / "kubelet.sock"))
     cfg = DevicePluginConfig(node_name="n1", device_split_count=4, socket_dir=str(sockdir),
-                             host_lib_dir=str(tmp_path / "host"), config_file="")
+                             host_lib_dir=str(tmp_path / "host"), config_file="", cu_share="mask")
     srv.add_node("n1")
     backend = StaticBackend(mi355x_node(8))
     plugin = VGPUDevicePlugin(cfg, backend, client, "n1")

@@ -66,7 +66,7 @@ def _host_path(value: str, mounts: list) -> str:
     return value
 
 
-def admit_pods(specs: list, device_index: int, workdir: str, *, policy: str = "hybrid",
+def admit_pods(specs: list, device_index: int, workdir: str, *, policy: str = "temporal",
                max_mask_slots: int = 2, memory_scaling: float = 1.0,
                device: Device | None = None) -> list[AdmittedPod]:
     """Admit `specs` (vgpu.bench.launch.PodSpec) onto one physical GPU."""

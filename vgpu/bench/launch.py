@@ -86,7 +86,7 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
                 graph: bool = True, cap_probe: bool = False, find: bool = False,
                 workdir: str | None = None, oversubscribe: bool = False,
                 hw_queues: int | None = None, fused: bool = True,
-                conv: str = "native", cu_share: str = "hybrid", memory_scaling: float = 1.0) -> list[Pod]:
+                conv: str = "native", cu_share: str = "temporal", memory_scaling: float = 1.0) -> list[Pod]:
     """Start one process per pod on physical device `device`.
 
     cu_share: how a fractional pod's compute share is enforced.

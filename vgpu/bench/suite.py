@@ -3,12 +3,14 @@ publishes (BASELINE.md rows 1.1–5.2) in three scenarios, mirroring the
 reference's comparison (README.md:234-257):
 
   exclusive          — one pod, whole GPU, no enforcement library
-  vgpu               — 2 pods × gpucores=50, gpumem=144000 (BASELINE.json config 2)
-  vgpu-temporal      — the same 2 pods in the GPU's temporal pool (no CU masks)
-  vgpu-cu25          — 4 pods × gpucores=25 (BASELINE.json config 3), device-plugin
-                       default share policy (hybrid: 2 CU masks + a temporal pool)
-  vgpu-cu25-temporal — the same 4 pods, all under the GPU-time limiter
+  vgpu               — 2 pods × gpucores=50, gpumem=144000 (BASELINE.json config 2),
+                       device-plugin default share policy (temporal pool)
+  vgpu-temporal      — the same, policy named explicitly
+  vgpu-mask          — the same 2 pods, one CU mask each
+  vgpu-cu25          — 4 pods × gpucores=25 (BASELINE.json config 3), default policy
+  vgpu-cu25-temporal — the same 4 pods, policy named explicitly
   vgpu-cu25-mask     — the same 4 pods, one CU mask each
+  vgpu-cu25-hybrid   — 2 CU masks + a temporal pool for the other two
 
 Prints one JSON line per (test, scenario) and a markdown table at the end.
     python -m vgpu.bench.suite [--tests 1.1,1.2,...] [--steps 20]
@@ -27,6 +29,8 @@ SCENARIOS = {
     "exclusive": ["--pods", "1", "--no-shim", "--gpucores", "100", "--gpumem", "0"],
     "vgpu": ["--pods", "2", "--gpucores", "50", "--gpumem", "144000"],
     "vgpu-temporal": ["--pods", "2", "--gpucores", "50", "--gpumem", "144000", "--cu-share", "temporal"],
+    "vgpu-mask": ["--pods", "2", "--gpucores", "50", "--gpumem", "144000", "--cu-share", "mask"],
+    "vgpu-cu25-hybrid": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "hybrid"],
     "vgpu-cu25": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000"],
     "vgpu-cu25-temporal": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "temporal"],
     "vgpu-cu25-mask": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "mask"],

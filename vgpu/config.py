@@ -53,11 +53,14 @@ class DevicePluginConfig:
     hsa_tools_intercept: bool = False     # also hand the shim ROCr's API table (HSA_TOOLS_LIB)
     partition_mode: str = ""             # SPX|DPX|QPX|CPX expected compute partition ("" = as found)
     # How a fractional vGPU's compute share is enforced (vgpu/deviceplugin/custate.py):
-    #   mask      an XCD-balanced CU mask per container (temporal only when no granules are free)
-    #   temporal  no per-container mask: the shim's GPU-time limiter with fair-share charging
+    #   temporal  (default) no per-container mask: the shim's GPU-time limiter with
+    #             work-conserving fair-share charging — the reference's time-sliced SM
+    #             limit; measured best or equal on 2 x 50 % and 4 x 25 % (docs/benchmarks.md)
+    #   mask      an XCD-balanced CU mask per container (spatial isolation; temporal only
+    #             when no granules are free)
     #   hybrid    CU masks for the first `max_mask_slots` fractional containers of a GPU, the
     #             rest share the remaining CUs (one pool mask) under the temporal limiter
-    cu_share: str = "hybrid"
+    cu_share: str = "temporal"
     max_mask_slots: int = 2
     rocr_cu_mask: bool = True             # also hand the masks to ROCr (HSA_CU_MASK: internal queues too)
     host_lock_dir: str = "/tmp/vgpulock"  # node-wide unified lock + per-GPU share boards

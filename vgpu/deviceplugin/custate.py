@@ -15,13 +15,16 @@ profiles/sharing_4way_r1.md and profiles/temporal_r2.md):
 
 * ``mask``: every fractional container gets its own XCD-balanced CU mask.
   When no granules are free, the container gets the pool instead.
-* ``temporal``: no per-container masks. Every fractional container is a pool
-  member: the shim's GPU-time limiter, charged through the per-GPU fair-share
-  board. On MI355X, 4 x 25 % temporal pods run at 1.04-1.06 x the exclusive
-  GPU, against 0.65 x with four masks.
-* ``hybrid`` (default): the first ``max_mask_slots`` fractional containers on a
-  GPU get masks, which is exact isolation. With two or fewer masked pods on a
-  GPU, masks still beat the exclusive GPU. Later containers join the pool.
+* ``temporal`` (default): no per-container masks. Every fractional container
+  is a pool member: the shim's GPU-time limiter, charged through the per-GPU
+  fair-share board. It throttles only under contention (work-conserving) and
+  is the reference's time-sliced SM limit. On MI355X, 4 x 25 % temporal pods
+  run at >= 0.96 x the exclusive GPU on all 10 ai-benchmark tests, against
+  0.65 x with four masks on ResNet-50. 2 x 50 % pods match or beat two masks
+  on 9 of 10 tests; the flagship goes from 24.2k to 25.4k images/s.
+* ``hybrid``: the first ``max_mask_slots`` fractional containers on a GPU get
+  masks, which is exact spatial isolation at equal throughput for two sharers.
+  Later containers join the pool.
 
 The pool of a device is every CU not held by a masked container; pool members
 share it in time. The shim scales a pool member's time limit by
@@ -59,7 +62,7 @@ class ShareGrant:
 
 
 class CUMaskState:
-    def __init__(self, containers_dir: str, layout: CULayout = MI355X, policy: str = "hybrid",
+    def __init__(self, containers_dir: str, layout: CULayout = MI355X, policy: str = "temporal",
                  max_mask_slots: int = 2, pack: str | None = None):
         if policy not in POLICIES:
             raise ValueError(f"cu_share policy must be one of {POLICIES}, got {policy!r}")
