@@ -42,7 +42,8 @@ def enforcement_label(args) -> str:
     if args.no_shim:
         return "none"
     if args.gpucores <= 0 or args.gpucores >= 100:
-        return "libvgpu.so (HBM cap; whole GPU, no compute limit)"
+        vm = " + virtual device memory" if args.oversubscribe or args.memory_scaling > 1 else ""
+        return f"libvgpu.so (HBM cap{vm}; whole GPU, no compute limit)"
     if args.cu_share == "group2":
         return "libvgpu.so (HBM cap + one CU mask per pod pair 2k,2k+1)"
     if args.cu_share == "group2i":
@@ -74,6 +75,10 @@ def main(argv=None) -> int:
                          "(hybrid|mask|temporal, vgpu/deviceplugin/custate.py) or an A/B tool")
     ap.add_argument("--core-policy", choices=("default", "force", "disable"), default="default",
                     help="GPU_CORE_UTILIZATION_POLICY of the pods (reference docs/config.md:34-38)")
+    ap.add_argument("--oversubscribe", action="store_true",
+                    help="virtual device memory (VGPU_OVERSUBSCRIBE): pod caps may exceed physical HBM")
+    ap.add_argument("--memory-scaling", type=float, default=1.0,
+                    help="device plugin --device-memory-scaling (reference README.md:283-287)")
     ap.add_argument("--no-cap-probe", action="store_true")
     ap.add_argument("--ready-timeout", type=float, default=1500.0)
     ap.add_argument("--cpu-smoke", action="store_true",
@@ -114,7 +119,8 @@ def main(argv=None) -> int:
     pods = launch_pods(specs, device, steps=args.steps, warmup=args.warmup, shim=not args.no_shim,
                        graph=not args.no_graph, cap_probe=not args.no_cap_probe,
                        find=not args.no_find, hw_queues=args.hw_queues or None,
-                       fused=not args.no_fused, conv=args.conv, cu_share=args.cu_share)
+                       fused=not args.no_fused, conv=args.conv, cu_share=args.cu_share,
+                       oversubscribe=args.oversubscribe, memory_scaling=args.memory_scaling)
     try:
         for p in pods:
             p.ready = p.read_tagged("READY", args.ready_timeout, progress=log)
@@ -199,6 +205,8 @@ def main(argv=None) -> int:
                 "hw_queues_per_pod": args.hw_queues,
                 "cu_share": args.cu_share,
                 "core_policy": args.core_policy,
+                "oversubscribe": args.oversubscribe or args.memory_scaling > 1,
+                "memory_scaling": args.memory_scaling,
             },
             "per_gpu_images_s": round(per_gpu, 2),
             "per_pod_images_s": [round(p.done["throughput"], 2) for p in pods],

@@ -11,6 +11,11 @@ reference's comparison (README.md:234-257):
   vgpu-cu25-temporal — the same 4 pods, policy named explicitly
   vgpu-cu25-mask     — the same 4 pods, one CU mask each
   vgpu-cu25-hybrid   — 2 CU masks + a temporal pool for the other two
+  vgpu-vmem          — the reference's "vGPU + virtual device memory" column:
+                       2 pods per GPU on a plugin with --device-memory-scaling=1.8,
+                       each capped at 230000 MiB (together 1.7 x the physical HBM,
+                       so the caps oversubscribe it) and no compute limit (reference benchmarks/ai-benchmark/
+                       vGPU-device-plugin(virtual device memory)/ai-benchmark.yml)
 
 Prints one JSON line per (test, scenario) and a markdown table at the end.
     python -m vgpu.bench.suite [--tests 1.1,1.2,...] [--steps 20]
@@ -34,6 +39,8 @@ SCENARIOS = {
     "vgpu-cu25": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000"],
     "vgpu-cu25-temporal": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "temporal"],
     "vgpu-cu25-mask": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "mask"],
+    "vgpu-vmem": ["--pods", "2", "--gpucores", "0", "--gpumem", "230000", "--oversubscribe",
+                  "--memory-scaling", "1.8"],
     "vgpu-cu25-temporal-q0": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "temporal",
                               "--hw-queues", "0"],
 }
