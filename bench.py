@@ -52,7 +52,7 @@ def enforcement_label(args) -> str:
             "per-pod XCD-balanced CU masks and/or GPU-time limiter with fair-share board")
 
 
-def main(argv=None) -> int:
+def make_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
@@ -83,7 +83,11 @@ def main(argv=None) -> int:
     ap.add_argument("--ready-timeout", type=float, default=1500.0)
     ap.add_argument("--cpu-smoke", action="store_true",
                     help="rehearse the multi-rank orchestration on CPU (tests; not a measurement)")
-    args = ap.parse_args(argv)
+    return ap
+
+
+def main(argv=None) -> int:
+    args = make_parser().parse_args(argv)
     if args.cpu_smoke:
         os.environ["VGPU_BENCH_CPU"] = "1"
         args.no_shim = True

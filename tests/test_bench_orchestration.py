@@ -66,3 +66,24 @@ def test_bench_eight_ranks_gloo_cpu_placement():
     assert [x["uuids"] for x in pl] == [[f"GPU-bench-{i}"] for i in range(8)]
     regions = [reg for x in pl for reg in x["regions"]]
     assert len(set(regions)) == 8 and all(regions)
+
+
+def test_ab_recipes_and_suite_scenarios_are_valid_bench_flags():
+    """Every A/B recipe variant (scripts/bench_ab.py) and suite scenario parses
+    with bench.py's own argument parser."""
+    import importlib.util
+    import bench
+    from vgpu.bench.suite import SCENARIOS
+    spec = importlib.util.spec_from_file_location("bench_ab", os.path.join(REPO, "scripts", "bench_ab.py"))
+    ab = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ab)
+    p = bench.make_parser()
+    for name, (base, variants, secs) in ab.RECIPES.items():
+        assert secs > 0
+        for tag, env, flags in variants:
+            p.parse_args(["--no-cap-probe", *base, *flags])
+    for flags in SCENARIOS.values():
+        p.parse_args(flags)
+    a = p.parse_args(SCENARIOS["vgpu-vmem"])
+    assert a.oversubscribe and a.memory_scaling == 1.8
+    assert a.pods * a.gpumem * (1 << 20) > 288e9  # the caps oversubscribe the physical HBM
