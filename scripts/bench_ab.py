@@ -34,6 +34,18 @@ RECIPES: dict[str, tuple[list, list, int]] = {
         ("mask", {}, ["--cu-share", "mask"]),
         ("exclusive", {}, EXCL),
     ], 300),
+    # Depth-first micro-batches over the first stages (VGPU_DF_CHUNKS / VGPU_DF_BLOCKS).
+    "depth-first": (["--steps", "30", "--warmup", "10"], [
+        ("base", {}, []),
+        ("c2_b3", {"VGPU_DF_CHUNKS": "2", "VGPU_DF_BLOCKS": "3"}, []),
+        ("c2_b7", {"VGPU_DF_CHUNKS": "2", "VGPU_DF_BLOCKS": "7"}, []),
+        ("c5_b3", {"VGPU_DF_CHUNKS": "5", "VGPU_DF_BLOCKS": "3"}, []),
+        ("c5_b7", {"VGPU_DF_CHUNKS": "5", "VGPU_DF_BLOCKS": "7"}, []),
+        ("c2_all", {"VGPU_DF_CHUNKS": "2"}, []),
+        ("c5_all", {"VGPU_DF_CHUNKS": "5"}, []),
+        ("excl", {}, EXCL),
+        ("excl_c5_b7", {"VGPU_DF_CHUNKS": "5", "VGPU_DF_BLOCKS": "7"}, EXCL),
+    ], 300),
     # Temporal limiter accuracy and fair share (profiles/temporal_r2.md).
     "temporal": (["--steps", "150"], [
         ("excl", {}, EXCL),

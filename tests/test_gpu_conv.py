@@ -147,6 +147,25 @@ def test_native_resnet_matches_module(gpu_build):
     assert rel < 0.05, float(rel)
 
 
+@pytest.mark.parametrize("blocks", [7, 1000])
+def test_native_resnet_depth_first_chunks(gpu_build, monkeypatch, blocks):
+    """VGPU_DF_CHUNKS: the stem and the first stages run on micro-batches one
+    after the other; the result equals the whole-batch forward."""
+    from vgpu.models.resnet import FusedResNetV2Inference, resnet_v2_50
+    torch.manual_seed(0)
+    m = resnet_v2_50().cuda().eval().to(torch.bfloat16).to(memory_format=CL)
+    x = torch.randn(5, 3, 96, 96, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=CL)
+    ref = FusedResNetV2Inference(m, conv="native")(x).float()
+    monkeypatch.setenv("VGPU_DF_CHUNKS", "2")
+    monkeypatch.setenv("VGPU_DF_BLOCKS", str(blocks))
+    fm = FusedResNetV2Inference(m, conv="native")
+    assert fm.df_chunks == 2 and fm.df_blocks == min(blocks, 16)
+    got = fm(x).float()
+    assert got.shape == ref.shape
+    rel = (got - ref).norm() / ref.norm()
+    assert rel < 1e-2, float(rel)
+
+
 def test_native_vgg_matches_module(gpu_build):
     from vgpu.models.vision import VGG16, NativeVGG16Inference
     torch.manual_seed(0)

@@ -159,6 +159,50 @@ def test_ddp_over_rccl_under_the_shim(gpu_build):
     assert res["backend"] == "nccl" and res["value"] > 0 and res["final_loss"] == res["final_loss"]
 
 
+def test_two_ddp_ranks_share_one_gpu_under_the_shim(gpu_build, tmp_path):
+    """Two data-parallel training ranks on the ONE GPU of the box, each a
+    capped 50 % vGPU with its own shared region (what two pods of one job get
+    on a shared GPU).  RCCL refuses two ranks on one device, so gradients go
+    over gloo; the replicas must end with identical weights and each region
+    must show only its own process's memory."""
+    import socket
+    from vgpu.native import preload_env
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    # per-rank region: torchrun's children inherit one env, so a tiny wrapper
+    # picks VGPU_SHARED_REGION from LOCAL_RANK before anything loads HIP.
+    env = preload_env(dict(os.environ))
+    env.update({"VGPU_DEVICE_MEMORY_LIMIT_0": "16g", "VGPU_DEVICE_CU_LIMIT_0": "50",
+                "VGPU_REGION_TEMPLATE": str(tmp_path / "rank{rank}" / "vgpu.cache"),
+                "PYTHONPATH": REPO + os.pathsep + env.get("PYTHONPATH", "")})
+    for r in range(2):
+        (tmp_path / f"rank{r}").mkdir()
+    code = ("import os,runpy,sys;"
+            "os.environ['VGPU_SHARED_REGION']=os.environ['VGPU_REGION_TEMPLATE'].format(rank=os.environ['LOCAL_RANK']);"
+            "sys.argv=['ddp']+sys.argv[1:];runpy.run_module('vgpu.parallel.ddp',run_name='__main__')")
+    wrapper = tmp_path / "rank_wrapper.py"
+    wrapper.write_text(code)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr=127.0.0.1", f"--master-port={port}", str(wrapper),
+                        "--workload", "1.2", "--steps", "3", "--warmup", "2", "--batch", "4", "--size", "128",
+                        "--backend", "gloo", "--device", "cuda"],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    print(res)
+    assert res["world"] == 2 and res["device"].startswith("cuda") and res["weights_in_sync"]
+    from vgpu.monitor.region import AttachedRegion
+    for rk in range(2):
+        reg = AttachedRegion(str(tmp_path / f"rank{rk}" / "vgpu.cache"))
+        try:
+            devs = reg.devices()
+            assert len(devs) == 1 and devs[0].mem_limit == 16 << 30 and devs[0].cu_limit == 50, (rk, devs)
+        finally:
+            reg.close()
+
+
 def test_array_3d_module_allocations_capped(gpu_build):
     """under an 8 GiB cap, hipMalloc3D and hipMallocArray past
     the cap fail, a hipModuleLoadData is charged to the module class, and the

@@ -75,3 +75,4 @@ def test_ddp_entry_point_under_torchrun():
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     res = json.loads(line)
     assert res["world"] == 2 and res["backend"] == "gloo" and res["value"] > 0
+    assert res["weights_in_sync"]

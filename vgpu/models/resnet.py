@@ -136,6 +136,9 @@ class FusedResNetV2Inference(nn.Module):
         self.fuse_tail = os.environ.get("VGPU_FUSE_TAIL", "1") != "0"
         # ... and the next identity block's conv1 into that tail (VGPU_FUSE_NEXT=0 disables)
         self.fuse_next = self.fuse_tail and os.environ.get("VGPU_FUSE_NEXT", "1") != "0"
+        # depth-first micro-batches over the first VGPU_DF_BLOCKS blocks (A/B knob)
+        self.df_chunks = int(os.environ.get("VGPU_DF_CHUNKS", "1"))
+        df_blocks = int(os.environ.get("VGPU_DF_BLOCKS", "1000"))
         from vgpu.ops.fused import bn_scale_shift
         m = m.eval()
         dt = m.stem.weight.dtype
@@ -166,6 +169,9 @@ class FusedResNetV2Inference(nn.Module):
                 })
             self.out_ss = bn_scale_shift(m.bn_out)
             self.fc = m.fc
+        # round the chunked prefix down to a stage start (a block with a projection shortcut)
+        starts = [i for i, b in enumerate(self.blocks) if b["sc"] is not None] + [len(self.blocks)]
+        self.df_blocks = max([s for s in starts if s <= df_blocks] or [len(self.blocks)])
 
     @torch.no_grad()
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -175,10 +181,33 @@ class FusedResNetV2Inference(nn.Module):
 
     def _forward_native(self, x: torch.Tensor) -> torch.Tensor:
         from vgpu.ops import conv as C
-        x = C.stem_conv(x.contiguous(memory_format=torch.channels_last), self.stem_w_s2d)
+        x = x.contiguous(memory_format=torch.channels_last)
+        k = min(self.df_chunks, x.shape[0])
+        if k > 1:
+            # Depth-first: the stem and the first df_blocks blocks run on k
+            # micro-batches one after the other, so each chunk's block
+            # activations are re-read from the 256 MB Infinity Cache instead
+            # of HBM; the rest of the network runs on the whole batch.
+            nb = self.df_blocks
+            outs = [self._blocks_native(C.maxpool3s2(C.stem_conv(xc, self.stem_w_s2d)), 0, nb)
+                    for xc in x.tensor_split(k, dim=0)]
+            if nb >= len(self.blocks):
+                return self.fc(torch.cat([C.scale_shift_relu_mean(o, *self.out_ss) for o in outs]))
+            x = torch.cat(outs).contiguous(memory_format=torch.channels_last)
+            x = self._blocks_native(x, nb, len(self.blocks))
+            return self.fc(C.scale_shift_relu_mean(x, *self.out_ss))
+        x = C.stem_conv(x, self.stem_w_s2d)
         x = C.maxpool3s2(x)
+        x = self._blocks_native(x, 0, len(self.blocks))
+        return self.fc(C.scale_shift_relu_mean(x, *self.out_ss))
+
+    def _blocks_native(self, x: torch.Tensor, first: int, last: int) -> torch.Tensor:
+        """Blocks [first, last); `last` must start a stage (or be the end) so no
+        fused next-block conv1 output crosses the boundary."""
+        from vgpu.ops import conv as C
         h_next = None
-        for i, b in enumerate(self.blocks):
+        for i in range(first, last):
+            b = self.blocks[i]
             pro = b["in"]
             if b["sc"] is None:
                 sc = x
@@ -186,7 +215,7 @@ class FusedResNetV2Inference(nn.Module):
                 sc = C.conv2d(x, b["sc"][0], stride=b["sc"][1], pro=pro)
             h = h_next if h_next is not None else C.conv2d(x, b["w1"], b["b1"], act="relu", pro=pro)
             h_next = None
-            nb = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
+            nb = self.blocks[i + 1] if i + 1 < last else None
             if (self.fuse_next and nb is not None and nb["sc"] is None
                     and C.conv23_supported(h.shape[1])):
                 # conv2 + conv3 + residual + the next block's BN+ReLU+conv1 (stages 1-2)
@@ -198,7 +227,7 @@ class FusedResNetV2Inference(nn.Module):
             else:
                 h = C.conv2d(h, b["w2"], b["b2"], stride=b["stride"], padding=1, act="relu")
                 x = C.conv2d(h, b["w3"], residual=sc)
-        return self.fc(C.scale_shift_relu_mean(x, *self.out_ss))
+        return x
 
     def _forward_miopen(self, x: torch.Tensor) -> torch.Tensor:
         from vgpu.ops.fused import add_scale_shift_act, bias_act_, scale_shift_act

@@ -29,8 +29,12 @@ import os
 import time
 
 
-def setup(backend: str | None = None):
-    """init_process_group from torchrun's env; returns (rank, world, device)."""
+def setup(backend: str | None = None, device: str | None = None):
+    """init_process_group from torchrun's env; returns (rank, world, device).
+
+    device="cuda" with backend="gloo" keeps the model on the GPU and reduces
+    over gloo: the only way to put several ranks on ONE GPU, which RCCL refuses
+    ("Duplicate GPU detected", profiles/r2/rccl_two_ranks_one_gpu.log)."""
     import torch
     import torch.distributed as dist
     rank = int(os.environ.get("RANK", "0"))
@@ -38,7 +42,7 @@ def setup(backend: str | None = None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
-    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    use_gpu = torch.cuda.is_available() and (backend != "gloo" or device == "cuda")
     if use_gpu:
         torch.cuda.set_device(local % torch.cuda.device_count())
         device = torch.device("cuda", torch.cuda.current_device())
@@ -78,10 +82,10 @@ def wrap(model, device, bucket_mb: int = 64):
 
 def train(workload: str = "1.2", steps: int = 20, warmup: int = 5, bucket_mb: int = 64,
           backend: str | None = None, shrink: bool = False, batch: int | None = None,
-          size: int | None = None) -> dict:
+          size: int | None = None, device: str | None = None) -> dict:
     import torch
     import torch.distributed as dist
-    rank, world, device = setup(backend)
+    rank, world, device = setup(backend, device)
     torch.manual_seed(1234)  # identical initial weights on every rank (DDP also broadcasts)
     w, model = build_model(workload, device, shrink=shrink)
     ddp = wrap(model, device, bucket_mb)
@@ -118,12 +122,18 @@ def train(workload: str = "1.2", steps: int = 20, warmup: int = 5, bucket_mb: in
     dist.barrier()
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], dtype=torch.float64, device=device if backend != "gloo" and device.type == "cuda" else "cpu")
+    # every rank must end with the same weights (the all-reduce worked)
+    chk = torch.stack([p.detach().float().sum() for p in model.parameters()]).sum().reshape(1).cpu().double()
+    chk_max, chk_min = chk.clone(), chk.clone()
+    dist.all_reduce(chk_max, op=dist.ReduceOp.MAX)
+    dist.all_reduce(chk_min, op=dist.ReduceOp.MIN)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall = float(t[0])
     res = {"metric": "ddp training images/s", "workload": workload, "world": world,
            "value": round(bsz * world * steps / wall, 2), "unit": "images/s",
            "ms_per_step": round(1e3 * wall / steps, 3), "bucket_mb": bucket_mb,
-           "backend": dist.get_backend(), "final_loss": float(loss.detach().float())}
+           "backend": dist.get_backend(), "device": str(device), "final_loss": float(loss.detach().float()),
+           "weights_in_sync": bool(float(chk_max[0]) == float(chk_min[0]))}
     return res
 
 
@@ -134,13 +144,14 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bucket-mb", type=int, default=64)
     ap.add_argument("--backend", default=None, help="nccl (RCCL) on GPU, gloo on CPU by default")
+    ap.add_argument("--device", default=None, help="cuda: keep the model on the GPU even over gloo")
     ap.add_argument("--shrink", action="store_true", help="one-block-per-stage model (CPU rehearsal)")
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--size", type=int, default=None)
     args = ap.parse_args(argv)
     import torch.distributed as dist
     res = train(args.workload, args.steps, args.warmup, args.bucket_mb, args.backend, args.shrink,
-                args.batch, args.size)
+                args.batch, args.size, args.device)
     if dist.get_rank() == 0:
         print(json.dumps(res), flush=True)
     dist.destroy_process_group()
