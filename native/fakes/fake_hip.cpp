@@ -124,7 +124,15 @@ uint64_t timeline_last_end() {
 
 struct FakeEvent {
   uint64_t at = 0;
+  hipStream_t stream = nullptr;  // where it was last recorded
 };
+
+// Stream capture, as the runtime behaves: a capture is invalidated when an
+// event recorded on the capturing stream is queried before the capture ends
+// (hipErrorStreamCaptureInvalidated at hipStreamEndCapture).
+// VGPU_FAKE_QUERY_US widens hipEventQuery so tests can hit that window.
+std::mutex g_cap_mu;
+std::map<hipStream_t, bool> g_capturing;  // stream -> invalidated
 
 hsa_status_t pick_gpu(hsa_agent_t a, void* data) {
   auto* v = (std::vector<hsa_agent_t>*)data;
@@ -225,13 +233,24 @@ hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) {
   return hipSuccess;
 }
 hipError_t hipEventCreate(hipEvent_t* e) { return hipEventCreateWithFlags(e, 0); }
-hipError_t hipEventRecord(hipEvent_t e, hipStream_t) {
+hipError_t hipEventRecord(hipEvent_t e, hipStream_t stream) {
   if (!e) return hipErrorInvalidHandle;
   reinterpret_cast<FakeEvent*>(e)->at = timeline_last_end();
+  reinterpret_cast<FakeEvent*>(e)->stream = stream;
   return hipSuccess;
 }
 hipError_t hipEventQuery(hipEvent_t e) {
   if (!e) return hipErrorInvalidHandle;
+  static const int delay_us = getenv("VGPU_FAKE_QUERY_US") ? atoi(getenv("VGPU_FAKE_QUERY_US")) : 0;
+  if (delay_us > 0) usleep(delay_us);
+  {
+    std::lock_guard<std::mutex> g(g_cap_mu);
+    auto it = g_capturing.find(reinterpret_cast<FakeEvent*>(e)->stream);
+    if (it != g_capturing.end()) {
+      it->second = true;
+      return hipErrorStreamCaptureUnsupported;
+    }
+  }
   return now_ns() >= reinterpret_cast<FakeEvent*>(e)->at ? hipSuccess : hipErrorNotReady;
 }
 hipError_t hipEventSynchronize(hipEvent_t e) {
@@ -243,8 +262,12 @@ hipError_t hipEventDestroy(hipEvent_t e) {
   delete reinterpret_cast<FakeEvent*>(e);
   return hipSuccess;
 }
-hipError_t hipStreamIsCapturing(hipStream_t, hipStreamCaptureStatus* st) {
-  if (st) *st = hipStreamCaptureStatusNone;
+hipError_t hipStreamIsCapturing(hipStream_t s, hipStreamCaptureStatus* st) {
+  std::lock_guard<std::mutex> g(g_cap_mu);
+  auto it = g_capturing.find(s);
+  if (st)
+    *st = it == g_capturing.end() ? hipStreamCaptureStatusNone
+                                  : (it->second ? hipStreamCaptureStatusInvalidated : hipStreamCaptureStatusActive);
   return hipSuccess;
 }
 hipError_t hipThreadExchangeStreamCaptureMode(hipStreamCaptureMode*) { return hipSuccess; }
@@ -329,10 +352,20 @@ hipError_t hipMemGetAddressRange(hipDeviceptr_t* base, size_t* size, hipDevicept
   *size = jt->second;
   return hipSuccess;
 }
-hipError_t hipStreamBeginCapture(hipStream_t, hipStreamCaptureMode) { return hipSuccess; }
-hipError_t hipStreamEndCapture(hipStream_t, hipGraph_t* g) {
-  if (g) *g = nullptr;
+hipError_t hipStreamBeginCapture(hipStream_t s, hipStreamCaptureMode) {
+  std::lock_guard<std::mutex> g(g_cap_mu);
+  if (g_capturing.count(s)) return hipErrorIllegalState;
+  g_capturing[s] = false;
   return hipSuccess;
+}
+hipError_t hipStreamEndCapture(hipStream_t s, hipGraph_t* g) {
+  if (g) *g = nullptr;
+  std::lock_guard<std::mutex> lk(g_cap_mu);
+  auto it = g_capturing.find(s);
+  if (it == g_capturing.end()) return hipErrorIllegalState;
+  const bool invalid = it->second;
+  g_capturing.erase(it);
+  return invalid ? hipErrorStreamCaptureInvalidated : hipSuccess;
 }
 
 hipError_t hipMalloc(void** p, size_t size) { return dev_alloc(p, size, tl_dev); }

@@ -213,12 +213,10 @@ void configure() {
   g_throttle_any.store(any, std::memory_order_release);
 }
 
-// Record one marker on `stream` (caller holds L.mu).  From the limiter thread
-// the record is made under the capture guard: a capture that begins on the
-// stream must not swallow our event.  Returns 1 when a marker was recorded.
-int record_marker(DevLimiter& L, hipStream_t stream, StreamTrack& t, bool from_app) {
-  std::shared_lock<std::shared_mutex> cap(g_capture_mu, std::defer_lock);
-  if (!from_app) cap.lock();
+// Record one marker on `stream` (caller holds L.mu; the limiter thread also
+// holds the capture guard, so a capture cannot begin on the stream and swallow
+// our event).  Returns 1 when a marker was recorded.
+int record_marker(DevLimiter& L, hipStream_t stream, StreamTrack& t) {
   if (g_open_captures.load(std::memory_order_acquire) > 0) return 0;
   hipEvent_t ev = nullptr;
   if (!L.free_ev.empty()) {
@@ -240,8 +238,17 @@ int record_marker(DevLimiter& L, hipStream_t stream, StreamTrack& t, bool from_a
 }
 
 // Poll the oldest markers of every stream of `dev`; charge completed intervals.
+//
+// The whole poll runs under the capture guard (shared): hipStreamBeginCapture
+// (exclusive) waits for a poll in progress, and no poll starts while a capture
+// is open.  Without it a poll that passed the open-captures check could query
+// a marker of a stream whose capture began a moment later, and the runtime
+// invalidates that capture (seen on MI355X: a torch graph capture on a stream
+// with markers from its eager warm-up failed at its first kernel with
+// hipErrorStreamCaptureInvalidated).
 bool reap(int dev, DevLimiter& L, uint64_t now_hint) {
   if (L.outstanding.load(std::memory_order_relaxed) == 0) return false;
+  std::shared_lock<std::shared_mutex> cap(g_capture_mu);
   if (g_open_captures.load(std::memory_order_acquire) > 0) return true;  // poll after the capture
   auto query = REAL_HIP(hipEventQuery);
   std::lock_guard<std::mutex> g(L.mu);
@@ -262,7 +269,7 @@ bool reap(int dev, DevLimiter& L, uint64_t now_hint) {
       ++done;
     }
     // Launches since the last marker are still uncovered: cover them now.
-    if (q.empty() && t.dirty) added += record_marker(L, it->first, t, /*from_app=*/false);
+    if (q.empty() && t.dirty) added += record_marker(L, it->first, t);
     if (q.empty() && !t.dirty)
       it = L.streams.erase(it);
     else
@@ -526,7 +533,7 @@ void limiter_track(int dev, hipStream_t stream) {
   auto is_cap = REAL_HIP(hipStreamIsCapturing);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if ((is_cap && is_cap(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) ||
-      !record_marker(L, stream, t, /*from_app=*/true)) {
+      !record_marker(L, stream, t)) {
     // captured (not executed now) or no marker possible: not tracked
     t.unmarked--;
     L.inflight.fetch_sub(1, std::memory_order_relaxed);

@@ -124,6 +124,32 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (sc == "capture_race") {
+    // Eager launches on a stream (limiter markers outstanding), a device sync,
+    // then a graph capture on that same stream, over and over: the limiter
+    // thread's polling must never invalidate the capture.
+    const int iters = argc > 2 ? atoi(argv[2]) : 50;
+    hipStream_t S = reinterpret_cast<hipStream_t>(0x5151);
+    int fails = 0, begun = 0;
+    for (int i = 0; i < iters; ++i) {
+      for (int k = 0; k < 4; ++k) hipLaunchKernel((const void*)&main, dim3(64), dim3(256), nullptr, 0, S);
+      hipDeviceSynchronize();
+      usleep((i * 37) % 300);
+      if (hipStreamBeginCapture(S, hipStreamCaptureModeGlobal) != hipSuccess) {
+        ++fails;
+        continue;
+      }
+      ++begun;
+      hipLaunchKernel((const void*)&main, dim3(64), dim3(256), nullptr, 0, S);
+      usleep(300);  // the capture stays open across limiter polls
+      hipGraph_t g = nullptr;
+      if (hipStreamEndCapture(S, &g) != hipSuccess) ++fails;
+    }
+    printf("captures=%d\ncapture_failures=%d\n", begun, fails);
+    print_region(dev);
+    return 0;
+  }
+
   if (sc == "arrays") {
     // Array / 3D / module allocations under the cap (reference cuArrayCreate_v2,
     // cuArray3DCreate_v2, cuModuleLoad*): refusable past it, charged by class.

@@ -46,6 +46,18 @@ RECIPES: dict[str, tuple[list, list, int]] = {
         ("excl", {}, EXCL),
         ("excl_c5_b7", {"VGPU_DF_CHUNKS": "5", "VGPU_DF_BLOCKS": "7"}, EXCL),
     ], 300),
+    # Flagship knobs under the default temporal share policy.
+    "temporal-knobs": (["--steps", "30", "--warmup", "10"], [
+        ("base", {}, []),
+        ("q2", {}, ["--hw-queues", "2"]),
+        ("q0", {}, ["--hw-queues", "0"]),
+        ("split2_q1", {"VGPU_POD_SPLIT": "2"}, []),
+        ("split2_q2", {"VGPU_POD_SPLIT": "2"}, ["--hw-queues", "2"]),
+        ("cus256", {"VGPU_CONV_CUS": "256"}, []),
+        ("dryrun", {"VGPU_LIMITER_DRYRUN": "1"}, []),
+        ("noshim", {}, ["--no-shim"]),
+        ("base_again", {}, []),
+    ], 300),
     # Temporal limiter accuracy and fair share (profiles/temporal_r2.md).
     "temporal": (["--steps", "150"], [
         ("excl", {}, EXCL),

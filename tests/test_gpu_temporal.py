@@ -50,3 +50,16 @@ def test_four_quarter_pods_fill_the_gpu_fairly(exclusive):
     fair = d["value"] / 4
     for v in d["per_pod_images_s"]:
         assert abs(v - fair) <= 0.15 * fair, d["per_pod_images_s"]
+
+
+def test_graph_capture_on_a_marked_stream_under_the_limiter(gpu_build, monkeypatch):
+    """Two micro-batch hipGraphs captured on streams that just ran eager work
+    (limiter markers outstanding on them) under the temporal limiter: the
+    limiter's polling must not invalidate the captures (it did, before its poll
+    ran under the capture guard: hipErrorStreamCaptureInvalidated)."""
+    monkeypatch.setenv("VGPU_POD_SPLIT", "2")
+    r = subprocess.run([sys.executable, "bench.py", "--no-cap-probe", "--steps", "20", "--warmup", "5",
+                        "--pods", "2", "--gpucores", "50", "--cu-share", "temporal"],
+                       capture_output=True, text=True, timeout=400, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "capture failed" not in r.stderr, r.stderr[-4000:]

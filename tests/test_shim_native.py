@@ -307,6 +307,17 @@ def test_temporal_limit_graph_launches(native_build):
     assert abs(_duty(o) - 0.25) < 0.05, o
 
 
+def test_limiter_poll_never_invalidates_a_stream_capture(native_build):
+    """A graph capture that begins on a stream right after eager launches on it
+    (markers outstanding, limiter thread polling them) must survive: the fake
+    runtime invalidates a capture whose stream's event is queried mid-capture,
+    as the real one does (MI355X: VGPU_POD_SPLIT=2 under the temporal policy)."""
+    o = run("capture_race", 60, env={"VGPU_DEVICE_CU_LIMIT_0": "50", "VGPU_CU_MASK_FROM_LIMIT": "false",
+                                     "GPU_CORE_UTILIZATION_POLICY": "force", "VGPU_FAKE_KERNEL_US": "50",
+                                     "VGPU_FAKE_QUERY_US": "150"}, timeout=120)
+    assert int(o["captures"]) == 60 and int(o["capture_failures"]) == 0, o
+
+
 def test_unlimited_runs_flat_out(native_build):
     o = run("duty", 1, env={"VGPU_FAKE_KERNEL_US": "500"}, timeout=60)
     assert _duty(o) > 0.95
