@@ -8,6 +8,8 @@ import socket
 import subprocess
 import sys
 
+import pytest
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -87,3 +89,24 @@ def test_ab_recipes_and_suite_scenarios_are_valid_bench_flags():
     a = p.parse_args(SCENARIOS["vgpu-vmem"])
     assert a.oversubscribe and a.memory_scaling == 1.8
     assert a.pods * a.gpumem * (1 << 20) > 288e9  # the caps oversubscribe the physical HBM
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_torchrun_on_the_gpu(gpu_build):
+    """The driver's multi-GPU launch (torchrun, one rank per GPU, gloo barrier,
+    MAX over ranks, one JSON line) on real hardware: the box has one GPU, so
+    both ranks map to it (HIP_VISIBLE_DEVICES=0,0) and run their pods there."""
+    port = _free_port()
+    env = dict(os.environ)
+    env["HIP_VISIBLE_DEVICES"] = "0,0"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--steps", "10", "--warmup", "3", "--no-cap-probe"],
+                       cwd=REPO, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and len(d["placement"]) == 2
+    assert sorted(x["rank"] for x in d["placement"]) == [0, 1]
+    assert all(x["device"] == "0" for x in d["placement"])
