@@ -30,7 +30,7 @@ extern "C" {
 #endif
 
 #define VGPU_BOARD_MAGIC 0x56424F44u /* "VBOD" */
-#define VGPU_BOARD_VERSION 1u
+#define VGPU_BOARD_VERSION 2u
 #define VGPU_BOARD_SLOTS 128
 #define VGPU_BOARD_STALE_NS 500000000ull /* a slot without heartbeat for 0.5 s is inactive */
 
@@ -44,6 +44,13 @@ typedef struct vgpu_board_slot {
   volatile uint64_t busy_ns;     /* wall time with work outstanding so far       */
   double v_mark;                 /* board virtual time at the last charge        */
   uint64_t claim_ns;             /* CLOCK_MONOTONIC of the claim                 */
+  /* Concurrency gate (VGPU_POOL_CONCURRENCY): at most N slots of the pool run
+   * at once; the others wait, oldest first, and a runner yields after its
+   * quantum when someone waits. */
+  volatile int32_t running;      /* 1 while admitted to the running set          */
+  int32_t reserved0;
+  volatile uint64_t run_start_ns;   /* CLOCK_MONOTONIC of the last admission     */
+  volatile uint64_t wait_since_ns;  /* waiting for admission since (0 = not)     */
 } vgpu_board_slot_t;
 
 typedef struct vgpu_board {

@@ -154,6 +154,7 @@ uint64_t board_charge(vgpu_board_t* b, int slot, uint64_t wall_ns, bool leave) {
   s.heartbeat_ns = now;
   if (leave) {
     s.active = 0;
+    s.running = 0;  // drained: give the running set to a waiter
     advance(b, now);
   }
   unlock(b);
@@ -174,6 +175,61 @@ double board_entitlement(vgpu_board_t* b, int slot) {
     if (live(s, now)) sum += s.limit_pct > 0 ? s.limit_pct : 1;
   }
   return self_w / sum;
+}
+
+namespace {
+bool fresh(const vgpu_board_slot_t& s, uint64_t now) {
+  return s.pid != 0 && now - s.heartbeat_ns < VGPU_BOARD_STALE_NS;
+}
+}  // namespace
+
+bool board_gate(vgpu_board_t* b, int slot, int max_running, uint64_t quantum_ns) {
+  if (!b || slot < 0 || max_running <= 0 || !lock(b)) return true;
+  const uint64_t now = mono_ns();
+  vgpu_board_slot_t& me = b->slot[slot];
+  me.heartbeat_ns = now;
+  // Oldest live waiter other than us (ties: lower slot).
+  int oldest = -1;
+  int running = 0;
+  for (int i = 0; i < VGPU_BOARD_SLOTS; ++i) {
+    const vgpu_board_slot_t& s = b->slot[i];
+    if (i == slot || !fresh(s, now)) continue;
+    running += s.running != 0;
+    if (s.wait_since_ns && (oldest < 0 || s.wait_since_ns < b->slot[oldest].wait_since_ns)) oldest = i;
+  }
+  bool go;
+  if (me.running) {
+    // Our turn is over and someone waits: stop launching and join the queue.
+    // We stay in the running set until our queued work has drained
+    // (board_charge(leave) clears `running`), so the waiter never overlaps it.
+    go = !(oldest >= 0 && now - me.run_start_ns > quantum_ns);
+    if (!go) {
+      if (!me.wait_since_ns) me.wait_since_ns = now;
+    } else if (me.wait_since_ns) {  // yielded, but nobody waits any more: a new turn
+      me.wait_since_ns = 0;
+      me.run_start_ns = now;
+    }
+  } else {
+    if (!me.wait_since_ns) me.wait_since_ns = now;
+    const bool first = oldest < 0 || me.wait_since_ns < b->slot[oldest].wait_since_ns ||
+                       (me.wait_since_ns == b->slot[oldest].wait_since_ns && slot < oldest);
+    go = running < max_running && first;
+    if (go) {
+      me.running = 1;
+      me.run_start_ns = now;
+      me.wait_since_ns = 0;
+    }
+  }
+  unlock(b);
+  return go;
+}
+
+int board_running_count(vgpu_board_t* b) {
+  if (!b) return 0;
+  const uint64_t now = mono_ns();
+  int n = 0;
+  for (int i = 0; i < VGPU_BOARD_SLOTS; ++i) n += fresh(b->slot[i], now) && b->slot[i].running;
+  return n;
 }
 
 int board_active_count(vgpu_board_t* b) {

@@ -13,6 +13,11 @@ void board_enter(vgpu_board_t* b, int slot);
 // Fair-share GPU ns accrued since the previous charge (wall_ns when there is no board).
 uint64_t board_charge(vgpu_board_t* b, int slot, uint64_t wall_ns, bool leave);
 int board_active_count(vgpu_board_t* b);
+// Concurrency gate: true when `slot` may launch now (it is, or just became, one
+// of at most `max_running` running slots); false while it must wait.  A runner
+// past `quantum_ns` yields to the oldest waiter.
+bool board_gate(vgpu_board_t* b, int slot, int max_running, uint64_t quantum_ns);
+int board_running_count(vgpu_board_t* b);
 double board_entitlement(vgpu_board_t* b, int slot);  // weighted fair share among active slots
 
 }  // namespace vgpu

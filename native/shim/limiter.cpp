@@ -102,6 +102,10 @@ struct DevLimiter {
   vgpu_board_t* board = nullptr;
   int board_slot = -1;
   bool board_tried = false;
+  // Concurrency gate of the temporal pool (VGPU_POOL_CONCURRENCY, 0 = off): at
+  // most max_running pool members of the GPU run at once, in run_quantum_ns turns.
+  int max_running = 0;
+  uint64_t run_quantum_ns = 0;
   // window statistics (limiter thread only)
   uint64_t win_charge = 0, win_busy = 0, win_start = 0;
   std::atomic<uint64_t> charged_total{0}, busy_total{0};
@@ -203,6 +207,13 @@ void configure() {
       // per-slice costs (clock ramp after idle, pipeline fill) are amortised.
       const double q_ms = env_first("VGPU_LIMITER_QUANTUM_MS") ? atof(env_first("VGPU_LIMITER_QUANTUM_MS")) : 200.0;
       L.quantum = (int64_t)(L.frac * q_ms * 1e6);
+      // Concurrency gate: several pods whose kernels each fill the GPU slow each
+      // other down more than time-slicing does (caches, HBM pages, CP queue
+      // switching), so a pool member may be held until fewer than N run.
+      const char* mr = env_first("VGPU_POOL_CONCURRENCY");
+      L.max_running = temporal_share && mr ? atoi(mr) : 0;
+      const char* rq = env_first("VGPU_POOL_QUANTUM_MS");
+      L.run_quantum_ns = (uint64_t)((rq ? atof(rq) : 50.0) * 1e6);
       if (L.cap < L.quantum) L.cap = L.quantum;
       L.tokens.store(L.cap);
       L.win_start = mono_ns();
@@ -482,6 +493,25 @@ bool limiter_on_launch(int dev, uint64_t wg, const void* fn) {
   // VGPU_LIMITER_DRYRUN=1: measure and charge, never wait (diagnostics).
   static const bool dryrun = env_bool(env_first("VGPU_LIMITER_DRYRUN"), false);
   if (dryrun) return true;
+  if (L.max_running > 0 && g_open_captures.load(std::memory_order_acquire) == 0) {
+    if (!L.board_tried) {
+      std::lock_guard<std::mutex> g(L.mu);
+      attach_board(dev, L);
+    }
+    if (L.board) {
+      uint64_t g0 = 0;
+      while (!board_gate(L.board, L.board_slot, L.max_running, L.run_quantum_ns)) {
+        if (!g0) g0 = mono_ns();
+        sleep_ns(100000);  // 0.1 ms
+        if (g_shutdown.load(std::memory_order_relaxed)) break;
+      }
+      if (g0) {
+        const uint64_t waited = mono_ns() - g0;
+        if (sl) __atomic_fetch_add(&sl->throttle_wait_ns, waited, __ATOMIC_RELAXED);
+        trace_emit(VGPU_EV_THROTTLE, dev, waited, wg);
+      }
+    }
+  }
   // Wait while the bucket cannot pay for the work already in flight; once
   // overdrawn, hold until it has refilled by a whole quantum.
   uint64_t t0 = 0;

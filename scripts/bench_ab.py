@@ -58,6 +58,27 @@ RECIPES: dict[str, tuple[list, list, int]] = {
         ("noshim", {}, ["--no-shim"]),
         ("base_again", {}, []),
     ], 300),
+    # ResNet-152 training at 4 x 25 %: where does the temporal pool lose to masks?
+    "share4-r152t": (P4 + ["--workload", "2.2", "--steps", "40", "--warmup", "5"], [
+        ("temporal", {}, ["--cu-share", "temporal"]),
+        ("temporal_dryrun", {"VGPU_LIMITER_DRYRUN": "1"}, ["--cu-share", "temporal"]),
+        ("noshim", {}, ["--no-shim"]),
+        ("mask", {}, ["--cu-share", "mask"]),
+        ("temporal_cus256", {"VGPU_CONV_CUS": "256"}, ["--cu-share", "temporal"]),
+        ("temporal_again", {}, ["--cu-share", "temporal"]),
+    ], 300),
+    # Concurrency gate of the temporal pool (VGPU_POOL_CONCURRENCY) at 4 x 25 %.
+    "pool-gate": (P4 + ["--steps", "40", "--warmup", "5", "--cu-share", "temporal"], [
+        ("w2.2_free", {}, ["--workload", "2.2"]),
+        ("w2.2_k2", {"VGPU_POOL_CONCURRENCY": "2"}, ["--workload", "2.2"]),
+        ("w2.1_free", {}, ["--workload", "2.1"]),
+        ("w2.1_k2", {"VGPU_POOL_CONCURRENCY": "2"}, ["--workload", "2.1"]),
+        ("w1.1_free", {}, ["--workload", "1.1"]),
+        ("w1.1_k2", {"VGPU_POOL_CONCURRENCY": "2"}, ["--workload", "1.1"]),
+        ("w5.1_free", {}, ["--workload", "5.1"]),
+        ("w5.1_k2", {"VGPU_POOL_CONCURRENCY": "2"}, ["--workload", "5.1"]),
+        ("w2.2_k2_q100", {"VGPU_POOL_CONCURRENCY": "2", "VGPU_POOL_QUANTUM_MS": "100"}, ["--workload", "2.2"]),
+    ], 300),
     # Temporal limiter accuracy and fair share (profiles/temporal_r2.md).
     "temporal": (["--steps", "150"], [
         ("excl", {}, EXCL),

@@ -366,6 +366,44 @@ def test_without_board_sharers_are_overcharged(native_build, tmp_path):
     assert sum(_duty(o) for o in pair) > 0.9
 
 
+def _group(tmp_path, n, concurrency, secs=2):
+    """n temporal-pool pods on one board, each with its own (fake) GPU timeline:
+    without a gate they all run flat out; with VGPU_POOL_CONCURRENCY=k only k
+    run at a time, so each is admitted about k/n of the time."""
+    lock = tmp_path / "lock"
+    lock.mkdir(exist_ok=True)
+    env = {"VGPU_DEVICE_CU_LIMIT_0": str(100 // n), "VGPU_CU_SHARE": "temporal",
+           "VGPU_CU_MASK_FROM_LIMIT": "false", "VGPU_FAKE_KERNEL_US": "500",
+           "VGPU_LOCK_DIR": str(lock), "VGPU_DEVICE_UUID_0": "GPU-test", "VGPU_POOL_QUANTUM_MS": "20"}
+    if concurrency:
+        env["VGPU_POOL_CONCURRENCY"] = str(concurrency)
+    e = {k: v for k, v in os.environ.items() if not k.startswith(("VGPU_", "CUDA_", "HIP_"))}
+    e.update({"LD_LIBRARY_PATH": str(FAKES_DIR), "LD_PRELOAD": str(shim_path())}, **env)
+    procs = [subprocess.Popen([str(FAKES_DIR / "shim_driver"), "duty", str(secs)], env=e,
+                              stdout=subprocess.PIPE, text=True) for _ in range(n)]
+    outs = []
+    for p in procs:
+        out, _ = p.communicate(timeout=60)
+        assert p.returncode == 0
+        outs.append(dict(l.split("=", 1) for l in out.splitlines() if "=" in l))
+    return [_duty(o) for o in outs]
+
+
+@pytest.mark.parametrize("n,k", [(3, 2), (4, 2), (3, 1)])
+def test_pool_concurrency_gate_round_robin(native_build, tmp_path, n, k):
+    """VGPU_POOL_CONCURRENCY=k: at most k of the n pool members run at once and
+    the turns rotate fairly (every pod gets about k/n of the time)."""
+    d = _group(tmp_path, n, k)
+    assert abs(sum(d) - k) < 0.2 * k, d
+    for x in d:
+        assert abs(x - k / n) < 0.12, d
+
+
+def test_pool_without_gate_runs_everyone(native_build, tmp_path):
+    d = _group(tmp_path, 3, 0)
+    assert all(x > 0.9 for x in d), d
+
+
 def test_pool_member_time_share_scaled_to_pool(native_build):
     """A 25 % vGPU in a 128-CU pool (device plugin hybrid policy) may keep the
     pool busy half of the time: its work never reaches the other 128 CUs."""
