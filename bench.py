@@ -79,6 +79,9 @@ def make_parser() -> argparse.ArgumentParser:
                     help="virtual device memory (VGPU_OVERSUBSCRIBE): pod caps may exceed physical HBM")
     ap.add_argument("--memory-scaling", type=float, default=1.0,
                     help="device plugin --device-memory-scaling (reference README.md:283-287)")
+    ap.add_argument("--pool-concurrency", type=int, default=None,
+                    help="device plugin --pool-concurrency: temporal-pool members of a GPU running at once "
+                         "(0 = all; default: the plugin's)")
     ap.add_argument("--no-cap-probe", action="store_true")
     ap.add_argument("--ready-timeout", type=float, default=1500.0)
     ap.add_argument("--cpu-smoke", action="store_true",
@@ -116,6 +119,8 @@ def main(argv=None) -> int:
         pg = dist
 
     device = visible_device_for(local_rank)
+    from vgpu.config import DevicePluginConfig
+    pool_conc = DevicePluginConfig().pool_concurrency if args.pool_concurrency is None else args.pool_concurrency
     pol_env = {} if args.core_policy == "default" else {"GPU_CORE_UTILIZATION_POLICY": args.core_policy}
     specs = [PodSpec(workload=args.workload, mem_mib=args.gpumem, cores=args.gpucores, extra_env=dict(pol_env))
              for _ in range(args.pods)]
@@ -124,7 +129,8 @@ def main(argv=None) -> int:
                        graph=not args.no_graph, cap_probe=not args.no_cap_probe,
                        find=not args.no_find, hw_queues=args.hw_queues or None,
                        fused=not args.no_fused, conv=args.conv, cu_share=args.cu_share,
-                       oversubscribe=args.oversubscribe, memory_scaling=args.memory_scaling)
+                       oversubscribe=args.oversubscribe, memory_scaling=args.memory_scaling,
+                       pool_concurrency=pool_conc)
     try:
         for p in pods:
             p.ready = p.read_tagged("READY", args.ready_timeout, progress=log)
@@ -208,6 +214,7 @@ def main(argv=None) -> int:
                 "conv": args.conv,
                 "hw_queues_per_pod": args.hw_queues,
                 "cu_share": args.cu_share,
+                "pool_concurrency": pool_conc,
                 "core_policy": args.core_policy,
                 "oversubscribe": args.oversubscribe or args.memory_scaling > 1,
                 "memory_scaling": args.memory_scaling,

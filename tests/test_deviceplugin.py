@@ -463,3 +463,19 @@ def test_partition_mode_mismatch_is_unhealthy_until_restored():
     # no expectation configured: any mode is fine
     cfg2 = DevicePluginConfig(node_name="n1", host_lib_dir="/tmp/vgpu-pm-test")
     assert all(VGPUDevicePlugin(cfg2, backend, None, "n1").health.values())
+
+
+def test_allocate_pool_concurrency_env(tmp_path):
+    """--pool-concurrency reaches every temporal-pool member as the shim's
+    VGPU_POOL_CONCURRENCY / VGPU_POOL_QUANTUM_MS; masked pods never get it."""
+    from vgpu.bench.control import admit_pods
+    from vgpu.bench.launch import PodSpec
+    pods = admit_pods([PodSpec(cores=25, mem_mib=70000)] * 4, 0, str(tmp_path / "a"), pool_concurrency=2)
+    for p in pods:
+        assert p.share == "temporal"
+        assert p.env["VGPU_POOL_CONCURRENCY"] == "2" and p.env["VGPU_POOL_QUANTUM_MS"] == "50"
+    pods = admit_pods([PodSpec(cores=25, mem_mib=70000)] * 2, 0, str(tmp_path / "b"))
+    assert all("VGPU_POOL_CONCURRENCY" not in p.env for p in pods)
+    pods = admit_pods([PodSpec(cores=25, mem_mib=70000)] * 2, 0, str(tmp_path / "c"), policy="mask",
+                      pool_concurrency=2)
+    assert all(p.share == "mask" and "VGPU_POOL_CONCURRENCY" not in p.env for p in pods)

@@ -86,7 +86,8 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
                 graph: bool = True, cap_probe: bool = False, find: bool = False,
                 workdir: str | None = None, oversubscribe: bool = False,
                 hw_queues: int | None = None, fused: bool = True,
-                conv: str = "native", cu_share: str = "temporal", memory_scaling: float = 1.0) -> list[Pod]:
+                conv: str = "native", cu_share: str = "temporal", memory_scaling: float = 1.0,
+                pool_concurrency: int = 0) -> list[Pod]:
     """Start one process per pod on physical device `device`.
 
     cu_share: how a fractional pod's compute share is enforced.
@@ -106,7 +107,8 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
     if cu_share in ("hybrid", "mask", "temporal"):
         from vgpu.bench.control import admit_pods
         admitted = admit_pods(specs, int(device) if device.isdigit() else 0, workdir, policy=cu_share,
-                              memory_scaling=max(memory_scaling, 2.0 if oversubscribe else 1.0))
+                              memory_scaling=max(memory_scaling, 2.0 if oversubscribe else 1.0),
+                              pool_concurrency=pool_concurrency)
     used = 0
     pods = []
     group_masks: dict[int, int] = {}

@@ -62,6 +62,10 @@ class DevicePluginConfig:
     #             rest share the remaining CUs (one pool mask) under the temporal limiter
     cu_share: str = "temporal"
     max_mask_slots: int = 2
+    # Temporal pool: at most this many pool members of one GPU run at a time,
+    # taking turns of pool_quantum_ms (VGPU_POOL_CONCURRENCY; 0 = all at once).
+    pool_concurrency: int = 0
+    pool_quantum_ms: float = 50.0
     rocr_cu_mask: bool = True             # also hand the masks to ROCr (HSA_CU_MASK: internal queues too)
     host_lock_dir: str = "/tmp/vgpulock"  # node-wide unified lock + per-GPU share boards
     device_list_strategy: str = "envvar"  # envvar (device nodes in the response) | cdi-annotations | cdi-cri

@@ -189,6 +189,9 @@ def build_container_grant(cfg: DevicePluginConfig, pod: dict, ctr_idx: int, devr
         # node-wide lock dir); no mask is derived from the limit.
         g.envs[ENV_CU_SHARE] = "temporal"
         g.envs["VGPU_CU_MASK_FROM_LIMIT"] = "false"
+        if cfg.pool_concurrency > 0:
+            g.envs["VGPU_POOL_CONCURRENCY"] = str(cfg.pool_concurrency)
+            g.envs["VGPU_POOL_QUANTUM_MS"] = f"{cfg.pool_quantum_ms:g}"
     if rocr_masks and cfg.rocr_cu_mask and "HSA_CU_MASK" not in env_names:
         # ROCr applies HSA_CU_MASK to every AQL queue it creates, its internal
         # blit/utility queue included — the one queue the shim's
