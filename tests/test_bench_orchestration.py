@@ -95,10 +95,11 @@ def test_ab_recipes_and_suite_scenarios_are_valid_bench_flags():
 def test_bench_two_ranks_torchrun_on_the_gpu(gpu_build):
     """The driver's multi-GPU launch (torchrun, one rank per GPU, gloo barrier,
     MAX over ranks, one JSON line) on real hardware: the box has one GPU, so
-    both ranks map to it (HIP_VISIBLE_DEVICES=0,0) and run their pods there."""
+    both ranks map to it (VGPU_BENCH_DEVICES=0,0; torchrun refuses a
+    HIP_VISIBLE_DEVICES longer than ROCR_VISIBLE_DEVICES) and run their pods there."""
     port = _free_port()
     env = dict(os.environ)
-    env["HIP_VISIBLE_DEVICES"] = "0,0"
+    env["VGPU_BENCH_DEVICES"] = "0,0"
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
                         "--steps", "10", "--warmup", "3", "--no-cap-probe"],

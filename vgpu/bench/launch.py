@@ -34,8 +34,11 @@ class PodSpec:
 
 
 def visible_device_for(local_rank: int) -> str:
-    """Device id (in the parent's visible-device numbering) for one rank."""
-    lst = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+    """Device id (in the parent's visible-device numbering) for one rank.
+    VGPU_BENCH_DEVICES (a rank -> device list, e.g. "0,0" to put two ranks on
+    one GPU in a rehearsal) takes precedence over the visible-device lists."""
+    lst = (os.environ.get("VGPU_BENCH_DEVICES") or os.environ.get("HIP_VISIBLE_DEVICES")
+           or os.environ.get("CUDA_VISIBLE_DEVICES"))
     if lst:
         ids = [s for s in lst.split(",") if s.strip()]
         return ids[local_rank % len(ids)].strip()
