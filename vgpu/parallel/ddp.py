@@ -123,7 +123,8 @@ def train(workload: str = "1.2", steps: int = 20, warmup: int = 5, bucket_mb: in
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], dtype=torch.float64, device=device if backend != "gloo" and device.type == "cuda" else "cpu")
     # every rank must end with the same weights (the all-reduce worked)
-    chk = torch.stack([p.detach().float().sum() for p in model.parameters()]).sum().reshape(1).cpu().double()
+    chk = torch.stack([p.detach().float().sum() for p in model.parameters()]).sum().reshape(1).double()
+    chk = chk if dist.get_backend() == "nccl" else chk.cpu()  # RCCL reduces device tensors only
     chk_max, chk_min = chk.clone(), chk.clone()
     dist.all_reduce(chk_max, op=dist.ReduceOp.MAX)
     dist.all_reduce(chk_min, op=dist.ReduceOp.MIN)
@@ -133,7 +134,7 @@ def train(workload: str = "1.2", steps: int = 20, warmup: int = 5, bucket_mb: in
            "value": round(bsz * world * steps / wall, 2), "unit": "images/s",
            "ms_per_step": round(1e3 * wall / steps, 3), "bucket_mb": bucket_mb,
            "backend": dist.get_backend(), "device": str(device), "final_loss": float(loss.detach().float()),
-           "weights_in_sync": bool(float(chk_max[0]) == float(chk_min[0]))}
+           "weights_in_sync": bool(float(chk_max[0].item()) == float(chk_min[0].item()))}
     return res
 
 
