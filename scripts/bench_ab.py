@@ -82,8 +82,9 @@ RECIPES: dict[str, tuple[list, list, int]] = {
     # Temporal limiter accuracy and fair share (profiles/temporal_r2.md).
     "temporal": (["--steps", "150"], [
         ("excl", {}, EXCL),
-        ("t1x25", {}, ["--pods", "1", "--gpucores", "25", "--cu-share", "temporal"]),
-        ("t1x50", {}, ["--pods", "1", "--gpucores", "50", "--cu-share", "temporal"]),
+        ("t1x25", {}, ["--pods", "1", "--gpucores", "25", "--cu-share", "temporal", "--core-policy", "force"]),
+        ("t1x50", {}, ["--pods", "1", "--gpucores", "50", "--cu-share", "temporal", "--core-policy", "force"]),
+        ("t1x25_default", {}, ["--pods", "1", "--gpucores", "25", "--cu-share", "temporal"]),
         ("t2x50", {}, ["--pods", "2", "--gpucores", "50", "--cu-share", "temporal"]),
         ("t4x25", {}, P4 + ["--cu-share", "temporal"]),
         ("m4x25", {}, P4 + ["--cu-share", "mask"]),
