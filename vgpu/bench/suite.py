@@ -65,7 +65,7 @@ def main(argv=None) -> int:
     from vgpu.models import WORKLOADS
     ap = argparse.ArgumentParser()
     ap.add_argument("--tests", default=",".join(WORKLOADS))
-    ap.add_argument("--scenarios", default="exclusive,vgpu,vgpu-cu25")
+    ap.add_argument("--scenarios", default="exclusive,vgpu,vgpu-cu25,vgpu-vmem")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--timeout", type=int, default=900)
