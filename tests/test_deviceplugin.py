@@ -479,3 +479,18 @@ def test_allocate_pool_concurrency_env(tmp_path):
     pods = admit_pods([PodSpec(cores=25, mem_mib=70000)] * 2, 0, str(tmp_path / "c"), policy="mask",
                       pool_concurrency=2)
     assert all(p.share == "mask" and "VGPU_POOL_CONCURRENCY" not in p.env for p in pods)
+
+
+def test_pod_annotation_overrides_share_policy(tmp_path):
+    """amd.com/cu-share on a pod overrides the node's policy for its containers:
+    a 'mask' pod on a temporal node gets exclusive CUs, the pool shares the rest."""
+    from vgpu.bench.control import admit_pods
+    from vgpu.bench.launch import PodSpec
+    specs = [PodSpec(cores=25, mem_mib=70000, cu_share="mask"), PodSpec(cores=25, mem_mib=70000),
+             PodSpec(cores=25, mem_mib=70000, cu_share="bogus")]
+    pods = admit_pods(specs, 0, str(tmp_path), policy="temporal")
+    assert pods[0].share == "mask" and pods[0].cu_mask_bits == 64
+    assert pods[1].share == "temporal" and pods[2].share == "temporal"
+    pool = int(pods[1].env["VGPU_CU_MASK_0"], 16)
+    mask = int(pods[0].env["VGPU_CU_MASK_0"], 16)
+    assert pool & mask == 0 and bin(pool).count("1") == 192

@@ -35,6 +35,7 @@ ANN_USE_GPUTYPE = "amd.com/use-gputype"
 ANN_NOUSE_GPUTYPE = "amd.com/nouse-gputype"
 ANN_NUMA_BIND = "amd.com/numa-bind"
 ANN_XGMI_BIND = "amd.com/xgmi-bind"          # new: keep multi-GPU pods on one xGMI hive
+ANN_CU_SHARE = "amd.com/cu-share"            # new: per-pod compute-share policy (mask|temporal|hybrid)
 ANN_WEBHOOK_IGNORE_LABEL = "4pd.io/webhook"  # label value "ignore" opts a pod out
 
 # ---- node annotations (device plugin → scheduler) ------------------------------------

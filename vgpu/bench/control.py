@@ -46,7 +46,7 @@ class AdmittedPod:
     share: str = "none"                           # mask | temporal | none
 
 
-def _pod(name: str, mem_mib: int, cores: int, priority: int | None) -> dict:
+def _pod(name: str, mem_mib: int, cores: int, priority: int | None, cu_share: str | None = None) -> dict:
     lim = {R.RESOURCE_COUNT: "1"}
     if mem_mib:
         lim[R.RESOURCE_MEM] = str(mem_mib)
@@ -55,7 +55,8 @@ def _pod(name: str, mem_mib: int, cores: int, priority: int | None) -> dict:
     if priority is not None:
         lim[R.RESOURCE_PRIORITY] = str(priority)
     return {"apiVersion": "v1", "kind": "Pod",
-            "metadata": {"name": name, "namespace": "bench", "uid": f"uid-{name}", "annotations": {}},
+            "metadata": {"name": name, "namespace": "bench", "uid": f"uid-{name}",
+                         "annotations": {R.ANN_CU_SHARE: cu_share} if cu_share else {}},
             "spec": {"containers": [{"name": "main", "image": "bench", "resources": {"limits": lim}}]}}
 
 
@@ -94,7 +95,7 @@ def admit_pods(specs: list, device_index: int, workdir: str, *, policy: str = "t
         out = []
         for i, sp in enumerate(specs):
             name = f"pod{i}"
-            pod = _pod(name, sp.mem_mib, sp.cores, sp.priority)
+            pod = _pod(name, sp.mem_mib, sp.cores, sp.priority, getattr(sp, "cu_share", None))
             review = handle_admission({"request": {"uid": name, "object": pod}})
             if not review["response"]["allowed"]:
                 raise RuntimeError(f"webhook refused {name}: {review}")

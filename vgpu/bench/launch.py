@@ -31,6 +31,7 @@ class PodSpec:
     cores: int = 50
     priority: int | None = None
     extra_env: dict = field(default_factory=dict)
+    cu_share: str | None = None   # per-pod policy override (annotation amd.com/cu-share)
 
 
 def visible_device_for(local_rank: int) -> str:

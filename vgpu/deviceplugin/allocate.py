@@ -37,7 +37,7 @@ from vgpu.k8s.nodelock import release_node_lock
 from vgpu.device.cualloc import CULayout
 
 from .cdi import device_names as cdi_device_names
-from .custate import CUMaskState
+from .custate import POLICIES, CUMaskState
 from .discovery import Device
 
 log = logging.getLogger("vgpu.deviceplugin.allocate")
@@ -161,8 +161,12 @@ def build_container_grant(cfg: DevicePluginConfig, pod: dict, ctr_idx: int, devr
             raise AllocateError(f"unknown device {d.uuid}")
     layouts = {d.uuid: CULayout(total_cus=devices[d.uuid].cus or 256,
                                 num_xcc=max(devices[d.uuid].num_xcc or 1, 1)) for d in ordered}
+    pod_policy = O.annotations(pod).get(R.ANN_CU_SHARE)
+    if pod_policy is not None and pod_policy not in POLICIES:
+        log.warning("pod %s: ignoring %s=%r (not one of %s)", O.name(pod), R.ANN_CU_SHARE, pod_policy, POLICIES)
+        pod_policy = None
     shares = {} if cfg.disable_core_limit else cu_state.allocate(
-        key, [(d.uuid, d.usedcores) for d in ordered], layouts)
+        key, [(d.uuid, d.usedcores) for d in ordered], layouts, policy=pod_policy)
     g = ContainerGrant()
     env_names = _ctr_env_names(pod, ctr_idx)
     fractional = False

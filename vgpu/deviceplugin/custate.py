@@ -19,9 +19,14 @@ profiles/sharing_4way_r1.md and profiles/temporal_r2.md):
   is a pool member: the shim's GPU-time limiter, charged through the per-GPU
   fair-share board. It throttles only under contention (work-conserving) and
   is the reference's time-sliced SM limit. On MI355X, 4 x 25 % temporal pods
-  run at >= 0.96 x the exclusive GPU on all 10 ai-benchmark tests, against
-  0.65 x with four masks on ResNet-50. 2 x 50 % pods match or beat two masks
-  on 9 of 10 tests; the flagship goes from 24.2k to 25.4k images/s.
+  run at >= 0.97 x the exclusive GPU on 9 of 10 ai-benchmark tests, against
+  0.65 x with four masks on ResNet-50; ResNet-152 training is the exception
+  (0.83-0.96 x; four masks 1.01 x). 2 x 50 % pods match or beat two masks on
+  9 of 10 tests; the flagship goes from 24.2k to 25.4k images/s.
+
+A pod may override the node's policy for its own containers with the
+annotation ``amd.com/cu-share: mask|temporal|hybrid`` (e.g. a training job
+that wants exclusive CUs on a temporal node).
 * ``hybrid``: the first ``max_mask_slots`` fractional containers on a GPU get
   masks, which is exact spatial isolation at equal throughput for two sharers.
   Later containers join the pool.
@@ -108,12 +113,15 @@ class CUMaskState:
         return sum(1 for g in self._grants().values() if uuid in g and g[uuid].mode == MODE_POOL)
 
     def allocate(self, container_key: str, requests: list[tuple[str, int]],
-                 layouts: dict[str, CULayout] | None = None) -> dict[str, ShareGrant]:
+                 layouts: dict[str, CULayout] | None = None, policy: str | None = None) -> dict[str, ShareGrant]:
         """requests: [(device uuid, cores %)] → {uuid: ShareGrant}.  Whole-device
         and best-effort requests (cores 0 or >= 100) get ShareGrant(0, "mask"):
         no mask, no limiter.  `layouts` gives each device's CU/XCD geometry (a CPX
-        compute partition is one XCD of 32 CUs; SPX is 8 × 32)."""
+        compute partition is one XCD of 32 CUs; SPX is 8 × 32).  `policy`
+        overrides the node's share policy for this container (pod annotation
+        amd.com/cu-share)."""
         layouts = layouts or {}
+        pol = policy if policy in POLICIES else self.policy
         with self._lock:
             grants = self._grants()
             grants.pop(container_key, None)  # re-allocation of the same container
@@ -135,7 +143,7 @@ class CUMaskState:
                     if sg.mode == MODE_MASK and sg.mask:
                         masked |= sg.mask
                         n_masked += 1
-                want_mask = self.policy == "mask" or (self.policy == "hybrid" and n_masked < self.max_mask_slots)
+                want_mask = pol == "mask" or (pol == "hybrid" and n_masked < self.max_mask_slots)
                 m = alloc_cu_mask(occupied, cores, lay, resolve_packing(self.pack, lay)) if want_mask else None
                 if m:
                     res[uuid] = ShareGrant(m, MODE_MASK)
