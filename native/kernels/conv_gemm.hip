@@ -1099,6 +1099,173 @@ hipError_t dispatch_pro(const ConvArgs& a, bool res, hipStream_t s) {
   return res ? launch_pro<KS, BM, 64, true>(a, s) : launch_pro<KS, BM, 64, false>(a, s);
 }
 
+// ---- Deep-pipelined prologue conv (1x1) for deep K and few workgroups per CU.
+// conv_pro's two stages give the weight DMA one K step of lead and the
+// activations about one and a half; with 2 blocks per CU that hides an HBM
+// round trip, but the stage-3/4 conv1 and shortcut layers (K = 512-2048, a few
+// hundred 128x128 tiles) leave one block per CU, and each K step then waits
+// for a full round trip (~1.8 us measured against ~0.1 us of MFMA).  Here
+// three LDS stages give the DMA two steps of lead and three activation
+// register sets give the loads three; the extra stage costs LDS (112 KB: one
+// block per CU), which these layers never had room to use anyway.
+// Per K step kt:  DMA B(kt+2) into stage (kt+2)%3; load A(kt+3) into register
+// set kt%3; MFMA on stage kt%3; prologue + ds_write of A(kt+1) (register set
+// (kt+1)%3) into stage (kt+1)%3; vmcnt(2*AR+BR) (= B(kt+1) landed); barrier.
+template <int BM, int BN, bool RES>
+__global__ void __launch_bounds__(kThreads, 1) conv_prodeep_kernel(const ConvArgs a) {
+  constexpr int NS = 3;
+  constexpr int AR = BM / 32, BR = BN / 32;
+  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int PIPE = NS * STAGE, EPI = (BM / 2) * (BN + 4) * 4;
+  constexpr int BODY = PIPE > EPI ? PIPE : EPI;
+  __shared__ __attribute__((aligned(16))) char smem[BODY + 2048 * 2 * 4];
+  float* sPar = reinterpret_cast<float*>(smem + BODY);
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int slot = t & 7, r0 = t >> 3;
+  const int lchunk = slot ^ (r0 & 7);
+  int m0, n0;
+  tile_origin(a, blockIdx.x, BM, BN, m0, n0);
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.x), 0, a.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.w), 0, (uint32_t)((int64_t)a.Cout * a.K * 2), 0x00020000);
+
+  int abase[AR];
+  bool aok[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int m = m0 + r0 + 32 * i;
+    aok[i] = m < a.M;
+    const int mm = aok[i] ? m : 0;
+    const int ow = mm % a.OW, t2 = mm / a.OW, oh = t2 % a.OH, n = t2 / a.OH;
+    abase[i] = ((n * a.H + oh * a.stride) * a.W + ow * a.stride) * a.C * 2;  // 1x1, pad 0
+  }
+  const uint32_t boff = (uint32_t)(((n0 + r0) * a.K + lchunk * 8) * 2);
+  for (int c = t * 4; c < a.C; c += kThreads * 4) {
+    *reinterpret_cast<float4*>(sPar + c) = *reinterpret_cast<const float4*>(a.pscale + c);
+    *reinterpret_cast<float4*>(sPar + a.C + c) = *reinterpret_cast<const float4*>(a.pshift + c);
+  }
+  __syncthreads();
+
+  auto issue_b = [&](int kt, int st) {
+    char* sB = smem + st * STAGE + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          wr, (lds_void_t*)(sB + (32 * i + wave * 8) * 128), 16,
+          boff + (uint32_t)((32 * i * a.K + kt * BK) * 2), 0, 0, 0);
+  };
+  auto load_a = [&](int kt, u32x4 (&ra)[AR]) {
+    const int toff = (kt * BK + slot * 8) * 2;
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      ra[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, aok[i] ? (uint32_t)(abase[i] + toff) : kOOB, 0, 0);
+  };
+  auto store_a = [&](int kt, int st, const u32x4 (&ra)[AR]) {
+    char* sA = smem + st * STAGE;
+    const int c = kt * BK + slot * 8;
+    const float4 s0 = *reinterpret_cast<const float4*>(sPar + c);
+    const float4 s1 = *reinterpret_cast<const float4*>(sPar + c + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(sPar + a.C + c);
+    const float4 h1 = *reinterpret_cast<const float4*>(sPar + a.C + c + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      float e[8];
+      unpack8(ra[i], e);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = fmaxf(e[j] * sc[j] + sh[j], 0.0f);
+        e[j] = aok[i] ? f : 0.0f;  // the M tail stays zero after the prologue
+      }
+      *reinterpret_cast<u32x4*>(sA + swz(r0 + 32 * i, slot)) = pack8(e);
+    }
+  };
+  auto compute = [&](int st, f32x4_t (&acc)[TM][TN]) {
+    const char* sA = smem + st * STAGE;
+    const char* sB = sA + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8_t*>(sA + swz(wm * WTM + i * 16 + fr, kk * 4 + fk));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(wn * WTN + j * 16 + fr, kk * 4 + fk));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.ktiles;  // the host guarantees nk >= 3
+  u32x4 ra0[AR], ra1[AR], ra2[AR];
+  u32x4 res[2][EpiShape<BM, BN>::RROWS];
+  load_a(0, ra0);
+  issue_b(0, 0);
+  load_a(1, ra1);
+  issue_b(1, 1);
+  load_a(2, ra2);
+  store_a(0, 0, ra0);
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(2 * AR + BR));  // B(0) landed; B(1), A(1), A(2) in flight
+  __builtin_amdgcn_s_waitcnt(kLgkm0);
+  __builtin_amdgcn_s_barrier();
+  // Past the last K step the loads re-fetch the last tile into a register set /
+  // stage nobody reads again: the body stays branch-free around loads.
+  auto step = [&](int kt, int st, u32x4 (&rl)[AR], u32x4 (&rs)[AR]) {
+    const int k1 = kt + 1 < nk ? kt + 1 : nk - 1;
+    const int k2 = kt + 2 < nk ? kt + 2 : nk - 1;
+    const int k3 = kt + 3 < nk ? kt + 3 : nk - 1;
+    issue_b(k2, st == 0 ? 2 : st - 1);   // (kt+2) % 3
+    load_a(k3, rl);                      // set kt % 3: A(kt) was stored last step
+    compute(st, acc);
+    store_a(k1, st == 2 ? 0 : st + 1, rs);  // A(kt+1) into stage (kt+1) % 3
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(2 * AR + BR));
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    __builtin_amdgcn_s_barrier();
+  };
+  int kt = 0;
+  for (; kt + 2 < nk; kt += 3) {
+    step(kt, 0, ra0, ra1);
+    step(kt + 1, 1, ra1, ra2);
+    step(kt + 2, 2, ra2, ra0);
+  }
+  if (kt < nk) step(kt, 0, ra0, ra1);
+  if (kt + 1 < nk) step(kt + 1, 1, ra1, ra2);
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // the trailing dummy loads, before LDS reuse
+  __syncthreads();
+  if constexpr (RES) load_residual<BM, BN>(a, m0, n0, res);
+  epilogue_halves<BM, BN, RES>(a, acc, m0, n0, smem, res);
+}
+
+template <int BM, int BN, bool RES>
+hipError_t launch_prodeep(ConvArgs a, hipStream_t s) {
+  a.nM = (a.M + BM - 1) / BM;
+  a.nN = a.Cout / BN;
+  a.nwg = a.nM * a.nN;
+  hipLaunchKernelGGL((conv_prodeep_kernel<BM, BN, RES>), dim3(a.nwg), dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+int g_forced_deep = -1;  // vgpu_conv_set_pro_deep: -1 = env VGPU_CONV_PRO_DEEP (default off), 0 off, 1 when eligible, 2 heuristic
+
 // epilogue_halves for a conv3 chunk whose output also feeds the next block's
 // conv1: besides storing y = acc + residual (bf16), each thread keeps
 // p = relu(bf16(y) * s[c] + t[c]) (the next block-entry BN+ReLU, rounded to
@@ -1619,6 +1786,7 @@ VGPU_API void vgpu_conv_set_stages(int n) { g_forced_stages = n; }
 // Benchmark knob: force 64- or 128-row tiles (0 = heuristic).
 VGPU_API void vgpu_conv_set_tile_m(int bm) { g_forced_bm = bm; }
 VGPU_API void vgpu_conv_set_big(int mode) { g_forced_big = mode; }  // -1 env/heuristic, 0 off, 1 when eligible
+VGPU_API void vgpu_conv_set_pro_deep(int mode) { g_forced_deep = mode; }  // -1 env/heuristic, 0 off, 1 when eligible
 
 // Fused conv2 (3x3, pad 1, stride s, C = W → W, bias + ReLU) + conv3 (1x1,
 // W → 4W) + residual; with w1n, also the next block's conv1 (1x1, 4W → W,
@@ -1790,8 +1958,23 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
     const int64_t tiles256 = (int64_t)((c.M + 255) / 256) * (Cout / 256);
     const bool big = big_ok && (g_forced_big == 1 ||
                                 (g_forced_big == 2 && C >= 1024 && tiles256 >= (int64_t)conv_cus()));
+    // Deep K with few tiles per owned CU: the 3-stage prologue kernel.
+    if (g_forced_deep < 0) {
+      const char* v = getenv("VGPU_CONV_PRO_DEEP");
+      // Off by default: at one block per CU the 3-stage kernel measured slower
+      // than conv_pro at two, even on the deep-K stage-4 layers
+      // (profiles/r2/ab/pro-deep: flagship 25.5k either way with the heuristic,
+      // 23.1k forced on every eligible layer; exclusive 22.1k -> 21.5k / 20.2k).
+      g_forced_deep = v ? (v[0] == '1' ? 1 : (v[0] == '2' ? 2 : 0)) : 0;
+    }
+    const bool deep_ok = pro && !glds && pro_dma_enabled() && KS == 1 && pad == 0 && C <= 2048 &&
+                         a.ktiles >= 3 && Cout % 128 == 0;
+    const bool deep = deep_ok && (g_forced_deep == 1 ||
+                                  (g_forced_deep == 2 && a.ktiles >= 8 && tiles128 <= (int64_t)conv_cus() * 2));
     if (big)
       e = has_res ? launch_big<true>(c, s) : launch_big<false>(c, s);
+    else if (deep)
+      e = has_res ? launch_prodeep<128, 128, true>(c, s) : launch_prodeep<128, 128, false>(c, s);
     else if (narrow)
       e = small ? launch_glds<4, 64, 64, false, false, 16>(c, s) : launch_glds<4, 128, 64, false, false, 16>(c, s);
     // Short K (≤ 2 steps) or 64-wide outputs: the persistent register kernel,

@@ -79,6 +79,17 @@ RECIPES: dict[str, tuple[list, list, int]] = {
         ("w5.1_k2", {"VGPU_POOL_CONCURRENCY": "2"}, ["--workload", "5.1"]),
         ("w2.2_k2_q100", {"VGPU_POOL_CONCURRENCY": "2", "VGPU_POOL_QUANTUM_MS": "100"}, ["--workload", "2.2"]),
     ], 300),
+    # 3-stage prologue conv kernel for deep-K layers (VGPU_CONV_PRO_DEEP).
+    "pro-deep": (["--steps", "30", "--warmup", "10"], [
+        ("off", {"VGPU_CONV_PRO_DEEP": "0"}, []),
+        ("heuristic", {}, []),
+        ("all", {"VGPU_CONV_PRO_DEEP": "1"}, []),
+        ("excl_off", {"VGPU_CONV_PRO_DEEP": "0"}, EXCL),
+        ("excl_heuristic", {}, EXCL),
+        ("excl_all", {"VGPU_CONV_PRO_DEEP": "1"}, EXCL),
+        ("off_again", {"VGPU_CONV_PRO_DEEP": "0"}, []),
+        ("all_again", {"VGPU_CONV_PRO_DEEP": "1"}, []),
+    ], 300),
     # Temporal limiter accuracy and fair share (profiles/temporal_r2.md).
     "temporal": (["--steps", "150"], [
         ("excl", {}, EXCL),

@@ -85,6 +85,36 @@ def test_conv_big_tile_matches_fp32(C, case):
     torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
 
 
+DEEP_CASES = [
+    # 3-stage prologue kernel (1x1, BN+ReLU prologue, Cout % 128 == 0), forced on
+    (3, 256, 13, 13, 512, 2, True, "none", False),   # strided projection shortcut, K = 4 steps
+    (1, 2048, 3, 3, 512, 1, True, "relu", False),    # deep K (32 steps), M = 9 < one tile
+    (4, 1024, 11, 11, 256, 1, False, "relu", False), # K = 16 steps, ragged M
+    (2, 192, 7, 9, 256, 1, True, "relu", True),      # K = 3 steps (the minimum), residual
+    (5, 320, 9, 7, 128, 1, True, "none", True),      # K = 5 steps: main loop + 2-step remainder
+]
+
+
+@pytest.mark.parametrize("case", DEEP_CASES, ids=lambda c: "x".join(map(str, c[:6])))
+def test_conv_pro_deep_matches_fp32(C, case):
+    from vgpu.native import load_kernels
+    n, c, h, w, cout, stride, has_bias, act, has_res = case
+    x = _t((n, c, h, w), 21)
+    wt = _t((cout, c, 1, 1), 22, scale=(2.0 / c) ** 0.5)
+    bias = _f((cout,), 23) if has_bias else None
+    pro = (_f((c,), 24, 0.5, 1.5), _f((c,), 25))
+    oh, ow = C.out_hw(h, w, 1, stride, 0)
+    res = _t((n, cout, oh, ow), 26) if has_res else None
+    lib = load_kernels()
+    lib.vgpu_conv_set_pro_deep(1)
+    try:
+        got = C.conv2d(x, wt, bias, stride=stride, act=act, pro=pro, residual=res)
+    finally:
+        lib.vgpu_conv_set_pro_deep(-1)
+    ref = C.conv2d_ref(x, wt, bias, stride=stride, act=act, pro=pro, residual=res)
+    torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
+
+
 def test_conv_asymmetric_exact(C):
     """Integer data (exact in bf16/fp32): catches any row/col or k-order swap."""
     n, c, h, w, cout = 1, 64, 4, 5, 128
