@@ -399,6 +399,30 @@ def test_pool_concurrency_gate_round_robin(native_build, tmp_path, n, k):
         assert abs(x - k / n) < 0.12, d
 
 
+def test_pool_gate_survives_a_killed_runner(native_build, tmp_path):
+    """A pool member SIGKILLed while it holds the only running slot must not
+    block the GPU: its board slot goes stale (0.5 s) and the waiter runs."""
+    import signal
+    import time
+    lock = tmp_path / "lock"
+    lock.mkdir()
+    env = {"VGPU_DEVICE_CU_LIMIT_0": "50", "VGPU_CU_SHARE": "temporal", "VGPU_CU_MASK_FROM_LIMIT": "false",
+           "VGPU_FAKE_KERNEL_US": "500", "VGPU_LOCK_DIR": str(lock), "VGPU_DEVICE_UUID_0": "GPU-test",
+           "VGPU_POOL_CONCURRENCY": "1", "VGPU_POOL_QUANTUM_MS": "10000"}
+    e = {k: v for k, v in os.environ.items() if not k.startswith(("VGPU_", "CUDA_", "HIP_"))}
+    e.update({"LD_LIBRARY_PATH": str(FAKES_DIR), "LD_PRELOAD": str(shim_path())}, **env)
+    a = subprocess.Popen([str(FAKES_DIR / "shim_driver"), "duty", "10"], env=e, stdout=subprocess.PIPE, text=True)
+    time.sleep(0.5)  # a holds the running slot (its quantum is 10 s)
+    b = subprocess.Popen([str(FAKES_DIR / "shim_driver"), "duty", "3"], env=e, stdout=subprocess.PIPE, text=True)
+    time.sleep(0.5)
+    a.send_signal(signal.SIGKILL)
+    a.wait(timeout=10)
+    out, _ = b.communicate(timeout=60)
+    assert b.returncode == 0
+    d = _duty(dict(l.split("=", 1) for l in out.splitlines() if "=" in l))
+    assert d > 0.5, d  # waited ~0.5 s for a, then ~1 s more for its slot to go stale, then ran
+
+
 def test_pool_without_gate_runs_everyone(native_build, tmp_path):
     d = _group(tmp_path, 3, 0)
     assert all(x > 0.9 for x in d), d
