@@ -34,6 +34,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #define VGPU_API extern "C" __attribute__((visibility("default")))
 
@@ -1587,7 +1588,15 @@ int conv_cus() {
   snprintf(name, sizeof name, "VGPU_DEVICE_CU_LIMIT_%d", dev);
   const char* lim = getenv(name);
   const int pct = lim ? atoi(lim) : 0;
+  const int phys = cus;
   if (!(masked && masked[0] == '1') && pct > 0 && pct < 100) cus = (cus * pct + 99) / 100;
+  // A temporal-pool member that runs with at most k-1 others at a time
+  // (VGPU_POOL_CONCURRENCY = k, the device plugin's --pool-concurrency) has
+  // 1/k of the GPU while it runs, whatever its long-run share.
+  const char* pc = getenv("VGPU_POOL_CONCURRENCY");
+  const char* share = getenv("VGPU_CU_SHARE");
+  const int k = pc ? atoi(pc) : 0;
+  if (k > 0 && share && !strcmp(share, "temporal") && phys / k > cus) cus = phys / k;
   cached[dev] = cus > 0 ? cus : 1;
   return cached[dev];
 }

@@ -90,6 +90,17 @@ RECIPES: dict[str, tuple[list, list, int]] = {
         ("off_again", {"VGPU_CONV_PRO_DEEP": "0"}, []),
         ("all_again", {"VGPU_CONV_PRO_DEEP": "1"}, []),
     ], 300),
+    # Pool gate with conv tiles sized for the CUs a running pod actually shares (256 / k).
+    "pool-gate-cus": (P4 + ["--steps", "40", "--warmup", "5", "--cu-share", "temporal"], [
+        ("w2.2_free", {}, ["--workload", "2.2"]),
+        ("w2.2_k2_c128", {"VGPU_POOL_CONCURRENCY": "2", "VGPU_CONV_CUS": "128"}, ["--workload", "2.2"]),
+        ("w2.2_free_c128", {"VGPU_CONV_CUS": "128"}, ["--workload", "2.2"]),
+        ("w1.2_free", {}, ["--workload", "1.2"]),
+        ("w1.2_k2_c128", {"VGPU_POOL_CONCURRENCY": "2", "VGPU_CONV_CUS": "128"}, ["--workload", "1.2"]),
+        ("w2.1_free", {}, ["--workload", "2.1"]),
+        ("w2.1_k2_c128", {"VGPU_POOL_CONCURRENCY": "2", "VGPU_CONV_CUS": "128"}, ["--workload", "2.1"]),
+        ("w2.2_free_again", {}, ["--workload", "2.2"]),
+    ], 300),
     # Temporal limiter accuracy and fair share (profiles/temporal_r2.md).
     "temporal": (["--steps", "150"], [
         ("excl", {}, EXCL),

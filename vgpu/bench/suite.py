@@ -11,6 +11,8 @@ reference's comparison (README.md:234-257):
   vgpu-cu25-temporal — the same 4 pods, policy named explicitly
   vgpu-cu25-mask     — the same 4 pods, one CU mask each
   vgpu-cu25-hybrid   — 2 CU masks + a temporal pool for the other two
+  vgpu-cu25-k2       — the 4 pods in the temporal pool, at most 2 running at a time
+                       (device plugin --pool-concurrency 2)
   vgpu-vmem          — the reference's "vGPU + virtual device memory" column:
                        2 pods per GPU on a plugin with --device-memory-scaling=1.8,
                        each capped at 230000 MiB (together 1.7 x the physical HBM,
@@ -41,6 +43,8 @@ SCENARIOS = {
     "vgpu-cu25-mask": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "mask"],
     "vgpu-vmem": ["--pods", "2", "--gpucores", "0", "--gpumem", "230000", "--oversubscribe",
                   "--memory-scaling", "1.8"],
+    "vgpu-cu25-k2": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "temporal",
+                     "--pool-concurrency", "2"],
     "vgpu-cu25-temporal-q0": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "temporal",
                               "--hw-queues", "0"],
 }
