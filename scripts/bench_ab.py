@@ -101,6 +101,16 @@ RECIPES: dict[str, tuple[list, list, int]] = {
         ("w2.1_k2_c128", {"VGPU_POOL_CONCURRENCY": "2", "VGPU_CONV_CUS": "128"}, ["--workload", "2.1"]),
         ("w2.2_free_again", {}, ["--workload", "2.2"]),
     ], 300),
+    # Conv dispatch knobs re-checked under the default temporal policy.
+    "conv-knobs": (["--steps", "30", "--warmup", "10"], [
+        ("base", {}, []),
+        ("big_all", {"VGPU_CONV_BIG": "1"}, []),
+        ("big_off", {"VGPU_CONV_BIG": "0"}, []),
+        ("1x1_big", {"VGPU_CONV_1X1_BIG": "1"}, []),
+        ("glds_pro", {"VGPU_CONV_GLDS_PRO": "1"}, []),
+        ("stages3", {"VGPU_CONV_STAGES": "3"}, []),
+        ("base_again", {}, []),
+    ], 300),
     # Temporal limiter accuracy and fair share (profiles/temporal_r2.md).
     "temporal": (["--steps", "150"], [
         ("excl", {}, EXCL),
