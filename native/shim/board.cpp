@@ -7,6 +7,7 @@
 #include <sys/file.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include "common.h"
 #include "state.h"
@@ -70,10 +71,29 @@ vgpu_board_t* board_map(const char* path) {
     return nullptr;
   }
   flock(fd, LOCK_EX);
+  // The layout version is part of the file name (limiter.cpp), so a board of
+  // another layout is never expected here.  Only an empty file or a board
+  // nobody finished initialising (magic 0: its creator died between ftruncate
+  // and init, both under this flock) is (re)initialised.  Anything else that
+  // does not match may be in use by a live process of another build, whose
+  // robust mutex must not be wiped under it: refuse it (wall-time charging).
+  struct {
+    uint32_t magic, version, size;
+    int32_t initialized;
+  } hdr = {};
   struct stat stt;
   fstat(fd, &stt);
-  const bool fresh = (size_t)stt.st_size < sz;
-  if (fresh && ftruncate(fd, (off_t)sz) != 0) {
+  const bool have_hdr = pread(fd, &hdr, sizeof hdr, 0) == (ssize_t)sizeof hdr;
+  const bool blank = !have_hdr || (hdr.magic == 0 && hdr.initialized == 0);
+  if (!blank && (hdr.magic != VGPU_BOARD_MAGIC || hdr.version != VGPU_BOARD_VERSION || hdr.size != sz ||
+                 !hdr.initialized || (size_t)stt.st_size < sz)) {
+    VLOG_WARN("share board %s has another layout (magic %#x version %u size %u); charging wall time", path,
+              hdr.magic, hdr.version, hdr.size);
+    flock(fd, LOCK_UN);
+    close(fd);
+    return nullptr;
+  }
+  if ((size_t)stt.st_size < sz && ftruncate(fd, (off_t)sz) != 0) {
     flock(fd, LOCK_UN);
     close(fd);
     return nullptr;
@@ -85,9 +105,7 @@ vgpu_board_t* board_map(const char* path) {
     return nullptr;
   }
   auto* b = (vgpu_board_t*)p;
-  if (fresh || b->magic != VGPU_BOARD_MAGIC || b->version != VGPU_BOARD_VERSION ||
-      b->struct_size != sz || !b->initialized)
-    init_board(b);
+  if (blank) init_board(b);
   flock(fd, LOCK_UN);
   close(fd);
   return b;
@@ -182,6 +200,16 @@ bool fresh(const vgpu_board_slot_t& s, uint64_t now) {
   return s.pid != 0 && now - s.heartbeat_ns < VGPU_BOARD_STALE_NS;
 }
 }  // namespace
+
+// The launch admitted by board_gate was not tracked after all (launch error,
+// no marker, capture): nothing will drain through board_charge(leave), so
+// leave the running set now unless tracked work of ours is still queued.
+void board_gate_abort(vgpu_board_t* b, int slot) {
+  if (!b || slot < 0 || !lock(b)) return;
+  vgpu_board_slot_t& me = b->slot[slot];
+  if (!me.active) me.running = 0;
+  unlock(b);
+}
 
 bool board_gate(vgpu_board_t* b, int slot, int max_running, uint64_t quantum_ns) {
   if (!b || slot < 0 || max_running <= 0 || !lock(b)) return true;

@@ -18,6 +18,7 @@ int board_active_count(vgpu_board_t* b);
 // past `quantum_ns` yields to the oldest waiter.
 bool board_gate(vgpu_board_t* b, int slot, int max_running, uint64_t quantum_ns);
 int board_running_count(vgpu_board_t* b);
+void board_gate_abort(vgpu_board_t* b, int slot);  // admitted launch was not tracked
 double board_entitlement(vgpu_board_t* b, int slot);  // weighted fair share among active slots
 
 }  // namespace vgpu

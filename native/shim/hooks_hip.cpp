@@ -317,7 +317,7 @@ __attribute__((visibility("default"))) hipError_t hipLaunchKernel(const void* f,
   const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
   vmem_scan_args(args);
   hipError_t rc = REAL_HIP(hipLaunchKernel)(f, grid, block, args, shmem, stream);
-  if (track && rc == hipSuccess) limiter_track(dev, stream);
+  if (track) limiter_track(dev, stream, rc);
   return rc;
 }
 
@@ -331,7 +331,7 @@ __attribute__((visibility("default"))) hipError_t hipExtLaunchKernel(const void*
   const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
   vmem_scan_args(args);
   hipError_t rc = REAL_HIP(hipExtLaunchKernel)(f, grid, block, args, shmem, stream, start, stop, flags);
-  if (track && rc == hipSuccess) limiter_track(dev, stream);
+  if (track) limiter_track(dev, stream, rc);
   return rc;
 }
 
@@ -345,7 +345,7 @@ __attribute__((visibility("default"))) hipError_t hipModuleLaunchKernel(
   if (extra) vmem_scan_extra(extra);
   else vmem_scan_args(params);
   hipError_t rc = REAL_HIP(hipModuleLaunchKernel)(f, gx, gy, gz, bx, by, bz, shmem, stream, params, extra);
-  if (track && rc == hipSuccess) limiter_track(dev, stream);
+  if (track) limiter_track(dev, stream, rc);
   return rc;
 }
 
@@ -362,7 +362,7 @@ __attribute__((visibility("default"))) hipError_t hipExtModuleLaunchKernel(
   else vmem_scan_args(params);
   hipError_t rc = REAL_HIP(hipExtModuleLaunchKernel)(f, gwx, gwy, gwz, lwx, lwy, lwz, shmem, stream,
                                                      params, extra, start, stop, flags);
-  if (track && rc == hipSuccess) limiter_track(dev, stream);
+  if (track) limiter_track(dev, stream, rc);
   return rc;
 }
 
@@ -402,7 +402,7 @@ __attribute__((visibility("default"))) hipError_t hipLaunchCooperativeKernel(con
   const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
   vmem_scan_args(params);
   hipError_t rc = REAL_HIP(hipLaunchCooperativeKernel)(f, grid, block, params, shmem, stream);
-  if (track && rc == hipSuccess) limiter_track(dev, stream);
+  if (track) limiter_track(dev, stream, rc);
   return rc;
 }
 
@@ -414,7 +414,7 @@ __attribute__((visibility("default"))) hipError_t hipModuleLaunchCooperativeKern
   const bool track = limiter_on_launch(dev, blocks3(gx, gy, gz));
   vmem_scan_args(params);
   hipError_t rc = REAL_HIP(hipModuleLaunchCooperativeKernel)(f, gx, gy, gz, bx, by, bz, shmem, stream, params);
-  if (track && rc == hipSuccess) limiter_track(dev, stream);
+  if (track) limiter_track(dev, stream, rc);
   return rc;
 }
 
@@ -425,7 +425,7 @@ __attribute__((visibility("default"))) hipError_t hipLaunchKernelExC(const hipLa
   const bool track = cfg && limiter_on_launch(dev, blocks3(cfg->gridDim.x, cfg->gridDim.y, cfg->gridDim.z), f);
   vmem_scan_args(args);
   hipError_t rc = REAL_HIP(hipLaunchKernelExC)(cfg, f, args);
-  if (track && rc == hipSuccess) limiter_track(dev, cfg->stream);
+  if (track) limiter_track(dev, cfg->stream, rc);
   return rc;
 }
 
@@ -445,7 +445,7 @@ __attribute__((visibility("default"))) hipError_t hipGraphLaunch(hipGraphExec_t 
   const int dev = cur_dev();
   const bool track = limiter_on_launch(dev, wg ? wg : fallback_tokens);
   hipError_t rc = REAL_HIP(hipGraphLaunch)(exec, stream);
-  if (track && rc == hipSuccess) limiter_track(dev, stream);
+  if (track) limiter_track(dev, stream, rc);
   return rc;
 }
 
@@ -480,8 +480,10 @@ __attribute__((visibility("default"))) hipError_t hipGraphExecDestroy(hipGraphEx
   return REAL_HIP(hipGraphExecDestroy)(exec);
 }
 
-// Stream capture bracketing (see g_open_captures).  A capture that ends in
-// another thread or never ends only delays marker polling, never correctness.
+// Stream capture bracketing (see g_open_captures).  While a capture is open the
+// limiter neither records nor polls markers on the capturing streams (their
+// launches are charged when the graph runs); eager work on other streams is
+// tracked and charged as usual.
 __attribute__((visibility("default"))) hipError_t hipStreamBeginCapture(hipStream_t stream,
                                                                         hipStreamCaptureMode mode) {
   {

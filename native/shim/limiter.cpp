@@ -142,7 +142,9 @@ void attach_board(int dev, DevLimiter& L) {
   struct stat stt;
   if (stat(lock_dir(), &stt) != 0 || !S_ISDIR(stt.st_mode)) return;
   char path[640];
-  snprintf(path, sizeof path, "%s/%s.board", lock_dir(), key);
+  // Layout version in the name: shims of different board layouts never share
+  // a mapping during a rolling upgrade.
+  snprintf(path, sizeof path, "%s/%s.v%u.board", lock_dir(), key, (unsigned)VGPU_BOARD_VERSION);
   L.board = board_map(path);
   if (!L.board) return;
   L.board_slot = board_claim(L.board, getpid(), self_host_pid(nullptr), (int)lround(L.frac * 100));
@@ -224,11 +226,20 @@ void configure() {
   g_throttle_any.store(any, std::memory_order_release);
 }
 
-// Record one marker on `stream` (caller holds L.mu; the limiter thread also
-// holds the capture guard, so a capture cannot begin on the stream and swallow
-// our event).  Returns 1 when a marker was recorded.
+// True while `stream` is being captured into a graph (a marker recorded or
+// queried there would join or invalidate the capture).
+bool stream_capturing(hipStream_t stream) {
+  if (g_open_captures.load(std::memory_order_acquire) == 0) return false;
+  auto is_cap = REAL_HIP(hipStreamIsCapturing);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return !is_cap || is_cap(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+}
+
+// Record one marker on `stream`, which the caller checked is not capturing
+// (caller holds L.mu; the limiter thread also holds the capture guard, so a
+// capture cannot begin on the stream and swallow our event).  Returns 1 when a
+// marker was recorded.
 int record_marker(DevLimiter& L, hipStream_t stream, StreamTrack& t) {
-  if (g_open_captures.load(std::memory_order_acquire) > 0) return 0;
   hipEvent_t ev = nullptr;
   if (!L.free_ev.empty()) {
     ev = L.free_ev.back();
@@ -259,8 +270,7 @@ int record_marker(DevLimiter& L, hipStream_t stream, StreamTrack& t) {
 // hipErrorStreamCaptureInvalidated).
 bool reap(int dev, DevLimiter& L, uint64_t now_hint) {
   if (L.outstanding.load(std::memory_order_relaxed) == 0) return false;
-  std::shared_lock<std::shared_mutex> cap(g_capture_mu);
-  if (g_open_captures.load(std::memory_order_acquire) > 0) return true;  // poll after the capture
+  std::shared_lock<std::shared_mutex> cap(g_capture_mu);  // no capture begins during the poll
   auto query = REAL_HIP(hipEventQuery);
   std::lock_guard<std::mutex> g(L.mu);
   int done = 0;
@@ -269,6 +279,12 @@ bool reap(int dev, DevLimiter& L, uint64_t now_hint) {
   for (auto it = L.streams.begin(); it != L.streams.end();) {
     StreamTrack& t = it->second;
     auto& q = t.q;
+    // A stream being captured is polled after its capture ends; the others
+    // (eager work while some capture is open elsewhere) are charged as usual.
+    if (stream_capturing(it->first)) {
+      ++it;
+      continue;
+    }
     while (!q.empty()) {
       hipError_t rc = query(q.front().ev);
       if (rc == hipErrorNotReady || rc == hipErrorStreamCaptureUnsupported ||
@@ -543,10 +559,16 @@ bool limiter_on_launch(int dev, uint64_t wg, const void* fn) {
   return true;
 }
 
-void limiter_track(int dev, hipStream_t stream) {
+void limiter_track(int dev, hipStream_t stream, hipError_t launch_rc) {
   if (dev < 0 || dev >= VGPU_MAX_DEVICES) return;
   DevLimiter& L = g_lim[dev];
-  if (g_open_captures.load(std::memory_order_acquire) > 0) return;  // no HIP calls mid-capture
+  // Not tracked: the launch failed, or it was captured into a graph (it runs
+  // when the graph is launched, and is charged then).  A concurrency-gate turn
+  // taken for it must not stay claimed with nothing to drain it.
+  auto untracked = [&] {
+    if (L.max_running > 0 && L.board && !L.outstanding.load()) board_gate_abort(L.board, L.board_slot);
+  };
+  if (launch_rc != hipSuccess || stream_capturing(stream)) return untracked();
   static const uint64_t interval_ns = [] {
     const char* v = env_first("VGPU_LIMITER_MARK_US");
     return (uint64_t)((v ? atof(v) : 0.0) * 1000.0);
@@ -560,14 +582,11 @@ void limiter_track(int dev, hipStream_t stream) {
     t.dirty = true;  // covered by the next marker (ours or the limiter thread's)
     return;
   }
-  auto is_cap = REAL_HIP(hipStreamIsCapturing);
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if ((is_cap && is_cap(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) ||
-      !record_marker(L, stream, t)) {
-    // captured (not executed now) or no marker possible: not tracked
+  if (!record_marker(L, stream, t)) {  // no marker possible: not tracked
     t.unmarked--;
     L.inflight.fetch_sub(1, std::memory_order_relaxed);
-    return;
+    g.unlock();
+    return untracked();
   }
   if (L.outstanding.fetch_add(1) == 0) {
     attach_board(dev, L);

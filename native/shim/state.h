@@ -92,13 +92,14 @@ void limiter_after_fork();
 // Called before every dispatch with the number of workgroups it launches;
 // blocks while the temporal limiter's bucket is overdrawn.  `fn` = the
 // kernel's host stub when known (RCCL kernels are exempt from throttling).
-// Returns true when the launch must be tracked: call limiter_track after a
-// successful launch on `stream`.
+// Returns true when the launch must be tracked: call limiter_track after the
+// launch on `stream` with its result.
 bool limiter_on_launch(int dev, uint64_t workgroups, const void* fn = nullptr);
-void limiter_track(int dev, hipStream_t stream);
-// Stream captures in progress anywhere in the process: the limiter thread makes
-// no HIP call while one is open (an event query can invalidate a global-mode
-// capture on another thread).
+void limiter_track(int dev, hipStream_t stream, hipError_t launch_rc);
+// Stream captures in progress anywhere in the process: while one is open the
+// limiter records and polls markers only on streams that are not capturing (an
+// event query on a capturing stream invalidates its capture), and capture
+// begin waits for a limiter poll in progress (g_capture_mu).
 extern std::atomic<int> g_open_captures;
 extern std::shared_mutex g_capture_mu;  // writers: capture begin; readers: limiter-thread markers
 void limiter_stats(int dev, uint64_t* charged_ns, uint64_t* busy_ns);

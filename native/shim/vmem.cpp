@@ -303,16 +303,27 @@ void pager_step() {
     std::shared_lock<std::shared_mutex> g(g_tab_mu);
     for (VRange* r : g_tab) r->uses.store(r->uses.load() / 2);
   }
-  std::vector<VRange*> hot;
+  // Snapshot the candidates by value under the table lock: a concurrent
+  // hipFree (vmem_release) may delete a range as soon as the lock is dropped,
+  // so a pointer is dereferenced again only after re-checking membership
+  // under g_move_mu (which vmem_release also holds).
+  struct Cand {
+    VRange* r;
+    uint32_t uses;
+  };
+  std::vector<Cand> hot;
   {
     std::shared_lock<std::shared_mutex> g(g_tab_mu);
     for (VRange* r : g_tab)
-      if (r->gpu_bytes < r->size && r->last_use.load() + k.hot_ticks >= tick && r->last_use.load()) hot.push_back(r);
+      if (r->gpu_bytes < r->size && r->last_use.load() + k.hot_ticks >= tick && r->last_use.load())
+        hot.push_back({r, r->uses.load()});
   }
   if (hot.empty()) return;
-  std::sort(hot.begin(), hot.end(), [](VRange* a, VRange* b) { return a->uses.load() > b->uses.load(); });
+  std::sort(hot.begin(), hot.end(), [](const Cand& a, const Cand& b) { return a.uses > b.uses; });
   uint64_t waiting = 0;
-  for (VRange* r : hot) {
+  int waiting_dev = -1;
+  for (const Cand& c : hot) {
+    VRange* r = c.r;
     std::lock_guard<std::mutex> m(g_move_mu);
     {  // freed meanwhile?
       std::shared_lock<std::shared_mutex> g(g_tab_mu);
@@ -323,6 +334,7 @@ void pager_step() {
       uint64_t n = std::min<uint64_t>(k.piece, r->size - r->gpu_bytes);
       if (!make_room_locked(r->dev, n, r, stale) || !promote_piece_locked(r)) {
         waiting += r->size - r->gpu_bytes;
+        waiting_dev = r->dev;
         break;
       }
     }
@@ -331,7 +343,7 @@ void pager_step() {
   if (waiting && tick - last_note >= 1000 / (uint64_t)k.tick_ms) {
     last_note = tick;
     VLOG_INFO("vmem: %llu bytes of used spilled ranges wait for HBM (free for the pager %llu)",
-              (unsigned long long)waiting, (unsigned long long)hbm_free(hot.front()->dev));
+              (unsigned long long)waiting, (unsigned long long)hbm_free(waiting_dev));
   }
 }
 

@@ -16,7 +16,7 @@ from vgpu.config import DevicePluginConfig
 from vgpu.device.base import init_default_devices
 from vgpu.device.cualloc import MI355X, parse_mask
 from vgpu.deviceplugin import api
-from vgpu.deviceplugin.custate import CUMaskState
+from vgpu.deviceplugin.custate import CUMaskState, ShareGrant
 from vgpu.deviceplugin.discovery import (EVT_POST_RESET, EVT_PRE_RESET, LINK_XGMI, SmiBackend,
                                          StaticBackend, mi355x_node)
 from vgpu.deviceplugin.register import register_once
@@ -153,6 +153,33 @@ def test_cumask_state_temporal_policy_never_masks(tmp_path):
         sg = st.allocate(f"u{i}_c", [("GPU-0", 25)])["GPU-0"]
         assert sg.temporal and sg.mask == 0
     assert st.used("GPU-0") == 0
+
+
+def test_mask_after_pool_members_shrinks_the_pool(native_build, tmp_path, monkeypatch):
+    """a temporal pod admitted BEFORE a mask pod runs on every CU
+    (mask 0).  The mask pod's CUs must still be exclusive: the earlier pool
+    member's grant and its live shared region shrink to the remaining pool."""
+    import os
+    from vgpu.monitor.region import AttachedRegion
+    st = CUMaskState(str(tmp_path), policy="temporal")
+    a = st.allocate("ua_c", [("GPU-0", 25)])["GPU-0"]
+    assert a.temporal and a.mask == 0
+    for k in list(os.environ):
+        if k.startswith("VGPU_"):
+            monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("VGPU_DEVICE_MEMORY_LIMIT_0", "8g")
+    monkeypatch.setenv("VGPU_DEVICE_UUID_0", "GPU-0")
+    live = AttachedRegion(str(tmp_path / "ua_c" / "vgpu.cache"), create=True)  # pool member is running
+    assert live.devices()[0].cu_mask == 0
+    m = st.allocate("um_c", [("GPU-0", 25)], policy="mask")["GPU-0"]
+    assert m.mode == "mask" and bin(m.mask).count("1") == 64
+    pool = ((1 << 256) - 1) & ~m.mask
+    assert st._grants()["ua_c"]["GPU-0"] == ShareGrant(pool, "pool")
+    assert live.devices()[0].cu_mask == pool
+    # later pool members get the same pool
+    b = st.allocate("ub_c", [("GPU-0", 25)])["GPU-0"]
+    assert b.temporal and b.mask == pool
+    live.close()
 
 
 def test_cumask_state_reads_round1_grant_format(tmp_path):

@@ -51,6 +51,7 @@ from vgpu.device.cualloc import MI355X, CULayout, alloc_cu_mask, resolve_packing
 log = logging.getLogger("vgpu.deviceplugin.custate")
 
 GRANT_FILE = "grant.json"
+REGION_FILE = "vgpu.cache"  # the container's shared region (allocate.py: VGPU_SHARED_REGION)
 MODE_MASK = "mask"
 MODE_POOL = "pool"
 POLICIES = ("mask", "temporal", "hybrid")
@@ -150,13 +151,62 @@ class CUMaskState:
                 else:
                     pool = full & ~masked
                     res[uuid] = ShareGrant(0 if pool == full else pool, MODE_POOL)
-            d = self.dir / container_key
-            d.mkdir(parents=True, exist_ok=True)
-            tmp = d / (GRANT_FILE + ".tmp")
-            tmp.write_text(json.dumps({k: {"mask": hex(v.mask), "mode": v.mode} for k, v in res.items()
-                                       if v.mask or v.mode == MODE_POOL}))
-            os.replace(tmp, d / GRANT_FILE)
+            self._write_grant(container_key, res)
+            grants[container_key] = res
+            for uuid, sg in res.items():
+                if sg.mode == MODE_MASK and sg.mask:
+                    lay = layouts.get(uuid, self.layout)
+                    self._reshape_pool(uuid, grants, (1 << lay.total_cus) - 1)
             return res
+
+    def _write_grant(self, container_key: str, res: dict[str, ShareGrant]) -> None:
+        d = self.dir / container_key
+        d.mkdir(parents=True, exist_ok=True)
+        tmp = d / (GRANT_FILE + ".tmp")
+        tmp.write_text(json.dumps({k: {"mask": hex(v.mask), "mode": v.mode} for k, v in res.items()
+                                   if v.mask or v.mode == MODE_POOL}))
+        os.replace(tmp, d / GRANT_FILE)
+
+    def _reshape_pool(self, uuid: str, grants: dict[str, dict[str, ShareGrant]], full: int) -> None:
+        """A masked grant took CUs of `uuid`: every pool member of that device
+        shrinks to the CUs no masked container holds, so the new container's CUs
+        are exclusive even when pool members were admitted before it (a pool
+        member with mask 0 runs on every CU).  The grant file is rewritten and,
+        when the container is running, its shared region's CU mask too: the
+        shim re-applies region masks to its live queues within ~10 ms
+        (limiter.cpp) and rescales its time share to the smaller pool."""
+        masked = 0
+        for g in grants.values():
+            sg = g.get(uuid)
+            if sg and sg.mode == MODE_MASK:
+                masked |= sg.mask
+        pool = full & ~masked
+        want = 0 if pool == full else pool
+        for key, g in grants.items():
+            sg = g.get(uuid)
+            if not sg or sg.mode != MODE_POOL or sg.mask == want:
+                continue
+            g[uuid] = ShareGrant(want, MODE_POOL)
+            self._write_grant(key, g)
+            self._update_region(key, uuid, want)
+            log.info("container %s: pool of %s reshaped to %d CUs", key, uuid, bin(want or full).count("1"))
+
+    def _update_region(self, container_key: str, uuid: str, mask: int) -> None:
+        path = self.dir / container_key / REGION_FILE
+        if not path.exists():
+            return
+        try:
+            from vgpu.monitor.region import AttachedRegion
+            r = AttachedRegion(str(path))
+        except (OSError, RuntimeError) as e:
+            log.warning("cannot reshape live region %s: %s", path, e)
+            return
+        try:
+            for d in r.devices():
+                if d.uuid == uuid:
+                    r.set_cu_mask(d.index, mask)
+        finally:
+            r.close()
 
     def gc(self, live_pod_uids: set[str], grace_s: float = 300.0) -> list[str]:
         """Remove container dirs whose pod UID is gone for longer than `grace_s`
