@@ -133,6 +133,7 @@ struct FakeEvent {
 // VGPU_FAKE_QUERY_US widens hipEventQuery so tests can hit that window.
 std::mutex g_cap_mu;
 std::map<hipStream_t, bool> g_capturing;  // stream -> invalidated
+std::map<hipStream_t, unsigned long long> g_capture_id;  // stream -> capture id
 
 hsa_status_t pick_gpu(hsa_agent_t a, void* data) {
   auto* v = (std::vector<hsa_agent_t>*)data;
@@ -356,16 +357,18 @@ hipError_t hipStreamBeginCapture(hipStream_t s, hipStreamCaptureMode) {
   std::lock_guard<std::mutex> g(g_cap_mu);
   if (g_capturing.count(s)) return hipErrorIllegalState;
   g_capturing[s] = false;
+  static unsigned long long next_id = 100;
+  g_capture_id[s] = ++next_id;
   return hipSuccess;
 }
-hipError_t hipStreamEndCapture(hipStream_t s, hipGraph_t* g) {
-  if (g) *g = nullptr;
+hipError_t hipStreamGetCaptureInfo(hipStream_t s, hipStreamCaptureStatus* st, unsigned long long* id) {
   std::lock_guard<std::mutex> lk(g_cap_mu);
   auto it = g_capturing.find(s);
-  if (it == g_capturing.end()) return hipErrorIllegalState;
-  const bool invalid = it->second;
-  g_capturing.erase(it);
-  return invalid ? hipErrorStreamCaptureInvalidated : hipSuccess;
+  if (st)
+    *st = it == g_capturing.end() ? hipStreamCaptureStatusNone
+                                  : (it->second ? hipStreamCaptureStatusInvalidated : hipStreamCaptureStatusActive);
+  if (id) *id = it == g_capturing.end() ? 0 : g_capture_id[s];
+  return hipSuccess;
 }
 
 hipError_t hipMalloc(void** p, size_t size) { return dev_alloc(p, size, tl_dev); }
@@ -512,6 +515,23 @@ struct FakeNode {
 struct FakeGraph {
   std::vector<FakeNode*> nodes;
 };
+// A capture yields an (empty) graph: enough for the shim's capture -> graph
+// -> exec bookkeeping.
+hipError_t hipStreamEndCapture(hipStream_t s, hipGraph_t* g) {
+  if (g) *g = nullptr;
+  std::lock_guard<std::mutex> lk(g_cap_mu);
+  auto it = g_capturing.find(s);
+  if (it == g_capturing.end()) return hipErrorIllegalState;
+  const bool invalid = it->second;
+  g_capturing.erase(it);
+  g_capture_id.erase(s);
+  if (!invalid && g) *g = reinterpret_cast<hipGraph_t>(new FakeGraph);
+  return invalid ? hipErrorStreamCaptureInvalidated : hipSuccess;
+}
+hipError_t hipGraphDestroy(hipGraph_t g) {
+  delete reinterpret_cast<FakeGraph*>(g);
+  return hipSuccess;
+}
 hipError_t hipGraphGetNodes(hipGraph_t g, hipGraphNode_t* nodes, size_t* n) {
   auto* fg = reinterpret_cast<FakeGraph*>(g);
   if (!fg || !n) return hipErrorInvalidValue;

@@ -82,7 +82,8 @@ typedef struct vgpu_proc_slot {
 typedef struct vgpu_device_cfg {
   char uuid[VGPU_UUID_LEN];
   uint64_t mem_limit;       /* bytes; 0 = unlimited                          */
-  uint64_t mem_physical;    /* bytes of HBM on the physical device (0 = unknown) */
+  uint64_t mem_physical;    /* the container's physical HBM budget (bytes; 0 = whole device):
+                             * virtual device memory keeps at most this much resident */
   uint32_t cu_limit;        /* percent of the device's CUs, 0 or >=100 = unlimited */
   uint32_t cu_total;        /* CUs on the physical device                    */
   uint64_t cu_mask[VGPU_CU_MASK_WORDS]; /* HSA logical CU mask; all-zero = no mask */

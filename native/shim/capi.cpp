@@ -150,6 +150,10 @@ __attribute__((visibility("default"))) void vgpu_self_add_swap(int dev, uint64_t
 
 // Virtual device memory pager counters: bytes promoted / demoted, migrations,
 // bytes of spilled ranges now resident in HBM, spilled ranges alive.
+__attribute__((visibility("default"))) uint64_t vgpu_self_graph_ranges(hipGraphExec_t exec) {
+  return vmem_graph_ranges(exec);
+}
+
 __attribute__((visibility("default"))) void vgpu_self_vmem_stats(uint64_t out[5]) {
   ensure_init();
   vmem_stats(&out[0], &out[1], &out[2], &out[3], &out[4]);

@@ -93,6 +93,18 @@ hipError_t charged_alloc(void** ptr, size_t size, int kind, F&& real_alloc) {
   suspend_gate();
   int dev = cur_dev();
   charge_context(dev);
+  if (kind == kDeviceBuf && vmem_wants_managed(dev, size)) {
+    // Virtual device memory with a physical budget: a managed range from the
+    // start, resident while the pod's budget has room (vmem.cpp).
+    if (!mem_reserve(dev, size, kHostSpill)) return hipErrorOutOfMemory;
+    hipError_t rc = vmem_alloc_managed(ptr, size, dev);
+    if (rc != hipSuccess) {
+      mem_unreserve(dev, size, kHostSpill);
+      return hipErrorOutOfMemory;
+    }
+    ledger_add(*ptr, size, dev, kHostSpill);
+    return rc;
+  }
   if (!mem_reserve(dev, size, kind)) return hipErrorOutOfMemory;
   const bool over = kind == kDeviceBuf && s.region && s.region->oversubscribe;
   hipError_t rc = over && vmem_should_spill(dev, size) ? hipErrorOutOfMemory : real_alloc();
@@ -315,7 +327,7 @@ __attribute__((visibility("default"))) hipError_t hipLaunchKernel(const void* f,
   ensure_init();
   const int dev = cur_dev();
   const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
-  vmem_scan_args(args);
+  vmem_scan_args(args, stream);
   hipError_t rc = REAL_HIP(hipLaunchKernel)(f, grid, block, args, shmem, stream);
   if (track) limiter_track(dev, stream, rc);
   return rc;
@@ -329,7 +341,7 @@ __attribute__((visibility("default"))) hipError_t hipExtLaunchKernel(const void*
   ensure_init();
   const int dev = cur_dev();
   const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
-  vmem_scan_args(args);
+  vmem_scan_args(args, stream);
   hipError_t rc = REAL_HIP(hipExtLaunchKernel)(f, grid, block, args, shmem, stream, start, stop, flags);
   if (track) limiter_track(dev, stream, rc);
   return rc;
@@ -342,8 +354,8 @@ __attribute__((visibility("default"))) hipError_t hipModuleLaunchKernel(
   ensure_init();
   const int dev = cur_dev();
   const bool track = limiter_on_launch(dev, blocks3(gx, gy, gz));
-  if (extra) vmem_scan_extra(extra);
-  else vmem_scan_args(params);
+  if (extra) vmem_scan_extra(extra, stream);
+  else vmem_scan_args(params, stream);
   hipError_t rc = REAL_HIP(hipModuleLaunchKernel)(f, gx, gy, gz, bx, by, bz, shmem, stream, params, extra);
   if (track) limiter_track(dev, stream, rc);
   return rc;
@@ -358,8 +370,8 @@ __attribute__((visibility("default"))) hipError_t hipExtModuleLaunchKernel(
   auto nb = [](uint32_t g, uint32_t l) { return l ? (g + l - 1) / l : g; };
   const int dev = cur_dev();
   const bool track = limiter_on_launch(dev, blocks3(nb(gwx, lwx), nb(gwy, lwy), nb(gwz, lwz)));
-  if (extra) vmem_scan_extra(extra);
-  else vmem_scan_args(params);
+  if (extra) vmem_scan_extra(extra, stream);
+  else vmem_scan_args(params, stream);
   hipError_t rc = REAL_HIP(hipExtModuleLaunchKernel)(f, gwx, gwy, gwz, lwx, lwy, lwz, shmem, stream,
                                                      params, extra, start, stop, flags);
   if (track) limiter_track(dev, stream, rc);
@@ -400,7 +412,7 @@ __attribute__((visibility("default"))) hipError_t hipLaunchCooperativeKernel(con
   if (g != hipSuccess) return g;
   const int dev = cur_dev();
   const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
-  vmem_scan_args(params);
+  vmem_scan_args(params, stream);
   hipError_t rc = REAL_HIP(hipLaunchCooperativeKernel)(f, grid, block, params, shmem, stream);
   if (track) limiter_track(dev, stream, rc);
   return rc;
@@ -412,7 +424,7 @@ __attribute__((visibility("default"))) hipError_t hipModuleLaunchCooperativeKern
   ensure_init();
   const int dev = cur_dev();
   const bool track = limiter_on_launch(dev, blocks3(gx, gy, gz));
-  vmem_scan_args(params);
+  vmem_scan_args(params, stream);
   hipError_t rc = REAL_HIP(hipModuleLaunchCooperativeKernel)(f, gx, gy, gz, bx, by, bz, shmem, stream, params);
   if (track) limiter_track(dev, stream, rc);
   return rc;
@@ -423,7 +435,7 @@ __attribute__((visibility("default"))) hipError_t hipLaunchKernelExC(const hipLa
   ensure_init();
   const int dev = cur_dev();
   const bool track = cfg && limiter_on_launch(dev, blocks3(cfg->gridDim.x, cfg->gridDim.y, cfg->gridDim.z), f);
-  vmem_scan_args(args);
+  vmem_scan_args(args, cfg ? cfg->stream : nullptr);
   hipError_t rc = REAL_HIP(hipLaunchKernelExC)(cfg, f, args);
   if (track) limiter_track(dev, cfg->stream, rc);
   return rc;
@@ -444,6 +456,7 @@ __attribute__((visibility("default"))) hipError_t hipGraphLaunch(hipGraphExec_t 
   uint64_t wg = graph_exec_workgroups(exec);
   const int dev = cur_dev();
   const bool track = limiter_on_launch(dev, wg ? wg : fallback_tokens);
+  vmem_graph_launched(exec);
   hipError_t rc = REAL_HIP(hipGraphLaunch)(exec, stream);
   if (track) limiter_track(dev, stream, rc);
   return rc;
@@ -454,7 +467,10 @@ __attribute__((visibility("default"))) hipError_t hipGraphInstantiate(hipGraphEx
                                                                       char* pLogBuffer, size_t bufferSize) {
   ensure_init();
   hipError_t rc = REAL_HIP(hipGraphInstantiate)(pExec, graph, pErrorNode, pLogBuffer, bufferSize);
-  if (rc == hipSuccess && pExec) graph_exec_record(*pExec, graph);
+  if (rc == hipSuccess && pExec) {
+    graph_exec_record(*pExec, graph);
+    vmem_graph_instantiated(graph, *pExec);
+  }
   return rc;
 }
 
@@ -463,7 +479,10 @@ __attribute__((visibility("default"))) hipError_t hipGraphInstantiateWithFlags(h
                                                                                unsigned long long flags) {
   ensure_init();
   hipError_t rc = REAL_HIP(hipGraphInstantiateWithFlags)(pExec, graph, flags);
-  if (rc == hipSuccess && pExec) graph_exec_record(*pExec, graph);
+  if (rc == hipSuccess && pExec) {
+    graph_exec_record(*pExec, graph);
+    vmem_graph_instantiated(graph, *pExec);
+  }
   return rc;
 }
 
@@ -471,13 +490,22 @@ __attribute__((visibility("default"))) hipError_t hipGraphInstantiateWithParams(
     hipGraphExec_t* pExec, hipGraph_t graph, hipGraphInstantiateParams* params) {
   ensure_init();
   hipError_t rc = REAL_HIP(hipGraphInstantiateWithParams)(pExec, graph, params);
-  if (rc == hipSuccess && pExec) graph_exec_record(*pExec, graph);
+  if (rc == hipSuccess && pExec) {
+    graph_exec_record(*pExec, graph);
+    vmem_graph_instantiated(graph, *pExec);
+  }
   return rc;
 }
 
 __attribute__((visibility("default"))) hipError_t hipGraphExecDestroy(hipGraphExec_t exec) {
   graph_exec_forget(exec);
+  vmem_graph_destroyed(exec);
   return REAL_HIP(hipGraphExecDestroy)(exec);
+}
+
+__attribute__((visibility("default"))) hipError_t hipGraphDestroy(hipGraph_t graph) {
+  vmem_graph_destroyed(graph);
+  return REAL_HIP(hipGraphDestroy)(graph);
 }
 
 // Stream capture bracketing (see g_open_captures).  While a capture is open the
@@ -509,7 +537,9 @@ __attribute__((visibility("default"))) hipError_t hipStreamBeginCaptureToGraph(
 
 __attribute__((visibility("default"))) hipError_t hipStreamEndCapture(hipStream_t stream,
                                                                       hipGraph_t* graph) {
+  const unsigned long long cid = vmem_capture_begin_id(stream);
   hipError_t rc = REAL_HIP(hipStreamEndCapture)(stream, graph);
+  if (cid) vmem_capture_ended(cid, rc == hipSuccess && graph ? *graph : nullptr);
   int cur = g_open_captures.load();
   while (cur > 0 && !g_open_captures.compare_exchange_weak(cur, cur - 1)) {
   }

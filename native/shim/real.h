@@ -93,6 +93,8 @@ using hipStreamBeginCapture = hipError_t (*)(hipStream_t, hipStreamCaptureMode);
 using hipStreamBeginCaptureToGraph = hipError_t (*)(hipStream_t, hipGraph_t, const hipGraphNode_t*,
                                                     const hipGraphEdgeData*, size_t, hipStreamCaptureMode);
 using hipStreamEndCapture = hipError_t (*)(hipStream_t, hipGraph_t*);
+using hipStreamGetCaptureInfo = hipError_t (*)(hipStream_t, hipStreamCaptureStatus*, unsigned long long*);
+using hipGraphDestroy = hipError_t (*)(hipGraph_t);
 using hipMalloc3D = hipError_t (*)(hipPitchedPtr*, hipExtent);
 using hipMallocArray = hipError_t (*)(hipArray_t*, const hipChannelFormatDesc*, size_t, size_t, unsigned int);
 using hipMalloc3DArray = hipError_t (*)(hipArray_t*, const hipChannelFormatDesc*, hipExtent, unsigned int);

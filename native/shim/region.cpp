@@ -31,6 +31,9 @@ DeviceLimits limits_from_env() {
     const char* v = env_first(a, b);
     L.mem_limit[i] = v ? parse_mem(v) : dflt_mem;
     if (v) maxdev = i;
+    snprintf(a, sizeof a, "VGPU_DEVICE_MEMORY_PHYSICAL_%d", i);
+    v = env_first(a);
+    L.mem_physical[i] = v ? parse_mem(v) : 0;
     snprintf(a, sizeof a, "VGPU_DEVICE_CU_LIMIT_%d", i);
     v = env_first(a);
     L.cu_limit[i] = v ? (uint32_t)atoi(v) : dflt_cu;
@@ -77,6 +80,7 @@ static void write_limits(vgpu_shared_region_t* r, const DeviceLimits& L) {
   for (int i = 0; i < VGPU_MAX_DEVICES; ++i) {
     vgpu_device_cfg_t& d = r->dev[i];
     d.mem_limit = L.mem_limit[i];
+    d.mem_physical = L.mem_physical[i];
     d.cu_limit = L.cu_limit[i];
     memcpy(d.cu_mask, L.cu_mask[i], sizeof(d.cu_mask));
     if (L.uuid[i][0]) memcpy(d.uuid, L.uuid[i], VGPU_UUID_LEN);
@@ -86,6 +90,7 @@ static void write_limits(vgpu_shared_region_t* r, const DeviceLimits& L) {
 static bool limits_differ(const vgpu_shared_region_t* r, const DeviceLimits& L) {
   for (int i = 0; i < VGPU_MAX_DEVICES; ++i) {
     if (r->dev[i].mem_limit != L.mem_limit[i]) return true;
+    if (r->dev[i].mem_physical != L.mem_physical[i]) return true;
     if (r->dev[i].cu_limit != L.cu_limit[i]) return true;
     if (memcmp(r->dev[i].cu_mask, L.cu_mask[i], sizeof(L.cu_mask[i]))) return true;
   }

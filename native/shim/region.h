@@ -17,6 +17,7 @@ namespace vgpu {
 struct DeviceLimits {
   int num_devices = 0;
   uint64_t mem_limit[VGPU_MAX_DEVICES] = {};
+  uint64_t mem_physical[VGPU_MAX_DEVICES] = {};  // physical HBM budget (VGPU_DEVICE_MEMORY_PHYSICAL_<i>)
   uint32_t cu_limit[VGPU_MAX_DEVICES] = {};
   uint64_t cu_mask[VGPU_MAX_DEVICES][VGPU_CU_MASK_WORDS] = {};
   char uuid[VGPU_MAX_DEVICES][VGPU_UUID_LEN] = {};

@@ -110,13 +110,27 @@ bool hsa_cpu_agent(hsa_agent_t* out);
 
 // Transparent virtual device memory (vmem.cpp).
 bool vmem_enabled();
-bool vmem_should_spill(int dev, uint64_t size);  // physical HBM (minus a runtime reserve) cannot take `size`
+// Physical HBM (minus a runtime reserve) or the pod's physical budget cannot
+// take `size` (already reserved against the cap).
+bool vmem_should_spill(int dev, uint64_t size);
+// With a physical budget, device allocations of at least VGPU_VMEM_MANAGED_MIN_MB
+// are managed ranges from the start (resident while the budget has room).
+bool vmem_wants_managed(int dev, uint64_t size);
+hipError_t vmem_alloc_managed(void** ptr, size_t size, int dev);
 hipError_t vmem_alloc_overflow(void** ptr, size_t size, int dev);
 bool vmem_owns(void* p);
 bool vmem_release(void* p);                 // forget a range before the real free; false if not ours
 bool vmem_make_room(int dev, uint64_t need); // demote cold promoted ranges; true if `need` now fits
-void vmem_scan_args(void** args);           // HIP-Clang stub argument array
-void vmem_scan_extra(void** extra);         // HIP_LAUNCH_PARAM_BUFFER_* kernarg blob
+void vmem_scan_args(void** args, hipStream_t stream);    // HIP-Clang stub argument array
+void vmem_scan_extra(void** extra, hipStream_t stream);  // HIP_LAUNCH_PARAM_BUFFER_* kernarg blob
+// Graphs: ranges named by captured launches follow capture -> graph -> exec,
+// and every launch of the exec stamps them.
+unsigned long long vmem_capture_begin_id(hipStream_t stream);  // 0 when not capturing
+void vmem_capture_ended(unsigned long long capture_id, hipGraph_t graph);
+void vmem_graph_instantiated(hipGraph_t graph, hipGraphExec_t exec);
+void vmem_graph_destroyed(const void* graph_or_exec);
+void vmem_graph_launched(hipGraphExec_t exec);
+uint64_t vmem_graph_ranges(hipGraphExec_t exec);
 void vmem_stats(uint64_t* in_bytes, uint64_t* out_bytes, uint64_t* moves, uint64_t* gpu_bytes, uint64_t* ranges);
 void vmem_stop();
 void vmem_after_fork();

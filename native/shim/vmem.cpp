@@ -17,21 +17,40 @@
 // process's queues paused by KFD during the move, so it is always safe.
 //
 // Design:
-//   * an allocation that no longer fits in physical HBM (the real allocator
-//     says out-of-memory, the container cap still has room) becomes a
-//     coarse-grained managed range that starts host-resident;
+//   * every pod has a physical HBM budget per device (region dev[].mem_physical,
+//     VGPU_DEVICE_MEMORY_PHYSICAL_<i>; the device plugin sets cap / memory
+//     scaling on an oversubscribed node, so co-located pods split the HBM
+//     instead of the first one to allocate taking it all).  0 = whole device;
+//   * with a budget, every device allocation of at least VGPU_VMEM_MANAGED_MIN_MB
+//     (32) is a coarse-grained managed range from the start, made resident at
+//     once while the budget (and physical HBM beyond the headroom) has room,
+//     after demoting cold ranges -- so memory a pod no longer uses can give way
+//     to memory it does (a second model, an idle KV pool).  Without a budget,
+//     only an allocation that no longer fits in physical HBM becomes a
+//     managed range (it starts host-resident);
 //   * every kernel launch scans its argument blob for pointers into those
 //     ranges (the HIP-Clang stub's argument array lives in the caller's
 //     frame; module launches carry a sized kernarg buffer) and stamps the
 //     range's last-use tick — no metadata, no device-side cost, and a missed
 //     or spurious hit only costs performance, never correctness;
+//   * launches captured into a hipGraph are scanned the same way at capture
+//     time and the ranges they name are kept per capture -> graph -> exec;
+//     every hipGraphLaunch stamps them (a replayed graph runs no hooks);
 //   * a pager thread promotes recently used host-resident ranges into HBM
-//     while physical HBM has room (beyond VGPU_VMEM_HEADROOM_MB), and demotes
-//     ranges it promoted earlier that went cold when a hotter one is waiting
-//     or when a new allocation needs the room;
+//     while the budget and physical HBM have room, and demotes ranges that
+//     went cold when a hotter one is waiting or a new allocation needs the
+//     room.  Hot ranges are never demoted for other hot ranges: when the hot
+//     set exceeds the budget the resident part stays put and the rest is read
+//     in place (zero-copy), which for a cyclic sweep beats any LRU exchange;
+//   * SIGUSR2 (suspend) demotes everything the process holds in HBM through
+//     managed ranges; after SIGUSR1 ranges come back as they are used;
 //   * charges never change (the cap counts HBM + host), only where they are
 //     booked: host_bytes <-> buffer/total bytes, plus swap_in/swap_out bytes
 //     and VGPU_EV_MIGRATE trace events.
+// KFD moves SVM pages at 6-7 GB/s up and 9-11 GB/s down on MI355X regardless
+// of piece size, transparent huge pages or concurrency (native/probes/
+// svm_rate.hip, profiles/vmem_r3.md), so the pager moves whole ranges in
+// 1 GiB pieces and never cycles.
 // VGPU_VMEM_MIGRATE=0 keeps the round-1 behaviour (pinned zero-copy spill).
 #include <pthread.h>
 
@@ -47,6 +66,7 @@
 #include <mutex>
 #include <shared_mutex>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "common.h"
@@ -87,6 +107,7 @@ struct Knobs {
   uint64_t hot_ticks = 20;   // used within the last second -> promote
   uint64_t cold_ticks = 40;  // unused for two seconds -> may be demoted
   uint64_t piece = 1ull << 30;
+  int64_t managed_min = 32ll << 20;  // with a physical budget: allocations this large are managed ranges
 };
 
 const Knobs& knobs() {
@@ -99,6 +120,10 @@ const Knobs& knobs() {
     if (const char* e = env_first("VGPU_VMEM_COLD_MS"))
       v.cold_ticks = std::max<uint64_t>(1, strtoull(e, nullptr, 10) / v.tick_ms);
     if (const char* e = env_first("VGPU_VMEM_PIECE_MB")) v.piece = std::max<uint64_t>(2, strtoull(e, nullptr, 10)) << 20;
+    if (const char* e = env_first("VGPU_VMEM_MANAGED_MIN_MB")) {
+      const long long mb = atoll(e);
+      v.managed_min = mb < 0 ? -1 : (int64_t)mb << 20;
+    }
     return v;
   }();
   return k;
@@ -111,11 +136,18 @@ VRange* find_locked(uintptr_t p) {
   return p < r->base + r->size ? r : nullptr;
 }
 
+// Ranges named by launches of the calling thread while its stream is being
+// captured (vmem_scan_*): they belong to the graph, not to this instant.
+thread_local std::vector<uintptr_t>* tl_sink = nullptr;
+std::atomic<int> g_wake{0};  // a launch named a range that is not fully in HBM
+
 inline void touch_word(uintptr_t w, uint64_t tick) {
   if (w < g_tab.front()->base || w >= g_tab.back()->base + g_tab.back()->size) return;
   if (VRange* r = find_locked(w)) {
     if (r->last_use.load(std::memory_order_relaxed) != tick) r->last_use.store(tick, std::memory_order_relaxed);
     r->uses.fetch_add(1, std::memory_order_relaxed);
+    if (r->gpu_bytes < r->size && !g_wake.load(std::memory_order_relaxed)) g_wake.store(1, std::memory_order_relaxed);
+    if (tl_sink) tl_sink->push_back(r->base);
   }
 }
 
@@ -240,6 +272,26 @@ uint64_t hbm_free(int dev) {
   return free_b;
 }
 
+// The pod's physical HBM budget on `dev` (0 = the whole device) and what its
+// processes hold in HBM now (every process of the container shares the budget).
+uint64_t phys_budget(int dev) {
+  State& s = st();
+  if (!s.region || dev < 0 || dev >= VGPU_MAX_DEVICES) return 0;
+  return __atomic_load_n(&s.region->dev[dev].mem_physical, __ATOMIC_RELAXED);
+}
+
+uint64_t pod_resident(int dev) {
+  State& s = st();
+  return s.region ? region_device_used(s.region, dev) : 0;
+}
+
+// `need` more bytes may become HBM-resident on `dev`.
+bool room_for(int dev, uint64_t need) {
+  const uint64_t b = phys_budget(dev);
+  if (b && pod_resident(dev) + need > b) return false;
+  return hbm_free(dev) >= need + knobs().headroom;
+}
+
 // Move the whole range back to host memory.  Caller holds g_move_mu.
 bool demote_locked(VRange* r) {
   if (!r->gpu_bytes) return true;
@@ -262,7 +314,7 @@ bool promote_piece_locked(VRange* r) {
   const Knobs& k = knobs();
   uint64_t n = std::min<uint64_t>(k.piece, r->size - r->gpu_bytes);
   if (!n) return false;
-  if (hbm_free(r->dev) < n + k.headroom) return false;  // make_room_locked ran first
+  if (!room_for(r->dev, n)) return false;  // make_room_locked ran first
   auto t0 = std::chrono::steady_clock::now();
   if (!prefetch(r->base + r->gpu_bytes, n, r->dev, true)) return false;
   uint64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
@@ -280,8 +332,7 @@ bool promote_piece_locked(VRange* r) {
 // Demote cold promoted ranges of `dev` (oldest first, never `keep`) until
 // `need` bytes of HBM are free beyond the headroom.  Caller holds g_move_mu.
 bool make_room_locked(int dev, uint64_t need, const VRange* keep, uint64_t newer_than) {
-  const Knobs& k = knobs();
-  if (hbm_free(dev) >= need + k.headroom) return true;
+  if (room_for(dev, need)) return true;
   std::vector<VRange*> cold;
   {
     std::shared_lock<std::shared_mutex> g(g_tab_mu);
@@ -290,16 +341,34 @@ bool make_room_locked(int dev, uint64_t need, const VRange* keep, uint64_t newer
   }
   std::sort(cold.begin(), cold.end(), [](VRange* a, VRange* b) { return a->last_use.load() < b->last_use.load(); });
   for (VRange* r : cold) {
-    if (hbm_free(dev) >= need + k.headroom) break;
+    if (room_for(dev, need)) break;
     demote_locked(r);
   }
-  return hbm_free(dev) >= need + k.headroom;
+  return room_for(dev, need);
 }
 
-void pager_step() {
+// Suspended (SIGUSR2): give back every byte of HBM our managed ranges hold.
+// Runs on the pager thread; in-flight work is safe (KFD pauses the queues).
+void evict_all() {
+  std::lock_guard<std::mutex> m(g_move_mu);
+  std::vector<VRange*> held;
+  {
+    std::shared_lock<std::shared_mutex> g(g_tab_mu);
+    for (VRange* r : g_tab)
+      if (r->gpu_bytes) held.push_back(r);
+  }
+  uint64_t n = 0;
+  for (VRange* r : held) {  // g_move_mu keeps vmem_release out: the pointers stay valid
+    n += r->gpu_bytes;
+    demote_locked(r);
+  }
+  if (n) VLOG_INFO("vmem: suspended, %llu bytes of HBM released to host memory", (unsigned long long)n);
+}
+
+void pager_step(bool advance) {
   const Knobs& k = knobs();
-  const uint64_t tick = g_tick.fetch_add(1) + 1;
-  if (tick % (1000 / k.tick_ms + 1) == 0) {
+  const uint64_t tick = advance ? g_tick.fetch_add(1) + 1 : g_tick.load();
+  if (advance && tick % (1000 / k.tick_ms + 1) == 0) {
     std::shared_lock<std::shared_mutex> g(g_tab_mu);
     for (VRange* r : g_tab) r->uses.store(r->uses.load() / 2);
   }
@@ -340,7 +409,7 @@ void pager_step() {
     }
   }
   static uint64_t last_note = 0;
-  if (waiting && tick - last_note >= 1000 / (uint64_t)k.tick_ms) {
+  if (waiting && advance && tick - last_note >= 1000 / (uint64_t)k.tick_ms) {
     last_note = tick;
     VLOG_INFO("vmem: %llu bytes of used spilled ranges wait for HBM (free for the pager %llu)",
               (unsigned long long)waiting, (unsigned long long)hbm_free(waiting_dev));
@@ -355,11 +424,27 @@ void pager_main() {
   (void)REAL_HIP(hipThreadExchangeStreamCaptureMode)(&mode);
   const Knobs& k = knobs();
   std::unique_lock<std::mutex> l(g_thr_mu);
+  bool evicted = false;
+  auto last = std::chrono::steady_clock::now();
   while (g_thr_run) {
-    g_thr_cv.wait_for(l, std::chrono::milliseconds(k.tick_ms));
+    // Poll every millisecond for a launch that named a non-resident range
+    // (promotion starts then, not at the next tick); the tick itself, which
+    // ages use counts and measures hot/cold windows, advances every tick_ms.
+    g_thr_cv.wait_for(l, std::chrono::milliseconds(1));
     if (!g_thr_run) break;
+    const auto now = std::chrono::steady_clock::now();
+    const bool tick = now - last >= std::chrono::milliseconds(k.tick_ms);
+    const bool woke = g_wake.exchange(0) != 0;
+    if (!tick && !woke) continue;
+    if (tick) last = now;
     l.unlock();
-    if (g_count.load() > 0) pager_step();
+    if (st().suspended.load(std::memory_order_relaxed)) {
+      if (!evicted && g_count.load() > 0) evict_all();
+      evicted = true;
+    } else {
+      evicted = false;
+      if (g_count.load() > 0) pager_step(tick);
+    }
     l.lock();
   }
   g_thr_alive.store(0);
@@ -385,7 +470,19 @@ bool vmem_should_spill(int dev, uint64_t size) {
     const char* e = env_first("VGPU_VMEM_RESERVE_MB");
     return (e ? strtoull(e, nullptr, 10) : 1024ull) << 20;
   }();
+  // Called after `size` was reserved against the cap, so the pod's resident
+  // bytes already include it.
+  const uint64_t b = phys_budget(dev);
+  if (b && pod_resident(dev) > b) return true;
   return hbm_free(dev) < size + reserve;
+}
+
+bool vmem_wants_managed(int dev, uint64_t size) {
+  const Knobs& k = knobs();
+  // Not while a graph capture is open: hipMemAdvise would be an unsafe call in
+  // a global-mode capture.  Those (activation) buffers take the plain path.
+  return vmem_enabled() && k.managed_min >= 0 && (uint64_t)k.managed_min <= size && phys_budget(dev) > 0 &&
+         g_open_captures.load(std::memory_order_acquire) == 0;
 }
 
 bool vmem_enabled() {
@@ -393,10 +490,10 @@ bool vmem_enabled() {
   return s.enabled && s.region && s.region->oversubscribe && knobs().on;
 }
 
-hipError_t vmem_alloc_overflow(void** ptr, size_t size, int dev) {
-  if (!vmem_enabled()) return hipErrorNotSupported;
-  hipError_t rc = REAL_HIP(hipMallocManaged)(ptr, size, hipMemAttachGlobal);
-  if (rc != hipSuccess) return rc;
+namespace {
+VRange* new_range(void** ptr, size_t size, int dev, hipError_t* rc) {
+  *rc = REAL_HIP(hipMallocManaged)(ptr, size, hipMemAttachGlobal);
+  if (*rc != hipSuccess) return nullptr;
   // Coarse-grained: coherent at kernel boundaries like hipMalloc memory, so
   // the GPU caches it (fine-grained managed memory bypasses them).
   (void)REAL_HIP(hipMemAdvise)(*ptr, size, hipMemAdviseSetCoarseGrain, dev);
@@ -411,6 +508,31 @@ hipError_t vmem_alloc_overflow(void** ptr, size_t size, int dev) {
     g_count.store((int)g_tab.size());
   }
   ensure_pager();
+  return r;
+}
+}  // namespace
+
+hipError_t vmem_alloc_overflow(void** ptr, size_t size, int dev) {
+  if (!vmem_enabled()) return hipErrorNotSupported;
+  hipError_t rc;
+  return new_range(ptr, size, dev, &rc) ? hipSuccess : rc;
+}
+
+hipError_t vmem_alloc_managed(void** ptr, size_t size, int dev) {
+  if (!vmem_enabled()) return hipErrorNotSupported;
+  hipError_t rc;
+  VRange* r = new_range(ptr, size, dev, &rc);
+  if (!r) return rc;
+  // Resident at once while the budget has room (after cold ranges made way);
+  // the rest, if any, is promoted by the pager once the range is in use.
+  const Knobs& k = knobs();
+  std::lock_guard<std::mutex> m(g_move_mu);
+  const uint64_t tick = g_tick.load();
+  const uint64_t stale = tick > k.cold_ticks ? tick - k.cold_ticks : 0;
+  while (r->gpu_bytes < r->size) {
+    const uint64_t n = std::min<uint64_t>(k.piece, r->size - r->gpu_bytes);
+    if (!make_room_locked(dev, n, r, stale) || !promote_piece_locked(r)) break;
+  }
   return hipSuccess;
 }
 
@@ -455,7 +577,52 @@ bool vmem_make_room(int dev, uint64_t need) {
   return make_room_locked(dev, need, nullptr, tick > k.cold_ticks ? tick - k.cold_ticks : 0);
 }
 
-void vmem_scan_args(void** args) {
+namespace {
+// Graph bookkeeping: ranges named by launches captured into a graph, keyed by
+// capture id while the capture is open, then by graph, then by executable.
+std::mutex g_gmu;
+std::unordered_map<unsigned long long, std::vector<uintptr_t>> g_cap_ranges;
+std::unordered_map<const void*, std::vector<uintptr_t>> g_graph_ranges;
+std::unordered_map<const void*, std::vector<uintptr_t>> g_exec_ranges;
+
+void merge(std::vector<uintptr_t>& into, const std::vector<uintptr_t>& from) {
+  into.insert(into.end(), from.begin(), from.end());
+  std::sort(into.begin(), into.end());
+  into.erase(std::unique(into.begin(), into.end()), into.end());
+}
+
+// Capture id of `stream` when it is being captured, else 0.
+unsigned long long capture_id(hipStream_t stream) {
+  if (g_open_captures.load(std::memory_order_acquire) == 0) return 0;
+  auto info = REAL_HIP(hipStreamGetCaptureInfo);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  if (!info || info(stream, &cs, &id) != hipSuccess || cs != hipStreamCaptureStatusActive) return 0;
+  return id ? id : 1;
+}
+
+// Runs `scan` (which stamps ranges); when `stream` is capturing, the ranges
+// it names are also recorded for the graph being captured.
+template <class F>
+void scan_for(hipStream_t stream, F&& scan) {
+  const unsigned long long cid = capture_id(stream);
+  if (!cid) {
+    scan();
+  } else {
+    std::vector<uintptr_t> hits;
+    tl_sink = &hits;
+    scan();
+    tl_sink = nullptr;
+    if (!hits.empty()) {
+      std::lock_guard<std::mutex> l(g_gmu);
+      merge(g_cap_ranges[cid], hits);
+    }
+  }
+  if (g_wake.load(std::memory_order_relaxed)) g_thr_cv.notify_one();
+}
+}  // namespace
+
+void vmem_scan_args(void** args, hipStream_t stream) {
   if (g_count.load(std::memory_order_relaxed) == 0 || !args) return;
   const uintptr_t lo = (uintptr_t)__builtin_frame_address(0);
   const uintptr_t hi = stack_top();
@@ -470,17 +637,21 @@ void vmem_scan_args(void** args) {
   }
   if (!n) return;
   std::sort(a, a + n);
-  const uint64_t tick = g_tick.load(std::memory_order_relaxed);
-  std::shared_lock<std::shared_mutex> g(g_tab_mu);
-  if (g_tab.empty()) return;
-  for (int i = 0; i < n; ++i) {
-    uintptr_t end = i + 1 < n ? a[i + 1] : a[i] + 1024;  // the last argument: a bounded look
-    end = std::min<uintptr_t>({end, a[i] + 4096, hi});
-    if (end > a[i]) scan_words_locked((const unsigned char*)a[i], end - a[i], tick);
-  }
+  scan_for(stream, [&] {
+    const uint64_t tick = g_tick.load(std::memory_order_relaxed);
+    std::shared_lock<std::shared_mutex> g(g_tab_mu);
+    if (g_tab.empty()) return;
+    for (int i = 0; i < n; ++i) {
+      // The last argument's size is unknown: a bounded look (PyTorch's
+      // elementwise kernels pass their operand pointer array last).
+      uintptr_t end = i + 1 < n ? a[i + 1] : a[i] + 512;
+      end = std::min<uintptr_t>({end, a[i] + 4096, hi});
+      if (end > a[i]) scan_words_locked((const unsigned char*)a[i], end - a[i], tick);
+    }
+  });
 }
 
-void vmem_scan_extra(void** extra) {
+void vmem_scan_extra(void** extra, hipStream_t stream) {
   if (g_count.load(std::memory_order_relaxed) == 0 || !extra) return;
   const void* buf = nullptr;
   size_t n = 0;
@@ -489,9 +660,63 @@ void vmem_scan_extra(void** extra) {
     else if (extra[i] == HIP_LAUNCH_PARAM_BUFFER_SIZE && extra[i + 1]) n = *(size_t*)extra[i + 1];
   }
   if (!buf || !n) return;
+  scan_for(stream, [&] {
+    const uint64_t tick = g_tick.load(std::memory_order_relaxed);
+    std::shared_lock<std::shared_mutex> g(g_tab_mu);
+    if (!g_tab.empty()) scan_words_locked((const unsigned char*)buf, std::min<size_t>(n, 4096), tick);
+  });
+}
+
+unsigned long long vmem_capture_begin_id(hipStream_t stream) { return capture_id(stream); }
+
+void vmem_capture_ended(unsigned long long cid, hipGraph_t graph) {
+  if (!cid) return;
+  std::lock_guard<std::mutex> l(g_gmu);
+  auto it = g_cap_ranges.find(cid);
+  if (it == g_cap_ranges.end()) return;
+  if (graph) merge(g_graph_ranges[graph], it->second);
+  g_cap_ranges.erase(it);
+}
+
+void vmem_graph_instantiated(hipGraph_t graph, hipGraphExec_t exec) {
+  std::lock_guard<std::mutex> l(g_gmu);
+  auto it = g_graph_ranges.find(graph);
+  if (it == g_graph_ranges.end()) {
+    g_exec_ranges.erase(exec);
+    return;
+  }
+  g_exec_ranges[exec] = it->second;
+}
+
+void vmem_graph_destroyed(const void* graph_or_exec) {
+  std::lock_guard<std::mutex> l(g_gmu);
+  g_graph_ranges.erase(graph_or_exec);
+  g_exec_ranges.erase(graph_or_exec);
+}
+
+// A replay runs none of our hooks: stamp every range its kernels name.
+void vmem_graph_launched(hipGraphExec_t exec) {
+  if (g_count.load(std::memory_order_relaxed) == 0) return;
+  std::vector<uintptr_t> bases;
+  {
+    std::lock_guard<std::mutex> l(g_gmu);
+    auto it = g_exec_ranges.find(exec);
+    if (it == g_exec_ranges.end()) return;
+    bases = it->second;
+  }
   const uint64_t tick = g_tick.load(std::memory_order_relaxed);
-  std::shared_lock<std::shared_mutex> g(g_tab_mu);
-  if (!g_tab.empty()) scan_words_locked((const unsigned char*)buf, std::min<size_t>(n, 4096), tick);
+  {
+    std::shared_lock<std::shared_mutex> g(g_tab_mu);
+    if (g_tab.empty()) return;
+    for (uintptr_t b : bases) touch_word(b, tick);
+  }
+  if (g_wake.load(std::memory_order_relaxed)) g_thr_cv.notify_one();
+}
+
+uint64_t vmem_graph_ranges(hipGraphExec_t exec) {
+  std::lock_guard<std::mutex> l(g_gmu);
+  auto it = g_exec_ranges.find(exec);
+  return it == g_exec_ranges.end() ? 0 : it->second.size();
 }
 
 void vmem_stats(uint64_t* in_bytes, uint64_t* out_bytes, uint64_t* moves, uint64_t* gpu_bytes,
@@ -523,6 +748,7 @@ void vmem_after_fork() {
   new (&g_thr_mu) std::mutex();
   new (&g_move_mu) std::mutex();
   new (&g_tab_mu) std::shared_mutex();
+  new (&g_gmu) std::mutex();
   g_thr_run = false;
   g_thr_alive.store(0);
 }

@@ -346,6 +346,106 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (sc == "vmem_budget" || sc == "vmem_thrash") {
+    // Virtual device memory with a physical budget (VGPU_DEVICE_MEMORY_PHYSICAL_0):
+    // allocations are managed ranges from the start.  vmem_budget: model B is
+    // loaded and goes idle, model A is loaded (B gives way), then a captured
+    // graph that uses B is replayed (B comes back, A gives way), then SIGUSR2
+    // empties HBM.  vmem_thrash: two hot ranges that do not fit together.
+    const size_t G = 1ull << 30;
+    auto vstats = sym<void (*)(uint64_t*)>("vgpu_self_vmem_stats");
+    auto self_region = sym<void* (*)()>("vgpu_self_region");
+    auto self_slot = sym<int (*)()>("vgpu_self_slot");
+    auto slot_u = [&]() -> vgpu_dev_usage_t& {
+      return ((vgpu_shared_region_t*)self_region())->procs[self_slot()].used[dev];
+    };
+    uint64_t peak_phys = 0;
+    auto note = [&] {
+      uint64_t p = fake_hip_physical_used(dev);
+      if (p > peak_phys) peak_phys = p;
+    };
+    auto launch = [&](void* p) {
+      int n = 1;
+      void* q = (char*)p + 64;
+      void* args[] = {&n, &q};
+      hipLaunchKernel((const void*)0x1, dim3(64), dim3(256), args, 0, nullptr);
+    };
+    auto gb = [&](void* p) { return (unsigned long long)fake_hip_managed_gpu_bytes(p); };
+    // The launch-argument scan reads a bounded window of the stub's frame past
+    // the last argument; keep the other range's pointer off the stack.
+    void** ab = new void*[2]();
+    void*& a = ab[0];
+    void*& b = ab[1];
+    if (sc == "vmem_thrash") {
+      int ra = hipMalloc(&a, 6 * G), rb = hipMalloc(&b, 6 * G);
+      printf("alloc_a=%d\nalloc_b=%d\n", ra, rb);
+      for (int t = 0; t < 120; ++t) {  // both hot, alternately, for 1.2 s
+        launch(t % 2 ? a : b);
+        note();
+        usleep(10000);
+      }
+      uint64_t v[5];
+      vstats(v);
+      printf("a_gpu=%llu\nb_gpu=%llu\nmoves=%llu\npeak_phys=%llu\n", gb(a), gb(b), (unsigned long long)v[2],
+             (unsigned long long)peak_phys);
+      hipFree(a);
+      hipFree(b);
+      return 0;
+    }
+    int rb = hipMalloc(&b, 6 * G);
+    printf("alloc_b=%d\nb_gpu_at_alloc=%llu\nbuffer_at_alloc=%llu\nhost_at_alloc=%llu\n", rb, gb(b),
+           (unsigned long long)slot_u().buffer_bytes, (unsigned long long)slot_u().host_bytes);
+    note();
+    usleep(300000);  // B idles past the cold window
+    int ra = hipMalloc(&a, 6 * G);
+    note();
+    printf("alloc_a=%d\na_gpu_at_alloc=%llu\nb_gpu_after_a=%llu\n", ra, gb(a), gb(b));
+    // capture a graph whose only kernel names B
+    hipStream_t st = (hipStream_t)0x77;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    hipStreamBeginCapture(st, hipStreamCaptureModeGlobal);
+    {
+      int n = 1;
+      void* q = (char*)b + 128;
+      void* args[] = {&n, &q};
+      hipLaunchKernel((const void*)0x1, dim3(64), dim3(256), args, 0, st);
+    }
+    int rc_end = hipStreamEndCapture(st, &graph);
+    int rc_inst = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    auto granges = sym<uint64_t (*)(hipGraphExec_t)>("vgpu_self_graph_ranges");
+    printf("end_capture=%d\ninstantiate=%d\ngraph_ranges=%llu\n", rc_end, rc_inst,
+           (unsigned long long)(granges ? granges(exec) : 999));
+    usleep(300000);  // A idles too (only B will be used from now on)
+    for (int t = 0; t < 60; ++t) {  // replay for 0.6 s
+      hipGraphLaunch(exec, st);
+      note();
+      usleep(10000);
+    }
+    printf("b_gpu_after_replay=%llu\na_gpu_after_replay=%llu\n", gb(b), gb(a));
+    raise(SIGUSR2);  // suspend: everything leaves HBM
+    usleep(300000);
+    printf("suspended_b_gpu=%llu\nsuspended_a_gpu=%llu\nsuspended_phys=%llu\nsuspended_host=%llu\n", gb(b), gb(a),
+           (unsigned long long)fake_hip_physical_used(dev), (unsigned long long)slot_u().host_bytes);
+    raise(SIGUSR1);
+    for (int t = 0; t < 60; ++t) {
+      hipGraphLaunch(exec, st);
+      note();
+      usleep(10000);
+    }
+    printf("resumed_b_gpu=%llu\npeak_phys=%llu\n", gb(b), (unsigned long long)peak_phys);
+    hipGraphExecDestroy(exec);
+    hipGraphDestroy(graph);
+    hipFree(a);
+    hipFree(b);
+    uint64_t v[5];
+    vstats(v);
+    printf("final_total=%llu\nfinal_host=%llu\nfinal_ranges=%llu\nfinal_physical=%llu\n",
+           (unsigned long long)slot_u().total_bytes, (unsigned long long)slot_u().host_bytes,
+           (unsigned long long)v[4], (unsigned long long)fake_hip_physical_used(dev));
+    return 0;
+  }
+
   if (sc == "spill") {
     // Oversubscription: allocate `n` chunks; report how many landed in host memory.
     size_t chunk = argc > 2 ? strtoull(argv[2], nullptr, 10) : (1ull << 30);

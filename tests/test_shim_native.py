@@ -161,6 +161,47 @@ def test_vmem_promotes_used_spill_and_demotes_it_when_cold(native_build):
         ("0", "0", "0", "0", "0")
 
 
+BUDGET_ENV = {**VMEM_ENV, "VGPU_FAKE_MEM": str(16 * GiB), "VGPU_DEVICE_MEMORY_LIMIT_0": "40g",
+              "VGPU_DEVICE_MEMORY_PHYSICAL_0": "8g"}
+
+
+def test_vmem_budget_graph_replay_and_suspend(native_build):
+    """with a physical HBM budget (8 GiB of a 16 GiB device,
+    cap 40 GiB) allocations are managed ranges; an idle model gives way to a
+    newly loaded one; a range used only inside a replayed hipGraph is promoted
+    (captured launches are scanned and follow capture -> graph -> exec) while
+    the now idle one is demoted; SIGUSR2 empties HBM and the range returns
+    after SIGUSR1.  Physical use never exceeds the budget."""
+    o = run("vmem_budget", env=BUDGET_ENV)
+    assert o["alloc_b"] == "0" and int(o["b_gpu_at_alloc"]) == 6 * GiB
+    assert int(o["buffer_at_alloc"]) == 6 * GiB and o["host_at_alloc"] == "0"
+    assert o["alloc_a"] == "0" and int(o["a_gpu_at_alloc"]) == 6 * GiB and o["b_gpu_after_a"] == "0"
+    assert (o["end_capture"], o["instantiate"], o["graph_ranges"]) == ("0", "0", "1")
+    assert int(o["b_gpu_after_replay"]) == 6 * GiB and o["a_gpu_after_replay"] == "0"
+    assert (o["suspended_b_gpu"], o["suspended_a_gpu"], o["suspended_phys"]) == ("0", "0", "0")
+    assert int(o["suspended_host"]) == 12 * GiB
+    assert int(o["resumed_b_gpu"]) == 6 * GiB
+    assert int(o["peak_phys"]) <= 8 * GiB
+    assert (o["final_total"], o["final_host"], o["final_ranges"], o["final_physical"]) == ("0", "0", "0", "0")
+
+
+def test_vmem_hot_set_beyond_budget_does_not_cycle(native_build):
+    """Two hot 6 GiB ranges against an 8 GiB budget: the resident part stays
+    put (no LRU exchange on a cyclic sweep), the rest is read in place."""
+    o = run("vmem_thrash", env=BUDGET_ENV)
+    assert int(o["a_gpu"]) + int(o["b_gpu"]) == 8 * GiB
+    assert int(o["moves"]) == 8  # the initial 1 GiB pieces only
+    assert int(o["peak_phys"]) <= 8 * GiB
+
+
+def test_vmem_budget_zero_copy_mode_spills_past_budget(native_build):
+    o = run("spill", GiB, 12, env={"VGPU_FAKE_MEM": str(16 * GiB), "VGPU_DEVICE_MEMORY_LIMIT_0": "40g",
+                                   "VGPU_OVERSUBSCRIBE": "true", "VGPU_VMEM_MIGRATE": "0",
+                                   "VGPU_DEVICE_MEMORY_PHYSICAL_0": "8g", "VGPU_VMEM_RESERVE_MB": "0"})
+    assert o["allocated"] == "12" and o["failed"] == "0"
+    assert int(o["physical_used"]) == 8 * GiB and int(o["slot_host_bytes"]) == 4 * GiB
+
+
 def test_vmem_off_keeps_zero_copy_spill(native_build):
     o = run("vmem", env={**VMEM_ENV, "VGPU_VMEM_MIGRATE": "0"})
     assert o["alloc_b"] == "0" and int(o["host_after_spill"]) == 4 * GiB

@@ -19,7 +19,24 @@ spilled weights it sees in kernel arguments back into HBM.  Run once with the
 pager and once with VGPU_VMEM_MIGRATE=0 (the round-1 zero-copy spill, which
 never moves back).  Reports tokens/s per window, swap-in bytes and migrations.
 
+Part D — model switch under a physical HBM budget, decode as hipGraph replay
+(VERDICT r2 item 1).  One pod, cap 400000 MiB, physical budget --budget-gib
+(VGPU_DEVICE_MEMORY_PHYSICAL_0, what the device plugin sets on an
+oversubscribed node), two Llama-3-8B instances (2 x 15 GiB: footprint >=
+1.3 x the budget), no neighbour process.  Model A is loaded, its decode step
+captured as a graph and replayed; A idles, model B is loaded, captured and
+served; then traffic switches back to A.  With the pager, B's load demotes
+the idle A, and A's graph replays (whose kernels the shim saw at capture
+time) bring A back while the now idle B gives way.  VGPU_VMEM_MIGRATE=0
+(zero-copy) keeps whatever did not fit at load time in host memory for good.
+
+Part E — one Llama-3-8B whose weights alone exceed the budget (a hot set
+larger than the budget, read cyclically every token): no pager can beat the
+host link here; the pager must simply not do worse than zero-copy.
+
     python -m vgpu.bench.vmem [--spill-gib 8] [--budget-gib 8] [--tokens 16] [--part-c]
+    python -m vgpu.bench.vmem --part-d [--budget-gib 22] [--modes pager,zero_copy]
+    python -m vgpu.bench.vmem --part-e [--budget-gib 11.5]
 """
 from __future__ import annotations
 
@@ -237,6 +254,135 @@ def part_c(leave_gib: float, tokens: int, ctx: int, windows: int, migrate: bool)
     return res
 
 
+def _stats_fn():
+    import ctypes
+    lib = ctypes.CDLL(None)
+    vstats = getattr(lib, "vgpu_self_vmem_stats", None)
+    host_bytes = getattr(lib, "vgpu_self_host_bytes", None)
+    if host_bytes is not None:
+        host_bytes.restype = ctypes.c_uint64
+
+    def stats():
+        v = (ctypes.c_uint64 * 5)()
+        if vstats is not None:
+            vstats(v)
+        return {"swap_in": v[0], "swap_out": v[1], "moves": v[2], "managed_in_hbm": v[3], "managed_ranges": v[4],
+                "host_bytes": host_bytes(0) if host_bytes else 0}
+    return stats
+
+
+class GraphDecoder:
+    """A Llama-3-8B instance with its decode step captured as one hipGraph."""
+
+    def __init__(self, cfg, ctx: int, seed: int):
+        import torch
+        from vgpu.models.llama import Llama
+        torch.manual_seed(seed)
+        with torch.device("meta"):
+            m = Llama(cfg)
+        self.m = m.to(torch.bfloat16).to_empty(device="cuda")
+        with torch.no_grad():
+            for p_ in self.m.parameters():
+                p_.normal_(0, 0.02)
+        self.m.eval()
+        self.kv = _kv(cfg, ctx, torch.device("cuda"))
+        self.tok = torch.randint(0, cfg.vocab, (1, 1), device="cuda")
+        self.pos = torch.zeros(1, dtype=torch.long, device="cuda")
+        self.ctx = ctx
+        self.n = 0
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s), torch.inference_mode():
+            for _ in range(2):
+                self.out = self.m.decode_static(self.tok, self.kv, self.pos)
+        torch.cuda.current_stream().wait_stream(s)
+        self.g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g), torch.inference_mode():
+            self.out = self.m.decode_static(self.tok, self.kv, self.pos)
+        torch.cuda.synchronize()
+
+    def window(self, tokens: int) -> float:
+        import torch
+        t0 = time.time()
+        for _ in range(tokens):
+            self.pos.fill_(self.n % self.ctx)
+            self.g.replay()
+            self.n += 1
+        torch.cuda.synchronize()
+        return round(tokens / (time.time() - t0), 2)
+
+
+def part_d_child(tokens: int, ctx: int, windows: int, idle_s: float) -> dict:
+    """Runs in the pod (libvgpu.so, oversubscribed, physical budget)."""
+    import torch
+    from vgpu.models.llama import LlamaConfig
+    stats = _stats_fn()
+    cfg = LlamaConfig.llama3_8b()
+    out = {}
+    t0 = time.time()
+    a = GraphDecoder(cfg, ctx, 1)
+    out["load_a_s"] = round(time.time() - t0, 2)
+    out["a_first"] = [a.window(tokens) for _ in range(2)]
+    out["after_a"] = stats()
+    time.sleep(idle_s)  # A idles: its ranges go cold
+    t0 = time.time()
+    b = GraphDecoder(cfg, ctx, 2)
+    out["load_b_s"] = round(time.time() - t0, 2)
+    out["after_load_b"] = stats()
+    series = []
+    t_rel = time.time()
+    for _ in range(windows):
+        series.append([round(time.time() - t_rel, 2), b.window(tokens)])
+    out["b_serving"] = series
+    out["after_b"] = stats()
+    series = []
+    t_rel = time.time()
+    for _ in range(windows):  # traffic switches back to A
+        series.append([round(time.time() - t_rel, 2), a.window(tokens)])
+    out["a_again"] = series
+    out["final"] = stats()
+    out["torch_mem_total"] = torch.cuda.mem_get_info()[1]
+    return out
+
+
+def part_e_child(tokens: int, ctx: int, windows: int) -> dict:
+    from vgpu.models.llama import LlamaConfig
+    stats = _stats_fn()
+    a = GraphDecoder(LlamaConfig.llama3_8b(), ctx, 1)
+    out = {"after_load": stats()}
+    t_rel = time.time()
+    out["serving"] = [[round(time.time() - t_rel, 2), a.window(tokens)] for _ in range(windows)]
+    out["final"] = stats()
+    return out
+
+
+def run_pod_child(part: str, budget_gib: float, migrate: bool, args: list[str], timeout: float = 1500) -> dict:
+    from vgpu.native import ensure_built, preload_env
+    ensure_built()
+    repo = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = preload_env()
+    env.update({"VGPU_DEVICE_MEMORY_LIMIT_0": "400000m", "VGPU_OVERSUBSCRIBE": "true", "PYTHONPATH": repo,
+                "VGPU_DEVICE_MEMORY_PHYSICAL_0": f"{int(budget_gib * 1024)}m",
+                "VGPU_LOG_LEVEL": env.get("VGPU_LOG_LEVEL", "3"), "VGPU_VMEM_MIGRATE": "1" if migrate else "0"})
+    if os.environ.get("VGPU_TRACE") and migrate:
+        env["VGPU_TRACE"] = os.environ["VGPU_TRACE"] + f".{part}"
+        env.setdefault("VGPU_TRACE_EVENTS", "1000000")
+    import tempfile
+    errf = tempfile.NamedTemporaryFile(mode="w+", prefix=f"vmem_{part}_", suffix=".log",
+                                       dir=os.environ.get("VGPU_VMEM_LOG_DIR") or None, delete=False)
+    r = subprocess.run([sys.executable, "-m", "vgpu.bench.vmem", f"--child-{part}", *args], env=env,
+                       stdout=subprocess.PIPE, stderr=errf, text=True, timeout=timeout)
+    tag = f"VMEM_{part.upper()} "
+    js = [l for l in r.stdout.splitlines() if l.startswith(tag)]
+    res = {"migrate": migrate, "budget_gib": budget_gib}
+    if js:
+        res.update(json.loads(js[-1][len(tag):]))
+    else:
+        errf.seek(0)
+        res["error"] = f"rc={r.returncode} " + errf.read()[-3000:]
+    return res
+
+
 def _kv(cfg, ctx, dev):
     import torch
     hd = cfg.dim // cfg.heads
@@ -257,6 +403,11 @@ def main(argv=None) -> int:
     ap.add_argument("--leave-gib", type=float, default=8.0)
     ap.add_argument("--windows", type=int, default=6)
     ap.add_argument("--modes", default="pager,zero_copy")
+    ap.add_argument("--child-d", action="store_true")
+    ap.add_argument("--child-e", action="store_true")
+    ap.add_argument("--part-d", action="store_true", help="model switch under a physical budget (graph decode)")
+    ap.add_argument("--part-e", action="store_true", help="hot set beyond the budget (graph decode)")
+    ap.add_argument("--idle-s", type=float, default=3.0)
     ap.add_argument("--skip-a", action="store_true")
     ap.add_argument("--skip-b", action="store_true")
     a = ap.parse_args(argv)
@@ -265,6 +416,24 @@ def main(argv=None) -> int:
         return 0
     if a.child_c:
         print("VMEM_C " + json.dumps(part_c_child(a.tokens, a.ctx, a.windows)), flush=True)
+        return 0
+    if a.child_d:
+        print("VMEM_D " + json.dumps(part_d_child(a.tokens, a.ctx, a.windows, a.idle_s)), flush=True)
+        return 0
+    if a.child_e:
+        print("VMEM_E " + json.dumps(part_e_child(a.tokens, a.ctx, a.windows)), flush=True)
+        return 0
+    if a.part_d or a.part_e:
+        part = "d" if a.part_d else "e"
+        out = {"config": f"amd.com/gpumem=400000 (MiB), VGPU_OVERSUBSCRIBE=true, physical budget {a.budget_gib} GiB, "
+                         + ("two Llama-3-8B bf16 (model switch)" if a.part_d else "one Llama-3-8B bf16")
+                         + ", decode step as one hipGraph replay, ctx " + str(a.ctx)}
+        for mode in a.modes.split(","):
+            out[mode] = run_pod_child(part, a.budget_gib, mode == "pager",
+                                      ["--tokens", str(a.tokens), "--ctx", str(a.ctx), "--windows", str(a.windows),
+                                       "--idle-s", str(a.idle_s)])
+            print(f"VMEM_{part.upper()}_RUN " + json.dumps(out[mode]), flush=True)
+        print(json.dumps(out), flush=True)
         return 0
     if a.part_c:
         out = {"config": "amd.com/gpumem=400000 (MiB), VGPU_OVERSUBSCRIBE=true, Llama-3-8B bf16 decode, "

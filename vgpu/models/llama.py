@@ -130,6 +130,36 @@ class Llama(nn.Module):
             x = layer(x, cos, sin, kv_caches[i] if kv_caches is not None else None, pos)
         return self.head(self.norm(x[:, -1:]))
 
+    @torch.no_grad()
+    def decode_static(self, tokens: torch.Tensor, kv_caches, pos: torch.Tensor) -> torch.Tensor:
+        """One decode step with every shape fixed (graph-capturable): `pos` is
+        a 1-element device tensor, the cache is written with index_copy_ and
+        attention runs over the whole cache with positions > pos masked."""
+        cos, sin = self.rope(tokens.device)
+        c, s_ = cos.index_select(0, pos), sin.index_select(0, pos)
+        x = self.embed(tokens)
+        B = x.shape[0]
+        ctx = kv_caches[0][0].shape[2]
+        mask = (torch.arange(ctx, device=tokens.device) <= pos)[None, None, None, :]
+        for i, layer in enumerate(self.layers):
+            a = layer.attn
+            h = layer.norm1(x)
+            q, k, v = a.wqkv(h).split([a.h * a.hd, a.kvh * a.hd, a.kvh * a.hd], dim=-1)
+            q = apply_rope(q.view(B, 1, a.h, a.hd).transpose(1, 2), c, s_)
+            k = apply_rope(k.view(B, 1, a.kvh, a.hd).transpose(1, 2), c, s_)
+            v = v.view(B, 1, a.kvh, a.hd).transpose(1, 2)
+            kc, vc = kv_caches[i]
+            kc.index_copy_(2, pos, k)
+            vc.index_copy_(2, pos, v)
+            rep = a.h // a.kvh
+            kk = kc.repeat_interleave(rep, dim=1) if rep > 1 else kc
+            vv = vc.repeat_interleave(rep, dim=1) if rep > 1 else vc
+            o = F.scaled_dot_product_attention(q, kk, vv, attn_mask=mask)
+            x = x + a.wo(o.transpose(1, 2).reshape(B, 1, -1))
+            g, u = layer.w13(layer.norm2(x)).chunk(2, dim=-1)
+            x = x + layer.w2(F.silu(g) * u)
+        return self.head(self.norm(x))
+
     def new_kv_cache(self, batch: int, seq: int, dtype=torch.bfloat16, device=None):
         hd = self.cfg.dim // self.cfg.heads
         shape = (batch, self.cfg.kv_heads, seq, hd)
