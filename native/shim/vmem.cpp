@@ -472,8 +472,11 @@ bool vmem_should_spill(int dev, uint64_t size) {
   }();
   // Called after `size` was reserved against the cap, so the pod's resident
   // bytes already include it.
+  // The budget yields to an open graph capture: its (small, graph-pool)
+  // buffers can neither become managed ranges nor pinned host memory while a
+  // global-mode capture is open, so they stay plain HBM; the cap still holds.
   const uint64_t b = phys_budget(dev);
-  if (b && pod_resident(dev) > b) return true;
+  if (b && pod_resident(dev) > b && g_open_captures.load(std::memory_order_acquire) == 0) return true;
   return hbm_free(dev) < size + reserve;
 }
 

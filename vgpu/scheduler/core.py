@@ -72,8 +72,12 @@ class Scheduler:
         self._stop = threading.Event()
         self.filter_latency_s: list[float] = []
         # Flat per-device state for the native scorer, kept current on pod
-        # add/remove and rebuilt when the node registry changes.
+        # add/remove, updated in place when a device's attributes change, and
+        # rebuilt -- by the registration pass, off the /filter path -- only
+        # when devices appear or vanish (_flat_stale).
         self._flat: N.FlatState | None = None
+        self._flat_stale = False
+        self._node_gen = 0
         self.informer_synced = threading.Event()
         self.informer_events = 0
         self.informer_relists = 0
@@ -131,17 +135,42 @@ class Scheduler:
     # ---- node registry (C3) ---------------------------------------------------------------
     def add_node(self, node_id: str, info: NodeInfo) -> None:
         with self._lock:
-            self._flat = None
             cur = self.nodes.get(node_id)
             if cur is None:
                 self.nodes[node_id] = copy.deepcopy(info)
             else:
                 known = {d.id for d in cur.devices}
-                cur.devices.extend(copy.deepcopy(d) for d in info.devices if d.id not in known)
+                new = [copy.deepcopy(d) for d in info.devices if d.id not in known]
+                if not new:
+                    return
+                cur.devices.extend(new)
+            self._structure_changed()
+
+    def _structure_changed(self) -> None:
+        """Devices appeared or vanished (caller holds the lock)."""
+        self._flat_stale = True
+        self._node_gen += 1
+
+    def rebuild_flat(self) -> None:
+        """Rebuild the flat state after a structural change.  The registration
+        thread is the only writer of the node registry, so it builds the new
+        device table without the lock (readers never mutate it) and takes the
+        lock only to add the pods' usage and swap it in."""
+        with self._lock:
+            if not self._flat_stale and self._flat is not None:
+                return
+            gen = self._node_gen
+        flat = N.FlatState(self.nodes, {})
+        with self._lock:
+            if gen != self._node_gen:
+                return  # changed again meanwhile: the next pass (or /filter) rebuilds
+            flat.apply_all(self.pods)
+            self._flat = flat
+            self._flat_stale = False
 
     def rm_node_devices(self, node_id: str, info: NodeInfo) -> None:
         with self._lock:
-            self._flat = None
+            self._structure_changed()
             cur = self.nodes.get(node_id)
             if cur is None:
                 return
@@ -208,20 +237,25 @@ class Scheduler:
                         log.error("patch node %s failed: %s", name, e)
                 info = NodeInfo(id=name)
                 with self._lock:
-                    self._flat = None  # device attributes may change below
                     cur = self.nodes.get(name)
+                    byid = {x.id: x for x in cur.devices} if cur is not None else {}
                     for i, d in enumerate(devs):
                         if not d.index:
                             d.index = i
-                        if cur is not None:
-                            m = next((x for x in cur.devices if x.id == d.id), None)
-                            if m is not None:
-                                m.devmem, m.devcore, m.count = d.devmem, d.devcore, d.count
-                                m.health, m.cus, m.xgmi_hive = d.health, d.cus, d.xgmi_hive
-                                continue
-                        info.devices.append(d)
-                self.add_node(name, info)
+                        m = byid.get(d.id)
+                        if m is None:
+                            info.devices.append(d)
+                            continue
+                        attrs = (d.devmem, d.devcore, d.count, d.health, d.cus, d.xgmi_hive)
+                        if attrs == (m.devmem, m.devcore, m.count, m.health, m.cus, m.xgmi_hive):
+                            continue  # unchanged: nothing to invalidate
+                        m.devmem, m.devcore, m.count, m.health, m.cus, m.xgmi_hive = attrs
+                        if self._flat is not None and not self._flat.update_device(name, m):
+                            self._structure_changed()
+                if info.devices:
+                    self.add_node(name, info)
                 self._registered[(name, hs_key)] = NodeInfo(id=name, devices=copy.deepcopy(devs))
+        self.rebuild_flat()
 
     def run_loops(self) -> None:
         """Background registration + ledger resync (daemon threads)."""
@@ -358,8 +392,9 @@ class Scheduler:
         from vgpu.device.amd import assert_xgmi
         from .score import NodeScore
         with self._lock:
-            if self._flat is None:
+            if self._flat is None or self._flat_stale:  # first call, or a change the registration pass has not folded in
                 self._flat = N.FlatState(self.nodes, self.pods)
+                self._flat_stale = False
             res, failed = self._flat.filter(
                 node_names, nums, check_type, annos, assert_xgmi(annos), config.SCHEDULER.xgmi_weight,
                 binpack_devices=config.SCHEDULER.gpu_scheduler_policy != "spread",
