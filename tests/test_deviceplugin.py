@@ -521,3 +521,19 @@ def test_pod_annotation_overrides_share_policy(tmp_path):
     pool = int(pods[1].env["VGPU_CU_MASK_0"], 16)
     mask = int(pods[0].env["VGPU_CU_MASK_0"], 16)
     assert pool & mask == 0 and bin(pool).count("1") == 192
+
+
+def test_oversubscribed_node_hands_out_physical_budgets(tmp_path):
+    """on a node with --device-memory-scaling 1.8 every
+    container gets a physical HBM budget of cap / 1.8 (the shim's virtual
+    device memory keeps at most that much resident), so co-located pods split
+    the HBM in proportion to their caps instead of first come, first served."""
+    from vgpu.bench.control import admit_pods
+    from vgpu.bench.launch import PodSpec
+    pods = admit_pods([PodSpec(cores=0, mem_mib=230000)] * 2, 0, str(tmp_path / "a"), memory_scaling=1.8)
+    for p in pods:
+        assert p.env["VGPU_OVERSUBSCRIBE"] == "true"
+        assert p.env["VGPU_DEVICE_MEMORY_LIMIT_0"] == "230000m"
+        assert p.env["VGPU_DEVICE_MEMORY_PHYSICAL_0"] == f"{int(230000 / 1.8)}m"
+    pods = admit_pods([PodSpec(cores=0, mem_mib=100000)], 0, str(tmp_path / "b"))
+    assert "VGPU_DEVICE_MEMORY_PHYSICAL_0" not in pods[0].env and "VGPU_OVERSUBSCRIBE" not in pods[0].env

@@ -24,6 +24,9 @@ ENV_CU_SHARE = "VGPU_CU_SHARE"
 ENV_UUID = "VGPU_DEVICE_UUID_{i}"
 ENV_SHARED_REGION = "VGPU_SHARED_REGION"
 ENV_OVERSUBSCRIBE = "VGPU_OVERSUBSCRIBE"
+# Physical HBM budget of an oversubscribed container (MiB, "m" suffix): virtual
+# device memory keeps at most this much resident (native/shim/vmem.cpp).
+ENV_MEM_PHYSICAL = "VGPU_DEVICE_MEMORY_PHYSICAL_{i}"
 ENV_PRIORITY = "VGPU_TASK_PRIORITY"
 ENV_CORE_POLICY = "GPU_CORE_UTILIZATION_POLICY"
 ENV_OOM_KILLER = "ACTIVE_OOM_KILLER"

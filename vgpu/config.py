@@ -47,6 +47,10 @@ class DevicePluginConfig:
     resource_name: str = "amd.com/gpu"
     device_split_count: int = 10          # chart default (values.yaml:89-94); CLI default 2 in the reference
     device_memory_scaling: float = 1.0    # >1 enables virtual device memory (oversubscription)
+    # With device_memory_scaling > 1, each container's physical HBM budget is its
+    # cap / scaling (VGPU_DEVICE_MEMORY_PHYSICAL_<i>): co-located pods split the
+    # HBM in proportion to their caps and page the rest (native/shim/vmem.cpp).
+    vmem_physical_budget: bool = True
     device_cores_scaling: float = 1.0
     disable_core_limit: bool = False
     hw_queues_per_vgpu: int = 1           # GPU_MAX_HW_QUEUES for fractional vGPUs (0 = runtime default)
