@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <atomic>
 #include <map>
+#include <set>
 #include <mutex>
 #include <vector>
 
@@ -373,10 +374,104 @@ hipError_t hipStreamGetCaptureInfo(hipStream_t s, hipStreamCaptureStatus* st, un
 
 hipError_t hipMalloc(void** p, size_t size) { return dev_alloc(p, size, tl_dev); }
 hipError_t hipExtMallocWithFlags(void** p, size_t size, unsigned int) { return dev_alloc(p, size, tl_dev); }
-hipError_t hipMallocAsync(void** p, size_t size, hipStream_t) { return dev_alloc(p, size, tl_dev); }
-hipError_t hipMallocFromPoolAsync(void** p, size_t size, hipMemPool_t, hipStream_t) {
-  return dev_alloc(p, size, tl_dev);
+// Stream-ordered pool (one per device): freed blocks stay reserved for reuse
+// until hipMemPoolTrimTo; allocations made while a stream is being captured
+// become the graph's alloc bytes (drawn from the graph pool at launch).
+struct FakePool {
+  std::map<uintptr_t, uint64_t> live, freed;  // block -> size
+  uint64_t reserved = 0;
+};
+std::map<int, FakePool> g_pools;
+std::map<unsigned long long, uint64_t> g_cap_alloc;  // capture id -> bytes
+uint64_t g_graph_mem[16] = {};
+hipError_t pool_alloc(void** p, size_t size, hipStream_t s) {
+  {
+    std::lock_guard<std::mutex> lk(g_cap_mu);
+    auto it = g_capturing.find(s);
+    if (it != g_capturing.end()) {  // graph alloc node: a VA now, memory at launch
+      g_cap_alloc[g_capture_id[s]] += size;
+      std::lock_guard<std::mutex> g(g_mu);
+      uintptr_t a = g_next | (1ull << 44);
+      g_next += ((size + 4095) / 4096) * 4096 + 4096;
+      *p = (void*)a;
+      return hipSuccess;
+    }
+  }
+  std::lock_guard<std::mutex> g(g_mu);
+  init_locked();
+  FakePool& fp = g_pools[tl_dev];
+  for (auto it = fp.freed.begin(); it != fp.freed.end(); ++it)
+    if (it->second >= size) {  // reuse a freed block: no new memory
+      fp.live[it->first] = it->second;
+      *p = (void*)it->first;
+      fp.freed.erase(it);
+      return hipSuccess;
+    }
+  Dev& d = g_devs[tl_dev];
+  if (d.used + size > d.total) return hipErrorOutOfMemory;
+  d.used += size;
+  fp.reserved += size;
+  uintptr_t a = g_next | (1ull << 43);
+  g_next += ((size + 4095) / 4096) * 4096 + 4096;
+  fp.live[a] = size;
+  *p = (void*)a;
+  return hipSuccess;
 }
+bool pool_free(void* p) {
+  std::lock_guard<std::mutex> g(g_mu);
+  for (auto& kv : g_pools) {
+    auto it = kv.second.live.find((uintptr_t)p);
+    if (it != kv.second.live.end()) {
+      kv.second.freed[it->first] = it->second;
+      kv.second.live.erase(it);
+      return true;
+    }
+  }
+  return false;
+}
+hipError_t hipMallocAsync(void** p, size_t size, hipStream_t s) { return pool_alloc(p, size, s); }
+hipError_t hipMallocFromPoolAsync(void** p, size_t size, hipMemPool_t, hipStream_t s) {
+  return pool_alloc(p, size, s);
+}
+hipError_t hipDeviceGetMemPool(hipMemPool_t* pool, int dev) {
+  *pool = reinterpret_cast<hipMemPool_t>((uintptr_t)0x9000 + dev);
+  return hipSuccess;
+}
+hipError_t hipMemPoolGetAttribute(hipMemPool_t pool, hipMemPoolAttr attr, void* value) {
+  std::lock_guard<std::mutex> g(g_mu);
+  const int dev = (int)((uintptr_t)pool - 0x9000);
+  if (attr != hipMemPoolAttrReservedMemCurrent) return hipErrorInvalidValue;
+  *(uint64_t*)value = g_pools.count(dev) ? g_pools[dev].reserved : 0;
+  return hipSuccess;
+}
+hipError_t hipMemPoolTrimTo(hipMemPool_t pool, size_t) {
+  std::lock_guard<std::mutex> g(g_mu);
+  const int dev = (int)((uintptr_t)pool - 0x9000);
+  FakePool& fp = g_pools[dev];
+  for (auto& kv : fp.freed) {
+    fp.reserved -= kv.second;
+    g_devs[dev].used -= kv.second;
+  }
+  fp.freed.clear();
+  return hipSuccess;
+}
+hipError_t hipDeviceGetGraphMemAttribute(int dev, hipGraphMemAttributeType attr, void* value) {
+  if (attr != hipGraphMemAttrReservedMemCurrent) return hipErrorInvalidValue;
+  std::lock_guard<std::mutex> g(g_mu);
+  *(uint64_t*)value = g_graph_mem[dev];
+  return hipSuccess;
+}
+hipError_t hipDeviceGraphMemTrim(int dev) {
+  std::lock_guard<std::mutex> g(g_mu);
+  g_devs[dev].used -= g_graph_mem[dev];
+  g_graph_mem[dev] = 0;
+  return hipSuccess;
+}
+hipError_t hipMallocHost(void** p, size_t size);
+hipError_t hipHostAlloc(void** p, size_t size, unsigned int flags);
+hipError_t hipFreeHost(void*) { return hipSuccess; }
+hipError_t hipHostRegister(void*, size_t, unsigned int) { return hipSuccess; }
+hipError_t hipHostUnregister(void*) { return hipSuccess; }
 // Managed (KFD SVM) ranges start host-resident and take no VRAM until the
 // fake HSA's hsa_amd_svm_prefetch_async moves them (fake_hip_svm_move).
 struct Managed {
@@ -412,9 +507,12 @@ hipError_t hipFree(void* p) {
   }
   return dev_free(p);
 }
-hipError_t hipFreeAsync(void* p, hipStream_t) { return dev_free(p); }
+hipError_t hipFreeAsync(void* p, hipStream_t) {
+  if (pool_free(p)) return hipSuccess;
+  return dev_free(p);
+}
 
-hipError_t hipHostMalloc(void** p, size_t size, unsigned int) {
+static hipError_t host_alloc(void** p, size_t size) {
   // Host memory: a fake address too (tests allocate hundreds of GB virtually).
   std::lock_guard<std::mutex> g(g_mu);
   uintptr_t a = g_next | (1ull << 46);
@@ -422,7 +520,11 @@ hipError_t hipHostMalloc(void** p, size_t size, unsigned int) {
   *p = (void*)a;
   return hipSuccess;
 }
+hipError_t hipHostMalloc(void** p, size_t size, unsigned int) { return host_alloc(p, size); }
 hipError_t hipHostFree(void*) { return hipSuccess; }
+// Not via hipHostMalloc: a preloaded interposer would see that call too.
+hipError_t hipMallocHost(void** p, size_t size) { return host_alloc(p, size); }
+hipError_t hipHostAlloc(void** p, size_t size, unsigned int) { return host_alloc(p, size); }
 
 hipError_t hipMemCreate(hipMemGenericAllocationHandle_t* h, size_t size,
                         const hipMemAllocationProp* prop, unsigned long long) {
@@ -514,6 +616,7 @@ struct FakeNode {
 };
 struct FakeGraph {
   std::vector<FakeNode*> nodes;
+  uint64_t alloc_bytes = 0;  // captured hipMallocAsync bytes (graph alloc nodes)
 };
 // A capture yields an (empty) graph: enough for the shim's capture -> graph
 // -> exec bookkeeping.
@@ -524,8 +627,14 @@ hipError_t hipStreamEndCapture(hipStream_t s, hipGraph_t* g) {
   if (it == g_capturing.end()) return hipErrorIllegalState;
   const bool invalid = it->second;
   g_capturing.erase(it);
+  const unsigned long long cid = g_capture_id[s];
   g_capture_id.erase(s);
-  if (!invalid && g) *g = reinterpret_cast<hipGraph_t>(new FakeGraph);
+  if (!invalid && g) {
+    auto* fg = new FakeGraph;
+    fg->alloc_bytes = g_cap_alloc[cid];
+    *g = reinterpret_cast<hipGraph_t>(fg);
+  }
+  g_cap_alloc.erase(cid);
   return invalid ? hipErrorStreamCaptureInvalidated : hipSuccess;
 }
 hipError_t hipGraphDestroy(hipGraph_t g) {
@@ -556,19 +665,36 @@ hipError_t hipGraphChildGraphNodeGetGraph(hipGraphNode_t node, hipGraph_t* g) {
   *g = reinterpret_cast<FakeNode*>(node)->child;
   return hipSuccess;
 }
+std::set<const void*> g_live_execs;  // a test may launch an exec it destroyed
 hipError_t hipGraphInstantiateWithFlags(hipGraphExec_t* e, hipGraph_t g, unsigned long long) {
   *e = reinterpret_cast<hipGraphExec_t>(new hipGraph_t(g));
+  std::lock_guard<std::mutex> l(g_mu);
+  g_live_execs.insert(*e);
   return hipSuccess;
 }
 hipError_t hipGraphInstantiate(hipGraphExec_t* e, hipGraph_t g, hipGraphNode_t*, char*, size_t) {
   return hipGraphInstantiateWithFlags(e, g, 0);
 }
 hipError_t hipGraphExecDestroy(hipGraphExec_t e) {
+  {
+    std::lock_guard<std::mutex> l(g_mu);
+    g_live_execs.erase(e);
+  }
   delete reinterpret_cast<hipGraph_t*>(e);
   return hipSuccess;
 }
-hipError_t hipGraphLaunch(hipGraphExec_t, hipStream_t) {
+hipError_t hipGraphLaunch(hipGraphExec_t e, hipStream_t) {
   init();
+  if (e) {  // alloc nodes draw on the device's graph pool (kept until hipDeviceGraphMemTrim)
+    std::lock_guard<std::mutex> g(g_mu);
+    auto* fg = g_live_execs.count(e) ? reinterpret_cast<FakeGraph*>(*reinterpret_cast<hipGraph_t*>(e)) : nullptr;
+    if (fg && fg->alloc_bytes > g_graph_mem[tl_dev]) {
+      const uint64_t grow = fg->alloc_bytes - g_graph_mem[tl_dev];
+      if (g_devs[tl_dev].used + grow > g_devs[tl_dev].total) return hipErrorOutOfMemory;
+      g_devs[tl_dev].used += grow;
+      g_graph_mem[tl_dev] = fg->alloc_bytes;
+    }
+  }
   g_graph_launches.fetch_add(1);
   g_launches.fetch_add(1);
   timeline_launch();

@@ -35,7 +35,7 @@ extern "C" {
 #endif
 
 #define VGPU_REGION_MAGIC 0x56475055u /* "VGPU" */
-#define VGPU_REGION_VERSION 3u
+#define VGPU_REGION_VERSION 4u
 #define VGPU_MAX_DEVICES 16
 #define VGPU_MAX_PROCS 1024
 #define VGPU_UUID_LEN 64
@@ -76,6 +76,9 @@ typedef struct vgpu_proc_slot {
   uint64_t throttle_wait_ns; /* time spent blocked in the dispatch limiter   */
   uint64_t oom_events;       /* allocations refused by the cap               */
   uint64_t last_launch_ns;   /* CLOCK_MONOTONIC of the latest dispatch       */
+  uint64_t pinned_host_bytes;/* page-locked host memory (hipHostMalloc & co.); not
+                              * charged against the HBM cap, optionally capped by
+                              * VGPU_PINNED_HOST_LIMIT                           */
   vgpu_dev_usage_t used[VGPU_MAX_DEVICES];
 } vgpu_proc_slot_t;
 

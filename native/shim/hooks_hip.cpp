@@ -151,6 +151,33 @@ bool uncharge(void* p, Alloc* a) {
   return true;
 }
 
+// Stream-ordered allocations are charged by their pool's reserved size (pools.cpp).
+hipError_t real_alloc_async(void** ptr, size_t size, hipMemPool_t pool, hipStream_t stream, bool from_pool) {
+  InHipAlloc in_alloc;
+  return from_pool ? REAL_HIP(hipMallocFromPoolAsync)(ptr, size, pool, stream)
+                   : REAL_HIP(hipMallocAsync)(ptr, size, stream);
+}
+
+// Page-locked host memory: booked per process, not against the HBM cap.
+template <class F>
+hipError_t pinned_alloc(void** ptr, size_t size, F&& real) {
+  ensure_init();
+  if (!st().enabled || size == 0) return real();
+  if (!pinned_reserve(size)) return hipErrorOutOfMemory;
+  hipError_t rc = real();
+  if (rc != hipSuccess) {
+    pinned_release(size);
+    return rc;
+  }
+  ledger_add(*ptr, size, -1, kPinnedHost);
+  return rc;
+}
+
+void pinned_forget(void* ptr) {
+  Alloc a;
+  if (ptr && ledger_take_if(ptr, kPinnedHost, &a)) pinned_release(a.size);
+}
+
 }  // namespace
 
 extern "C" {
@@ -174,16 +201,49 @@ __attribute__((visibility("default"))) hipError_t hipExtMallocWithFlags(void** p
 
 __attribute__((visibility("default"))) hipError_t hipMallocAsync(void** ptr, size_t size,
                                                                  hipStream_t stream) {
-  return charged_alloc(ptr, size, kDeviceBuf,
-                       [&] { return REAL_HIP(hipMallocAsync)(ptr, size, stream); });
+  return pool_alloc_async(ptr, size, stream, nullptr, real_alloc_async);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMallocFromPoolAsync(void** ptr, size_t size,
                                                                          hipMemPool_t pool,
                                                                          hipStream_t stream) {
-  return charged_alloc(ptr, size, kDeviceBuf, [&] {
-    return REAL_HIP(hipMallocFromPoolAsync)(ptr, size, pool, stream);
-  });
+  return pool_alloc_async(ptr, size, stream, pool, real_alloc_async);
+}
+
+// ---- page-locked host memory (pinned_host_bytes; VGPU_PINNED_HOST_LIMIT) -------------
+__attribute__((visibility("default"))) hipError_t hipHostMalloc(void** ptr, size_t size, unsigned int flags) {
+  return pinned_alloc(ptr, size, [&] { return REAL_HIP(hipHostMalloc)(ptr, size, flags); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipMallocHost(void** ptr, size_t size) {
+  return pinned_alloc(ptr, size, [&] { return REAL_HIP(hipMallocHost)(ptr, size); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipHostAlloc(void** ptr, size_t size, unsigned int flags) {
+  return pinned_alloc(ptr, size, [&] { return REAL_HIP(hipHostAlloc)(ptr, size, flags); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipHostRegister(void* p, size_t size, unsigned int flags) {
+  void* ptr = p;
+  return pinned_alloc(&ptr, size, [&] { return REAL_HIP(hipHostRegister)(p, size, flags); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipHostUnregister(void* p) {
+  ensure_init();
+  pinned_forget(p);
+  return REAL_HIP(hipHostUnregister)(p);
+}
+
+__attribute__((visibility("default"))) hipError_t hipHostFree(void* ptr) {
+  ensure_init();
+  pinned_forget(ptr);
+  return REAL_HIP(hipHostFree)(ptr);
+}
+
+__attribute__((visibility("default"))) hipError_t hipFreeHost(void* ptr) {
+  ensure_init();
+  pinned_forget(ptr);
+  return REAL_HIP(hipFreeHost)(ptr);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMallocManaged(void** ptr, size_t size,
@@ -455,10 +515,13 @@ __attribute__((visibility("default"))) hipError_t hipGraphLaunch(hipGraphExec_t 
   }();
   uint64_t wg = graph_exec_workgroups(exec);
   const int dev = cur_dev();
+  uint64_t tentative = 0;
+  if (!pools_graph_admit(exec, dev, &tentative)) return hipErrorOutOfMemory;  // alloc nodes past the cap
   const bool track = limiter_on_launch(dev, wg ? wg : fallback_tokens);
   vmem_graph_launched(exec);
   hipError_t rc = REAL_HIP(hipGraphLaunch)(exec, stream);
   if (track) limiter_track(dev, stream, rc);
+  pools_graph_launched(dev, tentative);
   return rc;
 }
 
@@ -470,6 +533,7 @@ __attribute__((visibility("default"))) hipError_t hipGraphInstantiate(hipGraphEx
   if (rc == hipSuccess && pExec) {
     graph_exec_record(*pExec, graph);
     vmem_graph_instantiated(graph, *pExec);
+    pools_graph_instantiated(graph, *pExec);
   }
   return rc;
 }
@@ -482,6 +546,7 @@ __attribute__((visibility("default"))) hipError_t hipGraphInstantiateWithFlags(h
   if (rc == hipSuccess && pExec) {
     graph_exec_record(*pExec, graph);
     vmem_graph_instantiated(graph, *pExec);
+    pools_graph_instantiated(graph, *pExec);
   }
   return rc;
 }
@@ -493,6 +558,7 @@ __attribute__((visibility("default"))) hipError_t hipGraphInstantiateWithParams(
   if (rc == hipSuccess && pExec) {
     graph_exec_record(*pExec, graph);
     vmem_graph_instantiated(graph, *pExec);
+    pools_graph_instantiated(graph, *pExec);
   }
   return rc;
 }
@@ -500,11 +566,13 @@ __attribute__((visibility("default"))) hipError_t hipGraphInstantiateWithParams(
 __attribute__((visibility("default"))) hipError_t hipGraphExecDestroy(hipGraphExec_t exec) {
   graph_exec_forget(exec);
   vmem_graph_destroyed(exec);
+  pools_graph_destroyed(exec);
   return REAL_HIP(hipGraphExecDestroy)(exec);
 }
 
 __attribute__((visibility("default"))) hipError_t hipGraphDestroy(hipGraph_t graph) {
   vmem_graph_destroyed(graph);
+  pools_graph_destroyed(graph);
   return REAL_HIP(hipGraphDestroy)(graph);
 }
 
@@ -539,7 +607,11 @@ __attribute__((visibility("default"))) hipError_t hipStreamEndCapture(hipStream_
                                                                       hipGraph_t* graph) {
   const unsigned long long cid = vmem_capture_begin_id(stream);
   hipError_t rc = REAL_HIP(hipStreamEndCapture)(stream, graph);
-  if (cid) vmem_capture_ended(cid, rc == hipSuccess && graph ? *graph : nullptr);
+  if (cid) {
+    hipGraph_t g = rc == hipSuccess && graph ? *graph : nullptr;
+    vmem_capture_ended(cid, g);
+    pools_capture_ended(cid, g);
+  }
   int cur = g_open_captures.load();
   while (cur > 0 && !g_open_captures.compare_exchange_weak(cur, cur - 1)) {
   }

@@ -66,6 +66,7 @@ static void atfork_child() {
   hostpid_after_fork();
   limiter_after_fork();
   vmem_after_fork();
+  pools_after_fork();
   if (s.region) {
     s.slot = region_claim_slot(s.region, s.pid, self_host_pid(nullptr), s.lim.priority);
     hostpid_publish();

@@ -338,7 +338,7 @@ void limiter_main() {
     hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
     (void)xm(&m);
   }
-  uint64_t last = mono_ns(), last_mask = last;
+  uint64_t last = mono_ns(), last_mask = last, last_pool = last;
   uint64_t mask_sig = 0;
   State& s = st();
   while (!g_shutdown.load(std::memory_order_relaxed)) {
@@ -387,6 +387,12 @@ void limiter_main() {
         L.win_charge = L.win_busy = 0;
         L.win_start = now;
       }
+    }
+    // Stream-ordered pools give memory back on their own (release threshold):
+    // keep their charge current.
+    if (now - last_pool >= 50000000ull) {
+      last_pool = now;
+      if (pools_any()) pools_sync(false);
     }
     // Re-apply CU masks when the region's masks change (elastic resizing by
     // the node monitor / device plugin).

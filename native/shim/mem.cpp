@@ -36,6 +36,8 @@ static void add_usage(vgpu_dev_usage_t& u, uint64_t size, int kind, bool add) {
   switch (kind) {
     case kIpcImport:
       return;  // another process's buffer: charged to its exporter only
+    case kPinnedHost:
+      return;  // host memory: pinned_host_bytes (pools.cpp), not the HBM cap
     case kHostSpill:
       op(&u.host_bytes);
       return;
@@ -62,7 +64,20 @@ static void note_peak(vgpu_dev_usage_t& u) {
   }
 }
 
+static bool mem_reserve_once(int dev, uint64_t size, int kind, bool quiet);
+
+// Reserve `size` against the container's cap.  Before refusing, memory that
+// stream-ordered pools hold for reuse is trimmed and re-read (pools.cpp).
 bool mem_reserve(int dev, uint64_t size, int kind) {
+  if (mem_reserve_once(dev, size, kind, true)) return true;
+  if (pools_any()) {
+    pools_sync(true);
+    if (mem_reserve_once(dev, size, kind, true)) return true;
+  }
+  return mem_reserve_once(dev, size, kind, false);
+}
+
+static bool mem_reserve_once(int dev, uint64_t size, int kind, bool quiet) {
   State& s = st();
   vgpu_proc_slot_t* sl = my_slot();
   if (!s.enabled || !sl || dev < 0 || dev >= VGPU_MAX_DEVICES) return true;
@@ -79,9 +94,9 @@ bool mem_reserve(int dev, uint64_t size, int kind) {
   }
   bool ok = used + size <= limit;
   if (ok) add_usage(sl->used[dev], size, kind, true);
-  else __atomic_fetch_add(&sl->oom_events, 1, __ATOMIC_RELAXED);
+  else if (!quiet) __atomic_fetch_add(&sl->oom_events, 1, __ATOMIC_RELAXED);
   region_unlock(s.region);
-  if (!ok) {
+  if (!ok && !quiet) {
     trace_emit(VGPU_EV_OOM, dev, size, limit);
     VLOG_WARN("Device %d OOM %llu / %llu (request %llu bytes)", dev,
               (unsigned long long)(used + size), (unsigned long long)limit,

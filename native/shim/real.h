@@ -95,6 +95,16 @@ using hipStreamBeginCaptureToGraph = hipError_t (*)(hipStream_t, hipGraph_t, con
 using hipStreamEndCapture = hipError_t (*)(hipStream_t, hipGraph_t*);
 using hipStreamGetCaptureInfo = hipError_t (*)(hipStream_t, hipStreamCaptureStatus*, unsigned long long*);
 using hipGraphDestroy = hipError_t (*)(hipGraph_t);
+using hipMemPoolGetAttribute = hipError_t (*)(hipMemPool_t, hipMemPoolAttr, void*);
+using hipMemPoolTrimTo = hipError_t (*)(hipMemPool_t, size_t);
+using hipDeviceGetMemPool = hipError_t (*)(hipMemPool_t*, int);
+using hipDeviceGetGraphMemAttribute = hipError_t (*)(int, hipGraphMemAttributeType, void*);
+using hipDeviceGraphMemTrim = hipError_t (*)(int);
+using hipMallocHost = hipError_t (*)(void**, size_t);
+using hipHostAlloc = hipError_t (*)(void**, size_t, unsigned int);
+using hipFreeHost = hipError_t (*)(void*);
+using hipHostRegister = hipError_t (*)(void*, size_t, unsigned int);
+using hipHostUnregister = hipError_t (*)(void*);
 using hipMalloc3D = hipError_t (*)(hipPitchedPtr*, hipExtent);
 using hipMallocArray = hipError_t (*)(hipArray_t*, const hipChannelFormatDesc*, size_t, size_t, unsigned int);
 using hipMalloc3DArray = hipError_t (*)(hipArray_t*, const hipChannelFormatDesc*, hipExtent, unsigned int);

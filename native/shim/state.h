@@ -30,6 +30,7 @@ enum AllocKind : int {
   kModule = 4,      // code object bytes
   kRuntime = 5,     // HSA pool allocations made outside the HIP hooks (runtime-internal)
   kIpcImport = 6,   // another process's buffer mapped through hipIpcOpenMemHandle (charged 0)
+  kPinnedHost = 7,  // page-locked host memory (hipHostMalloc & co.): pinned_host_bytes, not the HBM cap
 };
 
 struct Alloc {
@@ -103,6 +104,21 @@ void limiter_track(int dev, hipStream_t stream, hipError_t launch_rc);
 extern std::atomic<int> g_open_captures;
 extern std::shared_mutex g_capture_mu;  // writers: capture begin; readers: limiter-thread markers
 void limiter_stats(int dev, uint64_t* charged_ns, uint64_t* busy_ns);
+
+// Stream-ordered pools, graph memory and pinned host memory (pools.cpp).
+hipError_t pool_alloc_async(void** ptr, size_t size, hipStream_t stream, hipMemPool_t pool,
+                            hipError_t (*real)(void**, size_t, hipMemPool_t, hipStream_t, bool));
+void pools_sync(bool trim);
+bool pools_any();
+void pools_capture_ended(unsigned long long capture_id, hipGraph_t graph);
+void pools_graph_instantiated(hipGraph_t graph, hipGraphExec_t exec);
+void pools_graph_destroyed(const void* graph_or_exec);
+uint64_t pools_exec_bytes(hipGraphExec_t exec);
+bool pools_graph_admit(hipGraphExec_t exec, int dev, uint64_t* tentative);
+void pools_graph_launched(int dev, uint64_t tentative);
+bool pinned_reserve(uint64_t size);
+void pinned_release(uint64_t size);
+void pools_after_fork();
 
 // HSA agents behind HIP device ordinals (cumask.cpp).
 bool hsa_gpu_agent(int dev, hsa_agent_t* out);

@@ -446,6 +446,71 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (sc == "mempool") {
+    // Stream-ordered pool + graph alloc nodes + pinned host memory under an
+    // 8 GiB cap on a 16 GiB fake device: the charge follows what the pools
+    // really hold, and physical use never passes the cap.
+    const size_t G = 1ull << 30;
+    auto self_region = sym<void* (*)()>("vgpu_self_region");
+    auto self_slot = sym<int (*)()>("vgpu_self_slot");
+    auto slot = [&]() -> vgpu_proc_slot_t& { return ((vgpu_shared_region_t*)self_region())->procs[self_slot()]; };
+    uint64_t peak = 0;
+    auto show = [&](const char* k) {
+      uint64_t p = fake_hip_physical_used(dev);
+      if (p > peak) peak = p;
+      printf("%s_charge=%llu\n%s_phys=%llu\n", k, (unsigned long long)slot().used[dev].total_bytes, k,
+             (unsigned long long)p);
+    };
+    hipStream_t s0 = (hipStream_t)0x31;
+    void *a, *b, *c, *d;
+    printf("a=%d\n", hipMallocAsync(&a, 3 * G, s0));
+    printf("b=%d\n", hipMallocAsync(&b, 3 * G, s0));
+    show("ab");
+    hipFreeAsync(a, s0);
+    show("free_a");
+    printf("c=%d\n", hipMallocAsync(&c, 2 * G, s0));
+    show("c_reused");
+    hipFreeAsync(b, s0);
+    hipFreeAsync(c, s0);
+    printf("d=%d\n", hipMallocAsync(&d, 4 * G, s0));  // needs the pool trimmed first
+    show("d");
+    // graphs with alloc nodes
+    auto make_graph = [&](size_t bytes, hipGraphExec_t* ex) {
+      hipStream_t cs = (hipStream_t)0x32;
+      hipGraph_t g = nullptr;
+      void* q = nullptr;
+      hipStreamBeginCapture(cs, hipStreamCaptureModeGlobal);
+      hipMallocAsync(&q, bytes, cs);
+      hipFreeAsync(q, cs);
+      hipStreamEndCapture(cs, &g);
+      return hipGraphInstantiate(ex, g, nullptr, nullptr, 0);
+    };
+    hipGraphExec_t g3, g2, g6;
+    make_graph(3 * G, &g3);
+    show("captured");  // nothing charged at capture
+    printf("launch3=%d\n", hipGraphLaunch(g3, s0));
+    show("launch3");
+    make_graph(2 * G, &g2);
+    printf("launch2=%d\n", hipGraphLaunch(g2, s0));
+    show("launch2");
+    make_graph(6 * G, &g6);
+    printf("launch6=%d\n", hipGraphLaunch(g6, s0));  // 4 GiB live + 6 GiB graph pool > 8 GiB
+    show("launch6");
+    hipFreeAsync(d, s0);
+    // pinned host memory, VGPU_PINNED_HOST_LIMIT=1g
+    void *h1, *h2;
+    int r1 = hipHostMalloc(&h1, 512u << 20, 0);
+    int r2 = hipHostMalloc(&h2, 768u << 20, 0);
+    printf("pin1=%d\npin2=%d\npinned_after=%llu\n", r1, r2, (unsigned long long)slot().pinned_host_bytes);
+    hipHostFree(h1);
+    int r3 = hipMallocHost(&h2, 768u << 20);
+    printf("pin3=%d\npinned_final=%llu\n", r3, (unsigned long long)slot().pinned_host_bytes);
+    hipFreeHost(h2);
+    printf("pinned_zero=%llu\npeak_phys=%llu\n", (unsigned long long)slot().pinned_host_bytes,
+           (unsigned long long)peak);
+    return 0;
+  }
+
   if (sc == "spill") {
     // Oversubscription: allocate `n` chunks; report how many landed in host memory.
     size_t chunk = argc > 2 ? strtoull(argv[2], nullptr, 10) : (1ull << 30);

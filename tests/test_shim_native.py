@@ -209,6 +209,30 @@ def test_vmem_off_keeps_zero_copy_spill(native_build):
     assert o["final_total"] == "0" and o["final_host"] == "0"
 
 
+def test_stream_ordered_pool_and_graph_memory_follow_physical_use(native_build):
+    """hipMallocAsync memory is charged by what its pool
+    really holds (freed blocks stay charged until trimmed, reuse costs
+    nothing), the pool is trimmed before an allocation is refused, graph alloc
+    nodes are charged when the graph runs (not at capture), a graph whose alloc
+    nodes would pass the cap is refused, and physical use never passes the cap.
+    Page-locked host memory is booked per process and capped by
+    VGPU_PINNED_HOST_LIMIT."""
+    o = run("mempool", env={"VGPU_FAKE_MEM": str(16 * GiB), "VGPU_DEVICE_MEMORY_LIMIT_0": "8g",
+                            "VGPU_PINNED_HOST_LIMIT": "1g"})
+    g = lambda k: int(o[k]) / GiB  # noqa: E731
+    assert (o["a"], o["b"], o["c"], o["d"]) == ("0", "0", "0", "0")
+    for k in ("ab", "free_a", "c_reused", "d", "captured", "launch3", "launch2", "launch6"):
+        assert g(k + "_charge") == g(k + "_phys"), k  # the charge is the physical footprint
+    assert g("free_a_charge") == 6 and g("c_reused_charge") == 6  # held by the pool, reused
+    assert g("d_charge") == 4  # trimmed, then 4 GiB
+    assert g("captured_charge") == 4 and g("launch3_charge") == 7 and g("launch2_charge") == 7
+    assert o["launch6"] == "2" and g("launch6_phys") == 4  # hipErrorOutOfMemory, graph pool trimmed
+    assert g("peak_phys") <= 8
+    assert (o["pin1"], o["pin2"], o["pin3"]) == ("0", "2", "0")
+    assert int(o["pinned_after"]) == 512 << 20 and int(o["pinned_final"]) == 768 << 20
+    assert o["pinned_zero"] == "0"
+
+
 def test_oversubscribe_still_capped(native_build):
     o = run("spill", GiB, 30, env={"VGPU_FAKE_MEM": str(8 * GiB), "VGPU_DEVICE_MEMORY_LIMIT_0": "20g",
                                    "VGPU_OVERSUBSCRIBE": "true"})

@@ -326,12 +326,101 @@ def vmem(block_gib: int = 4, wait_s: int = 20) -> dict:
     return res
 
 
+def _vram_used_files() -> dict[str, int]:
+    import glob
+    out = {}
+    for f in glob.glob("/sys/bus/pci/devices/*/mem_info_vram_used"):
+        try:
+            out[f] = int(open(f).read())
+        except (OSError, ValueError):
+            pass
+    return out
+
+
+def asynccap(cap_mib: int = 8192, graph_mib: int = 1024) -> dict:
+    """Stream-ordered allocations under the cap: run with
+    PYTORCH_HIP_ALLOC_CONF=backend:hipMallocAsync.  Alloc / free / re-alloc
+    cycles of varying sizes up to OOM, then captured graphs whose temporaries
+    are graph alloc nodes.  amdgpu's own VRAM counter (mem_info_vram_used) is
+    sampled throughout; the peak over the pre-init baseline is reported."""
+    import random
+    base = _vram_used_files()  # before this process touches the GPU
+    import torch
+    p = torch.cuda.get_device_properties(0)
+    bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    path = f"/sys/bus/pci/devices/{bdf}/mem_info_vram_used"
+    if path not in base:
+        return {"error": f"no VRAM counter at {path}", "candidates": sorted(base)}
+    baseline = base[path]
+    peak = 0
+    samples = 0
+
+    def sample():
+        nonlocal peak, samples
+        torch.cuda.synchronize()
+        v = int(open(path).read()) - baseline
+        peak = max(peak, v)
+        samples += 1
+
+    rng = random.Random(0)
+    MiB = 1 << 20
+    reached = 0
+    ooms = 0
+    for rnd in range(3):
+        live = []
+        while True:
+            n = rng.choice([64, 256, 512, 768, 1024, 1536]) * MiB
+            try:
+                live.append(torch.empty(n, dtype=torch.uint8, device="cuda").fill_(rnd))
+            except torch.OutOfMemoryError:
+                ooms += 1
+                break
+            sample()
+        reached = max(reached, sum(t.numel() for t in live))
+        del live[::2]
+        sample()
+        while True:  # re-allocate other sizes into the holes and past them
+            n = rng.choice([96, 384, 640, 1280]) * MiB
+            try:
+                live.append(torch.empty(n, dtype=torch.uint8, device="cuda").fill_(rnd + 1))
+            except torch.OutOfMemoryError:
+                ooms += 1
+                break
+            sample()
+        del live
+        sample()
+    # graphs whose temporaries are stream-ordered allocations (graph alloc nodes)
+    x = torch.randn(graph_mib * MiB // 4, device="cuda")
+    graph_ok = 0
+    for k in (1, 2, 3):
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            y = (x * k + 1).relu().sum()  # warm-up outside the capture
+        torch.cuda.current_stream().wait_stream(s)
+        try:
+            with torch.cuda.graph(g):
+                y = ((x * k + 1).relu() * (x - k)).sum()
+            for _ in range(3):
+                g.replay()
+                sample()
+            graph_ok += 1
+        except (torch.OutOfMemoryError, RuntimeError) as e:
+            print("graph", k, "refused:", str(e)[:200], flush=True)
+        del g
+        sample()
+    return {"cap": cap_mib * MiB, "baseline": baseline, "peak_over_baseline": peak, "samples": samples,
+            "max_live_reached": reached, "ooms": ooms, "graphs_replayed": graph_ok, "y": float(y),
+            "backend": torch.cuda.get_allocator_backend()}
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     cmd = argv.pop(0) if argv else "census"
     nums = [int(a) for a in argv]
     out = {"census": census, "busy": busy, "cap": cap, "smi": smi, "graph": graph, "arrays": arrays,
-           "progress": progress, "vmem": vmem, "capheld": capheld}[cmd](*nums)
+           "progress": progress, "vmem": vmem, "capheld": capheld, "asynccap": asynccap}[cmd](*nums)
     out["shim"] = shim_stats()
     print("PROBE " + json.dumps(out), flush=True)
     return 0

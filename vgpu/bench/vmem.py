@@ -365,7 +365,8 @@ def run_pod_child(part: str, budget_gib: float, migrate: bool, args: list[str], 
                 "VGPU_DEVICE_MEMORY_PHYSICAL_0": f"{int(budget_gib * 1024)}m",
                 "VGPU_LOG_LEVEL": env.get("VGPU_LOG_LEVEL", "3"), "VGPU_VMEM_MIGRATE": "1" if migrate else "0"})
     if os.environ.get("VGPU_TRACE") and migrate:
-        env["VGPU_TRACE"] = os.environ["VGPU_TRACE"] + f".{part}"
+        env["VGPU_TRACE"] = os.path.join(os.environ["VGPU_TRACE"], f"part_{part}")
+        os.makedirs(env["VGPU_TRACE"], exist_ok=True)
         env.setdefault("VGPU_TRACE_EVENTS", "1000000")
     import tempfile
     errf = tempfile.NamedTemporaryFile(mode="w+", prefix=f"vmem_{part}_", suffix=".log",

@@ -19,7 +19,7 @@ MAX_PROCS = 1024
 UUID_LEN = 64
 CU_WORDS = 4
 MAGIC = 0x56475055
-VERSION = 3
+VERSION = 4
 PROC_FREE, PROC_RUNNING, PROC_SUSPENDED = 0, 1, 2
 # slot.host_pid_src (how the host pid was obtained)
 HOSTPID_UNVERIFIED, HOSTPID_KFD_DIFF, HOSTPID_MONITOR, HOSTPID_HOST_NS = 0, 1, 2, 3
@@ -36,7 +36,8 @@ class ProcSlot(ctypes.Structure):
                 ("priority", ctypes.c_int32), ("host_pid_src", ctypes.c_int32), ("reserved0", ctypes.c_int32),
                 ("start_ns", ctypes.c_uint64), ("launches", ctypes.c_uint64),
                 ("throttle_wait_ns", ctypes.c_uint64), ("oom_events", ctypes.c_uint64),
-                ("last_launch_ns", ctypes.c_uint64), ("used", DevUsage * MAX_DEVICES)]
+                ("last_launch_ns", ctypes.c_uint64), ("pinned_host_bytes", ctypes.c_uint64),
+                ("used", DevUsage * MAX_DEVICES)]
 
 
 class DeviceCfg(ctypes.Structure):
