@@ -5,7 +5,7 @@
 //
 // {"gpus":[{"uuid":..,"bdf":"0000:05:00.0","name":..,"vram":N,"vram_used":N,"cus":256,
 //           "numa":0,"render":128,"card":0,"kfd_id":N,"hive":N,"partition":"SPX",
-//           "mem_partition":"NPS1","gfx":0,"umc":0,"vendor":4098,
+//           "mem_partition":"NPS1","partition_id":0,"gfx":0,"umc":0,"vendor":4098,
 //           "processes":[{"pid":1,"vram":N,"cu":N,"gfx_ns":N}]}],
 //  "link":"xgmi"|"pcie", "events":[{"gpu":0,"type":3,"message":".."}]}
 // Telemetry ($VGPU_FAKE_AMDSMI_TELEMETRY, re-read on every call so a test can
@@ -263,6 +263,7 @@ amdsmi_status_t amdsmi_get_gpu_kfd_info(amdsmi_processor_handle h, amdsmi_kfd_in
   memset(info, 0, sizeof(*info));
   info->kfd_id = (uint64_t)(*g)["kfd_id"].num(1000 + idx(h));
   info->node_id = (uint32_t)(idx(h) + 1);
+  info->current_partition_id = (uint32_t)(*g)["partition_id"].num(0);
   return AMDSMI_STATUS_SUCCESS;
 }
 

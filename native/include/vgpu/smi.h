@@ -42,7 +42,8 @@ typedef struct vgpu_smi_device {
   uint32_t health;       /* 1 healthy */
   uint32_t gfx_activity; /* % */
   uint32_t umc_activity; /* % */
-  uint32_t reserved[7];
+  uint32_t partition_id; /* compute partition of its physical GPU (0 in SPX) */
+  uint32_t reserved[6];
 } vgpu_smi_device_t;
 
 typedef struct vgpu_smi_proc {

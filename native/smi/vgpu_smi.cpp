@@ -190,8 +190,10 @@ struct AmdSmi {
     }
     amdsmi_kfd_info_t kfd;
     if (amdsmi_get_gpu_kfd_info && amdsmi_get_gpu_kfd_info(p, &kfd) == AMDSMI_STATUS_SUCCESS &&
-        kfd.kfd_id != 0xFFFFFFFFFFFFFFFFull)
+        kfd.kfd_id != 0xFFFFFFFFFFFFFFFFull) {
       d->kfd_gpu_id = (uint32_t)kfd.kfd_id;
+      if (kfd.current_partition_id != 0xFFFFFFFFu) d->partition_id = kfd.current_partition_id;
+    }
     amdsmi_enumeration_info_t en;
     if (amdsmi_get_gpu_enumeration_info &&
         amdsmi_get_gpu_enumeration_info(p, &en) == AMDSMI_STATUS_SUCCESS) {

@@ -405,6 +405,9 @@ def test_every_example_pod_schedules_on_an_mi355x_node():
     cpx = usage(8, mem=MIB_288G // 8)
     for d in cpx:
         d.type = "AMD-MI355X-CPX"
+    cpx_mixed = copy.deepcopy(cpx)  # partition strategy mixed: CPX partitions are amd.com/gpu-cpx
+    for d in cpx_mixed:
+        d.resource = "amd.com/gpu-cpx"
     placed = {}
     for f in sorted(os.listdir(ex)):
         for p in yaml.safe_load_all(open(os.path.join(ex, f))):
@@ -412,11 +415,13 @@ def test_every_example_pod_schedules_on_an_mi355x_node():
             assert any(reqs), f
             annos = p["metadata"].get("annotations") or {}
             nodes = {"spx": NodeUsage(copy.deepcopy(spx)), "cpx": NodeUsage(copy.deepcopy(cpx)),
-                     "vmem": NodeUsage(usage(8, mem=MIB_288G * 3 // 2))}
+                     "vmem": NodeUsage(usage(8, mem=MIB_288G * 3 // 2)),
+                     "cpxmixed": NodeUsage(copy.deepcopy(cpx_mixed))}
             best = pick_node(calc_score(nodes, reqs, annos))
             assert best is not None, f
             placed[f] = best.node_id
     assert placed["compute-partition.yaml"] == "cpx"
+    assert placed["compute-partition-mixed.yaml"] == "cpxmixed"
     assert placed["specify-card-type-not-use.yaml"] != "cpx"
     assert placed["virtual-memory.yaml"] == "vmem"
 

@@ -60,8 +60,12 @@ def decode_node_devices(s: str) -> list[DeviceInfo]:
 
 
 def encode_node_devices_ext(devs: list[DeviceInfo]) -> str:
-    return json.dumps({d.id: {"cus": d.cus, "hive": d.xgmi_hive, "index": d.index} for d in devs},
-                      sort_keys=True, separators=(",", ":"))
+    def ext(d: DeviceInfo) -> dict:
+        e = {"cus": d.cus, "hive": d.xgmi_hive, "index": d.index}
+        if d.resource != DeviceInfo.resource:  # a partition under its own resource (mixed strategy)
+            e["res"] = d.resource
+        return e
+    return json.dumps({d.id: ext(d) for d in devs}, sort_keys=True, separators=(",", ":"))
 
 
 def apply_node_devices_ext(devs: list[DeviceInfo], s: str | None) -> list[DeviceInfo]:
@@ -77,6 +81,7 @@ def apply_node_devices_ext(devs: list[DeviceInfo], s: str | None) -> list[Device
             d.cus = int(e.get("cus", d.cus))
             d.xgmi_hive = str(e.get("hive", d.xgmi_hive))
             d.index = int(e.get("index", d.index))
+            d.resource = str(e.get("res", d.resource))
     return devs
 
 

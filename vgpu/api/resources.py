@@ -18,6 +18,8 @@ DEVICE_TYPE_PREFIX = "AMD-"          # device type string, e.g. "AMD-MI355X"
 
 # ---- extended resources (per container limits) --------------------------------
 RESOURCE_COUNT = "amd.com/gpu"
+# compute-partition count resources of a mixed-strategy node: amd.com/gpu-cpx ...
+PARTITION_SUFFIXES = ("dpx", "qpx", "cpx")
 RESOURCE_MEM = "amd.com/gpumem"
 RESOURCE_MEM_PERCENTAGE = "amd.com/gpumem-percentage"
 RESOURCE_CORES = "amd.com/gpucores"
@@ -81,6 +83,7 @@ class DeviceInfo:
     cus: int = 256
     xgmi_hive: str = ""
     index: int = 0
+    resource: str = "amd.com/gpu"   # count resource it is advertised under (partition strategy)
 
 
 @dataclass
@@ -91,6 +94,7 @@ class ContainerDeviceRequest:
     memreq: int = 0            # MiB
     mem_percentage: int = MEM_PERCENT_UNSET
     coresreq: int = 0
+    resource: str = "amd.com/gpu"  # count resource the container asked for (amd.com/gpu-cpx ...)
 
 
 @dataclass
@@ -124,3 +128,4 @@ class DeviceUsage:
     cus: int = 256
     xgmi_hive: str = ""
     pods: list = field(default_factory=list)
+    resource: str = "amd.com/gpu"

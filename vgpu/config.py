@@ -56,6 +56,9 @@ class DevicePluginConfig:
     hw_queues_per_vgpu: int = 1           # GPU_MAX_HW_QUEUES for fractional vGPUs (0 = runtime default)
     hsa_tools_intercept: bool = False     # also hand the shim ROCr's API table (HSA_TOOLS_LIB)
     partition_mode: str = ""             # SPX|DPX|QPX|CPX expected compute partition ("" = as found)
+    # MIG-strategy analogue (vgpu/deviceplugin/partitions.py): none | single | mixed
+    partition_strategy: str = "single"
+    partition_memory: str = "split"       # split: NPS domain memory / partitions sharing it | reported
     # How a fractional vGPU's compute share is enforced (vgpu/deviceplugin/custate.py):
     #   temporal  (default) no per-container mask: the shim's GPU-time limiter with
     #             work-conserving fair-share charging — the reference's time-sliced SM

@@ -87,21 +87,36 @@ class AMDDevices(Devices):
                         break
         return v
 
+    def count_resources(self) -> list[str]:
+        """amd.com/gpu plus the compute-partition resources of a node running the
+        mixed partition strategy (vgpu/deviceplugin/partitions.py)."""
+        return [self.resource_count] + [f"{self.resource_count}-{m}" for m in R.PARTITION_SUFFIXES]
+
+    def _count(self, ctr: dict) -> tuple[str, object]:
+        for name in self.count_resources():
+            v = self._get(ctr, name)
+            if v is not None:
+                return name, v
+        return self.resource_count, None
+
     def mutate_admission(self, ctr: dict) -> bool:
         lim = (ctr.get("resources") or {}).get("limits") or {}
         prio = lim.get(self.resource_priority)
         if prio is not None:
             env = ctr.setdefault("env", [])
             env.append({"name": ENV_PRIORITY, "value": str(parse_quantity(prio))})
-        return self._get(ctr, self.resource_count) is not None
+        return self._count(ctr)[1] is not None
 
     def check_type(self, annos: dict, dev: DeviceUsage, req: ContainerDeviceRequest):
         if req.type == self.vendor:
-            return True, check_gpu_type(annos, dev.type), assert_numa(annos)
+            # the count resource must be the one the device is advertised under
+            # (a amd.com/gpu-cpx request only fits CPX partitions of a mixed node)
+            ok = check_gpu_type(annos, dev.type) and dev.resource == req.resource
+            return True, ok, assert_numa(annos)
         return False, False, False
 
     def generate_resource_requests(self, ctr: dict) -> ContainerDeviceRequest:
-        v = self._get(ctr, self.resource_count)
+        res, v = self._count(ctr)
         n = parse_quantity(v)
         if v is None or n is None:
             return ContainerDeviceRequest(nums=0)
@@ -116,4 +131,4 @@ class AMDDevices(Devices):
         cores = parse_quantity(self._get(ctr, self.resource_cores))
         corenum = config.SCHEDULER.default_cores if cores is None else cores
         return ContainerDeviceRequest(nums=int(n), type=self.vendor, memreq=int(memnum),
-                                      mem_percentage=int(mempct), coresreq=int(corenum))
+                                      mem_percentage=int(mempct), coresreq=int(corenum), resource=res)

@@ -75,24 +75,28 @@ def main(argv=None) -> int:
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *_: stop.set())
 
-    plugin = None
+    plugins: list[VGPUDevicePlugin] = []
     registrar = None
+    crashes = CrashBudget()
     kubelet_sock = os.path.join(cfg.socket_dir, "kubelet.sock")
     while not stop.is_set():
-        if plugin is None:
+        if not plugins:
             try:
-                plugin = VGPUDevicePlugin(cfg, backend, client, cfg.node_name)
-                plugin.start()
-                registrar = Registrar(client, cfg.node_name, lambda: plugin.devices, cfg,
-                                      get_health=lambda: dict(plugin.health))
+                plugins = build_plugins(cfg, backend, client)
+                for p in plugins:
+                    p.start()
+                registrar = Registrar(client, cfg.node_name, lambda: [d for p in plugins for d in p.devices], cfg,
+                                      get_health=lambda: {u: h for p in plugins for u, h in p.health.items()})
                 registrar.start()
                 sock_id = socket_id(kubelet_sock)
             except Exception as e:
                 log.error("could not start plugin: %s; retrying in 30s", e)
-                if plugin is not None and not plugin.note_crash():
+                for p in plugins:
+                    p.stop()
+                plugins = []
+                if not crashes.note():
                     log.critical("crash budget exhausted")
                     return 1
-                plugin = None
                 stop.wait(30.0)
                 continue
         stop.wait(1.0)
@@ -101,12 +105,45 @@ def main(argv=None) -> int:
             log.info("kubelet restarted or SIGHUP: restarting plugin")
             restart.clear()
             registrar.stop()
-            plugin.stop()
-            plugin = None
-    if plugin is not None:
+            for p in plugins:
+                p.stop()
+            plugins = []
+    if plugins:
         registrar.stop()
-        plugin.stop()
+        for p in plugins:
+            p.stop()
     return 0
+
+
+class CrashBudget:
+    """More than MAX_RESTARTS_PER_HOUR failed starts within an hour is fatal
+    (reference plugin/server.go:171-199)."""
+
+    def __init__(self):
+        self._t: list[float] = []
+
+    def note(self) -> bool:
+        from .server import MAX_RESTARTS_PER_HOUR
+        now = time.time()
+        self._t = [t for t in self._t if now - t < 3600] + [now]
+        return len(self._t) <= MAX_RESTARTS_PER_HOUR
+
+
+def build_plugins(cfg: DevicePluginConfig, backend, client) -> list[VGPUDevicePlugin]:
+    """One device-plugin server per extended resource of the node's partition
+    strategy (vgpu/deviceplugin/partitions.py): amd.com/gpu, and with `mixed`
+    amd.com/gpu-dpx / -qpx / -cpx, each on its own socket."""
+    from .partitions import plan, socket_name
+    groups, bad = plan(backend.devices(), cfg.partition_strategy, cfg.resource_name, cfg.partition_memory)
+    out = []
+    for res, devs in sorted(groups.items()):
+        if not devs:
+            continue
+        out.append(VGPUDevicePlugin(cfg, backend, client, cfg.node_name, socket_name=socket_name(res, cfg.resource_name),
+                                    devices=devs, resource_name=res, unhealthy=bad))
+    if not out:
+        raise RuntimeError(f"no device to advertise under partition strategy {cfg.partition_strategy}")
+    return out
 
 
 if __name__ == "__main__":

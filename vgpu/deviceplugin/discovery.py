@@ -27,7 +27,7 @@ class _SmiDevice(ctypes.Structure):
                 ("numa_node", ctypes.c_int32), ("render_minor", ctypes.c_uint32), ("card", ctypes.c_uint32),
                 ("kfd_gpu_id", ctypes.c_uint32), ("index", ctypes.c_uint32), ("health", ctypes.c_uint32),
                 ("gfx_activity", ctypes.c_uint32), ("umc_activity", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32 * 7)]
+                ("partition_id", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 6)]
 
 
 class _SmiProc(ctypes.Structure):
@@ -91,6 +91,9 @@ class Device:
     gfx_activity: int = 0
     umc_activity: int = 0
     vendor_id: int = 0x1002
+    partition_id: int = 0          # compute partition of its physical GPU (0 in SPX)
+    resource: str = "amd.com/gpu"  # extended resource it is advertised under (partitions.py)
+    memory_shared_by: int = 1      # partitions sharing its NPS memory domain (partitions.py)
 
     @property
     def model(self) -> str:
@@ -114,6 +117,15 @@ class Proc:
     vram_bytes: int
     cu_occupancy: int = 0
     gfx_ns: int = 0
+
+
+# XCDs per compute partition of an 8-XCD part (MI355X / MI300X), for backends
+# that report the partition but not its XCD count (amdsmi).
+XCC_PER_PARTITION = {"SPX": 8, "DPX": 4, "QPX": 2, "CPX": 1}
+
+
+def xcc_of_partition(mode: str) -> int:
+    return XCC_PER_PARTITION.get((mode or "SPX").upper(), 8)
 
 
 class Backend:
@@ -165,11 +177,12 @@ class SmiBackend(Backend):
             out.append(Device(
                 uuid=d.uuid.decode() or f"GPU-{i}", index=i, bdf=d.bdf.decode(), name=d.name.decode(),
                 vram_total=d.vram_total, vram_used=d.vram_used, cus=d.cus or 256,
-                num_xcc=d.num_xcc or 8, numa=max(d.numa_node, 0), render_minor=d.render_minor,
+                num_xcc=d.num_xcc or xcc_of_partition(d.compute_partition.decode()), numa=max(d.numa_node, 0), render_minor=d.render_minor,
                 card=d.card, kfd_gpu_id=d.kfd_gpu_id, xgmi_hive=d.xgmi_hive,
                 compute_partition=d.compute_partition.decode() or "SPX",
                 memory_partition=d.memory_partition.decode() or "NPS1", health=bool(d.health),
-                gfx_activity=d.gfx_activity, umc_activity=d.umc_activity, vendor_id=d.vendor_id))
+                gfx_activity=d.gfx_activity, umc_activity=d.umc_activity, vendor_id=d.vendor_id,
+                partition_id=d.partition_id))
         return out
 
     def link(self, a: int, b: int) -> tuple[int, int]:

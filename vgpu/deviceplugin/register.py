@@ -36,7 +36,8 @@ def api_devices(devs: list[Device], cfg: DevicePluginConfig, health: dict[str, b
                               devmem=int((d.vram_total >> 20) * cfg.device_memory_scaling),
                               devcore=int(100 * cfg.device_cores_scaling), type=d.type,
                               numa=d.numa, health=ok, cus=d.cus,
-                              xgmi_hive=f"{d.xgmi_hive:x}" if d.xgmi_hive else "", index=d.index))
+                              xgmi_hive=f"{d.xgmi_hive:x}" if d.xgmi_hive else "", index=d.index,
+                              resource=d.resource))
     return out
 
 

@@ -52,16 +52,25 @@ def physical_of(fake_id: str) -> str:
 
 class VGPUDevicePlugin:
     def __init__(self, cfg: DevicePluginConfig, backend: Backend, client: KubeClient, node: str,
-                 socket_name: str = "amd-vgpu.sock"):
+                 socket_name: str = "amd-vgpu.sock", devices: list[Device] | None = None,
+                 resource_name: str | None = None, unhealthy: dict[str, str] | None = None):
+        """`devices` / `resource_name`: the subset this server advertises and its
+        extended resource (partition strategies, partitions.py); by default every
+        device the backend finds, under cfg.resource_name."""
         self.cfg = cfg
         self.backend = backend
         self.client = client
         self.node = node
         self.socket_path = os.path.join(cfg.socket_dir, socket_name)
-        self.devices = backend.devices()
+        self.resource_name = resource_name or cfg.resource_name
+        self.devices = backend.devices() if devices is None else devices
         self.by_uuid = {d.uuid: d for d in self.devices}
+        self.policy_unhealthy = dict(unhealthy or {})
         self.health: dict[str, bool] = {d.uuid: d.health and not self._partition_mismatch(d)
-                                        for d in self.devices}
+                                        and d.uuid not in self.policy_unhealthy for d in self.devices}
+        for u, why in self.policy_unhealthy.items():
+            if u in self.by_uuid:
+                log.warning("device %s advertised unhealthy: %s", u, why)
         for d in self.devices:
             if self._partition_mismatch(d):
                 log.warning("device %s is in compute partition %s, expected %s: advertised unhealthy",
@@ -229,7 +238,7 @@ class VGPUDevicePlugin:
             stub = api.Stub(ch, "Registration")
             stub.Register(api.RegisterRequest(
                 version=api.VERSION, endpoint=os.path.basename(self.socket_path),
-                resource_name=self.cfg.resource_name,
+                resource_name=self.resource_name,
                 options=api.DevicePluginOptions(get_preferred_allocation_available=True)), timeout=5)
 
     def start(self) -> None:
@@ -238,7 +247,7 @@ class VGPUDevicePlugin:
         self.serve()
         self.register()
         threading.Thread(target=self._health_loop, daemon=True, name="vgpu-health").start()
-        log.info("device plugin serving %d devices x %d vGPUs on %s", len(self.devices),
+        log.info("device plugin serving %s: %d devices x %d vGPUs on %s", self.resource_name, len(self.devices),
                  self.cfg.device_split_count, self.socket_path)
 
     def stop(self) -> None:
@@ -271,15 +280,16 @@ class VGPUDevicePlugin:
         * the device list itself: a vanished device → unhealthy."""
         if os.environ.get("DP_DISABLE_HEALTHCHECKS", "").lower() in ("all", "true", "1"):
             return
+        by_index = {d.index: d for d in self.devices}  # backend index -> our device (a subset per resource)
         for dev, typ, msg in self.backend.events(timeout_ms):
-            if dev < 0 or dev >= len(self.devices):
+            if dev not in by_index:
                 continue
-            uuid = self.devices[dev].uuid
+            uuid = by_index[dev].uuid
             if typ == EVT_PRE_RESET:
                 self.set_health(uuid, False, f"GPU reset: {msg}")
             elif typ == EVT_POST_RESET:
                 self._ecc_baseline.pop(uuid, None)  # counters restart with the device
-                if not self._partition_mismatch(self.devices[dev]):
+                if not self._partition_mismatch(by_index[dev]) and uuid not in self.policy_unhealthy:
                     self.set_health(uuid, True, f"GPU reset done: {msg}")
             elif typ == EVT_VMFAULT:
                 self.vm_faults[uuid] = self.vm_faults.get(uuid, 0) + 1
@@ -301,6 +311,8 @@ class VGPUDevicePlugin:
                 self.set_health(d.uuid, False, "device disappeared")
             elif not present[d.uuid].health:
                 self.set_health(d.uuid, False, "driver reports unhealthy")
+            elif d.uuid in self.policy_unhealthy:
+                continue
             elif self.cfg.partition_mode:
                 pd = present[d.uuid]
                 was_bad, d.compute_partition = self._partition_mismatch(d), pd.compute_partition

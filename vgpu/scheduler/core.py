@@ -246,10 +246,10 @@ class Scheduler:
                         if m is None:
                             info.devices.append(d)
                             continue
-                        attrs = (d.devmem, d.devcore, d.count, d.health, d.cus, d.xgmi_hive)
-                        if attrs == (m.devmem, m.devcore, m.count, m.health, m.cus, m.xgmi_hive):
+                        attrs = (d.devmem, d.devcore, d.count, d.health, d.cus, d.xgmi_hive, d.resource)
+                        if attrs == (m.devmem, m.devcore, m.count, m.health, m.cus, m.xgmi_hive, m.resource):
                             continue  # unchanged: nothing to invalidate
-                        m.devmem, m.devcore, m.count, m.health, m.cus, m.xgmi_hive = attrs
+                        m.devmem, m.devcore, m.count, m.health, m.cus, m.xgmi_hive, m.resource = attrs
                         if self._flat is not None and not self._flat.update_device(name, m):
                             self._structure_changed()
                 if info.devices:
@@ -309,7 +309,8 @@ class Scheduler:
                 overall[nid] = NodeUsage(devices=[
                     DeviceUsage(id=d.id, index=d.index, used=0, count=d.count, usedmem=0,
                                 totalmem=d.devmem, usedcores=0, totalcore=d.devcore, type=d.type,
-                                numa=d.numa, health=d.health, cus=d.cus, xgmi_hive=d.xgmi_hive)
+                                numa=d.numa, health=d.health, cus=d.cus, xgmi_hive=d.xgmi_hive,
+                                resource=d.resource)
                     for d in n.devices])
             for p in self.pods.values():
                 node = overall.get(p.node_id)

@@ -76,7 +76,8 @@ class FlatState:
         self.node_rank[np.asarray(ranks, dtype=np.int64)] = np.arange(len(ranks), dtype=np.int32)
         devs = [(n, d) for n in self.node_names for d in nodes[n].devices]
         self.dev_ids = [d.id for _, d in devs]
-        self.dev_types = [d.type for _, d in devs]
+        # a device "type" for eligibility is (type string, advertised resource)
+        self.dev_types = [(d.type, d.resource) for _, d in devs]
         self.types = sorted(set(self.dev_types))
         self.type_id = {t: i for i, t in enumerate(self.types)}
         self.hives: dict[str, int] = {}
@@ -89,7 +90,7 @@ class FlatState:
             self.arr["totalcore"] = [d.devcore for _, d in devs]
             self.arr["numa"] = [d.numa for _, d in devs]
             self.arr["health"] = [1 if d.health else 0 for _, d in devs]
-            self.arr["type_id"] = [self.type_id[d.type] for _, d in devs]
+            self.arr["type_id"] = [self.type_id[(d.type, d.resource)] for _, d in devs]
             self.arr["hive"] = [self._hive(d.xgmi_hive) for _, d in devs]
         self.dev_index: dict[tuple[str, str], int] = {(n, d.id): i for i, (n, d) in enumerate(devs)}
         counts = [len(nodes[n].devices) for n in self.node_names]
@@ -123,13 +124,14 @@ class FlatState:
         """Attribute change of a registered device, in place.  False when the
         change needs a rebuild (unknown device or a device type not in the table)."""
         i = self.dev_index.get((node_id, d.id))
-        if i is None or d.type not in self.type_id:
+        key = (d.type, d.resource)
+        if i is None or key not in self.type_id:
             return False
         r = self.arr[i]
         r["count"], r["totalmem"], r["totalcore"] = d.count, d.devmem, d.devcore
         r["numa"], r["health"], r["hive"] = d.numa, 1 if d.health else 0, self._hive(d.xgmi_hive)
-        r["type_id"] = self.type_id[d.type]
-        self.dev_types[i] = d.type
+        r["type_id"] = self.type_id[key]
+        self.dev_types[i] = key
         return True
 
     def apply(self, node_id: str, devices: list[list[ContainerDevice]], sign: int) -> None:
@@ -165,9 +167,9 @@ class FlatState:
         numa_bind = False
         for j, (c, k) in enumerate(reqs):
             rq[j] = (k.nums, k.mem_percentage, k.memreq, k.coresreq, c)
-            for t, tname in enumerate(self.types):
+            for t, (tname, tres) in enumerate(self.types):
                 stub = DeviceUsage(id="", index=0, used=0, count=0, usedmem=0, totalmem=0, usedcores=0,
-                                   totalcore=0, type=tname, numa=0, health=True)
+                                   totalcore=0, type=tname, numa=0, health=True, resource=tres)
                 ok, numa = check_type(annos, stub, k)
                 elig[j, t] = 1 if ok else 0
                 numa_bind |= bool(ok and numa)
