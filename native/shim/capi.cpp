@@ -96,6 +96,25 @@ __attribute__((visibility("default"))) int vgpu_region_set_cu_mask(void* rp, int
   return 0;
 }
 
+// Node monitor: record a host pid it resolved for `slot` (src = VGPU_HOSTPID_MONITOR).
+// Only a slot that still holds container pid `pid` and is unverified is
+// changed, so a slot reused meanwhile is left alone.  Returns 1 if written.
+__attribute__((visibility("default"))) int vgpu_region_set_host_pid(void* rp, int slot, int pid, int host_pid,
+                                                                    int src) {
+  auto* r = (vgpu_shared_region_t*)rp;
+  if (slot < 0 || slot >= VGPU_MAX_PROCS || host_pid <= 0) return -1;
+  if (region_lock(r) != 0) return -1;
+  vgpu_proc_slot_t& s = r->procs[slot];
+  int done = 0;
+  if (s.status != VGPU_PROC_FREE && s.pid == pid && s.host_pid_src == VGPU_HOSTPID_UNVERIFIED) {
+    s.host_pid = host_pid;
+    s.host_pid_src = src;
+    done = 1;
+  }
+  region_unlock(r);
+  return done;
+}
+
 // Signal every live process of the region (suspend_all / resume_all analogue).
 __attribute__((visibility("default"))) int vgpu_region_signal_all(void* rp, int sig, int host_ns) {
   auto* r = (vgpu_shared_region_t*)rp;

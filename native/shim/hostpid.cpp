@@ -13,12 +13,14 @@
 // brackets exactly that one call: flock(unified lock) → list KFD entries →
 // real open → list again → unlock.  The bracket is microseconds wide, so the
 // diff has one entry unless a process outside our lock opened /dev/kfd in the
-// same instant; an ambiguous diff is left to the node monitor
-// (vgpu/monitor/pids.py).  flock is released by the kernel when its holder
+// same instant; an ambiguous diff is left to the node monitor, which matches
+// NSpid + the pod's cgroup (vgpu/monitor/pids.py).  flock is released by the kernel when its holder
 // dies, so the reference's "unified_lock expired, removing" path is not needed.
 //
-// The resolved pid is what makes the temporal limiter's KFD cu_occupancy
-// sampling (limiter.cpp) and the monitor's pid-based work possible in a pod.
+// The resolved pid is what the share board (board.cpp) records per slot and
+// what the node monitor's host-side work needs in a pod: purging dead slots,
+// suspend/resume signals and process metrics.  (The temporal limiter charges
+// the GPU time of its own marker intervals and needs no pid, limiter.cpp.)
 #include <dirent.h>
 #include <dlfcn.h>
 #include <errno.h>

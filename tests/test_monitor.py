@@ -193,3 +193,53 @@ def test_host_telemetry_metrics():
     assert 'HostGPUECCErrors_total{deviceidx="0",deviceuuid="GPU-1111-00",type="uncorrectable"} 1.0' in text
     assert 'HostXGMIReadBytes_total{deviceidx="0",deviceuuid="GPU-1111-00"} 1.073741824e+09' in text
     assert 'GPU-1111-01"} 1050' not in text  # device 1 reports no telemetry
+
+
+def test_monitor_resolves_ambiguous_host_pids_then_purges(native_build, tmp_path, monkeypatch):
+    """slots the shim left unverified (ambiguous KFD diff)
+    get their host pid from the monitor (NSpid + the pod's cgroup, the closest
+    start before the slot's claim when a container pid repeats across the
+    pod's containers), src = MONITOR; the host-side purge then frees a slot
+    once its process is gone (reference feedback.go:83-162 setHostPid)."""
+    import subprocess
+    import time
+    from vgpu.monitor import pids
+    from vgpu.monitor.region import HOSTPID_MONITOR, HOSTPID_UNVERIFIED
+    r = make_region(tmp_path / "c" / "vgpu.cache", monkeypatch)
+    lib = r.lib
+    s7 = lib.vgpu_region_claim(r.ptr, 7, 7, 1)   # container pids, unverified
+    s9 = lib.vgpu_region_claim(r.ptr, 9, 9, 1)
+    assert r.r.procs[s7].host_pid_src == HOSTPID_UNVERIFIED
+    claim_ns = r.r.procs[s7].start_ns
+    live = [subprocess.Popen(["sleep", "60"]) for _ in range(2)]
+    a, b = live[0].pid, live[1].pid  # real host pids of the pod's two processes
+    uid = "1a2b3c4d-0000-1111-2222-333344445555"
+    proc = tmp_path / "proc"
+    tick = 1_000_000_000 // pids.CLK_TCK
+
+    def fake(pid, nspid, cgroup, start_ns):
+        d = proc / str(pid)
+        d.mkdir(parents=True)
+        (d / "status").write_text(f"Name:\tpython\nNSpid:\t{pid}\t{nspid}\n")
+        (d / "cgroup").write_text(f"0::/kubepods.slice/kubepods-burstable-{cgroup}.slice/cri-containerd-x.scope\n")
+        fields = ["S"] + ["0"] * 18 + [str(start_ns // tick)] + ["0"] * 10
+        (d / "stat").write_text(f"{pid} (python) " + " ".join(fields) + "\n")
+
+    pod = "pod" + uid.replace("-", "_")  # systemd cgroup driver form
+    fake(a, 7, pod, claim_ns - 2_000_000_000)        # container pid 7, started before the claim
+    fake(99991, 7, pod, claim_ns + 5_000_000_000)    # pid 7 of another container of the pod, started later
+    fake(b, 9, pod, claim_ns - 1_000_000_000)
+    fake(99992, 9, "podffffffff_0000", claim_ns)      # pid 9 of some other pod
+    assert pids.resolve_region(r, uid, str(proc)) == 2
+    assert (r.r.procs[s7].host_pid, r.r.procs[s7].host_pid_src) == (a, HOSTPID_MONITOR)
+    assert (r.r.procs[s9].host_pid, r.r.procs[s9].host_pid_src) == (b, HOSTPID_MONITOR)
+    assert pids.resolve_region(r, uid, str(proc)) == 0  # nothing left to resolve
+    assert r.purge(host_ns=True) == 0  # both alive
+    live[0].kill()
+    live[0].wait()
+    time.sleep(0.05)
+    assert r.purge(host_ns=True) == 1
+    assert r.r.procs[s7].status == 0 and r.r.procs[s9].status != 0
+    live[1].kill()
+    live[1].wait()
+    r.close()

@@ -22,6 +22,7 @@ from prometheus_client import REGISTRY, start_http_server
 from .feedback import observe
 from .metrics import MonitorCollector
 from .pathmonitor import PathMonitor
+from .pids import resolve_and_purge
 
 log = logging.getLogger("vgpu.monitor")
 
@@ -86,6 +87,7 @@ def main(argv=None) -> int:
     while not stop.wait(ns.interval):
         try:
             pm.scan()
+            resolve_and_purge(pm.regions)  # host pids the shim could not verify; dead slots freed
             observe({k: cr.region for k, cr in pm.regions.items()})
         except Exception as e:
             log.error("monitor pass failed: %s", e)

@@ -154,6 +154,11 @@ class AttachedRegion:
         words = (ctypes.c_uint64 * CU_WORDS)(*[(mask >> (64 * w)) & ((1 << 64) - 1) for w in range(CU_WORDS)])
         self.lib.vgpu_region_set_cu_mask(self.ptr, dev, words)
 
+    def set_host_pid(self, slot: int, pid: int, host_pid: int, src: int = HOSTPID_MONITOR) -> bool:
+        """Record a host pid the monitor resolved (only for a slot that still
+        holds container pid `pid` and is unverified)."""
+        return self.lib.vgpu_region_set_host_pid(self.ptr, slot, pid, host_pid, src) == 1
+
     def purge(self, host_ns: bool = True) -> int:
         return self.lib.vgpu_region_purge(self.ptr, 1 if host_ns else 0)
 

@@ -124,6 +124,7 @@ def load_capi() -> ctypes.CDLL:
     lib.vgpu_region_decay_recent.argtypes = [vp]
     lib.vgpu_region_set_cu_mask.argtypes = [vp, ci, ctypes.POINTER(ctypes.c_uint64)]
     lib.vgpu_region_signal_all.argtypes = [vp, ci, ci]
+    lib.vgpu_region_set_host_pid.argtypes = [vp, ci, ci, ci, ci]
     lib.vgpu_parse_mem.argtypes = [ctypes.c_char_p]
     lib.vgpu_parse_mem.restype = cu64
     lib.vgpu_parse_cu_mask.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64), ci]
