@@ -19,6 +19,13 @@ its last step).  The rank measures the wall time from GO to the last DONE;
 the job's ms_per_step is the MAX over ranks, and `value` is total images over
 all pods on all GPUs divided by that wall time (weak scaling: per-GPU work is
 fixed as N grows).
+
+The ranks coordinate over gloo (they never touch a GPU).  Before GO a
+preflight checks the placement: N distinct devices, one share board (device
+uuid) per GPU, one shared region per pod.  With N > 1, after the timed window
+pod 0 of every GPU joins one RCCL process group and all-reduces 64 MiB
+(`rccl_check` in the JSON): the multi-GPU data plane -- xGMI peer access, IPC
+buffers, RCCL kernels exempt from the limiter -- exercised under the shim.
 """
 from __future__ import annotations
 
@@ -89,6 +96,65 @@ def make_parser() -> argparse.ArgumentParser:
     return ap
 
 
+def preflight(placement: list[dict], world: int, shim: bool = True) -> bool:
+    """Multi-GPU placement checks before the timed window:
+    one rank per distinct device, one share board (device uuid) per GPU, one
+    shared region per pod.  A failure aborts the run rather than measuring a
+    misplaced one.  An explicit VGPU_BENCH_DEVICES map may put several ranks
+    on one GPU (a rehearsal on a 1-GPU box); returns False then."""
+    devices = [p["device"] for p in placement]
+    if len(set(devices)) != world:
+        if not os.environ.get("VGPU_BENCH_DEVICES"):
+            raise RuntimeError(f"preflight: {world} ranks on devices {devices}: need {world} distinct devices")
+        log(f"preflight: rehearsal, ranks share devices {devices} (VGPU_BENCH_DEVICES)")
+        return False
+    if not shim:
+        return True
+    boards = {}
+    for p in placement:
+        for u in set(p["uuids"]):
+            boards.setdefault(u, set()).add(p["device"])
+    shared = {u: sorted(d) for u, d in boards.items() if len(d) > 1 or not u}
+    if shared:
+        raise RuntimeError(f"preflight: share-board keys used by several GPUs: {shared}")
+    regions = [r for p in placement for r in p["regions"]]
+    if len(set(regions)) != len(regions) or not all(regions):
+        raise RuntimeError(f"preflight: shared regions not one per pod: {regions}")
+    return True
+
+
+def rccl_check(pg, rank: int, world: int, pod, log) -> dict | None:
+    """After the timed window: pod 0 of every GPU all-reduces over RCCL under
+    the shim (vgpu/bench/pod.py rccl_check).  Never fatal."""
+    import socket
+    port = None
+    if rank == 0:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+    box = [port]
+    pg.broadcast_object_list(box, src=0)
+    addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    try:
+        pod.send(f"RCCL {rank} {world} {addr} {box[0]}")
+        res = pod.read_tagged("RCCL", 240.0, progress=log)
+    except Exception as e:
+        res = {"rank": rank, "error": f"{type(e).__name__}: {e}"[:300]}
+    gathered = [None] * world
+    pg.all_gather_object(gathered, res)
+    ok = all(r.get("sum_ok") for r in gathered)
+    bw = [r.get("busbw_GBps") for r in gathered if r.get("busbw_GBps") is not None]
+    out = {"ok": ok, "world": world, "backend": gathered[0].get("backend"),
+           "busbw_GBps_min": min(bw) if bw else None, "ms_per_allreduce_64MiB":
+               max((r.get("ms_per_allreduce") or 0) for r in gathered)}
+    errs = [r["error"] for r in gathered if r.get("error")]
+    if errs:
+        out["errors"] = errs[:2]
+    log(f"rccl check: {out}")
+    return out
+
+
 def main(argv=None) -> int:
     args = make_parser().parse_args(argv)
     if args.cpu_smoke:
@@ -135,6 +201,14 @@ def main(argv=None) -> int:
         for p in pods:
             p.ready = p.read_tagged("READY", args.ready_timeout, progress=log)
             log(f"pod {p.idx} ready: {json.dumps(p.ready)}")
+        placement = [{"rank": rank, "local_rank": local_rank, "device": device,
+                      "uuids": [p.env.get("VGPU_DEVICE_UUID_0", "") for p in pods],
+                      "regions": [p.region for p in pods], "shares": [p.share for p in pods]}]
+        if pg:
+            gathered = [None] * world
+            pg.all_gather_object(gathered, placement[0])
+            placement = gathered
+        distinct = preflight(placement, world, shim=not args.no_shim)
         if pg:
             pg.barrier()
         for p in pods:
@@ -146,6 +220,16 @@ def main(argv=None) -> int:
         t_end = max(p.done["t1"] for p in pods)
         t_start = min(p.done["t0"] for p in pods)
         wall = t_end - t_start
+        rccl = None
+        if pg and pods and distinct:
+            rccl = rccl_check(pg, rank, world, pods[0], log)
+        elif pg:
+            rccl = {"skipped": "ranks share a GPU (rehearsal): RCCL runs one rank per GPU"}
+        for p in pods:
+            try:
+                p.send("EXIT")
+            except (BrokenPipeError, OSError):
+                pass
         for p in pods:
             p.proc.wait(timeout=120)
     finally:
@@ -153,15 +237,6 @@ def main(argv=None) -> int:
             if p.proc.poll() is None:
                 p.proc.kill()
 
-    # Where every rank's pods ran (device, vGPU uuid, shared region): gathered
-    # to rank 0 so a multi-GPU run shows its placement and region isolation.
-    placement = [{"rank": rank, "local_rank": local_rank, "device": device,
-                  "uuids": [p.env.get("VGPU_DEVICE_UUID_0", "") for p in pods],
-                  "regions": [p.region for p in pods], "shares": [p.share for p in pods]}]
-    if pg:
-        gathered = [None] * world
-        pg.all_gather_object(gathered, placement[0])
-        placement = gathered
     samples = sum(p.done["samples"] for p in pods)
     ms_step = 1e3 * wall / args.steps
     cap = []
@@ -225,6 +300,7 @@ def main(argv=None) -> int:
             "per_pod_share": [p.share for p in pods],
             "vram_cap": cap,
             "placement": placement,
+            "rccl_check": rccl,
         }
         print(json.dumps(res), flush=True)
     if pg:

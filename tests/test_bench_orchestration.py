@@ -44,6 +44,8 @@ def test_bench_two_ranks_gloo_cpu():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 50 * 2 * 2
     assert d["scaling"] == "weak" and d["ms_per_step"] > 0
+    # post-timing cross-GPU all-reduce among one pod per GPU (gloo in this rehearsal, RCCL on GPUs)
+    assert d["rccl_check"]["ok"] is True and d["rccl_check"]["world"] == 2, d["rccl_check"]
 
 
 def test_bench_eight_ranks_gloo_cpu_placement():
@@ -68,6 +70,25 @@ def test_bench_eight_ranks_gloo_cpu_placement():
     assert [x["uuids"] for x in pl] == [[f"GPU-bench-{i}"] for i in range(8)]
     regions = [reg for x in pl for reg in x["regions"]]
     assert len(set(regions)) == 8 and all(regions)
+    assert d["rccl_check"]["ok"] is True and d["rccl_check"]["world"] == 8, d["rccl_check"]
+
+
+def test_bench_preflight_refuses_a_misplaced_run():
+    """Two ranks on one device (without an explicit rehearsal map), or two GPUs
+    sharing a share-board key, or two pods sharing a region: refused before GO."""
+    import bench
+    ok = [{"rank": r, "device": str(r), "uuids": [f"GPU-{r}"] * 2, "regions": [f"/r{r}a", f"/r{r}b"]}
+          for r in range(2)]
+    assert bench.preflight(ok, 2) is True
+    same_dev = [dict(ok[0]), dict(ok[1], device="0")]
+    with pytest.raises(RuntimeError, match="distinct devices"):
+        bench.preflight(same_dev, 2)
+    same_board = [dict(ok[0]), dict(ok[1], uuids=["GPU-0"])]
+    with pytest.raises(RuntimeError, match="share-board"):
+        bench.preflight(same_board, 2)
+    same_region = [dict(ok[0]), dict(ok[1], regions=["/r0a"])]
+    with pytest.raises(RuntimeError, match="regions"):
+        bench.preflight(same_region, 2)
 
 
 def test_ab_recipes_and_suite_scenarios_are_valid_bench_flags():

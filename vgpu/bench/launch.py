@@ -146,7 +146,11 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
             mask_bits = bin(mask).count("1")
         if sp.priority is not None:
             cenv.setdefault("VGPU_TASK_PRIORITY", str(sp.priority))
-        env = dict(os.environ)
+        # A pod is its own program, not a torchrun worker: drop the launcher's
+        # rendezvous variables (TORCHELASTIC_USE_AGENT_STORE would make a pod's
+        # own process group wait on the agent's store).
+        env = {k: v for k, v in os.environ.items()
+               if not k.startswith(("TORCHELASTIC_", "TORCH_ELASTIC_")) and k not in TORCHRUN_VARS}
         env["HIP_VISIBLE_DEVICES"] = device
         env.pop("CUDA_VISIBLE_DEVICES", None)
         env["PYTHONPATH"] = str(REPO) + os.pathsep + env.get("PYTHONPATH", "")
@@ -179,6 +183,8 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
 
 
 ENV_PLACEHOLDER = "__VGPU_UNUSED_VISIBLE__"
+TORCHRUN_VARS = {"RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                 "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT"}
 
 
 def shim_available() -> bool:

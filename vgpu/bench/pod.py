@@ -5,6 +5,9 @@ Protocol (one JSON object per line on stdout, prefixed):
     READY {...}   after the untimed warmup and a device synchronize
     <- "GO"       read from stdin
     DONE {...}    after exactly `steps` steps and a device synchronize
+    <- "RCCL <rank> <world> <addr> <port>"   (optional, multi-GPU runs)
+    RCCL {...}    cross-GPU all-reduce among one pod per GPU, under the shim
+    <- "EXIT"
 Optional post-timing probe (--cap-probe): allocate 1 GiB blocks until the
 vGPU cap refuses, report how close to the cap that got (VRAM-cap accuracy).
 
@@ -249,7 +252,57 @@ def main(argv=None) -> int:
     if args.cap_probe and not cpu:
         res.update(cap_probe())
     emit("DONE", res)
+    if args.no_wait:
+        return 0
+    for line in sys.stdin:  # post-timing commands from the launcher
+        cmd = line.split()
+        if cmd and cmd[0] == "RCCL" and len(cmd) == 5:
+            emit("RCCL", rccl_check(int(cmd[1]), int(cmd[2]), cmd[3], int(cmd[4]), cpu))
+        else:
+            break
     return 0
+
+
+def rccl_check(rank: int, world: int, addr: str, port: int, cpu: bool, mib: int = 64, iters: int = 10) -> dict:
+    """The multi-GPU data plane under the enforcement library: one pod per GPU
+    forms a process group over RCCL (xGMI peer access and IPC buffers pass
+    through the shim; RCCL kernels are exempt from its limiter) and
+    all-reduces a `mib` MiB buffer.  Checks the sum and reports bus bandwidth.
+    Not part of the timed window."""
+    import datetime
+
+    import torch
+    import torch.distributed as dist
+    out = {"rank": rank, "world": world, "backend": "gloo" if cpu else "nccl"}
+    t0 = time.time()
+    try:
+        dev = torch.device("cpu") if cpu else torch.device("cuda", 0)
+        kw = {} if cpu else {"device_id": dev}
+        dist.init_process_group(out["backend"], init_method=f"tcp://{addr}:{port}", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=120), **kw)
+        out["init_s"] = round(time.time() - t0, 2)
+        n = (mib << 20) // 4
+        y = torch.full((n,), float(rank + 1), device=dev)
+        dist.all_reduce(y)
+        want = world * (world + 1) / 2
+        out["sum_ok"] = bool(torch.all(y == want).item())
+        x = torch.ones(n, device=dev)
+        for _ in range(3):
+            dist.all_reduce(x)
+        if not cpu:
+            torch.cuda.synchronize()
+        t1 = time.time()
+        for _ in range(iters):
+            dist.all_reduce(x)
+        if not cpu:
+            torch.cuda.synchronize()
+        dt = (time.time() - t1) / iters
+        out["ms_per_allreduce"] = round(1e3 * dt, 3)
+        out["busbw_GBps"] = round(2 * (world - 1) / world * n * 4 / dt / 1e9, 1)
+        dist.destroy_process_group()
+    except Exception as e:  # reported, never fatal for the benchmark
+        out["error"] = f"{type(e).__name__}: {e}"[:500]
+    return out
 
 
 if __name__ == "__main__":
