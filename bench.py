@@ -68,6 +68,8 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--workload", default="1.1", help="ai-benchmark test id (vgpu.models.WORKLOADS)")
     ap.add_argument("--gpumem", type=int, default=144000, help="per-pod amd.com/gpumem (MiB)")
     ap.add_argument("--gpucores", type=int, default=50, help="per-pod amd.com/gpucores (%%)")
+    ap.add_argument("--pod-cores", default="",
+                    help="comma list of per-pod amd.com/gpucores overriding --gpucores (e.g. 25,75)")
     ap.add_argument("--no-shim", action="store_true", help="run pods without enforcement")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-find", action="store_true",
@@ -188,8 +190,11 @@ def main(argv=None) -> int:
     from vgpu.config import DevicePluginConfig
     pool_conc = DevicePluginConfig().pool_concurrency if args.pool_concurrency is None else args.pool_concurrency
     pol_env = {} if args.core_policy == "default" else {"GPU_CORE_UTILIZATION_POLICY": args.core_policy}
-    specs = [PodSpec(workload=args.workload, mem_mib=args.gpumem, cores=args.gpucores, extra_env=dict(pol_env))
-             for _ in range(args.pods)]
+    cores = [int(c) for c in args.pod_cores.split(",") if c.strip()] if args.pod_cores else []
+    if cores and len(cores) != args.pods:
+        raise SystemExit(f"--pod-cores lists {len(cores)} values for {args.pods} pods")
+    specs = [PodSpec(workload=args.workload, mem_mib=args.gpumem, cores=cores[i] if cores else args.gpucores,
+                     extra_env=dict(pol_env)) for i in range(args.pods)]
     log(f"rank {rank}/{world}: launching {args.pods} pods of {w.name} (test {w.test_id}) on device {device}")
     pods = launch_pods(specs, device, steps=args.steps, warmup=args.warmup, shim=not args.no_shim,
                        graph=not args.no_graph, cap_probe=not args.no_cap_probe,
@@ -280,7 +285,7 @@ def main(argv=None) -> int:
                 "parallelism": f"vgpu: {args.pods} pods/GPU x {world} GPU(s)",
                 "pods_per_gpu": args.pods,
                 "gpumem_mib": args.gpumem,
-                "gpucores": args.gpucores,
+                "gpucores": args.gpucores if not cores else cores,
                 "enforcement": enforcement_label(args),
                 "cu_pack": os.environ.get("VGPU_CU_PACK", "spread"),
                 "hipgraph": not args.no_graph,

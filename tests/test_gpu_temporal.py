@@ -52,6 +52,17 @@ def test_four_quarter_pods_fill_the_gpu_fairly(exclusive):
         assert abs(v - fair) <= 0.15 * fair, d["per_pod_images_s"]
 
 
+def test_weighted_shares_under_contention(gpu_build):
+    """a 25 % and a 75 % pod contending for one GPU
+    (default policy: work-conserving weighted fair share through the share
+    board, limiter.cpp board_entitlement) get 1 : 3 of it, +-15 %."""
+    d = bench("--pods", "2", "--pod-cores", "25,75", "--gpumem", "100000", "--cu-share", "temporal")
+    a, b = d["per_pod_images_s"]
+    ratio = b / a
+    print("25 % vs 75 %:", a, b, "ratio", ratio)
+    assert 3 * 0.85 <= ratio <= 3 * 1.15, (a, b, ratio)
+
+
 def test_graph_capture_on_a_marked_stream_under_the_limiter(gpu_build, monkeypatch):
     """Two micro-batch hipGraphs captured on streams that just ran eager work
     (limiter markers outstanding on them) under the temporal limiter: the

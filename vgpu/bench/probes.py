@@ -326,6 +326,38 @@ def vmem(block_gib: int = 4, wait_s: int = 20) -> dict:
     return res
 
 
+def rcclloop(iters: int = 200, mib: int = 64, port: int = 0) -> dict:
+    """A world-size-1 RCCL process group all-reducing `mib` MiB `iters` times
+    (the collective path of a DDP pod), timed; the sum is checked."""
+    import datetime
+    import socket
+
+    import torch
+    import torch.distributed as dist
+    if not port:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            timeout=datetime.timedelta(seconds=120), device_id=dev)
+    x = torch.full(((mib << 20) // 4,), 3.0, device=dev)
+    dist.all_reduce(x)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for i in range(iters):
+        dist.all_reduce(x)
+        if i % 20 == 0:
+            torch.cuda.synchronize()
+            print(f"PROGRESS {i} {time.time():.3f}", flush=True)
+    torch.cuda.synchronize()
+    dt = time.time() - t0
+    ok = bool(torch.all(x == 3.0).item())
+    dist.destroy_process_group()
+    return {"iters": iters, "seconds": round(dt, 3), "ms_per_allreduce": round(1e3 * dt / iters, 3), "sum_ok": ok}
+
+
 def _vram_used_files() -> dict[str, int]:
     import glob
     out = {}
@@ -420,7 +452,7 @@ def main(argv=None) -> int:
     cmd = argv.pop(0) if argv else "census"
     nums = [int(a) for a in argv]
     out = {"census": census, "busy": busy, "cap": cap, "smi": smi, "graph": graph, "arrays": arrays,
-           "progress": progress, "vmem": vmem, "capheld": capheld, "asynccap": asynccap}[cmd](*nums)
+           "progress": progress, "vmem": vmem, "capheld": capheld, "asynccap": asynccap, "rcclloop": rcclloop}[cmd](*nums)
     out["shim"] = shim_stats()
     print("PROBE " + json.dumps(out), flush=True)
     return 0
