@@ -56,7 +56,10 @@ def test_weighted_shares_under_contention(gpu_build):
     """a 25 % and a 75 % pod contending for one GPU
     (default policy: work-conserving weighted fair share through the share
     board, limiter.cpp board_entitlement) get 1 : 3 of it, +-15 %."""
-    d = bench("--pods", "2", "--pod-cores", "25,75", "--gpumem", "100000", "--cu-share", "temporal")
+    # both pods run for the same 10 s window, far longer than the limiter's
+    # 200 ms quantum: the per-pod throughput ratio is the share ratio
+    d = bench("--pods", "2", "--pod-cores", "25,75", "--gpumem", "100000", "--cu-share", "temporal",
+              "--seconds", "10")
     a, b = d["per_pod_images_s"]
     ratio = b / a
     print("25 % vs 75 %:", a, b, "ratio", ratio)

@@ -205,6 +205,8 @@ def main(argv=None) -> int:
     ap.add_argument("--conv", choices=("native", "miopen"), default="native",
                     help="ResNet convolutions: fused MFMA kernels (native) or MIOpen + fused epilogues")
     ap.add_argument("--no-wait", action="store_true", help="do not wait for GO on stdin")
+    ap.add_argument("--seconds", type=float, default=0.0,
+                    help="run steps for this long instead of exactly --steps (share measurements)")
     args = ap.parse_args(argv)
 
     import torch
@@ -242,13 +244,22 @@ def main(argv=None) -> int:
             return 3
     sync()
     t0 = time.monotonic()
-    for _ in range(args.steps):
-        step()
+    steps = args.steps
+    if args.seconds > 0:  # a fixed window: every pod of a share test runs the whole time
+        steps = 0
+        while time.monotonic() - t0 < args.seconds:
+            step()
+            steps += 1
+            if steps % 8 == 0:
+                sync()  # keep the host within a few steps of the GPU
+    else:
+        for _ in range(steps):
+            step()
     sync()
     t1 = time.monotonic()
-    res = {"pod": args.pod_index, "t0": t0, "t1": t1, "steps": args.steps,
-           "samples": args.steps * w.batch, "ms_per_step": 1e3 * (t1 - t0) / max(args.steps, 1),
-           "throughput": args.steps * w.batch / max(t1 - t0, 1e-9)}
+    res = {"pod": args.pod_index, "t0": t0, "t1": t1, "steps": steps,
+           "samples": steps * w.batch, "ms_per_step": 1e3 * (t1 - t0) / max(steps, 1),
+           "throughput": steps * w.batch / max(t1 - t0, 1e-9)}
     if args.cap_probe and not cpu:
         res.update(cap_probe())
     emit("DONE", res)

@@ -22,6 +22,7 @@ the library is loaded in the process.
 from __future__ import annotations
 
 import json
+import os
 import sys
 import time
 
@@ -444,7 +445,7 @@ def asynccap(cap_mib: int = 8192, graph_mib: int = 1024) -> dict:
         sample()
     return {"cap": cap_mib * MiB, "baseline": baseline, "peak_over_baseline": peak, "samples": samples,
             "max_live_reached": reached, "ooms": ooms, "graphs_replayed": graph_ok, "y": float(y),
-            "backend": torch.cuda.get_allocator_backend()}
+            "backend": os.environ.get("PYTORCH_HIP_ALLOC_CONF", "")}
 
 
 def main(argv=None) -> int:
