@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 def test_hipmallocasync_backend_never_exceeds_the_cap(gpu_build):
     cap_mib = 8192
     res = probe(["asynccap", cap_mib, 1024], {"VGPU_DEVICE_MEMORY_LIMIT_0": f"{cap_mib}m",
-                                             "PYTORCH_HIP_ALLOC_CONF": "backend:hipMallocAsync"}, timeout=900)
+                                             "PYTORCH_HIP_ALLOC_CONF": "backend:cudaMallocAsync"}, timeout=900)
     assert "error" not in res, res
     cap = cap_mib << 20
     # amdgpu's own VRAM counter, this process's whole footprint (context included)
