@@ -79,7 +79,7 @@ def make_parser() -> argparse.ArgumentParser:
                     help="ResNet convolutions: fused MFMA implicit-GEMM kernels or MIOpen")
     ap.add_argument("--hw-queues", type=int, default=1,
                     help="GPU_MAX_HW_QUEUES per pod (vGPU HW-queue budget; 0 = runtime default)")
-    ap.add_argument("--cu-share", choices=("hybrid", "mask", "temporal", "group2", "group2i"), default="temporal",
+    ap.add_argument("--cu-share", choices=("hybrid", "mask", "temporal", "auto", "group2", "group2i"), default="temporal",
                     help="compute-share policy of fractional pods: the device plugin's "
                          "(hybrid|mask|temporal, vgpu/deviceplugin/custate.py) or an A/B tool")
     ap.add_argument("--core-policy", choices=("default", "force", "disable"), default="default",
@@ -98,6 +98,22 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--cpu-smoke", action="store_true",
                     help="rehearse the multi-rank orchestration on CPU (tests; not a measurement)")
     return ap
+
+
+def region_cus(path: str) -> int | None:
+    """CUs in a pod's shared-region mask right now (0 = every CU); None without a region."""
+    if not path or not os.path.exists(path):
+        return None
+    try:
+        from vgpu.monitor.region import AttachedRegion
+        r = AttachedRegion(path)
+        try:
+            devs = r.devices()
+            return bin(devs[0].cu_mask).count("1") if devs else None
+        finally:
+            r.close()
+    except Exception:
+        return None
 
 
 def preflight(placement: list[dict], world: int, shim: bool = True) -> bool:
@@ -227,6 +243,7 @@ def main(argv=None) -> int:
         t_end = max(p.done["t1"] for p in pods)
         t_start = min(p.done["t0"] for p in pods)
         wall = t_end - t_start
+        final_cus = [region_cus(p.region) for p in pods]  # CUs each pod ends on (auto policy may move it)
         rccl = None
         if pg and pods and distinct:
             rccl = rccl_check(pg, rank, world, pods[0], log)
@@ -305,6 +322,7 @@ def main(argv=None) -> int:
             "per_pod_images_s": [round(p.done["throughput"], 2) for p in pods],
             "per_pod_cu_mask_bits": [p.mask_bits for p in pods],
             "per_pod_share": [p.share for p in pods],
+            "per_pod_final_cus": final_cus,
             "vram_cap": cap,
             "placement": placement,
             "rccl_check": rccl,

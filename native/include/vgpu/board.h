@@ -30,7 +30,7 @@ extern "C" {
 #endif
 
 #define VGPU_BOARD_MAGIC 0x56424F44u /* "VBOD" */
-#define VGPU_BOARD_VERSION 2u
+#define VGPU_BOARD_VERSION 3u
 #define VGPU_BOARD_SLOTS 128
 #define VGPU_BOARD_STALE_NS 500000000ull /* a slot without heartbeat for 0.5 s is inactive */
 
@@ -51,6 +51,11 @@ typedef struct vgpu_board_slot {
   int32_t reserved0;
   volatile uint64_t run_start_ns;   /* CLOCK_MONOTONIC of the last admission     */
   volatile uint64_t wait_since_ns;  /* waiting for admission since (0 = not)     */
+  /* Adaptive share policy (VGPU_CU_SHARE=auto, limiter.cpp): CUs this slot
+   * holds exclusively while its dispatches are too small to fill the GPU
+   * (spatial mode); the auto pool members of the GPU run on the rest.
+   * 4 x 64 bits = 256 CUs, same logical bit order as the region's cu_mask. */
+  volatile uint64_t cu_claim[4];
 } vgpu_board_slot_t;
 
 typedef struct vgpu_board {

@@ -252,6 +252,55 @@ bool board_gate(vgpu_board_t* b, int slot, int max_running, uint64_t quantum_ns)
   return go;
 }
 
+// CUs claimed by the other live slots (spatial members of the auto policy).
+void board_claims_of_others(vgpu_board_t* b, int slot, uint64_t out[4]) {
+  for (int w = 0; w < 4; ++w) out[w] = 0;
+  if (!b) return;
+  const uint64_t now = mono_ns();
+  for (int i = 0; i < VGPU_BOARD_SLOTS; ++i) {
+    if (i == slot || !fresh(b->slot[i], now)) continue;
+    for (int w = 0; w < 4; ++w) out[w] |= __atomic_load_n(&b->slot[i].cu_claim[w], __ATOMIC_RELAXED);
+  }
+}
+
+// Claim `n` CUs in whole granules of one CU per XCD (logical bit i -> XCD
+// i % num_xcc, cumask.cpp) from `allowed` minus every other live claim; an
+// empty `n` releases the claim.  Under the board lock, so two slots never
+// claim the same CU.  Returns false when not enough CUs are free.
+bool board_claim_cus(vgpu_board_t* b, int slot, uint32_t n, uint32_t num_xcc, const uint64_t allowed[4],
+                     uint64_t out[4]) {
+  for (int w = 0; w < 4; ++w) out[w] = 0;
+  if (!b || slot < 0 || !lock(b)) return false;
+  vgpu_board_slot_t& me = b->slot[slot];
+  bool ok = true;
+  if (n == 0) {
+    for (int w = 0; w < 4; ++w) __atomic_store_n(&me.cu_claim[w], 0, __ATOMIC_RELAXED);
+  } else {
+    uint64_t taken[4] = {};
+    const uint64_t now = mono_ns();
+    for (int i = 0; i < VGPU_BOARD_SLOTS; ++i) {
+      if (i == slot || !fresh(b->slot[i], now)) continue;
+      for (int w = 0; w < 4; ++w) taken[w] |= b->slot[i].cu_claim[w];
+    }
+    const uint32_t g = num_xcc ? num_xcc : 1;  // CUs per granule (one per XCD)
+    uint32_t got = 0;
+    for (uint32_t base = 0; base + g <= 256 && got < n; base += g) {
+      bool free_g = true;
+      for (uint32_t k = base; k < base + g && free_g; ++k)
+        free_g = (allowed[k / 64] >> (k % 64) & 1) && !(taken[k / 64] >> (k % 64) & 1);
+      if (!free_g) continue;
+      for (uint32_t k = base; k < base + g; ++k) out[k / 64] |= 1ull << (k % 64);
+      got += g;
+    }
+    ok = got >= n;
+    if (!ok)
+      for (int w = 0; w < 4; ++w) out[w] = 0;
+    for (int w = 0; w < 4; ++w) __atomic_store_n(&me.cu_claim[w], out[w], __ATOMIC_RELAXED);
+  }
+  unlock(b);
+  return ok;
+}
+
 int board_running_count(vgpu_board_t* b) {
   if (!b) return 0;
   const uint64_t now = mono_ns();

@@ -19,6 +19,10 @@ int board_active_count(vgpu_board_t* b);
 bool board_gate(vgpu_board_t* b, int slot, int max_running, uint64_t quantum_ns);
 int board_running_count(vgpu_board_t* b);
 void board_gate_abort(vgpu_board_t* b, int slot);  // admitted launch was not tracked
+// Adaptive share policy: CU claims of spatial slots.
+void board_claims_of_others(vgpu_board_t* b, int slot, uint64_t out[4]);
+bool board_claim_cus(vgpu_board_t* b, int slot, uint32_t n, uint32_t num_xcc, const uint64_t allowed[4],
+                     uint64_t out[4]);
 double board_entitlement(vgpu_board_t* b, int slot);  // weighted fair share among active slots
 
 }  // namespace vgpu

@@ -36,40 +36,51 @@ inline uint64_t blocks3(unsigned x, unsigned y, unsigned z) {
   return (uint64_t)(x ? x : 1) * (y ? y : 1) * (z ? z : 1);
 }
 
-// Workgroups per launch of each executable graph (kernel nodes, recursively).
+// Workgroups and kernel nodes per launch of each executable graph (recursively).
+struct GraphWork {
+  uint64_t wg = 0;
+  uint32_t kernels = 0;
+};
 std::mutex g_graph_mu;
-std::unordered_map<const void*, uint64_t> g_graph_wg;
+std::unordered_map<const void*, GraphWork> g_graph_wg;
 
-uint64_t graph_workgroups(hipGraph_t g, int depth) {
+GraphWork graph_workgroups(hipGraph_t g, int depth) {
   auto get_nodes = REAL_HIP(hipGraphGetNodes);
   auto get_type = REAL_HIP(hipGraphNodeGetType);
   auto get_kernel = REAL_HIP(hipGraphKernelNodeGetParams);
   auto get_child = REAL_HIP(hipGraphChildGraphNodeGetGraph);
-  if (!g || depth > 8 || !get_nodes || !get_type || !get_kernel) return 0;
+  GraphWork out;
+  if (!g || depth > 8 || !get_nodes || !get_type || !get_kernel) return out;
   size_t n = 0;
-  if (get_nodes(g, nullptr, &n) != hipSuccess || n == 0) return 0;
+  if (get_nodes(g, nullptr, &n) != hipSuccess || n == 0) return out;
   std::vector<hipGraphNode_t> nodes(n);
-  if (get_nodes(g, nodes.data(), &n) != hipSuccess) return 0;
-  uint64_t wg = 0;
+  if (get_nodes(g, nodes.data(), &n) != hipSuccess) return out;
   for (size_t i = 0; i < n; ++i) {
     hipGraphNodeType t;
     if (get_type(nodes[i], &t) != hipSuccess) continue;
     if (t == hipGraphNodeTypeKernel) {
       hipKernelNodeParams kp{};
-      if (get_kernel(nodes[i], &kp) == hipSuccess) wg += blocks3(kp.gridDim.x, kp.gridDim.y, kp.gridDim.z);
+      if (get_kernel(nodes[i], &kp) == hipSuccess) {
+        out.wg += blocks3(kp.gridDim.x, kp.gridDim.y, kp.gridDim.z);
+        out.kernels++;
+      }
     } else if (t == hipGraphNodeTypeGraph && get_child) {
       hipGraph_t child = nullptr;
-      if (get_child(nodes[i], &child) == hipSuccess) wg += graph_workgroups(child, depth + 1);
+      if (get_child(nodes[i], &child) == hipSuccess) {
+        GraphWork c = graph_workgroups(child, depth + 1);
+        out.wg += c.wg;
+        out.kernels += c.kernels;
+      }
     }
   }
-  return wg;
+  return out;
 }
 
 void graph_exec_record(hipGraphExec_t exec, hipGraph_t graph) {
   if (!exec || !st().enabled) return;
-  const uint64_t wg = graph_workgroups(graph, 0);
+  const GraphWork w = graph_workgroups(graph, 0);
   std::lock_guard<std::mutex> l(g_graph_mu);
-  g_graph_wg[exec] = wg;
+  g_graph_wg[exec] = w;
 }
 
 void graph_exec_forget(hipGraphExec_t exec) {
@@ -77,10 +88,10 @@ void graph_exec_forget(hipGraphExec_t exec) {
   g_graph_wg.erase(exec);
 }
 
-uint64_t graph_exec_workgroups(hipGraphExec_t exec) {
+GraphWork graph_exec_work(hipGraphExec_t exec) {
   std::lock_guard<std::mutex> l(g_graph_mu);
   auto it = g_graph_wg.find(exec);
-  return it == g_graph_wg.end() ? 0 : it->second;
+  return it == g_graph_wg.end() ? GraphWork{} : it->second;
 }
 
 // Shared allocation path: reserve → real alloc → record (or unreserve).
@@ -513,11 +524,12 @@ __attribute__((visibility("default"))) hipError_t hipGraphLaunch(hipGraphExec_t 
     const char* v = getenv("VGPU_GRAPH_LAUNCH_TOKENS");
     return v ? strtoull(v, nullptr, 10) : 4096ull;
   }();
-  uint64_t wg = graph_exec_workgroups(exec);
+  const GraphWork gw = graph_exec_work(exec);
+  const uint64_t wg = gw.wg;
   const int dev = cur_dev();
   uint64_t tentative = 0;
   if (!pools_graph_admit(exec, dev, &tentative)) return hipErrorOutOfMemory;  // alloc nodes past the cap
-  const bool track = limiter_on_launch(dev, wg ? wg : fallback_tokens);
+  const bool track = limiter_on_launch(dev, wg ? wg : fallback_tokens, nullptr, gw.kernels);
   vmem_graph_launched(exec);
   hipError_t rc = REAL_HIP(hipGraphLaunch)(exec, stream);
   if (track) limiter_track(dev, stream, rc);

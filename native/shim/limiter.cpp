@@ -109,10 +109,19 @@ struct DevLimiter {
   // window statistics (limiter thread only)
   uint64_t win_charge = 0, win_busy = 0, win_start = 0;
   std::atomic<uint64_t> charged_total{0}, busy_total{0};
+  // Adaptive share policy (VGPU_CU_SHARE=auto): dispatch sizes of the last
+  // window, and whether this process holds CUs of its own (spatial mode).
+  int auto_share = 0;
+  std::atomic<uint64_t> wg_sum{0}, kern_n{0};
+  int spatial = 0;
+  int small_wins = 0, large_wins = 0;
+  bool pool0_saved = false;
+  uint64_t pool0[VGPU_CU_MASK_WORDS] = {};  // the plugin's pool mask at start (all-zero = every CU)
 };
 
 DevLimiter g_lim[VGPU_MAX_DEVICES];
 std::atomic<int> g_throttle_any{0};
+std::atomic<int> g_auto_any{0};
 std::atomic<int> g_thread_running{0};
 std::atomic<int> g_shutdown{0};
 std::atomic<int> g_thread_alive{0};
@@ -189,8 +198,22 @@ void configure() {
     const char* share = env_first("VGPU_CU_SHARE");
     // VGPU_CU_SHARE=temporal (device plugin, pool member): the share is
     // enforced in time; a mask, if any, is the pool of CUs the pool members share.
-    const bool temporal_share = share && !strcasecmp(share, "temporal");
+    // VGPU_CU_SHARE=auto: the same, until the process's dispatches turn out
+    // too small to fill the GPU; then it claims CUs of its own (auto_step).
+    const bool auto_share = share && !strcasecmp(share, "auto");
+    const bool temporal_share = auto_share || (share && !strcasecmp(share, "temporal"));
     bool want = lim > 0 && lim < 100 && s.lim.core_policy != 2;
+    DevLimiter& La = g_lim[d];
+    if (auto_share && want) {
+      La.auto_share = 1;
+      if (!La.pool0_saved && s.region) {
+        for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w)
+          La.pool0[w] = __atomic_load_n(&s.region->dev[d].cu_mask[w], __ATOMIC_RELAXED);
+        La.pool0_saved = true;
+      }
+      g_auto_any.store(1, std::memory_order_relaxed);
+    }
+    if (La.auto_share && La.spatial) want = false;  // own CUs: the mask is the share
     if (!temporal_share) {
       // A CU mask already enforces the share spatially; temporal limiting on
       // top of it only when explicitly forced.
@@ -201,7 +224,7 @@ void configure() {
     DevLimiter& L = g_lim[d];
     if (want && !L.active) {
       L.frac = lim / 100.0;
-      L.pool_scale_pending.store(temporal_share && has_mask ? 1 : 0);
+      L.pool_scale_pending.store(temporal_share && has_mask && !L.auto_share ? 1 : 0);
       const double burst_ms = env_first("VGPU_LIMITER_BURST_MS") ? atof(env_first("VGPU_LIMITER_BURST_MS")) : 50.0;
       L.cap = (int64_t)(L.frac * burst_ms * 1e6);
       // Time-slice quantum: a throttled pod runs in slices of ~quantum_ms of
@@ -330,6 +353,96 @@ bool reap(int dev, DevLimiter& L, uint64_t now_hint) {
   return left > 0;
 }
 
+void write_region_mask(int dev, const uint64_t m[VGPU_CU_MASK_WORDS]) {
+  State& s = st();
+  if (!s.region || region_lock(s.region) != 0) return;
+  for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) __atomic_store_n(&s.region->dev[dev].cu_mask[w], m[w], __ATOMIC_RELAXED);
+  region_unlock(s.region);
+}
+
+// Adaptive share policy, every ~200 ms (VGPU_CU_SHARE=auto; the device
+// plugin's default).  Measured on MI355X (docs/benchmarks.md, round 3): pods
+// whose dispatches fill the GPU (ResNet-50 b=50 inference: thousands of
+// workgroups) share it best in time -- CU masks cost them up to 34 % because a
+// masked queue's CUs idle while the CP time-slices it against another queue of
+// its pipe -- while pods of small dispatches (ResNet-152 b=10 training, LSTMs,
+// batch-1 DeepLab) interfere in time and run best on CUs of their own.  So a
+// pool member whose mean workgroups per dispatch stays below
+// VGPU_AUTO_SMALL_WG (default: the device's CU count) for two windows claims
+// an XCD-balanced set of its share's CUs on the share board and runs there,
+// unthrottled; the other auto pool members of the GPU shrink to the CUs nobody
+// claims.  Three large windows give the CUs back.
+void auto_step() {
+  State& s = st();
+  static const double small_wg_env = [] {
+    const char* e = env_first("VGPU_AUTO_SMALL_WG");
+    return e ? atof(e) : 0.0;
+  }();
+  for (int d = 0; d < VGPU_MAX_DEVICES; ++d) {
+    DevLimiter& L = g_lim[d];
+    if (!L.auto_share || !s.region) continue;
+    const uint64_t n = L.kern_n.exchange(0, std::memory_order_relaxed);
+    const uint64_t wg = L.wg_sum.exchange(0, std::memory_order_relaxed);
+    {
+      std::lock_guard<std::mutex> g(L.mu);
+      attach_board(d, L);
+    }
+    if (!L.board) continue;
+    const int phys = cumask_device_physical_cus(d);
+    const double small_wg = small_wg_env > 0 ? small_wg_env : (phys > 0 ? phys : 256);
+    if (n >= 16) {
+      const bool small = (double)wg / (double)n < small_wg;
+      L.small_wins = small ? L.small_wins + 1 : 0;
+      L.large_wins = small ? 0 : L.large_wins + 1;
+    }
+    uint64_t allowed[VGPU_CU_MASK_WORDS];
+    bool any = false;
+    for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) any |= L.pool0[w] != 0;
+    for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) {
+      const int lo = 64 * w;
+      const uint64_t full = phys <= lo ? 0 : (phys >= lo + 64 ? ~0ull : ((1ull << (phys - lo)) - 1));
+      allowed[w] = any ? L.pool0[w] : full;
+    }
+    uint64_t mask[VGPU_CU_MASK_WORDS] = {};
+    if (!L.spatial && L.small_wins >= 2 && s.region->proc_num <= 1) {
+      uint32_t nx = 8;
+      const uint32_t lim = s.region->dev[d].cu_limit;
+      const uint32_t want = ((uint32_t)((phys > 0 ? phys : 256) * lim + 99) / 100 + nx - 1) / nx * nx;
+      uint64_t got[4];
+      if (board_claim_cus(L.board, L.board_slot, want, nx, allowed, got)) {
+        L.spatial = 1;
+        write_region_mask(d, got);
+        VLOG_INFO("device %d: small dispatches (%.0f workgroups on average): %u CUs of our own", d,
+                  n ? (double)wg / (double)n : 0.0, want);
+        trace_emit(VGPU_EV_QUEUE, d, 1, want);
+      }
+      continue;
+    }
+    if (L.spatial && L.large_wins >= 3) {
+      uint64_t none[4];
+      board_claim_cus(L.board, L.board_slot, 0, 8, allowed, none);
+      L.spatial = 0;
+      VLOG_INFO("device %d: large dispatches again: back to the time-shared pool", d);
+      trace_emit(VGPU_EV_QUEUE, d, 0, 0);
+    }
+    if (L.spatial) continue;
+    // pool member: every allowed CU nobody claimed
+    uint64_t others[4];
+    board_claims_of_others(L.board, L.board_slot, others);
+    bool full = true;
+    for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) {
+      mask[w] = allowed[w] & ~others[w];
+      full &= mask[w] == allowed[w];
+    }
+    if (full && !any)
+      for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) mask[w] = 0;  // all CUs
+    bool same = true;
+    for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w)
+      same &= __atomic_load_n(&s.region->dev[d].cu_mask[w], __ATOMIC_RELAXED) == mask[w];
+    if (!same) write_region_mask(d, mask);
+  }
+}
+
 void limiter_main() {
   g_thread_alive.store(1);
   // Our polling must not be refused (or break) an application's graph capture
@@ -338,7 +451,7 @@ void limiter_main() {
     hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
     (void)xm(&m);
   }
-  uint64_t last = mono_ns(), last_mask = last, last_pool = last;
+  uint64_t last = mono_ns(), last_mask = last, last_pool = last, last_auto = last;
   uint64_t mask_sig = 0;
   State& s = st();
   while (!g_shutdown.load(std::memory_order_relaxed)) {
@@ -357,7 +470,12 @@ void limiter_main() {
     last = now;
     for (int d = 0; d < VGPU_MAX_DEVICES; ++d) {
       DevLimiter& L = g_lim[d];
-      if (!L.active) continue;
+      if (!L.active) {
+        // a spatial auto member is not throttled, but its CU claim lives only
+        // as long as its board slot stays fresh
+        if (L.auto_share && L.board) board_heartbeat(L.board, L.board_slot);
+        continue;
+      }
       // Credit rate.  force: the hard cap (limit % of wall time).  default:
       // work-conserving weighted fair share among the pods of this GPU that
       // have work outstanding (board entitlement) -- a pod alone is not held
@@ -387,6 +505,10 @@ void limiter_main() {
         L.win_charge = L.win_busy = 0;
         L.win_start = now;
       }
+    }
+    if (g_auto_any.load(std::memory_order_relaxed) && now - last_auto >= 200000000ull) {
+      last_auto = now;
+      auto_step();
     }
     // Stream-ordered pools give memory back on their own (release threshold):
     // keep their charge current.
@@ -490,7 +612,7 @@ void limiter_after_fork() {
   }
 }
 
-bool limiter_on_launch(int dev, uint64_t wg, const void* fn) {
+bool limiter_on_launch(int dev, uint64_t wg, const void* fn, uint32_t kernels) {
   State& s = st();
   if (!s.enabled) return false;
   suspend_gate();
@@ -499,6 +621,11 @@ bool limiter_on_launch(int dev, uint64_t wg, const void* fn) {
   if (sl) {
     __atomic_fetch_add(&sl->launches, 1, __ATOMIC_RELAXED);
     __atomic_store_n(&sl->last_launch_ns, mono_ns(), __ATOMIC_RELAXED);
+  }
+  if (g_auto_any.load(std::memory_order_relaxed) && dev >= 0 && dev < VGPU_MAX_DEVICES && kernels &&
+      g_lim[dev].auto_share) {
+    g_lim[dev].wg_sum.fetch_add(wg, std::memory_order_relaxed);
+    g_lim[dev].kern_n.fetch_add(kernels, std::memory_order_relaxed);
   }
   const bool throttling = g_throttle_any.load(std::memory_order_relaxed) != 0;
   if (__builtin_expect(!throttling && !trace_on(), 1)) return false;

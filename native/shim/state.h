@@ -95,7 +95,7 @@ void limiter_after_fork();
 // kernel's host stub when known (RCCL kernels are exempt from throttling).
 // Returns true when the launch must be tracked: call limiter_track after the
 // launch on `stream` with its result.
-bool limiter_on_launch(int dev, uint64_t workgroups, const void* fn = nullptr);
+bool limiter_on_launch(int dev, uint64_t workgroups, const void* fn = nullptr, uint32_t kernels = 1);
 void limiter_track(int dev, hipStream_t stream, hipError_t launch_rc);
 // Stream captures in progress anywhere in the process: while one is open the
 // limiter records and polls markers only on streams that are not capturing (an

@@ -529,6 +529,42 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (sc == "auto") {
+    // Adaptive share policy: launch kernels of `grid` workgroups for `secs`
+    // seconds, then report this container's region mask and its queue's mask.
+    unsigned grid = argc > 2 ? (unsigned)atoi(argv[2]) : 64;
+    double secs = argc > 3 ? atof(argv[3]) : 1.5;
+    void* p = nullptr;
+    hipMalloc(&p, 4096);  // runtime init: the queue exists
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (;;) {
+      clock_gettime(CLOCK_MONOTONIC, &b);
+      if ((b.tv_sec - a.tv_sec) + 1e-9 * (b.tv_nsec - a.tv_nsec) >= secs) break;
+      hipLaunchKernel((const void*)&main, dim3(grid), dim3(256), nullptr, 0, nullptr);
+      usleep(200);
+    }
+    hipDeviceSynchronize();
+    auto* r = (vgpu_shared_region_t*)sym<void* (*)()>("vgpu_self_region")();
+    int bits = 0;
+    printf("region_mask=");
+    for (int w = VGPU_CU_MASK_WORDS - 1; w >= 0; --w) {
+      printf("%016llx", (unsigned long long)r->dev[dev].cu_mask[w]);
+      bits += __builtin_popcountll(r->dev[dev].cu_mask[w]);
+    }
+    printf("\nregion_mask_bits=%d\n", bits);
+    uint32_t m[8] = {};
+    uint64_t agent = 0;
+    int words = fake_hsa_queue_mask(0, m, 8, &agent);
+    int qbits = 0;
+    for (int w = 0; w < words; ++w) qbits += __builtin_popcount(m[w]);
+    printf("queue_mask_bits=%d\n", words ? qbits : -1);
+    fflush(stdout);
+    usleep(argc > 4 ? atoi(argv[4]) * 1000 : 0);  // stay alive (the board keeps our claim while we live)
+    hipFree(p);
+    return 0;
+  }
+
   if (sc == "masks") {
     void* p = nullptr;
     hipMalloc(&p, 4096);  // forces runtime init (queue creation)

@@ -113,7 +113,7 @@ def admit_pods(specs: list, device_index: int, workdir: str, *, policy: str = "t
             region = Path(env.get("VGPU_SHARED_REGION", str(work / name / "vgpu.cache")))
             region.parent.mkdir(parents=True, exist_ok=True)
             mask = env.get("VGPU_CU_MASK_0", "0x0")
-            share = "temporal" if env.get("VGPU_CU_SHARE") == "temporal" else (
+            share = env["VGPU_CU_SHARE"] if env.get("VGPU_CU_SHARE") in ("temporal", "auto") else (
                 "mask" if int(mask, 16) else "none")
             out.append(AdmittedPod(name, env, grant, bin(int(mask, 16)).count("1"), share))
         return out

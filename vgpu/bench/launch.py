@@ -108,7 +108,7 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
     lock_dir = str(Path(workdir) / "vgpulock")
     Path(lock_dir).mkdir(parents=True, exist_ok=True)
     admitted = None
-    if cu_share in ("hybrid", "mask", "temporal"):
+    if cu_share in ("hybrid", "mask", "temporal", "auto"):
         from vgpu.bench.control import admit_pods
         admitted = admit_pods(specs, int(device) if device.isdigit() else 0, workdir, policy=cu_share,
                               memory_scaling=max(memory_scaling, 2.0 if oversubscribe else 1.0),

@@ -11,6 +11,9 @@ reference's comparison (README.md:234-257):
   vgpu-cu25-temporal — the same 4 pods, policy named explicitly
   vgpu-cu25-mask     — the same 4 pods, one CU mask each
   vgpu-cu25-hybrid   — 2 CU masks + a temporal pool for the other two
+  vgpu-cu25-auto     — the 4 pods under the adaptive policy: pool members that
+                       claim CUs of their own when their dispatches are small
+  vgpu-auto          — 2 pods, adaptive policy
   vgpu-cu25-k2       — the 4 pods in the temporal pool, at most 2 running at a time
                        (device plugin --pool-concurrency 2)
   vgpu-vmem          — the reference's "vGPU + virtual device memory" column:
@@ -41,6 +44,8 @@ SCENARIOS = {
     "vgpu-cu25": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000"],
     "vgpu-cu25-temporal": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "temporal"],
     "vgpu-cu25-mask": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "mask"],
+    "vgpu-cu25-auto": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "auto"],
+    "vgpu-auto": ["--pods", "2", "--gpucores", "50", "--gpumem", "144000", "--cu-share", "auto"],
     "vgpu-vmem": ["--pods", "2", "--gpucores", "0", "--gpumem", "230000", "--oversubscribe",
                   "--memory-scaling", "1.8"],
     "vgpu-cu25-k2": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "temporal",
@@ -62,7 +67,7 @@ def run(test: str, scen: str, steps: int, warmup: int, timeout: int) -> dict:
         return {"test": test, "scenario": scen, "error": r.stderr[-1500:]}
     d = json.loads(js[-1])
     return {"test": test, "scenario": scen, "images_s": d["value"], "per_pod": d["per_pod_images_s"],
-            "ms_per_step": d["ms_per_step"], "share": d.get("per_pod_share")}
+            "ms_per_step": d["ms_per_step"], "share": d.get("per_pod_share"), "final_cus": d.get("per_pod_final_cus")}
 
 
 def main(argv=None) -> int:

@@ -192,8 +192,9 @@ def build_container_grant(cfg: DevicePluginConfig, pod: dict, ctr_idx: int, devr
     if temporal:
         # Pool member: shares the device's unmasked CUs with the other pool
         # members under the shim's GPU-time limiter (fair-share board in the
-        # node-wide lock dir); no mask is derived from the limit.
-        g.envs[ENV_CU_SHARE] = "temporal"
+        # node-wide lock dir); no mask is derived from the limit.  Under the
+        # auto policy it may later claim CUs of its own (limiter.cpp auto_step).
+        g.envs[ENV_CU_SHARE] = "auto" if (pod_policy or cfg.cu_share) == "auto" else "temporal"
         g.envs["VGPU_CU_MASK_FROM_LIMIT"] = "false"
         if cfg.pool_concurrency > 0:
             g.envs["VGPU_POOL_CONCURRENCY"] = str(cfg.pool_concurrency)

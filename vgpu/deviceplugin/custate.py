@@ -30,6 +30,11 @@ that wants exclusive CUs on a temporal node).
 * ``hybrid``: the first ``max_mask_slots`` fractional containers on a GPU get
   masks, which is exact spatial isolation at equal throughput for two sharers.
   Later containers join the pool.
+* ``auto``: every fractional container starts as a pool member (like
+  ``temporal``); a member whose dispatches turn out too small to fill the GPU
+  claims CUs of its own on the share board at run time and runs there
+  unthrottled, the others shrink to the rest (native/shim/limiter.cpp
+  auto_step).  Spatial where it pays, temporal where it does not.
 
 The pool of a device is every CU not held by a masked container; pool members
 share it in time. The shim scales a pool member's time limit by
@@ -54,7 +59,7 @@ GRANT_FILE = "grant.json"
 REGION_FILE = "vgpu.cache"  # the container's shared region (allocate.py: VGPU_SHARED_REGION)
 MODE_MASK = "mask"
 MODE_POOL = "pool"
-POLICIES = ("mask", "temporal", "hybrid")
+POLICIES = ("mask", "temporal", "hybrid", "auto")
 
 
 @dataclass
