@@ -36,20 +36,34 @@ def summarize(files: list[str], tail: float) -> dict:
     rows = rows[int(len(rows) * (1 - tail)):]
     tot = 0.0
     small = {64: 0.0, 256: 0.0, 512: 0.0, 1024: 0.0}
+    cnt_small = {64: 0, 256: 0, 512: 0, 1024: 0}
+    wg_small = {64: 0, 256: 0, 512: 0, 1024: 0}
     wsum = 0.0
+    wg_tot = 0
+    sizes = []
     for r in rows:
         dt = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         wg_items = dims(r, "Workgroup_Size")
         grid = dims(r, "Grid_Size")
         wgs = max(1, grid // max(wg_items, 1))
+        sizes.append(wgs)
         tot += dt
         wsum += dt * wgs
+        wg_tot += wgs
         for k in small:
             if wgs < k:
                 small[k] += dt
+                cnt_small[k] += 1
+                wg_small[k] += wgs
+    sizes.sort()
+    n = max(len(rows), 1)
     return {"dispatches": len(rows), "busy_ms": round(tot / 1e6, 2),
             "time_weighted_mean_workgroups": round(wsum / max(tot, 1), 1),
-            **{f"time_frac_below_{k}_wg": round(v / max(tot, 1), 3) for k, v in small.items()}}
+            "mean_workgroups": round(wg_tot / n, 1), "median_workgroups": sizes[len(sizes) // 2] if sizes else 0,
+            **{f"time_frac_below_{k}_wg": round(v / max(tot, 1), 3) for k, v in small.items()},
+            **{f"count_frac_below_{k}_wg": round(v / n, 3) for k, v in cnt_small.items()},
+            **{f"wg_frac_below_{k}_wg": round(v / max(wg_tot, 1), 4) for k, v in wg_small.items()},
+            "mean_us": round(tot / n / 1e3, 2)}
 
 
 def main() -> int:

@@ -12,3 +12,4 @@ for t in ${TESTS:-1.1 1.2 2.1 2.2 3.1 3.2 4.1 4.2 5.1 5.2}; do
   rc=$?; echo "$t rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 python3 scripts/kernel_sizes.py $O > $O/summary.json && cat $O/summary.json
+find $O -name "*.csv" -delete  # traces are large; the summary is what we keep

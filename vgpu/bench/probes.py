@@ -387,6 +387,17 @@ def asynccap(cap_mib: int = 8192, graph_mib: int = 1024) -> dict:
     baseline = base[path]
     peak = 0
     samples = 0
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    pool = ctypes.c_void_p()
+    hip.hipDeviceGetMemPool(ctypes.byref(pool), 0)
+    phases: dict[str, dict] = {}
+    phase = "cycles"
+
+    def pool_attr(a: int) -> int:
+        v = ctypes.c_uint64(0)
+        hip.hipMemPoolGetAttribute(pool, a, ctypes.byref(v))
+        return v.value
 
     def sample():
         nonlocal peak, samples
@@ -394,6 +405,11 @@ def asynccap(cap_mib: int = 8192, graph_mib: int = 1024) -> dict:
         v = int(open(path).read()) - baseline
         peak = max(peak, v)
         samples += 1
+        ph = phases.setdefault(phase, {"peak_over_baseline": 0})
+        if v >= ph["peak_over_baseline"]:
+            st = shim_stats() or {}
+            ph.update({"peak_over_baseline": v, "pool_reserved": pool_attr(5), "pool_used": pool_attr(7),
+                       "shim_total": st.get("total"), "torch_reserved": torch.cuda.memory_reserved()})
 
     rng = random.Random(0)
     MiB = 1 << 20
@@ -423,6 +439,7 @@ def asynccap(cap_mib: int = 8192, graph_mib: int = 1024) -> dict:
         del live
         sample()
     # graphs whose temporaries are stream-ordered allocations (graph alloc nodes)
+    phase = "graphs"
     x = torch.randn(graph_mib * MiB // 4, device="cuda")
     graph_ok = 0
     for k in (1, 2, 3):
@@ -445,7 +462,7 @@ def asynccap(cap_mib: int = 8192, graph_mib: int = 1024) -> dict:
         sample()
     return {"cap": cap_mib * MiB, "baseline": baseline, "peak_over_baseline": peak, "samples": samples,
             "max_live_reached": reached, "ooms": ooms, "graphs_replayed": graph_ok, "y": float(y),
-            "backend": os.environ.get("PYTORCH_HIP_ALLOC_CONF", "")}
+            "backend": os.environ.get("PYTORCH_HIP_ALLOC_CONF", ""), "phases": phases}
 
 
 def main(argv=None) -> int:
