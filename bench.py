@@ -92,6 +92,8 @@ def make_parser() -> argparse.ArgumentParser:
                     help="device plugin --pool-concurrency: temporal-pool members of a GPU running at once "
                          "(0 = all; default: the plugin's)")
     ap.add_argument("--no-cap-probe", action="store_true")
+    ap.add_argument("--warmup-seconds", type=float, default=0.0,
+                    help="pods keep warming up (untimed) until this long has passed")
     ap.add_argument("--seconds", type=float, default=0.0,
                     help="share measurements: every pod runs steps for this long instead of exactly --steps")
     ap.add_argument("--ready-timeout", type=float, default=1500.0)
@@ -219,7 +221,7 @@ def main(argv=None) -> int:
                        find=not args.no_find, hw_queues=args.hw_queues or None,
                        fused=not args.no_fused, conv=args.conv, cu_share=args.cu_share,
                        oversubscribe=args.oversubscribe, memory_scaling=args.memory_scaling,
-                       pool_concurrency=pool_conc, seconds=args.seconds)
+                       pool_concurrency=pool_conc, seconds=args.seconds, warmup_seconds=args.warmup_seconds)
     try:
         for p in pods:
             p.ready = p.read_tagged("READY", args.ready_timeout, progress=log)

@@ -95,6 +95,27 @@ void timeline_launch() {
   std::lock_guard<std::mutex> g(g_tl_mu);
   const uint64_t now = now_ns();
   static const char* shared = getenv("VGPU_FAKE_GPU_TIMELINE");
+  // VGPU_FAKE_MASK_FACTOR: a process whose queue has a CU mask runs on CUs of
+  // its own (a private timeline), each launch taking dur x (256 / its CUs) x
+  // factor -- < 1 models workloads that run better spatially, > 1 worse.
+  static const char* mf = getenv("VGPU_FAKE_MASK_FACTOR");
+  if (mf && *mf) {
+    using qm_t = int (*)(int, uint32_t*, int, uint64_t*);
+    static qm_t qm = (qm_t)dlsym(RTLD_DEFAULT, "fake_hsa_queue_mask");
+    uint32_t m[8] = {};
+    uint64_t agent = 0;
+    const int words = qm ? qm(0, m, 8, &agent) : -1;
+    int bits = 0;
+    for (int w = 0; w < words && w < 8; ++w) bits += __builtin_popcount(m[w]);
+    if (bits > 0 && bits < 256) {
+      const uint64_t d = (uint64_t)(dur * (256.0 / bits) * atof(mf));
+      const uint64_t start = g_busy_until > now ? g_busy_until : now;
+      g_busy_until = start + d;
+      g_my_last_end = g_busy_until;
+      g_exec_ns.fetch_add(d);
+      return;
+    }
+  }
   if (shared && *shared) {
     int fd = open(shared, O_RDWR | O_CREAT, 0666);
     if (fd >= 0) {

@@ -33,6 +33,11 @@ extern "C" {
 #define VGPU_BOARD_VERSION 3u
 #define VGPU_BOARD_SLOTS 128
 #define VGPU_BOARD_STALE_NS 500000000ull /* a slot without heartbeat for 0.5 s is inactive */
+/* auto_phase */
+#define VGPU_AUTO_TEMPORAL 0      /* decided (or too few busy members): time sharing */
+#define VGPU_AUTO_EXPLORE_T 1     /* measuring time sharing                          */
+#define VGPU_AUTO_EXPLORE_S 2     /* measuring CU claims                             */
+#define VGPU_AUTO_SPATIAL 3       /* decided: every member on CUs of its own         */
 
 typedef struct vgpu_board_slot {
   int32_t pid;                   /* pid inside the owner's container (0 = free) */
@@ -56,6 +61,13 @@ typedef struct vgpu_board_slot {
    * (spatial mode); the auto pool members of the GPU run on the rest.
    * 4 x 64 bits = 256 CUs, same logical bit order as the region's cu_mask. */
   volatile uint64_t cu_claim[4];
+  volatile int32_t auto_member;     /* 1: the slot runs the adaptive (auto) policy            */
+  int32_t reserved2;
+  volatile uint64_t auto_launches;  /* its dispatches so far (progress signal)                */
+  uint64_t auto_mark;               /* auto_launches at the start of a measurement (leader)   */
+  uint64_t auto_seen;               /* auto_launches at the leader's last look                */
+  uint64_t auto_busy_ns;            /* when the leader last saw it progress                   */
+  double auto_rate[2];              /* dispatches/s measured time-shared [0] / on own CUs [1] */
 } vgpu_board_slot_t;
 
 typedef struct vgpu_board {
@@ -71,6 +83,14 @@ typedef struct vgpu_board {
   uint64_t last_ns;       /* CLOCK_MONOTONIC of the last advance              */
   int32_t n_active;       /* live active slots at the last advance            */
   int32_t reserved;
+  /* Adaptive share policy (auto): a per-GPU A/B between time sharing and CU
+   * claims, driven by the lowest live auto slot (limiter.cpp auto_step).   */
+  volatile int32_t auto_phase;     /* VGPU_AUTO_*                                       */
+  volatile int32_t auto_members;   /* busy members the current decision was made for    */
+  volatile uint64_t auto_phase_ns; /* CLOCK_MONOTONIC when the phase began              */
+  volatile int32_t auto_marked;    /* 1 once the phase's measurement window opened      */
+  int32_t reserved3;
+  volatile double auto_score;      /* mean own-CU / time-shared rate of the last A/B     */
   vgpu_board_slot_t slot[VGPU_BOARD_SLOTS];
 } vgpu_board_t;
 

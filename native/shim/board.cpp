@@ -3,6 +3,7 @@
 #include "board.h"
 
 #include <errno.h>
+#include <stdio.h>
 #include <fcntl.h>
 #include <sys/file.h>
 #include <sys/mman.h>
@@ -299,6 +300,102 @@ bool board_claim_cus(vgpu_board_t* b, int slot, uint32_t n, uint32_t num_xcc, co
   }
   unlock(b);
   return ok;
+}
+
+// ---- adaptive share policy (auto): a per-GPU A/B, board-coordinated --------------------
+void board_auto_join(vgpu_board_t* b, int slot) {
+  if (b && slot >= 0) __atomic_store_n(&b->slot[slot].auto_member, 1, __ATOMIC_RELEASE);
+}
+
+void board_auto_progress(vgpu_board_t* b, int slot, uint64_t dispatches) {
+  if (b && slot >= 0 && dispatches) __atomic_fetch_add(&b->slot[slot].auto_launches, dispatches, __ATOMIC_RELAXED);
+}
+
+int board_auto_phase(vgpu_board_t* b) { return b ? __atomic_load_n(&b->auto_phase, __ATOMIC_ACQUIRE) : 0; }
+
+// The lowest live auto member drives the per-GPU state machine:
+//   TEMPORAL/SPATIAL (decided) --(>= 2 busy members and a new member count, or
+//   `reexplore_ns` since the decision)--> EXPLORE_T --window--> EXPLORE_S
+//   --window--> SPATIAL if the members' mean dispatch rate on own CUs is at
+//   least `min_gain` x their time-shared rate, else TEMPORAL.
+// Each measurement window opens `settle_ns` after its phase began (masks
+// re-applied, queues refilled).  Fewer than two busy members: time sharing (a
+// lone pod is not held back there).  Returns the phase.
+int board_auto_lead(vgpu_board_t* b, int slot, uint64_t window_ns, uint64_t settle_ns, uint64_t reexplore_ns,
+                    double min_gain, char* note, size_t note_len) {
+  if (note && note_len) note[0] = 0;
+  if (!b || slot < 0 || !lock(b)) return board_auto_phase(b);
+  const uint64_t now = mono_ns();
+  int leader = -1, nb = 0;
+  int busy[VGPU_BOARD_SLOTS];
+  for (int i = 0; i < VGPU_BOARD_SLOTS; ++i) {
+    vgpu_board_slot_t& s = b->slot[i];
+    if (!fresh(s, now) || !s.auto_member) continue;
+    if (leader < 0) leader = i;
+    const uint64_t l = __atomic_load_n(&s.auto_launches, __ATOMIC_RELAXED);
+    if (l != s.auto_seen) {
+      s.auto_seen = l;
+      s.auto_busy_ns = now;
+    }
+    if (now - s.auto_busy_ns < 1000000000ull) busy[nb++] = i;
+  }
+  int phase = b->auto_phase;
+  if (leader != slot) {
+    unlock(b);
+    return phase;
+  }
+  auto go = [&](int p) {
+    __atomic_store_n(&b->auto_phase, p, __ATOMIC_RELEASE);
+    b->auto_phase_ns = now;
+    b->auto_marked = 0;
+    phase = p;
+  };
+  if (phase == VGPU_AUTO_TEMPORAL || phase == VGPU_AUTO_SPATIAL) {
+    if (nb < 2) {
+      if (phase == VGPU_AUTO_SPATIAL) go(VGPU_AUTO_TEMPORAL);
+      b->auto_members = nb;
+    } else if (nb != b->auto_members || now - b->auto_phase_ns > reexplore_ns) {
+      go(VGPU_AUTO_EXPLORE_T);
+    }
+  } else if (nb < 2) {
+    go(VGPU_AUTO_TEMPORAL);
+    b->auto_members = nb;
+  } else if (!b->auto_marked) {
+    if (now - b->auto_phase_ns >= settle_ns) {
+      for (int k = 0; k < nb; ++k) b->slot[busy[k]].auto_mark = b->slot[busy[k]].auto_seen;
+      b->auto_phase_ns = now;
+      b->auto_marked = 1;
+    }
+  } else if (now - b->auto_phase_ns >= window_ns) {
+    const double secs = (now - b->auto_phase_ns) * 1e-9;
+    const int idx = phase == VGPU_AUTO_EXPLORE_T ? 0 : 1;
+    for (int k = 0; k < nb; ++k) {
+      vgpu_board_slot_t& s = b->slot[busy[k]];
+      s.auto_rate[idx] = (double)(s.auto_seen - s.auto_mark) / secs;
+    }
+    if (phase == VGPU_AUTO_EXPLORE_T) {
+      go(VGPU_AUTO_EXPLORE_S);
+    } else {
+      double sum = 0;
+      int n = 0;
+      for (int k = 0; k < nb; ++k) {
+        const vgpu_board_slot_t& s = b->slot[busy[k]];
+        if (s.auto_rate[0] > 0) {
+          sum += s.auto_rate[1] / s.auto_rate[0];
+          ++n;
+        }
+      }
+      const double score = n ? sum / n : 0.0;
+      b->auto_score = score;
+      b->auto_members = nb;
+      go(score >= min_gain ? VGPU_AUTO_SPATIAL : VGPU_AUTO_TEMPORAL);
+      if (note && note_len)
+        snprintf(note, note_len, "%d busy members: own CUs run at %.3f x their time-shared rate -> %s", nb,
+                 score, phase == VGPU_AUTO_SPATIAL ? "CUs of their own" : "time sharing");
+    }
+  }
+  unlock(b);
+  return phase;
 }
 
 int board_running_count(vgpu_board_t* b) {

@@ -23,6 +23,11 @@ void board_gate_abort(vgpu_board_t* b, int slot);  // admitted launch was not tr
 void board_claims_of_others(vgpu_board_t* b, int slot, uint64_t out[4]);
 bool board_claim_cus(vgpu_board_t* b, int slot, uint32_t n, uint32_t num_xcc, const uint64_t allowed[4],
                      uint64_t out[4]);
+void board_auto_join(vgpu_board_t* b, int slot);
+void board_auto_progress(vgpu_board_t* b, int slot, uint64_t dispatches);
+int board_auto_phase(vgpu_board_t* b);
+int board_auto_lead(vgpu_board_t* b, int slot, uint64_t window_ns, uint64_t settle_ns, uint64_t reexplore_ns,
+                    double min_gain, char* note, size_t note_len);
 double board_entitlement(vgpu_board_t* b, int slot);  // weighted fair share among active slots
 
 }  // namespace vgpu

@@ -112,9 +112,9 @@ struct DevLimiter {
   // Adaptive share policy (VGPU_CU_SHARE=auto): dispatch sizes of the last
   // window, and whether this process holds CUs of its own (spatial mode).
   int auto_share = 0;
-  std::atomic<uint64_t> wg_sum{0}, kern_n{0};
+  std::atomic<uint64_t> kern_n{0};  // dispatches since the last auto_step (graph launch = 1)
   int spatial = 0;
-  int small_wins = 0, large_wins = 0;
+  bool auto_joined = false;
   bool pool0_saved = false;
   uint64_t pool0[VGPU_CU_MASK_WORDS] = {};  // the plugin's pool mask at start (all-zero = every CU)
 };
@@ -360,41 +360,44 @@ void write_region_mask(int dev, const uint64_t m[VGPU_CU_MASK_WORDS]) {
   region_unlock(s.region);
 }
 
-// Adaptive share policy, every ~200 ms (VGPU_CU_SHARE=auto; the device
-// plugin's default).  Measured on MI355X (docs/benchmarks.md, round 3): pods
-// whose dispatches fill the GPU (ResNet-50 b=50 inference: thousands of
-// workgroups) share it best in time -- CU masks cost them up to 34 % because a
-// masked queue's CUs idle while the CP time-slices it against another queue of
-// its pipe -- while pods of small dispatches (ResNet-152 b=10 training, LSTMs,
-// batch-1 DeepLab) interfere in time and run best on CUs of their own.  So a
-// pool member whose mean workgroups per dispatch stays below
-// VGPU_AUTO_SMALL_WG (default: the device's CU count) for two windows claims
-// an XCD-balanced set of its share's CUs on the share board and runs there,
-// unthrottled; the other auto pool members of the GPU shrink to the CUs nobody
-// claims.  Three large windows give the CUs back.
+// Adaptive share policy (VGPU_CU_SHARE=auto; the device plugin's default).
+// Measured on MI355X (docs/benchmarks.md): four 25 % pods of ResNet-50
+// inference (dispatches of thousands of workgroups) run 1.7 x faster time-shared
+// than on CU masks of their own -- a masked queue's CUs idle while the CP
+// time-slices it against another queue -- while ResNet-152 training, DeepLab
+// training and the LSTMs run 1.2-1.35 x faster on masks, and no per-dispatch
+// statistic the shim can see separates the two groups (scripts/kernel_sizes.py,
+// profiles/r3/policy).  So the pods of a GPU measure both: the share board runs
+// an A/B (board_auto_lead) -- a window time-shared, a window with every busy
+// member on an XCD-balanced claim of its share's CUs -- compares each member's
+// dispatch rate and keeps whichever was faster on average (re-measured when
+// the set of busy members changes, or every VGPU_AUTO_REEXPLORE_S).  A member
+// on its own CUs runs unthrottled; the other members of the GPU's pool shrink
+// to the CUs nobody claimed.
 void auto_step() {
   State& s = st();
-  static const double small_wg_env = [] {
-    const char* e = env_first("VGPU_AUTO_SMALL_WG");
-    return e ? atof(e) : 0.0;
-  }();
+  static const uint64_t window_ns = (uint64_t)(1e6 * (env_first("VGPU_AUTO_WINDOW_MS") ? atof(env_first("VGPU_AUTO_WINDOW_MS")) : 1500.0));
+  static const uint64_t settle_ns = (uint64_t)(1e6 * (env_first("VGPU_AUTO_SETTLE_MS") ? atof(env_first("VGPU_AUTO_SETTLE_MS")) : 300.0));
+  static const uint64_t reexplore_ns = (uint64_t)(1e9 * (env_first("VGPU_AUTO_REEXPLORE_S") ? atof(env_first("VGPU_AUTO_REEXPLORE_S")) : 300.0));
+  static const double min_gain = env_first("VGPU_AUTO_MIN_GAIN") ? atof(env_first("VGPU_AUTO_MIN_GAIN")) : 1.05;
   for (int d = 0; d < VGPU_MAX_DEVICES; ++d) {
     DevLimiter& L = g_lim[d];
     if (!L.auto_share || !s.region) continue;
-    const uint64_t n = L.kern_n.exchange(0, std::memory_order_relaxed);
-    const uint64_t wg = L.wg_sum.exchange(0, std::memory_order_relaxed);
     {
       std::lock_guard<std::mutex> g(L.mu);
       attach_board(d, L);
     }
     if (!L.board) continue;
-    const int phys = cumask_device_physical_cus(d);
-    const double small_wg = small_wg_env > 0 ? small_wg_env : (phys > 0 ? phys : 256);
-    if (n >= 16) {
-      const bool small = (double)wg / (double)n < small_wg;
-      L.small_wins = small ? L.small_wins + 1 : 0;
-      L.large_wins = small ? 0 : L.large_wins + 1;
+    if (!L.auto_joined) {
+      board_auto_join(L.board, L.board_slot);
+      L.auto_joined = true;
     }
+    board_auto_progress(L.board, L.board_slot, L.kern_n.exchange(0, std::memory_order_relaxed));
+    char note[160];
+    const int phase = board_auto_lead(L.board, L.board_slot, window_ns, settle_ns, reexplore_ns, min_gain, note,
+                                      sizeof note);
+    if (note[0]) VLOG_INFO("device %d: adaptive share: %s", d, note);
+    const int phys = cumask_device_physical_cus(d);
     uint64_t allowed[VGPU_CU_MASK_WORDS];
     bool any = false;
     for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) any |= L.pool0[w] != 0;
@@ -403,31 +406,28 @@ void auto_step() {
       const uint64_t full = phys <= lo ? 0 : (phys >= lo + 64 ? ~0ull : ((1ull << (phys - lo)) - 1));
       allowed[w] = any ? L.pool0[w] : full;
     }
-    uint64_t mask[VGPU_CU_MASK_WORDS] = {};
-    if (!L.spatial && L.small_wins >= 2 && s.region->proc_num <= 1) {
-      uint32_t nx = 8;
+    const bool want_own = (phase == VGPU_AUTO_EXPLORE_S || phase == VGPU_AUTO_SPATIAL) && s.region->proc_num <= 1;
+    if (want_own && !L.spatial) {
+      const uint32_t nx = 8;
       const uint32_t lim = s.region->dev[d].cu_limit;
       const uint32_t want = ((uint32_t)((phys > 0 ? phys : 256) * lim + 99) / 100 + nx - 1) / nx * nx;
       uint64_t got[4];
       if (board_claim_cus(L.board, L.board_slot, want, nx, allowed, got)) {
         L.spatial = 1;
         write_region_mask(d, got);
-        VLOG_INFO("device %d: small dispatches (%.0f workgroups on average): %u CUs of our own", d,
-                  n ? (double)wg / (double)n : 0.0, want);
         trace_emit(VGPU_EV_QUEUE, d, 1, want);
       }
       continue;
     }
-    if (L.spatial && L.large_wins >= 3) {
+    if (!want_own && L.spatial) {
       uint64_t none[4];
       board_claim_cus(L.board, L.board_slot, 0, 8, allowed, none);
       L.spatial = 0;
-      VLOG_INFO("device %d: large dispatches again: back to the time-shared pool", d);
       trace_emit(VGPU_EV_QUEUE, d, 0, 0);
     }
     if (L.spatial) continue;
     // pool member: every allowed CU nobody claimed
-    uint64_t others[4];
+    uint64_t others[4], mask[VGPU_CU_MASK_WORDS];
     board_claims_of_others(L.board, L.board_slot, others);
     bool full = true;
     for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) {
@@ -506,7 +506,7 @@ void limiter_main() {
         L.win_start = now;
       }
     }
-    if (g_auto_any.load(std::memory_order_relaxed) && now - last_auto >= 200000000ull) {
+    if (g_auto_any.load(std::memory_order_relaxed) && now - last_auto >= 50000000ull) {
       last_auto = now;
       auto_step();
     }
@@ -622,11 +622,8 @@ bool limiter_on_launch(int dev, uint64_t wg, const void* fn, uint32_t kernels) {
     __atomic_fetch_add(&sl->launches, 1, __ATOMIC_RELAXED);
     __atomic_store_n(&sl->last_launch_ns, mono_ns(), __ATOMIC_RELAXED);
   }
-  if (g_auto_any.load(std::memory_order_relaxed) && dev >= 0 && dev < VGPU_MAX_DEVICES && kernels &&
-      g_lim[dev].auto_share) {
-    g_lim[dev].wg_sum.fetch_add(wg, std::memory_order_relaxed);
-    g_lim[dev].kern_n.fetch_add(kernels, std::memory_order_relaxed);
-  }
+  if (g_auto_any.load(std::memory_order_relaxed) && dev >= 0 && dev < VGPU_MAX_DEVICES && g_lim[dev].auto_share)
+    g_lim[dev].kern_n.fetch_add(1, std::memory_order_relaxed);  // progress: one step of a graph replay, or one kernel
   const bool throttling = g_throttle_any.load(std::memory_order_relaxed) != 0;
   if (__builtin_expect(!throttling && !trace_on(), 1)) return false;
   const bool exempt = throttling && exempt_kernel(fn);

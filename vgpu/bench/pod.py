@@ -205,6 +205,8 @@ def main(argv=None) -> int:
     ap.add_argument("--conv", choices=("native", "miopen"), default="native",
                     help="ResNet convolutions: fused MFMA kernels (native) or MIOpen + fused epilogues")
     ap.add_argument("--no-wait", action="store_true", help="do not wait for GO on stdin")
+    ap.add_argument("--warmup-seconds", type=float, default=0.0,
+                    help="keep warming up until this long has passed (lets the adaptive share policy settle)")
     ap.add_argument("--seconds", type=float, default=0.0,
                     help="run steps for this long instead of exactly --steps (share measurements)")
     args = ap.parse_args(argv)
@@ -226,8 +228,12 @@ def main(argv=None) -> int:
     else:
         w, step = build(args)
         sync = torch.cuda.synchronize
+    t_w = time.monotonic()
     for _ in range(args.warmup):
         step()
+    while time.monotonic() - t_w < args.warmup_seconds:
+        step()
+        sync()
     sync()
     if cpu:
         emit("READY", {"pod": args.pod_index, "init_s": time.time() - t_init, "pid": os.getpid()})

@@ -44,8 +44,10 @@ SCENARIOS = {
     "vgpu-cu25": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000"],
     "vgpu-cu25-temporal": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "temporal"],
     "vgpu-cu25-mask": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "mask"],
-    "vgpu-cu25-auto": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "auto"],
-    "vgpu-auto": ["--pods", "2", "--gpucores", "50", "--gpumem", "144000", "--cu-share", "auto"],
+    "vgpu-cu25-auto": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "auto",
+                       "--warmup-seconds", "6"],
+    "vgpu-auto": ["--pods", "2", "--gpucores", "50", "--gpumem", "144000", "--cu-share", "auto",
+                  "--warmup-seconds", "6"],
     "vgpu-vmem": ["--pods", "2", "--gpucores", "0", "--gpumem", "230000", "--oversubscribe",
                   "--memory-scaling", "1.8"],
     "vgpu-cu25-k2": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "temporal",

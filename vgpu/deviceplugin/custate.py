@@ -31,10 +31,11 @@ that wants exclusive CUs on a temporal node).
   masks, which is exact spatial isolation at equal throughput for two sharers.
   Later containers join the pool.
 * ``auto``: every fractional container starts as a pool member (like
-  ``temporal``); a member whose dispatches turn out too small to fill the GPU
-  claims CUs of its own on the share board at run time and runs there
-  unthrottled, the others shrink to the rest (native/shim/limiter.cpp
-  auto_step).  Spatial where it pays, temporal where it does not.
+  ``temporal``); once two or more are busy, the pods of the GPU measure a
+  window time-shared and a window with each on an XCD-balanced claim of its
+  share's CUs (share-board A/B, native/shim/limiter.cpp auto_step) and keep
+  whichever ran their dispatches faster.  Spatial where it pays, temporal
+  where it does not; re-measured when the set of busy pods changes.
 
 The pool of a device is every CU not held by a masked container; pool members
 share it in time. The shim scales a pool member's time limit by
