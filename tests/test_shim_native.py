@@ -415,7 +415,7 @@ def test_fair_share_board_two_pods_use_whole_gpu(native_build, tmp_path):
     agg = _duty(a) + _duty(b)
     assert agg > 0.9, (a, b)
     assert abs(_duty(a) - 0.5) < 0.075 and abs(_duty(b) - 0.5) < 0.075
-    assert (tmp_path / "lock" / "GPU-test.v2.board").exists()
+    assert (tmp_path / "lock" / "GPU-test.v3.board").exists()
 
 
 def test_foreign_board_layout_is_never_reinitialised(native_build, tmp_path):
@@ -425,7 +425,7 @@ def test_foreign_board_layout_is_never_reinitialised(native_build, tmp_path):
     import struct
     lock = tmp_path / "lock"
     lock.mkdir()
-    board = lock / "GPU-test.v2.board"
+    board = lock / "GPU-test.v3.board"
     foreign = struct.pack("<IIIi", 0x56424F44, 7, 4096, 1) + bytes(range(256)) * 16
     board.write_bytes(foreign)
     a, b = _pair(tmp_path, 50, board=True)
