@@ -79,7 +79,7 @@ def make_parser() -> argparse.ArgumentParser:
                     help="ResNet convolutions: fused MFMA implicit-GEMM kernels or MIOpen")
     ap.add_argument("--hw-queues", type=int, default=1,
                     help="GPU_MAX_HW_QUEUES per pod (vGPU HW-queue budget; 0 = runtime default)")
-    ap.add_argument("--cu-share", choices=("hybrid", "mask", "temporal", "auto", "group2", "group2i"), default="temporal",
+    ap.add_argument("--cu-share", choices=("hybrid", "mask", "temporal", "auto", "group2", "group2i"), default="auto",
                     help="compute-share policy of fractional pods: the device plugin's "
                          "(hybrid|mask|temporal, vgpu/deviceplugin/custate.py) or an A/B tool")
     ap.add_argument("--core-policy", choices=("default", "force", "disable"), default="default",

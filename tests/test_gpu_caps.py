@@ -17,8 +17,11 @@ def test_hipmallocasync_backend_never_exceeds_the_cap(gpu_build):
                                              "PYTORCH_HIP_ALLOC_CONF": "backend:cudaMallocAsync"}, timeout=900)
     assert "error" not in res, res
     cap = cap_mib << 20
-    # amdgpu's own VRAM counter, this process's whole footprint (context included)
-    assert res["peak_over_baseline"] <= cap * 1.01, res
+    # KFD's per-process VRAM counter: every buffer object of this process, the
+    # runtime's own included (amdgpu's device-wide mem_info_vram_used lags frees
+    # by seconds and counts other processes: scripts/mempool_probe.py)
+    assert res["kfd_files"], res
+    assert res["kfd_vram_peak"] <= cap * 1.01, res
     assert res["max_live_reached"] >= 0.75 * cap, res  # the cap is reachable
     assert res["ooms"] >= 6 and res["graphs_replayed"] >= 1, res
 

@@ -21,6 +21,7 @@ the library is loaded in the process.
 """
 from __future__ import annotations
 
+import glob
 import json
 import os
 import sys
@@ -399,17 +400,38 @@ def asynccap(cap_mib: int = 8192, graph_mib: int = 1024) -> dict:
         hip.hipMemPoolGetAttribute(pool, a, ctypes.byref(v))
         return v.value
 
+    # KFD's own per-process VRAM counter (/sys/class/kfd/kfd/proc/<host pid>/vram_<gpu id>):
+    # updated when a buffer object is created or destroyed, unlike amdgpu's
+    # device-wide mem_info_vram_used, which lags frees and counts other processes.
+    selfpid = ctypes.CDLL(None).vgpu_self_host_pid  # int vgpu_self_host_pid(int* src)
+    src = ctypes.c_int(0)
+    hp = selfpid(ctypes.byref(src)) or os.getpid()
+    kfd_files = glob.glob(f"/sys/class/kfd/kfd/proc/{hp}/vram_*")
+    kfd_peak = 0
+
+    def kfd_vram() -> int:
+        tot = 0
+        for f in kfd_files:
+            try:
+                tot += int(open(f).read())
+            except (OSError, ValueError):
+                pass
+        return tot
+
     def sample():
-        nonlocal peak, samples
+        nonlocal peak, samples, kfd_peak
         torch.cuda.synchronize()
         v = int(open(path).read()) - baseline
         peak = max(peak, v)
+        k = kfd_vram()
+        kfd_peak = max(kfd_peak, k)
         samples += 1
-        ph = phases.setdefault(phase, {"peak_over_baseline": 0})
-        if v >= ph["peak_over_baseline"]:
+        ph = phases.setdefault(phase, {"kfd_peak": 0})
+        if k >= ph["kfd_peak"]:
             st = shim_stats() or {}
-            ph.update({"peak_over_baseline": v, "pool_reserved": pool_attr(5), "pool_used": pool_attr(7),
-                       "shim_total": st.get("total"), "torch_reserved": torch.cuda.memory_reserved()})
+            ph.update({"kfd_peak": k, "vram_used_over_baseline": v, "pool_reserved": pool_attr(5),
+                       "pool_used": pool_attr(7), "shim_total": st.get("total"),
+                       "torch_reserved": torch.cuda.memory_reserved()})
 
     rng = random.Random(0)
     MiB = 1 << 20
@@ -461,6 +483,7 @@ def asynccap(cap_mib: int = 8192, graph_mib: int = 1024) -> dict:
         del g
         sample()
     return {"cap": cap_mib * MiB, "baseline": baseline, "peak_over_baseline": peak, "samples": samples,
+            "kfd_vram_peak": kfd_peak, "kfd_files": kfd_files,
             "max_live_reached": reached, "ooms": ooms, "graphs_replayed": graph_ok, "y": float(y),
             "backend": os.environ.get("PYTORCH_HIP_ALLOC_CONF", ""), "phases": phases}
 

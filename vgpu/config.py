@@ -60,14 +60,16 @@ class DevicePluginConfig:
     partition_strategy: str = "single"
     partition_memory: str = "split"       # split: NPS domain memory / partitions sharing it | reported
     # How a fractional vGPU's compute share is enforced (vgpu/deviceplugin/custate.py):
-    #   temporal  (default) no per-container mask: the shim's GPU-time limiter with
-    #             work-conserving fair-share charging — the reference's time-sliced SM
-    #             limit; measured best or equal on 2 x 50 % and 4 x 25 % (docs/benchmarks.md)
+    #   auto      (default) pool members that measure, per GPU, time sharing against
+    #             CUs of their own (share-board A/B) and keep the faster: >= 0.98 x
+    #             exclusive on all 10 ai-benchmark tests at 4 x 25 % (docs/benchmarks.md)
+    #   temporal  no per-container mask: the shim's GPU-time limiter with
+    #             work-conserving fair-share charging (the reference's time-sliced SM limit)
     #   mask      an XCD-balanced CU mask per container (spatial isolation; temporal only
     #             when no granules are free)
     #   hybrid    CU masks for the first `max_mask_slots` fractional containers of a GPU, the
     #             rest share the remaining CUs (one pool mask) under the temporal limiter
-    cu_share: str = "temporal"
+    cu_share: str = "auto"
     max_mask_slots: int = 2
     # Temporal pool: at most this many pool members of one GPU run at a time,
     # taking turns of pool_quantum_ms (VGPU_POOL_CONCURRENCY; 0 = all at once).

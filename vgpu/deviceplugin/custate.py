@@ -15,7 +15,7 @@ profiles/sharing_4way_r1.md and profiles/temporal_r2.md):
 
 * ``mask``: every fractional container gets its own XCD-balanced CU mask.
   When no granules are free, the container gets the pool instead.
-* ``temporal`` (default): no per-container masks. Every fractional container
+* ``temporal``: no per-container masks. Every fractional container
   is a pool member: the shim's GPU-time limiter, charged through the per-GPU
   fair-share board. It throttles only under contention (work-conserving) and
   is the reference's time-sliced SM limit. On MI355X, 4 x 25 % temporal pods
@@ -74,7 +74,7 @@ class ShareGrant:
 
 
 class CUMaskState:
-    def __init__(self, containers_dir: str, layout: CULayout = MI355X, policy: str = "temporal",
+    def __init__(self, containers_dir: str, layout: CULayout = MI355X, policy: str = "auto",
                  max_mask_slots: int = 2, pack: str | None = None):
         if policy not in POLICIES:
             raise ValueError(f"cu_share policy must be one of {POLICIES}, got {policy!r}")
