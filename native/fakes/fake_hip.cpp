@@ -171,6 +171,8 @@ hsa_status_t first_pool(hsa_amd_memory_pool_t p, void* data) {
   return HSA_STATUS_SUCCESS;
 }
 
+void kfd_publish(int dev);
+
 void init_locked() {
   if (g_inited) return;
   g_inited = true;
@@ -194,12 +196,29 @@ void init_locked() {
               HSA_STATUS_SUCCESS)
         g_devs[i].used += runtime_alloc;
     }
+    kfd_publish(i);
   }
 }
 
 void init() {
   std::lock_guard<std::mutex> g(g_mu);
   init_locked();
+}
+
+// Fake KFD per-process VRAM counter (/sys/class/kfd/kfd/proc/<pid>/vram_<gpu id>):
+// with VGPU_FAKE_KFD_RUNTIME=<bytes> the device's used bytes plus that much
+// runtime-owned memory the HIP hooks never see (queues' context-save areas).
+void kfd_publish(int dev) {
+  static const char* rt = getenv("VGPU_FAKE_KFD_RUNTIME");
+  const char* dir = getenv("VGPU_KFD_PROC_DIR");
+  const char* hp = getenv("VGPU_FAKE_HOST_PID");
+  if (!rt || !dir || !hp) return;
+  char path[512];
+  snprintf(path, sizeof path, "%s/%s/vram_%d", dir, hp, 1000 + dev);
+  if (FILE* f = fopen(path, "w")) {
+    fprintf(f, "%llu\n", (unsigned long long)(g_devs[dev].used + strtoull(rt, nullptr, 10)));
+    fclose(f);
+  }
 }
 
 hipError_t dev_alloc(void** p, size_t size, int dev) {
@@ -211,6 +230,7 @@ hipError_t dev_alloc(void** p, size_t size, int dev) {
   if (hsa_amd_memory_pool_allocate(g_devs[dev].pool, size, 0, &hp) != HSA_STATUS_SUCCESS || !hp)
     return hipErrorOutOfMemory;
   g_devs[dev].used += size;
+  kfd_publish(dev);
   uintptr_t a = (uintptr_t)hp;
   g_allocs[a] = {dev, size};
   *p = (void*)a;
@@ -223,6 +243,7 @@ hipError_t dev_free(void* p) {
   auto it = g_allocs.find((uintptr_t)p);
   if (it == g_allocs.end()) return hipErrorInvalidValue;
   g_devs[it->second.first].used -= it->second.second;
+  kfd_publish(it->second.first);
   g_allocs.erase(it);
   hsa_amd_memory_pool_free(p);
   return hipSuccess;
@@ -403,17 +424,25 @@ struct FakePool {
   uint64_t reserved = 0;
 };
 std::map<int, FakePool> g_pools;
-std::map<unsigned long long, uint64_t> g_cap_alloc;  // capture id -> bytes
+// capture id -> peak bytes live at once (free nodes let the graph pool reuse memory)
+struct CapAlloc {
+  uint64_t live = 0, peak = 0;
+};
+std::map<unsigned long long, CapAlloc> g_cap_alloc;
+std::map<uintptr_t, std::pair<unsigned long long, uint64_t>> g_cap_ptr;  // captured block -> (cid, size)
 uint64_t g_graph_mem[16] = {};
 hipError_t pool_alloc(void** p, size_t size, hipStream_t s) {
   {
     std::lock_guard<std::mutex> lk(g_cap_mu);
     auto it = g_capturing.find(s);
     if (it != g_capturing.end()) {  // graph alloc node: a VA now, memory at launch
-      g_cap_alloc[g_capture_id[s]] += size;
+      CapAlloc& ca = g_cap_alloc[g_capture_id[s]];
+      ca.live += size;
+      ca.peak = std::max(ca.peak, ca.live);
       std::lock_guard<std::mutex> g(g_mu);
       uintptr_t a = g_next | (1ull << 44);
       g_next += ((size + 4095) / 4096) * 4096 + 4096;
+      g_cap_ptr[a] = {g_capture_id[s], size};
       *p = (void*)a;
       return hipSuccess;
     }
@@ -437,6 +466,15 @@ hipError_t pool_alloc(void** p, size_t size, hipStream_t s) {
   fp.live[a] = size;
   *p = (void*)a;
   return hipSuccess;
+}
+bool cap_free(void* p) {  // a free node of the capture that allocated the block
+  std::lock_guard<std::mutex> lk(g_cap_mu);
+  auto it = g_cap_ptr.find((uintptr_t)p);
+  if (it == g_cap_ptr.end()) return false;
+  auto ca = g_cap_alloc.find(it->second.first);
+  if (ca != g_cap_alloc.end()) ca->second.live -= std::min(ca->second.live, it->second.second);
+  g_cap_ptr.erase(it);
+  return true;
 }
 bool pool_free(void* p) {
   std::lock_guard<std::mutex> g(g_mu);
@@ -529,7 +567,7 @@ hipError_t hipFree(void* p) {
   return dev_free(p);
 }
 hipError_t hipFreeAsync(void* p, hipStream_t) {
-  if (pool_free(p)) return hipSuccess;
+  if (cap_free(p) || pool_free(p)) return hipSuccess;
   return dev_free(p);
 }
 
@@ -652,10 +690,12 @@ hipError_t hipStreamEndCapture(hipStream_t s, hipGraph_t* g) {
   g_capture_id.erase(s);
   if (!invalid && g) {
     auto* fg = new FakeGraph;
-    fg->alloc_bytes = g_cap_alloc[cid];
+    fg->alloc_bytes = g_cap_alloc[cid].peak;
     *g = reinterpret_cast<hipGraph_t>(fg);
   }
   g_cap_alloc.erase(cid);
+  for (auto it = g_cap_ptr.begin(); it != g_cap_ptr.end();)
+    it = it->second.first == cid ? g_cap_ptr.erase(it) : std::next(it);
   return invalid ? hipErrorStreamCaptureInvalidated : hipSuccess;
 }
 hipError_t hipGraphDestroy(hipGraph_t g) {

@@ -298,6 +298,7 @@ __attribute__((visibility("default"))) hipError_t hipFree(void* ptr) {
 
 __attribute__((visibility("default"))) hipError_t hipFreeAsync(void* ptr, hipStream_t stream) {
   ensure_init();
+  pools_capture_free(ptr);
   Alloc a;
   if (uncharge(ptr, &a) && a.kind == kHostSpill) {
     (void)REAL_HIP(hipStreamSynchronize)(stream);
@@ -345,6 +346,7 @@ __attribute__((visibility("default"))) hipError_t hipMemGetInfo(size_t* free_b, 
   uint64_t lim = mem_limit(dev);
   if (lim == 0) return rc;
   State& s = st();
+  mem_sync_runtime(dev);
   uint64_t used = mem_used(dev);
   uint64_t vfree = used >= lim ? 0 : lim - used;
   bool over = s.region && s.region->oversubscribe;

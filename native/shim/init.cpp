@@ -76,6 +76,7 @@ static void atfork_child() {
     s.ledger.clear();
   }
   for (auto& t : s.dev_touched) t.store(0);
+  mem_after_fork();
   trace_after_fork();
 }
 
@@ -87,6 +88,10 @@ static void do_init() {
   s.report_masked_cus = env_bool(env_first("VGPU_REPORT_MASKED_CUS"), false);
   s.active_oom_killer = env_bool(env_first("ACTIVE_OOM_KILLER"), false);
   s.context_charge = parse_mem(env_first("VGPU_CONTEXT_CHARGE"));
+  s.ctx_measure = env_bool(env_first("VGPU_CONTEXT_MEASURE"), true);
+  s.ctx_max = parse_mem(env_first("VGPU_CONTEXT_MAX"));
+  if (!s.ctx_max) s.ctx_max = 4ull << 30;
+  for (auto& f : s.kfd_vram_fd) f.store(-2);
   s.enabled = !disabled;
   if (!s.enabled) {
     VLOG_INFO("vgpu control disabled by environment");

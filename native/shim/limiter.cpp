@@ -515,6 +515,7 @@ void limiter_main() {
     if (now - last_pool >= 50000000ull) {
       last_pool = now;
       if (pools_any()) pools_sync(false);
+      for (int d = 0; d < VGPU_MAX_DEVICES; ++d) mem_sync_runtime(d);
     }
     // Re-apply CU masks when the region's masks change (elastic resizing by
     // the node monitor / device plugin).

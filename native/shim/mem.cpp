@@ -8,12 +8,16 @@
 // Here: the charge is RESERVED in the shared region under the robust lock
 // before the real allocator runs (so two processes racing for the last bytes
 // cannot both win), and released if the real call fails.
+#include <fcntl.h>
 #include <signal.h>
+#include <unistd.h>
 
 #include "common.h"
 #include "state.h"
 
 namespace vgpu {
+
+uint32_t cumask_driver_uid(int dev);  // KFD gpu_id of a device, 0 = unknown
 
 uint64_t mem_limit(int dev) {
   State& s = st();
@@ -69,6 +73,7 @@ static bool mem_reserve_once(int dev, uint64_t size, int kind, bool quiet);
 // Reserve `size` against the container's cap.  Before refusing, memory that
 // stream-ordered pools hold for reuse is trimmed and re-read (pools.cpp).
 bool mem_reserve(int dev, uint64_t size, int kind) {
+  if (mem_limit(dev)) mem_sync_runtime(dev);
   if (mem_reserve_once(dev, size, kind, true)) return true;
   if (pools_any()) {
     pools_sync(true);
@@ -166,12 +171,94 @@ bool ledger_take(void* p, Alloc* out) {
 
 void charge_context(int dev) {
   State& s = st();
-  if (!s.enabled || dev < 0 || dev >= VGPU_MAX_DEVICES || s.context_charge == 0) return;
+  if (!s.enabled || dev < 0 || dev >= VGPU_MAX_DEVICES) return;
   int expected = 0;
   if (!s.dev_touched[dev].compare_exchange_strong(expected, 1)) return;
-  if (vgpu_proc_slot_t* sl = my_slot()) {
-    __atomic_fetch_add(&sl->used[dev].context_bytes, s.context_charge, __ATOMIC_RELAXED);
-    __atomic_fetch_add(&sl->used[dev].total_bytes, s.context_charge, __ATOMIC_RELAXED);
+  vgpu_proc_slot_t* sl = my_slot();
+  if (!sl || s.context_charge == 0) return;
+  std::lock_guard<std::mutex> g(s.ctx_mu);
+  __atomic_fetch_add(&sl->used[dev].context_bytes, s.context_charge, __ATOMIC_RELAXED);
+  __atomic_fetch_add(&sl->used[dev].total_bytes, s.context_charge, __ATOMIC_RELAXED);
+  s.ctx_booked[dev] += s.context_charge;
+}
+
+// The runtime's own VRAM is invisible to the allocation hooks: every hardware
+// queue carries a context-save area sized for all 256 CUs (~0.5 GB per queue on
+// MI355X, measured: scripts/pool_kfd_probe.py), the stream-ordered pools' VM
+// heap keeps physical slack, code objects and scratch live in VRAM.  The
+// reference books a fixed context size; here KFD's per-process counter
+// (/sys/class/kfd/kfd/proc/<host pid>/vram_<gpu id>, updated as buffer objects
+// are created and destroyed) minus the ledger's charge IS that overhead.  It is
+// booked as context bytes, between VGPU_CONTEXT_CHARGE and VGPU_CONTEXT_MAX
+// (the upper bound guards against counters that also hold imported buffers).
+static int kfd_vram_fd(int dev) {
+  State& s = st();
+  int fd = s.kfd_vram_fd[dev].load(std::memory_order_acquire);
+  if (fd != -2) return fd;
+  // Not there yet (host pid unresolved, no KFD entry): look again at most every 100 ms.
+  static std::atomic<uint64_t> next_try[VGPU_MAX_DEVICES];
+  const uint64_t now = mono_ns();
+  if (now < next_try[dev].load(std::memory_order_relaxed)) return -1;
+  next_try[dev].store(now + 100000000ull, std::memory_order_relaxed);
+  int src = 0;
+  int pid = self_host_pid(&src);
+  if (src == VGPU_HOSTPID_UNVERIFIED) {
+    vgpu_proc_slot_t* sl = my_slot();
+    if (!sl || __atomic_load_n(&sl->host_pid_src, __ATOMIC_ACQUIRE) == VGPU_HOSTPID_UNVERIFIED)
+      return -1;  // not known yet: try again later
+    pid = __atomic_load_n(&sl->host_pid, __ATOMIC_RELAXED);
+  }
+  const uint32_t uid = cumask_driver_uid(dev);
+  if (pid <= 0 || !uid) return -1;
+  char path[512];
+  snprintf(path, sizeof path, "%s/%d/vram_%u", kfd_proc_dir(), pid, uid);
+  fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -1;
+  int expected = -2;
+  if (!s.kfd_vram_fd[dev].compare_exchange_strong(expected, fd)) {
+    if (fd >= 0) close(fd);
+    return expected;
+  }
+  VLOG_DEBUG("device %d: runtime VRAM measured from %s", dev, path);
+  return fd;
+}
+
+void mem_sync_runtime(int dev) {
+  State& s = st();
+  vgpu_proc_slot_t* sl = my_slot();
+  if (!s.enabled || !sl || !s.ctx_measure || dev < 0 || dev >= VGPU_MAX_DEVICES) return;
+  if (!s.dev_touched[dev].load(std::memory_order_relaxed)) return;
+  const int fd = kfd_vram_fd(dev);
+  if (fd < 0) return;
+  char buf[32];
+  const ssize_t n = pread(fd, buf, sizeof buf - 1, 0);
+  if (n <= 0) return;
+  buf[n] = 0;
+  const uint64_t kfd = strtoull(buf, nullptr, 10);
+  std::lock_guard<std::mutex> g(s.ctx_mu);
+  uint64_t& booked = s.ctx_booked[dev];
+  const uint64_t total = __atomic_load_n(&sl->used[dev].total_bytes, __ATOMIC_RELAXED);
+  const uint64_t seen = total > booked ? total - booked : 0;
+  uint64_t want = kfd > seen ? kfd - seen : 0;
+  want = std::min(std::max(want, s.context_charge), std::max(s.ctx_max, s.context_charge));
+  if (want == booked) return;
+  if (want > booked) {
+    __atomic_fetch_add(&sl->used[dev].context_bytes, want - booked, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&sl->used[dev].total_bytes, want - booked, __ATOMIC_RELAXED);
+  } else {
+    __atomic_fetch_sub(&sl->used[dev].context_bytes, booked - want, __ATOMIC_RELAXED);
+    __atomic_fetch_sub(&sl->used[dev].total_bytes, booked - want, __ATOMIC_RELAXED);
+  }
+  booked = want;
+}
+
+void mem_after_fork() {
+  State& s = st();
+  new (&s.ctx_mu) std::mutex();
+  for (int d = 0; d < VGPU_MAX_DEVICES; ++d) {
+    s.ctx_booked[d] = 0;
+    const int fd = s.kfd_vram_fd[d].exchange(-2);
+    if (fd >= 0) close(fd);
   }
 }
 

@@ -16,11 +16,13 @@
 //     refused for lack of room every pool is trimmed (hipMemPoolTrimTo) and
 //     re-read, and the limiter thread re-reads them every 50 ms;
 //   * launches captured into a graph are not charged at capture; an executable
-//     graph's alloc nodes (sizes recorded at capture) are checked against the
-//     cap before each hipGraphLaunch, and the device's graph pool
+//     graph's alloc nodes (the peak of bytes live at once between the captured
+//     hipMallocAsync / hipFreeAsync calls) are checked against the cap before
+//     each hipGraphLaunch, and the device's graph pool
 //     (hipGraphMemAttrReservedMemCurrent) is charged after it.
 // Page-locked host memory is booked per process (pinned_host_bytes) and refused
 // past VGPU_PINNED_HOST_LIMIT (MiB, container-wide) when set.
+#include <algorithm>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -41,9 +43,15 @@ struct PoolCharge {
 std::mutex g_pmu;
 std::unordered_map<const void*, PoolCharge> g_pools;  // hipMemPool_t -> charge
 uint64_t g_graph_charged[VGPU_MAX_DEVICES] = {};      // device graph pool charge
-// Graph alloc nodes: bytes allocated by captured hipMallocAsync, per capture id,
-// then per graph, then per executable.
-std::unordered_map<unsigned long long, uint64_t> g_cap_bytes;
+// Graph alloc nodes: the peak of bytes live at once among a capture's
+// hipMallocAsync / hipFreeAsync pairs (a graph's free nodes let the graph pool
+// reuse memory inside one launch), per capture id, then per graph, then per
+// executable.
+struct CapMem {
+  uint64_t live = 0, peak = 0;
+};
+std::unordered_map<unsigned long long, CapMem> g_cap_mem;
+std::unordered_map<const void*, std::pair<unsigned long long, uint64_t>> g_cap_ptrs;  // ptr -> (cid, size)
 std::unordered_map<const void*, uint64_t> g_graph_bytes, g_exec_bytes;
 
 uint64_t pool_reserved(hipMemPool_t pool) {
@@ -120,7 +128,10 @@ hipError_t pool_alloc_async(void** ptr, size_t size, hipStream_t stream, hipMemP
     hipError_t rc = real(ptr, size, pool, stream, from_pool);
     if (rc == hipSuccess) {
       std::lock_guard<std::mutex> l(g_pmu);
-      g_cap_bytes[cid] += size;
+      CapMem& m = g_cap_mem[cid];
+      m.live += size;
+      m.peak = std::max(m.peak, m.live);
+      g_cap_ptrs[*ptr] = {cid, (uint64_t)size};
     }
     return rc;
   }
@@ -137,6 +148,8 @@ hipError_t pool_alloc_async(void** ptr, size_t size, hipStream_t stream, hipMemP
     if (!mem_reserve(dev, size, kDeviceBuf)) return hipErrorOutOfMemory;
   }
   hipError_t rc = real(ptr, size, pool, stream, from_pool);
+  VLOG_DEBUG("stream-ordered alloc %zu bytes (pool %p, stream %p, device %d) -> %d", size, (void*)pool,
+             (void*)stream, dev, (int)rc);
   if (rc == hipSuccess && pool) {
     std::lock_guard<std::mutex> l(g_pmu);
     PoolCharge& c = g_pools[(const void*)pool];
@@ -149,12 +162,25 @@ hipError_t pool_alloc_async(void** ptr, size_t size, hipStream_t stream, hipMemP
 }
 
 // ---- graphs -------------------------------------------------------------------------------
+// hipFreeAsync of a block a capture allocated: a free node of that capture.
+void pools_capture_free(const void* ptr) {
+  if (!ptr) return;
+  std::lock_guard<std::mutex> l(g_pmu);
+  auto it = g_cap_ptrs.find(ptr);
+  if (it == g_cap_ptrs.end()) return;
+  auto m = g_cap_mem.find(it->second.first);
+  if (m != g_cap_mem.end()) m->second.live -= std::min(m->second.live, it->second.second);
+  g_cap_ptrs.erase(it);
+}
+
 void pools_capture_ended(unsigned long long cid, hipGraph_t graph) {
   std::lock_guard<std::mutex> l(g_pmu);
-  auto it = g_cap_bytes.find(cid);
-  if (it == g_cap_bytes.end()) return;
-  if (graph) g_graph_bytes[graph] += it->second;
-  g_cap_bytes.erase(it);
+  for (auto it = g_cap_ptrs.begin(); it != g_cap_ptrs.end();)
+    it = it->second.first == cid ? g_cap_ptrs.erase(it) : std::next(it);
+  auto it = g_cap_mem.find(cid);
+  if (it == g_cap_mem.end()) return;
+  if (graph) g_graph_bytes[graph] += it->second.peak;
+  g_cap_mem.erase(it);
 }
 
 void pools_graph_instantiated(hipGraph_t graph, hipGraphExec_t exec) {
@@ -242,7 +268,8 @@ void pools_after_fork() {
   new (&g_pmu) std::mutex();
   g_pools.clear();
   for (auto& c : g_graph_charged) c = 0;
-  g_cap_bytes.clear();
+  g_cap_mem.clear();
+  g_cap_ptrs.clear();
   g_graph_bytes.clear();
   g_exec_bytes.clear();
 }

@@ -57,6 +57,13 @@ struct State {
   std::atomic<int> suspended{0};
   std::atomic<int64_t> ipc_imported[VGPU_MAX_DEVICES] = {};  // bytes mapped from other processes
   std::atomic<int> dev_touched[VGPU_MAX_DEVICES] = {};
+  // Measured runtime memory (mem_sync_runtime): the context charge currently
+  // booked per device, and the KFD per-process VRAM counter it is measured from.
+  bool ctx_measure = true;        // VGPU_CONTEXT_MEASURE
+  uint64_t ctx_max = 0;           // VGPU_CONTEXT_MAX (default 4 GiB)
+  std::mutex ctx_mu;
+  uint64_t ctx_booked[VGPU_MAX_DEVICES] = {};
+  std::atomic<int> kfd_vram_fd[VGPU_MAX_DEVICES];
 };
 
 State& st();
@@ -85,6 +92,11 @@ uint64_t mem_limit(int dev);          // 0 = unlimited
 void ipc_import_account(int dev, int64_t delta);
 uint64_t mem_used(int dev);           // container-wide HBM + host charge
 void charge_context(int dev);         // first-touch context charge
+// Re-measure the runtime's own VRAM on `dev` (queues and their context-save
+// areas, VM-heap slack, code objects ...): KFD's per-process counter minus what
+// the ledger already charges becomes the context charge.
+void mem_sync_runtime(int dev);
+void mem_after_fork();
 
 // Compute limiting ------------------------------------------------------------
 void limiter_start();
@@ -109,6 +121,7 @@ void limiter_stats(int dev, uint64_t* charged_ns, uint64_t* busy_ns);
 hipError_t pool_alloc_async(void** ptr, size_t size, hipStream_t stream, hipMemPool_t pool,
                             hipError_t (*real)(void**, size_t, hipMemPool_t, hipStream_t, bool));
 void pools_sync(bool trim);
+void pools_capture_free(const void* ptr);  // hipFreeAsync of a block allocated in a capture
 bool pools_any();
 void pools_capture_ended(unsigned long long capture_id, hipGraph_t graph);
 void pools_graph_instantiated(hipGraph_t graph, hipGraphExec_t exec);

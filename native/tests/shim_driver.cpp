@@ -245,6 +245,30 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (sc == "runtime_vram") {
+    // 1 GiB buffers until the cap refuses one; the runtime's unseen VRAM
+    // (fake KFD counter) must count against the cap as context bytes.
+    auto self_region = sym<void* (*)()>("vgpu_self_region");
+    auto self_slot = sym<int (*)()>("vgpu_self_slot");
+    std::vector<void*> ps;
+    for (int i = 0; i < 64; ++i) {
+      void* p = nullptr;
+      if (hipMalloc(&p, 1ull << 30) != hipSuccess) break;
+      ps.push_back(p);
+    }
+    printf("buffers=%zu\n", ps.size());
+    size_t f = 0, t = 0;
+    hipMemGetInfo(&f, &t);
+    printf("free=%zu\n", f);
+    auto* r = (vgpu_shared_region_t*)self_region();
+    printf("context_bytes=%llu\n", (unsigned long long)r->procs[self_slot()].used[dev].context_bytes);
+    for (void* p : ps) hipFree(p);
+    hipMemGetInfo(&f, &t);
+    printf("context_after_free=%llu\n", (unsigned long long)r->procs[self_slot()].used[dev].context_bytes);
+    printf("free_after=%zu\n", f);
+    return 0;
+  }
+
   if (sc == "meminfo") {
     size_t f = 0, t = 0;
     hipMemGetInfo(&f, &t);
@@ -493,6 +517,21 @@ int main(int argc, char** argv) {
     make_graph(2 * G, &g2);
     printf("launch2=%d\n", hipGraphLaunch(g2, s0));
     show("launch2");
+    {  // two 3 GiB temporaries one after the other: the graph pool's 3 GiB holds both
+      hipStream_t cs = (hipStream_t)0x33;
+      hipGraph_t g = nullptr;
+      hipGraphExec_t g33;
+      void *q1 = nullptr, *q2 = nullptr;
+      hipStreamBeginCapture(cs, hipStreamCaptureModeGlobal);
+      hipMallocAsync(&q1, 3 * G, cs);
+      hipFreeAsync(q1, cs);
+      hipMallocAsync(&q2, 3 * G, cs);
+      hipFreeAsync(q2, cs);
+      hipStreamEndCapture(cs, &g);
+      hipGraphInstantiate(&g33, g, nullptr, nullptr, 0);
+      printf("launch33=%d\n", hipGraphLaunch(g33, s0));
+      show("launch33");
+    }
     make_graph(6 * G, &g6);
     printf("launch6=%d\n", hipGraphLaunch(g6, s0));  // 4 GiB live + 6 GiB graph pool > 8 GiB
     show("launch6");

@@ -221,11 +221,13 @@ def test_stream_ordered_pool_and_graph_memory_follow_physical_use(native_build):
                             "VGPU_PINNED_HOST_LIMIT": "1g"})
     g = lambda k: int(o[k]) / GiB  # noqa: E731
     assert (o["a"], o["b"], o["c"], o["d"]) == ("0", "0", "0", "0")
-    for k in ("ab", "free_a", "c_reused", "d", "captured", "launch3", "launch2", "launch6"):
+    for k in ("ab", "free_a", "c_reused", "d", "captured", "launch3", "launch2", "launch33", "launch6"):
         assert g(k + "_charge") == g(k + "_phys"), k  # the charge is the physical footprint
     assert g("free_a_charge") == 6 and g("c_reused_charge") == 6  # held by the pool, reused
     assert g("d_charge") == 4  # trimmed, then 4 GiB
     assert g("captured_charge") == 4 and g("launch3_charge") == 7 and g("launch2_charge") == 7
+    # alloc/free pairs inside one graph: the peak live bytes (3 GiB), not their sum (6 GiB)
+    assert o["launch33"] == "0" and g("launch33_charge") == 7
     assert o["launch6"] == "2" and g("launch6_phys") == 4  # hipErrorOutOfMemory, graph pool trimmed
     assert g("peak_phys") <= 8
     assert (o["pin1"], o["pin2"], o["pin3"]) == ("0", "2", "0")
@@ -342,6 +344,25 @@ def test_host_pid_ambiguous_diff_left_unverified(native_build, tmp_path):
     assert o["host_pid"] == "0"
     assert o["slot_host_src"] in ("0", "3")  # unverified (or host namespace on a bare host)
     assert "host pid unresolved: 2 new KFD" in o["_stderr"]
+
+
+def test_runtime_vram_counts_against_the_cap(native_build, tmp_path):
+    """The runtime's own VRAM (queue context-save areas, VM-heap slack) never
+    passes the allocation hooks; KFD's per-process counter minus the ledger is
+    booked as context bytes, so the cap covers what the process really holds."""
+    env = _kfd_env(tmp_path, 777010)
+    env["VGPU_FAKE_KFD_RUNTIME"] = str(600 << 20)
+    o = run("runtime_vram", env=env)
+    assert o["buffers"] == "7", o  # 7 GiB + 0.6 GiB of runtime fit in 8 GiB, 8 GiB would not
+    assert int(o["context_bytes"]) == 600 << 20
+    assert int(o["free"]) == (8 << 30) - (7 << 30) - (600 << 20)
+    assert int(o["context_after_free"]) == 600 << 20
+    assert int(o["free_after"]) == (8 << 30) - (600 << 20)
+    env["VGPU_CONTEXT_MEASURE"] = "0"
+    (tmp_path / "kfdproc" / "777010").rename(tmp_path / "kfdproc" / "old")
+    (tmp_path / "r.cache").unlink()
+    o = run("runtime_vram", env=env)
+    assert o["buffers"] == "8" and o["context_bytes"] == "0"
 
 
 def test_host_pid_without_lock_dir_still_resolves(native_build, tmp_path):
