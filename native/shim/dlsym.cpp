@@ -11,12 +11,15 @@
 // resolves HSA entry points by hand.  A lookup of a hooked name through a
 // handle of one of those libraries returns our interposer instead.
 //
-// RTLD_NEXT must keep its meaning ("the next object after the CALLER"): glibc
-// derives the caller from the return address, so `dlsym` below is a two-way
-// x86-64 trampoline — RTLD_NEXT tail-jumps straight into glibc's dlsym with
-// the caller's return address untouched, everything else tail-jumps into
-// vgpu_dlsym_hook.  Our own code resolves through vgpu::real_dlsym (never the
-// exported dlsym), so the shim never sees itself.
+// RTLD_NEXT and RTLD_DEFAULT must keep their meaning: glibc derives the caller
+// from the return address ("the next object after the caller"; "the caller's
+// lookup scope", which for a library dlopen'ed RTLD_LOCAL includes its own
+// dependencies — ctypes loads libamdhip64 that way, and HIP's stream-ordered
+// pool resolves optional ROCr entry points with RTLD_DEFAULT).  So `dlsym`
+// below is a two-way x86-64 trampoline: both pseudo-handles tail-jump straight
+// into glibc's dlsym with the caller's return address untouched, every real
+// handle tail-jumps into vgpu_dlsym_hook.  Our own code resolves through
+// vgpu::real_dlsym (never the exported dlsym), so the shim never sees itself.
 #include <dlfcn.h>
 #include <link.h>
 #include <pthread.h>
@@ -43,7 +46,7 @@ __attribute__((visibility("hidden"))) void* vgpu_dlsym_next_slow(void* handle, c
 }
 
 #ifndef VGPU_NO_DLSYM_OVERRIDE
-// RTLD_NEXT == (void*)-1 on glibc.
+// RTLD_NEXT == (void*)-1, RTLD_DEFAULT == 0 on glibc.
 __asm__(
     ".text\n"
     ".globl dlsym\n"
@@ -51,7 +54,10 @@ __asm__(
     ".p2align 4\n"
     "dlsym:\n"
     "  cmpq $-1, %rdi\n"
+    "  je 3f\n"
+    "  testq %rdi, %rdi\n"
     "  jne 1f\n"
+    "3:\n"
     "  movq vgpu_real_dlsym_ptr(%rip), %rax\n"
     "  testq %rax, %rax\n"
     "  jz 2f\n"
@@ -160,8 +166,9 @@ extern "C" void* vgpu_dlsym_hook(void* handle, const char* name) {
   return p;
 }
 
-// RTLD_NEXT before our constructor ran (another preload's constructor): the
-// lookup is made relative to this object, which is at most one object off.
+// RTLD_NEXT / RTLD_DEFAULT before our constructor ran (another preload's
+// constructor): the lookup is made relative to this object, which is at most
+// one object off.
 extern "C" void* vgpu_dlsym_next_slow(void* handle, const char* name) {
   return vgpu::real_dlsym(handle, name);
 }

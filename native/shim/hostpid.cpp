@@ -253,7 +253,7 @@ extern "C" {
 
 // Sanitizer runtimes intercept open themselves (host-side race / address
 // checking builds, tests/test_shim_robustness.py): those builds leave it alone.
-#if !defined(__SANITIZE_THREAD__) && !defined(__SANITIZE_ADDRESS__)
+#if !defined(__SANITIZE_THREAD__) && !defined(__SANITIZE_ADDRESS__) && !defined(VGPU_NO_OPEN_HOOK)
 __attribute__((visibility("default"))) int open(const char* path, int flags, ...) {
   mode_t mode = 0;
   if (flags & (O_CREAT | O_TMPFILE)) {

@@ -556,14 +556,20 @@ void priority_gate(vgpu_shared_region_t* r) {
 // kernel must be resident for a collective to progress, so throttling one
 // rank's launches stalls the others (distributed backend row;
 // §7.4 item 8).  A kernel is RCCL's when its host stub lives in librccl (or a
-// library matching VGPU_THROTTLE_EXEMPT).  Decided once per function pointer.
+// library matching VGPU_THROTTLE_EXEMPT).  Decided once per function pointer
+// and launching thread: the cache is thread-local, so a throttled launch takes
+// no lock here (multi-threaded launchers never serialise on it).
 bool exempt_kernel(const void* fn) {
   if (!fn) return false;
-  static std::mutex mu;
-  static std::unordered_map<const void*, bool> cache;
-  std::lock_guard<std::mutex> g(mu);
+  thread_local const void* last_fn = nullptr;
+  thread_local bool last_ex = false;
+  if (fn == last_fn) return last_ex;
+  thread_local std::unordered_map<const void*, bool> cache;
   auto it = cache.find(fn);
-  if (it != cache.end()) return it->second;
+  if (it != cache.end()) {
+    last_fn = fn;
+    return last_ex = it->second;
+  }
   bool ex = false;
   Dl_info di;
   if (dladdr(fn, &di) && di.dli_fname) {
@@ -572,7 +578,8 @@ bool exempt_kernel(const void* fn) {
          (extra && *extra && strstr(di.dli_fname, extra));
   }
   cache.emplace(fn, ex);
-  return ex;
+  last_fn = fn;
+  return last_ex = ex;
 }
 
 }  // namespace

@@ -245,6 +245,14 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (sc == "dlsym_scope") {
+    void* h = dlopen(getenv("SCOPE_LIB"), RTLD_LOCAL | RTLD_NOW);
+    auto lookup = h ? (int (*)())dlsym(h, "scope_lookup") : nullptr;
+    auto linked = h ? (int (*)())dlsym(h, "scope_linked") : nullptr;
+    printf("loaded=%d\nlookup=%d\nlinked=%d\n", h != nullptr, lookup ? lookup() : -2, linked ? linked() : -2);
+    return 0;
+  }
+
   if (sc == "runtime_vram") {
     // 1 GiB buffers until the cap refuses one; the runtime's unseen VRAM
     // (fake KFD counter) must count against the cap as context bytes.

@@ -23,6 +23,9 @@ def main() -> int:
     hip = ctypes.CDLL("libamdhip64.so.7")
     hip.hipSetDevice(0)
     hip.hipFree(ctypes.c_void_p(0))  # context
+    if os.environ.get("PROBE_MALLOC_FIRST"):
+        q = ctypes.c_void_p()
+        print("hipMalloc first:", hip.hipMalloc(ctypes.byref(q), ctypes.c_size_t(2 << 20)), flush=True)
     pid = os.getpid()
     try:
         selfpid = ctypes.CDLL(None).vgpu_self_host_pid

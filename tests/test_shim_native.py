@@ -346,6 +346,16 @@ def test_host_pid_ambiguous_diff_left_unverified(native_build, tmp_path):
     assert "host pid unresolved: 2 new KFD" in o["_stderr"]
 
 
+def test_dlsym_default_keeps_the_callers_scope(native_build):
+    """dlsym(RTLD_DEFAULT, ...) from a library dlopen'ed RTLD_LOCAL finds that
+    library's own dependencies under the shim (glibc searches the caller's
+    scope).  Without it, HIP's stream-ordered pool lost optional ROCr entry
+    points and every hipMallocAsync of a ctypes-loaded HIP failed."""
+    o = run("dlsym_scope", env={"SCOPE_LIB": str(FAKES_DIR / "libscope_user.so")})
+    assert o["loaded"] == "1" and o["linked"] == "42"
+    assert o["lookup"] == "42", o
+
+
 def test_runtime_vram_counts_against_the_cap(native_build, tmp_path):
     """The runtime's own VRAM (queue context-save areas, VM-heap slack) never
     passes the allocation hooks; KFD's per-process counter minus the ledger is

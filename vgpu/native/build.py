@@ -239,6 +239,16 @@ def build_fakes(force: bool = False) -> dict[str, Path]:
             _mark(rccl, [rccl_src])
         res["rccl"] = rccl
 
+    scope_src = NATIVE / "fakes" / "fake_scope.cpp"
+    if scope_src.exists():
+        dep, user = FAKES_OUT / "libscope_dep.so", FAKES_OUT / "libscope_user.so"
+        if force or not _stamp(user, [scope_src]):
+            _run([CXX, *COMMON, "-DSCOPE_DEP", scope_src, "-o", dep, "-shared", "-Wl,-soname,libscope_dep.so"])
+            _run([CXX, *COMMON, scope_src, "-o", user, "-shared", f"-L{FAKES_OUT}", "-l:libscope_dep.so",
+                  f"-Wl,-rpath,{FAKES_OUT}", "-ldl"])
+            _mark(user, [scope_src])
+        res["scope"] = user
+
     drv_src = NATIVE / "tests" / "shim_driver.cpp"
     drv = FAKES_OUT / "shim_driver"
     if force or not _stamp(drv, [drv_src, hip_src, hsa_src] + _headers()):
