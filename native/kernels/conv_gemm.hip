@@ -479,52 +479,33 @@ __device__ __forceinline__ void epilogue_halves(const ConvArgs& a, f32x4_t (&acc
   }
 }
 
-// PRO (block-entry BN+ReLU on the input, 1x1 / pad 0 only, so no padded
-// pixel exists that the prologue would turn non-zero): the raw input is DMA'd
-// like any other, and the per-channel affine + ReLU is applied to each A
-// fragment in registers between its ds_read and its MFMA.  The block's BN
-// scale/shift (C ≤ 2048 floats each) sit in LDS behind the two stages.
-//
 // CSM = 16: a narrow-input conv (the ResNet stem after space-to-depth: C = 16,
 // 4x4 taps) — a 64-wide K step then spans 64/C taps, so each lane derives its
 // own tap from its chunk.
-// NS = LDS stages: the DMA runs NS-1 K steps ahead of the MFMA.  With NS = 2
-// a step's DMA has one step of MFMA (~0.2 µs) to cover an HBM round trip
-// (≈1-2 µs), so every step waits; NS = 3 gives it two, and needs one barrier
-// per step (the barrier after the wait both publishes stage kt and retires
-// the reads of stage kt-1, which the next DMA overwrites).
-template <int KS, int BM, int BN, bool PRO, bool RES, int CSM = 0, int NS = 2>
+// Two LDS stages, one DMA step in flight: the second block per CU covers the
+// DMA latency (a 3-stage ring measured slower on every ResNet-50 shape,
+// profiles/conv_stages_r1.md).  Prologue convs take conv_pro_kernel (an
+// in-register prologue on the DMA'd A fragments measured VALU-bound and slower).
+template <int KS, int BM, int BN, bool RES, int CSM = 0>
 __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a) {
-  static_assert(!PRO || KS == 1, "the in-register prologue needs a padding-free conv");
-  static_assert(CSM == 0 || (!PRO && 64 % CSM == 0 && CSM % 8 == 0), "narrow-C variant");
+  static_assert(CSM == 0 || (64 % CSM == 0 && CSM % 8 == 0), "narrow-C variant");
   constexpr int AR = BM / 32, BR = BN / 32;  // DMA instructions per thread per K step
   constexpr int WTM = BM / 2, WTN = BN / 2;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int CS = BN + 4;
-  constexpr int PIPE = NS * STAGE;
+  constexpr int PIPE = 2 * STAGE;
   constexpr int HROWS = BM / 2, EPI = HROWS * CS * 4;  // epilogue staged in two row halves
   constexpr int BODY = PIPE > EPI ? PIPE : EPI;
-  constexpr int PARAMS = PRO ? 2048 * 2 * 4 : 0;     // scale[C] then shift[C]
-  constexpr int CPR = BN / 8, RSTEP = kThreads / CPR, RROWS = HROWS / RSTEP;
-  __shared__ __attribute__((aligned(16))) char smem[BODY + PARAMS];
+  __shared__ __attribute__((aligned(16))) char smem[BODY];
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int fr = lane & 15, fk = lane >> 4;
   const int lrow = t >> 3, lchunk = (t & 7) ^ (lrow & 7);
-  const int chunk = t % CPR, rfirst = t / CPR;
   int m0, n0;
   tile_origin(a, blockIdx.x, BM, BN, m0, n0);
-
-  float* sPar = reinterpret_cast<float*>(smem + BODY);
-  if constexpr (PRO) {  // before the first DMA: no ordinary load shares the pipeline with it
-    for (int c = t * 4; c < a.C; c += kThreads * 4) {
-      *reinterpret_cast<float4*>(sPar + c) = *reinterpret_cast<const float4*>(a.pscale + c);
-      *reinterpret_cast<float4*>(sPar + a.C + c) = *reinterpret_cast<const float4*>(a.pshift + c);
-    }
-  }
 
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(a.x), 0, a.x_bytes, 0x00020000);
@@ -582,7 +563,6 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (PRO) __syncthreads();  // parameters visible (no DMA in flight yet)
   // Short K loops (stage-1 1x1 convs: one K step) fetch the residual up front,
   // so its latency overlaps the A/B DMA; longer loops fetch it after the loop
   // (measured: early fetch costs 5-20 % on K ≥ 4 steps).
@@ -591,33 +571,16 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
   if constexpr (RES) {
     if (early_res) load_residual<BM, BN>(a, m0, n0, res);
   }
-  if constexpr (NS == 2) {
-    issue(0, 0);
-  } else {
-#pragma unroll
-    for (int p = 0; p < NS - 1; ++p) issue(p < a.ktiles ? p : a.ktiles - 1, p);
-  }
+  issue(0, 0);
   for (int kt = 0; kt < a.ktiles; ++kt) {
-    int st;
-    if constexpr (NS == 2) {
-      st = kt & 1;
-      if (kt + 1 < a.ktiles) {
-        issue(kt + 1, st ^ 1);
-        __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR + BR));
-      } else {
-        __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-      }
-      __builtin_amdgcn_s_barrier();
+    const int st = kt & 1;
+    if (kt + 1 < a.ktiles) {
+      issue(kt + 1, st ^ 1);
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR + BR));
     } else {
-      st = kt % NS;
-      // Steps kt .. kt+NS-2 are in flight; retire step kt.
-      __builtin_amdgcn_s_waitcnt(vmcnt_imm((NS - 2) * (AR + BR)));
-      __builtin_amdgcn_s_barrier();
-      // Past the end the DMA re-fetches the last step into a stage nobody reads
-      // again (it is (kt-1) % NS): the loop stays branch-free around loads.
-      const int kn = kt + NS - 1;
-      issue(kn < a.ktiles ? kn : a.ktiles - 1, kn % NS);
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
     }
+    __builtin_amdgcn_s_barrier();
     const char* sA = smem + st * STAGE;
     const char* sB = sA + A_BYTES;
 #pragma unroll
@@ -629,38 +592,13 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         bfr[j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(wn * WTN + j * 16 + fr, kk * 4 + fk));
-      if constexpr (PRO) {
-        // channels of this lane's 8 k-elements: cb*64 + kk*32 + fk*8 + (0..7)
-        const int c = (kt % a.cblocks) * BK + kk * 32 + fk * 8;
-        const float4 s0 = *reinterpret_cast<const float4*>(sPar + c);
-        const float4 s1 = *reinterpret_cast<const float4*>(sPar + c + 4);
-        const float4 h0 = *reinterpret_cast<const float4*>(sPar + a.C + c);
-        const float4 h1 = *reinterpret_cast<const float4*>(sPar + a.C + c + 4);
-        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-        const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          float e[8];
-          unpack8(__builtin_bit_cast(u32x4, af[i]), e);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) e[j] = fmaxf(e[j] * sc[j] + sh[j], 0.0f);
-          af[i] = __builtin_bit_cast(bf16x8_t, pack8(e));
-        }
-      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if constexpr (NS == 2) {
-      // Stage st fully read (this wave's ds_reads retired) before any wave refills it.
-      __builtin_amdgcn_s_waitcnt(kLgkm0);
-      __builtin_amdgcn_s_barrier();
-    }
-  }
-  if constexpr (NS > 2) {  // drain the dummy DMAs and all reads before the epilogue reuses LDS
-    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+    // Stage st fully read (this wave's ds_reads retired) before any wave refills it.
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     __builtin_amdgcn_s_barrier();
   }
@@ -874,50 +812,22 @@ hipError_t launch_big(ConvArgs a, hipStream_t s) {
 
 int g_forced_big = -1;  // vgpu_conv_set_big: -1 = env VGPU_CONV_BIG / heuristic, 0 = off, 1 = whenever eligible
 
-int g_forced_stages = -1;
-int g_forced_bm = 0;  // vgpu_conv_set_tile_m (A/B benchmarking); 0 = heuristic  // vgpu_conv_set_stages (A/B benchmarking); -1 = env / default
+int g_forced_bm = 0;  // vgpu_conv_set_tile_m (A/B benchmarking); 0 = heuristic
 
-int glds_stages(int bm, int bn, int ktiles) {
-  if (g_forced_stages < 0) {
-    const char* v = getenv("VGPU_CONV_STAGES");
-    g_forced_stages = v ? atoi(v) : 0;
-  }
-  if (g_forced_stages == 2 || g_forced_stages == 3) return g_forced_stages;
-  // Default 2: on every ResNet-50 shape the 3-stage ring measured slower
-  // (profiles/conv_stages_r1.md) — the second block per CU already covers the
-  // DMA latency, and the third stage costs it LDS.
-  (void)bm; (void)bn; (void)ktiles;
-  return 2;
-}
-
-template <int KS, int BM, int BN, bool PRO, bool RES, int CSM = 0>
+template <int KS, int BM, int BN, bool RES, int CSM = 0>
 hipError_t launch_glds(ConvArgs a, hipStream_t s) {
   a.nM = (a.M + BM - 1) / BM;
   a.nN = a.Cout / BN;
   a.nwg = a.nM * a.nN;
-  if (!PRO && glds_stages(BM, BN, a.ktiles) == 3)
-    hipLaunchKernelGGL((conv_glds_kernel<KS, BM, BN, PRO, RES, CSM, 3>), dim3(a.nwg), dim3(kThreads),
-                       0, s, a);
-  else
-    hipLaunchKernelGGL((conv_glds_kernel<KS, BM, BN, PRO, RES, CSM, 2>), dim3(a.nwg), dim3(kThreads),
-                       0, s, a);
+  hipLaunchKernelGGL((conv_glds_kernel<KS, BM, BN, RES, CSM>), dim3(a.nwg), dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 
-template <int KS, int BM, int BN, bool PRO>
-hipError_t dispatch_glds_r(const ConvArgs& a, bool res, hipStream_t s) {
-  return res ? launch_glds<KS, BM, BN, PRO, true>(a, s) : launch_glds<KS, BM, BN, PRO, false>(a, s);
-}
-
 template <int KS, int BM>
-hipError_t dispatch_glds(const ConvArgs& a, bool pro, bool res, hipStream_t s) {
-  if constexpr (KS == 1) {
-    if (pro)
-      return a.Cout % 128 == 0 ? dispatch_glds_r<1, BM, 128, true>(a, res, s)
-                               : dispatch_glds_r<1, BM, 64, true>(a, res, s);
-  }
-  return a.Cout % 128 == 0 ? dispatch_glds_r<KS, BM, 128, false>(a, res, s)
-                           : dispatch_glds_r<KS, BM, 64, false>(a, res, s);
+hipError_t dispatch_glds(const ConvArgs& a, bool res, hipStream_t s) {
+  if (a.Cout % 128 == 0)
+    return res ? launch_glds<KS, BM, 128, true>(a, s) : launch_glds<KS, BM, 128, false>(a, s);
+  return res ? launch_glds<KS, BM, 64, true>(a, s) : launch_glds<KS, BM, 64, false>(a, s);
 }
 
 // ---- Prologue convs (block-entry BN+ReLU on the input): A through registers,
@@ -1099,173 +1009,6 @@ hipError_t dispatch_pro(const ConvArgs& a, bool res, hipStream_t s) {
     return res ? launch_pro<KS, BM, 128, true>(a, s) : launch_pro<KS, BM, 128, false>(a, s);
   return res ? launch_pro<KS, BM, 64, true>(a, s) : launch_pro<KS, BM, 64, false>(a, s);
 }
-
-// ---- Deep-pipelined prologue conv (1x1) for deep K and few workgroups per CU.
-// conv_pro's two stages give the weight DMA one K step of lead and the
-// activations about one and a half; with 2 blocks per CU that hides an HBM
-// round trip, but the stage-3/4 conv1 and shortcut layers (K = 512-2048, a few
-// hundred 128x128 tiles) leave one block per CU, and each K step then waits
-// for a full round trip (~1.8 us measured against ~0.1 us of MFMA).  Here
-// three LDS stages give the DMA two steps of lead and three activation
-// register sets give the loads three; the extra stage costs LDS (112 KB: one
-// block per CU), which these layers never had room to use anyway.
-// Per K step kt:  DMA B(kt+2) into stage (kt+2)%3; load A(kt+3) into register
-// set kt%3; MFMA on stage kt%3; prologue + ds_write of A(kt+1) (register set
-// (kt+1)%3) into stage (kt+1)%3; vmcnt(2*AR+BR) (= B(kt+1) landed); barrier.
-template <int BM, int BN, bool RES>
-__global__ void __launch_bounds__(kThreads, 1) conv_prodeep_kernel(const ConvArgs a) {
-  constexpr int NS = 3;
-  constexpr int AR = BM / 32, BR = BN / 32;
-  constexpr int WTM = BM / 2, WTN = BN / 2;
-  constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
-  constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int PIPE = NS * STAGE, EPI = (BM / 2) * (BN + 4) * 4;
-  constexpr int BODY = PIPE > EPI ? PIPE : EPI;
-  __shared__ __attribute__((aligned(16))) char smem[BODY + 2048 * 2 * 4];
-  float* sPar = reinterpret_cast<float*>(smem + BODY);
-
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int fr = lane & 15, fk = lane >> 4;
-  const int slot = t & 7, r0 = t >> 3;
-  const int lchunk = slot ^ (r0 & 7);
-  int m0, n0;
-  tile_origin(a, blockIdx.x, BM, BN, m0, n0);
-
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(a.x), 0, a.x_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(a.w), 0, (uint32_t)((int64_t)a.Cout * a.K * 2), 0x00020000);
-
-  int abase[AR];
-  bool aok[AR];
-#pragma unroll
-  for (int i = 0; i < AR; ++i) {
-    const int m = m0 + r0 + 32 * i;
-    aok[i] = m < a.M;
-    const int mm = aok[i] ? m : 0;
-    const int ow = mm % a.OW, t2 = mm / a.OW, oh = t2 % a.OH, n = t2 / a.OH;
-    abase[i] = ((n * a.H + oh * a.stride) * a.W + ow * a.stride) * a.C * 2;  // 1x1, pad 0
-  }
-  const uint32_t boff = (uint32_t)(((n0 + r0) * a.K + lchunk * 8) * 2);
-  for (int c = t * 4; c < a.C; c += kThreads * 4) {
-    *reinterpret_cast<float4*>(sPar + c) = *reinterpret_cast<const float4*>(a.pscale + c);
-    *reinterpret_cast<float4*>(sPar + a.C + c) = *reinterpret_cast<const float4*>(a.pshift + c);
-  }
-  __syncthreads();
-
-  auto issue_b = [&](int kt, int st) {
-    char* sB = smem + st * STAGE + A_BYTES;
-#pragma unroll
-    for (int i = 0; i < BR; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          wr, (lds_void_t*)(sB + (32 * i + wave * 8) * 128), 16,
-          boff + (uint32_t)((32 * i * a.K + kt * BK) * 2), 0, 0, 0);
-  };
-  auto load_a = [&](int kt, u32x4 (&ra)[AR]) {
-    const int toff = (kt * BK + slot * 8) * 2;
-#pragma unroll
-    for (int i = 0; i < AR; ++i)
-      ra[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, aok[i] ? (uint32_t)(abase[i] + toff) : kOOB, 0, 0);
-  };
-  auto store_a = [&](int kt, int st, const u32x4 (&ra)[AR]) {
-    char* sA = smem + st * STAGE;
-    const int c = kt * BK + slot * 8;
-    const float4 s0 = *reinterpret_cast<const float4*>(sPar + c);
-    const float4 s1 = *reinterpret_cast<const float4*>(sPar + c + 4);
-    const float4 h0 = *reinterpret_cast<const float4*>(sPar + a.C + c);
-    const float4 h1 = *reinterpret_cast<const float4*>(sPar + a.C + c + 4);
-    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      float e[8];
-      unpack8(ra[i], e);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float f = fmaxf(e[j] * sc[j] + sh[j], 0.0f);
-        e[j] = aok[i] ? f : 0.0f;  // the M tail stays zero after the prologue
-      }
-      *reinterpret_cast<u32x4*>(sA + swz(r0 + 32 * i, slot)) = pack8(e);
-    }
-  };
-  auto compute = [&](int st, f32x4_t (&acc)[TM][TN]) {
-    const char* sA = smem + st * STAGE;
-    const char* sB = sA + A_BYTES;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8_t af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8_t*>(sA + swz(wm * WTM + i * 16 + fr, kk * 4 + fk));
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(wn * WTN + j * 16 + fr, kk * 4 + fk));
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  f32x4_t acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = a.ktiles;  // the host guarantees nk >= 3
-  u32x4 ra0[AR], ra1[AR], ra2[AR];
-  u32x4 res[2][EpiShape<BM, BN>::RROWS];
-  load_a(0, ra0);
-  issue_b(0, 0);
-  load_a(1, ra1);
-  issue_b(1, 1);
-  load_a(2, ra2);
-  store_a(0, 0, ra0);
-  __builtin_amdgcn_s_waitcnt(vmcnt_imm(2 * AR + BR));  // B(0) landed; B(1), A(1), A(2) in flight
-  __builtin_amdgcn_s_waitcnt(kLgkm0);
-  __builtin_amdgcn_s_barrier();
-  // Past the last K step the loads re-fetch the last tile into a register set /
-  // stage nobody reads again: the body stays branch-free around loads.
-  auto step = [&](int kt, int st, u32x4 (&rl)[AR], u32x4 (&rs)[AR]) {
-    const int k1 = kt + 1 < nk ? kt + 1 : nk - 1;
-    const int k2 = kt + 2 < nk ? kt + 2 : nk - 1;
-    const int k3 = kt + 3 < nk ? kt + 3 : nk - 1;
-    issue_b(k2, st == 0 ? 2 : st - 1);   // (kt+2) % 3
-    load_a(k3, rl);                      // set kt % 3: A(kt) was stored last step
-    compute(st, acc);
-    store_a(k1, st == 2 ? 0 : st + 1, rs);  // A(kt+1) into stage (kt+1) % 3
-    __builtin_amdgcn_s_waitcnt(vmcnt_imm(2 * AR + BR));
-    __builtin_amdgcn_s_waitcnt(kLgkm0);
-    __builtin_amdgcn_s_barrier();
-  };
-  int kt = 0;
-  for (; kt + 2 < nk; kt += 3) {
-    step(kt, 0, ra0, ra1);
-    step(kt + 1, 1, ra1, ra2);
-    step(kt + 2, 2, ra2, ra0);
-  }
-  if (kt < nk) step(kt, 0, ra0, ra1);
-  if (kt + 1 < nk) step(kt + 1, 1, ra1, ra2);
-  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // the trailing dummy loads, before LDS reuse
-  __syncthreads();
-  if constexpr (RES) load_residual<BM, BN>(a, m0, n0, res);
-  epilogue_halves<BM, BN, RES>(a, acc, m0, n0, smem, res);
-}
-
-template <int BM, int BN, bool RES>
-hipError_t launch_prodeep(ConvArgs a, hipStream_t s) {
-  a.nM = (a.M + BM - 1) / BM;
-  a.nN = a.Cout / BN;
-  a.nwg = a.nM * a.nN;
-  hipLaunchKernelGGL((conv_prodeep_kernel<BM, BN, RES>), dim3(a.nwg), dim3(kThreads), 0, s, a);
-  return hipGetLastError();
-}
-
-int g_forced_deep = -1;  // vgpu_conv_set_pro_deep: -1 = env VGPU_CONV_PRO_DEEP (default off), 0 off, 1 when eligible, 2 heuristic
 
 // epilogue_halves for a conv3 chunk whose output also feeds the next block's
 // conv1: besides storing y = acc + residual (bf16), each thread keeps
@@ -1555,15 +1298,6 @@ bool pro_dma_enabled() {
   return on == 1;
 }
 
-bool glds_pro_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* v = getenv("VGPU_CONV_GLDS_PRO");
-    on = (v && v[0] == '1') ? 1 : 0;
-  }
-  return on == 1;
-}
-
 // CUs this process can occupy on the current device — the grid-fill term of
 // the tile choice.  A vGPU pod owns an XCD-balanced CU mask of
 // VGPU_DEVICE_CU_LIMIT_<i> % of the device (the enforcement library's env
@@ -1790,12 +1524,9 @@ VGPU_API int vgpu_stem_space_to_depth(const void* x, void* X, int N, int H, int 
   return (int)hipGetLastError();
 }
 
-// Benchmark knob: LDS stages of the DMA conv (2 or 3; 0 = default).
-VGPU_API void vgpu_conv_set_stages(int n) { g_forced_stages = n; }
 // Benchmark knob: force 64- or 128-row tiles (0 = heuristic).
 VGPU_API void vgpu_conv_set_tile_m(int bm) { g_forced_bm = bm; }
 VGPU_API void vgpu_conv_set_big(int mode) { g_forced_big = mode; }  // -1 env/heuristic, 0 off, 1 when eligible
-VGPU_API void vgpu_conv_set_pro_deep(int mode) { g_forced_deep = mode; }  // -1 env/heuristic, 0 off, 1 when eligible
 
 // Fused conv2 (3x3, pad 1, stride s, C = W → W, bias + ReLU) + conv3 (1x1,
 // W → 4W) + residual; with w1n, also the next block's conv1 (1x1, 4W → W,
@@ -1949,11 +1680,9 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
     if (g_forced_bm == 64) small = true;
     if (g_forced_bm == 128) small = false;
     hipError_t e;
-    // LDS-DMA kernels for everything except a prologue on a padded conv
-    // (padding must stay zero AFTER the prologue).
-    // (The in-register prologue variant measured slower than the register
-    // path on every ResNet-50 shape — VALU-bound — so it is opt-in.)
-    const bool glds = glds_enabled() && (!pro || (glds_pro_enabled() && KS == 1 && pad == 0 && C <= 2048));
+    // LDS-DMA kernels for every conv without a prologue; prologue convs stage A
+    // through registers (conv_pro_kernel / conv_gemm_kernel).
+    const bool glds = glds_enabled() && !pro;
     // 256x256 tiles: 1x1 / stride 1 / no prologue, Cout % 256 == 0, deep K
     // (≥ 1024: below it these layers are HBM-bound and the 64-row tiles at 3
     // blocks per CU win — the ResNet-50 flagship measured 1 % slower with the
@@ -1967,33 +1696,18 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
     const int64_t tiles256 = (int64_t)((c.M + 255) / 256) * (Cout / 256);
     const bool big = big_ok && (g_forced_big == 1 ||
                                 (g_forced_big == 2 && C >= 1024 && tiles256 >= (int64_t)conv_cus()));
-    // Deep K with few tiles per owned CU: the 3-stage prologue kernel.
-    if (g_forced_deep < 0) {
-      const char* v = getenv("VGPU_CONV_PRO_DEEP");
-      // Off by default: at one block per CU the 3-stage kernel measured slower
-      // than conv_pro at two, even on the deep-K stage-4 layers
-      // (profiles/r2/ab/pro-deep: flagship 25.5k either way with the heuristic,
-      // 23.1k forced on every eligible layer; exclusive 22.1k -> 21.5k / 20.2k).
-      g_forced_deep = v ? (v[0] == '1' ? 1 : (v[0] == '2' ? 2 : 0)) : 0;
-    }
-    const bool deep_ok = pro && !glds && pro_dma_enabled() && KS == 1 && pad == 0 && C <= 2048 &&
-                         a.ktiles >= 3 && Cout % 128 == 0;
-    const bool deep = deep_ok && (g_forced_deep == 1 ||
-                                  (g_forced_deep == 2 && a.ktiles >= 8 && tiles128 <= (int64_t)conv_cus() * 2));
     if (big)
       e = has_res ? launch_big<true>(c, s) : launch_big<false>(c, s);
-    else if (deep)
-      e = has_res ? launch_prodeep<128, 128, true>(c, s) : launch_prodeep<128, 128, false>(c, s);
     else if (narrow)
-      e = small ? launch_glds<4, 64, 64, false, false, 16>(c, s) : launch_glds<4, 128, 64, false, false, 16>(c, s);
+      e = small ? launch_glds<4, 64, 64, false, 16>(c, s) : launch_glds<4, 128, 64, false, 16>(c, s);
     // Short K (≤ 2 steps) or 64-wide outputs: the persistent register kernel,
     // which overlaps the next tile's loads with this tile's epilogue, wins there.
-    else if (pro && !glds && pro_dma_enabled() && C <= 2048 && a.ktiles > 2 && Cout > 64)
+    else if (pro && pro_dma_enabled() && C <= 2048 && a.ktiles > 2 && Cout > 64)
       e = KS == 1 ? (small ? dispatch_pro<1, 64>(c, has_res, s) : dispatch_pro<1, 128>(c, has_res, s))
                   : (small ? dispatch_pro<3, 64>(c, has_res, s) : dispatch_pro<3, 128>(c, has_res, s));
     else if (glds)
-      e = KS == 1 ? (small ? dispatch_glds<1, 64>(c, pro, has_res, s) : dispatch_glds<1, 128>(c, pro, has_res, s))
-                  : (small ? dispatch_glds<3, 64>(c, pro, has_res, s) : dispatch_glds<3, 128>(c, pro, has_res, s));
+      e = KS == 1 ? (small ? dispatch_glds<1, 64>(c, has_res, s) : dispatch_glds<1, 128>(c, has_res, s))
+                  : (small ? dispatch_glds<3, 64>(c, has_res, s) : dispatch_glds<3, 128>(c, has_res, s));
     else if (KS == 1)
       e = small ? dispatch_bn<1, 64>(c, pro, has_res, s) : dispatch_bn<1, 128>(c, pro, has_res, s);
     else

@@ -34,18 +34,6 @@ RECIPES: dict[str, tuple[list, list, int]] = {
         ("mask", {}, ["--cu-share", "mask"]),
         ("exclusive", {}, EXCL),
     ], 300),
-    # Depth-first micro-batches over the first stages (VGPU_DF_CHUNKS / VGPU_DF_BLOCKS).
-    "depth-first": (["--steps", "30", "--warmup", "10"], [
-        ("base", {}, []),
-        ("c2_b3", {"VGPU_DF_CHUNKS": "2", "VGPU_DF_BLOCKS": "3"}, []),
-        ("c2_b7", {"VGPU_DF_CHUNKS": "2", "VGPU_DF_BLOCKS": "7"}, []),
-        ("c5_b3", {"VGPU_DF_CHUNKS": "5", "VGPU_DF_BLOCKS": "3"}, []),
-        ("c5_b7", {"VGPU_DF_CHUNKS": "5", "VGPU_DF_BLOCKS": "7"}, []),
-        ("c2_all", {"VGPU_DF_CHUNKS": "2"}, []),
-        ("c5_all", {"VGPU_DF_CHUNKS": "5"}, []),
-        ("excl", {}, EXCL),
-        ("excl_c5_b7", {"VGPU_DF_CHUNKS": "5", "VGPU_DF_BLOCKS": "7"}, EXCL),
-    ], 300),
     # Flagship knobs under the default temporal share policy.
     "temporal-knobs": (["--steps", "30", "--warmup", "10"], [
         ("base", {}, []),
@@ -79,17 +67,6 @@ RECIPES: dict[str, tuple[list, list, int]] = {
         ("w5.1_k2", {"VGPU_POOL_CONCURRENCY": "2"}, ["--workload", "5.1"]),
         ("w2.2_k2_q100", {"VGPU_POOL_CONCURRENCY": "2", "VGPU_POOL_QUANTUM_MS": "100"}, ["--workload", "2.2"]),
     ], 300),
-    # 3-stage prologue conv kernel for deep-K layers (VGPU_CONV_PRO_DEEP).
-    "pro-deep": (["--steps", "30", "--warmup", "10"], [
-        ("off", {"VGPU_CONV_PRO_DEEP": "0"}, []),
-        ("heuristic", {}, []),
-        ("all", {"VGPU_CONV_PRO_DEEP": "1"}, []),
-        ("excl_off", {"VGPU_CONV_PRO_DEEP": "0"}, EXCL),
-        ("excl_heuristic", {}, EXCL),
-        ("excl_all", {"VGPU_CONV_PRO_DEEP": "1"}, EXCL),
-        ("off_again", {"VGPU_CONV_PRO_DEEP": "0"}, []),
-        ("all_again", {"VGPU_CONV_PRO_DEEP": "1"}, []),
-    ], 300),
     # Pool gate with conv tiles sized for the CUs a running pod actually shares (256 / k).
     "pool-gate-cus": (P4 + ["--steps", "40", "--warmup", "5", "--cu-share", "temporal"], [
         ("w2.2_free", {}, ["--workload", "2.2"]),
@@ -107,8 +84,6 @@ RECIPES: dict[str, tuple[list, list, int]] = {
         ("big_all", {"VGPU_CONV_BIG": "1"}, []),
         ("big_off", {"VGPU_CONV_BIG": "0"}, []),
         ("1x1_big", {"VGPU_CONV_1X1_BIG": "1"}, []),
-        ("glds_pro", {"VGPU_CONV_GLDS_PRO": "1"}, []),
-        ("stages3", {"VGPU_CONV_STAGES": "3"}, []),
         ("base_again", {}, []),
     ], 300),
     # Temporal limiter accuracy and fair share (profiles/temporal_r2.md).

@@ -86,7 +86,7 @@ def test_conv_big_tile_matches_fp32(C, case):
 
 
 DEEP_CASES = [
-    # 3-stage prologue kernel (1x1, BN+ReLU prologue, Cout % 128 == 0), forced on
+    # deep-K 1x1 convs with a BN+ReLU prologue (conv_pro_kernel / register path)
     (3, 256, 13, 13, 512, 2, True, "none", False),   # strided projection shortcut, K = 4 steps
     (1, 2048, 3, 3, 512, 1, True, "relu", False),    # deep K (32 steps), M = 9 < one tile
     (4, 1024, 11, 11, 256, 1, False, "relu", False), # K = 16 steps, ragged M
@@ -96,8 +96,7 @@ DEEP_CASES = [
 
 
 @pytest.mark.parametrize("case", DEEP_CASES, ids=lambda c: "x".join(map(str, c[:6])))
-def test_conv_pro_deep_matches_fp32(C, case):
-    from vgpu.native import load_kernels
+def test_conv_prologue_deep_k_matches_fp32(C, case):
     n, c, h, w, cout, stride, has_bias, act, has_res = case
     x = _t((n, c, h, w), 21)
     wt = _t((cout, c, 1, 1), 22, scale=(2.0 / c) ** 0.5)
@@ -105,12 +104,7 @@ def test_conv_pro_deep_matches_fp32(C, case):
     pro = (_f((c,), 24, 0.5, 1.5), _f((c,), 25))
     oh, ow = C.out_hw(h, w, 1, stride, 0)
     res = _t((n, cout, oh, ow), 26) if has_res else None
-    lib = load_kernels()
-    lib.vgpu_conv_set_pro_deep(1)
-    try:
-        got = C.conv2d(x, wt, bias, stride=stride, act=act, pro=pro, residual=res)
-    finally:
-        lib.vgpu_conv_set_pro_deep(-1)
+    got = C.conv2d(x, wt, bias, stride=stride, act=act, pro=pro, residual=res)
     ref = C.conv2d_ref(x, wt, bias, stride=stride, act=act, pro=pro, residual=res)
     torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
 
@@ -175,25 +169,6 @@ def test_native_resnet_matches_module(gpu_build):
     got = fm(x.to(torch.bfloat16).contiguous(memory_format=CL)).float()
     rel = (got - ref).norm() / ref.norm()
     assert rel < 0.05, float(rel)
-
-
-@pytest.mark.parametrize("blocks", [7, 1000])
-def test_native_resnet_depth_first_chunks(gpu_build, monkeypatch, blocks):
-    """VGPU_DF_CHUNKS: the stem and the first stages run on micro-batches one
-    after the other; the result equals the whole-batch forward."""
-    from vgpu.models.resnet import FusedResNetV2Inference, resnet_v2_50
-    torch.manual_seed(0)
-    m = resnet_v2_50().cuda().eval().to(torch.bfloat16).to(memory_format=CL)
-    x = torch.randn(5, 3, 96, 96, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=CL)
-    ref = FusedResNetV2Inference(m, conv="native")(x).float()
-    monkeypatch.setenv("VGPU_DF_CHUNKS", "2")
-    monkeypatch.setenv("VGPU_DF_BLOCKS", str(blocks))
-    fm = FusedResNetV2Inference(m, conv="native")
-    assert fm.df_chunks == 2 and fm.df_blocks == min(blocks, 16)
-    got = fm(x).float()
-    assert got.shape == ref.shape
-    rel = (got - ref).norm() / ref.norm()
-    assert rel < 1e-2, float(rel)
 
 
 def test_native_vgg_matches_module(gpu_build):

@@ -46,8 +46,6 @@ def main(argv=None) -> int:
                     help="bottleneck tail conv2+conv3: fused kernel vs the two kernels (stages 1-2)")
     ap.add_argument("--ab-tile", action="store_true",
                     help="per layer, interleaved: 64-row vs 128-row tiles")
-    ap.add_argument("--ab-stages", action="store_true",
-                    help="per layer, interleaved: 2-stage vs 3-stage LDS-DMA ring (in place of MIOpen)")
     args = ap.parse_args(argv)
 
     import torch
@@ -130,20 +128,6 @@ def _run_layers(args, layers, timeit, C, F, cl, dev, tot_n=0.0, tot_m=0.0) -> in
         y = torch.empty(n, cout, oh, ow, device=dev, dtype=torch.bfloat16).contiguous(memory_format=cl)
         t_nat = timeit(lambda: C.conv2d(x, wt, bias, stride=stride, padding=pad,
                                         act="relu" if ba else "none", pro=pp, residual=r, out=y))
-        if args.ab_stages:
-            from vgpu.native import load_kernels
-            lib = load_kernels()
-            run = lambda: C.conv2d(x, wt, bias, stride=stride, padding=pad,  # noqa: E731
-                                   act="relu" if ba else "none", pro=pp, residual=r, out=y)
-            t2 = t3 = 0.0
-            for _ in range(3):
-                lib.vgpu_conv_set_stages(2)
-                t2 += timeit(run) / 3
-                lib.vgpu_conv_set_stages(3)
-                t3 += timeit(run) / 3
-            lib.vgpu_conv_set_stages(0)
-            print(json.dumps({"layer": name, "stages2_us": round(t2, 1), "stages3_us": round(t3, 1)}),
-                  flush=True)
         if args.ab_tile:
             from vgpu.native import load_kernels
             lib = load_kernels()

@@ -136,9 +136,6 @@ class FusedResNetV2Inference(nn.Module):
         self.fuse_tail = os.environ.get("VGPU_FUSE_TAIL", "1") != "0"
         # ... and the next identity block's conv1 into that tail (VGPU_FUSE_NEXT=0 disables)
         self.fuse_next = self.fuse_tail and os.environ.get("VGPU_FUSE_NEXT", "1") != "0"
-        # depth-first micro-batches over the first VGPU_DF_BLOCKS blocks (A/B knob)
-        self.df_chunks = int(os.environ.get("VGPU_DF_CHUNKS", "1"))
-        df_blocks = int(os.environ.get("VGPU_DF_BLOCKS", "1000"))
         from vgpu.ops.fused import bn_scale_shift
         m = m.eval()
         dt = m.stem.weight.dtype
@@ -169,9 +166,6 @@ class FusedResNetV2Inference(nn.Module):
                 })
             self.out_ss = bn_scale_shift(m.bn_out)
             self.fc = m.fc
-        # round the chunked prefix down to a stage start (a block with a projection shortcut)
-        starts = [i for i, b in enumerate(self.blocks) if b["sc"] is not None] + [len(self.blocks)]
-        self.df_blocks = max([s for s in starts if s <= df_blocks] or [len(self.blocks)])
 
     @torch.no_grad()
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -182,20 +176,6 @@ class FusedResNetV2Inference(nn.Module):
     def _forward_native(self, x: torch.Tensor) -> torch.Tensor:
         from vgpu.ops import conv as C
         x = x.contiguous(memory_format=torch.channels_last)
-        k = min(self.df_chunks, x.shape[0])
-        if k > 1:
-            # Depth-first: the stem and the first df_blocks blocks run on k
-            # micro-batches one after the other, so each chunk's block
-            # activations are re-read from the 256 MB Infinity Cache instead
-            # of HBM; the rest of the network runs on the whole batch.
-            nb = self.df_blocks
-            outs = [self._blocks_native(C.maxpool3s2(C.stem_conv(xc, self.stem_w_s2d)), 0, nb)
-                    for xc in x.tensor_split(k, dim=0)]
-            if nb >= len(self.blocks):
-                return self.fc(torch.cat([C.scale_shift_relu_mean(o, *self.out_ss) for o in outs]))
-            x = torch.cat(outs).contiguous(memory_format=torch.channels_last)
-            x = self._blocks_native(x, nb, len(self.blocks))
-            return self.fc(C.scale_shift_relu_mean(x, *self.out_ss))
         x = C.stem_conv(x, self.stem_w_s2d)
         x = C.maxpool3s2(x)
         x = self._blocks_native(x, 0, len(self.blocks))

@@ -62,7 +62,6 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_conv2d_nhwc.argtypes = [vp, vp, vp, vp, vp, vp, vp] + [ci] * 9 + [vp]
     lib.vgpu_maxpool_nhwc.argtypes = [vp, vp] + [ci] * 7 + [vp]
     lib.vgpu_conv_set_big.argtypes = [ci]
-    lib.vgpu_conv_set_pro_deep.argtypes = [ci]
     lib.vgpu_lstm_recurrence.argtypes = [vp, vp, vp, vp, ci, ci, ci, vp]
     lib.vgpu_lstm_recurrence.restype = ci
     lib.vgpu_lstm_forward_train.argtypes = [vp] * 5 + [ci, ci, ci, vp]
