@@ -7,8 +7,12 @@ Default config = BASELINE.json config 2: every GPU is split 2 ways, each pod
 bf16 inference at the reference's ai-benchmark shape (test 1.1: batch 50,
 346x346; reference README.md:244).  Weights are random-init and inputs
 synthetic.  Every pod runs under the in-container enforcement library
-(LD_PRELOAD libvgpu.so) with its own shared region, HBM cap and XCD-balanced
-CU mask — exactly what the device plugin's Allocate hands a container.
+(LD_PRELOAD libvgpu.so) with its own shared region, HBM cap and compute share,
+with exactly the env the device plugin's Allocate hands a container.  The share
+policy is the plugin's default, `auto` (`--cu-share`): the pods of a GPU
+measure time sharing under the fair-share GPU-time limiter against CUs of their
+own, and keep the faster (vgpu/deviceplugin/custate.py).  `mask` gives every pod
+an XCD-balanced CU mask; `temporal` only time-shares.
 
 Launch: ``python bench.py --gpus N --steps K --warmup W`` (N>1 under
 torch.distributed.run, one rank per GPU).  Each rank spawns its pods BEFORE
