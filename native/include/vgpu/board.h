@@ -30,7 +30,7 @@ extern "C" {
 #endif
 
 #define VGPU_BOARD_MAGIC 0x56424F44u /* "VBOD" */
-#define VGPU_BOARD_VERSION 3u
+#define VGPU_BOARD_VERSION 4u
 #define VGPU_BOARD_SLOTS 128
 #define VGPU_BOARD_STALE_NS 500000000ull /* a slot without heartbeat for 0.5 s is inactive */
 /* auto_phase */
@@ -38,6 +38,7 @@ extern "C" {
 #define VGPU_AUTO_EXPLORE_T 1     /* measuring time sharing                          */
 #define VGPU_AUTO_EXPLORE_S 2     /* measuring CU claims                             */
 #define VGPU_AUTO_SPATIAL 3       /* decided: every member on CUs of its own         */
+#define VGPU_AUTO_MEMO 16
 
 typedef struct vgpu_board_slot {
   int32_t pid;                   /* pid inside the owner's container (0 = free) */
@@ -91,6 +92,15 @@ typedef struct vgpu_board {
   volatile int32_t auto_marked;    /* 1 once the phase's measurement window opened      */
   int32_t reserved3;
   volatile double auto_score;      /* mean own-CU / time-shared rate of the last A/B     */
+  /* Decisions by busy-member count n (< VGPU_AUTO_MEMO): a count that comes back
+   * within the re-explore period (pods pausing between phases of a job) takes
+   * its earlier decision instead of a new A/B. */
+  volatile int32_t auto_memo_phase[16];
+  volatile uint64_t auto_memo_ns[16];   /* when decided, 0 = never              */
+  volatile double auto_memo_score[16];
+  volatile int32_t auto_pending_n;      /* a new busy-member count, acted on once */
+  int32_t reserved4;                    /* it has held for the settle time        */
+  volatile uint64_t auto_pending_ns;
   vgpu_board_slot_t slot[VGPU_BOARD_SLOTS];
 } vgpu_board_t;
 

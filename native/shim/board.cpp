@@ -320,7 +320,11 @@ int board_auto_phase(vgpu_board_t* b) { return b ? __atomic_load_n(&b->auto_phas
 //   least `min_gain` x their time-shared rate, else TEMPORAL.
 // Each measurement window opens `settle_ns` after its phase began (masks
 // re-applied, queues refilled).  Fewer than two busy members: time sharing (a
-// lone pod is not held back there).  Returns the phase.
+// lone pod is not held back there).  A decision is remembered per member
+// count: jobs that pause (a step barrier, a checkpoint, a benchmark waiting
+// for its peers) return to the decision of their count at once instead of
+// re-measuring; an exploration whose member count changes starts over (or
+// takes the remembered decision of the new count).  Returns the phase.
 int board_auto_lead(vgpu_board_t* b, int slot, uint64_t window_ns, uint64_t settle_ns, uint64_t reexplore_ns,
                     double min_gain, char* note, size_t note_len) {
   if (note && note_len) note[0] = 0;
@@ -350,16 +354,47 @@ int board_auto_lead(vgpu_board_t* b, int slot, uint64_t window_ns, uint64_t sett
     b->auto_marked = 0;
     phase = p;
   };
+  const bool memo_ok = nb < VGPU_AUTO_MEMO && b->auto_memo_ns[nb] && now - b->auto_memo_ns[nb] < reexplore_ns;
+  // A change of the busy-member count counts once it has held for `settle_ns`
+  // (pods of one job pause and resume a few ms apart).
+  bool count_changed = false;
+  if (nb != b->auto_members) {
+    if (b->auto_pending_n != nb) {
+      b->auto_pending_n = nb;
+      b->auto_pending_ns = now;
+    }
+    count_changed = now - b->auto_pending_ns >= settle_ns;
+  } else {
+    b->auto_pending_n = -1;
+  }
+  // A new busy-member count: its remembered decision, else a new A/B.
+  auto recount = [&] {
+    b->auto_members = nb;
+    if (memo_ok) {
+      go(b->auto_memo_phase[nb]);
+      b->auto_score = b->auto_memo_score[nb];
+      if (note && note_len)
+        snprintf(note, note_len, "%d busy members again: %s (decided %.1f s ago, %.3f x)", nb,
+                 phase == VGPU_AUTO_SPATIAL ? "CUs of their own" : "time sharing",
+                 (now - b->auto_memo_ns[nb]) * 1e-9, b->auto_memo_score[nb]);
+    } else {
+      go(VGPU_AUTO_EXPLORE_T);
+    }
+  };
   if (phase == VGPU_AUTO_TEMPORAL || phase == VGPU_AUTO_SPATIAL) {
     if (nb < 2) {
       if (phase == VGPU_AUTO_SPATIAL) go(VGPU_AUTO_TEMPORAL);
       b->auto_members = nb;
-    } else if (nb != b->auto_members || now - b->auto_phase_ns > reexplore_ns) {
+    } else if (nb != b->auto_members) {
+      if (count_changed) recount();
+    } else if (!memo_ok && now - b->auto_phase_ns > reexplore_ns) {
       go(VGPU_AUTO_EXPLORE_T);
     }
   } else if (nb < 2) {
     go(VGPU_AUTO_TEMPORAL);
     b->auto_members = nb;
+  } else if (nb != b->auto_members) {
+    if (count_changed) recount();  // the exploration's members changed: its rates would not compare
   } else if (!b->auto_marked) {
     if (now - b->auto_phase_ns >= settle_ns) {
       for (int k = 0; k < nb; ++k) b->slot[busy[k]].auto_mark = b->slot[busy[k]].auto_seen;
@@ -389,6 +424,11 @@ int board_auto_lead(vgpu_board_t* b, int slot, uint64_t window_ns, uint64_t sett
       b->auto_score = score;
       b->auto_members = nb;
       go(score >= min_gain ? VGPU_AUTO_SPATIAL : VGPU_AUTO_TEMPORAL);
+      if (nb < VGPU_AUTO_MEMO) {
+        b->auto_memo_phase[nb] = phase;
+        b->auto_memo_ns[nb] = now;
+        b->auto_memo_score[nb] = score;
+      }
       if (note && note_len)
         snprintf(note, note_len, "%d busy members: own CUs run at %.3f x their time-shared rate -> %s", nb,
                  score, phase == VGPU_AUTO_SPATIAL ? "CUs of their own" : "time sharing");

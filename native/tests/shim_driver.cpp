@@ -97,6 +97,10 @@ int main(int argc, char** argv) {
       unsigned grids[1] = {64};
       hipGraphInstantiateWithFlags(&ge, fake_hip_graph_create(grids, 1, 0), 0);
     }
+    // DRIVER_PAUSE="at,len": go idle for `len` s once `at` s have passed (a job
+    // waiting at a barrier); the run then lasts secs + len.
+    double pause_at = -1, pause_len = 0;
+    if (const char* pz = getenv("DRIVER_PAUSE")) sscanf(pz, "%lf,%lf", &pause_at, &pause_len);
     struct timespec a, b;
     clock_gettime(CLOCK_MONOTONIC, &a);
     const uint64_t e0 = fake_hip_exec_ns();
@@ -104,6 +108,12 @@ int main(int argc, char** argv) {
     for (;;) {
       clock_gettime(CLOCK_MONOTONIC, &b);
       double el = (b.tv_sec - a.tv_sec) + 1e-9 * (b.tv_nsec - a.tv_nsec);
+      if (pause_at >= 0 && el >= pause_at) {
+        hipDeviceSynchronize();
+        usleep((useconds_t)(pause_len * 1e6));
+        pause_at = -1;
+        secs += pause_len;
+      }
       if (el >= secs) break;
       if (graphs)
         hipGraphLaunch(ge, nullptr);

@@ -446,7 +446,7 @@ def test_fair_share_board_two_pods_use_whole_gpu(native_build, tmp_path):
     agg = _duty(a) + _duty(b)
     assert agg > 0.9, (a, b)
     assert abs(_duty(a) - 0.5) < 0.075 and abs(_duty(b) - 0.5) < 0.075
-    assert (tmp_path / "lock" / "GPU-test.v3.board").exists()
+    assert (tmp_path / "lock" / "GPU-test.v4.board").exists()
 
 
 def test_foreign_board_layout_is_never_reinitialised(native_build, tmp_path):
@@ -456,7 +456,7 @@ def test_foreign_board_layout_is_never_reinitialised(native_build, tmp_path):
     import struct
     lock = tmp_path / "lock"
     lock.mkdir()
-    board = lock / "GPU-test.v3.board"
+    board = lock / "GPU-test.v4.board"
     foreign = struct.pack("<IIIi", 0x56424F44, 7, 4096, 1) + bytes(range(256)) * 16
     board.write_bytes(foreign)
     a, b = _pair(tmp_path, 50, board=True)
@@ -617,7 +617,7 @@ def test_default_policy_lone_pod_unthrottled(native_build, tmp_path):
     assert _duty(o) > 0.9, o
 
 
-def _auto_ab(tmp_path, factor, n=4, secs=6.0):
+def _auto_ab(tmp_path, factor, n=4, secs=6.0, pause=None):
     """n auto pool members on one fake GPU (shared timeline, one share board);
     with a CU mask a member runs on a private timeline at (256 / its CUs) x
     `factor` per launch (VGPU_FAKE_MASK_FACTOR).  Returns per-pod launches and
@@ -628,6 +628,8 @@ def _auto_ab(tmp_path, factor, n=4, secs=6.0):
               "VGPU_LOCK_DIR": str(tmp_path), "VGPU_DEVICE_UUID_0": "GPU-auto", "VGPU_FAKE_KERNEL_US": "500",
               "VGPU_FAKE_GPU_TIMELINE": str(tmp_path / "tl"), "VGPU_FAKE_MASK_FACTOR": str(factor),
               "VGPU_AUTO_WINDOW_MS": "800", "VGPU_AUTO_SETTLE_MS": "150", "VGPU_LOG_LEVEL": "3"})
+    if pause:
+        e["DRIVER_PAUSE"] = pause
     procs = [subprocess.Popen([str(FAKES_DIR / "shim_driver"), "duty", str(secs)], env=e, stdout=subprocess.PIPE,
                               stderr=subprocess.PIPE, text=True) for _ in range(n)]
     launches, notes = [], []
@@ -650,6 +652,19 @@ def test_auto_policy_keeps_cu_claims_when_they_run_faster(native_build, tmp_path
 def test_auto_policy_stays_time_shared_when_claims_are_slower(native_build, tmp_path):
     launches, notes = _auto_ab(tmp_path, 1.5)
     assert len(notes) == 1 and notes[0].endswith("time sharing"), notes
+
+
+def test_auto_policy_remembers_its_decision_across_a_pause(native_build, tmp_path):
+    """Pods that pause together (a benchmark's GO barrier, a checkpoint) come
+    back to the decision made for their member count instead of a second A/B
+    whose windows would fall into their timed work."""
+    launches, notes = _auto_ab(tmp_path, 0.6, secs=6.0, pause="3.5,2.0")
+    decided = [x for x in notes if "busy members:" in x]
+    again = [x for x in notes if "busy members again" in x]
+    assert len(decided) == 1 and decided[0].endswith("CUs of their own"), notes
+    # (a member stalled for a moment after the resume may cost one more
+    # regrouping, which again takes the remembered decision)
+    assert again and all("4 busy members again: CUs of their own" in x for x in again), notes
 
 
 def test_auto_policy_lone_pod_never_explores(native_build, tmp_path):

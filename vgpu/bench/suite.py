@@ -65,6 +65,11 @@ def run(test: str, scen: str, steps: int, warmup: int, timeout: int) -> dict:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=REPO)
     except subprocess.TimeoutExpired:
         return {"test": test, "scenario": scen, "error": "timeout"}
+    if os.environ.get("VGPU_SUITE_LOGDIR"):  # keep each run's pod / shim log
+        d = os.environ["VGPU_SUITE_LOGDIR"]
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"{test}_{scen}.err"), "w") as f:
+            f.write(r.stderr)
     js = [l for l in r.stdout.splitlines() if l.startswith("{")]
     if r.returncode != 0 or not js:
         return {"test": test, "scenario": scen, "error": r.stderr[-1500:]}
