@@ -38,6 +38,7 @@ extern "C" {
 #define VGPU_AUTO_EXPLORE_T 1     /* measuring time sharing                          */
 #define VGPU_AUTO_EXPLORE_S 2     /* measuring CU claims                             */
 #define VGPU_AUTO_SPATIAL 3       /* decided: every member on CUs of its own         */
+#define VGPU_AUTO_EXPLORE_T2 4    /* measuring time sharing again (A/B/A)             */
 #define VGPU_AUTO_MEMO 16
 
 typedef struct vgpu_board_slot {
@@ -68,7 +69,9 @@ typedef struct vgpu_board_slot {
   uint64_t auto_mark;               /* auto_launches at the start of a measurement (leader)   */
   uint64_t auto_seen;               /* auto_launches at the leader's last look                */
   uint64_t auto_busy_ns;            /* when the leader last saw it progress                   */
-  double auto_rate[2];              /* dispatches/s measured time-shared [0] / on own CUs [1] */
+  double auto_rate[3];              /* dispatches/s: time-shared [0], own CUs [1], time-shared [2] */
+  double auto_hist[3];              /* dispatches/s in the last three steadiness buckets      */
+  uint64_t auto_bucket_mark;        /* auto_launches at the current bucket's start            */
 } vgpu_board_slot_t;
 
 typedef struct vgpu_board {
@@ -99,8 +102,9 @@ typedef struct vgpu_board {
   volatile uint64_t auto_memo_ns[16];   /* when decided, 0 = never              */
   volatile double auto_memo_score[16];
   volatile int32_t auto_pending_n;      /* a new busy-member count, acted on once */
-  int32_t reserved4;                    /* it has held for the settle time        */
-  volatile uint64_t auto_pending_ns;
+  volatile int32_t auto_want;           /* an A/B is due once the members are steady (tries left) */
+  volatile uint64_t auto_pending_ns;    /* it has held for the settle time        */
+  volatile uint64_t auto_bucket_ns;     /* start of the current steadiness bucket  */
   vgpu_board_slot_t slot[VGPU_BOARD_SLOTS];
 } vgpu_board_t;
 

@@ -1,5 +1,6 @@
 // Node-wide per-GPU share board (include/vgpu/board.h): fair-share charging of
 // GPU time between the pods that time-share one physical device.
+#include <algorithm>
 #include "board.h"
 
 #include <errno.h>
@@ -315,9 +316,17 @@ int board_auto_phase(vgpu_board_t* b) { return b ? __atomic_load_n(&b->auto_phas
 
 // The lowest live auto member drives the per-GPU state machine:
 //   TEMPORAL/SPATIAL (decided) --(>= 2 busy members and a new member count, or
-//   `reexplore_ns` since the decision)--> EXPLORE_T --window--> EXPLORE_S
+//   `reexplore_ns` since the decision; then, once every member's dispatch rate
+//   is steady)--> EXPLORE_T --window--> EXPLORE_S --window--> EXPLORE_T2
 //   --window--> SPATIAL if the members' mean dispatch rate on own CUs is at
-//   least `min_gain` x their time-shared rate, else TEMPORAL.
+//   least `min_gain` x their time-shared rate (the mean of the two time-shared
+//   windows), else TEMPORAL.
+// Steady: each busy member's rate over the last three `bucket_ns` buckets
+// varies by at most 30 % -- start-up (graph capture, kernel tuning, the first
+// iterations) is not what the pods will run, and an A/B measured there picks
+// the wrong mode.  A/B/A: when the two time-shared windows disagree by more
+// than 25 % the workload changed under the measurement; the A/B is retried
+// (at most three times per member count) and time sharing holds meanwhile.
 // Each measurement window opens `settle_ns` after its phase began (masks
 // re-applied, queues refilled).  Fewer than two busy members: time sharing (a
 // lone pod is not held back there).  A decision is remembered per member
@@ -326,7 +335,7 @@ int board_auto_phase(vgpu_board_t* b) { return b ? __atomic_load_n(&b->auto_phas
 // re-measuring; an exploration whose member count changes starts over (or
 // takes the remembered decision of the new count).  Returns the phase.
 int board_auto_lead(vgpu_board_t* b, int slot, uint64_t window_ns, uint64_t settle_ns, uint64_t reexplore_ns,
-                    double min_gain, char* note, size_t note_len) {
+                    double min_gain, uint64_t bucket_ns, char* note, size_t note_len) {
   if (note && note_len) note[0] = 0;
   if (!b || slot < 0 || !lock(b)) return board_auto_phase(b);
   const uint64_t now = mono_ns();
@@ -348,6 +357,28 @@ int board_auto_lead(vgpu_board_t* b, int slot, uint64_t window_ns, uint64_t sett
     unlock(b);
     return phase;
   }
+  // Steadiness buckets: per member, dispatches/s over the last three buckets.
+  if (!b->auto_bucket_ns) b->auto_bucket_ns = now;
+  if (now - b->auto_bucket_ns >= bucket_ns) {
+    const double dt = (now - b->auto_bucket_ns) * 1e-9;
+    for (int i = 0; i < VGPU_BOARD_SLOTS; ++i) {
+      vgpu_board_slot_t& s = b->slot[i];
+      if (!fresh(s, now) || !s.auto_member) continue;
+      s.auto_hist[2] = s.auto_hist[1];
+      s.auto_hist[1] = s.auto_hist[0];
+      s.auto_hist[0] = s.auto_bucket_mark ? (double)(s.auto_seen - s.auto_bucket_mark) / dt : 0.0;
+      s.auto_bucket_mark = s.auto_seen ? s.auto_seen : 1;
+    }
+    b->auto_bucket_ns = now;
+  }
+  auto steady = [&] {
+    for (int k = 0; k < nb; ++k) {
+      const double* h = b->slot[busy[k]].auto_hist;
+      const double lo = std::min(h[0], std::min(h[1], h[2])), hi = std::max(h[0], std::max(h[1], h[2]));
+      if (lo <= 0 || hi > 1.3 * lo) return false;
+    }
+    return true;
+  };
   auto go = [&](int p) {
     __atomic_store_n(&b->auto_phase, p, __ATOMIC_RELEASE);
     b->auto_phase_ns = now;
@@ -367,18 +398,20 @@ int board_auto_lead(vgpu_board_t* b, int slot, uint64_t window_ns, uint64_t sett
   } else {
     b->auto_pending_n = -1;
   }
-  // A new busy-member count: its remembered decision, else a new A/B.
+  // A new busy-member count: its remembered decision, else an A/B once steady.
   auto recount = [&] {
     b->auto_members = nb;
     if (memo_ok) {
       go(b->auto_memo_phase[nb]);
+      b->auto_want = 0;
       b->auto_score = b->auto_memo_score[nb];
       if (note && note_len)
         snprintf(note, note_len, "%d busy members again: %s (decided %.1f s ago, %.3f x)", nb,
                  phase == VGPU_AUTO_SPATIAL ? "CUs of their own" : "time sharing",
                  (now - b->auto_memo_ns[nb]) * 1e-9, b->auto_memo_score[nb]);
     } else {
-      go(VGPU_AUTO_EXPLORE_T);
+      if (phase != VGPU_AUTO_TEMPORAL) go(VGPU_AUTO_TEMPORAL);
+      b->auto_want = 3;
     }
   };
   if (phase == VGPU_AUTO_TEMPORAL || phase == VGPU_AUTO_SPATIAL) {
@@ -387,8 +420,10 @@ int board_auto_lead(vgpu_board_t* b, int slot, uint64_t window_ns, uint64_t sett
       b->auto_members = nb;
     } else if (nb != b->auto_members) {
       if (count_changed) recount();
+    } else if (b->auto_want > 0) {
+      if (steady()) go(VGPU_AUTO_EXPLORE_T);
     } else if (!memo_ok && now - b->auto_phase_ns > reexplore_ns) {
-      go(VGPU_AUTO_EXPLORE_T);
+      b->auto_want = 3;
     }
   } else if (nb < 2) {
     go(VGPU_AUTO_TEMPORAL);
@@ -403,35 +438,51 @@ int board_auto_lead(vgpu_board_t* b, int slot, uint64_t window_ns, uint64_t sett
     }
   } else if (now - b->auto_phase_ns >= window_ns) {
     const double secs = (now - b->auto_phase_ns) * 1e-9;
-    const int idx = phase == VGPU_AUTO_EXPLORE_T ? 0 : 1;
+    const int idx = phase == VGPU_AUTO_EXPLORE_T ? 0 : phase == VGPU_AUTO_EXPLORE_S ? 1 : 2;
     for (int k = 0; k < nb; ++k) {
       vgpu_board_slot_t& s = b->slot[busy[k]];
       s.auto_rate[idx] = (double)(s.auto_seen - s.auto_mark) / secs;
     }
     if (phase == VGPU_AUTO_EXPLORE_T) {
       go(VGPU_AUTO_EXPLORE_S);
+    } else if (phase == VGPU_AUTO_EXPLORE_S) {
+      go(VGPU_AUTO_EXPLORE_T2);
     } else {
-      double sum = 0;
+      double sum = 0, a0 = 0, a2 = 0;
       int n = 0;
       for (int k = 0; k < nb; ++k) {
         const vgpu_board_slot_t& s = b->slot[busy[k]];
-        if (s.auto_rate[0] > 0) {
-          sum += s.auto_rate[1] / s.auto_rate[0];
+        const double t = 0.5 * (s.auto_rate[0] + s.auto_rate[2]);
+        a0 += s.auto_rate[0];
+        a2 += s.auto_rate[2];
+        if (t > 0) {
+          sum += s.auto_rate[1] / t;
           ++n;
         }
       }
       const double score = n ? sum / n : 0.0;
-      b->auto_score = score;
       b->auto_members = nb;
-      go(score >= min_gain ? VGPU_AUTO_SPATIAL : VGPU_AUTO_TEMPORAL);
-      if (nb < VGPU_AUTO_MEMO) {
-        b->auto_memo_phase[nb] = phase;
-        b->auto_memo_ns[nb] = now;
-        b->auto_memo_score[nb] = score;
+      const bool consistent = a0 > 0 && a2 > 0 && std::max(a0, a2) <= 1.25 * std::min(a0, a2);
+      if (!consistent) {
+        b->auto_want = b->auto_want > 0 ? b->auto_want - 1 : 0;
+        go(VGPU_AUTO_TEMPORAL);
+        if (note && note_len)
+          snprintf(note, note_len,
+                   "%d busy members: time-shared windows disagree (%.0f vs %.0f dispatches/s), %s", nb, a0, a2,
+                   b->auto_want ? "measuring again once steady" : "keeping time sharing");
+      } else {
+        b->auto_score = score;
+        b->auto_want = 0;
+        go(score >= min_gain ? VGPU_AUTO_SPATIAL : VGPU_AUTO_TEMPORAL);
+        if (nb < VGPU_AUTO_MEMO) {
+          b->auto_memo_phase[nb] = phase;
+          b->auto_memo_ns[nb] = now;
+          b->auto_memo_score[nb] = score;
+        }
+        if (note && note_len)
+          snprintf(note, note_len, "%d busy members: own CUs run at %.3f x their time-shared rate -> %s", nb,
+                   score, phase == VGPU_AUTO_SPATIAL ? "CUs of their own" : "time sharing");
       }
-      if (note && note_len)
-        snprintf(note, note_len, "%d busy members: own CUs run at %.3f x their time-shared rate -> %s", nb,
-                 score, phase == VGPU_AUTO_SPATIAL ? "CUs of their own" : "time sharing");
     }
   }
   unlock(b);

@@ -27,7 +27,7 @@ void board_auto_join(vgpu_board_t* b, int slot);
 void board_auto_progress(vgpu_board_t* b, int slot, uint64_t dispatches);
 int board_auto_phase(vgpu_board_t* b);
 int board_auto_lead(vgpu_board_t* b, int slot, uint64_t window_ns, uint64_t settle_ns, uint64_t reexplore_ns,
-                    double min_gain, char* note, size_t note_len);
+                    double min_gain, uint64_t bucket_ns, char* note, size_t note_len);
 double board_entitlement(vgpu_board_t* b, int slot);  // weighted fair share among active slots
 
 }  // namespace vgpu

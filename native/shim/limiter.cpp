@@ -380,6 +380,7 @@ void auto_step() {
   static const uint64_t settle_ns = (uint64_t)(1e6 * (env_first("VGPU_AUTO_SETTLE_MS") ? atof(env_first("VGPU_AUTO_SETTLE_MS")) : 300.0));
   static const uint64_t reexplore_ns = (uint64_t)(1e9 * (env_first("VGPU_AUTO_REEXPLORE_S") ? atof(env_first("VGPU_AUTO_REEXPLORE_S")) : 300.0));
   static const double min_gain = env_first("VGPU_AUTO_MIN_GAIN") ? atof(env_first("VGPU_AUTO_MIN_GAIN")) : 1.05;
+  static const uint64_t bucket_ns = (uint64_t)(1e6 * (env_first("VGPU_AUTO_BUCKET_MS") ? atof(env_first("VGPU_AUTO_BUCKET_MS")) : 1000.0));
   for (int d = 0; d < VGPU_MAX_DEVICES; ++d) {
     DevLimiter& L = g_lim[d];
     if (!L.auto_share || !s.region) continue;
@@ -394,8 +395,8 @@ void auto_step() {
     }
     board_auto_progress(L.board, L.board_slot, L.kern_n.exchange(0, std::memory_order_relaxed));
     char note[160];
-    const int phase = board_auto_lead(L.board, L.board_slot, window_ns, settle_ns, reexplore_ns, min_gain, note,
-                                      sizeof note);
+    const int phase = board_auto_lead(L.board, L.board_slot, window_ns, settle_ns, reexplore_ns, min_gain, bucket_ns,
+                                      note, sizeof note);
     if (note[0]) VLOG_INFO("device %d: adaptive share: %s", d, note);
     const int phys = cumask_device_physical_cus(d);
     uint64_t allowed[VGPU_CU_MASK_WORDS];

@@ -627,7 +627,8 @@ def _auto_ab(tmp_path, factor, n=4, secs=6.0, pause=None):
               "VGPU_DEVICE_CU_LIMIT_0": str(100 // n), "VGPU_CU_SHARE": "auto", "VGPU_CU_MASK_FROM_LIMIT": "false",
               "VGPU_LOCK_DIR": str(tmp_path), "VGPU_DEVICE_UUID_0": "GPU-auto", "VGPU_FAKE_KERNEL_US": "500",
               "VGPU_FAKE_GPU_TIMELINE": str(tmp_path / "tl"), "VGPU_FAKE_MASK_FACTOR": str(factor),
-              "VGPU_AUTO_WINDOW_MS": "800", "VGPU_AUTO_SETTLE_MS": "150", "VGPU_LOG_LEVEL": "3"})
+              "VGPU_AUTO_WINDOW_MS": "700", "VGPU_AUTO_SETTLE_MS": "150", "VGPU_AUTO_BUCKET_MS": "300",
+              "VGPU_LOG_LEVEL": "3"})
     if pause:
         e["DRIVER_PAUSE"] = pause
     procs = [subprocess.Popen([str(FAKES_DIR / "shim_driver"), "duty", str(secs)], env=e, stdout=subprocess.PIPE,
@@ -658,7 +659,7 @@ def test_auto_policy_remembers_its_decision_across_a_pause(native_build, tmp_pat
     """Pods that pause together (a benchmark's GO barrier, a checkpoint) come
     back to the decision made for their member count instead of a second A/B
     whose windows would fall into their timed work."""
-    launches, notes = _auto_ab(tmp_path, 0.6, secs=6.0, pause="3.5,2.0")
+    launches, notes = _auto_ab(tmp_path, 0.6, secs=7.0, pause="5.0,2.0")
     decided = [x for x in notes if "busy members:" in x]
     again = [x for x in notes if "busy members again" in x]
     assert len(decided) == 1 and decided[0].endswith("CUs of their own"), notes

@@ -5,7 +5,7 @@ reference's comparison (README.md:234-257):
   exclusive          — one pod, whole GPU, no enforcement library
   vgpu               — 2 pods × gpucores=50, gpumem=144000 (BASELINE.json config 2),
                        device-plugin default share policy (auto: a share-board A/B
-                       of time sharing vs CUs of their own; 6 s of warmup let it settle)
+                       of time sharing vs CUs of their own; 12 s of warmup let it settle)
   vgpu-temporal      — the same, policy named explicitly
   vgpu-mask          — the same 2 pods, one CU mask each
   vgpu-cu25          — 4 pods × gpucores=25 (BASELINE.json config 3), default policy (auto)
@@ -38,17 +38,17 @@ REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 SCENARIOS = {
     "exclusive": ["--pods", "1", "--no-shim", "--gpucores", "100", "--gpumem", "0"],
-    "vgpu": ["--pods", "2", "--gpucores", "50", "--gpumem", "144000", "--warmup-seconds", "6"],
+    "vgpu": ["--pods", "2", "--gpucores", "50", "--gpumem", "144000", "--warmup-seconds", "12"],
     "vgpu-temporal": ["--pods", "2", "--gpucores", "50", "--gpumem", "144000", "--cu-share", "temporal"],
     "vgpu-mask": ["--pods", "2", "--gpucores", "50", "--gpumem", "144000", "--cu-share", "mask"],
     "vgpu-cu25-hybrid": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "hybrid"],
-    "vgpu-cu25": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--warmup-seconds", "6"],
+    "vgpu-cu25": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--warmup-seconds", "12"],
     "vgpu-cu25-temporal": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "temporal"],
     "vgpu-cu25-mask": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "mask"],
     "vgpu-cu25-auto": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "auto",
-                       "--warmup-seconds", "6"],
+                       "--warmup-seconds", "12"],
     "vgpu-auto": ["--pods", "2", "--gpucores", "50", "--gpumem", "144000", "--cu-share", "auto",
-                  "--warmup-seconds", "6"],
+                  "--warmup-seconds", "12"],
     "vgpu-vmem": ["--pods", "2", "--gpucores", "0", "--gpumem", "230000", "--oversubscribe",
                   "--memory-scaling", "1.8"],
     "vgpu-cu25-k2": ["--pods", "4", "--gpucores", "25", "--gpumem", "70000", "--cu-share", "temporal",
