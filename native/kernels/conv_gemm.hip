@@ -1010,29 +1010,36 @@ hipError_t dispatch_pro(const ConvArgs& a, bool res, hipStream_t s) {
   return res ? launch_pro<KS, BM, 64, true>(a, s) : launch_pro<KS, BM, 64, false>(a, s);
 }
 
-// epilogue_halves for a conv3 chunk whose output also feeds the next block's
-// conv1: besides storing y = acc + residual (bf16), each thread keeps
-// p = relu(bf16(y) * s[c] + t[c]) (the next block-entry BN+ReLU, rounded to
-// bf16 exactly as conv_pro's prologue stages it) for its rows in registers.
-template <int BM, int BN>
-__device__ __forceinline__ void epilogue_halves_next(const ConvArgs& a, f32x4_t (&acc)[BM / 32][BN / 32],
-                                                     int m0, int n0, char* smem,
-                                                     const u32x4 (&res)[2][EpiShape<BM, BN>::RROWS],
-                                                     const float* __restrict__ ps, const float* __restrict__ pt,
-                                                     u32x4 (&pv)[2][EpiShape<BM, BN>::RROWS]) {
+// conv23's conv3-chunk epilogue, one row half at a time: fp32 accumulators →
+// LDS staging → + residual → bf16 y.  The stores are unconditional buffer
+// stores (rows past M go to an out-of-range offset and are dropped), so every
+// thread issues exactly 2·RROWS of them: the kernel's counted vmcnt waits rely
+// on that count.  Barriers are raw (lgkmcnt only), so an LDS-DMA issued before
+// the epilogue's last LDS write (`mid`) stays in flight across the rest of it
+// (a __syncthreads() would drain it).
+// NEXT: also p = relu(bf16(y) * s[c] + t[c]) (the next block-entry BN+ReLU,
+// rounded to bf16 exactly as conv_pro's prologue stages it) for this thread's
+// rows, into registers; s/t are read from LDS (sPs/sPt), never from global
+// memory, for the same reason.
+template <int BM, int BN, bool NEXT, typename Mid>
+__device__ __forceinline__ void tail_epilogue(const ConvArgs& a, f32x4_t (&acc)[BM / 32][BN / 32], int m0, int n0,
+                                              char* smem, const u32x4 (&res)[2][EpiShape<BM, BN>::RROWS],
+                                              const float* sPs, const float* sPt,
+                                              u32x4 (&pv)[2][EpiShape<BM, BN>::RROWS], Mid mid) {
   constexpr int WTM = BM / 2, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
   constexpr int CS = BN + 4, HROWS = BM / 2;
-  constexpr int CPR = BN / 8, RSTEP = kThreads / CPR, RROWS = HROWS / RSTEP;
+  using E = EpiShape<BM, BN>;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fk = lane >> 4;
-  const int chunk = t % CPR, rfirst = t / CPR;
+  const int chunk = t % E::CPR, rfirst = t / E::CPR;
   const int col = n0 + chunk * 8;
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, a.y_bytes, 0x00020000);
   float sc[8], sh[8];
-  {
-    const float4 s0 = *reinterpret_cast<const float4*>(ps + col);
-    const float4 s1 = *reinterpret_cast<const float4*>(ps + col + 4);
-    const float4 h0 = *reinterpret_cast<const float4*>(pt + col);
-    const float4 h1 = *reinterpret_cast<const float4*>(pt + col + 4);
+  if constexpr (NEXT) {
+    const float4 s0 = *reinterpret_cast<const float4*>(sPs + col);
+    const float4 s1 = *reinterpret_cast<const float4*>(sPs + col + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(sPt + col);
+    const float4 h1 = *reinterpret_cast<const float4*>(sPt + col + 4);
     sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
     sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w; sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
   }
@@ -1048,26 +1055,47 @@ __device__ __forceinline__ void epilogue_halves_next(const ConvArgs& a, f32x4_t 
           for (int e = 0; e < 4; ++e)
             sC[(i * 16 + fk * 4 + e) * CS + wn * WTN + j * 16 + fr] = acc[i][j][e];
     }
-    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    __builtin_amdgcn_s_barrier();
+    // This half's staged rows + residual, all read before `mid`: an LDS-DMA
+    // issued by `mid` (past the epilogue's last LDS access — hipcc drains every
+    // in-flight LDS-DMA at the next ds_read/ds_write) overlaps the stores.
+    float v[E::RROWS][8];
 #pragma unroll
-    for (int i = 0; i < RROWS; ++i) {
-      const int r = rfirst + RSTEP * i, m = m0 + h * HROWS + r;
+    for (int i = 0; i < E::RROWS; ++i) {
+      const int r = rfirst + E::RSTEP * i;
       const float4 c0 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8);
       const float4 c1 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8 + 4);
-      float v[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
       float re[8];
       unpack8(res[h][i], re);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += re[j];
-      const u32x4 yv = pack8(v);
-      if (m < a.M) *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = yv;
-      float q[8];
-      unpack8(yv, q);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) q[j] = fmaxf(q[j] * sc[j] + sh[j], 0.0f);
-      pv[h][i] = pack8(q);
+      v[i][0] = c0.x + re[0]; v[i][1] = c0.y + re[1]; v[i][2] = c0.z + re[2]; v[i][3] = c0.w + re[3];
+      v[i][4] = c1.x + re[4]; v[i][5] = c1.y + re[5]; v[i][6] = c1.z + re[6]; v[i][7] = c1.w + re[7];
     }
-    __syncthreads();  // this half read out before the next staging / the A3 image reuses it
+    if (h == 1) {
+      __builtin_amdgcn_s_waitcnt(kLgkm0);
+      __builtin_amdgcn_s_barrier();  // every wave's staging reads done
+      __builtin_amdgcn_sched_barrier(0);
+      mid();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int i = 0; i < E::RROWS; ++i) {
+      const int r = rfirst + E::RSTEP * i, m = m0 + h * HROWS + r;
+      const u32x4 yv = pack8(v[i]);
+      __builtin_amdgcn_raw_buffer_store_b128(yv, yr, m < a.M ? (uint32_t)(((int64_t)m * a.Cout + col) * 2) : kOOB,
+                                             0, 0);
+      if constexpr (NEXT) {
+        float q[8];
+        unpack8(yv, q);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) q[j] = fmaxf(q[j] * sc[j] + sh[j], 0.0f);
+        pv[h][i] = pack8(q);
+      }
+    }
+    if (h == 0) {
+      __builtin_amdgcn_s_waitcnt(kLgkm0);
+      __builtin_amdgcn_s_barrier();  // half 0 read out before half 1 is staged
+    }
   }
 }
 
@@ -1109,8 +1137,12 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
   constexpr int P1 = 2 * STAGE, P2 = B2_BYTES + EPI;
   constexpr int P = P1 > P2 ? P1 : P2;
   constexpr int A2_BYTES = BM * 128 * KCH;
-  __shared__ __attribute__((aligned(16))) char smem[P + A2_BYTES];
+  // conv2 bias [W] and (NEXT) conv1's prologue scale/shift [4W] each live in
+  // LDS: a global load in phase 2 would make hipcc drain the in-flight DMA.
+  constexpr int PAR = (W + (NEXT ? 8 * W : 0)) * 4;
+  __shared__ __attribute__((aligned(16))) char smem[P + A2_BYTES + PAR];
   char* sA2 = smem + P;
+  float* sPar = reinterpret_cast<float*>(smem + P + A2_BYTES);
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -1139,6 +1171,15 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
     abase[i] = ((n * a.H + aih[i]) * a.W + aiw[i]) * a.C * 2;
   }
   const uint32_t boff = (uint32_t)((lrow * a.K + lchunk * 8) * 2);
+  for (int i = t * 4; i < W; i += kThreads * 4)
+    *reinterpret_cast<float4*>(sPar + i) = *reinterpret_cast<const float4*>(a.bias + i);
+  if constexpr (NEXT) {
+    for (int i = t * 4; i < 4 * W; i += kThreads * 4) {
+      *reinterpret_cast<float4*>(sPar + W + i) = *reinterpret_cast<const float4*>(c.pscale + i);
+      *reinterpret_cast<float4*>(sPar + 5 * W + i) = *reinterpret_cast<const float4*>(c.pshift + i);
+    }
+  }
+  __syncthreads();
 
   auto issue = [&](int kt, int st) {
     char* sA = smem + st * STAGE;
@@ -1183,13 +1224,49 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
     __builtin_amdgcn_s_barrier();
   }
 
+  // ---- phase 2: conv3 over 128-wide output chunks --------------------------------
+  // Per chunk ch the weight panel w3(ch) and the residual res(ch) are issued
+  // one step ahead (behind the previous chunk's work), so the chunk starts on a
+  // counted vmcnt that leaves the residual — and, without NEXT, the previous
+  // chunk's y stores — in flight:
+  //   wait w3(ch) · conv3 MMA · vmcnt(0) (res landed) · barrier ·
+  //   NEXT: load w1(ch) to registers ‖ epilogue + p · A3 image · w1 → LDS ·
+  //         conv1 MMA · issue w3/res(ch+1)
+  //   else: epilogue, with the DMA of w3(ch+1) issued behind its last LDS
+  //         write · issue res(ch+1)
+  // VMEM ops complete in issue order (loads, stores and LDS-DMA alike), so a
+  // counted wait retires everything older than its window; the epilogue's
+  // stores are unconditional, so their count is exact.  w1 goes through
+  // registers because hipcc drains every in-flight LDS-DMA at the next
+  // ds_write, and the epilogue and the A3 image are all ds_writes.
+  using E2 = EpiShape<BM, 128>;
+  constexpr int R = 2 * E2::RROWS;  // residual loads = y stores per thread per chunk
+  constexpr int WTM2 = BM / 2, TM2 = WTM2 / 16;
+  char* sB2 = smem;
+  char* sE = smem + B2_BYTES;
+  const int nchunks = b.Cout / BN2;
+  auto issue_w3 = [&](int ch) {
+#pragma unroll
+    for (int kc = 0; kc < KCH; ++kc)
+#pragma unroll
+      for (int i = 0; i < BN2 / 32; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            w3r, (lds_void_t*)(sB2 + kc * (BN2 * 128) + (32 * i + wave * 8) * 128), 16,
+            (uint32_t)(((ch * BN2 + lrow + 32 * i) * b.K + kc * 64 + lchunk * 8) * 2), 0, 0, 0);
+  };
+  u32x4 res[2][E2::RROWS];
+  // res(0) flies while the conv2 tile is turned into conv3's A image; w3(0)
+  // goes into the (free) phase-1 stages after that image's ds_writes, which
+  // would otherwise drain it.
+  load_residual<BM, BN2>(b, m0, 0, res);
+
   // conv2 bias + ReLU → bf16 → conv3's A image: lane (fr, fk) of subtile (i, j)
   // holds row i*16+fr (+wave offset), channels j*16+fk*4 .. +3.
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int c = wn * WTN + j * 16 + fk * 4;
-    const float4 bb = *reinterpret_cast<const float4*>(a.bias + c);
-    const int panel = c >> 6, cc = c & 63;
+    const int cc0 = wn * WTN + j * 16 + fk * 4;
+    const float4 bb = *reinterpret_cast<const float4*>(sPar + cc0);
+    const int panel = cc0 >> 6, cc = cc0 & 63;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int r = wm * WTM + i * 16 + fr;
@@ -1200,10 +1277,8 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
     }
   }
 
-  // ---- phase 2: conv3 over 128-wide output chunks --------------------------------
-  constexpr int WTM2 = BM / 2, TM2 = WTM2 / 16;
-  char* sB2 = smem;
-  const int nchunks = b.Cout / BN2;
+  issue_w3(0);
+
   // phase 3 (NEXT): conv1 of the next block, W outputs per row, K = 4W
   constexpr int TM3 = BM / 32, TN3 = W / 32;
   f32x4_t acc3[TM3][TN3];
@@ -1218,69 +1293,77 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
       0x00020000);
   for (int ch = 0; ch < nchunks; ++ch) {
     const int c0 = ch * BN2;
-#pragma unroll
-    for (int kc = 0; kc < KCH; ++kc)
-#pragma unroll
-      for (int i = 0; i < BN2 / 32; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            w3r, (lds_void_t*)(sB2 + kc * (BN2 * 128) + (32 * i + wave * 8) * 128), 16,
-            (uint32_t)(((c0 + lrow + 32 * i) * b.K + kc * 64 + lchunk * 8) * 2), 0, 0, 0);
-    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-    __syncthreads();  // B2 landed; A2 written (first chunk); previous chunk's staging read out
+    // w3(ch) landed; res(ch) may fly, and without NEXT the previous chunk's
+    // second-half stores (issued after w3(ch), behind the epilogue's last ds_write)
+    if (ch == 0)
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // res(0) was issued before w3(0)
+    else if (NEXT)
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(R));
+    else
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(R + R / 2));
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    __builtin_amdgcn_s_barrier();  // B2 visible; A2 written (first chunk); previous staging read out
     f32x4_t acc2[TM2][TN2];
 #pragma unroll
     for (int i = 0; i < TM2; ++i)
 #pragma unroll
       for (int j = 0; j < TN2; ++j) acc2[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kc = 0; kc < KCH; ++kc) {
-      const char* pA = sA2 + kc * (BM * 128);
-      const char* pB = sB2 + kc * (BN2 * 128);
-      mma_k64<TM2, TN2>(pA, pB, wm * WTM2, wn * 64, fr, fk, acc2);
-    }
-    // B2 reads must finish before the next chunk's DMA overwrites the panel;
-    // the staging area of the epilogue does not overlap it.
+    for (int kc = 0; kc < KCH; ++kc)
+      mma_k64<TM2, TN2>(sA2 + kc * (BM * 128), sB2 + kc * (BN2 * 128), wm * WTM2, wn * 64, fr, fk, acc2);
+    // res(ch) landed before any DMA is issued behind it (hipcc would otherwise
+    // drain that DMA at the residual's first use); B2 read out by every wave
+    // before the next DMA overwrites it.
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     __builtin_amdgcn_s_barrier();
-    u32x4 res[2][EpiShape<BM, BN2>::RROWS];
+    u32x4 pv[2][E2::RROWS];
     if constexpr (!NEXT) {
-      load_residual<BM, BN2>(b, m0, c0, res);
-      epilogue_halves<BM, BN2, true>(b, acc2, m0, c0, smem + B2_BYTES, res);
+      const bool more = ch + 1 < nchunks;
+      tail_epilogue<BM, BN2, false>(b, acc2, m0, c0, sE, res, sPar, sPar, pv, [&] {
+        if (more) issue_w3(ch + 1);
+      });
+      if (more) load_residual<BM, BN2>(b, m0, c0 + BN2, res);
     } else {
-      // conv1's weight K chunk [W rows][c0 .. c0+127] into the (now idle) B2
-      // slot, in flight behind the epilogue: two 64-wide K panels of W rows.
+      // conv1's weight K chunk [W rows][c0 .. c0+127] (two 64-wide K panels of
+      // W rows), in flight in registers behind the epilogue.
+      u32x4 w1v[2][W / 32];
 #pragma unroll
       for (int kc = 0; kc < 2; ++kc)
 #pragma unroll
         for (int i = 0; i < W / 32; ++i)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              w1r, (lds_void_t*)(sB2 + kc * (W * 128) + (32 * i + wave * 8) * 128), 16,
-              (uint32_t)(((lrow + 32 * i) * c.K + c0 + kc * 64 + lchunk * 8) * 2), 0, 0, 0);
-      load_residual<BM, BN2>(b, m0, c0, res);
-      u32x4 pv[2][EpiShape<BM, BN2>::RROWS];
-      char* sE = smem + B2_BYTES;
-      epilogue_halves_next<BM, BN2>(b, acc2, m0, c0, sE, res, c.pscale, c.pshift, pv);
+          w1v[kc][i] = __builtin_amdgcn_raw_buffer_load_b128(
+              w1r, (uint32_t)(((lrow + 32 * i) * c.K + c0 + kc * 64 + (t & 7) * 8) * 2), 0, 0);
+      tail_epilogue<BM, BN2, true>(b, acc2, m0, c0, sE, res, sPar + W, sPar + 5 * W, pv, [] {});
       // A3 image (BM rows x 128 channels = two 64-wide swizzled panels) in the
       // staging area, which the epilogue has finished reading.
       {
-        using E = EpiShape<BM, BN2>;
-        const int chunk = t % E::CPR, rfirst = t / E::CPR;
+        const int chunk = t % E2::CPR, rfirst = t / E2::CPR;
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
-          for (int i = 0; i < E::RROWS; ++i) {
-            const int r = h * E::HROWS + rfirst + E::RSTEP * i;
+          for (int i = 0; i < E2::RROWS; ++i) {
+            const int r = h * E2::HROWS + rfirst + E2::RSTEP * i;
             *reinterpret_cast<u32x4*>(sE + (chunk >> 3) * (BM * 128) + swz(r, chunk & 7)) = pv[h][i];
           }
       }
-      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-      __syncthreads();  // A3 written, conv1 weight chunk landed
+#pragma unroll
+      for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+        for (int i = 0; i < W / 32; ++i)
+          *reinterpret_cast<u32x4*>(sB2 + kc * (W * 128) + swz(lrow + 32 * i, t & 7)) = w1v[kc][i];
+      __builtin_amdgcn_s_waitcnt(kLgkm0);
+      __builtin_amdgcn_s_barrier();  // A3 written, conv1 weight chunk visible
 #pragma unroll
       for (int kc = 0; kc < 2; ++kc)
         mma_k64<TM3, TN3>(sE + kc * (BM * 128), sB2 + kc * (W * 128), wm * (BM / 2), wn * (W / 2), fr, fk,
                           acc3);
       __builtin_amdgcn_s_waitcnt(kLgkm0);
       __builtin_amdgcn_s_barrier();  // A3 / weight chunk read before the next chunk reuses them
+      if (ch + 1 < nchunks) {
+        issue_w3(ch + 1);
+        load_residual<BM, BN2>(b, m0, c0 + BN2, res);
+      }
     }
   }
   if constexpr (NEXT) {

@@ -94,6 +94,30 @@ def main(argv=None) -> int:
             tot[1] += t[1]
             print(json.dumps({"layer": name, "new_us": round(t[0], 1), "old_us": round(t[1], 1),
                               "bit_exact": bool(torch.equal(ys[0], ys[1]))}), flush=True)
+            if not hasattr(old, "vgpu_conv231_nhwc"):
+                continue
+            # + the next identity block's BN+ReLU+conv1 (conv231, stride-1 shapes)
+            w1n = (torch.randn(c, 4 * c, 1, 1, device=dev) * (2 / (4 * c)) ** 0.5).to(
+                torch.bfloat16).contiguous(memory_format=cl)
+            b1n = torch.zeros(c, device=dev)
+            ps, pt = torch.rand(4 * c, device=dev) + 0.5, torch.randn(4 * c, device=dev) * 0.1
+            hs = [torch.empty(n, c, oh, oh, device=dev, dtype=torch.bfloat16).contiguous(memory_format=cl)
+                  for _ in range(2)]
+
+            def run231(lib, y, h1):
+                rc = lib.vgpu_conv231_nhwc(P(x), P(w2), P(b2), P(w3), P(r), P(y), P(w1n), P(b1n), P(ps), P(pt),
+                                           P(h1), n, h, h, c, stride, C._stream())
+                assert rc == 0, rc
+            t = [0.0, 0.0]
+            for _ in range(3):
+                t[0] += timeit(lambda: run231(cur, ys[0], hs[0])) / 3
+                t[1] += timeit(lambda: run231(old, ys[1], hs[1])) / 3
+            tot[0] += t[0]
+            tot[1] += t[1]
+            print(json.dumps({"layer": name.replace("tail", "tail+next"), "new_us": round(t[0], 1),
+                              "old_us": round(t[1], 1),
+                              "bit_exact": bool(torch.equal(ys[0], ys[1]) and torch.equal(hs[0], hs[1]))}),
+                  flush=True)
     print(json.dumps({"total_new_us": round(tot[0], 1), "total_old_us": round(tot[1], 1)}), flush=True)
     return 0
 
