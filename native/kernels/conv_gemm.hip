@@ -74,8 +74,12 @@ __device__ __forceinline__ void unpack8(const u32x4 v, float (&f)[8]) {
   f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
   f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
 }
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+// One v_cvt_pk_bf16_f32 per pair (RNE, the same rounding as two scalar
+// conversions); the scalar form costs two conversions + shift + or.
 __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
 }
 __device__ __forceinline__ u32x4 pack8(const float (&f)[8]) {
   return u32x4{pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7])};
@@ -837,9 +841,8 @@ hipError_t dispatch_glds(const ConvArgs& a, bool res, hipStream_t s) {
 // (global → VGPR → affine+ReLU → ds_write, zero padding re-applied after the
 // prologue).  The weights need no transform and go HBM → LDS by DMA, which
 // halves the ds_write_b128 traffic that bounds the all-register kernel.
-// Per K step kt:  DMA B(kt+1) into the idle stage; load A(kt+2) into the free
-// register set; MFMA on stage kt; prologue + ds_write of A(kt+1) into the idle
-// stage; vmcnt(AR) (= B(kt+1) landed, A(kt+2) still in flight); barrier.
+// Pipeline: see the K loop (A two steps ahead in registers, B one step ahead
+// by DMA).
 template <int KS, int BM, int BN, bool RES>
 __global__ void __launch_bounds__(kThreads, 2) conv_pro_kernel(const ConvArgs a) {
   constexpr int AR = BM / 32, BR = BN / 32;
@@ -896,7 +899,8 @@ __global__ void __launch_bounds__(kThreads, 2) conv_pro_kernel(const ConvArgs a)
           boff + (uint32_t)((32 * i * a.K + kt * BK) * 2), 0, 0, 0);
   };
   auto load_a = [&](int kt, u32x4 (&ra)[AR], bool (&rv)[AR]) {
-    const int tap = kt / a.cblocks, cb = kt - tap * a.cblocks;
+    // 1x1: K = C, so the tap is 0 and the K step is the channel block.
+    const int tap = KS == 1 ? 0 : kt / a.cblocks, cb = kt - tap * a.cblocks;
     const int kh = tap / KS, kw = tap - kh * KS;
     const int toff = ((kh * a.W + kw) * a.C + cb * BK + slot * 8) * 2;
 #pragma unroll
@@ -910,7 +914,12 @@ __global__ void __launch_bounds__(kThreads, 2) conv_pro_kernel(const ConvArgs a)
   };
   auto store_a = [&](int kt, int st, u32x4 (&ra)[AR], const bool (&rv)[AR]) {
     char* sA = smem + st * STAGE;
-    const int c = (kt % a.cblocks) * BK + slot * 8;
+    const int c = (KS == 1 ? kt : kt % a.cblocks) * BK + slot * 8;
+    // Pin the A registers here: without it hipcc hoists this step's unpacking
+    // into the previous step, ahead of that step's barrier, and waits for the
+    // loads a step early.
+#pragma unroll
+    for (int i = 0; i < AR; ++i) asm volatile("" : "+v"(ra[i]));
     const float4 s0 = *reinterpret_cast<const float4*>(sPar + c);
     const float4 s1 = *reinterpret_cast<const float4*>(sPar + c + 4);
     const float4 h0 = *reinterpret_cast<const float4*>(sPar + a.C + c);
@@ -922,11 +931,13 @@ __global__ void __launch_bounds__(kThreads, 2) conv_pro_kernel(const ConvArgs a)
       float e[8];
       unpack8(ra[i], e);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float f = fmaxf(e[j] * sc[j] + sh[j], 0.0f);
-        e[j] = rv[i] ? f : 0.0f;  // padding / M tail stay zero after the prologue
-      }
-      *reinterpret_cast<u32x4*>(sA + swz(r0 + 32 * i, slot)) = pack8(e);
+      for (int j = 0; j < 8; ++j) e[j] = fmaxf(e[j] * sc[j] + sh[j], 0.0f);
+      u32x4 p = pack8(e);
+      // Zero padding stays zero after the prologue.  A 1x1 conv has no
+      // padding, and an M-tail row only feeds its own (never stored) output
+      // row, so it skips the select.
+      if constexpr (KS != 1) p = rv[i] ? p : u32x4{0u, 0u, 0u, 0u};
+      *reinterpret_cast<u32x4*>(sA + swz(r0 + 32 * i, slot)) = p;
     }
   };
   auto compute = [&](int st, f32x4_t (&acc)[TM][TN]) {
@@ -959,35 +970,52 @@ __global__ void __launch_bounds__(kThreads, 2) conv_pro_kernel(const ConvArgs a)
   bool rv0[AR], rv1[AR];
   const int nk = a.ktiles;
   u32x4 res[2][EpiShape<BM, BN>::RROWS];
+  // Per K step kt (stage st = kt & 1 holds A(kt), B(kt)):
+  //   prologue + ds_write of A(kt+1) into stage st^1 (registers X, loaded two
+  //   steps ago) · DMA B(kt+1) into st^1 · load A(kt+3) into X · MFMA on st ·
+  //   vmcnt(AR): retires B(kt+1) and A(kt+2) (set Y, loaded one step ago),
+  //   leaves A(kt+3) in flight · barrier.
+  // Every ds_write of a step precedes its DMA: hipcc makes a ds_write wait for
+  // all LDS-DMA in flight, which would serialise the pipeline.  The loads of
+  // A(kt+3) are issued behind the DMA, so the step's own wait does not retire
+  // them: they get two steps of lead.
   load_a(0, ra0, rv0);
-  issue_b(0, 0);
-  store_a(0, 0, ra0, rv0);
   load_a(nk > 1 ? 1 : 0, ra1, rv1);
+  store_a(0, 0, ra0, rv0);
+  issue_b(0, 0);
+  load_a(nk > 2 ? 2 : nk - 1, ra0, rv0);
   __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR));
   __builtin_amdgcn_s_waitcnt(kLgkm0);
   __builtin_amdgcn_s_barrier();
-  // Unrolled by two so the register sets stay static: step kt stores set
-  // (kt+1)&1 and refills set kt&1 with A(kt+2).
+  // Unrolled by two so the register sets stay static: step kt stores set X
+  // and refills it with A(kt+3).
   // Branch-free body: past the last K step the loads re-fetch the last tile into
   // the idle stage (never read) — a branch around a load would make hipcc wait
   // vmcnt(0) there and de-pipeline the loop.
-  auto step = [&](int kt, u32x4 (&rn)[AR], bool (&vn)[AR], u32x4 (&rs)[AR], bool (&vs)[AR]) {
+  auto step = [&](int kt, u32x4 (&rx)[AR], bool (&vx)[AR]) {
     const int st = kt & 1;
-    const int k1 = kt + 1 < nk ? kt + 1 : nk - 1, k2 = kt + 2 < nk ? kt + 2 : nk - 1;
+    const int k1 = kt + 1 < nk ? kt + 1 : nk - 1, k3 = kt + 3 < nk ? kt + 3 : nk - 1;
+    // sched_barriers keep hipcc's scheduler from reordering the phases (it
+    // would hoist the A loads above the ds_writes — so the step's wait retires
+    // them — and sink the MFMAs below the wait).
+    store_a(k1, st ^ 1, rx, vx);
+    __builtin_amdgcn_sched_barrier(0);
     issue_b(k1, st ^ 1);
-    load_a(k2, rn, vn);
+    __builtin_amdgcn_sched_barrier(0);
+    load_a(k3, rx, vx);
+    __builtin_amdgcn_sched_barrier(0);
     compute(st, acc);
-    store_a(k1, st ^ 1, rs, vs);
+    __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR));
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     __builtin_amdgcn_s_barrier();
   };
   int kt = 0;
   for (; kt + 1 < nk; kt += 2) {
-    step(kt, ra0, rv0, ra1, rv1);
-    step(kt + 1, ra1, rv1, ra0, rv0);
+    step(kt, ra1, rv1);
+    step(kt + 1, ra0, rv0);
   }
-  if (kt < nk) step(kt, ra0, rv0, ra1, rv1);
+  if (kt < nk) step(kt, ra1, rv1);
   __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // the trailing dummy loads, before LDS reuse
   __syncthreads();
   if constexpr (RES) load_residual<BM, BN>(a, m0, n0, res);
@@ -1785,7 +1813,8 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
       e = small ? launch_glds<4, 64, 64, false, 16>(c, s) : launch_glds<4, 128, 64, false, 16>(c, s);
     // Short K (≤ 2 steps) or 64-wide outputs: the persistent register kernel,
     // which overlaps the next tile's loads with this tile's epilogue, wins there.
-    else if (pro && pro_dma_enabled() && C <= 2048 && a.ktiles > 2 && Cout > 64)
+    // (conv_pro's 1x1 form assumes no padding: it skips the zero-padding select.)
+    else if (pro && pro_dma_enabled() && C <= 2048 && a.ktiles > 2 && Cout > 64 && (KS != 1 || pad == 0))
       e = KS == 1 ? (small ? dispatch_pro<1, 64>(c, has_res, s) : dispatch_pro<1, 128>(c, has_res, s))
                   : (small ? dispatch_pro<3, 64>(c, has_res, s) : dispatch_pro<3, 128>(c, has_res, s));
     else if (glds)
