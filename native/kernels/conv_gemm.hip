@@ -1622,6 +1622,152 @@ __global__ void __launch_bounds__(kThreads) s2d_stem_kernel(const uint16_t* __re
   Xp[1] = hi;
 }
 
+// ---- ResNet stem conv + 3x3/s2 max pool in one persistent kernel ----------
+// The stem conv (4x4/s1 over the space-to-depth input, C = 16, 64 outputs)
+// writes a 4x-wide activation (b=50 at 346²: 191 MB) that the max pool reads
+// straight back.  Here one task = one pooled output row (n, i): the stem rows
+// 2i-1 .. 2i+1 are computed from a 6-row input slab in LDS and rounded to bf16
+// into LDS row buffers (exactly what the unfused conv stores), then
+// max-pooled from there, so only the input slab and the pooled row touch HBM.
+// The 32 KB filter is loaded once per workgroup; the next task's slab is
+// fetched into registers while the current task computes.
+// The three stem rows are 3 x 11 pixel subtiles of 16; subtile s goes to wave
+// s % 8, which computes all 64 channels of it (4 B fragments shared by up to 5
+// A fragments per K step).  mfma(B, A) (transposed tile) so a lane holds 4
+// consecutive channels of one pixel.  K order (kh, kw, c) and the MFMA
+// sequence match the unfused stem conv, so the result is bit-identical to
+// conv + maxpool (tests/test_gpu_conv.py).
+constexpr int kSPThreads = 512;
+constexpr int kSPMaxOW = 176;   // 11 pixel subtiles of 16
+constexpr int kSPMaxWS = 180;
+
+__global__ void __launch_bounds__(kSPThreads, 1) stem_pool_kernel(const uint16_t* __restrict__ X,
+                                                                  const uint16_t* __restrict__ w,
+                                                                  uint16_t* __restrict__ y, int HS, int WS,
+                                                                  int OH, int OW, int PH, int PW, int tasks) {
+  constexpr int SW_BYTES = 4 * 64 * 128;         // [kh][cout][128 B] swizzled
+  constexpr int SR_BYTES = 3 * kSPMaxOW * 128;   // three bf16 stem rows [row][pixel][64 ch] swizzled
+  constexpr int SX_BYTES = 6 * kSPMaxWS * 32 + 512;  // 6 input rows [px][16 ch] + over-read pad
+  constexpr int XR = (6 * kSPMaxWS * 2 + kSPThreads - 1) / kSPThreads;  // slab chunks per thread
+  constexpr int NS = 5;                          // subtiles per wave (33 over 8 waves)
+  __shared__ __attribute__((aligned(16))) char smem[SW_BYTES + SR_BYTES + SX_BYTES];
+  char* sW = smem;
+  char* sR = smem + SW_BYTES;
+  char* sX = sR + SR_BYTES;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int MT = (OW + 15) >> 4;
+  const int rowc = WS * 2, nchunk = 6 * rowc;  // 16-B chunks per slab row / per slab
+
+  // filter → LDS once: chunk k = (cout, kh, slot)
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int k = t + kSPThreads * u, co = k >> 5, c16 = k & 31;
+    *reinterpret_cast<u32x4*>(sW + (c16 >> 3) * 8192 + swz(co, c16 & 7)) =
+        *reinterpret_cast<const u32x4*>(w + co * 256 + c16 * 8);
+  }
+  auto load_slab = [&](int task, u32x4 (&xr)[XR]) {
+    const int n = task / PH, r0 = 2 * (task - n * PH) - 1;
+#pragma unroll
+    for (int u = 0; u < XR; ++u) {
+      const int k = t + kSPThreads * u, q = k / rowc, rem = k - q * rowc, row = r0 + q;
+      const bool ok = k < nchunk && row >= 0 && row < HS;
+      xr[u] = ok ? *reinterpret_cast<const u32x4*>(X + ((int64_t)(n * HS + row) * WS) * 16 + rem * 8)
+                 : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store_slab = [&](const u32x4 (&xr)[XR]) {
+#pragma unroll
+    for (int u = 0; u < XR; ++u) {
+      const int k = t + kSPThreads * u;
+      if (k < nchunk) *reinterpret_cast<u32x4*>(sX + k * 16) = xr[u];
+    }
+  };
+  u32x4 xr[XR];
+  int task = blockIdx.x;
+  if (task < tasks) {
+    load_slab(task, xr);
+    store_slab(xr);
+  }
+  __syncthreads();
+  for (; task < tasks; task += gridDim.x) {
+    const int n = task / PH, pi = task - n * PH, r0 = 2 * pi - 1;
+    const int next = task + gridDim.x;
+    if (next < tasks) load_slab(next, xr);  // lands behind this task's compute
+    // this wave's subtiles s = wave + 8u: stem row rl = s / MT, pixels (s % MT)*16 ..
+    f32x4_t acc[NS][4];
+#pragma unroll
+    for (int u = 0; u < NS; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[u][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 4; ++kh)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8_t bfr[4], af[NS];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8_t*>(sW + kh * 8192 + swz(j * 16 + fr, kk * 4 + fk));
+#pragma unroll
+        for (int u = 0; u < NS; ++u) {
+          const int sidx = wave + 8 * u, rl = sidx / MT, m = sidx - rl * MT;
+          if (sidx < 3 * MT)  // wave-uniform; past the three rows there is nothing to read
+            af[u] = *reinterpret_cast<const bf16x8_t*>(
+                sX + (((rl + kh) * WS + m * 16 + fr) * 32) + (kk * 4 + fk) * 16);
+        }
+#pragma unroll
+        for (int u = 0; u < NS; ++u)
+          if (wave + 8 * u < 3 * MT)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[u], acc[u][j], 0, 0, 0);
+      }
+    // bf16 stem rows → LDS: lane holds pixel m*16+fr, channels j*16+fk*4 .. +3
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int sidx = wave + 8 * u, rl = sidx / MT, m = sidx - rl * MT;
+      if (rl >= 3) continue;
+      const int p = m * 16 + fr;
+      char* row = sR + rl * (kSPMaxOW * 128) + p * 128;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int slot = j * 2 + (fk >> 1);
+        *reinterpret_cast<uint2*>(row + ((slot ^ (p & 7)) << 4) + (fk & 1) * 8) =
+            uint2{pack2(acc[u][j][0], acc[u][j][1]), pack2(acc[u][j][2], acc[u][j][3])};
+      }
+    }
+    __syncthreads();
+    // 3x3/s2 window (rows of the task that exist, columns 2j-1 .. 2j+1)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int it = t + kSPThreads * k, j = it >> 3, q = it & 7;
+      if (j >= PW) continue;
+      float pm[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pm[e] = -INFINITY;
+#pragma unroll
+      for (int rl = 0; rl < 3; ++rl) {
+        if (r0 + rl < 0 || r0 + rl >= OH) continue;
+#pragma unroll
+        for (int dc = -1; dc <= 1; ++dc) {
+          const int c = 2 * j + dc;
+          if (c < 0 || c >= OW) continue;
+          float e[8];
+          unpack8(*reinterpret_cast<const u32x4*>(sR + rl * (kSPMaxOW * 128) + c * 128 + ((q ^ (c & 7)) << 4)), e);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) pm[u] = fmaxf(pm[u], e[u]);
+        }
+      }
+      *reinterpret_cast<u32x4*>(y + ((int64_t)(n * PH + pi) * PW + j) * 64 + q * 8) = pack8(pm);
+    }
+    if (next < tasks) {
+      __syncthreads();  // every wave done with the slab and the row buffers
+      store_slab(xr);
+      __syncthreads();
+    }
+  }
+}
+
 }  // namespace
 
 VGPU_API int vgpu_stem_space_to_depth(const void* x, void* X, int N, int H, int W, int pad, int HS,
@@ -1830,6 +1976,22 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
 }
 
 // NHWC bf16 max pool (k×k window, stride, symmetric zero-excluded padding), 16 B per lane.
+// Fused stem: X [N][HS][WS][16] (space-to-depth input), w [64][4][4][16] →
+// y [N][PH][PW][64] = maxpool3x3/s2/p1(conv4x4/s1(X, w)), bf16 NHWC.
+VGPU_API int vgpu_stem_pool_nhwc(const void* X, const void* w, void* y, int N, int HS, int WS, hipStream_t s) {
+  const int OH = HS - 3, OW = WS - 3;
+  if (N < 1 || OH < 1 || OW < 1 || OW > kSPMaxOW || WS > kSPMaxWS) return -1;
+  if ((int64_t)N * HS * WS * 16 >= ((int64_t)1 << 31)) return -1;
+  const int PH = (OH + 2 - 3) / 2 + 1, PW = (OW + 2 - 3) / 2 + 1;
+  if (PW * 8 > 2 * kSPThreads) return -1;
+  const int tasks = N * PH;
+  int grid = conv_cus();
+  if (grid > tasks) grid = tasks;
+  hipLaunchKernelGGL(stem_pool_kernel, dim3(grid), dim3(kSPThreads), 0, s, static_cast<const uint16_t*>(X),
+                     static_cast<const uint16_t*>(w), static_cast<uint16_t*>(y), HS, WS, OH, OW, PH, PW, tasks);
+  return (int)hipGetLastError();
+}
+
 VGPU_API int vgpu_maxpool_nhwc(const void* x, void* y, int N, int H, int W, int C, int k, int stride,
                                int pad, hipStream_t s) {
   if (C % 8 || k < 1 || stride < 1 || pad < 0 || 2 * pad >= k + 1 || N < 1 || N > 65535) return -1;

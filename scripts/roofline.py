@@ -32,12 +32,15 @@ def plan(batch: int, size: int, layers=(3, 4, 6, 3)):
     def conv_out(h, k, s, p):
         return (h + 2 * p - k) // s + 1
 
-    # stem: 7x7/s2/p3 conv 3->64 as space-to-depth + 4x4 conv, then 3x3/s2 max-pool
+    # stem: 7x7/s2/p3 conv 3->64 as space-to-depth + 4x4 conv, with the 3x3/s2
+    # max-pool fused (conv_gemm.hip stem_pool_kernel): the stem activation stays
+    # on chip (model FLOPs counted; the kernel recomputes one stem row in three)
     h = conv_out(size, 7, 2, 3)
     m = batch * h * h
-    out.append(("stem conv", 2 * m * 7 * 7 * 3 * 64, E * (batch * size * size * 3 + m * 64 + 7 * 7 * 3 * 64)))
     h2 = conv_out(h, 3, 2, 1)
-    out.append(("maxpool", 0, E * (m * 64 + batch * h2 * h2 * 64)))
+    hs = h + 3
+    out.append(("stem conv + maxpool", 2 * m * 7 * 7 * 3 * 64,
+                E * (batch * size * size * 3 + batch * hs * hs * 16 * 2 + batch * h2 * h2 * 64 + 7 * 7 * 3 * 64)))
     h = h2
     cin = 64
     blocks = []

@@ -195,6 +195,20 @@ def test_stem_space_to_depth_conv(C, hw):
     torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("nhw", [(2, 346, 346), (3, 64, 61), (1, 9, 10), (2, 351, 339)])
+def test_stem_pool_matches_conv_then_maxpool(C, nhw):
+    """Fused stem conv + 3x3/s2 max pool: bit-identical to the two kernels
+    (same K order and MFMA sequence; the stem row is rounded to bf16 before the
+    pool exactly where the unfused conv stores it)."""
+    n, h, w = nhw
+    x = _t((n, 3, h, w), 41)
+    ws2d = C.stem_weight_s2d(_t((64, 3, 7, 7), 42, scale=(2.0 / 147) ** 0.5))
+    got = C.stem_pool(x, ws2d)
+    ref = C.maxpool3s2(C.stem_conv(x, ws2d))
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=CL)
+    torch.testing.assert_close(got, ref, atol=0, rtol=0)
+
+
 @pytest.mark.parametrize("case", [(2, 64, 19, 17, 1), (2, 128, 21, 19, 2), (3, 128, 9, 9, 1),
                                   (4, 64, 64, 64, 1)])
 def test_conv23_matches_unfused(C, case):

@@ -176,8 +176,7 @@ class FusedResNetV2Inference(nn.Module):
     def _forward_native(self, x: torch.Tensor) -> torch.Tensor:
         from vgpu.ops import conv as C
         x = x.contiguous(memory_format=torch.channels_last)
-        x = C.stem_conv(x, self.stem_w_s2d)
-        x = C.maxpool3s2(x)
+        x = C.stem_pool(x, self.stem_w_s2d)  # stem conv + max pool, one kernel
         x = self._blocks_native(x, 0, len(self.blocks))
         return self.fc(C.scale_shift_relu_mean(x, *self.out_ss))
 

@@ -61,6 +61,7 @@ def load_kernels() -> ctypes.CDLL:
     ci = ctypes.c_int
     lib.vgpu_conv2d_nhwc.argtypes = [vp, vp, vp, vp, vp, vp, vp] + [ci] * 9 + [vp]
     lib.vgpu_maxpool_nhwc.argtypes = [vp, vp] + [ci] * 7 + [vp]
+    lib.vgpu_stem_pool_nhwc.argtypes = [vp, vp, vp] + [ci] * 3 + [vp]
     lib.vgpu_conv_set_big.argtypes = [ci]
     lib.vgpu_lstm_recurrence.argtypes = [vp, vp, vp, vp, ci, ci, ci, vp]
     lib.vgpu_lstm_recurrence.restype = ci
@@ -83,7 +84,8 @@ def load_kernels() -> ctypes.CDLL:
     for f in ("vgpu_bn_act_fwd_train", "vgpu_bn_act_bwd","vgpu_census", "vgpu_busy", "vgpu_gather_pages", "vgpu_scatter_pages",
               "vgpu_fill_pattern", "vgpu_verify_pattern", "vgpu_kernels_abi_version",
               "vgpu_bias_act_nhwc", "vgpu_scale_shift_act_nhwc", "vgpu_add_scale_shift_act_nhwc",
-              "vgpu_conv2d_nhwc", "vgpu_maxpool_nhwc", "vgpu_scale_shift_relu_mean_nhwc"):
+              "vgpu_conv2d_nhwc", "vgpu_maxpool_nhwc", "vgpu_stem_pool_nhwc",
+              "vgpu_scale_shift_relu_mean_nhwc"):
         getattr(lib, f).restype = ctypes.c_int
     _kernels = lib
     return lib

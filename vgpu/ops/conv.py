@@ -196,6 +196,25 @@ def stem_conv(x: torch.Tensor, w_s2d: torch.Tensor, k: int = 7, pad: int = 3) ->
     return conv2d(stem_space_to_depth(x, k, pad), w_s2d)
 
 
+def stem_pool(x: torch.Tensor, w_s2d: torch.Tensor, k: int = 7, pad: int = 3) -> torch.Tensor:
+    """maxpool3s2(stem_conv(x, w_s2d)) in one kernel (the stem activation never
+    reaches HBM); bit-identical to the two-kernel path, which it falls back to
+    for shapes the fused kernel does not take (stem rows wider than 176)."""
+    X = stem_space_to_depth(x, k, pad)
+    n, _, hs, ws = X.shape
+    if w_s2d.shape[0] != 64:
+        return maxpool3s2(conv2d(X, w_s2d))
+    oh, ow = hs - 3, ws - 3
+    ph, pw = out_hw(oh, ow, 3, 2, 1)
+    out = torch.empty((n, 64, ph, pw), dtype=x.dtype, device=x.device, memory_format=_CL)
+    rc = load_kernels().vgpu_stem_pool_nhwc(_ptr(X), _ptr(w_s2d), _ptr(out), n, hs, ws, _stream())
+    if rc == -1:
+        return maxpool3s2(conv2d(X, w_s2d))
+    if rc != 0:
+        raise RuntimeError(f"vgpu_stem_pool_nhwc: error {rc}")
+    return out
+
+
 def maxpool(x: torch.Tensor, k: int, stride: int, pad: int = 0) -> torch.Tensor:
     """k×k max pool, NHWC bf16 (ResNet stem: 3/2/1; VGG: 2/2/0)."""
     _nhwc(x, "x")
