@@ -1985,7 +1985,13 @@ VGPU_API int vgpu_stem_pool_nhwc(const void* X, const void* w, void* y, int N, i
   const int PH = (OH + 2 - 3) / 2 + 1, PW = (OW + 2 - 3) / 2 + 1;
   if (PW * 8 > 2 * kSPThreads) return -1;
   const int tasks = N * PH;
-  int grid = conv_cus();
+  // One workgroup per CU of the device (LDS allows one), not conv_cus(): a
+  // time-shared pod runs on every CU while it runs, and a masked one just
+  // queues the extra workgroups (the task loop takes any grid).
+  int dev = 0, grid = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&grid, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || grid < 1)
+    grid = 256;
   if (grid > tasks) grid = tasks;
   hipLaunchKernelGGL(stem_pool_kernel, dim3(grid), dim3(kSPThreads), 0, s, static_cast<const uint16_t*>(X),
                      static_cast<const uint16_t*>(w), static_cast<uint16_t*>(y), HS, WS, OH, OW, PH, PW, tasks);
