@@ -852,10 +852,16 @@ __global__ void __launch_bounds__(kThreads, 2) conv_pro_kernel(const ConvArgs a)
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int PIPE = 2 * STAGE, EPI = (BM / 2) * (BN + 4) * 4;
   constexpr int BODY = PIPE > EPI ? PIPE : EPI;
-  // BN scale/shift of the input channels live in LDS (C ≤ 2048): reading them
-  // with ordinary global loads inside the loop would make hipcc wait vmcnt(0)
-  // behind the weight DMA.
-  __shared__ __attribute__((aligned(16))) char smem[BODY + 2048 * 2 * 4];
+  // BN scale/shift of the input channels.  64-row tiles: they travel with the
+  // K step's A rows, loaded into registers with them two steps ahead — an LDS
+  // copy of all C channels costs 16 KB and with it the third workgroup per CU.
+  // 128-row tiles (two workgroups per CU either way): one LDS copy, read per
+  // step (the register form measured 2-7 % slower there: 58 more VGPRs).
+  // Never ordinary global loads in the loop: beside the DMA they make hipcc
+  // drain vmcnt(0).
+  constexpr bool PREG = BM == 64;
+  constexpr int PR = PREG ? 4 : 0;  // 16-B parameter loads per K step: 8 scales, 8 shifts
+  __shared__ __attribute__((aligned(16))) char smem[BODY + (PREG ? 0 : 2048 * 2 * 4)];
   float* sPar = reinterpret_cast<float*>(smem + BODY);
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -884,11 +890,17 @@ __global__ void __launch_bounds__(kThreads, 2) conv_pro_kernel(const ConvArgs a)
     abase[i] = ((n * a.H + aih[i]) * a.W + aiw[i]) * a.C * 2;
   }
   const uint32_t boff = (uint32_t)(((n0 + r0) * a.K + lchunk * 8) * 2);
-  for (int c = t * 4; c < a.C; c += kThreads * 4) {
-    *reinterpret_cast<float4*>(sPar + c) = *reinterpret_cast<const float4*>(a.pscale + c);
-    *reinterpret_cast<float4*>(sPar + a.C + c) = *reinterpret_cast<const float4*>(a.pshift + c);
+  const __amdgpu_buffer_rsrc_t psr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.pscale), 0, (uint32_t)(a.C * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ptr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.pshift), 0, (uint32_t)(a.C * 4), 0x00020000);
+  if constexpr (!PREG) {
+    for (int c = t * 4; c < a.C; c += kThreads * 4) {
+      *reinterpret_cast<float4*>(sPar + c) = *reinterpret_cast<const float4*>(a.pscale + c);
+      *reinterpret_cast<float4*>(sPar + a.C + c) = *reinterpret_cast<const float4*>(a.pshift + c);
+    }
+    __syncthreads();
   }
-  __syncthreads();
 
   auto issue_b = [&](int kt, int st) {
     char* sB = smem + st * STAGE + A_BYTES;
@@ -898,7 +910,7 @@ __global__ void __launch_bounds__(kThreads, 2) conv_pro_kernel(const ConvArgs a)
           wr, (lds_void_t*)(sB + (32 * i + wave * 8) * 128), 16,
           boff + (uint32_t)((32 * i * a.K + kt * BK) * 2), 0, 0, 0);
   };
-  auto load_a = [&](int kt, u32x4 (&ra)[AR], bool (&rv)[AR]) {
+  auto load_a = [&](int kt, u32x4 (&ra)[AR], bool (&rv)[AR], u32x4 (&rp)[PR ? PR : 1]) {
     // 1x1: K = C, so the tap is 0 and the K step is the channel block.
     const int tap = KS == 1 ? 0 : kt / a.cblocks, cb = kt - tap * a.cblocks;
     const int kh = tap / KS, kw = tap - kh * KS;
@@ -911,21 +923,40 @@ __global__ void __launch_bounds__(kThreads, 2) conv_pro_kernel(const ConvArgs a)
       rv[i] = v;
       ra[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, v ? (uint32_t)(abase[i] + toff) : kOOB, 0, 0);
     }
+    if constexpr (PREG) {
+      const uint32_t po = (uint32_t)((cb * BK + slot * 8) * 4);
+      rp[0] = __builtin_amdgcn_raw_buffer_load_b128(psr, po, 0, 0);
+      rp[1] = __builtin_amdgcn_raw_buffer_load_b128(psr, po + 16, 0, 0);
+      rp[2] = __builtin_amdgcn_raw_buffer_load_b128(ptr, po, 0, 0);
+      rp[3] = __builtin_amdgcn_raw_buffer_load_b128(ptr, po + 16, 0, 0);
+    }
   };
-  auto store_a = [&](int kt, int st, u32x4 (&ra)[AR], const bool (&rv)[AR]) {
+  auto store_a = [&](int kt, int st, u32x4 (&ra)[AR], const bool (&rv)[AR], u32x4 (&rp)[PR ? PR : 1]) {
     char* sA = smem + st * STAGE;
-    const int c = (KS == 1 ? kt : kt % a.cblocks) * BK + slot * 8;
-    // Pin the A registers here: without it hipcc hoists this step's unpacking
-    // into the previous step, ahead of that step's barrier, and waits for the
-    // loads a step early.
+    // Pin the staged registers here: without it hipcc hoists this step's
+    // unpacking into the previous step, ahead of that step's barrier, and
+    // waits for the loads a step early.
 #pragma unroll
     for (int i = 0; i < AR; ++i) asm volatile("" : "+v"(ra[i]));
-    const float4 s0 = *reinterpret_cast<const float4*>(sPar + c);
-    const float4 s1 = *reinterpret_cast<const float4*>(sPar + c + 4);
-    const float4 h0 = *reinterpret_cast<const float4*>(sPar + a.C + c);
-    const float4 h1 = *reinterpret_cast<const float4*>(sPar + a.C + c + 4);
-    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    float sc[8], sh[8];
+    if constexpr (PREG) {
+#pragma unroll
+      for (int i = 0; i < PR; ++i) asm volatile("" : "+v"(rp[i]));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sc[j] = __uint_as_float(rp[0][j]);
+        sc[4 + j] = __uint_as_float(rp[1][j]);
+        sh[j] = __uint_as_float(rp[2][j]);
+        sh[4 + j] = __uint_as_float(rp[3][j]);
+      }
+    } else {
+      const int c = (KS == 1 ? kt : kt % a.cblocks) * BK + slot * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sc[j] = sPar[c + j];
+        sh[j] = sPar[a.C + c + j];
+      }
+    }
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       float e[8];
@@ -966,25 +997,25 @@ __global__ void __launch_bounds__(kThreads, 2) conv_pro_kernel(const ConvArgs a)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  u32x4 ra0[AR], ra1[AR];
+  u32x4 ra0[AR], ra1[AR], rp0[PR ? PR : 1], rp1[PR ? PR : 1];
   bool rv0[AR], rv1[AR];
   const int nk = a.ktiles;
   u32x4 res[2][EpiShape<BM, BN>::RROWS];
   // Per K step kt (stage st = kt & 1 holds A(kt), B(kt)):
   //   prologue + ds_write of A(kt+1) into stage st^1 (registers X, loaded two
-  //   steps ago) · DMA B(kt+1) into st^1 · load A(kt+3) into X · MFMA on st ·
-  //   vmcnt(AR): retires B(kt+1) and A(kt+2) (set Y, loaded one step ago),
-  //   leaves A(kt+3) in flight · barrier.
+  //   steps ago, with its channels' BN scale/shift) · DMA B(kt+1) into st^1 ·
+  //   load A(kt+3) into X · MFMA on st · vmcnt(AR + PR): retires B(kt+1) and
+  //   A(kt+2) (set Y, loaded one step ago), leaves A(kt+3) in flight · barrier.
   // Every ds_write of a step precedes its DMA: hipcc makes a ds_write wait for
   // all LDS-DMA in flight, which would serialise the pipeline.  The loads of
   // A(kt+3) are issued behind the DMA, so the step's own wait does not retire
   // them: they get two steps of lead.
-  load_a(0, ra0, rv0);
-  load_a(nk > 1 ? 1 : 0, ra1, rv1);
-  store_a(0, 0, ra0, rv0);
+  load_a(0, ra0, rv0, rp0);
+  load_a(nk > 1 ? 1 : 0, ra1, rv1, rp1);
+  store_a(0, 0, ra0, rv0, rp0);
   issue_b(0, 0);
-  load_a(nk > 2 ? 2 : nk - 1, ra0, rv0);
-  __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR));
+  load_a(nk > 2 ? 2 : nk - 1, ra0, rv0, rp0);
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR + PR));
   __builtin_amdgcn_s_waitcnt(kLgkm0);
   __builtin_amdgcn_s_barrier();
   // Unrolled by two so the register sets stay static: step kt stores set X
@@ -992,30 +1023,30 @@ __global__ void __launch_bounds__(kThreads, 2) conv_pro_kernel(const ConvArgs a)
   // Branch-free body: past the last K step the loads re-fetch the last tile into
   // the idle stage (never read) — a branch around a load would make hipcc wait
   // vmcnt(0) there and de-pipeline the loop.
-  auto step = [&](int kt, u32x4 (&rx)[AR], bool (&vx)[AR]) {
+  auto step = [&](int kt, u32x4 (&rx)[AR], bool (&vx)[AR], u32x4 (&px)[PR ? PR : 1]) {
     const int st = kt & 1;
     const int k1 = kt + 1 < nk ? kt + 1 : nk - 1, k3 = kt + 3 < nk ? kt + 3 : nk - 1;
     // sched_barriers keep hipcc's scheduler from reordering the phases (it
     // would hoist the A loads above the ds_writes — so the step's wait retires
     // them — and sink the MFMAs below the wait).
-    store_a(k1, st ^ 1, rx, vx);
+    store_a(k1, st ^ 1, rx, vx, px);
     __builtin_amdgcn_sched_barrier(0);
     issue_b(k1, st ^ 1);
     __builtin_amdgcn_sched_barrier(0);
-    load_a(k3, rx, vx);
+    load_a(k3, rx, vx, px);
     __builtin_amdgcn_sched_barrier(0);
     compute(st, acc);
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR));
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR + PR));
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     __builtin_amdgcn_s_barrier();
   };
   int kt = 0;
   for (; kt + 1 < nk; kt += 2) {
-    step(kt, ra1, rv1);
-    step(kt + 1, ra0, rv0);
+    step(kt, ra1, rv1, rp1);
+    step(kt + 1, ra0, rv0, rp0);
   }
-  if (kt < nk) step(kt, ra1, rv1);
+  if (kt < nk) step(kt, ra1, rv1, rp1);
   __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // the trailing dummy loads, before LDS reuse
   __syncthreads();
   if constexpr (RES) load_residual<BM, BN>(a, m0, n0, res);
