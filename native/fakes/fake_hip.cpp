@@ -549,6 +549,45 @@ hipError_t hipMallocManaged(void** p, size_t size, unsigned int) {
   return hipSuccess;
 }
 hipError_t hipMemAdvise(const void*, size_t, hipMemoryAdvise, int) { return hipSuccess; }
+// A host<->device copy touching a managed range: KFD migrates the touched pages
+// to system memory (native/probes/managed_access.hip); device-to-device copies
+// run on the GPU and move nothing.  No bytes are copied (fake addresses).
+static void host_copy_touch_locked(const void* p, size_t n) {
+  auto it = g_managed.upper_bound((uintptr_t)p);
+  if (it == g_managed.begin()) return;
+  --it;
+  Managed& m = it->second;
+  if ((uintptr_t)p >= it->first + m.size) return;
+  const uint64_t lo = ((uintptr_t)p - it->first) & ~((2ull << 20) - 1);
+  const uint64_t hi = std::min<uint64_t>(m.size, ((uintptr_t)p - it->first + n + (2ull << 20) - 1) & ~((2ull << 20) - 1));
+  const uint64_t moved = m.gpu_bytes > lo ? std::min<uint64_t>(m.gpu_bytes, hi) - lo : 0;
+  m.gpu_bytes -= moved;
+  g_devs[m.dev].used -= moved;
+}
+static hipError_t fake_copy(void* dst, const void* src, size_t n, hipMemcpyKind kind) {
+  if (kind == hipMemcpyDeviceToDevice) return hipSuccess;
+  std::lock_guard<std::mutex> g(g_mu);
+  host_copy_touch_locked(dst, n);
+  host_copy_touch_locked(src, n);
+  return hipSuccess;
+}
+hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind k) { return fake_copy(d, s, n, k); }
+hipError_t hipMemcpyWithStream(void* d, const void* s, size_t n, hipMemcpyKind k, hipStream_t) {
+  return fake_copy(d, s, n, k);
+}
+hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind k, hipStream_t) {
+  return fake_copy(d, s, n, k);
+}
+hipError_t hipMemcpyHtoD(hipDeviceptr_t d, const void* s, size_t n) {
+  return fake_copy(d, s, n, hipMemcpyHostToDevice);
+}
+hipError_t hipMemcpyDtoH(void* d, hipDeviceptr_t s, size_t n) { return fake_copy(d, s, n, hipMemcpyDeviceToHost); }
+hipError_t hipMemcpyHtoDAsync(hipDeviceptr_t d, const void* s, size_t n, hipStream_t) {
+  return fake_copy(d, s, n, hipMemcpyHostToDevice);
+}
+hipError_t hipMemcpyDtoHAsync(void* d, hipDeviceptr_t s, size_t n, hipStream_t) {
+  return fake_copy(d, s, n, hipMemcpyDeviceToHost);
+}
 hipError_t hipDeviceGetPCIBusId(char*, int, int) { return hipErrorNotSupported; }  // no sysfs behind a fake
 hipError_t hipMallocPitch(void** p, size_t* pitch, size_t w, size_t h) {
   *pitch = ((w + 511) / 512) * 512;

@@ -191,6 +191,25 @@ void pinned_forget(void* ptr) {
 
 }  // namespace
 
+namespace {
+inline hipError_t after_sync_copy(hipError_t rc, const void* dst, const void* src, size_t n, hipMemcpyKind kind) {
+  if (rc == hipSuccess && kind != hipMemcpyDeviceToDevice) vmem_after_copy(dst, src, n);
+  return rc;
+}
+
+inline hipError_t after_async_copy(hipError_t rc, const void* dst, const void* src, size_t n, hipMemcpyKind kind,
+                                   hipStream_t stream) {
+  if (rc != hipSuccess || kind == hipMemcpyDeviceToDevice || !vmem_copy_touches(dst, src, n)) return rc;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (REAL_HIP(hipStreamIsCapturing)(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    (void)REAL_HIP(hipGetLastError)();
+    return rc;
+  }
+  if (REAL_HIP(hipStreamSynchronize)(stream) == hipSuccess) vmem_after_copy(dst, src, n);
+  return rc;
+}
+}  // namespace
+
 extern "C" {
 
 __attribute__((visibility("default"))) hipError_t hipSetDevice(int deviceId) {
@@ -280,6 +299,48 @@ __attribute__((visibility("default"))) hipError_t hipMallocPitch(void** ptr, siz
     }
   }
   return rc;
+}
+
+// ---- host copies touching managed ranges -----------------------------------------
+// KFD moves the pages such a copy touches to system memory; once the copy has
+// completed, vmem_after_copy puts the resident part back in HBM (vmem.cpp).
+// Device-to-device copies run on the GPU and leave pages where they are.  An
+// async copy is waited for first, except inside a stream capture (nothing has
+// run yet; the replayed copy node is not seen).
+
+__attribute__((visibility("default"))) hipError_t hipMemcpy(void* dst, const void* src, size_t n,
+                                                            hipMemcpyKind kind) {
+  return after_sync_copy(REAL_HIP(hipMemcpy)(dst, src, n, kind), dst, src, n, kind);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpyWithStream(void* dst, const void* src, size_t n,
+                                                                      hipMemcpyKind kind, hipStream_t stream) {
+  return after_sync_copy(REAL_HIP(hipMemcpyWithStream)(dst, src, n, kind, stream), dst, src, n, kind);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpyHtoD(hipDeviceptr_t dst, const void* src, size_t n) {
+  return after_sync_copy(REAL_HIP(hipMemcpyHtoD)(dst, src, n), dst, src, n, hipMemcpyHostToDevice);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpyDtoH(void* dst, hipDeviceptr_t src, size_t n) {
+  return after_sync_copy(REAL_HIP(hipMemcpyDtoH)(dst, src, n), dst, src, n, hipMemcpyDeviceToHost);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpyAsync(void* dst, const void* src, size_t n,
+                                                                 hipMemcpyKind kind, hipStream_t stream) {
+  return after_async_copy(REAL_HIP(hipMemcpyAsync)(dst, src, n, kind, stream), dst, src, n, kind, stream);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpyHtoDAsync(hipDeviceptr_t dst, const void* src, size_t n,
+                                                                     hipStream_t stream) {
+  return after_async_copy(REAL_HIP(hipMemcpyHtoDAsync)(dst, src, n, stream), dst, src, n, hipMemcpyHostToDevice,
+                          stream);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpyDtoHAsync(void* dst, hipDeviceptr_t src, size_t n,
+                                                                     hipStream_t stream) {
+  return after_async_copy(REAL_HIP(hipMemcpyDtoHAsync)(dst, src, n, stream), dst, src, n, hipMemcpyDeviceToHost,
+                          stream);
 }
 
 // Spilled allocations: a managed range (vmem.cpp) is freed by hipFree, a

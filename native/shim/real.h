@@ -55,6 +55,13 @@ using hipGetDevicePropertiesR0600 = hipError_t (*)(hipDeviceProp_tR0600*, int);
 using hipDeviceGetAttribute = hipError_t (*)(int*, hipDeviceAttribute_t, int);
 using hipGetLastError = hipError_t (*)();
 using hipStreamSynchronize = hipError_t (*)(hipStream_t);
+using hipMemcpy = hipError_t (*)(void*, const void*, size_t, hipMemcpyKind);
+using hipMemcpyWithStream = hipError_t (*)(void*, const void*, size_t, hipMemcpyKind, hipStream_t);
+using hipMemcpyAsync = hipError_t (*)(void*, const void*, size_t, hipMemcpyKind, hipStream_t);
+using hipMemcpyHtoD = hipError_t (*)(hipDeviceptr_t, const void*, size_t);
+using hipMemcpyDtoH = hipError_t (*)(void*, hipDeviceptr_t, size_t);
+using hipMemcpyHtoDAsync = hipError_t (*)(hipDeviceptr_t, const void*, size_t, hipStream_t);
+using hipMemcpyDtoHAsync = hipError_t (*)(void*, hipDeviceptr_t, size_t, hipStream_t);
 using hipLaunchKernel = hipError_t (*)(const void*, dim3, dim3, void**, size_t, hipStream_t);
 using hipExtLaunchKernel = hipError_t (*)(const void*, dim3, dim3, void**, size_t, hipStream_t,
                                           hipEvent_t, hipEvent_t, int);

@@ -539,6 +539,61 @@ hipError_t vmem_alloc_managed(void** ptr, size_t size, int dev) {
   return hipSuccess;
 }
 
+// ---- host copies ---------------------------------------------------------------------
+// hipMemcpy* between host memory and a managed range is carried out on the
+// host side: KFD migrates every page the copy touches to system memory first,
+// whatever the copy kind, pinned or pageable, sync or async (measured:
+// native/probes/managed_access.hip -- a promoted 512 MiB range reads at
+// 57 GB/s after one hipMemcpy into it, 6.1 TB/s before).  Those pages never
+// come back by themselves (XNACK off: the GPU reads them over the host link)
+// and the pager's books still call the range resident, so it would never
+// promote them either -- a VGG-16 pod whose weights were uploaded with
+// model.to("cuda") ran its FC GEMMs 55x slower.  After such a copy, the
+// resident part of each range it touched goes back to HBM, whole 2 MiB
+// granules at a time (KFD's migration granule).
+namespace {
+struct Span {
+  uintptr_t lo = 0;
+  uint64_t n = 0;
+  int dev = -1;
+};
+
+Span resident_span_locked(const void* p, size_t n) {
+  VRange* r = find_locked((uintptr_t)p);
+  if (!r || !r->gpu_bytes || !n) return {};
+  constexpr uintptr_t g = 2ull << 20;
+  const uintptr_t lo = std::max<uintptr_t>(r->base, (uintptr_t)p & ~(g - 1));
+  const uintptr_t hi = std::min<uintptr_t>(r->base + r->gpu_bytes, ((uintptr_t)p + n + g - 1) & ~(g - 1));
+  return hi > lo ? Span{lo, hi - lo, r->dev} : Span{};
+}
+}  // namespace
+
+bool vmem_copy_touches(const void* dst, const void* src, size_t n) {
+  if (g_count.load(std::memory_order_relaxed) == 0) return false;
+  std::shared_lock<std::shared_mutex> g(g_tab_mu);
+  return resident_span_locked(dst, n).n || resident_span_locked(src, n).n;
+}
+
+void vmem_after_copy(const void* dst, const void* src, size_t n) {
+  if (g_count.load(std::memory_order_relaxed) == 0) return;
+  std::lock_guard<std::mutex> m(g_move_mu);  // no demotion in between
+  Span sp[2];
+  {
+    std::shared_lock<std::shared_mutex> g(g_tab_mu);
+    sp[0] = resident_span_locked(dst, n);
+    sp[1] = resident_span_locked(src, n);
+  }
+  for (const Span& s : sp) {
+    if (!s.n) continue;
+    auto t0 = std::chrono::steady_clock::now();
+    if (!prefetch(s.lo, s.n, s.dev, true)) continue;
+    uint64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    trace_emit(VGPU_EV_MIGRATE, s.dev, s.n, (ns << 1) | 1);
+    VLOG_DEBUG("vmem: %llu bytes at %p back to HBM after a host copy (%.3f s)", (unsigned long long)s.n,
+               (void*)s.lo, ns / 1e9);
+  }
+}
+
 bool vmem_owns(void* p) {
   if (g_count.load(std::memory_order_relaxed) == 0) return false;
   std::shared_lock<std::shared_mutex> g(g_tab_mu);

@@ -388,6 +388,29 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (sc == "vmem_copy") {
+    // A managed-by-default range (physical budget) written by host copies:
+    // KFD moves the touched pages to host memory (fake HIP models it); the
+    // shim puts them back.  Device-to-device copies move nothing.
+    const size_t G = 1ull << 30;
+    void** ab = new void*[2]();
+    void*& a = ab[0];
+    int ra = hipMalloc(&a, 2 * G);
+    auto gb = [&](void* p) { return (unsigned long long)fake_hip_managed_gpu_bytes(p); };
+    char host[64];
+    printf("alloc=%d\ngpu_at_alloc=%llu\n", ra, gb(a));
+    int r1 = hipMemcpy((char*)a + 5 * (1 << 20), host, 64ull << 20, hipMemcpyHostToDevice);
+    printf("h2d=%d\ngpu_after_h2d=%llu\n", r1, gb(a));
+    int r2 = hipMemcpyWithStream(host, a, 4096, hipMemcpyDeviceToHost, nullptr);
+    printf("d2h=%d\ngpu_after_d2h=%llu\n", r2, gb(a));
+    int r3 = hipMemcpyAsync((char*)a + G, host, 3ull << 20, hipMemcpyDefault, nullptr);
+    printf("async=%d\ngpu_after_async=%llu\n", r3, gb(a));
+    int r4 = hipMemcpyHtoD((hipDeviceptr_t)((char*)a + 100), host, 10);
+    printf("htod=%d\ngpu_after_htod=%llu\n", r4, gb(a));
+    hipFree(a);
+    return 0;
+  }
+
   if (sc == "vmem_budget" || sc == "vmem_thrash") {
     // Virtual device memory with a physical budget (VGPU_DEVICE_MEMORY_PHYSICAL_0):
     // allocations are managed ranges from the start.  vmem_budget: model B is

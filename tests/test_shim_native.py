@@ -185,6 +185,17 @@ def test_vmem_budget_graph_replay_and_suspend(native_build):
     assert (o["final_total"], o["final_host"], o["final_ranges"], o["final_physical"]) == ("0", "0", "0", "0")
 
 
+def test_vmem_host_copy_pages_come_back(native_build):
+    """A host copy into or out of a resident managed range makes KFD move the
+    touched pages to host memory (measured on MI355X: 57 GB/s reads afterwards,
+    native/probes/managed_access.hip; the fake HIP models it).  The shim puts
+    the resident part back after sync, stream-sync and async copies."""
+    o = run("vmem_copy", env=BUDGET_ENV)
+    assert o["alloc"] == "0" and int(o["gpu_at_alloc"]) == 2 * GiB
+    for k in ("h2d", "d2h", "async", "htod"):
+        assert o[k] == "0" and int(o[f"gpu_after_{k}"]) == 2 * GiB, (k, o)
+
+
 def test_vmem_hot_set_beyond_budget_does_not_cycle(native_build):
     """Two hot 6 GiB ranges against an 8 GiB budget: the resident part stays
     put (no LRU exchange on a cyclic sweep), the rest is read in place."""
