@@ -552,6 +552,7 @@ hipError_t hipMemAdvise(const void*, size_t, hipMemoryAdvise, int) { return hipS
 // A host<->device copy touching a managed range: KFD migrates the touched pages
 // to system memory (native/probes/managed_access.hip); device-to-device copies
 // run on the GPU and move nothing.  No bytes are copied (fake addresses).
+static uint64_t g_host_touch_bytes = 0;  // bytes of managed ranges moved to host by copies
 static void host_copy_touch_locked(const void* p, size_t n) {
   auto it = g_managed.upper_bound((uintptr_t)p);
   if (it == g_managed.begin()) return;
@@ -563,6 +564,7 @@ static void host_copy_touch_locked(const void* p, size_t n) {
   const uint64_t moved = m.gpu_bytes > lo ? std::min<uint64_t>(m.gpu_bytes, hi) - lo : 0;
   m.gpu_bytes -= moved;
   g_devs[m.dev].used -= moved;
+  g_host_touch_bytes += moved;
 }
 static hipError_t fake_copy(void* dst, const void* src, size_t n, hipMemcpyKind kind) {
   if (kind == hipMemcpyDeviceToDevice) return hipSuccess;
@@ -572,6 +574,21 @@ static hipError_t fake_copy(void* dst, const void* src, size_t n, hipMemcpyKind 
   return hipSuccess;
 }
 hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind k) { return fake_copy(d, s, n, k); }
+hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned int) { return hipSuccess; }
+// Device memory and managed ranges are "device"; anything else is unregistered host memory.
+hipError_t hipPointerGetAttributes(hipPointerAttribute_t* a, const void* p) {
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_managed.upper_bound((uintptr_t)p);
+  if (it != g_managed.begin() && (uintptr_t)p < std::prev(it)->first + std::prev(it)->second.size) {
+    a->type = hipMemoryTypeManaged;
+    return hipSuccess;
+  }
+  return hipErrorInvalidValue;
+}
+uint64_t fake_hip_host_touch_bytes() {
+  std::lock_guard<std::mutex> g(g_mu);
+  return g_host_touch_bytes;
+}
 hipError_t hipMemcpyWithStream(void* d, const void* s, size_t n, hipMemcpyKind k, hipStream_t) {
   return fake_copy(d, s, n, k);
 }

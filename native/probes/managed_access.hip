@@ -187,6 +187,20 @@ int main() {
     CK(hipMemcpyAsync(c, ph, kBytes, hipMemcpyHostToDevice, 0));
     CK(hipDeviceSynchronize());
     run("after_pinned_h2d", c, out);
+    // Device-to-device copies from plain HBM into the promoted range: the
+    // staging route for host uploads, if they leave the pages in HBM.
+    prefetch_gpu(c);
+    CK(hipMemcpy(c, d, kBytes, hipMemcpyDeviceToDevice));
+    run("after_d2d", c, out);
+    CK(hipMemcpyAsync(c, d, kBytes, hipMemcpyDeviceToDevice, 0));
+    CK(hipDeviceSynchronize());
+    run("after_d2d_async", c, out);
+    CK(hipMemcpyAsync(c, d, kBytes, hipMemcpyDefault, 0));
+    CK(hipDeviceSynchronize());
+    run("after_d2d_default", c, out);
+    CK(hipMemcpyAsync(d, c, kBytes, hipMemcpyDeviceToDevice, 0));
+    CK(hipDeviceSynchronize());
+    run("after_d2d_from", c, out);
   }
   printf("done\n");
   return 0;

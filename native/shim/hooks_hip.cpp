@@ -191,7 +191,82 @@ void pinned_forget(void* ptr) {
 
 }  // namespace
 
+// ---- host copies touching managed ranges -----------------------------------------
+// KFD moves every page of a managed range that a host<->device copy touches
+// to system memory (native/probes/managed_access.hip: 57 GB/s reads after
+// one hipMemcpy, 6.1 TB/s before).  Device-to-device copies leave the pages in
+// HBM, so such a copy is staged: host <-> a plain HBM buffer by DMA, buffer <->
+// range on the GPU, stream-ordered in 64 MiB chunks (one staging buffer per
+// device; the next user's stream waits on the last one's event, the host
+// never does for an async copy).  Where staging cannot run (an open capture,
+// another current device) the copy runs as asked and vmem_after_copy puts the
+// resident part back in HBM once it has completed.
 namespace {
+constexpr size_t kStageBytes = 64ull << 20;
+struct Stage {
+  std::mutex mu;
+  void* buf = nullptr;
+  hipEvent_t done = nullptr;
+};
+Stage g_stage[VGPU_MAX_DEVICES];
+
+bool host_side(const void* p) {
+  hipPointerAttribute_t a{};
+  if (REAL_HIP(hipPointerGetAttributes)(&a, p) != hipSuccess) {
+    (void)REAL_HIP(hipGetLastError)();
+    return true;  // unregistered pageable memory
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+bool capturing(hipStream_t stream) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (REAL_HIP(hipStreamIsCapturing)(stream, &cs) != hipSuccess) {
+    (void)REAL_HIP(hipGetLastError)();
+    return true;
+  }
+  return cs != hipStreamCaptureStatusNone;
+}
+
+// true when the copy was staged (*rc is its result).
+bool staged_copy(void* dst, const void* src, size_t n, hipMemcpyKind kind, hipStream_t stream, hipError_t* rc) {
+  if (kind == hipMemcpyDeviceToDevice || n == 0) return false;
+  const int ddev = vmem_resident_dev(dst, n), sdev = vmem_resident_dev(src, n);
+  if ((ddev < 0) == (sdev < 0)) return false;  // neither side, or range to range (on the GPU)
+  const bool up = ddev >= 0;                    // host -> range
+  const int dev = up ? ddev : sdev;
+  if (kind == hipMemcpyDefault && !host_side(up ? src : dst)) return false;
+  if (dev != cur_dev() || dev >= VGPU_MAX_DEVICES || capturing(stream)) return false;
+  Stage& g = g_stage[dev];
+  std::lock_guard<std::mutex> l(g.mu);
+  if (!g.buf) {
+    if (REAL_HIP(hipMalloc)(&g.buf, kStageBytes) != hipSuccess ||
+        REAL_HIP(hipEventCreateWithFlags)(&g.done, hipEventDisableTiming) != hipSuccess) {
+      (void)REAL_HIP(hipGetLastError)();
+      if (g.buf) (void)REAL_HIP(hipFree)(g.buf);
+      g.buf = nullptr;
+      return false;
+    }
+  } else if (REAL_HIP(hipStreamWaitEvent)(stream, g.done, 0) != hipSuccess) {
+    (void)REAL_HIP(hipGetLastError)();
+    return false;
+  }
+  hipError_t r = hipSuccess;
+  for (size_t off = 0; off < n && r == hipSuccess; off += kStageBytes) {
+    const size_t c = std::min(kStageBytes, n - off);
+    if (up) {
+      r = REAL_HIP(hipMemcpyAsync)(g.buf, (const char*)src + off, c, hipMemcpyHostToDevice, stream);
+      if (r == hipSuccess) r = REAL_HIP(hipMemcpyAsync)((char*)dst + off, g.buf, c, hipMemcpyDeviceToDevice, stream);
+    } else {
+      r = REAL_HIP(hipMemcpyAsync)(g.buf, (const char*)src + off, c, hipMemcpyDeviceToDevice, stream);
+      if (r == hipSuccess) r = REAL_HIP(hipMemcpyAsync)((char*)dst + off, g.buf, c, hipMemcpyDeviceToHost, stream);
+    }
+  }
+  (void)REAL_HIP(hipEventRecord)(g.done, stream);
+  *rc = r;
+  return true;
+}
+
 inline hipError_t after_sync_copy(hipError_t rc, const void* dst, const void* src, size_t n, hipMemcpyKind kind) {
   if (rc == hipSuccess && kind != hipMemcpyDeviceToDevice) vmem_after_copy(dst, src, n);
   return rc;
@@ -200,13 +275,27 @@ inline hipError_t after_sync_copy(hipError_t rc, const void* dst, const void* sr
 inline hipError_t after_async_copy(hipError_t rc, const void* dst, const void* src, size_t n, hipMemcpyKind kind,
                                    hipStream_t stream) {
   if (rc != hipSuccess || kind == hipMemcpyDeviceToDevice || !vmem_copy_touches(dst, src, n)) return rc;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (REAL_HIP(hipStreamIsCapturing)(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
-    (void)REAL_HIP(hipGetLastError)();
-    return rc;
-  }
+  if (capturing(stream)) return rc;  // nothing has run yet; the replayed copy node is not seen
   if (REAL_HIP(hipStreamSynchronize)(stream) == hipSuccess) vmem_after_copy(dst, src, n);
   return rc;
+}
+
+// The hooks: staged when one side is a resident managed range, else copied as
+// asked (and repaired afterwards if it touched one anyway).
+using CopyFn = hipError_t (*)(void*, const void*, size_t, hipMemcpyKind, hipStream_t);
+hipError_t copy_sync(void* dst, const void* src, size_t n, hipMemcpyKind kind, hipStream_t stream, CopyFn real) {
+  hipError_t rc;
+  if (staged_copy(dst, src, n, kind, stream, &rc)) {
+    if (rc == hipSuccess) rc = REAL_HIP(hipStreamSynchronize)(stream);
+    return rc;
+  }
+  return after_sync_copy(real(dst, src, n, kind, stream), dst, src, n, kind);
+}
+
+hipError_t copy_async(void* dst, const void* src, size_t n, hipMemcpyKind kind, hipStream_t stream) {
+  hipError_t rc;
+  if (staged_copy(dst, src, n, kind, stream, &rc)) return rc;
+  return after_async_copy(REAL_HIP(hipMemcpyAsync)(dst, src, n, kind, stream), dst, src, n, kind, stream);
 }
 }  // namespace
 
@@ -301,46 +390,48 @@ __attribute__((visibility("default"))) hipError_t hipMallocPitch(void** ptr, siz
   return rc;
 }
 
-// ---- host copies touching managed ranges -----------------------------------------
-// KFD moves the pages such a copy touches to system memory; once the copy has
-// completed, vmem_after_copy puts the resident part back in HBM (vmem.cpp).
-// Device-to-device copies run on the GPU and leave pages where they are.  An
-// async copy is waited for first, except inside a stream capture (nothing has
-// run yet; the replayed copy node is not seen).
-
+// ---- host copies (staged or repaired; see copy_sync / copy_async above) ----------
 __attribute__((visibility("default"))) hipError_t hipMemcpy(void* dst, const void* src, size_t n,
                                                             hipMemcpyKind kind) {
-  return after_sync_copy(REAL_HIP(hipMemcpy)(dst, src, n, kind), dst, src, n, kind);
+  return copy_sync(dst, src, n, kind, nullptr, [](void* d, const void* s, size_t c, hipMemcpyKind k, hipStream_t) {
+    return REAL_HIP(hipMemcpy)(d, s, c, k);
+  });
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemcpyWithStream(void* dst, const void* src, size_t n,
                                                                       hipMemcpyKind kind, hipStream_t stream) {
-  return after_sync_copy(REAL_HIP(hipMemcpyWithStream)(dst, src, n, kind, stream), dst, src, n, kind);
+  return copy_sync(dst, src, n, kind, stream, [](void* d, const void* s, size_t c, hipMemcpyKind k, hipStream_t t) {
+    return REAL_HIP(hipMemcpyWithStream)(d, s, c, k, t);
+  });
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemcpyHtoD(hipDeviceptr_t dst, const void* src, size_t n) {
-  return after_sync_copy(REAL_HIP(hipMemcpyHtoD)(dst, src, n), dst, src, n, hipMemcpyHostToDevice);
+  return copy_sync(dst, src, n, hipMemcpyHostToDevice, nullptr,
+                   [](void* d, const void* s, size_t c, hipMemcpyKind, hipStream_t) {
+                     return REAL_HIP(hipMemcpyHtoD)(d, s, c);
+                   });
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemcpyDtoH(void* dst, hipDeviceptr_t src, size_t n) {
-  return after_sync_copy(REAL_HIP(hipMemcpyDtoH)(dst, src, n), dst, src, n, hipMemcpyDeviceToHost);
+  return copy_sync(dst, src, n, hipMemcpyDeviceToHost, nullptr,
+                   [](void* d, const void* s, size_t c, hipMemcpyKind, hipStream_t) {
+                     return REAL_HIP(hipMemcpyDtoH)(d, (hipDeviceptr_t)s, c);
+                   });
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemcpyAsync(void* dst, const void* src, size_t n,
                                                                  hipMemcpyKind kind, hipStream_t stream) {
-  return after_async_copy(REAL_HIP(hipMemcpyAsync)(dst, src, n, kind, stream), dst, src, n, kind, stream);
+  return copy_async(dst, src, n, kind, stream);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemcpyHtoDAsync(hipDeviceptr_t dst, const void* src, size_t n,
                                                                      hipStream_t stream) {
-  return after_async_copy(REAL_HIP(hipMemcpyHtoDAsync)(dst, src, n, stream), dst, src, n, hipMemcpyHostToDevice,
-                          stream);
+  return copy_async(dst, src, n, hipMemcpyHostToDevice, stream);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemcpyDtoHAsync(void* dst, hipDeviceptr_t src, size_t n,
                                                                      hipStream_t stream) {
-  return after_async_copy(REAL_HIP(hipMemcpyDtoHAsync)(dst, src, n, stream), dst, src, n, hipMemcpyDeviceToHost,
-                          stream);
+  return copy_async(dst, src, n, hipMemcpyDeviceToHost, stream);
 }
 
 // Spilled allocations: a managed range (vmem.cpp) is freed by hipFree, a

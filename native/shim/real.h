@@ -56,6 +56,8 @@ using hipDeviceGetAttribute = hipError_t (*)(int*, hipDeviceAttribute_t, int);
 using hipGetLastError = hipError_t (*)();
 using hipStreamSynchronize = hipError_t (*)(hipStream_t);
 using hipMemcpy = hipError_t (*)(void*, const void*, size_t, hipMemcpyKind);
+using hipStreamWaitEvent = hipError_t (*)(hipStream_t, hipEvent_t, unsigned int);
+using hipPointerGetAttributes = hipError_t (*)(hipPointerAttribute_t*, const void*);
 using hipMemcpyWithStream = hipError_t (*)(void*, const void*, size_t, hipMemcpyKind, hipStream_t);
 using hipMemcpyAsync = hipError_t (*)(void*, const void*, size_t, hipMemcpyKind, hipStream_t);
 using hipMemcpyHtoD = hipError_t (*)(hipDeviceptr_t, const void*, size_t);

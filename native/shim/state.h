@@ -163,6 +163,7 @@ uint64_t vmem_graph_ranges(hipGraphExec_t exec);
 // A host<->device copy that touched a managed range: KFD moved the pages it
 // touched to host memory behind the pager's back; put the resident part back.
 bool vmem_copy_touches(const void* dst, const void* src, size_t n);
+int vmem_resident_dev(const void* p, size_t n);  // device of a resident managed span in [p, p+n), else -1
 void vmem_after_copy(const void* dst, const void* src, size_t n);
 void vmem_stats(uint64_t* in_bytes, uint64_t* out_bytes, uint64_t* moves, uint64_t* gpu_bytes, uint64_t* ranges);
 void vmem_stop();

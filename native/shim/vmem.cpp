@@ -550,7 +550,9 @@ hipError_t vmem_alloc_managed(void** ptr, size_t size, int dev) {
 // promote them either -- a VGG-16 pod whose weights were uploaded with
 // model.to("cuda") ran its FC GEMMs 55x slower.  After such a copy, the
 // resident part of each range it touched goes back to HBM, whole 2 MiB
-// granules at a time (KFD's migration granule).
+// granules at a time (KFD's migration granule).  hooks_hip.cpp avoids most of
+// this by staging such copies through plain HBM (device-to-device copies leave
+// the pages where they are); this is the fallback (open captures, no staging).
 namespace {
 struct Span {
   uintptr_t lo = 0;
@@ -567,6 +569,13 @@ Span resident_span_locked(const void* p, size_t n) {
   return hi > lo ? Span{lo, hi - lo, r->dev} : Span{};
 }
 }  // namespace
+
+int vmem_resident_dev(const void* p, size_t n) {
+  if (g_count.load(std::memory_order_relaxed) == 0) return -1;
+  std::shared_lock<std::shared_mutex> g(g_tab_mu);
+  const Span s = resident_span_locked(p, n);
+  return s.n ? s.dev : -1;
+}
 
 bool vmem_copy_touches(const void* dst, const void* src, size_t n) {
   if (g_count.load(std::memory_order_relaxed) == 0) return false;

@@ -33,6 +33,7 @@ extern "C" uint64_t fake_hip_physical_used(int dev);
 extern "C" uint64_t fake_hsa_pool_used(int dev);
 extern "C" int fake_hsa_tools_loaded();
 extern "C" uint64_t fake_hip_managed_gpu_bytes(const void* p);
+extern "C" uint64_t fake_hip_host_touch_bytes();
 extern "C" hipGraph_t fake_hip_graph_create(const unsigned* grids, int n, unsigned child_grid);
 
 static hsa_status_t gpu_agent_cb(hsa_agent_t a, void* data) {
@@ -407,6 +408,8 @@ int main(int argc, char** argv) {
     printf("async=%d\ngpu_after_async=%llu\n", r3, gb(a));
     int r4 = hipMemcpyHtoD((hipDeviceptr_t)((char*)a + 100), host, 10);
     printf("htod=%d\ngpu_after_htod=%llu\n", r4, gb(a));
+    // staged copies never let KFD move a page; a range to range copy runs on the GPU
+    printf("host_touched=%llu\n", (unsigned long long)fake_hip_host_touch_bytes());
     hipFree(a);
     return 0;
   }

@@ -238,6 +238,19 @@ def test_vmem_spill_promoted_transparently(gpu_build):
     assert res["final"]["ranges"] == 0
 
 
+def test_vmem_host_copies_keep_managed_ranges_in_hbm(gpu_build):
+    """Round 3: under a physical budget every large allocation is a managed
+    range, and a host copy into or out of one made KFD move its pages to
+    system memory (VGG-16 under vgpu-vmem ran its FC layers at host-link
+    speed).  The shim stages such copies through plain HBM: after a D2H, a
+    sync H2D and an async pinned H2D the ranges still read at HBM speed."""
+    res = probe(["vmemcopy", 512], {"VGPU_DEVICE_MEMORY_LIMIT_0": "230000m", "VGPU_OVERSUBSCRIBE": "true",
+                                     "VGPU_DEVICE_MEMORY_PHYSICAL_0": "127000m"}, timeout=300)
+    assert res["ranges"] >= 1 and res["errors"] == 0, res
+    for k in ("fresh_GBps", "after_d2h_GBps", "after_h2d_GBps", "after_async_h2d_GBps"):
+        assert res[k] > 1000, (k, res)
+
+
 def test_rocr_cu_mask_env_matches_shim_masks(gpu_build):
     """Allocate also sets HSA_CU_MASK so ROCr masks the
     queues the shim never sees (its internal blit queue).  Same logical bits:

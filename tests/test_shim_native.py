@@ -188,12 +188,15 @@ def test_vmem_budget_graph_replay_and_suspend(native_build):
 def test_vmem_host_copy_pages_come_back(native_build):
     """A host copy into or out of a resident managed range makes KFD move the
     touched pages to host memory (measured on MI355X: 57 GB/s reads afterwards,
-    native/probes/managed_access.hip; the fake HIP models it).  The shim puts
-    the resident part back after sync, stream-sync and async copies."""
+    native/probes/managed_access.hip; the fake HIP models it).  The shim stages
+    such copies through plain HBM (device-to-device copies move no page), so
+    sync, stream-sync and async copies leave the range resident and KFD never
+    moves a page."""
     o = run("vmem_copy", env=BUDGET_ENV)
     assert o["alloc"] == "0" and int(o["gpu_at_alloc"]) == 2 * GiB
     for k in ("h2d", "d2h", "async", "htod"):
         assert o[k] == "0" and int(o[f"gpu_after_{k}"]) == 2 * GiB, (k, o)
+    assert o["host_touched"] == "0"
 
 
 def test_vmem_hot_set_beyond_budget_does_not_cycle(native_build):

@@ -328,6 +328,61 @@ def vmem(block_gib: int = 4, wait_s: int = 20) -> dict:
     return res
 
 
+def vmemcopy(mib: int = 512) -> dict:
+    """Host copies into and out of managed ranges (physical budget set, so a
+    large allocation is a managed range from the start).  Without the shim's
+    staging KFD moves every page such a copy touches to system memory and the
+    GPU reads it over the host link afterwards (native/probes/managed_access.hip).
+    Reads each range after: D2H from it, sync H2D into it, async H2D from
+    pinned memory into it."""
+    import ctypes
+
+    import torch
+    from vgpu.ops import kernels as K
+    lib = ctypes.CDLL(None)
+
+    def ranges():
+        v = (ctypes.c_uint64 * 5)()
+        lib.vgpu_self_vmem_stats(v)
+        return int(v[4])
+
+    def read_gbps(t, seed, reps=5):
+        K.verify_pattern(t, seed)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        errs = 0
+        for _ in range(reps):
+            errs += K.verify_pattern(t, seed)
+        torch.cuda.synchronize()
+        return round(reps * t.numel() / (time.time() - t0) / 1e9, 1), errs
+
+    n = mib << 20
+    src = torch.empty(n, dtype=torch.uint8, device="cuda")
+    K.fill_pattern(src, 7)
+    torch.cuda.synchronize()
+    res = {"ranges": ranges()}
+    res["fresh_GBps"], e0 = read_gbps(src, 7)
+    t0 = time.time()
+    h = src.cpu()  # D2H out of a managed range
+    res["d2h_ms"] = round((time.time() - t0) * 1e3, 1)
+    res["after_d2h_GBps"], e1 = read_gbps(src, 7)
+    dst = torch.empty(n, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    t0 = time.time()
+    dst.copy_(h)  # sync H2D into a managed range
+    torch.cuda.synchronize()
+    res["h2d_ms"] = round((time.time() - t0) * 1e3, 1)
+    res["after_h2d_GBps"], e2 = read_gbps(dst, 7)
+    hp = h.pin_memory()
+    dst2 = torch.empty(n, dtype=torch.uint8, device="cuda")
+    dst2.copy_(hp, non_blocking=True)  # async H2D from pinned memory
+    torch.cuda.synchronize()
+    res["after_async_h2d_GBps"], e3 = read_gbps(dst2, 7)
+    res["errors"] = e0 + e1 + e2 + e3
+    res["ranges_end"] = ranges()
+    return res
+
+
 def rcclloop(iters: int = 200, mib: int = 64, port: int = 0) -> dict:
     """A world-size-1 RCCL process group all-reducing `mib` MiB `iters` times
     (the collective path of a DDP pod), timed; the sum is checked."""
@@ -493,7 +548,7 @@ def main(argv=None) -> int:
     cmd = argv.pop(0) if argv else "census"
     nums = [int(a) for a in argv]
     out = {"census": census, "busy": busy, "cap": cap, "smi": smi, "graph": graph, "arrays": arrays,
-           "progress": progress, "vmem": vmem, "capheld": capheld, "asynccap": asynccap, "rcclloop": rcclloop}[cmd](*nums)
+           "progress": progress, "vmem": vmem, "vmemcopy": vmemcopy, "capheld": capheld, "asynccap": asynccap, "rcclloop": rcclloop}[cmd](*nums)
     out["shim"] = shim_stats()
     print("PROBE " + json.dumps(out), flush=True)
     return 0

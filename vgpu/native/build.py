@@ -207,7 +207,7 @@ def build_fakes(force: bool = False) -> dict[str, Path]:
         vs = FAKES_OUT / "hip.map"
         vs.write_text(_version_script(
             hip_src, "hip_4.2", versions,
-            "fake_hip_launches; fake_hip_launch_blocks; fake_hip_physical_used; fake_hip_graph_create; fake_hip_exec_ns; fake_hip_svm_move; fake_hip_managed_gpu_bytes;"))
+            "fake_hip_launches; fake_hip_launch_blocks; fake_hip_physical_used; fake_hip_graph_create; fake_hip_exec_ns; fake_hip_svm_move; fake_hip_managed_gpu_bytes; fake_hip_host_touch_bytes;"))
         _run([CXX, *COMMON, hip_src, "-o", hip, "-shared", "-Wl,-soname,libamdhip64.so.7",
               f"-Wl,--version-script={vs}", f"-L{FAKES_OUT}", "-l:libhsa-runtime64.so.1",
               f"-Wl,-rpath,{FAKES_OUT}", "-ldl", "-lpthread"])
