@@ -203,15 +203,15 @@ def build_fakes(force: bool = False) -> dict[str, Path]:
 
     hip_src = NATIVE / "fakes" / "fake_hip.cpp"
     hip = FAKES_OUT / "libamdhip64.so.7"
-    if force or not _stamp(hip, [hip_src, hsa_src], str(sorted(versions.items()))[:4096]):
+    hip_extra = ("fake_hip_launches; fake_hip_launch_blocks; fake_hip_physical_used; fake_hip_graph_create; "
+                 "fake_hip_exec_ns; fake_hip_svm_move; fake_hip_managed_gpu_bytes; fake_hip_host_touch_bytes;")
+    if force or not _stamp(hip, [hip_src, hsa_src], hip_extra + str(sorted(versions.items()))[:4096]):
         vs = FAKES_OUT / "hip.map"
-        vs.write_text(_version_script(
-            hip_src, "hip_4.2", versions,
-            "fake_hip_launches; fake_hip_launch_blocks; fake_hip_physical_used; fake_hip_graph_create; fake_hip_exec_ns; fake_hip_svm_move; fake_hip_managed_gpu_bytes; fake_hip_host_touch_bytes;"))
+        vs.write_text(_version_script(hip_src, "hip_4.2", versions, hip_extra))
         _run([CXX, *COMMON, hip_src, "-o", hip, "-shared", "-Wl,-soname,libamdhip64.so.7",
               f"-Wl,--version-script={vs}", f"-L{FAKES_OUT}", "-l:libhsa-runtime64.so.1",
               f"-Wl,-rpath,{FAKES_OUT}", "-ldl", "-lpthread"])
-        _mark(hip, [hip_src, hsa_src], str(sorted(versions.items()))[:4096])
+        _mark(hip, [hip_src, hsa_src], hip_extra + str(sorted(versions.items()))[:4096])
     res["hip"] = hip
 
     smi_src = NATIVE / "fakes" / "fake_amdsmi.cpp"
