@@ -636,12 +636,49 @@ bool vmem_release(void* p) {
   return true;
 }
 
+// Move the last `n` resident bytes of `r` back to host memory (the resident
+// part stays a prefix).  Caller holds g_move_mu.
+static bool demote_tail_locked(VRange* r, uint64_t n) {
+  n = std::min(n, r->gpu_bytes);
+  if (!n) return false;
+  auto t0 = std::chrono::steady_clock::now();
+  if (!prefetch(r->base + r->gpu_bytes - n, n, r->dev, false)) return false;
+  uint64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+  r->gpu_bytes -= n;
+  book_move(r->dev, n, false);
+  g_out_bytes.fetch_add(n);
+  g_moves.fetch_add(1);
+  trace_emit(VGPU_EV_MIGRATE, r->dev, n, ns << 1);
+  VLOG_INFO("vmem: %llu tail bytes of the range at %p to host memory for a plain allocation",
+            (unsigned long long)n, (void*)r->base);
+  return true;
+}
+
 bool vmem_make_room(int dev, uint64_t need) {
   if (g_count.load(std::memory_order_relaxed) == 0) return false;
   std::lock_guard<std::mutex> m(g_move_mu);
   const Knobs& k = knobs();
   const uint64_t tick = g_tick.load();
-  return make_room_locked(dev, need, nullptr, tick > k.cold_ticks ? tick - k.cold_ticks : 0);
+  if (make_room_locked(dev, need, nullptr, tick > k.cold_ticks ? tick - k.cold_ticks : 0)) return true;
+  // Nothing is cold and the budget is full of managed ranges.  An allocation
+  // below the managed size is activation / workspace sized and used by every
+  // kernel that follows: spilled, each of them would cross the host link.  It
+  // takes its room from the tail of the largest resident range instead, which
+  // kernels then read in place (a part E pod spilled 11 such buffers, ~190 MB,
+  // behind 11.8 GB of resident weights).  The caller has reserved `need`.
+  const uint64_t b = phys_budget(dev);
+  if (!b || k.managed_min < 0 || need >= (uint64_t)k.managed_min) return false;
+  constexpr uint64_t g = 2ull << 20;
+  while (pod_resident(dev) > b) {
+    VRange* big = nullptr;
+    {
+      std::shared_lock<std::shared_mutex> gl(g_tab_mu);
+      for (VRange* r : g_tab)
+        if (r->dev == dev && r->gpu_bytes && (!big || r->gpu_bytes > big->gpu_bytes)) big = r;
+    }
+    if (!big || !demote_tail_locked(big, (pod_resident(dev) - b + g - 1) & ~(g - 1))) return false;
+  }
+  return true;
 }
 
 namespace {

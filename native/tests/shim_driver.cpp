@@ -389,6 +389,31 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (sc == "vmem_small") {
+    // The budget is full of hot managed ranges; a plain (activation-sized)
+    // allocation takes its room from the largest range's tail instead of
+    // spilling to host memory.
+    const size_t G = 1ull << 30, M = 1ull << 20;
+    auto self_region = sym<void* (*)()>("vgpu_self_region");
+    auto self_slot = sym<int (*)()>("vgpu_self_slot");
+    auto slot_u = [&]() -> vgpu_dev_usage_t& {
+      return ((vgpu_shared_region_t*)self_region())->procs[self_slot()].used[dev];
+    };
+    void** ab = new void*[3]();
+    int ra = hipMalloc(&ab[0], 6 * G), rb = hipMalloc(&ab[1], 2 * G - 16 * M);
+    printf("alloc_a=%d\nalloc_b=%d\na_gpu=%llu\nb_gpu=%llu\nhost_before=%llu\n", ra, rb,
+           (unsigned long long)fake_hip_managed_gpu_bytes(ab[0]), (unsigned long long)fake_hip_managed_gpu_bytes(ab[1]),
+           (unsigned long long)slot_u().host_bytes);
+    int rc = hipMalloc(&ab[2], 20 * M);  // below VGPU_VMEM_MANAGED_MIN_MB: plain
+    printf("small=%d\na_gpu_after=%llu\nb_gpu_after=%llu\nhost_after=%llu\nphys=%llu\n", rc,
+           (unsigned long long)fake_hip_managed_gpu_bytes(ab[0]), (unsigned long long)fake_hip_managed_gpu_bytes(ab[1]),
+           (unsigned long long)slot_u().host_bytes, (unsigned long long)fake_hip_physical_used(dev));
+    hipFree(ab[2]);
+    hipFree(ab[1]);
+    hipFree(ab[0]);
+    return 0;
+  }
+
   if (sc == "vmem_copy") {
     // A managed-by-default range (physical budget) written by host copies:
     // KFD moves the touched pages to host memory (fake HIP models it); the

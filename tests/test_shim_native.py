@@ -199,6 +199,21 @@ def test_vmem_host_copy_pages_come_back(native_build):
     assert o["host_touched"] == "0"
 
 
+def test_vmem_small_allocation_takes_room_from_a_range_tail(native_build):
+    """The budget (8 GiB) is full of managed ranges that are all in use.  A
+    plain, activation-sized allocation (20 MiB, below the managed size) is not
+    spilled to host memory: the tail of the largest resident range moves out
+    instead, and physical use stays within the budget."""
+    o = run("vmem_small", env=BUDGET_ENV)
+    assert (o["alloc_a"], o["alloc_b"], o["small"]) == ("0", "0", "0")
+    assert int(o["a_gpu"]) == 6 * GiB and o["host_before"] == "0"
+    moved = 6 * GiB - int(o["a_gpu_after"])
+    assert 0 < moved <= 64 << 20 and moved % (2 << 20) == 0, o
+    assert int(o["host_after"]) == moved  # only the tail is on the host, not the new buffer
+    assert o["b_gpu_after"] == o["b_gpu"]
+    assert int(o["phys"]) <= 8 * GiB
+
+
 def test_vmem_hot_set_beyond_budget_does_not_cycle(native_build):
     """Two hot 6 GiB ranges against an 8 GiB budget: the resident part stays
     put (no LRU exchange on a cyclic sweep), the rest is read in place."""
