@@ -309,30 +309,12 @@ bool demote_locked(VRange* r) {
   return true;
 }
 
-// Bytes that may still become HBM-resident on `dev` (budget and physical HBM).
-uint64_t room_bytes(int dev) {
-  uint64_t room = hbm_free(dev);
-  room = room > knobs().headroom ? room - knobs().headroom : 0;
-  if (const uint64_t b = phys_budget(dev)) {
-    const uint64_t used = pod_resident(dev);
-    room = std::min<uint64_t>(room, b > used ? b - used : 0);
-  }
-  return room;
-}
-
-// Promote the next piece of `r`: a whole piece, or, when the budget cannot
-// take one any more, the 2 MiB granules that still fit (a 1 GiB piece that no
-// longer fits would otherwise leave up to 1 GiB of the budget unused).
-// Caller holds g_move_mu.  False when there is no room.
+// Promote the next piece of `r`.  Caller holds g_move_mu.  False when there is no room.
 bool promote_piece_locked(VRange* r) {
   const Knobs& k = knobs();
   uint64_t n = std::min<uint64_t>(k.piece, r->size - r->gpu_bytes);
   if (!n) return false;
-  if (!room_for(r->dev, n)) {  // make_room_locked ran first
-    constexpr uint64_t g = 2ull << 20;
-    n = std::min<uint64_t>(n, room_bytes(r->dev) & ~(g - 1));
-    if (!n) return false;
-  }
+  if (!room_for(r->dev, n)) return false;  // make_room_locked ran first
   auto t0 = std::chrono::steady_clock::now();
   if (!prefetch(r->base + r->gpu_bytes, n, r->dev, true)) return false;
   uint64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
@@ -419,8 +401,7 @@ void pager_step(bool advance) {
     const uint64_t stale = tick > k.cold_ticks ? tick - k.cold_ticks : 0;
     while (r->gpu_bytes < r->size) {
       uint64_t n = std::min<uint64_t>(k.piece, r->size - r->gpu_bytes);
-      (void)make_room_locked(r->dev, n, r, stale);  // cold ranges give way; a partial piece may still fit
-      if (!promote_piece_locked(r)) {
+      if (!make_room_locked(r->dev, n, r, stale) || !promote_piece_locked(r)) {
         waiting += r->size - r->gpu_bytes;
         waiting_dev = r->dev;
         break;
@@ -553,8 +534,7 @@ hipError_t vmem_alloc_managed(void** ptr, size_t size, int dev) {
   const uint64_t stale = tick > k.cold_ticks ? tick - k.cold_ticks : 0;
   while (r->gpu_bytes < r->size) {
     const uint64_t n = std::min<uint64_t>(k.piece, r->size - r->gpu_bytes);
-    (void)make_room_locked(dev, n, r, stale);
-    if (!promote_piece_locked(r)) break;
+    if (!make_room_locked(dev, n, r, stale) || !promote_piece_locked(r)) break;
   }
   return hipSuccess;
 }
