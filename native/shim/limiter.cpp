@@ -116,7 +116,12 @@ struct DevLimiter {
   int spatial = 0;
   bool auto_joined = false;
   bool pool0_saved = false;
-  uint64_t pool0[VGPU_CU_MASK_WORDS] = {};  // the plugin's pool mask at start (all-zero = every CU)
+  uint64_t pool0[VGPU_CU_MASK_WORDS] = {};  // the plugin's pool mask (all-zero = every CU)
+  // What this process last saw or wrote in the region's mask: anything else
+  // found there was written by the device plugin (a masked container arrived
+  // or left and the pool was reshaped, custate.py _reshape_pool) and becomes
+  // the new pool0.
+  uint64_t shim_mask[VGPU_CU_MASK_WORDS] = {};
 };
 
 DevLimiter g_lim[VGPU_MAX_DEVICES];
@@ -208,7 +213,7 @@ void configure() {
       La.auto_share = 1;
       if (!La.pool0_saved && s.region) {
         for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w)
-          La.pool0[w] = __atomic_load_n(&s.region->dev[d].cu_mask[w], __ATOMIC_RELAXED);
+          La.shim_mask[w] = La.pool0[w] = __atomic_load_n(&s.region->dev[d].cu_mask[w], __ATOMIC_RELAXED);
         La.pool0_saved = true;
       }
       g_auto_any.store(1, std::memory_order_relaxed);
@@ -353,11 +358,23 @@ bool reap(int dev, DevLimiter& L, uint64_t now_hint) {
   return left > 0;
 }
 
-void write_region_mask(int dev, const uint64_t m[VGPU_CU_MASK_WORDS]) {
+// The auto policy's write of its own mask: word by word, only over the value
+// it last saw (compare-and-swap), so a pool reshape the device plugin wrote
+// meanwhile wins and is picked up at the next step.  Returns false when the
+// region changed under us.
+bool write_own_mask(int dev, DevLimiter& L, const uint64_t m[VGPU_CU_MASK_WORDS]) {
   State& s = st();
-  if (!s.region || region_lock(s.region) != 0) return;
-  for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) __atomic_store_n(&s.region->dev[dev].cu_mask[w], m[w], __ATOMIC_RELAXED);
-  region_unlock(s.region);
+  if (!s.region) return false;
+  bool ok = true;
+  for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) {
+    uint64_t expect = L.shim_mask[w];
+    if (__atomic_compare_exchange_n(&s.region->dev[dev].cu_mask[w], &expect, m[w], false, __ATOMIC_RELAXED,
+                                    __ATOMIC_RELAXED))
+      L.shim_mask[w] = m[w];
+    else
+      ok = false;  // external value stays; shim_mask keeps the old one so the next step sees the change
+  }
+  return ok;
 }
 
 // Adaptive share policy (VGPU_CU_SHARE=auto; the device plugin's default).
@@ -399,6 +416,32 @@ void auto_step() {
                                       note, sizeof note);
     if (note[0]) VLOG_INFO("device %d: adaptive share: %s", d, note);
     const int phys = cumask_device_physical_cus(d);
+    // A mask we did not write: the plugin reshaped the pool (the
+    // stale pool0 widened a shrunk member back onto a masked container's CUs,
+    // and a spatial claim could pick CUs that container holds).  The plugin's
+    // value is the pool from now on; a claim we held is given up and re-made
+    // from the new pool at a later step.
+    {
+      uint64_t cur[VGPU_CU_MASK_WORDS];
+      bool ext = false;
+      for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) {
+        cur[w] = __atomic_load_n(&s.region->dev[d].cu_mask[w], __ATOMIC_RELAXED);
+        ext |= cur[w] != L.shim_mask[w];
+      }
+      if (ext) {
+        for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) L.shim_mask[w] = L.pool0[w] = cur[w];
+        int n = 0;
+        for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) n += __builtin_popcountll(cur[w]);
+        VLOG_INFO("device %d: adaptive share: pool reshaped by the device plugin to %d CUs", d, n ? n : phys);
+        if (L.spatial) {
+          uint64_t none[4], full_pool[VGPU_CU_MASK_WORDS];
+          for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) full_pool[w] = ~0ull;
+          board_claim_cus(L.board, L.board_slot, 0, 8, full_pool, none);
+          L.spatial = 0;
+          trace_emit(VGPU_EV_QUEUE, d, 0, 0);
+        }
+      }
+    }
     uint64_t allowed[VGPU_CU_MASK_WORDS];
     bool any = false;
     for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) any |= L.pool0[w] != 0;
@@ -414,9 +457,13 @@ void auto_step() {
       const uint32_t want = ((uint32_t)((phys > 0 ? phys : 256) * lim + 99) / 100 + nx - 1) / nx * nx;
       uint64_t got[4];
       if (board_claim_cus(L.board, L.board_slot, want, nx, allowed, got)) {
-        L.spatial = 1;
-        write_region_mask(d, got);
-        trace_emit(VGPU_EV_QUEUE, d, 1, want);
+        if (write_own_mask(d, L, got)) {
+          L.spatial = 1;
+          trace_emit(VGPU_EV_QUEUE, d, 1, want);
+        } else {
+          uint64_t none[4];
+          board_claim_cus(L.board, L.board_slot, 0, 8, allowed, none);  // pool changed meanwhile
+        }
       }
       continue;
     }
@@ -438,9 +485,8 @@ void auto_step() {
     if (full && !any)
       for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) mask[w] = 0;  // all CUs
     bool same = true;
-    for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w)
-      same &= __atomic_load_n(&s.region->dev[d].cu_mask[w], __ATOMIC_RELAXED) == mask[w];
-    if (!same) write_region_mask(d, mask);
+    for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) same &= L.shim_mask[w] == mask[w];
+    if (!same) (void)write_own_mask(d, L, mask);
   }
 }
 

@@ -700,3 +700,40 @@ def test_auto_policy_remembers_its_decision_across_a_pause(native_build, tmp_pat
 def test_auto_policy_lone_pod_never_explores(native_build, tmp_path):
     launches, notes = _auto_ab(tmp_path, 0.6, n=1, secs=2.0)
     assert notes == []
+
+
+def test_auto_member_keeps_a_pool_the_plugin_reshaped(native_build, tmp_path):
+    """ADVICE r3 (limiter.cpp auto_step): an auto pool member runs; a masked
+    container then arrives and the device plugin shrinks the member's pool in
+    its shared region (custate.py _reshape_pool).  The member must adopt the
+    plugin's pool instead of widening its mask back onto the new container's
+    CUs from the pool it saw at start."""
+    import threading
+    import time
+    from vgpu.monitor.region import AttachedRegion
+    region = tmp_path / "r.cache"
+    e = {k: v for k, v in os.environ.items() if not k.startswith(("VGPU_", "CUDA_", "HIP_"))}
+    e.update({"LD_LIBRARY_PATH": str(FAKES_DIR), "LD_PRELOAD": str(shim_path()),
+              "VGPU_DEVICE_CU_LIMIT_0": "50", "VGPU_CU_SHARE": "auto", "VGPU_CU_MASK_FROM_LIMIT": "false",
+              "VGPU_LOCK_DIR": str(tmp_path), "VGPU_DEVICE_UUID_0": "GPU-reshape", "VGPU_FAKE_KERNEL_US": "500",
+              "VGPU_SHARED_REGION": str(region), "VGPU_LOG_LEVEL": "3"})
+    p = subprocess.Popen([str(FAKES_DIR / "shim_driver"), "duty", "2.5"], env=e, stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    pool = (1 << 128) - 1  # the plugin's reshaped pool: the other 128 CUs went to a masked container
+    deadline = time.time() + 10
+    while not region.exists() and time.time() < deadline:
+        time.sleep(0.05)
+    time.sleep(0.8)
+    r = AttachedRegion(str(region))
+    try:
+        r.set_cu_mask(0, pool)
+        seen = []
+        for _ in range(10):  # the limiter runs auto_step every 50 ms
+            time.sleep(0.1)
+            seen.append(r.devices()[0].cu_mask)
+    finally:
+        r.close()
+    out, err = p.communicate(timeout=60)
+    assert p.returncode == 0, err[-2000:]
+    assert all(m == pool for m in seen), [hex(m) for m in seen]
+    assert "pool reshaped by the device plugin to 128 CUs" in err, err[-2000:]
