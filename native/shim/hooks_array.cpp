@@ -257,6 +257,21 @@ __attribute__((visibility("default"))) hipError_t hipModuleUnload(hipModule_t m)
 // The importer maps the same HBM, so it records the mapping (kIpcImport,
 // charged 0 bytes). A hipFree of an imported pointer then cannot uncharge an
 // unrelated buffer, and the monitor can report imported bytes.
+// A managed range (virtual device memory under a physical budget) is SVM, not
+// a device allocation: the runtime cannot export it.  Say so instead of the
+// runtime's bare invalid-value (PyTorch CUDA-IPC tensors / RCCL P2P buffers
+// of an oversubscribed pod: docs/config.md, virtual device memory).
+__attribute__((visibility("default"))) hipError_t hipIpcGetMemHandle(hipIpcMemHandle_t* handle, void* dev_ptr) {
+  ensure_init();
+  if (st().enabled && dev_ptr && vmem_contains(dev_ptr)) {
+    VLOG_WARN("hipIpcGetMemHandle(%p): a virtual-device-memory (managed) range cannot be exported over IPC; "
+              "set VGPU_VMEM_MANAGED_MIN_MB=-1 for pods that share device buffers between processes",
+              dev_ptr);
+    return hipErrorNotSupported;
+  }
+  return REAL_HIP(hipIpcGetMemHandle)(handle, dev_ptr);
+}
+
 __attribute__((visibility("default"))) hipError_t hipIpcOpenMemHandle(void** dev_ptr, hipIpcMemHandle_t handle,
                                                                       unsigned int flags) {
   ensure_init();

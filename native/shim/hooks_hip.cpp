@@ -95,8 +95,11 @@ GraphWork graph_exec_work(hipGraphExec_t exec) {
 }
 
 // Shared allocation path: reserve → real alloc → record (or unreserve).
+// managed_ok = false: an allocation whose flags a managed range cannot honour
+// (fine-grained / uncached hipExtMallocWithFlags) never becomes one — neither
+// under a physical budget nor as an oversubscription spill.
 template <class F>
-hipError_t charged_alloc(void** ptr, size_t size, int kind, F&& real_alloc) {
+hipError_t charged_alloc(void** ptr, size_t size, int kind, F&& real_alloc, bool managed_ok = true) {
   ensure_init();
   State& s = st();
   InHipAlloc in_alloc;
@@ -104,7 +107,7 @@ hipError_t charged_alloc(void** ptr, size_t size, int kind, F&& real_alloc) {
   suspend_gate();
   int dev = cur_dev();
   charge_context(dev);
-  if (kind == kDeviceBuf && vmem_wants_managed(dev, size)) {
+  if (kind == kDeviceBuf && managed_ok && vmem_wants_managed(dev, size)) {
     // Virtual device memory with a physical budget: a managed range from the
     // start, resident while the pod's budget has room (vmem.cpp).
     if (!mem_reserve(dev, size, kHostSpill)) return hipErrorOutOfMemory;
@@ -117,7 +120,7 @@ hipError_t charged_alloc(void** ptr, size_t size, int kind, F&& real_alloc) {
     return rc;
   }
   if (!mem_reserve(dev, size, kind)) return hipErrorOutOfMemory;
-  const bool over = kind == kDeviceBuf && s.region && s.region->oversubscribe;
+  const bool over = kind == kDeviceBuf && managed_ok && s.region && s.region->oversubscribe;
   hipError_t rc = over && vmem_should_spill(dev, size) ? hipErrorOutOfMemory : real_alloc();
   if (rc == hipErrorOutOfMemory && over) {
     // Virtual device memory: HBM is physically exhausted but the container's
@@ -314,8 +317,9 @@ __attribute__((visibility("default"))) hipError_t hipMalloc(void** ptr, size_t s
 
 __attribute__((visibility("default"))) hipError_t hipExtMallocWithFlags(void** ptr, size_t size,
                                                                         unsigned int flags) {
-  return charged_alloc(ptr, size, kDeviceBuf,
-                       [&] { return REAL_HIP(hipExtMallocWithFlags)(ptr, size, flags); });
+  return charged_alloc(
+      ptr, size, kDeviceBuf, [&] { return REAL_HIP(hipExtMallocWithFlags)(ptr, size, flags); },
+      flags == hipDeviceMallocDefault);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMallocAsync(void** ptr, size_t size,

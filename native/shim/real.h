@@ -130,6 +130,7 @@ using hipModuleLoad = hipError_t (*)(hipModule_t*, const char*);
 using hipModuleLoadData = hipError_t (*)(hipModule_t*, const void*);
 using hipModuleLoadDataEx = hipError_t (*)(hipModule_t*, const void*, unsigned int, hipJitOption*, void**);
 using hipModuleUnload = hipError_t (*)(hipModule_t);
+using hipIpcGetMemHandle = hipError_t (*)(hipIpcMemHandle_t*, void*);
 using hipIpcOpenMemHandle = hipError_t (*)(void**, hipIpcMemHandle_t, unsigned int);
 using hipIpcCloseMemHandle = hipError_t (*)(void*);
 using hipDeviceGetPCIBusId = hipError_t (*)(char*, int, int);

@@ -148,6 +148,8 @@ bool vmem_wants_managed(int dev, uint64_t size);
 hipError_t vmem_alloc_managed(void** ptr, size_t size, int dev);
 hipError_t vmem_alloc_overflow(void** ptr, size_t size, int dev);
 bool vmem_owns(void* p);
+// p lies inside a managed range (any offset).
+bool vmem_contains(const void* p);
 bool vmem_release(void* p);                 // forget a range before the real free; false if not ours
 bool vmem_make_room(int dev, uint64_t need); // demote cold promoted ranges; true if `need` now fits
 void vmem_scan_args(void** args, hipStream_t stream);    // HIP-Clang stub argument array

@@ -610,6 +610,12 @@ bool vmem_owns(void* p) {
   return r && r->base == (uintptr_t)p;
 }
 
+bool vmem_contains(const void* p) {
+  if (g_count.load(std::memory_order_relaxed) == 0) return false;
+  std::shared_lock<std::shared_mutex> g(g_tab_mu);
+  return find_locked((uintptr_t)p) != nullptr;
+}
+
 bool vmem_release(void* p) {
   if (!vmem_owns(p)) return false;
   std::lock_guard<std::mutex> m(g_move_mu);

@@ -414,6 +414,29 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (sc == "vmem_flags") {
+    // Under a physical budget plain hipMalloc becomes a managed range, but an
+    // allocation with fine-grained / uncached flags stays a device allocation
+    // (a managed range cannot honour them), and a managed range refuses IPC
+    // export with a clear error while the plain one exports.
+    const size_t G = 1ull << 30;
+    void** ab = new void*[3]();
+    int ra = hipMalloc(&ab[0], G);
+    int rf = hipExtMallocWithFlags(&ab[1], G, hipDeviceMallocFinegrained);
+    int rd = hipExtMallocWithFlags(&ab[2], G, hipDeviceMallocDefault);
+    hipIpcMemHandle_t h;
+    int im = hipIpcGetMemHandle(&h, ab[0]);
+    int imo = hipIpcGetMemHandle(&h, (char*)ab[0] + 4096);
+    int ifg = hipIpcGetMemHandle(&h, ab[1]);
+    printf("alloc=%d\nalloc_fine=%d\nalloc_default=%d\n", ra, rf, rd);
+    printf("managed_gpu=%llu\nfine_gpu=%llu\ndefault_gpu=%llu\n",
+           (unsigned long long)fake_hip_managed_gpu_bytes(ab[0]), (unsigned long long)fake_hip_managed_gpu_bytes(ab[1]),
+           (unsigned long long)fake_hip_managed_gpu_bytes(ab[2]));
+    printf("ipc_managed=%d\nipc_managed_offset=%d\nipc_fine=%d\n", im, imo, ifg);
+    for (int i = 0; i < 3; ++i) hipFree(ab[i]);
+    return 0;
+  }
+
   if (sc == "vmem_copy") {
     // A managed-by-default range (physical budget) written by host copies:
     // KFD moves the touched pages to host memory (fake HIP models it); the

@@ -737,3 +737,19 @@ def test_auto_member_keeps_a_pool_the_plugin_reshaped(native_build, tmp_path):
     assert p.returncode == 0, err[-2000:]
     assert all(m == pool for m in seen), [hex(m) for m in seen]
     assert "pool reshaped by the device plugin to 128 CUs" in err, err[-2000:]
+
+
+def test_vmem_budget_keeps_flagged_allocations_plain_and_refuses_managed_ipc(native_build):
+    """ADVICE r3 (hooks_hip.cpp charged_alloc): under a physical budget only
+    plain allocations become managed ranges; hipExtMallocWithFlags with
+    fine-grained flags keeps its semantics (a device allocation, exportable
+    over IPC), and exporting a managed range fails with hipErrorNotSupported
+    and a log line instead of the runtime's bare invalid-value."""
+    o = run("vmem_flags", env={**BUDGET_ENV, "VGPU_LOG_LEVEL": "2"})
+    assert (o["alloc"], o["alloc_fine"], o["alloc_default"]) == ("0", "0", "0")
+    assert int(o["managed_gpu"]) == GiB and int(o["default_gpu"]) == GiB  # managed ranges, resident
+    assert o["fine_gpu"] == "0"  # not a managed range
+    not_supported = "801"  # hipErrorNotSupported
+    assert o["ipc_managed"] == not_supported and o["ipc_managed_offset"] == not_supported
+    assert o["ipc_fine"] == "0"
+    assert "cannot be exported over IPC" in o["_stderr"]
