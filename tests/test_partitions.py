@@ -187,3 +187,26 @@ def test_mixed_node_serves_partitions_under_their_own_resource(cpx_cluster):
     cd2, env2, n2 = _schedule(c, mkpod("spxpod", mem=8192, cores=25), "amd.com/gpu")
     assert n2 == 4 * 4 and cd2.uuid.split("-")[1] in ("00", "01", "02", "03")
     assert bin(int(env2["VGPU_CU_MASK_0"], 16)).count("1") == 64  # 25 % of a whole 256-CU GPU
+
+
+def test_mixed_node_reset_event_reaches_the_partition_plugin(cpx_cluster):
+    """ADVICE r3 (server.py health_step): under `mixed` every resource's server
+    polls the one backend; a GPU pre-reset event for a CPX partition read first
+    by the amd.com/gpu server must still reach the amd.com/gpu-cpx server (and
+    its post-reset bring the partition back)."""
+    from vgpu.deviceplugin.server import EVT_POST_RESET, EVT_PRE_RESET
+    c = cpx_cluster(cpx_nps2_fixture(gpus=8, spx=(0, 1, 2, 3)), "mixed")
+    gpu, cpx = c["plugins"]["amd.com/gpu"], c["plugins"]["amd.com/gpu-cpx"]
+    for p in (gpu, cpx):  # the servers' own health threads must not race the test
+        p._stop.set()
+    target = cpx.devices[3]
+    backend = gpu.backend._fan.backend
+    backend.pending_events.append((target.index, EVT_PRE_RESET, "pre-reset"))
+    gpu.health_step(0)  # reads the backend first: the event is not one of its devices
+    cpx.health_step(0)
+    assert cpx.health[target.uuid] is False
+    assert all(gpu.health.get(d.uuid, True) for d in gpu.devices)
+    backend.pending_events.append((target.index, EVT_POST_RESET, "post-reset"))
+    cpx.health_step(0)
+    gpu.health_step(0)
+    assert cpx.health[target.uuid] is True

@@ -132,14 +132,19 @@ class CrashBudget:
 def build_plugins(cfg: DevicePluginConfig, backend, client) -> list[VGPUDevicePlugin]:
     """One device-plugin server per extended resource of the node's partition
     strategy (vgpu/deviceplugin/partitions.py): amd.com/gpu, and with `mixed`
-    amd.com/gpu-dpx / -qpx / -cpx, each on its own socket."""
+    amd.com/gpu-dpx / -qpx / -cpx, each on its own socket.  Several servers
+    share the backend's device-event stream through an EventFanout: reading
+    events consumes them (amdsmi's notification queue), so each server gets
+    every event on a queue of its own and keeps those of its devices."""
+    from .discovery import EventFanout
     from .partitions import plan, socket_name
     groups, bad = plan(backend.devices(), cfg.partition_strategy, cfg.resource_name, cfg.partition_memory)
+    groups = {res: devs for res, devs in groups.items() if devs}
+    fan = EventFanout(backend) if len(groups) > 1 else None
     out = []
     for res, devs in sorted(groups.items()):
-        if not devs:
-            continue
-        out.append(VGPUDevicePlugin(cfg, backend, client, cfg.node_name, socket_name=socket_name(res, cfg.resource_name),
+        out.append(VGPUDevicePlugin(cfg, fan.view() if fan else backend, client, cfg.node_name,
+                                    socket_name=socket_name(res, cfg.resource_name),
                                     devices=devs, resource_name=res, unhealthy=bad))
     if not out:
         raise RuntimeError(f"no device to advertise under partition strategy {cfg.partition_strategy}")

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes
 import json
+import threading
 from dataclasses import asdict, dataclass, field
 
 from vgpu.native import LIB_DIR, NativeMissing
@@ -208,6 +209,49 @@ class SmiBackend(Backend):
         buf = (_SmiEvent * 32)()
         n = self.lib.vgpu_smi_events(buf, 32, timeout_ms)
         return [(buf[i].device, buf[i].type, buf[i].message.decode(errors="replace")) for i in range(n)]
+
+
+class EventFanout:
+    """One consumer of `backend.events()` for several device-plugin servers
+    (mixed partition strategy).  The backend's events are consumed
+    by reading them, so per-server polling lost a reset to whichever server
+    read it first and dropped it as not its device.  Each server polls through
+    a view with its own queue; a poll of an empty queue reads the backend once
+    (one reader at a time) and appends what it got to every queue."""
+
+    def __init__(self, backend):
+        self.backend = backend
+        self._lock = threading.Lock()
+        self._queues: list[list[tuple[int, int, str]]] = []
+
+    def view(self) -> "_FanoutView":
+        q: list[tuple[int, int, str]] = []
+        with self._lock:
+            self._queues.append(q)
+        return _FanoutView(self, q)
+
+    def _events(self, q: list, timeout_ms: int) -> list[tuple[int, int, str]]:
+        with self._lock:
+            if not q:
+                ev = self.backend.events(timeout_ms)
+                for other in self._queues:
+                    other.extend(ev)
+            out = list(q)
+            q.clear()
+            return out
+
+
+class _FanoutView:
+    """The backend as one server sees it: everything but events() passes through."""
+
+    def __init__(self, fan: EventFanout, q: list):
+        self._fan, self._q = fan, q
+
+    def events(self, timeout_ms: int = 1000) -> list[tuple[int, int, str]]:
+        return self._fan._events(self._q, timeout_ms)
+
+    def __getattr__(self, name):
+        return getattr(self._fan.backend, name)
 
 
 class StaticBackend(Backend):
