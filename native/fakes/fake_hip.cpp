@@ -38,6 +38,7 @@ namespace {
 struct Dev {
   uint64_t total = 0;
   uint64_t used = 0;
+  uint64_t imported = 0;  // bytes mapped from other processes (IPC)
   hsa_queue_t* queue = nullptr;
   hsa_amd_memory_pool_t pool{0};
   void* runtime_buf = nullptr;
@@ -216,7 +217,8 @@ void kfd_publish(int dev) {
   char path[512];
   snprintf(path, sizeof path, "%s/%s/vram_%d", dir, hp, 1000 + dev);
   if (FILE* f = fopen(path, "w")) {
-    fprintf(f, "%llu\n", (unsigned long long)(g_devs[dev].used + strtoull(rt, nullptr, 10)));
+    // KFD counts buffers mapped from other processes (IPC imports) as well
+    fprintf(f, "%llu\n", (unsigned long long)(g_devs[dev].used + g_devs[dev].imported + strtoull(rt, nullptr, 10)));
     fclose(f);
   }
 }
@@ -356,7 +358,7 @@ hipError_t hipModuleLoadData(hipModule_t* m, const void* image) {
 hipError_t hipModuleUnload(hipModule_t m) { return dev_free((void*)m); }
 // IPC: a handle carries (address, size); opening it maps the exporter's
 // buffer at a new address without allocating device memory.
-std::map<uintptr_t, size_t> g_imports;
+std::map<uintptr_t, std::pair<int, size_t>> g_imports;  // address -> (device, size)
 uintptr_t g_import_next = 0x7e0000000000ull;
 hipError_t hipIpcGetMemHandle(hipIpcMemHandle_t* h, void* p) {
   std::lock_guard<std::mutex> g(g_mu);
@@ -374,13 +376,25 @@ hipError_t hipIpcOpenMemHandle(void** p, hipIpcMemHandle_t h, unsigned int) {
   memcpy(&sz, h.reserved + 8, 8);
   uintptr_t a = g_import_next;
   g_import_next += (sz + (1 << 21)) & ~((uintptr_t)(1 << 21) - 1);
-  g_imports[a] = sz;
+  g_imports[a] = {tl_dev, sz};
+  if (tl_dev >= 0 && tl_dev < (int)g_devs.size()) {
+    g_devs[tl_dev].imported += sz;
+    kfd_publish(tl_dev);
+  }
   *p = (void*)a;
   return hipSuccess;
 }
 hipError_t hipIpcCloseMemHandle(void* p) {
   std::lock_guard<std::mutex> g(g_mu);
-  return g_imports.erase((uintptr_t)p) ? hipSuccess : hipErrorInvalidValue;
+  auto it = g_imports.find((uintptr_t)p);
+  if (it == g_imports.end()) return hipErrorInvalidValue;
+  const int d = it->second.first;
+  if (d >= 0 && d < (int)g_devs.size()) {
+    g_devs[d].imported -= it->second.second;
+    kfd_publish(d);
+  }
+  g_imports.erase(it);
+  return hipSuccess;
 }
 hipError_t hipMemGetAddressRange(hipDeviceptr_t* base, size_t* size, hipDeviceptr_t p) {
   std::lock_guard<std::mutex> g(g_mu);
@@ -393,7 +407,7 @@ hipError_t hipMemGetAddressRange(hipDeviceptr_t* base, size_t* size, hipDevicept
   auto jt = g_imports.find((uintptr_t)p);
   if (jt == g_imports.end()) return hipErrorInvalidValue;
   *base = p;
-  *size = jt->second;
+  *size = jt->second.second;
   return hipSuccess;
 }
 hipError_t hipStreamBeginCapture(hipStream_t s, hipStreamCaptureMode) {

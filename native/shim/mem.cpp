@@ -234,7 +234,12 @@ void mem_sync_runtime(int dev) {
   const ssize_t n = pread(fd, buf, sizeof buf - 1, 0);
   if (n <= 0) return;
   buf[n] = 0;
-  const uint64_t kfd = strtoull(buf, nullptr, 10);
+  uint64_t kfd = strtoull(buf, nullptr, 10);
+  // KFD's per-process counter includes buffers mapped from other processes
+  // (IPC imports: DDP peers, torch CUDA-IPC tensors); their exporters hold
+  // the charge (hooks_array.cpp), so they are not this process's context.
+  const int64_t imported = s.ipc_imported[dev].load(std::memory_order_relaxed);
+  if (imported > 0) kfd = kfd > (uint64_t)imported ? kfd - (uint64_t)imported : 0;
   std::lock_guard<std::mutex> g(s.ctx_mu);
   uint64_t& booked = s.ctx_booked[dev];
   const uint64_t total = __atomic_load_n(&sl->used[dev].total_bytes, __ATOMIC_RELAXED);

@@ -228,7 +228,17 @@ int main(int argc, char** argv) {
       usleep(5000);
     }
     void* q = nullptr;
+    void* own = nullptr;  // with the KFD model on: a buffer of its own (the device is in use)
+    if (getenv("VGPU_FAKE_KFD_RUNTIME")) hipMalloc(&own, 16ull << 20);
     printf("open=%d\n", (int)hipIpcOpenMemHandle(&q, h, hipIpcMemLazyEnablePeerAccess));
+    if (getenv("VGPU_FAKE_KFD_RUNTIME")) {  // runtime VRAM measured from KFD, which counts the import
+      size_t f = 0, t = 0;
+      hipMemGetInfo(&f, &t);
+      auto self_slot = sym<int (*)()>("vgpu_self_slot");
+      auto* r = (vgpu_shared_region_t*)self_region();
+      printf("context_bytes=%llu\n", (unsigned long long)r->procs[self_slot()].used[dev].context_bytes);
+      hipFree(own);
+    }
     printf("imported=%lld\nbuffer=%llu\nregion_used=%llu\n", (long long)imported(dev),
            (unsigned long long)usage(dev, 2), (unsigned long long)used(self_region(), dev));
     hipFree(q);  // misuse: must not uncharge anything

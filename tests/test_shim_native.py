@@ -753,3 +753,25 @@ def test_vmem_budget_keeps_flagged_allocations_plain_and_refuses_managed_ipc(nat
     assert o["ipc_managed"] == not_supported and o["ipc_managed_offset"] == not_supported
     assert o["ipc_fine"] == "0"
     assert "cannot be exported over IPC" in o["_stderr"]
+
+
+def test_runtime_vram_excludes_ipc_imports(native_build, tmp_path):
+    """ADVICE r3 (mem.cpp mem_sync_runtime): KFD's per-process VRAM counter
+    includes buffers mapped from other processes.  The importer's context
+    charge (KFD counter minus its ledger) must not book the exporter's 1 GiB
+    buffer a second time."""
+    env = _kfd_env(tmp_path, 777020)
+    env["VGPU_FAKE_KFD_RUNTIME"] = str(600 << 20)
+    base = {k: v for k, v in os.environ.items() if not k.startswith(("VGPU_", "CUDA_", "HIP_"))}
+    base.update(LD_LIBRARY_PATH=str(FAKES_DIR), LD_PRELOAD=str(shim_path()))
+    exp_env = {**base, "VGPU_DEVICE_MEMORY_LIMIT_0": "8g", "VGPU_SHARED_REGION": env["VGPU_SHARED_REGION"]}
+    h = str(tmp_path / "handle")
+    exp = subprocess.Popen([str(FAKES_DIR / "shim_driver"), "ipc_export", h], env=exp_env, stdout=subprocess.PIPE,
+                           text=True)
+    imp = subprocess.run([str(FAKES_DIR / "shim_driver"), "ipc_import", h], env={**base, **env},
+                         capture_output=True, text=True, timeout=60)
+    exp.communicate(timeout=60)
+    assert imp.returncode == 0, imp.stderr
+    o = dict(l.split("=", 1) for l in imp.stdout.splitlines() if "=" in l)
+    assert o["open"] == "0" and o["imported"] == str(GiB)
+    assert int(o["context_bytes"]) == 600 << 20, o
