@@ -567,6 +567,8 @@ hipError_t hipMemAdvise(const void*, size_t, hipMemoryAdvise, int) { return hipS
 // to system memory (native/probes/managed_access.hip); device-to-device copies
 // run on the GPU and move nothing.  No bytes are copied (fake addresses).
 static uint64_t g_host_touch_bytes = 0;  // bytes of managed ranges moved to host by copies
+uint64_t g_copies2d = 0;
+std::atomic<uint64_t> g_memsets{0};
 static void host_copy_touch_locked(const void* p, size_t n) {
   auto it = g_managed.upper_bound((uintptr_t)p);
   if (it == g_managed.begin()) return;
@@ -580,18 +582,84 @@ static void host_copy_touch_locked(const void* p, size_t n) {
   g_devs[m.dev].used -= moved;
   g_host_touch_bytes += moved;
 }
+static bool device_mem_locked(const void* p) {
+  auto it = g_allocs.upper_bound((uintptr_t)p);
+  if (it != g_allocs.begin() && (uintptr_t)p < std::prev(it)->first + std::prev(it)->second.second) return true;
+  auto jt = g_managed.upper_bound((uintptr_t)p);
+  return jt != g_managed.begin() && (uintptr_t)p < std::prev(jt)->first + std::prev(jt)->second.size;
+}
+// A host<->device copy moves every managed page it touches to system memory
+// (KFD); device-to-device copies (explicit, or Default between device
+// memory) move nothing.
 static hipError_t fake_copy(void* dst, const void* src, size_t n, hipMemcpyKind kind) {
   if (kind == hipMemcpyDeviceToDevice) return hipSuccess;
   std::lock_guard<std::mutex> g(g_mu);
+  if (kind == hipMemcpyDefault && device_mem_locked(dst) && device_mem_locked(src)) return hipSuccess;
   host_copy_touch_locked(dst, n);
   host_copy_touch_locked(src, n);
   return hipSuccess;
 }
+static size_t span2d(size_t pitch, size_t w, size_t h) { return h ? pitch * (h - 1) + w : 0; }
+// (Entry points call static helpers, never each other: an exported call would
+// resolve to a preloaded interposer and be counted twice.)
+static hipError_t copy2d(void* d, size_t dp, const void* s, size_t sp, size_t w, size_t h, hipMemcpyKind k) {
+  if (k == hipMemcpyDeviceToDevice) return hipSuccess;
+  std::lock_guard<std::mutex> g(g_mu);
+  host_copy_touch_locked(d, span2d(dp, w, h));
+  host_copy_touch_locked(s, span2d(sp, w, h));
+  g_copies2d++;
+  return hipSuccess;
+}
+hipError_t hipMemcpy2D(void* d, size_t dp, const void* s, size_t sp, size_t w, size_t h, hipMemcpyKind k) {
+  return copy2d(d, dp, s, sp, w, h, k);
+}
+hipError_t hipMemcpy2DAsync(void* d, size_t dp, const void* s, size_t sp, size_t w, size_t h, hipMemcpyKind k,
+                            hipStream_t) {
+  return copy2d(d, dp, s, sp, w, h, k);
+}
+static hipError_t copy3d(const hipMemcpy3DParms* p) {
+  if (!p || p->kind == hipMemcpyDeviceToDevice) return hipSuccess;
+  std::lock_guard<std::mutex> g(g_mu);
+  const size_t n = p->extent.depth * p->extent.height * p->extent.width;
+  if (p->dstPtr.ptr) host_copy_touch_locked(p->dstPtr.ptr, n);
+  if (p->srcPtr.ptr) host_copy_touch_locked(p->srcPtr.ptr, n);
+  return hipSuccess;
+}
+hipError_t hipMemcpy3D(const hipMemcpy3DParms* p) { return copy3d(p); }
+hipError_t hipMemcpy3DAsync(const hipMemcpy3DParms* p, hipStream_t) { return copy3d(p); }
+hipError_t hipMemcpyToSymbol(const void*, const void* s, size_t n, size_t, hipMemcpyKind k) {
+  return fake_copy(nullptr, s, n, k);
+}
+hipError_t hipMemcpyToSymbolAsync(const void*, const void* s, size_t n, size_t, hipMemcpyKind k, hipStream_t) {
+  return fake_copy(nullptr, s, n, k);
+}
+hipError_t hipMemcpyFromSymbol(void* d, const void*, size_t n, size_t, hipMemcpyKind k) {
+  return fake_copy(d, nullptr, n, k);
+}
+hipError_t hipMemcpyFromSymbolAsync(void* d, const void*, size_t n, size_t, hipMemcpyKind k, hipStream_t) {
+  return fake_copy(d, nullptr, n, k);
+}
+// Memsets run on the GPU: no page moves.
+hipError_t hipMemset(void*, int, size_t) { g_memsets++; return hipSuccess; }
+hipError_t hipMemsetAsync(void*, int, size_t, hipStream_t) { g_memsets++; return hipSuccess; }
+hipError_t hipMemsetD8(hipDeviceptr_t, unsigned char, size_t) { g_memsets++; return hipSuccess; }
+hipError_t hipMemsetD8Async(hipDeviceptr_t, unsigned char, size_t, hipStream_t) { g_memsets++; return hipSuccess; }
+hipError_t hipMemsetD16(hipDeviceptr_t, unsigned short, size_t) { g_memsets++; return hipSuccess; }
+hipError_t hipMemsetD16Async(hipDeviceptr_t, unsigned short, size_t, hipStream_t) { g_memsets++; return hipSuccess; }
+hipError_t hipMemsetD32(hipDeviceptr_t, int, size_t) { g_memsets++; return hipSuccess; }
+hipError_t hipMemsetD32Async(hipDeviceptr_t, int, size_t, hipStream_t) { g_memsets++; return hipSuccess; }
+hipError_t hipMemset2D(void*, size_t, int, size_t, size_t) { g_memsets++; return hipSuccess; }
+hipError_t hipMemset2DAsync(void*, size_t, int, size_t, size_t, hipStream_t) { g_memsets++; return hipSuccess; }
 hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind k) { return fake_copy(d, s, n, k); }
 hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned int) { return hipSuccess; }
 // Device memory and managed ranges are "device"; anything else is unregistered host memory.
 hipError_t hipPointerGetAttributes(hipPointerAttribute_t* a, const void* p) {
   std::lock_guard<std::mutex> g(g_mu);
+  auto da = g_allocs.upper_bound((uintptr_t)p);
+  if (da != g_allocs.begin() && (uintptr_t)p < std::prev(da)->first + std::prev(da)->second.second) {
+    a->type = hipMemoryTypeDevice;
+    return hipSuccess;
+  }
   auto it = g_managed.upper_bound((uintptr_t)p);
   if (it != g_managed.begin() && (uintptr_t)p < std::prev(it)->first + std::prev(it)->second.size) {
     a->type = hipMemoryTypeManaged;
@@ -831,6 +899,73 @@ hipError_t hipGraphLaunch(hipGraphExec_t e, hipStream_t) {
   timeline_launch();
   return hipSuccess;
 }
+// Explicit graph construction (hipGraphAdd*Node): nodes join the fake graph;
+// an alloc node's bytes come from the graph pool at launch.
+hipError_t hipGraphCreate(hipGraph_t* g, unsigned int) {
+  *g = reinterpret_cast<hipGraph_t>(new FakeGraph);
+  return hipSuccess;
+}
+static hipGraphNode_t add_node(hipGraphNode_t* node, hipGraph_t g, FakeNode* n) {
+  reinterpret_cast<FakeGraph*>(g)->nodes.push_back(n);
+  if (node) *node = reinterpret_cast<hipGraphNode_t>(n);
+  return reinterpret_cast<hipGraphNode_t>(n);
+}
+hipError_t hipGraphAddKernelNode(hipGraphNode_t* node, hipGraph_t g, const hipGraphNode_t*, size_t,
+                                 const hipKernelNodeParams* p) {
+  if (!g || !p) return hipErrorInvalidValue;
+  add_node(node, g, new FakeNode{hipGraphNodeTypeKernel, p->gridDim, nullptr});
+  return hipSuccess;
+}
+static hipError_t set_kernel_params(hipGraphNode_t node, const hipKernelNodeParams* p) {
+  if (!node || !p) return hipErrorInvalidValue;
+  reinterpret_cast<FakeNode*>(node)->grid = p->gridDim;
+  return hipSuccess;
+}
+hipError_t hipGraphKernelNodeSetParams(hipGraphNode_t node, const hipKernelNodeParams* p) {
+  return set_kernel_params(node, p);
+}
+// (an executable's node is not its graph's: the fake leaves the graph alone)
+hipError_t hipGraphExecKernelNodeSetParams(hipGraphExec_t e, hipGraphNode_t node, const hipKernelNodeParams* p) {
+  return e && node && p ? hipSuccess : hipErrorInvalidValue;
+}
+hipError_t hipGraphExecUpdate(hipGraphExec_t e, hipGraph_t g, hipGraphNode_t*, hipGraphExecUpdateResult* r) {
+  if (!e || !g) return hipErrorInvalidValue;
+  *reinterpret_cast<hipGraph_t*>(e) = g;
+  if (r) *r = hipGraphExecUpdateSuccess;
+  return hipSuccess;
+}
+hipError_t hipGraphAddMemcpyNode(hipGraphNode_t* node, hipGraph_t g, const hipGraphNode_t*, size_t,
+                                 const hipMemcpy3DParms*) {
+  add_node(node, g, new FakeNode{hipGraphNodeTypeMemcpy, dim3(1, 1, 1), nullptr});
+  return hipSuccess;
+}
+hipError_t hipGraphAddMemcpyNode1D(hipGraphNode_t* node, hipGraph_t g, const hipGraphNode_t*, size_t, void*,
+                                   const void*, size_t, hipMemcpyKind) {
+  add_node(node, g, new FakeNode{hipGraphNodeTypeMemcpy, dim3(1, 1, 1), nullptr});
+  return hipSuccess;
+}
+hipError_t hipGraphAddMemsetNode(hipGraphNode_t* node, hipGraph_t g, const hipGraphNode_t*, size_t,
+                                 const hipMemsetParams*) {
+  add_node(node, g, new FakeNode{hipGraphNodeTypeMemset, dim3(1, 1, 1), nullptr});
+  return hipSuccess;
+}
+hipError_t hipGraphAddChildGraphNode(hipGraphNode_t* node, hipGraph_t g, const hipGraphNode_t*, size_t,
+                                     hipGraph_t child) {
+  add_node(node, g, new FakeNode{hipGraphNodeTypeGraph, dim3(1, 1, 1), child});
+  reinterpret_cast<FakeGraph*>(g)->alloc_bytes += reinterpret_cast<FakeGraph*>(child)->alloc_bytes;
+  return hipSuccess;
+}
+hipError_t hipGraphAddMemAllocNode(hipGraphNode_t* node, hipGraph_t g, const hipGraphNode_t*, size_t,
+                                   hipMemAllocNodeParams* p) {
+  if (!g || !p) return hipErrorInvalidValue;
+  add_node(node, g, new FakeNode{hipGraphNodeTypeMemAlloc, dim3(1, 1, 1), nullptr});
+  reinterpret_cast<FakeGraph*>(g)->alloc_bytes += p->bytesize;
+  std::lock_guard<std::mutex> l(g_mu);
+  p->dptr = (void*)g_next;
+  g_next += (p->bytesize + (1 << 21)) & ~((uintptr_t)(1 << 21) - 1);
+  return hipSuccess;
+}
+
 // Test helper: a graph of kernel nodes with grids (grids[i], 2, 1) plus, when
 // child_grid > 0, one child graph holding a kernel node of grid child_grid.
 hipGraph_t fake_hip_graph_create(const unsigned* grids, int n, unsigned child_grid) {
@@ -856,6 +991,7 @@ hipError_t hipGetProcAddress(const char* sym, void** pfn, int, uint64_t,
 
 // ---- test introspection ----
 uint64_t fake_hip_launches() { return g_launches.load(); }
+uint64_t fake_hip_memsets() { return g_memsets.load(); }
 uint64_t fake_hip_exec_ns() { return g_exec_ns.load(); }
 uint64_t fake_hip_launch_blocks() { return g_launch_blocks.load(); }
 uint64_t fake_hip_physical_used(int dev) {

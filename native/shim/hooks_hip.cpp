@@ -270,16 +270,29 @@ bool staged_copy(void* dst, const void* src, size_t n, hipMemcpyKind kind, hipSt
   return true;
 }
 
+
+// hipMemcpyDefault between device memory on both sides moves no page (the
+// range side is device memory; so is the other when it is not host memory).
+inline bool device_to_device(const void* dst, const void* src, hipMemcpyKind kind) {
+  if (kind == hipMemcpyDeviceToDevice) return true;
+  if (kind != hipMemcpyDefault) return false;
+  return !host_side(vmem_contains(dst) ? src : dst);
+}
+
 inline hipError_t after_sync_copy(hipError_t rc, const void* dst, const void* src, size_t n, hipMemcpyKind kind) {
-  if (rc == hipSuccess && kind != hipMemcpyDeviceToDevice) vmem_after_copy(dst, src, n);
+  if (rc == hipSuccess && vmem_copy_touches(dst, src, n) && !device_to_device(dst, src, kind))
+    vmem_after_copy(dst, src, n);
   return rc;
 }
 
+// Async: the repair waits for the copy on the pager thread (vmem_after_copy_async),
+// the caller's stream stays asynchronous; a blocking repair only if it cannot be queued.
 inline hipError_t after_async_copy(hipError_t rc, const void* dst, const void* src, size_t n, hipMemcpyKind kind,
                                    hipStream_t stream) {
-  if (rc != hipSuccess || kind == hipMemcpyDeviceToDevice || !vmem_copy_touches(dst, src, n)) return rc;
+  if (rc != hipSuccess || !vmem_copy_touches(dst, src, n) || device_to_device(dst, src, kind)) return rc;
   if (capturing(stream)) return rc;  // nothing has run yet; the replayed copy node is not seen
-  if (REAL_HIP(hipStreamSynchronize)(stream) == hipSuccess) vmem_after_copy(dst, src, n);
+  if (!vmem_after_copy_async(dst, src, n, stream) && REAL_HIP(hipStreamSynchronize)(stream) == hipSuccess)
+    vmem_after_copy(dst, src, n);
   return rc;
 }
 
@@ -299,6 +312,116 @@ hipError_t copy_async(void* dst, const void* src, size_t n, hipMemcpyKind kind, 
   hipError_t rc;
   if (staged_copy(dst, src, n, kind, stream, &rc)) return rc;
   return after_async_copy(REAL_HIP(hipMemcpyAsync)(dst, src, n, kind, stream), dst, src, n, kind, stream);
+}
+
+// Bytes a pitched 2-D region spans.
+inline size_t span2d(size_t pitch, size_t width, size_t height) { return height ? pitch * (height - 1) + width : 0; }
+
+// 2-D copies: host <-> resident range is staged like a 1-D
+// copy, in blocks of whole rows (packed in the staging buffer at pitch =
+// width); true when staged.  Rows wider than the buffer are not staged.
+bool staged_copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height,
+                   hipMemcpyKind kind, hipStream_t stream, hipError_t* rc) {
+  if (kind == hipMemcpyDeviceToDevice || !width || !height || width > kStageBytes) return false;
+  const size_t dn = span2d(dpitch, width, height), sn = span2d(spitch, width, height);
+  const int ddev = vmem_resident_dev(dst, dn), sdev = vmem_resident_dev(src, sn);
+  if ((ddev < 0) == (sdev < 0)) return false;
+  const bool up = ddev >= 0;
+  const int dev = up ? ddev : sdev;
+  if (kind == hipMemcpyDefault && !host_side(up ? src : dst)) return false;
+  if (dev != cur_dev() || dev >= VGPU_MAX_DEVICES || capturing(stream)) return false;
+  Stage& g = g_stage[dev];
+  std::lock_guard<std::mutex> l(g.mu);
+  if (!g.buf) {
+    if (REAL_HIP(hipMalloc)(&g.buf, kStageBytes) != hipSuccess ||
+        REAL_HIP(hipEventCreateWithFlags)(&g.done, hipEventDisableTiming) != hipSuccess) {
+      (void)REAL_HIP(hipGetLastError)();
+      if (g.buf) (void)REAL_HIP(hipFree)(g.buf);
+      g.buf = nullptr;
+      return false;
+    }
+  } else if (REAL_HIP(hipStreamWaitEvent)(stream, g.done, 0) != hipSuccess) {
+    (void)REAL_HIP(hipGetLastError)();
+    return false;
+  }
+  const size_t rows = kStageBytes / width;
+  auto cp = REAL_HIP(hipMemcpy2DAsync);
+  hipError_t r = hipSuccess;
+  for (size_t y = 0; y < height && r == hipSuccess; y += rows) {
+    const size_t h = std::min(rows, height - y);
+    char* d = (char*)dst + y * dpitch;
+    const char* s = (const char*)src + y * spitch;
+    if (up) {
+      r = cp(g.buf, width, s, spitch, width, h, hipMemcpyHostToDevice, stream);
+      if (r == hipSuccess) r = cp(d, dpitch, g.buf, width, width, h, hipMemcpyDeviceToDevice, stream);
+    } else {
+      r = cp(g.buf, width, s, spitch, width, h, hipMemcpyDeviceToDevice, stream);
+      if (r == hipSuccess) r = cp(d, dpitch, g.buf, width, width, h, hipMemcpyDeviceToHost, stream);
+    }
+  }
+  (void)REAL_HIP(hipEventRecord)(g.done, stream);
+  *rc = r;
+  return true;
+}
+
+// Extent of one side of a 3-D copy (linear memory; arrays are never managed ranges).
+inline const void* side3d(const hipPitchedPtr& p, const hipPos& pos, const hipExtent& e, size_t* n) {
+  if (!p.ptr || !e.width || !e.height || !e.depth) {
+    *n = 0;
+    return nullptr;
+  }
+  const size_t slice = p.pitch * (p.ysize ? p.ysize : e.height);
+  const char* base = (const char*)p.ptr + pos.z * slice + pos.y * p.pitch + pos.x;
+  *n = slice * (e.depth - 1) + p.pitch * (e.height - 1) + e.width;
+  return base;
+}
+
+// A 3-D copy touching a resident range: as asked, then repaired (sync) or
+// queued for repair (async).
+hipError_t after3d(hipError_t rc, const hipMemcpy3DParms* p, hipStream_t stream, bool async) {
+  if (rc != hipSuccess || !p) return rc;
+  size_t dn = 0, sn = 0;
+  const void* d = side3d(p->dstPtr, p->dstPos, p->extent, &dn);
+  const void* s = side3d(p->srcPtr, p->srcPos, p->extent, &sn);
+  const size_t n = std::max(dn, sn);
+  if (!d && !s) return rc;
+  return async ? after_async_copy(rc, d, s, n, p->kind, stream) : after_sync_copy(rc, d, s, n, p->kind);
+}
+
+// Memsets run on the GPU and are not expected to move pages; a resident range
+// they touched is still checked and put back if KFD moved anything
+// (VGPU_VMEM_MEMSET_REPAIR=0 skips the check).
+bool memset_repair_on() {
+  static const bool on = env_bool(env_first("VGPU_VMEM_MEMSET_REPAIR"), true);
+  return on;
+}
+inline hipError_t after_memset(hipError_t rc, const void* dst, size_t n) {
+  if (rc == hipSuccess && memset_repair_on() && vmem_copy_touches(dst, nullptr, n)) vmem_after_copy(dst, nullptr, n);
+  return rc;
+}
+inline hipError_t after_memset_async(hipError_t rc, const void* dst, size_t n, hipStream_t stream) {
+  if (rc != hipSuccess || !memset_repair_on() || !vmem_copy_touches(dst, nullptr, n) || capturing(stream)) return rc;
+  if (!vmem_after_copy_async(dst, nullptr, n, stream) && REAL_HIP(hipStreamSynchronize)(stream) == hipSuccess)
+    vmem_after_copy(dst, nullptr, n);
+  return rc;
+}
+
+// node -> graph for nodes added through our hooks (hipGraphKernelNodeSetParams names only the node)
+std::mutex g_node_mu;
+std::unordered_map<hipGraphNode_t, hipGraph_t> g_node_graph;
+void note_node(hipGraphNode_t node, hipGraph_t graph) {
+  std::lock_guard<std::mutex> l(g_node_mu);
+  g_node_graph[node] = graph;
+}
+hipGraph_t graph_of(hipGraphNode_t node) {
+  std::lock_guard<std::mutex> l(g_node_mu);
+  auto it = g_node_graph.find(node);
+  return it == g_node_graph.end() ? nullptr : it->second;
+}
+void forget_graph_nodes(hipGraph_t graph) {
+  std::lock_guard<std::mutex> l(g_node_mu);
+  for (auto it = g_node_graph.begin(); it != g_node_graph.end();)
+    it = it->second == graph ? g_node_graph.erase(it) : std::next(it);
 }
 }  // namespace
 
@@ -436,6 +559,125 @@ __attribute__((visibility("default"))) hipError_t hipMemcpyHtoDAsync(hipDevicept
 __attribute__((visibility("default"))) hipError_t hipMemcpyDtoHAsync(void* dst, hipDeviceptr_t src, size_t n,
                                                                      hipStream_t stream) {
   return copy_async(dst, src, n, hipMemcpyDeviceToHost, stream);
+}
+
+// ---- 2-D / 3-D / symbol copies and memsets --------------------------
+__attribute__((visibility("default"))) hipError_t hipMemcpy2D(void* dst, size_t dpitch, const void* src,
+                                                              size_t spitch, size_t width, size_t height,
+                                                              hipMemcpyKind kind) {
+  ensure_init();
+  hipError_t rc;
+  if (staged_copy2d(dst, dpitch, src, spitch, width, height, kind, nullptr, &rc)) {
+    if (rc == hipSuccess) rc = REAL_HIP(hipStreamSynchronize)(nullptr);
+    return rc;
+  }
+  rc = REAL_HIP(hipMemcpy2D)(dst, dpitch, src, spitch, width, height, kind);
+  return after_sync_copy(rc, dst, src, std::max(span2d(dpitch, width, height), span2d(spitch, width, height)), kind);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpy2DAsync(void* dst, size_t dpitch, const void* src,
+                                                                   size_t spitch, size_t width, size_t height,
+                                                                   hipMemcpyKind kind, hipStream_t stream) {
+  ensure_init();
+  hipError_t rc;
+  if (staged_copy2d(dst, dpitch, src, spitch, width, height, kind, stream, &rc)) return rc;
+  rc = REAL_HIP(hipMemcpy2DAsync)(dst, dpitch, src, spitch, width, height, kind, stream);
+  return after_async_copy(rc, dst, src, std::max(span2d(dpitch, width, height), span2d(spitch, width, height)), kind,
+                          stream);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpy3D(const hipMemcpy3DParms* p) {
+  ensure_init();
+  return after3d(REAL_HIP(hipMemcpy3D)(p), p, nullptr, false);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpy3DAsync(const hipMemcpy3DParms* p, hipStream_t stream) {
+  ensure_init();
+  return after3d(REAL_HIP(hipMemcpy3DAsync)(p, stream), p, stream, true);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpyToSymbol(const void* symbol, const void* src, size_t n,
+                                                                    size_t offset, hipMemcpyKind kind) {
+  ensure_init();
+  return after_sync_copy(REAL_HIP(hipMemcpyToSymbol)(symbol, src, n, offset, kind), nullptr, src, n, kind);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpyToSymbolAsync(const void* symbol, const void* src,
+                                                                         size_t n, size_t offset, hipMemcpyKind kind,
+                                                                         hipStream_t stream) {
+  ensure_init();
+  return after_async_copy(REAL_HIP(hipMemcpyToSymbolAsync)(symbol, src, n, offset, kind, stream), nullptr, src, n,
+                          kind, stream);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpyFromSymbol(void* dst, const void* symbol, size_t n,
+                                                                      size_t offset, hipMemcpyKind kind) {
+  ensure_init();
+  return after_sync_copy(REAL_HIP(hipMemcpyFromSymbol)(dst, symbol, n, offset, kind), dst, nullptr, n, kind);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpyFromSymbolAsync(void* dst, const void* symbol, size_t n,
+                                                                           size_t offset, hipMemcpyKind kind,
+                                                                           hipStream_t stream) {
+  ensure_init();
+  return after_async_copy(REAL_HIP(hipMemcpyFromSymbolAsync)(dst, symbol, n, offset, kind, stream), dst, nullptr, n,
+                          kind, stream);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemset(void* dst, int value, size_t n) {
+  ensure_init();
+  return after_memset(REAL_HIP(hipMemset)(dst, value, n), dst, n);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemsetAsync(void* dst, int value, size_t n, hipStream_t stream) {
+  ensure_init();
+  return after_memset_async(REAL_HIP(hipMemsetAsync)(dst, value, n, stream), dst, n, stream);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemsetD8(hipDeviceptr_t dst, unsigned char v, size_t n) {
+  ensure_init();
+  return after_memset(REAL_HIP(hipMemsetD8)(dst, v, n), dst, n);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemsetD8Async(hipDeviceptr_t dst, unsigned char v, size_t n,
+                                                                   hipStream_t stream) {
+  ensure_init();
+  return after_memset_async(REAL_HIP(hipMemsetD8Async)(dst, v, n, stream), dst, n, stream);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemsetD16(hipDeviceptr_t dst, unsigned short v, size_t n) {
+  ensure_init();
+  return after_memset(REAL_HIP(hipMemsetD16)(dst, v, n), dst, 2 * n);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemsetD16Async(hipDeviceptr_t dst, unsigned short v, size_t n,
+                                                                    hipStream_t stream) {
+  ensure_init();
+  return after_memset_async(REAL_HIP(hipMemsetD16Async)(dst, v, n, stream), dst, 2 * n, stream);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemsetD32(hipDeviceptr_t dst, int v, size_t n) {
+  ensure_init();
+  return after_memset(REAL_HIP(hipMemsetD32)(dst, v, n), dst, 4 * n);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemsetD32Async(hipDeviceptr_t dst, int v, size_t n,
+                                                                    hipStream_t stream) {
+  ensure_init();
+  return after_memset_async(REAL_HIP(hipMemsetD32Async)(dst, v, n, stream), dst, 4 * n, stream);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemset2D(void* dst, size_t pitch, int v, size_t width,
+                                                              size_t height) {
+  ensure_init();
+  return after_memset(REAL_HIP(hipMemset2D)(dst, pitch, v, width, height), dst, span2d(pitch, width, height));
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemset2DAsync(void* dst, size_t pitch, int v, size_t width,
+                                                                   size_t height, hipStream_t stream) {
+  ensure_init();
+  return after_memset_async(REAL_HIP(hipMemset2DAsync)(dst, pitch, v, width, height, stream), dst,
+                            span2d(pitch, width, height), stream);
 }
 
 // Spilled allocations: a managed range (vmem.cpp) is freed by hipFree, a
@@ -733,6 +975,112 @@ __attribute__((visibility("default"))) hipError_t hipGraphInstantiateWithParams(
   return rc;
 }
 
+// ---- explicitly built graphs ---------------------------------------------
+// Nodes added or updated through the graph API never pass a launch hook: their
+// kernel arguments and copy / memset pointers are read here, so the graph's
+// managed ranges follow graph -> exec -> replay like captured ones; alloc nodes
+// are charged at launch like captured hipMallocAsync's.
+__attribute__((visibility("default"))) hipError_t hipGraphAddKernelNode(hipGraphNode_t* node, hipGraph_t graph,
+                                                                        const hipGraphNode_t* deps, size_t n,
+                                                                        const hipKernelNodeParams* p) {
+  ensure_init();
+  hipError_t rc = REAL_HIP(hipGraphAddKernelNode)(node, graph, deps, n, p);
+  if (rc == hipSuccess && p) {
+    vmem_graph_note(graph, false, p->kernelParams, p->extra, nullptr, 0);
+    if (node) note_node(*node, graph);
+  }
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipGraphKernelNodeSetParams(hipGraphNode_t node,
+                                                                              const hipKernelNodeParams* p) {
+  ensure_init();
+  hipError_t rc = REAL_HIP(hipGraphKernelNodeSetParams)(node, p);
+  if (rc == hipSuccess && p)
+    if (hipGraph_t g = graph_of(node)) vmem_graph_note(g, false, p->kernelParams, p->extra, nullptr, 0);
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipGraphExecKernelNodeSetParams(hipGraphExec_t exec,
+                                                                                  hipGraphNode_t node,
+                                                                                  const hipKernelNodeParams* p) {
+  ensure_init();
+  hipError_t rc = REAL_HIP(hipGraphExecKernelNodeSetParams)(exec, node, p);
+  if (rc == hipSuccess && p) vmem_graph_note(exec, true, p->kernelParams, p->extra, nullptr, 0);
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipGraphExecUpdate(hipGraphExec_t exec, hipGraph_t graph,
+                                                                     hipGraphNode_t* error_node,
+                                                                     hipGraphExecUpdateResult* result) {
+  ensure_init();
+  hipError_t rc = REAL_HIP(hipGraphExecUpdate)(exec, graph, error_node, result);
+  if (rc == hipSuccess) {  // the executable now runs `graph`'s parameters
+    graph_exec_record(exec, graph);
+    vmem_graph_instantiated(graph, exec);
+    pools_graph_instantiated(graph, exec);
+  }
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipGraphAddMemcpyNode(hipGraphNode_t* node, hipGraph_t graph,
+                                                                        const hipGraphNode_t* deps, size_t n,
+                                                                        const hipMemcpy3DParms* p) {
+  ensure_init();
+  hipError_t rc = REAL_HIP(hipGraphAddMemcpyNode)(node, graph, deps, n, p);
+  if (rc == hipSuccess && p) {
+    const void* ptrs[2] = {p->srcPtr.ptr, p->dstPtr.ptr};
+    vmem_graph_note(graph, false, nullptr, nullptr, ptrs, 2);
+  }
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipGraphAddMemcpyNode1D(hipGraphNode_t* node, hipGraph_t graph,
+                                                                          const hipGraphNode_t* deps, size_t n,
+                                                                          void* dst, const void* src, size_t count,
+                                                                          hipMemcpyKind kind) {
+  ensure_init();
+  hipError_t rc = REAL_HIP(hipGraphAddMemcpyNode1D)(node, graph, deps, n, dst, src, count, kind);
+  if (rc == hipSuccess) {
+    const void* ptrs[2] = {src, dst};
+    vmem_graph_note(graph, false, nullptr, nullptr, ptrs, 2);
+  }
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipGraphAddMemsetNode(hipGraphNode_t* node, hipGraph_t graph,
+                                                                        const hipGraphNode_t* deps, size_t n,
+                                                                        const hipMemsetParams* p) {
+  ensure_init();
+  hipError_t rc = REAL_HIP(hipGraphAddMemsetNode)(node, graph, deps, n, p);
+  if (rc == hipSuccess && p) {
+    const void* ptrs[1] = {p->dst};
+    vmem_graph_note(graph, false, nullptr, nullptr, ptrs, 1);
+  }
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipGraphAddChildGraphNode(hipGraphNode_t* node, hipGraph_t graph,
+                                                                            const hipGraphNode_t* deps, size_t n,
+                                                                            hipGraph_t child) {
+  ensure_init();
+  hipError_t rc = REAL_HIP(hipGraphAddChildGraphNode)(node, graph, deps, n, child);
+  if (rc == hipSuccess) {
+    vmem_graph_child(graph, child);
+    pools_graph_child(graph, child);
+  }
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipGraphAddMemAllocNode(hipGraphNode_t* node, hipGraph_t graph,
+                                                                          const hipGraphNode_t* deps, size_t n,
+                                                                          hipMemAllocNodeParams* p) {
+  ensure_init();
+  hipError_t rc = REAL_HIP(hipGraphAddMemAllocNode)(node, graph, deps, n, p);
+  if (rc == hipSuccess && p && st().enabled) pools_graph_add_bytes(graph, p->bytesize);
+  return rc;
+}
+
 __attribute__((visibility("default"))) hipError_t hipGraphExecDestroy(hipGraphExec_t exec) {
   graph_exec_forget(exec);
   vmem_graph_destroyed(exec);
@@ -741,6 +1089,7 @@ __attribute__((visibility("default"))) hipError_t hipGraphExecDestroy(hipGraphEx
 }
 
 __attribute__((visibility("default"))) hipError_t hipGraphDestroy(hipGraph_t graph) {
+  forget_graph_nodes(graph);
   vmem_graph_destroyed(graph);
   pools_graph_destroyed(graph);
   return REAL_HIP(hipGraphDestroy)(graph);

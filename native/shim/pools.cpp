@@ -183,6 +183,24 @@ void pools_capture_ended(unsigned long long cid, hipGraph_t graph) {
   g_cap_mem.erase(it);
 }
 
+// hipGraphAddMemAllocNode: the node's bytes are charged at launch like a
+// captured hipMallocAsync's.  Free nodes are not netted out (an upper bound:
+// the graph pool may reuse a freed block inside one launch).
+void pools_graph_add_bytes(hipGraph_t graph, uint64_t bytes) {
+  if (!graph || !bytes) return;
+  std::lock_guard<std::mutex> l(g_pmu);
+  g_graph_bytes[graph] += bytes;
+}
+
+void pools_graph_child(hipGraph_t graph, hipGraph_t child) {
+  std::lock_guard<std::mutex> l(g_pmu);
+  auto it = g_graph_bytes.find(child);
+  if (it != g_graph_bytes.end() && it->second) {
+    const uint64_t b = it->second;
+    g_graph_bytes[graph] += b;
+  }
+}
+
 void pools_graph_instantiated(hipGraph_t graph, hipGraphExec_t exec) {
   std::lock_guard<std::mutex> l(g_pmu);
   auto it = g_graph_bytes.find(graph);

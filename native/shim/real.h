@@ -104,6 +104,40 @@ using hipStreamBeginCaptureToGraph = hipError_t (*)(hipStream_t, hipGraph_t, con
 using hipStreamEndCapture = hipError_t (*)(hipStream_t, hipGraph_t*);
 using hipStreamGetCaptureInfo = hipError_t (*)(hipStream_t, hipStreamCaptureStatus*, unsigned long long*);
 using hipGraphDestroy = hipError_t (*)(hipGraph_t);
+using hipGraphAddKernelNode = hipError_t (*)(hipGraphNode_t*, hipGraph_t, const hipGraphNode_t*, size_t,
+                                             const hipKernelNodeParams*);
+using hipGraphKernelNodeSetParams = hipError_t (*)(hipGraphNode_t, const hipKernelNodeParams*);
+using hipGraphExecKernelNodeSetParams = hipError_t (*)(hipGraphExec_t, hipGraphNode_t, const hipKernelNodeParams*);
+using hipGraphExecUpdate = hipError_t (*)(hipGraphExec_t, hipGraph_t, hipGraphNode_t*, hipGraphExecUpdateResult*);
+using hipGraphAddMemcpyNode = hipError_t (*)(hipGraphNode_t*, hipGraph_t, const hipGraphNode_t*, size_t,
+                                             const hipMemcpy3DParms*);
+using hipGraphAddMemcpyNode1D = hipError_t (*)(hipGraphNode_t*, hipGraph_t, const hipGraphNode_t*, size_t, void*,
+                                               const void*, size_t, hipMemcpyKind);
+using hipGraphAddMemsetNode = hipError_t (*)(hipGraphNode_t*, hipGraph_t, const hipGraphNode_t*, size_t,
+                                             const hipMemsetParams*);
+using hipGraphAddChildGraphNode = hipError_t (*)(hipGraphNode_t*, hipGraph_t, const hipGraphNode_t*, size_t,
+                                                 hipGraph_t);
+using hipGraphAddMemAllocNode = hipError_t (*)(hipGraphNode_t*, hipGraph_t, const hipGraphNode_t*, size_t,
+                                               hipMemAllocNodeParams*);
+using hipMemcpy2D = hipError_t (*)(void*, size_t, const void*, size_t, size_t, size_t, hipMemcpyKind);
+using hipMemcpy2DAsync = hipError_t (*)(void*, size_t, const void*, size_t, size_t, size_t, hipMemcpyKind,
+                                        hipStream_t);
+using hipMemcpy3D = hipError_t (*)(const hipMemcpy3DParms*);
+using hipMemcpy3DAsync = hipError_t (*)(const hipMemcpy3DParms*, hipStream_t);
+using hipMemcpyToSymbol = hipError_t (*)(const void*, const void*, size_t, size_t, hipMemcpyKind);
+using hipMemcpyToSymbolAsync = hipError_t (*)(const void*, const void*, size_t, size_t, hipMemcpyKind, hipStream_t);
+using hipMemcpyFromSymbol = hipError_t (*)(void*, const void*, size_t, size_t, hipMemcpyKind);
+using hipMemcpyFromSymbolAsync = hipError_t (*)(void*, const void*, size_t, size_t, hipMemcpyKind, hipStream_t);
+using hipMemset = hipError_t (*)(void*, int, size_t);
+using hipMemsetAsync = hipError_t (*)(void*, int, size_t, hipStream_t);
+using hipMemsetD8 = hipError_t (*)(hipDeviceptr_t, unsigned char, size_t);
+using hipMemsetD8Async = hipError_t (*)(hipDeviceptr_t, unsigned char, size_t, hipStream_t);
+using hipMemsetD16 = hipError_t (*)(hipDeviceptr_t, unsigned short, size_t);
+using hipMemsetD16Async = hipError_t (*)(hipDeviceptr_t, unsigned short, size_t, hipStream_t);
+using hipMemsetD32 = hipError_t (*)(hipDeviceptr_t, int, size_t);
+using hipMemsetD32Async = hipError_t (*)(hipDeviceptr_t, int, size_t, hipStream_t);
+using hipMemset2D = hipError_t (*)(void*, size_t, int, size_t, size_t);
+using hipMemset2DAsync = hipError_t (*)(void*, size_t, int, size_t, size_t, hipStream_t);
 using hipMemPoolGetAttribute = hipError_t (*)(hipMemPool_t, hipMemPoolAttr, void*);
 using hipMemPoolTrimTo = hipError_t (*)(hipMemPool_t, size_t);
 using hipDeviceGetMemPool = hipError_t (*)(hipMemPool_t*, int);

@@ -125,6 +125,9 @@ void pools_capture_free(const void* ptr);  // hipFreeAsync of a block allocated 
 bool pools_any();
 void pools_capture_ended(unsigned long long capture_id, hipGraph_t graph);
 void pools_graph_instantiated(hipGraph_t graph, hipGraphExec_t exec);
+// Explicit graph construction: an alloc node's bytes, a child graph's bytes.
+void pools_graph_add_bytes(hipGraph_t graph, uint64_t bytes);
+void pools_graph_child(hipGraph_t graph, hipGraph_t child);
 void pools_graph_destroyed(const void* graph_or_exec);
 uint64_t pools_exec_bytes(hipGraphExec_t exec);
 bool pools_graph_admit(hipGraphExec_t exec, int dev, uint64_t* tentative);
@@ -150,6 +153,13 @@ hipError_t vmem_alloc_overflow(void** ptr, size_t size, int dev);
 bool vmem_owns(void* p);
 // p lies inside a managed range (any offset).
 bool vmem_contains(const void* p);
+// Async form of vmem_after_copy: the repair runs on the pager thread once the
+// operation queued on `stream` has completed.  false: could not queue it.
+bool vmem_after_copy_async(const void* dst, const void* src, size_t n, hipStream_t stream);
+// Ranges named by an explicitly built graph node (kernel arguments, copy /
+// memset pointers) join `key`'s set: a hipGraph_t, or a hipGraphExec_t when exec.
+void vmem_graph_note(const void* key, bool exec, void** args, void** extra, const void* const* ptrs, int nptrs);
+void vmem_graph_child(hipGraph_t graph, hipGraph_t child);
 bool vmem_release(void* p);                 // forget a range before the real free; false if not ours
 bool vmem_make_room(int dev, uint64_t need); // demote cold promoted ranges; true if `need` now fits
 void vmem_scan_args(void** args, hipStream_t stream);    // HIP-Clang stub argument array

@@ -139,10 +139,18 @@ VRange* find_locked(uintptr_t p) {
 // Ranges named by launches of the calling thread while its stream is being
 // captured (vmem_scan_*): they belong to the graph, not to this instant.
 thread_local std::vector<uintptr_t>* tl_sink = nullptr;
+// Set while the arguments of an explicitly built graph node are read: the
+// ranges go to tl_sink only (nothing runs now, so nothing is stamped as used).
+thread_local bool tl_collect_only = false;
 std::atomic<int> g_wake{0};  // a launch named a range that is not fully in HBM
 
 inline void touch_word(uintptr_t w, uint64_t tick) {
   if (w < g_tab.front()->base || w >= g_tab.back()->base + g_tab.back()->size) return;
+  if (tl_collect_only) {
+    if (VRange* r = find_locked(w))
+      if (tl_sink) tl_sink->push_back(r->base);
+    return;
+  }
   if (VRange* r = find_locked(w)) {
     if (r->last_use.load(std::memory_order_relaxed) != tick) r->last_use.store(tick, std::memory_order_relaxed);
     r->uses.fetch_add(1, std::memory_order_relaxed);
@@ -416,6 +424,8 @@ void pager_step(bool advance) {
   }
 }
 
+void drain_repairs();
+
 void pager_main() {
   pthread_setname_np(pthread_self(), "vgpu-vmem");
   tl_device = -1;
@@ -432,6 +442,9 @@ void pager_main() {
     // ages use counts and measures hot/cold windows, advances every tick_ms.
     g_thr_cv.wait_for(l, std::chrono::milliseconds(1));
     if (!g_thr_run) break;
+    l.unlock();
+    drain_repairs();
+    l.lock();
     const auto now = std::chrono::steady_clock::now();
     const bool tick = now - last >= std::chrono::milliseconds(k.tick_ms);
     const bool woke = g_wake.exchange(0) != 0;
@@ -603,6 +616,73 @@ void vmem_after_copy(const void* dst, const void* src, size_t n) {
   }
 }
 
+// Async copies and memsets that touched a resident range without staging: the
+// repair (vmem_after_copy) waits for the operation on the pager thread behind an
+// event recorded on its stream, so the caller's stream stays asynchronous
+// (it used to hipStreamSynchronize in the caller).
+namespace {
+struct Repair {
+  hipEvent_t ev;
+  Span sp[2];
+};
+std::mutex g_rep_mu;
+std::vector<Repair> g_rep;
+std::atomic<int> g_rep_n{0};
+
+void drain_repairs() {
+  if (g_rep_n.load(std::memory_order_relaxed) == 0) return;
+  std::vector<Repair> done;
+  {
+    std::lock_guard<std::mutex> l(g_rep_mu);
+    for (auto it = g_rep.begin(); it != g_rep.end();) {
+      const hipError_t q = REAL_HIP(hipEventQuery)(it->ev);
+      if (q == hipErrorNotReady) {
+        ++it;
+        continue;
+      }
+      done.push_back(*it);
+      it = g_rep.erase(it);
+    }
+    g_rep_n.store((int)g_rep.size(), std::memory_order_relaxed);
+  }
+  (void)REAL_HIP(hipGetLastError)();
+  for (Repair& r : done) {
+    (void)REAL_HIP(hipEventDestroy)(r.ev);
+    std::lock_guard<std::mutex> m(g_move_mu);
+    for (const Span& s : r.sp)
+      if (s.n && prefetch(s.lo, s.n, s.dev, true)) {
+        trace_emit(VGPU_EV_MIGRATE, s.dev, s.n, 1);
+        VLOG_DEBUG("vmem: %llu bytes at %p back to HBM after an async copy", (unsigned long long)s.n, (void*)s.lo);
+      }
+  }
+}
+}  // namespace
+
+bool vmem_after_copy_async(const void* dst, const void* src, size_t n, hipStream_t stream) {
+  if (g_count.load(std::memory_order_relaxed) == 0) return true;
+  Repair r{};
+  {
+    std::shared_lock<std::shared_mutex> g(g_tab_mu);
+    r.sp[0] = resident_span_locked(dst, n);
+    r.sp[1] = resident_span_locked(src, n);
+  }
+  if (!r.sp[0].n && !r.sp[1].n) return true;
+  if (REAL_HIP(hipEventCreateWithFlags)(&r.ev, hipEventDisableTiming) != hipSuccess) {
+    (void)REAL_HIP(hipGetLastError)();
+    return false;
+  }
+  if (REAL_HIP(hipEventRecord)(r.ev, stream) != hipSuccess) {
+    (void)REAL_HIP(hipGetLastError)();
+    (void)REAL_HIP(hipEventDestroy)(r.ev);
+    return false;
+  }
+  ensure_pager();
+  std::lock_guard<std::mutex> l(g_rep_mu);
+  g_rep.push_back(r);
+  g_rep_n.store((int)g_rep.size(), std::memory_order_relaxed);
+  return true;
+}
+
 bool vmem_owns(void* p) {
   if (g_count.load(std::memory_order_relaxed) == 0) return false;
   std::shared_lock<std::shared_mutex> g(g_tab_mu);
@@ -732,10 +812,14 @@ void scan_for(hipStream_t stream, F&& scan) {
 }
 }  // namespace
 
-void vmem_scan_args(void** args, hipStream_t stream) {
-  if (g_count.load(std::memory_order_relaxed) == 0 || !args) return;
-  const uintptr_t lo = (uintptr_t)__builtin_frame_address(0);
-  const uintptr_t hi = stack_top();
+namespace {
+// The argument values of a launch (an array of pointers to them, as
+// hipLaunchKernel takes it): [lo, hi) is the part of the calling thread's
+// stack above the scanner; arrays or values outside it are not read (their
+// sizes are unknown, so nothing bounds a read there).  Sorted addresses bound
+// each value by the next one.
+template <class F>
+void with_arg_values(void** args, uintptr_t lo, uintptr_t hi, F&& each) {
   if ((uintptr_t)args < lo || (uintptr_t)args >= hi) return;  // not a stub frame: nothing safe to read
   uintptr_t a[64];
   int n = 0;
@@ -747,33 +831,49 @@ void vmem_scan_args(void** args, hipStream_t stream) {
   }
   if (!n) return;
   std::sort(a, a + n);
+  for (int i = 0; i < n; ++i) {
+    // The last argument's size is unknown: a bounded look (PyTorch's
+    // elementwise kernels pass their operand pointer array last).
+    uintptr_t end = i + 1 < n ? a[i + 1] : a[i] + 512;
+    end = std::min<uintptr_t>({end, a[i] + 4096, hi});
+    if (end > a[i]) each(a[i], end - a[i]);
+  }
+}
+
+// The kernarg buffer of a module launch's `extra` (HIP_LAUNCH_PARAM_BUFFER_*), bounded.
+bool extra_buffer(void** extra, const void** buf, size_t* n) {
+  *buf = nullptr;
+  *n = 0;
+  for (int i = 0; extra && i < 8 && extra[i] != HIP_LAUNCH_PARAM_END; i += 2) {
+    if (extra[i] == HIP_LAUNCH_PARAM_BUFFER_POINTER) *buf = extra[i + 1];
+    else if (extra[i] == HIP_LAUNCH_PARAM_BUFFER_SIZE && extra[i + 1]) *n = *(size_t*)extra[i + 1];
+  }
+  *n = std::min<size_t>(*n, 4096);
+  return *buf && *n;
+}
+}  // namespace
+
+void vmem_scan_args(void** args, hipStream_t stream) {
+  if (g_count.load(std::memory_order_relaxed) == 0 || !args) return;
+  const uintptr_t lo = (uintptr_t)__builtin_frame_address(0);
+  const uintptr_t hi = stack_top();
   scan_for(stream, [&] {
     const uint64_t tick = g_tick.load(std::memory_order_relaxed);
     std::shared_lock<std::shared_mutex> g(g_tab_mu);
     if (g_tab.empty()) return;
-    for (int i = 0; i < n; ++i) {
-      // The last argument's size is unknown: a bounded look (PyTorch's
-      // elementwise kernels pass their operand pointer array last).
-      uintptr_t end = i + 1 < n ? a[i + 1] : a[i] + 512;
-      end = std::min<uintptr_t>({end, a[i] + 4096, hi});
-      if (end > a[i]) scan_words_locked((const unsigned char*)a[i], end - a[i], tick);
-    }
+    with_arg_values(args, lo, hi, [&](uintptr_t p, size_t n) { scan_words_locked((const unsigned char*)p, n, tick); });
   });
 }
 
 void vmem_scan_extra(void** extra, hipStream_t stream) {
   if (g_count.load(std::memory_order_relaxed) == 0 || !extra) return;
-  const void* buf = nullptr;
-  size_t n = 0;
-  for (int i = 0; i < 8 && extra[i] != HIP_LAUNCH_PARAM_END; i += 2) {
-    if (extra[i] == HIP_LAUNCH_PARAM_BUFFER_POINTER) buf = extra[i + 1];
-    else if (extra[i] == HIP_LAUNCH_PARAM_BUFFER_SIZE && extra[i + 1]) n = *(size_t*)extra[i + 1];
-  }
-  if (!buf || !n) return;
+  const void* buf;
+  size_t n;
+  if (!extra_buffer(extra, &buf, &n)) return;
   scan_for(stream, [&] {
     const uint64_t tick = g_tick.load(std::memory_order_relaxed);
     std::shared_lock<std::shared_mutex> g(g_tab_mu);
-    if (!g_tab.empty()) scan_words_locked((const unsigned char*)buf, std::min<size_t>(n, 4096), tick);
+    if (!g_tab.empty()) scan_words_locked((const unsigned char*)buf, n, tick);
   });
 }
 
@@ -802,6 +902,44 @@ void vmem_graph_destroyed(const void* graph_or_exec) {
   std::lock_guard<std::mutex> l(g_gmu);
   g_graph_ranges.erase(graph_or_exec);
   g_exec_ranges.erase(graph_or_exec);
+}
+
+// Explicitly built graphs (hipGraphAdd*Node, *SetParams, hipGraphExec*SetParams):
+// the ranges a node's kernel arguments or copy / memset pointers name join
+// the graph's (or executable's) set, as captured launches do.
+void vmem_graph_note(const void* key, bool exec, void** args, void** extra, const void* const* ptrs, int nptrs) {
+  if (g_count.load(std::memory_order_relaxed) == 0 || !key) return;
+  const uintptr_t lo = (uintptr_t)__builtin_frame_address(0);
+  const uintptr_t hi = stack_top();
+  std::vector<uintptr_t> hits;
+  {
+    std::shared_lock<std::shared_mutex> g(g_tab_mu);
+    if (g_tab.empty()) return;
+    tl_sink = &hits;
+    tl_collect_only = true;
+    if (args) with_arg_values(args, lo, hi, [&](uintptr_t p, size_t n) { scan_words_locked((const unsigned char*)p, n, 0); });
+    const void* buf;
+    size_t n;
+    if (extra && extra_buffer(extra, &buf, &n)) scan_words_locked((const unsigned char*)buf, n, 0);
+    for (int i = 0; i < nptrs; ++i)
+      if (ptrs[i]) touch_word((uintptr_t)ptrs[i], 0);
+    tl_collect_only = false;
+    tl_sink = nullptr;
+  }
+  if (hits.empty()) return;
+  std::sort(hits.begin(), hits.end());
+  hits.erase(std::unique(hits.begin(), hits.end()), hits.end());
+  std::lock_guard<std::mutex> l(g_gmu);
+  merge(exec ? g_exec_ranges[key] : g_graph_ranges[key], hits);
+}
+
+void vmem_graph_child(hipGraph_t graph, hipGraph_t child) {
+  std::lock_guard<std::mutex> l(g_gmu);
+  auto it = g_graph_ranges.find(child);
+  if (it != g_graph_ranges.end() && !it->second.empty()) {
+    const std::vector<uintptr_t> c = it->second;  // merge may rehash the map
+    merge(g_graph_ranges[graph], c);
+  }
 }
 
 // A replay runs none of our hooks: stamp every range its kernels name.

@@ -775,3 +775,43 @@ def test_runtime_vram_excludes_ipc_imports(native_build, tmp_path):
     o = dict(l.split("=", 1) for l in imp.stdout.splitlines() if "=" in l)
     assert o["open"] == "0" and o["imported"] == str(GiB)
     assert int(o["context_bytes"]) == 600 << 20, o
+
+
+def test_vmem_2d_3d_symbol_copies_and_memsets_keep_ranges_in_hbm(native_build):
+    """the copy / memset entry points beyond hipMemcpy on a
+    resident managed range.  2-D host copies are staged through plain HBM (KFD
+    moves no page); a 3-D host copy runs as asked and the pages it moved come
+    back (sync: before it returns; async: on the pager thread, the caller's
+    stream staying asynchronous); memsets and device-to-device symbol copies
+    move nothing."""
+    o = run("vmem_copy2", env={**BUDGET_ENV})
+    full = str(2 * GiB)
+    assert o["alloc"] == "0" and o["gpu_at_alloc"] == full
+    assert (o["copy2d"], o["copy2d_async"]) == ("0", "0")
+    assert o["gpu_after_2d"] == full and o["touched_after_2d"] == "0"   # staged
+    assert (o["memset"], o["memset_async"], o["memset_d32"], o["memset_d8_async"]) == ("0",) * 4
+    assert o["memsets"] == "4" and o["gpu_after_memset"] == full
+    assert o["copy3d"] == "0" and int(o["touched_after_3d"]) > 0        # KFD moved pages ...
+    assert o["gpu_after_3d"] == full                                     # ... and they came back
+    assert o["copy3d_async"] == "0" and o["gpu_after_3d_async"] == full
+    assert o["to_symbol"] == "0" and o["gpu_after_symbol"] == full
+
+
+def test_vmem_explicitly_built_graphs_are_tracked(native_build):
+    """a graph built with hipGraphAddKernelNode (no capture)
+    names a range that went cold; replaying it promotes that range like a
+    captured graph does.  Memset / memcpy nodes in a child graph, in-place
+    executable updates (hipGraphExecKernelNodeSetParams, hipGraphExecUpdate)
+    and alloc nodes (charged at launch) are tracked as well."""
+    o = run("vmem_graph_api", env={**BUDGET_ENV})
+    assert (o["alloc_a"], o["alloc_b"]) == ("0", "0")
+    assert o["b_gpu_after_a"] == "0"                      # B went cold and gave way to A
+    assert (o["add_kernel"], o["instantiate"], o["graph_ranges"]) == ("0", "0", "1")
+    assert o["b_gpu_after_replay"] == str(6 * GiB)       # the explicit graph's range came back
+    assert int(o["a_gpu_after_replay"]) <= 2 * GiB
+    assert (o["add_memset"], o["add_memcpy1d"], o["add_child"], o["add_alloc"]) == ("0",) * 4
+    assert o["child_ranges"] == "1" and o["launch_alloc"] == "0"
+    assert o["alloc_charged"] == str(GiB)                 # the alloc node's bytes, at launch
+    assert o["empty_ranges"] == "0"
+    assert o["exec_set_params"] == "0" and o["exec_ranges_after_set"] == "1"
+    assert o["exec_update"] == "0" and o["exec_ranges_after_update"] == "1"  # now runs g's parameters (B)
