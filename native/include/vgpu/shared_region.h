@@ -47,6 +47,9 @@ extern "C" {
 #define VGPU_HOSTPID_MONITOR 2    /* node monitor (hostPID) matched NSpid + cgroup (vgpu/monitor/pids.py) */
 #define VGPU_HOSTPID_HOST_NS 3    /* process runs in the host pid namespace */
 
+/* vgpu_device_cfg_t.flags */
+#define VGPU_DEV_FLAG_SUSPEND_EVICT 1u /* suspend (SIGUSR2) evicts the container's HBM (VGPU_SUSPEND_EVICT) */
+
 /* process slot status */
 #define VGPU_PROC_FREE 0
 #define VGPU_PROC_RUNNING 1
@@ -94,7 +97,7 @@ typedef struct vgpu_device_cfg {
    * monitor (hostPID view of KFD cu_occupancy), consumed by the temporal
    * limiter when the shim has no verified host pid of its own. */
   volatile uint32_t busy_permille;      /* 0..1000 of the device's CUs            */
-  uint32_t reserved1;
+  uint32_t flags;                       /* VGPU_DEV_FLAG_*                          */
   volatile uint64_t busy_ns;            /* CLOCK_MONOTONIC of the sample; 0 = none */
 } vgpu_device_cfg_t;
 

@@ -54,6 +54,7 @@ DeviceLimits limits_from_env() {
   L.num_devices = maxdev + 1;
   if (L.num_devices == 0 && (dflt_mem || dflt_cu)) L.num_devices = VGPU_MAX_DEVICES;
   L.oversubscribe = env_bool(env_first("VGPU_OVERSUBSCRIBE", "CUDA_OVERSUBSCRIBE"), false);
+  L.suspend_evict = env_bool(env_first("VGPU_SUSPEND_EVICT"), false);
   const char* p = env_first("VGPU_TASK_PRIORITY", "CUDA_TASK_PRIORITY");
   L.priority = p ? atoi(p) : 1;
   const char* pol = env_first("GPU_CORE_UTILIZATION_POLICY");
@@ -81,6 +82,7 @@ static void write_limits(vgpu_shared_region_t* r, const DeviceLimits& L) {
     vgpu_device_cfg_t& d = r->dev[i];
     d.mem_limit = L.mem_limit[i];
     d.mem_physical = L.mem_physical[i];
+    d.flags = L.suspend_evict ? (d.flags | VGPU_DEV_FLAG_SUSPEND_EVICT) : (d.flags & ~VGPU_DEV_FLAG_SUSPEND_EVICT);
     d.cu_limit = L.cu_limit[i];
     memcpy(d.cu_mask, L.cu_mask[i], sizeof(d.cu_mask));
     if (L.uuid[i][0]) memcpy(d.uuid, L.uuid[i], VGPU_UUID_LEN);

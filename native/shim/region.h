@@ -22,6 +22,7 @@ struct DeviceLimits {
   uint64_t cu_mask[VGPU_MAX_DEVICES][VGPU_CU_MASK_WORDS] = {};
   char uuid[VGPU_MAX_DEVICES][VGPU_UUID_LEN] = {};
   int oversubscribe = 0;
+  int suspend_evict = 0;  // VGPU_SUSPEND_EVICT: managed ranges so a suspend can evict HBM
   int priority = 1;
   int core_policy = 0;  // 0 default, 1 force, 2 disable
 };

@@ -108,6 +108,10 @@ struct Knobs {
   uint64_t cold_ticks = 40;  // unused for two seconds -> may be demoted
   uint64_t piece = 1ull << 30;
   int64_t managed_min = 32ll << 20;  // with a physical budget: allocations this large are managed ranges
+  // VGPU_SUSPEND_EVICT (device plugin --suspend-evict): managed ranges without a
+  // budget or oversubscription, resident like hipMalloc memory, so a suspend
+  // (SIGUSR2) can give the container's HBM back.
+  bool suspend_evict = false;
 };
 
 const Knobs& knobs() {
@@ -120,6 +124,7 @@ const Knobs& knobs() {
     if (const char* e = env_first("VGPU_VMEM_COLD_MS"))
       v.cold_ticks = std::max<uint64_t>(1, strtoull(e, nullptr, 10) / v.tick_ms);
     if (const char* e = env_first("VGPU_VMEM_PIECE_MB")) v.piece = std::max<uint64_t>(2, strtoull(e, nullptr, 10)) << 20;
+    v.suspend_evict = env_bool(env_first("VGPU_SUSPEND_EVICT"), false);
     if (const char* e = env_first("VGPU_VMEM_MANAGED_MIN_MB")) {
       const long long mb = atoll(e);
       v.managed_min = mb < 0 ? -1 : (int64_t)mb << 20;
@@ -497,13 +502,13 @@ bool vmem_wants_managed(int dev, uint64_t size) {
   const Knobs& k = knobs();
   // Not while a graph capture is open: hipMemAdvise would be an unsafe call in
   // a global-mode capture.  Those (activation) buffers take the plain path.
-  return vmem_enabled() && k.managed_min >= 0 && (uint64_t)k.managed_min <= size && phys_budget(dev) > 0 &&
-         g_open_captures.load(std::memory_order_acquire) == 0;
+  return vmem_enabled() && k.managed_min >= 0 && (uint64_t)k.managed_min <= size &&
+         (phys_budget(dev) > 0 || k.suspend_evict) && g_open_captures.load(std::memory_order_acquire) == 0;
 }
 
 bool vmem_enabled() {
   State& s = st();
-  return s.enabled && s.region && s.region->oversubscribe && knobs().on;
+  return s.enabled && s.region && (s.region->oversubscribe || knobs().suspend_evict) && knobs().on;
 }
 
 namespace {

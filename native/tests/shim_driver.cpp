@@ -448,6 +448,65 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (sc == "idle") {
+    // A live process of the container that does nothing for `secs` (the
+    // monitor's feedback tests signal it); prints the suspend / resume it saw.
+    double secs = argc > 2 ? atof(argv[2]) : 2.0;
+    void* p = nullptr;
+    hipMalloc(&p, 1 << 20);  // initialises the shim: slot claimed, signal handlers installed
+    auto self_region = sym<void* (*)()>("vgpu_self_region");
+    auto self_slot = sym<int (*)()>("vgpu_self_slot");
+    auto* r = (vgpu_shared_region_t*)self_region();
+    printf("slot=%d\n", self_slot());
+    fflush(stdout);
+    int saw_suspend = 0, saw_resume = 0, prev = VGPU_PROC_RUNNING;
+    for (double t = 0; t < secs; t += 0.01) {
+      const int stt = __atomic_load_n(&r->procs[self_slot()].status, __ATOMIC_RELAXED);
+      if (stt == VGPU_PROC_SUSPENDED && prev != VGPU_PROC_SUSPENDED) ++saw_suspend;
+      if (stt == VGPU_PROC_RUNNING && prev == VGPU_PROC_SUSPENDED) ++saw_resume;
+      prev = stt;
+      usleep(10000);
+    }
+    printf("saw_suspend=%d\nsaw_resume=%d\n", saw_suspend, saw_resume);
+    hipFree(p);
+    return 0;
+  }
+
+  if (sc == "suspend_evict") {
+    // VGPU_SUSPEND_EVICT without oversubscription or a budget: a large
+    // allocation is a resident managed range, a small one stays plain; a
+    // suspend (SIGUSR2, what the monitor sends a blocked low-priority pod)
+    // gives the HBM back, a resume (SIGUSR1) and a launch bring it back.
+    const size_t G = 1ull << 30;
+    auto gb = [&](void* p) { return (unsigned long long)fake_hip_managed_gpu_bytes(p); };
+    auto self_region = sym<void* (*)()>("vgpu_self_region");
+    auto self_slot = sym<int (*)()>("vgpu_self_slot");
+    auto slot_u = [&]() -> vgpu_dev_usage_t& {
+      return ((vgpu_shared_region_t*)self_region())->procs[self_slot()].used[dev];
+    };
+    void** ab = new void*[2]();
+    int ra = hipMalloc(&ab[0], 4 * G), rs = hipMalloc(&ab[1], 16ull << 20);
+    printf("alloc=%d\nsmall=%d\ngpu_at_alloc=%llu\nsmall_managed=%llu\nphys_at_alloc=%llu\n", ra, rs, gb(ab[0]),
+           gb(ab[1]), (unsigned long long)fake_hip_physical_used(dev));
+    raise(SIGUSR2);
+    for (int i = 0; i < 200 && gb(ab[0]); ++i) usleep(5000);
+    printf("suspended_gpu=%llu\nsuspended_phys=%llu\nsuspended_host=%llu\nsuspended_total=%llu\n", gb(ab[0]),
+           (unsigned long long)fake_hip_physical_used(dev), (unsigned long long)slot_u().host_bytes,
+           (unsigned long long)slot_u().total_bytes);
+    raise(SIGUSR1);
+    for (int t = 0; t < 100 && gb(ab[0]) < 4 * G; ++t) {
+      int n = 1;
+      void* q = (char*)ab[0] + 64;
+      void* args[] = {&n, &q};
+      hipLaunchKernel((const void*)0x1, dim3(64), dim3(256), args, 0, nullptr);
+      usleep(10000);
+    }
+    printf("resumed_gpu=%llu\nresumed_host=%llu\n", gb(ab[0]), (unsigned long long)slot_u().host_bytes);
+    hipFree(ab[1]);
+    hipFree(ab[0]);
+    return 0;
+  }
+
   if (sc == "vmem_copy2") {
     // The remaining copy / memset entry points on a resident managed range
     // (VERDICT r3 #4): 2-D host copies are staged (KFD never moves a page),

@@ -537,3 +537,15 @@ def test_oversubscribed_node_hands_out_physical_budgets(tmp_path):
         assert p.env["VGPU_DEVICE_MEMORY_PHYSICAL_0"] == f"{int(230000 / 1.8)}m"
     pods = admit_pods([PodSpec(cores=0, mem_mib=100000)], 0, str(tmp_path / "b"))
     assert "VGPU_DEVICE_MEMORY_PHYSICAL_0" not in pods[0].env and "VGPU_OVERSUBSCRIBE" not in pods[0].env
+
+
+def test_suspend_evict_flag_reaches_the_container(tmp_path):
+    """--suspend-evict (chart devicePlugin.suspendEvict) hands
+    every container VGPU_SUSPEND_EVICT, which the shim records in its region
+    so the monitor knows a suspend frees that container's HBM."""
+    from vgpu.bench.control import admit_pods
+    from vgpu.bench.launch import PodSpec
+    pods = admit_pods([PodSpec(cores=50, mem_mib=100000)], 0, str(tmp_path / "a"), suspend_evict=True)
+    assert pods[0].env["VGPU_SUSPEND_EVICT"] == "true"
+    pods = admit_pods([PodSpec(cores=50, mem_mib=100000)], 0, str(tmp_path / "b"))
+    assert "VGPU_SUSPEND_EVICT" not in pods[0].env

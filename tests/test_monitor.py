@@ -18,7 +18,7 @@ from vgpu.native import FAKES_DIR, shim_path
 GiB = 1 << 30
 
 
-def make_region(path, monkeypatch, uuid="GPU-0", limit="8g", prio=1, cu=0):
+def make_region(path, monkeypatch, uuid="GPU-0", limit="8g", prio=1, cu=0, evict=False):
     for k in list(os.environ):
         if k.startswith("VGPU_"):
             monkeypatch.delenv(k, raising=False)
@@ -27,6 +27,8 @@ def make_region(path, monkeypatch, uuid="GPU-0", limit="8g", prio=1, cu=0):
     monkeypatch.setenv("VGPU_TASK_PRIORITY", str(prio))
     if cu:
         monkeypatch.setenv("VGPU_DEVICE_CU_LIMIT_0", str(cu))
+    if evict:
+        monkeypatch.setenv("VGPU_SUSPEND_EVICT", "true")
     os.makedirs(os.path.dirname(path), exist_ok=True)
     return AttachedRegion(str(path), create=True)
 
@@ -243,3 +245,50 @@ def test_monitor_resolves_ambiguous_host_pids_then_purges(native_build, tmp_path
     live[1].kill()
     live[1].wait()
     r.close()
+
+
+def test_feedback_evicting_suspend_with_hysteresis(native_build, tmp_path, monkeypatch):
+    """a low-priority container that opted into suspend-with-
+    eviction (VGPU_SUSPEND_EVICT) and stays blocked by a high-priority task
+    for SUSPEND_AFTER observations gets SIGUSR2 (its shim then moves its
+    managed ranges to host memory); once unblocked it gets SIGUSR1.  A
+    container without the opt-in is only blocked, never signalled."""
+    from vgpu.monitor import feedback
+    monkeypatch.setattr(feedback, "SIGNAL_HOST_NS", False)
+    hi = make_region(tmp_path / "hi" / "vgpu.cache", monkeypatch, prio=0)
+    lo_path = tmp_path / "lo" / "vgpu.cache"
+    lo = make_region(lo_path, monkeypatch, prio=1, evict=True)
+    plain_path = tmp_path / "pl" / "vgpu.cache"
+    plain = make_region(plain_path, monkeypatch, prio=1)
+    assert lo.suspend_evict and not plain.suspend_evict and not hi.suspend_evict
+    env = {k: v for k, v in os.environ.items() if not k.startswith(("VGPU_", "CUDA_", "HIP_"))}
+    env.update(LD_LIBRARY_PATH=str(FAKES_DIR), LD_PRELOAD=str(shim_path()), VGPU_DEVICE_MEMORY_LIMIT_0="8g",
+               VGPU_DEVICE_UUID_0="GPU-0", VGPU_TASK_PRIORITY="1")
+    procs = {}
+    for name, path, ev in (("lo", lo_path, "true"), ("pl", plain_path, "false")):
+        procs[name] = subprocess.Popen([str(FAKES_DIR / "shim_driver"), "idle", "4"],
+                                       env={**env, "VGPU_SHARED_REGION": str(path), "VGPU_SUSPEND_EVICT": ev},
+                                       stdout=subprocess.PIPE, text=True)
+    deadline = time.time() + 20
+    while time.time() < deadline and not (lo.live_slots() and plain.live_slots()):
+        time.sleep(0.05)
+    regions = {"hi": hi, "lo": lo, "pl": plain}
+    hi.set_recent_kernel(2)
+    observe(regions)                       # blocked once: not yet suspended
+    time.sleep(0.2)
+    assert not lo.suspended()
+    hi.set_recent_kernel(2)
+    observe(regions)                       # blocked twice: SIGUSR2
+    time.sleep(0.3)
+    assert lo.suspended() and not plain.suspended()
+    observe(regions)                       # high-priority task idle (decayed): still blocked this pass
+    observe(regions)
+    observe(regions)                       # unblocked: SIGUSR1
+    time.sleep(0.3)
+    assert not lo.suspended() and lo.recent_kernel >= 0
+    outs = {n: dict(l.split("=", 1) for l in p.communicate(timeout=30)[0].splitlines() if "=" in l)
+            for n, p in procs.items()}
+    assert outs["lo"]["saw_suspend"] == "1" and outs["lo"]["saw_resume"] == "1", outs
+    assert outs["pl"]["saw_suspend"] == "0", outs
+    for r in regions.values():
+        r.close()

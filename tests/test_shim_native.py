@@ -815,3 +815,20 @@ def test_vmem_explicitly_built_graphs_are_tracked(native_build):
     assert o["empty_ranges"] == "0"
     assert o["exec_set_params"] == "0" and o["exec_ranges_after_set"] == "1"
     assert o["exec_update"] == "0" and o["exec_ranges_after_update"] == "1"  # now runs g's parameters (B)
+
+
+def test_suspend_evict_frees_hbm_without_a_budget(native_build):
+    """VERDICT r3 #6 (reference libvgpu.so suspend_all / sig_swap_stub): with
+    VGPU_SUSPEND_EVICT (device plugin --suspend-evict) a normal, not
+    oversubscribed pod's large allocations are resident managed ranges; a
+    suspend moves them to host memory (its HBM is free for another pod), a
+    resume and the next use bring them back.  Small buffers stay plain."""
+    o = run("suspend_evict", env={"VGPU_FAKE_MEM": str(16 * GiB), "VGPU_DEVICE_MEMORY_LIMIT_0": "12g",
+                                  "VGPU_SUSPEND_EVICT": "true", "VGPU_VMEM_TICK_MS": "10",
+                                  "VGPU_VMEM_HEADROOM_MB": "256"})
+    assert (o["alloc"], o["small"]) == ("0", "0")
+    assert o["gpu_at_alloc"] == str(4 * GiB) and o["small_managed"] == "0"
+    assert int(o["phys_at_alloc"]) >= 4 * GiB
+    assert o["suspended_gpu"] == "0" and int(o["suspended_phys"]) < GiB
+    assert o["suspended_host"] == str(4 * GiB)
+    assert o["resumed_gpu"] == str(4 * GiB) and o["resumed_host"] == "0"

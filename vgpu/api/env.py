@@ -27,6 +27,9 @@ ENV_OVERSUBSCRIBE = "VGPU_OVERSUBSCRIBE"
 # Physical HBM budget of an oversubscribed container (MiB, "m" suffix): virtual
 # device memory keeps at most this much resident (native/shim/vmem.cpp).
 ENV_MEM_PHYSICAL = "VGPU_DEVICE_MEMORY_PHYSICAL_{i}"
+# Opt-in: allocations >= VGPU_VMEM_MANAGED_MIN_MB are managed ranges even without
+# oversubscription, so a suspended container's HBM can be evicted to host memory.
+ENV_SUSPEND_EVICT = "VGPU_SUSPEND_EVICT"
 ENV_PRIORITY = "VGPU_TASK_PRIORITY"
 ENV_CORE_POLICY = "GPU_CORE_UTILIZATION_POLICY"
 ENV_OOM_KILLER = "ACTIVE_OOM_KILLER"

@@ -69,7 +69,8 @@ def _host_path(value: str, mounts: list) -> str:
 
 def admit_pods(specs: list, device_index: int, workdir: str, *, policy: str = "temporal",
                max_mask_slots: int = 2, memory_scaling: float = 1.0,
-               device: Device | None = None, pool_concurrency: int = 0) -> list[AdmittedPod]:
+               device: Device | None = None, pool_concurrency: int = 0,
+               suspend_evict: bool = False) -> list[AdmittedPod]:
     """Admit `specs` (vgpu.bench.launch.PodSpec) onto one physical GPU."""
     init_default_devices()
     config.SCHEDULER = SchedulerConfig(gpu_scheduler_policy="binpack")
@@ -80,7 +81,7 @@ def admit_pods(specs: list, device_index: int, workdir: str, *, policy: str = "t
     cfg = DevicePluginConfig(node_name=NODE, device_split_count=max(10, len(specs)), config_file="",
                              host_lib_dir=str(host_lib), host_lock_dir=str(lock), cu_share=policy,
                              max_mask_slots=max_mask_slots, device_memory_scaling=memory_scaling,
-                             pool_concurrency=pool_concurrency)
+                             pool_concurrency=pool_concurrency, suspend_evict=suspend_evict)
     dev = device or Device(uuid=f"GPU-bench-{device_index}", index=device_index,
                            render_minor=128 + device_index, card=device_index)
     srv = FakeApiServer()

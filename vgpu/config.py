@@ -55,6 +55,11 @@ class DevicePluginConfig:
     disable_core_limit: bool = False
     hw_queues_per_vgpu: int = 1           # GPU_MAX_HW_QUEUES for fractional vGPUs (0 = runtime default)
     hsa_tools_intercept: bool = False     # also hand the shim ROCr's API table (HSA_TOOLS_LIB)
+    # Suspend that frees HBM on any node (VGPU_SUSPEND_EVICT): device allocations of
+    # >= 32 MiB become managed ranges the shim can move to host memory, so a pod the
+    # monitor suspends for a higher-priority one (SIGUSR2) gives its HBM back, and
+    # gets it again when resumed (native/shim/vmem.cpp, vgpu/monitor/feedback.py).
+    suspend_evict: bool = False
     partition_mode: str = ""             # SPX|DPX|QPX|CPX expected compute partition ("" = as found)
     # MIG-strategy analogue (vgpu/deviceplugin/partitions.py): none | single | mixed
     partition_strategy: str = "single"

@@ -26,7 +26,7 @@ from dataclasses import dataclass, field
 from vgpu.api import resources as R
 from vgpu.api.codec import decode_pod_devices, encode_pod_devices
 from vgpu.api.env import (ENV_CU_LIMIT, ENV_CU_MASK, ENV_CU_SHARE, ENV_CORE_POLICY, ENV_DISABLE_CONTROL, ENV_MEM_LIMIT,
-                          ENV_MEM_PHYSICAL, ENV_OVERSUBSCRIBE, ENV_SHARED_REGION, ENV_UUID, PRELOAD_FILE, SHIM_NAME,
+                          ENV_MEM_PHYSICAL, ENV_OVERSUBSCRIBE, ENV_SHARED_REGION, ENV_SUSPEND_EVICT, ENV_UUID, PRELOAD_FILE, SHIM_NAME,
                           format_mask)
 from vgpu.api.resources import ContainerDevice
 from vgpu.config import DevicePluginConfig
@@ -214,6 +214,8 @@ def build_container_grant(cfg: DevicePluginConfig, pod: dict, ctr_idx: int, devr
         g.envs["HSA_TOOLS_LIB"] = f"{CONTAINER_LIB_DIR}/{SHIM_NAME}"
     if cfg.device_memory_scaling > 1:
         g.envs[ENV_OVERSUBSCRIBE] = "true"
+    if cfg.suspend_evict:
+        g.envs[ENV_SUSPEND_EVICT] = "true"
     if cfg.disable_core_limit:
         g.envs[ENV_CORE_POLICY] = "disable"
     host_cache = f"{cfg.host_lib_dir}/containers/{key}"

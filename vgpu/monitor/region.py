@@ -21,6 +21,7 @@ CU_WORDS = 4
 MAGIC = 0x56475055
 VERSION = 4
 PROC_FREE, PROC_RUNNING, PROC_SUSPENDED = 0, 1, 2
+DEV_FLAG_SUSPEND_EVICT = 1  # shared_region.h VGPU_DEV_FLAG_SUSPEND_EVICT
 # slot.host_pid_src (how the host pid was obtained)
 HOSTPID_UNVERIFIED, HOSTPID_KFD_DIFF, HOSTPID_MONITOR, HOSTPID_HOST_NS = 0, 1, 2, 3
 
@@ -44,7 +45,7 @@ class DeviceCfg(ctypes.Structure):
     _fields_ = [("uuid", ctypes.c_char * UUID_LEN), ("mem_limit", ctypes.c_uint64),
                 ("mem_physical", ctypes.c_uint64), ("cu_limit", ctypes.c_uint32),
                 ("cu_total", ctypes.c_uint32), ("cu_mask", ctypes.c_uint64 * CU_WORDS),
-                ("busy_permille", ctypes.c_uint32), ("reserved1", ctypes.c_uint32), ("busy_ns", ctypes.c_uint64)]
+                ("busy_permille", ctypes.c_uint32), ("flags", ctypes.c_uint32), ("busy_ns", ctypes.c_uint64)]
 
 
 class Region(ctypes.Structure):
@@ -88,6 +89,7 @@ class DeviceView:
     swap_out: int
     busy_permille: int = 0   # fair-share GPU time of the last limiter window (shim-published)
     busy_ns: int = 0
+    flags: int = 0           # DEV_FLAG_*
 
 
 class AttachedRegion:
@@ -125,12 +127,22 @@ class AttachedRegion:
             out.append(DeviceView(i, d.uuid.decode(errors="replace"), d.mem_limit, d.cu_limit, mask,
                                   agg["total_bytes"], agg["host_bytes"], agg["context_bytes"],
                                   agg["module_bytes"], agg["buffer_bytes"], agg["swap_in_bytes"],
-                                  agg["swap_out_bytes"], d.busy_permille, d.busy_ns))
+                                  agg["swap_out_bytes"], d.busy_permille, d.busy_ns, d.flags))
         return out
 
     @property
     def priority(self) -> int:
         return self.r.priority
+
+    @property
+    def suspend_evict(self) -> bool:
+        """The container opted into suspend-with-eviction (VGPU_SUSPEND_EVICT)."""
+        n = self.r.num_devices if 0 < self.r.num_devices <= MAX_DEVICES else 0
+        return any(self.r.dev[i].flags & DEV_FLAG_SUSPEND_EVICT for i in range(n))
+
+    def suspended(self) -> bool:
+        """Any live process of the container is suspended (SIGUSR2)."""
+        return any(s.status == PROC_SUSPENDED for s in self.live_slots())
 
     @property
     def recent_kernel(self) -> int:
