@@ -212,6 +212,10 @@ __attribute__((visibility("default"))) void vgpu_self_gpu_time(int dev, uint64_t
   limiter_stats(dev, charged, busy);
 }
 
+__attribute__((visibility("default"))) void vgpu_self_share_state(int dev, int64_t out[8]) {
+  limiter_share_state(dev, out);
+}
+
 __attribute__((visibility("default"))) void vgpu_self_on_launch(int dev, uint64_t wg) {
   ensure_init();
   limiter_on_launch(dev, wg);

@@ -783,6 +783,34 @@ void limiter_track(int dev, hipStream_t stream, hipError_t launch_rc) {
 }
 
 // Fair-share GPU ns charged / wall ns busy so far on `dev` (tests, metrics).
+// What the compute-share policy of `dev` is doing (bench / tests):
+// out[0] auto phase of the GPU's share board (-1: not an auto member / no board),
+// out[1] busy members the board's decision was made for, out[2] 1 when the
+// board holds a decision for that member count, out[3] 1 while this process
+// runs on CUs of its own, out[4] CUs in the region's mask (0 = every CU),
+// out[5] 1 while the temporal limiter is active for the device, out[6] ns this
+// process has waited in the limiter, out[7] reserved.
+void limiter_share_state(int dev, int64_t out[8]) {
+  for (int i = 0; i < 8; ++i) out[i] = 0;
+  out[0] = -1;
+  if (dev < 0 || dev >= VGPU_MAX_DEVICES) return;
+  DevLimiter& L = g_lim[dev];
+  if (L.auto_share && L.board) {
+    vgpu_board_t* b = L.board;
+    out[0] = __atomic_load_n(&b->auto_phase, __ATOMIC_ACQUIRE);
+    const int n = __atomic_load_n(&b->auto_members, __ATOMIC_RELAXED);
+    out[1] = n;
+    out[2] = n > 0 && n < VGPU_AUTO_MEMO && __atomic_load_n(&b->auto_memo_ns[n], __ATOMIC_RELAXED) != 0;
+  }
+  out[3] = L.spatial;
+  State& s = st();
+  if (s.region)
+    for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w)
+      out[4] += __builtin_popcountll(__atomic_load_n(&s.region->dev[dev].cu_mask[w], __ATOMIC_RELAXED));
+  out[5] = L.active ? 1 : 0;
+  if (vgpu_proc_slot_t* sl = my_slot()) out[6] = (int64_t)__atomic_load_n(&sl->throttle_wait_ns, __ATOMIC_RELAXED);
+}
+
 void limiter_stats(int dev, uint64_t* charged, uint64_t* busy) {
   if (dev < 0 || dev >= VGPU_MAX_DEVICES) return;
   if (charged) *charged = g_lim[dev].charged_total.load();

@@ -116,6 +116,7 @@ void limiter_track(int dev, hipStream_t stream, hipError_t launch_rc);
 extern std::atomic<int> g_open_captures;
 extern std::shared_mutex g_capture_mu;  // writers: capture begin; readers: limiter-thread markers
 void limiter_stats(int dev, uint64_t* charged_ns, uint64_t* busy_ns);
+void limiter_share_state(int dev, int64_t out[8]);
 
 // Stream-ordered pools, graph memory and pinned host memory (pools.cpp).
 hipError_t pool_alloc_async(void** ptr, size_t size, hipStream_t stream, hipMemPool_t pool,

@@ -17,6 +17,8 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include <thread>
+#include <vector>
 
 #include <amd_smi/amdsmi.h>
 #include <hsa/hsa.h>
@@ -445,6 +447,73 @@ int main(int argc, char** argv) {
            (unsigned long long)fake_hip_managed_gpu_bytes(ab[2]));
     printf("ipc_managed=%d\nipc_managed_offset=%d\nipc_fine=%d\n", im, imo, ifg);
     for (int i = 0; i < 3; ++i) hipFree(ab[i]);
+    return 0;
+  }
+
+  if (sc == "multidev") {
+    // One container holding every visible device (a multi-GPU pod, VERDICT r3
+    // #5): per-device caps and limiter share boards, device switches per
+    // thread, IPC between two of its devices charged to the exporter only.
+    int n = 0;
+    hipGetDeviceCount(&n);
+    printf("devices=%d\n", n);
+    auto usage = sym<uint64_t (*)(int, int)>("vgpu_self_usage");
+    auto imported = sym<int64_t (*)(int)>("vgpu_self_ipc_imported");
+    std::vector<std::vector<void*>> held(n);
+    for (int d = 0; d < n; ++d) {
+      hipSetDevice(d);
+      size_t f = 0, t = 0;
+      hipMemGetInfo(&f, &t);
+      int k = 0;
+      for (; k < 64; ++k) {
+        void* p = nullptr;
+        if (hipMalloc(&p, 1ull << 30) != hipSuccess) break;
+        held[d].push_back(p);
+      }
+      int dcur = -1;
+      hipGetDevice(&dcur);
+      hipLaunchKernel((const void*)0x1, dim3(64), dim3(256), nullptr, 0, nullptr);  // joins the device's board
+      printf("dev%d_total=%zu\ndev%d_blocks=%d\ndev%d_current=%d\ndev%d_charged=%llu\n", d, t, d, k, d, dcur, d,
+             (unsigned long long)usage(d, 2));
+    }
+    hipDeviceSynchronize();
+    for (int d = 0; d < n; ++d) {
+      hipSetDevice(d);
+      for (void* p : held[d]) hipFree(p);
+      printf("dev%d_after_free=%llu\n", d, (unsigned long long)usage(d, 2));
+    }
+    hipSetDevice(n - 1);
+    // another thread has its own current device
+    int other = -1;
+    std::thread th([&] {
+      hipSetDevice(n > 1 ? 1 : 0);
+      void* p = nullptr;
+      if (hipMalloc(&p, 1 << 20) == hipSuccess) hipFree(p);
+      hipGetDevice(&other);
+    });
+    th.join();
+    int mine = -1;
+    hipGetDevice(&mine);
+    printf("thread_device=%d\nmain_device=%d\n", other, mine);
+    // IPC between two devices of the container (a DDP peer in one process)
+    if (n >= 6) {
+      hipSetDevice(3);
+      void* src = nullptr;
+      hipMalloc(&src, 256ull << 20);
+      hipIpcMemHandle_t h;
+      hipIpcGetMemHandle(&h, src);
+      hipSetDevice(5);
+      const uint64_t before5 = usage(5, 2);
+      void* q = nullptr;
+      int ro = hipIpcOpenMemHandle(&q, h, hipIpcMemLazyEnablePeerAccess);
+      printf("ipc_open=%d\nipc_imported_dev5=%lld\nipc_charged_dev5=%llu\nipc_exporter_dev3=%llu\n", ro,
+             (long long)imported(5), (unsigned long long)(usage(5, 2) - before5),
+             (unsigned long long)usage(3, 2));
+      hipIpcCloseMemHandle(q);
+      printf("ipc_imported_after_close=%lld\n", (long long)imported(5));
+      hipSetDevice(3);
+      hipFree(src);
+    }
     return 0;
   }
 

@@ -132,3 +132,30 @@ def test_bench_two_ranks_torchrun_on_the_gpu(gpu_build):
     assert d["n_gpus"] == 2 and d["value"] > 0 and len(d["placement"]) == 2
     assert sorted(x["rank"] for x in d["placement"]) == [0, 1]
     assert all(x["device"] == "0" for x in d["placement"])
+
+
+def test_pod_gpus_eight_rank_ddp_rehearsal_cpu():
+    """`bench.py --pod-gpus 8` admits ONE pod asking for 8 vGPUs
+    through the control plane (webhook, scheduler, Allocate: one cap / share
+    per device) and runs DDP with one rank per device inside it; here the
+    orchestration is rehearsed on CPU (gloo).  The replicas must agree after
+    the all-reduced updates."""
+    env = dict(os.environ)
+    env.pop("HIP_VISIBLE_DEVICES", None)
+    r = subprocess.run([sys.executable, "bench.py", "--pod-gpus", "8", "--cpu-smoke", "--steps", "2",
+                        "--warmup", "1"], cwd=REPO, capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 8 and d["config"]["parallelism"] == "ddp8 inside one vGPU pod"
+    assert d["config"]["backend"] == "gloo" and d["replicas_agree"] is True and d["value"] > 0
+
+
+def test_rccl_transport_parser():
+    sys.path.insert(0, REPO)
+    from bench import rccl_transports
+    text = ("host:1:2 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[1] via P2P/IPC\n"
+            "host:1:2 [1] NCCL INFO Channel 01/0 : 1[1] -> 0[0] via P2P/direct pointer\n"
+            "host:1:2 [0] NCCL INFO Channel 02/0 : 0[0] -> 1[1] via SHM/direct/direct\n"
+            "unrelated line\n")
+    t = rccl_transports(text)
+    assert t == {"0->1": ["P2P/IPC", "SHM/direct/direct"], "1->0": ["P2P/direct"]}

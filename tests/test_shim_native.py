@@ -832,3 +832,28 @@ def test_suspend_evict_frees_hbm_without_a_budget(native_build):
     assert o["suspended_gpu"] == "0" and int(o["suspended_phys"]) < GiB
     assert o["suspended_host"] == str(4 * GiB)
     assert o["resumed_gpu"] == str(4 * GiB) and o["resumed_host"] == "0"
+
+
+def test_multi_gpu_container_per_device_caps_boards_and_ipc(native_build, tmp_path):
+    """one container granted 8 devices (a multi-GPU pod): each
+    device keeps its own cap and its own fair-share board (keyed by its uuid),
+    hipSetDevice is per thread, and an IPC mapping between two of the
+    container's devices is charged to the exporting device only."""
+    env = {"VGPU_FAKE_GPUS": "8", "VGPU_CU_SHARE": "temporal", "VGPU_CU_MASK_FROM_LIMIT": "false",
+           "VGPU_LOCK_DIR": str(tmp_path), "VGPU_SHARED_REGION": str(tmp_path / "r.cache")}
+    for i in range(8):
+        env[f"VGPU_DEVICE_MEMORY_LIMIT_{i}"] = f"{i + 1}g"
+        env[f"VGPU_DEVICE_UUID_{i}"] = f"GPU-md-{i}"
+        env[f"VGPU_DEVICE_CU_LIMIT_{i}"] = "50"
+    o = run("multidev", env=env)
+    assert o["devices"] == "8"
+    for i in range(8):
+        assert int(o[f"dev{i}_total"]) == (i + 1) * GiB           # hipMemGetInfo: that device's cap
+        assert o[f"dev{i}_blocks"] == str(i + 1)                    # refused exactly past it
+        assert o[f"dev{i}_current"] == str(i)
+        assert int(o[f"dev{i}_charged"]) == (i + 1) * GiB and o[f"dev{i}_after_free"] == "0"
+        assert (tmp_path / f"GPU-md-{i}.v4.board").exists()        # one share board per device
+    assert o["thread_device"] == "1" and o["main_device"] == "7"
+    assert o["ipc_open"] == "0" and int(o["ipc_imported_dev5"]) == 256 << 20
+    assert o["ipc_charged_dev5"] == "0" and int(o["ipc_exporter_dev3"]) == 256 << 20
+    assert o["ipc_imported_after_close"] == "0"

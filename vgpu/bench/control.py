@@ -46,8 +46,9 @@ class AdmittedPod:
     share: str = "none"                           # mask | temporal | none
 
 
-def _pod(name: str, mem_mib: int, cores: int, priority: int | None, cu_share: str | None = None) -> dict:
-    lim = {R.RESOURCE_COUNT: "1"}
+def _pod(name: str, mem_mib: int, cores: int, priority: int | None, cu_share: str | None = None,
+         count: int = 1) -> dict:
+    lim = {R.RESOURCE_COUNT: str(count)}
     if mem_mib:
         lim[R.RESOURCE_MEM] = str(mem_mib)
     if cores:
@@ -122,6 +123,57 @@ def admit_pods(specs: list, device_index: int, workdir: str, *, policy: str = "t
         srv.stop()
 
 
+def admit_multi_gpu_pod(device_indices: list[int], workdir: str, *, mem_mib: int = 0, cores: int = 0,
+                        policy: str = "auto", suspend_evict: bool = False) -> AdmittedPod:
+    """Admit ONE pod that asks for `len(device_indices)` vGPUs (amd.com/gpu: N)
+    on a node whose devices are those physical GPUs: webhook, scheduler
+    filter/bind (one device per requested vGPU), Allocate.  The returned env
+    holds one cap / compute share / uuid per device (VGPU_*_<i>, i = the
+    device's position inside the container) and one shared region."""
+    init_default_devices()
+    config.SCHEDULER = SchedulerConfig(gpu_scheduler_policy="binpack")
+    work = Path(workdir)
+    host_lib = work / "host"
+    lock = work / "vgpulock"
+    lock.mkdir(parents=True, exist_ok=True)
+    n = len(device_indices)
+    cfg = DevicePluginConfig(node_name=NODE, device_split_count=10, config_file="", host_lib_dir=str(host_lib),
+                             host_lock_dir=str(lock), cu_share=policy, suspend_evict=suspend_evict)
+    devs = [Device(uuid=f"GPU-bench-{d}", index=d, render_minor=128 + d, card=d, numa=0, xgmi_hive=0x1111)
+            for d in device_indices]
+    srv = FakeApiServer()
+    url = srv.start()
+    try:
+        client = KubeClient(url)
+        srv.add_node(NODE)
+        register_once(client, NODE, devs, cfg)
+        sched = Scheduler(client)
+        sched.register_from_node_annotations_once()
+        cu_state = CUMaskState(str(host_lib / "containers"), policy=policy)
+        name = "ddp"
+        pod = _pod(name, mem_mib, cores, None, count=n)
+        review = handle_admission({"request": {"uid": name, "object": pod}})
+        if not review["response"]["allowed"]:
+            raise RuntimeError(f"webhook refused {name}: {review}")
+        srv.add_pod(pod)
+        r = sched.filter({"pod": client.get_pod("bench", name), "nodenames": [NODE]})
+        if r.get("nodenames") != [NODE]:
+            raise RuntimeError(f"scheduler could not place the {n}-GPU pod: {r}")
+        b = sched.bind({"podName": name, "podNamespace": "bench", "podUID": f"uid-{name}", "node": NODE})
+        if b.get("error"):
+            raise RuntimeError(f"bind {name}: {b['error']}")
+        ids = [f"{d.uuid}-0" for d in devs]
+        grant = allocate(client, cfg, R.VENDOR, [ids], {d.uuid: d for d in devs}, cu_state, NODE)[0]
+        env = {k: _host_path(v, grant.mounts) for k, v in grant.envs.items()}
+        env["VGPU_LOCK_DIR"] = str(lock)
+        region = Path(env.get("VGPU_SHARED_REGION", str(work / name / "vgpu.cache")))
+        region.parent.mkdir(parents=True, exist_ok=True)
+        share = env.get("VGPU_CU_SHARE", "none")
+        return AdmittedPod(name, env, grant, 0, share)
+    finally:
+        srv.stop()
+
+
 def container_visible_env(device_index: int) -> dict:
     """Device selection for a host process standing in for the container (the
     container would only see its own render node)."""
@@ -138,7 +190,7 @@ def apply_env(base: dict, env: dict) -> dict:
     return out
 
 
-__all__ = ["admit_pods", "AdmittedPod", "apply_env", "container_visible_env", "NODE"]
+__all__ = ["admit_pods", "admit_multi_gpu_pod", "AdmittedPod", "apply_env", "container_visible_env", "NODE"]
 
 if __name__ == "__main__":  # pragma: no cover - manual inspection
     import json

@@ -91,7 +91,8 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
                 workdir: str | None = None, oversubscribe: bool = False,
                 hw_queues: int | None = None, fused: bool = True,
                 conv: str = "native", cu_share: str = "temporal", memory_scaling: float = 1.0,
-                pool_concurrency: int = 0, seconds: float = 0.0, warmup_seconds: float = 0.0) -> list[Pod]:
+                pool_concurrency: int = 0, seconds: float = 0.0, warmup_seconds: float = 0.0,
+                decide_timeout: float = 0.0) -> list[Pod]:
     """Start one process per pod on physical device `device`.
 
     cu_share: how a fractional pod's compute share is enforced.
@@ -177,6 +178,8 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
             cmd += ["--seconds", str(seconds)]
         if warmup_seconds > 0:
             cmd += ["--warmup-seconds", str(warmup_seconds)]
+        if decide_timeout > 0:
+            cmd += ["--decide-timeout", str(decide_timeout), "--share-members", str(len(specs))]
         proc = subprocess.Popen(cmd, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                 text=True, bufsize=1, cwd=str(REPO))
         pod = Pod(i, proc, cenv.get("VGPU_SHARED_REGION", ""), {k: v for k, v in cenv.items()})

@@ -171,6 +171,27 @@ def split_replay(model, x, split: int):
     return replay
 
 
+_PHASES = {-1: None, 0: "temporal", 1: "exploring", 2: "exploring", 3: "spatial", 4: "exploring"}
+
+
+def share_state(dev: int = 0) -> dict | None:
+    """The enforcement library's compute-share state in this process
+    (limiter.cpp limiter_share_state): the auto policy's phase and whether it
+    has decided for the current busy-member count, this pod's CUs and its
+    limiter wait.  None when the library is not loaded."""
+    import ctypes
+    try:
+        fn = ctypes.CDLL(None).vgpu_self_share_state
+    except (OSError, AttributeError):
+        return None
+    out = (ctypes.c_int64 * 8)()
+    fn(ctypes.c_int(dev), out)
+    phase = _PHASES.get(int(out[0]), "exploring")
+    return {"policy": "spatial" if out[3] else phase, "auto_phase": phase, "members": int(out[1]),
+            "decided": bool(out[2]) and phase in ("temporal", "spatial"), "own_cus": bool(out[3]),
+            "cus": int(out[4]), "limiter_active": bool(out[5]), "limiter_wait_ms": round(out[6] / 1e6, 3)}
+
+
 def cap_probe() -> dict:
     import torch
     free, total = torch.cuda.mem_get_info()
@@ -209,6 +230,11 @@ def main(argv=None) -> int:
                     help="keep warming up until this long has passed (lets the adaptive share policy settle)")
     ap.add_argument("--seconds", type=float, default=0.0,
                     help="run steps for this long instead of exactly --steps (share measurements)")
+    ap.add_argument("--decide-timeout", type=float, default=0.0,
+                    help="under the adaptive share policy, keep warming up (untimed) until the GPU's "
+                         "pods have decided between time sharing and CUs of their own, at most this long")
+    ap.add_argument("--share-members", type=int, default=1,
+                    help="pods that share this GPU and run at once (the decision --decide-timeout waits for)")
     args = ap.parse_args(argv)
 
     import torch
@@ -235,6 +261,23 @@ def main(argv=None) -> int:
         step()
         sync()
     sync()
+    # The adaptive policy (VGPU_CU_SHARE=auto) A/Bs time sharing against CU
+    # claims over ~5 s of the pods' own work (limiter.cpp auto_step); a timed
+    # window that starts before the decision measures the A/B, not the policy.
+    decide = {"waited_s": 0.0}
+    if not cpu and args.decide_timeout > 0 and os.environ.get("VGPU_CU_SHARE", "") == "auto":
+        t_d = time.monotonic()
+        while time.monotonic() - t_d < args.decide_timeout:
+            st = share_state()
+            if st is None or not st["limiter_active"] and not st["own_cus"] and st["auto_phase"] is None:
+                break  # not an auto member (whole GPU, or no library)
+            if st["members"] == args.share_members and (st["decided"] or args.share_members < 2):
+                break  # decided for all of this GPU's pods busy at once (a lone pod has nothing to decide)
+            for _ in range(4):
+                step()
+            sync()
+        decide["waited_s"] = round(time.monotonic() - t_d, 2)
+        decide["state"] = share_state()
     if cpu:
         emit("READY", {"pod": args.pod_index, "init_s": time.time() - t_init, "pid": os.getpid()})
     else:
@@ -243,7 +286,7 @@ def main(argv=None) -> int:
         emit("READY", {"pod": args.pod_index, "init_s": time.time() - t_init, "mem_free": free,
                        "mem_total": total, "prop_total": props.total_memory,
                        "cus": props.multi_processor_count, "pid": os.getpid(),
-                       "allocated": torch.cuda.memory_allocated()})
+                       "allocated": torch.cuda.memory_allocated(), "decide": decide})
     if not args.no_wait:
         line = sys.stdin.readline()
         if line.strip() != "GO":
@@ -266,6 +309,8 @@ def main(argv=None) -> int:
     res = {"pod": args.pod_index, "t0": t0, "t1": t1, "steps": steps,
            "samples": steps * w.batch, "ms_per_step": 1e3 * (t1 - t0) / max(steps, 1),
            "throughput": steps * w.batch / max(t1 - t0, 1e-9)}
+    if not cpu:
+        res["share"] = share_state()  # the policy the timed window ran under
     if args.cap_probe and not cpu:
         res.update(cap_probe())
     emit("DONE", res)
@@ -282,15 +327,21 @@ def main(argv=None) -> int:
 
 def rccl_check(rank: int, world: int, addr: str, port: int, cpu: bool, mib: int = 64, iters: int = 10) -> dict:
     """The multi-GPU data plane under the enforcement library: one pod per GPU
-    forms a process group over RCCL (xGMI peer access and IPC buffers pass
-    through the shim; RCCL kernels are exempt from its limiter) and
-    all-reduces a `mib` MiB buffer.  Checks the sum and reports bus bandwidth.
-    Not part of the timed window."""
+    forms a process group over RCCL (RCCL kernels are exempt from the shim's
+    limiter) and all-reduces a `mib` MiB buffer.  Checks the sum, reports bus
+    bandwidth and the transport RCCL chose per peer (NCCL_DEBUG=INFO): a pod
+    sees only its own GPU, so expect SHM, not P2P/xGMI (that path is
+    bench.py --pod-gpus).  Not part of the timed window."""
     import datetime
 
     import torch
     import torch.distributed as dist
     out = {"rank": rank, "world": world, "backend": "gloo" if cpu else "nccl"}
+    dbg = f"/tmp/vgpu-rccl-{os.getpid()}.log"
+    if not cpu:
+        os.environ.setdefault("NCCL_DEBUG", "INFO")
+        os.environ.setdefault("NCCL_DEBUG_SUBSYS", "INIT,GRAPH")
+        os.environ["NCCL_DEBUG_FILE"] = dbg
     t0 = time.time()
     try:
         dev = torch.device("cpu") if cpu else torch.device("cuda", 0)
@@ -317,6 +368,10 @@ def rccl_check(rank: int, world: int, addr: str, port: int, cpu: bool, mib: int 
         out["ms_per_allreduce"] = round(1e3 * dt, 3)
         out["busbw_GBps"] = round(2 * (world - 1) / world * n * 4 / dt / 1e9, 1)
         dist.destroy_process_group()
+        if not cpu and os.path.exists(dbg):
+            sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[2]))
+            from bench import rccl_transports
+            out["transport"] = rccl_transports(open(dbg, errors="replace").read())
     except Exception as e:  # reported, never fatal for the benchmark
         out["error"] = f"{type(e).__name__}: {e}"[:500]
     return out
