@@ -31,6 +31,9 @@
 #include <map>
 #include <set>
 #include <mutex>
+#include <string>
+#include <sys/stat.h>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -174,6 +177,39 @@ hsa_status_t first_pool(hsa_amd_memory_pool_t p, void* data) {
 
 void kfd_publish(int dev);
 
+// Fake KFD cu_occupancy (VGPU_FAKE_KFD_OCC with VGPU_KFD_PROC_DIR and
+// VGPU_FAKE_HOST_PID): a thread keeps <dir>/<host pid>/stats_<gpu id>/cu_occupancy
+// at 64 while this process's timeline has work in flight, else 0.
+void occ_thread_start(int ndev) {
+  const char* on = getenv("VGPU_FAKE_KFD_OCC");
+  const char* dir = getenv("VGPU_KFD_PROC_DIR");
+  const char* hp = getenv("VGPU_FAKE_HOST_PID");
+  if (!on || !dir || !hp) return;
+  std::string base = std::string(dir) + "/" + hp;
+  std::thread([base, ndev] {
+    std::vector<std::string> files;
+    for (int d = 0; d < ndev; ++d) {
+      const std::string sd = base + "/stats_" + std::to_string(1000 + d);
+      mkdir(base.c_str(), 0755);
+      mkdir(sd.c_str(), 0755);
+      files.push_back(sd + "/cu_occupancy");
+    }
+    int last = -1;
+    for (;;) {
+      const int v = timeline_last_end() > now_ns() ? 64 : 0;
+      if (v != last) {
+        for (auto& f : files)
+          if (FILE* fp = fopen(f.c_str(), "w")) {
+            fprintf(fp, "%d\n", v);
+            fclose(fp);
+          }
+        last = v;
+      }
+      usleep(200);
+    }
+  }).detach();
+}
+
 void init_locked() {
   if (g_inited) return;
   g_inited = true;
@@ -184,6 +220,7 @@ void init_locked() {
   const char* ra = getenv("VGPU_FAKE_RUNTIME_ALLOC");
   uint64_t runtime_alloc = ra ? strtoull(ra, nullptr, 10) : 0;
   g_devs.assign(n, Dev{});
+  occ_thread_start(n);
   std::vector<hsa_agent_t> gpus;
   hsa_iterate_agents(pick_gpu, &gpus);
   for (int i = 0; i < n; ++i) {
@@ -279,9 +316,13 @@ hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) {
   return hipSuccess;
 }
 hipError_t hipEventCreate(hipEvent_t* e) { return hipEventCreateWithFlags(e, 0); }
+// VGPU_FAKE_EARLY_EVENTS=f: an event completes once a fraction f of the work
+// queued before it has run (a profiler that rewrites completion signals).
 hipError_t hipEventRecord(hipEvent_t e, hipStream_t stream) {
   if (!e) return hipErrorInvalidHandle;
-  reinterpret_cast<FakeEvent*>(e)->at = timeline_last_end();
+  static const double early = getenv("VGPU_FAKE_EARLY_EVENTS") ? atof(getenv("VGPU_FAKE_EARLY_EVENTS")) : 1.0;
+  const uint64_t end = timeline_last_end(), now = now_ns();
+  reinterpret_cast<FakeEvent*>(e)->at = end > now && early < 1.0 ? now + (uint64_t)(early * (end - now)) : end;
   reinterpret_cast<FakeEvent*>(e)->stream = stream;
   return hipSuccess;
 }

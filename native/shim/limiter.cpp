@@ -33,6 +33,7 @@
 // graph replay as for a stream of tiny kernels, needs no host-PID mapping,
 // and converges on hardware without calibration.
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <math.h>
 #include <strings.h>
 #include <sys/stat.h>
@@ -117,6 +118,18 @@ struct DevLimiter {
   bool auto_joined = false;
   bool pool0_saved = false;
   uint64_t pool0[VGPU_CU_MASK_WORDS] = {};  // the plugin's pool mask (all-zero = every CU)
+  // Marker-independent busy check: KFD's cu_occupancy of this
+  // process on the device, sampled every occ_period_ns.  A sample with waves on
+  // the CUs counts the time since the previous sample as busy; every window the
+  // busy time the samples saw beyond what the markers charged is charged too, so
+  // work whose markers complete early (a profiler rewriting completion signals:
+  // 3.4 x the share under rocprofv3, profiles/r3/temporal) still pays.
+  int occ_fd = -2;                 // -2 not opened yet, -1 unavailable
+  uint64_t occ_next_try_ns = 0;
+  uint64_t occ_last_ns = 0, occ_window_start = 0;
+  uint64_t occ_busy_acc = 0;       // busy wall the samples saw in this window
+  uint64_t occ_mark_acc = 0;       // wall the markers charged in this window
+  std::atomic<uint64_t> occ_extra_total{0};  // charged on the occupancy evidence alone
   // What this process last saw or wrote in the region's mask: anything else
   // found there was written by the device plugin (a masked container arrived
   // or left and the pool was reshaped, custate.py _reshape_pool) and becomes
@@ -351,6 +364,7 @@ bool reap(int dev, DevLimiter& L, uint64_t now_hint) {
   L.ema_charge.store(old ? (old * 3 + per) / 4 : per, std::memory_order_relaxed);
   L.win_charge += charge;
   L.win_busy += wall;
+  L.occ_mark_acc += wall;
   L.charged_total.fetch_add(charge, std::memory_order_relaxed);
   L.busy_total.fetch_add(wall, std::memory_order_relaxed);
   trace_emit(VGPU_EV_GPU_TIME, dev, charge, wall);
@@ -490,6 +504,75 @@ void auto_step() {
   }
 }
 
+// ---- occupancy cross-check -------------------------------------------------------------
+uint64_t occ_period_ns() {
+  static const uint64_t p = (uint64_t)(1e3 * (env_first("VGPU_LIMITER_OCC_US") ? atof(env_first("VGPU_LIMITER_OCC_US"))
+                                                                                  : 2000.0));
+  return p;  // 0 disables the check
+}
+
+int occ_open(int dev, DevLimiter& L, uint64_t now) {
+  if (L.occ_fd != -2 && L.occ_fd != -1) return L.occ_fd;
+  if (L.occ_fd == -1 && now < L.occ_next_try_ns) return -1;
+  L.occ_next_try_ns = now + 500000000ull;  // host pid / KFD entry may appear later: look again in 0.5 s
+  L.occ_fd = -1;
+  int src = 0;
+  int pid = self_host_pid(&src);
+  if (src == VGPU_HOSTPID_UNVERIFIED) {
+    vgpu_proc_slot_t* sl = my_slot();
+    if (!sl || __atomic_load_n(&sl->host_pid_src, __ATOMIC_ACQUIRE) == VGPU_HOSTPID_UNVERIFIED) return -1;
+    pid = __atomic_load_n(&sl->host_pid, __ATOMIC_RELAXED);
+  }
+  const uint32_t uid = cumask_driver_uid(dev);
+  if (pid <= 0 || !uid) return -1;
+  char path[512];
+  snprintf(path, sizeof path, "%s/%d/stats_%u/cu_occupancy", kfd_proc_dir(), pid, uid);
+  const int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd >= 0) {
+    L.occ_fd = fd;
+    VLOG_INFO("device %d: limiter cross-checks its markers with %s", dev, path);
+  }
+  return fd;
+}
+
+void occ_step(int dev, DevLimiter& L, uint64_t now) {
+  const uint64_t period = occ_period_ns();
+  if (!period) return;
+  if (L.occ_last_ns && now - L.occ_last_ns < period) return;
+  const int fd = occ_open(dev, L, now);
+  if (fd < 0) return;
+  char buf[32];
+  const ssize_t n = pread(fd, buf, sizeof buf - 1, 0);
+  if (n <= 0) return;
+  buf[n] = 0;
+  const long occ = strtol(buf, nullptr, 10);
+  const uint64_t dt = L.occ_last_ns ? std::min<uint64_t>(now - L.occ_last_ns, 2 * period) : 0;
+  L.occ_last_ns = now;
+  if (occ > 0) L.occ_busy_acc += dt;
+  if (!L.occ_window_start) L.occ_window_start = now;
+  static const uint64_t window = 100000000ull;  // reconcile every 100 ms
+  if (now - L.occ_window_start < window) return;
+  // Charge what the samples saw beyond the markers' charge, less a tolerance
+  // for sampling error (one period either way, 10 %).
+  const uint64_t seen = L.occ_busy_acc, marked = L.occ_mark_acc;
+  const uint64_t slack = period + marked / 10;
+  if (seen > marked + slack) {
+    const uint64_t extra = seen - marked - slack;
+    std::lock_guard<std::mutex> g(L.mu);
+    // Processor sharing as for marker charges: k pods busy at once pay 1/k each
+    // (the board's virtual time is tied to marker intervals, so scale directly).
+    const int k = L.board ? std::max(1, (int)__atomic_load_n(&L.board->n_active, __ATOMIC_RELAXED)) : 1;
+    const uint64_t charge = extra / (uint64_t)k;
+    L.tokens.fetch_sub((int64_t)charge, std::memory_order_relaxed);
+    L.win_charge += charge;
+    L.charged_total.fetch_add(charge, std::memory_order_relaxed);
+    L.occ_extra_total.fetch_add(charge, std::memory_order_relaxed);
+    trace_emit(VGPU_EV_GPU_TIME, dev, charge, extra);
+  }
+  L.occ_busy_acc = L.occ_mark_acc = 0;
+  L.occ_window_start = now;
+}
+
 void limiter_main() {
   g_thread_alive.store(1);
   // Our polling must not be refused (or break) an application's graph capture
@@ -537,6 +620,7 @@ void limiter_main() {
         if (nv > L.cap) nv = L.cap;
       } while (!L.tokens.compare_exchange_weak(cur, nv, std::memory_order_relaxed));
       if (L.board) board_heartbeat(L.board, L.board_slot);
+      occ_step(d, L, now);
       // Publish this process's fair-share utilization of the last ~120 ms window
       // (the reference watcher's cadence) for the monitor's metrics.
       if (now - L.win_start >= 120000000ull) {
@@ -789,7 +873,8 @@ void limiter_track(int dev, hipStream_t stream, hipError_t launch_rc) {
 // board holds a decision for that member count, out[3] 1 while this process
 // runs on CUs of its own, out[4] CUs in the region's mask (0 = every CU),
 // out[5] 1 while the temporal limiter is active for the device, out[6] ns this
-// process has waited in the limiter, out[7] reserved.
+// process has waited in the limiter, out[7] ns charged on KFD occupancy
+// evidence beyond the markers (occ_step).
 void limiter_share_state(int dev, int64_t out[8]) {
   for (int i = 0; i < 8; ++i) out[i] = 0;
   out[0] = -1;
@@ -809,6 +894,7 @@ void limiter_share_state(int dev, int64_t out[8]) {
       out[4] += __builtin_popcountll(__atomic_load_n(&s.region->dev[dev].cu_mask[w], __ATOMIC_RELAXED));
   out[5] = L.active ? 1 : 0;
   if (vgpu_proc_slot_t* sl = my_slot()) out[6] = (int64_t)__atomic_load_n(&sl->throttle_wait_ns, __ATOMIC_RELAXED);
+  out[7] = (int64_t)L.occ_extra_total.load(std::memory_order_relaxed);
 }
 
 void limiter_stats(int dev, uint64_t* charged, uint64_t* busy) {

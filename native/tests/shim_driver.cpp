@@ -95,7 +95,10 @@ int main(int argc, char** argv) {
     // Launch back-to-back for `secs` of wall time (the fake timeline gives each
     // launch VGPU_FAKE_KERNEL_US of GPU time); report GPU time executed / wall.
     double secs = argc > 2 ? atof(argv[2]) : 1.0;
-    const bool graphs = argc > 3 && !strcmp(argv[3], "graph");
+    // "graph": hipGraphLaunch instead of kernel launches; "graphsync": each
+    // replay followed by a device synchronize (a benchmark's step loop)
+    const bool graphs = argc > 3 && !strncmp(argv[3], "graph", 5);
+    const bool step_sync = argc > 3 && !strcmp(argv[3], "graphsync");
     hipGraphExec_t ge = nullptr;
     if (graphs) {
       unsigned grids[1] = {64};
@@ -123,6 +126,7 @@ int main(int argc, char** argv) {
         hipGraphLaunch(ge, nullptr);
       else
         hipLaunchKernel((const void*)&main, dim3(64), dim3(256), nullptr, 0, nullptr);
+      if (step_sync) hipDeviceSynchronize();
       ++n;
     }
     hipDeviceSynchronize();

@@ -857,3 +857,23 @@ def test_multi_gpu_container_per_device_caps_boards_and_ipc(native_build, tmp_pa
     assert o["ipc_open"] == "0" and int(o["ipc_imported_dev5"]) == 256 << 20
     assert o["ipc_charged_dev5"] == "0" and int(o["ipc_exporter_dev3"]) == 256 << 20
     assert o["ipc_imported_after_close"] == "0"
+
+
+@pytest.mark.parametrize("occ_us", ["2000", "0"])
+def test_limiter_occupancy_cross_check_under_early_markers(native_build, tmp_path, occ_us):
+    """under rocprofv3 the limiter's stream markers completed
+    early and a 25 % pod ran at 3.4 x its share.  Model: markers complete
+    after a quarter of the work before them (VGPU_FAKE_EARLY_EVENTS=0.25).
+    With the KFD cu_occupancy cross-check (default) the busy time the samples
+    see beyond the markers' charge is charged too and the pod stays near 25 %;
+    with the check off (VGPU_LIMITER_OCC_US=0) it escapes."""
+    env = _kfd_env(tmp_path, 777030)
+    env.update({"VGPU_DEVICE_CU_LIMIT_0": "25", "VGPU_CU_MASK_FROM_LIMIT": "false",
+                "GPU_CORE_UTILIZATION_POLICY": "force", "VGPU_FAKE_KERNEL_US": "2000",
+                "VGPU_FAKE_EARLY_EVENTS": "0.25", "VGPU_FAKE_KFD_OCC": "1", "VGPU_LIMITER_OCC_US": occ_us})
+    o = run("duty", 3, "graphsync", env=env, timeout=90)  # replay + synchronize per step, like a benchmark pod
+    duty = _duty(o)
+    if occ_us == "0":
+        assert duty > 0.5, o       # the hole: markers alone under-charge
+    else:
+        assert 0.18 < duty < 0.36, (duty, o["_stderr"][-1500:])
