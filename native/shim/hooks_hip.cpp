@@ -133,6 +133,7 @@ hipError_t charged_alloc(void** ptr, size_t size, int kind, F&& real_alloc, bool
       rc = real_alloc();
       if (rc == hipSuccess) {
         ledger_add(*ptr, size, dev, kind);
+        vmem_note_plain(dev);
         return rc;
       }
       (void)REAL_HIP(hipGetLastError)();
@@ -155,6 +156,7 @@ hipError_t charged_alloc(void** ptr, size_t size, int kind, F&& real_alloc, bool
     return rc;
   }
   ledger_add(*ptr, size, dev, kind);
+  if (kind == kDeviceBuf) vmem_note_plain(dev);
   return rc;
 }
 

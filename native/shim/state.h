@@ -163,6 +163,7 @@ void vmem_graph_note(const void* key, bool exec, void** args, void** extra, cons
 void vmem_graph_child(hipGraph_t graph, hipGraph_t child);
 bool vmem_release(void* p);                 // forget a range before the real free; false if not ours
 bool vmem_make_room(int dev, uint64_t need); // demote cold promoted ranges; true if `need` now fits
+void vmem_note_plain(int dev);               // a plain buffer was placed: update the plain high-water mark
 void vmem_scan_args(void** args, hipStream_t stream);    // HIP-Clang stub argument array
 void vmem_scan_extra(void** extra, hipStream_t stream);  // HIP_LAUNCH_PARAM_BUFFER_* kernarg blob
 // Graphs: ranges named by captured launches follow capture -> graph -> exec,

@@ -50,7 +50,9 @@
 // KFD moves SVM pages at 6-7 GB/s up and 9-11 GB/s down on MI355X regardless
 // of piece size, transparent huge pages or concurrency (native/probes/
 // svm_rate.hip, profiles/vmem_r3.md), so the pager moves whole ranges in
-// 1 GiB pieces and never cycles.
+// 1 GiB pieces and never cycles; the last piece that fits is cut to the
+// budget's remaining room, after the plain buffers' recent high-water mark
+// (plain_reserve: activations are placed ahead of weights).
 // VGPU_VMEM_MIGRATE=0 keeps the round-1 behaviour (pinned zero-copy spill).
 #include <pthread.h>
 
@@ -112,6 +114,7 @@ struct Knobs {
   // budget or oversubscription, resident like hipMalloc memory, so a suspend
   // (SIGUSR2) can give the container's HBM back.
   bool suspend_evict = false;
+  uint64_t plain_window_ms = 30000;  // plain high-water mark window (plain_reserve)
 };
 
 const Knobs& knobs() {
@@ -125,6 +128,7 @@ const Knobs& knobs() {
       v.cold_ticks = std::max<uint64_t>(1, strtoull(e, nullptr, 10) / v.tick_ms);
     if (const char* e = env_first("VGPU_VMEM_PIECE_MB")) v.piece = std::max<uint64_t>(2, strtoull(e, nullptr, 10)) << 20;
     v.suspend_evict = env_bool(env_first("VGPU_SUSPEND_EVICT"), false);
+    if (const char* e = env_first("VGPU_VMEM_PLAIN_WINDOW_MS")) v.plain_window_ms = std::max(1ull, strtoull(e, nullptr, 10));
     if (const char* e = env_first("VGPU_VMEM_MANAGED_MIN_MB")) {
       const long long mb = atoll(e);
       v.managed_min = mb < 0 ? -1 : (int64_t)mb << 20;
@@ -298,12 +302,64 @@ uint64_t pod_resident(int dev) {
   return s.region ? region_device_used(s.region, dev) : 0;
 }
 
-// `need` more bytes may become HBM-resident on `dev`.
-bool room_for(int dev, uint64_t need) {
-  const uint64_t b = phys_budget(dev);
-  if (b && pod_resident(dev) + need > b) return false;
-  return hbm_free(dev) >= need + knobs().headroom;
+// ---- plain HBM ahead of managed ranges ----------------------------
+// Plain buffers (below the managed size: activations, workspaces, the graph
+// pool) are read by nearly every kernel; a managed range's last bytes are read
+// once per sweep.  So under a budget the pager reserves the pod's recent
+// high-water mark of plain bytes before it places managed bytes: a plain
+// allocation that the caching allocator frees and makes again finds its room
+// still free instead of taking it back from a range's tail (one move out, one
+// back in, per cycle).  The mark is the maximum over the current and the last
+// VGPU_VMEM_PLAIN_WINDOW_MS (30 s) window, so a transient peak (model loading)
+// stops reserving HBM after at most two windows.
+std::atomic<uint64_t> g_plain_peak[VGPU_MAX_DEVICES];
+std::atomic<uint64_t> g_plain_prev[VGPU_MAX_DEVICES];
+
+uint64_t plain_now(int dev) {
+  const uint64_t all = pod_resident(dev), mine = promoted_bytes(dev);
+  return all > mine ? all - mine : 0;
 }
+
+void note_plain(int dev) {
+  if (dev < 0 || dev >= VGPU_MAX_DEVICES || !phys_budget(dev)) return;
+  const uint64_t p = plain_now(dev);
+  uint64_t cur = g_plain_peak[dev].load(std::memory_order_relaxed);
+  while (p > cur && !g_plain_peak[dev].compare_exchange_weak(cur, p, std::memory_order_relaxed)) {
+  }
+}
+
+void rotate_plain_window() {
+  for (int d = 0; d < VGPU_MAX_DEVICES; ++d) {
+    g_plain_prev[d].store(g_plain_peak[d].exchange(0, std::memory_order_relaxed), std::memory_order_relaxed);
+    note_plain(d);
+  }
+}
+
+// HBM of `dev`'s budget that placing managed bytes must leave to plain buffers
+// beyond what they hold now.
+uint64_t plain_reserve(int dev) {
+  if (dev < 0 || dev >= VGPU_MAX_DEVICES) return 0;
+  const uint64_t mark = std::max(g_plain_peak[dev].load(std::memory_order_relaxed),
+                                 g_plain_prev[dev].load(std::memory_order_relaxed));
+  const uint64_t p = plain_now(dev);
+  return mark > p ? mark - p : 0;
+}
+
+// Bytes that may still become HBM-resident on `dev`: the budget (less the plain
+// reserve when managed bytes are placed) and physical HBM beyond the headroom.
+uint64_t room_left(int dev, bool managed) {
+  uint64_t room = UINT64_MAX;
+  if (const uint64_t b = phys_budget(dev)) {
+    const uint64_t used = pod_resident(dev) + (managed ? plain_reserve(dev) : 0);
+    room = b > used ? b - used : 0;
+    if (!room) return 0;
+  }
+  const uint64_t f = hbm_free(dev), h = knobs().headroom;
+  return std::min(room, f > h ? f - h : 0);
+}
+
+// `need` more bytes may become HBM-resident on `dev`.
+bool room_for(int dev, uint64_t need, bool managed = true) { return room_left(dev, managed) >= need; }
 
 // Move the whole range back to host memory.  Caller holds g_move_mu.
 bool demote_locked(VRange* r) {
@@ -323,11 +379,20 @@ bool demote_locked(VRange* r) {
 }
 
 // Promote the next piece of `r`.  Caller holds g_move_mu.  False when there is no room.
+// A piece that does not fit whole is cut to the room left, in whole 2 MiB
+// granules (KFD's migration granule), so the budget fills up: the resident set
+// can then match a zero-copy pod's, which keeps the first budget-full of bytes
+// allocated.  The plain reserve keeps later plain buffers from taking that
+// room back (the round-3 attempt without it cycled tails out and in).
 bool promote_piece_locked(VRange* r) {
   const Knobs& k = knobs();
+  constexpr uint64_t kGranule = 2ull << 20;
   uint64_t n = std::min<uint64_t>(k.piece, r->size - r->gpu_bytes);
   if (!n) return false;
-  if (!room_for(r->dev, n)) return false;  // make_room_locked ran first
+  if (!room_for(r->dev, n)) {  // make_room_locked ran first
+    n = room_left(r->dev, true) & ~(kGranule - 1);
+    if (!n) return false;
+  }
   auto t0 = std::chrono::steady_clock::now();
   if (!prefetch(r->base + r->gpu_bytes, n, r->dev, true)) return false;
   uint64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
@@ -344,8 +409,8 @@ bool promote_piece_locked(VRange* r) {
 
 // Demote cold promoted ranges of `dev` (oldest first, never `keep`) until
 // `need` bytes of HBM are free beyond the headroom.  Caller holds g_move_mu.
-bool make_room_locked(int dev, uint64_t need, const VRange* keep, uint64_t newer_than) {
-  if (room_for(dev, need)) return true;
+bool make_room_locked(int dev, uint64_t need, const VRange* keep, uint64_t newer_than, bool managed = true) {
+  if (room_for(dev, need, managed)) return true;
   std::vector<VRange*> cold;
   {
     std::shared_lock<std::shared_mutex> g(g_tab_mu);
@@ -354,10 +419,10 @@ bool make_room_locked(int dev, uint64_t need, const VRange* keep, uint64_t newer
   }
   std::sort(cold.begin(), cold.end(), [](VRange* a, VRange* b) { return a->last_use.load() < b->last_use.load(); });
   for (VRange* r : cold) {
-    if (room_for(dev, need)) break;
+    if (room_for(dev, need, managed)) break;
     demote_locked(r);
   }
-  return room_for(dev, need);
+  return room_for(dev, need, managed);
 }
 
 // Suspended (SIGUSR2): give back every byte of HBM our managed ranges hold.
@@ -384,6 +449,17 @@ void pager_step(bool advance) {
   if (advance && tick % (1000 / k.tick_ms + 1) == 0) {
     std::shared_lock<std::shared_mutex> g(g_tab_mu);
     for (VRange* r : g_tab) r->uses.store(r->uses.load() / 2);
+  }
+  if (advance) {
+    if (tick % std::max<uint64_t>(1, k.plain_window_ms / k.tick_ms) == 0) rotate_plain_window();
+    bool seen[VGPU_MAX_DEVICES] = {};
+    {
+      std::shared_lock<std::shared_mutex> g(g_tab_mu);
+      for (VRange* r : g_tab)
+        if (r->dev >= 0 && r->dev < VGPU_MAX_DEVICES) seen[r->dev] = true;
+    }
+    for (int d = 0; d < VGPU_MAX_DEVICES; ++d)
+      if (seen[d]) note_plain(d);
   }
   // Snapshot the candidates by value under the table lock: a concurrent
   // hipFree (vmem_release) may delete a range as soon as the lock is dropped,
@@ -414,7 +490,8 @@ void pager_step(bool advance) {
     const uint64_t stale = tick > k.cold_ticks ? tick - k.cold_ticks : 0;
     while (r->gpu_bytes < r->size) {
       uint64_t n = std::min<uint64_t>(k.piece, r->size - r->gpu_bytes);
-      if (!make_room_locked(r->dev, n, r, stale) || !promote_piece_locked(r)) {
+      (void)make_room_locked(r->dev, n, r, stale);  // what it could not free, a cut piece may still use
+      if (!promote_piece_locked(r)) {
         waiting += r->size - r->gpu_bytes;
         waiting_dev = r->dev;
         break;
@@ -552,7 +629,8 @@ hipError_t vmem_alloc_managed(void** ptr, size_t size, int dev) {
   const uint64_t stale = tick > k.cold_ticks ? tick - k.cold_ticks : 0;
   while (r->gpu_bytes < r->size) {
     const uint64_t n = std::min<uint64_t>(k.piece, r->size - r->gpu_bytes);
-    if (!make_room_locked(dev, n, r, stale) || !promote_piece_locked(r)) break;
+    (void)make_room_locked(dev, n, r, stale);
+    if (!promote_piece_locked(r)) break;
   }
   return hipSuccess;
 }
@@ -750,7 +828,7 @@ bool vmem_make_room(int dev, uint64_t need) {
   std::lock_guard<std::mutex> m(g_move_mu);
   const Knobs& k = knobs();
   const uint64_t tick = g_tick.load();
-  if (make_room_locked(dev, need, nullptr, tick > k.cold_ticks ? tick - k.cold_ticks : 0)) return true;
+  if (make_room_locked(dev, need, nullptr, tick > k.cold_ticks ? tick - k.cold_ticks : 0, false)) return true;
   // Nothing is cold and the budget is full of managed ranges.  An allocation
   // below the managed size is activation / workspace sized and used by every
   // kernel that follows: spilled, each of them would cross the host link.  It
@@ -770,6 +848,11 @@ bool vmem_make_room(int dev, uint64_t need) {
     if (!big || !demote_tail_locked(big, (pod_resident(dev) - b + g - 1) & ~(g - 1))) return false;
   }
   return true;
+}
+
+void vmem_note_plain(int dev) {
+  if (g_count.load(std::memory_order_relaxed) == 0) return;
+  note_plain(dev);
 }
 
 namespace {

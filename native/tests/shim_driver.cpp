@@ -431,6 +431,69 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (sc == "vmem_fill") {
+    // Part E in miniature: weights larger than the budget, then
+    // activation-sized plain buffers, then a cyclic sweep over every weight.
+    // The budget fills to the byte (cut last piece), the plain buffers stay in
+    // HBM, and a plain buffer freed and made again finds its room still free
+    // (the plain high-water mark is reserved): no tail goes out and back.
+    const size_t G = 1ull << 30, M = 1ull << 20;
+    auto vstats = sym<void (*)(uint64_t*)>("vgpu_self_vmem_stats");
+    auto self_region = sym<void* (*)()>("vgpu_self_region");
+    auto self_slot = sym<int (*)()>("vgpu_self_slot");
+    auto slot_u = [&]() -> vgpu_dev_usage_t& {
+      return ((vgpu_shared_region_t*)self_region())->procs[self_slot()].used[dev];
+    };
+    uint64_t peak_phys = 0;
+    auto note = [&] { peak_phys = std::max<uint64_t>(peak_phys, fake_hip_physical_used(dev)); };
+    const size_t wsz = 2 * G + 900 * M;
+    void** w = new void*[3]();
+    void** p = new void*[5]();
+    int rw = 0, rp = 0;
+    for (int i = 0; i < 3; ++i) rw |= hipMalloc(&w[i], wsz);
+    note();
+    uint64_t gpu_load = 0;
+    for (int i = 0; i < 3; ++i) gpu_load += fake_hip_managed_gpu_bytes(w[i]);
+    for (int i = 0; i < 5; ++i) rp |= hipMalloc(&p[i], 30 * M);  // below the managed size: plain
+    note();
+    auto launch = [&](void* q) {
+      int n = 1;
+      void* a = (char*)q + 64;
+      void* args[] = {&n, &a};
+      hipLaunchKernel((const void*)0x1, dim3(64), dim3(256), args, 0, nullptr);
+    };
+    auto sweep = [&](int ms) {
+      for (int t = 0; t < ms / 10; ++t) {
+        launch(w[t % 3]);
+        note();
+        usleep(10000);
+      }
+    };
+    sweep(600);
+    uint64_t v[5];
+    vstats(v);
+    uint64_t gpu_mid = 0;
+    for (int i = 0; i < 3; ++i) gpu_mid += fake_hip_managed_gpu_bytes(w[i]);
+    const uint64_t out_mid = v[1], moves_mid = v[2];
+    hipFree(p[4]);  // the caching allocator gives one back ...
+    sweep(300);     // ... the pager runs meanwhile ...
+    int again = hipMalloc(&p[4], 30 * M);  // ... and it comes back
+    note();
+    sweep(200);
+    vstats(v);
+    uint64_t gpu_end = 0;
+    for (int i = 0; i < 3; ++i) gpu_end += fake_hip_managed_gpu_bytes(w[i]);
+    printf("alloc_w=%d\nalloc_p=%d\nagain=%d\ngpu_load=%llu\ngpu_mid=%llu\ngpu_end=%llu\nout_mid=%llu\nout_end=%llu\n"
+           "moves_mid=%llu\nmoves_end=%llu\nhost=%llu\nphys=%llu\npeak_phys=%llu\n",
+           rw, rp, again, (unsigned long long)gpu_load, (unsigned long long)gpu_mid, (unsigned long long)gpu_end,
+           (unsigned long long)out_mid, (unsigned long long)v[1], (unsigned long long)moves_mid,
+           (unsigned long long)v[2], (unsigned long long)slot_u().host_bytes,
+           (unsigned long long)fake_hip_physical_used(dev), (unsigned long long)peak_phys);
+    for (int i = 0; i < 5; ++i) hipFree(p[i]);
+    for (int i = 0; i < 3; ++i) hipFree(w[i]);
+    return 0;
+  }
+
   if (sc == "vmem_flags") {
     // Under a physical budget plain hipMalloc becomes a managed range, but an
     // allocation with fine-grained / uncached flags stays a device allocation

@@ -214,6 +214,29 @@ def test_vmem_small_allocation_takes_room_from_a_range_tail(native_build):
     assert int(o["phys"]) <= 8 * GiB
 
 
+def test_vmem_budget_fills_and_plain_buffers_keep_their_room(native_build):
+    """VERDICT r3 #3 (part E in miniature): 3 x 2.88 GiB of weights against an
+    8 GiB budget fill it to the byte (the last piece is cut to the room left,
+    where the round-3 pager stopped at 7.76 GiB), five 30 MiB plain buffers
+    made afterwards take their room from range tails and stay in HBM, and one
+    freed and made again finds its room still free: the pager reserves the
+    plain high-water mark, so no tail goes out and back in."""
+    o = run("vmem_fill", env=BUDGET_ENV)
+    M = 1 << 20
+    assert (o["alloc_w"], o["alloc_p"], o["again"]) == ("0", "0", "0")
+    assert int(o["gpu_load"]) == 8 * GiB
+    assert int(o["gpu_mid"]) == 8 * GiB - 150 * M == int(o["gpu_end"])
+    assert int(o["out_mid"]) == 150 * M == int(o["out_end"])
+    assert o["moves_end"] == o["moves_mid"]
+    assert int(o["host"]) == 3 * (2 * GiB + 900 * M) - int(o["gpu_end"])  # only weight bytes on the host
+    assert int(o["peak_phys"]) <= 8 * GiB
+    # the mark is a window: once the peak has aged out (two 100 ms windows), the
+    # pager gives the freed room to the weights and the re-made buffer takes it back
+    o = run("vmem_fill", env={**BUDGET_ENV, "VGPU_VMEM_PLAIN_WINDOW_MS": "100"})
+    assert int(o["out_end"]) == int(o["out_mid"]) + 30 * M
+    assert int(o["peak_phys"]) <= 8 * GiB
+
+
 def test_vmem_hot_set_beyond_budget_does_not_cycle(native_build):
     """Two hot 6 GiB ranges against an 8 GiB budget: the resident part stays
     put (no LRU exchange on a cyclic sweep), the rest is read in place."""
