@@ -60,9 +60,12 @@ struct ConvArgs {
   int N, H, W, C, Cout, OH, OW, stride, pad;
   int M, K, ktiles, cblocks, nM, nN, nwg, act;
   uint32_t x_bytes, y_bytes;  // buffer-resource extents (< 2^31: the host splits the batch)
+  int nmajor;                 // conv_halo_kernel: workgroups of one XCD share an N tile
 };
 
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+// Keep `v` in a VGPR as it is here (no rematerialisation, no hoisting past this point).
+__device__ __forceinline__ void pin_vgpr(uint32_t& v) { asm volatile("" : "+v"(v)); }
 __device__ __forceinline__ uint16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(uint16_t, b);
@@ -812,6 +815,277 @@ hipError_t launch_big(ConvArgs a, hipStream_t s) {
   a.nwg = a.nM * a.nN;
   hipLaunchKernelGGL((conv_big_kernel<RES, 4>), dim3(a.nwg), dim3(kBigThreads), 0, s, a);
   return hipGetLastError();
+}
+
+// ---- 3x3 / stride-1 convs from a halo tile in LDS ----------------------------
+// The LDS-DMA kernel above re-gathers every A row from L2 once per filter tap:
+// per 64-channel block a 128-row tile moves 9 × 16 KB of A into the CU, and a
+// stage-3/4 layer runs at the per-CU L2→LDS rate (≈70 GB/s; s4 conv2 50 µs ≈
+// 1.77 MB per workgroup pair / 70 GB/s).  Here a workgroup owns BM consecutive
+// output pixels (m order) and, per 64-channel block, DMAs the input rows those
+// pixels touch — their 3x3 neighbourhood, a contiguous pixel range of the NHWC
+// input since the rows are whole image rows — into LDS once; all 9 taps read
+// their A fragments from that halo image.  A traffic per channel block falls
+// from 9·BM·128 B to (rows spanned + 2)·W·128 B (stage 3, BM 256: 295 KB →
+// 42 KB), so the weights dominate what a CU takes in and the tile can grow to
+// 256 × 128 (8 waves of 64 × 64) at one workgroup per CU.
+//
+// A fragment addresses are per lane and per tap (pixel → halo row + swizzled
+// slot), computed once per tile: 9 × TM registers.  Padding taps and M-tail
+// rows point at a zero row — the last row of the halo image, beyond every
+// tile's pixel range (the host guarantees the bound), which the DMA fills
+// with zeros from out-of-range offsets.  Consecutive pixels map to
+// consecutive halo rows for every tap, so the slot ^ (row & 7) swizzle stays
+// conflict-free for ds_read_b128 at any row offset.
+//
+// Pipeline (K order: channel block major, tap minor; K step = tap·cblocks + cb):
+// the weight panel of step s+1 is DMA'd while step s multiplies; the halo of
+// block cb+1 is DMA'd at tap 0 of block cb behind that panel, into the other
+// halo stage, and must land by tap 2.  Past the end the DMAs are dummies
+// (out-of-range source → zeros) into stages nobody reads again, so every
+// thread issues the same DMA count and the counted vmcnt waits stay exact.
+// NMAJOR: workgroups of one XCD share an N tile (weight panels stay in that
+// XCD's L2 when the whole filter does not fit, e.g. stage 4: 4.7 MB).
+template <int BM, int BN, int HPMAX>
+__global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvArgs a) {
+  constexpr int T = BM * BN / 64, WN = BN / 64;
+  constexpr int TM = 4, TN = 4;                       // wave tile 64 x 64
+  constexpr int RPI = T / 8;                          // LDS rows (128 B) per DMA instruction
+  constexpr int HI = HPMAX / RPI, BR = BN / RPI;      // DMA instructions per thread: halo, panel
+  constexpr int HSTAGE = HPMAX * 128, BSTAGE = BN * 128;
+  constexpr int CS = 64 + 4, SLAB = 16 * CS * 4;      // epilogue: per-wave 16-row slab (fp32)
+  constexpr int BODY = 2 * HSTAGE + 2 * BSTAGE;
+  static_assert(HPMAX % RPI == 0 && BN % RPI == 0, "DMA shape");
+  static_assert((T / 64) * SLAB <= BODY, "epilogue slabs fit in the pipeline stages");
+  __shared__ __attribute__((aligned(16))) char smem[BODY];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int lrow = t >> 3, lchunk = (t & 7) ^ (lrow & 7);
+  int m0, n0;
+  if (a.nmajor) {
+    const int xcd = blockIdx.x & 7, q = a.nwg >> 3, r8 = a.nwg & 7;
+    const int id = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (blockIdx.x >> 3);
+    const int ni = id / a.nM;
+    m0 = (id - ni * a.nM) * BM;
+    n0 = ni * BN;
+  } else {
+    tile_origin(a, blockIdx.x, BM, BN, m0, n0);
+  }
+  const int W = a.W, H = a.H;
+  const int rows_total = a.N * H;
+  const int r0 = m0 / W, mlast = (m0 + BM < a.M ? m0 + BM : a.M) - 1, r1 = mlast / W;
+  const int g_lo = r0 > 0 ? r0 - 1 : 0, g_hi = r1 + 1 < rows_total ? r1 + 1 : rows_total - 1;
+  const int hp = (g_hi - g_lo + 1) * W;  // halo pixels of this tile (< HPMAX)
+  const int pix0 = g_lo * W;
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.x), 0, a.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.w), 0, (uint32_t)((int64_t)a.Cout * a.K * 2), 0x00020000);
+
+  // Halo DMA sources (channel block 0); block cb adds cb·128 B.  A literal
+  // array bound: a lambda capturing a local array of value-dependent size
+  // fails substitution in the host pass, which then emits no launch stub.
+  static_assert(HI <= 6, "halo DMA registers");
+  uint32_t hsrc[6];
+#pragma unroll
+  for (int i = 0; i < HI; ++i) {
+    const int h = i * RPI + lrow;
+    hsrc[i] = h < hp ? (uint32_t)(((pix0 + h) * a.C + lchunk * 8) * 2) : kOOB;
+  }
+  const uint32_t boff = (uint32_t)(((n0 + lrow) * a.K + lchunk * 8) * 2);
+  auto issue_h = [&](int cb, int hs) {  // cb == cblocks: dummy (zeros into the idle stage)
+    char* sH = smem + hs * HSTAGE;
+    const bool live = cb < a.cblocks;
+#pragma unroll
+    for (int i = 0; i < HI; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          xr, (lds_void_t*)(sH + (i * RPI + wave * 8) * 128), 16,
+          (live && hsrc[i] != kOOB) ? hsrc[i] + (uint32_t)(cb * 128) : kOOB, 0, 0, 0);
+  };
+  auto issue_b = [&](int kt, int bs) {  // kt < 0: dummy
+    char* sB = smem + 2 * HSTAGE + bs * BSTAGE;
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          wr, (lds_void_t*)(sB + (i * RPI + wave * 8) * 128), 16,
+          kt >= 0 ? boff + (uint32_t)((i * RPI * a.K + kt * BK) * 2) : kOOB, 0, 0, 0);
+  };
+
+  // Per-lane, per-tap A fragment addresses: byte offsets in a halo stage of
+  // k-half 0 (logical slot fk, low 16 bits) and k-half 1 (slot 4 + fk = the
+  // same ^ 64, high 16 bits) — one register per (tap, row tile).  Unpacked at
+  // each use; pinned per channel block so hipcc cannot hoist 72 unpacked
+  // addresses out of the loop (it did: 256 VGPRs and spills).
+  constexpr int ZROW = HPMAX - 1;
+  static_assert(HSTAGE <= 65536, "16-bit halo addresses");
+  uint32_t aaddr[9][TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + fr;
+    const bool mok = m < a.M;
+    const int row = (mok ? m : m0) / W;
+    const int ow = (mok ? m : m0) - row * W, oh = row % H;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int ih = oh + kh - 1, iw = ow + kw - 1;
+        const bool v = mok & ((unsigned)ih < (unsigned)H) & ((unsigned)iw < (unsigned)W);
+        const int h = v ? (row + kh - 1 - g_lo) * W + iw : ZROW;
+        const uint32_t a0 = (uint32_t)(h * 128 + ((fk ^ (h & 7)) << 4));
+        aaddr[kh * 3 + kw][i] = a0 | ((a0 ^ 64u) << 16);
+      }
+  }
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int tap, const char* sH, const char* sB) {
+    bf16x8_t af[2][TM], bfr[2][TN];
+    auto rd = [&](int kk) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[kk][i] = *reinterpret_cast<const bf16x8_t*>(sH + (kk ? aaddr[tap][i] >> 16 : aaddr[tap][i] & 0xffffu));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[kk][j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(wn * 64 + j * 16 + fr, kk * 4 + fk));
+    };
+    auto mm = [&](int kk) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+    };
+    rd(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    __builtin_amdgcn_sched_barrier(0);
+    rd(1);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(1);
+  };
+
+  const int nb = a.cblocks;
+  issue_h(0, 0);
+  issue_b(0, 0);
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+  __builtin_amdgcn_s_barrier();
+  int bs = 0;
+  for (int cb = 0; cb < nb; ++cb) {
+    const int hs = cb & 1;
+    const char* sH = smem + hs * HSTAGE;
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) pin_vgpr(aaddr[tp][i]);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      // next step's panel: (tap+1, cb), or (0, cb+1) after the last tap; a dummy past the end
+      const int kn = tap < 8 ? (tap + 1) * nb + cb : (cb + 1 < nb ? cb + 1 : -1);
+      issue_b(kn, bs ^ 1);
+      if (tap == 0) {
+        issue_h(cb + 1, hs ^ 1);
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(BR + HI));
+      } else if (tap == 1) {
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(BR + HI));
+      } else {
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(BR));
+      }
+      __builtin_amdgcn_s_barrier();
+      compute(tap, sH, smem + 2 * HSTAGE + bs * BSTAGE);
+      __builtin_amdgcn_s_waitcnt(kLgkm0);
+      __builtin_amdgcn_s_barrier();
+      bs ^= 1;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // trailing dummy DMAs, before the slabs reuse LDS
+  __builtin_amdgcn_s_barrier();
+
+  // Epilogue: per wave, four 16-row passes through its own slab (no workgroup barrier).
+  float* sC = reinterpret_cast<float*>(smem + wave * SLAB);
+  const int ecol = (lane & 7) * 8, erow = lane >> 3;
+  const int col = n0 + wn * 64 + ecol;
+  float bb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bb[j] = 0.0f;
+  if (a.bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(a.bias + col);
+    const float4 b1 = *reinterpret_cast<const float4*>(a.bias + col + 4);
+    bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
+    bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sC[(fk * 4 + e) * CS + j * 16 + fr] = acc[i][j][e];
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int row = erow + 8 * r, m = m0 + wm * 64 + i * 16 + row;
+      const float4 c0 = *reinterpret_cast<const float4*>(sC + row * CS + ecol);
+      const float4 c1 = *reinterpret_cast<const float4*>(sC + row * CS + ecol + 4);
+      float v[8] = {c0.x + bb[0], c0.y + bb[1], c0.z + bb[2], c0.w + bb[3],
+                    c1.x + bb[4], c1.y + bb[5], c1.z + bb[6], c1.w + bb[7]};
+      if (a.act) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);
+      }
+      if (m < a.M) *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = pack8(v);
+    }
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+  }
+}
+
+int g_forced_halo = -1;  // vgpu_conv_set_halo: -1 = env VGPU_CONV_HALO, 0 = off, 1 = on, 2 / 3 = on with BM 256 / 128
+
+bool halo_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* v = getenv("VGPU_CONV_HALO");
+    on = (v && (v[0] == '0' || v[0] == 'n' || v[0] == 'f')) ? 0 : 1;
+  }
+  return on == 1;
+}
+
+unsigned long long g_halo_launches = 0;  // vgpu_conv_halo_launches (tests: the halo path ran)
+
+template <int BM, int BN, int HPMAX>
+hipError_t launch_halo(ConvArgs a, hipStream_t s) {
+  ++g_halo_launches;
+  a.nM = (a.M + BM - 1) / BM;
+  a.nN = a.Cout / BN;
+  a.nwg = a.nM * a.nN;
+  // N-major placement when the filter outgrows an XCD's L2 share (4 MiB).
+  a.nmajor = (int64_t)a.Cout * a.K * 2 > ((int64_t)5 << 19) ? 1 : 0;
+  hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
+  return hipGetLastError();
+}
+
+// Halo pixels a BM-pixel tile of a W-wide image can need: rows spanned + 2.
+inline int halo_pixels(int bm, int w) { return ((bm - 1) / w + 4) * w; }
+
+// 3x3 / stride 1 / pad 1, no prologue / residual, Cout % 128 == 0.  Returns
+// hipErrorNotSupported when no halo instantiation fits (the caller falls back).
+hipError_t dispatch_halo(const ConvArgs& a, hipStream_t s) {
+  if (a.Cout % 128) return hipErrorNotSupported;
+  const int64_t tiles256 = (int64_t)((a.M + 255) / 256) * (a.Cout / 128);
+  const bool big = g_forced_halo == 2 || (g_forced_halo != 3 && tiles256 * 5 >= (int64_t)conv_cus() * 3);
+  if (big && halo_pixels(256, a.W) <= 383) return launch_halo<256, 128, 384>(a, s);
+  if (g_forced_halo != 2 && halo_pixels(128, a.W) <= 191) return launch_halo<128, 128, 192>(a, s);
+  return hipErrorNotSupported;
 }
 
 int g_forced_big = -1;  // vgpu_conv_set_big: -1 = env VGPU_CONV_BIG / heuristic, 0 = off, 1 = whenever eligible
@@ -1815,6 +2089,8 @@ VGPU_API int vgpu_stem_space_to_depth(const void* x, void* X, int N, int H, int 
 // Benchmark knob: force 64- or 128-row tiles (0 = heuristic).
 VGPU_API void vgpu_conv_set_tile_m(int bm) { g_forced_bm = bm; }
 VGPU_API void vgpu_conv_set_big(int mode) { g_forced_big = mode; }  // -1 env/heuristic, 0 off, 1 when eligible
+VGPU_API void vgpu_conv_set_halo(int mode) { g_forced_halo = mode; }  // -1 env, 0 off, 1 on, 2/3 BM 256/128
+VGPU_API unsigned long long vgpu_conv_halo_launches() { return g_halo_launches; }
 
 // Fused conv2 (3x3, pad 1, stride s, C = W → W, bias + ReLU) + conv3 (1x1,
 // W → 4W) + residual; with w1n, also the next block's conv1 (1x1, 4W → W,
@@ -1984,7 +2260,12 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
     const int64_t tiles256 = (int64_t)((c.M + 255) / 256) * (Cout / 256);
     const bool big = big_ok && (g_forced_big == 1 ||
                                 (g_forced_big == 2 && C >= 1024 && tiles256 >= (int64_t)conv_cus()));
-    if (big)
+    // 3x3 / stride 1 without prologue or residual: the halo-tile kernel.
+    const bool halo = (g_forced_halo < 0 ? halo_enabled() : g_forced_halo > 0) && !narrow && !pro && !has_res &&
+                      KS == 3 && stride == 1 && pad == 1;
+    if (halo && (e = dispatch_halo(c, s)) != hipErrorNotSupported) {
+      // launched (or a launch error)
+    } else if (big)
       e = has_res ? launch_big<true>(c, s) : launch_big<false>(c, s);
     else if (narrow)
       e = small ? launch_glds<4, 64, 64, false, 16>(c, s) : launch_glds<4, 128, 64, false, 16>(c, s);

@@ -59,16 +59,26 @@ def main() -> int:
     ap.add_argument("--busy", type=float, default=3.0)
     ap.add_argument("--period-us", type=float, default=1000.0)
     a = ap.parse_args()
+    kfd = "/sys/class/kfd/kfd/proc"
+    before = set(os.listdir(kfd)) if os.path.isdir(kfd) else set()
     p = subprocess.Popen([sys.executable, "-c", CHILD, str(a.idle), str(a.busy)], stdout=subprocess.PIPE, text=True)
     line = p.stdout.readline()
     if not line.startswith("READY"):
         print(json.dumps({"error": "child did not start", "line": line}))
         return 1
-    files = glob.glob(f"/sys/class/kfd/kfd/proc/{p.pid}/stats_*/cu_occupancy")
+    # KFD names processes by host pid; inside a container the child's pid
+    # differs, so take the entry that appeared with it.
+    new = sorted(set(os.listdir(kfd)) - before) if os.path.isdir(kfd) else []
+    cands = [str(p.pid)] + new
+    files = []
+    for c in cands:
+        files = glob.glob(f"{kfd}/{c}/stats_*/cu_occupancy")
+        if files:
+            break
     if not files:
         p.wait()
-        print(json.dumps({"error": "no cu_occupancy file", "dir": os.listdir(f"/sys/class/kfd/kfd/proc/{p.pid}")
-                          if os.path.isdir(f"/sys/class/kfd/kfd/proc/{p.pid}") else None}))
+        print(json.dumps({"error": "no cu_occupancy file", "new_kfd_entries": new,
+                          "listing": {c: os.listdir(f"{kfd}/{c}") for c in new if os.path.isdir(f"{kfd}/{c}")}}))
         return 1
     fds = [os.open(f, os.O_RDONLY) for f in files]
     t_start = time.monotonic()

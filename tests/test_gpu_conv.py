@@ -85,6 +85,57 @@ def test_conv_big_tile_matches_fp32(C, case):
     torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
 
 
+HALO_CASES = [
+    # 3x3 / stride 1 on the halo-tile kernel: n, c, h, w, cout, bias, act, tile (2: BM 256, 3: BM 128)
+    (2, 64, 11, 11, 128, True, "relu", 3),      # one channel block, tiles span two images
+    (5, 512, 11, 11, 512, False, "none", 3),    # ResNet stage 4 (N-major placement: 4.7 MB filter)
+    (3, 256, 22, 22, 256, True, "relu", 2),     # ResNet stage 3 on 256-row tiles, ragged last tile
+    (2, 128, 16, 16, 256, True, "none", 2),     # ResNet-152 stage 3, M < one 256-row tile
+    (7, 128, 8, 8, 128, False, "relu", 3),      # two images per tile
+    (3, 64, 9, 1, 128, True, "none", 3),        # W = 1: every kw != 1 tap is padding
+    (9, 64, 1, 16, 128, False, "none", 2),      # H = 1: every kh != 1 tap is padding
+    (1, 192, 5, 7, 384, True, "relu", 1),       # heuristic tile, M = 35 < one tile, three N tiles
+]
+
+
+@pytest.mark.parametrize("case", HALO_CASES, ids=lambda c: "x".join(map(str, c[:5])) + f"-t{c[7]}")
+def test_conv_halo_matches_fp32(C, case):
+    from vgpu.native import load_kernels
+    n, c, h, w, cout, has_bias, act, tile = case
+    x = _t((n, c, h, w), 41)
+    wt = _t((cout, c, 3, 3), 42, scale=(2.0 / (9 * c)) ** 0.5)
+    bias = _f((cout,), 43) if has_bias else None
+    lib = load_kernels()
+    lib.vgpu_conv_set_halo(tile)
+    before = lib.vgpu_conv_halo_launches()
+    try:
+        got = C.conv2d(x, wt, bias, stride=1, padding=1, act=act)
+    finally:
+        lib.vgpu_conv_set_halo(-1)
+    assert lib.vgpu_conv_halo_launches() == before + 1, "the halo kernel did not run"  # no silent fallback
+    ref = C.conv2d_ref(x, wt, bias, stride=1, padding=1, act=act)
+    torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("tile", [2, 3])
+def test_conv_halo_integer_exact(C, tile):
+    """Integer data through the halo kernel: any tap / row / slot mix-up is visible."""
+    from vgpu.native import load_kernels
+    g = torch.Generator(device="cpu").manual_seed(tile)
+    x = torch.randint(-2, 3, (6, 128, 7, 9), generator=g).to(torch.bfloat16).cuda().contiguous(memory_format=CL)
+    wt = torch.randint(-2, 3, (256, 128, 3, 3), generator=g).to(torch.bfloat16).cuda().contiguous(memory_format=CL)
+    lib = load_kernels()
+    lib.vgpu_conv_set_halo(tile)
+    before = lib.vgpu_conv_halo_launches()
+    try:
+        got = C.conv2d(x, wt, stride=1, padding=1)
+    finally:
+        lib.vgpu_conv_set_halo(-1)
+    assert lib.vgpu_conv_halo_launches() == before + 1
+    # fp32 sums of these integers are exact; the kernel rounds them once to bf16
+    assert torch.equal(got.float(), C.conv2d_ref(x, wt, stride=1, padding=1).to(torch.bfloat16).float())
+
+
 DEEP_CASES = [
     # deep-K 1x1 convs with a BN+ReLU prologue (conv_pro_kernel / register path)
     (3, 256, 13, 13, 512, 2, True, "none", False),   # strided projection shortcut, K = 4 steps

@@ -63,6 +63,8 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_maxpool_nhwc.argtypes = [vp, vp] + [ci] * 7 + [vp]
     lib.vgpu_stem_pool_nhwc.argtypes = [vp, vp, vp] + [ci] * 3 + [vp]
     lib.vgpu_conv_set_big.argtypes = [ci]
+    lib.vgpu_conv_set_halo.argtypes = [ci]
+    lib.vgpu_conv_halo_launches.restype = ctypes.c_ulonglong
     lib.vgpu_lstm_recurrence.argtypes = [vp, vp, vp, vp, ci, ci, ci, vp]
     lib.vgpu_lstm_recurrence.restype = ci
     lib.vgpu_lstm_forward_train.argtypes = [vp] * 5 + [ci, ci, ci, vp]

@@ -126,8 +126,22 @@ def build_kernels(force: bool = False) -> Path:
     _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
           "-fvisibility=hidden", f"-I{NATIVE / 'include'}", "-mcode-object-version=5",
           *srcs, "-o", target])
+    _check_stubs(target)
     _mark(target, inputs, ARCH)
     return target
+
+
+def _check_stubs(lib: Path) -> None:
+    """A kernel template whose host-side instantiation fails substitution (e.g.
+    a lambda capturing a local array of value-dependent size) links anyway,
+    with an undefined launch stub, and only fails at dlopen on the GPU box.
+    Refuse such a library here."""
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    out = subprocess.run([nm, "-D", "--undefined-only", str(lib)], capture_output=True, text=True).stdout
+    bad = [ln.split()[-1] for ln in out.splitlines() if "__device_stub__" in ln]
+    if bad:
+        lib.unlink(missing_ok=True)
+        raise RuntimeError(f"{lib.name}: undefined kernel launch stubs {bad}")
 
 
 def build_probe_module(force: bool = False) -> Path:
@@ -204,7 +218,7 @@ def build_fakes(force: bool = False) -> dict[str, Path]:
     hip_src = NATIVE / "fakes" / "fake_hip.cpp"
     hip = FAKES_OUT / "libamdhip64.so.7"
     hip_extra = ("fake_hip_launches; fake_hip_launch_blocks; fake_hip_physical_used; fake_hip_graph_create; "
-                 "fake_hip_exec_ns; fake_hip_svm_move; fake_hip_managed_gpu_bytes; fake_hip_host_touch_bytes; fake_hip_memsets;")
+                 "fake_hip_exec_ns; fake_hip_svm_move; fake_hip_managed_gpu_bytes; fake_hip_host_touch_bytes; fake_hip_memsets; fake_hip_prefetch_overflows;")
     if force or not _stamp(hip, [hip_src, hsa_src], hip_extra + str(sorted(versions.items()))[:4096]):
         vs = FAKES_OUT / "hip.map"
         vs.write_text(_version_script(hip_src, "hip_4.2", versions, hip_extra))
