@@ -604,6 +604,43 @@ hipError_t hipMallocManaged(void** p, size_t size, unsigned int) {
   return hipSuccess;
 }
 hipError_t hipMemAdvise(const void*, size_t, hipMemoryAdvise, int) { return hipSuccess; }
+// hipMemPrefetchAsync on a managed range (resident part = a prefix).  Asked for
+// more VRAM than is free, the real KFD evicts the process's own buffers to make
+// room (profiles/vmem_r2.md); the fake moves what fits and counts the request
+// (fake_hip_prefetch_overflows), so tests can assert that none reaches it.
+static uint64_t g_prefetch_over = 0;
+static hipError_t prefetch_locked(const void* p, size_t n, int device) {
+  auto it = g_managed.upper_bound((uintptr_t)p);
+  if (it == g_managed.begin()) return hipErrorInvalidValue;
+  --it;
+  Managed& m = it->second;
+  const uint64_t off = (uintptr_t)p - it->first;
+  if (off >= m.size) return hipErrorInvalidValue;
+  Dev& d = g_devs[m.dev];
+  if (device < 0) {
+    const uint64_t keep = std::min<uint64_t>(m.gpu_bytes, off);
+    d.used -= m.gpu_bytes - keep;
+    m.gpu_bytes = keep;
+    return hipSuccess;
+  }
+  const uint64_t want = std::min<uint64_t>(m.size, off + n);
+  uint64_t add = want > m.gpu_bytes ? want - m.gpu_bytes : 0;
+  if (d.used + add > d.total) {
+    ++g_prefetch_over;
+    add = d.total - d.used;
+  }
+  m.gpu_bytes += add;
+  d.used += add;
+  return hipSuccess;
+}
+hipError_t hipMemPrefetchAsync(const void* p, size_t n, int device, hipStream_t) {
+  std::lock_guard<std::mutex> g(g_mu);
+  return prefetch_locked(p, n, device);
+}
+hipError_t hipMemPrefetchAsync_v2(const void* p, size_t n, hipMemLocation loc, unsigned int, hipStream_t) {
+  std::lock_guard<std::mutex> g(g_mu);
+  return prefetch_locked(p, n, loc.type == hipMemLocationTypeDevice ? loc.id : -1);
+}
 // A host<->device copy touching a managed range: KFD migrates the touched pages
 // to system memory (native/probes/managed_access.hip); device-to-device copies
 // run on the GPU and move nothing.  No bytes are copied (fake addresses).
@@ -1060,6 +1097,10 @@ int fake_hip_svm_move(const void* p, uint64_t n, int to_gpu) {
     d.used -= sub;
   }
   return 1;
+}
+uint64_t fake_hip_prefetch_overflows() {
+  std::lock_guard<std::mutex> g(g_mu);
+  return g_prefetch_over;
 }
 uint64_t fake_hip_managed_gpu_bytes(const void* p) {
   std::lock_guard<std::mutex> g(g_mu);

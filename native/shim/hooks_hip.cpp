@@ -11,6 +11,7 @@
 // Every hook: (1) lazily initialises, (2) passes straight through when
 // control is disabled, (3) keeps the fast path to a couple of relaxed atomics.
 #include <algorithm>
+#include <functional>
 #include <mutex>
 #include <shared_mutex>
 #include <unordered_map>
@@ -498,6 +499,32 @@ __attribute__((visibility("default"))) hipError_t hipMallocManaged(void** ptr, s
                                                                    unsigned int flags) {
   return charged_alloc(ptr, size, kManaged,
                        [&] { return REAL_HIP(hipMallocManaged)(ptr, size, flags); });
+}
+
+// Application prefetches of managed memory: cut to what HBM holds beyond the
+// headroom, and left to the pager inside its own ranges (vmem_prefetch_allowed).
+static hipError_t prefetch_hook(const void* p, size_t n, int dev, const std::function<hipError_t(size_t)>& real) {
+  ensure_init();
+  if (!st().enabled || !p || !n) return real(n);
+  const size_t m = vmem_prefetch_allowed(p, n, dev);
+  if (m < n)
+    VLOG_INFO("prefetch of %zu bytes at %p to %s cut to %zu (%s)", n, p, dev < 0 ? "host" : "HBM", m,
+              vmem_contains(p) ? "the pager owns the range" : "HBM free beyond the headroom");
+  return m ? real(m) : hipSuccess;
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemPrefetchAsync(const void* p, size_t n, int device,
+                                                                      hipStream_t stream) {
+  return prefetch_hook(p, n, device,
+                       [&](size_t m) { return REAL_HIP(hipMemPrefetchAsync)(p, m, device, stream); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemPrefetchAsync_v2(const void* p, size_t n,
+                                                                         hipMemLocation loc, unsigned int flags,
+                                                                         hipStream_t stream) {
+  const int dev = loc.type == hipMemLocationTypeDevice ? loc.id : -1;
+  return prefetch_hook(p, n, dev,
+                       [&](size_t m) { return REAL_HIP(hipMemPrefetchAsync_v2)(p, m, loc, flags, stream); });
 }
 
 __attribute__((visibility("default"))) hipError_t hipMallocPitch(void** ptr, size_t* pitch,

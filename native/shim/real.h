@@ -169,6 +169,8 @@ using hipIpcOpenMemHandle = hipError_t (*)(void**, hipIpcMemHandle_t, unsigned i
 using hipIpcCloseMemHandle = hipError_t (*)(void*);
 using hipDeviceGetPCIBusId = hipError_t (*)(char*, int, int);
 using hipMemAdvise = hipError_t (*)(const void*, size_t, hipMemoryAdvise, int);
+using hipMemPrefetchAsync = hipError_t (*)(const void*, size_t, int, hipStream_t);
+using hipMemPrefetchAsync_v2 = hipError_t (*)(const void*, size_t, hipMemLocation, unsigned int, hipStream_t);
 using hipMemGetAddressRange = hipError_t (*)(hipDeviceptr_t*, size_t*, hipDeviceptr_t);
 using hipGetProcAddress = hipError_t (*)(const char*, void**, int, uint64_t,
                                          hipDriverProcAddressQueryResult*);

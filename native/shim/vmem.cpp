@@ -850,6 +850,23 @@ bool vmem_make_room(int dev, uint64_t need) {
   return true;
 }
 
+// The application's own hipMemPrefetchAsync.  A prefetch is a hint, so the
+// shim may shorten it.  Into a range the pager owns it does nothing: the pager
+// keeps the books of what is resident, and pages moved behind its back would
+// never be promoted again (to host) or would overrun the budget (to HBM).
+// Elsewhere a prefetch into HBM is cut to the HBM free beyond the headroom, in
+// whole 2 MiB granules.  Asked to migrate more than is free, KFD makes room by
+// evicting the process's own buffers (profiles/vmem_r2.md: pages that stay on
+// the host, one run hung); hbm_free() counts SVM pages (sysfs VRAM counters),
+// which hipMemGetInfo does not, so the cut holds with a small headroom.
+size_t vmem_prefetch_allowed(const void* p, size_t n, int dev) {
+  if (vmem_contains(p)) return 0;
+  if (dev < 0) return n;
+  const uint64_t f = hbm_free(dev), h = knobs().headroom;
+  const uint64_t room = f > h ? (f - h) & ~((2ull << 20) - 1) : 0;
+  return (size_t)std::min<uint64_t>(n, room);
+}
+
 void vmem_note_plain(int dev) {
   if (g_count.load(std::memory_order_relaxed) == 0) return;
   note_plain(dev);

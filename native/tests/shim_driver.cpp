@@ -35,6 +35,7 @@ extern "C" uint64_t fake_hip_physical_used(int dev);
 extern "C" uint64_t fake_hsa_pool_used(int dev);
 extern "C" int fake_hsa_tools_loaded();
 extern "C" uint64_t fake_hip_managed_gpu_bytes(const void* p);
+extern "C" uint64_t fake_hip_prefetch_overflows();
 extern "C" uint64_t fake_hip_host_touch_bytes();
 extern "C" uint64_t fake_hip_memsets();
 extern "C" hipGraph_t fake_hip_graph_create(const unsigned* grids, int n, unsigned child_grid);
@@ -491,6 +492,40 @@ int main(int argc, char** argv) {
            (unsigned long long)fake_hip_physical_used(dev), (unsigned long long)peak_phys);
     for (int i = 0; i < 5; ++i) hipFree(p[i]);
     for (int i = 0; i < 3; ++i) hipFree(w[i]);
+    return 0;
+  }
+
+  if (sc == "prefetch") {
+    // The application's own prefetches (full-HBM hang): into HBM
+    // they are cut to the free HBM beyond the headroom; into a range the pager
+    // owns (oversubscribed pod) they do nothing.
+    const size_t G = 1ull << 30;
+    void** q = new void*[3]();
+    if (argc > 2 && std::string(argv[2]) == "owned") {
+      int ro = hipMalloc(&q[2], 1 * G);  // a managed range the pager owns (physical budget set)
+      const uint64_t before = fake_hip_managed_gpu_bytes(q[2]);
+      int r4 = hipMemPrefetchAsync(q[2], 1 * G, hipCpuDeviceId, nullptr);
+      printf("owned_alloc=%d\nowned_before=%llu\nowned_prefetch=%d\nowned_after=%llu\n", ro,
+             (unsigned long long)before, r4, (unsigned long long)fake_hip_managed_gpu_bytes(q[2]));
+      hipFree(q[2]);
+      return 0;
+    }
+    int rm = hipMallocManaged(&q[0], 8 * G, hipMemAttachGlobal);
+    int rb = hipMalloc(&q[1], 10 * G);  // 6 GiB of the 16 left
+    int r1 = hipMemPrefetchAsync(q[0], 8 * G, dev, nullptr);
+    printf("alloc_m=%d\nalloc_b=%d\nprefetch=%d\nm_gpu=%llu\noverflows=%llu\n", rm, rb, r1,
+           (unsigned long long)fake_hip_managed_gpu_bytes(q[0]), (unsigned long long)fake_hip_prefetch_overflows());
+    hipMemLocation loc{};
+    loc.type = hipMemLocationTypeHost;
+    int r2 = hipMemPrefetchAsync_v2(q[0], 8 * G, loc, 0, nullptr);
+    printf("to_host=%d\nm_gpu_host=%llu\n", r2, (unsigned long long)fake_hip_managed_gpu_bytes(q[0]));
+    hipFree(q[1]);
+    loc.type = hipMemLocationTypeDevice;
+    loc.id = dev;
+    int r3 = hipMemPrefetchAsync_v2(q[0], 8 * G, loc, 0, nullptr);
+    printf("v2=%d\nm_gpu_v2=%llu\noverflows_end=%llu\n", r3, (unsigned long long)fake_hip_managed_gpu_bytes(q[0]),
+           (unsigned long long)fake_hip_prefetch_overflows());
+    hipFree(q[0]);
     return 0;
   }
 

@@ -237,6 +237,29 @@ def test_vmem_budget_fills_and_plain_buffers_keep_their_room(native_build):
     assert int(o["peak_phys"]) <= 8 * GiB
 
 
+def test_application_prefetch_never_overfills_hbm(native_build):
+    """VERDICT r3 #3 (the full-HBM hang): asked to migrate more than free VRAM,
+    KFD evicts the process's own buffers (profiles/vmem_r2.md).  The fake
+    counts such requests.  Without the shim an 8 GiB prefetch into the 6 GiB
+    left overflows; under it the prefetch is cut to the free HBM beyond the
+    256 MiB headroom (2 MiB granules) and nothing overflows, through both
+    entry points.  Inside a range the pager owns, a prefetch does nothing (its
+    books stay true)."""
+    e = {"VGPU_FAKE_MEM": str(16 * GiB), "VGPU_DEVICE_MEMORY_LIMIT_0": "40g", "VGPU_VMEM_HEADROOM_MB": "256"}
+    raw = run("prefetch", env=e, preload=False)
+    assert raw["overflows"] == "1" and int(raw["m_gpu"]) == 6 * GiB
+    o = run("prefetch", env=e)
+    assert (o["alloc_m"], o["alloc_b"], o["prefetch"], o["to_host"], o["v2"]) == ("0",) * 5
+    assert int(o["m_gpu"]) == 6 * GiB - (256 << 20)
+    assert o["m_gpu_host"] == "0"
+    assert int(o["m_gpu_v2"]) == 8 * GiB  # room again once the 10 GiB block is gone
+    assert o["overflows_end"] == "0"
+    own = run("prefetch", "owned", env={**e, "VGPU_OVERSUBSCRIBE": "true", "VGPU_DEVICE_MEMORY_PHYSICAL_0": "8g",
+                                        "VGPU_VMEM_RESERVE_MB": "0"})
+    assert own["owned_alloc"] == "0" and int(own["owned_before"]) == GiB
+    assert own["owned_prefetch"] == "0" and int(own["owned_after"]) == GiB
+
+
 def test_vmem_hot_set_beyond_budget_does_not_cycle(native_build):
     """Two hot 6 GiB ranges against an 8 GiB budget: the resident part stays
     put (no LRU exchange on a cyclic sweep), the rest is read in place."""
