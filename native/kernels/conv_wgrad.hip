@@ -58,12 +58,28 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, b);
 }
 
+// LDS images of [pixel][channel] tiles are XOR-swizzled by 32-B column group:
+// a 32-lane half of a transposed read covers pixel rows {8g+q, 8g+8+q} (q<4)
+// at one 32-B column, which in plain 256-B (or 128-B) rows all sit on the same
+// 8 banks -- an 8-way (4-way) conflict on every read.  Row r's 16-B chunk ch
+// lives at slot ch ^ swz(r): 256-B rows permute the 8 column groups by
+// (r&3, r>>3 & 1), 128-B rows the 4 groups of each half row by (r>>1 & 1,
+// r>>3 & 1) -- the eight rows a half reads then hit eight distinct bank
+// groups.  Rows r and r+4 (the two reads of one operand) share a swizzle.
+template <int RS>
+__device__ __forceinline__ int swz(int r) {
+  if constexpr (RS == 256) return ((((r & 3) << 1) | ((r >> 3) & 1)) << 1);
+  else return ((((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1);
+}
+
 // Two transposed 4-pixel reads → the 8 k-values (pixels 8g..8g+7) of one
-// MFMA operand row (channel base + lane&15).  `tile` is a [KP][RS/2] bf16 image.
+// MFMA operand row (channel base + lane&15).  `tile` is a [KP][RS/2] bf16 image
+// stored with swz<RS>.
 template <int RS>
 __device__ __forceinline__ bf16x8_t tr_operand(const lds_char* tile, int base_ch, int lane) {
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const lds_char* a0 = tile + (8 * g + q) * RS + (base_ch + 4 * p) * 2;
+  const int r = 8 * g + q, byte = (base_ch + 4 * p) * 2;
+  const lds_char* a0 = tile + r * RS + (((byte >> 4) ^ swz<RS>(r)) << 4) + (byte & 15);
   const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
   const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * RS));
   const s16x4 v[2] = {lo, hi};
@@ -124,12 +140,12 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(const WgradArgs a) {
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = t + i * kThreads, r = idx / CPA, ch = idx - r * CPA;
-      *reinterpret_cast<u32x4*>(sA + r * RSA + ch * 16) = ra[i];
+      *reinterpret_cast<u32x4*>(sA + r * RSA + ((ch ^ swz<RSA>(r)) << 4)) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int idx = t + i * kThreads, r = idx / CPB, ch = idx - r * CPB;
-      *reinterpret_cast<u32x4*>(sB + r * RSB + ch * 16) = rb[i];
+      *reinterpret_cast<u32x4*>(sB + r * RSB + ((ch ^ swz<RSB>(r)) << 4)) = rb[i];
     }
   };
 
@@ -310,7 +326,7 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(const WgradArgs a) 
   auto store = [&](int st, const u32x4& rd, const u32x4 (&rx)[LX]) {
     char* sD = smem + st * STAGE;
     char* sX = sD + DY_BYTES;
-    *reinterpret_cast<u32x4*>(sD + (t >> 3) * RS + (t & 7) * 16) = rd;
+    *reinterpret_cast<u32x4*>(sD + (t >> 3) * RS + (((t & 7) ^ swz<RS>(t >> 3)) << 4)) = rd;
 #pragma unroll
     for (int i = 0; i < LX; ++i) {
       const int idx = t + i * kThreads;

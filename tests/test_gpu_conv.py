@@ -275,8 +275,15 @@ def test_conv23_matches_unfused(C, case):
     ref = C.conv2d_ref(h2.contiguous(memory_format=CL), w3, residual=res)
     assert got.shape == ref.shape and got.is_contiguous(memory_format=CL)
     torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
-    # and bit-for-bit against the unfused native pair
-    h2n = C.conv2d(x, w2, b2, stride=stride, padding=1, act="relu")
+    # and bit-for-bit against the unfused native pair on the per-tap kernel
+    # (same K order; the halo kernel sums channel-block major, tap minor)
+    from vgpu.native import load_kernels
+    lib = load_kernels()
+    lib.vgpu_conv_set_halo(0)
+    try:
+        h2n = C.conv2d(x, w2, b2, stride=stride, padding=1, act="relu")
+    finally:
+        lib.vgpu_conv_set_halo(-1)
     unf = C.conv2d(h2n, w3, residual=res)
     torch.testing.assert_close(got, unf, atol=0, rtol=0)
 

@@ -274,9 +274,8 @@ def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, ks: int, *, stride: int = 1,
 
 
 # Weight gradient in training: the native kernel where it measured ahead of
-# MIOpen — few output tiles over a long pixel reduction: 1x1 convolutions over
-# ≥ 32k output pixels (ResNet stages 1-2 at ai-benchmark sizes) and stride-1
-# 3x3 over ≥ 64k (stage 1, on the tap-fused kernel); profiles/wgrad_r1.md.
+# MIOpen: every 1x1 convolution, and stride-1 3x3 over ≥ 64k output pixels
+# (stage 1, on the tap-fused kernel); profiles/wgrad_r1.md, profiles/r4/train.
 # MIOpen elsewhere.  VGPU_CONV_WGRAD=0: always MIOpen; =all: always native.
 _WGRAD_MODE = os.environ.get("VGPU_CONV_WGRAD", "auto")
 
@@ -287,7 +286,10 @@ def _wgrad_native(dy: torch.Tensor, ks: int, stride: int) -> bool:
     if _WGRAD_MODE == "all":
         return True
     pixels = dy.shape[0] * dy.shape[2] * dy.shape[3]
-    return (ks == 1 and pixels >= 32768) or (ks == 3 and stride == 1 and pixels >= 65536)
+    # Every 1x1 (stride 1 or 2) since the swizzled LDS images (round 4:
+    # 23-36 us vs MIOpen's 27-43 us before its zero-fill and cast passes,
+    # profiles/r4/train/convtrain_wgrad_swizzle.log); 3x3 only on stage 1.
+    return ks == 1 or (ks == 3 and stride == 1 and pixels >= 65536)
 
 
 class _ConvTrainFn(torch.autograd.Function):
