@@ -182,7 +182,23 @@ int cumask_reapply_all() {
     if (mask_for_device(q.second, *a, m)) {
       apply_mask(q.first, q.second, *a);
     } else {
-      real_cu_set_mask(q.first, 0, nullptr);  // all CUs
+      // Back to every CU: an explicit all-ones mask.  A zero-length mask is not
+      // a reset (ROCr leaves the queue on its previous CUs), which kept an
+      // auto pod on its spatial claim through the time-shared window after it
+      // (profiles/r4: the A/B/A windows disagreed 554 vs 297 dispatches/s).
+      const uint32_t cus = a->cus ? a->cus : 256;
+      const uint32_t bits = std::min<uint32_t>(((cus + 31) / 32) * 32, VGPU_CU_MASK_WORDS * 64);
+      uint32_t words32[VGPU_CU_MASK_WORDS * 2];
+      for (uint32_t i = 0; i < VGPU_CU_MASK_WORDS * 2; ++i) {
+        const uint32_t lo = 32 * i;
+        words32[i] = cus <= lo ? 0u : (cus >= lo + 32 ? ~0u : ((1u << (cus - lo)) - 1));
+      }
+      const hsa_status_t rc = real_cu_set_mask(q.first, bits, words32);
+      if (rc != HSA_STATUS_SUCCESS && (int)rc != (int)HSA_STATUS_CU_MASK_REDUCED)
+        VLOG_WARN("hsa_amd_queue_cu_set_mask (all CUs) failed on device %d: %d", q.second, (int)rc);
+      else
+        VLOG_INFO("device %d queue %p: CU mask reset to all %u CUs", q.second, (void*)q.first, cus);
+      trace_emit(VGPU_EV_QUEUE, q.second, (uint64_t)(uintptr_t)q.first, (uint64_t)cus);
     }
     ++n;
   }

@@ -260,6 +260,17 @@ void configure() {
       if (L.cap < L.quantum) L.cap = L.quantum;
       L.tokens.store(L.cap);
       L.win_start = mono_ns();
+      // Re-activated (an auto member back from CUs of its own): markers left
+      // from before were not reaped meanwhile, so the busy interval and the
+      // board's fair-share mark still date from then.  Charging that whole gap
+      // on the first poll overdrew the bucket and held the pod through the
+      // next time-shared window (its A/B/A windows disagreed 2:1, profiles/r4).
+      std::lock_guard<std::mutex> g(L.mu);
+      const uint64_t now = mono_ns();
+      L.act_mark_ns = L.last_poll_ns = now;
+      L.occ_last_ns = L.occ_window_start = now;
+      L.occ_busy_acc = L.occ_mark_acc = 0;
+      if (L.board) (void)board_charge(L.board, L.board_slot, 0, L.outstanding.load() == 0);
     }
     L.active = want;
     any |= want;
