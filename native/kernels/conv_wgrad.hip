@@ -420,12 +420,16 @@ hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s) {
 
 namespace {
 int g_wgrad3 = -1;  // VGPU_CONV_WGRAD3=0 disables the tap-fused 3x3 path (A/B)
-bool wgrad3_eligible(int KS, int stride, int pad) {
+// The tap-fused 3x3 kernel wins on long pixel reductions (ResNet stage 1:
+// 44.6-47.4 us vs 55.8-57.7 per tap); from stage 2 on the per-tap GEMMs on the
+// swizzled images are faster (43.3 vs 54.5 at 38k pixels, 44.1 vs 54.6 at 9.7k;
+// profiles/r4/train/convtrain_wgrad_*.log).
+bool wgrad3_eligible(int KS, int stride, int pad, int64_t P) {
   if (g_wgrad3 < 0) {
     const char* v = getenv("VGPU_CONV_WGRAD3");
     g_wgrad3 = (v && v[0] == '0') ? 0 : 1;
   }
-  return g_wgrad3 == 1 && KS == 3 && pad == 1 && (stride == 1 || stride == 2);
+  return g_wgrad3 == 1 && KS == 3 && pad == 1 && (stride == 1 || stride == 2) && P >= 65536;
 }
 
 // Split-K factor for a shape; -1 = unsupported.
@@ -433,7 +437,7 @@ int64_t wgrad_splits(int N, int H, int W, int C, int Cout, int KS, int stride, i
   const int OH = (H + 2 * pad - KS) / stride + 1, OW = (W + 2 * pad - KS) / stride + 1;
   if (OH < 1 || OW < 1 || C % 64 || Cout % 64) return -1;
   const int64_t P = (int64_t)N * OH * OW;
-  const bool fused3 = wgrad3_eligible(KS, stride, pad);
+  const bool fused3 = wgrad3_eligible(KS, stride, pad, P);
   const int bm = fused3 ? 64 : Cout % 128 == 0 ? 128 : 64, bn = fused3 ? 64 : C % 128 == 0 ? 128 : 64;
   const int64_t tiles = fused3 ? (int64_t)(C / 64) * (Cout / 64) : (int64_t)(KS * KS * C / bn) * (Cout / bm);
   const int64_t steps_total = fused3 ? (int64_t)N * OH * ((OW + 31) / 32) : (P + KP - 1) / KP;
@@ -500,7 +504,7 @@ VGPU_API int vgpu_conv_wgrad_nhwc(const void* dy, const void* x, void* dw, void*
   a.splits = (int)sp;
   a.dw = static_cast<uint16_t*>(dw);
   hipError_t e;
-  if (wgrad3_eligible(KS, stride, pad)) {
+  if (wgrad3_eligible(KS, stride, pad, P)) {
     a.nseg = (a.OW + 31) / 32;
     const int64_t steps_total = (int64_t)N * a.OH * a.nseg;
     a.steps = (int)((steps_total + a.splits - 1) / a.splits);

@@ -378,7 +378,26 @@ def vmemcopy(mib: int = 512) -> dict:
     dst2.copy_(hp, non_blocking=True)  # async H2D from pinned memory
     torch.cuda.synchronize()
     res["after_async_h2d_GBps"], e3 = read_gbps(dst2, 7)
-    res["errors"] = e0 + e1 + e2 + e3
+    # 2-D copies and memsets.  hipMemcpy2D host -> range
+    # (4 KiB rows: the pattern survives, pitch = width), then hipMemset over
+    # the first half of another range and the pattern refilled on the GPU.
+    hip = ctypes.CDLL("libamdhip64.so")
+    dst3 = torch.empty(n, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    w = 4096
+    rc2 = hip.hipMemcpy2D(ctypes.c_void_p(dst3.data_ptr()), ctypes.c_size_t(w), ctypes.c_void_p(hp.data_ptr()),
+                          ctypes.c_size_t(w), ctypes.c_size_t(w), ctypes.c_size_t(n // w), 1)  # HostToDevice
+    torch.cuda.synchronize()
+    res["memcpy2d_rc"] = rc2
+    res["after_memcpy2d_GBps"], e4 = read_gbps(dst3, 7)
+    rc3 = hip.hipMemset(ctypes.c_void_p(dst2.data_ptr()), 0, ctypes.c_size_t(n // 2))
+    torch.cuda.synchronize()
+    res["memset_rc"] = rc3
+    res["memset_zeroed"] = bool(int(dst2[: n // 2].count_nonzero()) == 0)
+    K.fill_pattern(dst2, 7)
+    torch.cuda.synchronize()
+    res["after_memset_GBps"], e5 = read_gbps(dst2, 7)
+    res["errors"] = e0 + e1 + e2 + e3 + e4 + e5
     res["ranges_end"] = ranges()
     return res
 
@@ -543,12 +562,140 @@ def asynccap(cap_mib: int = 8192, graph_mib: int = 1024) -> dict:
             "backend": os.environ.get("PYTORCH_HIP_ALLOC_CONF", ""), "phases": phases}
 
 
+def _sysfs_vram(dev: int = 0) -> tuple[int, int] | None:
+    """(total, used) bytes from amdgpu's VRAM counters (they count KFD SVM pages,
+    which hipMemGetInfo does not); None when unreadable."""
+    import ctypes
+    buf = ctypes.create_string_buffer(64)
+    if ctypes.CDLL("libamdhip64.so").hipDeviceGetPCIBusId(buf, 64, dev) != 0:
+        return None
+    base = f"/sys/bus/pci/devices/{buf.value.decode().lower()}"
+    try:
+        with open(f"{base}/mem_info_vram_total") as f:
+            total = int(f.read())
+        with open(f"{base}/mem_info_vram_used") as f:
+            used = int(f.read())
+        return total, used
+    except OSError:
+        return None
+
+
+def vmemfull(gib: int = 4) -> dict:
+    """The full-HBM migration case (native/probes/svm_probe.hip
+    part F): an application-managed range of `gib` GiB, filled and moved to host
+    memory; a plain balloon then leaves gib/2 GiB of HBM free; the application
+    prefetches the whole range back into HBM.  Under the shim the prefetch is cut
+    to the free HBM beyond VGPU_VMEM_HEADROOM_MB, so KFD is never asked to
+    migrate into a full device.  Reports the prefetch time, the data check, the
+    read bandwidth and physical free HBM before and after."""
+    import ctypes
+
+    import torch
+    from vgpu.native import load_kernels
+    import faulthandler
+    faulthandler.dump_traceback_later(60, repeat=True)
+    hip = ctypes.CDLL("libamdhip64.so")
+    kl = load_kernels()
+    n = gib << 30
+    vr = _sysfs_vram()
+    if vr is None:
+        return {"error": "sysfs VRAM counters unreadable"}
+    torch.empty(1, device="cuda")
+    ptr = ctypes.c_void_p()
+    rc = hip.hipMallocManaged(ctypes.byref(ptr), ctypes.c_size_t(n), ctypes.c_uint(1))
+    if rc:
+        return {"error": f"hipMallocManaged {rc}"}
+    s0 = ctypes.c_void_p(0)
+    kl.vgpu_fill_pattern(ptr, n, 77, s0)
+    torch.cuda.synchronize()
+    hip.hipMemPrefetchAsync(ptr, ctypes.c_size_t(n), ctypes.c_int(-1), s0)
+    torch.cuda.synchronize()
+    total, used = _sysfs_vram()
+    leave = n // 2
+    balloon_bytes = max(0, total - used - leave)
+    balloon = torch.empty(balloon_bytes, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    free_before = (lambda t: t[0] - t[1])(_sysfs_vram())
+    t0 = time.time()
+    rc = hip.hipMemPrefetchAsync(ptr, ctypes.c_size_t(n), ctypes.c_int(0), s0)
+    torch.cuda.synchronize()
+    dt = time.time() - t0
+    free_after = (lambda t: t[0] - t[1])(_sysfs_vram())
+    err = torch.zeros(1, dtype=torch.int64, device="cuda")
+    kl.vgpu_verify_pattern(ptr, n, 77, ctypes.c_void_p(err.data_ptr()), s0)
+    torch.cuda.synchronize()
+    errors = int(err.item())
+    t1 = time.time()
+    for _ in range(3):
+        kl.vgpu_verify_pattern(ptr, n, 77, ctypes.c_void_p(err.data_ptr()), s0)
+    torch.cuda.synchronize()
+    gbps = round(3 * n / (time.time() - t1) / 1e9, 1)
+    del balloon
+    torch.cuda.empty_cache()
+    hip.hipFree(ptr)
+    faulthandler.cancel_dump_traceback_later()
+    return {"bytes": n, "total": total, "used_at_start": used, "balloon": balloon_bytes,
+            "free_before": free_before, "free_after": free_after,
+            "prefetch_rc": rc, "prefetch_s": round(dt, 3), "errors": errors, "read_GBps": gbps,
+            "headroom_mb": int(os.environ.get("VGPU_VMEM_HEADROOM_MB", "2048"))}
+
+
+def evictee(gib: int = 64, block_gib: int = 4) -> dict:
+    """The low-priority side of an evicting suspend.  Allocates
+    `gib` GiB in `block_gib` blocks (managed ranges under VGPU_SUSPEND_EVICT),
+    fills each with the K3 pattern, prints `READY {json}` and then serves
+    commands read from stdin: `STATS` (one `STATS {json}` line: vmem counters,
+    host bytes), `VERIFY` (check every block, report errors and read GB/s) and
+    `EXIT`.  The driver suspends / resumes it with SIGUSR2 / SIGUSR1 in between."""
+    import ctypes
+
+    import torch
+    from vgpu.ops import kernels as K
+    lib = ctypes.CDLL(None)
+    host_bytes = lib.vgpu_self_host_bytes
+    host_bytes.restype = ctypes.c_uint64
+
+    def stats():
+        v = (ctypes.c_uint64 * 5)()
+        lib.vgpu_self_vmem_stats(v)
+        return {"swap_in": v[0], "swap_out": v[1], "moves": v[2], "in_hbm": v[3], "ranges": v[4],
+                "host_bytes": int(host_bytes(0))}
+
+    blocks = []
+    for i in range(gib // block_gib):
+        t = torch.empty(block_gib << 30, dtype=torch.uint8, device="cuda")
+        K.fill_pattern(t, 100 + i)
+        blocks.append(t)
+    torch.cuda.synchronize()
+    print("READY " + json.dumps(stats()), flush=True)
+    res = {}
+    for line in sys.stdin:
+        cmd = line.strip()
+        if cmd == "STATS":
+            print("STATS " + json.dumps(stats()), flush=True)
+        elif cmd == "VERIFY":
+            t0 = time.time()
+            errs = sum(K.verify_pattern(b, 100 + i) for i, b in enumerate(blocks))
+            torch.cuda.synchronize()
+            first = time.time() - t0
+            t0 = time.time()
+            errs += sum(K.verify_pattern(b, 100 + i) for i, b in enumerate(blocks))
+            torch.cuda.synchronize()
+            res = {"errors": errs, "first_pass_s": round(first, 3),
+                   "second_pass_GBps": round(gib * (1 << 30) / (time.time() - t0) / 1e9, 1), **stats()}
+            print("VERIFIED " + json.dumps(res), flush=True)
+        elif cmd == "EXIT":
+            break
+    return res
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     cmd = argv.pop(0) if argv else "census"
     nums = [int(a) for a in argv]
     out = {"census": census, "busy": busy, "cap": cap, "smi": smi, "graph": graph, "arrays": arrays,
-           "progress": progress, "vmem": vmem, "vmemcopy": vmemcopy, "capheld": capheld, "asynccap": asynccap, "rcclloop": rcclloop}[cmd](*nums)
+           "progress": progress, "vmem": vmem, "vmemcopy": vmemcopy, "capheld": capheld, "asynccap": asynccap, "rcclloop": rcclloop,
+           "vmemfull": vmemfull, "evictee": evictee}[cmd](*nums)
     out["shim"] = shim_stats()
     print("PROBE " + json.dumps(out), flush=True)
     return 0

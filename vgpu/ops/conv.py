@@ -274,8 +274,8 @@ def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, ks: int, *, stride: int = 1,
 
 
 # Weight gradient in training: the native kernel where it measured ahead of
-# MIOpen: every 1x1 convolution, and stride-1 3x3 over ≥ 64k output pixels
-# (stage 1, on the tap-fused kernel); profiles/wgrad_r1.md, profiles/r4/train.
+# MIOpen: every 1x1 convolution, and 3x3 over ≥ 8k output pixels (tap-fused
+# kernel on stage 1, per-tap GEMMs after); profiles/wgrad_r1.md, profiles/r4/train.
 # MIOpen elsewhere.  VGPU_CONV_WGRAD=0: always MIOpen; =all: always native.
 _WGRAD_MODE = os.environ.get("VGPU_CONV_WGRAD", "auto")
 
@@ -288,8 +288,10 @@ def _wgrad_native(dy: torch.Tensor, ks: int, stride: int) -> bool:
     pixels = dy.shape[0] * dy.shape[2] * dy.shape[3]
     # Every 1x1 (stride 1 or 2) since the swizzled LDS images (round 4:
     # 23-36 us vs MIOpen's 27-43 us before its zero-fill and cast passes,
-    # profiles/r4/train/convtrain_wgrad_swizzle.log); 3x3 only on stage 1.
-    return ks == 1 or (ks == 3 and stride == 1 and pixels >= 65536)
+    # profiles/r4/train/convtrain_wgrad_swizzle.log); 3x3 down to ResNet
+    # stage 3 (parity with MIOpen's kernel there, and no zero-fill / cast
+    # passes); stage 4 (2.4k pixels) stays on MIOpen (59 vs 44 us).
+    return ks == 1 or (ks == 3 and pixels >= 8192)
 
 
 class _ConvTrainFn(torch.autograd.Function):
