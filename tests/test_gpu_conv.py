@@ -376,3 +376,28 @@ def test_conv_wgrad_matches_fp32(C, n, c, h, w, cout, ks, stride, pad):
     torch.testing.assert_close(dw.float(), ref, atol=1e-2 * scale, rtol=1e-2)
     # deterministic: split-K partials are reduced in a fixed order
     assert torch.equal(dw, C.conv2d_wgrad(dy, x, ks, stride=stride, padding=pad))
+
+
+def test_dgrad_filters_batched_flip_matches_torch(C):
+    """One launch builds every stride-1 conv's data-gradient filter
+    (native/kernels/weights.hip): w'[c][kh][kw][co] = w[co][2-kh][2-kw][c],
+    bit-exact against transpose + flip, and _ConvTrainFn picks it up."""
+    from torch import nn
+    convs = [nn.Conv2d(64, 128, 3, padding=1, bias=False), nn.Conv2d(256, 64, 1, bias=False),
+             nn.Conv2d(128, 128, 3, padding=1, bias=False), nn.Conv2d(512, 1024, 1, bias=False),
+             nn.Conv2d(128, 128, 3, stride=2, padding=1, bias=False)]  # strided: not part of the set
+    for m in convs:
+        m.to("cuda", torch.bfloat16).to(memory_format=CL)
+    d = C.DgradFilters(convs)
+    assert len(d.convs) == 4
+    d.refresh()
+    torch.cuda.synchronize()
+    for m, wt in zip(d.convs, d.bufs):
+        ref = m.weight.transpose(0, 1)
+        if m.kernel_size[0] > 1:
+            ref = ref.flip(2, 3)
+        assert torch.equal(wt, ref.contiguous(memory_format=CL))
+        assert C._dgrad_filter(m.weight) is wt
+    with torch.no_grad():
+        convs[0].weight.add_(1)  # a changed weight is not served stale
+    assert C._dgrad_filter(convs[0].weight) is not d.bufs[0]

@@ -16,7 +16,8 @@ from torch import nn
 import torch.nn.functional as F
 
 from vgpu.ops.bn import batched_step_counters, bn_act, bn_act_res
-from vgpu.ops.conv import conv_train
+from vgpu.ops.conv import DgradFilters, conv_train
+from vgpu.ops.conv import native_train_enabled as _conv_train_native
 
 
 class PreActBottleneck(nn.Module):
@@ -89,6 +90,11 @@ class ResNetV2(nn.Module):
                 nn.init.zeros_(m.bias)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.training and torch.is_grad_enabled() and x.is_cuda and _conv_train_native():
+            # every stride-1 conv's data-gradient filter in one launch (vgpu.ops.conv.DgradFilters)
+            if getattr(self, "_dgrad", None) is None:
+                self._dgrad = DgradFilters([m for m in self.modules() if isinstance(m, nn.Conv2d)])
+            self._dgrad.refresh()
         with batched_step_counters():
             x = self.pool(self.stem(x))
             x = self.blocks(x)

@@ -83,6 +83,11 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_conv_wgrad_workspace.restype = i64
     lib.vgpu_conv_wgrad_nhwc.argtypes = [vp] * 4 + [i64] + [ci] * 8 + [vp]
     lib.vgpu_conv_wgrad_nhwc.restype = ci
+    lib.vgpu_wt_flip_tiles.argtypes = [ci, ci, ci]
+    lib.vgpu_wt_flip_tiles.restype = ci
+    lib.vgpu_wt_flip_batched.argtypes = [vp, ci, ci, vp]
+    lib.vgpu_wt_flip_batched.restype = ci
+    lib.vgpu_wt_desc_size.restype = ci
     for f in ("vgpu_bn_act_fwd_train", "vgpu_bn_act_bwd","vgpu_census", "vgpu_busy", "vgpu_gather_pages", "vgpu_scatter_pages",
               "vgpu_fill_pattern", "vgpu_verify_pattern", "vgpu_kernels_abi_version",
               "vgpu_bias_act_nhwc", "vgpu_scale_shift_act_nhwc", "vgpu_add_scale_shift_act_nhwc",
