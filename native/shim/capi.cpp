@@ -178,6 +178,11 @@ __attribute__((visibility("default"))) void vgpu_self_vmem_stats(uint64_t out[5]
   vmem_stats(&out[0], &out[1], &out[2], &out[3], &out[4]);
 }
 
+__attribute__((visibility("default"))) void vgpu_self_vmem_budget(int dev, uint64_t out[8]) {
+  ensure_init();
+  vmem_budget_books(dev, out);
+}
+
 __attribute__((visibility("default"))) uint64_t vgpu_self_host_bytes(int dev) {
   ensure_init();
   vgpu_proc_slot_t* sl = my_slot();

@@ -55,6 +55,7 @@
 // (plain_reserve: activations are placed ahead of weights).
 // VGPU_VMEM_MIGRATE=0 keeps the round-1 behaviour (pinned zero-copy spill).
 #include <pthread.h>
+#include <sys/mman.h>
 
 #include <new>
 
@@ -115,6 +116,8 @@ struct Knobs {
   // (SIGUSR2) can give the container's HBM back.
   bool suspend_evict = false;
   uint64_t plain_window_ms = 30000;  // plain high-water mark window (plain_reserve)
+  bool cut_pieces = true;            // VGPU_VMEM_CUT_PIECES=0: whole pieces only (A/B)
+  bool thp = false;                  // VGPU_VMEM_THP=1: madvise(MADV_HUGEPAGE) on managed ranges (A/B)
 };
 
 const Knobs& knobs() {
@@ -129,6 +132,8 @@ const Knobs& knobs() {
     if (const char* e = env_first("VGPU_VMEM_PIECE_MB")) v.piece = std::max<uint64_t>(2, strtoull(e, nullptr, 10)) << 20;
     v.suspend_evict = env_bool(env_first("VGPU_SUSPEND_EVICT"), false);
     if (const char* e = env_first("VGPU_VMEM_PLAIN_WINDOW_MS")) v.plain_window_ms = std::max(1ull, strtoull(e, nullptr, 10));
+    v.cut_pieces = env_bool(env_first("VGPU_VMEM_CUT_PIECES"), true);
+    v.thp = env_bool(env_first("VGPU_VMEM_THP"), false);
     if (const char* e = env_first("VGPU_VMEM_MANAGED_MIN_MB")) {
       const long long mb = atoll(e);
       v.managed_min = mb < 0 ? -1 : (int64_t)mb << 20;
@@ -390,6 +395,7 @@ bool promote_piece_locked(VRange* r) {
   uint64_t n = std::min<uint64_t>(k.piece, r->size - r->gpu_bytes);
   if (!n) return false;
   if (!room_for(r->dev, n)) {  // make_room_locked ran first
+    if (!k.cut_pieces) return false;
     n = room_left(r->dev, true) & ~(kGranule - 1);
     if (!n) return false;
   }
@@ -596,6 +602,9 @@ VRange* new_range(void** ptr, size_t size, int dev, hipError_t* rc) {
   // the GPU caches it (fine-grained managed memory bypasses them).
   (void)REAL_HIP(hipMemAdvise)(*ptr, size, hipMemAdviseSetCoarseGrain, dev);
   (void)REAL_HIP(hipGetLastError)();
+  // Host-resident parts are read in place over the host link; 2 MiB host pages
+  // let the GPU map them with larger fragments (fewer translation misses).
+  if (knobs().thp) (void)madvise(*ptr, size, MADV_HUGEPAGE);
   auto* r = new VRange((uintptr_t)*ptr, size, dev);
   r->last_use.store(g_tick.load());  // allocated now: in use now
   {
@@ -1082,6 +1091,27 @@ void vmem_stats(uint64_t* in_bytes, uint64_t* out_bytes, uint64_t* moves, uint64
   for (VRange* r : g_tab) gb += r->gpu_bytes;
   *gpu_bytes = gb;
   *ranges = g_tab.size();
+}
+
+// The budget's books on `dev`: budget, pod resident, this process's managed
+// bytes in HBM, plain bytes, plain reserve, managed bytes on the host,
+// managed ranges larger than 1 GiB partly in HBM, physical free HBM.
+void vmem_budget_books(int dev, uint64_t out[8]) {
+  for (int i = 0; i < 8; ++i) out[i] = 0;
+  if (dev < 0 || dev >= VGPU_MAX_DEVICES) return;
+  out[0] = phys_budget(dev);
+  out[1] = pod_resident(dev);
+  out[2] = promoted_bytes(dev);
+  out[3] = plain_now(dev);
+  out[4] = plain_reserve(dev);
+  std::shared_lock<std::shared_mutex> g(g_tab_mu);
+  for (VRange* r : g_tab) {
+    if (r->dev != dev) continue;
+    out[5] += r->size - r->gpu_bytes;
+    out[6] += r->gpu_bytes && r->gpu_bytes < r->size;
+  }
+  g.unlock();
+  out[7] = hbm_free(dev);
 }
 
 void vmem_stop() {

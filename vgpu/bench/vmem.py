@@ -262,12 +262,20 @@ def _stats_fn():
     if host_bytes is not None:
         host_bytes.restype = ctypes.c_uint64
 
+    books_fn = getattr(lib, "vgpu_self_vmem_budget", None)
+
     def stats():
         v = (ctypes.c_uint64 * 5)()
         if vstats is not None:
             vstats(v)
-        return {"swap_in": v[0], "swap_out": v[1], "moves": v[2], "managed_in_hbm": v[3], "managed_ranges": v[4],
-                "host_bytes": host_bytes(0) if host_bytes else 0}
+        out = {"swap_in": v[0], "swap_out": v[1], "moves": v[2], "managed_in_hbm": v[3], "managed_ranges": v[4],
+               "host_bytes": host_bytes(0) if host_bytes else 0}
+        if books_fn is not None:
+            b = (ctypes.c_uint64 * 8)()
+            books_fn(ctypes.c_int(0), b)
+            out["books"] = dict(zip(("budget", "pod_resident", "managed_in_hbm", "plain", "plain_reserve",
+                                     "managed_on_host", "partial_ranges", "hbm_free"), [int(x) for x in b]))
+        return out
     return stats
 
 
