@@ -729,6 +729,10 @@ hipError_t hipMemsetD32Async(hipDeviceptr_t, int, size_t, hipStream_t) { g_memse
 hipError_t hipMemset2D(void*, size_t, int, size_t, size_t) { g_memsets++; return hipSuccess; }
 hipError_t hipMemset2DAsync(void*, size_t, int, size_t, size_t, hipStream_t) { g_memsets++; return hipSuccess; }
 hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind k) { return fake_copy(d, s, n, k); }
+// Peer copies: copy engine, device to device; no page of a managed range moves.
+std::atomic<uint64_t> g_peer_copies{0};
+hipError_t hipMemcpyPeer(void*, int, const void*, int, size_t) { g_peer_copies++; return hipSuccess; }
+hipError_t hipMemcpyPeerAsync(void*, int, const void*, int, size_t, hipStream_t) { g_peer_copies++; return hipSuccess; }
 hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned int) { return hipSuccess; }
 // Device memory and managed ranges are "device"; anything else is unregistered host memory.
 hipError_t hipPointerGetAttributes(hipPointerAttribute_t* a, const void* p) {
@@ -1098,6 +1102,7 @@ int fake_hip_svm_move(const void* p, uint64_t n, int to_gpu) {
   }
   return 1;
 }
+uint64_t fake_hip_peer_copies() { return g_peer_copies.load(); }
 uint64_t fake_hip_prefetch_overflows() {
   std::lock_guard<std::mutex> g(g_mu);
   return g_prefetch_over;

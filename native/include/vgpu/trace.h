@@ -27,6 +27,7 @@ enum vgpu_trace_type {
   VGPU_EV_QUEUE = 8,         /* a = queue address, b = CUs in its mask (0 = all) */
   VGPU_EV_GPU_TIME = 9,      /* a = fair-share GPU ns charged, b = wall ns busy */
   VGPU_EV_MIGRATE = 10,      /* a = bytes, b = (ns << 1) | 1 to HBM, 0 to host */
+  VGPU_EV_COPY = 11,         /* peer copy: dev = destination, a = bytes, b = source device */
 };
 
 typedef struct vgpu_trace_event {

@@ -501,6 +501,32 @@ __attribute__((visibility("default"))) hipError_t hipMallocManaged(void** ptr, s
                        [&] { return REAL_HIP(hipMallocManaged)(ptr, size, flags); });
 }
 
+// Peer copies (the multi-GPU pod's device-to-device path; reference
+// cuMemcpyPeer): a copy engine moves the bytes, so no page of a managed range
+// migrates, but the ranges on either side are in use -- the pager learns it
+// as it does from a kernel launch.  Peer copies carry no compute charge.
+__attribute__((visibility("default"))) hipError_t hipMemcpyPeer(void* dst, int dst_dev, const void* src, int src_dev,
+                                                                size_t n) {
+  ensure_init();
+  if (st().enabled) {
+    vmem_note_use(dst, nullptr);
+    vmem_note_use(src, nullptr);
+    trace_emit(VGPU_EV_COPY, dst_dev, n, (uint64_t)src_dev);
+  }
+  return REAL_HIP(hipMemcpyPeer)(dst, dst_dev, src, src_dev, n);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpyPeerAsync(void* dst, int dst_dev, const void* src,
+                                                                     int src_dev, size_t n, hipStream_t stream) {
+  ensure_init();
+  if (st().enabled) {
+    vmem_note_use(dst, stream);
+    vmem_note_use(src, stream);
+    trace_emit(VGPU_EV_COPY, dst_dev, n, (uint64_t)src_dev);
+  }
+  return REAL_HIP(hipMemcpyPeerAsync)(dst, dst_dev, src, src_dev, n, stream);
+}
+
 // Application prefetches of managed memory: cut to what HBM holds beyond the
 // headroom, and left to the pager inside its own ranges (vmem_prefetch_allowed).
 static hipError_t prefetch_hook(const void* p, size_t n, int dev, const std::function<hipError_t(size_t)>& real) {

@@ -170,6 +170,8 @@ using hipIpcCloseMemHandle = hipError_t (*)(void*);
 using hipDeviceGetPCIBusId = hipError_t (*)(char*, int, int);
 using hipMemAdvise = hipError_t (*)(const void*, size_t, hipMemoryAdvise, int);
 using hipMemPrefetchAsync = hipError_t (*)(const void*, size_t, int, hipStream_t);
+using hipMemcpyPeer = hipError_t (*)(void*, int, const void*, int, size_t);
+using hipMemcpyPeerAsync = hipError_t (*)(void*, int, const void*, int, size_t, hipStream_t);
 using hipMemPrefetchAsync_v2 = hipError_t (*)(const void*, size_t, hipMemLocation, unsigned int, hipStream_t);
 using hipMemGetAddressRange = hipError_t (*)(hipDeviceptr_t*, size_t*, hipDeviceptr_t);
 using hipGetProcAddress = hipError_t (*)(const char*, void**, int, uint64_t,

@@ -167,7 +167,8 @@ void vmem_note_plain(int dev);
 // Bytes of an application prefetch of [p, p+n) to `dev` (< 0: host) that may run:
 // 0 for a range the pager owns, else at most the HBM free beyond the headroom.
 size_t vmem_prefetch_allowed(const void* p, size_t n, int dev);
-void vmem_budget_books(int dev, uint64_t out[8]);               // a plain buffer was placed: update the plain high-water mark
+void vmem_budget_books(int dev, uint64_t out[8]);
+void vmem_note_use(const void* p, hipStream_t stream);  // a peer copy touches p's range               // a plain buffer was placed: update the plain high-water mark
 void vmem_scan_args(void** args, hipStream_t stream);    // HIP-Clang stub argument array
 void vmem_scan_extra(void** extra, hipStream_t stream);  // HIP_LAUNCH_PARAM_BUFFER_* kernarg blob
 // Graphs: ranges named by captured launches follow capture -> graph -> exec,

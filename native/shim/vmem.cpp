@@ -991,6 +991,17 @@ void vmem_scan_extra(void** extra, hipStream_t stream) {
   });
 }
 
+// A copy engine operation (peer copy) that reads or writes [p, p+n): the
+// ranges it touches are in use, as if a kernel had named them.
+void vmem_note_use(const void* p, hipStream_t stream) {
+  if (g_count.load(std::memory_order_relaxed) == 0 || !p) return;
+  scan_for(stream, [&] {
+    const uint64_t tick = g_tick.load(std::memory_order_relaxed);
+    std::shared_lock<std::shared_mutex> g(g_tab_mu);
+    if (!g_tab.empty()) touch_word((uintptr_t)p, tick);
+  });
+}
+
 unsigned long long vmem_capture_begin_id(hipStream_t stream) { return capture_id(stream); }
 
 void vmem_capture_ended(unsigned long long cid, hipGraph_t graph) {

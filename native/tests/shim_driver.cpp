@@ -36,6 +36,7 @@ extern "C" uint64_t fake_hsa_pool_used(int dev);
 extern "C" int fake_hsa_tools_loaded();
 extern "C" uint64_t fake_hip_managed_gpu_bytes(const void* p);
 extern "C" uint64_t fake_hip_prefetch_overflows();
+extern "C" uint64_t fake_hip_peer_copies();
 extern "C" uint64_t fake_hip_host_touch_bytes();
 extern "C" uint64_t fake_hip_memsets();
 extern "C" hipGraph_t fake_hip_graph_create(const unsigned* grids, int n, unsigned child_grid);
@@ -492,6 +493,29 @@ int main(int argc, char** argv) {
            (unsigned long long)fake_hip_physical_used(dev), (unsigned long long)peak_phys);
     for (int i = 0; i < 5; ++i) hipFree(p[i]);
     for (int i = 0; i < 3; ++i) hipFree(w[i]);
+    return 0;
+  }
+
+  if (sc == "peer") {
+    // A managed range that spilled (HBM full of plain buffers) is used only by
+    // peer copies: once HBM has room the pager promotes it, as it would after
+    // a kernel launch named it.
+    const size_t G = 1ull << 30;
+    void** q = new void*[4]();
+    int ra = hipMalloc(&q[0], 6 * G), rb = hipMalloc(&q[1], 4 * G);  // plain 6 GiB, then a 4 GiB spill (8 GiB device)
+    const uint64_t before = fake_hip_managed_gpu_bytes(q[1]);
+    usleep(300000);  // past the hot window of its allocation: only the copies below use it
+    hipFree(q[0]);   // room
+    usleep(100000);
+    const uint64_t idle = fake_hip_managed_gpu_bytes(q[1]);
+    for (int i = 0; i < 50; ++i) {
+      hipMemcpyPeerAsync(q[2] ? q[2] : (void*)0x1000, 1, (char*)q[1] + 4096, dev, 1 << 20, nullptr);
+      usleep(10000);
+    }
+    printf("alloc_a=%d\nalloc_b=%d\nb_gpu_before=%llu\nb_gpu_idle=%llu\nb_gpu_after=%llu\npeer_copies=%llu\n", ra,
+           rb, (unsigned long long)before, (unsigned long long)idle, (unsigned long long)fake_hip_managed_gpu_bytes(q[1]),
+           (unsigned long long)fake_hip_peer_copies());
+    hipFree(q[1]);
     return 0;
   }
 

@@ -237,6 +237,17 @@ def test_vmem_budget_fills_and_plain_buffers_keep_their_room(native_build):
     assert int(o["peak_phys"]) <= 8 * GiB
 
 
+def test_peer_copies_mark_managed_ranges_in_use(native_build):
+    """hipMemcpyPeer{,Async} (the multi-GPU pod's device-to-device path;
+    reference cuMemcpyPeer) pass through, and the managed ranges they touch
+    count as used: a spilled range that only peer copies read is promoted once
+    HBM has room, as after a kernel launch."""
+    o = run("peer", env=VMEM_ENV)
+    assert (o["alloc_a"], o["alloc_b"]) == ("0", "0") and o["peer_copies"] == "50"
+    assert int(o["b_gpu_idle"]) < 4 * GiB          # not in use: the rest stays on the host
+    assert int(o["b_gpu_after"]) == 4 * GiB        # read by peer copies: promoted
+
+
 def test_application_prefetch_never_overfills_hbm(native_build):
     """VERDICT r3 #3 (the full-HBM hang): asked to migrate more than free VRAM,
     KFD evicts the process's own buffers (profiles/vmem_r2.md).  The fake

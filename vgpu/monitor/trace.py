@@ -18,7 +18,7 @@ import os
 
 MAGIC = 0x56545243
 TYPES = {1: "alloc", 2: "free", 3: "oom", 4: "launch", 5: "throttle", 6: "suspend",
-         7: "priority_block", 8: "queue", 9: "gpu_time", 10: "migrate"}
+         7: "priority_block", 8: "queue", 9: "gpu_time", 10: "migrate", 11: "copy"}
 
 
 class Event(ctypes.Structure):
