@@ -496,6 +496,35 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (sc == "launchcost") {
+    // Host cost of a tracked eager launch (weak item r3 #7): T threads, each
+    // launching K kernels back to back on its own stream; ns per launch.
+    const int T = argc > 2 ? atoi(argv[2]) : 1;
+    const int K = argc > 3 ? atoi(argv[3]) : 20000;
+    void* p = nullptr;
+    hipMalloc(&p, 4096);  // runtime init
+    std::atomic<int> go{0};
+    std::vector<std::thread> th;
+    struct timespec a, b;
+    for (int i = 0; i < T; ++i)
+      th.emplace_back([&, i] {
+        hipStream_t st = (hipStream_t)(uintptr_t)(0x1000 + 64 * i);
+        while (!go.load()) {
+        }
+        for (int k = 0; k < K; ++k) hipLaunchKernel((const void*)&main, dim3(64), dim3(256), nullptr, 0, st);
+      });
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    go = 1;
+    for (auto& t : th) t.join();
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    hipDeviceSynchronize();
+    const double ns = (b.tv_sec - a.tv_sec) * 1e9 + (b.tv_nsec - a.tv_nsec);
+    printf("threads=%d\nlaunches=%d\nns_per_launch=%.1f\nns_per_launch_per_thread=%.1f\n", T, T * K,
+           ns / ((double)T * K), ns / K);
+    hipFree(p);
+    return 0;
+  }
+
   if (sc == "peer") {
     // A managed range that spilled (HBM full of plain buffers) is used only by
     // peer copies: once HBM has room the pager promotes it, as it would after

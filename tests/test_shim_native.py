@@ -934,3 +934,14 @@ def test_limiter_occupancy_cross_check_under_early_markers(native_build, tmp_pat
         assert duty > 0.5, o       # the hole: markers alone under-charge
     else:
         assert 0.18 < duty < 0.36, (duty, o["_stderr"][-1500:])
+
+
+def test_launch_cost_scenario_reports_per_launch_host_cost(native_build, tmp_path):
+    """The launch-cost probe behind docs/benchmarks.md (round 4): T threads
+    launching on their own streams under the temporal limiter; every launch is
+    tracked (one marker each) and the run completes."""
+    env = {"VGPU_FAKE_KERNEL_US": "0", "VGPU_LOCK_DIR": str(tmp_path), "VGPU_DEVICE_UUID_0": "GPU-lc",
+           "VGPU_DEVICE_CU_LIMIT_0": "50", "VGPU_CU_MASK_FROM_LIMIT": "false", "VGPU_CU_SHARE": "temporal"}
+    o = run("launchcost", 4, 2000, env=env, timeout=120)
+    assert o["threads"] == "4" and o["launches"] == "8000"
+    assert 0 < float(o["ns_per_launch"]) < 1e6
