@@ -31,6 +31,7 @@
 // XCD-aware (bijective remap) so the N-tiles sharing an A panel run on one
 // XCD's L2.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -42,6 +43,7 @@ namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 // Native 16-B vector (HIP's u32x4 is a class; copies of it go through memcpy
 // and defeat register promotion of the staging arrays).
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
@@ -846,10 +848,13 @@ hipError_t launch_big(ConvArgs a, hipStream_t s) {
 // thread issues the same DMA count and the counted vmcnt waits stay exact.
 // NMAJOR: workgroups of one XCD share an N tile (weight panels stay in that
 // XCD's L2 when the whole filter does not fit, e.g. stage 4: 4.7 MB).
-template <int BM, int BN, int HPMAX>
+// M32: the wave's 64 x 64 tile as 2 x 2 v_mfma_f32_32x32x16_bf16 instead of
+// 4 x 4 16x16x32 -- half the MFMA issues for the same operand bytes, and 18
+// instead of 36 A-address registers (A/B knob VGPU_CONV_HALO_M32).
+template <int BM, int BN, int HPMAX, bool M32 = false>
 __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvArgs a) {
   constexpr int T = BM * BN / 64, WN = BN / 64;
-  constexpr int TM = 4, TN = 4;                       // wave tile 64 x 64
+  constexpr int TM = M32 ? 2 : 4, TN = M32 ? 2 : 4;  // wave tile 64 x 64
   constexpr int RPI = T / 8;                          // LDS rows (128 B) per DMA instruction
   constexpr int HI = HPMAX / RPI, BR = BN / RPI;      // DMA instructions per thread: halo, panel
   constexpr int HSTAGE = HPMAX * 128, BSTAGE = BN * 128;
@@ -924,7 +929,7 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
   uint32_t aaddr[9][TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int m = m0 + wm * 64 + i * 16 + fr;
+    const int m = M32 ? m0 + wm * 64 + i * 32 + (lane & 31) : m0 + wm * 64 + i * 16 + fr;
     const bool mok = m < a.M;
     const int row = (mok ? m : m0) / W;
     const int ow = (mok ? m : m0) - row * W, oh = row % H;
@@ -935,16 +940,57 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
         const int ih = oh + kh - 1, iw = ow + kw - 1;
         const bool v = mok & ((unsigned)ih < (unsigned)H) & ((unsigned)iw < (unsigned)W);
         const int h = v ? (row + kh - 1 - g_lo) * W + iw : ZROW;
-        const uint32_t a0 = (uint32_t)(h * 128 + ((fk ^ (h & 7)) << 4));
-        aaddr[kh * 3 + kw][i] = a0 | ((a0 ^ 64u) << 16);
+        if constexpr (M32) {
+          // k-step ks (16 channels) of lane half kb reads chunk 2·ks + kb: the
+          // address of ks = that of ks 0 XOR (ks << 5)
+          aaddr[kh * 3 + kw][i] = (uint32_t)(h * 128 + (((lane >> 5) ^ (h & 7)) << 4));
+        } else {
+          const uint32_t a0 = (uint32_t)(h * 128 + ((fk ^ (h & 7)) << 4));
+          aaddr[kh * 3 + kw][i] = a0 | ((a0 ^ 64u) << 16);
+        }
       }
   }
 
-  f32x4_t acc[TM][TN];
+  typedef typename std::conditional<M32, f32x16_t, f32x4_t>::type acc_t;
+  acc_t acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) acc[i][j] = acc_t{};
+
+  // 32x32x16: four 16-channel k-steps per tap; operands of step ks+1 are read
+  // while step ks multiplies (lgkmcnt(4): the newer 4 reads may stay in flight).
+  auto compute32 = [&](int tap, const char* sH, const char* sB) {
+    bf16x8_t af[2][TM], bfr[2][TN];
+    auto rd = [&](int ks, int buf) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[buf][i] = *reinterpret_cast<const bf16x8_t*>(sH + (aaddr[tap][i] ^ (uint32_t)(ks << 5)));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[buf][j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(wn * 64 + j * 32 + (lane & 31), ks * 2 + (lane >> 5)));
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int cur = ks & 1;
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks < 3) {
+        rd(ks + 1, cur ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(lgkm_imm(TM + TN));
+      } else {
+        __builtin_amdgcn_s_waitcnt(kLgkm0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          if constexpr (M32)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][i], bfr[cur][j], acc[i][j], 0, 0, 0);
+    }
+  };
 
   auto compute = [&](int tap, const char* sH, const char* sB) {
     bf16x8_t af[2][TM], bfr[2][TN];
@@ -961,7 +1007,8 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+          if constexpr (!M32)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
     };
     rd(0);
     __builtin_amdgcn_sched_barrier(0);
@@ -1003,7 +1050,10 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
         __builtin_amdgcn_s_waitcnt(vmcnt_imm(BR));
       }
       __builtin_amdgcn_s_barrier();
-      compute(tap, sH, smem + 2 * HSTAGE + bs * BSTAGE);
+      if constexpr (M32)
+        compute32(tap, sH, smem + 2 * HSTAGE + bs * BSTAGE);
+      else
+        compute(tap, sH, smem + 2 * HSTAGE + bs * BSTAGE);
       __builtin_amdgcn_s_waitcnt(kLgkm0);
       __builtin_amdgcn_s_barrier();
       bs ^= 1;
@@ -1025,16 +1075,29 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
     bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
     bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
   }
+  // 16x16 tiles: pass p = row tile i.  32x32 tiles: pass p = half (p & 1) of row
+  // tile p >> 1; lane l holds rows 8b + 4(l >> 5) + e (b = 0..3) of column l & 31.
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
+  for (int p = 0; p < 4; ++p) {
+    if constexpr (M32) {
+      const int i = p >> 1, hb = (p & 1) * 2;
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) sC[(fk * 4 + e) * CS + j * 16 + fr] = acc[i][j][e];
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            sC[(8 * b + 4 * (lane >> 5) + e) * CS + j * 32 + (lane & 31)] = acc[i][j][4 * (hb + b) + e];
+    } else {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sC[(fk * 4 + e) * CS + j * 16 + fr] = acc[p][j][e];
+    }
     __builtin_amdgcn_s_waitcnt(kLgkm0);
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
-      const int row = erow + 8 * r, m = m0 + wm * 64 + i * 16 + row;
+      const int row = erow + 8 * r, m = m0 + wm * 64 + p * 16 + row;
       const float4 c0 = *reinterpret_cast<const float4*>(sC + row * CS + ecol);
       const float4 c1 = *reinterpret_cast<const float4*>(sC + row * CS + ecol + 4);
       float v[8] = {c0.x + bb[0], c0.y + bb[1], c0.z + bb[2], c0.w + bb[3],
@@ -1062,6 +1125,15 @@ bool halo_enabled() {
 
 unsigned long long g_halo_launches = 0;  // vgpu_conv_halo_launches (tests: the halo path ran)
 
+int g_halo_m32 = -1;  // VGPU_CONV_HALO_M32=1: the 32x32x16 MFMA variant (A/B)
+bool halo_m32() {
+  if (g_halo_m32 < 0) {
+    const char* v = getenv("VGPU_CONV_HALO_M32");
+    g_halo_m32 = (v && v[0] == '1') ? 1 : 0;
+  }
+  return g_halo_m32 == 1;
+}
+
 template <int BM, int BN, int HPMAX>
 hipError_t launch_halo(ConvArgs a, hipStream_t s) {
   ++g_halo_launches;
@@ -1070,7 +1142,10 @@ hipError_t launch_halo(ConvArgs a, hipStream_t s) {
   a.nwg = a.nM * a.nN;
   // N-major placement when the filter outgrows an XCD's L2 share (4 MiB).
   a.nmajor = (int64_t)a.Cout * a.K * 2 > ((int64_t)5 << 19) ? 1 : 0;
-  hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
+  if (halo_m32())
+    hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, true>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, false>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
   return hipGetLastError();
 }
 
@@ -2091,6 +2166,7 @@ VGPU_API void vgpu_conv_set_tile_m(int bm) { g_forced_bm = bm; }
 VGPU_API void vgpu_conv_set_big(int mode) { g_forced_big = mode; }  // -1 env/heuristic, 0 off, 1 when eligible
 VGPU_API void vgpu_conv_set_halo(int mode) { g_forced_halo = mode; }  // -1 env, 0 off, 1 on, 2/3 BM 256/128
 VGPU_API unsigned long long vgpu_conv_halo_launches() { return g_halo_launches; }
+VGPU_API void vgpu_conv_set_halo_m32(int on) { g_halo_m32 = on < 0 ? -1 : (on ? 1 : 0); }  // -1: env
 
 // Fused conv2 (3x3, pad 1, stride s, C = W → W, bias + ReLU) + conv3 (1x1,
 // W → 4W) + residual; with w1n, also the next block's conv1 (1x1, 4W → W,

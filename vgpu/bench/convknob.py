@@ -20,6 +20,8 @@ from vgpu.bench.convnative import layer_shapes
 KNOBS = {
     # name: (setter, [(tag, value)])
     "halo": ("vgpu_conv_set_halo", [("off", 0), ("auto", -1), ("bm256", 2), ("bm128", 3)]),
+    # the halo kernel's MFMA shape (auto tile choice): 16x16x32 vs 32x32x16
+    "m32": ("vgpu_conv_set_halo_m32", [("m16", 0), ("m32", 1)]),
 }
 
 
