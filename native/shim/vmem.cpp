@@ -493,7 +493,12 @@ void pager_step(bool advance) {
       std::shared_lock<std::shared_mutex> g(g_tab_mu);
       if (std::find(g_tab.begin(), g_tab.end(), r) == g_tab.end()) continue;
     }
-    const uint64_t stale = tick > k.cold_ticks ? tick - k.cold_ticks : 0;
+    // Room for a hot range may come from any range that is not hot itself
+    // (unused for the hot window): hot ranges are never exchanged for each
+    // other, but a model whose traffic stopped a second ago gives way at once
+    // instead of after the 2 s cold window that new allocations wait for
+    // (a model switch started promoting one second earlier).
+    const uint64_t stale = tick > k.hot_ticks ? tick - k.hot_ticks : 0;
     while (r->gpu_bytes < r->size) {
       uint64_t n = std::min<uint64_t>(k.piece, r->size - r->gpu_bytes);
       (void)make_room_locked(r->dev, n, r, stale);  // what it could not free, a cut piece may still use
