@@ -308,7 +308,12 @@ class DgradFilters:
     takes a filter from here when the weight has not changed since."""
 
     def __init__(self, convs):
+        self._all = list(convs)
+        self._build()
+
+    def _build(self):
         import struct
+        convs = self._all
         self.convs = [c for c in convs if c.stride == (1, 1) and c.kernel_size[0] in (1, 3)
                       and c.weight.is_cuda and c.weight.dtype == torch.bfloat16
                       and c.weight.is_contiguous(memory_format=_CL) and c.groups == 1
@@ -330,11 +335,19 @@ class DgradFilters:
             raw += struct.pack("<QQiiii", w.data_ptr(), wt.data_ptr(), c.out_channels, c.in_channels, ks, tile0)
             tile0 += lib.vgpu_wt_flip_tiles(c.out_channels, c.in_channels, ks)
         self.tiles = tile0
+        self.ptrs = [c.weight.data_ptr() for c in self.convs]
         self.desc = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.convs[0].weight.device)
 
     def refresh(self) -> None:
         if self.desc is None:
             return
+        # The table holds raw weight addresses: a weight re-allocated since
+        # (model.to(...), load_state_dict with assign=True) would be read from
+        # freed memory, so rebuild first.
+        if any(c.weight.data_ptr() != p for c, p in zip(self.convs, self.ptrs)):
+            self._build()
+            if self.desc is None:
+                return
         rc = load_kernels().vgpu_wt_flip_batched(_ptr(self.desc), len(self.convs), self.tiles, _stream())
         if rc != 0:
             raise RuntimeError(f"vgpu_wt_flip_batched: error {rc}")
