@@ -32,9 +32,11 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kUnroll = 4;           // rows in flight per thread
+constexpr int kUnroll = 4;           // rows in flight per thread (default; 8 via vgpu_bn_set_tuning)
 constexpr int kMaxChunk = 512;       // channels per reduction workgroup
-constexpr int kTargetBlocks = 1024;  // reduction grid ≈ 4 workgroups per CU
+constexpr int kTargetBlocks = 1024;  // reduction grid ≈ 4 workgroups per CU (default)
+int g_target_blocks = kTargetBlocks;  // A/B: vgpu_bn_set_tuning
+int g_unroll = kUnroll;
 constexpr int kFinC = 8;             // finalize: channels per workgroup
 constexpr int kFinG = 64;            //           partial groups per workgroup (tree-merged)
 constexpr int kMaxGrid = 256 * 8;
@@ -82,7 +84,7 @@ __device__ __forceinline__ void load8(const float* __restrict__ p, float (&o)[8]
 // `rows_per_block` rows of one channel chunk into partial[blockIdx.x][c].
 //   kMode 0: (Σ (x - x₀), Σ (x - x₀)²)         x₀ = row 0 (the shift)
 //   kMode 1: (Σ dz, Σ dz · x̂)                   dz = dy · act'(x·s + t)
-template <int kMode, int kAct, typename P>
+template <int kMode, int kAct, typename P, int kU = kUnroll>
 __global__ void __launch_bounds__(kThreads) bn_reduce_kernel(
     const bf16x8* __restrict__ x, const bf16x8* __restrict__ dy, const P* __restrict__ gamma,
     const P* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -120,11 +122,11 @@ __global__ void __launch_bounds__(kThreads) bn_reduce_kernel(
   for (int j = 0; j < 8; ++j) a1[j] = a2[j] = 0.0f;
 
   const int64_t rbase = (int64_t)blockIdx.x * rows_per_block + ro;
-  for (int k = 0; k < rows_per_block; k += rpb * kUnroll) {
-    bf16x8 v[kUnroll], g[kUnroll];
-    float ok[kUnroll];
+  for (int k = 0; k < rows_per_block; k += rpb * kU) {
+    bf16x8 v[kU], g[kU];
+    float ok[kU];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < kU; ++u) {
       const int64_t r = rbase + k + u * rpb;
       const bool in = live & (r < M);
       ok[u] = in ? 1.0f : 0.0f;
@@ -133,7 +135,7 @@ __global__ void __launch_bounds__(kThreads) bn_reduce_kernel(
       if constexpr (kMode == 1) g[u] = dy[idx];
     }
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < kU; ++u) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float xf = bf2f(v[u].v[j]);
@@ -319,10 +321,10 @@ Plan make_plan(int64_t M, int C) {
   p.chunk = C <= kMaxChunk ? C : kMaxChunk;
   p.nchunks = (C + p.chunk - 1) / p.chunk;
   p.rpb = kThreads / (p.chunk / 8);
-  int64_t target = kTargetBlocks / p.nchunks;
+  int64_t target = g_target_blocks / p.nchunks;
   if (target < 1) target = 1;
   int64_t iters = (M + p.rpb * target - 1) / (p.rpb * target);
-  iters = (iters + kUnroll - 1) / kUnroll * kUnroll;
+  iters = (iters + g_unroll - 1) / g_unroll * g_unroll;
   p.rows_per_block = (int)(p.rpb * iters);
   p.G = (M + p.rows_per_block - 1) / p.rows_per_block;
   return p;
@@ -347,8 +349,12 @@ int fwd_train(const void* x, void* y, const void* gamma, const void* beta, void*
   auto* partial = reinterpret_cast<float2*>(ws);
   float* coef = ws + 2 * p.G * C;
   const auto* xv = static_cast<const bf16x8*>(x);
-  hipLaunchKernelGGL((bn_reduce_kernel<0, 0, P>), dim3((unsigned)p.G, p.nchunks), dim3(kThreads), 0, s, xv,
-                     nullptr, nullptr, nullptr, nullptr, nullptr, partial, M, C, p.chunk, p.rows_per_block);
+  if (g_unroll == 8)
+    hipLaunchKernelGGL((bn_reduce_kernel<0, 0, P, 8>), dim3((unsigned)p.G, p.nchunks), dim3(kThreads), 0, s, xv,
+                       nullptr, nullptr, nullptr, nullptr, nullptr, partial, M, C, p.chunk, p.rows_per_block);
+  else
+    hipLaunchKernelGGL((bn_reduce_kernel<0, 0, P>), dim3((unsigned)p.G, p.nchunks), dim3(kThreads), 0, s, xv,
+                       nullptr, nullptr, nullptr, nullptr, nullptr, partial, M, C, p.chunk, p.rows_per_block);
   hipLaunchKernelGGL((bn_fwd_finalize_kernel<P>), dim3((C + kFinC - 1) / kFinC), dim3(kFinC * kFinG), 0, s,
                      partial, p.G, static_cast<const uint16_t*>(x), static_cast<const P*>(gamma),
                      static_cast<const P*>(beta), static_cast<P*>(run_mean), static_cast<P*>(run_var), mean,
@@ -371,8 +377,12 @@ void bwd_launch(const bf16x8* dyv, const bf16x8* xv, bf16x8* dxv, const P* gamma
   const Plan p = make_plan(M, C);
   auto* partial = reinterpret_cast<float2*>(ws);
   float* coef = ws + 2 * p.G * C;
-  hipLaunchKernelGGL((bn_reduce_kernel<1, kAct, P>), dim3((unsigned)p.G, p.nchunks), dim3(kThreads), 0, s,
-                     xv, dyv, gamma, beta, mean, invstd, partial, M, C, p.chunk, p.rows_per_block);
+  if (g_unroll == 8)
+    hipLaunchKernelGGL((bn_reduce_kernel<1, kAct, P, 8>), dim3((unsigned)p.G, p.nchunks), dim3(kThreads), 0, s,
+                       xv, dyv, gamma, beta, mean, invstd, partial, M, C, p.chunk, p.rows_per_block);
+  else
+    hipLaunchKernelGGL((bn_reduce_kernel<1, kAct, P>), dim3((unsigned)p.G, p.nchunks), dim3(kThreads), 0, s,
+                       xv, dyv, gamma, beta, mean, invstd, partial, M, C, p.chunk, p.rows_per_block);
   hipLaunchKernelGGL((bn_bwd_finalize_kernel<P>), dim3((C + kFinC - 1) / kFinC), dim3(kFinC * kFinG), 0, s,
                      partial, p.G, gamma, beta, mean, invstd, dgamma, dbeta, coef, M, C);
   const uint64_t nvec = (uint64_t)M * (C / 8);
@@ -449,4 +459,11 @@ VGPU_API int vgpu_bn_act_bwd(const void* dy, const void* x, void* dx, const void
                              int64_t M, int C, int act, int param_bf16, void* stream) {
   return vgpu_bn_act_bwd_add(dy, x, dx, gamma, beta, mean, invstd, dgamma, dbeta, ws, M, C, act, param_bf16,
                              nullptr, stream);
+}
+
+// A/B of the reduction's shape (vgpu.bench.bnab): workgroups targeted over the
+// chip and rows in flight per thread (4 or 8).  Call before sizing workspaces.
+VGPU_API void vgpu_bn_set_tuning(int target_blocks, int unroll) {
+  g_target_blocks = target_blocks > 0 ? target_blocks : kTargetBlocks;
+  g_unroll = unroll == 8 ? 8 : kUnroll;
 }

@@ -80,6 +80,7 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_bn_act_bwd.argtypes = [vp] * 10 + [i64, ci, ci, ci, vp]
     lib.vgpu_bn_act_bwd_add.argtypes = [vp] * 10 + [i64, ci, ci, ci, vp, vp]
     lib.vgpu_bn_act_bwd_add.restype = ci
+    lib.vgpu_bn_set_tuning.argtypes = [ci, ci]
     lib.vgpu_conv_wgrad_workspace.argtypes = [ci] * 8
     lib.vgpu_conv_wgrad_workspace.restype = i64
     lib.vgpu_conv_wgrad_nhwc.argtypes = [vp] * 4 + [i64] + [ci] * 8 + [vp]
