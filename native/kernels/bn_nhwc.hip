@@ -38,7 +38,9 @@ constexpr int kTargetBlocks = 1024;  // reduction grid ≈ 4 workgroups per CU (
 int g_target_blocks = kTargetBlocks;  // A/B: vgpu_bn_set_tuning
 int g_unroll = kUnroll;
 constexpr int kFinC = 8;             // finalize: channels per workgroup
-constexpr int kFinG = 64;            //           partial groups per workgroup (tree-merged)
+constexpr int kFinG = 128;           //           partial groups per workgroup (tree-merged):
+                                     // ≤ 8 loads per thread at G = 1024, ≤ 19 at the epilogue
+                                     // statistics' G = M / 64 of ResNet stage 1 (2366)
 constexpr int kMaxGrid = 256 * 8;
 
 struct alignas(16) bf16x8 {
@@ -179,7 +181,7 @@ __device__ __forceinline__ void merge_partials(const float2* __restrict__ partia
   s1 = 0.0;
   s2 = 0.0;
   if (c < C) {
-#pragma unroll 4
+#pragma unroll 8
     for (int64_t g = grp; g < G; g += kFinG) {
       const float2 p = partial[g * C + c];
       s1 += p.x;
@@ -214,7 +216,7 @@ __global__ void __launch_bounds__(kFinC * kFinG) bn_fwd_finalize_kernel(
   const double m1 = s1 / n;
   double var = s2 / n - m1 * m1;
   if (var < 0.0) var = 0.0;
-  const double mu = (double)bf2f(x[c]) + m1;
+  const double mu = (x ? (double)bf2f(x[c]) : 0.0) + m1;  // x: the reduction's shift row (null: unshifted sums)
   const float is = (float)(1.0 / sqrt(var + (double)eps));
   mean[c] = (float)mu;
   invstd[c] = is;
@@ -344,10 +346,10 @@ inline bool shape_ok(int64_t M, int C) { return M >= 1 && C >= 8 && C % 8 == 0 &
 template <typename P>
 int fwd_train(const void* x, void* y, const void* gamma, const void* beta, void* run_mean, void* run_var,
               float* mean, float* invstd, float* ws, int64_t M, int C, float eps, float momentum, int act,
-              hipStream_t s) {
+              hipStream_t s, float* coef_out = nullptr) {
   const Plan p = make_plan(M, C);
   auto* partial = reinterpret_cast<float2*>(ws);
-  float* coef = ws + 2 * p.G * C;
+  float* coef = coef_out ? coef_out : ws + 2 * p.G * C;  // s, t
   const auto* xv = static_cast<const bf16x8*>(x);
   if (g_unroll == 8)
     hipLaunchKernelGGL((bn_reduce_kernel<0, 0, P, 8>), dim3((unsigned)p.G, p.nchunks), dim3(kThreads), 0, s, xv,
@@ -463,6 +465,95 @@ VGPU_API int vgpu_bn_act_bwd(const void* dy, const void* x, void* dx, const void
 
 // A/B of the reduction's shape (vgpu.bench.bnab): workgroups targeted over the
 // chip and rows in flight per thread (4 or 8).  Call before sizing workspaces.
+// ---- statistics from the producing / consuming convolution's epilogue ------------------
+// (native/kernels/conv_gemm.hip vgpu_conv2d_nhwc_bn): `partial` holds G = ceil(M / 64)
+// fp32 pairs per channel, [G][C], so no reduction pass over the activation runs here.
+
+// Forward from (Σ x, Σ x²) pairs: finalize (mean / invstd, running stats) + apply.
+// coef: fp32 [4][C] out = s, t, mean, invstd (what the backward's fused epilogue reads).
+VGPU_API int vgpu_bn_act_fwd_partials(const float* partial, int64_t G, const void* x, void* y, const void* gamma,
+                                      const void* beta, void* run_mean, void* run_var, float* coef, int64_t M,
+                                      int C, float eps, float momentum, int act, int param_bf16, void* stream) {
+  if (!shape_ok(M, C) || !partial || G != (M + 63) / 64 || !aligned16(x) || !aligned16(y) || !aligned16(coef) ||
+      (!run_mean) != (!run_var) || act < 0 || act > 2)
+    return (int)hipErrorInvalidValue;
+  auto s = (hipStream_t)stream;
+  const auto* pp = reinterpret_cast<const float2*>(partial);
+  float* mean = coef + 2 * C;
+  float* invstd = coef + 3 * C;
+  const dim3 fg((C + kFinC - 1) / kFinC), fb(kFinC * kFinG);
+  if (param_bf16)
+    hipLaunchKernelGGL((bn_fwd_finalize_kernel<uint16_t>), fg, fb, 0, s, pp, G, nullptr,
+                       static_cast<const uint16_t*>(gamma), static_cast<const uint16_t*>(beta),
+                       static_cast<uint16_t*>(run_mean), static_cast<uint16_t*>(run_var), mean, invstd, coef, M, C,
+                       eps, momentum);
+  else
+    hipLaunchKernelGGL((bn_fwd_finalize_kernel<float>), fg, fb, 0, s, pp, G, nullptr,
+                       static_cast<const float*>(gamma), static_cast<const float*>(beta),
+                       static_cast<float*>(run_mean), static_cast<float*>(run_var), mean, invstd, coef, M, C, eps,
+                       momentum);
+  const uint64_t nvec = (uint64_t)M * (C / 8);
+  const auto* xv = static_cast<const bf16x8*>(x);
+  auto* yv = static_cast<bf16x8*>(y);
+  switch (act) {
+    case 0: hipLaunchKernelGGL(bn_apply_kernel<0>, dim3(grid_for(nvec)), dim3(kThreads), 0, s, xv, yv, coef, nvec, C / 8); break;
+    case 1: hipLaunchKernelGGL(bn_apply_kernel<1>, dim3(grid_for(nvec)), dim3(kThreads), 0, s, xv, yv, coef, nvec, C / 8); break;
+    default: hipLaunchKernelGGL(bn_apply_kernel<2>, dim3(grid_for(nvec)), dim3(kThreads), 0, s, xv, yv, coef, nvec, C / 8); break;
+  }
+  return (int)hipGetLastError();
+}
+
+// The unfused forward (reduction pass) that also leaves s, t, mean, invstd in
+// coef [4][C] (mean / invstd are coef + 2C / + 3C); ws as vgpu_bn_act_fwd_train.
+VGPU_API int vgpu_bn_act_fwd_train_coef(const void* x, void* y, const void* gamma, const void* beta, void* run_mean,
+                                        void* run_var, float* coef, float* ws, int64_t M, int C, float eps,
+                                        float momentum, int act, int param_bf16, void* stream) {
+  if (!shape_ok(M, C) || !coef || !aligned16(coef) || !aligned16(x) || !aligned16(y) || !aligned16(ws) ||
+      (!run_mean) != (!run_var))
+    return (int)hipErrorInvalidValue;
+  auto s = (hipStream_t)stream;
+  if (param_bf16)
+    return fwd_train<uint16_t>(x, y, gamma, beta, run_mean, run_var, coef + 2 * C, coef + 3 * C, ws, M, C, eps,
+                               momentum, act, s, coef);
+  return fwd_train<float>(x, y, gamma, beta, run_mean, run_var, coef + 2 * C, coef + 3 * C, ws, M, C, eps, momentum,
+                          act, s, coef);
+}
+
+// Backward from (Σ dz, Σ dz·x̂) pairs, dz = dy·act'(·) already applied by the
+// data-gradient epilogue: finalize (dγ, dβ, folded coefficients) + dx = s·dz + cc·x + b
+// (+ add).  ws: 4·C fp32.
+VGPU_API int vgpu_bn_bwd_partials(const float* partial, int64_t G, const void* dz, const void* x, void* dx,
+                                  const void* gamma, const void* beta, const float* mean, const float* invstd,
+                                  void* dgamma, void* dbeta, float* ws, int64_t M, int C, int param_bf16,
+                                  const void* add, void* stream) {
+  if (!shape_ok(M, C) || !partial || G != (M + 63) / 64 || !aligned16(dz) || !aligned16(x) || !aligned16(dx) ||
+      !aligned16(ws) || !mean || !invstd || (add && !aligned16(add)))
+    return (int)hipErrorInvalidValue;
+  auto s = (hipStream_t)stream;
+  const auto* pp = reinterpret_cast<const float2*>(partial);
+  const dim3 fg((C + kFinC - 1) / kFinC), fb(kFinC * kFinG);
+  if (param_bf16)
+    hipLaunchKernelGGL((bn_bwd_finalize_kernel<uint16_t>), fg, fb, 0, s, pp, G,
+                       static_cast<const uint16_t*>(gamma), static_cast<const uint16_t*>(beta), mean, invstd,
+                       static_cast<uint16_t*>(dgamma), static_cast<uint16_t*>(dbeta), ws, M, C);
+  else
+    hipLaunchKernelGGL((bn_bwd_finalize_kernel<float>), fg, fb, 0, s, pp, G, static_cast<const float*>(gamma),
+                       static_cast<const float*>(beta), mean, invstd, static_cast<float*>(dgamma),
+                       static_cast<float*>(dbeta), ws, M, C);
+  const uint64_t nvec = (uint64_t)M * (C / 8);
+  const auto* dzv = static_cast<const bf16x8*>(dz);
+  const auto* xv = static_cast<const bf16x8*>(x);
+  auto* dxv = static_cast<bf16x8*>(dx);
+  const auto* addv = static_cast<const bf16x8*>(add);
+  if (addv)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<0, true>), dim3(grid_for(nvec)), dim3(kThreads), 0, s, dzv, xv, dxv, ws,
+                       addv, nvec, C / 8);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<0, false>), dim3(grid_for(nvec)), dim3(kThreads), 0, s, dzv, xv, dxv, ws,
+                       addv, nvec, C / 8);
+  return (int)hipGetLastError();
+}
+
 VGPU_API void vgpu_bn_set_tuning(int target_blocks, int unroll) {
   g_target_blocks = target_blocks > 0 ? target_blocks : kTargetBlocks;
   g_unroll = unroll == 8 ? 8 : kUnroll;

@@ -63,7 +63,23 @@ struct ConvArgs {
   int M, K, ktiles, cblocks, nM, nN, nwg, act;
   uint32_t x_bytes, y_bytes;  // buffer-resource extents (< 2^31: the host splits the batch)
   int nmajor;                 // conv_halo_kernel: workgroups of one XCD share an N tile
+  // Training BatchNorm statistics from the epilogue (vgpu_conv2d_nhwc_bn; glds / halo only).
+  // stats: per 64-row group g and output channel c, stats[g·Cout + c] = (Σ v, Σ v·q) over
+  // the group's stored (bf16) values v: q = v (forward: the next BN's Σx, Σx²), or with
+  // bnx, q = (x - mean)·invstd and v = dy·act'(x·s + t) replacing dy (backward of the
+  // BN whose output this conv's data gradient is; bncoef = s, t, mean, invstd [4][Cout]).
+  float2* stats;
+  const uint16_t* bnx;
+  const float* bncoef;
+  int bnact;  // 1 relu, 2 relu6, 0 none
 };
+
+// d act / d z as PyTorch defines it (threshold_backward / hardtanh_backward).
+__device__ __forceinline__ float bn_act_grad(int act, float z) {
+  if (act == 1) return z > 0.0f ? 1.0f : 0.0f;
+  if (act == 2) return (z > 0.0f && z < 6.0f) ? 1.0f : 0.0f;
+  return 1.0f;
+}
 
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 // Keep `v` in a VGPR as it is here (no rematerialisation, no hoisting past this point).
@@ -432,7 +448,9 @@ __device__ __forceinline__ void load_residual(const ConvArgs& a, int m0, int n0,
     }
 }
 
-template <int BM, int BN, bool RES>
+// ST (BatchNorm statistics, ConvArgs::stats): 0 none, 1 forward (of the stored
+// values), 2 backward (masked by the BN's activation derivative; ConvArgs::bnx).
+template <int BM, int BN, bool RES, int ST = 0>
 __device__ __forceinline__ void epilogue_halves(const ConvArgs& a, f32x4_t (&acc)[BM / 32][BN / 32],
                                                 int m0, int n0, char* smem,
                                                 const u32x4 (&res)[2][EpiShape<BM, BN>::RROWS]) {
@@ -453,6 +471,34 @@ __device__ __forceinline__ void epilogue_halves(const ConvArgs& a, f32x4_t (&acc
     bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
   }
   float* sC = reinterpret_cast<float*>(smem);
+  // BatchNorm statistics (a.stats, uniform): per-thread sums over its rows, merged
+  // per 64-row group through LDS past the staging area (the pipeline stages are free).
+  constexpr bool st = ST != 0, bwd = ST == 2;
+  static_assert(!(bwd && RES), "backward statistics take no residual");
+  float s1[8], s2[8], bs[8], bt[8], bmu[8], bis[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = bs[j] = bt[j] = bmu[j] = bis[j] = 0.0f;
+  u32x4 xb[2][RROWS];
+  if constexpr (bwd) {
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t*>(a.bnx), 0, a.y_bytes, 0x00020000);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < RROWS; ++i) {
+        const int m = m0 + h * HROWS + rfirst + RSTEP * i;
+        xb[h][i] = __builtin_amdgcn_raw_buffer_load_b128(
+            xr, m < a.M ? (uint32_t)(((int64_t)m * a.Cout + col) * 2) : kOOB, 0, 0);
+      }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bs[j] = a.bncoef[col + j];
+      bt[j] = a.bncoef[a.Cout + col + j];
+      bmu[j] = a.bncoef[2 * a.Cout + col + j];
+      bis[j] = a.bncoef[3 * a.Cout + col + j];
+    }
+  }
+  float2* sS = reinterpret_cast<float2*>(smem + HROWS * CS * 4);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     if (wm == h) {
@@ -482,9 +528,47 @@ __device__ __forceinline__ void epilogue_halves(const ConvArgs& a, f32x4_t (&acc
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);
       }
-      if (m < a.M) *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = pack8(v);
+      float xf[8];
+      if constexpr (bwd) {
+        unpack8(xb[h][i], xf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= bn_act_grad(a.bnact, fmaf(xf[j], bs[j], bt[j]));
+      }
+      const u32x4 o = pack8(v);
+      if (m < a.M) *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = o;
+      if constexpr (st) {
+        float q[8];
+        unpack8(o, q);  // the stored (bf16) values
+        const float ok = m < a.M ? 1.0f : 0.0f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = q[j] * ok;
+          s1[j] += d;
+          s2[j] = fmaf(d, bwd ? (xf[j] - bmu[j]) * bis[j] : d, s2[j]);
+        }
+      }
     }
-    if (h == 0) __syncthreads();  // half 0 read out before half 1 is staged
+    // 64-row group complete: BM 128 after each half, BM 64 after both.
+    if (st && ((h + 1) * HROWS) % 64 == 0) {  // h is unrolled: folds
+      const int g = (m0 + (h + 1) * HROWS - 64) / 64;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sS[rfirst * BN + chunk * 8 + j] = make_float2(s1[j], s2[j]);
+        s1[j] = s2[j] = 0.0f;
+      }
+      __syncthreads();
+      if (t < BN && g * 64 < a.M) {
+        float2 acc2 = make_float2(0.0f, 0.0f);
+#pragma unroll
+        for (int q = 0; q < RSTEP; ++q) {
+          const float2 p = sS[q * BN + t];
+          acc2.x += p.x;
+          acc2.y += p.y;
+        }
+        a.stats[(int64_t)g * a.Cout + n0 + t] = acc2;
+      }
+    }
+    if (h == 0) __syncthreads();  // half 0 read out (and its group merged) before half 1 is staged
   }
 }
 
@@ -495,7 +579,7 @@ __device__ __forceinline__ void epilogue_halves(const ConvArgs& a, f32x4_t (&acc
 // DMA latency (a 3-stage ring measured slower on every ResNet-50 shape,
 // profiles/conv_stages_r1.md).  Prologue convs take conv_pro_kernel (an
 // in-register prologue on the DMA'd A fragments measured VALU-bound and slower).
-template <int KS, int BM, int BN, bool RES, int CSM = 0>
+template <int KS, int BM, int BN, bool RES, int CSM = 0, int ST = 0>
 __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a) {
   static_assert(CSM == 0 || (64 % CSM == 0 && CSM % 8 == 0), "narrow-C variant");
   constexpr int AR = BM / 32, BR = BN / 32;  // DMA instructions per thread per K step
@@ -507,6 +591,7 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
   constexpr int PIPE = 2 * STAGE;
   constexpr int HROWS = BM / 2, EPI = HROWS * CS * 4;  // epilogue staged in two row halves
   constexpr int BODY = PIPE > EPI ? PIPE : EPI;
+  static_assert(ST == 0 || EPI + (kThreads / (BN / 8)) * BN * 8 <= BODY, "statistics merge area fits");
   __shared__ __attribute__((aligned(16))) char smem[BODY];
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -614,7 +699,7 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
   if constexpr (RES) {
     if (!early_res) load_residual<BM, BN>(a, m0, n0, res);
   }
-  epilogue_halves<BM, BN, RES>(a, acc, m0, n0, smem, res);
+  epilogue_halves<BM, BN, RES, ST>(a, acc, m0, n0, smem, res);
 }
 
 // ---- 256x256 tile for large 1x1 / stride-1 convs without a prologue ----------
@@ -851,8 +936,11 @@ hipError_t launch_big(ConvArgs a, hipStream_t s) {
 // M32: the wave's 64 x 64 tile as 2 x 2 v_mfma_f32_32x32x16_bf16 instead of
 // 4 x 4 16x16x32 -- half the MFMA issues for the same operand bytes, and 18
 // instead of 36 A-address registers (A/B knob VGPU_CONV_HALO_M32).
-template <int BM, int BN, int HPMAX, bool M32 = false>
+// ST = 1: forward BatchNorm statistics of the stored values (ConvArgs::stats), one
+// 64-row group per wave, merged through the wave's own slab.
+template <int BM, int BN, int HPMAX, bool M32 = false, int ST = 0>
 __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvArgs a) {
+  static_assert(ST == 0 || ST == 1, "halo: forward statistics only");
   constexpr int T = BM * BN / 64, WN = BN / 64;
   constexpr int TM = M32 ? 2 : 4, TN = M32 ? 2 : 4;  // wave tile 64 x 64
   constexpr int RPI = T / 8;                          // LDS rows (128 B) per DMA instruction
@@ -1075,6 +1163,9 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
     bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
     bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
   }
+  float s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.0f;
   // 16x16 tiles: pass p = row tile i.  32x32 tiles: pass p = half (p & 1) of row
   // tile p >> 1; lane l holds rows 8b + 4(l >> 5) + e (b = 0..3) of column l & 31.
 #pragma unroll
@@ -1106,9 +1197,39 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);
       }
-      if (m < a.M) *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = pack8(v);
+      const u32x4 o = pack8(v);
+      if (m < a.M) *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = o;
+      if constexpr (ST != 0) {
+        float q[8];
+        unpack8(o, q);
+        const float ok = m < a.M ? 1.0f : 0.0f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = q[j] * ok;
+          s1[j] += d;
+          s2[j] = fmaf(d, d, s2[j]);
+        }
+      }
     }
     __builtin_amdgcn_s_waitcnt(kLgkm0);
+  }
+  if constexpr (ST != 0) {
+    // lanes of one column chunk (lane & 7) hold erow = lane >> 3: merge the 8 rows
+    float2* sS = reinterpret_cast<float2*>(sC);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sS[erow * 64 + ecol + j] = make_float2(s1[j], s2[j]);
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    const int g = (m0 + wm * 64) / 64;
+    if (g * 64 < a.M) {
+      float2 r = make_float2(0.0f, 0.0f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float2 p = sS[q * 64 + lane];
+        r.x += p.x;
+        r.y += p.y;
+      }
+      a.stats[(int64_t)g * a.Cout + n0 + wn * 64 + lane] = r;
+    }
   }
 }
 
@@ -1142,7 +1263,9 @@ hipError_t launch_halo(ConvArgs a, hipStream_t s) {
   a.nwg = a.nM * a.nN;
   // N-major placement when the filter outgrows an XCD's L2 share (4 MiB).
   a.nmajor = (int64_t)a.Cout * a.K * 2 > ((int64_t)5 << 19) ? 1 : 0;
-  if (halo_m32())
+  if (a.stats)
+    hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, false, 1>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
+  else if (halo_m32())
     hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, true>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
   else
     hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, false>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
@@ -1167,17 +1290,26 @@ int g_forced_big = -1;  // vgpu_conv_set_big: -1 = env VGPU_CONV_BIG / heuristic
 
 int g_forced_bm = 0;  // vgpu_conv_set_tile_m (A/B benchmarking); 0 = heuristic
 
-template <int KS, int BM, int BN, bool RES, int CSM = 0>
+template <int KS, int BM, int BN, bool RES, int CSM = 0, int ST = 0>
 hipError_t launch_glds(ConvArgs a, hipStream_t s) {
   a.nM = (a.M + BM - 1) / BM;
   a.nN = a.Cout / BN;
   a.nwg = a.nM * a.nN;
-  hipLaunchKernelGGL((conv_glds_kernel<KS, BM, BN, RES, CSM>), dim3(a.nwg), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL((conv_glds_kernel<KS, BM, BN, RES, CSM, ST>), dim3(a.nwg), dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 
 template <int KS, int BM>
 hipError_t dispatch_glds(const ConvArgs& a, bool res, hipStream_t s) {
+  if (a.stats) {  // training BatchNorm statistics in the epilogue (backward: no residual)
+    const bool bwd = a.bnx != nullptr;
+    if (bwd && res) return hipErrorNotSupported;
+    if (a.Cout % 128 == 0)
+      return bwd ? launch_glds<KS, BM, 128, false, 0, 2>(a, s)
+                 : (res ? launch_glds<KS, BM, 128, true, 0, 1>(a, s) : launch_glds<KS, BM, 128, false, 0, 1>(a, s));
+    return bwd ? launch_glds<KS, BM, 64, false, 0, 2>(a, s)
+               : (res ? launch_glds<KS, BM, 64, true, 0, 1>(a, s) : launch_glds<KS, BM, 64, false, 0, 1>(a, s));
+  }
   if (a.Cout % 128 == 0)
     return res ? launch_glds<KS, BM, 128, true>(a, s) : launch_glds<KS, BM, 128, false>(a, s);
   return res ? launch_glds<KS, BM, 64, true>(a, s) : launch_glds<KS, BM, 64, false>(a, s);
@@ -2263,11 +2395,42 @@ VGPU_API int vgpu_conv231_nhwc(const void* x, const void* w2, const float* b2, c
   return conv23_impl(x, w2, b2, w3, res, y, w1n, b1n, psn, ptn, h1n, N, H, W, C, stride, s);
 }
 
+namespace {
+int conv2d_impl(const void* x, const void* w, void* y, const void* res, const float* bias, const float* pscale,
+                const float* pshift, int N, int H, int W, int C, int Cout, int KS, int stride, int pad, int act,
+                float* stats, const void* bnx, const float* bncoef, int bnact, hipStream_t s);
+}  // namespace
+
 // Returns 0, a hipError_t, or -1 for an unsupported shape (checked before any launch).
 VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void* res,
                               const float* bias, const float* pscale, const float* pshift, int N,
                               int H, int W, int C, int Cout, int KS, int stride, int pad, int act,
                               hipStream_t s) {
+  return conv2d_impl(x, w, y, res, bias, pscale, pshift, N, H, W, C, Cout, KS, stride, pad, act, nullptr,
+                     nullptr, nullptr, 0, s);
+}
+
+// Training convolution with the BatchNorm statistics of its output from the
+// epilogue (ConvArgs::stats): stats = fp32 pairs [ceil(M / 64)][Cout], M = N·OH·OW.
+//   bnx == nullptr: forward — (Σ y, Σ y²) per 64-row group of the stored y.
+//   bnx = x of the BN whose output's gradient this conv computes (a data
+//   gradient): y = dy·act'(x·s + t) is stored instead of dy, and the pairs are
+//   (Σ y, Σ y·(x - mean)·invstd); bncoef = s, t, mean, invstd [4][Cout], bnact
+//   its activation (1 relu, 2 relu6, 0 none).  No residual then.
+// The LDS-DMA kernels only (no prologue, C % 64 == 0); returns -1 when the
+// shape takes another kernel (the caller runs the unfused path).
+VGPU_API int vgpu_conv2d_nhwc_bn(const void* x, const void* w, void* y, const void* res, int N, int H, int W,
+                                 int C, int Cout, int KS, int stride, int pad, float* stats, const void* bnx,
+                                 const float* bncoef, int bnact, hipStream_t s) {
+  if (!stats || (bnx && (!bncoef || res)) || bnact < 0 || bnact > 2) return -1;
+  return conv2d_impl(x, w, y, res, nullptr, nullptr, nullptr, N, H, W, C, Cout, KS, stride, pad, 0, stats, bnx,
+                     bncoef, bnact, s);
+}
+
+namespace {
+int conv2d_impl(const void* x, const void* w, void* y, const void* res, const float* bias, const float* pscale,
+                const float* pshift, int N, int H, int W, int C, int Cout, int KS, int stride, int pad, int act,
+                float* stats, const void* bnx, const float* bncoef, int bnact, hipStream_t s) {
   // C % 64 == 0 with 1x1 / 3x3 filters, or the narrow stem form (C = 16, 4x4,
   // stride 1, no prologue: a 7x7/s2 conv on a space-to-depth input).
   const bool narrow = C == 16 && KS == 4 && stride == 1 && pscale == nullptr;
@@ -2290,12 +2453,17 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
   a.cblocks = C / 64;
   a.ktiles = a.K / 64;
   a.act = act != 0;
+  a.stats = reinterpret_cast<float2*>(stats);
+  a.bnx = static_cast<const uint16_t*>(bnx);
+  a.bncoef = bncoef;
+  a.bnact = bnact;
   const bool pro = pscale != nullptr, has_res = res != nullptr;
+  if (stats && (narrow || pro || !glds_enabled())) return -1;
   // Buffer offsets are 32-bit: run the batch in slices whose activations stay < 2 GiB.
   const int64_t xi = (int64_t)H * W * C * 2, yi = (int64_t)a.OH * a.OW * Cout * 2;
   const int64_t lim = ((int64_t)1 << 31) - 1;
   const int64_t per = lim / (xi > yi ? xi : yi);
-  if (per < 1) return -1;
+  if (per < 1 || (stats && per < N)) return -1;  // statistics: one slice (group rows are global)
   const int bn = (Cout % 128 == 0) ? 128 : 64;
   for (int n0 = 0; n0 < N; n0 += (int)per) {
     const int nb = (int)((N - n0) < per ? (N - n0) : per);
@@ -2334,11 +2502,11 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
     }
     const bool big_ok = !narrow && !pro && KS == 1 && stride == 1 && pad == 0 && Cout % 256 == 0 && C >= 128;
     const int64_t tiles256 = (int64_t)((c.M + 255) / 256) * (Cout / 256);
-    const bool big = big_ok && (g_forced_big == 1 ||
+    const bool big = !stats && big_ok && (g_forced_big == 1 ||
                                 (g_forced_big == 2 && C >= 1024 && tiles256 >= (int64_t)conv_cus()));
     // 3x3 / stride 1 without prologue or residual: the halo-tile kernel.
     const bool halo = (g_forced_halo < 0 ? halo_enabled() : g_forced_halo > 0) && !narrow && !pro && !has_res &&
-                      KS == 3 && stride == 1 && pad == 1;
+                      KS == 3 && stride == 1 && pad == 1 && !bnx;
     if (halo && (e = dispatch_halo(c, s)) != hipErrorNotSupported) {
       // launched (or a launch error)
     } else if (big)
@@ -2358,10 +2526,12 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
       e = small ? dispatch_bn<1, 64>(c, pro, has_res, s) : dispatch_bn<1, 128>(c, pro, has_res, s);
     else
       e = small ? dispatch_bn<3, 64>(c, pro, has_res, s) : dispatch_bn<3, 128>(c, pro, has_res, s);
+    if (e == hipErrorNotSupported && stats) return -1;
     if (e != hipSuccess) return (int)e;
   }
   return 0;
 }
+}  // namespace
 
 // NHWC bf16 max pool (k×k window, stride, symmetric zero-excluded padding), 16 B per lane.
 // Fused stem: X [N][HS][WS][16] (space-to-depth input), w [64][4][4][16] →

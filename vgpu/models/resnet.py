@@ -15,6 +15,7 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
+from vgpu.ops import bnconv
 from vgpu.ops.bn import batched_step_counters, bn_act, bn_act_res
 from vgpu.ops.conv import DgradFilters, conv_train
 from vgpu.ops.conv import native_train_enabled as _conv_train_native
@@ -54,6 +55,25 @@ class PreActBottleneck(nn.Module):
         y = bn_act(conv_train(pre, self.conv1), self.bn1)
         y = bn_act(conv_train(y, self.conv2), self.bn2)
         return conv_train(y, self.conv3, residual=sc)
+
+    def forward_fused(self, x: torch.Tensor, st: torch.Tensor | None):
+        """Training step with the BatchNorm statistics carried by the convs
+        (vgpu.ops.bnconv): `st` are x's (Σ, Σ²) pairs from the previous block's
+        conv3 epilogue (None: reduced here); returns (out, out's pairs)."""
+        if self.shortcut is None:
+            h1, st1, x = bnconv.bn_conv(x, self.bn_in, self.conv1, stats_in=st, res_out=True)
+            sc = x
+        else:
+            pre = bn_act(x, self.bn_in)
+            sc = conv_train(pre, self.shortcut)
+            h1, st1 = bnconv.conv_stats(pre, self.conv1)
+        h2, st2 = bnconv.bn_conv(h1, self.bn1, self.conv2, stats_in=st1)
+        return bnconv.bn_conv(h2, self.bn2, self.conv3, residual=sc, stats_in=st2)
+
+    def fused_eligible(self, x: torch.Tensor) -> bool:
+        # the block's inner tensors share x's dtype / device / layout; every
+        # ResNet-V2 conv has C, Cout % 64 == 0 (bn_conv falls back per shape)
+        return not self.fused and torch.is_grad_enabled() and bnconv.eligible(x, self.bn_in, self.conv1)
 
 
 def _fold_bn(conv: nn.Conv2d, bn: nn.BatchNorm2d) -> nn.Conv2d:
@@ -97,7 +117,12 @@ class ResNetV2(nn.Module):
             self._dgrad.refresh()
         with batched_step_counters():
             x = self.pool(self.stem(x))
-            x = self.blocks(x)
+            if self.training and all(b.fused_eligible(x) for b in self.blocks[:1]):
+                st = None
+                for b in self.blocks:
+                    x, st = b.forward_fused(x, st)
+            else:
+                x = self.blocks(x)
             x = bn_act(x, self.bn_out)
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)

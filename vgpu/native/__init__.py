@@ -81,6 +81,15 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_bn_act_bwd_add.argtypes = [vp] * 10 + [i64, ci, ci, ci, vp, vp]
     lib.vgpu_bn_act_bwd_add.restype = ci
     lib.vgpu_bn_set_tuning.argtypes = [ci, ci]
+    # BatchNorm statistics from the conv epilogue (vgpu.ops.bnconv)
+    lib.vgpu_conv2d_nhwc_bn.argtypes = [vp] * 4 + [ci] * 8 + [vp, vp, vp, ci, vp]
+    lib.vgpu_conv2d_nhwc_bn.restype = ci
+    lib.vgpu_bn_act_fwd_partials.argtypes = [vp, i64] + [vp] * 7 + [i64, ci, cf, cf, ci, ci, vp]
+    lib.vgpu_bn_act_fwd_partials.restype = ci
+    lib.vgpu_bn_act_fwd_train_coef.argtypes = [vp] * 8 + [i64, ci, cf, cf, ci, ci, vp]
+    lib.vgpu_bn_act_fwd_train_coef.restype = ci
+    lib.vgpu_bn_bwd_partials.argtypes = [vp, i64] + [vp] * 10 + [i64, ci, ci, vp, vp]
+    lib.vgpu_bn_bwd_partials.restype = ci
     lib.vgpu_conv_wgrad_workspace.argtypes = [ci] * 8
     lib.vgpu_conv_wgrad_workspace.restype = i64
     lib.vgpu_conv_wgrad_nhwc.argtypes = [vp] * 4 + [i64] + [ci] * 8 + [vp]

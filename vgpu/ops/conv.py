@@ -385,24 +385,31 @@ class _ConvTrainFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         dy = dy.contiguous(memory_format=_CL)
-        s, p = ctx.stride, ctx.padding
-        need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
-        common = ([0], [s, s], [p, p], [1, 1], False, [0, 0], 1)
-        bw = torch.ops.aten.convolution_backward
-        dx = dw = None
-        native_dw = need_dw and _wgrad_native(dy, w.shape[2], s)
-        if s == 1:
-            if need_dx:
-                ks = w.shape[2]
-                dx = conv2d(dy, _dgrad_filter(w), stride=1, padding=ks - 1 - p)
-        elif need_dx:
-            dx, dw, _ = bw(dy, x, w, *common, [True, need_dw and not native_dw, False])
-        if native_dw:
-            dw = conv2d_wgrad(dy, x, w.shape[2], stride=s, padding=p)
-        elif need_dw and dw is None:
-            dw = bw(dy, x, w, *common, [False, True, False])[1]
+        dx, dw = conv_backward(dy, x, w, ctx.stride, ctx.padding, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
         dres = dy if ctx.has_res and ctx.needs_input_grad[2] else None
         return dx, dw, dres, None, None
+
+
+def conv_backward(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, p: int, need_dx: bool,
+                  need_dw: bool, *, skip_dx: bool = False) -> tuple[torch.Tensor | None, torch.Tensor | None]:
+    """(dx, dw) of y = conv(x, w, stride s, padding p): dx on the MFMA kernel for
+    stride 1 (MIOpen otherwise), dw per _wgrad_native.  skip_dx: the caller
+    computed a stride-1 dx itself (vgpu.ops.bnconv's fused data gradient)."""
+    common = ([0], [s, s], [p, p], [1, 1], False, [0, 0], 1)
+    bw = torch.ops.aten.convolution_backward
+    dx = dw = None
+    native_dw = need_dw and _wgrad_native(dy, w.shape[2], s)
+    if s == 1:
+        if need_dx and not skip_dx:
+            ks = w.shape[2]
+            dx = conv2d(dy, _dgrad_filter(w), stride=1, padding=ks - 1 - p)
+    elif need_dx:
+        dx, dw, _ = bw(dy, x, w, *common, [True, need_dw and not native_dw, False])
+    if native_dw:
+        dw = conv2d_wgrad(dy, x, w.shape[2], stride=s, padding=p)
+    elif need_dw and dw is None:
+        dw = bw(dy, x, w, *common, [False, True, False])[1]
+    return dx, dw
 
 
 def native_train_enabled() -> bool:
