@@ -473,8 +473,7 @@ __device__ __forceinline__ void epilogue_halves(const ConvArgs& a, f32x4_t (&acc
   float* sC = reinterpret_cast<float*>(smem);
   // BatchNorm statistics (a.stats, uniform): per-thread sums over its rows, merged
   // per 64-row group through LDS past the staging area (the pipeline stages are free).
-  constexpr bool st = ST != 0, bwd = ST == 2;
-  static_assert(!(bwd && RES), "backward statistics take no residual");
+  constexpr bool st = ST != 0, bwd = ST == 2;  // bwd + RES: dy = acc + res (a second gradient of the BN output)
   float s1[8], s2[8], bs[8], bt[8], bmu[8], bis[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = bs[j] = bt[j] = bmu[j] = bis[j] = 0.0f;
@@ -1303,11 +1302,10 @@ template <int KS, int BM>
 hipError_t dispatch_glds(const ConvArgs& a, bool res, hipStream_t s) {
   if (a.stats) {  // training BatchNorm statistics in the epilogue (backward: no residual)
     const bool bwd = a.bnx != nullptr;
-    if (bwd && res) return hipErrorNotSupported;
     if (a.Cout % 128 == 0)
-      return bwd ? launch_glds<KS, BM, 128, false, 0, 2>(a, s)
+      return bwd ? (res ? launch_glds<KS, BM, 128, true, 0, 2>(a, s) : launch_glds<KS, BM, 128, false, 0, 2>(a, s))
                  : (res ? launch_glds<KS, BM, 128, true, 0, 1>(a, s) : launch_glds<KS, BM, 128, false, 0, 1>(a, s));
-    return bwd ? launch_glds<KS, BM, 64, false, 0, 2>(a, s)
+    return bwd ? (res ? launch_glds<KS, BM, 64, true, 0, 2>(a, s) : launch_glds<KS, BM, 64, false, 0, 2>(a, s))
                : (res ? launch_glds<KS, BM, 64, true, 0, 1>(a, s) : launch_glds<KS, BM, 64, false, 0, 1>(a, s));
   }
   if (a.Cout % 128 == 0)
@@ -2416,13 +2414,14 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
 //   bnx = x of the BN whose output's gradient this conv computes (a data
 //   gradient): y = dy·act'(x·s + t) is stored instead of dy, and the pairs are
 //   (Σ y, Σ y·(x - mean)·invstd); bncoef = s, t, mean, invstd [4][Cout], bnact
-//   its activation (1 relu, 2 relu6, 0 none).  No residual then.
+//   its activation (1 relu, 2 relu6, 0 none).  A residual there is a second
+//   gradient of the BN output (a projection shortcut's), added before the mask.
 // The LDS-DMA kernels only (no prologue, C % 64 == 0); returns -1 when the
 // shape takes another kernel (the caller runs the unfused path).
 VGPU_API int vgpu_conv2d_nhwc_bn(const void* x, const void* w, void* y, const void* res, int N, int H, int W,
                                  int C, int Cout, int KS, int stride, int pad, float* stats, const void* bnx,
                                  const float* bncoef, int bnact, hipStream_t s) {
-  if (!stats || (bnx && (!bncoef || res)) || bnact < 0 || bnact > 2) return -1;
+  if (!stats || (bnx && !bncoef) || bnact < 0 || bnact > 2) return -1;
   return conv2d_impl(x, w, y, res, nullptr, nullptr, nullptr, N, H, W, C, Cout, KS, stride, pad, 0, stats, bnx,
                      bncoef, bnact, s);
 }

@@ -235,3 +235,41 @@ def test_resnet_training_step_fused_matches_unfused(F):
     for (k, b1), b2 in zip(m.named_buffers(), m2.buffers()):
         if b1.dtype.is_floating_point:
             torch.testing.assert_close(b1.float(), b2.float(), atol=2e-2, rtol=2e-2, msg=k)
+
+
+@pytest.mark.parametrize("c,width,sc_stride", [(64, 64, 1), (256, 128, 2)])
+def test_bn_conv_with_projection_shortcut_matches_fp32_reference(F, c, width, sc_stride):
+    """A projection block's entry: pre = relu(bn(x)) feeds conv1 and the
+    shortcut; the shortcut's data gradient joins conv1's in the fused epilogue."""
+    import copy
+    from torch import nn
+    torch.manual_seed(1)
+    n, h, w = 4, 18, 18
+    bn = nn.BatchNorm2d(c).cuda().train()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    conv1 = nn.Conv2d(c, width, 1, bias=False).cuda().to(torch.bfloat16).to(memory_format=CL)
+    sc = nn.Conv2d(c, 4 * width, 1, stride=sc_stride, bias=False).cuda().to(torch.bfloat16).to(memory_format=CL)
+    bn_r = copy.deepcopy(bn)
+    x = _x((n, c, h, w), 31).requires_grad_()
+    F.set_enabled(True)
+    try:
+        z, st, s_out = F.bn_conv(x, bn, conv1, shortcut=sc)
+    finally:
+        F.set_enabled(False)
+    xr = x.detach().float().requires_grad_()
+    w1r = conv1.weight.detach().float().requires_grad_()
+    wsr = sc.weight.detach().float().requires_grad_()
+    pre = torch.nn.functional.batch_norm(xr, None, None, bn_r.weight, bn_r.bias, training=True).clamp_min(0)
+    zr = torch.nn.functional.conv2d(pre, w1r)
+    sr = torch.nn.functional.conv2d(pre, wsr, stride=sc_stride)
+    for got, ref in ((z, zr), (s_out, sr)):
+        torch.testing.assert_close(got.float(), ref, atol=3e-2 * ref.abs().max().item(), rtol=3e-2)
+    gz, gs = _x(tuple(z.shape), 32), _x(tuple(s_out.shape), 33)
+    torch.autograd.backward([z, s_out], [gz, gs])
+    torch.autograd.backward([zr, sr], [gz.float(), gs.float()])
+    for got, ref in ((x.grad, xr.grad), (bn.weight.grad, bn_r.weight.grad), (bn.bias.grad, bn_r.bias.grad),
+                     (conv1.weight.grad, w1r.grad), (sc.weight.grad, wsr.grad)):
+        tol = 3e-2 * ref.abs().max().item() + 1e-3
+        torch.testing.assert_close(got.float(), ref.float(), atol=tol, rtol=5e-2)

@@ -64,9 +64,7 @@ class PreActBottleneck(nn.Module):
             h1, st1, x = bnconv.bn_conv(x, self.bn_in, self.conv1, stats_in=st, res_out=True)
             sc = x
         else:
-            pre = bn_act(x, self.bn_in)
-            sc = conv_train(pre, self.shortcut)
-            h1, st1 = bnconv.conv_stats(pre, self.conv1)
+            h1, st1, sc = bnconv.bn_conv(x, self.bn_in, self.conv1, stats_in=st, shortcut=self.shortcut)
         h2, st2 = bnconv.bn_conv(h1, self.bn1, self.conv2, stats_in=st1)
         return bnconv.bn_conv(h2, self.bn2, self.conv3, residual=sc, stats_in=st2)
 

@@ -105,12 +105,14 @@ class _BNConvFn(torch.autograd.Function):
     """z = conv(act(bn(x)), w) (+ residual), with
     stats_in: (Σx, Σx²) pairs of x from its producer's epilogue (empty: reduce here),
     stats_out: also return z's pairs for the next BN,
-    res_out: also return x itself, whose gradient (an identity shortcut's) is
-    summed into dx by the BN's dx pass."""
+    extra output (third): with res_out, x itself, whose gradient (an identity
+    shortcut's) is summed into dx by the BN's dx pass; with a shortcut weight
+    wsc, the projection shortcut conv(act(bn(x)), wsc, stride sc_stride), whose
+    data gradient is added to conv's in the fused epilogue."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, run_mean, run_var, w, residual, stats_in, momentum: float, eps: float,
-                act: int, stride: int, padding: int, stats_out: bool, res_out: bool):
+    def forward(ctx, x, gamma, beta, run_mean, run_var, w, residual, stats_in, wsc, momentum: float, eps: float,
+                act: int, stride: int, padding: int, sc_stride: int, stats_out: bool, res_out: bool):
         lib = load_kernels()
         n, c, h, wd = x.shape
         m = n * h * wd
@@ -134,26 +136,35 @@ class _BNConvFn(torch.autograd.Function):
             if rc != 0:
                 raise RuntimeError(f"vgpu_bn_act_fwd_train_coef: hipError {rc}")
         z, st = _conv_out(y, w, stride, padding, residual, stats_out)
-        ctx.save_for_backward(x, y, w, gamma, beta, coef)
-        ctx.act, ctx.pb, ctx.stride, ctx.padding = act, pb, stride, padding
+        ctx.save_for_backward(x, y, w, gamma, beta, coef, wsc)
+        ctx.act, ctx.pb, ctx.stride, ctx.padding, ctx.sc_stride = act, pb, stride, padding, sc_stride
         ctx.has_res = residual is not None
         st = st if st is not None else _none_stats(x)
         ctx.mark_non_differentiable(st)
         if res_out:
             return z, st, x.view_as(x)
+        if wsc is not None:
+            return z, st, conv2d(y, wsc, stride=sc_stride, padding=0)
         return z, st
 
     @staticmethod
-    def backward(ctx, dz, _dst, dxres=None):
-        x, y, w, gamma, beta, coef = ctx.saved_tensors
+    def backward(ctx, dz, _dst, dextra=None):
+        x, y, w, gamma, beta, coef, wsc = ctx.saved_tensors
         lib = load_kernels()
         dz = dz.contiguous(memory_format=_CL)
-        if dxres is not None:
-            dxres = dxres.contiguous(memory_format=_CL)
         n, c, h, wd = x.shape
         m = n * h * wd
         s, p = ctx.stride, ctx.padding
         cout, _, ks, _ = w.shape
+        dxres = dysc = dwsc = None
+        if dextra is not None:
+            dextra = dextra.contiguous(memory_format=_CL)
+            if wsc is None:
+                dxres = dextra
+            else:
+                # the shortcut's own gradients: dw now, its data gradient joins conv's below
+                dysc, dwsc = conv_backward(dextra, y, wsc, ctx.sc_stride, 0, True, ctx.needs_input_grad[8])
+                dysc = dysc.contiguous(memory_format=_CL)
         need_dx = any(ctx.needs_input_grad[:3])
         dgamma = torch.empty_like(gamma) if gamma is not None and ctx.needs_input_grad[1] else None
         dbeta = torch.empty_like(beta) if beta is not None and ctx.needs_input_grad[2] else None
@@ -161,13 +172,13 @@ class _BNConvFn(torch.autograd.Function):
         dx = torch.empty_like(x, memory_format=_CL) if need_dx else None
         fused = False
         if need_dx and s == 1:
-            # data gradient of the conv with the BN backward's reduction in its epilogue
+            # data gradient of the conv (+ the shortcut's) with the BN backward's reduction in its epilogue
             dpre = torch.empty_like(x, memory_format=_CL)
             part = torch.empty((_groups(m), c, 2), dtype=torch.float32, device=x.device)
             oh, ow = dz.shape[2], dz.shape[3]
             rc = lib.vgpu_conv2d_nhwc_bn(
-                B._ptr(dz), B._ptr(_dgrad_filter(w)), B._ptr(dpre), None, n, oh, ow, cout, c, ks, 1, ks - 1 - p,
-                B._ptr(part), B._ptr(x), B._ptr(coef), ctx.act, B._stream())
+                B._ptr(dz), B._ptr(_dgrad_filter(w)), B._ptr(dpre), B._ptr(dysc), n, oh, ow, cout, c, ks, 1,
+                ks - 1 - p, B._ptr(part), B._ptr(x), B._ptr(coef), ctx.act, B._stream())
             if rc == 0:
                 ws = torch.empty(4 * c, dtype=torch.float32, device=x.device)
                 rc = lib.vgpu_bn_bwd_partials(
@@ -182,6 +193,8 @@ class _BNConvFn(torch.autograd.Function):
         dy_bn, dw = conv_backward(dz, y, w, s, p, need_dx and not fused, ctx.needs_input_grad[5])
         if need_dx and not fused:
             dy_bn = dy_bn.contiguous(memory_format=_CL)
+            if dysc is not None:
+                dy_bn = dy_bn + dysc
             rc = lib.vgpu_bn_act_bwd_add(
                 B._ptr(dy_bn), B._ptr(x), B._ptr(dx), B._ptr(gamma), B._ptr(beta), B._ptr(mean), B._ptr(invstd),
                 B._ptr(dgamma), B._ptr(dbeta), B._ptr(B._workspace(lib, m, c, x.device)), m, c, ctx.act, ctx.pb,
@@ -189,7 +202,7 @@ class _BNConvFn(torch.autograd.Function):
             if rc != 0:
                 raise RuntimeError(f"vgpu_bn_act_bwd: hipError {rc}")
         dres = dz if ctx.has_res and ctx.needs_input_grad[6] else None
-        return (dx, dgamma, dbeta, None, None, dw, dres, None, None, None, None, None, None, None, None)
+        return (dx, dgamma, dbeta, None, None, dw, dres, None, dwsc, None, None, None, None, None, None, None, None)
 
 
 def eligible(x: torch.Tensor, bn: nn.BatchNorm2d | None, conv: nn.Conv2d) -> bool:
@@ -210,16 +223,21 @@ def _bump(bn: nn.BatchNorm2d) -> bool:
 
 def bn_conv(x: torch.Tensor, bn: nn.BatchNorm2d, conv: nn.Conv2d, *, act: str = "relu",
             residual: torch.Tensor | None = None, stats_in: torch.Tensor | None = None,
-            stats_out: bool = True, res_out: bool = False):
-    """(conv(act(bn(x))) + residual, its statistics or None[, x]) — see the module
-    docstring.  Call only when eligible(x, bn, conv)."""
+            stats_out: bool = True, res_out: bool = False, shortcut: nn.Conv2d | None = None):
+    """(conv(act(bn(x))) + residual, its statistics or None[, x | shortcut(act(bn(x)))])
+    — see the module docstring.  Call only when eligible(x, bn, conv) (and, with
+    a shortcut, eligible(x, None, shortcut): 1x1, no padding)."""
+    if res_out and shortcut is not None:
+        raise ValueError("res_out and shortcut are exclusive")
     track = _bump(bn)
     outs = _BNConvFn.apply(
         x, bn.weight, bn.bias, bn.running_mean if track else None, bn.running_var if track else None,
         conv.weight, residual, stats_in if stats_in is not None else _none_stats(x),
-        bn.momentum if track else 0.0, bn.eps, B.ACT[act], conv.stride[0], conv.padding[0], stats_out, res_out)
+        shortcut.weight if shortcut is not None else None,
+        bn.momentum if track else 0.0, bn.eps, B.ACT[act], conv.stride[0], conv.padding[0],
+        shortcut.stride[0] if shortcut is not None else 1, stats_out, res_out)
     st = outs[1] if outs[1].numel() else None
-    return (outs[0], st, outs[2]) if res_out else (outs[0], st)
+    return (outs[0], st, outs[2]) if len(outs) == 3 else (outs[0], st)
 
 
 def conv_stats(x: torch.Tensor, conv: nn.Conv2d, residual: torch.Tensor | None = None):
