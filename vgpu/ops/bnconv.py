@@ -40,6 +40,10 @@ from vgpu.ops.conv import _dgrad_filter, conv2d, conv_backward, out_hw, train_el
 
 _CL = torch.channels_last
 _ENABLED = os.environ.get("VGPU_BN_FUSE", "0") == "1"
+# 3x3 data gradients with the BN statistics take the per-tap LDS-DMA kernel, not
+# the (faster) halo-tile kernel; VGPU_BN_FUSE_3X3=0 keeps those on halo + the
+# unfused BN backward instead (A/B).
+_FUSE_3X3 = os.environ.get("VGPU_BN_FUSE_3X3", "1") != "0"
 
 
 def enabled() -> bool:
@@ -171,7 +175,7 @@ class _BNConvFn(torch.autograd.Function):
         mean, invstd = coef[2 * c:3 * c], coef[3 * c:]
         dx = torch.empty_like(x, memory_format=_CL) if need_dx else None
         fused = False
-        if need_dx and s == 1:
+        if need_dx and s == 1 and (ks == 1 or _FUSE_3X3):
             # data gradient of the conv (+ the shortcut's) with the BN backward's reduction in its epilogue
             dpre = torch.empty_like(x, memory_format=_CL)
             part = torch.empty((_groups(m), c, 2), dtype=torch.float32, device=x.device)
