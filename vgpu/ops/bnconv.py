@@ -25,7 +25,8 @@ forward uses E[z²] - E[z]², fine for conv outputs whose |mean| is within a few
 std); the values summed are the stored bf16 ones, as the unfused path sees them.
 tests/test_gpu_bn.py compares both directions with the fp32 PyTorch reference.
 
-VGPU_BN_FUSE=1 enables it in vgpu.models.resnet (A/B against the unfused path).
+On by default in vgpu.models.resnet training (1.2: 2 760 -> 2 991 images/s, 2.2:
+815 -> 909, profiles/r4/train/bnfuse/); VGPU_BN_FUSE=0 runs the unfused path (A/B).
 """
 from __future__ import annotations
 
@@ -39,7 +40,7 @@ from vgpu.ops import bn as B
 from vgpu.ops.conv import _dgrad_filter, conv2d, conv_backward, out_hw, train_eligible
 
 _CL = torch.channels_last
-_ENABLED = os.environ.get("VGPU_BN_FUSE", "0") == "1"
+_ENABLED = os.environ.get("VGPU_BN_FUSE", "1") != "0"
 # 3x3 data gradients with the BN statistics take the per-tap LDS-DMA kernel, not
 # the (faster) halo-tile kernel; VGPU_BN_FUSE_3X3=0 keeps those on halo + the
 # unfused BN backward instead (A/B).
@@ -90,6 +91,7 @@ class _ConvStatsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, residual, stride: int, padding: int):
         z, st = _conv_out(x, w, stride, padding, residual, True)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.padding, ctx.has_res = stride, padding, residual is not None
         st = st if st is not None else _none_stats(x)
@@ -99,6 +101,8 @@ class _ConvStatsFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dz, _dst):
         x, w = ctx.saved_tensors
+        if dz is None:
+            return None, None, None, None, None
         dz = dz.contiguous(memory_format=_CL)
         dx, dw = conv_backward(dz, x, w, ctx.stride, ctx.padding, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
         dres = dz if ctx.has_res and ctx.needs_input_grad[2] else None
@@ -140,6 +144,10 @@ class _BNConvFn(torch.autograd.Function):
             if rc != 0:
                 raise RuntimeError(f"vgpu_bn_act_fwd_train_coef: hipError {rc}")
         z, st = _conv_out(y, w, stride, padding, residual, stats_out)
+        # Undefined output gradients stay None: autograd would otherwise zero-fill
+        # one fp32 tensor per node for the statistics output (50 fills, 3.5 % of
+        # a ResNet-V2-50 step, profiles/r4/train/rocprof_train_1.2_fused_r4.md).
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(x, y, w, gamma, beta, coef, wsc)
         ctx.act, ctx.pb, ctx.stride, ctx.padding, ctx.sc_stride = act, pb, stride, padding, sc_stride
         ctx.has_res = residual is not None
@@ -155,6 +163,10 @@ class _BNConvFn(torch.autograd.Function):
     def backward(ctx, dz, _dst, dextra=None):
         x, y, w, gamma, beta, coef, wsc = ctx.saved_tensors
         lib = load_kernels()
+        if dz is None:  # only the extra output was used
+            n_, _, h_, w_ = x.shape
+            oh, ow = out_hw(h_, w_, w.shape[2], ctx.stride, ctx.padding)
+            dz = torch.zeros((n_, w.shape[0], oh, ow), dtype=x.dtype, device=x.device, memory_format=_CL)
         dz = dz.contiguous(memory_format=_CL)
         n, c, h, wd = x.shape
         m = n * h * wd
