@@ -271,3 +271,23 @@ def test_bn_conv_with_projection_shortcut_matches_fp32_reference(F, c, width, sc
                      (conv1.weight.grad, w1r.grad), (sc.weight.grad, wsr.grad)):
         tol = 3e-2 * ref.abs().max().item() + 1e-3
         torch.testing.assert_close(got.float(), ref.float(), atol=tol, rtol=5e-2)
+
+
+@pytest.mark.parametrize("n,c,h,w,k,s,p", [(4, 64, 37, 41, 3, 2, 1), (2, 128, 16, 16, 2, 2, 0), (3, 64, 9, 9, 3, 1, 1)])
+def test_training_maxpool_matches_pytorch(gpu_build, n, c, h, w, k, s, p):
+    """Native training max pool (winning-tap bytes + gather backward) against
+    torch's max_pool2d on the same bf16 tensors: forward and dx bit-exact."""
+    from vgpu.ops.conv import maxpool_train
+    x = _x((n, c, h, w), 41)
+    x[0, :, 0, 0] = x[0, :, 0, 1]          # ties: the first maximum wins in both
+    pool = torch.nn.MaxPool2d(k, s, p)
+    xa = x.clone().requires_grad_()
+    xb = x.clone().requires_grad_()
+    ya = maxpool_train(xa, pool)
+    yb = pool(xb)
+    assert ya.is_contiguous(memory_format=CL)
+    torch.testing.assert_close(ya, yb, atol=0, rtol=0)
+    g = _x(tuple(ya.shape), 42)
+    ya.backward(g)
+    yb.backward(g)
+    torch.testing.assert_close(xa.grad, xb.grad, atol=0, rtol=0)

@@ -17,7 +17,7 @@ import torch.nn.functional as F
 
 from vgpu.ops import bnconv
 from vgpu.ops.bn import batched_step_counters, bn_act, bn_act_res
-from vgpu.ops.conv import DgradFilters, conv_train
+from vgpu.ops.conv import DgradFilters, conv_train, maxpool_train
 from vgpu.ops.conv import native_train_enabled as _conv_train_native
 
 
@@ -114,7 +114,8 @@ class ResNetV2(nn.Module):
                 self._dgrad = DgradFilters([m for m in self.modules() if isinstance(m, nn.Conv2d)])
             self._dgrad.refresh()
         with batched_step_counters():
-            x = self.pool(self.stem(x))
+            x = self.stem(x)
+            x = maxpool_train(x, self.pool) if self.training and torch.is_grad_enabled() else self.pool(x)
             if self.training and all(b.fused_eligible(x) for b in self.blocks[:1]):
                 st = None
                 for b in self.blocks:

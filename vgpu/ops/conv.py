@@ -231,6 +231,52 @@ def maxpool3s2(x: torch.Tensor) -> torch.Tensor:
     return maxpool(x, 3, 2, 1)
 
 
+class _MaxPoolTrainFn(torch.autograd.Function):
+    """k×k max pool with a one-byte winning-tap index per output element
+    (native/kernels/pool_train.hip); backward gathers dy per input pixel."""
+
+    @staticmethod
+    def forward(ctx, x, k: int, stride: int, pad: int):
+        n, c, h, w = x.shape
+        oh, ow = out_hw(h, w, k, stride, pad)
+        y = torch.empty((n, c, oh, ow), dtype=x.dtype, device=x.device, memory_format=_CL)
+        idx = torch.empty((n, oh, ow, c), dtype=torch.uint8, device=x.device)
+        rc = load_kernels().vgpu_maxpool_fwd_idx_nhwc(_ptr(x), _ptr(y), _ptr(idx), n, h, w, c, k, stride, pad,
+                                                     _stream())
+        if rc != 0:
+            raise RuntimeError(f"vgpu_maxpool_fwd_idx_nhwc: error {rc}")
+        ctx.save_for_backward(idx)
+        ctx.cfg = (n, c, h, w, k, stride, pad)
+        ctx.mark_non_differentiable(idx)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        n, c, h, w, k, stride, pad = ctx.cfg
+        dy = dy.contiguous(memory_format=_CL)
+        dx = torch.empty((n, c, h, w), dtype=dy.dtype, device=dy.device, memory_format=_CL)
+        rc = load_kernels().vgpu_maxpool_bwd_nhwc(_ptr(dy), _ptr(idx), _ptr(dx), n, h, w, c, k, stride, pad,
+                                                 _stream())
+        if rc != 0:
+            raise RuntimeError(f"vgpu_maxpool_bwd_nhwc: error {rc}")
+        return dx, None, None, None
+
+
+def maxpool_train(x: torch.Tensor, pool: torch.nn.MaxPool2d) -> torch.Tensor:
+    """pool(x) with the native forward / backward for bf16 channels_last CUDA
+    tensors (square window, no dilation, no ceil mode), else the module."""
+    k, s, p = pool.kernel_size, pool.stride, pool.padding
+    k = k if isinstance(k, int) else (k[0] if k[0] == k[1] else None)
+    s = s if isinstance(s, int) else (s[0] if s[0] == s[1] else None)
+    p = p if isinstance(p, int) else (p[0] if p[0] == p[1] else None)
+    if (not _TRAIN_NATIVE or k is None or s is None or p is None or pool.ceil_mode or pool.dilation not in (1, (1, 1))
+            or pool.return_indices or not x.is_cuda or x.dtype != torch.bfloat16 or x.dim() != 4
+            or not x.is_contiguous(memory_format=_CL) or x.shape[1] % 8 or 2 * p > k):
+        return pool(x)
+    return _MaxPoolTrainFn.apply(x, k, s, p)
+
+
 def scale_shift_relu_mean(x: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor) -> torch.Tensor:
     """mean over H,W of relu(x*scale[c] + shift[c]) → [N, C] bf16 (final BN+ReLU+pool)."""
     _nhwc(x, "x")
