@@ -72,6 +72,11 @@ struct ConvArgs {
   const uint16_t* bnx;
   const float* bncoef;
   int bnact;  // 1 relu, 2 relu6, 0 none
+  // Backward statistics only: res_stride 2 = the residual is the compact data
+  // gradient of a 1x1 / stride-2 projection shortcut, [N][res_h][res_w][Cout],
+  // which lands on the even (h, w) pixels of this conv's OH x OW output (zero elsewhere).
+  int res_stride, res_h, res_w;
+  uint32_t res_bytes;
 };
 
 // d act / d z as PyTorch defines it (threshold_backward / hardtanh_backward).
@@ -431,20 +436,27 @@ struct EpiShape {
 
 // Residual rows this thread adds in the epilogue (both halves), issued early —
 // before the first DMA of the K loop — so their latency hides behind the loop.
-template <int BM, int BN>
+template <int BM, int BN, bool STRIDED = false>
 __device__ __forceinline__ void load_residual(const ConvArgs& a, int m0, int n0,
                                               u32x4 (&res)[2][EpiShape<BM, BN>::RROWS]) {
   using E = EpiShape<BM, BN>;
   const int t = threadIdx.x, chunk = t % E::CPR, rfirst = t / E::CPR;
+  const bool strided = STRIDED && a.res_stride == 2;
   const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(a.res), 0, a.y_bytes, 0x00020000);
+      const_cast<uint16_t*>(a.res), 0, strided ? a.res_bytes : a.y_bytes, 0x00020000);
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int i = 0; i < E::RROWS; ++i) {
       const int m = m0 + h * E::HROWS + rfirst + E::RSTEP * i;
-      res[h][i] = __builtin_amdgcn_raw_buffer_load_b128(
-          rr, m < a.M ? (uint32_t)(((int64_t)m * a.Cout + n0 + chunk * 8) * 2) : kOOB, 0, 0);
+      uint32_t off = m < a.M ? (uint32_t)(((int64_t)m * a.Cout + n0 + chunk * 8) * 2) : kOOB;
+      if (strided && m < a.M) {
+        const int ow = m % a.OW, t2 = m / a.OW, oh = t2 % a.OH, n = t2 / a.OH;
+        off = ((oh | ow) & 1) ? kOOB
+                              : (uint32_t)(((((int64_t)n * a.res_h + (oh >> 1)) * a.res_w + (ow >> 1)) * a.Cout +
+                                            n0 + chunk * 8) * 2);
+      }
+      res[h][i] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
     }
 }
 
@@ -662,7 +674,7 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
   u32x4 res[2][EpiShape<BM, BN>::RROWS];
   const bool early_res = RES && a.ktiles <= 1;
   if constexpr (RES) {
-    if (early_res) load_residual<BM, BN>(a, m0, n0, res);
+    if (early_res) load_residual<BM, BN, ST == 2>(a, m0, n0, res);
   }
   issue(0, 0);
   for (int kt = 0; kt < a.ktiles; ++kt) {
@@ -696,7 +708,7 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
     __builtin_amdgcn_s_barrier();
   }
   if constexpr (RES) {
-    if (!early_res) load_residual<BM, BN>(a, m0, n0, res);
+    if (!early_res) load_residual<BM, BN, ST == 2>(a, m0, n0, res);
   }
   epilogue_halves<BM, BN, RES, ST>(a, acc, m0, n0, smem, res);
 }
@@ -2396,7 +2408,7 @@ VGPU_API int vgpu_conv231_nhwc(const void* x, const void* w2, const float* b2, c
 namespace {
 int conv2d_impl(const void* x, const void* w, void* y, const void* res, const float* bias, const float* pscale,
                 const float* pshift, int N, int H, int W, int C, int Cout, int KS, int stride, int pad, int act,
-                float* stats, const void* bnx, const float* bncoef, int bnact, hipStream_t s);
+                float* stats, const void* bnx, const float* bncoef, int bnact, int res_stride, hipStream_t s);
 }  // namespace
 
 // Returns 0, a hipError_t, or -1 for an unsupported shape (checked before any launch).
@@ -2405,7 +2417,7 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
                               int H, int W, int C, int Cout, int KS, int stride, int pad, int act,
                               hipStream_t s) {
   return conv2d_impl(x, w, y, res, bias, pscale, pshift, N, H, W, C, Cout, KS, stride, pad, act, nullptr,
-                     nullptr, nullptr, 0, s);
+                     nullptr, nullptr, 0, 1, s);
 }
 
 // Training convolution with the BatchNorm statistics of its output from the
@@ -2415,21 +2427,24 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
 //   gradient): y = dy·act'(x·s + t) is stored instead of dy, and the pairs are
 //   (Σ y, Σ y·(x - mean)·invstd); bncoef = s, t, mean, invstd [4][Cout], bnact
 //   its activation (1 relu, 2 relu6, 0 none).  A residual there is a second
-//   gradient of the BN output (a projection shortcut's), added before the mask.
+//   gradient of the BN output (a projection shortcut's), added before the mask;
+//   res_stride 2: that of a 1x1 / stride-2 shortcut in compact form
+//   [N][ceil(OH/2)][ceil(OW/2)][Cout] (its even pixels; the others get none).
 // The LDS-DMA kernels only (no prologue, C % 64 == 0); returns -1 when the
 // shape takes another kernel (the caller runs the unfused path).
 VGPU_API int vgpu_conv2d_nhwc_bn(const void* x, const void* w, void* y, const void* res, int N, int H, int W,
                                  int C, int Cout, int KS, int stride, int pad, float* stats, const void* bnx,
-                                 const float* bncoef, int bnact, hipStream_t s) {
-  if (!stats || (bnx && !bncoef) || bnact < 0 || bnact > 2) return -1;
+                                 const float* bncoef, int bnact, int res_stride, hipStream_t s) {
+  if (!stats || (bnx && !bncoef) || bnact < 0 || bnact > 2 || (res_stride != 1 && (res_stride != 2 || !bnx || !res)))
+    return -1;
   return conv2d_impl(x, w, y, res, nullptr, nullptr, nullptr, N, H, W, C, Cout, KS, stride, pad, 0, stats, bnx,
-                     bncoef, bnact, s);
+                     bncoef, bnact, res_stride, s);
 }
 
 namespace {
 int conv2d_impl(const void* x, const void* w, void* y, const void* res, const float* bias, const float* pscale,
                 const float* pshift, int N, int H, int W, int C, int Cout, int KS, int stride, int pad, int act,
-                float* stats, const void* bnx, const float* bncoef, int bnact, hipStream_t s) {
+                float* stats, const void* bnx, const float* bncoef, int bnact, int res_stride, hipStream_t s) {
   // C % 64 == 0 with 1x1 / 3x3 filters, or the narrow stem form (C = 16, 4x4,
   // stride 1, no prologue: a 7x7/s2 conv on a space-to-depth input).
   const bool narrow = C == 16 && KS == 4 && stride == 1 && pscale == nullptr;
@@ -2456,6 +2471,15 @@ int conv2d_impl(const void* x, const void* w, void* y, const void* res, const fl
   a.bnx = static_cast<const uint16_t*>(bnx);
   a.bncoef = bncoef;
   a.bnact = bnact;
+  a.res_stride = res_stride;
+  a.res_h = (a.OH + 1) / 2;
+  a.res_w = (a.OW + 1) / 2;
+  a.res_bytes = 0;
+  if (res_stride == 2) {
+    const int64_t rb = (int64_t)N * a.res_h * a.res_w * Cout * 2;
+    if (rb >= ((int64_t)1 << 31)) return -1;
+    a.res_bytes = (uint32_t)rb;
+  }
   const bool pro = pscale != nullptr, has_res = res != nullptr;
   if (stats && (narrow || pro || !glds_enabled())) return -1;
   // Buffer offsets are 32-bit: run the batch in slices whose activations stay < 2 GiB.

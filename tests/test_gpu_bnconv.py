@@ -112,7 +112,7 @@ def test_backward_statistics_mask_and_sum_the_data_gradient(F, n, c, h, w, ks, a
     lib.vgpu_conv_set_halo(0)   # the fused backward never takes the halo kernel: compare like with like
     try:
         rc = lib.vgpu_conv2d_nhwc_bn(_ptr(dz), _ptr(wt), _ptr(out), None, n, h, w, cout, c, ks, 1, ks - 1 - pad,
-                                     _ptr(st), _ptr(x), _ptr(coef), act, _stream())
+                                     _ptr(st), _ptr(x), _ptr(coef), act, 1, _stream())
         dy = C.conv2d(dz, wt, stride=1, padding=ks - 1 - pad)   # the plain data gradient, same kernel
         torch.cuda.synchronize()
     finally:
@@ -235,14 +235,15 @@ def test_resnet_training_step_fused_matches_unfused(F):
             torch.testing.assert_close(b1.float(), b2.float(), atol=2e-2, rtol=2e-2, msg=k)
 
 
-@pytest.mark.parametrize("c,width,sc_stride", [(64, 64, 1), (256, 128, 2)])
-def test_bn_conv_with_projection_shortcut_matches_fp32_reference(F, c, width, sc_stride):
+@pytest.mark.parametrize("c,width,sc_stride,h", [(64, 64, 1, 18), (256, 128, 2, 18), (128, 64, 2, 19)])
+def test_bn_conv_with_projection_shortcut_matches_fp32_reference(F, c, width, sc_stride, h):
     """A projection block's entry: pre = relu(bn(x)) feeds conv1 and the
-    shortcut; the shortcut's data gradient joins conv1's in the fused epilogue."""
+    shortcut; the shortcut's data gradient joins conv1's in the fused epilogue
+    (stride 2: as a compact 1x1 GEMM result added at the even pixels)."""
     import copy
     from torch import nn
     torch.manual_seed(1)
-    n, h, w = 4, 18, 18
+    n, w = 4, h
     bn = nn.BatchNorm2d(c).cuda().train()
     with torch.no_grad():
         bn.weight.uniform_(0.5, 1.5)

@@ -86,7 +86,7 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_maxpool_bwd_nhwc.argtypes = [vp, vp, vp] + [ci] * 7 + [vp]
     lib.vgpu_maxpool_bwd_nhwc.restype = ci
     # BatchNorm statistics from the conv epilogue (vgpu.ops.bnconv)
-    lib.vgpu_conv2d_nhwc_bn.argtypes = [vp] * 4 + [ci] * 8 + [vp, vp, vp, ci, vp]
+    lib.vgpu_conv2d_nhwc_bn.argtypes = [vp] * 4 + [ci] * 8 + [vp, vp, vp, ci, ci, vp]
     lib.vgpu_conv2d_nhwc_bn.restype = ci
     lib.vgpu_bn_act_fwd_partials.argtypes = [vp, i64] + [vp] * 7 + [i64, ci, cf, cf, ci, ci, vp]
     lib.vgpu_bn_act_fwd_partials.restype = ci

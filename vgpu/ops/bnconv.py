@@ -71,7 +71,7 @@ def _conv_out(x: torch.Tensor, w: torch.Tensor, stride: int, padding: int, resid
         st = torch.empty((_groups(n * oh * ow), cout, 2), dtype=torch.float32, device=x.device)
         rc = load_kernels().vgpu_conv2d_nhwc_bn(
             B._ptr(x), B._ptr(w), B._ptr(z), B._ptr(residual), n, h, wd, c, cout, ks, stride, padding,
-            B._ptr(st), None, None, 0, B._stream())
+            B._ptr(st), None, None, 0, 1, B._stream())
         if rc == 0:
             return z, st
         if rc != -1:
@@ -173,10 +173,18 @@ class _BNConvFn(torch.autograd.Function):
         s, p = ctx.stride, ctx.padding
         cout, _, ks, _ = w.shape
         dxres = dysc = dwsc = None
+        res_stride = 1
         if dextra is not None:
             dextra = dextra.contiguous(memory_format=_CL)
             if wsc is None:
                 dxres = dextra
+            elif ctx.sc_stride == 2 and wsc.shape[2] == 1 and s == 1:
+                # 1x1 / stride-2 shortcut: its data gradient is a 1x1 GEMM on the
+                # compact grid, added at the even pixels by the fused epilogue
+                # (no MIOpen transposed conv, no 3/4-zero full-size tensor)
+                dysc = conv2d(dextra, _dgrad_filter(wsc))
+                res_stride = 2
+                _, dwsc = conv_backward(dextra, y, wsc, 2, 0, False, ctx.needs_input_grad[8])
             else:
                 # the shortcut's own gradients: dw now, its data gradient joins conv's below
                 dysc, dwsc = conv_backward(dextra, y, wsc, ctx.sc_stride, 0, True, ctx.needs_input_grad[8])
@@ -194,7 +202,7 @@ class _BNConvFn(torch.autograd.Function):
             oh, ow = dz.shape[2], dz.shape[3]
             rc = lib.vgpu_conv2d_nhwc_bn(
                 B._ptr(dz), B._ptr(_dgrad_filter(w)), B._ptr(dpre), B._ptr(dysc), n, oh, ow, cout, c, ks, 1,
-                ks - 1 - p, B._ptr(part), B._ptr(x), B._ptr(coef), ctx.act, B._stream())
+                ks - 1 - p, B._ptr(part), B._ptr(x), B._ptr(coef), ctx.act, res_stride, B._stream())
             if rc == 0:
                 ws = torch.empty(4 * c, dtype=torch.float32, device=x.device)
                 rc = lib.vgpu_bn_bwd_partials(
@@ -209,7 +217,10 @@ class _BNConvFn(torch.autograd.Function):
         dy_bn, dw = conv_backward(dz, y, w, s, p, need_dx and not fused, ctx.needs_input_grad[5])
         if need_dx and not fused:
             dy_bn = dy_bn.contiguous(memory_format=_CL)
-            if dysc is not None:
+            if dysc is not None and res_stride == 2:
+                dy_bn = dy_bn.clone()
+                dy_bn[:, :, ::2, ::2] += dysc
+            elif dysc is not None:
                 dy_bn = dy_bn + dysc
             rc = lib.vgpu_bn_act_bwd_add(
                 B._ptr(dy_bn), B._ptr(x), B._ptr(dx), B._ptr(gamma), B._ptr(beta), B._ptr(mean), B._ptr(invstd),

@@ -360,7 +360,10 @@ class DgradFilters:
     def _build(self):
         import struct
         convs = self._all
-        self.convs = [c for c in convs if c.stride == (1, 1) and c.kernel_size[0] in (1, 3)
+        # stride-1 convs (their data gradient is a conv with this filter) and 1x1
+        # projection shortcuts of any stride (a 1x1 GEMM on the compact grid)
+        self.convs = [c for c in convs if (c.stride == (1, 1) or c.kernel_size == (1, 1))
+                      and c.kernel_size[0] in (1, 3)
                       and c.weight.is_cuda and c.weight.dtype == torch.bfloat16
                       and c.weight.is_contiguous(memory_format=_CL) and c.groups == 1
                       and c.in_channels % 64 == 0 and c.out_channels % 64 == 0]
