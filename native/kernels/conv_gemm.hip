@@ -1257,11 +1257,15 @@ bool halo_enabled() {
 
 unsigned long long g_halo_launches = 0;  // vgpu_conv_halo_launches (tests: the halo path ran)
 
-int g_halo_m32 = -1;  // VGPU_CONV_HALO_M32=1: the 32x32x16 MFMA variant (A/B)
+// The 32x32x16 MFMA variant, default since it measured bit-identical and faster
+// on every halo layer (stage 3 35.6 -> 34.0 us, stage 4 39.3 -> 35.2, r152
+// stage 4 35.5 -> 31.2; flagship 26 767 -> 27 386 images/s on one box,
+// profiles/r4/kernels/convknob_m32.log).  VGPU_CONV_HALO_M32=0: 16x16x32.
+int g_halo_m32 = -1;
 bool halo_m32() {
   if (g_halo_m32 < 0) {
     const char* v = getenv("VGPU_CONV_HALO_M32");
-    g_halo_m32 = (v && v[0] == '1') ? 1 : 0;
+    g_halo_m32 = (v && v[0] == '0') ? 0 : 1;
   }
   return g_halo_m32 == 1;
 }

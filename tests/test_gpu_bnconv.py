@@ -204,31 +204,43 @@ def test_bn_conv_node_matches_fp32_reference(F, c, cout, ks, stride, res, stats_
 
 
 def test_resnet_training_step_fused_matches_unfused(F):
-    """ResNet-V2 (identity and projection blocks, 3x3/s2 convs) one training step
-    with the fused BN statistics against the unfused native path: logits and
-    every gradient agree (different summation order only)."""
+    """ResNet-V2 (identity and projection blocks, 3x3/s2 convs) one training
+    step, fused BN statistics vs the unfused native path, each against an fp32
+    copy of the model: the fused path's gradients are no further from fp32
+    than the unfused path's (both are bf16; early-layer gradients of a deep
+    random-init net carry a few % of bf16 noise, so the paths are not compared
+    with each other directly), and the running statistics agree."""
     import copy
     from vgpu.models import resnet as R
     torch.manual_seed(0)
-    m = R.ResNetV2([2, 2, 1, 1]).cuda().to(memory_format=CL).to(torch.bfloat16).train()
+    m32 = R.ResNetV2([2, 2, 1, 1]).cuda().to(memory_format=CL).train()
+    m = copy.deepcopy(m32).to(torch.bfloat16)
     m2 = copy.deepcopy(m)
     x = _x((4, 3, 96, 96), 9)
 
-    def step(model, fused):
+    def step(model, inp, fused):
         F.set_enabled(fused)
         try:
             model.zero_grad(set_to_none=True)
-            out = model(x).float()
+            out = model(inp).float()
             out.logsumexp(-1).sum().backward()
         finally:
             F.set_enabled(False)
         return out.detach(), {k: p.grad.float().clone() for k, p in model.named_parameters()}
 
-    out_f, g_f = step(m, True)
-    out_u, g_u = step(m2, False)
+    out_f, g_f = step(m, x, True)
+    out_u, g_u = step(m2, x, False)
+    out_r, g_r = step(m32, x.float(), False)
     cos = lambda a, b: torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()  # noqa: E731
-    assert cos(out_f, out_u) > 0.999
-    bad = [(k, round(cos(g_f[k], g_u[k]), 4)) for k in g_f if g_u[k].norm() > 0 and cos(g_f[k], g_u[k]) < 0.99]
+    assert cos(out_f, out_r) > 0.99 and cos(out_f, out_u) > 0.995
+    bad = []
+    for k in g_r:
+        nr = g_r[k].norm()
+        if nr == 0:
+            continue
+        ef, eu = ((g_f[k] - g_r[k]).norm() / nr).item(), ((g_u[k] - g_r[k]).norm() / nr).item()
+        if ef > 1.5 * eu + 0.02:
+            bad.append((k, round(ef, 3), round(eu, 3)))
     assert not bad, bad
     for (k, b1), b2 in zip(m.named_buffers(), m2.buffers()):
         if b1.dtype.is_floating_point:

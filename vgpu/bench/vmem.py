@@ -32,11 +32,17 @@ time) bring A back while the now idle B gives way.  VGPU_VMEM_MIGRATE=0
 
 Part E — one Llama-3-8B whose weights alone exceed the budget (a hot set
 larger than the budget, read cyclically every token): no pager can beat the
-host link here; the pager must simply not do worse than zero-copy.
+host link here; the pager must simply not do worse than zero-copy.  The
+budget is the pod's whole HBM, runtime context included: the context grows
+after the weights are placed (queues' context-save areas, code objects), which
+the pager answers by demoting managed bytes while zero-copy cannot, so a
+zero-copy pod ends up over its budget by that growth (1.19 GB in
+profiles/r4/vmem/part_e_books.log).  --context-charge books the context up
+front for both modes (VGPU_CONTEXT_CHARGE), so both hold the same HBM.
 
     python -m vgpu.bench.vmem [--spill-gib 8] [--budget-gib 8] [--tokens 16] [--part-c]
     python -m vgpu.bench.vmem --part-d [--budget-gib 22] [--modes pager,zero_copy]
-    python -m vgpu.bench.vmem --part-e [--budget-gib 11.5]
+    python -m vgpu.bench.vmem --part-e [--budget-gib 11.5] [--context-charge-mib 0]
 """
 from __future__ import annotations
 
@@ -364,13 +370,15 @@ def part_e_child(tokens: int, ctx: int, windows: int) -> dict:
     return out
 
 
-def run_pod_child(part: str, budget_gib: float, migrate: bool, args: list[str], timeout: float = 1500) -> dict:
+def run_pod_child(part: str, budget_gib: float, migrate: bool, args: list[str], timeout: float = 1500,
+                  context_mib: int = 0) -> dict:
     from vgpu.native import ensure_built, preload_env
     ensure_built()
     repo = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     env = preload_env()
     env.update({"VGPU_DEVICE_MEMORY_LIMIT_0": "400000m", "VGPU_OVERSUBSCRIBE": "true", "PYTHONPATH": repo,
                 "VGPU_DEVICE_MEMORY_PHYSICAL_0": f"{int(budget_gib * 1024)}m",
+                **({"VGPU_CONTEXT_CHARGE": f"{context_mib}m"} if context_mib else {}),
                 "VGPU_LOG_LEVEL": env.get("VGPU_LOG_LEVEL", "3"), "VGPU_VMEM_MIGRATE": "1" if migrate else "0"})
     if os.environ.get("VGPU_TRACE") and migrate:
         env["VGPU_TRACE"] = os.path.join(os.environ["VGPU_TRACE"], f"part_{part}")
@@ -383,7 +391,7 @@ def run_pod_child(part: str, budget_gib: float, migrate: bool, args: list[str], 
                        stdout=subprocess.PIPE, stderr=errf, text=True, timeout=timeout)
     tag = f"VMEM_{part.upper()} "
     js = [l for l in r.stdout.splitlines() if l.startswith(tag)]
-    res = {"migrate": migrate, "budget_gib": budget_gib}
+    res = {"migrate": migrate, "budget_gib": budget_gib, "context_charge_mib": context_mib}
     if js:
         res.update(json.loads(js[-1][len(tag):]))
     else:
@@ -417,6 +425,8 @@ def main(argv=None) -> int:
     ap.add_argument("--part-d", action="store_true", help="model switch under a physical budget (graph decode)")
     ap.add_argument("--part-e", action="store_true", help="hot set beyond the budget (graph decode)")
     ap.add_argument("--idle-s", type=float, default=3.0)
+    ap.add_argument("--context-charge-mib", type=int, default=0,
+                    help="book this much runtime context at first use (both modes; see Part E)")
     ap.add_argument("--skip-a", action="store_true")
     ap.add_argument("--skip-b", action="store_true")
     a = ap.parse_args(argv)
@@ -440,7 +450,7 @@ def main(argv=None) -> int:
         for mode in a.modes.split(","):
             out[mode] = run_pod_child(part, a.budget_gib, mode == "pager",
                                       ["--tokens", str(a.tokens), "--ctx", str(a.ctx), "--windows", str(a.windows),
-                                       "--idle-s", str(a.idle_s)])
+                                       "--idle-s", str(a.idle_s)], context_mib=a.context_charge_mib)
             print(f"VMEM_{part.upper()}_RUN " + json.dumps(out[mode]), flush=True)
         print(json.dumps(out), flush=True)
         return 0
