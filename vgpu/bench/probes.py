@@ -610,11 +610,28 @@ def vmemfull(gib: int = 4) -> dict:
     torch.cuda.synchronize()
     hip.hipMemPrefetchAsync(ptr, ctypes.c_size_t(n), ctypes.c_int(-1), s0)
     torch.cuda.synchronize()
-    total, used = _sysfs_vram()
+    # Device-wide counters: memory another process is still releasing (the
+    # test before this one may have just exited with 255 GB) shows up here, so
+    # wait until the counter settles, then top the balloon up until only
+    # `leave` is free.
+    prev, t_end = None, time.time() + 20
+    while time.time() < t_end:
+        used = _sysfs_vram()[1]
+        if prev is not None and abs(used - prev) < (256 << 20):
+            break
+        prev = used
+        time.sleep(0.5)
     leave = n // 2
-    balloon_bytes = max(0, total - used - leave)
-    balloon = torch.empty(balloon_bytes, dtype=torch.uint8, device="cuda")
-    torch.cuda.synchronize()
+    balloon = []
+    for _ in range(8):
+        total, used = _sysfs_vram()
+        extra = total - used - leave
+        if extra < (512 << 20):
+            break
+        balloon.append(torch.empty(extra, dtype=torch.uint8, device="cuda"))
+        torch.cuda.synchronize()
+        time.sleep(0.2)
+    balloon_bytes = sum(b.numel() for b in balloon)
     free_before = (lambda t: t[0] - t[1])(_sysfs_vram())
     t0 = time.time()
     rc = hip.hipMemPrefetchAsync(ptr, ctypes.c_size_t(n), ctypes.c_int(0), s0)
