@@ -3,6 +3,8 @@
 // Reference behaviour: libvgpu.so cuInit → pthread_once(preInit) → postInit
 // (allocator_init, set_task_pid, init_utilization_watcher), exit_handler, and
 // SIGUSR2/SIGUSR1 → sig_swap_stub / sig_restore_stub.
+#include <dlfcn.h>
+#include <execinfo.h>
 #include <signal.h>
 
 #include "common.h"
@@ -55,6 +57,39 @@ static void install_signal(int sig, void (*fn)(int)) {
   sa.sa_handler = fn;
   sa.sa_flags = SA_RESTART;
   sigaction(sig, &sa, nullptr);
+}
+
+// VGPU_CRASH_TRACE=1: on SIGSEGV / SIGBUS / SIGABRT print the native stack
+// (module + offset per frame, for addr2line against the same build) to stderr,
+// then die as the signal would have.  Diagnostics only; async-signal-safe calls.
+static void crash_trace(int sig, siginfo_t* info, void*) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  char line[160];
+  const int k = snprintf(line, sizeof line, "[vgpu] signal %d at address %p, native stack:\n", sig,
+                         info ? info->si_addr : nullptr);
+  if (k > 0) (void)!write(2, line, (size_t)k);
+  for (int i = 0; i < n; ++i) {
+    Dl_info di;
+    int m;
+    if (dladdr(frames[i], &di) && di.dli_fname)
+      m = snprintf(line, sizeof line, "  #%d %s+0x%lx %s\n", i, di.dli_fname,
+                   (unsigned long)((char*)frames[i] - (char*)di.dli_fbase), di.dli_sname ? di.dli_sname : "");
+    else
+      m = snprintf(line, sizeof line, "  #%d %p\n", i, frames[i]);
+    if (m > 0) (void)!write(2, line, (size_t)m);
+  }
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
+static void install_crash_trace() {
+  if (!env_bool(env_first("VGPU_CRASH_TRACE"), false)) return;
+  struct sigaction sa;
+  memset(&sa, 0, sizeof sa);
+  sa.sa_sigaction = crash_trace;
+  sa.sa_flags = SA_SIGINFO | SA_RESETHAND;
+  for (int sig : {SIGSEGV, SIGBUS, SIGABRT}) sigaction(sig, &sa, nullptr);
 }
 
 static void atfork_child() {
@@ -110,6 +145,7 @@ static void do_init() {
     hostpid_publish();
   }
   trace_open();
+  install_crash_trace();
   install_signal(SIGUSR2, sig_suspend);
   install_signal(SIGUSR1, sig_resume);
   atexit(on_exit_release);
