@@ -338,7 +338,7 @@ def test_side_stream_weight_gradients_in_a_captured_step(F):
         torch.cuda.synchronize()
     finally:
         F.set_enabled(False)
-        F.set_side_stream(True)
+        F.set_side_stream(False)
     assert F._side_pending is None  # joined at the end of every backward
     for (k, p1), p2 in zip(m.named_parameters(), m2.parameters()):
         cos = torch.nn.functional.cosine_similarity(p1.grad.float().flatten(), p2.grad.float().flatten(), dim=0)

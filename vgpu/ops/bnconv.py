@@ -70,8 +70,11 @@ def _groups(m: int) -> int:
 # callback), and the inputs stay referenced until then.  Off under
 # torch.distributed (DDP's gradient hooks read each gradient as soon as its
 # node returns) and when the parameter already has a gradient (accumulation
-# would read it on the main stream); VGPU_WGRAD_STREAM=0 turns it off.
-_SIDE = os.environ.get("VGPU_WGRAD_STREAM", "1") != "0"
+# would read it on the main stream).  Opt-in (VGPU_WGRAD_STREAM=1): under the
+# enforcement library the replay of such a two-stream step graph crashed
+# (profiles/r4/train/bnfuse/side_stream_crash.log), and without it the serial
+# step measured the same (3 112 images/s).
+_SIDE = os.environ.get("VGPU_WGRAD_STREAM", "0") == "1"
 _side_streams: dict = {}
 _side_lock = threading.Lock()
 _side_pending: list | None = None  # inputs kept alive until the join (one backward at a time)
