@@ -326,18 +326,23 @@ def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, ks: int, *, stride: int = 1,
 _WGRAD_MODE = os.environ.get("VGPU_CONV_WGRAD", "auto")
 
 
-def _wgrad_native(dy: torch.Tensor, ks: int, stride: int) -> bool:
+def _wgrad_native(dy: torch.Tensor, ks: int, stride: int, c: int = 0) -> bool:
     if _WGRAD_MODE == "0":
         return False
     if _WGRAD_MODE == "all":
         return True
     pixels = dy.shape[0] * dy.shape[2] * dy.shape[3]
-    # Every 1x1 (stride 1 or 2) since the swizzled LDS images (round 4:
-    # 23-36 us vs MIOpen's 27-43 us before its zero-fill and cast passes,
-    # profiles/r4/train/convtrain_wgrad_swizzle.log); 3x3 down to ResNet
-    # stage 3 (parity with MIOpen's kernel there, and no zero-fill / cast
-    # passes); stage 4 (2.4k pixels) stays on MIOpen (59 vs 44 us).
-    return ks == 1 or (ks == 3 and pixels >= 8192)
+    # 1x1 (stride 1 or 2) from 1k output pixels: the swizzled LDS images run
+    # 23-36 us vs MIOpen's 27-43 us plus its zero-fill and cast passes
+    # (profiles/r4/train/convtrain_wgrad_swizzle.log); at ResNet-V2-152's
+    # stage 4 (640 pixels) MIOpen's kernel wins (16-20 vs 24-33 us,
+    # convtrain_b10_256.log).  3x3 from 8k pixels, and from 2k when C <= 256
+    # (2.2's stage 3: 26.0 vs 25.1 us, even before MIOpen's two extra
+    # passes); ResNet-V2-50's stage 4 (2.4k pixels, C = 512) stays on MIOpen
+    # (59 vs 44 us), as do 640-pixel 3x3s (40 vs 20 us).
+    if ks == 1:
+        return pixels >= 1024
+    return ks == 3 and (pixels >= 8192 or (pixels >= 2048 and 0 < c <= 256))
 
 
 # ---- data-gradient filters, one launch per step ------------------------------------------
@@ -447,7 +452,7 @@ def conv_backward(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, p:
     common = ([0], [s, s], [p, p], [1, 1], False, [0, 0], 1)
     bw = torch.ops.aten.convolution_backward
     dx = dw = None
-    native_dw = need_dw and _wgrad_native(dy, w.shape[2], s)
+    native_dw = need_dw and _wgrad_native(dy, w.shape[2], s, w.shape[1])
     if s == 1:
         if need_dx and not skip_dx:
             ks = w.shape[2]
