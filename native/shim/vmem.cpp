@@ -117,7 +117,10 @@ struct Knobs {
   bool suspend_evict = false;
   uint64_t plain_window_ms = 30000;  // plain high-water mark window (plain_reserve)
   bool cut_pieces = true;            // VGPU_VMEM_CUT_PIECES=0: whole pieces only (A/B)
-  bool thp = false;                  // VGPU_VMEM_THP=1: madvise(MADV_HUGEPAGE) on managed ranges (A/B)
+  // madvise(MADV_HUGEPAGE) on managed ranges: their host-resident pages are read
+  // over the host link in 2 MiB pages (part E at equal HBM: 6.9-7.3 -> 7.5 tok/s,
+  // zero-copy 7.8; profiles/r4/vmem/part_e_context_charge*.log).  VGPU_VMEM_THP=0: off.
+  bool thp = true;
 };
 
 const Knobs& knobs() {
@@ -133,7 +136,7 @@ const Knobs& knobs() {
     v.suspend_evict = env_bool(env_first("VGPU_SUSPEND_EVICT"), false);
     if (const char* e = env_first("VGPU_VMEM_PLAIN_WINDOW_MS")) v.plain_window_ms = std::max(1ull, strtoull(e, nullptr, 10));
     v.cut_pieces = env_bool(env_first("VGPU_VMEM_CUT_PIECES"), true);
-    v.thp = env_bool(env_first("VGPU_VMEM_THP"), false);
+    v.thp = env_bool(env_first("VGPU_VMEM_THP"), true);
     if (const char* e = env_first("VGPU_VMEM_MANAGED_MIN_MB")) {
       const long long mb = atoll(e);
       v.managed_min = mb < 0 ? -1 : (int64_t)mb << 20;
