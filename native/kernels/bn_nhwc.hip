@@ -313,6 +313,171 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const bf16x8* __
   }
 }
 
+// ---- finalize + apply in one launch for small layers ------------------------------
+// With the statistics from the conv epilogues (G = ceil(M / 64) pairs per
+// channel), a small layer's finalize is a ~5 µs launch of its own for a few µs
+// of apply: ResNet-V2-152 b=10 runs 300 of them per step, 14 % of its GPU time
+// (profiles/r4/train/bnfuse/).  Here every workgroup of the apply owns a
+// 64-channel chunk and a row range, merges that chunk's G pairs itself (fp64,
+// the same sums the finalize forms) and applies; row range 0 also writes the
+// saved statistics / running stats (forward) or dγ, dβ (backward).  Used when
+// G <= kFuseMaxG, so the redundant merges stay a fraction of the apply's bytes.
+constexpr int kFuseMaxG = 160;
+constexpr int kFuseC = 64;
+constexpr int kFuseT = 1024;               // 16 lanes per channel: ≤ 10 pair loads each at G = 160
+constexpr int kFuseQ = kFuseT / kFuseC;
+
+__device__ __forceinline__ void merge_chunk(const float2* __restrict__ partial, int64_t G, int C, int c0,
+                                            double (&r1)[kFuseQ][kFuseC], double (&r2)[kFuseQ][kFuseC]) {
+  const int cl = threadIdx.x & (kFuseC - 1), q = threadIdx.x >> 6;
+  double s1 = 0.0, s2 = 0.0;
+#pragma unroll 4
+  for (int64_t g = q; g < G; g += kFuseQ) {
+    const float2 p = partial[g * C + c0 + cl];
+    s1 += p.x;
+    s2 += p.y;
+  }
+  r1[q][cl] = s1;
+  r2[q][cl] = s2;
+  __syncthreads();
+}
+
+template <int kAct, typename P>
+__global__ void __launch_bounds__(kFuseT) bn_fwd_fused_kernel(
+    const float2* __restrict__ partial, int64_t G, const bf16x8* __restrict__ x, bf16x8* __restrict__ y,
+    const P* __restrict__ gamma, const P* __restrict__ beta, P* __restrict__ run_mean, P* __restrict__ run_var,
+    float* __restrict__ coef, int64_t M, int C, float eps, float momentum, int64_t rows_per) {
+  __shared__ double r1[kFuseQ][kFuseC], r2[kFuseQ][kFuseC];
+  __shared__ float sS[kFuseC], sT[kFuseC];
+  const int c0 = blockIdx.x * kFuseC;
+  merge_chunk(partial, G, C, c0, r1, r2);
+  if (threadIdx.x < kFuseC) {
+    const int c = c0 + threadIdx.x;
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < kFuseQ; ++q) {
+      s1 += r1[q][threadIdx.x];
+      s2 += r2[q][threadIdx.x];
+    }
+    const double n = (double)M, mu = s1 / n;
+    double var = s2 / n - mu * mu;
+    if (var < 0.0) var = 0.0;
+    const float is = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = ldp(gamma, c, 1.0f) * is, sh = ldp(beta, c, 0.0f) - (float)mu * sc;
+    sS[threadIdx.x] = sc;
+    sT[threadIdx.x] = sh;
+    if (blockIdx.y == 0) {
+      coef[c] = sc;
+      coef[C + c] = sh;
+      coef[2 * C + c] = (float)mu;
+      coef[3 * C + c] = is;
+      if (run_mean) {
+        const float unbiased = (float)(M > 1 ? var * n / (n - 1.0) : var);
+        stp(run_mean, c, (1.0f - momentum) * ldp(run_mean, c, 0.0f) + momentum * (float)mu);
+        stp(run_var, c, (1.0f - momentum) * ldp(run_var, c, 0.0f) + momentum * unbiased);
+      }
+    }
+  }
+  __syncthreads();
+  const int cg = threadIdx.x & 7, ro = threadIdx.x >> 3;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = sS[cg * 8 + j];
+    sh[j] = sT[cg * 8 + j];
+  }
+  const int cvec = C >> 3, cv = (c0 >> 3) + cg;
+  const int64_t r_end = (int64_t)(blockIdx.y + 1) * rows_per < M ? (int64_t)(blockIdx.y + 1) * rows_per : M;
+  for (int64_t r = (int64_t)blockIdx.y * rows_per + ro; r < r_end; r += kFuseT / 8) {
+    const bf16x8 v = x[r * cvec + cv];
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.v[k] = f2bf(act_fwd<kAct>(fmaf(bf2f(v.v[k]), sc[k], sh[k])));
+    y[r * cvec + cv] = o;
+  }
+}
+
+// dz already carries act' (the data-gradient epilogue applied it): dx = s·dz + cc·x + b (+ add).
+template <bool kAdd, typename P>
+__global__ void __launch_bounds__(kFuseT) bn_bwd_fused_kernel(
+    const float2* __restrict__ partial, int64_t G, const bf16x8* __restrict__ dz, const bf16x8* __restrict__ x,
+    bf16x8* __restrict__ dx, const bf16x8* __restrict__ add, const P* __restrict__ gamma,
+    const float* __restrict__ mean, const float* __restrict__ invstd, P* __restrict__ dgamma, P* __restrict__ dbeta,
+    int64_t M, int C, int64_t rows_per) {
+  __shared__ double r1[kFuseQ][kFuseC], r2[kFuseQ][kFuseC];
+  __shared__ float sS[kFuseC], sC[kFuseC], sB[kFuseC];
+  const int c0 = blockIdx.x * kFuseC;
+  merge_chunk(partial, G, C, c0, r1, r2);
+  if (threadIdx.x < kFuseC) {
+    const int c = c0 + threadIdx.x;
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < kFuseQ; ++q) {
+      s1 += r1[q][threadIdx.x];
+      s2 += r2[q][threadIdx.x];
+    }
+    const float db = (float)s1, dg = (float)s2;
+    if (blockIdx.y == 0) {
+      if (dgamma) stp(dgamma, c, dg);
+      if (dbeta) stp(dbeta, c, db);
+    }
+    const float is = invstd[c], mu = mean[c];
+    const float sc = ldp(gamma, c, 1.0f) * is;
+    const float inv_m = (float)(1.0 / (double)M);
+    const float cc = -sc * is * dg * inv_m;
+    sS[threadIdx.x] = sc;
+    sC[threadIdx.x] = cc;
+    sB[threadIdx.x] = -sc * db * inv_m - mu * cc;
+  }
+  __syncthreads();
+  const int cg = threadIdx.x & 7, ro = threadIdx.x >> 3;
+  float sc[8], cc[8], bb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = sS[cg * 8 + j];
+    cc[j] = sC[cg * 8 + j];
+    bb[j] = sB[cg * 8 + j];
+  }
+  const int cvec = C >> 3, cv = (c0 >> 3) + cg;
+  const int64_t r_end = (int64_t)(blockIdx.y + 1) * rows_per < M ? (int64_t)(blockIdx.y + 1) * rows_per : M;
+  for (int64_t r = (int64_t)blockIdx.y * rows_per + ro; r < r_end; r += kFuseT / 8) {
+    const int64_t i = r * cvec + cv;
+    const bf16x8 v = x[i], g = dz[i];
+    bf16x8 rr;
+    if constexpr (kAdd) rr = add[i];
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float d = fmaf(sc[k], bf2f(g.v[k]), fmaf(cc[k], bf2f(v.v[k]), bb[k]));
+      if constexpr (kAdd) d += bf2f(rr.v[k]);
+      o.v[k] = f2bf(d);
+    }
+    dx[i] = o;
+  }
+}
+
+// Row ranges per 64-channel chunk: ~one workgroup per CU over the layer, at
+// least 128 rows (one pass of the 1024 threads) each.
+inline dim3 fused_grid(int64_t M, int C, int64_t& rows_per) {
+  const int chunks = C / kFuseC;
+  int64_t R = (256 + chunks - 1) / chunks;  // ~one 1024-thread workgroup per CU
+  const int64_t rmax = (M + kFuseT / 8 - 1) / (kFuseT / 8);
+  if (R > rmax) R = rmax;
+  if (R < 1) R = 1;
+  rows_per = (M + R - 1) / R;
+  R = (M + rows_per - 1) / rows_per;
+  return dim3((unsigned)chunks, (unsigned)R);
+}
+
+int g_fuse_small = -1;  // VGPU_BN_FUSE_SMALL=0 / vgpu_bn_set_fuse_small: separate finalize launches
+inline bool fused_ok(int64_t G, int C) {
+  if (g_fuse_small < 0) {
+    const char* v = getenv("VGPU_BN_FUSE_SMALL");
+    g_fuse_small = (v && v[0] == '0') ? 0 : 1;
+  }
+  return g_fuse_small == 1 && G <= kFuseMaxG && C % kFuseC == 0;
+}
+
 struct Plan {
   int chunk, nchunks, rpb, rows_per_block;
   int64_t G;
@@ -481,6 +646,23 @@ VGPU_API int vgpu_bn_act_fwd_partials(const float* partial, int64_t G, const voi
   const auto* pp = reinterpret_cast<const float2*>(partial);
   float* mean = coef + 2 * C;
   float* invstd = coef + 3 * C;
+  if (fused_ok(G, C)) {
+    int64_t rows_per;
+    const dim3 grid = fused_grid(M, C, rows_per);
+    const auto* xv = static_cast<const bf16x8*>(x);
+    auto* yv = static_cast<bf16x8*>(y);
+#define VGPU_BN_FWD_FUSED(A, P_)                                                                                   \
+  hipLaunchKernelGGL((bn_fwd_fused_kernel<A, P_>), grid, dim3(kFuseT), 0, s, pp, G, xv, yv,                      \
+                     static_cast<const P_*>(gamma), static_cast<const P_*>(beta), static_cast<P_*>(run_mean),      \
+                     static_cast<P_*>(run_var), coef, M, C, eps, momentum, rows_per)
+    if (param_bf16) {
+      if (act == 0) VGPU_BN_FWD_FUSED(0, uint16_t); else if (act == 1) VGPU_BN_FWD_FUSED(1, uint16_t); else VGPU_BN_FWD_FUSED(2, uint16_t);
+    } else {
+      if (act == 0) VGPU_BN_FWD_FUSED(0, float); else if (act == 1) VGPU_BN_FWD_FUSED(1, float); else VGPU_BN_FWD_FUSED(2, float);
+    }
+#undef VGPU_BN_FWD_FUSED
+    return (int)hipGetLastError();
+  }
   const dim3 fg((C + kFinC - 1) / kFinC), fb(kFinC * kFinG);
   if (param_bf16)
     hipLaunchKernelGGL((bn_fwd_finalize_kernel<uint16_t>), fg, fb, 0, s, pp, G, nullptr,
@@ -531,6 +713,25 @@ VGPU_API int vgpu_bn_bwd_partials(const float* partial, int64_t G, const void* d
     return (int)hipErrorInvalidValue;
   auto s = (hipStream_t)stream;
   const auto* pp = reinterpret_cast<const float2*>(partial);
+  if (fused_ok(G, C)) {
+    int64_t rows_per;
+    const dim3 grid = fused_grid(M, C, rows_per);
+    const auto* dzv = static_cast<const bf16x8*>(dz);
+    const auto* xv = static_cast<const bf16x8*>(x);
+    auto* dxv = static_cast<bf16x8*>(dx);
+    const auto* addv = static_cast<const bf16x8*>(add);
+#define VGPU_BN_BWD_FUSED(K, P_)                                                                                   \
+  hipLaunchKernelGGL((bn_bwd_fused_kernel<K, P_>), grid, dim3(kFuseT), 0, s, pp, G, dzv, xv, dxv, addv,          \
+                     static_cast<const P_*>(gamma), mean, invstd, static_cast<P_*>(dgamma), static_cast<P_*>(dbeta), \
+                     M, C, rows_per)
+    if (param_bf16) {
+      if (addv) VGPU_BN_BWD_FUSED(true, uint16_t); else VGPU_BN_BWD_FUSED(false, uint16_t);
+    } else {
+      if (addv) VGPU_BN_BWD_FUSED(true, float); else VGPU_BN_BWD_FUSED(false, float);
+    }
+#undef VGPU_BN_BWD_FUSED
+    return (int)hipGetLastError();
+  }
   const dim3 fg((C + kFinC - 1) / kFinC), fb(kFinC * kFinG);
   if (param_bf16)
     hipLaunchKernelGGL((bn_bwd_finalize_kernel<uint16_t>), fg, fb, 0, s, pp, G,
@@ -553,6 +754,9 @@ VGPU_API int vgpu_bn_bwd_partials(const float* partial, int64_t G, const void* d
                        addv, nvec, C / 8);
   return (int)hipGetLastError();
 }
+
+// A/B and tests: 1 = finalize + apply in one launch for small layers (default), 0 = never, -1 = env.
+VGPU_API void vgpu_bn_set_fuse_small(int on) { g_fuse_small = on < 0 ? -1 : (on ? 1 : 0); }
 
 VGPU_API void vgpu_bn_set_tuning(int target_blocks, int unroll) {
   g_target_blocks = target_blocks > 0 ? target_blocks : kTargetBlocks;

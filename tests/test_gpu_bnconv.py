@@ -140,14 +140,18 @@ def _bn_conv_ref(x, bn, weight, stride, padding, act, residual):
     return z + residual.float() if residual is not None else z
 
 
+@pytest.mark.parametrize("fuse_small", [1, 0])
 @pytest.mark.parametrize("c,cout,ks,stride,res,stats_in", [
     (64, 256, 1, 1, True, False), (256, 64, 1, 1, False, True), (64, 64, 3, 1, False, True),
     (128, 128, 3, 2, False, True)])
-def test_bn_conv_node_matches_fp32_reference(F, c, cout, ks, stride, res, stats_in):
+def test_bn_conv_node_matches_fp32_reference(F, c, cout, ks, stride, res, stats_in, fuse_small):
     """bn_conv: z, running stats, dx, dγ, dβ, dw against fp32 PyTorch; with
-    stats_in the BN's statistics come from a producing conv's epilogue."""
+    stats_in the BN's statistics come from a producing conv's epilogue.
+    fuse_small 1: finalize + apply in one launch (these layers are small), 0:
+    the separate finalize kernels."""
     import copy
     from torch import nn
+    _lib().vgpu_bn_set_fuse_small(fuse_small)
     torch.manual_seed(0)
     n, h, w = 4, 19, 17
     bn = nn.BatchNorm2d(c).cuda().train()
@@ -201,6 +205,7 @@ def test_bn_conv_node_matches_fp32_reference(F, c, cout, ks, stride, res, stats_
     if res:
         torch.testing.assert_close(r.grad.float(), gz.float())
     assert x_leaf.grad is not None and torch.isfinite(x_leaf.grad.float()).all()
+    _lib().vgpu_bn_set_fuse_small(-1)
 
 
 def test_resnet_training_step_fused_matches_unfused(F):

@@ -81,6 +81,7 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_bn_act_bwd_add.argtypes = [vp] * 10 + [i64, ci, ci, ci, vp, vp]
     lib.vgpu_bn_act_bwd_add.restype = ci
     lib.vgpu_bn_set_tuning.argtypes = [ci, ci]
+    lib.vgpu_bn_set_fuse_small.argtypes = [ci]
     lib.vgpu_maxpool_fwd_idx_nhwc.argtypes = [vp, vp, vp] + [ci] * 7 + [vp]
     lib.vgpu_maxpool_fwd_idx_nhwc.restype = ci
     lib.vgpu_maxpool_bwd_nhwc.argtypes = [vp, vp, vp] + [ci] * 7 + [vp]
