@@ -966,7 +966,19 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int fr = lane & 15, fk = lane >> 4;
-  const int lrow = t >> 3, lchunk = (t & 7) ^ (lrow & 7);
+  // LDS images: 16-B chunk c of row r sits in slot c ^ f(r).  The 16x16 reads
+  // (16 rows x 4 k-chunks per lane group) are conflict-free with f = r & 7;
+  // the 32x32 reads (32 consecutive rows, one k-chunk per 32-lane half) put two
+  // rows on one bank group in every ds_read_b128 lane group with it (4 extra
+  // LDS cycles per read: SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS = 4.1 in
+  // profiles/r4/kernels/pmc_flagship_r4.md), and none with f = (r & 7) ^ bit 3.
+  // DMA rows are i·RPI + lrow with RPI a multiple of 16, so f of the LDS row is f(lrow).
+  const int lrow = t >> 3;
+  const int lchunk = (t & 7) ^ (lrow & 7) ^ (M32 ? (lrow >> 3) & 1 : 0);
+  auto swzh = [](int row, int slot) {  // swz() with this kernel's f
+    return row * 128 + ((slot ^ (row & 7) ^ (M32 ? (row >> 3) & 1 : 0)) << 4);
+  };
+  static_assert(!M32 || (T / 8) % 16 == 0, "rows per DMA instruction keep bit 3 of the row");
   int m0, n0;
   if (a.nmajor) {
     const int xcd = blockIdx.x & 7, q = a.nwg >> 3, r8 = a.nwg & 7;
@@ -1042,7 +1054,7 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
         if constexpr (M32) {
           // k-step ks (16 channels) of lane half kb reads chunk 2·ks + kb: the
           // address of ks = that of ks 0 XOR (ks << 5)
-          aaddr[kh * 3 + kw][i] = (uint32_t)(h * 128 + (((lane >> 5) ^ (h & 7)) << 4));
+          aaddr[kh * 3 + kw][i] = (uint32_t)swzh(h, lane >> 5);
         } else {
           const uint32_t a0 = (uint32_t)(h * 128 + ((fk ^ (h & 7)) << 4));
           aaddr[kh * 3 + kw][i] = a0 | ((a0 ^ 64u) << 16);
@@ -1067,7 +1079,7 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
         af[buf][i] = *reinterpret_cast<const bf16x8_t*>(sH + (aaddr[tap][i] ^ (uint32_t)(ks << 5)));
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        bfr[buf][j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(wn * 64 + j * 32 + (lane & 31), ks * 2 + (lane >> 5)));
+        bfr[buf][j] = *reinterpret_cast<const bf16x8_t*>(sB + swzh(wn * 64 + j * 32 + (lane & 31), ks * 2 + (lane >> 5)));
     };
     rd(0, 0);
 #pragma unroll
