@@ -70,6 +70,7 @@
 #include <shared_mutex>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "common.h"
@@ -121,6 +122,9 @@ struct Knobs {
   // over the host link in 2 MiB pages (part E at equal HBM: 6.9-7.3 -> 7.5 tok/s,
   // zero-copy 7.8; profiles/r4/vmem/part_e_context_charge*.log).  VGPU_VMEM_THP=0: off.
   bool thp = true;
+  // A graph launch whose ranges are mostly on the host waits (at most this
+  // long) for the pager to bring them in — a model switch (vmem_graph_launched).
+  uint64_t gate_ms = 10000;
 };
 
 const Knobs& knobs() {
@@ -137,6 +141,7 @@ const Knobs& knobs() {
     if (const char* e = env_first("VGPU_VMEM_PLAIN_WINDOW_MS")) v.plain_window_ms = std::max(1ull, strtoull(e, nullptr, 10));
     v.cut_pieces = env_bool(env_first("VGPU_VMEM_CUT_PIECES"), true);
     v.thp = env_bool(env_first("VGPU_VMEM_THP"), true);
+    if (const char* e = env_first("VGPU_VMEM_GATE_MS")) v.gate_ms = strtoull(e, nullptr, 10);
     if (const char* e = env_first("VGPU_VMEM_MANAGED_MIN_MB")) {
       const long long mb = atoll(e);
       v.managed_min = mb < 0 ? -1 : (int64_t)mb << 20;
@@ -160,6 +165,11 @@ thread_local std::vector<uintptr_t>* tl_sink = nullptr;
 // ranges go to tl_sink only (nothing runs now, so nothing is stamped as used).
 thread_local bool tl_collect_only = false;
 std::atomic<int> g_wake{0};  // a launch named a range that is not fully in HBM
+// Tick at which a gated graph launch (vmem_graph_launched) started waiting, 0
+// when none: ranges unused since then may give way at once.
+std::atomic<uint64_t> g_gate_tick{0};
+std::mutex g_nogate_mu;
+std::unordered_set<const void*> g_nogate;  // executables whose gate gave up (they do not fit)
 
 inline void touch_word(uintptr_t w, uint64_t tick) {
   if (w < g_tab.front()->base || w >= g_tab.back()->base + g_tab.back()->size) return;
@@ -501,7 +511,9 @@ void pager_step(bool advance) {
     // other, but a model whose traffic stopped a second ago gives way at once
     // instead of after the 2 s cold window that new allocations wait for
     // (a model switch started promoting one second earlier).
-    const uint64_t stale = tick > k.hot_ticks ? tick - k.hot_ticks : 0;
+    // While a launch is gated on this promotion, its graph's ranges carry the
+    // gate's tick and everything older is idle: it may give way at once.
+    const uint64_t stale = std::max(tick > k.hot_ticks ? tick - k.hot_ticks : 0, g_gate_tick.load());
     while (r->gpu_bytes < r->size) {
       uint64_t n = std::min<uint64_t>(k.piece, r->size - r->gpu_bytes);
       (void)make_room_locked(r->dev, n, r, stale);  // what it could not free, a cut piece may still use
@@ -1032,9 +1044,13 @@ void vmem_graph_instantiated(hipGraph_t graph, hipGraphExec_t exec) {
 }
 
 void vmem_graph_destroyed(const void* graph_or_exec) {
-  std::lock_guard<std::mutex> l(g_gmu);
-  g_graph_ranges.erase(graph_or_exec);
-  g_exec_ranges.erase(graph_or_exec);
+  {
+    std::lock_guard<std::mutex> l(g_gmu);
+    g_graph_ranges.erase(graph_or_exec);
+    g_exec_ranges.erase(graph_or_exec);
+  }
+  std::lock_guard<std::mutex> l(g_nogate_mu);
+  g_nogate.erase(graph_or_exec);
 }
 
 // Explicitly built graphs (hipGraphAdd*Node, *SetParams, hipGraphExec*SetParams):
@@ -1076,6 +1092,31 @@ void vmem_graph_child(hipGraph_t graph, hipGraph_t child) {
 }
 
 // A replay runs none of our hooks: stamp every range its kernels name.
+namespace {
+// Bytes of the graph's ranges (all, and not in HBM) and their device.
+void graph_bytes(const std::vector<uintptr_t>& bases, uint64_t* total, uint64_t* host, int* dev) {
+  *total = *host = 0;
+  *dev = -1;
+  std::shared_lock<std::shared_mutex> g(g_tab_mu);
+  if (g_tab.empty()) return;
+  for (uintptr_t b : bases)
+    if (VRange* r = find_locked(b)) {
+      *total += r->size;
+      *host += r->size - std::min<uint64_t>(r->gpu_bytes, r->size);
+      *dev = r->dev;
+    }
+}
+}  // namespace
+
+// A replayed graph runs no hooks, so its ranges are stamped here.  If most of
+// them are on the host (a model switch back: part D), the launch waits for the
+// pager first: replays reading over the host link while KFD pauses the queues
+// for every migration piece ran both slowly — promotion at 1.5 GB/s beside the
+// replays against 7 GB/s alone, a 10 s switch (profiles/r4/vmem/part_d_*).
+// Only graphs whose ranges fit the budget beside the plain buffers are gated
+// (a hot set beyond the budget — part E — is read in place, never waited
+// for), at most VGPU_VMEM_GATE_MS (0: never), and an executable whose gate
+// made no progress for a second is not gated again.
 void vmem_graph_launched(hipGraphExec_t exec) {
   if (g_count.load(std::memory_order_relaxed) == 0) return;
   std::vector<uintptr_t> bases;
@@ -1085,13 +1126,73 @@ void vmem_graph_launched(hipGraphExec_t exec) {
     if (it == g_exec_ranges.end()) return;
     bases = it->second;
   }
-  const uint64_t tick = g_tick.load(std::memory_order_relaxed);
+  const Knobs& k = knobs();
+  constexpr uint64_t kGateMin = 1ull << 30;
+  uint64_t total = 0, host = 0;
+  int dev = -1;
+  bool gate = false;
+  if (k.gate_ms && k.on && !st().suspended.load(std::memory_order_relaxed)) {
+    graph_bytes(bases, &total, &host, &dev);
+    if (host >= kGateMin && dev >= 0) {
+      const uint64_t b = phys_budget(dev), plain = plain_now(dev);
+      const uint64_t room = b ? (b > plain ? b - plain : 0) : UINT64_MAX;
+      std::lock_guard<std::mutex> l(g_nogate_mu);
+      gate = total <= room && !g_nogate.count(exec);
+    }
+  }
+  // A gated launch stamps its ranges one tick ahead, so whatever ran before
+  // it is older than the gate.
+  const uint64_t tick = gate ? g_tick.fetch_add(1) + 1 : g_tick.load(std::memory_order_relaxed);
   {
     std::shared_lock<std::shared_mutex> g(g_tab_mu);
     if (g_tab.empty()) return;
     for (uintptr_t b : bases) touch_word(b, tick);
   }
   if (g_wake.load(std::memory_order_relaxed)) g_thr_cv.notify_one();
+  if (!gate) return;
+  uint64_t expected = 0;
+  g_gate_tick.compare_exchange_strong(expected, tick);
+  const auto t0 = std::chrono::steady_clock::now();
+  auto t_prog = t0;
+  uint64_t left = host;
+  bool done = false;
+  VLOG_INFO("vmem: launch waits for %llu bytes of its graph's ranges to reach HBM", (unsigned long long)host);
+  auto t_stamp = t0;
+  while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(k.gate_ms)) {
+    g_wake.store(1, std::memory_order_relaxed);
+    g_thr_cv.notify_one();
+    std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    if (std::chrono::steady_clock::now() - t_stamp > std::chrono::milliseconds(100)) {
+      // still in use: keep the graph's ranges inside the pager's hot window
+      t_stamp = std::chrono::steady_clock::now();
+      const uint64_t now_tick = g_tick.load(std::memory_order_relaxed);
+      std::shared_lock<std::shared_mutex> g(g_tab_mu);
+      if (!g_tab.empty())
+        for (uintptr_t b : bases) touch_word(b, now_tick);
+    }
+    uint64_t tot2, h2;
+    int d2;
+    graph_bytes(bases, &tot2, &h2, &d2);
+    if (h2 < kGateMin) {
+      done = true;
+      break;
+    }
+    const auto now = std::chrono::steady_clock::now();
+    if (h2 < left) {
+      left = h2;
+      t_prog = now;
+    } else if (now - t_prog > std::chrono::milliseconds(1000 + (int64_t)k.hot_ticks * k.tick_ms)) {
+      break;  // no room to be had: read in place from now on
+    }
+  }
+  expected = tick;
+  g_gate_tick.compare_exchange_strong(expected, 0);
+  if (!done) {
+    std::lock_guard<std::mutex> l(g_nogate_mu);
+    g_nogate.insert(exec);
+  }
+  VLOG_INFO("vmem: gated launch went on after %.3f s (%llu bytes still on the host)",
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(), (unsigned long long)left);
 }
 
 uint64_t vmem_graph_ranges(hipGraphExec_t exec) {
