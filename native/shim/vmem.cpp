@@ -1127,7 +1127,8 @@ void vmem_graph_launched(hipGraphExec_t exec) {
     bases = it->second;
   }
   const Knobs& k = knobs();
-  constexpr uint64_t kGateMin = 1ull << 30;
+  constexpr uint64_t kGateMin = 1ull << 30;  // gate a launch with this much of its graph on the host
+  constexpr uint64_t kGateEnd = 64ull << 20;  // and let it go once less is left (the last piece, cut)
   uint64_t total = 0, host = 0;
   int dev = -1;
   bool gate = false;
@@ -1173,7 +1174,7 @@ void vmem_graph_launched(hipGraphExec_t exec) {
     uint64_t tot2, h2;
     int d2;
     graph_bytes(bases, &tot2, &h2, &d2);
-    if (h2 < kGateMin) {
+    if (h2 < kGateEnd) {
       done = true;
       break;
     }
