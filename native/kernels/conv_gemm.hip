@@ -1290,7 +1290,9 @@ hipError_t launch_halo(ConvArgs a, hipStream_t s) {
   a.nwg = a.nM * a.nN;
   // N-major placement when the filter outgrows an XCD's L2 share (4 MiB).
   a.nmajor = (int64_t)a.Cout * a.K * 2 > ((int64_t)5 << 19) ? 1 : 0;
-  if (a.stats)
+  if (a.stats && halo_m32())
+    hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, true, 1>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
+  else if (a.stats)
     hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, false, 1>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
   else if (halo_m32())
     hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, true>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
