@@ -127,6 +127,7 @@ static void do_init() {
   s.ctx_max = parse_mem(env_first("VGPU_CONTEXT_MAX"));
   if (!s.ctx_max) s.ctx_max = 4ull << 30;
   for (auto& f : s.kfd_vram_fd) f.store(-2);
+  install_crash_trace();  // diagnostics work with control disabled too
   s.enabled = !disabled;
   if (!s.enabled) {
     VLOG_INFO("vgpu control disabled by environment");
@@ -145,7 +146,6 @@ static void do_init() {
     hostpid_publish();
   }
   trace_open();
-  install_crash_trace();
   install_signal(SIGUSR2, sig_suspend);
   install_signal(SIGUSR1, sig_resume);
   atexit(on_exit_release);
