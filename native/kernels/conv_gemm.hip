@@ -951,7 +951,7 @@ hipError_t launch_big(ConvArgs a, hipStream_t s) {
 // 64-row group per wave, merged through the wave's own slab.
 template <int BM, int BN, int HPMAX, bool M32 = false, int ST = 0>
 __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvArgs a) {
-  static_assert(ST == 0 || ST == 1, "halo: forward statistics only");
+  static_assert(ST == 0 || ST == 1 || (ST == 2 && M32), "halo: backward statistics on the 32x32 variant");
   constexpr int T = BM * BN / 64, WN = BN / 64;
   constexpr int TM = M32 ? 2 : 4, TN = M32 ? 2 : 4;  // wave tile 64 x 64
   constexpr int RPI = T / 8;                          // LDS rows (128 B) per DMA instruction
@@ -1189,10 +1189,33 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
   float s1[8], s2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.0f;
+  // ST = 2 (a data gradient feeding a BN backward): the BN's x and coefficients
+  // (vgpu_conv2d_nhwc_bn), x read per pass beside the accumulator staging.
+  float ks_[8], kt_[8], kmu[8], kis[8];
+  const __amdgpu_buffer_rsrc_t xr2 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(ST == 2 ? a.bnx : a.y), 0, ST == 2 ? a.y_bytes : 0u, 0x00020000);
+  if constexpr (ST == 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ks_[j] = a.bncoef[col + j];
+      kt_[j] = a.bncoef[a.Cout + col + j];
+      kmu[j] = a.bncoef[2 * a.Cout + col + j];
+      kis[j] = a.bncoef[3 * a.Cout + col + j];
+    }
+  }
   // 16x16 tiles: pass p = row tile i.  32x32 tiles: pass p = half (p & 1) of row
   // tile p >> 1; lane l holds rows 8b + 4(l >> 5) + e (b = 0..3) of column l & 31.
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
+    u32x4 xb[2];
+    if constexpr (ST == 2) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int m = m0 + wm * 64 + p * 16 + erow + 8 * r;
+        xb[r] = __builtin_amdgcn_raw_buffer_load_b128(
+            xr2, m < a.M ? (uint32_t)(((int64_t)m * a.Cout + col) * 2) : kOOB, 0, 0);
+      }
+    }
     if constexpr (M32) {
       const int i = p >> 1, hb = (p & 1) * 2;
 #pragma unroll
@@ -1220,6 +1243,12 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);
       }
+      float xf[8];
+      if constexpr (ST == 2) {
+        unpack8(xb[r], xf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= bn_act_grad(a.bnact, fmaf(xf[j], ks_[j], kt_[j]));
+      }
       const u32x4 o = pack8(v);
       if (m < a.M) *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = o;
       if constexpr (ST != 0) {
@@ -1230,7 +1259,7 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
         for (int j = 0; j < 8; ++j) {
           const float d = q[j] * ok;
           s1[j] += d;
-          s2[j] = fmaf(d, d, s2[j]);
+          s2[j] = fmaf(d, ST == 2 ? (xf[j] - kmu[j]) * kis[j] : d, s2[j]);
         }
       }
     }
@@ -1290,7 +1319,9 @@ hipError_t launch_halo(ConvArgs a, hipStream_t s) {
   a.nwg = a.nM * a.nN;
   // N-major placement when the filter outgrows an XCD's L2 share (4 MiB).
   a.nmajor = (int64_t)a.Cout * a.K * 2 > ((int64_t)5 << 19) ? 1 : 0;
-  if (a.stats && halo_m32())
+  if (a.stats && a.bnx)  // the dispatch sends backward statistics here only with the 32x32 variant
+    hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, true, 2>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
+  else if (a.stats && halo_m32())
     hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, true, 1>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
   else if (a.stats)
     hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, false, 1>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
@@ -2547,7 +2578,7 @@ int conv2d_impl(const void* x, const void* w, void* y, const void* res, const fl
                                 (g_forced_big == 2 && C >= 1024 && tiles256 >= (int64_t)conv_cus()));
     // 3x3 / stride 1 without prologue or residual: the halo-tile kernel.
     const bool halo = (g_forced_halo < 0 ? halo_enabled() : g_forced_halo > 0) && !narrow && !pro && !has_res &&
-                      KS == 3 && stride == 1 && pad == 1 && !bnx;
+                      KS == 3 && stride == 1 && pad == 1 && (!bnx || halo_m32());
     if (halo && (e = dispatch_halo(c, s)) != hipErrorNotSupported) {
       // launched (or a launch error)
     } else if (big)

@@ -90,11 +90,13 @@ def test_forward_statistics_match_the_stored_output(F, n, c, h, w, cout, ks, str
     torch.testing.assert_close(st.double(), want, atol=1e-3 * want.abs().max().item() + 1e-4, rtol=1e-4)
 
 
-@pytest.mark.parametrize("n,c,h,w,ks,act,tile_m", [
-    (2, 64, 9, 11, 1, 1, 64), (3, 128, 17, 13, 1, 1, 128), (2, 256, 8, 8, 1, 2, 0),
-    (2, 64, 23, 21, 3, 1, 64), (2, 128, 15, 15, 3, 1, 128), (2, 128, 11, 11, 3, 0, 0)])
-def test_backward_statistics_mask_and_sum_the_data_gradient(F, n, c, h, w, ks, act, tile_m):
-    """dgrad epilogue with the BN's x: stores dy·act'(x·s + t) and (Σ, Σ·x̂)."""
+@pytest.mark.parametrize("n,c,h,w,ks,act,tile_m,halo", [
+    (2, 64, 9, 11, 1, 1, 64, 0), (3, 128, 17, 13, 1, 1, 128, 0), (2, 256, 8, 8, 1, 2, 0, 0),
+    (2, 64, 23, 21, 3, 1, 64, 0), (2, 128, 15, 15, 3, 1, 128, 0), (2, 128, 11, 11, 3, 0, 0, 0),
+    (4, 128, 15, 15, 3, 1, 0, 1), (20, 256, 11, 11, 3, 1, 0, 1), (3, 128, 16, 16, 3, 2, 0, 1)])
+def test_backward_statistics_mask_and_sum_the_data_gradient(F, n, c, h, w, ks, act, tile_m, halo):
+    """dgrad epilogue with the BN's x: stores dy·act'(x·s + t) and (Σ, Σ·x̂)
+    (halo 1: the 3x3 data gradient on the 32x32 halo kernel)."""
     from vgpu.ops import conv as C
     lib = _lib()
     cout = 128
@@ -109,16 +111,19 @@ def test_backward_statistics_mask_and_sum_the_data_gradient(F, n, c, h, w, ks, a
     out = torch.empty_like(x)
     st = torch.empty(((n * h * w + 63) // 64, c, 2), dtype=torch.float32, device="cuda")
     lib.vgpu_conv_set_tile_m(tile_m)
-    lib.vgpu_conv_set_halo(0)   # the fused backward never takes the halo kernel: compare like with like
+    lib.vgpu_conv_set_halo(halo)   # the same kernel family for the fused and the plain data gradient
     try:
+        before = lib.vgpu_conv_halo_launches()
         rc = lib.vgpu_conv2d_nhwc_bn(_ptr(dz), _ptr(wt), _ptr(out), None, n, h, w, cout, c, ks, 1, ks - 1 - pad,
                                      _ptr(st), _ptr(x), _ptr(coef), act, 1, _stream())
+        ran_halo = lib.vgpu_conv_halo_launches() > before
         dy = C.conv2d(dz, wt, stride=1, padding=ks - 1 - pad)   # the plain data gradient, same kernel
         torch.cuda.synchronize()
     finally:
         lib.vgpu_conv_set_tile_m(0)
         lib.vgpu_conv_set_halo(-1)
     assert rc == 0
+    assert ran_halo == bool(halo)
     s, t, mu, inv = (coef[i * c:(i + 1) * c].view(1, c, 1, 1) for i in range(4))
     pre = x.float() * s + t
     mask = (pre > 0).float() if act == 1 else (((pre > 0) & (pre < 6)).float() if act == 2 else torch.ones_like(pre))
