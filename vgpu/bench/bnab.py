@@ -8,6 +8,13 @@ apply) and backward (reduce + finalize + apply) per layer, interleaved.
 
 One JSON line per shape plus totals.  Every variant's outputs are compared with
 the first's (the reduction order changes, so up to bf16 rounding).
+
+The timings are of eager autograd calls: on MI355X every shape measured
+227-233 µs for every variant (round 4), i.e. the host's launch path, not the
+kernels — use rocprofv3 kernel times to compare variants.  Since round 4 the
+training path takes its BatchNorm statistics from the conv epilogues
+(vgpu.ops.bnconv), so these reduction kernels run only where that does not
+apply.
 """
 from __future__ import annotations
 
