@@ -254,47 +254,35 @@ __global__ void __launch_bounds__(kFinC * kFinG) bn_bwd_finalize_kernel(
   coef[3 * C + c] = -s * db * inv_m - mu * cc;
 }
 
-// The apply passes stream the activation: kU vectors per thread in flight per
-// iteration (their loads issued before any arithmetic) — one per iteration left
-// ~8 MB in flight chip-wide, under what HBM3E latency needs.
-template <int kAct, int kU = 4>
+#define VGPU_BN_GRID_LOOP(i, ci, nvec, cvec)                                       \
+  const uint64_t stride_ = (uint64_t)gridDim.x * kThreads;                         \
+  const uint32_t cstep_ = (uint32_t)(stride_ % (cvec));                            \
+  uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;                      \
+  uint32_t ci = (uint32_t)(i % (cvec));                                            \
+  for (; i < (nvec); i += stride_, ci = (ci + cstep_ >= (cvec)) ? ci + cstep_ - (cvec) : ci + cstep_)
+
+template <int kAct>
 __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const bf16x8* __restrict__ x,
                                                             bf16x8* __restrict__ y,
                                                             const float* __restrict__ coef,
                                                             uint64_t nvec, uint32_t cvec) {
   const float* sc = coef;
   const float* sh = coef + cvec * 8;
-  const uint64_t stride = (uint64_t)gridDim.x * kThreads;
-  const uint32_t cstep = (uint32_t)(stride % cvec);
-  uint64_t i0 = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  uint32_t ci = (uint32_t)(i0 % cvec);
-  for (; i0 < nvec; i0 += kU * stride) {
-    bf16x8 v[kU];
-    uint32_t cu[kU];
+  VGPU_BN_GRID_LOOP(i, ci, nvec, cvec) {
+    const bf16x8 v = x[i];
+    float s[8], t[8];
+    load8(sc + ci * 8, s);
+    load8(sh + ci * 8, t);
+    bf16x8 o;
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const uint64_t i = i0 + u * stride;
-      v[u] = x[i < nvec ? i : i0];
-      cu[u] = ci;
-      ci = ci + cstep >= cvec ? ci + cstep - cvec : ci + cstep;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const uint64_t i = i0 + u * stride;
-      float s[8], t[8];
-      load8(sc + cu[u] * 8, s);
-      load8(sh + cu[u] * 8, t);
-      bf16x8 o;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) o.v[k] = f2bf(act_fwd<kAct>(fmaf(bf2f(v[u].v[k]), s[k], t[k])));
-      if (i < nvec) y[i] = o;
-    }
+    for (int k = 0; k < 8; ++k) o.v[k] = f2bf(act_fwd<kAct>(fmaf(bf2f(v.v[k]), s[k], t[k])));
+    y[i] = o;
   }
 }
 
 // kAdd: dx += add (a second gradient of x, e.g. the identity shortcut's),
 // summed in fp32 before the one bf16 rounding — replaces an autograd add pass.
-template <int kAct, bool kAdd, int kU = 2>
+template <int kAct, bool kAdd>
 __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const bf16x8* __restrict__ dy,
                                                                 const bf16x8* __restrict__ x,
                                                                 bf16x8* __restrict__ dx,
@@ -302,41 +290,26 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const bf16x8* __
                                                                 const bf16x8* __restrict__ add,
                                                                 uint64_t nvec, uint32_t cvec) {
   const uint32_t C = cvec * 8;
-  const uint64_t stride = (uint64_t)gridDim.x * kThreads;
-  const uint32_t cstep = (uint32_t)(stride % cvec);
-  uint64_t i0 = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  uint32_t ci = (uint32_t)(i0 % cvec);
-  for (; i0 < nvec; i0 += kU * stride) {
-    bf16x8 v[kU], g[kU], r[kU];
-    uint32_t cu[kU];
+  VGPU_BN_GRID_LOOP(i, ci, nvec, cvec) {
+    const bf16x8 v = x[i];
+    const bf16x8 g = dy[i];
+    bf16x8 r;
+    if constexpr (kAdd) r = add[i];
+    float s[8], t[8], cc[8], b[8];
+    load8(coef + ci * 8, s);
+    load8(coef + C + ci * 8, t);
+    load8(coef + 2 * C + ci * 8, cc);
+    load8(coef + 3 * C + ci * 8, b);
+    bf16x8 o;
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const uint64_t i = i0 + u * stride, ii = i < nvec ? i : i0;
-      v[u] = x[ii];
-      g[u] = dy[ii];
-      if constexpr (kAdd) r[u] = add[ii];
-      cu[u] = ci;
-      ci = ci + cstep >= cvec ? ci + cstep - cvec : ci + cstep;
+    for (int k = 0; k < 8; ++k) {
+      const float xf = bf2f(v.v[k]);
+      const float dz = bf2f(g.v[k]) * act_grad<kAct>(fmaf(xf, s[k], t[k]));
+      float d = fmaf(s[k], dz, fmaf(cc[k], xf, b[k]));
+      if constexpr (kAdd) d += bf2f(r.v[k]);
+      o.v[k] = f2bf(d);
     }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const uint64_t i = i0 + u * stride;
-      float s[8], t[8], cc[8], b[8];
-      load8(coef + cu[u] * 8, s);
-      load8(coef + C + cu[u] * 8, t);
-      load8(coef + 2 * C + cu[u] * 8, cc);
-      load8(coef + 3 * C + cu[u] * 8, b);
-      bf16x8 o;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float xf = bf2f(v[u].v[k]);
-        const float dz = bf2f(g[u].v[k]) * act_grad<kAct>(fmaf(xf, s[k], t[k]));
-        float d = fmaf(s[k], dz, fmaf(cc[k], xf, b[k]));
-        if constexpr (kAdd) d += bf2f(r[u].v[k]);
-        o.v[k] = f2bf(d);
-      }
-      if (i < nvec) dx[i] = o;
-    }
+    dx[i] = o;
   }
 }
 
