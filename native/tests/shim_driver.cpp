@@ -4,6 +4,7 @@
 //
 // It links the fake libamdhip64.so.7 exactly the way libc10_hip.so links the
 // real one, so every hip* call below goes through the preloaded interposer.
+#include <chrono>
 #include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 #include <signal.h>
@@ -970,7 +971,11 @@ int main(int argc, char** argv) {
            (unsigned long long)(granges ? granges(exec) : 999));
     usleep(300000);  // A idles too (only B will be used from now on)
     for (int t = 0; t < 60; ++t) {  // replay for 0.6 s
+      const auto t0 = std::chrono::steady_clock::now();
       hipGraphLaunch(exec, st);
+      if (t == 0)  // gated: B is in HBM before its first replay runs (vmem_graph_launched)
+        printf("b_gpu_after_first_launch=%llu\nfirst_launch_ms=%lld\n", gb(b),
+               (long long)std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count());
       note();
       usleep(10000);
     }

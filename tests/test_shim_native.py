@@ -178,6 +178,8 @@ def test_vmem_budget_graph_replay_and_suspend(native_build):
     assert o["alloc_a"] == "0" and int(o["a_gpu_at_alloc"]) == 6 * GiB and o["b_gpu_after_a"] == "0"
     assert (o["end_capture"], o["instantiate"], o["graph_ranges"]) == ("0", "0", "1")
     assert int(o["b_gpu_after_replay"]) == 6 * GiB and o["a_gpu_after_replay"] == "0"
+    # the first replay waited for the pager (a model switch), bounded
+    assert int(o["b_gpu_after_first_launch"]) == 6 * GiB and int(o["first_launch_ms"]) < 5000
     assert (o["suspended_b_gpu"], o["suspended_a_gpu"], o["suspended_phys"]) == ("0", "0", "0")
     assert int(o["suspended_host"]) == 12 * GiB
     assert int(o["resumed_b_gpu"]) == 6 * GiB
