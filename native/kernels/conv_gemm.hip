@@ -1004,8 +1004,8 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
   // Halo DMA sources (channel block 0); block cb adds cb·128 B.  A literal
   // array bound: a lambda capturing a local array of value-dependent size
   // fails substitution in the host pass, which then emits no launch stub.
-  static_assert(HI <= 9, "halo DMA registers");
-  uint32_t hsrc[9];
+  static_assert(HI <= 6, "halo DMA registers");
+  uint32_t hsrc[6];
 #pragma unroll
   for (int i = 0; i < HI; ++i) {
     const int h = i * RPI + lrow;
@@ -1335,19 +1335,6 @@ hipError_t launch_halo(ConvArgs a, hipStream_t s) {
 // Halo pixels a BM-pixel tile of a W-wide image can need: rows spanned + 2.
 inline int halo_pixels(int bm, int w) { return ((bm - 1) / w + 4) * w; }
 
-// 64-row tiles (two waves, each still a 64x64 wave tile) when 128-row tiles
-// leave most CUs idle: ResNet-V2-152 b=10 stage 3 has 4 840 rows = 76 tiles of
-// 128x128 on 256 CUs.  Twice the workgroups at half the LDS traffic per CU.
-// VGPU_CONV_HALO_SMALL=0: off.
-int g_halo_small = -1;
-bool halo_small() {
-  if (g_halo_small < 0) {
-    const char* v = getenv("VGPU_CONV_HALO_SMALL");
-    g_halo_small = (v && v[0] == '0') ? 0 : 1;
-  }
-  return g_halo_small == 1;
-}
-
 // 3x3 / stride 1 / pad 1, no prologue / residual, Cout % 128 == 0.  Returns
 // hipErrorNotSupported when no halo instantiation fits (the caller falls back).
 hipError_t dispatch_halo(const ConvArgs& a, hipStream_t s) {
@@ -1355,9 +1342,6 @@ hipError_t dispatch_halo(const ConvArgs& a, hipStream_t s) {
   const int64_t tiles256 = (int64_t)((a.M + 255) / 256) * (a.Cout / 128);
   const bool big = g_forced_halo == 2 || (g_forced_halo != 3 && tiles256 * 5 >= (int64_t)conv_cus() * 3);
   if (big && halo_pixels(256, a.W) <= 383) return launch_halo<256, 128, 384>(a, s);
-  const int64_t tiles128 = (int64_t)((a.M + 127) / 128) * (a.Cout / 128);
-  if (g_forced_halo < 2 && halo_small() && tiles128 < (int64_t)conv_cus() && halo_pixels(64, a.W) <= 143)
-    return launch_halo<64, 128, 144>(a, s);
   if (g_forced_halo != 2 && halo_pixels(128, a.W) <= 191) return launch_halo<128, 128, 192>(a, s);
   return hipErrorNotSupported;
 }
@@ -2374,7 +2358,6 @@ VGPU_API void vgpu_conv_set_big(int mode) { g_forced_big = mode; }  // -1 env/he
 VGPU_API void vgpu_conv_set_halo(int mode) { g_forced_halo = mode; }  // -1 env, 0 off, 1 on, 2/3 BM 256/128
 VGPU_API unsigned long long vgpu_conv_halo_launches() { return g_halo_launches; }
 VGPU_API void vgpu_conv_set_halo_m32(int on) { g_halo_m32 = on < 0 ? -1 : (on ? 1 : 0); }  // -1: env
-VGPU_API void vgpu_conv_set_halo_small(int on) { g_halo_small = on < 0 ? -1 : (on ? 1 : 0); }  // -1: env
 
 // Fused conv2 (3x3, pad 1, stride s, C = W → W, bias + ReLU) + conv3 (1x1,
 // W → 4W) + residual; with w1n, also the next block's conv1 (1x1, 4W → W,

@@ -142,38 +142,6 @@ def test_conv_halo_integer_exact(C, tile, m32):
     assert torch.equal(got.float(), C.conv2d_ref(x, wt, stride=1, padding=1).to(torch.bfloat16).float())
 
 
-SMALL_HALO_CASES = [
-    # grids of 128-row tiles that leave CUs idle take 64-row tiles (conv_gemm.hip halo_small)
-    (10, 256, 22, 22, 256, True, "relu"),   # ResNet-V2-152 b=10 stage 3: 76 tiles of 128x128
-    (10, 512, 11, 11, 512, False, "none"),  # stage 4 (N-major placement)
-    (3, 128, 13, 17, 128, True, "none"),    # odd width, ragged last tile
-    (1, 64, 9, 1, 128, False, "relu"),      # W = 1
-]
-
-
-@pytest.mark.parametrize("case", SMALL_HALO_CASES, ids=lambda c: "x".join(map(str, c[:5])))
-def test_conv_halo_small_tiles_match_fp32_and_the_128_row_tiles(C, case):
-    from vgpu.native import load_kernels
-    n, c, h, w, cout, has_bias, act = case
-    x = _t((n, c, h, w), 51)
-    wt = _t((cout, c, 3, 3), 52, scale=(2.0 / (9 * c)) ** 0.5)
-    bias = _f((cout,), 53) if has_bias else None
-    lib = load_kernels()
-    outs = []
-    try:
-        for small in (1, 0):
-            lib.vgpu_conv_set_halo_small(small)
-            before = lib.vgpu_conv_halo_launches()
-            outs.append(C.conv2d(x, wt, bias, stride=1, padding=1, act=act))
-            assert lib.vgpu_conv_halo_launches() == before + 1, "the halo kernel did not run"
-    finally:
-        lib.vgpu_conv_set_halo_small(-1)
-    ref = C.conv2d_ref(x, wt, bias, stride=1, padding=1, act=act)
-    torch.testing.assert_close(outs[0].float(), ref, atol=3e-2, rtol=2e-2)
-    # same K order per output element: bit-identical to the 128-row tiles
-    assert torch.equal(outs[0], outs[1])
-
-
 DEEP_CASES = [
     # deep-K 1x1 convs with a BN+ReLU prologue (conv_pro_kernel / register path)
     (3, 256, 13, 13, 512, 2, True, "none", False),   # strided projection shortcut, K = 4 steps

@@ -66,7 +66,6 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_conv_set_halo.argtypes = [ci]
     lib.vgpu_conv_halo_launches.restype = ctypes.c_ulonglong
     lib.vgpu_conv_set_halo_m32.argtypes = [ci]
-    lib.vgpu_conv_set_halo_small.argtypes = [ci]
     lib.vgpu_lstm_recurrence.argtypes = [vp, vp, vp, vp, ci, ci, ci, vp]
     lib.vgpu_lstm_recurrence.restype = ci
     lib.vgpu_lstm_forward_train.argtypes = [vp] * 5 + [ci, ci, ci, vp]
