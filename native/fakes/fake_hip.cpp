@@ -52,8 +52,29 @@ std::vector<Dev> g_devs;
 std::map<uintptr_t, std::pair<int, uint64_t>> g_allocs;  // ptr -> (dev, size)
 uintptr_t g_next = 0x7f0000000000ull;
 thread_local int tl_dev = 0;
-std::atomic<uint64_t> g_launches{0};
-std::atomic<uint64_t> g_launch_blocks{0};
+// Launch counters sharded per thread: a launch from one thread touches no
+// cache line another launching thread writes (the shim's launch-path cost is
+// measured on this runtime, `shim_driver launchcost`).
+struct alignas(64) Shard {
+  std::atomic<uint64_t> v{0};
+};
+struct Sharded {
+  Shard s[64];
+  void add(uint64_t n) {
+    static std::atomic<unsigned> next{0};
+    thread_local unsigned me = next.fetch_add(1) & 63;
+    s[me].v.fetch_add(n, std::memory_order_relaxed);
+  }
+  uint64_t load() const {
+    uint64_t t = 0;
+    for (const Shard& x : s) t += x.v.load(std::memory_order_relaxed);
+    return t;
+  }
+  void fetch_add(uint64_t n) { add(n); }
+};
+Sharded g_launches;
+std::atomic<uint64_t> g_branchy_single_queue{0};  // graph launches the real runtime would crash on
+Sharded g_launch_blocks;
 std::atomic<uint64_t> g_graph_launches{0};
 bool g_inited = false;
 
@@ -75,7 +96,7 @@ uint64_t now_ns() {
 }
 std::mutex g_tl_mu;
 uint64_t g_busy_until = 0;   // private timeline
-uint64_t g_my_last_end = 0;  // end of this process's latest launch
+std::atomic<uint64_t> g_my_last_end{0};  // end of this process's latest launch
 std::atomic<uint64_t> g_exec_ns{0};
 
 void sleep_until(uint64_t t) {
@@ -91,10 +112,7 @@ void timeline_launch() {
   const uint64_t dur = (uint64_t)us * 1000;
   // A full AQL queue blocks the submitter: keep at most ~20 ms queued.
   uint64_t last;
-  {
-    std::lock_guard<std::mutex> g(g_tl_mu);
-    last = g_my_last_end;
-  }
+  last = g_my_last_end.load();
   if (last > 20000000ull) sleep_until(last - 20000000ull);
   std::lock_guard<std::mutex> g(g_tl_mu);
   const uint64_t now = now_ns();
@@ -142,10 +160,7 @@ void timeline_launch() {
   g_exec_ns.fetch_add(dur);
 }
 
-uint64_t timeline_last_end() {
-  std::lock_guard<std::mutex> g(g_tl_mu);
-  return g_my_last_end;
-}
+uint64_t timeline_last_end() { return g_my_last_end.load(std::memory_order_acquire); }
 
 
 struct FakeEvent {
@@ -238,9 +253,12 @@ void init_locked() {
   }
 }
 
+std::atomic<int> g_init_done{0};
 void init() {
+  if (g_init_done.load(std::memory_order_acquire)) return;  // launch path: no lock once initialised
   std::lock_guard<std::mutex> g(g_mu);
   init_locked();
+  g_init_done.store(1, std::memory_order_release);
 }
 
 // Fake KFD per-process VRAM counter (/sys/class/kfd/kfd/proc/<pid>/vram_<gpu id>):
@@ -307,6 +325,31 @@ hipError_t hipSetDevice(int d) {
   return hipSuccess;
 }
 hipError_t hipGetDevice(int* d) { *d = tl_dev; return hipSuccess; }
+// Streams remember the device they were created on (hipStreamGetDevice);
+// handles never created here (a test's made-up stream) belong to the current device.
+std::mutex g_stream_mu;
+std::map<hipStream_t, int> g_stream_dev;
+std::atomic<uintptr_t> g_next_stream{0x7000000};
+hipError_t hipStreamCreateWithFlags(hipStream_t* st, unsigned int) {
+  if (!st) return hipErrorInvalidValue;
+  *st = reinterpret_cast<hipStream_t>(g_next_stream.fetch_add(64));
+  std::lock_guard<std::mutex> g(g_stream_mu);
+  g_stream_dev[*st] = tl_dev;
+  return hipSuccess;
+}
+hipError_t hipStreamCreate(hipStream_t* st) { return hipStreamCreateWithFlags(st, 0); }
+hipError_t hipStreamGetDevice(hipStream_t st, hipDevice_t* d) {
+  if (!d) return hipErrorInvalidValue;
+  std::lock_guard<std::mutex> g(g_stream_mu);
+  auto it = g_stream_dev.find(st);
+  *d = it == g_stream_dev.end() ? tl_dev : it->second;
+  return hipSuccess;
+}
+hipError_t hipStreamDestroy(hipStream_t st) {
+  std::lock_guard<std::mutex> g(g_stream_mu);
+  g_stream_dev.erase(st);
+  return hipSuccess;
+}
 hipError_t hipGetDeviceCount(int* n) { init(); *n = (int)g_devs.size(); return hipSuccess; }
 hipError_t hipGetLastError() { return hipSuccess; }
 hipError_t hipStreamSynchronize(hipStream_t) { sleep_until(timeline_last_end()); return hipSuccess; }
@@ -892,9 +935,11 @@ struct FakeNode {
   hipGraphNodeType type;
   dim3 grid;
   hipGraph_t child;
+  const void* func = nullptr;  // kernel nodes: the host stub (hipKernelNodeParams::func)
 };
 struct FakeGraph {
   std::vector<FakeNode*> nodes;
+  std::vector<std::pair<FakeNode*, FakeNode*>> edges;  // dependencies (from, to)
   uint64_t alloc_bytes = 0;  // captured hipMallocAsync bytes (graph alloc nodes)
 };
 // A capture yields an (empty) graph: enough for the shim's capture -> graph
@@ -940,6 +985,7 @@ hipError_t hipGraphKernelNodeGetParams(hipGraphNode_t node, hipKernelNodeParams*
   *p = hipKernelNodeParams{};
   p->gridDim = fn->grid;
   p->blockDim = dim3(256, 1, 1);
+  p->func = const_cast<void*>(fn->func);
   return hipSuccess;
 }
 hipError_t hipGraphChildGraphNodeGetGraph(hipGraphNode_t node, hipGraph_t* g) {
@@ -976,6 +1022,22 @@ hipError_t hipGraphLaunch(hipGraphExec_t e, hipStream_t) {
       g_graph_mem[tl_dev] = fg->alloc_bytes;
     }
   }
+  // The ROCm 7 runtime's multi-stream executor reads past its stream list when
+  // GPU_MAX_HW_QUEUES=1 and the graph has parallel branches (a node with two
+  // successors): the real runtime segfaults, the fake refuses the launch.
+  if (e) {
+    static const bool one_queue = getenv("GPU_MAX_HW_QUEUES") && atoi(getenv("GPU_MAX_HW_QUEUES")) == 1;
+    std::lock_guard<std::mutex> g(g_mu);
+    auto* fg = g_live_execs.count(e) ? reinterpret_cast<FakeGraph*>(*reinterpret_cast<hipGraph_t*>(e)) : nullptr;
+    if (one_queue && fg) {
+      std::map<FakeNode*, int> succ;
+      for (auto& ed : fg->edges)
+        if (++succ[ed.first] > 1) {
+          g_branchy_single_queue.fetch_add(1);
+          return hipErrorLaunchFailure;
+        }
+    }
+  }
   g_graph_launches.fetch_add(1);
   g_launches.fetch_add(1);
   timeline_launch();
@@ -992,10 +1054,41 @@ static hipGraphNode_t add_node(hipGraphNode_t* node, hipGraph_t g, FakeNode* n) 
   if (node) *node = reinterpret_cast<hipGraphNode_t>(n);
   return reinterpret_cast<hipGraphNode_t>(n);
 }
-hipError_t hipGraphAddKernelNode(hipGraphNode_t* node, hipGraph_t g, const hipGraphNode_t*, size_t,
+hipError_t hipGraphAddKernelNode(hipGraphNode_t* node, hipGraph_t g, const hipGraphNode_t* deps, size_t ndeps,
                                  const hipKernelNodeParams* p) {
   if (!g || !p) return hipErrorInvalidValue;
-  add_node(node, g, new FakeNode{hipGraphNodeTypeKernel, p->gridDim, nullptr});
+  hipGraphNode_t n = add_node(node, g, new FakeNode{hipGraphNodeTypeKernel, p->gridDim, nullptr, p->func});
+  for (size_t i = 0; i < ndeps; ++i)
+    reinterpret_cast<FakeGraph*>(g)->edges.push_back({reinterpret_cast<FakeNode*>(deps[i]), reinterpret_cast<FakeNode*>(n)});
+  return hipSuccess;
+}
+hipError_t hipGraphGetEdges(hipGraph_t g, hipGraphNode_t* from, hipGraphNode_t* to, size_t* n) {
+  if (!g || !n) return hipErrorInvalidValue;
+  auto& e = reinterpret_cast<FakeGraph*>(g)->edges;
+  if (from && to)
+    for (size_t i = 0; i < e.size() && i < *n; ++i) {
+      from[i] = reinterpret_cast<hipGraphNode_t>(e[i].first);
+      to[i] = reinterpret_cast<hipGraphNode_t>(e[i].second);
+    }
+  *n = e.size();
+  return hipSuccess;
+}
+hipError_t hipGraphAddDependencies(hipGraph_t g, const hipGraphNode_t* from, const hipGraphNode_t* to, size_t n) {
+  if (!g) return hipErrorInvalidValue;
+  for (size_t i = 0; i < n; ++i)
+    reinterpret_cast<FakeGraph*>(g)->edges.push_back(
+        {reinterpret_cast<FakeNode*>(from[i]), reinterpret_cast<FakeNode*>(to[i])});
+  return hipSuccess;
+}
+hipError_t hipGraphRemoveDependencies(hipGraph_t g, const hipGraphNode_t* from, const hipGraphNode_t* to, size_t n) {
+  if (!g) return hipErrorInvalidValue;
+  auto& e = reinterpret_cast<FakeGraph*>(g)->edges;
+  for (size_t i = 0; i < n; ++i) {
+    auto it = std::find(e.begin(), e.end(), std::make_pair(reinterpret_cast<FakeNode*>(from[i]),
+                                                           reinterpret_cast<FakeNode*>(to[i])));
+    if (it == e.end()) return hipErrorInvalidValue;
+    e.erase(it);
+  }
   return hipSuccess;
 }
 static hipError_t set_kernel_params(hipGraphNode_t node, const hipKernelNodeParams* p) {
@@ -1073,6 +1166,7 @@ hipError_t hipGetProcAddress(const char* sym, void** pfn, int, uint64_t,
 
 // ---- test introspection ----
 uint64_t fake_hip_launches() { return g_launches.load(); }
+uint64_t fake_hip_branchy_single_queue_launches() { return g_branchy_single_queue.load(); }
 uint64_t fake_hip_memsets() { return g_memsets.load(); }
 uint64_t fake_hip_exec_ns() { return g_exec_ns.load(); }
 uint64_t fake_hip_launch_blocks() { return g_launch_blocks.load(); }

@@ -49,6 +49,11 @@ extern "C" {
 
 /* vgpu_device_cfg_t.flags */
 #define VGPU_DEV_FLAG_SUSPEND_EVICT 1u /* suspend (SIGUSR2) evicts the container's HBM (VGPU_SUSPEND_EVICT) */
+/* Bits 16-31 of vgpu_device_cfg_t.flags: generation of the device plugin's
+ * writes of cu_mask (vgpu_region_set_cu_mask bumps it).  The processes of a
+ * container also write the mask (adaptive share claims); only a generation
+ * change means the plugin reshaped the pool. */
+#define VGPU_DEV_POOL_GEN_SHIFT 16
 
 /* process slot status */
 #define VGPU_PROC_FREE 0

@@ -92,6 +92,11 @@ __attribute__((visibility("default"))) int vgpu_region_set_cu_mask(void* rp, int
   if (region_lock(r) != 0) return -1;
   for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w)
     __atomic_store_n(&r->dev[dev].cu_mask[w], words[w], __ATOMIC_RELAXED);
+  // New plugin generation (after the words: a reader that sees it sees them).
+  uint32_t f = __atomic_load_n(&r->dev[dev].flags, __ATOMIC_RELAXED);
+  const uint32_t gen = ((f >> VGPU_DEV_POOL_GEN_SHIFT) + 1) & 0xffffu;
+  f = (f & ((1u << VGPU_DEV_POOL_GEN_SHIFT) - 1)) | (gen << VGPU_DEV_POOL_GEN_SHIFT);
+  __atomic_store_n(&r->dev[dev].flags, f, __ATOMIC_RELEASE);
   region_unlock(r);
   return 0;
 }

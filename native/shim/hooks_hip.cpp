@@ -27,6 +27,31 @@ namespace {
 
 inline int cur_dev() { return tl_device; }
 
+// The device a launch onto `stream` runs on: the stream's own device, not the
+// calling thread's current one (a multi-GPU process launches onto another
+// device's stream, or replays a graph on it, with any device current).  The
+// null / per-thread streams belong to the current device.  Cached per thread;
+// a destroyed stream bumps the generation (its handle may be reused).
+std::atomic<uint32_t> g_stream_gen{0};
+inline int launch_dev(hipStream_t stream) {
+  if (!stream || stream == hipStreamPerThread) return tl_device;
+  struct Entry {
+    hipStream_t s;
+    int dev;
+    uint32_t gen;
+  };
+  thread_local Entry cache[8] = {};
+  thread_local unsigned next = 0;
+  const uint32_t gen = g_stream_gen.load(std::memory_order_relaxed);
+  for (const Entry& e : cache)
+    if (e.s == stream && e.gen == gen) return e.dev;
+  hipDevice_t d = -1;
+  auto get = REAL_HIP(hipStreamGetDevice);
+  if (!get || get(stream, &d) != hipSuccess || d < 0 || d >= VGPU_MAX_DEVICES) return tl_device;
+  cache[next++ & 7] = Entry{stream, (int)d, gen};
+  return (int)d;
+}
+
 // Marks the real runtime call of an allocation hook (see tl_in_hip_alloc).
 struct InHipAlloc {
   InHipAlloc() { ++tl_in_hip_alloc; }
@@ -41,6 +66,7 @@ inline uint64_t blocks3(unsigned x, unsigned y, unsigned z) {
 struct GraphWork {
   uint64_t wg = 0;
   uint32_t kernels = 0;
+  uint32_t collectives = 0;  // kernel nodes whose host stub is RCCL's (exempt_kernel)
 };
 std::mutex g_graph_mu;
 std::unordered_map<const void*, GraphWork> g_graph_wg;
@@ -64,6 +90,7 @@ GraphWork graph_workgroups(hipGraph_t g, int depth) {
       if (get_kernel(nodes[i], &kp) == hipSuccess) {
         out.wg += blocks3(kp.gridDim.x, kp.gridDim.y, kp.gridDim.z);
         out.kernels++;
+        if (exempt_kernel(kp.func)) out.collectives++;
       }
     } else if (t == hipGraphNodeTypeGraph && get_child) {
       hipGraph_t child = nullptr;
@@ -71,6 +98,7 @@ GraphWork graph_workgroups(hipGraph_t g, int depth) {
         GraphWork c = graph_workgroups(child, depth + 1);
         out.wg += c.wg;
         out.kernels += c.kernels;
+        out.collectives += c.collectives;
       }
     }
   }
@@ -529,9 +557,19 @@ __attribute__((visibility("default"))) hipError_t hipMemcpyPeerAsync(void* dst, 
 
 // Application prefetches of managed memory: cut to what HBM holds beyond the
 // headroom, and left to the pager inside its own ranges (vmem_prefetch_allowed).
-static hipError_t prefetch_hook(const void* p, size_t n, int dev, const std::function<hipError_t(size_t)>& real) {
+// A process with neither virtual device memory nor managed memory of its own
+// has nothing a prefetch could overfill HBM with and pays nothing here (ADVICE
+// r4: the HBM-free query is several runtime and sysfs calls), and a prefetch
+// being captured into a graph is left alone (no runtime queries inside a capture).
+static hipError_t prefetch_hook(const void* p, size_t n, int dev, hipStream_t stream,
+                                const std::function<hipError_t(size_t)>& real) {
   ensure_init();
-  if (!st().enabled || !p || !n) return real(n);
+  if (!st().enabled || !p || !n || (!vmem_enabled() && !app_has_managed())) return real(n);
+  if (g_open_captures.load(std::memory_order_acquire) > 0) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    auto is_cap = REAL_HIP(hipStreamIsCapturing);
+    if (!is_cap || is_cap(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return real(n);
+  }
   const size_t m = vmem_prefetch_allowed(p, n, dev);
   if (m < n)
     VLOG_INFO("prefetch of %zu bytes at %p to %s cut to %zu (%s)", n, p, dev < 0 ? "host" : "HBM", m,
@@ -541,7 +579,7 @@ static hipError_t prefetch_hook(const void* p, size_t n, int dev, const std::fun
 
 __attribute__((visibility("default"))) hipError_t hipMemPrefetchAsync(const void* p, size_t n, int device,
                                                                       hipStream_t stream) {
-  return prefetch_hook(p, n, device,
+  return prefetch_hook(p, n, device, stream,
                        [&](size_t m) { return REAL_HIP(hipMemPrefetchAsync)(p, m, device, stream); });
 }
 
@@ -549,7 +587,7 @@ __attribute__((visibility("default"))) hipError_t hipMemPrefetchAsync_v2(const v
                                                                          hipMemLocation loc, unsigned int flags,
                                                                          hipStream_t stream) {
   const int dev = loc.type == hipMemLocationTypeDevice ? loc.id : -1;
-  return prefetch_hook(p, n, dev,
+  return prefetch_hook(p, n, dev, stream,
                        [&](size_t m) { return REAL_HIP(hipMemPrefetchAsync_v2)(p, m, loc, flags, stream); });
 }
 
@@ -851,7 +889,7 @@ __attribute__((visibility("default"))) hipError_t hipLaunchKernel(const void* f,
                                                                   void** args, size_t shmem,
                                                                   hipStream_t stream) {
   ensure_init();
-  const int dev = cur_dev();
+  const int dev = launch_dev(stream);
   const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
   vmem_scan_args(args, stream);
   hipError_t rc = REAL_HIP(hipLaunchKernel)(f, grid, block, args, shmem, stream);
@@ -865,7 +903,7 @@ __attribute__((visibility("default"))) hipError_t hipExtLaunchKernel(const void*
                                                                      hipEvent_t start, hipEvent_t stop,
                                                                      int flags) {
   ensure_init();
-  const int dev = cur_dev();
+  const int dev = launch_dev(stream);
   const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
   vmem_scan_args(args, stream);
   hipError_t rc = REAL_HIP(hipExtLaunchKernel)(f, grid, block, args, shmem, stream, start, stop, flags);
@@ -878,7 +916,7 @@ __attribute__((visibility("default"))) hipError_t hipModuleLaunchKernel(
     unsigned int by, unsigned int bz, unsigned int shmem, hipStream_t stream, void** params,
     void** extra) {
   ensure_init();
-  const int dev = cur_dev();
+  const int dev = launch_dev(stream);
   const bool track = limiter_on_launch(dev, blocks3(gx, gy, gz));
   if (extra) vmem_scan_extra(extra, stream);
   else vmem_scan_args(params, stream);
@@ -894,7 +932,7 @@ __attribute__((visibility("default"))) hipError_t hipExtModuleLaunchKernel(
   ensure_init();
   // Global work size is in work-items here.
   auto nb = [](uint32_t g, uint32_t l) { return l ? (g + l - 1) / l : g; };
-  const int dev = cur_dev();
+  const int dev = launch_dev(stream);
   const bool track = limiter_on_launch(dev, blocks3(nb(gwx, lwx), nb(gwy, lwy), nb(gwz, lwz)));
   if (extra) vmem_scan_extra(extra, stream);
   else vmem_scan_args(params, stream);
@@ -936,7 +974,7 @@ __attribute__((visibility("default"))) hipError_t hipLaunchCooperativeKernel(con
   ensure_init();
   hipError_t g = cooperative_guard(f, grid, block, shmem);
   if (g != hipSuccess) return g;
-  const int dev = cur_dev();
+  const int dev = launch_dev(stream);
   const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
   vmem_scan_args(params, stream);
   hipError_t rc = REAL_HIP(hipLaunchCooperativeKernel)(f, grid, block, params, shmem, stream);
@@ -948,7 +986,7 @@ __attribute__((visibility("default"))) hipError_t hipModuleLaunchCooperativeKern
     hipFunction_t f, unsigned int gx, unsigned int gy, unsigned int gz, unsigned int bx,
     unsigned int by, unsigned int bz, unsigned int shmem, hipStream_t stream, void** params) {
   ensure_init();
-  const int dev = cur_dev();
+  const int dev = launch_dev(stream);
   const bool track = limiter_on_launch(dev, blocks3(gx, gy, gz));
   vmem_scan_args(params, stream);
   hipError_t rc = REAL_HIP(hipModuleLaunchCooperativeKernel)(f, gx, gy, gz, bx, by, bz, shmem, stream, params);
@@ -959,12 +997,30 @@ __attribute__((visibility("default"))) hipError_t hipModuleLaunchCooperativeKern
 __attribute__((visibility("default"))) hipError_t hipLaunchKernelExC(const hipLaunchConfig_t* cfg,
                                                                      const void* f, void** args) {
   ensure_init();
-  const int dev = cur_dev();
+  const int dev = cfg ? launch_dev(cfg->stream) : cur_dev();
   const bool track = cfg && limiter_on_launch(dev, blocks3(cfg->gridDim.x, cfg->gridDim.y, cfg->gridDim.z), f);
   vmem_scan_args(args, cfg ? cfg->stream : nullptr);
   hipError_t rc = REAL_HIP(hipLaunchKernelExC)(cfg, f, args);
   if (track) limiter_track(dev, cfg->stream, rc);
   return rc;
+}
+
+// Synchronize: the caller's batched launch counters become visible in its
+// region slot (the monitor and tests read them), then the real call.
+__attribute__((visibility("default"))) hipError_t hipDeviceSynchronize() {
+  limiter_flush_thread();
+  return REAL_HIP(hipDeviceSynchronize)();
+}
+__attribute__((visibility("default"))) hipError_t hipStreamSynchronize(hipStream_t stream) {
+  limiter_flush_thread();
+  return REAL_HIP(hipStreamSynchronize)(stream);
+}
+
+// A destroyed stream's handle may come back for another device's stream:
+// invalidate the launch hooks' stream -> device caches.
+__attribute__((visibility("default"))) hipError_t hipStreamDestroy(hipStream_t stream) {
+  g_stream_gen.fetch_add(1, std::memory_order_relaxed);
+  return REAL_HIP(hipStreamDestroy)(stream);
 }
 
 // Graphs: a hipGraphLaunch bypasses every per-kernel hook, so each executable
@@ -981,10 +1037,12 @@ __attribute__((visibility("default"))) hipError_t hipGraphLaunch(hipGraphExec_t 
   }();
   const GraphWork gw = graph_exec_work(exec);
   const uint64_t wg = gw.wg;
-  const int dev = cur_dev();
+  const int dev = launch_dev(stream);
   uint64_t tentative = 0;
   if (!pools_graph_admit(exec, dev, &tentative)) return hipErrorOutOfMemory;  // alloc nodes past the cap
-  const bool track = limiter_on_launch(dev, wg ? wg : fallback_tokens, nullptr, gw.kernels);
+  // A graph with RCCL kernel nodes (a DDP step captured whole) is exempt as an
+  // eager RCCL kernel is: holding it would stall the collective's peer ranks.
+  const bool track = limiter_on_launch(dev, wg ? wg : fallback_tokens, nullptr, gw.kernels, gw.collectives > 0);
   vmem_graph_launched(exec);
   hipError_t rc = REAL_HIP(hipGraphLaunch)(exec, stream);
   if (track) limiter_track(dev, stream, rc);
@@ -992,10 +1050,98 @@ __attribute__((visibility("default"))) hipError_t hipGraphLaunch(hipGraphExec_t 
   return rc;
 }
 
+// ---- graphs under one hardware queue ---------------------------------------------------
+// The HIP runtime (ROCm 7, hip::Graph::UpdateStreams) runs a graph's parallel
+// branches on extra streams and picks them by skipping every stream that shares
+// the launch stream's hardware queue -- with no bound on that walk.  Under
+// GPU_MAX_HW_QUEUES=1 (the device plugin's default for a fractional vGPU) every
+// stream shares it: the walk reads past the stream list and the first replay of
+// a graph with parallel branches segfaults (a two-stream training step,
+// profiles/r5/side_stream/crash_stack.md: the faulting frame is UpdateStreams +
+// 0xb1, reached from GraphExec::Run).  With one hardware queue the branches
+// cannot overlap anyway, so before instantiation the graph's nodes are chained
+// in a topological order: edges between consecutive nodes are added and every
+// other edge (implied by the chain) is removed, which leaves the runtime one
+// branch.  Results are unchanged -- a chain only removes concurrency.
+bool single_hw_queue() {
+  static const int one = [] {
+    const char* v = getenv("GPU_MAX_HW_QUEUES");
+    return v && atoi(v) == 1 && env_bool(env_first("VGPU_GRAPH_CHAIN"), true) ? 1 : 0;
+  }();
+  return one != 0;
+}
+
+std::atomic<uint64_t> g_graphs_chained{0};
+
+void chain_graph(hipGraph_t g) {
+  auto get_nodes = REAL_HIP(hipGraphGetNodes);
+  auto get_edges = REAL_HIP(hipGraphGetEdges);
+  auto add_deps = REAL_HIP(hipGraphAddDependencies);
+  auto rm_deps = REAL_HIP(hipGraphRemoveDependencies);
+  if (!g || !get_nodes || !get_edges || !add_deps || !rm_deps) return;
+  size_t n = 0, ne = 0;
+  if (get_nodes(g, nullptr, &n) != hipSuccess || n < 2) return;
+  std::vector<hipGraphNode_t> nodes(n);
+  if (get_nodes(g, nodes.data(), &n) != hipSuccess) return;
+  if (get_edges(g, nullptr, nullptr, &ne) != hipSuccess) return;
+  std::vector<hipGraphNode_t> from(ne), to(ne);
+  if (ne && get_edges(g, from.data(), to.data(), &ne) != hipSuccess) return;
+  std::unordered_map<hipGraphNode_t, size_t> idx;
+  for (size_t i = 0; i < n; ++i) idx[nodes[i]] = i;
+  std::vector<std::vector<size_t>> out(n);
+  std::vector<size_t> indeg(n, 0);
+  for (size_t e = 0; e < ne; ++e) {
+    auto a = idx.find(from[e]), b = idx.find(to[e]);
+    if (a == idx.end() || b == idx.end()) return;
+    out[a->second].push_back(b->second);
+    ++indeg[b->second];
+  }
+  // Kahn's algorithm, lowest node index first among the ready ones (capture order).
+  std::vector<size_t> order;
+  order.reserve(n);
+  std::vector<size_t> ready;
+  for (size_t i = 0; i < n; ++i)
+    if (!indeg[i]) ready.push_back(i);
+  while (!ready.empty()) {
+    auto m = std::min_element(ready.begin(), ready.end());
+    const size_t u = *m;
+    ready.erase(m);
+    order.push_back(u);
+    for (size_t v : out[u])
+      if (--indeg[v] == 0) ready.push_back(v);
+  }
+  if (order.size() != n) return;  // not a DAG: leave it to the runtime's own error
+  std::vector<size_t> pos(n);
+  for (size_t k = 0; k < n; ++k) pos[order[k]] = k;
+  bool chain = ne == n - 1;
+  for (size_t e = 0; chain && e < ne; ++e) chain = pos[idx[to[e]]] == pos[idx[from[e]]] + 1;
+  if (chain) return;
+  std::vector<char> linked(n, 0);  // consecutive pair (k, k+1) already an edge
+  for (size_t e = 0; e < ne; ++e) {
+    const size_t a = pos[idx[from[e]]], b = pos[idx[to[e]]];
+    if (b == a + 1 && !linked[a]) {
+      linked[a] = 1;
+      continue;
+    }
+    if (rm_deps(g, &from[e], &to[e], 1) != hipSuccess) {
+      (void)REAL_HIP(hipGetLastError)();
+      return;
+    }
+  }
+  for (size_t k = 0; k + 1 < n; ++k)
+    if (!linked[k] && add_deps(g, &nodes[order[k]], &nodes[order[k + 1]], 1) != hipSuccess) {
+      (void)REAL_HIP(hipGetLastError)();
+      return;
+    }
+  if (g_graphs_chained.fetch_add(1) == 0)
+    VLOG_INFO("GPU_MAX_HW_QUEUES=1: graph of %zu nodes with parallel branches chained before instantiation", n);
+}
+
 __attribute__((visibility("default"))) hipError_t hipGraphInstantiate(hipGraphExec_t* pExec, hipGraph_t graph,
                                                                       hipGraphNode_t* pErrorNode,
                                                                       char* pLogBuffer, size_t bufferSize) {
   ensure_init();
+  if (single_hw_queue()) chain_graph(graph);
   hipError_t rc = REAL_HIP(hipGraphInstantiate)(pExec, graph, pErrorNode, pLogBuffer, bufferSize);
   if (rc == hipSuccess && pExec) {
     graph_exec_record(*pExec, graph);
@@ -1009,6 +1155,7 @@ __attribute__((visibility("default"))) hipError_t hipGraphInstantiateWithFlags(h
                                                                                hipGraph_t graph,
                                                                                unsigned long long flags) {
   ensure_init();
+  if (single_hw_queue()) chain_graph(graph);
   hipError_t rc = REAL_HIP(hipGraphInstantiateWithFlags)(pExec, graph, flags);
   if (rc == hipSuccess && pExec) {
     graph_exec_record(*pExec, graph);
@@ -1021,6 +1168,7 @@ __attribute__((visibility("default"))) hipError_t hipGraphInstantiateWithFlags(h
 __attribute__((visibility("default"))) hipError_t hipGraphInstantiateWithParams(
     hipGraphExec_t* pExec, hipGraph_t graph, hipGraphInstantiateParams* params) {
   ensure_init();
+  if (single_hw_queue()) chain_graph(graph);
   hipError_t rc = REAL_HIP(hipGraphInstantiateWithParams)(pExec, graph, params);
   if (rc == hipSuccess && pExec) {
     graph_exec_record(*pExec, graph);

@@ -18,13 +18,17 @@
 // snapshot, not time), so the limiter measures the GPU time of its OWN work:
 //
 //   * after every tracked launch (kernel, module kernel, graph) the hook
-//     records a timing-free marker event on the launch's stream;
-//   * the limiter thread polls the oldest markers (hipEventQuery, 100 µs) and
-//     turns "this process had work outstanding on the device from t0 to t1"
-//     into a charge.  With a share board (board.cpp; node-wide, one per GPU)
-//     the charge is the processor-sharing virtual time of the interval — each
-//     of k concurrently busy pods pays 1/k of the wall time — otherwise it is
-//     the wall time itself;
+//     records a timing-free marker event on the launch's stream and pushes it
+//     onto the launching thread's own ring (one single-producer /
+//     single-consumer ring per thread and device: no lock and no shared
+//     read-modify-write on the launch path — the reference's rate_limiter is
+//     one CAS per cuLaunchKernel, SURVEY.md §3.5 hot loop #1);
+//   * the limiter thread drains the rings (hipEventQuery, 100 µs) and turns
+//     "this process had work outstanding on the device from t0 to t1" into a
+//     charge.  With a share board (board.cpp; node-wide, one per GPU) the
+//     charge is the processor-sharing virtual time of the interval — each of k
+//     concurrently busy pods pays 1/k of the wall time — otherwise it is the
+//     wall time itself;
 //   * a token bucket in GPU-nanoseconds refills at limit% of wall time, and
 //     the launch hook blocks while the bucket, minus the estimated cost of the
 //     work already in flight, is negative.
@@ -39,8 +43,6 @@
 #include <sys/stat.h>
 
 #include <condition_variable>
-#include <deque>
-#include <shared_mutex>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -63,26 +65,37 @@ extern int cumask_device_physical_cus(int dev);
 
 namespace {
 
+// ---- per-thread marker rings -----------------------------------------------------------
+constexpr uint32_t kRing = 1024;  // markers in flight per thread and device (power of two)
+constexpr uint32_t kMask = kRing - 1;
+
 struct Marker {
   hipEvent_t ev;
   uint64_t submit_ns;
-  uint32_t launches;  // launches this marker covers (since the previous one on its stream)
+  hipStream_t stream;
+  uint32_t launches;  // launches this marker covers
 };
 
-// Per-stream marker state.  By default every tracked launch records a marker.
-// With VGPU_LIMITER_MARK_US > 0 a launch records one only when the stream has
-// none in flight or the last one is older than that interval; the launches in
-// between are "dirty" and the limiter thread covers them with a marker of its
-// own once the older markers have completed (no GPU time goes uncharged).
-// Measured on MI355X (4 x 25 % temporal pods, profiles/temporal_r2.md) the
-// sparse mode is slower: an event recorded from the limiter thread on the
-// application's stream costs more than the per-launch record it saves.
-struct StreamTrack {
-  std::deque<Marker> q;
-  uint64_t last_mark_ns = 0;
-  uint32_t unmarked = 0;  // launches since the last marker
-  bool dirty = false;
+// One launching thread's markers on one device.  The thread (producer) writes
+// ring[head], the limiter thread (consumer) retires ring[tail] once its event
+// has completed and hands the event back through `fring` for reuse.
+struct Track {
+  // producer side
+  alignas(64) std::atomic<uint32_t> head{0};
+  std::atomic<uint32_t> ftail{0};     // next free event to take (producer advances)
+  std::atomic<uint64_t> launches{0};  // tracked launches, monotonic (owner stores only)
+  hipEvent_t spare = nullptr;         // an event whose record failed, reused next time
+  // consumer side
+  alignas(64) std::atomic<uint32_t> tail{0};
+  std::atomic<uint32_t> fhead{0};     // free events handed back (consumer advances)
+  std::atomic<uint64_t> pub_seen{0};  // `launches` when the consumer last published inflight
+  uint64_t charged = 0;               // launches retired (consumer only)
+  std::atomic<int> dead{0};           // the owning thread exited
+  Marker ring[kRing];
+  hipEvent_t fring[kRing];
 };
+
+std::atomic<uint32_t> g_track_gen{1};  // bumped at fork: the child's thread-local tracks are stale
 
 struct DevLimiter {
   int active = 0;             // temporal limiting configured for this device
@@ -92,17 +105,21 @@ struct DevLimiter {
   int64_t cap = 0;            // bucket depth (ns)
   int64_t quantum = 0;        // an overdrawn bucket must refill this far before launches resume
   std::atomic<int> hold{0};   // 1 while waiting for the quantum
-  std::atomic<int> outstanding{0};     // markers in flight
-  std::atomic<int64_t> inflight{0};    // tracked launches not yet charged
-  std::atomic<int64_t> ema_charge{0};  // charged ns per launch
-  std::mutex mu;              // guards streams / free_ev / act_mark_ns / board
-  std::unordered_map<hipStream_t, StreamTrack> streams;
-  std::vector<hipEvent_t> free_ev;
+  std::atomic<int64_t> inflight_pub{0};  // tracked launches not yet charged, as of the last drain
+  std::atomic<int64_t> ema_charge{0};    // charged ns per launch
+  std::atomic<int> idle{1};   // consumer: nothing outstanding (a producer that sees it wakes the thread)
+  std::atomic<int> busy{0};   // consumer: a busy interval is open (act_mark_ns valid)
+  std::mutex tracks_mu;       // guards `tracks` (registration; the consumer's pass)
+  std::vector<Track*> tracks;
+  std::mutex mu;              // guards act_mark_ns / board attach
   uint64_t act_mark_ns = 0;   // start of the not-yet-charged busy interval
+  uint64_t activated_ns = 0;  // last (re-)activation: markers from before are not charged
+  uint64_t interval_charge = 0;  // charged since the previous marker completion (per-launch estimate)
   uint64_t last_poll_ns = 0;  // previous poll that found work still in flight
   vgpu_board_t* board = nullptr;
   int board_slot = -1;
   bool board_tried = false;
+  std::atomic<int> board_ready{0};  // attach_board ran (the launch path checks this without the lock)
   // Concurrency gate of the temporal pool (VGPU_POOL_CONCURRENCY, 0 = off): at
   // most max_running pool members of the GPU run at once, in run_quantum_ns turns.
   int max_running = 0;
@@ -113,11 +130,12 @@ struct DevLimiter {
   // Adaptive share policy (VGPU_CU_SHARE=auto): dispatch sizes of the last
   // window, and whether this process holds CUs of its own (spatial mode).
   int auto_share = 0;
-  std::atomic<uint64_t> kern_n{0};  // dispatches since the last auto_step (graph launch = 1)
+  std::atomic<uint64_t> kern_n{0};  // dispatches since the last auto_step (graph launch = 1), batched per thread
   int spatial = 0;
   bool auto_joined = false;
   bool pool0_saved = false;
   uint64_t pool0[VGPU_CU_MASK_WORDS] = {};  // the plugin's pool mask (all-zero = every CU)
+  uint32_t pool_gen = 0;                    // the plugin's mask-write generation pool0 was taken at
   // Marker-independent busy check: KFD's cu_occupancy of this
   // process on the device, sampled every occ_period_ns.  A sample with waves on
   // the CUs counts the time since the previous sample as busy; every window the
@@ -128,12 +146,13 @@ struct DevLimiter {
   uint64_t occ_next_try_ns = 0;
   uint64_t occ_last_ns = 0, occ_window_start = 0;
   uint64_t occ_busy_acc = 0;       // busy wall the samples saw in this window
-  uint64_t occ_mark_acc = 0;       // wall the markers charged in this window
+  uint64_t occ_mark_acc = 0;       // wall the markers charged in this window (reaped intervals)
+  uint64_t occ_credit = 0;         // in-flight interval time already credited to the previous window
+  std::atomic<uint64_t> untracked_ns{0};  // last launch the markers deliberately do not charge
   std::atomic<uint64_t> occ_extra_total{0};  // charged on the occupancy evidence alone
-  // What this process last saw or wrote in the region's mask: anything else
-  // found there was written by the device plugin (a masked container arrived
-  // or left and the pool was reshaped, custate.py _reshape_pool) and becomes
-  // the new pool0.
+  // What this process last saw or wrote in the region's mask (its own CAS
+  // writes and sibling processes' writes); pool0 changes only when the device
+  // plugin's generation in the region's flags moves (custate.py _reshape_pool).
   uint64_t shim_mask[VGPU_CU_MASK_WORDS] = {};
 };
 
@@ -145,6 +164,81 @@ std::atomic<int> g_shutdown{0};
 std::atomic<int> g_thread_alive{0};
 std::mutex g_cv_mu;
 std::condition_variable g_cv;
+
+// Debt is bounded: tokens never fall below -(cap + 1 s), so a
+// replay of up to a second is still paid in full while no accumulation of
+// charges can hold a pod for longer than that debt's refill.
+void charge_tokens(DevLimiter& L, int64_t ns) {
+  if (ns <= 0) return;
+  const int64_t floor = -(L.cap + 1000000000ll);
+  int64_t cur = L.tokens.load(std::memory_order_relaxed), nv;
+  do {
+    nv = cur - ns;
+    if (nv < floor) nv = floor;
+  } while (!L.tokens.compare_exchange_weak(cur, nv, std::memory_order_relaxed));
+}
+
+// The calling thread's track for `dev` (created and registered on first use).
+struct ThreadTracks {
+  Track* t[VGPU_MAX_DEVICES] = {};
+  uint32_t gen = 0;
+  ~ThreadTracks() {
+    if (gen != g_track_gen.load(std::memory_order_relaxed)) return;  // stale copy (forked child)
+    for (Track* x : t)
+      if (x) x->dead.store(1, std::memory_order_release);  // the limiter thread frees it once drained
+  }
+};
+thread_local ThreadTracks tl_tracks;
+
+Track* my_track(int dev) {
+  ThreadTracks& tt = tl_tracks;
+  const uint32_t gen = g_track_gen.load(std::memory_order_relaxed);
+  if (__builtin_expect(tt.gen != gen, 0)) {
+    for (auto& x : tt.t) x = nullptr;  // forked: the parent's rings are not ours (leaked in the child)
+    tt.gen = gen;
+  }
+  Track* t = tt.t[dev];
+  if (__builtin_expect(t != nullptr, 1)) return t;
+  t = new Track();
+  DevLimiter& L = g_lim[dev];
+  {
+    std::lock_guard<std::mutex> g(L.tracks_mu);
+    L.tracks.push_back(t);
+  }
+  tt.t[dev] = t;
+  return t;
+}
+
+// Launches this thread made on `dev` that the last drain had not seen yet.
+int64_t own_unpublished(int dev) {
+  Track* t = tl_tracks.t[dev];
+  if (!t || tl_tracks.gen != g_track_gen.load(std::memory_order_relaxed)) return 0;
+  return (int64_t)(t->launches.load(std::memory_order_relaxed) - t->pub_seen.load(std::memory_order_relaxed));
+}
+
+// Per-thread batching of the region slot's counters and the auto policy's
+// dispatch count: a launch touches no cache line another thread writes.
+struct ThreadCounts {
+  uint64_t launches = 0, kern[VGPU_MAX_DEVICES] = {};
+  uint64_t last_flush_ns = 0;
+  uint32_t since = 0;
+};
+thread_local ThreadCounts tl_counts;
+
+void flush_counts(ThreadCounts& c, uint64_t now) {
+  if (vgpu_proc_slot_t* sl = my_slot()) {
+    if (c.launches) __atomic_fetch_add(&sl->launches, c.launches, __ATOMIC_RELAXED);
+    __atomic_store_n(&sl->last_launch_ns, now, __ATOMIC_RELAXED);
+  }
+  c.launches = 0;
+  for (int d = 0; d < VGPU_MAX_DEVICES; ++d)
+    if (c.kern[d]) {
+      g_lim[d].kern_n.fetch_add(c.kern[d], std::memory_order_relaxed);
+      c.kern[d] = 0;
+    }
+  c.since = 0;
+  c.last_flush_ns = now;
+}
 
 const char* lock_dir() {
   const char* d = env_first("VGPU_LOCK_DIR");
@@ -204,6 +298,10 @@ void apply_pool_scale(int dev, DevLimiter& L) {
   L.tokens.store(L.cap);
 }
 
+uint32_t pool_gen_of(const vgpu_device_cfg_t& d) {
+  return (__atomic_load_n(&d.flags, __ATOMIC_ACQUIRE) >> VGPU_DEV_POOL_GEN_SHIFT) & 0xffffu;
+}
+
 // Decide per device whether temporal throttling applies.
 void configure() {
   State& s = st();
@@ -227,6 +325,7 @@ void configure() {
       if (!La.pool0_saved && s.region) {
         for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w)
           La.shim_mask[w] = La.pool0[w] = __atomic_load_n(&s.region->dev[d].cu_mask[w], __ATOMIC_RELAXED);
+        La.pool_gen = pool_gen_of(s.region->dev[d]);
         La.pool0_saved = true;
       }
       g_auto_any.store(1, std::memory_order_relaxed);
@@ -267,10 +366,10 @@ void configure() {
       // next time-shared window (its A/B/A windows disagreed 2:1, profiles/r4).
       std::lock_guard<std::mutex> g(L.mu);
       const uint64_t now = mono_ns();
-      L.act_mark_ns = L.last_poll_ns = now;
+      L.act_mark_ns = L.last_poll_ns = L.activated_ns = now;
       L.occ_last_ns = L.occ_window_start = now;
-      L.occ_busy_acc = L.occ_mark_acc = 0;
-      if (L.board) (void)board_charge(L.board, L.board_slot, 0, L.outstanding.load() == 0);
+      L.occ_busy_acc = L.occ_mark_acc = L.occ_credit = 0;
+      if (L.board) (void)board_charge(L.board, L.board_slot, 0, !L.busy.load());
     }
     L.active = want;
     any |= want;
@@ -287,100 +386,141 @@ bool stream_capturing(hipStream_t stream) {
   return !is_cap || is_cap(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
 }
 
-// Record one marker on `stream`, which the caller checked is not capturing
-// (caller holds L.mu; the limiter thread also holds the capture guard, so a
-// capture cannot begin on the stream and swallow our event).  Returns 1 when a
-// marker was recorded.
-int record_marker(DevLimiter& L, hipStream_t stream, StreamTrack& t) {
-  hipEvent_t ev = nullptr;
-  if (!L.free_ev.empty()) {
-    ev = L.free_ev.back();
-    L.free_ev.pop_back();
-  } else if (REAL_HIP(hipEventCreateWithFlags)(&ev, hipEventDisableTiming) != hipSuccess) {
-    return 0;
+// Hand a completed marker's event back to its producer (or destroy it when
+// the producer's free ring is full).
+void recycle_event(Track* t, hipEvent_t ev) {
+  const uint32_t fh = t->fhead.load(std::memory_order_relaxed);
+  if (fh - t->ftail.load(std::memory_order_acquire) >= kRing) {
+    REAL_HIP(hipEventDestroy)(ev);
+    return;
   }
-  if (REAL_HIP(hipEventRecord)(ev, stream) != hipSuccess) {
-    L.free_ev.push_back(ev);
-    return 0;
-  }
-  const uint64_t now = mono_ns();
-  t.q.push_back({ev, now, t.unmarked});
-  t.unmarked = 0;
-  t.last_mark_ns = now;
-  t.dirty = false;
-  return 1;
+  t->fring[fh & kMask] = ev;
+  t->fhead.store(fh + 1, std::memory_order_release);
 }
 
-// Poll the oldest markers of every stream of `dev`; charge completed intervals.
+void free_track(Track* t) {
+  const uint32_t fh = t->fhead.load(std::memory_order_acquire);
+  for (uint32_t i = t->ftail.load(std::memory_order_acquire); i != fh; ++i) REAL_HIP(hipEventDestroy)(t->fring[i & kMask]);
+  if (t->spare) REAL_HIP(hipEventDestroy)(t->spare);
+  delete t;
+}
+
+// Drain the rings of `dev`: retire completed markers, charge the busy wall
+// time since the previous charge, publish the in-flight launch count.
 //
-// The whole poll runs under the capture guard (shared): hipStreamBeginCapture
-// (exclusive) waits for a poll in progress, and no poll starts while a capture
-// is open.  Without it a poll that passed the open-captures check could query
-// a marker of a stream whose capture began a moment later, and the runtime
-// invalidates that capture (seen on MI355X: a torch graph capture on a stream
-// with markers from its eager warm-up failed at its first kernel with
+// The whole pass runs under the capture guard (shared): hipStreamBeginCapture
+// (exclusive) waits for a pass in progress, and no pass starts while a capture
+// is being opened.  Without it a pass that passed the open-captures check could
+// query a marker of a stream whose capture began a moment later, and the
+// runtime invalidates that capture (seen on MI355X: a torch graph capture on a
+// stream with markers from its eager warm-up failed at its first kernel with
 // hipErrorStreamCaptureInvalidated).
-bool reap(int dev, DevLimiter& L, uint64_t now_hint) {
-  if (L.outstanding.load(std::memory_order_relaxed) == 0) return false;
-  std::shared_lock<std::shared_mutex> cap(g_capture_mu);  // no capture begins during the poll
+bool reap(int dev, DevLimiter& L) {
+  std::shared_lock<std::shared_mutex> cap(g_capture_mu);
   auto query = REAL_HIP(hipEventQuery);
-  std::lock_guard<std::mutex> g(L.mu);
-  int done = 0;
-  int added = 0;
-  int64_t covered = 0;
-  for (auto it = L.streams.begin(); it != L.streams.end();) {
-    StreamTrack& t = it->second;
-    auto& q = t.q;
-    // A stream being captured is polled after its capture ends; the others
-    // (eager work while some capture is open elsewhere) are charged as usual.
-    if (stream_capturing(it->first)) {
-      ++it;
-      continue;
+  int done = 0, left = 0;
+  int64_t covered = 0, inflight = 0;
+  uint64_t first_submit = UINT64_MAX;  // oldest marker not retired before this pass
+  std::vector<Track*> gone;
+  {
+    std::lock_guard<std::mutex> g(L.tracks_mu);
+    for (size_t i = 0; i < L.tracks.size();) {
+      Track* t = L.tracks[i];
+      uint32_t tl = t->tail.load(std::memory_order_relaxed);
+      const uint32_t h = t->head.load(std::memory_order_acquire);
+      if (tl != h && t->ring[tl & kMask].submit_ns < first_submit) first_submit = t->ring[tl & kMask].submit_ns;
+      uint64_t cov = 0;
+      while (tl != h) {
+        Marker& m = t->ring[tl & kMask];
+        // A stream being captured is polled after its capture ends.
+        if (stream_capturing(m.stream)) break;
+        const hipError_t rc = query(m.ev);
+        if (rc == hipErrorNotReady || rc == hipErrorStreamCaptureUnsupported || rc == hipErrorStreamCaptureImplicit)
+          break;
+        recycle_event(t, m.ev);  // complete (or invalid: never wait on it again)
+        cov += m.launches;
+        ++tl;
+        ++done;
+      }
+      t->tail.store(tl, std::memory_order_release);
+      t->charged += cov;
+      covered += (int64_t)cov;
+      left += (int)(h - tl);
+      const uint64_t produced = t->launches.load(std::memory_order_relaxed);
+      inflight += (int64_t)(produced - t->charged);
+      t->pub_seen.store(produced, std::memory_order_relaxed);
+      if (tl == h && t->dead.load(std::memory_order_acquire) && t->head.load(std::memory_order_acquire) == tl) {
+        gone.push_back(t);
+        L.tracks[i] = L.tracks.back();
+        L.tracks.pop_back();
+        continue;
+      }
+      ++i;
     }
-    while (!q.empty()) {
-      hipError_t rc = query(q.front().ev);
-      if (rc == hipErrorNotReady || rc == hipErrorStreamCaptureUnsupported ||
-          rc == hipErrorStreamCaptureImplicit)
-        break;
-      L.free_ev.push_back(q.front().ev);  // complete (or invalid: never wait on it again)
-      covered += q.front().launches;
-      q.pop_front();
-      ++done;
-    }
-    // Launches since the last marker are still uncovered: cover them now.
-    if (q.empty() && t.dirty) added += record_marker(L, it->first, t);
-    if (q.empty() && !t.dirty)
-      it = L.streams.erase(it);
-    else
-      ++it;
   }
-  if (added) L.outstanding.fetch_add(added);
+  for (Track* t : gone) free_track(t);
+  L.inflight_pub.store(inflight > 0 ? inflight : 0, std::memory_order_relaxed);
   const uint64_t polled = mono_ns();
-  if (!done) {
+  std::lock_guard<std::mutex> g(L.mu);
+  if (!done && !left) return false;
+  if (!L.busy.load(std::memory_order_relaxed)) {
+    // Idle -> busy: the interval starts at the oldest marker's submission.
+    attach_board(dev, L);
+    L.act_mark_ns = first_submit < polled ? first_submit : polled;
+    if (L.act_mark_ns < L.activated_ns) L.act_mark_ns = L.activated_ns;
     L.last_poll_ns = polled;
-    return true;
+    L.busy.store(1, std::memory_order_relaxed);
+    if (L.board) board_enter(L.board, L.board_slot);
   }
-  // The completion happened between the previous poll and this one.
-  uint64_t now = L.last_poll_ns > L.act_mark_ns ? (L.last_poll_ns + polled) / 2 : polled;
-  if (now < L.act_mark_ns) now = L.act_mark_ns;
-  L.last_poll_ns = polled;
-  const int left = L.outstanding.fetch_sub(done) - done;  // includes markers added above
+  uint64_t now;
+  if (!done) {
+    // Still running: charge the busy time so far every 2 ms instead of in one
+    // lump at completion, so the bucket drains while a long replay runs and
+    // its refill is not lost to the bucket's cap (a 350 ms replay against a
+    // 100 ms bucket ran at 0.4 of a 0.5 share), and the occupancy cross-check
+    // compares like with like.
+    L.last_poll_ns = polled;
+    if (polled - L.act_mark_ns < 2000000ull) return true;
+    now = polled;
+  } else {
+    // The completion happened between the previous poll and this one.
+    now = L.last_poll_ns > L.act_mark_ns ? (L.last_poll_ns + polled) / 2 : polled;
+    if (now < L.act_mark_ns) now = L.act_mark_ns;
+    L.last_poll_ns = polled;
+  }
   const uint64_t wall = now > L.act_mark_ns ? now - L.act_mark_ns : 0;
   L.act_mark_ns = now;
-  const uint64_t charge = L.board ? board_charge(L.board, L.board_slot, wall, left == 0) : wall;
-  L.tokens.fetch_sub((int64_t)charge, std::memory_order_relaxed);
-  L.inflight.fetch_sub(covered, std::memory_order_relaxed);
-  const int64_t per = covered > 0 ? (int64_t)(charge / covered) : (int64_t)charge;
-  const int64_t old = L.ema_charge.load(std::memory_order_relaxed);
-  L.ema_charge.store(old ? (old * 3 + per) / 4 : per, std::memory_order_relaxed);
+  const uint64_t charge = L.board ? board_charge(L.board, L.board_slot, wall, done && left == 0) : wall;
+  charge_tokens(L, (int64_t)charge);
+  L.interval_charge += charge;
+  if (done) {
+    // per-launch cost estimate from everything charged since the previous completion
+    const int64_t per = covered > 0 ? (int64_t)(L.interval_charge / covered) : (int64_t)L.interval_charge;
+    const int64_t old = L.ema_charge.load(std::memory_order_relaxed);
+    L.ema_charge.store(old ? (old * 3 + per) / 4 : per, std::memory_order_relaxed);
+    L.interval_charge = 0;
+  }
   L.win_charge += charge;
   L.win_busy += wall;
   L.occ_mark_acc += wall;
   L.charged_total.fetch_add(charge, std::memory_order_relaxed);
   L.busy_total.fetch_add(wall, std::memory_order_relaxed);
   trace_emit(VGPU_EV_GPU_TIME, dev, charge, wall);
-  (void)now_hint;
+  if (left == 0) {
+    L.busy.store(0, std::memory_order_relaxed);
+    // Publish idleness, then look once more: a producer that pushed before
+    // the store may not have seen it (and did not wake us).
+    L.idle.store(1, std::memory_order_seq_cst);
+  }
   return left > 0;
+}
+
+// Any marker waiting in a ring of `dev`.
+bool rings_pending(DevLimiter& L) {
+  std::lock_guard<std::mutex> g(L.tracks_mu);
+  for (Track* t : L.tracks)
+    if (t->tail.load(std::memory_order_relaxed) != t->head.load(std::memory_order_acquire)) return true;
+  return false;
 }
 
 // The auto policy's write of its own mask: word by word, only over the value
@@ -441,19 +581,19 @@ void auto_step() {
                                       note, sizeof note);
     if (note[0]) VLOG_INFO("device %d: adaptive share: %s", d, note);
     const int phys = cumask_device_physical_cus(d);
-    // A mask we did not write: the plugin reshaped the pool (the
-    // stale pool0 widened a shrunk member back onto a masked container's CUs,
-    // and a spatial claim could pick CUs that container holds).  The plugin's
-    // value is the pool from now on; a claim we held is given up and re-made
-    // from the new pool at a later step.
+    // The region's mask is shared by every process of the container: a value
+    // we did not write is either a sibling process's (its own claim or reset:
+    // adopted as what we last saw, so our CAS writes stay valid) or the device
+    // plugin's pool reshape, which moves the generation in the region's flags
+    // (reading every foreign value as a reshape made siblings adopt
+    // each other's claims as their pool).  A reshape is the pool from now on; a
+    // claim we held is given up and re-made from the new pool at a later step.
     {
       uint64_t cur[VGPU_CU_MASK_WORDS];
-      bool ext = false;
-      for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) {
-        cur[w] = __atomic_load_n(&s.region->dev[d].cu_mask[w], __ATOMIC_RELAXED);
-        ext |= cur[w] != L.shim_mask[w];
-      }
-      if (ext) {
+      for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) cur[w] = __atomic_load_n(&s.region->dev[d].cu_mask[w], __ATOMIC_RELAXED);
+      const uint32_t gen = pool_gen_of(s.region->dev[d]);
+      if (gen != L.pool_gen) {
+        L.pool_gen = gen;
         for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) L.shim_mask[w] = L.pool0[w] = cur[w];
         int n = 0;
         for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) n += __builtin_popcountll(cur[w]);
@@ -465,6 +605,8 @@ void auto_step() {
           L.spatial = 0;
           trace_emit(VGPU_EV_QUEUE, d, 0, 0);
         }
+      } else {
+        for (int w = 0; w < VGPU_CU_MASK_WORDS; ++w) L.shim_mask[w] = cur[w];
       }
     }
     uint64_t allowed[VGPU_CU_MASK_WORDS];
@@ -546,6 +688,15 @@ int occ_open(int dev, DevLimiter& L, uint64_t now) {
   return fd;
 }
 
+// Every 100 ms: the busy wall the occupancy samples saw against the wall the
+// markers account for in the same window.  The markers' share of a window is
+// the reaped intervals plus the interval still in flight up to now, minus the
+// in-flight part already credited to the previous window (reap books an
+// interval whole when its marker completes, so a replay longer than the window
+// is neither charged twice nor missing from the window it ran in).
+// Windows in which this process made launches the markers deliberately do not
+// charge (RCCL kernels and graphs, launches while the monitor reports no
+// contention) are skipped: occupancy cannot tell that work from the rest.
 void occ_step(int dev, DevLimiter& L, uint64_t now) {
   const uint64_t period = occ_period_ns();
   if (!period) return;
@@ -563,24 +714,30 @@ void occ_step(int dev, DevLimiter& L, uint64_t now) {
   if (!L.occ_window_start) L.occ_window_start = now;
   static const uint64_t window = 100000000ull;  // reconcile every 100 ms
   if (now - L.occ_window_start < window) return;
-  // Charge what the samples saw beyond the markers' charge, less a tolerance
+  std::lock_guard<std::mutex> g(L.mu);
+  const uint64_t inflight = L.busy.load(std::memory_order_relaxed) && now > L.act_mark_ns ? now - L.act_mark_ns : 0;
+  const uint64_t marked_raw = L.occ_mark_acc + inflight;
+  const uint64_t marked = marked_raw > L.occ_credit ? marked_raw - L.occ_credit : 0;
+  const uint64_t unt = L.untracked_ns.load(std::memory_order_relaxed);
+  const bool skip = unt && unt + 2 * period >= L.occ_window_start;
+  // Charge what the samples saw beyond the markers' share, less a tolerance
   // for sampling error (one period either way, 10 %).
-  const uint64_t seen = L.occ_busy_acc, marked = L.occ_mark_acc;
+  const uint64_t seen = L.occ_busy_acc;
   const uint64_t slack = period + marked / 10;
-  if (seen > marked + slack) {
+  if (!skip && seen > marked + slack) {
     const uint64_t extra = seen - marked - slack;
-    std::lock_guard<std::mutex> g(L.mu);
     // Processor sharing as for marker charges: k pods busy at once pay 1/k each
     // (the board's virtual time is tied to marker intervals, so scale directly).
     const int k = L.board ? std::max(1, (int)__atomic_load_n(&L.board->n_active, __ATOMIC_RELAXED)) : 1;
     const uint64_t charge = extra / (uint64_t)k;
-    L.tokens.fetch_sub((int64_t)charge, std::memory_order_relaxed);
+    charge_tokens(L, (int64_t)charge);
     L.win_charge += charge;
     L.charged_total.fetch_add(charge, std::memory_order_relaxed);
     L.occ_extra_total.fetch_add(charge, std::memory_order_relaxed);
     trace_emit(VGPU_EV_GPU_TIME, dev, charge, extra);
   }
   L.occ_busy_acc = L.occ_mark_acc = 0;
+  L.occ_credit = inflight;
   L.occ_window_start = now;
 }
 
@@ -598,8 +755,14 @@ void limiter_main() {
   while (!g_shutdown.load(std::memory_order_relaxed)) {
     bool busy = false;
     if (g_throttle_any.load(std::memory_order_relaxed))
-      for (int d = 0; d < VGPU_MAX_DEVICES; ++d)
-        if (g_lim[d].active) busy |= reap(d, g_lim[d], 0);
+      for (int d = 0; d < VGPU_MAX_DEVICES; ++d) {
+        DevLimiter& L = g_lim[d];
+        if (!L.active) continue;
+        L.idle.store(0, std::memory_order_relaxed);
+        busy |= reap(d, L);
+        // reap published idleness: a marker pushed meanwhile is picked up now
+        if (!busy && L.idle.load(std::memory_order_seq_cst) && rings_pending(L)) busy = true;
+      }
     if (busy) {
       sleep_ns(100000);  // 100 µs: completion-time resolution while work is in flight
     } else {
@@ -694,6 +857,15 @@ void priority_gate(vgpu_shared_region_t* r) {
   __atomic_store_n(&r->recent_kernel, 2, __ATOMIC_RELAXED);
 }
 
+// A launch the markers deliberately do not charge (cross-check skips its window).
+void note_untracked(DevLimiter& L) {
+  const uint64_t now = mono_ns();
+  if (now - L.untracked_ns.load(std::memory_order_relaxed) > 1000000ull)
+    L.untracked_ns.store(now, std::memory_order_relaxed);
+}
+
+}  // namespace
+
 // Collective kernels (RCCL) are exempt from the temporal limiter: every rank's
 // kernel must be resident for a collective to progress, so throttling one
 // rank's launches stalls the others (distributed backend row;
@@ -724,7 +896,11 @@ bool exempt_kernel(const void* fn) {
   return last_ex = ex;
 }
 
-}  // namespace
+// Publish the calling thread's batched launch counts now (synchronize hooks:
+// a caller that waited for its work reads current slot counters).
+void limiter_flush_thread() {
+  if (tl_counts.since) flush_counts(tl_counts, mono_ns());
+}
 
 void limiter_start() {
   configure();
@@ -740,6 +916,7 @@ void limiter_stop() {
   g_shutdown.store(1);
   g_cv.notify_all();
   for (int i = 0; i < 200 && g_thread_alive.load(); ++i) sleep_ns(1000000);
+  if (tl_counts.since) flush_counts(tl_counts, mono_ns());
   for (auto& L : g_lim)
     if (L.board) {
       board_release(L.board, L.board_slot);
@@ -751,44 +928,58 @@ void limiter_after_fork() {
   // The child has no limiter thread and no live markers of its own.
   g_thread_running.store(0);
   g_thread_alive.store(0);
+  g_track_gen.fetch_add(1);
+  tl_counts = ThreadCounts{};
   for (auto& L : g_lim) {
-    L.streams.clear();
-    L.free_ev.clear();
-    L.outstanding.store(0);
-    L.inflight.store(0);
+    L.tracks.clear();  // the parent's rings (leaked in the child; their events belong to the parent)
+    L.inflight_pub.store(0);
+    L.busy.store(0);
+    L.idle.store(1);
     L.board = nullptr;
     L.board_slot = -1;
     L.board_tried = false;
+    L.board_ready.store(0);
   }
 }
 
-bool limiter_on_launch(int dev, uint64_t wg, const void* fn, uint32_t kernels) {
+bool limiter_on_launch(int dev, uint64_t wg, const void* fn, uint32_t kernels, bool collective) {
   State& s = st();
   if (!s.enabled) return false;
   suspend_gate();
-  vgpu_proc_slot_t* sl = my_slot();
   if (s.region) priority_gate(s.region);
-  if (sl) {
-    __atomic_fetch_add(&sl->launches, 1, __ATOMIC_RELAXED);
-    __atomic_store_n(&sl->last_launch_ns, mono_ns(), __ATOMIC_RELAXED);
+  ThreadCounts& c = tl_counts;
+  ++c.launches;
+  const bool ok_dev = dev >= 0 && dev < VGPU_MAX_DEVICES;
+  if (g_auto_any.load(std::memory_order_relaxed) && ok_dev && g_lim[dev].auto_share)
+    ++c.kern[dev];  // progress: one step of a graph replay, or one kernel
+  // Batched: the slot counters and the auto policy's count are shared lines.
+  if (++c.since >= 64) flush_counts(c, mono_ns());
+  else if (c.since == 1) {
+    const uint64_t now = mono_ns();
+    if (now - c.last_flush_ns > 1000000ull) flush_counts(c, now);  // an idle thread's first launch: current
   }
-  if (g_auto_any.load(std::memory_order_relaxed) && dev >= 0 && dev < VGPU_MAX_DEVICES && g_lim[dev].auto_share)
-    g_lim[dev].kern_n.fetch_add(1, std::memory_order_relaxed);  // progress: one step of a graph replay, or one kernel
+  (void)kernels;
   const bool throttling = g_throttle_any.load(std::memory_order_relaxed) != 0;
   if (__builtin_expect(!throttling && !trace_on(), 1)) return false;
-  const bool exempt = throttling && exempt_kernel(fn);
+  const bool exempt = throttling && (collective || exempt_kernel(fn));
   trace_emit(VGPU_EV_LAUNCH, dev, wg, exempt ? 1 : 0);
-  if (!throttling || exempt) return false;
-  if (dev < 0 || dev >= VGPU_MAX_DEVICES) return false;
+  if (!throttling || !ok_dev) return false;
   DevLimiter& L = g_lim[dev];
   if (!L.active) return false;
+  if (exempt) {
+    note_untracked(L);
+    return false;
+  }
   if (__builtin_expect(L.pool_scale_pending.load(std::memory_order_relaxed), 0)) apply_pool_scale(dev, L);
   if (s.region && s.lim.core_policy != 1 &&
-      __atomic_load_n(&s.region->utilization_switch, __ATOMIC_RELAXED) == 0)
+      __atomic_load_n(&s.region->utilization_switch, __ATOMIC_RELAXED) == 0) {
+    note_untracked(L);
     return false;  // monitor says no contention: run unthrottled
+  }
   // VGPU_LIMITER_DRYRUN=1: measure and charge, never wait (diagnostics).
   static const bool dryrun = env_bool(env_first("VGPU_LIMITER_DRYRUN"), false);
   if (dryrun) return true;
+  vgpu_proc_slot_t* sl = my_slot();
   if (L.max_running > 0 && g_open_captures.load(std::memory_order_acquire) == 0) {
     if (!L.board_tried) {
       std::lock_guard<std::mutex> g(L.mu);
@@ -809,13 +1000,14 @@ bool limiter_on_launch(int dev, uint64_t wg, const void* fn, uint32_t kernels) {
     }
   }
   // Wait while the bucket cannot pay for the work already in flight; once
-  // overdrawn, hold until it has refilled by a whole quantum.
+  // overdrawn, hold until it has refilled by a whole quantum.  In flight: the
+  // launches the last drain saw uncharged, plus this thread's since then.
   uint64_t t0 = 0;
   for (;;) {
     // Until the first marker completes, assume 1 ms per launch in flight.
     int64_t per = L.ema_charge.load(std::memory_order_relaxed);
     if (per <= 0) per = 1000000;
-    const int64_t pending = L.inflight.load(std::memory_order_relaxed) * per;
+    const int64_t pending = (L.inflight_pub.load(std::memory_order_relaxed) + own_unpublished(dev)) * per;
     const int64_t avail = L.tokens.load(std::memory_order_relaxed) - pending;
     if (L.hold.load(std::memory_order_relaxed)) {
       if (avail >= L.quantum) {
@@ -839,6 +1031,9 @@ bool limiter_on_launch(int dev, uint64_t wg, const void* fn, uint32_t kernels) {
   return true;
 }
 
+// After a tracked launch: record a marker on its stream and push it onto this
+// thread's ring.  Lock-free; the only shared write is a wake-up of the limiter
+// thread when it has gone idle.
 void limiter_track(int dev, hipStream_t stream, hipError_t launch_rc) {
   if (dev < 0 || dev >= VGPU_MAX_DEVICES) return;
   DevLimiter& L = g_lim[dev];
@@ -846,38 +1041,46 @@ void limiter_track(int dev, hipStream_t stream, hipError_t launch_rc) {
   // when the graph is launched, and is charged then).  A concurrency-gate turn
   // taken for it must not stay claimed with nothing to drain it.
   auto untracked = [&] {
-    if (L.max_running > 0 && L.board && !L.outstanding.load()) board_gate_abort(L.board, L.board_slot);
+    if (L.max_running > 0 && L.board && !L.busy.load(std::memory_order_relaxed) && !rings_pending(L))
+      board_gate_abort(L.board, L.board_slot);
   };
   if (launch_rc != hipSuccess || stream_capturing(stream)) return untracked();
-  static const uint64_t interval_ns = [] {
-    const char* v = env_first("VGPU_LIMITER_MARK_US");
-    return (uint64_t)((v ? atof(v) : 0.0) * 1000.0);
-  }();
-  std::unique_lock<std::mutex> g(L.mu);
-  StreamTrack& t = L.streams[stream];
-  const uint64_t now = mono_ns();
-  t.unmarked++;
-  L.inflight.fetch_add(1, std::memory_order_relaxed);
-  if (!t.q.empty() && now - t.last_mark_ns < interval_ns) {
-    t.dirty = true;  // covered by the next marker (ours or the limiter thread's)
-    return;
+  if (__builtin_expect(!L.board_ready.load(std::memory_order_acquire), 0)) {
+    std::lock_guard<std::mutex> g(L.mu);  // once per device: join the GPU's share board now
+    attach_board(dev, L);
+    L.board_ready.store(1, std::memory_order_release);
   }
-  if (!record_marker(L, stream, t)) {  // no marker possible: not tracked
-    t.unmarked--;
-    L.inflight.fetch_sub(1, std::memory_order_relaxed);
-    g.unlock();
+  Track* t = my_track(dev);
+  const uint32_t h = t->head.load(std::memory_order_relaxed);
+  // Ring full (kRing markers of this thread in flight): the launch runs
+  // inside the busy interval those markers keep open, and is not counted in
+  // flight (an uncovered launch would never be retired and would hold the
+  // bucket's quantum check forever).
+  if (h - t->tail.load(std::memory_order_acquire) >= kRing) return;
+  hipEvent_t ev = t->spare;
+  t->spare = nullptr;
+  if (!ev) {
+    const uint32_t ft = t->ftail.load(std::memory_order_relaxed);
+    if (ft != t->fhead.load(std::memory_order_acquire)) {
+      ev = t->fring[ft & kMask];
+      t->ftail.store(ft + 1, std::memory_order_release);
+    } else if (REAL_HIP(hipEventCreateWithFlags)(&ev, hipEventDisableTiming) != hipSuccess) {
+      return untracked();
+    }
+  }
+  if (REAL_HIP(hipEventRecord)(ev, stream) != hipSuccess) {
+    t->spare = ev;
     return untracked();
   }
-  if (L.outstanding.fetch_add(1) == 0) {
-    attach_board(dev, L);
-    L.act_mark_ns = now;
-    if (L.board) board_enter(L.board, L.board_slot);
-  }
-  g.unlock();
-  g_cv.notify_one();
+  t->ring[h & kMask] = Marker{ev, mono_ns(), stream, 1};
+  t->launches.store(t->launches.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
+  t->head.store(h + 1, std::memory_order_release);
+  // Wake the limiter thread if it went idle (see reap: it re-checks the rings
+  // after publishing idleness, so a push that misses the flag is not lost).
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  if (L.idle.load(std::memory_order_relaxed) && L.idle.exchange(0, std::memory_order_relaxed)) g_cv.notify_one();
 }
 
-// Fair-share GPU ns charged / wall ns busy so far on `dev` (tests, metrics).
 // What the compute-share policy of `dev` is doing (bench / tests):
 // out[0] auto phase of the GPU's share board (-1: not an auto member / no board),
 // out[1] busy members the board's decision was made for, out[2] 1 when the
@@ -908,6 +1111,7 @@ void limiter_share_state(int dev, int64_t out[8]) {
   out[7] = (int64_t)L.occ_extra_total.load(std::memory_order_relaxed);
 }
 
+// Fair-share GPU ns charged / wall ns busy so far on `dev` (tests, metrics).
 void limiter_stats(int dev, uint64_t* charged, uint64_t* busy) {
   if (dev < 0 || dev >= VGPU_MAX_DEVICES) return;
   if (charged) *charged = g_lim[dev].charged_total.load();

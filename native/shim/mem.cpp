@@ -126,6 +126,10 @@ void ipc_import_account(int dev, int64_t delta) {
   st().ipc_imported[dev].fetch_add(delta, std::memory_order_relaxed);
 }
 
+std::atomic<int64_t> g_app_managed{0};  // live hipMallocManaged allocations of the application
+
+bool app_has_managed() { return g_app_managed.load(std::memory_order_relaxed) > 0; }
+
 void ledger_add(void* p, uint64_t size, int dev, int kind) {
   State& s = st();
   trace_emit(VGPU_EV_ALLOC, dev, size, (uint64_t)kind);
@@ -133,6 +137,7 @@ void ledger_add(void* p, uint64_t size, int dev, int kind) {
     std::lock_guard<std::mutex> g(s.ledger_mu);
     s.ledger[(uintptr_t)p] = Alloc{size, dev, kind};
   }
+  if (kind == kManaged) g_app_managed.fetch_add(1, std::memory_order_relaxed);
   vgpu_proc_slot_t* sl = my_slot();
   if (sl && dev >= 0 && dev < VGPU_MAX_DEVICES) note_peak(sl->used[dev]);
 }
@@ -144,6 +149,7 @@ bool ledger_take_if(void* p, int kind, Alloc* out) {
   if (it == s.ledger.end() || it->second.kind != kind) return false;
   *out = it->second;
   s.ledger.erase(it);
+  if (out->kind == kManaged) g_app_managed.fetch_sub(1, std::memory_order_relaxed);
   trace_emit(VGPU_EV_FREE, out->dev, out->size, (uint64_t)out->kind);
   return true;
 }
@@ -165,6 +171,7 @@ bool ledger_take(void* p, Alloc* out) {
     *out = it->second;
     s.ledger.erase(it);
   }
+  if (out->kind == kManaged) g_app_managed.fetch_sub(1, std::memory_order_relaxed);
   trace_emit(VGPU_EV_FREE, out->dev, out->size, (uint64_t)out->kind);
   return true;
 }

@@ -55,6 +55,7 @@ using hipGetDevicePropertiesR0600 = hipError_t (*)(hipDeviceProp_tR0600*, int);
 using hipDeviceGetAttribute = hipError_t (*)(int*, hipDeviceAttribute_t, int);
 using hipGetLastError = hipError_t (*)();
 using hipStreamSynchronize = hipError_t (*)(hipStream_t);
+using hipDeviceSynchronize = hipError_t (*)();
 using hipMemcpy = hipError_t (*)(void*, const void*, size_t, hipMemcpyKind);
 using hipStreamWaitEvent = hipError_t (*)(hipStream_t, hipEvent_t, unsigned int);
 using hipPointerGetAttributes = hipError_t (*)(hipPointerAttribute_t*, const void*);
@@ -91,12 +92,17 @@ using hipGraphGetNodes = hipError_t (*)(hipGraph_t, hipGraphNode_t*, size_t*);
 using hipGraphNodeGetType = hipError_t (*)(hipGraphNode_t, hipGraphNodeType*);
 using hipGraphKernelNodeGetParams = hipError_t (*)(hipGraphNode_t, hipKernelNodeParams*);
 using hipGraphChildGraphNodeGetGraph = hipError_t (*)(hipGraphNode_t, hipGraph_t*);
+using hipGraphGetEdges = hipError_t (*)(hipGraph_t, hipGraphNode_t*, hipGraphNode_t*, size_t*);
+using hipGraphAddDependencies = hipError_t (*)(hipGraph_t, const hipGraphNode_t*, const hipGraphNode_t*, size_t);
+using hipGraphRemoveDependencies = hipError_t (*)(hipGraph_t, const hipGraphNode_t*, const hipGraphNode_t*, size_t);
 using hipOccupancyMaxActiveBlocksPerMultiprocessor = hipError_t (*)(int*, const void*, int, size_t);
 using hipEventCreateWithFlags = hipError_t (*)(hipEvent_t*, unsigned);
 using hipEventRecord = hipError_t (*)(hipEvent_t, hipStream_t);
 using hipEventQuery = hipError_t (*)(hipEvent_t);
 using hipEventDestroy = hipError_t (*)(hipEvent_t);
 using hipStreamIsCapturing = hipError_t (*)(hipStream_t, hipStreamCaptureStatus*);
+using hipStreamGetDevice = hipError_t (*)(hipStream_t, hipDevice_t*);
+using hipStreamDestroy = hipError_t (*)(hipStream_t);
 using hipThreadExchangeStreamCaptureMode = hipError_t (*)(hipStreamCaptureMode*);
 using hipStreamBeginCapture = hipError_t (*)(hipStream_t, hipStreamCaptureMode);
 using hipStreamBeginCaptureToGraph = hipError_t (*)(hipStream_t, hipGraph_t, const hipGraphNode_t*,

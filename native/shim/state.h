@@ -85,6 +85,7 @@ void mem_unreserve(int dev, uint64_t size, int kind);
 void ledger_add(void* p, uint64_t size, int dev, int kind);
 bool ledger_take(void* p, Alloc* out);
 bool ledger_take_if(void* p, int kind, Alloc* out);  // only an entry of that kind
+bool app_has_managed();  // the application holds hipMallocManaged memory of its own
 // Account without the cap check (runtime-internal memory the application
 // cannot be refused): it still counts against the next hipMalloc.
 void mem_charge_nofail(int dev, uint64_t size, int kind);
@@ -106,9 +107,15 @@ void limiter_after_fork();
 // blocks while the temporal limiter's bucket is overdrawn.  `fn` = the
 // kernel's host stub when known (RCCL kernels are exempt from throttling).
 // Returns true when the launch must be tracked: call limiter_track after the
-// launch on `stream` with its result.
-bool limiter_on_launch(int dev, uint64_t workgroups, const void* fn = nullptr, uint32_t kernels = 1);
+// launch on `stream` with its result.  collective: a graph with RCCL kernel
+// nodes (exempt like an eager RCCL kernel: never held, never charged).
+bool limiter_on_launch(int dev, uint64_t workgroups, const void* fn = nullptr, uint32_t kernels = 1,
+                       bool collective = false);
+// The kernel whose host stub is `fn` is a collective's (its library is RCCL's,
+// or matches VGPU_THROTTLE_EXEMPT).
+bool exempt_kernel(const void* fn);
 void limiter_track(int dev, hipStream_t stream, hipError_t launch_rc);
+void limiter_flush_thread();  // publish this thread's batched slot counters
 // Stream captures in progress anywhere in the process: while one is open the
 // limiter records and polls markers only on streams that are not capturing (an
 // event query on a capturing stream invalidates its capture), and capture

@@ -733,9 +733,16 @@ void vmem_after_copy(const void* dst, const void* src, size_t n) {
 // event recorded on its stream, so the caller's stream stays asynchronous
 // (it used to hipStreamSynchronize in the caller).
 namespace {
+// Only the operation's addresses: the resident spans are re-derived at drain
+// time under g_move_mu: meanwhile the pager or vmem_make_room may
+// have demoted the range, a suspend-evict moved it to host, or hipFree
+// released it -- prefetching spans captured at queue time would pull stale
+// pages back into HBM behind the books.
 struct Repair {
   hipEvent_t ev;
-  Span sp[2];
+  const void* dst;
+  const void* src;
+  size_t n;
 };
 std::mutex g_rep_mu;
 std::vector<Repair> g_rep;
@@ -761,7 +768,14 @@ void drain_repairs() {
   for (Repair& r : done) {
     (void)REAL_HIP(hipEventDestroy)(r.ev);
     std::lock_guard<std::mutex> m(g_move_mu);
-    for (const Span& s : r.sp)
+    if (st().suspended.load(std::memory_order_relaxed)) continue;  // suspend-evict owns the placement now
+    Span sp[2];
+    {
+      std::shared_lock<std::shared_mutex> g(g_tab_mu);
+      sp[0] = resident_span_locked(r.dst, r.n);  // released ranges are gone: no span
+      sp[1] = resident_span_locked(r.src, r.n);
+    }
+    for (const Span& s : sp)
       if (s.n && prefetch(s.lo, s.n, s.dev, true)) {
         trace_emit(VGPU_EV_MIGRATE, s.dev, s.n, 1);
         VLOG_DEBUG("vmem: %llu bytes at %p back to HBM after an async copy", (unsigned long long)s.n, (void*)s.lo);
@@ -772,13 +786,11 @@ void drain_repairs() {
 
 bool vmem_after_copy_async(const void* dst, const void* src, size_t n, hipStream_t stream) {
   if (g_count.load(std::memory_order_relaxed) == 0) return true;
-  Repair r{};
+  Repair r{nullptr, dst, src, n};
   {
     std::shared_lock<std::shared_mutex> g(g_tab_mu);
-    r.sp[0] = resident_span_locked(dst, n);
-    r.sp[1] = resident_span_locked(src, n);
+    if (!resident_span_locked(dst, n).n && !resident_span_locked(src, n).n) return true;
   }
-  if (!r.sp[0].n && !r.sp[1].n) return true;
   if (REAL_HIP(hipEventCreateWithFlags)(&r.ev, hipEventDisableTiming) != hipSuccess) {
     (void)REAL_HIP(hipGetLastError)();
     return false;

@@ -16,6 +16,8 @@
 
 #include <atomic>
 #include <string>
+#include <sched.h>
+#include <map>
 #include <thread>
 #include <vector>
 #include <thread>
@@ -31,6 +33,7 @@
 extern "C" int fake_hsa_queue_count();
 extern "C" int fake_hsa_queue_mask(int idx, uint32_t* out, int max_words, uint64_t* agent);
 extern "C" uint64_t fake_hip_launches();
+extern "C" uint64_t fake_hip_branchy_single_queue_launches();
 extern "C" uint64_t fake_hip_exec_ns();
 extern "C" uint64_t fake_hip_physical_used(int dev);
 extern "C" uint64_t fake_hsa_pool_used(int dev);
@@ -100,10 +103,28 @@ int main(int argc, char** argv) {
     double secs = argc > 2 ? atof(argv[2]) : 1.0;
     // "graph": hipGraphLaunch instead of kernel launches; "graphsync": each
     // replay followed by a device synchronize (a benchmark's step loop)
+    // "graphrccl": the graph's one kernel node is an RCCL kernel (a collective
+    // captured into a training step's graph).
     const bool graphs = argc > 3 && !strncmp(argv[3], "graph", 5);
     const bool step_sync = argc > 3 && !strcmp(argv[3], "graphsync");
     hipGraphExec_t ge = nullptr;
-    if (graphs) {
+    if (graphs && !strcmp(argv[3], "graphrccl")) {
+      void* h = dlopen("librccl_fake.so", RTLD_NOW);
+      void* fn = h ? dlsym(h, "rccl_fake_kernel_stub") : nullptr;
+      if (!fn) {
+        printf("error=no_rccl_fake\n");
+        return 1;
+      }
+      hipGraph_t g = nullptr;
+      hipGraphCreate(&g, 0);
+      hipKernelNodeParams kp{};
+      kp.func = fn;
+      kp.gridDim = dim3(64, 1, 1);
+      kp.blockDim = dim3(256, 1, 1);
+      hipGraphNode_t node = nullptr;
+      hipGraphAddKernelNode(&node, g, nullptr, 0, &kp);
+      hipGraphInstantiateWithFlags(&ge, g, 0);
+    } else if (graphs) {
       unsigned grids[1] = {64};
       hipGraphInstantiateWithFlags(&ge, fake_hip_graph_create(grids, 1, 0), 0);
     }
@@ -142,6 +163,69 @@ int main(int argc, char** argv) {
     if (gt) gt(dev, &charged, &busy);
     printf("charged_s=%.6f\nbusy_s=%.6f\n", charged * 1e-9, busy * 1e-9);
     print_region(dev);
+    return 0;
+  }
+
+  if (sc == "forkjoin") {
+    // A fork/join graph (A -> {B, C} -> D: two parallel branches, as a
+    // two-stream capture produces) instantiated and replayed.  Under
+    // GPU_MAX_HW_QUEUES=1 the real runtime crashes on such a graph; the shim
+    // chains it before instantiation.
+    hipGraph_t g = nullptr;
+    hipGraphCreate(&g, 0);
+    hipKernelNodeParams kp{};
+    kp.func = (void*)&main;
+    kp.gridDim = dim3(64, 1, 1);
+    kp.blockDim = dim3(256, 1, 1);
+    hipGraphNode_t a = nullptr, b = nullptr, c = nullptr, d = nullptr;
+    hipGraphAddKernelNode(&a, g, nullptr, 0, &kp);
+    hipGraphAddKernelNode(&b, g, &a, 1, &kp);
+    hipGraphAddKernelNode(&c, g, &a, 1, &kp);
+    hipGraphNode_t bc[2] = {b, c};
+    hipGraphAddKernelNode(&d, g, bc, 2, &kp);
+    hipGraphExec_t e = nullptr;
+    const int ri = hipGraphInstantiate(&e, g, nullptr, nullptr, 0);
+    int rl = 0;
+    for (int i = 0; i < 5; ++i) rl |= hipGraphLaunch(e, nullptr);
+    hipDeviceSynchronize();
+    size_t ne = 0;
+    hipGraphGetEdges(g, nullptr, nullptr, &ne);
+    std::vector<hipGraphNode_t> from(ne), to(ne);
+    hipGraphGetEdges(g, from.data(), to.data(), &ne);
+    std::map<hipGraphNode_t, int> outd, ind;
+    for (size_t i = 0; i < ne; ++i) {
+      outd[from[i]]++;
+      ind[to[i]]++;
+    }
+    int maxo = 0, maxi = 0;
+    for (auto& kv : outd) maxo = std::max(maxo, kv.second);
+    for (auto& kv : ind) maxi = std::max(maxi, kv.second);
+    printf("instantiate=%d\nlaunch=%d\nedges=%zu\nmax_out=%d\nmax_in=%d\nbranchy_refused=%llu\nfake_launches=%llu\n",
+           ri, rl, ne, maxo, maxi, (unsigned long long)fake_hip_branchy_single_queue_launches(),
+           (unsigned long long)fake_hip_launches());
+    return 0;
+  }
+
+  if (sc == "stream_dev") {
+    // Launches onto device 3's stream while device 0 is current: the limiter
+    // charges device 3 (the stream's device), not the thread's current one.
+    hipStream_t s3 = nullptr;
+    hipSetDevice(3);
+    hipStreamCreate(&s3);
+    hipSetDevice(0);
+    for (int i = 0; i < 200; ++i) hipLaunchKernel((const void*)&main, dim3(64), dim3(256), nullptr, 0, s3);
+    hipDeviceSynchronize();
+    usleep(50000);  // the limiter thread retires the last markers
+    auto gt = sym<void (*)(int, uint64_t*, uint64_t*)>("vgpu_self_gpu_time");
+    for (int d : {0, 3}) {
+      uint64_t charged = 0, busy = 0;
+      if (gt) gt(d, &charged, &busy);
+      printf("dev%d_busy_ns=%llu\n", d, (unsigned long long)busy);
+    }
+    int cur = -1;
+    hipGetDevice(&cur);
+    printf("current=%d\n", cur);
+    hipStreamDestroy(s3);
     return 0;
   }
 
@@ -506,13 +590,20 @@ int main(int argc, char** argv) {
     hipMalloc(&p, 4096);  // runtime init
     std::atomic<int> go{0};
     std::vector<std::thread> th;
+    std::vector<double> own(T, 0.0);  // each thread's own loop time (ns)
     struct timespec a, b;
+    auto now = [] {
+      struct timespec t;
+      clock_gettime(CLOCK_MONOTONIC, &t);
+      return t.tv_sec * 1e9 + t.tv_nsec;
+    };
     for (int i = 0; i < T; ++i)
       th.emplace_back([&, i] {
         hipStream_t st = (hipStream_t)(uintptr_t)(0x1000 + 64 * i);
-        while (!go.load()) {
-        }
+        while (!go.load()) sched_yield();  // no spinning thread holds a CPU another launcher needs
+        const double t0 = now();
         for (int k = 0; k < K; ++k) hipLaunchKernel((const void*)&main, dim3(64), dim3(256), nullptr, 0, st);
+        own[i] = now() - t0;
       });
     clock_gettime(CLOCK_MONOTONIC, &a);
     go = 1;
@@ -520,8 +611,11 @@ int main(int argc, char** argv) {
     clock_gettime(CLOCK_MONOTONIC, &b);
     hipDeviceSynchronize();
     const double ns = (b.tv_sec - a.tv_sec) * 1e9 + (b.tv_nsec - a.tv_nsec);
+    double mean = 0;
+    for (double o : own) mean += o / T;
+    // per thread: a launching thread's own time per launch, averaged over the threads
     printf("threads=%d\nlaunches=%d\nns_per_launch=%.1f\nns_per_launch_per_thread=%.1f\n", T, T * K,
-           ns / ((double)T * K), ns / K);
+           ns / ((double)T * K), mean / K);
     hipFree(p);
     return 0;
   }
@@ -835,6 +929,7 @@ int main(int argc, char** argv) {
     int ral = hipGraphAddMemAllocNode(nullptr, g2, nullptr, 0, &ap);
     hipGraphExec_t e2 = nullptr;
     hipGraphInstantiate(&e2, g2, nullptr, nullptr, 0);
+    usleep(300000);  // the pager's moves from the replays above have settled (they rebook buffer bytes)
     const uint64_t buf0 = usage(dev, 2);
     int rl = hipGraphLaunch(e2, nullptr);
     printf("add_memset=%d\nadd_memcpy1d=%d\nadd_child=%d\nadd_alloc=%d\nchild_ranges=%llu\nlaunch_alloc=%d\n"
@@ -1207,6 +1302,7 @@ int main(int argc, char** argv) {
     for (int i = 0; i < n; ++i) hipLaunchKernel((const void*)&main, dim3(grid), dim3(256), nullptr, 0, nullptr);
     hipModuleLaunchKernel(nullptr, grid, 1, 1, 256, 1, 1, 0, nullptr, nullptr, nullptr);
     hipGraphLaunch(nullptr, nullptr);
+    hipDeviceSynchronize();  // slot counters are batched per thread until a sync
     printf("fake_launches=%llu\n", (unsigned long long)fake_hip_launches());
     print_region(dev);
     return 0;

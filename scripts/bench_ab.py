@@ -113,9 +113,6 @@ RECIPES: dict[str, tuple[list, list, int]] = {
     ], 300),
     # Limiter marker spacing on a dispatch-heavy and a graph workload (profiles/r2/weak).
     "markers": (P4 + ["--steps", "40", "--warmup", "5", "--cu-share", "temporal"], [
-        ("w1.1_m0", {"VGPU_LIMITER_MARK_US": "0"}, ["--workload", "1.1"]),
-        ("w1.1_m500", {"VGPU_LIMITER_MARK_US": "500"}, ["--workload", "1.1"]),
-        ("w4.2_m0", {"VGPU_LIMITER_MARK_US": "0"}, ["--workload", "4.2"]),
         ("w4.2_dryrun", {"VGPU_LIMITER_DRYRUN": "1"}, ["--workload", "4.2"]),
         ("w4.2_noshim", {}, ["--workload", "4.2", "--no-shim"]),
     ], 300),

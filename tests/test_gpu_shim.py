@@ -414,3 +414,17 @@ def test_suspend_evict_gives_64gb_to_a_high_priority_pod(gpu_build):
         if a.poll() is None:
             a.kill()
             a.wait()
+
+
+def test_two_stream_training_graph_replays_with_one_hw_queue(gpu_build):
+    """a training step whose graph has a side-stream branch
+    crashed (SIGSEGV) on its first replay in a vGPU pod.  Cause, from the
+    native stack (profiles/r5/side_stream): the HIP runtime's
+    hip::Graph::UpdateStreams walks past its parallel-stream list when
+    GPU_MAX_HW_QUEUES=1, the device plugin's default for a fractional vGPU.
+    Under the enforcement library such a graph is chained at instantiation and
+    replays; the result equals the eager steps."""
+    res = probe(["forkjoin", 5, 1024], {"VGPU_DEVICE_MEMORY_LIMIT_0": "64g", "GPU_MAX_HW_QUEUES": "1",
+                                         "VGPU_LOG_LEVEL": "3"})
+    assert res["hw_queues"] == "1" and res["replays"] == 5
+    assert res["max_err"] < 1e-4, res

@@ -73,3 +73,42 @@ def test_region_lock_recovers_from_dead_owner(native_build, tmp_path):
         "print(lib.vgpu_region_lock(r));lib.vgpu_region_unlock(r)")
     r = subprocess.run([sys.executable, "-c", taker], capture_output=True, text=True, timeout=30, env=env)
     assert r.stdout.strip() == "0", r.stderr
+
+
+def _forkjoin(preload, env_extra=None):
+    env = {k: v for k, v in os.environ.items() if not k.startswith(("VGPU_", "HIP_", "GPU_MAX"))}
+    env.update({"LD_LIBRARY_PATH": str(FAKES_DIR), "GPU_MAX_HW_QUEUES": "1"})
+    if preload:
+        env["LD_PRELOAD"] = preload
+    env.update(env_extra or {})
+    r = subprocess.run([str(FAKES_DIR / "shim_driver"), "forkjoin"], env=env, capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return dict(l.split("=", 1) for l in r.stdout.splitlines() if "=" in l), r.stderr
+
+
+@pytest.mark.parametrize("san", ["", "address"])
+def test_fork_join_graph_replays_under_one_hw_queue(native_build, san):
+    """the bench pod's two-stream training graph died with
+    SIGSEGV on its first replay.  The native stack (profiles/r5/side_stream)
+    puts the fault in the HIP runtime, hip::Graph::UpdateStreams: under
+    GPU_MAX_HW_QUEUES=1 (the device plugin's default for a fractional vGPU) its
+    walk for a parallel stream on another hardware queue runs past the list.
+    The fake runtime refuses such a launch.  A fork/join graph (A -> {B, C} ->
+    D) replays under the shim, whose instantiate hook chains the nodes (one
+    branch: the single queue serialises them anyway); plain and ASan builds."""
+    raw, _ = _forkjoin(None)
+    assert raw["launch"] != "0" and raw["branchy_refused"] == "5"  # the runtime bug, modelled
+    if san:
+        runtime = _gcc_runtime("libasan.so")
+        if runtime is None:
+            pytest.skip("libasan.so not available")
+        from vgpu.native import build
+        preload = f"{runtime} {build.build_shim(sanitize=san)}"
+        extra = {"ASAN_OPTIONS": "detect_leaks=0:halt_on_error=1"}
+    else:
+        preload, extra = str(shim_path()), {}
+    o, err = _forkjoin(preload, extra)
+    assert "AddressSanitizer" not in err, err[-3000:]
+    assert (o["instantiate"], o["launch"], o["branchy_refused"], o["fake_launches"]) == ("0", "0", "0", "5")
+    assert (o["edges"], o["max_out"], o["max_in"]) == ("3", "1", "1")  # a chain

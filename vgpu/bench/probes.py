@@ -157,6 +157,60 @@ def graph(blocks_a: int = 1000, blocks_b: int = 3000) -> dict:
     return {"blocks": [blocks_a, blocks_b], "replays": 2}
 
 
+def forkjoin(replays: int = 5, width: int = 1024) -> dict:
+    """A two-stream training step captured as one graph and replayed: the
+    forward and the data-gradient chain on the capture stream, the weight
+    gradients of the first layer on a side stream (a parallel branch of the
+    graph), joined before the SGD update.  Returns the replayed parameters'
+    max deviation from the same steps run eagerly.  Under GPU_MAX_HW_QUEUES=1
+    the HIP runtime's multi-stream executor crashes on such a graph unless the
+    enforcement library chains it (hooks_hip.cpp chain_graph)."""
+    import torch
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    x = torch.randn(512, width, device=dev)
+    w1 = torch.randn(width, width, device=dev) / width ** 0.5
+    w2 = torch.randn(width, width, device=dev) / width ** 0.5
+    lr = 1e-3
+
+    def step(w1, w2, side):
+        main = torch.cuda.current_stream()
+        h = torch.relu(x @ w1)
+        y = h @ w2
+        dy = 2 * y / y.numel()
+        g2 = h.t() @ dy
+        dh = (dy @ w2.t()) * (h > 0)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            g1 = x.t() @ dh          # the branch: weight gradient of layer 1
+        w2.sub_(lr * g2)
+        main.wait_stream(side)
+        w1.sub_(lr * g1)
+
+    ref1, ref2 = w1.clone(), w2.clone()
+    side = torch.cuda.Stream()
+    for _ in range(2 + replays):  # eager reference: the warmup steps + the replays
+        step(ref1, ref2, side)
+    torch.cuda.synchronize()
+    cap = torch.cuda.Stream()
+    cap.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(cap):
+        for _ in range(2):  # warmup on the capture stream, as torch requires
+            step(w1, w2, side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cap):
+        step(w1, w2, side)
+    for _ in range(replays - 1):
+        g.replay()
+    torch.cuda.synchronize()
+    # capture does not run the step: 2 warmup + (replays - 1) replays so far
+    g.replay()
+    torch.cuda.synchronize()
+    err = max((w1 - ref1).abs().max().item(), (w2 - ref2).abs().max().item())
+    return {"replays": replays, "max_err": err, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "")}
+
+
 def arrays(cap_mib: int = 8192) -> dict:
     """Array-class allocations through the real HIP runtime (ctypes): under a
     cap of `cap_mib`, the second 6 GiB hipMalloc3D and a 4 GiB hipMallocArray
@@ -711,7 +765,7 @@ def main(argv=None) -> int:
     cmd = argv.pop(0) if argv else "census"
     nums = [int(a) for a in argv]
     out = {"census": census, "busy": busy, "cap": cap, "smi": smi, "graph": graph, "arrays": arrays,
-           "progress": progress, "vmem": vmem, "vmemcopy": vmemcopy, "capheld": capheld, "asynccap": asynccap, "rcclloop": rcclloop,
+           "progress": progress, "forkjoin": forkjoin, "vmem": vmem, "vmemcopy": vmemcopy, "capheld": capheld, "asynccap": asynccap, "rcclloop": rcclloop,
            "vmemfull": vmemfull, "evictee": evictee}[cmd](*nums)
     out["shim"] = shim_stats()
     print("PROBE " + json.dumps(out), flush=True)

@@ -31,7 +31,6 @@ On by default in vgpu.models.resnet training (1.2: 2 760 -> 2 991 images/s, 2.2:
 from __future__ import annotations
 
 import os
-import threading
 
 import torch
 from torch import nn
@@ -59,63 +58,6 @@ def set_enabled(on: bool) -> None:
 
 def _groups(m: int) -> int:
     return (m + 63) // 64
-
-
-# ---- weight gradients on a side stream ------------------------------------------------
-# A weight gradient is off the backward's critical chain (data gradient → BN →
-# next data gradient): nothing but the optimizer reads it.  On a second stream
-# (a parallel branch of the captured step graph) it fills the GPU while the
-# chain runs its latency-bound finalize / apply kernels.  The main stream joins
-# the side stream once, when the backward pass ends (an autograd engine
-# callback), and the inputs stay referenced until then.  Off under
-# torch.distributed (DDP's gradient hooks read each gradient as soon as its
-# node returns) and when the parameter already has a gradient (accumulation
-# would read it on the main stream).  Opt-in (VGPU_WGRAD_STREAM=1): under the
-# enforcement library the replay of such a two-stream step graph crashed
-# (profiles/r4/train/bnfuse/side_stream_crash.log), and without it the serial
-# step measured the same (3 112 images/s).
-_SIDE = os.environ.get("VGPU_WGRAD_STREAM", "0") == "1"
-_side_streams: dict = {}
-_side_lock = threading.Lock()
-_side_pending: list | None = None  # inputs kept alive until the join (one backward at a time)
-
-
-def set_side_stream(on: bool) -> None:
-    global _SIDE
-    _SIDE = bool(on)
-
-
-def _side_ok(*params) -> bool:
-    if not _SIDE or any(p is not None and p.grad is not None for p in params):
-        return False
-    dist = getattr(torch, "distributed", None)
-    return not (dist is not None and dist.is_available() and dist.is_initialized())
-
-
-def _on_side(fn, keep):
-    """fn() on the device's side stream after the main stream's work so far;
-    `keep` (its inputs) stays referenced until the join at the end of backward."""
-    main = torch.cuda.current_stream()
-    side = _side_streams.get(main.device)
-    if side is None:
-        side = _side_streams[main.device] = torch.cuda.Stream(device=main.device)
-    side.wait_stream(main)
-    with torch.cuda.stream(side):
-        out = fn()
-    global _side_pending
-    with _side_lock:
-        if _side_pending is None:
-            _side_pending = []
-
-            def join():
-                global _side_pending
-                main.wait_stream(side)
-                with _side_lock:
-                    _side_pending = None
-
-            torch.autograd.Variable._execution_engine.queue_callback(join)
-        _side_pending.append(keep)
-    return out
 
 
 def _conv_out(x: torch.Tensor, w: torch.Tensor, stride: int, padding: int, residual, want_stats: bool):
@@ -242,10 +184,7 @@ class _BNConvFn(torch.autograd.Function):
                 # (no MIOpen transposed conv, no 3/4-zero full-size tensor)
                 dysc = conv2d(dextra, _dgrad_filter(wsc))
                 res_stride = 2
-                if ctx.needs_input_grad[8] and _side_ok(wsc):
-                    dwsc = _on_side(lambda: conv_backward(dextra, y, wsc, 2, 0, False, True)[1], (dextra, y))
-                else:
-                    _, dwsc = conv_backward(dextra, y, wsc, 2, 0, False, ctx.needs_input_grad[8])
+                _, dwsc = conv_backward(dextra, y, wsc, 2, 0, False, ctx.needs_input_grad[8])
             else:
                 # the shortcut's own gradients: dw now, its data gradient joins conv's below
                 dysc, dwsc = conv_backward(dextra, y, wsc, ctx.sc_stride, 0, True, ctx.needs_input_grad[8])
@@ -275,11 +214,7 @@ class _BNConvFn(torch.autograd.Function):
                 fused = True
             elif rc != -1:
                 raise RuntimeError(f"vgpu_conv2d_nhwc_bn (backward): error {rc}")
-        if (fused or not need_dx) and ctx.needs_input_grad[5] and _side_ok(w):
-            dy_bn = None
-            dw = _on_side(lambda: conv_backward(dz, y, w, s, p, False, True)[1], (dz, y))
-        else:
-            dy_bn, dw = conv_backward(dz, y, w, s, p, need_dx and not fused, ctx.needs_input_grad[5])
+        dy_bn, dw = conv_backward(dz, y, w, s, p, need_dx and not fused, ctx.needs_input_grad[5])
         if need_dx and not fused:
             dy_bn = dy_bn.contiguous(memory_format=_CL)
             if dysc is not None and res_stride == 2:
