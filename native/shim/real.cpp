@@ -72,6 +72,12 @@ void* rsmi_lib_handle() {
   return v;
 }
 
+bool called_from_smi_lib(void* ret_addr) {
+  Dl_info di;
+  return ret_addr && dladdr(ret_addr, &di) && di.dli_fname && strstr(di.dli_fname, "smi") &&
+         !is_own_address(ret_addr);
+}
+
 void* smi_real(const char* name, void* ret_addr, void* (*fallback_handle)()) {
   // 1. A call from inside an smi library (libamd_smi calling its bundled
   //    rsmi_* through the GOT): that library's own definition.

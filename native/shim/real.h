@@ -27,6 +27,10 @@ void* recorded_real(const char* name);
 bool is_own_address(void* p);
 // The real smi entry point for a hook called from `ret_addr` (see real.cpp).
 void* smi_real(const char* name, void* ret_addr, void* (*fallback_handle)());
+// The caller (a return address) is code of an smi library: libamd_smi calling
+// its own or its bundled rocm-smi's entry points through the GOT.  Device-list
+// and index virtualisation apply to the application only.
+bool called_from_smi_lib(void* ret_addr);
 void* rsmi_lib_handle();
 
 }  // namespace vgpu

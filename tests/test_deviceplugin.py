@@ -311,6 +311,9 @@ def test_allocate_multi_gpu_prefers_one_numa(cluster):
     uuids = [e[f"VGPU_DEVICE_UUID_{i}"] for i in range(4)]
     idx = [next(d.index for d in c["plugin"].devices if d.uuid == u) for u in uuids]
     assert idx == sorted(idx)
+    # each ordinal's PCI address: the shim's smi hooks list only these GPUs
+    bdfs = [e[f"VGPU_DEVICE_BDF_{i}"] for i in range(4)]
+    assert bdfs == [next(d.bdf for d in c["plugin"].devices if d.uuid == u) for u in uuids] and all(bdfs)
 
 
 def test_allocate_hsa_tools_intercept_knob(cluster):

@@ -168,3 +168,44 @@ def test_smi_process_lists_pass_through_without_control(native_build, tmp_path):
     o = run("smi", env={"VGPU_FAKE_AMDSMI_JSON": str(f), "VGPU_FAKE_RSMI_PIDS": "4242,5151",
                         "VGPU_DISABLE_CONTROL": "true"})
     assert o["smi_procs"] == "4242,5151" and o["rsmi_procs"] == "4242,5151"
+
+
+def _smi8(tmp_path, extra_pid=None):
+    gpus = [{"uuid": f"GPU-{i}", "bdf": f"0000:{0x05 + 0x10 * i:02x}:00.0", "vram": 288 * GiB,
+             "vram_used": (i + 1) * GiB, "processes": [{"pid": 4242 + i, "vram": GiB}]} for i in range(8)]
+    if extra_pid:
+        gpus[5]["processes"].append({"pid": extra_pid, "vram": GiB})
+    f = tmp_path / "smi8.json"
+    f.write_text(json.dumps({"gpus": gpus}))
+    return str(f)
+
+
+def test_smi_device_identity_by_pci_address(native_build, tmp_path):
+    """VERDICT r4 #6 (reference libvgpu.so handle_remap, nvmlDeviceGetCount_v2,
+    nvmlDeviceGetHandleByIndex_v2): the node has 8 GPUs and the container holds
+    physical GPU 5 as its ordinal 0 (VGPU_DEVICE_BDF_0 from the device plugin).
+    amdsmi lists one processor handle -- GPU 5's -- with the pod's cap, usage
+    and processes; rocm-smi reports one device whose index 0 is GPU 5 and
+    refuses index 1."""
+    from test_shim_native import _kfd_env
+    env = _kfd_env(tmp_path, 777200)
+    env.update({"VGPU_FAKE_AMDSMI_JSON": _smi8(tmp_path, 777200), "VGPU_FAKE_GPUS": "8",
+                "VGPU_DEVICE_MEMORY_LIMIT_0": "100g", "VGPU_DEVICE_BDF_0": "0000:55:00.0"})
+    o = run("smi_ident", env=env)
+    assert o["gpus"] == "1" and o["sockets"] == "1"
+    assert o["gpu0_bdf"] == "0000:55:00.0"
+    assert int(o["gpu0_total"]) == 100 * GiB and int(o["gpu0_used"]) == GiB
+    assert o["gpu0_procs"] == "777200"
+    assert o["rsmi_devices"] == "1" and o["rsmi_pci0"] == "0000:55:00.0" and o["rsmi_pci0_rc"] == "0"
+    assert int(o["rsmi_total0"]) == 100 * GiB
+    assert o["rsmi_past_rc"] != "0"
+
+
+def test_smi_device_list_unfiltered_without_addresses_or_control(native_build, tmp_path):
+    """Without the container's PCI addresses (no device-plugin env, HIP not
+    loaded) or with control disabled, every GPU stays listed as before."""
+    base = {"VGPU_FAKE_AMDSMI_JSON": _smi8(tmp_path), "VGPU_FAKE_GPUS": "8"}
+    o = run("smi_ident", env={**base, "VGPU_DEVICE_MEMORY_LIMIT_0": "100g"})
+    assert o["gpus"] == "8" and o["rsmi_devices"] == "8" and o["gpu0_bdf"] == "0000:05:00.0"
+    o = run("smi_ident", env={**base, "VGPU_DEVICE_BDF_0": "0000:55:00.0", "VGPU_DISABLE_CONTROL": "true"})
+    assert o["gpus"] == "8" and o["rsmi_devices"] == "8"

@@ -22,6 +22,7 @@ ENV_CU_MASK = "VGPU_CU_MASK_{i}"
 # a VGPU_CU_MASK_<i> given with it is the shared pool the container runs on.
 ENV_CU_SHARE = "VGPU_CU_SHARE"
 ENV_UUID = "VGPU_DEVICE_UUID_{i}"
+ENV_BDF = "VGPU_DEVICE_BDF_{i}"  # PCI address of ordinal i: the shim matches smi handles by it
 ENV_SHARED_REGION = "VGPU_SHARED_REGION"
 ENV_OVERSUBSCRIBE = "VGPU_OVERSUBSCRIBE"
 # Physical HBM budget of an oversubscribed container (MiB, "m" suffix): virtual

@@ -26,7 +26,8 @@ from dataclasses import dataclass, field
 from vgpu.api import resources as R
 from vgpu.api.codec import decode_pod_devices, encode_pod_devices
 from vgpu.api.env import (ENV_CU_LIMIT, ENV_CU_MASK, ENV_CU_SHARE, ENV_CORE_POLICY, ENV_DISABLE_CONTROL, ENV_MEM_LIMIT,
-                          ENV_MEM_PHYSICAL, ENV_OVERSUBSCRIBE, ENV_SHARED_REGION, ENV_SUSPEND_EVICT, ENV_UUID, PRELOAD_FILE, SHIM_NAME,
+                          ENV_BDF, ENV_MEM_PHYSICAL, ENV_OVERSUBSCRIBE, ENV_SHARED_REGION, ENV_SUSPEND_EVICT, ENV_UUID, PRELOAD_FILE,
+                          SHIM_NAME,
                           format_mask)
 from vgpu.api.resources import ContainerDevice
 from vgpu.config import DevicePluginConfig
@@ -178,6 +179,11 @@ def build_container_grant(cfg: DevicePluginConfig, pod: dict, ctr_idx: int, devr
         if cfg.device_memory_scaling > 1 and cfg.vmem_physical_budget and d.usedmem > 0:
             g.envs[ENV_MEM_PHYSICAL.format(i=i)] = f"{int(d.usedmem / cfg.device_memory_scaling)}m"
         g.envs[ENV_UUID.format(i=i)] = d.uuid
+        if dev.bdf:
+            # amd-smi / rocm-smi inside the pod enumerate every GPU of the node
+            # (sysfs is not namespaced): the shim keeps and orders the ones
+            # whose PCI address is the container's (hooks_smi.cpp).
+            g.envs[ENV_BDF.format(i=i)] = dev.bdf
         if 0 < d.usedcores < 100 and not cfg.disable_core_limit:
             fractional = True
             g.envs[ENV_CU_LIMIT.format(i=i)] = str(d.usedcores)
