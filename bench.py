@@ -34,7 +34,7 @@ peers' memory; the JSON records the transport it chose per peer
 (NCCL_DEBUG=INFO: typically SHM), and xGMI peer access is claimed only where
 it says P2P.  The path that does exercise P2P/xGMI under the shim is one pod
 holding several GPUs: `--pod-gpus N` (DDP training inside one amd.com/gpu: N
-pod, vgpu/bench/ddp.py).
+pod, vgpu/parallel/ddp.py).
 """
 from __future__ import annotations
 
@@ -114,8 +114,8 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--pod-gpus", type=int, default=0,
                     help="instead of the headline: ONE vGPU pod granted this many GPUs (amd.com/gpu: N, "
                          "through Allocate) runs ResNet-V2-50 DDP training over RCCL inside it, one rank "
-                         "per device under the enforcement library (vgpu/bench/ddp.py)")
-    ap.add_argument("--ddp-bucket-mb", type=int, default=100)
+                         "per device under the enforcement library (vgpu/parallel/ddp.py)")
+    ap.add_argument("--ddp-bucket-mb", type=int, default=64)
     return ap
 
 
@@ -169,31 +169,36 @@ def pod_gpus_main(args) -> int:
     port = s.getsockname()[1]
     s.close()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
-           "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "vgpu.bench.ddp",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "vgpu.parallel.ddp",
            "--workload", "1.2", "--steps", str(args.steps), "--warmup", str(args.warmup),
-           "--bucket-mb", str(args.ddp_bucket_mb)] + (["--cpu-smoke"] if args.cpu_smoke else [])
+           "--bucket-mb", str(args.ddp_bucket_mb)]
+    if args.cpu_smoke:
+        cmd += ["--shrink", "--backend", "gloo", "--batch", "2", "--size", "64"]
+    if args.no_graph:
+        cmd += ["--no-graph"]
     log(f"one {n}-GPU pod on devices {devices} (share {pod.share}): {' '.join(cmd[2:])}")
     t0 = time.monotonic()
     r = subprocess.run(cmd, env=env, cwd=str(REPO), capture_output=True, text=True, timeout=1800)
     wall = time.monotonic() - t0
     text = r.stdout + r.stderr
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("DDP ")]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not lines:
         sys.stderr.write(text[-6000:])
         raise SystemExit(f"DDP pod failed (rc={r.returncode})")
-    d = json.loads(lines[-1][4:])
+    d = json.loads(lines[-1])
     transports = rccl_transports(text)
     kinds = sorted({t.split("/")[0] for v in transports.values() for t in v})
     res = {
         "metric": "ResNet-V2-50 DDP training, one multi-GPU vGPU pod (images/s)",
-        "value": d["images_per_s"], "unit": "images/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+        "value": d["value"], "unit": "images/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": d["ms_per_step"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": d["dtype"], "data": "synthetic inputs, random-init weights",
         "config": {"model": "ResNet-V2-50 (ai-benchmark test 1.2, training)", "global_batch": n * d["batch_per_rank"],
                    "seq_len": 346, "parallelism": f"ddp{n} inside one vGPU pod", "backend": d["backend"],
-                   "bucket_mb": d["bucket_mb"], "pod_env_share": pod.share, "enforcement":
+                   "bucket_mb": d["bucket_mb"], "buckets": d["buckets"], "hipgraph": d["graph"],
+                   "pod_env_share": pod.share, "enforcement":
                    "none (cpu rehearsal)" if args.cpu_smoke or args.no_shim else "libvgpu.so in every rank"},
-        "replicas_agree": d["replicas_agree"],
+        "replicas_agree": d["weights_in_sync"],
         # what RCCL chose per peer (NCCL_DEBUG=INFO): P2P = xGMI peer access, SHM = host memory
         "rccl_transport": transports, "rccl_transport_kinds": kinds,
         "pod_wall_s": round(wall, 1),

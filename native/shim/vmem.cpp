@@ -733,16 +733,16 @@ void vmem_after_copy(const void* dst, const void* src, size_t n) {
 // event recorded on its stream, so the caller's stream stays asynchronous
 // (it used to hipStreamSynchronize in the caller).
 namespace {
-// Only the operation's addresses: the resident spans are re-derived at drain
-// time under g_move_mu: meanwhile the pager or vmem_make_room may
-// have demoted the range, a suspend-evict moved it to host, or hipFree
-// released it -- prefetching spans captured at queue time would pull stale
-// pages back into HBM behind the books.
+// The resident spans the operation touched, as of queueing.  At drain time
+// they are cut to what is still resident under g_move_mu:
+// meanwhile the pager or vmem_make_room may have demoted the range, a
+// suspend-evict moved it to host, or hipFree released it -- prefetching the
+// queued spans whole would pull stale pages back into HBM behind the books.
+// A span never grows at drain time: the pager's later promotions are its own
+// (a grown span re-migrated pages a kernel was writing, round 5 vmemcopy).
 struct Repair {
   hipEvent_t ev;
-  const void* dst;
-  const void* src;
-  size_t n;
+  Span sp[2];
 };
 std::mutex g_rep_mu;
 std::vector<Repair> g_rep;
@@ -772,8 +772,13 @@ void drain_repairs() {
     Span sp[2];
     {
       std::shared_lock<std::shared_mutex> g(g_tab_mu);
-      sp[0] = resident_span_locked(r.dst, r.n);  // released ranges are gone: no span
-      sp[1] = resident_span_locked(r.src, r.n);
+      for (int k = 0; k < 2; ++k) {
+        const Span& q = r.sp[k];
+        if (!q.n) continue;
+        const Span now = resident_span_locked((const void*)q.lo, q.n);  // released ranges: no span
+        const uintptr_t lo = std::max(q.lo, now.lo), hi = std::min(q.lo + q.n, now.lo + now.n);
+        if (now.n && hi > lo && now.dev == q.dev) sp[k] = Span{lo, hi - lo, q.dev};
+      }
     }
     for (const Span& s : sp)
       if (s.n && prefetch(s.lo, s.n, s.dev, true)) {
@@ -786,11 +791,13 @@ void drain_repairs() {
 
 bool vmem_after_copy_async(const void* dst, const void* src, size_t n, hipStream_t stream) {
   if (g_count.load(std::memory_order_relaxed) == 0) return true;
-  Repair r{nullptr, dst, src, n};
+  Repair r{};
   {
     std::shared_lock<std::shared_mutex> g(g_tab_mu);
-    if (!resident_span_locked(dst, n).n && !resident_span_locked(src, n).n) return true;
+    r.sp[0] = resident_span_locked(dst, n);
+    r.sp[1] = resident_span_locked(src, n);
   }
+  if (!r.sp[0].n && !r.sp[1].n) return true;
   if (REAL_HIP(hipEventCreateWithFlags)(&r.ev, hipEventDisableTiming) != hipSuccess) {
     (void)REAL_HIP(hipGetLastError)();
     return false;

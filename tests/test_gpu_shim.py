@@ -157,6 +157,8 @@ def test_ddp_over_rccl_under_the_shim(gpu_build):
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     print(res)
     assert res["backend"] == "nccl" and res["value"] > 0 and res["final_loss"] == res["final_loss"]
+    # the whole DDP step (collectives included) replays as one hipGraph
+    assert res["graph"] is True and res["weights_in_sync"], res
 
 
 def test_two_ddp_ranks_share_one_gpu_under_the_shim(gpu_build, tmp_path):

@@ -1,6 +1,7 @@
 """Data-parallel training harness (vgpu/parallel/ddp.py) on CPU over gloo with
-world_size 2: gradients are the average over ranks, replicas stay identical,
-and the torchrun entry point prints the aggregate throughput line."""
+world_size 2: the flat-buffer bucketed all-reduce gives every rank the
+average gradient, replicas stay identical, and the torchrun entry point prints
+the aggregate throughput line."""
 import json
 import os
 import socket
@@ -32,11 +33,15 @@ def _worker(rank: int, world: int, port: int, out):
     torch.manual_seed(0)
     _, model = D.build_model("1.2", device, shrink=True)
     ref = copy.deepcopy(model)
-    m = D.wrap(model, device, bucket_mb=1)
+    grads = D.GradBuckets(model.parameters(), bucket_mb=1)  # several buckets: exercises the hooks' order
+    assert len(grads.buckets) > 1
     g = torch.Generator().manual_seed(rank)
     x = torch.randn(2, 3, 32, 32, generator=g).contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 10, (2,), generator=g)
-    torch.nn.functional.cross_entropy(m(x), y).backward()
+    for _ in range(2):  # a second step: begin() re-arms the buckets and zeroes the flat buffer
+        grads.begin()
+        torch.nn.functional.cross_entropy(model(x), y).backward()
+        grads.finish()
     ddp_grad = torch.cat([p.grad.flatten() for p in model.parameters()])
     torch.nn.functional.cross_entropy(ref(x), y).backward()
     local = torch.cat([p.grad.flatten() for p in ref.parameters()])
