@@ -116,7 +116,10 @@ class GradBuckets:
             cur, cur_bytes, hi = [], 0, n
             for p in reversed(ps):
                 off -= p.numel()
-                p.grad = flat[off:off + p.numel()].view_as(p)
+                # the parameter's own (dense) strides -- channels_last conv weights
+                # included: autograd accumulates in place only into a grad that
+                # obeys the layout contract, and the fused optimizer needs it too
+                p.grad = torch.as_strided(flat, p.size(), p.stride(), off)
                 cur.append(p)
                 cur_bytes += p.numel() * p.element_size()
                 if cur_bytes >= cap:
