@@ -47,6 +47,7 @@ typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 // Native 16-B vector (HIP's u32x4 is a class; copies of it go through memcpy
 // and defeat register promotion of the staging arrays).
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
 
 constexpr int kThreads = 256;
 constexpr int BK = 64;
@@ -1602,6 +1603,266 @@ hipError_t launch_pro(ConvArgs a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---- Persistent 1x1 conv with the block-entry BN+ReLU prologue (round 5) ----
+//
+// conv_pro_kernel launches one workgroup per tile.  On the ResNet-50 1x1 convs
+// a tile is 4-16 K steps, so every tile paid its pipeline fill (three A loads
+// and a weight DMA deep) and its epilogue (two LDS staging passes behind
+// barriers) in series: 2-2.6 TB/s on layers the roofline calls HBM-bound
+// (profiles/r4/kernels/pmc_flagship_r4_final.md).  Here a workgroup walks tiles
+// b, b+G, ... as one flattened sequence of K steps: the A loads run three steps
+// ahead and the weight DMA one step ahead straight across tile boundaries, so
+// the next tile's first steps are in flight while the current tile finishes.
+//
+// The epilogue never touches LDS, so it needs no barrier and leaves the
+// pipeline's stages alone: the MFMA is transposed (acc = W·Aᵀ), which leaves
+// each lane 4 consecutive output channels of one pixel, and bias, residual,
+// ReLU and the bf16 store are done from registers (one 8-byte store per 16x16
+// sub-tile; the four lanes of a pixel write 32 contiguous bytes).  The
+// residual of a tile is fetched two K steps before its epilogue.
+//
+// Stride 1 or 2, no padding, C % 64 == 0, Cout % BN == 0.
+template <int BM, int BN, bool RES>
+__global__ void __launch_bounds__(kThreads, 2) conv1x1_pro_kernel(const ConvArgs a) {
+  constexpr int AR = BM / 32, BR = BN / 32;
+  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2048 * 2 * 4];
+  float* sPar = reinterpret_cast<float*>(smem + 2 * STAGE);
+  const int G = gridDim.x;
+  if ((int)blockIdx.x >= a.nwg) return;
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int slot = t & 7, r0 = t >> 3;
+  const int lchunk = slot ^ (r0 & 7);
+  const int nk = a.ktiles;                                       // K steps per tile (= C / 64)
+  const int ntile = (a.nwg - (int)blockIdx.x + G - 1) / G;       // tiles of this workgroup
+  const int nsteps = ntile * nk;
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.x), 0, a.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.w), 0, (uint32_t)((int64_t)a.Cout * a.K * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, a.y_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(RES ? a.res : a.x), 0, RES ? a.y_bytes : 0u, 0x00020000);
+
+  for (int c = t * 4; c < a.C; c += kThreads * 4) {
+    *reinterpret_cast<float4*>(sPar + c) = *reinterpret_cast<const float4*>(a.pscale + c);
+    *reinterpret_cast<float4*>(sPar + a.C + c) = *reinterpret_cast<const float4*>(a.pshift + c);
+  }
+
+  // ---- A load cursor (three steps ahead): the tile it loads and its rows
+  int la_tile = blockIdx.x, la_kt = 0;
+  int abase[AR];
+  auto setup_rows = [&](int tile) {
+    int m0, n0;
+    tile_origin(a, tile, BM, BN, m0, n0);
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int m = m0 + r0 + 32 * i;
+      // An M-tail row reads past the buffer (zeros) and feeds only its own,
+      // never stored, output row.
+      if (m < a.M) {
+        const int ow = m % a.OW, t2 = m / a.OW, oh = t2 % a.OH, n = t2 / a.OH;
+        abase[i] = ((n * a.H + oh * a.stride) * a.W + ow * a.stride) * a.C * 2;
+      } else {
+        abase[i] = (int)kOOB;
+      }
+    }
+  };
+  setup_rows(la_tile);
+  auto load_a = [&](u32x4 (&ra)[AR]) {
+    const uint32_t toff = (uint32_t)((la_kt * BK + slot * 8) * 2);
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      ra[i] = __builtin_amdgcn_raw_buffer_load_b128(
+          xr, abase[i] == (int)kOOB ? kOOB : (uint32_t)abase[i] + toff, 0, 0);
+    if (++la_kt == nk) {  // the next load starts the workgroup's next tile
+      la_kt = 0;
+      la_tile += G;
+      if (la_tile < a.nwg) setup_rows(la_tile);
+    }
+  };
+  // ---- weight DMA for global step s (one step ahead)
+  auto issue_b = [&](int s, int st) {
+    const int tile = (int)blockIdx.x + (s / nk) * G, kt = s % nk;
+    int m0, n0;
+    tile_origin(a, tile < a.nwg ? tile : (int)blockIdx.x, BM, BN, m0, n0);
+    const uint32_t boff = (uint32_t)(((n0 + r0) * a.K + kt * BK + lchunk * 8) * 2);
+    char* sB = smem + st * STAGE + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          wr, (lds_void_t*)(sB + (32 * i + wave * 8) * 128), 16, boff + (uint32_t)(32 * i * a.K * 2), 0, 0, 0);
+  };
+  // ---- BN+ReLU prologue of step s's A rows, into stage st
+  auto store_a = [&](int s, int st, u32x4 (&ra)[AR]) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i) asm volatile("" : "+v"(ra[i]));
+    const int c = (s % nk) * BK + slot * 8;
+    float sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = sPar[c + j];
+      sh[j] = sPar[a.C + c + j];
+    }
+    char* sA = smem + st * STAGE;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      float e[8];
+      unpack8(ra[i], e);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) e[j] = fmaxf(e[j] * sc[j] + sh[j], 0.0f);
+      *reinterpret_cast<u32x4*>(sA + swz(r0 + 32 * i, slot)) = pack8(e);
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  u32x2 res[TM][TN];
+
+  // The tile whose accumulators these are (epilogue) and its residual fetch.
+  auto epi_origin = [&](int s, int& m0, int& n0) {
+    tile_origin(a, (int)blockIdx.x + (s / nk) * G, BM, BN, m0, n0);
+  };
+  auto load_res = [&](int s) {
+    int m0, n0;
+    epi_origin(s, m0, n0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm * WTM + i * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int c = n0 + wn * WTN + j * 16 + fk * 4;
+        const uint32_t off = m < a.M ? (uint32_t)(((int64_t)m * a.Cout + c) * 2) : kOOB;
+        res[i][j] = __builtin_amdgcn_raw_buffer_load_b64(rr, off, 0, 0);
+      }
+    }
+  };
+  auto epilogue = [&](int s) {
+    int m0, n0;
+    epi_origin(s, m0, n0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int c = n0 + wn * WTN + j * 16 + fk * 4;
+      const float4 bb = a.bias ? *reinterpret_cast<const float4*>(a.bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm * WTM + i * 16 + fr;
+        float v0 = acc[i][j][0] + bb.x, v1 = acc[i][j][1] + bb.y, v2 = acc[i][j][2] + bb.z,
+              v3 = acc[i][j][3] + bb.w;
+        if constexpr (RES) {
+          const u32x2 r = res[i][j];
+          v0 += __uint_as_float(r.x << 16);
+          v1 += __uint_as_float(r.x & 0xffff0000u);
+          v2 += __uint_as_float(r.y << 16);
+          v3 += __uint_as_float(r.y & 0xffff0000u);
+        }
+        if (a.act) {
+          v0 = fmaxf(v0, 0.f);
+          v1 = fmaxf(v1, 0.f);
+          v2 = fmaxf(v2, 0.f);
+          v3 = fmaxf(v3, 0.f);
+        }
+        const uint32_t off = m < a.M ? (uint32_t)(((int64_t)m * a.Cout + c) * 2) : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{pack2(v0, v1), pack2(v2, v3)}, yr, off, 0, 0);
+        acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  auto compute = [&](int st) {
+    const char* sA = smem + st * STAGE;
+    mma_k64<TM, TN, true>(sA, sA + A_BYTES, wm * WTM, wn * WTN, fr, fk, acc);
+  };
+
+  // Prologue: A(0), A(1) into X / Y; stage 0 <- A(0) (+ prologue), B(0); A(2) into X.
+  u32x4 ra0[AR], ra1[AR];
+  __syncthreads();  // sPar
+  load_a(ra0);
+  if (nsteps > 1) load_a(ra1);
+  store_a(0, 0, ra0);
+  issue_b(0, 0);
+  if (nsteps > 2) load_a(ra0);
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+  __builtin_amdgcn_s_waitcnt(kLgkm0);
+  __builtin_amdgcn_s_barrier();
+  // Step s (stage st = s & 1 holds step s): A(s+1) from its register set into
+  // st^1 with the prologue, B(s+1) by DMA into st^1, A(s+3) issued into that
+  // set, the residual of a tile two steps before its end, MFMA on st,
+  // epilogue at a tile's last step, then a counted wait that retires
+  // B(s+1) and A(s+2) and leaves A(s+3) (and the residual) in flight.
+  auto step = [&](int s, u32x4 (&rx)[AR]) {
+    const int st = s & 1;
+    const bool more1 = s + 1 < nsteps, more3 = s + 3 < nsteps;
+    const bool resload = RES && (s % nk) == (nk >= 2 ? nk - 2 : 0);
+    if (more1) store_a(s + 1, st ^ 1, rx);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more1) issue_b(s + 1, st ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (resload) load_res(s);
+    if (more3) load_a(rx);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(st);
+    __builtin_amdgcn_sched_barrier(0);
+    const bool last = (s % nk) == nk - 1;
+    if (last) epilogue(s);
+    __builtin_amdgcn_sched_barrier(0);
+    // In flight past this wait: A(s+3) and, at a tile's end, the epilogue's
+    // stores issued after it (VMEM ops retire in issue order; the stores are
+    // retired by the next step's wait).
+    if (!more3)
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+    else if (last)
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR + TM * TN));
+    else
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR));
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    __builtin_amdgcn_s_barrier();
+  };
+  int s = 0;
+  for (; s + 1 < nsteps; s += 2) {
+    step(s, ra1);
+    step(s + 1, ra0);
+  }
+  if (s < nsteps) step(s, ra1);
+}
+
+template <int BM, int BN, bool RES>
+hipError_t launch_1x1_pro(ConvArgs a, hipStream_t s) {
+  static int occ = 0;  // resident workgroups per CU (LDS: two)
+  if (occ == 0) {
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, conv1x1_pro_kernel<BM, BN, RES>, kThreads, 0) !=
+            hipSuccess ||
+        o < 1)
+      o = 1;
+    occ = o;
+  }
+  a.nM = (a.M + BM - 1) / BM;
+  a.nN = a.Cout / BN;
+  a.nwg = a.nM * a.nN;
+  int grid = conv_cus() * occ;
+  grid = grid < 8 ? 8 : grid & ~7;  // multiple of 8: the XCD-aware tile numbering
+  if (a.nwg <= grid) grid = a.nwg;
+  hipLaunchKernelGGL((conv1x1_pro_kernel<BM, BN, RES>), dim3(grid), dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int BM>
+hipError_t dispatch_1x1_pro(const ConvArgs& a, bool res, hipStream_t s) {
+  if (a.Cout % 128 == 0)
+    return res ? launch_1x1_pro<BM, 128, true>(a, s) : launch_1x1_pro<BM, 128, false>(a, s);
+  return res ? launch_1x1_pro<BM, 64, true>(a, s) : launch_1x1_pro<BM, 64, false>(a, s);
+}
+
 template <int KS, int BM>
 hipError_t dispatch_pro(const ConvArgs& a, bool res, hipStream_t s) {
   if (a.Cout % 128 == 0)
@@ -2015,6 +2276,17 @@ int conv_cus() {
   if (k > 0 && share && !strcmp(share, "temporal") && phys / k > cus) cus = phys / k;
   cached[dev] = cus > 0 ? cus : 1;
   return cached[dev];
+}
+
+// Round-5 A/B (to be settled and removed): the persistent register-epilogue
+// 1x1 prologue kernel (default) vs conv_pro_kernel (VGPU_CONV_1X1P=0).
+bool conv_1x1_pro_persistent() {
+  static int on = -1;
+  if (on < 0) {
+    const char* v = getenv("VGPU_CONV_1X1P");
+    on = (v && v[0] == '0') ? 0 : 1;
+  }
+  return on == 1;
 }
 
 // A/B knob: 128-row tiles for non-prologue 1x1 convs too (VGPU_CONV_1X1_BIG=1).
@@ -2588,6 +2860,8 @@ int conv2d_impl(const void* x, const void* w, void* y, const void* res, const fl
     // Short K (≤ 2 steps) or 64-wide outputs: the persistent register kernel,
     // which overlaps the next tile's loads with this tile's epilogue, wins there.
     // (conv_pro's 1x1 form assumes no padding: it skips the zero-padding select.)
+    else if (pro && KS == 1 && pad == 0 && C <= 2048 && a.ktiles >= 2 && conv_1x1_pro_persistent())
+      e = small ? dispatch_1x1_pro<64>(c, has_res, s) : dispatch_1x1_pro<128>(c, has_res, s);
     else if (pro && pro_dma_enabled() && C <= 2048 && a.ktiles > 2 && Cout > 64 && (KS != 1 || pad == 0))
       e = KS == 1 ? (small ? dispatch_pro<1, 64>(c, has_res, s) : dispatch_pro<1, 128>(c, has_res, s))
                   : (small ? dispatch_pro<3, 64>(c, has_res, s) : dispatch_pro<3, 128>(c, has_res, s));

@@ -149,6 +149,12 @@ DEEP_CASES = [
     (4, 1024, 11, 11, 256, 1, False, "relu", False), # K = 16 steps, ragged M
     (2, 192, 7, 9, 256, 1, True, "relu", True),      # K = 3 steps (the minimum), residual
     (5, 320, 9, 7, 128, 1, True, "none", True),      # K = 5 steps: main loop + 2-step remainder
+    # persistent 1x1 prologue kernel: thousands of tiles, several per workgroup,
+    # the A loads running across tile boundaries (conv1x1_pro_kernel)
+    (64, 256, 64, 64, 256, 1, True, "relu", True),   # 4096 tiles, K = 4 steps, residual
+    (32, 256, 64, 64, 512, 2, False, "none", False), # strided projection shortcut, 1024 tiles
+    (48, 128, 48, 47, 256, 1, True, "relu", True),   # K = 2 steps, ragged M
+    (24, 1024, 22, 22, 256, 1, True, "relu", False), # stage-3 conv1 shape (BM 64 tiles), K = 16 steps
 ]
 
 
