@@ -47,7 +47,6 @@ typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 // Native 16-B vector (HIP's u32x4 is a class; copies of it go through memcpy
 // and defeat register promotion of the staging arrays).
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
-typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
 
 constexpr int kThreads = 256;
 constexpr int BK = 64;
@@ -945,16 +944,17 @@ hipError_t launch_big(ConvArgs a, hipStream_t s) {
 // thread issues the same DMA count and the counted vmcnt waits stay exact.
 // NMAJOR: workgroups of one XCD share an N tile (weight panels stay in that
 // XCD's L2 when the whole filter does not fit, e.g. stage 4: 4.7 MB).
-// M32: the wave's 64 x 64 tile as 2 x 2 v_mfma_f32_32x32x16_bf16 instead of
-// 4 x 4 16x16x32 -- half the MFMA issues for the same operand bytes, and 18
-// instead of 36 A-address registers (A/B knob VGPU_CONV_HALO_M32).
+// The wave's 64 x 64 tile is 2 x 2 v_mfma_f32_32x32x16_bf16: half the MFMA
+// issues of 4 x 4 16x16x32 for the same operand bytes and 18 instead of 36
+// A-address registers (the 16x16 form lost on every halo layer,
+// profiles/r4/kernels/convknob_m32.log, and was removed in round 5).
 // ST = 1: forward BatchNorm statistics of the stored values (ConvArgs::stats), one
 // 64-row group per wave, merged through the wave's own slab.
-template <int BM, int BN, int HPMAX, bool M32 = false, int ST = 0>
+template <int BM, int BN, int HPMAX, int ST = 0>
 __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvArgs a) {
-  static_assert(ST == 0 || ST == 1 || (ST == 2 && M32), "halo: backward statistics on the 32x32 variant");
+  static_assert(ST == 0 || ST == 1 || ST == 2, "halo: statistics mode");
   constexpr int T = BM * BN / 64, WN = BN / 64;
-  constexpr int TM = M32 ? 2 : 4, TN = M32 ? 2 : 4;  // wave tile 64 x 64
+  constexpr int TM = 2, TN = 2;                       // wave tile 64 x 64 in 32x32 MFMAs
   constexpr int RPI = T / 8;                          // LDS rows (128 B) per DMA instruction
   constexpr int HI = HPMAX / RPI, BR = BN / RPI;      // DMA instructions per thread: halo, panel
   constexpr int HSTAGE = HPMAX * 128, BSTAGE = BN * 128;
@@ -967,19 +967,18 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int fr = lane & 15, fk = lane >> 4;
-  // LDS images: 16-B chunk c of row r sits in slot c ^ f(r).  The 16x16 reads
-  // (16 rows x 4 k-chunks per lane group) are conflict-free with f = r & 7;
-  // the 32x32 reads (32 consecutive rows, one k-chunk per 32-lane half) put two
-  // rows on one bank group in every ds_read_b128 lane group with it (4 extra
-  // LDS cycles per read: SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS = 4.1 in
+  // LDS images: 16-B chunk c of row r sits in slot c ^ f(r).  The 32x32 reads
+  // (32 consecutive rows, one k-chunk per 32-lane half) put two rows on one
+  // bank group in every ds_read_b128 lane group with f = r & 7 (4 extra LDS
+  // cycles per read: SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS = 4.1 in
   // profiles/r4/kernels/pmc_flagship_r4.md), and none with f = (r & 7) ^ bit 3.
   // DMA rows are i·RPI + lrow with RPI a multiple of 16, so f of the LDS row is f(lrow).
   const int lrow = t >> 3;
-  const int lchunk = (t & 7) ^ (lrow & 7) ^ (M32 ? (lrow >> 3) & 1 : 0);
+  const int lchunk = (t & 7) ^ (lrow & 7) ^ ((lrow >> 3) & 1);
   auto swzh = [](int row, int slot) {  // swz() with this kernel's f
-    return row * 128 + ((slot ^ (row & 7) ^ (M32 ? (row >> 3) & 1 : 0)) << 4);
+    return row * 128 + ((slot ^ (row & 7) ^ ((row >> 3) & 1)) << 4);
   };
-  static_assert(!M32 || (T / 8) % 16 == 0, "rows per DMA instruction keep bit 3 of the row");
+  static_assert((T / 8) % 16 == 0, "rows per DMA instruction keep bit 3 of the row");
   int m0, n0;
   if (a.nmajor) {
     const int xcd = blockIdx.x & 7, q = a.nwg >> 3, r8 = a.nwg & 7;
@@ -1031,17 +1030,15 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
           kt >= 0 ? boff + (uint32_t)((i * RPI * a.K + kt * BK) * 2) : kOOB, 0, 0, 0);
   };
 
-  // Per-lane, per-tap A fragment addresses: byte offsets in a halo stage of
-  // k-half 0 (logical slot fk, low 16 bits) and k-half 1 (slot 4 + fk = the
-  // same ^ 64, high 16 bits) — one register per (tap, row tile).  Unpacked at
-  // each use; pinned per channel block so hipcc cannot hoist 72 unpacked
-  // addresses out of the loop (it did: 256 VGPRs and spills).
+  // Per-lane, per-tap A fragment addresses: the byte offset in a halo stage of
+  // the lane's k-step-0 chunk, one register per (tap, row tile); pinned per
+  // channel block so hipcc cannot hoist derived addresses out of the loop.
   constexpr int ZROW = HPMAX - 1;
   static_assert(HSTAGE <= 65536, "16-bit halo addresses");
   uint32_t aaddr[9][TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int m = M32 ? m0 + wm * 64 + i * 32 + (lane & 31) : m0 + wm * 64 + i * 16 + fr;
+    const int m = m0 + wm * 64 + i * 32 + (lane & 31);
     const bool mok = m < a.M;
     const int row = (mok ? m : m0) / W;
     const int ow = (mok ? m : m0) - row * W, oh = row % H;
@@ -1052,23 +1049,17 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
         const int ih = oh + kh - 1, iw = ow + kw - 1;
         const bool v = mok & ((unsigned)ih < (unsigned)H) & ((unsigned)iw < (unsigned)W);
         const int h = v ? (row + kh - 1 - g_lo) * W + iw : ZROW;
-        if constexpr (M32) {
-          // k-step ks (16 channels) of lane half kb reads chunk 2·ks + kb: the
-          // address of ks = that of ks 0 XOR (ks << 5)
-          aaddr[kh * 3 + kw][i] = (uint32_t)swzh(h, lane >> 5);
-        } else {
-          const uint32_t a0 = (uint32_t)(h * 128 + ((fk ^ (h & 7)) << 4));
-          aaddr[kh * 3 + kw][i] = a0 | ((a0 ^ 64u) << 16);
-        }
+        // k-step ks (16 channels) of lane half kb reads chunk 2·ks + kb: the
+        // address of ks = that of ks 0 XOR (ks << 5)
+        aaddr[kh * 3 + kw][i] = (uint32_t)swzh(h, lane >> 5);
       }
   }
 
-  typedef typename std::conditional<M32, f32x16_t, f32x4_t>::type acc_t;
-  acc_t acc[TM][TN];
+  f32x16_t acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = acc_t{};
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16_t{};
 
   // 32x32x16: four 16-channel k-steps per tap; operands of step ks+1 are read
   // while step ks multiplies (lgkmcnt(4): the newer 4 reads may stay in flight).
@@ -1099,40 +1090,8 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          if constexpr (M32)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][i], bfr[cur][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][i], bfr[cur][j], acc[i][j], 0, 0, 0);
     }
-  };
-
-  auto compute = [&](int tap, const char* sH, const char* sB) {
-    bf16x8_t af[2][TM], bfr[2][TN];
-    auto rd = [&](int kk) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        af[kk][i] = *reinterpret_cast<const bf16x8_t*>(sH + (kk ? aaddr[tap][i] >> 16 : aaddr[tap][i] & 0xffffu));
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bfr[kk][j] = *reinterpret_cast<const bf16x8_t*>(sB + swz(wn * 64 + j * 16 + fr, kk * 4 + fk));
-    };
-    auto mm = [&](int kk) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          if constexpr (!M32)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
-    };
-    rd(0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_waitcnt(kLgkm0);
-    __builtin_amdgcn_sched_barrier(0);
-    rd(1);
-    __builtin_amdgcn_sched_barrier(0);
-    mm(0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_waitcnt(kLgkm0);
-    __builtin_amdgcn_sched_barrier(0);
-    mm(1);
   };
 
   const int nb = a.cblocks;
@@ -1162,10 +1121,7 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
         __builtin_amdgcn_s_waitcnt(vmcnt_imm(BR));
       }
       __builtin_amdgcn_s_barrier();
-      if constexpr (M32)
-        compute32(tap, sH, smem + 2 * HSTAGE + bs * BSTAGE);
-      else
-        compute(tap, sH, smem + 2 * HSTAGE + bs * BSTAGE);
+      compute32(tap, sH, smem + 2 * HSTAGE + bs * BSTAGE);
       __builtin_amdgcn_s_waitcnt(kLgkm0);
       __builtin_amdgcn_s_barrier();
       bs ^= 1;
@@ -1204,8 +1160,8 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
       kis[j] = a.bncoef[3 * a.Cout + col + j];
     }
   }
-  // 16x16 tiles: pass p = row tile i.  32x32 tiles: pass p = half (p & 1) of row
-  // tile p >> 1; lane l holds rows 8b + 4(l >> 5) + e (b = 0..3) of column l & 31.
+  // Pass p = half (p & 1) of row tile p >> 1; lane l holds rows
+  // 8b + 4(l >> 5) + e (b = 0..3) of column l & 31.
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     u32x4 xb[2];
@@ -1217,7 +1173,7 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
             xr2, m < a.M ? (uint32_t)(((int64_t)m * a.Cout + col) * 2) : kOOB, 0, 0);
       }
     }
-    if constexpr (M32) {
+    {
       const int i = p >> 1, hb = (p & 1) * 2;
 #pragma unroll
       for (int j = 0; j < TN; ++j)
@@ -1226,11 +1182,6 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             sC[(8 * b + 4 * (lane >> 5) + e) * CS + j * 32 + (lane & 31)] = acc[i][j][4 * (hb + b) + e];
-    } else {
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sC[(fk * 4 + e) * CS + j * 16 + fr] = acc[p][j][e];
     }
     __builtin_amdgcn_s_waitcnt(kLgkm0);
 #pragma unroll
@@ -1299,19 +1250,6 @@ bool halo_enabled() {
 
 unsigned long long g_halo_launches = 0;  // vgpu_conv_halo_launches (tests: the halo path ran)
 
-// The 32x32x16 MFMA variant, default since it measured bit-identical and faster
-// on every halo layer (stage 3 35.6 -> 34.0 us, stage 4 39.3 -> 35.2, r152
-// stage 4 35.5 -> 31.2; flagship 26 767 -> 27 386 images/s on one box,
-// profiles/r4/kernels/convknob_m32.log).  VGPU_CONV_HALO_M32=0: 16x16x32.
-int g_halo_m32 = -1;
-bool halo_m32() {
-  if (g_halo_m32 < 0) {
-    const char* v = getenv("VGPU_CONV_HALO_M32");
-    g_halo_m32 = (v && v[0] == '0') ? 0 : 1;
-  }
-  return g_halo_m32 == 1;
-}
-
 template <int BM, int BN, int HPMAX>
 hipError_t launch_halo(ConvArgs a, hipStream_t s) {
   ++g_halo_launches;
@@ -1320,16 +1258,12 @@ hipError_t launch_halo(ConvArgs a, hipStream_t s) {
   a.nwg = a.nM * a.nN;
   // N-major placement when the filter outgrows an XCD's L2 share (4 MiB).
   a.nmajor = (int64_t)a.Cout * a.K * 2 > ((int64_t)5 << 19) ? 1 : 0;
-  if (a.stats && a.bnx)  // the dispatch sends backward statistics here only with the 32x32 variant
-    hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, true, 2>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
-  else if (a.stats && halo_m32())
-    hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, true, 1>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
+  if (a.stats && a.bnx)
+    hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, 2>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
   else if (a.stats)
-    hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, false, 1>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
-  else if (halo_m32())
-    hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, true>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
+    hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, 1>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
   else
-    hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX, false>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
+    hipLaunchKernelGGL((conv_halo_kernel<BM, BN, HPMAX>), dim3(a.nwg), dim3(BM * BN / 64), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1603,266 +1537,6 @@ hipError_t launch_pro(ConvArgs a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// ---- Persistent 1x1 conv with the block-entry BN+ReLU prologue (round 5) ----
-//
-// conv_pro_kernel launches one workgroup per tile.  On the ResNet-50 1x1 convs
-// a tile is 4-16 K steps, so every tile paid its pipeline fill (three A loads
-// and a weight DMA deep) and its epilogue (two LDS staging passes behind
-// barriers) in series: 2-2.6 TB/s on layers the roofline calls HBM-bound
-// (profiles/r4/kernels/pmc_flagship_r4_final.md).  Here a workgroup walks tiles
-// b, b+G, ... as one flattened sequence of K steps: the A loads run three steps
-// ahead and the weight DMA one step ahead straight across tile boundaries, so
-// the next tile's first steps are in flight while the current tile finishes.
-//
-// The epilogue never touches LDS, so it needs no barrier and leaves the
-// pipeline's stages alone: the MFMA is transposed (acc = W·Aᵀ), which leaves
-// each lane 4 consecutive output channels of one pixel, and bias, residual,
-// ReLU and the bf16 store are done from registers (one 8-byte store per 16x16
-// sub-tile; the four lanes of a pixel write 32 contiguous bytes).  The
-// residual of a tile is fetched two K steps before its epilogue.
-//
-// Stride 1 or 2, no padding, C % 64 == 0, Cout % BN == 0.
-template <int BM, int BN, bool RES>
-__global__ void __launch_bounds__(kThreads, 2) conv1x1_pro_kernel(const ConvArgs a) {
-  constexpr int AR = BM / 32, BR = BN / 32;
-  constexpr int WTM = BM / 2, WTN = BN / 2;
-  constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
-  constexpr int STAGE = A_BYTES + B_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2048 * 2 * 4];
-  float* sPar = reinterpret_cast<float*>(smem + 2 * STAGE);
-  const int G = gridDim.x;
-  if ((int)blockIdx.x >= a.nwg) return;
-
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int fr = lane & 15, fk = lane >> 4;
-  const int slot = t & 7, r0 = t >> 3;
-  const int lchunk = slot ^ (r0 & 7);
-  const int nk = a.ktiles;                                       // K steps per tile (= C / 64)
-  const int ntile = (a.nwg - (int)blockIdx.x + G - 1) / G;       // tiles of this workgroup
-  const int nsteps = ntile * nk;
-
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(a.x), 0, a.x_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(a.w), 0, (uint32_t)((int64_t)a.Cout * a.K * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, a.y_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(RES ? a.res : a.x), 0, RES ? a.y_bytes : 0u, 0x00020000);
-
-  for (int c = t * 4; c < a.C; c += kThreads * 4) {
-    *reinterpret_cast<float4*>(sPar + c) = *reinterpret_cast<const float4*>(a.pscale + c);
-    *reinterpret_cast<float4*>(sPar + a.C + c) = *reinterpret_cast<const float4*>(a.pshift + c);
-  }
-
-  // ---- A load cursor (three steps ahead): the tile it loads and its rows
-  int la_tile = blockIdx.x, la_kt = 0;
-  int abase[AR];
-  auto setup_rows = [&](int tile) {
-    int m0, n0;
-    tile_origin(a, tile, BM, BN, m0, n0);
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int m = m0 + r0 + 32 * i;
-      // An M-tail row reads past the buffer (zeros) and feeds only its own,
-      // never stored, output row.
-      if (m < a.M) {
-        const int ow = m % a.OW, t2 = m / a.OW, oh = t2 % a.OH, n = t2 / a.OH;
-        abase[i] = ((n * a.H + oh * a.stride) * a.W + ow * a.stride) * a.C * 2;
-      } else {
-        abase[i] = (int)kOOB;
-      }
-    }
-  };
-  setup_rows(la_tile);
-  auto load_a = [&](u32x4 (&ra)[AR]) {
-    const uint32_t toff = (uint32_t)((la_kt * BK + slot * 8) * 2);
-#pragma unroll
-    for (int i = 0; i < AR; ++i)
-      ra[i] = __builtin_amdgcn_raw_buffer_load_b128(
-          xr, abase[i] == (int)kOOB ? kOOB : (uint32_t)abase[i] + toff, 0, 0);
-    if (++la_kt == nk) {  // the next load starts the workgroup's next tile
-      la_kt = 0;
-      la_tile += G;
-      if (la_tile < a.nwg) setup_rows(la_tile);
-    }
-  };
-  // ---- weight DMA for global step s (one step ahead)
-  auto issue_b = [&](int s, int st) {
-    const int tile = (int)blockIdx.x + (s / nk) * G, kt = s % nk;
-    int m0, n0;
-    tile_origin(a, tile < a.nwg ? tile : (int)blockIdx.x, BM, BN, m0, n0);
-    const uint32_t boff = (uint32_t)(((n0 + r0) * a.K + kt * BK + lchunk * 8) * 2);
-    char* sB = smem + st * STAGE + A_BYTES;
-#pragma unroll
-    for (int i = 0; i < BR; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          wr, (lds_void_t*)(sB + (32 * i + wave * 8) * 128), 16, boff + (uint32_t)(32 * i * a.K * 2), 0, 0, 0);
-  };
-  // ---- BN+ReLU prologue of step s's A rows, into stage st
-  auto store_a = [&](int s, int st, u32x4 (&ra)[AR]) {
-#pragma unroll
-    for (int i = 0; i < AR; ++i) asm volatile("" : "+v"(ra[i]));
-    const int c = (s % nk) * BK + slot * 8;
-    float sc[8], sh[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sc[j] = sPar[c + j];
-      sh[j] = sPar[a.C + c + j];
-    }
-    char* sA = smem + st * STAGE;
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      float e[8];
-      unpack8(ra[i], e);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) e[j] = fmaxf(e[j] * sc[j] + sh[j], 0.0f);
-      *reinterpret_cast<u32x4*>(sA + swz(r0 + 32 * i, slot)) = pack8(e);
-    }
-  };
-
-  f32x4_t acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  u32x2 res[TM][TN];
-
-  // The tile whose accumulators these are (epilogue) and its residual fetch.
-  auto epi_origin = [&](int s, int& m0, int& n0) {
-    tile_origin(a, (int)blockIdx.x + (s / nk) * G, BM, BN, m0, n0);
-  };
-  auto load_res = [&](int s) {
-    int m0, n0;
-    epi_origin(s, m0, n0);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wm * WTM + i * 16 + fr;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int c = n0 + wn * WTN + j * 16 + fk * 4;
-        const uint32_t off = m < a.M ? (uint32_t)(((int64_t)m * a.Cout + c) * 2) : kOOB;
-        res[i][j] = __builtin_amdgcn_raw_buffer_load_b64(rr, off, 0, 0);
-      }
-    }
-  };
-  auto epilogue = [&](int s) {
-    int m0, n0;
-    epi_origin(s, m0, n0);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int c = n0 + wn * WTN + j * 16 + fk * 4;
-      const float4 bb = a.bias ? *reinterpret_cast<const float4*>(a.bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int m = m0 + wm * WTM + i * 16 + fr;
-        float v0 = acc[i][j][0] + bb.x, v1 = acc[i][j][1] + bb.y, v2 = acc[i][j][2] + bb.z,
-              v3 = acc[i][j][3] + bb.w;
-        if constexpr (RES) {
-          const u32x2 r = res[i][j];
-          v0 += __uint_as_float(r.x << 16);
-          v1 += __uint_as_float(r.x & 0xffff0000u);
-          v2 += __uint_as_float(r.y << 16);
-          v3 += __uint_as_float(r.y & 0xffff0000u);
-        }
-        if (a.act) {
-          v0 = fmaxf(v0, 0.f);
-          v1 = fmaxf(v1, 0.f);
-          v2 = fmaxf(v2, 0.f);
-          v3 = fmaxf(v3, 0.f);
-        }
-        const uint32_t off = m < a.M ? (uint32_t)(((int64_t)m * a.Cout + c) * 2) : kOOB;
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2{pack2(v0, v1), pack2(v2, v3)}, yr, off, 0, 0);
-        acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-  };
-  auto compute = [&](int st) {
-    const char* sA = smem + st * STAGE;
-    mma_k64<TM, TN, true>(sA, sA + A_BYTES, wm * WTM, wn * WTN, fr, fk, acc);
-  };
-
-  // Prologue: A(0), A(1) into X / Y; stage 0 <- A(0) (+ prologue), B(0); A(2) into X.
-  u32x4 ra0[AR], ra1[AR];
-  __syncthreads();  // sPar
-  load_a(ra0);
-  if (nsteps > 1) load_a(ra1);
-  store_a(0, 0, ra0);
-  issue_b(0, 0);
-  if (nsteps > 2) load_a(ra0);
-  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-  __builtin_amdgcn_s_waitcnt(kLgkm0);
-  __builtin_amdgcn_s_barrier();
-  // Step s (stage st = s & 1 holds step s): A(s+1) from its register set into
-  // st^1 with the prologue, B(s+1) by DMA into st^1, A(s+3) issued into that
-  // set, the residual of a tile two steps before its end, MFMA on st,
-  // epilogue at a tile's last step, then a counted wait that retires
-  // B(s+1) and A(s+2) and leaves A(s+3) (and the residual) in flight.
-  auto step = [&](int s, u32x4 (&rx)[AR]) {
-    const int st = s & 1;
-    const bool more1 = s + 1 < nsteps, more3 = s + 3 < nsteps;
-    const bool resload = RES && (s % nk) == (nk >= 2 ? nk - 2 : 0);
-    if (more1) store_a(s + 1, st ^ 1, rx);
-    __builtin_amdgcn_sched_barrier(0);
-    if (more1) issue_b(s + 1, st ^ 1);
-    __builtin_amdgcn_sched_barrier(0);
-    if (resload) load_res(s);
-    if (more3) load_a(rx);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(st);
-    __builtin_amdgcn_sched_barrier(0);
-    const bool last = (s % nk) == nk - 1;
-    if (last) epilogue(s);
-    __builtin_amdgcn_sched_barrier(0);
-    // In flight past this wait: A(s+3) and, at a tile's end, the epilogue's
-    // stores issued after it (VMEM ops retire in issue order; the stores are
-    // retired by the next step's wait).
-    if (!more3)
-      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-    else if (last)
-      __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR + TM * TN));
-    else
-      __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR));
-    __builtin_amdgcn_s_waitcnt(kLgkm0);
-    __builtin_amdgcn_s_barrier();
-  };
-  int s = 0;
-  for (; s + 1 < nsteps; s += 2) {
-    step(s, ra1);
-    step(s + 1, ra0);
-  }
-  if (s < nsteps) step(s, ra1);
-}
-
-template <int BM, int BN, bool RES>
-hipError_t launch_1x1_pro(ConvArgs a, hipStream_t s) {
-  static int occ = 0;  // resident workgroups per CU (LDS: two)
-  if (occ == 0) {
-    int o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, conv1x1_pro_kernel<BM, BN, RES>, kThreads, 0) !=
-            hipSuccess ||
-        o < 1)
-      o = 1;
-    occ = o;
-  }
-  a.nM = (a.M + BM - 1) / BM;
-  a.nN = a.Cout / BN;
-  a.nwg = a.nM * a.nN;
-  int grid = conv_cus() * occ;
-  grid = grid < 8 ? 8 : grid & ~7;  // multiple of 8: the XCD-aware tile numbering
-  if (a.nwg <= grid) grid = a.nwg;
-  hipLaunchKernelGGL((conv1x1_pro_kernel<BM, BN, RES>), dim3(grid), dim3(kThreads), 0, s, a);
-  return hipGetLastError();
-}
-
-template <int BM>
-hipError_t dispatch_1x1_pro(const ConvArgs& a, bool res, hipStream_t s) {
-  if (a.Cout % 128 == 0)
-    return res ? launch_1x1_pro<BM, 128, true>(a, s) : launch_1x1_pro<BM, 128, false>(a, s);
-  return res ? launch_1x1_pro<BM, 64, true>(a, s) : launch_1x1_pro<BM, 64, false>(a, s);
-}
-
 template <int KS, int BM>
 hipError_t dispatch_pro(const ConvArgs& a, bool res, hipStream_t s) {
   if (a.Cout % 128 == 0)
@@ -1982,7 +1656,7 @@ __device__ __forceinline__ void tail_epilogue(const ConvArgs& a, f32x4_t (&acc)[
 // block accumulates in registers across the chunks.  Saves the next block's
 // re-read of the 4W-wide activation (stage 1 at b=50: 194 MB per block).
 // Numerics equal conv23 + conv_pro (same bf16 roundings, same K order).
-template <int BM, int W, bool NEXT = false>
+template <int BM, int W, bool NEXT = false, int NS1 = 3>
 __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, const ConvArgs b,
                                                              const ConvArgs c) {
   constexpr int KCH = W / 64;                // conv3 K chunks (64 channels each)
@@ -1994,15 +1668,19 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
   constexpr int BN2 = 128, TN2 = 4;           // conv3 output chunk; 64 columns per wave
   constexpr int B2_BYTES = BN2 * 128 * KCH;
   constexpr int EPI = (BM / 2) * (BN2 + 4) * 4;
-  constexpr int P1 = 2 * STAGE, P2 = B2_BYTES + EPI;
-  constexpr int P = P1 > P2 ? P1 : P2;
   constexpr int A2_BYTES = BM * 128 * KCH;
+  // Phase 1's NS1-stage DMA ring and phase 2's [conv3 panel | epilogue staging |
+  // conv3 A image] share one region: the A image is written only after the
+  // last phase-1 step, so a 3-deep ring still leaves two workgroups per CU.
+  constexpr int P1 = NS1 * STAGE, P2 = B2_BYTES + EPI + A2_BYTES;
+  constexpr int P = P1 > P2 ? P1 : P2;
   // conv2 bias [W] and (NEXT) conv1's prologue scale/shift [4W] each live in
   // LDS: a global load in phase 2 would make hipcc drain the in-flight DMA.
   constexpr int PAR = (W + (NEXT ? 8 * W : 0)) * 4;
-  __shared__ __attribute__((aligned(16))) char smem[P + A2_BYTES + PAR];
-  char* sA2 = smem + P;
-  float* sPar = reinterpret_cast<float*>(smem + P + A2_BYTES);
+  static_assert(2 * (P + PAR) <= 160 * 1024, "conv23: two workgroups per CU");
+  __shared__ __attribute__((aligned(16))) char smem[P + PAR];
+  char* sA2 = smem + B2_BYTES + EPI;
+  float* sPar = reinterpret_cast<float*>(smem + P);
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -2068,20 +1746,44 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  issue(0, 0);
-  for (int kt = 0; kt < a.ktiles; ++kt) {
-    const int st = kt & 1;
-    if (kt + 1 < a.ktiles) {
-      issue(kt + 1, st ^ 1);
-      __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR + BR));
-    } else {
-      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+  if constexpr (NS1 == 2) {
+    issue(0, 0);
+    for (int kt = 0; kt < a.ktiles; ++kt) {
+      const int st = kt & 1;
+      if (kt + 1 < a.ktiles) {
+        issue(kt + 1, st ^ 1);
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR + BR));
+      } else {
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+      }
+      __builtin_amdgcn_s_barrier();
+      const char* sA = smem + st * STAGE;
+      mma_k64<TM, TN, true>(sA, sA + A_BYTES, wm * WTM, wn * WTN, fr, fk, acc);
+      __builtin_amdgcn_s_waitcnt(kLgkm0);
+      __builtin_amdgcn_s_barrier();
     }
-    __builtin_amdgcn_s_barrier();
-    const char* sA = smem + st * STAGE;
-    mma_k64<TM, TN, true>(sA, sA + A_BYTES, wm * WTM, wn * WTN, fr, fk, acc);
+  } else {
+    // Two steps in flight behind the MMA, one barrier per step: step kt's wait
+    // + barrier also proves every wave finished step kt-1's reads of the stage
+    // that issue(kt+2) refills.
+    static_assert(NS1 == 3, "conv23: 2- or 3-stage phase 1");
+    issue(0, 0);
+    if (a.ktiles > 1) issue(1, 1);
+    int st = 0;
+    for (int kt = 0; kt < a.ktiles; ++kt) {
+      if (kt + 1 < a.ktiles)
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR + BR));
+      else
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+      __builtin_amdgcn_s_waitcnt(kLgkm0);
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < a.ktiles) issue(kt + 2, st == 0 ? 2 : st - 1);
+      const char* sA = smem + st * STAGE;
+      mma_k64<TM, TN, true>(sA, sA + A_BYTES, wm * WTM, wn * WTN, fr, fk, acc);
+      st = st == 2 ? 0 : st + 1;
+    }
     __builtin_amdgcn_s_waitcnt(kLgkm0);
-    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();  // the stages are read out before the A image overwrites them
   }
 
   // ---- phase 2: conv3 over 128-wide output chunks --------------------------------
@@ -2232,15 +1934,6 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
   }
 }
 
-bool pro_dma_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* v = getenv("VGPU_CONV_PRO_DMA");
-    on = (v && (v[0] == '0' || v[0] == 'n' || v[0] == 'f')) ? 0 : 1;
-  }
-  return on == 1;
-}
-
 // CUs this process can occupy on the current device — the grid-fill term of
 // the tile choice.  A vGPU pod owns an XCD-balanced CU mask of
 // VGPU_DEVICE_CU_LIMIT_<i> % of the device (the enforcement library's env
@@ -2278,32 +1971,12 @@ int conv_cus() {
   return cached[dev];
 }
 
-// Round-5 A/B (to be settled and removed): the persistent register-epilogue
-// 1x1 prologue kernel (default) vs conv_pro_kernel (VGPU_CONV_1X1P=0).
-bool conv_1x1_pro_persistent() {
-  static int on = -1;
-  if (on < 0) {
-    const char* v = getenv("VGPU_CONV_1X1P");
-    on = (v && v[0] == '0') ? 0 : 1;
-  }
-  return on == 1;
-}
-
 // A/B knob: 128-row tiles for non-prologue 1x1 convs too (VGPU_CONV_1X1_BIG=1).
 bool conv_1x1_big() {
   static int on = -1;
   if (on < 0) {
     const char* v = getenv("VGPU_CONV_1X1_BIG");
     on = (v && v[0] == '1') ? 1 : 0;
-  }
-  return on == 1;
-}
-
-bool glds_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* v = getenv("VGPU_CONV_GLDS");
-    on = (v && (v[0] == '0' || v[0] == 'n' || v[0] == 'f')) ? 0 : 1;
   }
   return on == 1;
 }
@@ -2629,7 +2302,6 @@ VGPU_API void vgpu_conv_set_tile_m(int bm) { g_forced_bm = bm; }
 VGPU_API void vgpu_conv_set_big(int mode) { g_forced_big = mode; }  // -1 env/heuristic, 0 off, 1 when eligible
 VGPU_API void vgpu_conv_set_halo(int mode) { g_forced_halo = mode; }  // -1 env, 0 off, 1 on, 2/3 BM 256/128
 VGPU_API unsigned long long vgpu_conv_halo_launches() { return g_halo_launches; }
-VGPU_API void vgpu_conv_set_halo_m32(int on) { g_halo_m32 = on < 0 ? -1 : (on ? 1 : 0); }  // -1: env
 
 // Fused conv2 (3x3, pad 1, stride s, C = W → W, bias + ReLU) + conv3 (1x1,
 // W → 4W) + residual; with w1n, also the next block's conv1 (1x1, 4W → W,
@@ -2692,17 +2364,22 @@ static int conv23_impl(const void* x, const void* w2, const float* b2, const voi
     }
     const int bm = C == 64 ? 128 : 64;
     c.nM = (c.M + bm - 1) / bm; c.nN = 1; c.nwg = c.nM;
+    static const bool ns2 = getenv("VGPU_CONV23_NS") && atoi(getenv("VGPU_CONV23_NS")) == 2;  // A/B
+#define VGPU_C23(BM_, W_, NX_)                                                                          \
+  do {                                                                                                 \
+    if (ns2)                                                                                           \
+      hipLaunchKernelGGL((conv23_kernel<BM_, W_, NX_, 2>), dim3(c.nwg), dim3(kThreads), 0, s, c, d, e); \
+    else                                                                                               \
+      hipLaunchKernelGGL((conv23_kernel<BM_, W_, NX_, 3>), dim3(c.nwg), dim3(kThreads), 0, s, c, d, e); \
+  } while (0)
     if (C == 64) {
-      if (next)
-        hipLaunchKernelGGL((conv23_kernel<128, 64, true>), dim3(c.nwg), dim3(kThreads), 0, s, c, d, e);
-      else
-        hipLaunchKernelGGL((conv23_kernel<128, 64>), dim3(c.nwg), dim3(kThreads), 0, s, c, d, e);
+      if (next) VGPU_C23(128, 64, true);
+      else VGPU_C23(128, 64, false);
     } else {
-      if (next)
-        hipLaunchKernelGGL((conv23_kernel<64, 128, true>), dim3(c.nwg), dim3(kThreads), 0, s, c, d, e);
-      else
-        hipLaunchKernelGGL((conv23_kernel<64, 128>), dim3(c.nwg), dim3(kThreads), 0, s, c, d, e);
+      if (next) VGPU_C23(64, 128, true);
+      else VGPU_C23(64, 128, false);
     }
+#undef VGPU_C23
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return (int)err;
   }
@@ -2802,7 +2479,7 @@ int conv2d_impl(const void* x, const void* w, void* y, const void* res, const fl
     a.res_bytes = (uint32_t)rb;
   }
   const bool pro = pscale != nullptr, has_res = res != nullptr;
-  if (stats && (narrow || pro || !glds_enabled())) return -1;
+  if (stats && (narrow || pro)) return -1;
   // Buffer offsets are 32-bit: run the batch in slices whose activations stay < 2 GiB.
   const int64_t xi = (int64_t)H * W * C * 2, yi = (int64_t)a.OH * a.OW * Cout * 2;
   const int64_t lim = ((int64_t)1 << 31) - 1;
@@ -2834,7 +2511,7 @@ int conv2d_impl(const void* x, const void* w, void* y, const void* res, const fl
     hipError_t e;
     // LDS-DMA kernels for every conv without a prologue; prologue convs stage A
     // through registers (conv_pro_kernel / conv_gemm_kernel).
-    const bool glds = glds_enabled() && !pro;
+    const bool glds = !pro;
     // 256x256 tiles: 1x1 / stride 1 / no prologue, Cout % 256 == 0, deep K
     // (≥ 1024: below it these layers are HBM-bound and the 64-row tiles at 3
     // blocks per CU win — the ResNet-50 flagship measured 1 % slower with the
@@ -2850,7 +2527,7 @@ int conv2d_impl(const void* x, const void* w, void* y, const void* res, const fl
                                 (g_forced_big == 2 && C >= 1024 && tiles256 >= (int64_t)conv_cus()));
     // 3x3 / stride 1 without prologue or residual: the halo-tile kernel.
     const bool halo = (g_forced_halo < 0 ? halo_enabled() : g_forced_halo > 0) && !narrow && !pro && !has_res &&
-                      KS == 3 && stride == 1 && pad == 1 && (!bnx || halo_m32());
+                      KS == 3 && stride == 1 && pad == 1;
     if (halo && (e = dispatch_halo(c, s)) != hipErrorNotSupported) {
       // launched (or a launch error)
     } else if (big)
@@ -2860,9 +2537,7 @@ int conv2d_impl(const void* x, const void* w, void* y, const void* res, const fl
     // Short K (≤ 2 steps) or 64-wide outputs: the persistent register kernel,
     // which overlaps the next tile's loads with this tile's epilogue, wins there.
     // (conv_pro's 1x1 form assumes no padding: it skips the zero-padding select.)
-    else if (pro && KS == 1 && pad == 0 && C <= 2048 && a.ktiles >= 2 && conv_1x1_pro_persistent())
-      e = small ? dispatch_1x1_pro<64>(c, has_res, s) : dispatch_1x1_pro<128>(c, has_res, s);
-    else if (pro && pro_dma_enabled() && C <= 2048 && a.ktiles > 2 && Cout > 64 && (KS != 1 || pad == 0))
+    else if (pro && C <= 2048 && a.ktiles > 2 && Cout > 64 && (KS != 1 || pad == 0))
       e = KS == 1 ? (small ? dispatch_pro<1, 64>(c, has_res, s) : dispatch_pro<1, 128>(c, has_res, s))
                   : (small ? dispatch_pro<3, 64>(c, has_res, s) : dispatch_pro<3, 128>(c, has_res, s));
     else if (glds)

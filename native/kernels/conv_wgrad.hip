@@ -412,130 +412,6 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(const WgradArgs a) 
   }
 }
 
-// ---- LDS-DMA variant (128 x 128 tiles) -------------------------------------------------
-// The register-staged kernel above spends its K step on global -> VGPR ->
-// ds_write traffic with one step of lead, and measured latency-bound (~1 us
-// per 32-pixel step).  Here both operands move HBM/L2 -> LDS by
-// buffer_load ... lds into an NS-deep ring of 16 KB stages (dy and x rows as
-// they sit in memory, 256-B rows, the swz<256> image realised by having each
-// lane fetch the logical chunk its physical slot holds), so step k+NS-1 is in
-// flight while step k multiplies, behind a counted vmcnt and one barrier per
-// step.  No staging registers: 2 workgroups per CU (64 KB of LDS each).
-// KS1: 1x1 / stride 1 / pad 0 -- the x row of a pixel is the pixel (no
-// im2col arithmetic).  Steps past the split's end are dummy DMAs (out-of-range
-// offsets, zeros) into stages nobody reads, so the counted waits stay exact.
-constexpr int kNS = 4;
-template <bool KS1>
-__global__ void __launch_bounds__(kThreads, 2) wgrad_glds_kernel(const WgradArgs a) {
-  constexpr int BM = 128, BN = 128, RS = 256;
-  constexpr int A_BYTES = KP * RS, STAGE = 2 * A_BYTES;  // dy [32][128] + x [32][128]
-  constexpr int TM = 4, TN = 4;                          // wave tile 64 x 64
-  __shared__ __attribute__((aligned(16))) char smem[kNS * STAGE];
-
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int tap = blockIdx.x / a.cblocks, cb = blockIdx.x - tap * a.cblocks;
-  const int kh = tap / a.KS, kw = tap - kh * a.KS;
-  const int m0 = blockIdx.y * BM;
-  const int split = blockIdx.z;
-  const int step0 = split * a.steps;
-  const int ohw = a.OH * a.OW;
-  const int nsteps = min(a.steps, (a.P + KP - 1) / KP - step0);
-
-  const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(a.dy), 0, a.dy_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(a.x), 0, a.x_bytes, 0x00020000);
-
-  // This lane's share of a step: rows 16g + 4w + lane/16 (g = 0, 1) of each
-  // image; physical slot lane%16 holds logical chunk slot ^ swz(row).
-  int rows[2], chk[2];
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    rows[g] = 16 * g + 4 * wave + (lane >> 4);
-    chk[g] = (lane & 15) ^ swz<RS>(rows[g]);
-  }
-  auto issue = [&](int step, int st) {  // step >= nsteps: dummy
-    char* sA = smem + st * STAGE;
-    char* sB = sA + A_BYTES;
-    const bool live = step < nsteps;
-    const int pbase = (step0 + step) * KP;
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      const int r = rows[g], pix = pbase + r;
-      const bool pv = live & (pix < a.P);
-      const uint32_t doff = pv ? (uint32_t)(((int64_t)pix * a.Cout + m0 + chk[g] * 8) * 2) : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (lds_void_t*)(sA + (16 * g + 4 * wave) * RS), 16, doff,
-                                               0, 0, 0);
-      uint32_t xoff;
-      if constexpr (KS1) {
-        xoff = pv ? (uint32_t)(((int64_t)pix * a.C + cb * BN + chk[g] * 8) * 2) : kOOB;
-      } else {
-        const int n = pix / ohw, rem = pix - n * ohw, oh = rem / a.OW, ow = rem - oh * a.OW;
-        const int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
-        const bool v = pv & ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
-        xoff = v ? (uint32_t)(((((int64_t)n * a.H + ih) * a.W + iw) * a.C + cb * BN + chk[g] * 8) * 2) : kOOB;
-      }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void_t*)(sB + (16 * g + 4 * wave) * RS), 16, xoff,
-                                               0, 0, 0);
-    }
-  };
-
-  f32x4_t acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int k = 0; k < kNS - 1; ++k) issue(k, k);
-  for (int k = 0; k < nsteps; ++k) {
-    // step k's 4 DMAs landed; those of the kNS-2 later steps may stay in flight
-    __builtin_amdgcn_s_waitcnt(vmcnt_imm_w(4 * (kNS - 2)));
-    __builtin_amdgcn_s_barrier();  // every lane's step-k DMA landed; stage (k-1) % kNS read by all
-    issue(k + kNS - 1, (k + kNS - 1) % kNS);
-    const lds_char* sA = (const lds_char*)smem + (k % kNS) * STAGE;
-    const lds_char* sB = sA + A_BYTES;
-    bf16x8_t af[TM], bf[TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) af[i] = tr_operand<RS>(sA, wm * 64 + i * 16, lane);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) bf[j] = tr_operand<RS>(sB, wn * 64 + j * 16, lane);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_waitcnt(kLgkm0w);  // this wave's reads of stage k retired before the next barrier
-  }
-  __builtin_amdgcn_s_waitcnt(vmcnt_imm_w(0));  // trailing dummy DMAs
-
-  const int fr = lane & 15, fk = lane >> 4;
-  const int col0 = tap * a.C + cb * BN + wn * 64;
-  if (a.splits == 1) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int co = m0 + wm * 64 + i * 16 + fk * 4 + e;
-          a.dw[(int64_t)co * a.Ktot + col0 + j * 16 + fr] = f2bf(acc[i][j][e]);
-        }
-    return;
-  }
-  float* out = a.ws + (int64_t)split * a.Cout * a.Ktot;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int co = m0 + wm * 64 + i * 16 + fk * 4 + e;
-        out[(int64_t)co * a.Ktot + col0 + j * 16 + fr] = acc[i][j][e];
-      }
-}
-
 template <int BM, int BN>
 hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((wgrad_kernel<BM, BN>), dim3(a.Ktot / BN, a.Cout / BM, a.splits), dim3(kThreads),
@@ -546,15 +422,6 @@ hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s) {
 }  // namespace
 
 namespace {
-int g_wgrad_glds = -1;  // VGPU_CONV_WGRAD_GLDS=1: the LDS-DMA 128x128 kernel (A/B; default off)
-bool wgrad_glds_on() {
-  if (g_wgrad_glds < 0) {
-    const char* v = getenv("VGPU_CONV_WGRAD_GLDS");
-    g_wgrad_glds = (v && v[0] == '1') ? 1 : 0;
-  }
-  return g_wgrad_glds == 1;
-}
-
 int g_wgrad3 = -1;  // VGPU_CONV_WGRAD3=0 disables the tap-fused 3x3 path (A/B)
 // The tap-fused 3x3 kernel wins on long pixel reductions (ResNet stage 1:
 // 44.6-47.4 us vs 55.8-57.7 per tap); from stage 2 on the per-tap GEMMs on the
@@ -651,14 +518,7 @@ VGPU_API int vgpu_conv_wgrad_nhwc(const void* dy, const void* x, void* dw, void*
   } else {
     const int64_t steps_total = (P + KP - 1) / KP;
     a.steps = (int)((steps_total + a.splits - 1) / a.splits);
-    if (bm == 128 && bn == 128 && wgrad_glds_on()) {
-      const dim3 grid(a.Ktot / 128, a.Cout / 128, a.splits);
-      if (KS == 1 && stride == 1 && pad == 0)
-        hipLaunchKernelGGL((wgrad_glds_kernel<true>), grid, dim3(kThreads), 0, s, a);
-      else
-        hipLaunchKernelGGL((wgrad_glds_kernel<false>), grid, dim3(kThreads), 0, s, a);
-      e = hipGetLastError();
-    } else if (bm == 128 && bn == 128) e = launch_wgrad<128, 128>(a, s);
+    if (bm == 128 && bn == 128) e = launch_wgrad<128, 128>(a, s);
     else if (bm == 128) e = launch_wgrad<128, 64>(a, s);
     else if (bn == 128) e = launch_wgrad<64, 128>(a, s);
     else e = launch_wgrad<64, 64>(a, s);
@@ -673,4 +533,3 @@ VGPU_API int vgpu_conv_wgrad_nhwc(const void* dy, const void* x, void* dw, void*
   return (int)hipGetLastError();
 }
 
-VGPU_API void vgpu_conv_wgrad_set_glds(int on) { g_wgrad_glds = on < 0 ? -1 : (on ? 1 : 0); }  // -1: env

@@ -4,7 +4,7 @@ chip x rows in flight per thread, on every BatchNorm shape of a ResNet-V2-50
 training step (ai-benchmark 1.2: b=20, 346²).  Forward (reduce + finalize +
 apply) and backward (reduce + finalize + apply) per layer, interleaved.
 
-    python -m vgpu.bench.bnab [--batch 20 --size 346] [--variants 1024x4,512x8,2048x4,1024x8]
+    python scripts/bnab.py [--batch 20 --size 346] [--variants 1024x4,512x8,2048x4,1024x8]
 
 One JSON line per shape plus totals.  Every variant's outputs are compared with
 the first's (the reduction order changes, so up to bf16 rounding).
@@ -17,6 +17,12 @@ training path takes its BatchNorm statistics from the conv epilogues
 apply.
 """
 from __future__ import annotations
+
+import os as _os
+import sys as _sys
+
+_here = _os.path.dirname(_os.path.abspath(__file__))
+_sys.path[:0] = [_here, _os.path.dirname(_here)]  # scripts/ and the repo root
 
 import argparse
 import json

@@ -1,7 +1,7 @@
 """In-process A/B of two builds of the native convolution (box-to-box variance
 is ±10 % per layer, so kernel changes are judged in one process).
 
-    python -m vgpu.bench.convab --other vgpu/_lib/libvgpu_conv_ab.so [--batch 50 --size 346]
+    python scripts/convab.py --other vgpu/_lib/libvgpu_conv_ab.so [--batch 50 --size 346]
 
 `--other` is a shared library exporting the same `vgpu_conv2d_nhwc` /
 `vgpu_conv23_nhwc` ABI (e.g. the previous commit's conv_gemm.hip built alone);
@@ -11,11 +11,17 @@ line per layer reports both times.
 """
 from __future__ import annotations
 
+import os as _os
+import sys as _sys
+
+_here = _os.path.dirname(_os.path.abspath(__file__))
+_sys.path[:0] = [_here, _os.path.dirname(_here)]  # scripts/ and the repo root
+
 import argparse
 import ctypes
 import json
 
-from vgpu.bench.convnative import layer_shapes
+from convnative import layer_shapes  # noqa: E402
 
 
 def main(argv=None) -> int:

@@ -1,8 +1,14 @@
 """Micro-benchmark of ResNet-V2-50 layer shapes (b=50, 346²) on MI355X:
 MIOpen conv (channels_last) vs GEMM formulations, and elementwise passes.
-Prints one JSON line per case.  python -m vgpu.bench.convbench
+Prints one JSON line per case.  python scripts/convbench.py
 """
 from __future__ import annotations
+
+import os as _os
+import sys as _sys
+
+_here = _os.path.dirname(_os.path.abspath(__file__))
+_sys.path[:0] = [_here, _os.path.dirname(_here)]  # scripts/ and the repo root
 
 import json
 import sys

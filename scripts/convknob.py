@@ -2,7 +2,7 @@
 (box-to-box variance is ±10 % per kernel, so variants are compared in one
 process, interleaved).
 
-    python -m vgpu.bench.convknob [--knob halo] [--batch 50 --size 346] [--extra]
+    python scripts/convknob.py [--knob halo] [--batch 50 --size 346] [--extra]
 
 --knob halo: 3x3 / stride-1 layers with the halo-tile kernel off (LDS-DMA
 per-tap gathers), on (heuristic tile) and forced to 256- / 128-row tiles
@@ -12,16 +12,20 @@ One JSON line per layer: µs and TFLOP/s per variant.
 """
 from __future__ import annotations
 
+import os as _os
+import sys as _sys
+
+_here = _os.path.dirname(_os.path.abspath(__file__))
+_sys.path[:0] = [_here, _os.path.dirname(_here)]  # scripts/ and the repo root
+
 import argparse
 import json
 
-from vgpu.bench.convnative import layer_shapes
+from convnative import layer_shapes  # noqa: E402
 
 KNOBS = {
     # name: (setter, [(tag, value)])
     "halo": ("vgpu_conv_set_halo", [("off", 0), ("auto", -1), ("bm256", 2), ("bm128", 3)]),
-    # the halo kernel's MFMA shape (auto tile choice): 16x16x32 vs 32x32x16
-    "m32": ("vgpu_conv_set_halo_m32", [("m16", 0), ("m32", 1)]),
 }
 
 

@@ -1,13 +1,19 @@
 """Per-layer timing of the MFMA implicit-GEMM convolution against MIOpen on the
 ResNet-V2-50 layer shapes of ai-benchmark test 1.1 (b=50, 346²).
 
-    python -m vgpu.bench.convnative [--batch 50 --size 346 --iters 20]
+    python scripts/convnative.py [--batch 50 --size 346 --iters 20]
 
 Prints one JSON line per layer: native µs (with its fused prologue/epilogue),
 MIOpen µs (bare convolution after find), TFLOP/s, and the native kernel's
 effective HBM bandwidth (compulsory bytes / time).
 """
 from __future__ import annotations
+
+import os as _os
+import sys as _sys
+
+_here = _os.path.dirname(_os.path.abspath(__file__))
+_sys.path[:0] = [_here, _os.path.dirname(_here)]  # scripts/ and the repo root
 
 import argparse
 import json

@@ -2,7 +2,7 @@
 (ai-benchmark test 1.2: b=20, 346²): MIOpen forward / backward-data /
 backward-weight against the native candidates.
 
-    python -m vgpu.bench.convtrain [--batch 20 --size 346 --iters 20]
+    python scripts/convtrain.py [--batch 20 --size 346 --iters 20]
 
 Native candidates per layer (stride-1 only for the data gradient):
   fwd    native MFMA implicit GEMM (vgpu.ops.conv.conv2d)
@@ -14,10 +14,16 @@ One JSON line per layer plus a total line.
 """
 from __future__ import annotations
 
+import os as _os
+import sys as _sys
+
+_here = _os.path.dirname(_os.path.abspath(__file__))
+_sys.path[:0] = [_here, _os.path.dirname(_here)]  # scripts/ and the repo root
+
 import argparse
 import json
 
-from vgpu.bench.convnative import layer_shapes
+from convnative import layer_shapes  # noqa: E402
 
 
 def main(argv=None) -> int:

@@ -39,11 +39,11 @@ for s in "${STAGES[@]}"; do
     bench) step bench 900 python bench.py || exit 1
            grep '^{' "$OUT/bench.log" | tail -1 > "$OUT/bench.json" ;;
     excl)  step bench_excl 600 python bench.py --pods 1 --gpucores 100 --gpumem 0 --no-cap-probe || exit 1 ;;
-    conv)  step convnative 600 python -m vgpu.bench.convnative || exit 1 ;;
+    conv)  step convnative 600 python scripts/convnative.py || exit 1 ;;
     prof)  step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_native/%pid%" -o run -- python3 bench.py --steps 20 --warmup 5 --no-cap-probe || exit 1 ;;
     shim) step pytest_shim 900 python -u -m pytest tests/test_gpu_shim.py -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider
           rc=$?; ok_or_testfail $rc || exit $rc ;;
-    halo) step convknob_halo 300 python -m vgpu.bench.convknob --knob halo --extra || exit 1 ;;
+    halo) step convknob_halo 300 python scripts/convknob.py --knob halo --extra || exit 1 ;;
     pmc)  step pmc 900 bash scripts/pmc_flagship.sh || exit 1
           step pmc_summary 60 python scripts/pmc_summary.py gpurun_out/pmc_flagship --last 88 || exit 1 ;;
     suite) step suite 2400 python -u -m vgpu.bench.suite --scenarios "${SCEN:-exclusive,vgpu,vgpu-cu25}" \

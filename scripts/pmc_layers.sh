@@ -12,7 +12,7 @@ for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VA
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   echo "=== pass $i: $grp"
-  timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 -m vgpu.bench.convnative --only "$L" --no-miopen --iters 3 > $OUT/p$i.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 scripts/convnative.py --only "$L" --no-miopen --iters 3 > $OUT/p$i.log 2>&1
   rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/p$i.log; exit $rc; }
 done
 exit 0

@@ -98,9 +98,8 @@ HALO_CASES = [
 ]
 
 
-@pytest.mark.parametrize("m32", [0, 1], ids=["mfma16", "mfma32"])
 @pytest.mark.parametrize("case", HALO_CASES, ids=lambda c: "x".join(map(str, c[:5])) + f"-t{c[7]}")
-def test_conv_halo_matches_fp32(C, case, m32):
+def test_conv_halo_matches_fp32(C, case):
     from vgpu.native import load_kernels
     n, c, h, w, cout, has_bias, act, tile = case
     x = _t((n, c, h, w), 41)
@@ -108,21 +107,18 @@ def test_conv_halo_matches_fp32(C, case, m32):
     bias = _f((cout,), 43) if has_bias else None
     lib = load_kernels()
     lib.vgpu_conv_set_halo(tile)
-    lib.vgpu_conv_set_halo_m32(m32)
     before = lib.vgpu_conv_halo_launches()
     try:
         got = C.conv2d(x, wt, bias, stride=1, padding=1, act=act)
     finally:
         lib.vgpu_conv_set_halo(-1)
-        lib.vgpu_conv_set_halo_m32(-1)
     assert lib.vgpu_conv_halo_launches() == before + 1, "the halo kernel did not run"  # no silent fallback
     ref = C.conv2d_ref(x, wt, bias, stride=1, padding=1, act=act)
     torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("m32", [0, 1], ids=["mfma16", "mfma32"])
 @pytest.mark.parametrize("tile", [2, 3])
-def test_conv_halo_integer_exact(C, tile, m32):
+def test_conv_halo_integer_exact(C, tile):
     """Integer data through the halo kernel: any tap / row / slot mix-up is visible."""
     from vgpu.native import load_kernels
     g = torch.Generator(device="cpu").manual_seed(tile)
@@ -130,13 +126,11 @@ def test_conv_halo_integer_exact(C, tile, m32):
     wt = torch.randint(-2, 3, (256, 128, 3, 3), generator=g).to(torch.bfloat16).cuda().contiguous(memory_format=CL)
     lib = load_kernels()
     lib.vgpu_conv_set_halo(tile)
-    lib.vgpu_conv_set_halo_m32(m32)
     before = lib.vgpu_conv_halo_launches()
     try:
         got = C.conv2d(x, wt, stride=1, padding=1)
     finally:
         lib.vgpu_conv_set_halo(-1)
-        lib.vgpu_conv_set_halo_m32(-1)
     assert lib.vgpu_conv_halo_launches() == before + 1
     # fp32 sums of these integers are exact; the kernel rounds them once to bf16
     assert torch.equal(got.float(), C.conv2d_ref(x, wt, stride=1, padding=1).to(torch.bfloat16).float())
@@ -379,25 +373,18 @@ WGRAD_CASES = [
 ]
 
 
-@pytest.mark.parametrize("glds", [1, 0], ids=["glds", "regstaged"])
 @pytest.mark.parametrize("n,c,h,w,cout,ks,stride,pad", WGRAD_CASES)
-def test_conv_wgrad_matches_fp32(C, n, c, h, w, cout, ks, stride, pad, glds):
-    from vgpu.native import load_kernels
-    lib = load_kernels()
-    lib.vgpu_conv_wgrad_set_glds(glds)
-    try:
-        x = _t((n, c, h, w), 11)
-        oh, ow = C.out_hw(h, w, ks, stride, pad)
-        dy = _t((n, cout, oh, ow), 12)
-        dw = C.conv2d_wgrad(dy, x, ks, stride=stride, padding=pad)
-        assert dw.shape == (cout, c, ks, ks) and dw.is_contiguous(memory_format=CL)
-        ref = torch.nn.grad.conv2d_weight(x.float(), (cout, c, ks, ks), dy.float(), stride=stride, padding=pad)
-        scale = ref.abs().max().item()
-        torch.testing.assert_close(dw.float(), ref, atol=1e-2 * scale, rtol=1e-2)
-        # deterministic: split-K partials are reduced in a fixed order
-        assert torch.equal(dw, C.conv2d_wgrad(dy, x, ks, stride=stride, padding=pad))
-    finally:
-        lib.vgpu_conv_wgrad_set_glds(-1)
+def test_conv_wgrad_matches_fp32(C, n, c, h, w, cout, ks, stride, pad):
+    x = _t((n, c, h, w), 11)
+    oh, ow = C.out_hw(h, w, ks, stride, pad)
+    dy = _t((n, cout, oh, ow), 12)
+    dw = C.conv2d_wgrad(dy, x, ks, stride=stride, padding=pad)
+    assert dw.shape == (cout, c, ks, ks) and dw.is_contiguous(memory_format=CL)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (cout, c, ks, ks), dy.float(), stride=stride, padding=pad)
+    scale = ref.abs().max().item()
+    torch.testing.assert_close(dw.float(), ref, atol=1e-2 * scale, rtol=1e-2)
+    # deterministic: split-K partials are reduced in a fixed order
+    assert torch.equal(dw, C.conv2d_wgrad(dy, x, ks, stride=stride, padding=pad))
 
 
 def test_dgrad_filters_batched_flip_matches_torch(C):

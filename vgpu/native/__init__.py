@@ -65,7 +65,6 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_conv_set_big.argtypes = [ci]
     lib.vgpu_conv_set_halo.argtypes = [ci]
     lib.vgpu_conv_halo_launches.restype = ctypes.c_ulonglong
-    lib.vgpu_conv_set_halo_m32.argtypes = [ci]
     lib.vgpu_lstm_recurrence.argtypes = [vp, vp, vp, vp, ci, ci, ci, vp]
     lib.vgpu_lstm_recurrence.restype = ci
     lib.vgpu_lstm_forward_train.argtypes = [vp] * 5 + [ci, ci, ci, vp]
@@ -99,7 +98,6 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_conv_wgrad_workspace.restype = i64
     lib.vgpu_conv_wgrad_nhwc.argtypes = [vp] * 4 + [i64] + [ci] * 8 + [vp]
     lib.vgpu_conv_wgrad_nhwc.restype = ci
-    lib.vgpu_conv_wgrad_set_glds.argtypes = [ci]
     lib.vgpu_wt_flip_tiles.argtypes = [ci, ci, ci]
     lib.vgpu_wt_flip_tiles.restype = ci
     lib.vgpu_wt_flip_batched.argtypes = [vp, ci, ci, vp]
