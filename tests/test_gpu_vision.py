@@ -1,0 +1,70 @@
+"""Native training paths of the non-ResNet suite models against the fp32
+PyTorch modules: VGG-16's conv + bias + ReLU layers (vgpu.ops.conv.
+conv_bias_relu_train) and, per kernel, the fused op in both directions."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last
+
+
+def _x(shape, seed, scale=1.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(shape, generator=g) * scale).to(torch.bfloat16).cuda().contiguous(memory_format=CL)
+
+
+def _rel(a: torch.Tensor, b: torch.Tensor) -> float:
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+
+
+def test_conv_bias_relu_train_matches_fp32(gpu_build):
+    from vgpu.ops import conv as C
+    conv = torch.nn.Conv2d(128, 256, 3, padding=1).cuda().to(torch.bfloat16).to(memory_format=CL)
+    ref = copy.deepcopy(conv).float()
+    x = _x((2, 128, 20, 18), 1).requires_grad_(True)
+    xr = x.detach().float().requires_grad_(True)
+    calls = []
+    orig = C._ConvBiasReLUTrainFn.apply
+    C._ConvBiasReLUTrainFn.apply = lambda *a: (calls.append(1), orig(*a))[1]
+    try:
+        y = C.conv_bias_relu_train(x, conv)
+    finally:
+        C._ConvBiasReLUTrainFn.apply = orig
+    assert calls, "the native path did not run"
+    yr = torch.relu(ref(xr))
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
+    dy = _x(tuple(y.shape), 2)
+    y.backward(dy)
+    yr.backward(dy.float())
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(conv.weight.grad, ref.weight.grad) < 2e-2
+    assert _rel(conv.bias.grad, ref.bias.grad) < 2e-2
+
+
+def test_vgg16_native_training_step_matches_fp32(gpu_build):
+    from vgpu.models.vision import VGG16
+    from vgpu.ops import conv as C
+    torch.manual_seed(0)
+    m32 = VGG16(num_classes=10).cuda().to(memory_format=CL).train()
+    m = copy.deepcopy(m32).to(torch.bfloat16)
+    x = _x((2, 3, 64, 64), 3)
+    tgt = torch.tensor([1, 7], device="cuda")
+    calls = []
+    orig = C._ConvBiasReLUTrainFn.apply
+    C._ConvBiasReLUTrainFn.apply = lambda *a: (calls.append(1), orig(*a))[1]
+    try:
+        out = m(x)
+    finally:
+        C._ConvBiasReLUTrainFn.apply = orig
+    assert len(calls) == 12, "every C % 64 == 0 conv should run natively"  # 13 convs, the first has C = 3
+    out32 = m32(x.float())
+    assert _rel(out, out32) < 5e-2
+    torch.nn.functional.cross_entropy(out.float(), tgt).backward()
+    torch.nn.functional.cross_entropy(out32, tgt).backward()
+    convs = [i for i, mod in enumerate(m.features) if isinstance(mod, torch.nn.Conv2d)]
+    for i in convs[1:4] + convs[-2:]:
+        assert _rel(m.features[i].weight.grad, m32.features[i].weight.grad) < 6e-2, i
+        assert _rel(m.features[i].bias.grad, m32.features[i].bias.grad) < 6e-2, i

@@ -435,7 +435,13 @@ def vmemcopy(mib: int = 512) -> dict:
     # 2-D copies and memsets.  hipMemcpy2D host -> range
     # (4 KiB rows: the pattern survives, pitch = width), then hipMemset over
     # the first half of another range and the pattern refilled on the GPU.
-    hip = ctypes.CDLL("libamdhip64.so")
+    # The process-wide symbols, as an application's own calls resolve them (the
+    # shim's hooks first when it is preloaded): a handle on libamdhip64.so would
+    # call the runtime directly, and a memset the shim never sees races its pager
+    # (the runtime's memset of a managed range moved pages to host memory).
+    hip = ctypes.CDLL(None)
+    if not hasattr(hip, "hipMemset"):
+        hip = ctypes.CDLL("libamdhip64.so")
     dst3 = torch.empty(n, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
     w = 4096

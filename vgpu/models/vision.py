@@ -37,8 +37,39 @@ class VGG16(nn.Module):
             nn.Linear(4096, num_classes))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.pool(self.features(x))
+        if self.training and torch.is_grad_enabled() and x.is_cuda:
+            x = self._train_features(x)
+        else:
+            x = self.features(x)
+        if x.shape[-2:] != (7, 7):
+            x = self.pool(x)
         return self.classifier(torch.flatten(x, 1))
+
+    def _train_features(self, x: torch.Tensor) -> torch.Tensor:
+        """Training forward on the native kernels: each conv +
+        ReLU pair with C % 64 == 0 is one MFMA conv with bias + ReLU in its
+        epilogue and native data / weight gradients (vgpu.ops.conv.
+        conv_bias_relu_train), max pools keep a one-byte argmax for a gather
+        backward, and every stride-1 data-gradient filter is rebuilt by one
+        batched launch per step.  Other shapes (the 3-channel first conv) run
+        through the modules."""
+        from vgpu.ops.conv import DgradFilters, conv_bias_relu_train, maxpool_train, native_train_enabled
+        if native_train_enabled():
+            if getattr(self, "_dgrad", None) is None:
+                self._dgrad = DgradFilters([m for m in self.features if isinstance(m, nn.Conv2d)])
+            self._dgrad.refresh()
+        x = x.contiguous(memory_format=torch.channels_last)
+        mods = list(self.features)
+        i = 0
+        while i < len(mods):
+            m = mods[i]
+            if isinstance(m, nn.Conv2d) and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU):
+                x = conv_bias_relu_train(x, m).contiguous(memory_format=torch.channels_last)
+                i += 2
+                continue
+            x = maxpool_train(x, m) if isinstance(m, nn.MaxPool2d) else m(x)
+            i += 1
+        return x
 
 
 class NativeVGG16Inference(nn.Module):

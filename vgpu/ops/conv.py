@@ -490,6 +490,44 @@ def conv_train(x: torch.Tensor, conv: torch.nn.Conv2d, residual: torch.Tensor | 
     return _ConvTrainFn.apply(x, conv.weight, residual, conv.stride[0], conv.padding[0])
 
 
+class _ConvBiasReLUTrainFn(torch.autograd.Function):
+    """y = relu(conv(x, w) + b) in one MFMA kernel pass (bias + ReLU in the
+    epilogue).  Backward: g = dy masked by y > 0 (one threshold pass), db =
+    Σ g in fp32, then dx / dw exactly as _ConvTrainFn (conv_backward).  The
+    VGG-16 training path (vgpu.models.vision.VGG16)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride: int, padding: int):
+        y = conv2d(x, w, b, stride=stride, padding=padding, act="relu")
+        ctx.save_for_backward(x, w, y)
+        ctx.stride, ctx.padding = stride, padding
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        g = torch.ops.aten.threshold_backward(dy.contiguous(memory_format=_CL), y, 0)
+        db = torch.sum(g, dim=(0, 2, 3), dtype=torch.float32) if ctx.needs_input_grad[2] else None
+        dx, dw = conv_backward(g, x, w, ctx.stride, ctx.padding, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        return dx, dw, db, None, None
+
+
+def conv_bias_relu_train(x: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor:
+    """relu(conv(x)) with the module's semantics (bias included); bf16
+    channels_last CUDA tensors of supported shapes run natively, anything else
+    through the module."""
+    w = conv.weight
+    ok = (_TRAIN_NATIVE and conv.bias is not None and x.is_cuda and x.dtype == torch.bfloat16
+          and w.dtype == torch.bfloat16 and x.dim() == 4 and x.is_contiguous(memory_format=_CL)
+          and w.is_contiguous(memory_format=_CL) and conv.groups == 1 and conv.dilation == (1, 1)
+          and conv.kernel_size[0] == conv.kernel_size[1] and conv.stride[0] == conv.stride[1]
+          and conv.padding[0] == conv.padding[1] and isinstance(conv.padding[0], int)
+          and conv.kernel_size[0] in (1, 3) and supported(conv.in_channels, conv.out_channels, conv.kernel_size[0]))
+    if not ok:
+        return F.relu(conv(x))
+    return _ConvBiasReLUTrainFn.apply(x, w, conv.bias.float(), conv.stride[0], conv.padding[0])
+
+
 # ---- fp32 references -----------------------------------------------------------------
 def conv2d_ref(x, w, bias=None, *, stride=1, padding=0, act="none", pro=None, residual=None):
     xf = x.float()
