@@ -32,6 +32,7 @@
 #include <set>
 #include <mutex>
 #include <string>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <thread>
 #include <vector>
@@ -712,9 +713,40 @@ static bool device_mem_locked(const void* p) {
 // A host<->device copy moves every managed page it touches to system memory
 // (KFD); device-to-device copies (explicit, or Default between device
 // memory) move nothing.
+// VMM (hipMemAddressReserve / hipMemMap): reserved ranges are PROT_NONE
+// anonymous memory, a mapping makes them read/write zero pages (the handle's
+// contents do not survive an unmap: tests only map fresh handles), and copies
+// between a mapped range and fake host memory (addresses with no storage)
+// keep the bytes in g_host_data, so data that goes out and comes back can be
+// checked.
+static std::map<uintptr_t, size_t> g_vmm_mapped;
+static std::map<uintptr_t, std::vector<char>> g_host_data;  // fake host address -> bytes copied there
+static bool vmm_mapped_locked(const void* p, size_t n) {
+  auto it = g_vmm_mapped.upper_bound((uintptr_t)p);
+  return it != g_vmm_mapped.begin() && (uintptr_t)p + n <= std::prev(it)->first + std::prev(it)->second;
+}
+static bool vmm_copy_locked(void* dst, const void* src, size_t n) {
+  const bool din = vmm_mapped_locked(dst, n), sin = vmm_mapped_locked(src, n);
+  if (!din && !sin) return false;
+  if (din && sin) {
+    memmove(dst, src, n);
+  } else if (sin) {  // range -> host: keep the bytes under the host address
+    std::vector<char> v((const char*)src, (const char*)src + n);
+    g_host_data[(uintptr_t)dst] = std::move(v);
+  } else {  // host -> range: from bytes stored at (or inside) a host copy
+    auto it = g_host_data.upper_bound((uintptr_t)src);
+    if (it != g_host_data.begin()) {
+      --it;
+      const size_t off = (uintptr_t)src - it->first;
+      if (off + n <= it->second.size()) memcpy(dst, it->second.data() + off, n);
+    }
+  }
+  return true;
+}
 static hipError_t fake_copy(void* dst, const void* src, size_t n, hipMemcpyKind kind) {
   if (kind == hipMemcpyDeviceToDevice) return hipSuccess;
   std::lock_guard<std::mutex> g(g_mu);
+  if (vmm_copy_locked(dst, src, n)) return hipSuccess;
   if (kind == hipMemcpyDefault && device_mem_locked(dst) && device_mem_locked(src)) return hipSuccess;
   host_copy_touch_locked(dst, n);
   host_copy_touch_locked(src, n);
@@ -843,7 +875,11 @@ static hipError_t host_alloc(void** p, size_t size) {
   return hipSuccess;
 }
 hipError_t hipHostMalloc(void** p, size_t size, unsigned int) { return host_alloc(p, size); }
-hipError_t hipHostFree(void*) { return hipSuccess; }
+hipError_t hipHostFree(void* p) {
+  std::lock_guard<std::mutex> g(g_mu);
+  g_host_data.erase((uintptr_t)p);
+  return hipSuccess;
+}
 // Not via hipHostMalloc: a preloaded interposer would see that call too.
 hipError_t hipMallocHost(void** p, size_t size) { return host_alloc(p, size); }
 hipError_t hipHostAlloc(void** p, size_t size, unsigned int) { return host_alloc(p, size); }
@@ -856,6 +892,32 @@ hipError_t hipMemCreate(hipMemGenericAllocationHandle_t* h, size_t size,
   return rc;
 }
 hipError_t hipMemRelease(hipMemGenericAllocationHandle_t h) { return dev_free((void*)h); }
+hipError_t hipMemGetAllocationGranularity(size_t* g, const hipMemAllocationProp*, hipMemAllocationGranularity_flags) {
+  *g = 4096;
+  return hipSuccess;
+}
+hipError_t hipMemAddressReserve(void** p, size_t size, size_t, void*, unsigned long long) {
+  void* a = mmap(nullptr, size, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  if (a == MAP_FAILED) return hipErrorOutOfMemory;
+  *p = a;
+  return hipSuccess;
+}
+hipError_t hipMemAddressFree(void* p, size_t size) { return munmap(p, size) == 0 ? hipSuccess : hipErrorInvalidValue; }
+hipError_t hipMemMap(void* p, size_t size, size_t, hipMemGenericAllocationHandle_t, unsigned long long) {
+  if (mmap(p, size, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_FIXED, -1, 0) == MAP_FAILED)
+    return hipErrorInvalidValue;
+  std::lock_guard<std::mutex> g(g_mu);
+  g_vmm_mapped[(uintptr_t)p] = size;
+  return hipSuccess;
+}
+hipError_t hipMemUnmap(void* p, size_t size) {
+  std::lock_guard<std::mutex> g(g_mu);
+  g_vmm_mapped.erase((uintptr_t)p);
+  // back to an inaccessible reservation: the contents are gone
+  mmap(p, size, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_FIXED | MAP_NORESERVE, -1, 0);
+  return hipSuccess;
+}
+hipError_t hipMemSetAccess(void*, size_t, const hipMemAccessDesc*, size_t) { return hipSuccess; }
 
 hipError_t hipMemGetInfo(size_t* f, size_t* t) {
   std::lock_guard<std::mutex> g(g_mu);

@@ -183,6 +183,13 @@ __attribute__((visibility("default"))) void vgpu_self_vmem_stats(uint64_t out[5]
   vmem_stats(&out[0], &out[1], &out[2], &out[3], &out[4]);
 }
 
+// VMM suspend vehicle (vmm.cpp): ranges, bytes, evicted bytes, last suspend /
+// resume ns, completed suspend-resume cycles.
+__attribute__((visibility("default"))) void vgpu_self_vmm_stats(uint64_t out[6]) {
+  ensure_init();
+  vmm_stats(out);
+}
+
 __attribute__((visibility("default"))) void vgpu_self_vmem_budget(int dev, uint64_t out[8]) {
   ensure_init();
   vmem_budget_books(dev, out);

@@ -269,6 +269,7 @@ __attribute__((visibility("default"))) hipError_t hipIpcGetMemHandle(hipIpcMemHa
               dev_ptr);
     return hipErrorNotSupported;
   }
+  vmm_ipc_exported(dev_ptr);
   return REAL_HIP(hipIpcGetMemHandle)(handle, dev_ptr);
 }
 

@@ -136,6 +136,17 @@ hipError_t charged_alloc(void** ptr, size_t size, int kind, F&& real_alloc, bool
   suspend_gate();
   int dev = cur_dev();
   charge_context(dev);
+  if (kind == kDeviceBuf && managed_ok && vmm_wanted(dev, size)) {
+    // Suspend with eviction, no oversubscription: a VMM mapping the evict
+    // thread can copy out and unmap (vmm.cpp); plain memory if VMM fails.
+    if (!mem_reserve(dev, size, kind)) return hipErrorOutOfMemory;
+    if (vmm_alloc(ptr, size, dev) == hipSuccess) {
+      ledger_add(*ptr, size, dev, kind);
+      return hipSuccess;
+    }
+    (void)REAL_HIP(hipGetLastError)();
+    mem_unreserve(dev, size, kind);
+  }
   if (kind == kDeviceBuf && managed_ok && vmem_wants_managed(dev, size)) {
     // Virtual device memory with a physical budget: a managed range from the
     // start, resident while the pod's budget has room (vmem.cpp).
@@ -535,6 +546,7 @@ __attribute__((visibility("default"))) hipError_t hipMallocManaged(void** ptr, s
 // as it does from a kernel launch.  Peer copies carry no compute charge.
 __attribute__((visibility("default"))) hipError_t hipMemcpyPeer(void* dst, int dst_dev, const void* src, int src_dev,
                                                                 size_t n) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   if (st().enabled) {
     vmem_note_use(dst, nullptr);
@@ -546,6 +558,7 @@ __attribute__((visibility("default"))) hipError_t hipMemcpyPeer(void* dst, int d
 
 __attribute__((visibility("default"))) hipError_t hipMemcpyPeerAsync(void* dst, int dst_dev, const void* src,
                                                                      int src_dev, size_t n, hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   if (st().enabled) {
     vmem_note_use(dst, stream);
@@ -613,6 +626,7 @@ __attribute__((visibility("default"))) hipError_t hipMallocPitch(void** ptr, siz
 // ---- host copies (staged or repaired; see copy_sync / copy_async above) ----------
 __attribute__((visibility("default"))) hipError_t hipMemcpy(void* dst, const void* src, size_t n,
                                                             hipMemcpyKind kind) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   return copy_sync(dst, src, n, kind, nullptr, [](void* d, const void* s, size_t c, hipMemcpyKind k, hipStream_t) {
     return REAL_HIP(hipMemcpy)(d, s, c, k);
   });
@@ -620,12 +634,14 @@ __attribute__((visibility("default"))) hipError_t hipMemcpy(void* dst, const voi
 
 __attribute__((visibility("default"))) hipError_t hipMemcpyWithStream(void* dst, const void* src, size_t n,
                                                                       hipMemcpyKind kind, hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   return copy_sync(dst, src, n, kind, stream, [](void* d, const void* s, size_t c, hipMemcpyKind k, hipStream_t t) {
     return REAL_HIP(hipMemcpyWithStream)(d, s, c, k, t);
   });
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemcpyHtoD(hipDeviceptr_t dst, const void* src, size_t n) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   return copy_sync(dst, src, n, hipMemcpyHostToDevice, nullptr,
                    [](void* d, const void* s, size_t c, hipMemcpyKind, hipStream_t) {
                      return REAL_HIP(hipMemcpyHtoD)(d, s, c);
@@ -633,6 +649,7 @@ __attribute__((visibility("default"))) hipError_t hipMemcpyHtoD(hipDeviceptr_t d
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemcpyDtoH(void* dst, hipDeviceptr_t src, size_t n) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   return copy_sync(dst, src, n, hipMemcpyDeviceToHost, nullptr,
                    [](void* d, const void* s, size_t c, hipMemcpyKind, hipStream_t) {
                      return REAL_HIP(hipMemcpyDtoH)(d, (hipDeviceptr_t)s, c);
@@ -641,16 +658,19 @@ __attribute__((visibility("default"))) hipError_t hipMemcpyDtoH(void* dst, hipDe
 
 __attribute__((visibility("default"))) hipError_t hipMemcpyAsync(void* dst, const void* src, size_t n,
                                                                  hipMemcpyKind kind, hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   return copy_async(dst, src, n, kind, stream);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemcpyHtoDAsync(hipDeviceptr_t dst, const void* src, size_t n,
                                                                      hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   return copy_async(dst, src, n, hipMemcpyHostToDevice, stream);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemcpyDtoHAsync(void* dst, hipDeviceptr_t src, size_t n,
                                                                      hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   return copy_async(dst, src, n, hipMemcpyDeviceToHost, stream);
 }
 
@@ -658,6 +678,7 @@ __attribute__((visibility("default"))) hipError_t hipMemcpyDtoHAsync(void* dst, 
 __attribute__((visibility("default"))) hipError_t hipMemcpy2D(void* dst, size_t dpitch, const void* src,
                                                               size_t spitch, size_t width, size_t height,
                                                               hipMemcpyKind kind) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   hipError_t rc;
   if (staged_copy2d(dst, dpitch, src, spitch, width, height, kind, nullptr, &rc)) {
@@ -671,6 +692,7 @@ __attribute__((visibility("default"))) hipError_t hipMemcpy2D(void* dst, size_t 
 __attribute__((visibility("default"))) hipError_t hipMemcpy2DAsync(void* dst, size_t dpitch, const void* src,
                                                                    size_t spitch, size_t width, size_t height,
                                                                    hipMemcpyKind kind, hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   hipError_t rc;
   if (staged_copy2d(dst, dpitch, src, spitch, width, height, kind, stream, &rc)) return rc;
@@ -680,17 +702,20 @@ __attribute__((visibility("default"))) hipError_t hipMemcpy2DAsync(void* dst, si
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemcpy3D(const hipMemcpy3DParms* p) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   return after3d(REAL_HIP(hipMemcpy3D)(p), p, nullptr, false);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemcpy3DAsync(const hipMemcpy3DParms* p, hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   return after3d(REAL_HIP(hipMemcpy3DAsync)(p, stream), p, stream, true);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemcpyToSymbol(const void* symbol, const void* src, size_t n,
                                                                     size_t offset, hipMemcpyKind kind) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   return after_sync_copy(REAL_HIP(hipMemcpyToSymbol)(symbol, src, n, offset, kind), nullptr, src, n, kind);
 }
@@ -698,6 +723,7 @@ __attribute__((visibility("default"))) hipError_t hipMemcpyToSymbol(const void* 
 __attribute__((visibility("default"))) hipError_t hipMemcpyToSymbolAsync(const void* symbol, const void* src,
                                                                          size_t n, size_t offset, hipMemcpyKind kind,
                                                                          hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   return after_async_copy(REAL_HIP(hipMemcpyToSymbolAsync)(symbol, src, n, offset, kind, stream), nullptr, src, n,
                           kind, stream);
@@ -705,6 +731,7 @@ __attribute__((visibility("default"))) hipError_t hipMemcpyToSymbolAsync(const v
 
 __attribute__((visibility("default"))) hipError_t hipMemcpyFromSymbol(void* dst, const void* symbol, size_t n,
                                                                       size_t offset, hipMemcpyKind kind) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   return after_sync_copy(REAL_HIP(hipMemcpyFromSymbol)(dst, symbol, n, offset, kind), dst, nullptr, n, kind);
 }
@@ -712,62 +739,73 @@ __attribute__((visibility("default"))) hipError_t hipMemcpyFromSymbol(void* dst,
 __attribute__((visibility("default"))) hipError_t hipMemcpyFromSymbolAsync(void* dst, const void* symbol, size_t n,
                                                                            size_t offset, hipMemcpyKind kind,
                                                                            hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   return after_async_copy(REAL_HIP(hipMemcpyFromSymbolAsync)(dst, symbol, n, offset, kind, stream), dst, nullptr, n,
                           kind, stream);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemset(void* dst, int value, size_t n) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   return after_memset(REAL_HIP(hipMemset)(dst, value, n), dst, n);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemsetAsync(void* dst, int value, size_t n, hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   return after_memset_async(REAL_HIP(hipMemsetAsync)(dst, value, n, stream), dst, n, stream);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemsetD8(hipDeviceptr_t dst, unsigned char v, size_t n) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   return after_memset(REAL_HIP(hipMemsetD8)(dst, v, n), dst, n);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemsetD8Async(hipDeviceptr_t dst, unsigned char v, size_t n,
                                                                    hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   return after_memset_async(REAL_HIP(hipMemsetD8Async)(dst, v, n, stream), dst, n, stream);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemsetD16(hipDeviceptr_t dst, unsigned short v, size_t n) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   return after_memset(REAL_HIP(hipMemsetD16)(dst, v, n), dst, 2 * n);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemsetD16Async(hipDeviceptr_t dst, unsigned short v, size_t n,
                                                                     hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   return after_memset_async(REAL_HIP(hipMemsetD16Async)(dst, v, n, stream), dst, 2 * n, stream);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemsetD32(hipDeviceptr_t dst, int v, size_t n) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   return after_memset(REAL_HIP(hipMemsetD32)(dst, v, n), dst, 4 * n);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemsetD32Async(hipDeviceptr_t dst, int v, size_t n,
                                                                     hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   return after_memset_async(REAL_HIP(hipMemsetD32Async)(dst, v, n, stream), dst, 4 * n, stream);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemset2D(void* dst, size_t pitch, int v, size_t width,
                                                               size_t height) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   return after_memset(REAL_HIP(hipMemset2D)(dst, pitch, v, width, height), dst, span2d(pitch, width, height));
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemset2DAsync(void* dst, size_t pitch, int v, size_t width,
                                                                    size_t height, hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   return after_memset_async(REAL_HIP(hipMemset2DAsync)(dst, pitch, v, width, height, stream), dst,
                             span2d(pitch, width, height), stream);
@@ -784,6 +822,7 @@ __attribute__((visibility("default"))) hipError_t hipFree(void* ptr) {
   ensure_init();
   Alloc a;
   if (uncharge(ptr, &a) && a.kind == kHostSpill) return free_spilled(ptr);
+  if (vmm_free(ptr)) return hipSuccess;
   return REAL_HIP(hipFree)(ptr);
 }
 
@@ -794,6 +833,11 @@ __attribute__((visibility("default"))) hipError_t hipFreeAsync(void* ptr, hipStr
   if (uncharge(ptr, &a) && a.kind == kHostSpill) {
     (void)REAL_HIP(hipStreamSynchronize)(stream);
     return free_spilled(ptr);
+  }
+  if (vmm_owns(ptr)) {
+    (void)REAL_HIP(hipStreamSynchronize)(stream);
+    (void)vmm_free(ptr);
+    return hipSuccess;
   }
   return REAL_HIP(hipFreeAsync)(ptr, stream);
 }
@@ -888,6 +932,7 @@ __attribute__((visibility("default"))) hipError_t hipDeviceGetAttribute(int* pi,
 __attribute__((visibility("default"))) hipError_t hipLaunchKernel(const void* f, dim3 grid, dim3 block,
                                                                   void** args, size_t shmem,
                                                                   hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   const int dev = launch_dev(stream);
   const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
@@ -902,6 +947,7 @@ __attribute__((visibility("default"))) hipError_t hipExtLaunchKernel(const void*
                                                                      size_t shmem, hipStream_t stream,
                                                                      hipEvent_t start, hipEvent_t stop,
                                                                      int flags) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   const int dev = launch_dev(stream);
   const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
@@ -915,6 +961,7 @@ __attribute__((visibility("default"))) hipError_t hipModuleLaunchKernel(
     hipFunction_t f, unsigned int gx, unsigned int gy, unsigned int gz, unsigned int bx,
     unsigned int by, unsigned int bz, unsigned int shmem, hipStream_t stream, void** params,
     void** extra) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   const int dev = launch_dev(stream);
   const bool track = limiter_on_launch(dev, blocks3(gx, gy, gz));
@@ -929,6 +976,7 @@ __attribute__((visibility("default"))) hipError_t hipExtModuleLaunchKernel(
     hipFunction_t f, uint32_t gwx, uint32_t gwy, uint32_t gwz, uint32_t lwx, uint32_t lwy,
     uint32_t lwz, size_t shmem, hipStream_t stream, void** params, void** extra, hipEvent_t start,
     hipEvent_t stop, uint32_t flags) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   // Global work size is in work-items here.
   auto nb = [](uint32_t g, uint32_t l) { return l ? (g + l - 1) / l : g; };
@@ -971,6 +1019,7 @@ __attribute__((visibility("default"))) hipError_t hipLaunchCooperativeKernel(con
                                                                              dim3 block, void** params,
                                                                              unsigned int shmem,
                                                                              hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   hipError_t g = cooperative_guard(f, grid, block, shmem);
   if (g != hipSuccess) return g;
@@ -985,6 +1034,7 @@ __attribute__((visibility("default"))) hipError_t hipLaunchCooperativeKernel(con
 __attribute__((visibility("default"))) hipError_t hipModuleLaunchCooperativeKernel(
     hipFunction_t f, unsigned int gx, unsigned int gy, unsigned int gz, unsigned int bx,
     unsigned int by, unsigned int bz, unsigned int shmem, hipStream_t stream, void** params) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   const int dev = launch_dev(stream);
   const bool track = limiter_on_launch(dev, blocks3(gx, gy, gz));
@@ -996,6 +1046,7 @@ __attribute__((visibility("default"))) hipError_t hipModuleLaunchCooperativeKern
 
 __attribute__((visibility("default"))) hipError_t hipLaunchKernelExC(const hipLaunchConfig_t* cfg,
                                                                      const void* f, void** args) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   const int dev = cfg ? launch_dev(cfg->stream) : cur_dev();
   const bool track = cfg && limiter_on_launch(dev, blocks3(cfg->gridDim.x, cfg->gridDim.y, cfg->gridDim.z), f);
@@ -1030,6 +1081,7 @@ __attribute__((visibility("default"))) hipError_t hipStreamDestroy(hipStream_t s
 // Graphs the walk cannot see (instantiated before the shim, or updated in
 // place) fall back to VGPU_GRAPH_LAUNCH_TOKENS.
 __attribute__((visibility("default"))) hipError_t hipGraphLaunch(hipGraphExec_t exec, hipStream_t stream) {
+  HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   static uint64_t fallback_tokens = [] {
     const char* v = getenv("VGPU_GRAPH_LAUNCH_TOKENS");

@@ -101,6 +101,7 @@ static void atfork_child() {
   hostpid_after_fork();
   limiter_after_fork();
   vmem_after_fork();
+  vmm_after_fork();
   pools_after_fork();
   if (s.region) {
     s.slot = region_claim_slot(s.region, s.pid, self_host_pid(nullptr), s.lim.priority);
@@ -166,9 +167,15 @@ void ensure_init() {
 
 void suspend_gate() {
   State& s = st();
-  if (__builtin_expect(!s.suspended.load(std::memory_order_relaxed), 1)) return;
+  auto held = [&] {
+    return s.suspended.load(std::memory_order_relaxed) || s.vmm_evicted.load(std::memory_order_relaxed);
+  };
+  if (__builtin_expect(!held(), 1)) return;
+  // Inside a HookScope that passed the gate already: the evict thread waits for
+  // this call to finish, so waiting here would deadlock with it.
+  if (vmm_in_scope()) return;
   uint64_t t0 = mono_ns();
-  while (s.suspended.load(std::memory_order_relaxed)) sleep_ns(1000000);  // 1 ms
+  while (held()) sleep_ns(1000000);  // 1 ms
   const uint64_t waited = mono_ns() - t0;
   if (vgpu_proc_slot_t* sl = my_slot())
     __atomic_fetch_add(&sl->throttle_wait_ns, waited, __ATOMIC_RELAXED);

@@ -53,6 +53,14 @@ using hipFreeAsync = hipError_t (*)(void*, hipStream_t);
 using hipMemCreate = hipError_t (*)(hipMemGenericAllocationHandle_t*, size_t,
                                     const hipMemAllocationProp*, unsigned long long);
 using hipMemRelease = hipError_t (*)(hipMemGenericAllocationHandle_t);
+using hipMemAddressReserve = hipError_t (*)(void**, size_t, size_t, void*, unsigned long long);
+using hipMemAddressFree = hipError_t (*)(void*, size_t);
+using hipMemMap = hipError_t (*)(void*, size_t, size_t, hipMemGenericAllocationHandle_t, unsigned long long);
+using hipMemUnmap = hipError_t (*)(void*, size_t);
+using hipMemSetAccess = hipError_t (*)(void*, size_t, const hipMemAccessDesc*, size_t);
+using hipMemGetAllocationGranularity = hipError_t (*)(size_t*, const hipMemAllocationProp*,
+                                                      hipMemAllocationGranularity_flags);
+using hipStreamCreateWithFlags = hipError_t (*)(hipStream_t*, unsigned int);
 using hipMemGetInfo = hipError_t (*)(size_t*, size_t*);
 using hipDeviceTotalMem = hipError_t (*)(size_t*, hipDevice_t);
 using hipGetDevicePropertiesR0600 = hipError_t (*)(hipDeviceProp_tR0600*, int);

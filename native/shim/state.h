@@ -55,6 +55,8 @@ struct State {
   std::unordered_map<uintptr_t, Alloc> ledger;
 
   std::atomic<int> suspended{0};
+  // VMM ranges are on the host (vmm.cpp): launches and copies wait like suspended
+  std::atomic<int> vmm_evicted{0};
   std::atomic<int64_t> ipc_imported[VGPU_MAX_DEVICES] = {};  // bytes mapped from other processes
   std::atomic<int> dev_touched[VGPU_MAX_DEVICES] = {};
   // Measured runtime memory (mem_sync_runtime): the context charge currently
@@ -209,6 +211,32 @@ bool trace_on();
 void trace_emit(uint32_t type, int dev, uint64_t a, uint64_t b);
 
 extern thread_local int tl_device;
+
+// VMM-backed allocations for suspend with eviction (vmm.cpp) -------------------------
+bool vmm_wanted(int dev, uint64_t size);
+hipError_t vmm_alloc(void** ptr, size_t size, int dev);
+bool vmm_free(void* p);                 // unmap + release + free the VA; false if not ours
+bool vmm_owns(const void* p);
+void vmm_ipc_exported(const void* p);   // never evict a range another process may map
+void vmm_stats(uint64_t out[6]);        // ranges, bytes, evicted bytes, suspend ns, resume ns, cycles
+void vmm_after_fork();
+void vmem_book_move(int dev, uint64_t bytes, bool to_gpu);
+extern std::atomic<int> g_vmm_live;
+std::atomic<int>* vmm_hook_enter();
+bool vmm_in_scope();  // the calling thread is inside a HookScope past its gate
+// Brackets a hook from its gate to the end of its real call while VMM ranges
+// exist: the evict thread waits for every open scope before unmapping.
+struct HookScope {
+  std::atomic<int>* f = nullptr;
+  HookScope() {
+    if (__builtin_expect(g_vmm_live.load(std::memory_order_relaxed) != 0, 0)) f = vmm_hook_enter();
+  }
+  ~HookScope() {
+    if (f) f->store(0, std::memory_order_release);
+  }
+  HookScope(const HookScope&) = delete;
+  HookScope& operator=(const HookScope&) = delete;
+};
 // Non-zero while a HIP allocation hook is inside the real runtime call: the
 // HSA pool interposer must not charge the same bytes again.
 extern thread_local int tl_in_hip_alloc;

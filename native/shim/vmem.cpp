@@ -1221,6 +1221,8 @@ uint64_t vmem_graph_ranges(hipGraphExec_t exec) {
   return it == g_exec_ranges.end() ? 0 : it->second.size();
 }
 
+void vmem_book_move(int dev, uint64_t bytes, bool to_gpu) { book_move(dev, bytes, to_gpu); }
+
 void vmem_stats(uint64_t* in_bytes, uint64_t* out_bytes, uint64_t* moves, uint64_t* gpu_bytes,
                 uint64_t* ranges) {
   *in_bytes = g_in_bytes.load();

@@ -1,0 +1,379 @@
+// VMM-backed device memory: the copy-engine vehicle of suspend with eviction
+// (VERDICT r4 #7).
+//
+// Reference: the NVIDIA libvgpu.so exports cuMemAddressReserve / cuMemCreate /
+// cuMemMap and suspends a container with suspend_all (SURVEY.md §2.6 E1d,
+// E1g); README.md:285-287.  Round 3 gave a suspended container's HBM back
+// through KFD SVM ranges (vmem.cpp evict_all): every page migrates at ~10 GB/s,
+// 64 GiB in 6 s.  Here, with VGPU_SUSPEND_EVICT and neither oversubscription
+// nor a physical budget, device allocations of at least VGPU_VMEM_MANAGED_MIN_MB
+// (32 MiB) are VMM mappings instead: a reserved VA range, one device handle,
+// mapped and made accessible (64 GiB: 0.05 s, scripts/evict_probe.py).  On
+// SIGUSR2 the evict thread closes the launch gate, waits until no hook is
+// between the gate and its real call, drains the device, copies every range
+// to pinned host memory with the copy engines (1 GiB chunks: the next chunk
+// is pinned while the previous one copies), then unmaps the range and
+// releases its handle -- the HBM is free at once.  On SIGUSR1 it re-creates
+// the handles, maps them at the same VAs, copies back and opens the gate;
+// the pinned chunks are released after.  Pointers never change.
+// VGPU_SUSPEND_VMM=false keeps the SVM vehicle.  Limits: memory another
+// process imports through IPC must not be evicted, so a range whose IPC
+// handle was taken stays resident (vmm_ipc_exported).
+#include <sys/mman.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "common.h"
+#include "real.h"
+#include "state.h"
+
+namespace vgpu {
+
+std::atomic<int> g_vmm_live{0};
+
+namespace {
+
+constexpr size_t kChunk = 1ull << 30;
+
+struct Range {
+  uintptr_t va = 0;
+  size_t size = 0;   // mapped bytes (the request rounded up to the granularity)
+  int dev = 0;
+  hipMemGenericAllocationHandle_t h = nullptr;  // nullptr while evicted
+  bool ipc = false;                             // an IPC handle was taken: never evicted
+  std::vector<std::pair<void*, size_t>> host;   // evicted contents, pinned chunks
+};
+
+std::mutex g_mu;  // g_ranges and every Range in it
+std::map<uintptr_t, Range> g_ranges;
+std::atomic<uint64_t> g_bytes{0}, g_evicted{0}, g_suspend_ns{0}, g_resume_ns{0}, g_cycles{0};
+
+// Per-thread "inside a gated hook" flags (HookScope): the evict thread waits
+// for all of them after closing the gate, so no launch or copy that passed
+// the gate before it closed can reach the runtime after the ranges are gone.
+struct Flag {
+  std::atomic<int> in{0};
+  Flag* next = nullptr;
+};
+std::atomic<Flag*> g_flags{nullptr};
+thread_local Flag* tl_flag = nullptr;
+
+std::mutex g_thr_mu;
+bool g_thr = false;
+
+bool knob_on() {
+  static const bool on = env_bool(env_first("VGPU_SUSPEND_VMM"), true) &&
+                         env_bool(env_first("VGPU_SUSPEND_EVICT"), false);
+  return on;
+}
+
+size_t granule(int dev) {
+  static size_t g[VGPU_MAX_DEVICES] = {};
+  if (dev < 0 || dev >= VGPU_MAX_DEVICES) return 2u << 20;
+  if (!g[dev]) {
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = dev;
+    size_t v = 0;
+    auto fn = REAL_HIP(hipMemGetAllocationGranularity);
+    if (!fn || fn(&v, &prop, hipMemAllocationGranularityRecommended) != hipSuccess || !v) v = 4096;
+    g[dev] = std::max<size_t>(v, 2u << 20);  // whole 2 MiB fragments
+  }
+  return g[dev];
+}
+
+hipMemAllocationProp dev_prop(int dev) {
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = dev;
+  return prop;
+}
+
+// Create a handle for `r` and map it at r.va with read/write access.
+hipError_t map_range(Range& r) {
+  const hipMemAllocationProp prop = dev_prop(r.dev);
+  hipMemGenericAllocationHandle_t h = nullptr;
+  hipError_t rc = REAL_HIP(hipMemCreate)(&h, r.size, &prop, 0);
+  if (rc != hipSuccess) return rc;
+  rc = REAL_HIP(hipMemMap)((void*)r.va, r.size, 0, h, 0);
+  if (rc != hipSuccess) {
+    (void)REAL_HIP(hipMemRelease)(h);
+    return rc;
+  }
+  hipMemAccessDesc acc = {};
+  acc.location.type = hipMemLocationTypeDevice;
+  acc.location.id = r.dev;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  rc = REAL_HIP(hipMemSetAccess)((void*)r.va, r.size, &acc, 1);
+  if (rc != hipSuccess) {
+    (void)REAL_HIP(hipMemUnmap)((void*)r.va, r.size);
+    (void)REAL_HIP(hipMemRelease)(h);
+    return rc;
+  }
+  r.h = h;
+  return hipSuccess;
+}
+
+void unmap_range(Range& r) {
+  if (!r.h) return;
+  (void)REAL_HIP(hipMemUnmap)((void*)r.va, r.size);
+  (void)REAL_HIP(hipMemRelease)(r.h);
+  r.h = nullptr;
+}
+
+// The devices with ranges, each made current on this thread in turn.
+template <class F>
+void per_device(F&& f) {
+  bool seen[VGPU_MAX_DEVICES] = {};
+  for (auto& e : g_ranges)
+    if (e.second.dev >= 0 && e.second.dev < VGPU_MAX_DEVICES) seen[e.second.dev] = true;
+  for (int d = 0; d < VGPU_MAX_DEVICES; ++d)
+    if (seen[d] && REAL_HIP(hipSetDevice)(d) == hipSuccess) f(d);
+}
+
+void wait_hooks() {
+  for (Flag* f = g_flags.load(std::memory_order_acquire); f; f = f->next)
+    while (f->in.load(std::memory_order_acquire)) sleep_ns(20000);
+}
+
+hipStream_t copy_stream(int dev) {
+  static hipStream_t s[VGPU_MAX_DEVICES] = {};
+  if (!s[dev] && REAL_HIP(hipStreamCreateWithFlags)(&s[dev], hipStreamNonBlocking) != hipSuccess) s[dev] = nullptr;
+  return s[dev];
+}
+
+void evict() {
+  State& S = st();
+  S.vmm_evicted.store(1, std::memory_order_seq_cst);
+  wait_hooks();
+  const uint64_t t0 = mono_ns();
+  std::lock_guard<std::mutex> l(g_mu);
+  per_device([](int) { (void)REAL_HIP(hipDeviceSynchronize)(); });
+  uint64_t moved = 0;
+  bool short_of_host = false;
+  per_device([&](int dev) {
+    hipStream_t s = copy_stream(dev);
+    for (auto& e : g_ranges) {
+      Range& r = e.second;
+      if (r.dev != dev || !r.h || r.ipc || short_of_host) continue;
+      for (size_t off = 0; off < r.size; off += kChunk) {
+        const size_t c = std::min(kChunk, r.size - off);
+        void* p = nullptr;
+        if (REAL_HIP(hipHostMalloc)(&p, c, hipHostMallocDefault) != hipSuccess || !p) {
+          (void)REAL_HIP(hipGetLastError)();
+          short_of_host = true;
+          break;
+        }
+        r.host.emplace_back(p, c);
+        // Pinning the next chunk overlaps this copy.
+        (void)REAL_HIP(hipMemcpyAsync)(p, (const char*)r.va + off, c, hipMemcpyDeviceToHost, s);
+      }
+    }
+    (void)REAL_HIP(hipStreamSynchronize)(s);
+    for (auto& e : g_ranges) {
+      Range& r = e.second;
+      if (r.dev != dev || !r.h || r.ipc) continue;
+      size_t held = 0;
+      for (auto& c : r.host) held += c.second;
+      if (held != r.size) {  // host memory ran out part-way: this range stays
+        for (auto& c : r.host) (void)REAL_HIP(hipHostFree)(c.first);
+        r.host.clear();
+        continue;
+      }
+      unmap_range(r);
+      vmem_book_move(dev, r.size, false);
+      moved += r.size;
+    }
+  });
+  if (short_of_host) VLOG_WARN("vmm: host memory ran out while evicting; some ranges stay in HBM");
+  g_evicted.store(moved);
+  g_suspend_ns.store(mono_ns() - t0);
+  VLOG_INFO("vmm: suspended, %llu bytes of HBM released in %.3f s", (unsigned long long)moved,
+            (mono_ns() - t0) / 1e9);
+}
+
+void restore() {
+  const uint64_t t0 = mono_ns();
+  std::vector<std::pair<void*, size_t>> to_free;
+  {
+    std::lock_guard<std::mutex> l(g_mu);
+    per_device([&](int dev) {
+      hipStream_t s = copy_stream(dev);
+      for (auto& e : g_ranges) {
+        Range& r = e.second;
+        if (r.dev != dev || r.h) continue;
+        // HBM taken meanwhile by someone else: keep trying, the gate stays closed.
+        hipError_t rc;
+        while ((rc = map_range(r)) != hipSuccess) {
+          (void)REAL_HIP(hipGetLastError)();
+          VLOG_WARN("vmm: cannot map %zu bytes back at %p (error %d); retrying", r.size, (void*)r.va, (int)rc);
+          sleep_ns(100000000ull);
+        }
+        size_t off = 0;
+        for (auto& c : r.host) {
+          (void)REAL_HIP(hipMemcpyAsync)((char*)r.va + off, c.first, c.second, hipMemcpyHostToDevice, s);
+          off += c.second;
+        }
+        vmem_book_move(dev, r.size, true);
+      }
+      (void)REAL_HIP(hipStreamSynchronize)(s);
+      for (auto& e : g_ranges) {
+        Range& r = e.second;
+        if (r.dev != dev) continue;
+        for (auto& c : r.host) to_free.push_back(c);
+        r.host.clear();
+      }
+    });
+  }
+  g_resume_ns.store(mono_ns() - t0);
+  g_evicted.store(0);
+  g_cycles.fetch_add(1);
+  st().vmm_evicted.store(0, std::memory_order_seq_cst);  // the gate opens with the data back
+  VLOG_INFO("vmm: resumed in %.3f s", (mono_ns() - t0) / 1e9);
+  for (auto& c : to_free) (void)REAL_HIP(hipHostFree)(c.first);
+}
+
+void evict_main() {
+  pthread_setname_np(pthread_self(), "vgpu-vmm");
+  tl_device = -1;
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  (void)REAL_HIP(hipThreadExchangeStreamCaptureMode)(&mode);
+  State& S = st();
+  bool out = false;
+  for (;;) {
+    sleep_ns(1000000);  // 1 ms: the signal handlers only flip a flag
+    const bool sus = S.suspended.load(std::memory_order_relaxed) != 0;
+    if (sus && !out) {
+      evict();
+      out = true;
+    } else if (!sus && out) {
+      restore();
+      out = false;
+    }
+  }
+}
+
+void ensure_thread() {
+  std::lock_guard<std::mutex> l(g_thr_mu);
+  if (g_thr) return;
+  g_thr = true;
+  std::thread(evict_main).detach();
+}
+
+}  // namespace
+
+bool vmm_wanted(int dev, uint64_t size) {
+  State& s = st();
+  if (!knob_on() || !s.enabled || !s.region || s.region->oversubscribe) return false;
+  if (dev < 0 || dev >= VGPU_MAX_DEVICES || s.region->dev[dev].mem_physical) return false;
+  static const int64_t min = [] {
+    const char* e = env_first("VGPU_VMEM_MANAGED_MIN_MB");
+    const long long mb = e ? atoll(e) : 32;
+    return mb < 0 ? (int64_t)-1 : (int64_t)mb << 20;
+  }();
+  // Not inside a graph capture: VA and handle calls are not capturable.
+  return min >= 0 && size >= (uint64_t)min && g_open_captures.load(std::memory_order_acquire) == 0 &&
+         REAL_HIP(hipMemAddressReserve) && REAL_HIP(hipMemMap) && REAL_HIP(hipMemSetAccess);
+}
+
+hipError_t vmm_alloc(void** ptr, size_t size, int dev) {
+  Range r;
+  r.dev = dev;
+  const size_t g = granule(dev);
+  r.size = (size + g - 1) / g * g;
+  void* va = nullptr;
+  hipError_t rc = REAL_HIP(hipMemAddressReserve)(&va, r.size, g, nullptr, 0);
+  if (rc != hipSuccess) return rc;
+  r.va = (uintptr_t)va;
+  if ((rc = map_range(r)) != hipSuccess) {
+    (void)REAL_HIP(hipMemAddressFree)(va, r.size);
+    return rc;
+  }
+  {
+    std::lock_guard<std::mutex> l(g_mu);
+    g_ranges[r.va] = r;
+  }
+  g_bytes.fetch_add(r.size);
+  g_vmm_live.store(1, std::memory_order_release);
+  ensure_thread();
+  *ptr = va;
+  return hipSuccess;
+}
+
+bool vmm_free(void* p) {
+  if (!g_vmm_live.load(std::memory_order_relaxed) || !p) return false;
+  std::lock_guard<std::mutex> l(g_mu);
+  auto it = g_ranges.find((uintptr_t)p);
+  if (it == g_ranges.end()) return false;
+  Range& r = it->second;
+  unmap_range(r);
+  for (auto& c : r.host) (void)REAL_HIP(hipHostFree)(c.first);
+  (void)REAL_HIP(hipMemAddressFree)((void*)r.va, r.size);
+  g_bytes.fetch_sub(r.size);
+  g_ranges.erase(it);
+  return true;
+}
+
+bool vmm_owns(const void* p) {
+  if (!g_vmm_live.load(std::memory_order_relaxed) || !p) return false;
+  std::lock_guard<std::mutex> l(g_mu);
+  auto it = g_ranges.upper_bound((uintptr_t)p);
+  if (it == g_ranges.begin()) return false;
+  --it;
+  return (uintptr_t)p < it->second.va + it->second.size;
+}
+
+void vmm_ipc_exported(const void* p) {
+  if (!g_vmm_live.load(std::memory_order_relaxed) || !p) return;
+  std::lock_guard<std::mutex> l(g_mu);
+  auto it = g_ranges.upper_bound((uintptr_t)p);
+  if (it == g_ranges.begin()) return;
+  --it;
+  if ((uintptr_t)p < it->second.va + it->second.size) it->second.ipc = true;
+}
+
+std::atomic<int>* vmm_hook_enter() {
+  Flag* f = tl_flag;
+  if (!f) {
+    f = new Flag();  // one per thread, never freed (the evict thread walks the list)
+    Flag* head = g_flags.load(std::memory_order_relaxed);
+    do f->next = head;
+    while (!g_flags.compare_exchange_weak(head, f, std::memory_order_release, std::memory_order_relaxed));
+    tl_flag = f;
+  }
+  State& s = st();
+  for (;;) {
+    f->in.store(1, std::memory_order_relaxed);
+    std::atomic_thread_fence(std::memory_order_seq_cst);  // pairs with evict(): gate store, then flag loads
+    if (!s.suspended.load(std::memory_order_relaxed) && !s.vmm_evicted.load(std::memory_order_relaxed)) return &f->in;
+    f->in.store(0, std::memory_order_release);
+    suspend_gate();
+  }
+}
+
+bool vmm_in_scope() { return tl_flag && tl_flag->in.load(std::memory_order_relaxed); }
+
+void vmm_stats(uint64_t out[6]) {
+  std::lock_guard<std::mutex> l(g_mu);
+  out[0] = g_ranges.size();
+  out[1] = g_bytes.load();
+  out[2] = g_evicted.load();
+  out[3] = g_suspend_ns.load();
+  out[4] = g_resume_ns.load();
+  out[5] = g_cycles.load();
+}
+
+void vmm_after_fork() {
+  // The child shares no device state with the parent's mappings.
+  g_ranges.clear();
+  g_vmm_live.store(0);
+  g_thr = false;
+}
+
+}  // namespace vgpu

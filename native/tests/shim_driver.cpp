@@ -826,6 +826,72 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (sc == "suspend_vmm") {
+    // VGPU_SUSPEND_EVICT, VMM vehicle (vmm.cpp): a large allocation is a VMM
+    // mapping, a small one stays plain.  SIGUSR2 copies the mapping out and
+    // releases its handle while a launcher thread is held at the gate; SIGUSR1
+    // maps it back at the same address with its bytes.
+    const size_t M = 1ull << 20;
+    auto stats = sym<void (*)(uint64_t*)>("vgpu_self_vmm_stats");
+    auto self_region = sym<void* (*)()>("vgpu_self_region");
+    auto self_slot = sym<int (*)()>("vgpu_self_slot");
+    auto host_bytes = [&]() -> unsigned long long {
+      return ((vgpu_shared_region_t*)self_region())->procs[self_slot()].used[dev].host_bytes;
+    };
+    uint64_t v[6];
+    void* p = nullptr;
+    void* small = nullptr;
+    int ra = hipMalloc(&p, 96 * M), rs = hipMalloc(&small, 8 * M);
+    stats(v);
+    printf("alloc=%d\nsmall=%d\nranges=%llu\nbytes=%llu\nphys_at_alloc=%llu\n", ra, rs, (unsigned long long)v[0],
+           (unsigned long long)v[1], (unsigned long long)fake_hip_physical_used(dev));
+    unsigned char* b = (unsigned char*)p;
+    for (size_t i = 0; i < 96 * M; i += 4096) b[i] = (unsigned char)(i >> 12) | 1;
+    std::atomic<int> stop{0};
+    std::atomic<long> launches{0};
+    std::thread th([&] {
+      while (!stop.load()) {
+        int n = 1;
+        void* q = p;
+        void* args[] = {&n, &q};
+        hipLaunchKernel((const void*)0x1, dim3(1), dim3(64), args, 0, nullptr);
+        launches.fetch_add(1);
+      }
+    });
+    usleep(20000);
+    raise(SIGUSR2);
+    for (int i = 0; i < 400; ++i) {
+      stats(v);
+      if (v[2]) break;
+      usleep(5000);
+    }
+    const long l0 = launches.load();
+    usleep(50000);
+    const long l1 = launches.load();
+    printf("evicted=%llu\nsuspend_ns=%llu\nphys_suspended=%llu\nhost_suspended=%llu\nlaunches_while_evicted=%ld\n",
+           (unsigned long long)v[2], (unsigned long long)v[3], (unsigned long long)fake_hip_physical_used(dev),
+           host_bytes(), l1 - l0);
+    raise(SIGUSR1);
+    for (int i = 0; i < 400; ++i) {
+      stats(v);
+      if (v[5]) break;
+      usleep(5000);
+    }
+    usleep(20000);
+    stop.store(1);
+    th.join();
+    long bad = 0;
+    for (size_t i = 0; i < 96 * M; i += 4096) bad += b[i] != ((unsigned char)(i >> 12) | 1);
+    printf("cycles=%llu\nresume_ns=%llu\npattern_errors=%ld\nphys_resumed=%llu\nhost_resumed=%llu\nlaunches_after=%ld\n",
+           (unsigned long long)v[5], (unsigned long long)v[4], bad, (unsigned long long)fake_hip_physical_used(dev),
+           host_bytes(), launches.load() - l1);
+    hipFree(small);
+    hipFree(p);
+    stats(v);
+    printf("ranges_end=%llu\nphys_end=%llu\n", (unsigned long long)v[0], (unsigned long long)fake_hip_physical_used(dev));
+    return 0;
+  }
+
   if (sc == "vmem_copy2") {
     // The remaining copy / memset entry points on a resident managed range
     // (VERDICT r3 #4): 2-D host copies are staged (KFD never moves a page),

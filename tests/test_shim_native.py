@@ -883,14 +883,37 @@ def test_suspend_evict_frees_hbm_without_a_budget(native_build):
     suspend moves them to host memory (its HBM is free for another pod), a
     resume and the next use bring them back.  Small buffers stay plain."""
     o = run("suspend_evict", env={"VGPU_FAKE_MEM": str(16 * GiB), "VGPU_DEVICE_MEMORY_LIMIT_0": "12g",
-                                  "VGPU_SUSPEND_EVICT": "true", "VGPU_VMEM_TICK_MS": "10",
-                                  "VGPU_VMEM_HEADROOM_MB": "256"})
+                                  "VGPU_SUSPEND_EVICT": "true", "VGPU_SUSPEND_VMM": "false",
+                                  "VGPU_VMEM_TICK_MS": "10", "VGPU_VMEM_HEADROOM_MB": "256"})
     assert (o["alloc"], o["small"]) == ("0", "0")
     assert o["gpu_at_alloc"] == str(4 * GiB) and o["small_managed"] == "0"
     assert int(o["phys_at_alloc"]) >= 4 * GiB
     assert o["suspended_gpu"] == "0" and int(o["suspended_phys"]) < GiB
     assert o["suspended_host"] == str(4 * GiB)
     assert o["resumed_gpu"] == str(4 * GiB) and o["resumed_host"] == "0"
+
+
+def test_suspend_evict_vmm_vehicle_copies_out_and_back(native_build):
+    """with VGPU_SUSPEND_EVICT and no oversubscription, a large
+    allocation is a VMM mapping (vmm.cpp).  SIGUSR2 closes the launch gate,
+    waits for a launcher thread's hook in flight, copies the mapping to host
+    memory and releases its handle (the fake device's physical use drops);
+    no launch gets through while it is out.  SIGUSR1 maps it back at the same
+    address with every byte intact, and the launcher runs again."""
+    M = 1 << 20
+    o = run("suspend_vmm", env={"VGPU_FAKE_MEM": str(16 * GiB), "VGPU_DEVICE_MEMORY_LIMIT_0": "12g",
+                                "VGPU_SUSPEND_EVICT": "true"})
+    assert (o["alloc"], o["small"]) == ("0", "0")
+    assert (o["ranges"], o["bytes"]) == ("1", str(96 * M))        # the 8 MiB buffer stays plain
+    phys0 = int(o["phys_at_alloc"])
+    assert o["evicted"] == str(96 * M)
+    assert phys0 - int(o["phys_suspended"]) == 96 * M             # the handle's HBM went back
+    assert o["host_suspended"] == str(96 * M)                     # booked as host memory meanwhile
+    assert o["launches_while_evicted"] == "0"
+    assert o["cycles"] == "1" and o["pattern_errors"] == "0"
+    assert int(o["phys_resumed"]) == phys0 and o["host_resumed"] == "0"
+    assert int(o["launches_after"]) > 0
+    assert o["ranges_end"] == "0"
 
 
 def test_multi_gpu_container_per_device_caps_boards_and_ipc(native_build, tmp_path):
