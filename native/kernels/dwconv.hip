@@ -1,0 +1,255 @@
+// Depthwise 3x3 convolution for NHWC bf16 activations (MobileNet-V2 / DeepLab-v3
+// training): forward, data gradient and weight gradient, any
+// stride and dilation, padding = dilation ("same" for k = 3).
+//
+// A depthwise conv is 9 multiply-adds per output element: no GEMM, nothing
+// for the MFMA, HBM / L2-bound.  Every kernel gives a thread 8 consecutive
+// channels of one pixel (one 16-byte load per tap: a 64-lane wavefront reads
+// 1 KiB contiguous runs of a pixel's channels) and keeps the weights as fp32
+// [9][C] (the host op transposes the [C,1,3,3] filter once per step).
+//   * forward: one thread per (output pixel, 8 channels), 9 taps gathered;
+//   * data gradient: one thread per (input pixel, 8 channels) gathers the
+//     output pixels whose window holds it (stride-divisible taps only) -- no
+//     atomics, no zero-fill;
+//   * weight gradient: thread (slab, 8 channels) accumulates 9 x 8 fp32
+//     products over its slab of output pixels into a partial row; a second
+//     kernel sums the slabs in a fixed order (deterministic).
+// fp32 accumulation, one bf16 rounding per output (forward / data gradient).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define VGPU_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr int kThreads = 256;
+
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+
+__device__ __forceinline__ void unpack8(const u32x4 v, float (&f)[8]) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  typedef __attribute__((ext_vector_type(2))) float f2;
+  typedef __attribute__((ext_vector_type(2))) __bf16 b2;
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{lo, hi}, b2));
+}
+
+__device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
+  return u32x4{pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7])};
+}
+
+__device__ __forceinline__ void load_w8(const float* __restrict__ w, int C, int tap, int c8, float (&f)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(w + (int64_t)tap * C + c8);
+  const float4 b = *reinterpret_cast<const float4*>(w + (int64_t)tap * C + c8 + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+  f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
+struct Shape {
+  int N, H, W, C, OH, OW, stride, dil;
+};
+
+__global__ void __launch_bounds__(kThreads) dw_fwd_kernel(const u32x4* __restrict__ x, const float* __restrict__ w,
+                                                          u32x4* __restrict__ y, const Shape s, int64_t total) {
+  const int cv = s.C / 8;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < total; i += (int64_t)gridDim.x * kThreads) {
+    const int cg = (int)(i % cv);
+    int64_t r = i / cv;
+    const int ow = (int)(r % s.OW);
+    r /= s.OW;
+    const int oh = (int)(r % s.OH);
+    const int n = (int)(r / s.OH);
+    const int h0 = oh * s.stride - s.dil, w0 = ow * s.stride - s.dil;
+    const u32x4* xn = x + (int64_t)n * s.H * s.W * cv + cg;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = h0 + kh * s.dil;
+      if ((unsigned)ih >= (unsigned)s.H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = w0 + kw * s.dil;
+        if ((unsigned)iw >= (unsigned)s.W) continue;
+        float xv[8], wv[8];
+        unpack8(xn[((int64_t)ih * s.W + iw) * cv], xv);
+        load_w8(w, s.C, kh * 3 + kw, cg * 8, wv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = fmaf(xv[j], wv[j], acc[j]);
+      }
+    }
+    y[i] = pack8(acc);
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) dw_dgrad_kernel(const u32x4* __restrict__ dy, const float* __restrict__ w,
+                                                            u32x4* __restrict__ dx, const Shape s, int64_t total) {
+  const int cv = s.C / 8;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < total; i += (int64_t)gridDim.x * kThreads) {
+    const int cg = (int)(i % cv);
+    int64_t r = i / cv;
+    const int iw = (int)(r % s.W);
+    r /= s.W;
+    const int ih = (int)(r % s.H);
+    const int n = (int)(r / s.H);
+    const u32x4* dyn = dy + (int64_t)n * s.OH * s.OW * cv + cg;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      // ih = oh·stride - dil + kh·dil
+      const int th = ih + s.dil - kh * s.dil;
+      if (th < 0 || th % s.stride) continue;
+      const int oh = th / s.stride;
+      if (oh >= s.OH) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int tw = iw + s.dil - kw * s.dil;
+        if (tw < 0 || tw % s.stride) continue;
+        const int ow = tw / s.stride;
+        if (ow >= s.OW) continue;
+        float gv[8], wv[8];
+        unpack8(dyn[((int64_t)oh * s.OW + ow) * cv], gv);
+        load_w8(w, s.C, kh * 3 + kw, cg * 8, wv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = fmaf(gv[j], wv[j], acc[j]);
+      }
+    }
+    dx[i] = pack8(acc);
+  }
+}
+
+// Thread t: channel group t % cv, slab t / cv; slab covers output pixels
+// [slab·per, (slab+1)·per).  part[slab][tap][C].
+__global__ void __launch_bounds__(kThreads) dw_wgrad_kernel(const u32x4* __restrict__ dy, const u32x4* __restrict__ x,
+                                                            float* __restrict__ part, const Shape s, int slabs,
+                                                            int64_t per) {
+  const int cv = s.C / 8;
+  const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (t >= (int64_t)slabs * cv) return;
+  const int cg = (int)(t % cv), slab = (int)(t / cv);
+  const int64_t P = (int64_t)s.N * s.OH * s.OW;
+  const int64_t p0 = slab * per, p1 = p0 + per < P ? p0 + per : P;
+  float acc[9][8];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
+  for (int64_t p = p0; p < p1; ++p) {
+    const int ow = (int)(p % s.OW);
+    const int64_t r = p / s.OW;
+    const int oh = (int)(r % s.OH);
+    const int n = (int)(r / s.OH);
+    float g[8];
+    unpack8(dy[p * cv + cg], g);
+    const int h0 = oh * s.stride - s.dil, w0 = ow * s.stride - s.dil;
+    const u32x4* xn = x + (int64_t)n * s.H * s.W * cv + cg;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = h0 + kh * s.dil;
+      if ((unsigned)ih >= (unsigned)s.H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = w0 + kw * s.dil;
+        if ((unsigned)iw >= (unsigned)s.W) continue;
+        float xv[8];
+        unpack8(xn[((int64_t)ih * s.W + iw) * cv], xv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[kh * 3 + kw][j] = fmaf(g[j], xv[j], acc[kh * 3 + kw][j]);
+      }
+    }
+  }
+  float* out = part + (int64_t)slab * 9 * s.C + cg * 8;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    *reinterpret_cast<float4*>(out + (int64_t)k * s.C) = make_float4(acc[k][0], acc[k][1], acc[k][2], acc[k][3]);
+    *reinterpret_cast<float4*>(out + (int64_t)k * s.C + 4) = make_float4(acc[k][4], acc[k][5], acc[k][6], acc[k][7]);
+  }
+}
+
+// dw[tap][c] = Σ_slab part[slab][tap][c], slabs in order.
+__global__ void __launch_bounds__(kThreads) dw_wgrad_reduce_kernel(const float* __restrict__ part,
+                                                                   float* __restrict__ dw, int n9c, int slabs) {
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n9c) return;
+  float a = 0.f;
+  for (int sl = 0; sl < slabs; ++sl) a += part[(int64_t)sl * n9c + i];
+  dw[i] = a;
+}
+
+bool make_shape(Shape& s, int N, int H, int W, int C, int stride, int dil) {
+  if (N < 1 || H < 1 || W < 1 || C < 8 || C % 8 || stride < 1 || dil < 1) return false;
+  s = Shape{N, H, W, C, (H - 1) / stride + 1, (W - 1) / stride + 1, stride, dil};
+  return true;
+}
+
+int grid_for(int64_t total) {
+  const int64_t b = (total + kThreads - 1) / kThreads;
+  return (int)(b < 65536 ? (b > 0 ? b : 1) : 65536);
+}
+
+// Slabs of the weight gradient: about 64k threads (a few waves per CU), each
+// slab at least 16 output pixels.
+void wgrad_split(const Shape& s, int& slabs, int64_t& per) {
+  const int64_t P = (int64_t)s.N * s.OH * s.OW;
+  const int cv = s.C / 8;
+  int64_t want = 65536 / cv;
+  if (want < 1) want = 1;
+  const int64_t most = (P + 15) / 16;
+  if (want > most) want = most;
+  if (want < 1) want = 1;
+  per = (P + want - 1) / want;
+  slabs = (int)((P + per - 1) / per);
+}
+
+}  // namespace
+
+VGPU_API int vgpu_dwconv3_fwd_nhwc(const void* x, const float* w9c, void* y, int N, int H, int W, int C, int stride,
+                                   int dil, hipStream_t st) {
+  Shape s;
+  if (!make_shape(s, N, H, W, C, stride, dil)) return -1;
+  const int64_t total = (int64_t)N * s.OH * s.OW * (C / 8);
+  hipLaunchKernelGGL(dw_fwd_kernel, dim3(grid_for(total)), dim3(kThreads), 0, st, (const u32x4*)x, w9c, (u32x4*)y,
+                     s, total);
+  return (int)hipGetLastError();
+}
+
+VGPU_API int vgpu_dwconv3_dgrad_nhwc(const void* dy, const float* w9c, void* dx, int N, int H, int W, int C,
+                                     int stride, int dil, hipStream_t st) {
+  Shape s;
+  if (!make_shape(s, N, H, W, C, stride, dil)) return -1;
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  hipLaunchKernelGGL(dw_dgrad_kernel, dim3(grid_for(total)), dim3(kThreads), 0, st, (const u32x4*)dy, w9c,
+                     (u32x4*)dx, s, total);
+  return (int)hipGetLastError();
+}
+
+VGPU_API int64_t vgpu_dwconv3_wgrad_workspace(int N, int H, int W, int C, int stride, int dil) {
+  Shape s;
+  if (!make_shape(s, N, H, W, C, stride, dil)) return -1;
+  int slabs;
+  int64_t per;
+  wgrad_split(s, slabs, per);
+  return (int64_t)slabs * 9 * C * 4;
+}
+
+// dw9c: fp32 [9][C].  ws: vgpu_dwconv3_wgrad_workspace bytes.
+VGPU_API int vgpu_dwconv3_wgrad_nhwc(const void* dy, const void* x, float* dw9c, void* ws, int64_t ws_bytes, int N,
+                                     int H, int W, int C, int stride, int dil, hipStream_t st) {
+  Shape s;
+  if (!make_shape(s, N, H, W, C, stride, dil)) return -1;
+  int slabs;
+  int64_t per;
+  wgrad_split(s, slabs, per);
+  if (ws_bytes < (int64_t)slabs * 9 * C * 4) return -2;
+  const int64_t threads = (int64_t)slabs * (C / 8);
+  hipLaunchKernelGGL(dw_wgrad_kernel, dim3((int)((threads + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
+                     (const u32x4*)dy, (const u32x4*)x, (float*)ws, s, slabs, per);
+  const int n9c = 9 * C;
+  hipLaunchKernelGGL(dw_wgrad_reduce_kernel, dim3((n9c + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
+                     (const float*)ws, dw9c, n9c, slabs);
+  return (int)hipGetLastError();
+}

@@ -68,3 +68,66 @@ def test_vgg16_native_training_step_matches_fp32(gpu_build):
     for i in convs[1:4] + convs[-2:]:
         assert _rel(m.features[i].weight.grad, m32.features[i].weight.grad) < 6e-2, i
         assert _rel(m.features[i].bias.grad, m32.features[i].bias.grad) < 6e-2, i
+
+
+DW_CASES = [  # n, c, h, w, stride, dilation
+    (2, 32, 19, 17, 1, 1),
+    (1, 96, 33, 30, 2, 1),
+    (1, 144, 16, 16, 1, 2),
+    (2, 960, 9, 11, 1, 2),
+    (1, 64, 7, 5, 2, 1),
+]
+
+
+@pytest.mark.parametrize("n,c,h,w,stride,dil", DW_CASES)
+def test_dwconv3_matches_fp32(gpu_build, n, c, h, w, stride, dil):
+    """Depthwise 3x3 (native/kernels/dwconv.hip) forward, data and weight
+    gradients against the fp32 PyTorch grouped conv."""
+    from vgpu.ops import dwconv as D
+    conv = torch.nn.Conv2d(c, c, 3, stride, dil, dilation=dil, groups=c, bias=False).cuda()
+    conv = conv.to(torch.bfloat16).to(memory_format=CL)
+    ref = copy.deepcopy(conv).float()
+    x = _x((n, c, h, w), 5).requires_grad_(True)
+    xr = x.detach().float().requires_grad_(True)
+    assert D.eligible(x, conv)
+    y = D.dwconv_train(x, conv)
+    yr = ref(xr)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=CL)
+    torch.testing.assert_close(y.float(), yr, atol=2e-2, rtol=2e-2)
+    dy = _x(tuple(y.shape), 6)
+    y.backward(dy)
+    yr.backward(dy.float())
+    assert _rel(x.grad, xr.grad) < 1e-2
+    assert _rel(conv.weight.grad, ref.weight.grad) < 1e-2
+    # deterministic weight gradient
+    w1 = D.dwconv3_wgrad(dy, x.detach(), stride, dil)
+    assert torch.equal(w1, D.dwconv3_wgrad(dy, x.detach(), stride, dil))
+
+
+def test_deeplab_native_training_step_matches_fp32(gpu_build):
+    """DeepLab-v3 (MobileNet-V2 + ASPP) training step: depthwise and 1x1 convs
+    on the native kernels (bf16) against the fp32 modules."""
+    from vgpu.models.vision import DeepLabV3
+    from vgpu.ops import dwconv as D
+    torch.manual_seed(0)
+    m32 = DeepLabV3(num_classes=5).cuda().to(memory_format=CL).train()
+    m = copy.deepcopy(m32).to(torch.bfloat16)
+    x = _x((2, 3, 64, 64), 7)
+    tgt = torch.randint(0, 5, (2, 64, 64), device="cuda")
+    calls = []
+    orig = D._DWConvFn.apply
+    D._DWConvFn.apply = lambda *a: (calls.append(1), orig(*a))[1]
+    try:
+        out = m(x)
+    finally:
+        D._DWConvFn.apply = orig
+    assert len(calls) == 17, len(calls)  # every inverted residual's depthwise conv
+    out32 = m32(x.float())
+    assert _rel(out, out32) < 0.1
+    torch.nn.functional.cross_entropy(out.float(), tgt).backward()
+    torch.nn.functional.cross_entropy(out32, tgt).backward()
+    feats = m.backbone.features
+    for i in (1, 5, 12):
+        dw_b = feats[i].body[-2][0].weight.grad
+        dw_r = m32.backbone.features[i].body[-2][0].weight.grad
+        assert _rel(dw_b, dw_r) < 0.15, i

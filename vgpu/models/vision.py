@@ -117,10 +117,24 @@ class NativeVGG16Inference(nn.Module):
 
 class ConvBNAct(nn.Sequential):
     """conv → BatchNorm → (ReLU6); the BN + activation pair runs as one native
-    training kernel pair (vgpu.ops.bn) on bf16 channels_last tensors."""
+    training kernel pair (vgpu.ops.bn) on bf16 channels_last tensors.  On CUDA
+    the conv is native too where a kernel exists: depthwise 3x3 (any stride /
+    dilation, vgpu.ops.dwconv) and 1x1 / 3x3 with C, Cout % 64 == 0
+    (vgpu.ops.conv.conv_train); the rest (the 3-channel stem, dilated ASPP
+    convs, channel counts off the MFMA tiles) stay on the module."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return bn_act(self[0](x), self[1], "relu6" if len(self) > 2 else "none")
+        conv = self[0]
+        if x.is_cuda:
+            from vgpu.ops import dwconv
+            if dwconv.eligible(x, conv):
+                y = dwconv.dwconv_train(x, conv)
+            else:
+                from vgpu.ops.conv import conv_train
+                y = conv_train(x, conv)
+        else:
+            y = conv(x)
+        return bn_act(y, self[1], "relu6" if len(self) > 2 else "none")
 
 
 def _conv_bn(cin: int, cout: int, k: int, stride: int = 1, groups: int = 1, dilation: int = 1,
