@@ -1677,7 +1677,8 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
   // conv2 bias [W] and (NEXT) conv1's prologue scale/shift [4W] each live in
   // LDS: a global load in phase 2 would make hipcc drain the in-flight DMA.
   constexpr int PAR = (W + (NEXT ? 8 * W : 0)) * 4;
-  static_assert(2 * (P + PAR) <= 160 * 1024, "conv23: two workgroups per CU");
+  static_assert(P + PAR <= 160 * 1024, "conv23: LDS");
+  static_assert((BM == 128 && W == 128) || 2 * (P + PAR) <= 160 * 1024, "conv23: two workgroups per CU");
   __shared__ __attribute__((aligned(16))) char smem[P + PAR];
   char* sA2 = smem + B2_BYTES + EPI;
   float* sPar = reinterpret_cast<float*>(smem + P);
@@ -2362,7 +2363,8 @@ static int conv23_impl(const void* x, const void* w2, const float* b2, const voi
       e.y = cn.y + (int64_t)n0 * (hi / 2);
       e.y_bytes = (uint32_t)(nb * hi);
     }
-    const int bm = C == 64 ? 128 : 64;
+    static const bool bm128 = getenv("VGPU_CONV23_BM128") && atoi(getenv("VGPU_CONV23_BM128")) == 1;  // A/B
+    const int bm = C == 64 || bm128 ? 128 : 64;
     c.nM = (c.M + bm - 1) / bm; c.nN = 1; c.nwg = c.nM;
     static const bool ns2 = getenv("VGPU_CONV23_NS") && atoi(getenv("VGPU_CONV23_NS")) == 2;  // A/B
 #define VGPU_C23(BM_, W_, NX_)                                                                          \
@@ -2375,6 +2377,9 @@ static int conv23_impl(const void* x, const void* w2, const float* b2, const voi
     if (C == 64) {
       if (next) VGPU_C23(128, 64, true);
       else VGPU_C23(128, 64, false);
+    } else if (bm128) {
+      if (next) VGPU_C23(128, 128, true);
+      else VGPU_C23(128, 128, false);
     } else {
       if (next) VGPU_C23(64, 128, true);
       else VGPU_C23(64, 128, false);
