@@ -273,17 +273,9 @@ bool capturing(hipStream_t stream) {
   return cs != hipStreamCaptureStatusNone;
 }
 
-// true when the copy was staged (*rc is its result).
-bool staged_copy(void* dst, const void* src, size_t n, hipMemcpyKind kind, hipStream_t stream, hipError_t* rc) {
-  if (kind == hipMemcpyDeviceToDevice || n == 0) return false;
-  const int ddev = vmem_resident_dev(dst, n), sdev = vmem_resident_dev(src, n);
-  if ((ddev < 0) == (sdev < 0)) return false;  // neither side, or range to range (on the GPU)
-  const bool up = ddev >= 0;                    // host -> range
-  const int dev = up ? ddev : sdev;
-  if (kind == hipMemcpyDefault && !host_side(up ? src : dst)) return false;
-  if (dev != cur_dev() || dev >= VGPU_MAX_DEVICES || capturing(stream)) return false;
-  Stage& g = g_stage[dev];
-  std::lock_guard<std::mutex> l(g.mu);
+// The device's staging buffer, allocated on first use; `stream` waits for its
+// previous user.  Called with g.mu held.
+bool stage_ready(Stage& g, hipStream_t stream) {
   if (!g.buf) {
     if (REAL_HIP(hipMalloc)(&g.buf, kStageBytes) != hipSuccess ||
         REAL_HIP(hipEventCreateWithFlags)(&g.done, hipEventDisableTiming) != hipSuccess) {
@@ -296,6 +288,46 @@ bool staged_copy(void* dst, const void* src, size_t n, hipMemcpyKind kind, hipSt
     (void)REAL_HIP(hipGetLastError)();
     return false;
   }
+  return true;
+}
+
+// Memsets of a resident managed range are staged too: the runtime's memset of
+// a managed (SVM) range can fill it from the host behind the call's return,
+// moving its pages to system memory and racing the kernels that follow (the
+// vmemcopy probe lost 64 MiB of a later fill this way, rounds 4-5).  Instead
+// the fill pattern is written once into the plain staging buffer and copied
+// into the range device-to-device, stream-ordered; no page moves.  `fill`
+// writes `bytes` (a multiple of 4) of the pattern at `buf` on `stream`.
+template <class Fill>
+bool staged_memset(void* dst, size_t n, hipStream_t stream, bool sync, hipError_t* rc, Fill&& fill) {
+  if (n == 0) return false;
+  const int dev = vmem_resident_dev(dst, n);
+  if (dev < 0 || dev != cur_dev() || dev >= VGPU_MAX_DEVICES || capturing(stream)) return false;
+  Stage& g = g_stage[dev];
+  std::lock_guard<std::mutex> l(g.mu);
+  if (!stage_ready(g, stream)) return false;
+  hipError_t r = fill(g.buf, std::min(kStageBytes, (n + 3) & ~size_t(3)), stream);
+  for (size_t off = 0; off < n && r == hipSuccess; off += kStageBytes)
+    r = REAL_HIP(hipMemcpyAsync)((char*)dst + off, g.buf, std::min(kStageBytes, n - off), hipMemcpyDeviceToDevice,
+                                 stream);
+  (void)REAL_HIP(hipEventRecord)(g.done, stream);
+  if (r == hipSuccess && sync) r = REAL_HIP(hipStreamSynchronize)(stream);
+  *rc = r;
+  return true;
+}
+
+// true when the copy was staged (*rc is its result).
+bool staged_copy(void* dst, const void* src, size_t n, hipMemcpyKind kind, hipStream_t stream, hipError_t* rc) {
+  if (kind == hipMemcpyDeviceToDevice || n == 0) return false;
+  const int ddev = vmem_resident_dev(dst, n), sdev = vmem_resident_dev(src, n);
+  if ((ddev < 0) == (sdev < 0)) return false;  // neither side, or range to range (on the GPU)
+  const bool up = ddev >= 0;                    // host -> range
+  const int dev = up ? ddev : sdev;
+  if (kind == hipMemcpyDefault && !host_side(up ? src : dst)) return false;
+  if (dev != cur_dev() || dev >= VGPU_MAX_DEVICES || capturing(stream)) return false;
+  Stage& g = g_stage[dev];
+  std::lock_guard<std::mutex> l(g.mu);
+  if (!stage_ready(g, stream)) return false;
   hipError_t r = hipSuccess;
   for (size_t off = 0; off < n && r == hipSuccess; off += kStageBytes) {
     const size_t c = std::min(kStageBytes, n - off);
@@ -745,21 +777,42 @@ __attribute__((visibility("default"))) hipError_t hipMemcpyFromSymbolAsync(void*
                           kind, stream);
 }
 
+// Byte / 16-bit / 32-bit fills of the staging buffer (staged_memset).
+inline auto fill8(unsigned char v) {
+  return [v](void* b, size_t bytes, hipStream_t s) { return REAL_HIP(hipMemsetD8Async)((hipDeviceptr_t)b, v, bytes, s); };
+}
+inline auto fill16(unsigned short v) {
+  return [v](void* b, size_t bytes, hipStream_t s) {
+    return REAL_HIP(hipMemsetD16Async)((hipDeviceptr_t)b, v, bytes / 2, s);
+  };
+}
+inline auto fill32(int v) {
+  return [v](void* b, size_t bytes, hipStream_t s) {
+    return REAL_HIP(hipMemsetD32Async)((hipDeviceptr_t)b, v, bytes / 4, s);
+  };
+}
+
 __attribute__((visibility("default"))) hipError_t hipMemset(void* dst, int value, size_t n) {
   HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
+  hipError_t rc;
+  if (staged_memset(dst, n, nullptr, true, &rc, fill8((unsigned char)value))) return rc;
   return after_memset(REAL_HIP(hipMemset)(dst, value, n), dst, n);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemsetAsync(void* dst, int value, size_t n, hipStream_t stream) {
   HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
+  hipError_t rc;
+  if (staged_memset(dst, n, stream, false, &rc, fill8((unsigned char)value))) return rc;
   return after_memset_async(REAL_HIP(hipMemsetAsync)(dst, value, n, stream), dst, n, stream);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemsetD8(hipDeviceptr_t dst, unsigned char v, size_t n) {
   HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
+  hipError_t rc;
+  if (staged_memset(dst, n, nullptr, true, &rc, fill8(v))) return rc;
   return after_memset(REAL_HIP(hipMemsetD8)(dst, v, n), dst, n);
 }
 
@@ -767,12 +820,16 @@ __attribute__((visibility("default"))) hipError_t hipMemsetD8Async(hipDeviceptr_
                                                                    hipStream_t stream) {
   HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
+  hipError_t rc;
+  if (staged_memset(dst, n, stream, false, &rc, fill8(v))) return rc;
   return after_memset_async(REAL_HIP(hipMemsetD8Async)(dst, v, n, stream), dst, n, stream);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemsetD16(hipDeviceptr_t dst, unsigned short v, size_t n) {
   HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
+  hipError_t rc;
+  if (staged_memset(dst, 2 * n, nullptr, true, &rc, fill16(v))) return rc;
   return after_memset(REAL_HIP(hipMemsetD16)(dst, v, n), dst, 2 * n);
 }
 
@@ -780,12 +837,16 @@ __attribute__((visibility("default"))) hipError_t hipMemsetD16Async(hipDeviceptr
                                                                     hipStream_t stream) {
   HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
+  hipError_t rc;
+  if (staged_memset(dst, 2 * n, stream, false, &rc, fill16(v))) return rc;
   return after_memset_async(REAL_HIP(hipMemsetD16Async)(dst, v, n, stream), dst, 2 * n, stream);
 }
 
 __attribute__((visibility("default"))) hipError_t hipMemsetD32(hipDeviceptr_t dst, int v, size_t n) {
   HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
+  hipError_t rc;
+  if (staged_memset(dst, 4 * n, nullptr, true, &rc, fill32(v))) return rc;
   return after_memset(REAL_HIP(hipMemsetD32)(dst, v, n), dst, 4 * n);
 }
 
@@ -793,6 +854,8 @@ __attribute__((visibility("default"))) hipError_t hipMemsetD32Async(hipDeviceptr
                                                                     hipStream_t stream) {
   HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
+  hipError_t rc;
+  if (staged_memset(dst, 4 * n, stream, false, &rc, fill32(v))) return rc;
   return after_memset_async(REAL_HIP(hipMemsetD32Async)(dst, v, n, stream), dst, 4 * n, stream);
 }
 
