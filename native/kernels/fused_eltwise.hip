@@ -178,3 +178,80 @@ VGPU_API int vgpu_add_scale_shift_act_nhwc(const void* a, const void* b, void* s
   }
   return (int)hipGetLastError();
 }
+
+// ---- ReLU backward + bias gradient (training conv + bias + ReLU, VGG-16) ------------
+//   g <- (y > 0) ? dy : 0 ;  db[c] = Σ_rows g[., c]   (fp32, deterministic)
+// One pass over dy and y instead of a threshold kernel and a PyTorch column
+// reduction that re-reads g (12 µs per VGG layer at b=2: profiles/r5/train).
+// Block = one slab of kSlabRows rows: thread t owns channel group t % cv and
+// rows t / cv, t / cv + 256 / cv, ...; lanes of one group are merged through
+// LDS into part[slab][C]; relu_bias_grad_reduce sums the slabs in order.
+namespace {
+constexpr int kSlabRows = 256;
+
+__global__ void __launch_bounds__(kThreads) relu_bias_grad_kernel(const bf16x8* __restrict__ dy,
+                                                                  const bf16x8* __restrict__ y,
+                                                                  bf16x8* __restrict__ g, float* __restrict__ part,
+                                                                  uint64_t rows, uint32_t cv) {
+  __shared__ float red[kThreads][9];  // 8 sums + pad (bank spread)
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = kThreads / cv;  // rows in flight per block pass
+  const uint32_t cg = t % cv, r0 = t / cv;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (r0 < per) {
+    const uint64_t row_lo = (uint64_t)blockIdx.x * kSlabRows;
+    const uint64_t row_hi = row_lo + kSlabRows < rows ? row_lo + kSlabRows : rows;
+    for (uint64_t r = row_lo + r0; r < row_hi; r += per) {
+      const uint64_t i = r * cv + cg;
+      const bf16x8 a = dy[i], b = y[i];
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = bf2f(b.v[j]) > 0.0f ? bf2f(a.v[j]) : 0.0f;
+        o.v[j] = v != 0.0f ? a.v[j] : (uint16_t)0;
+        s[j] += v;
+      }
+      g[i] = o;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[t][j] = s[j];
+  __syncthreads();
+  if (t < cv) {
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (uint32_t k = 0; k < per; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += red[k * cv + t][j];
+    float* out = part + (uint64_t)blockIdx.x * cv * 8 + t * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = a[j];
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) relu_bias_grad_reduce_kernel(const float* __restrict__ part,
+                                                                         float* __restrict__ db, uint32_t c,
+                                                                         uint32_t slabs) {
+  const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= c) return;
+  float a = 0.f;
+  for (uint32_t k = 0; k < slabs; ++k) a += part[(uint64_t)k * c + i];
+  db[i] = a;
+}
+}  // namespace
+
+VGPU_API int64_t vgpu_relu_bias_grad_workspace(uint64_t rows, uint32_t c) {
+  return (int64_t)((rows + kSlabRows - 1) / kSlabRows) * c * 4;
+}
+
+// dy, y, g: [rows, c] bf16 (NHWC); db: fp32 [c]; ws: vgpu_relu_bias_grad_workspace bytes.
+VGPU_API int vgpu_relu_bias_grad_nhwc(const void* dy, const void* y, void* g, float* db, void* ws, uint64_t rows,
+                                      uint32_t c, hipStream_t stream) {
+  if (c % 8 || c / 8 > kThreads || rows == 0) return -1;
+  const uint32_t cv = c / 8;
+  const uint32_t slabs = (uint32_t)((rows + kSlabRows - 1) / kSlabRows);
+  hipLaunchKernelGGL(relu_bias_grad_kernel, dim3(slabs), dim3(kThreads), 0, stream, (const bf16x8*)dy,
+                     (const bf16x8*)y, (bf16x8*)g, (float*)ws, rows, cv);
+  hipLaunchKernelGGL(relu_bias_grad_reduce_kernel, dim3((c + kThreads - 1) / kThreads), dim3(kThreads), 0, stream,
+                     (const float*)ws, db, c, slabs);
+  return (int)hipGetLastError();
+}

@@ -166,3 +166,32 @@ def test_deeplab_native_training_step_matches_torch(gpu_build):
         gt = mt.backbone.features[i].body[-2][0].weight.grad
         print("deeplab block", i, "dw grad cos", round(_cos(g, gt), 4), "rel", round(_rel(g, gt), 4))
         assert _cos(g, gt) > 0.95, i
+
+
+def test_resize_bilinear_backward_matches_pytorch(gpu_build):
+    """The GEMM backward of the bilinear resize (vgpu.ops.interp) against
+    PyTorch's atomic scatter, DeepLab's two shapes, fp32."""
+    from vgpu.ops.interp import resize_bilinear
+    for ih, oh, c in ((24, 384, 21), (1, 24, 256)):
+        x = torch.randn(2, c, ih, ih, device="cuda").contiguous(memory_format=CL).requires_grad_(True)
+        xr = x.detach().clone().requires_grad_(True)
+        y = resize_bilinear(x, (oh, oh))
+        yr = torch.nn.functional.interpolate(xr, size=(oh, oh), mode="bilinear", align_corners=False)
+        torch.testing.assert_close(y, yr)
+        dy = torch.randn_like(yr)
+        y.backward(dy)
+        yr.backward(dy)
+        torch.testing.assert_close(x.grad, xr.grad, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 112, 112), (2, 512, 14, 14), (3, 96, 7, 9), (1, 2048, 3, 3)])
+def test_relu_bias_grad_matches_torch(gpu_build, shape):
+    """One-pass ReLU backward + bias gradient (fused_eltwise.hip) against
+    threshold_backward and an fp32 column sum."""
+    from vgpu.ops.conv import relu_bias_grad
+    dy = _x(shape, 8)
+    y = _x(shape, 9)
+    g, db = relu_bias_grad(dy, y)
+    gt = torch.ops.aten.threshold_backward(dy, y, 0)
+    assert torch.equal(g, gt)
+    torch.testing.assert_close(db, gt.float().sum(dim=(0, 2, 3)), atol=1e-2, rtol=1e-4)

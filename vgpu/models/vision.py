@@ -14,6 +14,7 @@ from torch import nn
 import torch.nn.functional as F
 
 from vgpu.ops.bn import batched_step_counters, bn_act
+from vgpu.ops.interp import resize_bilinear
 
 
 class VGG16(nn.Module):
@@ -199,8 +200,7 @@ class ASPP(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         h, w = x.shape[-2:]
         feats = [b(x) for b in self.branches]
-        feats.append(F.interpolate(self.image_pool(x), size=(h, w), mode="bilinear",
-                                   align_corners=False))
+        feats.append(resize_bilinear(self.image_pool(x), (h, w)))
         return self.project(torch.cat(feats, dim=1))
 
 
@@ -215,7 +215,7 @@ class DeepLabV3(nn.Module):
         h, w = x.shape[-2:]
         with batched_step_counters():
             y = self.head(self.aspp(self.backbone(x)))
-        return F.interpolate(y, size=(h, w), mode="bilinear", align_corners=False)
+        return resize_bilinear(y, (h, w))
 
 
 class LSTMSentiment(nn.Module):

@@ -58,6 +58,10 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_bias_act_nhwc.argtypes = [vp, vp, u64, u32, ctypes.c_int, vp]
     lib.vgpu_scale_shift_act_nhwc.argtypes = [vp, vp, vp, vp, u64, u32, ctypes.c_int, vp]
     lib.vgpu_add_scale_shift_act_nhwc.argtypes = [vp, vp, vp, vp, vp, vp, u64, u32, ctypes.c_int, vp]
+    lib.vgpu_relu_bias_grad_workspace.argtypes = [u64, u32]
+    lib.vgpu_relu_bias_grad_workspace.restype = ctypes.c_int64
+    lib.vgpu_relu_bias_grad_nhwc.argtypes = [vp, vp, vp, vp, vp, u64, u32, vp]
+    lib.vgpu_relu_bias_grad_nhwc.restype = ctypes.c_int
     ci = ctypes.c_int
     lib.vgpu_conv2d_nhwc.argtypes = [vp, vp, vp, vp, vp, vp, vp] + [ci] * 9 + [vp]
     lib.vgpu_maxpool_nhwc.argtypes = [vp, vp] + [ci] * 7 + [vp]

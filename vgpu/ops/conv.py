@@ -506,10 +506,26 @@ class _ConvBiasReLUTrainFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, y = ctx.saved_tensors
-        g = torch.ops.aten.threshold_backward(dy.contiguous(memory_format=_CL), y, 0)
-        db = torch.sum(g, dim=(0, 2, 3), dtype=torch.float32) if ctx.needs_input_grad[2] else None
+        g, db = relu_bias_grad(dy.contiguous(memory_format=_CL), y)
         dx, dw = conv_backward(g, x, w, ctx.stride, ctx.padding, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
-        return dx, dw, db, None, None
+        return dx, dw, db if ctx.needs_input_grad[2] else None, None, None
+
+
+def relu_bias_grad(dy: torch.Tensor, y: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """(g, db): g = dy where y > 0 else 0 (bf16, channels_last), db = Σ g over
+    N, H, W in fp32 -- one pass (native/kernels/fused_eltwise.hip)."""
+    _nhwc(dy, "dy")
+    _nhwc(y, "y")
+    n, c, h, w = y.shape
+    rows = n * h * w
+    lib = load_kernels()
+    g = torch.empty_like(y, memory_format=_CL)
+    db = torch.empty(c, dtype=torch.float32, device=y.device)
+    ws = torch.empty(max(lib.vgpu_relu_bias_grad_workspace(rows, c) // 4, 1), dtype=torch.float32, device=y.device)
+    rc = lib.vgpu_relu_bias_grad_nhwc(_ptr(dy), _ptr(y), _ptr(g), _ptr(db), _ptr(ws), rows, c, _stream())
+    if rc != 0:
+        raise RuntimeError(f"vgpu_relu_bias_grad_nhwc: error {rc}")
+    return g, db
 
 
 def conv_bias_relu_train(x: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor:
