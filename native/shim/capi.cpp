@@ -184,8 +184,9 @@ __attribute__((visibility("default"))) void vgpu_self_vmem_stats(uint64_t out[5]
 }
 
 // VMM suspend vehicle (vmm.cpp): ranges, bytes, evicted bytes, last suspend /
-// resume ns, completed suspend-resume cycles.
-__attribute__((visibility("default"))) void vgpu_self_vmm_stats(uint64_t out[6]) {
+// resume ns, completed suspend-resume cycles, the last suspend's pinning ns and
+// the last resume's re-mapping ns.
+__attribute__((visibility("default"))) void vgpu_self_vmm_stats(uint64_t out[8]) {
   ensure_init();
   vmm_stats(out);
 }

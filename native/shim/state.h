@@ -218,7 +218,7 @@ hipError_t vmm_alloc(void** ptr, size_t size, int dev);
 bool vmm_free(void* p);                 // unmap + release + free the VA; false if not ours
 bool vmm_owns(const void* p);
 void vmm_ipc_exported(const void* p);   // never evict a range another process may map
-void vmm_stats(uint64_t out[6]);        // ranges, bytes, evicted bytes, suspend ns, resume ns, cycles
+void vmm_stats(uint64_t out[8]);  // ranges, bytes, evicted bytes, suspend ns, resume ns, cycles, pin ns, map ns
 void vmm_after_fork();
 void vmem_book_move(int dev, uint64_t bytes, bool to_gpu);
 extern std::atomic<int> g_vmm_live;

@@ -51,6 +51,69 @@ struct Range {
 std::mutex g_mu;  // g_ranges and every Range in it
 std::map<uintptr_t, Range> g_ranges;
 std::atomic<uint64_t> g_bytes{0}, g_evicted{0}, g_suspend_ns{0}, g_resume_ns{0}, g_cycles{0};
+std::atomic<uint64_t> g_pin_ns{0}, g_map_ns{0};  // last suspend's pinning, last resume's re-mapping
+
+// VGPU_SUSPEND_HOST_RESERVE=true: keep pinned 1 GiB chunks for every mapped
+// GiB, pinned in the background while the pod runs and reused across
+// suspends, so a suspend only copies.  Getting fresh pinned host memory runs
+// at ~23 GB/s on MI355X nodes whatever the thread count (64 GiB: 2.8 s;
+// scripts/pin_probe.py, profiles/r5/vmem) -- more than the copy itself
+// (1.2 s).  The price is host memory equal to the pod's VMM bytes.
+std::mutex g_pool_mu;
+std::vector<void*> g_pool;
+
+bool reserve_on() {
+  static const bool on = env_bool(env_first("VGPU_SUSPEND_HOST_RESERVE"), false);
+  return on;
+}
+
+void* host_chunk(size_t c) {
+  if (c == kChunk) {
+    std::lock_guard<std::mutex> l(g_pool_mu);
+    if (!g_pool.empty()) {
+      void* p = g_pool.back();
+      g_pool.pop_back();
+      return p;
+    }
+  }
+  void* p = nullptr;
+  if (REAL_HIP(hipHostMalloc)(&p, c, hipHostMallocDefault) != hipSuccess || !p) {
+    (void)REAL_HIP(hipGetLastError)();
+    return nullptr;
+  }
+  return p;
+}
+
+void release_chunk(void* p, size_t c) {
+  if (reserve_on() && c == kChunk) {
+    std::lock_guard<std::mutex> l(g_pool_mu);
+    g_pool.push_back(p);
+    return;
+  }
+  (void)REAL_HIP(hipHostFree)(p);
+}
+
+// One more pooled chunk if the pool is short of the mapped whole GiBs; false
+// when nothing was needed.
+bool grow_reserve() {
+  uint64_t need = 0;
+  {
+    std::lock_guard<std::mutex> l(g_mu);
+    for (auto& e : g_ranges) need += e.second.size / kChunk;
+  }
+  {
+    std::lock_guard<std::mutex> l(g_pool_mu);
+    if (g_pool.size() >= need) return false;
+  }
+  void* p = nullptr;
+  if (REAL_HIP(hipHostMalloc)(&p, kChunk, hipHostMallocDefault) != hipSuccess || !p) {
+    (void)REAL_HIP(hipGetLastError)();
+    return false;
+  }
+  std::lock_guard<std::mutex> l(g_pool_mu);
+  g_pool.push_back(p);
+  return true;
+}
 
 // Per-thread "inside a gated hook" flags (HookScope): the evict thread waits
 // for all of them after closing the gate, so no launch or copy that passed
@@ -142,10 +205,17 @@ void wait_hooks() {
     while (f->in.load(std::memory_order_acquire)) sleep_ns(20000);
 }
 
-hipStream_t copy_stream(int dev) {
-  static hipStream_t s[VGPU_MAX_DEVICES] = {};
-  if (!s[dev] && REAL_HIP(hipStreamCreateWithFlags)(&s[dev], hipStreamNonBlocking) != hipSuccess) s[dev] = nullptr;
-  return s[dev];
+// Two copy streams per device: consecutive chunks alternate between them, so
+// two SDMA engines share the host link.
+constexpr int kStreams = 2;
+hipStream_t copy_stream(int dev, int k) {
+  static hipStream_t s[VGPU_MAX_DEVICES][kStreams] = {};
+  if (!s[dev][k] && REAL_HIP(hipStreamCreateWithFlags)(&s[dev][k], hipStreamNonBlocking) != hipSuccess)
+    s[dev][k] = nullptr;
+  return s[dev][k];
+}
+void sync_streams(int dev) {
+  for (int k = 0; k < kStreams; ++k) (void)REAL_HIP(hipStreamSynchronize)(copy_stream(dev, k));
 }
 
 void evict() {
@@ -155,34 +225,36 @@ void evict() {
   const uint64_t t0 = mono_ns();
   std::lock_guard<std::mutex> l(g_mu);
   per_device([](int) { (void)REAL_HIP(hipDeviceSynchronize)(); });
-  uint64_t moved = 0;
+  uint64_t moved = 0, pin_ns = 0;
   bool short_of_host = false;
   per_device([&](int dev) {
-    hipStream_t s = copy_stream(dev);
+    int k = 0;
     for (auto& e : g_ranges) {
       Range& r = e.second;
       if (r.dev != dev || !r.h || r.ipc || short_of_host) continue;
       for (size_t off = 0; off < r.size; off += kChunk) {
         const size_t c = std::min(kChunk, r.size - off);
-        void* p = nullptr;
-        if (REAL_HIP(hipHostMalloc)(&p, c, hipHostMallocDefault) != hipSuccess || !p) {
-          (void)REAL_HIP(hipGetLastError)();
+        const uint64_t p0 = mono_ns();
+        void* p = host_chunk(c);
+        pin_ns += mono_ns() - p0;
+        if (!p) {
           short_of_host = true;
           break;
         }
         r.host.emplace_back(p, c);
         // Pinning the next chunk overlaps this copy.
-        (void)REAL_HIP(hipMemcpyAsync)(p, (const char*)r.va + off, c, hipMemcpyDeviceToHost, s);
+        (void)REAL_HIP(hipMemcpyAsync)(p, (const char*)r.va + off, c, hipMemcpyDeviceToHost,
+                                       copy_stream(dev, k++ % kStreams));
       }
     }
-    (void)REAL_HIP(hipStreamSynchronize)(s);
+    sync_streams(dev);
     for (auto& e : g_ranges) {
       Range& r = e.second;
       if (r.dev != dev || !r.h || r.ipc) continue;
       size_t held = 0;
       for (auto& c : r.host) held += c.second;
       if (held != r.size) {  // host memory ran out part-way: this range stays
-        for (auto& c : r.host) (void)REAL_HIP(hipHostFree)(c.first);
+        for (auto& c : r.host) release_chunk(c.first, c.second);
         r.host.clear();
         continue;
       }
@@ -193,6 +265,7 @@ void evict() {
   });
   if (short_of_host) VLOG_WARN("vmm: host memory ran out while evicting; some ranges stay in HBM");
   g_evicted.store(moved);
+  g_pin_ns.store(pin_ns);
   g_suspend_ns.store(mono_ns() - t0);
   VLOG_INFO("vmm: suspended, %llu bytes of HBM released in %.3f s", (unsigned long long)moved,
             (mono_ns() - t0) / 1e9);
@@ -200,29 +273,33 @@ void evict() {
 
 void restore() {
   const uint64_t t0 = mono_ns();
+  uint64_t map_ns = 0;
   std::vector<std::pair<void*, size_t>> to_free;
   {
     std::lock_guard<std::mutex> l(g_mu);
     per_device([&](int dev) {
-      hipStream_t s = copy_stream(dev);
+      int k = 0;
       for (auto& e : g_ranges) {
         Range& r = e.second;
         if (r.dev != dev || r.h) continue;
         // HBM taken meanwhile by someone else: keep trying, the gate stays closed.
         hipError_t rc;
+        const uint64_t m0 = mono_ns();
         while ((rc = map_range(r)) != hipSuccess) {
           (void)REAL_HIP(hipGetLastError)();
           VLOG_WARN("vmm: cannot map %zu bytes back at %p (error %d); retrying", r.size, (void*)r.va, (int)rc);
           sleep_ns(100000000ull);
         }
+        map_ns += mono_ns() - m0;
         size_t off = 0;
         for (auto& c : r.host) {
-          (void)REAL_HIP(hipMemcpyAsync)((char*)r.va + off, c.first, c.second, hipMemcpyHostToDevice, s);
+          (void)REAL_HIP(hipMemcpyAsync)((char*)r.va + off, c.first, c.second, hipMemcpyHostToDevice,
+                                         copy_stream(dev, k++ % kStreams));
           off += c.second;
         }
         vmem_book_move(dev, r.size, true);
       }
-      (void)REAL_HIP(hipStreamSynchronize)(s);
+      sync_streams(dev);
       for (auto& e : g_ranges) {
         Range& r = e.second;
         if (r.dev != dev) continue;
@@ -232,11 +309,12 @@ void restore() {
     });
   }
   g_resume_ns.store(mono_ns() - t0);
+  g_map_ns.store(map_ns);
   g_evicted.store(0);
   g_cycles.fetch_add(1);
   st().vmm_evicted.store(0, std::memory_order_seq_cst);  // the gate opens with the data back
   VLOG_INFO("vmm: resumed in %.3f s", (mono_ns() - t0) / 1e9);
-  for (auto& c : to_free) (void)REAL_HIP(hipHostFree)(c.first);
+  for (auto& c : to_free) release_chunk(c.first, c.second);
 }
 
 void evict_main() {
@@ -255,6 +333,9 @@ void evict_main() {
     } else if (!sus && out) {
       restore();
       out = false;
+    } else if (!sus && reserve_on()) {
+      while (!S.suspended.load(std::memory_order_relaxed) && grow_reserve()) {
+      }
     }
   }
 }
@@ -313,7 +394,7 @@ bool vmm_free(void* p) {
   if (it == g_ranges.end()) return false;
   Range& r = it->second;
   unmap_range(r);
-  for (auto& c : r.host) (void)REAL_HIP(hipHostFree)(c.first);
+  for (auto& c : r.host) release_chunk(c.first, c.second);
   (void)REAL_HIP(hipMemAddressFree)((void*)r.va, r.size);
   g_bytes.fetch_sub(r.size);
   g_ranges.erase(it);
@@ -359,7 +440,7 @@ std::atomic<int>* vmm_hook_enter() {
 
 bool vmm_in_scope() { return tl_flag && tl_flag->in.load(std::memory_order_relaxed); }
 
-void vmm_stats(uint64_t out[6]) {
+void vmm_stats(uint64_t out[8]) {
   std::lock_guard<std::mutex> l(g_mu);
   out[0] = g_ranges.size();
   out[1] = g_bytes.load();
@@ -367,6 +448,8 @@ void vmm_stats(uint64_t out[6]) {
   out[3] = g_suspend_ns.load();
   out[4] = g_resume_ns.load();
   out[5] = g_cycles.load();
+  out[6] = g_pin_ns.load();
+  out[7] = g_map_ns.load();
 }
 
 void vmm_after_fork() {

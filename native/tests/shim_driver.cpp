@@ -838,7 +838,7 @@ int main(int argc, char** argv) {
     auto host_bytes = [&]() -> unsigned long long {
       return ((vgpu_shared_region_t*)self_region())->procs[self_slot()].used[dev].host_bytes;
     };
-    uint64_t v[6];
+    uint64_t v[8];
     void* p = nullptr;
     void* small = nullptr;
     int ra = hipMalloc(&p, 96 * M), rs = hipMalloc(&small, 8 * M);

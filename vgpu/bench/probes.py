@@ -735,11 +735,12 @@ def evictee(gib: int = 64, block_gib: int = 4) -> dict:
     def stats():
         v = (ctypes.c_uint64 * 5)()
         lib.vgpu_self_vmem_stats(v)
-        m = (ctypes.c_uint64 * 6)()
+        m = (ctypes.c_uint64 * 8)()
         lib.vgpu_self_vmm_stats(m)  # the VMM vehicle (VGPU_SUSPEND_VMM, default with VGPU_SUSPEND_EVICT)
         return {"swap_in": v[0], "swap_out": v[1], "moves": v[2], "in_hbm": v[3], "ranges": v[4],
                 "host_bytes": int(host_bytes(0)), "vmm_ranges": m[0], "vmm_bytes": m[1], "vmm_evicted": m[2],
-                "vmm_suspend_s": round(m[3] / 1e9, 3), "vmm_resume_s": round(m[4] / 1e9, 3), "vmm_cycles": m[5]}
+                "vmm_suspend_s": round(m[3] / 1e9, 3), "vmm_resume_s": round(m[4] / 1e9, 3), "vmm_cycles": m[5],
+                "vmm_pin_s": round(m[6] / 1e9, 3), "vmm_map_s": round(m[7] / 1e9, 3)}
 
     blocks = []
     for i in range(gib // block_gib):
