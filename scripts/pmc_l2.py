@@ -38,7 +38,7 @@ def main() -> int:
     for f, (n, ns, req, hit, miss) in agg.items():
         gb = req * 128 / 1e9
         print(f"| {f} | {n} | {ns / 1e3:.1f} | {req / 1e6:.2f} | {100 * hit / max(hit + miss, 1):.1f} | "
-              f"{gb:.2f} | {gb / max(ns, 1) * 1e9 / 1e12:.2f} |")
+              f"{gb:.2f} | {gb / max(ns, 1) * 1e6:.2f} |")
     return 0
 
 
