@@ -429,17 +429,18 @@ __device__ __forceinline__ void mma_k64(const char* sA, const char* sB, int arow
 // coalesced bias + residual + act + store.  The residual loads of a half
 // overlap its accumulator staging.  Needs (BM/2)·(BN+4)·4 bytes of LDS and a
 // block-wide barrier behind the last read of the pipeline stages.
-template <int BM, int BN>
+// NT: threads of the workgroup (conv23 also runs 512-thread tiles).
+template <int BM, int BN, int NT = kThreads>
 struct EpiShape {
-  static constexpr int HROWS = BM / 2, CPR = BN / 8, RSTEP = kThreads / CPR, RROWS = HROWS / RSTEP;
+  static constexpr int HROWS = BM / 2, CPR = BN / 8, RSTEP = NT / CPR, RROWS = HROWS / RSTEP;
 };
 
 // Residual rows this thread adds in the epilogue (both halves), issued early —
 // before the first DMA of the K loop — so their latency hides behind the loop.
-template <int BM, int BN, bool STRIDED = false>
+template <int BM, int BN, bool STRIDED = false, int NT = kThreads>
 __device__ __forceinline__ void load_residual(const ConvArgs& a, int m0, int n0,
-                                              u32x4 (&res)[2][EpiShape<BM, BN>::RROWS]) {
-  using E = EpiShape<BM, BN>;
+                                              u32x4 (&res)[2][EpiShape<BM, BN, NT>::RROWS]) {
+  using E = EpiShape<BM, BN, NT>;
   const int t = threadIdx.x, chunk = t % E::CPR, rfirst = t / E::CPR;
   const bool strided = STRIDED && a.res_stride == 2;
   const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
@@ -462,13 +463,18 @@ __device__ __forceinline__ void load_residual(const ConvArgs& a, int m0, int n0,
 
 // ST (BatchNorm statistics, ConvArgs::stats): 0 none, 1 forward (of the stored
 // values), 2 backward (masked by the BN's activation derivative; ConvArgs::bnx).
-template <int BM, int BN, bool RES, int ST = 0>
-__device__ __forceinline__ void epilogue_halves(const ConvArgs& a, f32x4_t (&acc)[BM / 32][BN / 32],
+// NT threads = (NT / 128) x 2 waves; each row half is staged by the wave rows
+// that own it.
+template <int BM, int BN, bool RES, int ST = 0, int NT = kThreads>
+__device__ __forceinline__ void epilogue_halves(const ConvArgs& a,
+                                                f32x4_t (&acc)[BM / (NT / 128) / 16][BN / 32],
                                                 int m0, int n0, char* smem,
-                                                const u32x4 (&res)[2][EpiShape<BM, BN>::RROWS]) {
-  constexpr int WTM = BM / 2, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
+                                                const u32x4 (&res)[2][EpiShape<BM, BN, NT>::RROWS]) {
+  static_assert(ST == 0 || NT == kThreads, "statistics: 256-thread tiles");
+  constexpr int WGM = NT / 128, WPH = WGM / 2;  // wave rows, wave rows per half
+  constexpr int WTM = BM / WGM, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
   constexpr int CS = BN + 4, HROWS = BM / 2;
-  constexpr int CPR = BN / 8, RSTEP = kThreads / CPR, RROWS = HROWS / RSTEP;
+  constexpr int CPR = BN / 8, RSTEP = NT / CPR, RROWS = HROWS / RSTEP;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fk = lane >> 4;
   const int chunk = t % CPR, rfirst = t / CPR;
@@ -512,14 +518,15 @@ __device__ __forceinline__ void epilogue_halves(const ConvArgs& a, f32x4_t (&acc
   float2* sS = reinterpret_cast<float2*>(smem + HROWS * CS * 4);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    if (wm == h) {
+    if (wm / WPH == h) {
+      const int r0 = (wm % WPH) * WTM;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            sC[(i * 16 + fk * 4 + e) * CS + wn * WTN + j * 16 + fr] = acc[i][j][e];
+            sC[(r0 + i * 16 + fk * 4 + e) * CS + wn * WTN + j * 16 + fr] = acc[i][j][e];
     }
     __syncthreads();
 #pragma unroll
@@ -1555,14 +1562,16 @@ hipError_t dispatch_pro(const ConvArgs& a, bool res, hipStream_t s) {
 // rounded to bf16 exactly as conv_pro's prologue stages it) for this thread's
 // rows, into registers; s/t are read from LDS (sPs/sPt), never from global
 // memory, for the same reason.
-template <int BM, int BN, bool NEXT, typename Mid>
-__device__ __forceinline__ void tail_epilogue(const ConvArgs& a, f32x4_t (&acc)[BM / 32][BN / 32], int m0, int n0,
-                                              char* smem, const u32x4 (&res)[2][EpiShape<BM, BN>::RROWS],
+template <int BM, int BN, bool NEXT, int NT = kThreads, typename Mid>
+__device__ __forceinline__ void tail_epilogue(const ConvArgs& a, f32x4_t (&acc)[BM / (NT / 128) / 16][BN / 32],
+                                              int m0, int n0, char* smem,
+                                              const u32x4 (&res)[2][EpiShape<BM, BN, NT>::RROWS],
                                               const float* sPs, const float* sPt,
-                                              u32x4 (&pv)[2][EpiShape<BM, BN>::RROWS], Mid mid) {
-  constexpr int WTM = BM / 2, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
+                                              u32x4 (&pv)[2][EpiShape<BM, BN, NT>::RROWS], Mid mid) {
+  constexpr int WGM = NT / 128, WPH = WGM / 2;
+  constexpr int WTM = BM / WGM, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
   constexpr int CS = BN + 4, HROWS = BM / 2;
-  using E = EpiShape<BM, BN>;
+  using E = EpiShape<BM, BN, NT>;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fk = lane >> 4;
   const int chunk = t % E::CPR, rfirst = t / E::CPR;
@@ -1580,14 +1589,15 @@ __device__ __forceinline__ void tail_epilogue(const ConvArgs& a, f32x4_t (&acc)[
   float* sC = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    if (wm == h) {
+    if (wm / WPH == h) {
+      const int r0 = (wm % WPH) * WTM;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            sC[(i * 16 + fk * 4 + e) * CS + wn * WTN + j * 16 + fr] = acc[i][j][e];
+            sC[(r0 + i * 16 + fk * 4 + e) * CS + wn * WTN + j * 16 + fr] = acc[i][j][e];
     }
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     __builtin_amdgcn_s_barrier();
@@ -1656,12 +1666,19 @@ __device__ __forceinline__ void tail_epilogue(const ConvArgs& a, f32x4_t (&acc)[
 // block accumulates in registers across the chunks.  Saves the next block's
 // re-read of the 4W-wide activation (stage 1 at b=50: 194 MB per block).
 // Numerics equal conv23 + conv_pro (same bf16 roundings, same K order).
-template <int BM, int W, bool NEXT = false, int NS1 = 3>
-__global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, const ConvArgs b,
-                                                             const ConvArgs c) {
+// NT = 512 (stage 2, BM 128): eight waves as a 4 x 2 grid, each with the
+// same 32 x 64 sub-tile as the 256-thread BM-64 form, so the conv2 / conv3 /
+// conv1 weight panels a CU pulls through L2 serve twice the rows (they are
+// ~70 % of the tail's 1.1-1.4 GB of L2 traffic per call,
+// profiles/r5/kernels/pmc_l2_r5.md) at the same eight waves per CU.
+template <int BM, int W, bool NEXT = false, int NS1 = 3, int NT = kThreads>
+__global__ void __launch_bounds__(NT, 512 / NT) conv23_kernel(const ConvArgs a, const ConvArgs b,
+                                                              const ConvArgs c) {
   constexpr int KCH = W / 64;                // conv3 K chunks (64 channels each)
-  constexpr int AR = BM / 32, BR = W / 32;   // phase-1 DMA instructions per thread per step
-  constexpr int WTM = BM / 2, WTN = W / 2;
+  constexpr int RPI = NT / 8;                // LDS rows per DMA instruction
+  constexpr int WGM = NT / 128;              // wave rows (x 2 wave columns)
+  constexpr int AR = BM / RPI, BR = W / RPI; // phase-1 DMA instructions per thread per step
+  constexpr int WTM = BM / WGM, WTN = W / 2;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int A_BYTES = BM * 128, B_BYTES = W * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
@@ -1678,7 +1695,7 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
   // LDS: a global load in phase 2 would make hipcc drain the in-flight DMA.
   constexpr int PAR = (W + (NEXT ? 8 * W : 0)) * 4;
   static_assert(P + PAR <= 160 * 1024, "conv23: LDS");
-  static_assert((BM == 128 && W == 128) || 2 * (P + PAR) <= 160 * 1024, "conv23: two workgroups per CU");
+  static_assert(NT == 512 || 2 * (P + PAR) <= 160 * 1024, "conv23: two workgroups per CU");
   __shared__ __attribute__((aligned(16))) char smem[P + PAR];
   char* sA2 = smem + B2_BYTES + EPI;
   float* sPar = reinterpret_cast<float*>(smem + P);
@@ -1701,7 +1718,7 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
   bool aok[AR];
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
-    const int m = m0 + lrow + 32 * i;
+    const int m = m0 + lrow + RPI * i;
     aok[i] = m < a.M;
     const int mm = aok[i] ? m : 0;
     const int ow = mm % a.OW, t2 = mm / a.OW, oh = t2 % a.OH, n = t2 / a.OH;
@@ -1710,10 +1727,10 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
     abase[i] = ((n * a.H + aih[i]) * a.W + aiw[i]) * a.C * 2;
   }
   const uint32_t boff = (uint32_t)((lrow * a.K + lchunk * 8) * 2);
-  for (int i = t * 4; i < W; i += kThreads * 4)
+  for (int i = t * 4; i < W; i += NT * 4)
     *reinterpret_cast<float4*>(sPar + i) = *reinterpret_cast<const float4*>(a.bias + i);
   if constexpr (NEXT) {
-    for (int i = t * 4; i < 4 * W; i += kThreads * 4) {
+    for (int i = t * 4; i < 4 * W; i += NT * 4) {
       *reinterpret_cast<float4*>(sPar + W + i) = *reinterpret_cast<const float4*>(c.pscale + i);
       *reinterpret_cast<float4*>(sPar + 5 * W + i) = *reinterpret_cast<const float4*>(c.pshift + i);
     }
@@ -1731,14 +1748,14 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
       const int ih = aih[i] + kh, iw = aiw[i] + kw;
       const bool v = aok[i] & ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          xr, (lds_void_t*)(sA + (32 * i + wave * 8) * 128), 16,
+          xr, (lds_void_t*)(sA + (RPI * i + wave * 8) * 128), 16,
           v ? (uint32_t)(abase[i] + toff) : kOOB, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          wr, (lds_void_t*)(sB + (32 * i + wave * 8) * 128), 16,
-          boff + (uint32_t)((32 * i * a.K + kt * BK) * 2), 0, 0, 0);
+          wr, (lds_void_t*)(sB + (RPI * i + wave * 8) * 128), 16,
+          boff + (uint32_t)((RPI * i * a.K + kt * BK) * 2), 0, 0, 0);
   };
 
   // ---- phase 1: conv2 --------------------------------------------------------------
@@ -1802,9 +1819,9 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
   // stores are unconditional, so their count is exact.  w1 goes through
   // registers because hipcc drains every in-flight LDS-DMA at the next
   // ds_write, and the epilogue and the A3 image are all ds_writes.
-  using E2 = EpiShape<BM, 128>;
+  using E2 = EpiShape<BM, 128, NT>;
   constexpr int R = 2 * E2::RROWS;  // residual loads = y stores per thread per chunk
-  constexpr int WTM2 = BM / 2, TM2 = WTM2 / 16;
+  constexpr int WTM2 = BM / WGM, TM2 = WTM2 / 16;
   char* sB2 = smem;
   char* sE = smem + B2_BYTES;
   const int nchunks = b.Cout / BN2;
@@ -1812,16 +1829,16 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
 #pragma unroll
     for (int kc = 0; kc < KCH; ++kc)
 #pragma unroll
-      for (int i = 0; i < BN2 / 32; ++i)
+      for (int i = 0; i < BN2 / RPI; ++i)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            w3r, (lds_void_t*)(sB2 + kc * (BN2 * 128) + (32 * i + wave * 8) * 128), 16,
-            (uint32_t)(((ch * BN2 + lrow + 32 * i) * b.K + kc * 64 + lchunk * 8) * 2), 0, 0, 0);
+            w3r, (lds_void_t*)(sB2 + kc * (BN2 * 128) + (RPI * i + wave * 8) * 128), 16,
+            (uint32_t)(((ch * BN2 + lrow + RPI * i) * b.K + kc * 64 + lchunk * 8) * 2), 0, 0, 0);
   };
   u32x4 res[2][E2::RROWS];
   // res(0) flies while the conv2 tile is turned into conv3's A image; w3(0)
   // goes into the (free) phase-1 stages after that image's ds_writes, which
   // would otherwise drain it.
-  load_residual<BM, BN2>(b, m0, 0, res);
+  load_residual<BM, BN2, false, NT>(b, m0, 0, res);
 
   // conv2 bias + ReLU → bf16 → conv3's A image: lane (fr, fk) of subtile (i, j)
   // holds row i*16+fr (+wave offset), channels j*16+fk*4 .. +3.
@@ -1843,7 +1860,7 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
   issue_w3(0);
 
   // phase 3 (NEXT): conv1 of the next block, W outputs per row, K = 4W
-  constexpr int TM3 = BM / 32, TN3 = W / 32;
+  constexpr int TM3 = BM / WGM / 16, TN3 = W / 32;
   f32x4_t acc3[TM3][TN3];
   if constexpr (NEXT) {
 #pragma unroll
@@ -1883,21 +1900,21 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
     u32x4 pv[2][E2::RROWS];
     if constexpr (!NEXT) {
       const bool more = ch + 1 < nchunks;
-      tail_epilogue<BM, BN2, false>(b, acc2, m0, c0, sE, res, sPar, sPar, pv, [&] {
+      tail_epilogue<BM, BN2, false, NT>(b, acc2, m0, c0, sE, res, sPar, sPar, pv, [&] {
         if (more) issue_w3(ch + 1);
       });
-      if (more) load_residual<BM, BN2>(b, m0, c0 + BN2, res);
+      if (more) load_residual<BM, BN2, false, NT>(b, m0, c0 + BN2, res);
     } else {
       // conv1's weight K chunk [W rows][c0 .. c0+127] (two 64-wide K panels of
       // W rows), in flight in registers behind the epilogue.
-      u32x4 w1v[2][W / 32];
+      u32x4 w1v[2][W / RPI];
 #pragma unroll
       for (int kc = 0; kc < 2; ++kc)
 #pragma unroll
-        for (int i = 0; i < W / 32; ++i)
+        for (int i = 0; i < W / RPI; ++i)
           w1v[kc][i] = __builtin_amdgcn_raw_buffer_load_b128(
-              w1r, (uint32_t)(((lrow + 32 * i) * c.K + c0 + kc * 64 + (t & 7) * 8) * 2), 0, 0);
-      tail_epilogue<BM, BN2, true>(b, acc2, m0, c0, sE, res, sPar + W, sPar + 5 * W, pv, [] {});
+              w1r, (uint32_t)(((lrow + RPI * i) * c.K + c0 + kc * 64 + (t & 7) * 8) * 2), 0, 0);
+      tail_epilogue<BM, BN2, true, NT>(b, acc2, m0, c0, sE, res, sPar + W, sPar + 5 * W, pv, [] {});
       // A3 image (BM rows x 128 channels = two 64-wide swizzled panels) in the
       // staging area, which the epilogue has finished reading.
       {
@@ -1913,27 +1930,29 @@ __global__ void __launch_bounds__(kThreads, 2) conv23_kernel(const ConvArgs a, c
 #pragma unroll
       for (int kc = 0; kc < 2; ++kc)
 #pragma unroll
-        for (int i = 0; i < W / 32; ++i)
-          *reinterpret_cast<u32x4*>(sB2 + kc * (W * 128) + swz(lrow + 32 * i, t & 7)) = w1v[kc][i];
+        for (int i = 0; i < W / RPI; ++i)
+          *reinterpret_cast<u32x4*>(sB2 + kc * (W * 128) + swz(lrow + RPI * i, t & 7)) = w1v[kc][i];
       __builtin_amdgcn_s_waitcnt(kLgkm0);
       __builtin_amdgcn_s_barrier();  // A3 written, conv1 weight chunk visible
 #pragma unroll
       for (int kc = 0; kc < 2; ++kc)
-        mma_k64<TM3, TN3>(sE + kc * (BM * 128), sB2 + kc * (W * 128), wm * (BM / 2), wn * (W / 2), fr, fk,
+        mma_k64<TM3, TN3>(sE + kc * (BM * 128), sB2 + kc * (W * 128), wm * (BM / WGM), wn * (W / 2), fr, fk,
                           acc3);
       __builtin_amdgcn_s_waitcnt(kLgkm0);
       __builtin_amdgcn_s_barrier();  // A3 / weight chunk read before the next chunk reuses them
       if (ch + 1 < nchunks) {
         issue_w3(ch + 1);
-        load_residual<BM, BN2>(b, m0, c0 + BN2, res);
+        load_residual<BM, BN2, false, NT>(b, m0, c0 + BN2, res);
       }
     }
   }
   if constexpr (NEXT) {
-    u32x4 none[2][EpiShape<BM, W>::RROWS];
-    epilogue_halves<BM, W, false>(c, acc3, m0, 0, smem, none);
+    u32x4 none[2][EpiShape<BM, W, NT>::RROWS];
+    epilogue_halves<BM, W, false, 0, NT>(c, acc3, m0, 0, smem, none);
   }
 }
+
+int g_conv23_wide = -1;  // vgpu_conv23_set_wide: -1 = env VGPU_CONV23_WIDE
 
 // CUs this process can occupy on the current device — the grid-fill term of
 // the tile choice.  A vGPU pod owns an XCD-balanced CU mask of
@@ -2363,8 +2382,9 @@ static int conv23_impl(const void* x, const void* w2, const float* b2, const voi
       e.y = cn.y + (int64_t)n0 * (hi / 2);
       e.y_bytes = (uint32_t)(nb * hi);
     }
-    static const bool bm128 = getenv("VGPU_CONV23_BM128") && atoi(getenv("VGPU_CONV23_BM128")) == 1;  // A/B
-    const int bm = C == 64 || bm128 ? 128 : 64;
+    if (g_conv23_wide < 0) g_conv23_wide = getenv("VGPU_CONV23_WIDE") && atoi(getenv("VGPU_CONV23_WIDE")) == 1;
+    const bool wide = g_conv23_wide == 1;  // A/B: stage 2 on 512-thread 128-row tiles
+    const int bm = C == 64 || wide ? 128 : 64;
     c.nM = (c.M + bm - 1) / bm; c.nN = 1; c.nwg = c.nM;
     static const bool ns2 = getenv("VGPU_CONV23_NS") && atoi(getenv("VGPU_CONV23_NS")) == 2;  // A/B
 #define VGPU_C23(BM_, W_, NX_)                                                                          \
@@ -2377,9 +2397,11 @@ static int conv23_impl(const void* x, const void* w2, const float* b2, const voi
     if (C == 64) {
       if (next) VGPU_C23(128, 64, true);
       else VGPU_C23(128, 64, false);
-    } else if (bm128) {
-      if (next) VGPU_C23(128, 128, true);
-      else VGPU_C23(128, 128, false);
+    } else if (wide) {  // 512-thread 128-row tiles
+      if (next)
+        hipLaunchKernelGGL((conv23_kernel<128, 128, true, 3, 512>), dim3(c.nwg), dim3(512), 0, s, c, d, e);
+      else
+        hipLaunchKernelGGL((conv23_kernel<128, 128, false, 3, 512>), dim3(c.nwg), dim3(512), 0, s, c, d, e);
     } else {
       if (next) VGPU_C23(64, 128, true);
       else VGPU_C23(64, 128, false);
@@ -2390,6 +2412,8 @@ static int conv23_impl(const void* x, const void* w2, const float* b2, const voi
   }
   return 0;
 }
+
+VGPU_API void vgpu_conv23_set_wide(int on) { g_conv23_wide = on < 0 ? -1 : (on ? 1 : 0); }
 
 VGPU_API int vgpu_conv23_nhwc(const void* x, const void* w2, const float* b2, const void* w3,
                               const void* res, void* y, int N, int H, int W, int C, int stride,

@@ -413,6 +413,12 @@ def test_suspend_evict_gives_64gb_to_a_high_priority_pod(gpu_build, vehicle):
                             "torch.cuda.synchronize(); print('HELD', n)", str(want_gib)],
                            capture_output=True, text=True, timeout=300, cwd=REPO)
         assert r.returncode == 0 and f"HELD {want_gib}" in r.stdout, r.stderr[-3000:]
+        # the driver hands the exited pod's VRAM back asynchronously (clearing
+        # it): resume once it is free again, so the resume time is the vehicle's
+        t0 = time.time()
+        while time.time() - t0 < 120 and total - _vram_used()[1] < free0 + 60 * GiB:
+            time.sleep(0.5)
+        print("VRAM back after the high-priority pod in", round(time.time() - t0, 2), "s")
         a.send_signal(signal.SIGUSR1)
         a.stdin.write("VERIFY\n")
         a.stdin.flush()

@@ -97,9 +97,8 @@ def test_vgg16_native_training_step_matches_fp32(gpu_build):
     for i in convs[1:]:
         g, gt = m.features[i].weight.grad, mt.features[i].weight.grad
         print("vgg conv", i, "cos", round(_cos(g, gt), 4), "rel", round(_rel(g, gt), 4))
-        assert _cos(g, gt) > 0.95, i
-        assert _cos(m.features[i].bias.grad, mt.features[i].bias.grad) > 0.95, i
-    assert _rel(m.features[convs[-1]].weight.grad, mt.features[convs[-1]].weight.grad) < 0.05
+        assert _cos(g, gt) > 0.97, i
+        assert _cos(m.features[i].bias.grad, mt.features[i].bias.grad) > 0.97, i
 
 
 DW_CASES = [  # n, c, h, w, stride, dilation
