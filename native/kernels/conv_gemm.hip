@@ -1666,11 +1666,11 @@ __device__ __forceinline__ void tail_epilogue(const ConvArgs& a, f32x4_t (&acc)[
 // block accumulates in registers across the chunks.  Saves the next block's
 // re-read of the 4W-wide activation (stage 1 at b=50: 194 MB per block).
 // Numerics equal conv23 + conv_pro (same bf16 roundings, same K order).
-// NT = 512 (stage 2, BM 128): eight waves as a 4 x 2 grid, each with the
-// same 32 x 64 sub-tile as the 256-thread BM-64 form, so the conv2 / conv3 /
-// conv1 weight panels a CU pulls through L2 serve twice the rows (they are
-// ~70 % of the tail's 1.1-1.4 GB of L2 traffic per call,
-// profiles/r5/kernels/pmc_l2_r5.md) at the same eight waves per CU.
+// NT: the workgroup runs (NT / 128) x 2 waves of 32 x 64 (or 64 x 64) sub-tiles.
+// Round 5 measured NT = 512 with 128-row stage-2 tiles -- half the weight-panel
+// L2 traffic per row (profiles/r5/kernels/pmc_l2_r5.md) -- and a 3-stage vs a
+// 2-stage conv2 ring: the ring won 0.5 %, the wide tile lost 0.5 % (one
+// workgroup per CU); the tails are latency-, not L2-bandwidth-bound.
 template <int BM, int W, bool NEXT = false, int NS1 = 3, int NT = kThreads>
 __global__ void __launch_bounds__(NT, 512 / NT) conv23_kernel(const ConvArgs a, const ConvArgs b,
                                                               const ConvArgs c) {
@@ -1764,27 +1764,11 @@ __global__ void __launch_bounds__(NT, 512 / NT) conv23_kernel(const ConvArgs a, 
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  if constexpr (NS1 == 2) {
-    issue(0, 0);
-    for (int kt = 0; kt < a.ktiles; ++kt) {
-      const int st = kt & 1;
-      if (kt + 1 < a.ktiles) {
-        issue(kt + 1, st ^ 1);
-        __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR + BR));
-      } else {
-        __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-      }
-      __builtin_amdgcn_s_barrier();
-      const char* sA = smem + st * STAGE;
-      mma_k64<TM, TN, true>(sA, sA + A_BYTES, wm * WTM, wn * WTN, fr, fk, acc);
-      __builtin_amdgcn_s_waitcnt(kLgkm0);
-      __builtin_amdgcn_s_barrier();
-    }
-  } else {
+  {
     // Two steps in flight behind the MMA, one barrier per step: step kt's wait
     // + barrier also proves every wave finished step kt-1's reads of the stage
     // that issue(kt+2) refills.
-    static_assert(NS1 == 3, "conv23: 2- or 3-stage phase 1");
+    static_assert(NS1 == 3, "conv23: 3-stage phase 1");
     issue(0, 0);
     if (a.ktiles > 1) issue(1, 1);
     int st = 0;
@@ -1951,8 +1935,6 @@ __global__ void __launch_bounds__(NT, 512 / NT) conv23_kernel(const ConvArgs a, 
     epilogue_halves<BM, W, false, 0, NT>(c, acc3, m0, 0, smem, none);
   }
 }
-
-int g_conv23_wide = -1;  // vgpu_conv23_set_wide: -1 = env VGPU_CONV23_WIDE
 
 // CUs this process can occupy on the current device — the grid-fill term of
 // the tile choice.  A vGPU pod owns an XCD-balanced CU mask of
@@ -2382,38 +2364,24 @@ static int conv23_impl(const void* x, const void* w2, const float* b2, const voi
       e.y = cn.y + (int64_t)n0 * (hi / 2);
       e.y_bytes = (uint32_t)(nb * hi);
     }
-    if (g_conv23_wide < 0) g_conv23_wide = getenv("VGPU_CONV23_WIDE") && atoi(getenv("VGPU_CONV23_WIDE")) == 1;
-    const bool wide = g_conv23_wide == 1;  // A/B: stage 2 on 512-thread 128-row tiles
-    const int bm = C == 64 || wide ? 128 : 64;
+    const int bm = C == 64 ? 128 : 64;
     c.nM = (c.M + bm - 1) / bm; c.nN = 1; c.nwg = c.nM;
-    static const bool ns2 = getenv("VGPU_CONV23_NS") && atoi(getenv("VGPU_CONV23_NS")) == 2;  // A/B
-#define VGPU_C23(BM_, W_, NX_)                                                                          \
-  do {                                                                                                 \
-    if (ns2)                                                                                           \
-      hipLaunchKernelGGL((conv23_kernel<BM_, W_, NX_, 2>), dim3(c.nwg), dim3(kThreads), 0, s, c, d, e); \
-    else                                                                                               \
-      hipLaunchKernelGGL((conv23_kernel<BM_, W_, NX_, 3>), dim3(c.nwg), dim3(kThreads), 0, s, c, d, e); \
-  } while (0)
     if (C == 64) {
-      if (next) VGPU_C23(128, 64, true);
-      else VGPU_C23(128, 64, false);
-    } else if (wide) {  // 512-thread 128-row tiles
       if (next)
-        hipLaunchKernelGGL((conv23_kernel<128, 128, true, 3, 512>), dim3(c.nwg), dim3(512), 0, s, c, d, e);
+        hipLaunchKernelGGL((conv23_kernel<128, 64, true>), dim3(c.nwg), dim3(kThreads), 0, s, c, d, e);
       else
-        hipLaunchKernelGGL((conv23_kernel<128, 128, false, 3, 512>), dim3(c.nwg), dim3(512), 0, s, c, d, e);
+        hipLaunchKernelGGL((conv23_kernel<128, 64>), dim3(c.nwg), dim3(kThreads), 0, s, c, d, e);
     } else {
-      if (next) VGPU_C23(64, 128, true);
-      else VGPU_C23(64, 128, false);
+      if (next)
+        hipLaunchKernelGGL((conv23_kernel<64, 128, true>), dim3(c.nwg), dim3(kThreads), 0, s, c, d, e);
+      else
+        hipLaunchKernelGGL((conv23_kernel<64, 128>), dim3(c.nwg), dim3(kThreads), 0, s, c, d, e);
     }
-#undef VGPU_C23
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return (int)err;
   }
   return 0;
 }
-
-VGPU_API void vgpu_conv23_set_wide(int on) { g_conv23_wide = on < 0 ? -1 : (on ? 1 : 0); }
 
 VGPU_API int vgpu_conv23_nhwc(const void* x, const void* w2, const float* b2, const void* w3,
                               const void* res, void* y, int N, int H, int W, int C, int stride,

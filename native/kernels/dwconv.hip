@@ -11,9 +11,12 @@
 //   * data gradient: one thread per (input pixel, 8 channels) gathers the
 //     output pixels whose window holds it (stride-divisible taps only) -- no
 //     atomics, no zero-fill;
-//   * weight gradient: thread (slab, 8 channels) accumulates 9 x 8 fp32
-//     products over its slab of output pixels into a partial row; a second
-//     kernel sums the slabs in a fixed order (deterministic).
+//   * weight gradient: a block takes a slab of output pixels (8 per thread
+//     for any C), its threads' 9 x 8 fp32 sums are merged in LDS into one
+//     partial row per slab, and a second kernel sums the slabs in a fixed
+//     order, 16 threads per element (deterministic).  (A first version gave
+//     each thread its own slab: 64k partial rows whose one-thread-per-element
+//     reduce cost 59 µs a layer, profiles/r5/train/prof_4_2_after.md.)
 // fp32 accumulation, one bf16 rounding per output (forward / data gradient).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -122,62 +125,90 @@ __global__ void __launch_bounds__(kThreads) dw_dgrad_kernel(const u32x4* __restr
   }
 }
 
-// Thread t: channel group t % cv, slab t / cv; slab covers output pixels
-// [slab·per, (slab+1)·per).  part[slab][tap][C].
+// Block = one slab of pb output pixels (pb = 8 · (256 / cv): 8 pixels per
+// thread whatever C): thread t owns channel group t % cv and pixels
+// p0 + t / cv + k · (256 / cv).  Its 9 x 8 sums are merged across the block
+// through LDS, one tap at a time, into part[slab][tap][C].
 __global__ void __launch_bounds__(kThreads) dw_wgrad_kernel(const u32x4* __restrict__ dy, const u32x4* __restrict__ x,
-                                                            float* __restrict__ part, const Shape s, int slabs,
-                                                            int64_t per) {
-  const int cv = s.C / 8;
-  const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (t >= (int64_t)slabs * cv) return;
-  const int cg = (int)(t % cv), slab = (int)(t / cv);
+                                                            float* __restrict__ part, const Shape s, int pb) {
+  __shared__ float red[kThreads][9];
+  const int cv = s.C / 8, nsub = kThreads / cv;
+  const int t = threadIdx.x, cg = t % cv, sub = t / cv;
   const int64_t P = (int64_t)s.N * s.OH * s.OW;
-  const int64_t p0 = slab * per, p1 = p0 + per < P ? p0 + per : P;
+  const int64_t p0 = (int64_t)blockIdx.x * pb, p1 = p0 + pb < P ? p0 + pb : P;
   float acc[9][8];
 #pragma unroll
   for (int k = 0; k < 9; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
-  for (int64_t p = p0; p < p1; ++p) {
-    const int ow = (int)(p % s.OW);
-    const int64_t r = p / s.OW;
-    const int oh = (int)(r % s.OH);
-    const int n = (int)(r / s.OH);
-    float g[8];
-    unpack8(dy[p * cv + cg], g);
-    const int h0 = oh * s.stride - s.dil, w0 = ow * s.stride - s.dil;
-    const u32x4* xn = x + (int64_t)n * s.H * s.W * cv + cg;
+  if (sub < nsub) {
+    for (int64_t p = p0 + sub; p < p1; p += nsub) {
+      const int ow = (int)(p % s.OW);
+      const int64_t r = p / s.OW;
+      const int oh = (int)(r % s.OH);
+      const int n = (int)(r / s.OH);
+      float g[8];
+      unpack8(dy[p * cv + cg], g);
+      const int h0 = oh * s.stride - s.dil, w0 = ow * s.stride - s.dil;
+      const u32x4* xn = x + (int64_t)n * s.H * s.W * cv + cg;
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh) {
-      const int ih = h0 + kh * s.dil;
-      if ((unsigned)ih >= (unsigned)s.H) continue;
+      for (int kh = 0; kh < 3; ++kh) {
+        const int ih = h0 + kh * s.dil;
+        if ((unsigned)ih >= (unsigned)s.H) continue;
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        const int iw = w0 + kw * s.dil;
-        if ((unsigned)iw >= (unsigned)s.W) continue;
-        float xv[8];
-        unpack8(xn[((int64_t)ih * s.W + iw) * cv], xv);
+        for (int kw = 0; kw < 3; ++kw) {
+          const int iw = w0 + kw * s.dil;
+          if ((unsigned)iw >= (unsigned)s.W) continue;
+          float xv[8];
+          unpack8(xn[((int64_t)ih * s.W + iw) * cv], xv);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[kh * 3 + kw][j] = fmaf(g[j], xv[j], acc[kh * 3 + kw][j]);
+          for (int j = 0; j < 8; ++j) acc[kh * 3 + kw][j] = fmaf(g[j], xv[j], acc[kh * 3 + kw][j]);
+        }
       }
     }
   }
-  float* out = part + (int64_t)slab * 9 * s.C + cg * 8;
+  float* out = part + (int64_t)blockIdx.x * 9 * s.C;
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
-    *reinterpret_cast<float4*>(out + (int64_t)k * s.C) = make_float4(acc[k][0], acc[k][1], acc[k][2], acc[k][3]);
-    *reinterpret_cast<float4*>(out + (int64_t)k * s.C + 4) = make_float4(acc[k][4], acc[k][5], acc[k][6], acc[k][7]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[t][j] = acc[k][j];
+    __syncthreads();
+    if (t < cv) {
+      float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < nsub; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += red[q * cv + t][j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) out[(int64_t)k * s.C + t * 8 + j] = a[j];
+    }
+    __syncthreads();
   }
 }
 
-// dw[tap][c] = Σ_slab part[slab][tap][c], slabs in order.
+// dw[i] = Σ_slab part[slab][i] for i < 9C: 16 threads per element (slab
+// residues mod 16, four accumulators each), merged in a fixed order.
 __global__ void __launch_bounds__(kThreads) dw_wgrad_reduce_kernel(const float* __restrict__ part,
                                                                    float* __restrict__ dw, int n9c, int slabs) {
-  const int i = blockIdx.x * kThreads + threadIdx.x;
-  if (i >= n9c) return;
-  float a = 0.f;
-  for (int sl = 0; sl < slabs; ++sl) a += part[(int64_t)sl * n9c + i];
-  dw[i] = a;
+  __shared__ float red[16][17];
+  const int el = threadIdx.x % 16, q = threadIdx.x / 16, i = blockIdx.x * 16 + el;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (i < n9c) {
+    int k = q;
+    for (; k + 48 < slabs; k += 64) {
+      a0 += part[(int64_t)k * n9c + i];
+      a1 += part[(int64_t)(k + 16) * n9c + i];
+      a2 += part[(int64_t)(k + 32) * n9c + i];
+      a3 += part[(int64_t)(k + 48) * n9c + i];
+    }
+    for (; k < slabs; k += 16) a0 += part[(int64_t)k * n9c + i];
+  }
+  red[q][el] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (q == 0 && i < n9c) {
+    float a = 0.f;
+    for (int r = 0; r < 16; ++r) a += red[r][el];
+    dw[i] = a;
+  }
 }
 
 bool make_shape(Shape& s, int N, int H, int W, int C, int stride, int dil) {
@@ -191,18 +222,13 @@ int grid_for(int64_t total) {
   return (int)(b < 65536 ? (b > 0 ? b : 1) : 65536);
 }
 
-// Slabs of the weight gradient: about 64k threads (a few waves per CU), each
-// slab at least 16 output pixels.
-void wgrad_split(const Shape& s, int& slabs, int64_t& per) {
+// Pixels per weight-gradient block: 8 per thread whatever C.
+int wgrad_pb(const Shape& s) { return 8 * (kThreads / (s.C / 8)); }
+
+int wgrad_slabs(const Shape& s) {
   const int64_t P = (int64_t)s.N * s.OH * s.OW;
-  const int cv = s.C / 8;
-  int64_t want = 65536 / cv;
-  if (want < 1) want = 1;
-  const int64_t most = (P + 15) / 16;
-  if (want > most) want = most;
-  if (want < 1) want = 1;
-  per = (P + want - 1) / want;
-  slabs = (int)((P + per - 1) / per);
+  const int pb = wgrad_pb(s);
+  return (int)((P + pb - 1) / pb);
 }
 
 }  // namespace
@@ -229,27 +255,21 @@ VGPU_API int vgpu_dwconv3_dgrad_nhwc(const void* dy, const float* w9c, void* dx,
 
 VGPU_API int64_t vgpu_dwconv3_wgrad_workspace(int N, int H, int W, int C, int stride, int dil) {
   Shape s;
-  if (!make_shape(s, N, H, W, C, stride, dil)) return -1;
-  int slabs;
-  int64_t per;
-  wgrad_split(s, slabs, per);
-  return (int64_t)slabs * 9 * C * 4;
+  if (!make_shape(s, N, H, W, C, stride, dil) || C / 8 > kThreads) return -1;
+  return (int64_t)wgrad_slabs(s) * 9 * C * 4;
 }
 
 // dw9c: fp32 [9][C].  ws: vgpu_dwconv3_wgrad_workspace bytes.
 VGPU_API int vgpu_dwconv3_wgrad_nhwc(const void* dy, const void* x, float* dw9c, void* ws, int64_t ws_bytes, int N,
                                      int H, int W, int C, int stride, int dil, hipStream_t st) {
   Shape s;
-  if (!make_shape(s, N, H, W, C, stride, dil)) return -1;
-  int slabs;
-  int64_t per;
-  wgrad_split(s, slabs, per);
+  if (!make_shape(s, N, H, W, C, stride, dil) || C / 8 > kThreads) return -1;
+  const int slabs = wgrad_slabs(s);
   if (ws_bytes < (int64_t)slabs * 9 * C * 4) return -2;
-  const int64_t threads = (int64_t)slabs * (C / 8);
-  hipLaunchKernelGGL(dw_wgrad_kernel, dim3((int)((threads + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
-                     (const u32x4*)dy, (const u32x4*)x, (float*)ws, s, slabs, per);
+  hipLaunchKernelGGL(dw_wgrad_kernel, dim3(slabs), dim3(kThreads), 0, st, (const u32x4*)dy, (const u32x4*)x,
+                     (float*)ws, s, wgrad_pb(s));
   const int n9c = 9 * C;
-  hipLaunchKernelGGL(dw_wgrad_reduce_kernel, dim3((n9c + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
-                     (const float*)ws, dw9c, n9c, slabs);
+  hipLaunchKernelGGL(dw_wgrad_reduce_kernel, dim3((n9c + 15) / 16), dim3(kThreads), 0, st, (const float*)ws, dw9c,
+                     n9c, slabs);
   return (int)hipGetLastError();
 }

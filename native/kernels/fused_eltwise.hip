@@ -182,12 +182,13 @@ VGPU_API int vgpu_add_scale_shift_act_nhwc(const void* a, const void* b, void* s
 // ---- ReLU backward + bias gradient (training conv + bias + ReLU, VGG-16) ------------
 //   g <- (y > 0) ? dy : 0 ;  db[c] = Σ_rows g[., c]   (fp32, deterministic)
 // One pass over dy and y instead of a threshold kernel and a PyTorch column
-// reduction that re-reads g (12 µs per VGG layer at b=2: profiles/r5/train).
-// Block = one slab of kSlabRows rows: thread t owns channel group t % cv and
-// rows t / cv, t / cv + 256 / cv, ...; lanes of one group are merged through
-// LDS into part[slab][C]; relu_bias_grad_reduce sums the slabs in order.
+// reduction that re-reads g (profiles/r5/train).  Block = one slab of
+// kIters · (256 / cv) rows: thread t owns channel group t % cv and every
+// (256 / cv)-th row from t / cv, kIters of them with all loads issued first;
+// lanes of one group are merged through LDS into part[slab][C]; the reduce
+// kernel sums the slabs in a fixed order, 16 threads per channel.
 namespace {
-constexpr int kSlabRows = 256;
+constexpr int kIters = 8;
 
 __global__ void __launch_bounds__(kThreads) relu_bias_grad_kernel(const bf16x8* __restrict__ dy,
                                                                   const bf16x8* __restrict__ y,
@@ -199,48 +200,79 @@ __global__ void __launch_bounds__(kThreads) relu_bias_grad_kernel(const bf16x8* 
   const uint32_t cg = t % cv, r0 = t / cv;
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (r0 < per) {
-    const uint64_t row_lo = (uint64_t)blockIdx.x * kSlabRows;
-    const uint64_t row_hi = row_lo + kSlabRows < rows ? row_lo + kSlabRows : rows;
-    for (uint64_t r = row_lo + r0; r < row_hi; r += per) {
-      const uint64_t i = r * cv + cg;
-      const bf16x8 a = dy[i], b = y[i];
+    const uint64_t row0 = (uint64_t)blockIdx.x * per * kIters + r0;
+    bf16x8 a[kIters], b[kIters];
+#pragma unroll
+    for (int k = 0; k < kIters; ++k) {
+      const uint64_t r = row0 + (uint64_t)k * per;
+      if (r < rows) {
+        a[k] = dy[r * cv + cg];
+        b[k] = y[r * cv + cg];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kIters; ++k) {
+      const uint64_t r = row0 + (uint64_t)k * per;
+      if (r >= rows) continue;
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float v = bf2f(b.v[j]) > 0.0f ? bf2f(a.v[j]) : 0.0f;
-        o.v[j] = v != 0.0f ? a.v[j] : (uint16_t)0;
-        s[j] += v;
+        const bool on = bf2f(b[k].v[j]) > 0.0f;
+        o.v[j] = on ? a[k].v[j] : (uint16_t)0;
+        s[j] += on ? bf2f(a[k].v[j]) : 0.0f;
       }
-      g[i] = o;
+      g[r * cv + cg] = o;
     }
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) red[t][j] = s[j];
   __syncthreads();
   if (t < cv) {
-    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (uint32_t k = 0; k < per; ++k)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] += red[k * cv + t][j];
+      for (int j = 0; j < 8; ++j) acc[j] += red[k * cv + t][j];
     float* out = part + (uint64_t)blockIdx.x * cv * 8 + t * 8;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) out[j] = a[j];
+    for (int j = 0; j < 8; ++j) out[j] = acc[j];
   }
 }
 
+// 16 channels per block, 16 threads per channel (slab residues mod 16), merged in order.
 __global__ void __launch_bounds__(kThreads) relu_bias_grad_reduce_kernel(const float* __restrict__ part,
                                                                          float* __restrict__ db, uint32_t c,
                                                                          uint32_t slabs) {
-  const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
-  if (i >= c) return;
-  float a = 0.f;
-  for (uint32_t k = 0; k < slabs; ++k) a += part[(uint64_t)k * c + i];
-  db[i] = a;
+  __shared__ float red[16][17];
+  const uint32_t cl = threadIdx.x % 16, q = threadIdx.x / 16, ch = blockIdx.x * 16 + cl;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (ch < c) {
+    uint32_t k = q;
+    for (; k + 48 < slabs; k += 64) {
+      a0 += part[(uint64_t)k * c + ch];
+      a1 += part[(uint64_t)(k + 16) * c + ch];
+      a2 += part[(uint64_t)(k + 32) * c + ch];
+      a3 += part[(uint64_t)(k + 48) * c + ch];
+    }
+    for (; k < slabs; k += 16) a0 += part[(uint64_t)k * c + ch];
+  }
+  red[q][cl] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (q == 0 && ch < c) {
+    float a = 0.f;
+    for (int i = 0; i < 16; ++i) a += red[i][cl];
+    db[ch] = a;
+  }
+}
+
+uint32_t rbg_slabs(uint64_t rows, uint32_t cv) {
+  const uint64_t slab_rows = (uint64_t)(kThreads / cv) * kIters;
+  return (uint32_t)((rows + slab_rows - 1) / slab_rows);
 }
 }  // namespace
 
 VGPU_API int64_t vgpu_relu_bias_grad_workspace(uint64_t rows, uint32_t c) {
-  return (int64_t)((rows + kSlabRows - 1) / kSlabRows) * c * 4;
+  if (c % 8 || c / 8 > kThreads || c == 0) return -1;
+  return (int64_t)rbg_slabs(rows, c / 8) * c * 4;
 }
 
 // dy, y, g: [rows, c] bf16 (NHWC); db: fp32 [c]; ws: vgpu_relu_bias_grad_workspace bytes.
@@ -248,10 +280,10 @@ VGPU_API int vgpu_relu_bias_grad_nhwc(const void* dy, const void* y, void* g, fl
                                       uint32_t c, hipStream_t stream) {
   if (c % 8 || c / 8 > kThreads || rows == 0) return -1;
   const uint32_t cv = c / 8;
-  const uint32_t slabs = (uint32_t)((rows + kSlabRows - 1) / kSlabRows);
+  const uint32_t slabs = rbg_slabs(rows, cv);
   hipLaunchKernelGGL(relu_bias_grad_kernel, dim3(slabs), dim3(kThreads), 0, stream, (const bf16x8*)dy,
                      (const bf16x8*)y, (bf16x8*)g, (float*)ws, rows, cv);
-  hipLaunchKernelGGL(relu_bias_grad_reduce_kernel, dim3((c + kThreads - 1) / kThreads), dim3(kThreads), 0, stream,
+  hipLaunchKernelGGL(relu_bias_grad_reduce_kernel, dim3((c + 15) / 16), dim3(kThreads), 0, stream,
                      (const float*)ws, db, c, slabs);
   return (int)hipGetLastError();
 }

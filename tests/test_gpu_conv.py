@@ -266,19 +266,9 @@ def test_stem_pool_matches_conv_then_maxpool(C, nhw):
     torch.testing.assert_close(got, ref, atol=0, rtol=0)
 
 
-@pytest.fixture(params=[0, 1], ids=["bm64", "wide512"])
-def wide(request):
-    """conv23's stage-2 (W = 128) tile: 64 rows x 256 threads, or 128 rows x 512."""
-    from vgpu.native import load_kernels
-    lib = load_kernels()
-    lib.vgpu_conv23_set_wide(request.param)
-    yield request.param
-    lib.vgpu_conv23_set_wide(-1)
-
-
 @pytest.mark.parametrize("case", [(2, 64, 19, 17, 1), (2, 128, 21, 19, 2), (3, 128, 9, 9, 1),
                                   (4, 64, 64, 64, 1), (2, 128, 40, 37, 1)])
-def test_conv23_matches_unfused(C, case, wide):
+def test_conv23_matches_unfused(C, case):
     n, c, h, w, stride = case
     x = _t((n, c, h, w), 21)
     w2 = _t((c, c, 3, 3), 22, scale=(2.0 / (9 * c)) ** 0.5)
@@ -306,7 +296,7 @@ def test_conv23_matches_unfused(C, case, wide):
 
 @pytest.mark.parametrize("case", [(2, 64, 19, 17, 1), (2, 128, 21, 19, 2), (3, 128, 9, 9, 1),
                                   (4, 64, 64, 64, 1), (1, 64, 7, 5, 1), (2, 128, 40, 37, 1)])
-def test_conv231_matches_conv23_then_conv1(C, case, wide):
+def test_conv231_matches_conv23_then_conv1(C, case):
     """Tail + next block's BN+ReLU+conv1 in one kernel: bit-for-bit equal to
     conv23 followed by the prologue conv1 (same roundings, same K order)."""
     n, c, h, w, stride = case

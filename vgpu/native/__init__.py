@@ -68,7 +68,6 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_stem_pool_nhwc.argtypes = [vp, vp, vp] + [ci] * 3 + [vp]
     lib.vgpu_conv_set_big.argtypes = [ci]
     lib.vgpu_conv_set_halo.argtypes = [ci]
-    lib.vgpu_conv23_set_wide.argtypes = [ci]
     lib.vgpu_conv_halo_launches.restype = ctypes.c_ulonglong
     lib.vgpu_lstm_recurrence.argtypes = [vp, vp, vp, vp, ci, ci, ci, vp]
     lib.vgpu_lstm_recurrence.restype = ci
