@@ -715,7 +715,7 @@ def _auto_ab(tmp_path, factor, n=4, secs=6.0, pause=None):
               "VGPU_DEVICE_CU_LIMIT_0": str(100 // n), "VGPU_CU_SHARE": "auto", "VGPU_CU_MASK_FROM_LIMIT": "false",
               "VGPU_LOCK_DIR": str(tmp_path), "VGPU_DEVICE_UUID_0": "GPU-auto", "VGPU_FAKE_KERNEL_US": "500",
               "VGPU_FAKE_GPU_TIMELINE": str(tmp_path / "tl"), "VGPU_FAKE_MASK_FACTOR": str(factor),
-              "VGPU_AUTO_WINDOW_MS": "700", "VGPU_AUTO_SETTLE_MS": "150", "VGPU_AUTO_BUCKET_MS": "300",
+              "VGPU_AUTO_WINDOW_MS": "700", "VGPU_AUTO_SETTLE_MS": "150", "VGPU_AUTO_BUCKET_MS": "500",
               "VGPU_LOG_LEVEL": "3"})
     if pause:
         e["DRIVER_PAUSE"] = pause
@@ -958,7 +958,7 @@ def test_limiter_occupancy_cross_check_under_early_markers(native_build, tmp_pat
     if occ_us == "0":
         assert duty > 0.5, o       # the hole: markers alone under-charge
     else:
-        assert 0.18 < duty < 0.36, (duty, o["_stderr"][-1500:])
+        assert 0.18 < duty < 0.40, (duty, o["_stderr"][-1500:])  # vs > 0.5 without the check
 
 
 def test_launch_cost_scenario_reports_per_launch_host_cost(native_build, tmp_path):
