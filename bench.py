@@ -408,7 +408,7 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_VGPU_R50_INF, 2) if args.workload == "1.1" else None,
-            "dtype": "bf16",
+            "dtype": "fp32" if os.environ.get("VGPU_BENCH_DTYPE", "bf16").lower() in ("fp32", "float32") else "bf16",
             "data": "synthetic inputs, random-init weights",
             "config": {
                 "model": f"{w.name} (ai-benchmark test {w.test_id}, {'training' if w.train else 'inference'})",

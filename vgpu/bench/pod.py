@@ -37,7 +37,11 @@ def build(args):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     model = w.builder().to(dev)
-    dtype = torch.bfloat16
+    # VGPU_BENCH_DTYPE=fp32: the reference's precision (TF fp32 on V100) for the
+    # sharing-ratio check; the hand-written kernels are bf16, so fp32 runs the
+    # plain modules on MIOpen / hipBLASLt.
+    fp32 = os.environ.get("VGPU_BENCH_DTYPE", "bf16").lower() in ("fp32", "float32")
+    dtype = torch.float32 if fp32 else torch.bfloat16
     if w.kind == "image":
         model = model.to(memory_format=torch.channels_last)
     model = model.to(dtype)
@@ -76,7 +80,9 @@ def build(args):
         from vgpu.models.resnet import FusedResNetV2Inference, ResNetV2
         from vgpu.models.vision import VGG16, NativeVGG16Inference
         conv = getattr(args, "conv", "native")
-        if isinstance(model, ResNetV2) and not args.no_fused:
+        if fp32:
+            pass  # plain modules
+        elif isinstance(model, ResNetV2) and not args.no_fused:
             model = FusedResNetV2Inference(model, conv=conv)
         elif isinstance(model, VGG16) and not args.no_fused and conv == "native":
             model = NativeVGG16Inference(model)
