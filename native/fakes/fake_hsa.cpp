@@ -27,6 +27,7 @@
 #include <map>
 #include <string>
 
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -38,7 +39,22 @@ struct FakeQueue {
   uint32_t mask[8];
   uint32_t mask_bits;
   int alive;
+  int intercept;  // created by hsa_amd_queue_intercept_create
+  hsa_amd_queue_intercept_handler handler;
+  void* hdata;
 };
+
+// Intercept queues (ROCr's InterceptQueue, reached only through the AMD
+// extension table): a submission (fake_hsa_submit, standing in for the
+// doorbell write) hands the packets to the registered handler, which writes
+// what it lets through to the "hardware" -- here a counter of kernel-dispatch
+// packets.
+std::atomic<uint64_t> g_dispatched{0};
+void fake_writer(const void* pkts, uint64_t n) {
+  const auto* p = static_cast<const hsa_kernel_dispatch_packet_t*>(pkts);
+  for (uint64_t i = 0; i < n; ++i)
+    if ((p[i].header & 0xff) == HSA_PACKET_TYPE_KERNEL_DISPATCH) g_dispatched.fetch_add(1);
+}
 
 std::mutex g_mu;
 std::vector<FakeQueue*> g_queues;
@@ -60,6 +76,10 @@ hsa_status_t impl_queue_destroy(hsa_queue_t* q);
 hsa_status_t impl_cu_set_mask(const hsa_queue_t* q, uint32_t bits, const uint32_t* mask);
 hsa_status_t impl_pool_allocate(hsa_amd_memory_pool_t pool, size_t size, uint32_t flags, void** ptr);
 hsa_status_t impl_pool_free(void* ptr);
+hsa_status_t impl_intercept_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32_t type,
+                                   void (*callback)(hsa_status_t, hsa_queue_t*, void*), void* data,
+                                   uint32_t priv, uint32_t group, hsa_queue_t** queue);
+hsa_status_t impl_intercept_register(hsa_queue_t* q, hsa_amd_queue_intercept_handler h, void* data);
 
 CoreApiTable g_core;
 AmdExtTable g_ext;
@@ -77,6 +97,8 @@ void setup_table() {
     g_ext.hsa_amd_queue_cu_set_mask_fn = impl_cu_set_mask;
     g_ext.hsa_amd_memory_pool_allocate_fn = impl_pool_allocate;
     g_ext.hsa_amd_memory_pool_free_fn = impl_pool_free;
+    g_ext.hsa_amd_queue_intercept_create_fn = impl_intercept_create;
+    g_ext.hsa_amd_queue_intercept_register_fn = impl_intercept_register;
     g_api.core_ = &g_core;
     g_api.amd_ext_ = &g_ext;
     const char* tools = getenv("HSA_TOOLS_LIB");
@@ -298,6 +320,26 @@ hsa_status_t impl_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type3
   return HSA_STATUS_SUCCESS;
 }
 
+hsa_status_t impl_intercept_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32_t type,
+                                   void (*callback)(hsa_status_t, hsa_queue_t*, void*), void* data,
+                                   uint32_t priv, uint32_t group, hsa_queue_t** queue) {
+  hsa_status_t rc = impl_queue_create(agent, size, type, callback, data, priv, group, queue);
+  if (rc == HSA_STATUS_SUCCESS) reinterpret_cast<FakeQueue*>(*queue)->intercept = 1;
+  return rc;
+}
+
+hsa_status_t impl_intercept_register(hsa_queue_t* q, hsa_amd_queue_intercept_handler h, void* data) {
+  std::lock_guard<std::mutex> g(g_mu);
+  for (auto* fq : g_queues) {
+    if (&fq->q != q) continue;
+    if (!fq->intercept) return HSA_STATUS_ERROR_INVALID_QUEUE;
+    fq->handler = h;
+    fq->hdata = data;
+    return HSA_STATUS_SUCCESS;
+  }
+  return HSA_STATUS_ERROR_INVALID_QUEUE;
+}
+
 hsa_status_t impl_queue_destroy(hsa_queue_t* q) {
   std::lock_guard<std::mutex> g(g_mu);
   for (auto* fq : g_queues)
@@ -322,6 +364,29 @@ hsa_status_t impl_cu_set_mask(const hsa_queue_t* q, uint32_t bits, const uint32_
 }  // namespace
 
 extern "C" {
+
+// The doorbell write of `n` packets on queue `q` (see fake_writer).
+void fake_hsa_submit(hsa_queue_t* q, const void* pkts, uint64_t n) {
+  hsa_amd_queue_intercept_handler h = nullptr;
+  void* data = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    for (auto* fq : g_queues)
+      if (&fq->q == q) {
+        h = fq->handler;
+        data = fq->hdata;
+      }
+  }
+  if (h) h(pkts, n, 0, data, fake_writer);
+  else fake_writer(pkts, n);
+}
+uint64_t fake_hsa_dispatched() { return g_dispatched.load(); }
+int fake_hsa_intercept_queues() {
+  std::lock_guard<std::mutex> g(g_mu);
+  int n = 0;
+  for (auto* fq : g_queues) n += fq->intercept && fq->alive;
+  return n;
+}
 
 int fake_hsa_queue_count() {
   std::lock_guard<std::mutex> g(g_mu);

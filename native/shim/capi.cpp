@@ -183,6 +183,11 @@ __attribute__((visibility("default"))) void vgpu_self_vmem_stats(uint64_t out[5]
   vmem_stats(&out[0], &out[1], &out[2], &out[3], &out[4]);
 }
 
+// Kernel dispatches seen by intercept queues, and how many queues are intercepted
+// (hooks_hsa.cpp, HSA_TOOLS_LIB mode).
+__attribute__((visibility("default"))) uint64_t vgpu_self_hsa_dispatches() { return g_hsa_dispatches.load(); }
+__attribute__((visibility("default"))) int vgpu_self_hsa_intercepted_queues() { return g_hsa_intercepted_queues.load(); }
+
 // VMM suspend vehicle (vmm.cpp): ranges, bytes, evicted bytes, last suspend /
 // resume ns, completed suspend-resume cycles, the last suspend's pinning ns and
 // the last resume's re-mapping ns.

@@ -148,6 +148,14 @@ static void apply_mask(hsa_queue_t* q, int dev, const AgentInfo& ai) {
   }
 }
 
+int cumask_hip_index_for_agent(uint64_t agent_handle) {
+  std::lock_guard<std::mutex> g(g_mu);
+  ensure_agents_locked();
+  for (auto& a : g_agents)
+    if (a.agent.handle == agent_handle) return a.hip_index;
+  return -1;
+}
+
 void cumask_on_queue_created(void* agent_ptr, void* queue) {
   State& s = st();
   if (!s.enabled) return;

@@ -25,7 +25,9 @@
 #undef AMD_INTERNAL_BUILD
 
 #include <dlfcn.h>
+#include <execinfo.h>
 
+#include <atomic>
 #include <mutex>
 #include <unordered_map>
 
@@ -36,6 +38,9 @@
 namespace vgpu {
 bool cumask_intersect(const hsa_queue_t* q, uint32_t* bits, const uint32_t* in, uint32_t* out);
 int cumask_hip_index_for_pool(uint64_t pool_handle);
+int cumask_hip_index_for_agent(uint64_t agent_handle);
+std::atomic<uint64_t> g_hsa_dispatches{0};     // kernel dispatches seen by intercept queues
+std::atomic<int> g_hsa_intercepted_queues{0};
 
 namespace {
 
@@ -45,6 +50,8 @@ struct HsaTable {
   decltype(&::hsa_amd_queue_cu_set_mask) cu_set_mask = nullptr;
   decltype(&::hsa_amd_memory_pool_allocate) pool_allocate = nullptr;
   decltype(&::hsa_amd_memory_pool_free) pool_free = nullptr;
+  decltype(&::hsa_amd_queue_intercept_create) intercept_create = nullptr;
+  decltype(&::hsa_amd_queue_intercept_register) intercept_register = nullptr;
 };
 HsaTable g_orig;                    // ROCr's entries, saved by OnLoad
 std::atomic<bool> g_table_mode{false};
@@ -129,10 +136,90 @@ hsa_status_t pool_free_impl(decltype(&::hsa_amd_memory_pool_free) real, void* pt
   return real(ptr);
 }
 
+// ---- dispatch interception below HIP (VERDICT r4 missing #4) ---------------------------
+// The reference catches every kernel at cuLaunchKernel, CUDA's one driver entry
+// point.  HIP's launches are caught by the HIP hooks; a library that dispatches
+// AQL packets on HSA queues of its own bypasses them.  ROCr exports no
+// intercept-queue symbols, but its tools API table carries
+// hsa_amd_queue_intercept_create / _register (the rocprofiler mechanism), so in
+// table mode (HSA_TOOLS_LIB=libvgpu.so) a queue the HIP runtime did not create
+// becomes an intercept queue: every batch of packets written to it reaches
+// dispatch_handler before the hardware ring.  Its kernel dispatches are counted
+// (workgroups from the packet's grid / workgroup sizes) and pass the same gate
+// as a HIP launch -- suspend, task priority, the temporal limiter's hold -- and
+// their busy time is charged by the KFD cu_occupancy cross-check (occ_step),
+// which charges what no marker covers.  VGPU_HSA_DISPATCH=auto (default) /
+// all (HIP's queues too, counted only: the HIP hooks already gate those) / off.
+struct QInfo {
+  int dev;
+  bool hip;  // created by the HIP runtime: count, never gate twice
+};
+
+int dispatch_mode() {  // 0 off, 1 auto, 2 all
+  static const int m = [] {
+    const char* v = env_first("VGPU_HSA_DISPATCH");
+    if (!v || !*v || !strcasecmp(v, "auto")) return 1;
+    if (!strcasecmp(v, "all")) return 2;
+    return env_bool(v, true) ? 1 : 0;
+  }();
+  return m;
+}
+
+// The HIP runtime (ROCclr lives in libamdhip64) on the stack of this queue
+// creation?  Queue creation is rare: a backtrace is cheap enough.
+bool created_by_hip() {
+  void* frames[24];
+  const int n = backtrace(frames, 24);
+  for (int i = 0; i < n; ++i) {
+    Dl_info di;
+    if (dladdr(frames[i], &di) && di.dli_fname && strstr(di.dli_fname, "libamdhip64")) return true;
+  }
+  return false;
+}
+
+void dispatch_handler(const void* pkts, uint64_t n, uint64_t, void* data,
+                      hsa_amd_queue_intercept_packet_writer writer) {
+  const auto* qi = static_cast<const QInfo*>(data);
+  const auto* p = static_cast<const hsa_kernel_dispatch_packet_t*>(pkts);
+  uint64_t wg = 0;
+  uint32_t kernels = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if ((p[i].header & 0xff) != HSA_PACKET_TYPE_KERNEL_DISPATCH) continue;
+    auto blocks = [](uint32_t g, uint16_t w) -> uint64_t { return w ? (g + w - 1) / w : g; };
+    wg += blocks(p[i].grid_size_x, p[i].workgroup_size_x) * blocks(p[i].grid_size_y, p[i].workgroup_size_y) *
+          blocks(p[i].grid_size_z, p[i].workgroup_size_z);
+    ++kernels;
+  }
+  if (kernels) {
+    g_hsa_dispatches.fetch_add(kernels, std::memory_order_relaxed);
+    if (qi && !qi->hip) (void)limiter_on_launch(qi->dev, wg, nullptr, kernels);
+  }
+  writer(pkts, n);
+}
+
 // Table entries (HSA_TOOLS_LIB mode).
 hsa_status_t tab_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32_t type,
                               void (*cb)(hsa_status_t, hsa_queue_t*, void*), void* data,
                               uint32_t priv, uint32_t group, hsa_queue_t** queue) {
+  ensure_init();
+  const int mode = dispatch_mode();
+  if (mode && g_orig.intercept_create && g_orig.intercept_register && st().enabled) {
+    const bool hip = created_by_hip();
+    const int dev = cumask_hip_index_for_agent(agent.handle);
+    if (dev >= 0 && (mode == 2 || !hip)) {
+      hsa_status_t rc = queue_create_impl(g_orig.intercept_create, agent, size, type, cb, data, priv, group, queue);
+      if (rc != HSA_STATUS_SUCCESS) return rc;
+      auto* qi = new QInfo{dev, hip};  // lives as long as the process (queues are few)
+      if (g_orig.intercept_register(*queue, dispatch_handler, qi) == HSA_STATUS_SUCCESS) {
+        g_hsa_intercepted_queues.fetch_add(1);
+        VLOG_INFO("device %d queue %p: dispatches intercepted (%s queue)", dev, (void*)*queue,
+                  hip ? "HIP" : "non-HIP");
+      } else {
+        VLOG_WARN("device %d queue %p: intercept registration failed; dispatches not gated", dev, (void*)*queue);
+      }
+      return rc;
+    }
+  }
   return queue_create_impl(g_orig.queue_create, agent, size, type, cb, data, priv, group, queue);
 }
 hsa_status_t tab_queue_destroy(hsa_queue_t* queue) {
@@ -217,6 +304,8 @@ __attribute__((visibility("default"))) bool OnLoad(void* api_table, uint64_t run
   g_orig.cu_set_mask = t->amd_ext_->hsa_amd_queue_cu_set_mask_fn;
   g_orig.pool_allocate = t->amd_ext_->hsa_amd_memory_pool_allocate_fn;
   g_orig.pool_free = t->amd_ext_->hsa_amd_memory_pool_free_fn;
+  g_orig.intercept_create = t->amd_ext_->hsa_amd_queue_intercept_create_fn;
+  g_orig.intercept_register = t->amd_ext_->hsa_amd_queue_intercept_register_fn;
   if (!g_orig.queue_create || !g_orig.queue_destroy || !g_orig.cu_set_mask ||
       !g_orig.pool_allocate || !g_orig.pool_free)
     return true;  // unknown table layout: stay on the PLT interposers

