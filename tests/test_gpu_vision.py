@@ -20,11 +20,12 @@ def _rel(a: torch.Tensor, b: torch.Tensor) -> float:
     return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
 
 
-def test_conv_bias_relu_train_matches_fp32(gpu_build):
+@pytest.mark.parametrize("cin,cout", [(128, 256), (3, 64)], ids=["c128", "c3-padded"])
+def test_conv_bias_relu_train_matches_fp32(gpu_build, cin, cout):
     from vgpu.ops import conv as C
-    conv = torch.nn.Conv2d(128, 256, 3, padding=1).cuda().to(torch.bfloat16).to(memory_format=CL)
+    conv = torch.nn.Conv2d(cin, cout, 3, padding=1).cuda().to(torch.bfloat16).to(memory_format=CL)
     ref = copy.deepcopy(conv).float()
-    x = _x((2, 128, 20, 18), 1).requires_grad_(True)
+    x = _x((2, cin, 20, 18), 1).requires_grad_(True)
     xr = x.detach().float().requires_grad_(True)
     calls = []
     orig = C._ConvBiasReLUTrainFn.apply
