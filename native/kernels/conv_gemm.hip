@@ -342,7 +342,8 @@ __global__ void __launch_bounds__(kThreads, 2) conv_gemm_kernel(const ConvArgs a
         _Pragma("unroll") for (int j = 0; j < 8; ++j) v[j] += re[j];                         \
       }                                                                                      \
       if (a.act) {                                                                           \
-        _Pragma("unroll") for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);              \
+        const float hi_ = a.act == 2 ? 6.0f : INFINITY;                                      \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) v[j] = fminf(fmaxf(v[j], 0.0f), hi_);  \
       }                                                                                      \
       if (m < a.M) *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = pack8(v);    \
     }                                                                                        \
@@ -542,9 +543,10 @@ __device__ __forceinline__ void epilogue_halves(const ConvArgs& a,
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += re[j];
       }
-      if (a.act) {
+      if (a.act) {  // 1 ReLU, 2 ReLU6
+        const float hi = a.act == 2 ? 6.0f : INFINITY;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);
+        for (int j = 0; j < 8; ++j) v[j] = fminf(fmaxf(v[j], 0.0f), hi);
       }
       float xf[8];
       if constexpr (bwd) {
@@ -903,9 +905,10 @@ __global__ void __launch_bounds__(kBigThreads, 1) conv_big_kernel(const ConvArgs
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += re[j];
       }
-      if (a.act) {
+      if (a.act) {  // 1 ReLU, 2 ReLU6
+        const float hi = a.act == 2 ? 6.0f : INFINITY;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);
+        for (int j = 0; j < 8; ++j) v[j] = fminf(fmaxf(v[j], 0.0f), hi);
       }
       if (m < a.M) *reinterpret_cast<u32x4*>(a.y + (int64_t)m * a.Cout + col) = pack8(v);
     }
@@ -1198,9 +1201,10 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
       const float4 c1 = *reinterpret_cast<const float4*>(sC + row * CS + ecol + 4);
       float v[8] = {c0.x + bb[0], c0.y + bb[1], c0.z + bb[2], c0.w + bb[3],
                     c1.x + bb[4], c1.y + bb[5], c1.z + bb[6], c1.w + bb[7]};
-      if (a.act) {
+      if (a.act) {  // 1 ReLU, 2 ReLU6
+        const float hi = a.act == 2 ? 6.0f : INFINITY;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);
+        for (int j = 0; j < 8; ++j) v[j] = fminf(fmaxf(v[j], 0.0f), hi);
       }
       float xf[8];
       if constexpr (ST == 2) {
@@ -2461,7 +2465,7 @@ int conv2d_impl(const void* x, const void* w, void* y, const void* res, const fl
   a.K = KS * KS * C;
   a.cblocks = C / 64;
   a.ktiles = a.K / 64;
-  a.act = act != 0;
+  a.act = act;  // 0 none, 1 ReLU, 2 ReLU6
   a.stats = reinterpret_cast<float2*>(stats);
   a.bnx = static_cast<const uint16_t*>(bnx);
   a.bncoef = bncoef;

@@ -57,7 +57,10 @@ struct Shape {
   int N, H, W, C, OH, OW, stride, dil;
 };
 
+// bias (fp32 [C], optional) and act (0 none, 1 ReLU, 2 ReLU6): a folded
+// BatchNorm + activation in inference (vgpu.models.vision DeepLab fusion).
 __global__ void __launch_bounds__(kThreads) dw_fwd_kernel(const u32x4* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ bias, int act,
                                                           u32x4* __restrict__ y, const Shape s, int64_t total) {
   const int cv = s.C / 8;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < total; i += (int64_t)gridDim.x * kThreads) {
@@ -84,6 +87,17 @@ __global__ void __launch_bounds__(kThreads) dw_fwd_kernel(const u32x4* __restric
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] = fmaf(xv[j], wv[j], acc[j]);
       }
+    }
+    if (bias) {
+      const float4 b0 = *reinterpret_cast<const float4*>(bias + cg * 8);
+      const float4 b1 = *reinterpret_cast<const float4*>(bias + cg * 8 + 4);
+      acc[0] += b0.x; acc[1] += b0.y; acc[2] += b0.z; acc[3] += b0.w;
+      acc[4] += b1.x; acc[5] += b1.y; acc[6] += b1.z; acc[7] += b1.w;
+    }
+    if (act) {
+      const float hi = act == 2 ? 6.0f : INFINITY;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = fminf(fmaxf(acc[j], 0.0f), hi);
     }
     y[i] = pack8(acc);
   }
@@ -233,13 +247,13 @@ int wgrad_slabs(const Shape& s) {
 
 }  // namespace
 
-VGPU_API int vgpu_dwconv3_fwd_nhwc(const void* x, const float* w9c, void* y, int N, int H, int W, int C, int stride,
-                                   int dil, hipStream_t st) {
+VGPU_API int vgpu_dwconv3_fwd_nhwc(const void* x, const float* w9c, const float* bias, int act, void* y, int N,
+                                   int H, int W, int C, int stride, int dil, hipStream_t st) {
   Shape s;
-  if (!make_shape(s, N, H, W, C, stride, dil)) return -1;
+  if (!make_shape(s, N, H, W, C, stride, dil) || act < 0 || act > 2) return -1;
   const int64_t total = (int64_t)N * s.OH * s.OW * (C / 8);
-  hipLaunchKernelGGL(dw_fwd_kernel, dim3(grid_for(total)), dim3(kThreads), 0, st, (const u32x4*)x, w9c, (u32x4*)y,
-                     s, total);
+  hipLaunchKernelGGL(dw_fwd_kernel, dim3(grid_for(total)), dim3(kThreads), 0, st, (const u32x4*)x, w9c, bias, act,
+                     (u32x4*)y, s, total);
   return (int)hipGetLastError();
 }
 

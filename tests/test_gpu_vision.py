@@ -195,3 +195,34 @@ def test_relu_bias_grad_matches_torch(gpu_build, shape):
     gt = torch.ops.aten.threshold_backward(dy, y, 0)
     assert torch.equal(g, gt)
     torch.testing.assert_close(db, gt.float().sum(dim=(0, 2, 3)), atol=1e-2, rtol=1e-4)
+
+
+def test_deeplab_fused_inference_matches_unfused(gpu_build):
+    """4.1: BatchNorm folded into the convs (bias + ReLU6 in the native conv /
+    depthwise epilogues) against the same model's unfused eval forward."""
+    from vgpu.models.vision import DeepLabV3
+    torch.manual_seed(0)
+    m = DeepLabV3(num_classes=21).cuda().to(memory_format=CL)
+    for mod in m.modules():  # non-trivial running statistics
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_mean.uniform_(-0.2, 0.2)
+            mod.running_var.uniform_(0.5, 1.5)
+    m = m.to(torch.bfloat16).eval()
+    x = _x((2, 3, 128, 128), 11)
+    with torch.inference_mode():
+        ref = m(x)
+        m.fuse_for_inference()
+        got = m(x)
+    print("deeplab fused rel", _rel(got, ref), "cos", _cos(got, ref))
+    assert _cos(got, ref) > 0.999 and _rel(got, ref) < 0.05
+
+
+def test_conv_relu6_epilogue_matches_fp32(gpu_build):
+    from vgpu.ops import conv as C
+    x = _x((2, 128, 9, 11), 12, scale=3.0)
+    w = _x((64, 128, 1, 1), 13, scale=0.3)
+    b = (torch.randn(64, device="cuda") * 2).float()
+    got = C.conv2d(x, w, b, act="relu6")
+    ref = C.conv2d_ref(x, w, b, act="relu6")
+    assert float(got.max()) <= 6.0
+    torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)

@@ -124,8 +124,41 @@ class ConvBNAct(nn.Sequential):
     (vgpu.ops.conv.conv_train); the rest (the 3-channel stem, dilated ASPP
     convs, channel counts off the MFMA tiles) stay on the module."""
 
+    def fuse(self) -> None:
+        """Inference: fold the BatchNorm's running statistics into the conv
+        (w' = w·s, b' = β - μ·s with s = γ / √(σ² + ε)), so the layer is one
+        kernel with bias + activation in its epilogue.  Stale once trained again."""
+        conv, bn = self[0], self[1]
+        with torch.no_grad():
+            s = bn.weight.float() / torch.sqrt(bn.running_var.float() + bn.eps)
+            b = bn.bias.float() - bn.running_mean.float() * s
+            if conv.bias is not None:
+                b = b + conv.bias.float() * s
+            w = (conv.weight.float() * s.view(-1, 1, 1, 1)).to(conv.weight.dtype)
+        self._fused = (w.contiguous(memory_format=torch.channels_last), b.contiguous(),
+                       w.float().reshape(w.shape[0], -1).t().contiguous() if conv.groups > 1 else None)
+
+    def _forward_fused(self, x: torch.Tensor) -> torch.Tensor:
+        from vgpu.ops import conv as C
+        from vgpu.ops import dwconv
+        conv = self[0]
+        w, b, w9c = self._fused
+        act = "relu6" if len(self) > 2 else "none"
+        cl = x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)
+        if cl and w9c is not None and dwconv.eligible(x, conv):
+            return dwconv.dwconv3(x, w9c, conv.stride[0], conv.dilation[0], b, act)
+        if (cl and conv.groups == 1 and conv.dilation == (1, 1) and conv.kernel_size[0] == conv.kernel_size[1]
+                and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
+                and C.supported(conv.in_channels, conv.out_channels, conv.kernel_size[0])
+                and conv.kernel_size[0] in (1, 3)):
+            return C.conv2d(x, w, b, stride=conv.stride[0], padding=conv.padding[0], act=act)
+        y = F.conv2d(x, w, b.to(x.dtype), conv.stride, conv.padding, conv.dilation, conv.groups)
+        return F.hardtanh_(y, 0.0, 6.0) if act == "relu6" else y
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         conv = self[0]
+        if not self.training and getattr(self, "_fused", None) is not None:
+            return self._forward_fused(x)
         if x.is_cuda:
             from vgpu.ops import dwconv
             if dwconv.eligible(x, conv):
@@ -216,6 +249,14 @@ class DeepLabV3(nn.Module):
         with batched_step_counters():
             y = self.head(self.aspp(self.backbone(x)))
         return resize_bilinear(y, (h, w))
+
+    def fuse_for_inference(self) -> None:
+        """Fold every conv → BatchNorm (→ ReLU6) into one conv with bias and
+        activation in the kernel epilogue (ConvBNAct.fuse): 4.1 then runs
+        one kernel per layer instead of a conv plus a BN-apply pass."""
+        for m in self.modules():
+            if isinstance(m, ConvBNAct):
+                m.fuse()
 
 
 class LSTMSentiment(nn.Module):

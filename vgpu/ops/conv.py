@@ -45,13 +45,16 @@ def out_hw(h: int, w: int, ks: int, stride: int, pad: int) -> tuple[int, int]:
     return (h + 2 * pad - ks) // stride + 1, (w + 2 * pad - ks) // stride + 1
 
 
+_ACTS = {"none": 0, "relu": 1, "relu6": 2}  # the kernels' epilogue activation codes
+
+
 def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *,
            stride: int = 1, padding: int = 0, act: str = "none",
            pro: tuple[torch.Tensor, torch.Tensor] | None = None,
            residual: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """x [N,C,H,W] bf16 channels_last; w [Cout,C,k,k] bf16 channels_last;
     bias fp32 [Cout]; pro = (scale, shift) fp32 [C] (BN+ReLU on the input);
-    residual [N,Cout,OH,OW] bf16 channels_last; act 'none' | 'relu'."""
+    residual [N,Cout,OH,OW] bf16 channels_last; act 'none' | 'relu' | 'relu6'."""
     _nhwc(x, "x")
     _nhwc(w, "w")
     n, c, h, wd = x.shape
@@ -59,7 +62,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
     if cw != c or ks != ks2 or not supported(c, cout, ks):
         raise ValueError(f"unsupported conv: x {tuple(x.shape)} w {tuple(w.shape)}")
     oh, ow = out_hw(h, wd, ks, stride, padding)
-    if act not in ("none", "relu"):
+    if act not in _ACTS:
         raise ValueError(act)
     for p in ((bias,) + (pro if pro is not None else ())):
         if p is not None and (p.dtype != torch.float32 or not p.is_contiguous() or not p.is_cuda):
@@ -79,7 +82,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
     rc = load_kernels().vgpu_conv2d_nhwc(
         _ptr(x), _ptr(w), _ptr(out), _ptr(residual), _ptr(bias),
         _ptr(pro[0] if pro else None), _ptr(pro[1] if pro else None),
-        n, h, wd, c, cout, ks, stride, padding, 1 if act == "relu" else 0, _stream())
+        n, h, wd, c, cout, ks, stride, padding, _ACTS[act], _stream())
     if rc != 0:
         raise RuntimeError(f"vgpu_conv2d_nhwc: error {rc}")
     return out
@@ -568,6 +571,8 @@ def conv2d_ref(x, w, bias=None, *, stride=1, padding=0, act="none", pro=None, re
         y = y + residual.float()
     if act == "relu":
         y = y.clamp_min(0)
+    elif act == "relu6":
+        y = y.clamp(0, 6)
     return y
 
 

@@ -21,7 +21,7 @@ def _lib():
     lib = load_kernels()
     if not _BOUND:
         vp, ci = ctypes.c_void_p, ctypes.c_int
-        lib.vgpu_dwconv3_fwd_nhwc.argtypes = [vp, vp, vp] + [ci] * 6 + [vp]
+        lib.vgpu_dwconv3_fwd_nhwc.argtypes = [vp, vp, vp, ci, vp] + [ci] * 6 + [vp]
         lib.vgpu_dwconv3_fwd_nhwc.restype = ci
         lib.vgpu_dwconv3_dgrad_nhwc.argtypes = [vp, vp, vp] + [ci] * 6 + [vp]
         lib.vgpu_dwconv3_dgrad_nhwc.restype = ci
@@ -45,12 +45,18 @@ def out_hw(h: int, w: int, stride: int) -> tuple[int, int]:
     return (h - 1) // stride + 1, (w - 1) // stride + 1
 
 
-def dwconv3(x: torch.Tensor, w9c: torch.Tensor, stride: int, dil: int) -> torch.Tensor:
-    """x [N,C,H,W] bf16 channels_last, w9c fp32 [9, C] (tap-major) -> y."""
+_ACTS = {"none": 0, "relu": 1, "relu6": 2}
+
+
+def dwconv3(x: torch.Tensor, w9c: torch.Tensor, stride: int, dil: int, bias: torch.Tensor | None = None,
+            act: str = "none") -> torch.Tensor:
+    """x [N,C,H,W] bf16 channels_last, w9c fp32 [9, C] (tap-major), optional
+    fp32 bias [C] and activation -> y."""
     n, c, h, w = x.shape
     oh, ow = out_hw(h, w, stride)
     y = torch.empty((n, c, oh, ow), dtype=x.dtype, device=x.device, memory_format=_CL)
-    rc = _lib().vgpu_dwconv3_fwd_nhwc(_p(x), _p(w9c), _p(y), n, h, w, c, stride, dil, _stream())
+    rc = _lib().vgpu_dwconv3_fwd_nhwc(_p(x), _p(w9c), None if bias is None else _p(bias), _ACTS[act], _p(y), n, h, w,
+                                      c, stride, dil, _stream())
     if rc != 0:
         raise RuntimeError(f"vgpu_dwconv3_fwd_nhwc: error {rc}")
     return y
