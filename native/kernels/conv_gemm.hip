@@ -2171,7 +2171,8 @@ __global__ void __launch_bounds__(kSPThreads, 1) stem_pool_kernel(const uint16_t
   constexpr int SR_BYTES = 3 * kSPMaxOW * 128;   // three bf16 stem rows [row][pixel][64 ch] swizzled
   constexpr int SX_BYTES = 6 * kSPMaxWS * 32 + 512;  // 6 input rows [px][16 ch] + over-read pad
   constexpr int XR = (6 * kSPMaxWS * 2 + kSPThreads - 1) / kSPThreads;  // slab chunks per thread
-  constexpr int NS = 5;                          // subtiles per wave (33 over 8 waves)
+  constexpr int NF = 4;                          // whole subtiles per wave (32 of at most 33)
+  constexpr int NU = 4;                          // remainder units (subtile, 16-channel block) per wave
   __shared__ __attribute__((aligned(16))) char smem[SW_BYTES + SR_BYTES + SX_BYTES];
   char* sW = smem;
   char* sR = smem + SW_BYTES;
@@ -2216,47 +2217,72 @@ __global__ void __launch_bounds__(kSPThreads, 1) stem_pool_kernel(const uint16_t
     const int n = task / PH, pi = task - n * PH, r0 = 2 * pi - 1;
     const int next = task + gridDim.x;
     if (next < tasks) load_slab(next, xr);  // lands behind this task's compute
-    // this wave's subtiles s = wave + 8u: stem row rl = s / MT, pixels (s % MT)*16 ..
-    f32x4_t acc[NS][4];
+    // Work split (balanced, round 5): the first 8 * (S / 8) of the S = 3 * MT
+    // pixel subtiles go whole to waves (subtile wave + 8u), the remainder is
+    // cut into (subtile, 16-channel block) units dealt round-robin (unit k ->
+    // wave k % 8), so no wave carries a whole extra subtile (was 5 vs 4 of 33:
+    // 34 % of the stem's wave time parked at the barrier, pmc_flagship_r4_final.md).
+    // stem row rl = s / MT, pixels (s % MT) * 16 ..
+    const int S = 3 * MT, F = S >> 3, R = S - 8 * F;
+    f32x4_t acc[NF][4], accu[NU];
 #pragma unroll
-    for (int u = 0; u < NS; ++u)
+    for (int u = 0; u < NF; ++u)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[u][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < NU; ++k) accu[k] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kh = 0; kh < 4; ++kh)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        bf16x8_t bfr[4], af[NS];
+        bf16x8_t bfr[4], af[NF], au[NU], bu[NU];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           bfr[j] = *reinterpret_cast<const bf16x8_t*>(sW + kh * 8192 + swz(j * 16 + fr, kk * 4 + fk));
 #pragma unroll
-        for (int u = 0; u < NS; ++u) {
+        for (int u = 0; u < NF; ++u) {
           const int sidx = wave + 8 * u, rl = sidx / MT, m = sidx - rl * MT;
-          if (sidx < 3 * MT)  // wave-uniform; past the three rows there is nothing to read
+          if (u < F)  // wave-uniform
             af[u] = *reinterpret_cast<const bf16x8_t*>(
                 sX + (((rl + kh) * WS + m * 16 + fr) * 32) + (kk * 4 + fk) * 16);
         }
 #pragma unroll
-        for (int u = 0; u < NS; ++u)
-          if (wave + 8 * u < 3 * MT)
+        for (int k = 0; k < NU; ++k) {
+          const int unit = wave + 8 * k, sidx = 8 * F + (unit >> 2), j = unit & 3;
+          if (unit < 4 * R) {  // wave-uniform
+            const int rl = sidx / MT, m = sidx - rl * MT;
+            au[k] = *reinterpret_cast<const bf16x8_t*>(
+                sX + (((rl + kh) * WS + m * 16 + fr) * 32) + (kk * 4 + fk) * 16);
+            bu[k] = *reinterpret_cast<const bf16x8_t*>(sW + kh * 8192 + swz(j * 16 + fr, kk * 4 + fk));
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < NF; ++u)
+          if (u < F)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
               acc[u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[u], acc[u][j], 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < NU; ++k)
+          if (wave + 8 * k < 4 * R) accu[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bu[k], au[k], accu[k], 0, 0, 0);
       }
     // bf16 stem rows → LDS: lane holds pixel m*16+fr, channels j*16+fk*4 .. +3
-#pragma unroll
-    for (int u = 0; u < NS; ++u) {
-      const int sidx = wave + 8 * u, rl = sidx / MT, m = sidx - rl * MT;
-      if (rl >= 3) continue;
-      const int p = m * 16 + fr;
+    auto put = [&](int sidx, int j, const f32x4_t& v) {
+      const int rl = sidx / MT, m = sidx - rl * MT, p = m * 16 + fr;
       char* row = sR + rl * (kSPMaxOW * 128) + p * 128;
+      const int slot = j * 2 + (fk >> 1);
+      *reinterpret_cast<uint2*>(row + ((slot ^ (p & 7)) << 4) + (fk & 1) * 8) =
+          uint2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+    };
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int slot = j * 2 + (fk >> 1);
-        *reinterpret_cast<uint2*>(row + ((slot ^ (p & 7)) << 4) + (fk & 1) * 8) =
-            uint2{pack2(acc[u][j][0], acc[u][j][1]), pack2(acc[u][j][2], acc[u][j][3])};
-      }
+    for (int u = 0; u < NF; ++u)
+      if (u < F)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) put(wave + 8 * u, j, acc[u][j]);
+#pragma unroll
+    for (int k = 0; k < NU; ++k) {
+      const int unit = wave + 8 * k;
+      if (unit < 4 * R) put(8 * F + (unit >> 2), unit & 3, accu[k]);
     }
     __syncthreads();
     // 3x3/s2 window (rows of the task that exist, columns 2j-1 .. 2j+1)
