@@ -2235,7 +2235,7 @@ __global__ void __launch_bounds__(kSPThreads, 1) stem_pool_kernel(const uint16_t
     for (int kh = 0; kh < 4; ++kh)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        bf16x8_t bfr[4], af[NF], au[NU], bu[NU];
+        bf16x8_t bfr[4], af[NF], au[NU];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           bfr[j] = *reinterpret_cast<const bf16x8_t*>(sW + kh * 8192 + swz(j * 16 + fr, kk * 4 + fk));
@@ -2253,7 +2253,7 @@ __global__ void __launch_bounds__(kSPThreads, 1) stem_pool_kernel(const uint16_t
             const int rl = sidx / MT, m = sidx - rl * MT;
             au[k] = *reinterpret_cast<const bf16x8_t*>(
                 sX + (((rl + kh) * WS + m * 16 + fr) * 32) + (kk * 4 + fk) * 16);
-            bu[k] = *reinterpret_cast<const bf16x8_t*>(sW + kh * 8192 + swz(j * 16 + fr, kk * 4 + fk));
+            (void)j;
           }
         }
 #pragma unroll
@@ -2263,8 +2263,13 @@ __global__ void __launch_bounds__(kSPThreads, 1) stem_pool_kernel(const uint16_t
             for (int j = 0; j < 4; ++j)
               acc[u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[u], acc[u][j], 0, 0, 0);
 #pragma unroll
-        for (int k = 0; k < NU; ++k)
-          if (wave + 8 * k < 4 * R) accu[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bu[k], au[k], accu[k], 0, 0, 0);
+        for (int k = 0; k < NU; ++k) {
+          const int unit = wave + 8 * k, j = unit & 3;  // wave-uniform: a select, not a second LDS read
+          if (unit < 4 * R) {
+            const bf16x8_t b = j == 0 ? bfr[0] : j == 1 ? bfr[1] : j == 2 ? bfr[2] : bfr[3];
+            accu[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, au[k], accu[k], 0, 0, 0);
+          }
+        }
       }
     // bf16 stem rows → LDS: lane holds pixel m*16+fr, channels j*16+fk*4 .. +3
     auto put = [&](int sidx, int j, const f32x4_t& v) {
