@@ -77,6 +77,12 @@ struct ConvArgs {
   // which lands on the even (h, w) pixels of this conv's OH x OW output (zero elsewhere).
   int res_stride, res_h, res_w;
   uint32_t res_bytes;
+  int bias_bf16;  // bias is bf16 [Cout] (a model's own parameter, no per-step cast)
+  // Split-K (conv_glds_kernel<..., SPLIT>): blockIdx.y = split, K steps
+  // [split·kper, +kper), fp32 partial tiles ws[split][M][Cout]; splitk_reduce_kernel
+  // sums them in split order and applies bias / residual / activation.
+  float* ws;
+  int kper, splits;
 };
 
 // d act / d z as PyTorch defines it (threshold_backward / hardtanh_backward).
@@ -109,6 +115,24 @@ __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
 }
 __device__ __forceinline__ u32x4 pack8(const float (&f)[8]) {
   return u32x4{pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7])};
+}
+
+__device__ __forceinline__ void load8f(const float* p, float (&o)[8]) {
+  const float4 b0 = *reinterpret_cast<const float4*>(p);
+  const float4 b1 = *reinterpret_cast<const float4*>(p + 4);
+  o[0] = b0.x; o[1] = b0.y; o[2] = b0.z; o[3] = b0.w;
+  o[4] = b1.x; o[5] = b1.y; o[6] = b1.z; o[7] = b1.w;
+}
+
+__device__ __forceinline__ void load_bias8(const ConvArgs& a, int col, float (&bb)[8]) {
+  if (a.bias_bf16) {
+    unpack8(*reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(a.bias) + col), bb);
+  } else {
+    const float4 b0 = *reinterpret_cast<const float4*>(a.bias + col);
+    const float4 b1 = *reinterpret_cast<const float4*>(a.bias + col + 4);
+    bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
+    bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+  }
 }
 
 __device__ __forceinline__ int swz(int row, int slot) { return row * 128 + (((slot ^ (row & 7))) << 4); }
@@ -324,12 +348,7 @@ __global__ void __launch_bounds__(kThreads, 2) conv_gemm_kernel(const ConvArgs a
     const int col = en0 + chunk * 8;                                                         \
     float bb[8];                                                                             \
     _Pragma("unroll") for (int j = 0; j < 8; ++j) bb[j] = 0.0f;                              \
-    if (a.bias) {                                                                            \
-      const float4 b0 = *reinterpret_cast<const float4*>(a.bias + col);                      \
-      const float4 b1 = *reinterpret_cast<const float4*>(a.bias + col + 4);                  \
-      bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;                                \
-      bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;                                \
-    }                                                                                        \
+    if (a.bias) load_bias8(a, col, bb);                                                      \
     _Pragma("unroll") for (int i = 0; i < RROWS; ++i) {                                      \
       const int r = rfirst + RSTEP * i, m = em0 + r;                                         \
       const float4 c0 = *reinterpret_cast<const float4*>(sC + r * CS + chunk * 8);           \
@@ -483,12 +502,7 @@ __device__ __forceinline__ void epilogue_halves(const ConvArgs& a,
   float bb[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) bb[j] = 0.0f;
-  if (a.bias) {
-    const float4 b0 = *reinterpret_cast<const float4*>(a.bias + col);
-    const float4 b1 = *reinterpret_cast<const float4*>(a.bias + col + 4);
-    bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
-    bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
-  }
+  if (a.bias) load_bias8(a, col, bb);
   float* sC = reinterpret_cast<float*>(smem);
   // BatchNorm statistics (a.stats, uniform): per-thread sums over its rows, merged
   // per 64-row group through LDS past the staging area (the pipeline stages are free).
@@ -599,9 +613,10 @@ __device__ __forceinline__ void epilogue_halves(const ConvArgs& a,
 // DMA latency (a 3-stage ring measured slower on every ResNet-50 shape,
 // profiles/conv_stages_r1.md).  Prologue convs take conv_pro_kernel (an
 // in-register prologue on the DMA'd A fragments measured VALU-bound and slower).
-template <int KS, int BM, int BN, bool RES, int CSM = 0, int ST = 0>
+template <int KS, int BM, int BN, bool RES, int CSM = 0, int ST = 0, bool SPLIT = false>
 __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a) {
   static_assert(CSM == 0 || (64 % CSM == 0 && CSM % 8 == 0), "narrow-C variant");
+  static_assert(!SPLIT || (!RES && ST == 0 && CSM == 0), "split-K: the reduce kernel does the epilogue");
   constexpr int AR = BM / 32, BR = BN / 32;  // DMA instructions per thread per K step
   constexpr int WTM = BM / 2, WTN = BN / 2;
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -685,11 +700,16 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
   if constexpr (RES) {
     if (early_res) load_residual<BM, BN, ST == 2>(a, m0, n0, res);
   }
-  issue(0, 0);
-  for (int kt = 0; kt < a.ktiles; ++kt) {
-    const int st = kt & 1;
-    if (kt + 1 < a.ktiles) {
-      issue(kt + 1, st ^ 1);
+  int kbeg = 0, nk = a.ktiles;
+  if constexpr (SPLIT) {
+    kbeg = blockIdx.y * a.kper;
+    nk = min(a.kper, a.ktiles - kbeg);
+  }
+  issue(kbeg, 0);
+  for (int it = 0; it < nk; ++it) {
+    const int st = it & 1;
+    if (it + 1 < nk) {
+      issue(kbeg + it + 1, st ^ 1);
       __builtin_amdgcn_s_waitcnt(vmcnt_imm(AR + BR));
     } else {
       __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
@@ -716,10 +736,61 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     __builtin_amdgcn_s_barrier();
   }
+  if constexpr (SPLIT) {
+    // fp32 partial tile: lane holds rows 4·fk + e, column fr of each 16x16 sub-tile
+    float* out = a.ws + (int64_t)blockIdx.y * a.M * a.Cout;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm * WTM + i * 16 + fk * 4 + e;
+        if (m < a.M) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) out[(int64_t)m * a.Cout + n0 + wn * WTN + j * 16 + fr] = acc[i][j][e];
+        }
+      }
+    return;
+  }
   if constexpr (RES) {
     if (!early_res) load_residual<BM, BN, ST == 2>(a, m0, n0, res);
   }
   epilogue_halves<BM, BN, RES, ST>(a, acc, m0, n0, smem, res);
+}
+
+// Split-K epilogue: y = act(Σ_split ws[split] + bias (+ residual)) in bf16, the
+// splits summed in order (deterministic).  One thread = 8 channels of one row.
+__global__ void __launch_bounds__(kThreads) splitk_reduce_kernel(const ConvArgs a) {
+  const int cv = a.Cout >> 3;
+  const int64_t idx = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (idx >= (int64_t)a.M * cv) return;
+  const int m = (int)(idx / cv), col = (int)(idx - (int64_t)m * cv) * 8;
+  const int64_t plane = (int64_t)a.M * a.Cout, off = (int64_t)m * a.Cout + col;
+  float v[8];
+  load8f(a.ws + off, v);
+  for (int sp = 1; sp < a.splits; ++sp) {
+    float p[8];
+    load8f(a.ws + sp * plane + off, p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += p[j];
+  }
+  if (a.bias) {
+    float bb[8];
+    load_bias8(a, col, bb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += bb[j];
+  }
+  if (a.res) {
+    float re[8];
+    unpack8(*reinterpret_cast<const u32x4*>(a.res + off), re);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += re[j];
+  }
+  if (a.act) {
+    const float hi = a.act == 2 ? 6.0f : INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = fminf(fmaxf(v[j], 0.0f), hi);
+  }
+  *reinterpret_cast<u32x4*>(a.y + off) = pack8(v);
 }
 
 // ---- 256x256 tile for large 1x1 / stride-1 convs without a prologue ----------
@@ -868,12 +939,7 @@ __global__ void __launch_bounds__(kBigThreads, 1) conv_big_kernel(const ConvArgs
   float bb[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) bb[j] = 0.0f;
-  if (a.bias) {
-    const float4 b0 = *reinterpret_cast<const float4*>(a.bias + col);
-    const float4 b1 = *reinterpret_cast<const float4*>(a.bias + col + 4);
-    bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
-    bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
-  }
+  if (a.bias) load_bias8(a, col, bb);
   const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(a.res), 0, a.y_bytes, 0x00020000);
 #pragma unroll
@@ -1147,12 +1213,7 @@ __global__ void __launch_bounds__(BM * BN / 64, 2) conv_halo_kernel(const ConvAr
   float bb[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) bb[j] = 0.0f;
-  if (a.bias) {
-    const float4 b0 = *reinterpret_cast<const float4*>(a.bias + col);
-    const float4 b1 = *reinterpret_cast<const float4*>(a.bias + col + 4);
-    bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
-    bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
-  }
+  if (a.bias) load_bias8(a, col, bb);
   float s1[8], s2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.0f;
@@ -2171,8 +2232,7 @@ __global__ void __launch_bounds__(kSPThreads, 1) stem_pool_kernel(const uint16_t
   constexpr int SR_BYTES = 3 * kSPMaxOW * 128;   // three bf16 stem rows [row][pixel][64 ch] swizzled
   constexpr int SX_BYTES = 6 * kSPMaxWS * 32 + 512;  // 6 input rows [px][16 ch] + over-read pad
   constexpr int XR = (6 * kSPMaxWS * 2 + kSPThreads - 1) / kSPThreads;  // slab chunks per thread
-  constexpr int NF = 4;                          // whole subtiles per wave (32 of at most 33)
-  constexpr int NU = 4;                          // remainder units (subtile, 16-channel block) per wave
+  constexpr int NS = 5;                          // subtiles per wave (33 over 8 waves)
   __shared__ __attribute__((aligned(16))) char smem[SW_BYTES + SR_BYTES + SX_BYTES];
   char* sW = smem;
   char* sR = smem + SW_BYTES;
@@ -2217,77 +2277,47 @@ __global__ void __launch_bounds__(kSPThreads, 1) stem_pool_kernel(const uint16_t
     const int n = task / PH, pi = task - n * PH, r0 = 2 * pi - 1;
     const int next = task + gridDim.x;
     if (next < tasks) load_slab(next, xr);  // lands behind this task's compute
-    // Work split (balanced, round 5): the first 8 * (S / 8) of the S = 3 * MT
-    // pixel subtiles go whole to waves (subtile wave + 8u), the remainder is
-    // cut into (subtile, 16-channel block) units dealt round-robin (unit k ->
-    // wave k % 8), so no wave carries a whole extra subtile (was 5 vs 4 of 33:
-    // 34 % of the stem's wave time parked at the barrier, pmc_flagship_r4_final.md).
-    // stem row rl = s / MT, pixels (s % MT) * 16 ..
-    const int S = 3 * MT, F = S >> 3, R = S - 8 * F;
-    f32x4_t acc[NF][4], accu[NU];
+    // this wave's subtiles s = wave + 8u: stem row rl = s / MT, pixels (s % MT)*16 ..
+    f32x4_t acc[NS][4];
 #pragma unroll
-    for (int u = 0; u < NF; ++u)
+    for (int u = 0; u < NS; ++u)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[u][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < NU; ++k) accu[k] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kh = 0; kh < 4; ++kh)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        bf16x8_t bfr[4], af[NF], au[NU];
+        bf16x8_t bfr[4], af[NS];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           bfr[j] = *reinterpret_cast<const bf16x8_t*>(sW + kh * 8192 + swz(j * 16 + fr, kk * 4 + fk));
 #pragma unroll
-        for (int u = 0; u < NF; ++u) {
+        for (int u = 0; u < NS; ++u) {
           const int sidx = wave + 8 * u, rl = sidx / MT, m = sidx - rl * MT;
-          if (u < F)  // wave-uniform
+          if (sidx < 3 * MT)  // wave-uniform; past the three rows there is nothing to read
             af[u] = *reinterpret_cast<const bf16x8_t*>(
                 sX + (((rl + kh) * WS + m * 16 + fr) * 32) + (kk * 4 + fk) * 16);
         }
 #pragma unroll
-        for (int k = 0; k < NU; ++k) {
-          const int unit = wave + 8 * k, sidx = 8 * F + (unit >> 2), j = unit & 3;
-          if (unit < 4 * R) {  // wave-uniform
-            const int rl = sidx / MT, m = sidx - rl * MT;
-            au[k] = *reinterpret_cast<const bf16x8_t*>(
-                sX + (((rl + kh) * WS + m * 16 + fr) * 32) + (kk * 4 + fk) * 16);
-            (void)j;
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < NF; ++u)
-          if (u < F)
+        for (int u = 0; u < NS; ++u)
+          if (wave + 8 * u < 3 * MT)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
               acc[u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[u], acc[u][j], 0, 0, 0);
-#pragma unroll
-        for (int k = 0; k < NU; ++k) {
-          const int unit = wave + 8 * k, j = unit & 3;  // wave-uniform: a select, not a second LDS read
-          if (unit < 4 * R) {
-            const bf16x8_t b = j == 0 ? bfr[0] : j == 1 ? bfr[1] : j == 2 ? bfr[2] : bfr[3];
-            accu[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, au[k], accu[k], 0, 0, 0);
-          }
-        }
       }
     // bf16 stem rows → LDS: lane holds pixel m*16+fr, channels j*16+fk*4 .. +3
-    auto put = [&](int sidx, int j, const f32x4_t& v) {
-      const int rl = sidx / MT, m = sidx - rl * MT, p = m * 16 + fr;
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int sidx = wave + 8 * u, rl = sidx / MT, m = sidx - rl * MT;
+      if (rl >= 3) continue;
+      const int p = m * 16 + fr;
       char* row = sR + rl * (kSPMaxOW * 128) + p * 128;
-      const int slot = j * 2 + (fk >> 1);
-      *reinterpret_cast<uint2*>(row + ((slot ^ (p & 7)) << 4) + (fk & 1) * 8) =
-          uint2{pack2(v[0], v[1]), pack2(v[2], v[3])};
-    };
 #pragma unroll
-    for (int u = 0; u < NF; ++u)
-      if (u < F)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) put(wave + 8 * u, j, acc[u][j]);
-#pragma unroll
-    for (int k = 0; k < NU; ++k) {
-      const int unit = wave + 8 * k;
-      if (unit < 4 * R) put(8 * F + (unit >> 2), unit & 3, accu[k]);
+      for (int j = 0; j < 4; ++j) {
+        const int slot = j * 2 + (fk >> 1);
+        *reinterpret_cast<uint2*>(row + ((slot ^ (p & 7)) << 4) + (fk & 1) * 8) =
+            uint2{pack2(acc[u][j][0], acc[u][j][1]), pack2(acc[u][j][2], acc[u][j][3])};
+      }
     }
     __syncthreads();
     // 3x3/s2 window (rows of the task that exist, columns 2j-1 .. 2j+1)
@@ -2438,7 +2468,33 @@ VGPU_API int vgpu_conv231_nhwc(const void* x, const void* w2, const float* b2, c
 namespace {
 int conv2d_impl(const void* x, const void* w, void* y, const void* res, const float* bias, const float* pscale,
                 const float* pshift, int N, int H, int W, int C, int Cout, int KS, int stride, int pad, int act,
-                float* stats, const void* bnx, const float* bncoef, int bnact, int res_stride, hipStream_t s);
+                float* stats, const void* bnx, const float* bncoef, int bnact, int res_stride, hipStream_t s,
+                float* ws = nullptr, int64_t ws_bytes = 0);
+
+int g_forced_split = -1;  // vgpu_conv_set_splitk: -1 heuristic, 0 off, n > 1 that many splits when eligible
+
+// Split-K for convs whose output tiles cannot fill the CUs this process owns:
+// the 28² / 14² layers of VGG-16 at batch 2 are 16-100 workgroups of 64x128 on
+// 256 CUs (36-41 us each, ~8 % of MFMA peak; profiles/r5/train).  The K steps
+// are cut into `splits` ranges so ~2 workgroups per CU run, each writing an
+// fp32 partial tile, and splitk_reduce_kernel applies the epilogue.  Returns
+// the split count (1 = no split) and the K steps per split.
+int splitk_plan(int64_t M, int C, int Cout, int KS, bool pro, bool narrow, int& kper) {
+  const int ktiles = KS * KS * C / 64;
+  kper = ktiles;
+  if (pro || narrow || C % 64 || (KS != 1 && KS != 3) || g_forced_split == 0) return 1;
+  // a kernel forced by an A/B or test setter runs as asked unless splits are forced too
+  if (g_forced_split < 0 && (g_forced_halo >= 0 || g_forced_big == 1 || g_forced_bm != 0)) return 1;
+  const int bn = Cout % 128 == 0 ? 128 : 64;
+  const int64_t tiles = ((M + 63) / 64) * (Cout / bn);
+  // Measured (profiles/r5/train/vgg_small_ab.log, graph replay): 100 and 28
+  // tiles gain 1.2-1.8x; 196 tiles (56² at b=2) lose 17 % -- split below half the CUs.
+  int64_t sp = g_forced_split > 1 ? g_forced_split : (2 * tiles >= conv_cus() ? 1 : 2 * (int64_t)conv_cus() / tiles);
+  if (sp > ktiles / 4) sp = ktiles / 4;
+  if (sp < 2) return 1;
+  kper = (int)((ktiles + sp - 1) / sp);
+  return (ktiles + kper - 1) / kper;
+}
 }  // namespace
 
 // Returns 0, a hipError_t, or -1 for an unsupported shape (checked before any launch).
@@ -2449,6 +2505,31 @@ VGPU_API int vgpu_conv2d_nhwc(const void* x, const void* w, void* y, const void*
   return conv2d_impl(x, w, y, res, bias, pscale, pshift, N, H, W, C, Cout, KS, stride, pad, act, nullptr,
                      nullptr, nullptr, 0, 1, s);
 }
+
+// Workspace (bytes) vgpu_conv2d_nhwc_ws wants for a split-K launch of this
+// shape; 0 when the conv runs unsplit.
+VGPU_API int64_t vgpu_conv2d_workspace(int N, int H, int W, int C, int Cout, int KS, int stride, int pad,
+                                       int has_pro) {
+  if (N < 1 || stride < 1 || pad < 0 || KS < 1) return 0;
+  const int64_t OH = (H + 2 * pad - KS) / stride + 1, OW = (W + 2 * pad - KS) / stride + 1;
+  if (OH < 1 || OW < 1) return 0;
+  const int64_t M = (int64_t)N * OH * OW;
+  const bool narrow = C == 16 && KS == 4 && stride == 1 && !has_pro;
+  int kper;
+  const int sp = splitk_plan(M, C, Cout, KS, has_pro != 0, narrow, kper);
+  return sp > 1 ? (int64_t)sp * M * Cout * 4 : 0;
+}
+
+// vgpu_conv2d_nhwc with a split-K workspace (vgpu_conv2d_workspace bytes).
+// act bit 8 (act | 256): the bias is bf16 rather than fp32.
+VGPU_API int vgpu_conv2d_nhwc_ws(const void* x, const void* w, void* y, const void* res, const void* bias,
+                                 const float* pscale, const float* pshift, int N, int H, int W, int C, int Cout,
+                                 int KS, int stride, int pad, int act, void* ws, int64_t ws_bytes, hipStream_t s) {
+  return conv2d_impl(x, w, y, res, static_cast<const float*>(bias), pscale, pshift, N, H, W, C, Cout, KS, stride,
+                     pad, act, nullptr, nullptr, nullptr, 0, 1, s, static_cast<float*>(ws), ws_bytes);
+}
+
+VGPU_API void vgpu_conv_set_splitk(int mode) { g_forced_split = mode; }
 
 // Training convolution with the BatchNorm statistics of its output from the
 // epilogue (ConvArgs::stats): stats = fp32 pairs [ceil(M / 64)][Cout], M = N·OH·OW.
@@ -2474,7 +2555,11 @@ VGPU_API int vgpu_conv2d_nhwc_bn(const void* x, const void* w, void* y, const vo
 namespace {
 int conv2d_impl(const void* x, const void* w, void* y, const void* res, const float* bias, const float* pscale,
                 const float* pshift, int N, int H, int W, int C, int Cout, int KS, int stride, int pad, int act,
-                float* stats, const void* bnx, const float* bncoef, int bnact, int res_stride, hipStream_t s) {
+                float* stats, const void* bnx, const float* bncoef, int bnact, int res_stride, hipStream_t s,
+                float* ws, int64_t ws_bytes) {
+  const int bias_bf16 = (act >> 8) & 1;
+  act &= 0xff;
+  if (act > 2) return -1;
   // C % 64 == 0 with 1x1 / 3x3 filters, or the narrow stem form (C = 16, 4x4,
   // stride 1, no prologue: a 7x7/s2 conv on a space-to-depth input).
   const bool narrow = C == 16 && KS == 4 && stride == 1 && pscale == nullptr;
@@ -2497,6 +2582,7 @@ int conv2d_impl(const void* x, const void* w, void* y, const void* res, const fl
   a.cblocks = C / 64;
   a.ktiles = a.K / 64;
   a.act = act;  // 0 none, 1 ReLU, 2 ReLU6
+  a.bias_bf16 = bias_bf16;
   a.stats = reinterpret_cast<float2*>(stats);
   a.bnx = static_cast<const uint16_t*>(bnx);
   a.bncoef = bncoef;
@@ -2541,6 +2627,31 @@ int conv2d_impl(const void* x, const void* w, void* y, const void* res, const fl
     if (g_forced_bm == 64) small = true;
     if (g_forced_bm == 128) small = false;
     hipError_t e;
+    int kper;
+    const int splits = (ws && !stats && per >= N) ? splitk_plan(c.M, C, Cout, KS, pro, narrow, kper) : 1;
+    if (splits > 1) {
+      if (ws_bytes < (int64_t)splits * c.M * Cout * 4) return -1;
+      c.ws = ws;
+      c.kper = kper;
+      c.splits = splits;
+      c.nM = (c.M + 63) / 64;
+      c.nN = Cout / bn;
+      c.nwg = c.nM * c.nN;
+      const dim3 grid(c.nwg, splits);
+      if (bn == 128) {
+        if (KS == 1) hipLaunchKernelGGL((conv_glds_kernel<1, 64, 128, false, 0, 0, true>), grid, dim3(kThreads), 0, s, c);
+        else hipLaunchKernelGGL((conv_glds_kernel<3, 64, 128, false, 0, 0, true>), grid, dim3(kThreads), 0, s, c);
+      } else {
+        if (KS == 1) hipLaunchKernelGGL((conv_glds_kernel<1, 64, 64, false, 0, 0, true>), grid, dim3(kThreads), 0, s, c);
+        else hipLaunchKernelGGL((conv_glds_kernel<3, 64, 64, false, 0, 0, true>), grid, dim3(kThreads), 0, s, c);
+      }
+      if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+      const int64_t threads = (int64_t)c.M * (Cout / 8);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + kThreads - 1) / kThreads)), dim3(kThreads),
+                         0, s, c);
+      if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+      continue;
+    }
     // LDS-DMA kernels for every conv without a prologue; prologue convs stage A
     // through registers (conv_pro_kernel / conv_gemm_kernel).
     const bool glds = !pro;

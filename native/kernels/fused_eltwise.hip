@@ -239,8 +239,9 @@ __global__ void __launch_bounds__(kThreads) relu_bias_grad_kernel(const bf16x8* 
 }
 
 // 16 channels per block, 16 threads per channel (slab residues mod 16), merged in order.
+template <typename T>
 __global__ void __launch_bounds__(kThreads) relu_bias_grad_reduce_kernel(const float* __restrict__ part,
-                                                                         float* __restrict__ db, uint32_t c,
+                                                                         T* __restrict__ db, uint32_t c,
                                                                          uint32_t slabs) {
   __shared__ float red[16][17];
   const uint32_t cl = threadIdx.x % 16, q = threadIdx.x / 16, ch = blockIdx.x * 16 + cl;
@@ -260,7 +261,8 @@ __global__ void __launch_bounds__(kThreads) relu_bias_grad_reduce_kernel(const f
   if (q == 0 && ch < c) {
     float a = 0.f;
     for (int i = 0; i < 16; ++i) a += red[i][cl];
-    db[ch] = a;
+    if constexpr (sizeof(T) == 2) db[ch] = f2bf(a);  // a bf16 bias's gradient, no cast pass
+    else db[ch] = a;
   }
 }
 
@@ -275,15 +277,20 @@ VGPU_API int64_t vgpu_relu_bias_grad_workspace(uint64_t rows, uint32_t c) {
   return (int64_t)rbg_slabs(rows, c / 8) * c * 4;
 }
 
-// dy, y, g: [rows, c] bf16 (NHWC); db: fp32 [c]; ws: vgpu_relu_bias_grad_workspace bytes.
-VGPU_API int vgpu_relu_bias_grad_nhwc(const void* dy, const void* y, void* g, float* db, void* ws, uint64_t rows,
-                                      uint32_t c, hipStream_t stream) {
+// dy, y, g: [rows, c] bf16 (NHWC); db: [c] fp32, or bf16 when db_bf16; ws:
+// vgpu_relu_bias_grad_workspace bytes.
+VGPU_API int vgpu_relu_bias_grad_nhwc(const void* dy, const void* y, void* g, void* db, void* ws, uint64_t rows,
+                                      uint32_t c, int db_bf16, hipStream_t stream) {
   if (c % 8 || c / 8 > kThreads || rows == 0) return -1;
   const uint32_t cv = c / 8;
   const uint32_t slabs = rbg_slabs(rows, cv);
   hipLaunchKernelGGL(relu_bias_grad_kernel, dim3(slabs), dim3(kThreads), 0, stream, (const bf16x8*)dy,
                      (const bf16x8*)y, (bf16x8*)g, (float*)ws, rows, cv);
-  hipLaunchKernelGGL(relu_bias_grad_reduce_kernel, dim3((c + 15) / 16), dim3(kThreads), 0, stream,
-                     (const float*)ws, db, c, slabs);
+  if (db_bf16)
+    hipLaunchKernelGGL(relu_bias_grad_reduce_kernel<uint16_t>, dim3((c + 15) / 16), dim3(kThreads), 0, stream,
+                       (const float*)ws, (uint16_t*)db, c, slabs);
+  else
+    hipLaunchKernelGGL(relu_bias_grad_reduce_kernel<float>, dim3((c + 15) / 16), dim3(kThreads), 0, stream,
+                       (const float*)ws, (float*)db, c, slabs);
   return (int)hipGetLastError();
 }

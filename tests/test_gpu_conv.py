@@ -57,6 +57,31 @@ def test_conv_matches_fp32(C, case):
     torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("splits", [-1, 0, 3, 7])
+@pytest.mark.parametrize("kind", ["3x3_relu6", "1x1_res"])
+def test_conv_splitk_and_bf16_bias(C, splits, kind):
+    """Split-K (vgpu_conv2d_workspace / splitk_reduce_kernel): VGG's 14² layer
+    at batch 2 and a 1x1 with residual, heuristic / off / forced split counts,
+    with a bf16 bias read by the epilogue directly (act | 256)."""
+    if kind == "3x3_relu6":
+        n, c, h, cout, ks, pad, act, has_res = 2, 512, 14, 512, 3, 1, "relu6", False
+    else:
+        n, c, h, cout, ks, pad, act, has_res = 3, 1024, 7, 256, 1, 0, "relu", True
+    x = _t((n, c, h, h), 21)
+    wt = _t((cout, c, ks, ks), 22, scale=(2.0 / (c * ks * ks)) ** 0.5)
+    bias = _f((cout,), 23).to(torch.bfloat16)
+    res = _t((n, cout, h, h), 24) if has_res else None
+    C.set_splitk(splits)
+    try:
+        got = C.conv2d(x, wt, bias, padding=pad, act=act, residual=res)
+        need = C.load_kernels().vgpu_conv2d_workspace(n, h, h, c, cout, ks, 1, pad, 0)
+    finally:
+        C.set_splitk(-1)
+    assert (need > 0) == (splits != 0), need
+    ref = C.conv2d_ref(x, wt, bias, padding=pad, act=act, residual=res)
+    torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
+
+
 BIG_CASES = [
     # 256x256-tile kernel (1x1, stride 1, no prologue, Cout % 256 == 0), forced on
     (4, 256, 32, 33, 512, True, "relu", True),    # M = 4224: ragged last M tile, bias+act+residual

@@ -412,7 +412,7 @@ def test_suspend_evict_gives_64gb_to_a_high_priority_pod(gpu_build, vehicle):
         else:
             assert ready["ranges"] == 16 and ready["in_hbm"] >= 64 * GiB, ready
         if vehicle == "vmm_reserve":
-            time.sleep(6)  # the reserve is pinned in the background (~23 GB/s)
+            time.sleep(10)  # the reserve is pinned in the background (13-23 GB/s)
         total, used0 = _vram_used()
         free0 = total - used0
         a.send_signal(signal.SIGUSR2)
@@ -449,8 +449,15 @@ def test_suspend_evict_gives_64gb_to_a_high_priority_pod(gpu_build, vehicle):
         assert v["errors"] == 0, v
         if vehicle.startswith("vmm"):
             assert v["vmm_cycles"] == 1 and v["vmm_evicted"] == 0, v
-            limit = 2.0 if vehicle == "vmm_reserve" else 4.0  # 2 s each way
-            assert v["vmm_suspend_s"] <= limit and v["vmm_resume_s"] <= limit, v
+            # 2 s each way.  Without the reserve the suspend also
+            # waits for the kernel to clear 64 GiB of fresh host pages (13-23 GB/s
+            # depending on the node, profiles/r5/vmem): the vehicle's own part
+            # (copies and unmapping, the time not spent pinning) is held to 2 s.
+            assert v["vmm_resume_s"] <= 2.0, v
+            if vehicle == "vmm_reserve":
+                assert v["vmm_suspend_s"] <= 2.0, v
+            else:
+                assert v["vmm_suspend_s"] - v["vmm_pin_s"] <= 2.0 and v["vmm_suspend_s"] <= 8.0, v
         else:
             assert v["swap_out"] >= 64 * GiB, v
         a.stdin.write("EXIT\n")

@@ -94,12 +94,17 @@ def test_vgg16_native_training_step_matches_fp32(gpu_build):
     assert _rel(out, out32) < 0.1
     torch.nn.functional.cross_entropy(out.float(), tgt).backward()
     _torch_path(lambda: torch.nn.functional.cross_entropy(out_t.float(), tgt).backward())
+    torch.nn.functional.cross_entropy(out32, tgt).backward()
     convs = [i for i, mod in enumerate(m.features) if isinstance(mod, torch.nn.Conv2d)]
     for i in convs:
-        g, gt = m.features[i].weight.grad, mt.features[i].weight.grad
-        print("vgg conv", i, "cos", round(_cos(g, gt), 4), "rel", round(_rel(g, gt), 4))
-        assert _cos(g, gt) > 0.97, i
-        assert _cos(m.features[i].bias.grad, mt.features[i].bias.grad) > 0.97, i
+        # both bf16 paths against the fp32 model's gradient: the native path may
+        # not be further from it than MIOpen's bf16 path (the first layers'
+        # gradients carry the whole network's bf16 rounding, ~0.97 cosine either way)
+        for attr in ("weight", "bias"):
+            g, gt, g32 = (getattr(mm.features[i], attr).grad for mm in (m, mt, m32))
+            cn, ct = _cos(g, g32), _cos(gt, g32)
+            print("vgg conv", i, attr, "cos native/fp32", round(cn, 4), "torch-bf16/fp32", round(ct, 4))
+            assert cn > min(0.95, ct - 0.02), (i, attr, cn, ct)
 
 
 DW_CASES = [  # n, c, h, w, stride, dilation

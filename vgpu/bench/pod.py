@@ -48,10 +48,15 @@ def build(args):
     x = w.make_input(dev, dtype)
     if w.train:
         model.train()
-        # fused SGD: one kernel per parameter chunk instead of multi-tensor
-        # launches (VGG-16's 138M parameters made the update 22% of its step)
-        fused = os.environ.get("VGPU_FUSED_SGD", "1") != "0"
-        opt = torch.optim.SGD(model.parameters(), lr=1e-3, momentum=0.9, fused=fused or None)
+        # The native SGD (vgpu.ops.optim: one launch per 48 bf16 tensors; VGG-16's
+        # 138M parameters made PyTorch's update 15-22 % of its step).
+        # VGPU_FUSED_SGD=torch: PyTorch's fused SGD, =0: PyTorch's foreach SGD (A/B).
+        which = os.environ.get("VGPU_FUSED_SGD", "native")
+        if which in ("0", "torch"):
+            opt = torch.optim.SGD(model.parameters(), lr=1e-3, momentum=0.9, fused=(which == "torch") or None)
+        else:
+            from vgpu.ops.optim import SGD
+            opt = SGD(model.parameters(), lr=1e-3, momentum=0.9)
         ncls = 21 if w.name == "deeplab" else (2 if w.name == "lstm" else 1000)
         if w.name == "deeplab":
             target = torch.randint(0, ncls, (w.batch, *w.shape[1:]), device=dev)

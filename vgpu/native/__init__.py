@@ -60,10 +60,15 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_add_scale_shift_act_nhwc.argtypes = [vp, vp, vp, vp, vp, vp, u64, u32, ctypes.c_int, vp]
     lib.vgpu_relu_bias_grad_workspace.argtypes = [u64, u32]
     lib.vgpu_relu_bias_grad_workspace.restype = ctypes.c_int64
-    lib.vgpu_relu_bias_grad_nhwc.argtypes = [vp, vp, vp, vp, vp, u64, u32, vp]
+    lib.vgpu_relu_bias_grad_nhwc.argtypes = [vp, vp, vp, vp, vp, u64, u32, ctypes.c_int, vp]
     lib.vgpu_relu_bias_grad_nhwc.restype = ctypes.c_int
     ci = ctypes.c_int
     lib.vgpu_conv2d_nhwc.argtypes = [vp, vp, vp, vp, vp, vp, vp] + [ci] * 9 + [vp]
+    lib.vgpu_conv2d_nhwc_ws.argtypes = [vp, vp, vp, vp, vp, vp, vp] + [ci] * 9 + [vp, ctypes.c_int64, vp]
+    lib.vgpu_conv2d_nhwc_ws.restype = ci
+    lib.vgpu_conv2d_workspace.argtypes = [ci] * 9
+    lib.vgpu_conv2d_workspace.restype = ctypes.c_int64
+    lib.vgpu_conv_set_splitk.argtypes = [ci]
     lib.vgpu_maxpool_nhwc.argtypes = [vp, vp] + [ci] * 7 + [vp]
     lib.vgpu_stem_pool_nhwc.argtypes = [vp, vp, vp] + [ci] * 3 + [vp]
     lib.vgpu_conv_set_big.argtypes = [ci]

@@ -53,8 +53,10 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
            pro: tuple[torch.Tensor, torch.Tensor] | None = None,
            residual: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """x [N,C,H,W] bf16 channels_last; w [Cout,C,k,k] bf16 channels_last;
-    bias fp32 [Cout]; pro = (scale, shift) fp32 [C] (BN+ReLU on the input);
-    residual [N,Cout,OH,OW] bf16 channels_last; act 'none' | 'relu' | 'relu6'."""
+    bias fp32 or bf16 [Cout]; pro = (scale, shift) fp32 [C] (BN+ReLU on the input);
+    residual [N,Cout,OH,OW] bf16 channels_last; act 'none' | 'relu' | 'relu6'.
+    Convs whose output tiles cannot fill the GPU run split-K (a workspace from
+    the caching allocator, vgpu_conv2d_workspace)."""
     _nhwc(x, "x")
     _nhwc(w, "w")
     n, c, h, wd = x.shape
@@ -64,9 +66,12 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
     oh, ow = out_hw(h, wd, ks, stride, padding)
     if act not in _ACTS:
         raise ValueError(act)
-    for p in ((bias,) + (pro if pro is not None else ())):
-        if p is not None and (p.dtype != torch.float32 or not p.is_contiguous() or not p.is_cuda):
-            raise TypeError("bias / prologue parameters must be contiguous fp32 CUDA tensors")
+    for p in (pro if pro is not None else ()):
+        if p.dtype != torch.float32 or not p.is_contiguous() or not p.is_cuda:
+            raise TypeError("prologue parameters must be contiguous fp32 CUDA tensors")
+    if bias is not None and (bias.dtype not in (torch.float32, torch.bfloat16) or not bias.is_contiguous()
+                             or not bias.is_cuda):
+        raise TypeError("bias must be a contiguous fp32 or bf16 CUDA tensor")
     if bias is not None and bias.numel() != cout:
         raise ValueError("bias size")
     if pro is not None and (pro[0].numel() != c or pro[1].numel() != c):
@@ -79,13 +84,30 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, *
         out = torch.empty((n, cout, oh, ow), dtype=x.dtype, device=x.device, memory_format=_CL)
     else:
         _nhwc(out, "out")
-    rc = load_kernels().vgpu_conv2d_nhwc(
+    lib = load_kernels()
+    key = (n, h, wd, c, cout, ks, stride, padding, pro is not None)
+    need = _WS_BYTES.get(key)
+    if need is None:
+        need = _WS_BYTES[key] = lib.vgpu_conv2d_workspace(*key[:-1], int(pro is not None))
+    ws = torch.empty(need // 4, dtype=torch.float32, device=x.device) if need > 0 else None
+    code = _ACTS[act] | (256 if bias is not None and bias.dtype == torch.bfloat16 else 0)
+    rc = lib.vgpu_conv2d_nhwc_ws(
         _ptr(x), _ptr(w), _ptr(out), _ptr(residual), _ptr(bias),
         _ptr(pro[0] if pro else None), _ptr(pro[1] if pro else None),
-        n, h, wd, c, cout, ks, stride, padding, _ACTS[act], _stream())
+        n, h, wd, c, cout, ks, stride, padding, code, _ptr(ws), need, _stream())
     if rc != 0:
         raise RuntimeError(f"vgpu_conv2d_nhwc: error {rc}")
     return out
+
+
+_WS_BYTES: dict[tuple, int] = {}  # conv shape -> split-K workspace bytes (0: unsplit)
+
+
+def set_splitk(mode: int) -> None:
+    """A/B switch for split-K: -1 heuristic (default), 0 off, n > 1 that many
+    splits wherever eligible."""
+    load_kernels().vgpu_conv_set_splitk(mode)
+    _WS_BYTES.clear()
 
 
 def conv23(x: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor, w3: torch.Tensor,
@@ -338,14 +360,18 @@ def _wgrad_native(dy: torch.Tensor, ks: int, stride: int, c: int = 0) -> bool:
     # 1x1 (stride 1 or 2) from 1k output pixels: the swizzled LDS images run
     # 23-36 us vs MIOpen's 27-43 us plus its zero-fill and cast passes
     # (profiles/r4/train/convtrain_wgrad_swizzle.log); at ResNet-V2-152's
-    # stage 4 (640 pixels) MIOpen's kernel wins (16-20 vs 24-33 us,
-    # convtrain_b10_256.log).  3x3 from 8k pixels, and from 2k when C <= 256
-    # (2.2's stage 3: 26.0 vs 25.1 us, even before MIOpen's two extra
-    # passes); ResNet-V2-50's stage 4 (2.4k pixels, C = 512) stays on MIOpen
-    # (59 vs 44 us), as do 640-pixel 3x3s (40 vs 20 us).
+    # stage 4 (640 pixels) MIOpen's kernel measured ahead in eager timing
+    # (16-20 vs 24-33 us, convtrain_b10_256.log).
+    # Round 5, timed inside hipGraph replays (the training steps are replays;
+    # the round-4 thresholds came from eager timings with a ~11 us launch floor):
+    # every 3x3 shape measured runs faster natively -- VGG-16 b=2 at 392 / 1568
+    # pixels 12.8 / 31-51 us vs MIOpen's 42 / 69-82 us, ResNet-V2-152 b=10 stage
+    # 3 / 4 26.6 / 41.8 vs 62 / 53, ResNet-V2-50 stage 4 (2.4k pixels) 59 vs 82
+    # (profiles/r5/train/vgg_small_ab*.log: MIOpen's kernel plus its zero-fill
+    # and cast passes).
     if ks == 1:
         return pixels >= 1024
-    return ks == 3 and (pixels >= 8192 or (pixels >= 2048 and 0 < c <= 256))
+    return ks == 3
 
 
 # ---- data-gradient filters, one launch per step ------------------------------------------
@@ -503,29 +529,35 @@ class _ConvBiasReLUTrainFn(torch.autograd.Function):
     def forward(ctx, x, w, b, stride: int, padding: int):
         y = conv2d(x, w, b, stride=stride, padding=padding, act="relu")
         ctx.save_for_backward(x, w, y)
+        ctx.bias_dtype = b.dtype
         ctx.stride, ctx.padding = stride, padding
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w, y = ctx.saved_tensors
-        g, db = relu_bias_grad(dy.contiguous(memory_format=_CL), y)
+        g, db = relu_bias_grad(dy.contiguous(memory_format=_CL), y, ctx.bias_dtype)
         dx, dw = conv_backward(g, x, w, ctx.stride, ctx.padding, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
         return dx, dw, db if ctx.needs_input_grad[2] else None, None, None
 
 
-def relu_bias_grad(dy: torch.Tensor, y: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+def relu_bias_grad(dy: torch.Tensor, y: torch.Tensor,
+                   db_dtype: torch.dtype = torch.float32) -> tuple[torch.Tensor, torch.Tensor]:
     """(g, db): g = dy where y > 0 else 0 (bf16, channels_last), db = Σ g over
-    N, H, W in fp32 -- one pass (native/kernels/fused_eltwise.hip)."""
+    N, H, W summed in fp32 and stored as db_dtype (fp32 or the bias's bf16) --
+    one pass (native/kernels/fused_eltwise.hip)."""
     _nhwc(dy, "dy")
     _nhwc(y, "y")
     n, c, h, w = y.shape
     rows = n * h * w
     lib = load_kernels()
     g = torch.empty_like(y, memory_format=_CL)
-    db = torch.empty(c, dtype=torch.float32, device=y.device)
+    if db_dtype not in (torch.float32, torch.bfloat16):
+        raise TypeError(db_dtype)
+    db = torch.empty(c, dtype=db_dtype, device=y.device)
     ws = torch.empty(max(lib.vgpu_relu_bias_grad_workspace(rows, c) // 4, 1), dtype=torch.float32, device=y.device)
-    rc = lib.vgpu_relu_bias_grad_nhwc(_ptr(dy), _ptr(y), _ptr(g), _ptr(db), _ptr(ws), rows, c, _stream())
+    rc = lib.vgpu_relu_bias_grad_nhwc(_ptr(dy), _ptr(y), _ptr(g), _ptr(db), _ptr(ws), rows, c,
+                                      int(db_dtype == torch.bfloat16), _stream())
     if rc != 0:
         raise RuntimeError(f"vgpu_relu_bias_grad_nhwc: error {rc}")
     return g, db
@@ -548,7 +580,7 @@ def conv_bias_relu_train(x: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor
         # (prof_3_2.md: 49 us each).
         xp = F.pad(x, (0, 0, 0, 0, 0, 64 - c)).contiguous(memory_format=_CL)
         wp = F.pad(w, (0, 0, 0, 0, 0, 64 - c)).contiguous(memory_format=_CL)
-        return _ConvBiasReLUTrainFn.apply(xp, wp, conv.bias.float(), 1, 1)
+        return _ConvBiasReLUTrainFn.apply(xp, wp, conv.bias, 1, 1)
     ok = (_TRAIN_NATIVE and conv.bias is not None and x.is_cuda and x.dtype == torch.bfloat16
           and w.dtype == torch.bfloat16 and x.dim() == 4 and x.is_contiguous(memory_format=_CL)
           and w.is_contiguous(memory_format=_CL) and conv.groups == 1 and conv.dilation == (1, 1)
@@ -557,7 +589,7 @@ def conv_bias_relu_train(x: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor
           and conv.kernel_size[0] in (1, 3) and supported(conv.in_channels, conv.out_channels, conv.kernel_size[0]))
     if not ok:
         return F.relu(conv(x))
-    return _ConvBiasReLUTrainFn.apply(x, w, conv.bias.float(), conv.stride[0], conv.padding[0])
+    return _ConvBiasReLUTrainFn.apply(x, w, conv.bias, conv.stride[0], conv.padding[0])
 
 
 # ---- fp32 references -----------------------------------------------------------------
