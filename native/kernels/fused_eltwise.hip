@@ -190,10 +190,20 @@ VGPU_API int vgpu_add_scale_shift_act_nhwc(const void* a, const void* b, void* s
 namespace {
 constexpr int kIters = 8;
 
+// Pooled variant (POOL): dy is the gradient of a k×k / stride-k max pool of y
+// ([N][H/k][W/k][C]) with its one-byte-per-element argmax (pool_train.hip);
+// the row's gradient is gathered from its window (the pool backward fused in).
+struct PoolGeo {
+  const bf16x8* dyp;
+  const uint2* idx;
+  int H, W, OH, OW, k;
+};
+
+template <bool POOL>
 __global__ void __launch_bounds__(kThreads) relu_bias_grad_kernel(const bf16x8* __restrict__ dy,
                                                                   const bf16x8* __restrict__ y,
                                                                   bf16x8* __restrict__ g, float* __restrict__ part,
-                                                                  uint64_t rows, uint32_t cv) {
+                                                                  uint64_t rows, uint32_t cv, const PoolGeo pg) {
   __shared__ float red[kThreads][9];  // 8 sums + pad (bank spread)
   const uint32_t t = threadIdx.x;
   const uint32_t per = kThreads / cv;  // rows in flight per block pass
@@ -202,11 +212,28 @@ __global__ void __launch_bounds__(kThreads) relu_bias_grad_kernel(const bf16x8* 
   if (r0 < per) {
     const uint64_t row0 = (uint64_t)blockIdx.x * per * kIters + r0;
     bf16x8 a[kIters], b[kIters];
+    uint32_t tap[kIters];
 #pragma unroll
     for (int k = 0; k < kIters; ++k) {
       const uint64_t r = row0 + (uint64_t)k * per;
       if (r < rows) {
-        a[k] = dy[r * cv + cg];
+        if constexpr (POOL) {
+          const uint32_t iw = (uint32_t)(r % pg.W), t2 = (uint32_t)(r / pg.W), ih = t2 % pg.H, n = t2 / pg.H;
+          const uint32_t oh = ih / pg.k, ow = iw / pg.k;
+          tap[k] = 0xffu;  // rows past the last full window receive no gradient
+          if (oh < (uint32_t)pg.OH && ow < (uint32_t)pg.OW) {
+            const uint64_t o = (((uint64_t)n * pg.OH + oh) * pg.OW + ow) * cv + cg;
+            a[k] = pg.dyp[o];
+            const uint2 t = pg.idx[o];
+            tap[k] = (ih - oh * pg.k) * pg.k + (iw - ow * pg.k);
+            // per channel j: keep dy where the window's argmax is this row
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if ((((j < 4 ? t.x : t.y) >> (8 * (j & 3))) & 0xffu) != tap[k]) a[k].v[j] = 0;
+          }
+        } else {
+          a[k] = dy[r * cv + cg];
+        }
         b[k] = y[r * cv + cg];
       }
     }
@@ -214,6 +241,12 @@ __global__ void __launch_bounds__(kThreads) relu_bias_grad_kernel(const bf16x8* 
     for (int k = 0; k < kIters; ++k) {
       const uint64_t r = row0 + (uint64_t)k * per;
       if (r >= rows) continue;
+      if constexpr (POOL) {
+        if (tap[k] == 0xffu) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) a[k].v[j] = 0;
+        }
+      }
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -284,8 +317,31 @@ VGPU_API int vgpu_relu_bias_grad_nhwc(const void* dy, const void* y, void* g, vo
   if (c % 8 || c / 8 > kThreads || rows == 0) return -1;
   const uint32_t cv = c / 8;
   const uint32_t slabs = rbg_slabs(rows, cv);
-  hipLaunchKernelGGL(relu_bias_grad_kernel, dim3(slabs), dim3(kThreads), 0, stream, (const bf16x8*)dy,
-                     (const bf16x8*)y, (bf16x8*)g, (float*)ws, rows, cv);
+  hipLaunchKernelGGL(relu_bias_grad_kernel<false>, dim3(slabs), dim3(kThreads), 0, stream, (const bf16x8*)dy,
+                     (const bf16x8*)y, (bf16x8*)g, (float*)ws, rows, cv, PoolGeo{});
+  if (db_bf16)
+    hipLaunchKernelGGL(relu_bias_grad_reduce_kernel<uint16_t>, dim3((c + 15) / 16), dim3(kThreads), 0, stream,
+                       (const float*)ws, (uint16_t*)db, c, slabs);
+  else
+    hipLaunchKernelGGL(relu_bias_grad_reduce_kernel<float>, dim3((c + 15) / 16), dim3(kThreads), 0, stream,
+                       (const float*)ws, (float*)db, c, slabs);
+  return (int)hipGetLastError();
+}
+
+// The same with the gradient arriving through a k×k / stride-k max pool of y
+// (no padding): dyp [N][H/k][W/k][c] and its argmax bytes idx (the layout of
+// vgpu_maxpool_fwd_idx_nhwc); y, g: [N][H][W][c].  One pass instead of the
+// pool backward plus this one (VGG-16's five conv + ReLU + pool blocks).
+VGPU_API int vgpu_pool_relu_bias_grad_nhwc(const void* dyp, const void* idx, const void* y, void* g, void* db,
+                                           void* ws, int N, int H, int W, uint32_t c, int k, int db_bf16,
+                                           hipStream_t stream) {
+  if (c % 8 || c / 8 > kThreads || N < 1 || H < 1 || W < 1 || k < 1 || k > 15 || H < k || W < k) return -1;
+  const uint32_t cv = c / 8;
+  const uint64_t rows = (uint64_t)N * H * W;
+  const uint32_t slabs = rbg_slabs(rows, cv);
+  const PoolGeo pg{(const bf16x8*)dyp, (const uint2*)idx, H, W, H / k, W / k, k};
+  hipLaunchKernelGGL(relu_bias_grad_kernel<true>, dim3(slabs), dim3(kThreads), 0, stream, nullptr,
+                     (const bf16x8*)y, (bf16x8*)g, (float*)ws, rows, cv, pg);
   if (db_bf16)
     hipLaunchKernelGGL(relu_bias_grad_reduce_kernel<uint16_t>, dim3((c + 15) / 16), dim3(kThreads), 0, stream,
                        (const float*)ws, (uint16_t*)db, c, slabs);

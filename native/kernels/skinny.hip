@@ -1,0 +1,326 @@
+// Fully connected layers at a handful of rows (batch ≤ 8: VGG-16 training at
+// b=2, ai-benchmark test 3.2).  Each of the three GEMMs of a training step is
+// a stream over the [N][K] weight with the batch rows riding along:
+//
+//   forward  y[b][n]  = act(Σ_k x[b][k]·W[n][k] + bias[n])       reads W once
+//   dgrad    dx[b][k] = Σ_n g[b][n]·W[n][k]                      reads W once
+//   wgrad    dW[n][k] = Σ_b g[b][n]·x[b][k],  db[n] = Σ_b g[b][n] writes dW once
+//
+// with g = dy·act'(y) formed on the fly from the layer's own output (no mask
+// pass).  hipBLASLt ran fc1 (25088 → 4096, 205 MB of bf16 weights) at 75 / 50
+// / 66 us for these three (profiles/r5/train/vgg_b2_kernels.md); each is one
+// pass over 205 MB, 26 us at 8 TB/s.  The MFMA is of no use at 2 rows: the
+// math is 2 FLOP per weight byte, so these are VALU dot products fed by 16-B
+// loads, sized for bytes in flight.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define VGPU_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr int kThreads = 256;
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+
+__device__ __forceinline__ void unpack8(const u32x4 v, float (&f)[8]) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  typedef __attribute__((ext_vector_type(2))) float f2;
+  typedef __attribute__((ext_vector_type(2))) __bf16 b2;
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{a, b}, b2));
+}
+__device__ __forceinline__ float act_f(int act, float v) {
+  return act == 1 ? fmaxf(v, 0.0f) : act == 2 ? fminf(fmaxf(v, 0.0f), 6.0f) : v;
+}
+// d act / d z from the stored output y (relu: y > 0; relu6: 0 < y < 6)
+__device__ __forceinline__ float act_grad(int act, float y) {
+  return act == 1 ? (y > 0.0f ? 1.0f : 0.0f) : act == 2 ? ((y > 0.0f && y < 6.0f) ? 1.0f : 0.0f) : 1.0f;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---- forward: one wave per R = 2 output rows, the K loop unrolled by U ------------
+constexpr int kR = 2, kU = 4;
+template <int B>
+__global__ void __launch_bounds__(kThreads) skinny_fwd_kernel(const uint16_t* __restrict__ x,
+                                                              const uint16_t* __restrict__ w,
+                                                              const uint16_t* __restrict__ bias,
+                                                              uint16_t* __restrict__ y, int N, int K, int act) {
+  const int lane = threadIdx.x & 63;
+  const int n0 = (blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)) * kR;
+  if (n0 >= N) return;
+  float acc[kR][B];
+#pragma unroll
+  for (int r = 0; r < kR; ++r)
+#pragma unroll
+    for (int b = 0; b < B; ++b) acc[r][b] = 0.0f;
+  const int kv = K >> 3;  // 16-B chunks per row
+  const u32x4* W0 = reinterpret_cast<const u32x4*>(w + (int64_t)n0 * K);
+  const u32x4* X = reinterpret_cast<const u32x4*>(x);
+  for (int c0 = lane; c0 < kv; c0 += 64 * kU) {
+    u32x4 wv[kU][kR], xv[kU][B];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int c = c0 + 64 * u;
+      if (c < kv) {
+#pragma unroll
+        for (int r = 0; r < kR; ++r) wv[u][r] = W0[(int64_t)r * kv + c];
+#pragma unroll
+        for (int b = 0; b < B; ++b) xv[u][b] = X[(int64_t)b * kv + c];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (c0 + 64 * u >= kv) continue;
+      float xf[B][8];
+#pragma unroll
+      for (int b = 0; b < B; ++b) unpack8(xv[u][b], xf[b]);
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        float wf[8];
+        unpack8(wv[u][r], wf);
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[r][b] = fmaf(wf[j], xf[b][j], acc[r][b]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kR; ++r)
+#pragma unroll
+    for (int b = 0; b < B; ++b) acc[r][b] = wave_sum(acc[r][b]);
+  if (lane < kR * B) {  // lane (r, b) stores one output
+    const int r = lane / B, b = lane % B;
+    float v = 0.0f;
+#pragma unroll
+    for (int rr = 0; rr < kR; ++rr)
+#pragma unroll
+      for (int bb = 0; bb < B; ++bb)
+        if (rr == r && bb == b) v = acc[rr][bb];
+    if (bias) v += bf2f(bias[n0 + r]);
+    y[(int64_t)b * N + n0 + r] = f2bf(act_f(act, v));
+  }
+}
+
+// ---- data gradient: blocks own 64 chunks of 8 columns × an N range -------------
+// 4 waves split the block's rows; thread = 8 consecutive k.  g for the block's
+// rows is formed into LDS first.  Partials of the NS row splits go to ws and
+// skinny_dgrad_reduce sums them in order.
+constexpr int kDgRows = 256;  // rows per block (64 per wave)
+template <int B>
+__global__ void __launch_bounds__(kThreads) skinny_dgrad_kernel(const uint16_t* __restrict__ dy,
+                                                                const uint16_t* __restrict__ yout,
+                                                                const uint16_t* __restrict__ w,
+                                                                float* __restrict__ ws, int N, int K, int act) {
+  __shared__ float sg[B][kDgRows];
+  __shared__ float red[3][B][64][9];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int kv = K >> 3;
+  const int c = blockIdx.x * 64 + lane;
+  const int nb = blockIdx.y * kDgRows;
+  for (int i = t; i < B * kDgRows; i += kThreads) {
+    const int b = i / kDgRows, r = i - b * kDgRows, n = nb + r;
+    float g = 0.0f;
+    if (n < N) {
+      g = bf2f(dy[(int64_t)b * N + n]);
+      if (yout) g *= act_grad(act, bf2f(yout[(int64_t)b * N + n]));
+    }
+    sg[b][r] = g;
+  }
+  __syncthreads();
+  float acc[B][8];
+#pragma unroll
+  for (int b = 0; b < B; ++b)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[b][j] = 0.0f;
+  if (c < kv) {
+    const int r0 = wave * (kDgRows / 4);
+    const u32x4* W = reinterpret_cast<const u32x4*>(w) + c;
+    constexpr int RU = 8;
+    for (int r = r0; r < r0 + kDgRows / 4; r += RU) {
+      u32x4 wv[RU];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        const int n = nb + r + u;
+        wv[u] = n < N ? W[(int64_t)n * kv] : u32x4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        float wf[8];
+        unpack8(wv[u], wf);
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+          const float g = sg[b][r + u];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[b][j] = fmaf(g, wf[j], acc[b][j]);
+        }
+      }
+    }
+  }
+  // waves 1-3 hand their partial sums to wave 0 (fixed order)
+  if (wave > 0) {
+#pragma unroll
+    for (int b = 0; b < B; ++b)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[wave - 1][b][lane][j] = acc[b][j];
+  }
+  __syncthreads();
+  if (wave == 0 && c < kv) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int b = 0; b < B; ++b)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[b][j] += red[q][b][lane][j];
+    float* out = ws + (int64_t)blockIdx.y * B * K;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      float4* o = reinterpret_cast<float4*>(out + (int64_t)b * K + c * 8);
+      o[0] = float4{acc[b][0], acc[b][1], acc[b][2], acc[b][3]};
+      o[1] = float4{acc[b][4], acc[b][5], acc[b][6], acc[b][7]};
+    }
+  }
+}
+
+// dx = bf16(Σ_split ws[split]) — one thread per 8 values.
+__global__ void __launch_bounds__(kThreads) skinny_dgrad_reduce_kernel(const float* __restrict__ ws,
+                                                                       uint16_t* __restrict__ dx, int64_t total8,
+                                                                       int splits) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= total8) return;
+  const float4* p = reinterpret_cast<const float4*>(ws) + i * 2;
+  float4 a = p[0], b = p[1];
+  for (int s = 1; s < splits; ++s) {
+    const float4* q = p + (int64_t)s * total8 * 2;
+    const float4 c = q[0], d = q[1];
+    a.x += c.x; a.y += c.y; a.z += c.z; a.w += c.w;
+    b.x += d.x; b.y += d.y; b.z += d.z; b.w += d.w;
+  }
+  reinterpret_cast<u32x4*>(dx)[i] = u32x4{pack2(a.x, a.y), pack2(a.z, a.w), pack2(b.x, b.y), pack2(b.z, b.w)};
+}
+
+// ---- weight gradient: thread = 8 columns of kRows rows; x chunk held in registers
+constexpr int kWgRows = 8;
+template <int B>
+__global__ void __launch_bounds__(kThreads) skinny_wgrad_kernel(const uint16_t* __restrict__ dy,
+                                                                const uint16_t* __restrict__ yout,
+                                                                const uint16_t* __restrict__ x,
+                                                                uint16_t* __restrict__ dw, uint16_t* __restrict__ db,
+                                                                int N, int K, int act) {
+  const int kv = K >> 3;
+  const int c = blockIdx.x * kThreads + threadIdx.x;
+  const int n0 = blockIdx.y * kWgRows;
+  float g[kWgRows][B];
+#pragma unroll
+  for (int r = 0; r < kWgRows; ++r)
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const int n = n0 + r;
+      float v = 0.0f;
+      if (n < N) {
+        v = bf2f(dy[(int64_t)b * N + n]);
+        if (yout) v *= act_grad(act, bf2f(yout[(int64_t)b * N + n]));
+      }
+      g[r][b] = v;
+    }
+  if (db && blockIdx.x == 0 && threadIdx.x < kWgRows && n0 + (int)threadIdx.x < N) {
+    float s = 0.0f;
+#pragma unroll
+    for (int r = 0; r < kWgRows; ++r)
+      if (r == (int)threadIdx.x)
+#pragma unroll
+        for (int b = 0; b < B; ++b) s += g[r][b];
+    db[n0 + threadIdx.x] = f2bf(s);
+  }
+  if (c >= kv) return;
+  float xf[B][8];
+#pragma unroll
+  for (int b = 0; b < B; ++b) unpack8(reinterpret_cast<const u32x4*>(x)[(int64_t)b * kv + c], xf[b]);
+#pragma unroll
+  for (int r = 0; r < kWgRows; ++r) {
+    if (n0 + r >= N) break;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float s = 0.0f;
+#pragma unroll
+      for (int b = 0; b < B; ++b) s = fmaf(g[r][b], xf[b][j], s);
+      o[j] = s;
+    }
+    reinterpret_cast<u32x4*>(dw)[(int64_t)(n0 + r) * kv + c] =
+        u32x4{pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7])};
+  }
+}
+
+inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+#define VGPU_SKINNY_SWITCH(B, KERNEL, GRID, ...)                                                          \
+  switch (B) {                                                                                            \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(kThreads), 0, s, __VA_ARGS__); break;                \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(kThreads), 0, s, __VA_ARGS__); break;                \
+    case 3: hipLaunchKernelGGL(KERNEL<3>, GRID, dim3(kThreads), 0, s, __VA_ARGS__); break;                \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(kThreads), 0, s, __VA_ARGS__); break;                \
+    case 8: hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(kThreads), 0, s, __VA_ARGS__); break;                \
+    default: return -1;                                                                                   \
+  }
+
+VGPU_API int vgpu_skinny_supported(int B, int N, int K) {
+  return (B == 1 || B == 2 || B == 3 || B == 4 || B == 8) && N % kR == 0 && K % 8 == 0 && N > 0 && K > 0;
+}
+
+// y [B][N] = act(x [B][K] · W[N][K]ᵀ + bias) (bf16; bias bf16 or null; act 0/1/2).
+VGPU_API int vgpu_skinny_fwd(const void* x, const void* w, const void* bias, void* y, int B, int N, int K, int act,
+                             hipStream_t s) {
+  if (!vgpu_skinny_supported(B, N, K) || !al16(x) || !al16(w) || act < 0 || act > 2) return -1;
+  const dim3 grid((N / kR + 3) / 4);
+  VGPU_SKINNY_SWITCH(B, skinny_fwd_kernel, grid, (const uint16_t*)x, (const uint16_t*)w, (const uint16_t*)bias,
+                     (uint16_t*)y, N, K, act)
+  return (int)hipGetLastError();
+}
+
+// Workspace (bytes) of vgpu_skinny_dgrad: fp32 partials of the row splits.
+VGPU_API int64_t vgpu_skinny_dgrad_workspace(int B, int N, int K) {
+  return (int64_t)((N + kDgRows - 1) / kDgRows) * B * K * 4;
+}
+
+// dx [B][K] = (dy·act'(y)) [B][N] · W [N][K]; yout = the layer's output (null: no activation).
+VGPU_API int vgpu_skinny_dgrad(const void* dy, const void* yout, const void* w, void* dx, void* ws, int64_t ws_bytes,
+                               int B, int N, int K, int act, hipStream_t s) {
+  if (!vgpu_skinny_supported(B, N, K) || !al16(w) || !al16(dx) || !al16(ws)) return -1;
+  if (ws_bytes < vgpu_skinny_dgrad_workspace(B, N, K)) return -1;
+  const int splits = (N + kDgRows - 1) / kDgRows;
+  const dim3 grid((K / 8 + 63) / 64, splits);
+  VGPU_SKINNY_SWITCH(B, skinny_dgrad_kernel, grid, (const uint16_t*)dy, (const uint16_t*)yout, (const uint16_t*)w,
+                     (float*)ws, N, K, act)
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const int64_t total8 = (int64_t)B * K / 8;
+  hipLaunchKernelGGL(skinny_dgrad_reduce_kernel, dim3((unsigned)((total8 + kThreads - 1) / kThreads)), dim3(kThreads),
+                     0, s, (const float*)ws, (uint16_t*)dx, total8, splits);
+  return (int)hipGetLastError();
+}
+
+// dW [N][K] = gᵀ · x, db [N] = Σ_b g (db may be null), g = dy·act'(y).
+VGPU_API int vgpu_skinny_wgrad(const void* dy, const void* yout, const void* x, void* dw, void* db, int B, int N,
+                               int K, int act, hipStream_t s) {
+  if (!vgpu_skinny_supported(B, N, K) || !al16(x) || !al16(dw)) return -1;
+  const dim3 grid((K / 8 + kThreads - 1) / kThreads, (N + kWgRows - 1) / kWgRows);
+  VGPU_SKINNY_SWITCH(B, skinny_wgrad_kernel, grid, (const uint16_t*)dy, (const uint16_t*)yout, (const uint16_t*)x,
+                     (uint16_t*)dw, (uint16_t*)db, N, K, act)
+  return (int)hipGetLastError();
+}

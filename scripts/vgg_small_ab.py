@@ -17,31 +17,12 @@ import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vgpu.ops import conv as C  # noqa: E402
+from vgpu.utils.timing import graph_time_us  # noqa: E402
 
 CL = torch.channels_last
 
 
-def graph_us(fn, iters=20, reps=5):
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        for _ in range(3):
-            fn()
-    torch.cuda.current_stream().wait_stream(s)
-    torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        for _ in range(iters):
-            fn()
-    best = []
-    for _ in range(reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        g.replay()
-        e1.record()
-        torch.cuda.synchronize()
-        best.append(e0.elapsed_time(e1) * 1e3 / iters)
-    return round(sorted(best)[len(best) // 2], 2)
+graph_us = graph_time_us
 
 
 def wgrad_gemm(dy, x, ks=3, pad=1):

@@ -80,14 +80,16 @@ def test_vgg16_native_training_step_matches_fp32(gpu_build):
     mt = copy.deepcopy(m)
     x = _x((2, 3, 64, 64), 3)
     tgt = torch.tensor([1, 7], device="cuda")
-    calls = []
-    orig = C._ConvBiasReLUTrainFn.apply
+    calls, pcalls = [], []
+    orig, porig = C._ConvBiasReLUTrainFn.apply, C._ConvBiasReLUPoolTrainFn.apply
     C._ConvBiasReLUTrainFn.apply = lambda *a: (calls.append(1), orig(*a))[1]
+    C._ConvBiasReLUPoolTrainFn.apply = lambda *a: (pcalls.append(1), porig(*a))[1]
     try:
         out = m(x)
     finally:
-        C._ConvBiasReLUTrainFn.apply = orig
-    assert len(calls) == 13, "every conv should run natively (the first on channel-padded input)"
+        C._ConvBiasReLUTrainFn.apply, C._ConvBiasReLUPoolTrainFn.apply = orig, porig
+    # every conv natively (the first on channel-padded input), the five before a pool fused with it
+    assert len(calls) == 8 and len(pcalls) == 5, (len(calls), len(pcalls))
     out_t = _torch_path(lambda: mt(x))
     out32 = m32(x.float())
     print("vgg out rel: native/fp32", _rel(out, out32), "torch-bf16/fp32", _rel(out_t, out32))
@@ -231,3 +233,71 @@ def test_conv_relu6_epilogue_matches_fp32(gpu_build):
     ref = C.conv2d_ref(x, w, b, act="relu6")
     assert float(got.max()) <= 6.0
     torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("case", [(2, 4096, 25088, "relu"), (2, 1000, 4096, "none"), (3, 64, 520, "relu"),
+                                  (8, 130, 1032, "relu6"), (1, 256, 64, "none")])
+def test_skinny_linear_matches_fp32(gpu_build, case):
+    """vgpu.ops.linear (native/kernels/skinny.hip): forward with bias +
+    activation, dx, dW and db against fp32 PyTorch of the same bf16 values."""
+    from vgpu.ops.linear import _SkinnyLinearFn, _ACTS
+    b, n, k, act = case
+    g = torch.Generator().manual_seed(n + k)
+    x = (torch.randn(b, k, generator=g)).to(torch.bfloat16).cuda().requires_grad_()
+    w = (torch.randn(n, k, generator=g) * k ** -0.5).to(torch.bfloat16).cuda().requires_grad_()
+    bias = (torch.randn(n, generator=g) * 0.1).to(torch.bfloat16).cuda().requires_grad_()
+    y = _SkinnyLinearFn.apply(x, w, bias, _ACTS[act])
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, bias))
+    yr = torch.nn.functional.linear(xr, wr, br)
+    yr = torch.relu(yr) if act == "relu" else (yr.clamp(0, 6) if act == "relu6" else yr)
+    torch.testing.assert_close(y.float(), yr, atol=2e-2, rtol=2e-2)
+    dy = torch.randn(b, n, generator=g).to(torch.bfloat16).cuda()
+    y.backward(dy)
+    # the reference's mask comes from the kernel's own (bf16) output, as the
+    # native backward does
+    mask = (y.detach().float() > 0).float() if act == "relu" else (
+        ((y.detach().float() > 0) & (y.detach().float() < 6)).float() if act == "relu6" else 1.0)
+    gr = dy.float() * mask
+    torch.testing.assert_close(x.grad.float(), gr @ wr.detach(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(w.grad.float(), gr.t() @ xr.detach(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(bias.grad.float(), gr.sum(0), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("case", [(2, 64, 64, 16, 16), (2, 128, 256, 14, 14), (1, 512, 512, 7, 9)])
+def test_conv_bias_relu_pool_train_matches_fp32(gpu_build, case):
+    """conv + bias + ReLU + 2x2 max pool with the pool backward fused into the
+    ReLU / bias-gradient pass (vgpu_pool_relu_bias_grad_nhwc; odd sizes drop
+    the last row / column like max_pool2d) against fp32 PyTorch."""
+    from vgpu.ops import conv as C
+    n, c, cout, h, w = case
+    conv = torch.nn.Conv2d(c, cout, 3, padding=1).cuda().to(torch.bfloat16).to(memory_format=CL)
+    pool = torch.nn.MaxPool2d(2, 2)
+    x = _x((n, c, h, w), 5).requires_grad_()
+    calls = []
+    orig = C._ConvBiasReLUPoolTrainFn.apply
+    C._ConvBiasReLUPoolTrainFn.apply = lambda *a: (calls.append(1), orig(*a))[1]
+    try:
+        y = C.conv_bias_relu_pool_train(x, conv, pool)
+    finally:
+        C._ConvBiasReLUPoolTrainFn.apply = orig
+    assert calls, "the fused path should run"
+    # the unfused native pair (conv_bias_relu_train, maxpool_train): same slabs,
+    # same sums -- bit-identical values and gradients
+    x2 = x.detach().clone().requires_grad_()
+    conv2 = copy.deepcopy(conv)
+    y2 = C.maxpool_train(C.conv_bias_relu_train(x2, conv2).contiguous(memory_format=CL), pool)
+    xr = x.detach().float().requires_grad_()
+    wr, br = conv.weight.detach().float().requires_grad_(), conv.bias.detach().float().requires_grad_()
+    yr = torch.nn.functional.max_pool2d(torch.relu(torch.nn.functional.conv2d(xr, wr, br, padding=1)), 2, 2)
+    assert _rel(y, yr) < 2e-2
+    dy = _x(tuple(y.shape), 6)
+    y.backward(dy)
+    y2.backward(dy)
+    yr.backward(dy.float())
+    assert torch.equal(y, y2) and torch.equal(x.grad, x2.grad)
+    assert torch.equal(conv.weight.grad, conv2.weight.grad) and torch.equal(conv.bias.grad, conv2.bias.grad)
+    # against fp32: a max-pool window decided differently by bf16 rounding
+    # reroutes a gradient, hence the looser bounds (the exact check is above)
+    assert _rel(x.grad, xr.grad) < 6e-2
+    assert _rel(conv.weight.grad, wr.grad) < 6e-2
+    assert _rel(conv.bias.grad, br.grad) < 6e-2

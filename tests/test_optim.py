@@ -10,7 +10,11 @@ from vgpu.ops.optim import SGD
 def _params(device, dtype, seed=0):
     g = torch.Generator().manual_seed(seed)
     shapes = [(64, 3, 3, 3), (64,), (4096, 25088 // 49), (1000,), (7, 5)]  # (7, 5): odd size, fallback
-    return [torch.nn.Parameter((torch.randn(s, generator=g) * 0.1).to(device=device, dtype=dtype)) for s in shapes]
+    ps = [torch.nn.Parameter((torch.randn(s, generator=g) * 0.1).to(device=device, dtype=dtype)) for s in shapes]
+    # a channels_last conv weight (the models' layout): dense, not contiguous
+    ps.append(torch.nn.Parameter((torch.randn(128, 64, 3, 3, generator=g) * 0.1).to(device=device, dtype=dtype)
+                                 .contiguous(memory_format=torch.channels_last)))
+    return ps
 
 
 def _run(opt_cls, params, steps, **kw):
@@ -18,7 +22,7 @@ def _run(opt_cls, params, steps, **kw):
     g = torch.Generator().manual_seed(1)
     for _ in range(steps):
         for p in params:
-            p.grad = (torch.randn(p.shape, generator=g) * 0.01).to(device=p.device, dtype=p.dtype)
+            p.grad = torch.empty_like(p).copy_((torch.randn(p.shape, generator=g) * 0.01))
         opt.step()
     return [p.detach().float().cpu() for p in params]
 
@@ -46,7 +50,7 @@ def test_sgd_native_bf16_matches_torch_fused(gpu_build, kw):
         a = _run(SGD, _params("cuda", torch.bfloat16), 4, **kw)
     finally:
         O.sgd_bf16_ = orig
-    assert calls and sum(calls) == 4 * 4, calls  # 4 eligible tensors per step, natively
+    assert calls and sum(calls) == 4 * 5, calls  # 5 eligible tensors per step, natively
     b = _run(torch.optim.SGD, _params("cuda", torch.bfloat16), 4, fused=True, **kw)
     for x, y in zip(a, b):
         # fp32 math, bf16 storage on both sides; fma vs mul+add rounding moves a

@@ -38,13 +38,21 @@ class VGG16(nn.Module):
             nn.Linear(4096, num_classes))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if self.training and torch.is_grad_enabled() and x.is_cuda:
+        train = self.training and torch.is_grad_enabled() and x.is_cuda
+        if train:
             x = self._train_features(x)
         else:
             x = self.features(x)
         if x.shape[-2:] != (7, 7):
             x = self.pool(x)
-        return self.classifier(torch.flatten(x, 1))
+        x = torch.flatten(x, 1)
+        from vgpu.ops.conv import native_train_enabled
+        if train and native_train_enabled():
+            # batch ≤ 8: each FC layer + ReLU on the skinny kernels (vgpu.ops.linear)
+            from vgpu.ops.linear import linear_act
+            fc1, _, fc2, _, fc3 = self.classifier
+            return linear_act(linear_act(linear_act(x.contiguous(), fc1, "relu"), fc2, "relu"), fc3)
+        return self.classifier(x)
 
     def _train_features(self, x: torch.Tensor) -> torch.Tensor:
         """Training forward on the native kernels: each conv +
@@ -54,7 +62,8 @@ class VGG16(nn.Module):
         backward, and every stride-1 data-gradient filter is rebuilt by one
         batched launch per step.  Other shapes (the 3-channel first conv) run
         through the modules."""
-        from vgpu.ops.conv import DgradFilters, conv_bias_relu_train, maxpool_train, native_train_enabled
+        from vgpu.ops.conv import (DgradFilters, conv_bias_relu_pool_train, conv_bias_relu_train, maxpool_train,
+                                   native_train_enabled)
         if native_train_enabled():
             if getattr(self, "_dgrad", None) is None:
                 self._dgrad = DgradFilters([m for m in self.features if isinstance(m, nn.Conv2d)])
@@ -65,6 +74,11 @@ class VGG16(nn.Module):
         while i < len(mods):
             m = mods[i]
             if isinstance(m, nn.Conv2d) and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU):
+                if i + 2 < len(mods) and isinstance(mods[i + 2], nn.MaxPool2d):
+                    # conv + ReLU + pool: the pool backward fused into the ReLU / bias gradient
+                    x = conv_bias_relu_pool_train(x, m, mods[i + 2])
+                    i += 3
+                    continue
                 x = conv_bias_relu_train(x, m).contiguous(memory_format=torch.channels_last)
                 i += 2
                 continue

@@ -563,6 +563,73 @@ def relu_bias_grad(dy: torch.Tensor, y: torch.Tensor,
     return g, db
 
 
+class _ConvBiasReLUPoolTrainFn(torch.autograd.Function):
+    """maxpool_k×k/stride k(relu(conv(x, w) + b)): the conv with bias + ReLU
+    in its epilogue, then the pool with its one-byte argmax.  Backward: the
+    pool's gradient gather, the ReLU mask and the bias gradient in ONE pass
+    (vgpu_pool_relu_bias_grad_nhwc), then dx / dw as _ConvTrainFn.  VGG-16's
+    five conv + ReLU + pool blocks."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride: int, padding: int, k: int):
+        y = conv2d(x, w, b, stride=stride, padding=padding, act="relu")
+        n, c, h, wd = y.shape
+        oh, ow = h // k, wd // k
+        p = torch.empty((n, c, oh, ow), dtype=y.dtype, device=y.device, memory_format=_CL)
+        idx = torch.empty((n, oh, ow, c), dtype=torch.uint8, device=y.device)
+        rc = load_kernels().vgpu_maxpool_fwd_idx_nhwc(_ptr(y), _ptr(p), _ptr(idx), n, h, wd, c, k, k, 0, _stream())
+        if rc != 0:
+            raise RuntimeError(f"vgpu_maxpool_fwd_idx_nhwc: error {rc}")
+        ctx.save_for_backward(x, w, y, idx)
+        ctx.mark_non_differentiable(idx)
+        ctx.stride, ctx.padding, ctx.k, ctx.bias_dtype = stride, padding, k, b.dtype
+        return p
+
+    @staticmethod
+    def backward(ctx, dp):
+        x, w, y, idx = ctx.saved_tensors
+        dp = dp.contiguous(memory_format=_CL)
+        n, c, h, wd = y.shape
+        lib = load_kernels()
+        g = torch.empty_like(y, memory_format=_CL)
+        db = torch.empty(c, dtype=ctx.bias_dtype, device=y.device)
+        ws = torch.empty(max(lib.vgpu_relu_bias_grad_workspace(n * h * wd, c) // 4, 1), dtype=torch.float32,
+                         device=y.device)
+        rc = lib.vgpu_pool_relu_bias_grad_nhwc(_ptr(dp), _ptr(idx), _ptr(y), _ptr(g), _ptr(db), _ptr(ws), n, h, wd,
+                                               c, ctx.k, int(ctx.bias_dtype == torch.bfloat16), _stream())
+        if rc != 0:
+            raise RuntimeError(f"vgpu_pool_relu_bias_grad_nhwc: error {rc}")
+        dx, dw = conv_backward(g, x, w, ctx.stride, ctx.padding, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        return dx, dw, db if ctx.needs_input_grad[2] else None, None, None, None
+
+
+def conv_bias_relu_pool_train(x: torch.Tensor, conv: torch.nn.Conv2d, pool: torch.nn.MaxPool2d) -> torch.Tensor:
+    """pool(relu(conv(x))) with the module semantics; the fused native path for
+    a k×k / stride-k unpadded pool after a native-eligible conv, else the
+    unfused ops."""
+    k, s_, p_ = pool.kernel_size, pool.stride, pool.padding
+    k = k if isinstance(k, int) else (k[0] if k[0] == k[1] else None)
+    s_ = s_ if isinstance(s_, int) else (s_[0] if s_[0] == s_[1] else None)
+    p_ = p_ if isinstance(p_, int) else (p_[0] if p_[0] == p_[1] else -1)
+    w = conv.weight
+    ok = (k is not None and s_ == k and p_ == 0 and not pool.ceil_mode and pool.dilation in (1, (1, 1))
+          and not pool.return_indices and _conv_bias_relu_ok(x, conv)
+          and conv.out_channels % 8 == 0 and conv.out_channels <= 2048 and w.dtype == torch.bfloat16)
+    if not ok:
+        return maxpool_train(conv_bias_relu_train(x, conv).contiguous(memory_format=_CL), pool)
+    return _ConvBiasReLUPoolTrainFn.apply(x, w, conv.bias, conv.stride[0], conv.padding[0], k)
+
+
+def _conv_bias_relu_ok(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
+    w = conv.weight
+    return (_TRAIN_NATIVE and conv.bias is not None and x.is_cuda and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and x.dim() == 4 and x.is_contiguous(memory_format=_CL)
+            and w.is_contiguous(memory_format=_CL) and conv.groups == 1 and conv.dilation == (1, 1)
+            and conv.kernel_size[0] == conv.kernel_size[1] and conv.stride[0] == conv.stride[1]
+            and conv.padding[0] == conv.padding[1] and isinstance(conv.padding[0], int)
+            and conv.kernel_size[0] in (1, 3) and supported(conv.in_channels, conv.out_channels, conv.kernel_size[0]))
+
+
 def conv_bias_relu_train(x: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor:
     """relu(conv(x)) with the module's semantics (bias included); bf16
     channels_last CUDA tensors of supported shapes run natively, anything else
@@ -581,13 +648,7 @@ def conv_bias_relu_train(x: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor
         xp = F.pad(x, (0, 0, 0, 0, 0, 64 - c)).contiguous(memory_format=_CL)
         wp = F.pad(w, (0, 0, 0, 0, 0, 64 - c)).contiguous(memory_format=_CL)
         return _ConvBiasReLUTrainFn.apply(xp, wp, conv.bias, 1, 1)
-    ok = (_TRAIN_NATIVE and conv.bias is not None and x.is_cuda and x.dtype == torch.bfloat16
-          and w.dtype == torch.bfloat16 and x.dim() == 4 and x.is_contiguous(memory_format=_CL)
-          and w.is_contiguous(memory_format=_CL) and conv.groups == 1 and conv.dilation == (1, 1)
-          and conv.kernel_size[0] == conv.kernel_size[1] and conv.stride[0] == conv.stride[1]
-          and conv.padding[0] == conv.padding[1] and isinstance(conv.padding[0], int)
-          and conv.kernel_size[0] in (1, 3) and supported(conv.in_channels, conv.out_channels, conv.kernel_size[0]))
-    if not ok:
+    if not _conv_bias_relu_ok(x, conv):
         return F.relu(conv(x))
     return _ConvBiasReLUTrainFn.apply(x, w, conv.bias, conv.stride[0], conv.padding[0])
 

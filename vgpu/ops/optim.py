@@ -33,10 +33,18 @@ def _lib():
     return lib
 
 
-def _native_ok(p: torch.Tensor) -> bool:
+def _dense(t: torch.Tensor) -> bool:
+    return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
+
+
+def _native_ok(p: torch.Tensor, buf: torch.Tensor | None) -> bool:
+    """The update is elementwise over storage: p, its gradient and its momentum
+    buffer must be dense with identical strides (channels_last conv weights
+    included), bf16, 16-B aligned, numel % 8 == 0."""
     g = p.grad
     return (p.is_cuda and p.dtype == torch.bfloat16 and g is not None and not g.is_sparse
-            and g.dtype == torch.bfloat16 and p.is_contiguous() and g.is_contiguous()
+            and g.dtype == torch.bfloat16 and _dense(p) and g.stride() == p.stride()
+            and (buf is None or buf.stride() == p.stride())
             and p.numel() % 8 == 0 and p.data_ptr() % 16 == 0 and g.data_ptr() % 16 == 0)
 
 
@@ -84,8 +92,9 @@ class SGD(torch.optim.Optimizer):
             for p in group["params"]:
                 if p.grad is None:
                     continue
-                if native and _native_ok(p):
-                    (cont_p if "momentum_buffer" in self.state[p] else first_p).append(p)
+                buf = self.state[p].get("momentum_buffer")
+                if native and _native_ok(p, buf):
+                    (first_p if buf is None else cont_p).append(p)
                 else:
                     rest.append(p)
             for ps, first in ((first_p, True), (cont_p, False)):
@@ -93,7 +102,7 @@ class SGD(torch.optim.Optimizer):
                     continue
                 if first:
                     for p in ps:
-                        self.state[p]["momentum_buffer"] = torch.empty_like(p, memory_format=torch.contiguous_format)
+                        self.state[p]["momentum_buffer"] = torch.empty_like(p, memory_format=torch.preserve_format)
                 bufs = [self.state[p]["momentum_buffer"] for p in ps]
                 sgd_bf16_(ps, [p.grad for p in ps], bufs, first=first, **hp)
             if rest:

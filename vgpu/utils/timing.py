@@ -29,3 +29,29 @@ def interleaved_us(fns: Sequence[Callable[[], object]], rounds: int = 3, iters: 
         for i, fn in enumerate(fns):
             tot[i] += cuda_time_us(fn, iters) / rounds
     return tot
+
+
+def graph_time_us(fn: Callable[[], object], iters: int = 20, reps: int = 5) -> float:
+    """Median µs per call of fn replayed from a hipGraph of `iters` calls
+    (host launch overhead excluded: the training steps are graph replays)."""
+    import torch
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    times = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1) * 1e3 / iters)
+    return round(sorted(times)[len(times) // 2], 2)
