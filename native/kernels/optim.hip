@@ -76,9 +76,11 @@ __global__ void __launch_bounds__(kThreads) sgd_bf16_kernel(const SgdSegs s, flo
   for (int u = 0; u < kIters; ++u) {
     const int i = u * kThreads + threadIdx.x;
     if (i < nv) {
-      pv[u] = P[i];
-      gv[u] = G[i];
-      if (!FIRST) mv[u] = M[i];
+      // every byte is touched once: nontemporal, so the stream does not evict
+      // what the next step's first kernels would find in L2 / MALL
+      pv[u] = __builtin_nontemporal_load(&P[i]);
+      gv[u] = __builtin_nontemporal_load(&G[i]);
+      if (!FIRST) mv[u] = __builtin_nontemporal_load(&M[i]);
     }
   }
 #pragma unroll
@@ -91,8 +93,8 @@ __global__ void __launch_bounds__(kThreads) sgd_bf16_kernel(const SgdSegs s, flo
     if (!FIRST) { mw[0] = mv[u].x; mw[1] = mv[u].y; mw[2] = mv[u].z; mw[3] = mv[u].w; }
 #pragma unroll
     for (int k = 0; k < 4; ++k) step2<FIRST, NESTEROV>(pw[k], gw[k], mw[k], lr, mom, damp1, wd, po[k], mo[k]);
-    P[i] = u32x4{po[0], po[1], po[2], po[3]};
-    M[i] = u32x4{mo[0], mo[1], mo[2], mo[3]};
+    __builtin_nontemporal_store(u32x4{po[0], po[1], po[2], po[3]}, &P[i]);
+    __builtin_nontemporal_store(u32x4{mo[0], mo[1], mo[2], mo[3]}, &M[i]);
   }
 }
 

@@ -52,7 +52,10 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 // ---- forward: one wave per R = 2 output rows, the K loop unrolled by U ------------
-constexpr int kR = 2, kU = 4;
+// kU = 8: 256 B of weight per lane in flight.  In a training step fc1's 205 MB
+// no longer sits in the 256 MB MALL, and at kU = 4 the pass ran at ~3 TB/s
+// (68 us; profiles/r5/train/vgg_b2_step_kernels.md).
+constexpr int kR = 2, kU = 8;
 template <int B>
 __global__ void __launch_bounds__(kThreads) skinny_fwd_kernel(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
@@ -260,8 +263,10 @@ __global__ void __launch_bounds__(kThreads) skinny_wgrad_kernel(const uint16_t* 
       for (int b = 0; b < B; ++b) s = fmaf(g[r][b], xf[b][j], s);
       o[j] = s;
     }
-    reinterpret_cast<u32x4*>(dw)[(int64_t)(n0 + r) * kv + c] =
-        u32x4{pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7])};
+    // nontemporal: dW (205 MB for fc1) would otherwise push W out of the MALL
+    // between this layer's data gradient and the optimizer
+    __builtin_nontemporal_store(u32x4{pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7])},
+                                &reinterpret_cast<u32x4*>(dw)[(int64_t)(n0 + r) * kv + c]);
   }
 }
 

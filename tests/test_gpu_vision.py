@@ -202,6 +202,13 @@ def test_relu_bias_grad_matches_torch(gpu_build, shape):
     gt = torch.ops.aten.threshold_backward(dy, y, 0)
     assert torch.equal(g, gt)
     torch.testing.assert_close(db, gt.float().sum(dim=(0, 2, 3)), atol=1e-2, rtol=1e-4)
+    # the last-block reduction hands its ticket slot back: repeated launches
+    # (and the bf16 output) give the same, deterministic sums
+    for _ in range(3):
+        g2, db2 = relu_bias_grad(dy, y)
+        assert torch.equal(g2, g) and torch.equal(db2, db)
+    _, db16 = relu_bias_grad(dy, y, torch.bfloat16)
+    assert torch.equal(db16, db.to(torch.bfloat16))
 
 
 def test_deeplab_fused_inference_matches_unfused(gpu_build):

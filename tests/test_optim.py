@@ -58,3 +58,23 @@ def test_sgd_native_bf16_matches_torch_fused(gpu_build, kw):
         if x.numel() >= 4096:  # the (7, 5) fallback tensor runs PyTorch's foreach SGD here
             assert (x != y).float().mean().item() < 1e-3
         torch.testing.assert_close(x, y, atol=1e-3, rtol=1.6e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("rows,c", [(2, 1000), (50, 1000), (7, 2), (3, 4097)])
+def test_cross_entropy_matches_torch(gpu_build, dtype, rows, c):
+    """vgpu.ops.loss.cross_entropy (native/kernels/loss.hip): the mean loss and
+    dlogits against F.cross_entropy on the fp32 logits."""
+    from vgpu.ops.loss import cross_entropy
+    g = torch.Generator().manual_seed(rows * c)
+    x = (torch.randn(rows, c, generator=g) * 3).to(dtype).cuda().requires_grad_()
+    t = torch.randint(0, c, (rows,), generator=g).cuda()
+    loss = cross_entropy(x, t)
+    (loss * 2.0).backward()
+    xr = x.detach().float().requires_grad_()
+    lr = torch.nn.functional.cross_entropy(xr, t)
+    (lr * 2.0).backward()
+    torch.testing.assert_close(loss, lr, atol=1e-4, rtol=1e-4)
+    tol = dict(atol=2e-3, rtol=2e-2) if dtype == torch.bfloat16 else dict(atol=1e-6, rtol=1e-4)
+    torch.testing.assert_close(x.grad.float(), xr.grad, **tol)

@@ -62,12 +62,18 @@ def build(args):
             target = torch.randint(0, ncls, (w.batch, *w.shape[1:]), device=dev)
         else:
             target = torch.randint(0, ncls, (w.batch,), device=dev)
-        lossf = torch.nn.CrossEntropyLoss()
+        torch_loss = torch.nn.CrossEntropyLoss()
+        from vgpu.ops.loss import cross_entropy
+
+        def lossf(out, tgt):
+            # classification logits: one native pass for the loss and its gradient
+            # (vgpu.ops.loss); DeepLab's per-pixel loss stays on PyTorch
+            return cross_entropy(out, tgt) if out.dim() == 2 and not fp32 else torch_loss(out.float(), tgt)
 
         def step():
             opt.zero_grad(set_to_none=True)
             out = model(x)
-            loss = lossf(out.float(), target)
+            loss = lossf(out, target)
             loss.backward()
             opt.step()
             return loss
@@ -77,7 +83,7 @@ def build(args):
             # are allocated inside the graph's pool on capture and rewritten in
             # place on every replay (PyTorch "whole network capture").
             out = model(x)
-            loss = lossf(out.float(), target)
+            loss = lossf(out, target)
             loss.backward()
             opt.step()
     else:
