@@ -227,11 +227,50 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(const WgradArgs a) {
 // through LDS — deterministic for a given split count.  L grows with the split
 // count (≈ 4 splits per lane): with 16 lanes at 2-8 splits most threads idled
 // and the pass ran at 9.6 us for 19 MB (VGG-16 b=2, profiles/r5/train).
+// Optional second job of the reduce launch: a bias gradient db[c] = Σ_slab
+// part[slab][c] (the per-slab partials of vgpu_relu_bias_grad_partial_nhwc),
+// 16 channels per block, 16 threads per channel over the slab residues,
+// merged in a fixed order.  Folding it in saves the bias-gradient launch of
+// every conv + bias + ReLU layer (VGG-16: 13 per step at ~4.7 us).
+struct DbJob {
+  const float* part;
+  void* db;
+  int c, slabs, bf16;
+};
+
+__device__ void db_reduce_block(const DbJob& j, int blk) {
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x % 16, q = threadIdx.x / 16, ch = blk * 16 + cl;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (ch < j.c) {
+    int k = q;
+    for (; k + 48 < j.slabs; k += 64) {
+      a0 += j.part[(int64_t)k * j.c + ch];
+      a1 += j.part[(int64_t)(k + 16) * j.c + ch];
+      a2 += j.part[(int64_t)(k + 32) * j.c + ch];
+      a3 += j.part[(int64_t)(k + 48) * j.c + ch];
+    }
+    for (; k < j.slabs; k += 16) a0 += j.part[(int64_t)k * j.c + ch];
+  }
+  red[q][cl] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (q == 0 && ch < j.c) {
+    float a = 0.f;
+    for (int i = 0; i < 16; ++i) a += red[i][cl];
+    if (j.bf16) static_cast<uint16_t*>(j.db)[ch] = f2bf(a);
+    else static_cast<float*>(j.db)[ch] = a;
+  }
+}
+
 template <int L>
 __global__ void __launch_bounds__(kThreads) wgrad_reduce_kernel(const float* __restrict__ ws,
                                                                 uint16_t* __restrict__ dw,
                                                                 int64_t n4, int64_t stride4,
-                                                                int splits) {
+                                                                int splits, const DbJob job, int dw_blocks) {
+  if ((int)blockIdx.x >= dw_blocks) {  // block-uniform: the bias-gradient job
+    db_reduce_block(job, blockIdx.x - dw_blocks);
+    return;
+  }
   __shared__ f32x4_t part[L][kThreads / L];
   const int e = threadIdx.x % (kThreads / L), j = threadIdx.x / (kThreads / L);
   const int64_t i = blockIdx.x * (int64_t)(kThreads / L) + e;
@@ -265,10 +304,13 @@ __global__ void __launch_bounds__(kThreads) wgrad_reduce_kernel(const float* __r
 }
 
 template <int L>
-hipError_t launch_wgrad_reduce(const float* ws, uint16_t* dw, int64_t n4, int splits, hipStream_t s) {
+hipError_t launch_wgrad_reduce(const float* ws, uint16_t* dw, int64_t n4, int splits, const DbJob& job,
+                               hipStream_t s) {
   const int64_t per = kThreads / L;
-  hipLaunchKernelGGL((wgrad_reduce_kernel<L>), dim3((unsigned)((n4 + per - 1) / per)), dim3(kThreads), 0, s, ws, dw,
-                     n4, n4, splits);
+  const int dw_blocks = n4 > 0 ? (int)((n4 + per - 1) / per) : 0;
+  const int db_blocks = job.part ? (job.c + 15) / 16 : 0;
+  hipLaunchKernelGGL((wgrad_reduce_kernel<L>), dim3((unsigned)(dw_blocks + db_blocks)), dim3(kThreads), 0, s, ws,
+                     dw, n4, n4, splits, job, dw_blocks);
   return hipGetLastError();
 }
 
@@ -494,9 +536,37 @@ VGPU_API int64_t vgpu_conv_wgrad_workspace(int N, int H, int W, int C, int Cout,
 // dy [N][OH][OW][Cout] and x [N][H][W][C] bf16 NHWC.  `ws` must hold
 // vgpu_conv_wgrad_workspace(...) bytes.  Returns 0, a hipError_t, or -1 for an
 // unsupported shape (checked before any launch).
+namespace {
+int wgrad_impl(const void* dy, const void* x, void* dw, void* ws, int64_t ws_bytes, int N, int H, int W, int C,
+               int Cout, int KS, int stride, int pad, const DbJob& job, hipStream_t s);
+}  // namespace
+
 VGPU_API int vgpu_conv_wgrad_nhwc(const void* dy, const void* x, void* dw, void* ws, int64_t ws_bytes,
                                   int N, int H, int W, int C, int Cout, int KS, int stride, int pad,
                                   hipStream_t s) {
+  return wgrad_impl(dy, x, dw, ws, ws_bytes, N, H, W, C, Cout, KS, stride, pad, DbJob{}, s);
+}
+
+// The same, and db[c] (fp32, or bf16 when db_bf16) = Σ_slab dbpart[slab][c]
+// in the reduce launch (a launch of its own when the weight gradient needs no
+// reduce).  dbpart: vgpu_relu_bias_grad_partial_nhwc's partials.
+VGPU_API int vgpu_conv_wgrad_db_nhwc(const void* dy, const void* x, void* dw, void* ws, int64_t ws_bytes, int N,
+                                     int H, int W, int C, int Cout, int KS, int stride, int pad, const float* dbpart,
+                                     int slabs, int dbc, void* db, int db_bf16, hipStream_t s) {
+  if (!dbpart || !db || slabs < 1 || dbc < 1) return -1;
+  return wgrad_impl(dy, x, dw, ws, ws_bytes, N, H, W, C, Cout, KS, stride, pad,
+                    DbJob{dbpart, db, dbc, slabs, db_bf16}, s);
+}
+
+// db alone (the layer's weight gradient ran elsewhere).
+VGPU_API int vgpu_bias_grad_reduce(const float* dbpart, int slabs, int dbc, void* db, int db_bf16, hipStream_t s) {
+  if (!dbpart || !db || slabs < 1 || dbc < 1) return -1;
+  return (int)launch_wgrad_reduce<1>(nullptr, nullptr, 0, 0, DbJob{dbpart, db, dbc, slabs, db_bf16}, s);
+}
+
+namespace {
+int wgrad_impl(const void* dy, const void* x, void* dw, void* ws, int64_t ws_bytes, int N, int H, int W, int C,
+               int Cout, int KS, int stride, int pad, const DbJob& job, hipStream_t s) {
   if (C % 64 || Cout % 64 || KS < 1 || stride < 1 || pad < 0 || N < 1) return -1;
   WgradArgs a{};
   a.dy = static_cast<const uint16_t*>(dy);
@@ -537,16 +607,18 @@ VGPU_API int vgpu_conv_wgrad_nhwc(const void* dy, const void* x, void* dw, void*
     else e = launch_wgrad<64, 64>(a, s);
   }
   if (e != hipSuccess) return (int)e;
-  if (a.splits == 1) return 0;  // the K loop wrote bf16 directly
+  if (a.splits == 1)  // the K loop wrote bf16 directly; the bias job (if any) alone
+    return job.part ? (int)launch_wgrad_reduce<1>(nullptr, nullptr, 0, 0, job, s) : 0;
   const int64_t n4 = (int64_t)Cout * a.Ktot / 4;
   const float* wsf = static_cast<const float*>(ws);
   uint16_t* dwp = static_cast<uint16_t*>(dw);
   const int nsp = a.splits;
-  if (nsp >= 64) e = launch_wgrad_reduce<16>(wsf, dwp, n4, nsp, s);
-  else if (nsp >= 32) e = launch_wgrad_reduce<8>(wsf, dwp, n4, nsp, s);
-  else if (nsp >= 16) e = launch_wgrad_reduce<4>(wsf, dwp, n4, nsp, s);
-  else if (nsp >= 8) e = launch_wgrad_reduce<2>(wsf, dwp, n4, nsp, s);
-  else e = launch_wgrad_reduce<1>(wsf, dwp, n4, nsp, s);
+  if (nsp >= 64) e = launch_wgrad_reduce<16>(wsf, dwp, n4, nsp, job, s);
+  else if (nsp >= 32) e = launch_wgrad_reduce<8>(wsf, dwp, n4, nsp, job, s);
+  else if (nsp >= 16) e = launch_wgrad_reduce<4>(wsf, dwp, n4, nsp, job, s);
+  else if (nsp >= 8) e = launch_wgrad_reduce<2>(wsf, dwp, n4, nsp, job, s);
+  else e = launch_wgrad_reduce<1>(wsf, dwp, n4, nsp, job, s);
   return (int)e;
 }
+}  // namespace
 

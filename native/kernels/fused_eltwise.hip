@@ -350,3 +350,27 @@ VGPU_API int vgpu_pool_relu_bias_grad_nhwc(const void* dyp, const void* idx, con
                        (const float*)ws, (float*)db, c, slabs);
   return (int)hipGetLastError();
 }
+
+// Partials only (no reduce launch): ws receives [slabs][c] fp32 and *slabs_out
+// their count; the bias gradient is summed by vgpu_conv_wgrad_db_nhwc's reduce
+// launch (or vgpu_bias_grad_reduce).  pooled: dy is [N][H/k][W/k][c] with its
+// argmax idx, as in vgpu_pool_relu_bias_grad_nhwc (k = 0: not pooled).
+VGPU_API int vgpu_relu_bias_grad_partial_nhwc(const void* dy, const void* idx, const void* y, void* g, void* ws,
+                                              int N, int H, int W, uint32_t c, int k, int* slabs_out,
+                                              hipStream_t stream) {
+  if (c % 8 || c / 8 > kThreads || N < 1 || H < 1 || W < 1 || k < 0 || k > 15 || (k && (H < k || W < k)))
+    return -1;
+  const uint32_t cv = c / 8;
+  const uint64_t rows = (uint64_t)N * H * W;
+  const uint32_t slabs = rbg_slabs(rows, cv);
+  if (k) {
+    const PoolGeo pg{(const bf16x8*)dy, (const uint2*)idx, H, W, H / k, W / k, k};
+    hipLaunchKernelGGL(relu_bias_grad_kernel<true>, dim3(slabs), dim3(kThreads), 0, stream, nullptr,
+                       (const bf16x8*)y, (bf16x8*)g, (float*)ws, rows, cv, pg);
+  } else {
+    hipLaunchKernelGGL(relu_bias_grad_kernel<false>, dim3(slabs), dim3(kThreads), 0, stream, (const bf16x8*)dy,
+                       (const bf16x8*)y, (bf16x8*)g, (float*)ws, rows, cv, PoolGeo{});
+  }
+  if (slabs_out) *slabs_out = (int)slabs;
+  return (int)hipGetLastError();
+}

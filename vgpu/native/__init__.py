@@ -64,6 +64,13 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_relu_bias_grad_nhwc.restype = ctypes.c_int
     lib.vgpu_pool_relu_bias_grad_nhwc.argtypes = [vp] * 6 + [ctypes.c_int] * 3 + [u32, ctypes.c_int, ctypes.c_int, vp]
     lib.vgpu_pool_relu_bias_grad_nhwc.restype = ctypes.c_int
+    lib.vgpu_relu_bias_grad_partial_nhwc.argtypes = [vp] * 5 + [ctypes.c_int] * 3 + [u32, ctypes.c_int, vp, vp]
+    lib.vgpu_relu_bias_grad_partial_nhwc.restype = ctypes.c_int
+    lib.vgpu_conv_wgrad_db_nhwc.argtypes = [vp] * 4 + [ctypes.c_int64] + [ctypes.c_int] * 8 + [vp] + \
+        [ctypes.c_int] * 2 + [vp, ctypes.c_int, vp]
+    lib.vgpu_conv_wgrad_db_nhwc.restype = ctypes.c_int
+    lib.vgpu_bias_grad_reduce.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, vp]
+    lib.vgpu_bias_grad_reduce.restype = ctypes.c_int
     ci = ctypes.c_int
     lib.vgpu_conv2d_nhwc.argtypes = [vp, vp, vp, vp, vp, vp, vp] + [ci] * 9 + [vp]
     lib.vgpu_conv2d_nhwc_ws.argtypes = [vp, vp, vp, vp, vp, vp, vp] + [ci] * 9 + [vp, ctypes.c_int64, vp]

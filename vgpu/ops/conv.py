@@ -320,7 +320,7 @@ _TRAIN_NATIVE = os.environ.get("VGPU_NATIVE_CONV_TRAIN", "1") != "0"
 
 
 def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, ks: int, *, stride: int = 1,
-                 padding: int = 0) -> torch.Tensor:
+                 padding: int = 0, db_job: tuple | None = None) -> torch.Tensor:
     """Weight gradient of y = conv2d(x, w, stride, padding) for a [Cout, C, ks, ks]
     channels_last bf16 weight, on the MFMA kernel (native/kernels/conv_wgrad.hip:
     split-K over output pixels, fp32 partials, deterministic reduce).
@@ -337,8 +337,14 @@ def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, ks: int, *, stride: int = 1,
         raise ValueError("unsupported wgrad shape")
     ws = torch.empty(max(need // 4, 1), dtype=torch.float32, device=x.device)
     dw = torch.empty((cout, c, ks, ks), dtype=x.dtype, device=x.device, memory_format=_CL)
-    rc = lib.vgpu_conv_wgrad_nhwc(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), need, n, h, wd, c, cout,
-                                  ks, stride, padding, _stream())
+    if db_job is not None:  # (partials, slabs, db): the bias gradient summed in the same reduce launch
+        part, slabs, db = db_job
+        rc = lib.vgpu_conv_wgrad_db_nhwc(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), need, n, h, wd, c, cout, ks, stride,
+                                         padding, _ptr(part), slabs, db.numel(), _ptr(db),
+                                         int(db.dtype == torch.bfloat16), _stream())
+    else:
+        rc = lib.vgpu_conv_wgrad_nhwc(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), need, n, h, wd, c, cout,
+                                      ks, stride, padding, _stream())
     if rc != 0:
         raise RuntimeError(f"vgpu_conv_wgrad_nhwc: error {rc}")
     return dw
@@ -474,7 +480,8 @@ class _ConvTrainFn(torch.autograd.Function):
 
 
 def conv_backward(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, p: int, need_dx: bool,
-                  need_dw: bool, *, skip_dx: bool = False) -> tuple[torch.Tensor | None, torch.Tensor | None]:
+                  need_dw: bool, *, skip_dx: bool = False,
+                  db_job: tuple | None = None) -> tuple[torch.Tensor | None, torch.Tensor | None]:
     """(dx, dw) of y = conv(x, w, stride s, padding p): dx on the MFMA kernel for
     stride 1 (MIOpen otherwise), dw per _wgrad_native.  skip_dx: the caller
     computed a stride-1 dx itself (vgpu.ops.bnconv's fused data gradient)."""
@@ -489,9 +496,16 @@ def conv_backward(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, p:
     elif need_dx:
         dx, dw, _ = bw(dy, x, w, *common, [True, need_dw and not native_dw, False])
     if native_dw:
-        dw = conv2d_wgrad(dy, x, w.shape[2], stride=s, padding=p)
+        dw = conv2d_wgrad(dy, x, w.shape[2], stride=s, padding=p, db_job=db_job)
+        db_job = None
     elif need_dw and dw is None:
         dw = bw(dy, x, w, *common, [False, True, False])[1]
+    if db_job is not None:  # no native weight-gradient reduce to ride along with
+        part, slabs, db = db_job
+        rc = load_kernels().vgpu_bias_grad_reduce(_ptr(part), slabs, db.numel(), _ptr(db),
+                                                  int(db.dtype == torch.bfloat16), _stream())
+        if rc != 0:
+            raise RuntimeError(f"vgpu_bias_grad_reduce: error {rc}")
     return dx, dw
 
 
@@ -536,9 +550,34 @@ class _ConvBiasReLUTrainFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, y = ctx.saved_tensors
-        g, db = relu_bias_grad(dy.contiguous(memory_format=_CL), y, ctx.bias_dtype)
-        dx, dw = conv_backward(g, x, w, ctx.stride, ctx.padding, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
-        return dx, dw, db if ctx.needs_input_grad[2] else None, None, None
+        g, part, slabs = relu_bias_grad_partial(dy.contiguous(memory_format=_CL), y)
+        db = torch.empty(y.shape[1], dtype=ctx.bias_dtype, device=y.device) if ctx.needs_input_grad[2] else None
+        dx, dw = conv_backward(g, x, w, ctx.stride, ctx.padding, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                               db_job=(part, slabs, db) if db is not None else None)
+        return dx, dw, db, None, None
+
+
+def relu_bias_grad_partial(dy: torch.Tensor, y: torch.Tensor, idx: torch.Tensor | None = None,
+                           k: int = 0) -> tuple[torch.Tensor, torch.Tensor, int]:
+    """(g, partials, slabs): g = dy·[y > 0] (dy arriving through a k×k / stride-k
+    max pool with argmax idx when k > 0) and the per-slab column sums of g, fp32
+    [slabs, C] -- the bias gradient is summed by the weight gradient's reduce
+    launch (conv_backward's db_job)."""
+    _nhwc(dy, "dy")
+    _nhwc(y, "y")
+    n, c, h, w = y.shape
+    lib = load_kernels()
+    g = torch.empty_like(y, memory_format=_CL)
+    need = lib.vgpu_relu_bias_grad_workspace(n * h * w, c)
+    if need < 0:
+        raise ValueError("unsupported relu_bias_grad shape")
+    part = torch.empty(max(need // 4, 1), dtype=torch.float32, device=y.device)
+    slabs = ctypes.c_int(0)
+    rc = lib.vgpu_relu_bias_grad_partial_nhwc(_ptr(dy), _ptr(idx), _ptr(y), _ptr(g), _ptr(part), n, h, w, c, k,
+                                              ctypes.byref(slabs), _stream())
+    if rc != 0:
+        raise RuntimeError(f"vgpu_relu_bias_grad_partial_nhwc: error {rc}")
+    return g, part, slabs.value
 
 
 def relu_bias_grad(dy: torch.Tensor, y: torch.Tensor,
@@ -589,18 +628,11 @@ class _ConvBiasReLUPoolTrainFn(torch.autograd.Function):
     def backward(ctx, dp):
         x, w, y, idx = ctx.saved_tensors
         dp = dp.contiguous(memory_format=_CL)
-        n, c, h, wd = y.shape
-        lib = load_kernels()
-        g = torch.empty_like(y, memory_format=_CL)
-        db = torch.empty(c, dtype=ctx.bias_dtype, device=y.device)
-        ws = torch.empty(max(lib.vgpu_relu_bias_grad_workspace(n * h * wd, c) // 4, 1), dtype=torch.float32,
-                         device=y.device)
-        rc = lib.vgpu_pool_relu_bias_grad_nhwc(_ptr(dp), _ptr(idx), _ptr(y), _ptr(g), _ptr(db), _ptr(ws), n, h, wd,
-                                               c, ctx.k, int(ctx.bias_dtype == torch.bfloat16), _stream())
-        if rc != 0:
-            raise RuntimeError(f"vgpu_pool_relu_bias_grad_nhwc: error {rc}")
-        dx, dw = conv_backward(g, x, w, ctx.stride, ctx.padding, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
-        return dx, dw, db if ctx.needs_input_grad[2] else None, None, None, None
+        g, part, slabs = relu_bias_grad_partial(dp, y, idx=idx, k=ctx.k)
+        db = torch.empty(y.shape[1], dtype=ctx.bias_dtype, device=y.device) if ctx.needs_input_grad[2] else None
+        dx, dw = conv_backward(g, x, w, ctx.stride, ctx.padding, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                               db_job=(part, slabs, db) if db is not None else None)
+        return dx, dw, db, None, None, None
 
 
 def conv_bias_relu_pool_train(x: torch.Tensor, conv: torch.nn.Conv2d, pool: torch.nn.MaxPool2d) -> torch.Tensor:
