@@ -374,3 +374,29 @@ VGPU_API int vgpu_relu_bias_grad_partial_nhwc(const void* dy, const void* idx, c
   if (slabs_out) *slabs_out = (int)slabs;
   return (int)hipGetLastError();
 }
+
+// ---- zero-pad the channel dimension of a [rows][c] bf16 tensor to cp ---------------
+// One pass (F.pad is a fill plus a copy): VGG-16's 3-channel first layer runs
+// the MFMA conv on 64 channels, its input and weight padded every step.
+namespace {
+__global__ void __launch_bounds__(kThreads) pad_channels_kernel(const uint16_t* __restrict__ x,
+                                                                bf16x8* __restrict__ y, uint64_t rows, uint32_t c,
+                                                                uint32_t cpv) {
+  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= rows * cpv) return;
+  const uint64_t r = i / cpv;
+  const uint32_t c0 = (uint32_t)(i - r * cpv) * 8;
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o.v[j] = c0 + j < c ? x[r * c + c0 + j] : (uint16_t)0;
+  y[i] = o;
+}
+}  // namespace
+
+VGPU_API int vgpu_pad_channels(const void* x, void* y, uint64_t rows, uint32_t c, uint32_t cp, hipStream_t stream) {
+  if (cp % 8 || cp < c || rows == 0 || !aligned16(y)) return -1;
+  const uint64_t n = rows * (cp / 8);
+  hipLaunchKernelGGL(pad_channels_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0, stream,
+                     (const uint16_t*)x, (bf16x8*)y, rows, c, cp / 8);
+  return (int)hipGetLastError();
+}

@@ -217,12 +217,38 @@ __global__ void __launch_bounds__(kThreads) skinny_dgrad_reduce_kernel(const flo
 
 // ---- weight gradient: thread = 8 columns of kRows rows; x chunk held in registers
 constexpr int kWgRows = 8;
+// The data gradient's split sum rides along: blocks of the extra grid row
+// (blockIdx.y == row_groups) reduce ws into dx instead (one launch fewer).
+struct DxJob {
+  const float* ws;
+  uint16_t* dx;
+  int64_t total8;
+  int splits;
+};
+
 template <int B>
 __global__ void __launch_bounds__(kThreads) skinny_wgrad_kernel(const uint16_t* __restrict__ dy,
                                                                 const uint16_t* __restrict__ yout,
                                                                 const uint16_t* __restrict__ x,
                                                                 uint16_t* __restrict__ dw, uint16_t* __restrict__ db,
-                                                                int N, int K, int act) {
+                                                                int N, int K, int act, const DxJob job,
+                                                                int row_groups) {
+  if ((int)blockIdx.y >= row_groups) {  // block-uniform: the dx reduce job
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < job.total8;
+         i += (int64_t)gridDim.x * kThreads) {
+      const float4* p = reinterpret_cast<const float4*>(job.ws) + i * 2;
+      float4 a = p[0], b = p[1];
+      for (int sp = 1; sp < job.splits; ++sp) {
+        const float4* q = p + (int64_t)sp * job.total8 * 2;
+        const float4 c = q[0], d = q[1];
+        a.x += c.x; a.y += c.y; a.z += c.z; a.w += c.w;
+        b.x += d.x; b.y += d.y; b.z += d.z; b.w += d.w;
+      }
+      reinterpret_cast<u32x4*>(job.dx)[i] =
+          u32x4{pack2(a.x, a.y), pack2(a.z, a.w), pack2(b.x, b.y), pack2(b.z, b.w)};
+    }
+    return;
+  }
   const int kv = K >> 3;
   const int c = blockIdx.x * kThreads + threadIdx.x;
   const int n0 = blockIdx.y * kWgRows;
@@ -324,8 +350,30 @@ VGPU_API int vgpu_skinny_dgrad(const void* dy, const void* yout, const void* w, 
 VGPU_API int vgpu_skinny_wgrad(const void* dy, const void* yout, const void* x, void* dw, void* db, int B, int N,
                                int K, int act, hipStream_t s) {
   if (!vgpu_skinny_supported(B, N, K) || !al16(x) || !al16(dw)) return -1;
-  const dim3 grid((K / 8 + kThreads - 1) / kThreads, (N + kWgRows - 1) / kWgRows);
+  const int rg = (N + kWgRows - 1) / kWgRows;
+  const dim3 grid((K / 8 + kThreads - 1) / kThreads, rg);
   VGPU_SKINNY_SWITCH(B, skinny_wgrad_kernel, grid, (const uint16_t*)dy, (const uint16_t*)yout, (const uint16_t*)x,
-                     (uint16_t*)dw, (uint16_t*)db, N, K, act)
+                     (uint16_t*)dw, (uint16_t*)db, N, K, act, DxJob{}, rg)
+  return (int)hipGetLastError();
+}
+
+// The whole backward of a skinny layer in two launches: the data gradient's
+// row splits into ws, then dW / db with the split sum into dx riding along.
+VGPU_API int vgpu_skinny_backward(const void* dy, const void* yout, const void* x, const void* w, void* dx, void* dw,
+                                  void* db, void* ws, int64_t ws_bytes, int B, int N, int K, int act,
+                                  hipStream_t s) {
+  if (!vgpu_skinny_supported(B, N, K) || !al16(x) || !al16(dw) || !al16(w) || !al16(dx) || !al16(ws)) return -1;
+  if (ws_bytes < vgpu_skinny_dgrad_workspace(B, N, K)) return -1;
+  const int splits = (N + kDgRows - 1) / kDgRows;
+  const dim3 g1((K / 8 + 63) / 64, splits);
+  VGPU_SKINNY_SWITCH(B, skinny_dgrad_kernel, g1, (const uint16_t*)dy, (const uint16_t*)yout, (const uint16_t*)w,
+                     (float*)ws, N, K, act)
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const int rg = (N + kWgRows - 1) / kWgRows;
+  const dim3 g2((K / 8 + kThreads - 1) / kThreads, rg + 1);
+  const DxJob job{(const float*)ws, (uint16_t*)dx, (int64_t)B * K / 8, splits};
+  VGPU_SKINNY_SWITCH(B, skinny_wgrad_kernel, g2, (const uint16_t*)dy, (const uint16_t*)yout, (const uint16_t*)x,
+                     (uint16_t*)dw, (uint16_t*)db, N, K, act, job, rg)
   return (int)hipGetLastError();
 }

@@ -308,3 +308,15 @@ def test_conv_bias_relu_pool_train_matches_fp32(gpu_build, case):
     assert _rel(x.grad, xr.grad) < 6e-2
     assert _rel(conv.weight.grad, wr.grad) < 6e-2
     assert _rel(conv.bias.grad, br.grad) < 6e-2
+
+
+def test_pad_channels_matches_fpad(gpu_build):
+    """vgpu_pad_channels (one pass) against F.pad on NHWC bf16, with its gradient."""
+    from vgpu.ops.conv import pad_channels
+    x = _x((2, 3, 9, 7), 11).requires_grad_()
+    y = pad_channels(x, 64)
+    yr = torch.nn.functional.pad(x.detach(), (0, 0, 0, 0, 0, 61))
+    assert y.is_contiguous(memory_format=CL) and torch.equal(y, yr)
+    dy = _x(tuple(y.shape), 12)
+    y.backward(dy)
+    assert torch.equal(x.grad, dy[:, :3])

@@ -71,6 +71,8 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_conv_wgrad_db_nhwc.restype = ctypes.c_int
     lib.vgpu_bias_grad_reduce.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, vp]
     lib.vgpu_bias_grad_reduce.restype = ctypes.c_int
+    lib.vgpu_pad_channels.argtypes = [vp, vp, u64, u32, u32, vp]
+    lib.vgpu_pad_channels.restype = ctypes.c_int
     ci = ctypes.c_int
     lib.vgpu_conv2d_nhwc.argtypes = [vp, vp, vp, vp, vp, vp, vp] + [ci] * 9 + [vp]
     lib.vgpu_conv2d_nhwc_ws.argtypes = [vp, vp, vp, vp, vp, vp, vp] + [ci] * 9 + [vp, ctypes.c_int64, vp]

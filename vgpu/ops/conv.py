@@ -662,6 +662,31 @@ def _conv_bias_relu_ok(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
             and conv.kernel_size[0] in (1, 3) and supported(conv.in_channels, conv.out_channels, conv.kernel_size[0]))
 
 
+class _PadChannelsFn(torch.autograd.Function):
+    """Zero channels appended to an NHWC bf16 tensor in one kernel pass;
+    the gradient is the leading-channel slice."""
+
+    @staticmethod
+    def forward(ctx, x, cp: int):
+        n, c, h, w = x.shape
+        y = torch.empty((n, cp, h, w), dtype=x.dtype, device=x.device, memory_format=_CL)
+        rc = load_kernels().vgpu_pad_channels(_ptr(x), _ptr(y), n * h * w, c, cp, _stream())
+        if rc != 0:
+            raise RuntimeError(f"vgpu_pad_channels: error {rc}")
+        ctx.c = c
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy[:, :ctx.c].contiguous(memory_format=_CL), None
+
+
+def pad_channels(x: torch.Tensor, cp: int) -> torch.Tensor:
+    """x [N, C, H, W] bf16 channels_last → [N, cp, H, W] with zero channels C..cp-1."""
+    _nhwc(x, "x")
+    return _PadChannelsFn.apply(x, cp)
+
+
 def conv_bias_relu_train(x: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor:
     """relu(conv(x)) with the module's semantics (bias included); bf16
     channels_last CUDA tensors of supported shapes run natively, anything else
@@ -677,8 +702,8 @@ def conv_bias_relu_train(x: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor
         # conv and native weight gradient -- ~21x the MACs of the 3 real
         # channels, still far less time than MIOpen's two kernels at 224²
         # (prof_3_2.md: 49 us each).
-        xp = F.pad(x, (0, 0, 0, 0, 0, 64 - c)).contiguous(memory_format=_CL)
-        wp = F.pad(w, (0, 0, 0, 0, 0, 64 - c)).contiguous(memory_format=_CL)
+        xp = pad_channels(x.contiguous(memory_format=_CL), 64)
+        wp = pad_channels(w.contiguous(memory_format=_CL), 64)
         return _ConvBiasReLUTrainFn.apply(xp, wp, conv.bias, 1, 1)
     if not _conv_bias_relu_ok(x, conv):
         return F.relu(conv(x))

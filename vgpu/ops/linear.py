@@ -32,6 +32,8 @@ def _lib():
         lib.vgpu_skinny_dgrad.restype = ci
         lib.vgpu_skinny_wgrad.argtypes = [vp] * 5 + [ci] * 4 + [vp]
         lib.vgpu_skinny_wgrad.restype = ci
+        lib.vgpu_skinny_backward.argtypes = [vp] * 8 + [ctypes.c_int64] + [ci] * 4 + [vp]
+        lib.vgpu_skinny_backward.restype = ci
         _BOUND = True
     return lib
 
@@ -69,6 +71,14 @@ class _SkinnyLinearFn(torch.autograd.Function):
         lib = _lib()
         yo = y if ctx.act else None
         dx = dw = db = None
+        if ctx.needs_input_grad[0] and ctx.needs_input_grad[1]:  # both: two launches in all
+            need = lib.vgpu_skinny_dgrad_workspace(bsz, n, k)
+            ws = torch.empty(need // 4, dtype=torch.float32, device=x.device)
+            dx, dw = torch.empty_like(x), torch.empty_like(w)
+            db = torch.empty(n, dtype=w.dtype, device=w.device) if ctx.has_b else None
+            _check(lib.vgpu_skinny_backward(_p(dy), _p(yo), _p(x), _p(w), _p(dx), _p(dw), _p(db), _p(ws), need, bsz,
+                                            n, k, ctx.act, _stream()), "vgpu_skinny_backward")
+            return dx, dw, db, None
         if ctx.needs_input_grad[0]:
             need = lib.vgpu_skinny_dgrad_workspace(bsz, n, k)
             ws = torch.empty(need // 4, dtype=torch.float32, device=x.device)
