@@ -441,6 +441,8 @@ def main(argv=None) -> int:
             "per_pod_policy": [(p.done.get("share") or {}).get("policy") for p in pods],
             "per_pod_cus": [(p.done.get("share") or {}).get("cus") for p in pods],
             "per_pod_limiter_wait_ms": [(p.done.get("share") or {}).get("limiter_wait_ms") for p in pods],
+            "per_pod_occ_charged_ms": [(p.done.get("share") or {}).get("occ_charged_ms") for p in pods],
+            "per_pod_host_pid_src": [(p.done.get("share") or {}).get("host_pid_src") for p in pods],
             "per_pod_decide_wait_s": [((p.ready or {}).get("decide") or {}).get("waited_s") for p in pods],
             "vram_cap": cap,
             "placement": placement,

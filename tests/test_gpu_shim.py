@@ -355,7 +355,12 @@ def _bench_value(args, profiler_dir=None, timeout=400):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=REPO)
     assert r.returncode == 0, r.stderr[-4000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
-    return json.loads(line)["value"]
+    res = json.loads(line)
+    print(args[-6:], "limiter wait", res.get("per_pod_limiter_wait_ms"), "occupancy charge",
+          res.get("per_pod_occ_charged_ms"), "host pid source", res.get("per_pod_host_pid_src"))
+    if profiler_dir:  # the pods' enforcement-library log lines (host pid resolution, cross-check)
+        print("\n".join(ln for ln in r.stderr.splitlines() if "vgpu" in ln.lower())[-3000:])
+    return res["value"]
 
 
 def test_limiter_share_holds_under_rocprof(gpu_build, tmp_path):

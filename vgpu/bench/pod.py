@@ -204,9 +204,17 @@ def share_state(dev: int = 0) -> dict | None:
     out = (ctypes.c_int64 * 8)()
     fn(ctypes.c_int(dev), out)
     phase = _PHASES.get(int(out[0]), "exploring")
+    src = ctypes.c_int(0)
+    try:
+        host_pid = int(ctypes.CDLL(None).vgpu_self_host_pid(ctypes.byref(src)))
+    except (OSError, AttributeError):
+        host_pid = 0
     return {"policy": "spatial" if out[3] else phase, "auto_phase": phase, "members": int(out[1]),
             "decided": bool(out[2]) and phase in ("temporal", "spatial"), "own_cus": bool(out[3]),
-            "cus": int(out[4]), "limiter_active": bool(out[5]), "limiter_wait_ms": round(out[6] / 1e6, 3)}
+            "cus": int(out[4]), "limiter_active": bool(out[5]), "limiter_wait_ms": round(out[6] / 1e6, 3),
+            # the KFD cu_occupancy cross-check: what it charged beyond the markers,
+            # and how the host pid it needs was found (0 = unresolved)
+            "occ_charged_ms": round(out[7] / 1e6, 3), "host_pid_src": int(src.value) if host_pid > 0 else 0}
 
 
 def cap_probe() -> dict:
