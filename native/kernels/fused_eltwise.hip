@@ -218,11 +218,14 @@ __global__ void __launch_bounds__(kThreads) relu_bias_grad_kernel(const bf16x8* 
       const uint64_t r = row0 + (uint64_t)k * per;
       if (r < rows) {
         if constexpr (POOL) {
-          const uint32_t iw = (uint32_t)(r % pg.W), t2 = (uint32_t)(r / pg.W), ih = t2 % pg.H, n = t2 / pg.H;
+          // 32-bit index math (rows < 2^31, checked on the host): the 64-bit
+          // div / mod pair per row made this pass ~1.8x the unpooled one
+          const uint32_t r32 = (uint32_t)r, W = (uint32_t)pg.W, H = (uint32_t)pg.H;
+          const uint32_t t2 = r32 / W, iw = r32 - t2 * W, n = t2 / H, ih = t2 - n * H;
           const uint32_t oh = ih / pg.k, ow = iw / pg.k;
           tap[k] = 0xffu;  // rows past the last full window receive no gradient
           if (oh < (uint32_t)pg.OH && ow < (uint32_t)pg.OW) {
-            const uint64_t o = (((uint64_t)n * pg.OH + oh) * pg.OW + ow) * cv + cg;
+            const uint64_t o = (uint64_t)((n * (uint32_t)pg.OH + oh) * (uint32_t)pg.OW + ow) * cv + cg;
             a[k] = pg.dyp[o];
             const uint2 t = pg.idx[o];
             tap[k] = (ih - oh * pg.k) * pg.k + (iw - ow * pg.k);
@@ -336,6 +339,7 @@ VGPU_API int vgpu_pool_relu_bias_grad_nhwc(const void* dyp, const void* idx, con
                                            void* ws, int N, int H, int W, uint32_t c, int k, int db_bf16,
                                            hipStream_t stream) {
   if (c % 8 || c / 8 > kThreads || N < 1 || H < 1 || W < 1 || k < 1 || k > 15 || H < k || W < k) return -1;
+  if ((uint64_t)N * H * W >= (1ull << 31)) return -1;
   const uint32_t cv = c / 8;
   const uint64_t rows = (uint64_t)N * H * W;
   const uint32_t slabs = rbg_slabs(rows, cv);
@@ -360,6 +364,7 @@ VGPU_API int vgpu_relu_bias_grad_partial_nhwc(const void* dy, const void* idx, c
                                               hipStream_t stream) {
   if (c % 8 || c / 8 > kThreads || N < 1 || H < 1 || W < 1 || k < 0 || k > 15 || (k && (H < k || W < k)))
     return -1;
+  if ((uint64_t)N * H * W >= (1ull << 31)) return -1;
   const uint32_t cv = c / 8;
   const uint64_t rows = (uint64_t)N * H * W;
   const uint32_t slabs = rbg_slabs(rows, cv);

@@ -52,10 +52,10 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 // ---- forward: one wave per R = 2 output rows, the K loop unrolled by U ------------
-// kU = 8: 256 B of weight per lane in flight.  In a training step fc1's 205 MB
-// no longer sits in the 256 MB MALL, and at kU = 4 the pass ran at ~3 TB/s
-// (68 us; profiles/r5/train/vgg_b2_step_kernels.md).
-constexpr int kR = 2, kU = 8;
+// R = 4 rows per wave share each x load (x is re-read from L2 by every wave),
+// U = 4: 256 B of weight per lane in flight.  In a training step fc1's 205 MB
+// no longer sits in the 256 MB MALL; R = 2 / U = 4 ran at ~3 TB/s (68 us).
+constexpr int kR = 4, kU = 4;
 template <int B>
 __global__ void __launch_bounds__(kThreads) skinny_fwd_kernel(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
