@@ -83,6 +83,12 @@ struct ConvArgs {
   // sums them in split order and applies bias / residual / activation.
   float* ws;
   int kper, splits;
+  // Split-K data gradient into a ReLU layer (splitk_reduce_kernel): the output
+  // is masked by gmask > 0 (the ReLU's own output) and per-block column sums of
+  // the stored bf16 values go to gpart[block][Cout] -- that layer's bias-gradient
+  // partials, so its separate ReLU-backward pass disappears (VGG-16 training).
+  const uint16_t* gmask;
+  float* gpart;
 };
 
 // d act / d z as PyTorch defines it (threshold_backward / hardtanh_backward).
@@ -758,39 +764,65 @@ __global__ void __launch_bounds__(kThreads, 2) conv_glds_kernel(const ConvArgs a
 }
 
 // Split-K epilogue: y = act(Σ_split ws[split] + bias (+ residual)) in bf16, the
-// splits summed in order (deterministic).  One thread = 8 channels of one row.
+// splits summed in order (deterministic).  One thread = 8 channels of one row;
+// a block covers 256 / (Cout / 8) whole rows.  With gmask: y ·= [gmask > 0] and
+// the block's column sums of the stored values go to gpart[block].
 __global__ void __launch_bounds__(kThreads) splitk_reduce_kernel(const ConvArgs a) {
+  __shared__ float red[kThreads][9];
   const int cv = a.Cout >> 3;
   const int64_t idx = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (idx >= (int64_t)a.M * cv) return;
-  const int m = (int)(idx / cv), col = (int)(idx - (int64_t)m * cv) * 8;
-  const int64_t plane = (int64_t)a.M * a.Cout, off = (int64_t)m * a.Cout + col;
-  float v[8];
-  load8f(a.ws + off, v);
-  for (int sp = 1; sp < a.splits; ++sp) {
-    float p[8];
-    load8f(a.ws + sp * plane + off, p);
+  const bool valid = idx < (int64_t)a.M * cv;
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (valid) {
+    const int m = (int)(idx / cv), col = (int)(idx - (int64_t)m * cv) * 8;
+    const int64_t plane = (int64_t)a.M * a.Cout, off = (int64_t)m * a.Cout + col;
+    load8f(a.ws + off, v);
+    for (int sp = 1; sp < a.splits; ++sp) {
+      float p[8];
+      load8f(a.ws + sp * plane + off, p);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] += p[j];
-  }
-  if (a.bias) {
-    float bb[8];
-    load_bias8(a, col, bb);
+      for (int j = 0; j < 8; ++j) v[j] += p[j];
+    }
+    if (a.bias) {
+      float bb[8];
+      load_bias8(a, col, bb);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] += bb[j];
-  }
-  if (a.res) {
-    float re[8];
-    unpack8(*reinterpret_cast<const u32x4*>(a.res + off), re);
+      for (int j = 0; j < 8; ++j) v[j] += bb[j];
+    }
+    if (a.res) {
+      float re[8];
+      unpack8(*reinterpret_cast<const u32x4*>(a.res + off), re);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] += re[j];
-  }
-  if (a.act) {
-    const float hi = a.act == 2 ? 6.0f : INFINITY;
+      for (int j = 0; j < 8; ++j) v[j] += re[j];
+    }
+    if (a.act) {
+      const float hi = a.act == 2 ? 6.0f : INFINITY;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = fminf(fmaxf(v[j], 0.0f), hi);
+      for (int j = 0; j < 8; ++j) v[j] = fminf(fmaxf(v[j], 0.0f), hi);
+    }
+    if (a.gmask) {
+      float mk[8];
+      unpack8(*reinterpret_cast<const u32x4*>(a.gmask + off), mk);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = mk[j] > 0.0f ? v[j] : 0.0f;
+    }
+    const u32x4 o = pack8(v);
+    *reinterpret_cast<u32x4*>(a.y + off) = o;
+    unpack8(o, v);  // the partial sums add the stored (rounded) values
   }
-  *reinterpret_cast<u32x4*>(a.y + off) = pack8(v);
+  if (!a.gpart) return;  // kernel-uniform
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = valid ? v[j] : 0.0f;
+  __syncthreads();
+  if ((int)threadIdx.x < cv) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < kThreads / cv; ++r)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += red[r * cv + threadIdx.x][j];
+    float* out = a.gpart + (int64_t)blockIdx.x * a.Cout + threadIdx.x * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = acc[j];
+  }
 }
 
 // ---- 256x256 tile for large 1x1 / stride-1 convs without a prologue ----------
@@ -2469,7 +2501,7 @@ namespace {
 int conv2d_impl(const void* x, const void* w, void* y, const void* res, const float* bias, const float* pscale,
                 const float* pshift, int N, int H, int W, int C, int Cout, int KS, int stride, int pad, int act,
                 float* stats, const void* bnx, const float* bncoef, int bnact, int res_stride, hipStream_t s,
-                float* ws = nullptr, int64_t ws_bytes = 0);
+                float* ws = nullptr, int64_t ws_bytes = 0, const void* gmask = nullptr, float* gpart = nullptr);
 
 int g_forced_split = -1;  // vgpu_conv_set_splitk: -1 heuristic, 0 off, n > 1 that many splits when eligible
 
@@ -2531,6 +2563,24 @@ VGPU_API int vgpu_conv2d_nhwc_ws(const void* x, const void* w, void* y, const vo
 
 VGPU_API void vgpu_conv_set_splitk(int mode) { g_forced_split = mode; }
 
+// Split-K data gradient into a ReLU layer: y = conv(x, w) · [gmask > 0] and
+// gpart[block][Cout] the per-block column sums of y (that layer's bias-gradient
+// partials; *blocks_out of them).  Only when this shape runs split-K
+// (vgpu_conv2d_workspace > 0): returns -1 otherwise, before any launch.
+VGPU_API int vgpu_conv2d_masked_splitk(const void* x, const void* w, void* y, int N, int H, int W, int C, int Cout,
+                                       int KS, int pad, const void* gmask, void* gpart, int64_t gpart_bytes,
+                                       void* ws, int64_t ws_bytes, int* blocks_out, hipStream_t s) {
+  if (!gmask || !gpart || !ws || Cout % 8 || kThreads % (Cout / 8) || KS < 1 || pad < 0) return -1;
+  const int64_t OH = H + 2 * pad - KS + 1, OW = W + 2 * pad - KS + 1;
+  if (OH < 1 || OW < 1) return -1;
+  const int64_t M = (int64_t)N * OH * OW;
+  const int64_t blocks = (M * (Cout / 8) + kThreads - 1) / kThreads;
+  if (vgpu_conv2d_workspace(N, H, W, C, Cout, KS, 1, pad, 0) <= 0 || gpart_bytes < blocks * Cout * 4) return -1;
+  if (blocks_out) *blocks_out = (int)blocks;
+  return conv2d_impl(x, w, y, nullptr, nullptr, nullptr, nullptr, N, H, W, C, Cout, KS, 1, pad, 0, nullptr, nullptr,
+                     nullptr, 0, 1, s, static_cast<float*>(ws), ws_bytes, gmask, static_cast<float*>(gpart));
+}
+
 // Training convolution with the BatchNorm statistics of its output from the
 // epilogue (ConvArgs::stats): stats = fp32 pairs [ceil(M / 64)][Cout], M = N·OH·OW.
 //   bnx == nullptr: forward — (Σ y, Σ y²) per 64-row group of the stored y.
@@ -2556,7 +2606,7 @@ namespace {
 int conv2d_impl(const void* x, const void* w, void* y, const void* res, const float* bias, const float* pscale,
                 const float* pshift, int N, int H, int W, int C, int Cout, int KS, int stride, int pad, int act,
                 float* stats, const void* bnx, const float* bncoef, int bnact, int res_stride, hipStream_t s,
-                float* ws, int64_t ws_bytes) {
+                float* ws, int64_t ws_bytes, const void* gmask, float* gpart) {
   const int bias_bf16 = (act >> 8) & 1;
   act &= 0xff;
   if (act > 2) return -1;
@@ -2629,11 +2679,14 @@ int conv2d_impl(const void* x, const void* w, void* y, const void* res, const fl
     hipError_t e;
     int kper;
     const int splits = (ws && !stats && per >= N) ? splitk_plan(c.M, C, Cout, KS, pro, narrow, kper) : 1;
+    if (gmask && splits <= 1) return -1;  // the masked form exists only as a split-K reduce
     if (splits > 1) {
       if (ws_bytes < (int64_t)splits * c.M * Cout * 4) return -1;
       c.ws = ws;
       c.kper = kper;
       c.splits = splits;
+      c.gmask = static_cast<const uint16_t*>(gmask);
+      c.gpart = gpart;
       c.nM = (c.M + 63) / 64;
       c.nN = Cout / bn;
       c.nwg = c.nM * c.nN;

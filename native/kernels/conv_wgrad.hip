@@ -236,6 +236,7 @@ struct DbJob {
   const float* part;
   void* db;
   int c, slabs, bf16;
+  int stride;  // floats between consecutive entries (2: the .x of float2 BN statistics)
 };
 
 __device__ void db_reduce_block(const DbJob& j, int blk) {
@@ -244,13 +245,14 @@ __device__ void db_reduce_block(const DbJob& j, int blk) {
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (ch < j.c) {
     int k = q;
+    const int st = j.stride > 0 ? j.stride : 1;
     for (; k + 48 < j.slabs; k += 64) {
-      a0 += j.part[(int64_t)k * j.c + ch];
-      a1 += j.part[(int64_t)(k + 16) * j.c + ch];
-      a2 += j.part[(int64_t)(k + 32) * j.c + ch];
-      a3 += j.part[(int64_t)(k + 48) * j.c + ch];
+      a0 += j.part[((int64_t)k * j.c + ch) * st];
+      a1 += j.part[((int64_t)(k + 16) * j.c + ch) * st];
+      a2 += j.part[((int64_t)(k + 32) * j.c + ch) * st];
+      a3 += j.part[((int64_t)(k + 48) * j.c + ch) * st];
     }
-    for (; k < j.slabs; k += 16) a0 += j.part[(int64_t)k * j.c + ch];
+    for (; k < j.slabs; k += 16) a0 += j.part[((int64_t)k * j.c + ch) * st];
   }
   red[q][cl] = (a0 + a1) + (a2 + a3);
   __syncthreads();
@@ -552,16 +554,17 @@ VGPU_API int vgpu_conv_wgrad_nhwc(const void* dy, const void* x, void* dw, void*
 // reduce).  dbpart: vgpu_relu_bias_grad_partial_nhwc's partials.
 VGPU_API int vgpu_conv_wgrad_db_nhwc(const void* dy, const void* x, void* dw, void* ws, int64_t ws_bytes, int N,
                                      int H, int W, int C, int Cout, int KS, int stride, int pad, const float* dbpart,
-                                     int slabs, int dbc, void* db, int db_bf16, hipStream_t s) {
-  if (!dbpart || !db || slabs < 1 || dbc < 1) return -1;
+                                     int slabs, int dbc, void* db, int db_bf16, int db_stride, hipStream_t s) {
+  if (!dbpart || !db || slabs < 1 || dbc < 1 || db_stride < 1) return -1;
   return wgrad_impl(dy, x, dw, ws, ws_bytes, N, H, W, C, Cout, KS, stride, pad,
-                    DbJob{dbpart, db, dbc, slabs, db_bf16}, s);
+                    DbJob{dbpart, db, dbc, slabs, db_bf16, db_stride}, s);
 }
 
 // db alone (the layer's weight gradient ran elsewhere).
-VGPU_API int vgpu_bias_grad_reduce(const float* dbpart, int slabs, int dbc, void* db, int db_bf16, hipStream_t s) {
-  if (!dbpart || !db || slabs < 1 || dbc < 1) return -1;
-  return (int)launch_wgrad_reduce<1>(nullptr, nullptr, 0, 0, DbJob{dbpart, db, dbc, slabs, db_bf16}, s);
+VGPU_API int vgpu_bias_grad_reduce(const float* dbpart, int slabs, int dbc, void* db, int db_bf16, int db_stride,
+                                   hipStream_t s) {
+  if (!dbpart || !db || slabs < 1 || dbc < 1 || db_stride < 1) return -1;
+  return (int)launch_wgrad_reduce<1>(nullptr, nullptr, 0, 0, DbJob{dbpart, db, dbc, slabs, db_bf16, db_stride}, s);
 }
 
 namespace {

@@ -320,3 +320,34 @@ def test_pad_channels_matches_fpad(gpu_build):
     dy = _x(tuple(y.shape), 12)
     y.backward(dy)
     assert torch.equal(x.grad, dy[:, :3])
+
+
+@pytest.mark.parametrize("case", [(2, 64, 128, 56), (2, 256, 512, 28), (2, 512, 512, 14)])
+def test_relu_mask_in_next_dgrad_matches_unfused(gpu_build, case):
+    """Two conv + ReLU layers: with in_relu the second layer's data gradient
+    applies the first layer's ReLU mask (BN-statistics epilogue, or the split-K
+    reduce on the 28² / 14² shapes) and hands over its bias partials
+    (dgrad_into_relu).  Gradients equal the unfused path's; bias gradients are
+    summed in another grouping (within fp32 rounding)."""
+    from vgpu.ops import conv as C
+    n, c1, c2, hw = case
+    torch.manual_seed(c1 + hw)
+    l1 = torch.nn.Conv2d(c1, c2, 3, padding=1).cuda().to(torch.bfloat16).to(memory_format=CL)
+    l2 = torch.nn.Conv2d(c2, c2, 3, padding=1).cuda().to(torch.bfloat16).to(memory_format=CL)
+    x0 = _x((n, c1, hw, hw), 7)
+    dy = _x((n, c2, hw, hw), 8)
+    grads = []
+    for fused in (False, True):
+        for mod in (l1, l2):
+            mod.weight.grad = mod.bias.grad = None
+        x = x0.clone().requires_grad_()
+        C._RELU_LINK.clear()
+        h = C.conv_bias_relu_train(x, l1)
+        y = C.conv_bias_relu_train(h, l2, in_relu=fused)
+        y.backward(dy)
+        if fused:
+            assert not C._RELU_LINK, "the first layer's backward should have taken the link"
+        grads.append([x.grad.clone(), l1.weight.grad.clone(), l1.bias.grad.clone(), l2.weight.grad.clone()])
+    (gx0, gw10, gb10, gw20), (gx1, gw11, gb11, gw21) = grads
+    assert torch.equal(gx0, gx1) and torch.equal(gw10, gw11) and torch.equal(gw20, gw21)
+    torch.testing.assert_close(gb11.float(), gb10.float(), atol=2e-2, rtol=1e-2)

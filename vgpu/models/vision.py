@@ -68,22 +68,29 @@ class VGG16(nn.Module):
             if getattr(self, "_dgrad", None) is None:
                 self._dgrad = DgradFilters([m for m in self.features if isinstance(m, nn.Conv2d)])
             self._dgrad.refresh()
+        from vgpu.ops import conv as C
+        C._RELU_LINK.clear()
         x = x.contiguous(memory_format=torch.channels_last)
         mods = list(self.features)
         i = 0
+        in_relu = False  # x is the output of the previous conv + ReLU (no pool between)
         while i < len(mods):
             m = mods[i]
             if isinstance(m, nn.Conv2d) and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU):
                 if i + 2 < len(mods) and isinstance(mods[i + 2], nn.MaxPool2d):
                     # conv + ReLU + pool: the pool backward fused into the ReLU / bias gradient
-                    x = conv_bias_relu_pool_train(x, m, mods[i + 2])
+                    x = conv_bias_relu_pool_train(x, m, mods[i + 2], in_relu=in_relu)
                     i += 3
+                    in_relu = False
                     continue
-                x = conv_bias_relu_train(x, m).contiguous(memory_format=torch.channels_last)
+                # the data gradient of the next conv applies this layer's ReLU mask
+                x = conv_bias_relu_train(x, m, in_relu=in_relu).contiguous(memory_format=torch.channels_last)
                 i += 2
+                in_relu = True
                 continue
             x = maxpool_train(x, m) if isinstance(m, nn.MaxPool2d) else m(x)
             i += 1
+            in_relu = False
         return x
 
 

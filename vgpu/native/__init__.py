@@ -67,9 +67,12 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_relu_bias_grad_partial_nhwc.argtypes = [vp] * 5 + [ctypes.c_int] * 3 + [u32, ctypes.c_int, vp, vp]
     lib.vgpu_relu_bias_grad_partial_nhwc.restype = ctypes.c_int
     lib.vgpu_conv_wgrad_db_nhwc.argtypes = [vp] * 4 + [ctypes.c_int64] + [ctypes.c_int] * 8 + [vp] + \
-        [ctypes.c_int] * 2 + [vp, ctypes.c_int, vp]
+        [ctypes.c_int] * 2 + [vp, ctypes.c_int, ctypes.c_int, vp]
     lib.vgpu_conv_wgrad_db_nhwc.restype = ctypes.c_int
-    lib.vgpu_bias_grad_reduce.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, vp]
+    lib.vgpu_bias_grad_reduce.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, vp]
+    lib.vgpu_conv2d_masked_splitk.argtypes = [vp] * 3 + [ctypes.c_int] * 7 + [vp, vp, ctypes.c_int64, vp,
+                                                                            ctypes.c_int64, vp, vp]
+    lib.vgpu_conv2d_masked_splitk.restype = ctypes.c_int
     lib.vgpu_bias_grad_reduce.restype = ctypes.c_int
     lib.vgpu_pad_channels.argtypes = [vp, vp, u64, u32, u32, vp]
     lib.vgpu_pad_channels.restype = ctypes.c_int

@@ -337,11 +337,11 @@ def conv2d_wgrad(dy: torch.Tensor, x: torch.Tensor, ks: int, *, stride: int = 1,
         raise ValueError("unsupported wgrad shape")
     ws = torch.empty(max(need // 4, 1), dtype=torch.float32, device=x.device)
     dw = torch.empty((cout, c, ks, ks), dtype=x.dtype, device=x.device, memory_format=_CL)
-    if db_job is not None:  # (partials, slabs, db): the bias gradient summed in the same reduce launch
-        part, slabs, db = db_job
+    if db_job is not None:  # (partials, slabs, db, stride): the bias gradient summed in the same reduce launch
+        part, slabs, db, pst = db_job
         rc = lib.vgpu_conv_wgrad_db_nhwc(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), need, n, h, wd, c, cout, ks, stride,
                                          padding, _ptr(part), slabs, db.numel(), _ptr(db),
-                                         int(db.dtype == torch.bfloat16), _stream())
+                                         int(db.dtype == torch.bfloat16), pst, _stream())
     else:
         rc = lib.vgpu_conv_wgrad_nhwc(_ptr(dy), _ptr(x), _ptr(dw), _ptr(ws), need, n, h, wd, c, cout,
                                       ks, stride, padding, _stream())
@@ -501,9 +501,9 @@ def conv_backward(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, p:
     elif need_dw and dw is None:
         dw = bw(dy, x, w, *common, [False, True, False])[1]
     if db_job is not None:  # no native weight-gradient reduce to ride along with
-        part, slabs, db = db_job
+        part, slabs, db, pst = db_job
         rc = load_kernels().vgpu_bias_grad_reduce(_ptr(part), slabs, db.numel(), _ptr(db),
-                                                  int(db.dtype == torch.bfloat16), _stream())
+                                                  int(db.dtype == torch.bfloat16), pst, _stream())
         if rc != 0:
             raise RuntimeError(f"vgpu_bias_grad_reduce: error {rc}")
     return dx, dw
@@ -540,21 +540,105 @@ class _ConvBiasReLUTrainFn(torch.autograd.Function):
     VGG-16 training path (vgpu.models.vision.VGG16)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, stride: int, padding: int):
+    def forward(ctx, x, w, b, stride: int, padding: int, in_relu: bool = False):
         y = conv2d(x, w, b, stride=stride, padding=padding, act="relu")
         ctx.save_for_backward(x, w, y)
         ctx.bias_dtype = b.dtype
-        ctx.stride, ctx.padding = stride, padding
+        ctx.stride, ctx.padding, ctx.in_relu = stride, padding, in_relu
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w, y = ctx.saved_tensors
-        g, part, slabs = relu_bias_grad_partial(dy.contiguous(memory_format=_CL), y)
+        link = _RELU_LINK.pop(dy.data_ptr(), None)
+        if link is not None and dy.is_contiguous(memory_format=_CL):
+            # the next layer's data gradient already applied this layer's ReLU mask
+            # and summed its bias-gradient partials (dgrad_into_relu)
+            g, (part, slabs, pst) = dy, link
+        else:
+            g, part, slabs = relu_bias_grad_partial(dy.contiguous(memory_format=_CL), y)
+            pst = 1
         db = torch.empty(y.shape[1], dtype=ctx.bias_dtype, device=y.device) if ctx.needs_input_grad[2] else None
-        dx, dw = conv_backward(g, x, w, ctx.stride, ctx.padding, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
-                               db_job=(part, slabs, db) if db is not None else None)
-        return dx, dw, db, None, None
+        dx, dw = _backward_into(ctx, g, x, w, (part, slabs, db, pst) if db is not None else None)
+        return dx, dw, db, None, None, None
+
+
+# data_ptr of a gradient already masked for its ReLU layer -> (partials, count,
+# stride) of that layer's bias gradient: dgrad_into_relu hands them from one
+# conv + ReLU layer's backward to the previous layer's (VGG16._train_features
+# clears it each forward; an entry nobody pops is just dropped then).
+_RELU_LINK: dict[int, tuple] = {}
+_RELU_COEF: dict[tuple, torch.Tensor] = {}
+
+
+def _relu_coef(c: int, device) -> torch.Tensor:
+    """BN coefficients (s, t, mean, invstd) = (1, 0, 0, 1): the statistics
+    epilogue then masks by x > 0 and sums (Σv, Σv·x)."""
+    key = (c, str(device))
+    t = _RELU_COEF.get(key)
+    if t is None:
+        t = torch.zeros((4, c), dtype=torch.float32, device=device)
+        t[0] = 1.0
+        t[3] = 1.0
+        _RELU_COEF[key] = t
+    return t
+
+
+def dgrad_into_relu(dy: torch.Tensor, w: torch.Tensor, padding: int, mask: torch.Tensor):
+    """Stride-1 data gradient of conv(x, w) masked by [mask > 0] -- the ReLU of
+    the layer that produced x (mask = x) -- plus that layer's bias-gradient
+    partial sums: (g, partials, count, stride) or None when no fused kernel
+    takes the shape.  Split-K shapes mask in the split reduce; the others use
+    the BatchNorm-statistics epilogue with unit coefficients (Σ v per 64 rows)."""
+    ks = w.shape[2]
+    wf = _dgrad_filter(w)
+    n, c, h, wd = dy.shape
+    cout = wf.shape[0]
+    p2 = ks - 1 - padding
+    oh, ow = out_hw(h, wd, ks, 1, p2)
+    if (n, cout, oh, ow) != tuple(mask.shape) or not mask.is_contiguous(memory_format=_CL):
+        return None
+    lib = load_kernels()
+    out = torch.empty((n, cout, oh, ow), dtype=dy.dtype, device=dy.device, memory_format=_CL)
+    need = lib.vgpu_conv2d_workspace(n, h, wd, c, cout, ks, 1, p2, 0)
+    m = n * oh * ow
+    if need > 0 and 256 % (cout // 8) == 0:
+        blocks = (m * (cout // 8) + 255) // 256
+        gpart = torch.empty(blocks * cout, dtype=torch.float32, device=dy.device)
+        ws = torch.empty(need // 4, dtype=torch.float32, device=dy.device)
+        nb = ctypes.c_int(0)
+        rc = lib.vgpu_conv2d_masked_splitk(_ptr(dy), _ptr(wf), _ptr(out), n, h, wd, c, cout, ks, p2, _ptr(mask),
+                                           _ptr(gpart), gpart.numel() * 4, _ptr(ws), need, ctypes.byref(nb),
+                                           _stream())
+        if rc == 0:
+            return out, gpart, nb.value, 1
+        if rc != -1:
+            raise RuntimeError(f"vgpu_conv2d_masked_splitk: error {rc}")
+        return None
+    groups = (m + 63) // 64
+    stats = torch.empty(groups * cout * 2, dtype=torch.float32, device=dy.device)
+    rc = lib.vgpu_conv2d_nhwc_bn(_ptr(dy), _ptr(wf), _ptr(out), None, n, h, wd, c, cout, ks, 1, p2, _ptr(stats),
+                                 _ptr(mask), _ptr(_relu_coef(cout, dy.device)), 1, 1, _stream())
+    if rc == 0:
+        return out, stats, groups, 2
+    if rc != -1:
+        raise RuntimeError(f"vgpu_conv2d_nhwc_bn: error {rc}")
+    return None
+
+
+def _backward_into(ctx, g, x, w, db_job):
+    """dx, dw of a conv + ReLU layer from its masked gradient g.  When the
+    layer's input is itself a ReLU output (ctx.in_relu), dx comes out masked for
+    that layer with its bias partials linked for its backward."""
+    need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+    if need_dx and ctx.in_relu and ctx.stride == 1:
+        fused = dgrad_into_relu(g, w, ctx.padding, x)
+        if fused is not None:
+            dx, part, count, pst = fused
+            _RELU_LINK[dx.data_ptr()] = (part, count, pst)
+            _, dw = conv_backward(g, x, w, 1, ctx.padding, True, need_dw, skip_dx=True, db_job=db_job)
+            return dx, dw
+    return conv_backward(g, x, w, ctx.stride, ctx.padding, need_dx, need_dw, db_job=db_job)
 
 
 def relu_bias_grad_partial(dy: torch.Tensor, y: torch.Tensor, idx: torch.Tensor | None = None,
@@ -610,7 +694,8 @@ class _ConvBiasReLUPoolTrainFn(torch.autograd.Function):
     five conv + ReLU + pool blocks."""
 
     @staticmethod
-    def forward(ctx, x, w, b, stride: int, padding: int, k: int):
+    def forward(ctx, x, w, b, stride: int, padding: int, k: int, in_relu: bool = False):
+        ctx.in_relu = in_relu
         y = conv2d(x, w, b, stride=stride, padding=padding, act="relu")
         n, c, h, wd = y.shape
         oh, ow = h // k, wd // k
@@ -630,12 +715,12 @@ class _ConvBiasReLUPoolTrainFn(torch.autograd.Function):
         dp = dp.contiguous(memory_format=_CL)
         g, part, slabs = relu_bias_grad_partial(dp, y, idx=idx, k=ctx.k)
         db = torch.empty(y.shape[1], dtype=ctx.bias_dtype, device=y.device) if ctx.needs_input_grad[2] else None
-        dx, dw = conv_backward(g, x, w, ctx.stride, ctx.padding, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
-                               db_job=(part, slabs, db) if db is not None else None)
-        return dx, dw, db, None, None, None
+        dx, dw = _backward_into(ctx, g, x, w, (part, slabs, db, 1) if db is not None else None)
+        return dx, dw, db, None, None, None, None
 
 
-def conv_bias_relu_pool_train(x: torch.Tensor, conv: torch.nn.Conv2d, pool: torch.nn.MaxPool2d) -> torch.Tensor:
+def conv_bias_relu_pool_train(x: torch.Tensor, conv: torch.nn.Conv2d, pool: torch.nn.MaxPool2d,
+                              in_relu: bool = False) -> torch.Tensor:
     """pool(relu(conv(x))) with the module semantics; the fused native path for
     a k×k / stride-k unpadded pool after a native-eligible conv, else the
     unfused ops."""
@@ -649,7 +734,7 @@ def conv_bias_relu_pool_train(x: torch.Tensor, conv: torch.nn.Conv2d, pool: torc
           and conv.out_channels % 8 == 0 and conv.out_channels <= 2048 and w.dtype == torch.bfloat16)
     if not ok:
         return maxpool_train(conv_bias_relu_train(x, conv).contiguous(memory_format=_CL), pool)
-    return _ConvBiasReLUPoolTrainFn.apply(x, w, conv.bias, conv.stride[0], conv.padding[0], k)
+    return _ConvBiasReLUPoolTrainFn.apply(x, w, conv.bias, conv.stride[0], conv.padding[0], k, in_relu)
 
 
 def _conv_bias_relu_ok(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
@@ -687,7 +772,7 @@ def pad_channels(x: torch.Tensor, cp: int) -> torch.Tensor:
     return _PadChannelsFn.apply(x, cp)
 
 
-def conv_bias_relu_train(x: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor:
+def conv_bias_relu_train(x: torch.Tensor, conv: torch.nn.Conv2d, in_relu: bool = False) -> torch.Tensor:
     """relu(conv(x)) with the module's semantics (bias included); bf16
     channels_last CUDA tensors of supported shapes run natively, anything else
     through the module."""
@@ -707,7 +792,7 @@ def conv_bias_relu_train(x: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor
         return _ConvBiasReLUTrainFn.apply(xp, wp, conv.bias, 1, 1)
     if not _conv_bias_relu_ok(x, conv):
         return F.relu(conv(x))
-    return _ConvBiasReLUTrainFn.apply(x, w, conv.bias, conv.stride[0], conv.padding[0])
+    return _ConvBiasReLUTrainFn.apply(x, w, conv.bias, conv.stride[0], conv.padding[0], in_relu)
 
 
 # ---- fp32 references -----------------------------------------------------------------
