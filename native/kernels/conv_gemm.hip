@@ -89,6 +89,13 @@ struct ConvArgs {
   // partials, so its separate ReLU-backward pass disappears (VGG-16 training).
   const uint16_t* gmask;
   float* gpart;
+  // ... and when that layer is followed by a k×k / stride-k max pool (this conv's
+  // x is the pool's output): the gradient is scattered through the pool's
+  // argmax bytes pidx [M][Cout] into gfull [N][OH·k][OW·k][Cout], masked by
+  // gmask (the ReLU output, full resolution) -- y is not written.
+  const uint8_t* pidx;
+  uint16_t* gfull;
+  int pk;
 };
 
 // d act / d z as PyTorch defines it (threshold_backward / hardtanh_backward).
@@ -800,15 +807,43 @@ __global__ void __launch_bounds__(kThreads) splitk_reduce_kernel(const ConvArgs 
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = fminf(fmaxf(v[j], 0.0f), hi);
     }
-    if (a.gmask) {
-      float mk[8];
-      unpack8(*reinterpret_cast<const u32x4*>(a.gmask + off), mk);
+    if (a.gfull) {
+      // scatter through the pool: window tap t of pooled pixel m gets v where
+      // the argmax byte says t and the ReLU output there is positive
+      const uint2 tt = *reinterpret_cast<const uint2*>(a.pidx + off);
+      const int ow = m % a.OW, t2 = m / a.OW, oh = t2 % a.OH, n = t2 / a.OH;
+      const int FW = a.OW * a.pk, FH = a.OH * a.pk;
+      float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const u32x4 vb = pack8(v);  // the pool gradient as the unfused path stores it (bf16)
+      float vr[8];
+      unpack8(vb, vr);
+      for (int dh = 0; dh < a.pk; ++dh)
+        for (int dw = 0; dw < a.pk; ++dw) {
+          const uint32_t tap = dh * a.pk + dw;
+          const int64_t fo = (((int64_t)n * FH + oh * a.pk + dh) * FW + ow * a.pk + dw) * a.Cout + col;
+          float mk[8], g[8];
+          unpack8(*reinterpret_cast<const u32x4*>(a.gmask + fo), mk);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = mk[j] > 0.0f ? v[j] : 0.0f;
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t tj = ((j < 4 ? tt.x : tt.y) >> (8 * (j & 3))) & 0xffu;
+            g[j] = (tj == tap && mk[j] > 0.0f) ? vr[j] : 0.0f;
+            sum[j] += g[j];
+          }
+          *reinterpret_cast<u32x4*>(a.gfull + fo) = pack8(g);
+        }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = sum[j];
+    } else {
+      if (a.gmask) {
+        float mk[8];
+        unpack8(*reinterpret_cast<const u32x4*>(a.gmask + off), mk);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = mk[j] > 0.0f ? v[j] : 0.0f;
+      }
+      const u32x4 o = pack8(v);
+      *reinterpret_cast<u32x4*>(a.y + off) = o;
+      unpack8(o, v);  // the partial sums add the stored (rounded) values
     }
-    const u32x4 o = pack8(v);
-    *reinterpret_cast<u32x4*>(a.y + off) = o;
-    unpack8(o, v);  // the partial sums add the stored (rounded) values
   }
   if (!a.gpart) return;  // kernel-uniform
 #pragma unroll
@@ -2501,7 +2536,8 @@ namespace {
 int conv2d_impl(const void* x, const void* w, void* y, const void* res, const float* bias, const float* pscale,
                 const float* pshift, int N, int H, int W, int C, int Cout, int KS, int stride, int pad, int act,
                 float* stats, const void* bnx, const float* bncoef, int bnact, int res_stride, hipStream_t s,
-                float* ws = nullptr, int64_t ws_bytes = 0, const void* gmask = nullptr, float* gpart = nullptr);
+                float* ws = nullptr, int64_t ws_bytes = 0, const void* gmask = nullptr, float* gpart = nullptr,
+                const void* pidx = nullptr, void* gfull = nullptr, int pk = 0);
 
 int g_forced_split = -1;  // vgpu_conv_set_splitk: -1 heuristic, 0 off, n > 1 that many splits when eligible
 
@@ -2581,6 +2617,27 @@ VGPU_API int vgpu_conv2d_masked_splitk(const void* x, const void* w, void* y, in
                      nullptr, 0, 1, s, static_cast<float*>(ws), ws_bytes, gmask, static_cast<float*>(gpart));
 }
 
+// The same for a ReLU layer followed by a k×k / stride-k max pool whose output
+// this conv's x-gradient is: the split reduce scatters through the pool's
+// argmax bytes pidx [N][OH][OW][Cout] into gfull [N][OH·k][OW·k][Cout], masked
+// by gmask (the ReLU output at full resolution), and sums gpart; y is not written.
+VGPU_API int vgpu_conv2d_masked_pool_splitk(const void* x, const void* w, int N, int H, int W, int C, int Cout,
+                                            int KS, int pad, const void* pidx, int pk, const void* gmask, void* gfull,
+                                            void* gpart, int64_t gpart_bytes, void* ws, int64_t ws_bytes,
+                                            int* blocks_out, hipStream_t s) {
+  if (!pidx || !gfull || pk < 1 || pk > 15) return -1;
+  const int64_t OH = H + 2 * pad - KS + 1, OW = W + 2 * pad - KS + 1;
+  if (OH < 1 || OW < 1 || (int64_t)N * OH * pk * OW * pk * Cout * 2 >= ((int64_t)1 << 31)) return -1;
+  if (!gmask || !gpart || !ws || Cout % 8 || kThreads % (Cout / 8) || KS < 1 || pad < 0) return -1;
+  const int64_t M = (int64_t)N * OH * OW;
+  const int64_t blocks = (M * (Cout / 8) + kThreads - 1) / kThreads;
+  if (vgpu_conv2d_workspace(N, H, W, C, Cout, KS, 1, pad, 0) <= 0 || gpart_bytes < blocks * Cout * 4) return -1;
+  if (blocks_out) *blocks_out = (int)blocks;
+  return conv2d_impl(x, w, nullptr, nullptr, nullptr, nullptr, nullptr, N, H, W, C, Cout, KS, 1, pad, 0, nullptr,
+                     nullptr, nullptr, 0, 1, s, static_cast<float*>(ws), ws_bytes, gmask, static_cast<float*>(gpart),
+                     pidx, gfull, pk);
+}
+
 // Training convolution with the BatchNorm statistics of its output from the
 // epilogue (ConvArgs::stats): stats = fp32 pairs [ceil(M / 64)][Cout], M = N·OH·OW.
 //   bnx == nullptr: forward — (Σ y, Σ y²) per 64-row group of the stored y.
@@ -2606,7 +2663,8 @@ namespace {
 int conv2d_impl(const void* x, const void* w, void* y, const void* res, const float* bias, const float* pscale,
                 const float* pshift, int N, int H, int W, int C, int Cout, int KS, int stride, int pad, int act,
                 float* stats, const void* bnx, const float* bncoef, int bnact, int res_stride, hipStream_t s,
-                float* ws, int64_t ws_bytes, const void* gmask, float* gpart) {
+                float* ws, int64_t ws_bytes, const void* gmask, float* gpart, const void* pidx, void* gfull,
+                int pk) {
   const int bias_bf16 = (act >> 8) & 1;
   act &= 0xff;
   if (act > 2) return -1;
@@ -2687,6 +2745,9 @@ int conv2d_impl(const void* x, const void* w, void* y, const void* res, const fl
       c.splits = splits;
       c.gmask = static_cast<const uint16_t*>(gmask);
       c.gpart = gpart;
+      c.pidx = static_cast<const uint8_t*>(pidx);
+      c.gfull = static_cast<uint16_t*>(gfull);
+      c.pk = pk;
       c.nM = (c.M + 63) / 64;
       c.nN = Cout / bn;
       c.nwg = c.nM * c.nN;

@@ -51,19 +51,20 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// ---- forward: one wave per R = 2 output rows, the K loop unrolled by U ------------
-// R = 4 rows per wave share each x load (x is re-read from L2 by every wave),
-// U = 4: 256 B of weight per lane in flight.  In a training step fc1's 205 MB
-// no longer sits in the 256 MB MALL; R = 2 / U = 4 ran at ~3 TB/s (68 us).
-constexpr int kR = 4, kU = 4;
+// ---- forward: a block per R = 4 output rows, its 4 waves splitting K ---------------
+// Each wave streams every 4th 512-column chunk of the R rows (U = 4 chunks'
+// loads in flight), the four partial dot products meet in LDS.  4096 waves for
+// fc1: one wave per SIMD with the whole K each ran the pass at ~3.5 TB/s in a
+// training step, loads and math strictly alternating (68 us for 205 MB).
+constexpr int kR = 4, kU = 4, kFwdWaves = kThreads / 64;
 template <int B>
 __global__ void __launch_bounds__(kThreads) skinny_fwd_kernel(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               const uint16_t* __restrict__ bias,
                                                               uint16_t* __restrict__ y, int N, int K, int act) {
-  const int lane = threadIdx.x & 63;
-  const int n0 = (blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)) * kR;
-  if (n0 >= N) return;
+  __shared__ float part[kFwdWaves][kR * B];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * kR;
   float acc[kR][B];
 #pragma unroll
   for (int r = 0; r < kR; ++r)
@@ -72,11 +73,11 @@ __global__ void __launch_bounds__(kThreads) skinny_fwd_kernel(const uint16_t* __
   const int kv = K >> 3;  // 16-B chunks per row
   const u32x4* W0 = reinterpret_cast<const u32x4*>(w + (int64_t)n0 * K);
   const u32x4* X = reinterpret_cast<const u32x4*>(x);
-  for (int c0 = lane; c0 < kv; c0 += 64 * kU) {
+  for (int c0 = wave * 64 + lane; c0 < kv; c0 += 64 * kFwdWaves * kU) {
     u32x4 wv[kU][kR], xv[kU][B];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const int c = c0 + 64 * u;
+      const int c = c0 + 64 * kFwdWaves * u;
       if (c < kv) {
 #pragma unroll
         for (int r = 0; r < kR; ++r) wv[u][r] = W0[(int64_t)r * kv + c];
@@ -86,7 +87,7 @@ __global__ void __launch_bounds__(kThreads) skinny_fwd_kernel(const uint16_t* __
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      if (c0 + 64 * u >= kv) continue;
+      if (c0 + 64 * kFwdWaves * u >= kv) continue;
       float xf[B][8];
 #pragma unroll
       for (int b = 0; b < B; ++b) unpack8(xv[u][b], xf[b]);
@@ -104,15 +105,16 @@ __global__ void __launch_bounds__(kThreads) skinny_fwd_kernel(const uint16_t* __
 #pragma unroll
   for (int r = 0; r < kR; ++r)
 #pragma unroll
-    for (int b = 0; b < B; ++b) acc[r][b] = wave_sum(acc[r][b]);
-  if (lane < kR * B) {  // lane (r, b) stores one output
-    const int r = lane / B, b = lane % B;
+    for (int b = 0; b < B; ++b) {
+      const float v = wave_sum(acc[r][b]);
+      if (lane == 0) part[wave][r * B + b] = v;
+    }
+  __syncthreads();
+  if (threadIdx.x < kR * B && n0 + (int)threadIdx.x / B < N) {  // thread (r, b) stores one output
+    const int r = threadIdx.x / B, b = threadIdx.x % B;
     float v = 0.0f;
 #pragma unroll
-    for (int rr = 0; rr < kR; ++rr)
-#pragma unroll
-      for (int bb = 0; bb < B; ++bb)
-        if (rr == r && bb == b) v = acc[rr][bb];
+    for (int q = 0; q < kFwdWaves; ++q) v += part[q][threadIdx.x];  // fixed order
     if (bias) v += bf2f(bias[n0 + r]);
     y[(int64_t)b * N + n0 + r] = f2bf(act_f(act, v));
   }
@@ -318,7 +320,7 @@ VGPU_API int vgpu_skinny_supported(int B, int N, int K) {
 VGPU_API int vgpu_skinny_fwd(const void* x, const void* w, const void* bias, void* y, int B, int N, int K, int act,
                              hipStream_t s) {
   if (!vgpu_skinny_supported(B, N, K) || !al16(x) || !al16(w) || act < 0 || act > 2) return -1;
-  const dim3 grid((N / kR + 3) / 4);
+  const dim3 grid(N / kR);
   VGPU_SKINNY_SWITCH(B, skinny_fwd_kernel, grid, (const uint16_t*)x, (const uint16_t*)w, (const uint16_t*)bias,
                      (uint16_t*)y, N, K, act)
   return (int)hipGetLastError();

@@ -351,3 +351,36 @@ def test_relu_mask_in_next_dgrad_matches_unfused(gpu_build, case):
     (gx0, gw10, gb10, gw20), (gx1, gw11, gb11, gw21) = grads
     assert torch.equal(gx0, gx1) and torch.equal(gw10, gw11) and torch.equal(gw20, gw21)
     torch.testing.assert_close(gb11.float(), gb10.float(), atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("case", [(2, 256, 512, 28), (2, 128, 256, 56)])
+def test_pool_backward_in_next_dgrad_matches_unfused(gpu_build, case):
+    """A conv + ReLU + 2x2 pool block feeding a conv whose data gradient runs
+    split-K: with in_relu=2 that split reduce scatters through the pool's
+    argmax, applies the block's ReLU mask and sums its bias partials
+    (dgrad_into_pool); the block's own pooled ReLU pass is skipped.  Same
+    gradients as the unfused path (bias sums regrouped)."""
+    from vgpu.ops import conv as C
+    n, c1, c2, hw = case
+    torch.manual_seed(c1 + hw)
+    l1 = torch.nn.Conv2d(c1, c2, 3, padding=1).cuda().to(torch.bfloat16).to(memory_format=CL)
+    l2 = torch.nn.Conv2d(c2, c2, 3, padding=1).cuda().to(torch.bfloat16).to(memory_format=CL)
+    pool = torch.nn.MaxPool2d(2, 2)
+    x0 = _x((n, c1, hw, hw), 9)
+    dy = _x((n, c2, hw // 2, hw // 2), 10)
+    grads = []
+    for mode in (0, 2):
+        for mod in (l1, l2):
+            mod.weight.grad = mod.bias.grad = None
+        x = x0.clone().requires_grad_()
+        C._RELU_LINK.clear()
+        C._POOL_SRC.clear()
+        h = C.conv_bias_relu_pool_train(x, l1, pool)
+        y = C.conv_bias_relu_train(h, l2, in_relu=mode)
+        y.backward(dy)
+        if mode == 2:
+            assert not C._RELU_LINK, "the pool block's backward should have taken the link"
+        grads.append([x.grad.clone(), l1.weight.grad.clone(), l1.bias.grad.clone(), l2.weight.grad.clone()])
+    (gx0, gw10, gb10, gw20), (gx1, gw11, gb11, gw21) = grads
+    assert torch.equal(gx0, gx1) and torch.equal(gw10, gw11) and torch.equal(gw20, gw21)
+    torch.testing.assert_close(gb11.float(), gb10.float(), atol=2e-2, rtol=1e-2)

@@ -70,10 +70,15 @@ class VGG16(nn.Module):
             self._dgrad.refresh()
         from vgpu.ops import conv as C
         C._RELU_LINK.clear()
+        C._POOL_SRC.clear()
         x = x.contiguous(memory_format=torch.channels_last)
         mods = list(self.features)
         i = 0
-        in_relu = False  # x is the output of the previous conv + ReLU (no pool between)
+        # what x is for the next conv: 0 anything, 1 the previous conv + ReLU's
+        # output, 2 a fused conv + ReLU + pool block's output (each feeds only
+        # the next conv here); the next conv's data gradient then does that
+        # layer's ReLU (and pool) backward
+        in_relu = 0
         while i < len(mods):
             m = mods[i]
             if isinstance(m, nn.Conv2d) and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU):
@@ -81,16 +86,15 @@ class VGG16(nn.Module):
                     # conv + ReLU + pool: the pool backward fused into the ReLU / bias gradient
                     x = conv_bias_relu_pool_train(x, m, mods[i + 2], in_relu=in_relu)
                     i += 3
-                    in_relu = False
+                    in_relu = 2
                     continue
-                # the data gradient of the next conv applies this layer's ReLU mask
                 x = conv_bias_relu_train(x, m, in_relu=in_relu).contiguous(memory_format=torch.channels_last)
                 i += 2
-                in_relu = True
+                in_relu = 1
                 continue
             x = maxpool_train(x, m) if isinstance(m, nn.MaxPool2d) else m(x)
             i += 1
-            in_relu = False
+            in_relu = 0
         return x
 
 

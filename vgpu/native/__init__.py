@@ -73,6 +73,10 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_conv2d_masked_splitk.argtypes = [vp] * 3 + [ctypes.c_int] * 7 + [vp, vp, ctypes.c_int64, vp,
                                                                             ctypes.c_int64, vp, vp]
     lib.vgpu_conv2d_masked_splitk.restype = ctypes.c_int
+    lib.vgpu_conv2d_masked_pool_splitk.argtypes = [vp, vp] + [ctypes.c_int] * 7 + [vp, ctypes.c_int, vp, vp, vp,
+                                                                                  ctypes.c_int64, vp, ctypes.c_int64,
+                                                                                  vp, vp]
+    lib.vgpu_conv2d_masked_pool_splitk.restype = ctypes.c_int
     lib.vgpu_bias_grad_reduce.restype = ctypes.c_int
     lib.vgpu_pad_channels.argtypes = [vp, vp, u64, u32, u32, vp]
     lib.vgpu_pad_channels.restype = ctypes.c_int

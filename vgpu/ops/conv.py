@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -551,10 +552,10 @@ class _ConvBiasReLUTrainFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, w, y = ctx.saved_tensors
         link = _RELU_LINK.pop(dy.data_ptr(), None)
-        if link is not None and dy.is_contiguous(memory_format=_CL):
+        if link is not None and link[0] == "mask" and dy.is_contiguous(memory_format=_CL):
             # the next layer's data gradient already applied this layer's ReLU mask
             # and summed its bias-gradient partials (dgrad_into_relu)
-            g, (part, slabs, pst) = dy, link
+            g, (_, part, slabs, pst) = dy, link
         else:
             g, part, slabs = relu_bias_grad_partial(dy.contiguous(memory_format=_CL), y)
             pst = 1
@@ -569,6 +570,43 @@ class _ConvBiasReLUTrainFn(torch.autograd.Function):
 # clears it each forward; an entry nobody pops is just dropped then).
 _RELU_LINK: dict[int, tuple] = {}
 _RELU_COEF: dict[tuple, torch.Tensor] = {}
+# data_ptr of a fused conv + ReLU + pool block's output -> (argmax, ReLU output,
+# k, weakref to that output).  Used only for a consumer told (in_relu == 2) that
+# the block's output feeds it alone: its x-gradient is then never formed.
+_POOL_SRC: dict[int, tuple] = {}
+
+
+def dgrad_into_pool(dy: torch.Tensor, w: torch.Tensor, padding: int, idx: torch.Tensor, yfull: torch.Tensor, k: int):
+    """Stride-1 data gradient of conv(x, w) where x = maxpool_k(yfull) and yfull
+    a ReLU output: scattered through the pool's argmax into yfull's resolution,
+    masked by yfull > 0, with the bias partials of yfull's layer -- (g_full,
+    partials, count) -- or None unless the conv runs split-K."""
+    ks = w.shape[2]
+    wf = _dgrad_filter(w)
+    n, c, h, wd = dy.shape
+    cout = wf.shape[0]
+    p2 = ks - 1 - padding
+    oh, ow = out_hw(h, wd, ks, 1, p2)
+    if (tuple(idx.shape) != (n, oh, ow, cout) or tuple(yfull.shape) != (n, cout, oh * k, ow * k)
+            or not yfull.is_contiguous(memory_format=_CL) or 256 % (cout // 8)):
+        return None
+    lib = load_kernels()
+    need = lib.vgpu_conv2d_workspace(n, h, wd, c, cout, ks, 1, p2, 0)
+    if need <= 0:
+        return None
+    blocks = (n * oh * ow * (cout // 8) + 255) // 256
+    gpart = torch.empty(blocks * cout, dtype=torch.float32, device=dy.device)
+    ws = torch.empty(need // 4, dtype=torch.float32, device=dy.device)
+    g = torch.empty_like(yfull, memory_format=_CL)
+    nb = ctypes.c_int(0)
+    rc = lib.vgpu_conv2d_masked_pool_splitk(_ptr(dy), _ptr(wf), n, h, wd, c, cout, ks, p2, _ptr(idx), k, _ptr(yfull),
+                                            _ptr(g), _ptr(gpart), gpart.numel() * 4, _ptr(ws), need,
+                                            ctypes.byref(nb), _stream())
+    if rc == -1:
+        return None
+    if rc != 0:
+        raise RuntimeError(f"vgpu_conv2d_masked_pool_splitk: error {rc}")
+    return g, gpart, nb.value
 
 
 def _relu_coef(c: int, device) -> torch.Tensor:
@@ -631,11 +669,22 @@ def _backward_into(ctx, g, x, w, db_job):
     layer's input is itself a ReLU output (ctx.in_relu), dx comes out masked for
     that layer with its bias partials linked for its backward."""
     need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
-    if need_dx and ctx.in_relu and ctx.stride == 1:
+    if need_dx and ctx.in_relu == 1 and ctx.stride == 1:
         fused = dgrad_into_relu(g, w, ctx.padding, x)
         if fused is not None:
             dx, part, count, pst = fused
-            _RELU_LINK[dx.data_ptr()] = (part, count, pst)
+            _RELU_LINK[dx.data_ptr()] = ("mask", part, count, pst)
+            _, dw = conv_backward(g, x, w, 1, ctx.padding, True, need_dw, skip_dx=True, db_job=db_job)
+            return dx, dw
+    src = _POOL_SRC.get(x.data_ptr()) if need_dx and ctx.in_relu == 2 and ctx.stride == 1 else None
+    if src is not None and src[3]() is not None and src[3]().data_ptr() == x.data_ptr():
+        fused = dgrad_into_pool(g, w, ctx.padding, *src[:3])
+        if fused is not None:
+            gfull, part, count = fused
+            # x's gradient proper is never formed: the pool block's backward takes
+            # gfull through the link (x feeds this conv only)
+            dx = torch.empty_like(x, memory_format=_CL)
+            _RELU_LINK[dx.data_ptr()] = ("pool", gfull, part, count)
             _, dw = conv_backward(g, x, w, 1, ctx.padding, True, need_dw, skip_dx=True, db_job=db_job)
             return dx, dw
     return conv_backward(g, x, w, ctx.stride, ctx.padding, need_dx, need_dw, db_job=db_job)
@@ -707,20 +756,28 @@ class _ConvBiasReLUPoolTrainFn(torch.autograd.Function):
         ctx.save_for_backward(x, w, y, idx)
         ctx.mark_non_differentiable(idx)
         ctx.stride, ctx.padding, ctx.k, ctx.bias_dtype = stride, padding, k, b.dtype
+        _POOL_SRC[p.data_ptr()] = (idx, y, k, weakref.ref(p))  # for the next conv's fused data gradient
         return p
 
     @staticmethod
     def backward(ctx, dp):
         x, w, y, idx = ctx.saved_tensors
-        dp = dp.contiguous(memory_format=_CL)
-        g, part, slabs = relu_bias_grad_partial(dp, y, idx=idx, k=ctx.k)
+        link = _RELU_LINK.pop(dp.data_ptr(), None)
+        if link is not None and link[0] == "pool":
+            # the next conv's split data gradient scattered through this pool,
+            # masked by this ReLU and summed the bias partials (dgrad_into_pool);
+            # dp itself was never written
+            _, g, part, slabs = link
+        else:
+            dp = dp.contiguous(memory_format=_CL)
+            g, part, slabs = relu_bias_grad_partial(dp, y, idx=idx, k=ctx.k)
         db = torch.empty(y.shape[1], dtype=ctx.bias_dtype, device=y.device) if ctx.needs_input_grad[2] else None
         dx, dw = _backward_into(ctx, g, x, w, (part, slabs, db, 1) if db is not None else None)
         return dx, dw, db, None, None, None, None
 
 
 def conv_bias_relu_pool_train(x: torch.Tensor, conv: torch.nn.Conv2d, pool: torch.nn.MaxPool2d,
-                              in_relu: bool = False) -> torch.Tensor:
+                              in_relu: int = 0) -> torch.Tensor:
     """pool(relu(conv(x))) with the module semantics; the fused native path for
     a k×k / stride-k unpadded pool after a native-eligible conv, else the
     unfused ops."""
@@ -772,10 +829,13 @@ def pad_channels(x: torch.Tensor, cp: int) -> torch.Tensor:
     return _PadChannelsFn.apply(x, cp)
 
 
-def conv_bias_relu_train(x: torch.Tensor, conv: torch.nn.Conv2d, in_relu: bool = False) -> torch.Tensor:
+def conv_bias_relu_train(x: torch.Tensor, conv: torch.nn.Conv2d, in_relu: int = 0) -> torch.Tensor:
     """relu(conv(x)) with the module's semantics (bias included); bf16
     channels_last CUDA tensors of supported shapes run natively, anything else
-    through the module."""
+    through the module.  in_relu: 1 when x is the previous conv + ReLU's output
+    and feeds only this conv, 2 when x is a fused conv + ReLU + pool block's
+    output and feeds only this conv -- the data gradient then does that layer's
+    ReLU (and pool) backward (dgrad_into_relu / dgrad_into_pool)."""
     w = conv.weight
     c = conv.in_channels
     if (0 < c < 64 and conv.out_channels % 64 == 0 and _TRAIN_NATIVE and conv.bias is not None and x.is_cuda
