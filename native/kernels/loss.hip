@@ -64,6 +64,34 @@ __global__ void __launch_bounds__(kThreads) xent_kernel(const T* __restrict__ x,
   }
 }
 
+// Up to 64 rows: one block does every row and the mean (one launch in all).
+template <typename T>
+__global__ void __launch_bounds__(kThreads) xent_small_kernel(const T* __restrict__ x, const int64_t* __restrict__ tgt,
+                                                              float* __restrict__ loss_rows, float* __restrict__ loss,
+                                                              T* __restrict__ dx, int rows, int C, float scale) {
+  __shared__ float sh[kThreads / 64];
+  float total = 0.0f;
+  for (int row = 0; row < rows; ++row) {
+    const T* xr = x + (int64_t)row * C;
+    float m = -INFINITY;
+    for (int c = threadIdx.x; c < C; c += kThreads) m = fmaxf(m, ld(xr, c));
+    m = block_reduce<T>(m, sh, true);
+    float s = 0.0f;
+    for (int c = threadIdx.x; c < C; c += kThreads) s += __expf(ld(xr, c) - m);
+    s = block_reduce<T>(s, sh, false);
+    const int64_t t = tgt[row];
+    const float lse = m + __logf(s), inv = 1.0f / s;
+    const float l = (t >= 0 && t < C) ? lse - ld(xr, t) : 0.0f;
+    total += l;
+    if (threadIdx.x == 0) loss_rows[row] = l;
+    for (int c = threadIdx.x; c < C; c += kThreads) {
+      const float p = __expf(ld(xr, c) - m) * inv;
+      st(dx, (int64_t)row * C + c, (p - (c == t ? 1.0f : 0.0f)) * scale);
+    }
+  }
+  if (threadIdx.x == 0) loss[0] = total / (float)rows;  // rows summed in order
+}
+
 // mean of the row losses in a fixed order (one block)
 __global__ void __launch_bounds__(kThreads) mean_kernel(const float* __restrict__ v, float* __restrict__ out,
                                                         int n) {
@@ -83,6 +111,15 @@ VGPU_API int vgpu_cross_entropy_fwd_bwd(const void* logits, const int64_t* tgt, 
                                         void* dlogits, int rows, int C, int is_bf16, hipStream_t s) {
   if (rows < 1 || C < 1) return -1;
   const float scale = 1.0f / (float)rows;
+  if (rows <= 64) {
+    if (is_bf16)
+      hipLaunchKernelGGL(xent_small_kernel<uint16_t>, dim3(1), dim3(kThreads), 0, s, (const uint16_t*)logits, tgt,
+                         loss_rows, loss, (uint16_t*)dlogits, rows, C, scale);
+    else
+      hipLaunchKernelGGL(xent_small_kernel<float>, dim3(1), dim3(kThreads), 0, s, (const float*)logits, tgt,
+                         loss_rows, loss, (float*)dlogits, rows, C, scale);
+    return (int)hipGetLastError();
+  }
   if (is_bf16)
     hipLaunchKernelGGL(xent_kernel<uint16_t>, dim3(rows), dim3(kThreads), 0, s, (const uint16_t*)logits, tgt,
                        loss_rows, (uint16_t*)dlogits, C, scale);

@@ -62,7 +62,7 @@ def test_sgd_native_bf16_matches_torch_fused(gpu_build, kw):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("rows,c", [(2, 1000), (50, 1000), (7, 2), (3, 4097)])
+@pytest.mark.parametrize("rows,c", [(2, 1000), (50, 1000), (7, 2), (3, 4097), (100, 1000)])
 def test_cross_entropy_matches_torch(gpu_build, dtype, rows, c):
     """vgpu.ops.loss.cross_entropy (native/kernels/loss.hip): the mean loss and
     dlogits against F.cross_entropy on the fp32 logits."""
