@@ -384,3 +384,25 @@ def test_pool_backward_in_next_dgrad_matches_unfused(gpu_build, case):
     (gx0, gw10, gb10, gw20), (gx1, gw11, gb11, gw21) = grads
     assert torch.equal(gx0, gx1) and torch.equal(gw10, gw11) and torch.equal(gw20, gw21)
     torch.testing.assert_close(gb11.float(), gb10.float(), atol=2e-2, rtol=1e-2)
+
+
+def test_pool_block_nchw_output_matches(gpu_build):
+    """The last conv + ReLU + pool block writes NCHW (a following flatten is a
+    view) and reads its gradient in that layout: same values and gradients as
+    the channels_last block."""
+    from vgpu.ops import conv as C
+    torch.manual_seed(3)
+    conv = torch.nn.Conv2d(512, 512, 3, padding=1).cuda().to(torch.bfloat16).to(memory_format=CL)
+    pool = torch.nn.MaxPool2d(2, 2)
+    x0 = _x((2, 512, 14, 14), 13)
+    dy = torch.randn(2, 512 * 49, generator=torch.Generator().manual_seed(14)).to(torch.bfloat16).cuda()
+    res = []
+    for nchw in (False, True):
+        conv.weight.grad = conv.bias.grad = None
+        x = x0.clone().requires_grad_()
+        y = C.conv_bias_relu_pool_train(x, conv, pool, out_nchw=nchw)
+        assert y.is_contiguous() == nchw
+        torch.flatten(y, 1).backward(dy)
+        res.append([y.contiguous(), x.grad.clone(), conv.weight.grad.clone(), conv.bias.grad.clone()])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
