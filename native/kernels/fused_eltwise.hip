@@ -197,6 +197,7 @@ struct PoolGeo {
   const bf16x8* dyp;
   const uint2* idx;
   int H, W, OH, OW, k;
+  int nchw;  // dyp is [N][C][OH][OW] (the gradient of an NCHW-written pool output)
 };
 
 template <bool POOL>
@@ -226,7 +227,15 @@ __global__ void __launch_bounds__(kThreads) relu_bias_grad_kernel(const bf16x8* 
           tap[k] = 0xffu;  // rows past the last full window receive no gradient
           if (oh < (uint32_t)pg.OH && ow < (uint32_t)pg.OW) {
             const uint64_t o = (uint64_t)((n * (uint32_t)pg.OH + oh) * (uint32_t)pg.OW + ow) * cv + cg;
-            a[k] = pg.dyp[o];
+            if (pg.nchw) {
+              const uint16_t* d = reinterpret_cast<const uint16_t*>(pg.dyp);
+              const uint64_t hw = (uint64_t)pg.OH * pg.OW;
+              const uint64_t base = ((uint64_t)n * cv * 8 + cg * 8) * hw + (uint64_t)oh * pg.OW + ow;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) a[k].v[j] = d[base + j * hw];
+            } else {
+              a[k] = pg.dyp[o];
+            }
             const uint2 t = pg.idx[o];
             tap[k] = (ih - oh * pg.k) * pg.k + (iw - ow * pg.k);
             // per channel j: keep dy where the window's argmax is this row
@@ -355,6 +364,10 @@ VGPU_API int vgpu_pool_relu_bias_grad_nhwc(const void* dyp, const void* idx, con
   return (int)hipGetLastError();
 }
 
+VGPU_API int vgpu_relu_bias_grad_partial2(const void* dy, const void* idx, const void* y, void* g, void* ws, int N,
+                                          int H, int W, uint32_t c, int k, int dy_nchw, int* slabs_out,
+                                          hipStream_t stream);
+
 // Partials only (no reduce launch): ws receives [slabs][c] fp32 and *slabs_out
 // their count; the bias gradient is summed by vgpu_conv_wgrad_db_nhwc's reduce
 // launch (or vgpu_bias_grad_reduce).  pooled: dy is [N][H/k][W/k][c] with its
@@ -362,6 +375,13 @@ VGPU_API int vgpu_pool_relu_bias_grad_nhwc(const void* dyp, const void* idx, con
 VGPU_API int vgpu_relu_bias_grad_partial_nhwc(const void* dy, const void* idx, const void* y, void* g, void* ws,
                                               int N, int H, int W, uint32_t c, int k, int* slabs_out,
                                               hipStream_t stream) {
+  return vgpu_relu_bias_grad_partial2(dy, idx, y, g, ws, N, H, W, c, k, 0, slabs_out, stream);
+}
+
+// k > 0 and dy_nchw: the pooled gradient is NCHW-contiguous (a flatten's).
+VGPU_API int vgpu_relu_bias_grad_partial2(const void* dy, const void* idx, const void* y, void* g, void* ws, int N,
+                                          int H, int W, uint32_t c, int k, int dy_nchw, int* slabs_out,
+                                          hipStream_t stream) {
   if (c % 8 || c / 8 > kThreads || N < 1 || H < 1 || W < 1 || k < 0 || k > 15 || (k && (H < k || W < k)))
     return -1;
   if ((uint64_t)N * H * W >= (1ull << 31)) return -1;
@@ -369,7 +389,7 @@ VGPU_API int vgpu_relu_bias_grad_partial_nhwc(const void* dy, const void* idx, c
   const uint64_t rows = (uint64_t)N * H * W;
   const uint32_t slabs = rbg_slabs(rows, cv);
   if (k) {
-    const PoolGeo pg{(const bf16x8*)dy, (const uint2*)idx, H, W, H / k, W / k, k};
+    const PoolGeo pg{(const bf16x8*)dy, (const uint2*)idx, H, W, H / k, W / k, k, dy_nchw};
     hipLaunchKernelGGL(relu_bias_grad_kernel<true>, dim3(slabs), dim3(kThreads), 0, stream, nullptr,
                        (const bf16x8*)y, (bf16x8*)g, (float*)ws, rows, cv, pg);
   } else {

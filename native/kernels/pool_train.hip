@@ -35,11 +35,13 @@ __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
 }
 
 // One thread per (output pixel, 8 channels); grid-stride over N·OH·OW·C/8.
+// nchw: y is written [N][C][OH][OW] (the layout a following flatten reads
+// without a copy; idx stays NHWC).
 __global__ void __launch_bounds__(kThreads) maxpool_fwd_idx_kernel(const u32x4* __restrict__ x,
                                                                    u32x4* __restrict__ y,
                                                                    u32x2* __restrict__ idx, int H, int W,
                                                                    int cv, int OH, int OW, int k, int stride,
-                                                                   int pad, int64_t total) {
+                                                                   int pad, int64_t total, int nchw) {
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * kThreads) {
     const int c = (int)(i % cv);
@@ -74,7 +76,17 @@ __global__ void __launch_bounds__(kThreads) maxpool_fwd_idx_kernel(const u32x4* 
           }
       }
     }
-    y[i] = u32x4{pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7])};
+    if (nchw) {
+      uint16_t* yh = reinterpret_cast<uint16_t*>(y);
+      const int64_t hw = (int64_t)OH * OW, base = ((int64_t)n * cv * 8 + c * 8) * hw + (int64_t)oh * OW + ow;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        __bf16 b = (__bf16)m[j];
+        yh[base + j * hw] = __builtin_bit_cast(uint16_t, b);
+      }
+    } else {
+      y[i] = u32x4{pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7])};
+    }
     idx[i] = u32x2{t8[0] | t8[1] << 8 | t8[2] << 16 | t8[3] << 24, t8[4] | t8[5] << 8 | t8[6] << 16 | t8[7] << 24};
   }
 }
@@ -144,7 +156,20 @@ VGPU_API int vgpu_maxpool_fwd_idx_nhwc(const void* x, void* y, void* idx, int N,
   const int64_t total = (int64_t)N * OH * OW * cv;
   hipLaunchKernelGGL(maxpool_fwd_idx_kernel, dim3(grid_for(total)), dim3(kThreads), 0, s,
                      static_cast<const u32x4*>(x), static_cast<u32x4*>(y), static_cast<u32x2*>(idx), H, W, cv, OH,
-                     OW, k, stride, pad, total);
+                     OW, k, stride, pad, total, 0);
+  return (int)hipGetLastError();
+}
+
+// The same with y written NCHW-contiguous (x and idx stay NHWC).
+VGPU_API int vgpu_maxpool_fwd_idx_nchw_out(const void* x, void* y, void* idx, int N, int H, int W, int C, int k,
+                                           int stride, int pad, hipStream_t s) {
+  int OH, OW;
+  if (!shape_ok(N, H, W, C, k, stride, pad, OH, OW)) return -1;
+  const int cv = C / 8;
+  const int64_t total = (int64_t)N * OH * OW * cv;
+  hipLaunchKernelGGL(maxpool_fwd_idx_kernel, dim3(grid_for(total)), dim3(kThreads), 0, s,
+                     static_cast<const u32x4*>(x), static_cast<u32x4*>(y), static_cast<u32x2*>(idx), H, W, cv, OH,
+                     OW, k, stride, pad, total, 1);
   return (int)hipGetLastError();
 }
 

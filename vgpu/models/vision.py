@@ -84,7 +84,8 @@ class VGG16(nn.Module):
             if isinstance(m, nn.Conv2d) and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU):
                 if i + 2 < len(mods) and isinstance(mods[i + 2], nn.MaxPool2d):
                     # conv + ReLU + pool: the pool backward fused into the ReLU / bias gradient
-                    x = conv_bias_relu_pool_train(x, m, mods[i + 2], in_relu=in_relu)
+                    # the last block writes NCHW: the classifier's flatten is then a view
+                    x = conv_bias_relu_pool_train(x, m, mods[i + 2], in_relu=in_relu, out_nchw=i + 3 == len(mods))
                     i += 3
                     in_relu = 2
                     continue

@@ -110,6 +110,10 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_bn_set_fuse_small.argtypes = [ci]
     lib.vgpu_maxpool_fwd_idx_nhwc.argtypes = [vp, vp, vp] + [ci] * 7 + [vp]
     lib.vgpu_maxpool_fwd_idx_nhwc.restype = ci
+    lib.vgpu_maxpool_fwd_idx_nchw_out.argtypes = [vp, vp, vp] + [ci] * 7 + [vp]
+    lib.vgpu_maxpool_fwd_idx_nchw_out.restype = ci
+    lib.vgpu_relu_bias_grad_partial2.argtypes = [vp] * 5 + [ci] * 3 + [u32, ci, ci, vp, vp]
+    lib.vgpu_relu_bias_grad_partial2.restype = ci
     lib.vgpu_maxpool_bwd_nhwc.argtypes = [vp, vp, vp] + [ci] * 7 + [vp]
     lib.vgpu_maxpool_bwd_nhwc.restype = ci
     # BatchNorm statistics from the conv epilogue (vgpu.ops.bnconv)

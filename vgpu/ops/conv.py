@@ -691,12 +691,16 @@ def _backward_into(ctx, g, x, w, db_job):
 
 
 def relu_bias_grad_partial(dy: torch.Tensor, y: torch.Tensor, idx: torch.Tensor | None = None,
-                           k: int = 0) -> tuple[torch.Tensor, torch.Tensor, int]:
+                           k: int = 0, dy_nchw: bool = False) -> tuple[torch.Tensor, torch.Tensor, int]:
     """(g, partials, slabs): g = dy·[y > 0] (dy arriving through a k×k / stride-k
     max pool with argmax idx when k > 0) and the per-slab column sums of g, fp32
     [slabs, C] -- the bias gradient is summed by the weight gradient's reduce
-    launch (conv_backward's db_job)."""
-    _nhwc(dy, "dy")
+    launch (conv_backward's db_job).  dy_nchw: the pooled dy is NCHW-contiguous."""
+    if dy_nchw:
+        if not (k > 0 and dy.is_cuda and dy.dtype == torch.bfloat16 and dy.is_contiguous()):
+            raise ValueError("dy_nchw needs a pooled, contiguous bf16 dy")
+    else:
+        _nhwc(dy, "dy")
     _nhwc(y, "y")
     n, c, h, w = y.shape
     lib = load_kernels()
@@ -706,10 +710,10 @@ def relu_bias_grad_partial(dy: torch.Tensor, y: torch.Tensor, idx: torch.Tensor 
         raise ValueError("unsupported relu_bias_grad shape")
     part = torch.empty(max(need // 4, 1), dtype=torch.float32, device=y.device)
     slabs = ctypes.c_int(0)
-    rc = lib.vgpu_relu_bias_grad_partial_nhwc(_ptr(dy), _ptr(idx), _ptr(y), _ptr(g), _ptr(part), n, h, w, c, k,
-                                              ctypes.byref(slabs), _stream())
+    rc = lib.vgpu_relu_bias_grad_partial2(_ptr(dy), _ptr(idx), _ptr(y), _ptr(g), _ptr(part), n, h, w, c, k,
+                                          int(dy_nchw), ctypes.byref(slabs), _stream())
     if rc != 0:
-        raise RuntimeError(f"vgpu_relu_bias_grad_partial_nhwc: error {rc}")
+        raise RuntimeError(f"vgpu_relu_bias_grad_partial2: error {rc}")
     return g, part, slabs.value
 
 
@@ -743,16 +747,21 @@ class _ConvBiasReLUPoolTrainFn(torch.autograd.Function):
     five conv + ReLU + pool blocks."""
 
     @staticmethod
-    def forward(ctx, x, w, b, stride: int, padding: int, k: int, in_relu: bool = False):
-        ctx.in_relu = in_relu
+    def forward(ctx, x, w, b, stride: int, padding: int, k: int, in_relu: bool = False, out_nchw: bool = False):
+        ctx.in_relu, ctx.out_nchw = in_relu, out_nchw
         y = conv2d(x, w, b, stride=stride, padding=padding, act="relu")
         n, c, h, wd = y.shape
         oh, ow = h // k, wd // k
-        p = torch.empty((n, c, oh, ow), dtype=y.dtype, device=y.device, memory_format=_CL)
         idx = torch.empty((n, oh, ow, c), dtype=torch.uint8, device=y.device)
-        rc = load_kernels().vgpu_maxpool_fwd_idx_nhwc(_ptr(y), _ptr(p), _ptr(idx), n, h, wd, c, k, k, 0, _stream())
+        if out_nchw:  # a flatten follows: NCHW output makes it a view, no copy either way
+            p = torch.empty((n, c, oh, ow), dtype=y.dtype, device=y.device)
+            fn = load_kernels().vgpu_maxpool_fwd_idx_nchw_out
+        else:
+            p = torch.empty((n, c, oh, ow), dtype=y.dtype, device=y.device, memory_format=_CL)
+            fn = load_kernels().vgpu_maxpool_fwd_idx_nhwc
+        rc = fn(_ptr(y), _ptr(p), _ptr(idx), n, h, wd, c, k, k, 0, _stream())
         if rc != 0:
-            raise RuntimeError(f"vgpu_maxpool_fwd_idx_nhwc: error {rc}")
+            raise RuntimeError(f"maxpool forward: error {rc}")
         ctx.save_for_backward(x, w, y, idx)
         ctx.mark_non_differentiable(idx)
         ctx.stride, ctx.padding, ctx.k, ctx.bias_dtype = stride, padding, k, b.dtype
@@ -768,16 +777,18 @@ class _ConvBiasReLUPoolTrainFn(torch.autograd.Function):
             # masked by this ReLU and summed the bias partials (dgrad_into_pool);
             # dp itself was never written
             _, g, part, slabs = link
+        elif ctx.out_nchw:
+            g, part, slabs = relu_bias_grad_partial(dp.contiguous(), y, idx=idx, k=ctx.k, dy_nchw=True)
         else:
             dp = dp.contiguous(memory_format=_CL)
             g, part, slabs = relu_bias_grad_partial(dp, y, idx=idx, k=ctx.k)
         db = torch.empty(y.shape[1], dtype=ctx.bias_dtype, device=y.device) if ctx.needs_input_grad[2] else None
         dx, dw = _backward_into(ctx, g, x, w, (part, slabs, db, 1) if db is not None else None)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
 def conv_bias_relu_pool_train(x: torch.Tensor, conv: torch.nn.Conv2d, pool: torch.nn.MaxPool2d,
-                              in_relu: int = 0) -> torch.Tensor:
+                              in_relu: int = 0, out_nchw: bool = False) -> torch.Tensor:
     """pool(relu(conv(x))) with the module semantics; the fused native path for
     a k×k / stride-k unpadded pool after a native-eligible conv, else the
     unfused ops."""
@@ -791,7 +802,7 @@ def conv_bias_relu_pool_train(x: torch.Tensor, conv: torch.nn.Conv2d, pool: torc
           and conv.out_channels % 8 == 0 and conv.out_channels <= 2048 and w.dtype == torch.bfloat16)
     if not ok:
         return maxpool_train(conv_bias_relu_train(x, conv).contiguous(memory_format=_CL), pool)
-    return _ConvBiasReLUPoolTrainFn.apply(x, w, conv.bias, conv.stride[0], conv.padding[0], k, in_relu)
+    return _ConvBiasReLUPoolTrainFn.apply(x, w, conv.bias, conv.stride[0], conv.padding[0], k, in_relu, out_nchw)
 
 
 def _conv_bias_relu_ok(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
