@@ -139,13 +139,19 @@ __global__ void __launch_bounds__(kThreads) dw_dgrad_kernel(const u32x4* __restr
   }
 }
 
-// Block = one slab of pb output pixels (pb = 8 · (256 / cv): 8 pixels per
-// thread whatever C): thread t owns channel group t % cv and pixels
-// p0 + t / cv + k · (256 / cv).  Its 9 x 8 sums are merged across the block
-// through LDS, one tap at a time, into part[slab][tap][C].
+// Block = one slab of pb output pixels (pb = kWgPix · (256 / cv)): thread t owns
+// channel group t % cv and pixels p0 + t / cv + k · (256 / cv), two pixels'
+// loads in flight.  Its 9 x 8 sums are merged across the block one tap at a
+// time with every thread taking part: P = 256 / C threads per channel each
+// fold a strided share of the sub-rows, then C threads fold the P shares
+// (fixed order).  The first version had only C / 8 threads walk all sub-rows
+// for each tap at 8 pixels per thread: 30 us per DeepLab layer, 10 % of its
+// training step (profiles/r5/train/deeplab_step_kernels.md).
+constexpr int kWgPix = 8;
 __global__ void __launch_bounds__(kThreads) dw_wgrad_kernel(const u32x4* __restrict__ dy, const u32x4* __restrict__ x,
                                                             float* __restrict__ part, const Shape s, int pb) {
-  __shared__ float red[kThreads][9];
+  __shared__ float red[kThreads * 8];  // [sub][C] for one tap (nsub · C = 256 · 8 floats)
+  __shared__ float red2[kThreads];
   const int cv = s.C / 8, nsub = kThreads / cv;
   const int t = threadIdx.x, cg = t % cv, sub = t / cv;
   const int64_t P = (int64_t)s.N * s.OH * s.OW;
@@ -155,47 +161,58 @@ __global__ void __launch_bounds__(kThreads) dw_wgrad_kernel(const u32x4* __restr
   for (int k = 0; k < 9; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
-  if (sub < nsub) {
-    for (int64_t p = p0 + sub; p < p1; p += nsub) {
-      const int ow = (int)(p % s.OW);
-      const int64_t r = p / s.OW;
-      const int oh = (int)(r % s.OH);
-      const int n = (int)(r / s.OH);
-      float g[8];
-      unpack8(dy[p * cv + cg], g);
-      const int h0 = oh * s.stride - s.dil, w0 = ow * s.stride - s.dil;
-      const u32x4* xn = x + (int64_t)n * s.H * s.W * cv + cg;
+  auto pixel = [&](int64_t p) {
+    const int ow = (int)(p % s.OW);
+    const int64_t r = p / s.OW;
+    const int oh = (int)(r % s.OH);
+    const int n = (int)(r / s.OH);
+    float g[8];
+    unpack8(dy[p * cv + cg], g);
+    const int h0 = oh * s.stride - s.dil, w0 = ow * s.stride - s.dil;
+    const u32x4* xn = x + (int64_t)n * s.H * s.W * cv + cg;
+    u32x4 xv[9];
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        const int ih = h0 + kh * s.dil;
-        if ((unsigned)ih >= (unsigned)s.H) continue;
-#pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
-          const int iw = w0 + kw * s.dil;
-          if ((unsigned)iw >= (unsigned)s.W) continue;
-          float xv[8];
-          unpack8(xn[((int64_t)ih * s.W + iw) * cv], xv);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[kh * 3 + kw][j] = fmaf(g[j], xv[j], acc[kh * 3 + kw][j]);
-        }
-      }
+    for (int k = 0; k < 9; ++k) {
+      const int ih = h0 + (k / 3) * s.dil, iw = w0 + (k % 3) * s.dil;
+      const bool ok = (unsigned)ih < (unsigned)s.H && (unsigned)iw < (unsigned)s.W;
+      xv[k] = ok ? xn[((int64_t)ih * s.W + iw) * cv] : u32x4{0u, 0u, 0u, 0u};
     }
-  }
-  float* out = part + (int64_t)blockIdx.x * 9 * s.C;
 #pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      float xf[8];
+      unpack8(xv[k], xf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[k][j] = fmaf(g[j], xf[j], acc[k][j]);
+    }
+  };
+  if (sub < nsub)
+    for (int64_t p = p0 + sub; p < p1; p += nsub) pixel(p);
+  const int C = s.C;
+  const int PP = kThreads / C > 0 ? kThreads / C : 1;  // threads per channel in the first fold
+  float* out = part + (int64_t)blockIdx.x * 9 * C;
+#pragma unroll 1
   for (int k = 0; k < 9; ++k) {
+    if (sub < nsub) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) red[t][j] = acc[k][j];
-    __syncthreads();
-    if (t < cv) {
-      float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int q = 0; q < nsub; ++q)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] += red[q * cv + t][j];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) out[(int64_t)k * s.C + t * 8 + j] = a[j];
+      for (int j = 0; j < 8; ++j) red[sub * C + cg * 8 + j] = acc[k][j];
     }
     __syncthreads();
+    // fold 1: thread (e, q) sums sub-rows q, q + PP, ... of element e
+    for (int e0 = 0; e0 < C; e0 += kThreads / PP) {
+      const int e = e0 + t % (kThreads / PP), q = t / (kThreads / PP);
+      float a = 0.f;
+      if (e < C && q < PP)
+        for (int r = q; r < nsub; r += PP) a += red[r * C + e];
+      if (e < C && q < PP) red2[q * (kThreads / PP) + (e - e0)] = a;
+      __syncthreads();
+      // fold 2: the PP shares of each element in order
+      if (t < kThreads / PP && e0 + t < C) {
+        float b = 0.f;
+        for (int q2 = 0; q2 < PP; ++q2) b += red2[q2 * (kThreads / PP) + t];
+        out[(int64_t)k * C + e0 + t] = b;
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -236,8 +253,8 @@ int grid_for(int64_t total) {
   return (int)(b < 65536 ? (b > 0 ? b : 1) : 65536);
 }
 
-// Pixels per weight-gradient block: 8 per thread whatever C.
-int wgrad_pb(const Shape& s) { return 8 * (kThreads / (s.C / 8)); }
+// Pixels per weight-gradient block: kWgPix per thread whatever C.
+int wgrad_pb(const Shape& s) { return kWgPix * (kThreads / (s.C / 8)); }
 
 int wgrad_slabs(const Shape& s) {
   const int64_t P = (int64_t)s.N * s.OH * s.OW;

@@ -12,7 +12,10 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 marker = sys.argv[2] if len(sys.argv) > 2 else "sgd_bf16"
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
-end, start = idx[-1], idx[-2] + 1
+# consecutive marker launches (an optimizer split over several launches) form
+# one boundary: the step runs from after one run of them to the end of the next
+runs = [i for j, i in enumerate(idx) if j + 1 == len(idx) or idx[j + 1] != i + 1]
+end, start = runs[-1], runs[-2] + 1
 agg = {}
 tot = 0.0
 for r in rows[start:end + 1]:
