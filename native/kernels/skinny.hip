@@ -56,8 +56,10 @@ __device__ __forceinline__ float wave_sum(float v) {
 // loads in flight), the four partial dot products meet in LDS.  4096 waves for
 // fc1: one wave per SIMD with the whole K each ran the pass at ~3.5 TB/s in a
 // training step, loads and math strictly alternating (68 us for 205 MB).
-constexpr int kR = 4, kU = 4, kFwdWaves = kThreads / 64;
-template <int B>
+// Two rows per block: 2048 blocks for fc1, 31.2 / 7.6 / 4.0 us for VGG-16's fc1-3
+// against 32.6 / 8.6 / 4.8 with four rows; eight chunks in flight lost (44.6 us).
+constexpr int kFwdRows = 2, kFwdWaves = kThreads / 64;
+template <int B, int kR, int kU>
 __global__ void __launch_bounds__(kThreads) skinny_fwd_kernel(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               const uint16_t* __restrict__ bias,
@@ -124,8 +126,8 @@ __global__ void __launch_bounds__(kThreads) skinny_fwd_kernel(const uint16_t* __
 // 4 waves split the block's rows; thread = 8 consecutive k.  g for the block's
 // rows is formed into LDS first.  Partials of the NS row splits go to ws and
 // skinny_dgrad_reduce sums them in order.
-constexpr int kDgRows = 256;  // rows per block (64 per wave)
-template <int B>
+constexpr int kDgRows = 256;  // rows per block (64 per wave); 128 rows or 16 loads in flight ran no faster
+template <int B, int kDgRows, int RU>
 __global__ void __launch_bounds__(kThreads) skinny_dgrad_kernel(const uint16_t* __restrict__ dy,
                                                                 const uint16_t* __restrict__ yout,
                                                                 const uint16_t* __restrict__ w,
@@ -154,7 +156,6 @@ __global__ void __launch_bounds__(kThreads) skinny_dgrad_kernel(const uint16_t* 
   if (c < kv) {
     const int r0 = wave * (kDgRows / 4);
     const u32x4* W = reinterpret_cast<const u32x4*>(w) + c;
-    constexpr int RU = 8;
     for (int r = r0; r < r0 + kDgRows / 4; r += RU) {
       u32x4 wv[RU];
 #pragma unroll
@@ -228,13 +229,24 @@ struct DxJob {
   int splits;
 };
 
+// Optimizer-in-backward: with p set, the weight gradient never reaches memory.
+// Each bf16-rounded dW element updates p and its momentum buffer m exactly as
+// sgd_bf16_kernel (native/kernels/optim.hip) would, saving the dW write and
+// its read back (2 x 205 MB for VGG-16's fc1).
+struct SgdJob {
+  uint16_t* p;
+  uint16_t* m;
+  float lr, mom, damp1, wd;
+  int nesterov, first;
+};
+
 template <int B>
 __global__ void __launch_bounds__(kThreads) skinny_wgrad_kernel(const uint16_t* __restrict__ dy,
                                                                 const uint16_t* __restrict__ yout,
                                                                 const uint16_t* __restrict__ x,
                                                                 uint16_t* __restrict__ dw, uint16_t* __restrict__ db,
                                                                 int N, int K, int act, const DxJob job,
-                                                                int row_groups) {
+                                                                int row_groups, const SgdJob sj) {
   if ((int)blockIdx.y >= row_groups) {  // block-uniform: the dx reduce job
     for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < job.total8;
          i += (int64_t)gridDim.x * kThreads) {
@@ -291,6 +303,26 @@ __global__ void __launch_bounds__(kThreads) skinny_wgrad_kernel(const uint16_t* 
       for (int b = 0; b < B; ++b) s = fmaf(g[r][b], xf[b][j], s);
       o[j] = s;
     }
+    if (sj.p) {
+      const int64_t at = (int64_t)(n0 + r) * kv + c;
+      u32x4* P = reinterpret_cast<u32x4*>(sj.p) + at;
+      u32x4* M = reinterpret_cast<u32x4*>(sj.m) + at;
+      float pf[8], mf[8] = {};
+      unpack8(__builtin_nontemporal_load(P), pf);
+      if (!sj.first) unpack8(__builtin_nontemporal_load(M), mf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gg = fmaf(sj.wd, pf[j], bf2f(f2bf(o[j])));  // the gradient as bf16, as unfused
+        mf[j] = sj.first ? gg : fmaf(sj.mom, mf[j], sj.damp1 * gg);
+        const float d = sj.nesterov ? fmaf(sj.mom, mf[j], gg) : mf[j];
+        pf[j] = fmaf(-sj.lr, d, pf[j]);
+      }
+      __builtin_nontemporal_store(
+          u32x4{pack2(pf[0], pf[1]), pack2(pf[2], pf[3]), pack2(pf[4], pf[5]), pack2(pf[6], pf[7])}, P);
+      __builtin_nontemporal_store(
+          u32x4{pack2(mf[0], mf[1]), pack2(mf[2], mf[3]), pack2(mf[4], mf[5]), pack2(mf[6], mf[7])}, M);
+      continue;
+    }
     // nontemporal: dW (205 MB for fc1) would otherwise push W out of the MALL
     // between this layer's data gradient and the optimizer
     __builtin_nontemporal_store(u32x4{pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7])},
@@ -302,6 +334,16 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 }  // namespace
 
+#define VGPU_SKINNY_SWITCH_T(B, KERNEL, P, Q, GRID, ...)                                                  \
+  switch (B) {                                                                                            \
+    case 1: hipLaunchKernelGGL((KERNEL<1, P, Q>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break;        \
+    case 2: hipLaunchKernelGGL((KERNEL<2, P, Q>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break;        \
+    case 3: hipLaunchKernelGGL((KERNEL<3, P, Q>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break;        \
+    case 4: hipLaunchKernelGGL((KERNEL<4, P, Q>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break;        \
+    case 8: hipLaunchKernelGGL((KERNEL<8, P, Q>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break;        \
+    default: return -1;                                                                                   \
+  }
+
 #define VGPU_SKINNY_SWITCH(B, KERNEL, GRID, ...)                                                          \
   switch (B) {                                                                                            \
     case 1: hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(kThreads), 0, s, __VA_ARGS__); break;                \
@@ -312,17 +354,24 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
     default: return -1;                                                                                   \
   }
 
+static int launch_dgrad(int B, dim3 grid, const void* dy, const void* yout, const void* w, void* ws, int N, int K,
+                        int act, hipStream_t s) {
+  VGPU_SKINNY_SWITCH_T(B, skinny_dgrad_kernel, kDgRows, 8, grid, (const uint16_t*)dy, (const uint16_t*)yout,
+                       (const uint16_t*)w, (float*)ws, N, K, act)
+  return 0;
+}
+
 VGPU_API int vgpu_skinny_supported(int B, int N, int K) {
-  return (B == 1 || B == 2 || B == 3 || B == 4 || B == 8) && N % kR == 0 && K % 8 == 0 && N > 0 && K > 0;
+  return (B == 1 || B == 2 || B == 3 || B == 4 || B == 8) && N % 4 == 0 && K % 8 == 0 && N > 0 && K > 0;
 }
 
 // y [B][N] = act(x [B][K] · W[N][K]ᵀ + bias) (bf16; bias bf16 or null; act 0/1/2).
 VGPU_API int vgpu_skinny_fwd(const void* x, const void* w, const void* bias, void* y, int B, int N, int K, int act,
                              hipStream_t s) {
   if (!vgpu_skinny_supported(B, N, K) || !al16(x) || !al16(w) || act < 0 || act > 2) return -1;
-  const dim3 grid(N / kR);
-  VGPU_SKINNY_SWITCH(B, skinny_fwd_kernel, grid, (const uint16_t*)x, (const uint16_t*)w, (const uint16_t*)bias,
-                     (uint16_t*)y, N, K, act)
+  const dim3 grid(N / kFwdRows);
+  VGPU_SKINNY_SWITCH_T(B, skinny_fwd_kernel, kFwdRows, 4, grid, (const uint16_t*)x, (const uint16_t*)w,
+                       (const uint16_t*)bias, (uint16_t*)y, N, K, act)
   return (int)hipGetLastError();
 }
 
@@ -338,8 +387,7 @@ VGPU_API int vgpu_skinny_dgrad(const void* dy, const void* yout, const void* w, 
   if (ws_bytes < vgpu_skinny_dgrad_workspace(B, N, K)) return -1;
   const int splits = (N + kDgRows - 1) / kDgRows;
   const dim3 grid((K / 8 + 63) / 64, splits);
-  VGPU_SKINNY_SWITCH(B, skinny_dgrad_kernel, grid, (const uint16_t*)dy, (const uint16_t*)yout, (const uint16_t*)w,
-                     (float*)ws, N, K, act)
+  if (launch_dgrad(B, grid, dy, yout, w, ws, N, K, act, s)) return -1;
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const int64_t total8 = (int64_t)B * K / 8;
@@ -355,27 +403,46 @@ VGPU_API int vgpu_skinny_wgrad(const void* dy, const void* yout, const void* x, 
   const int rg = (N + kWgRows - 1) / kWgRows;
   const dim3 grid((K / 8 + kThreads - 1) / kThreads, rg);
   VGPU_SKINNY_SWITCH(B, skinny_wgrad_kernel, grid, (const uint16_t*)dy, (const uint16_t*)yout, (const uint16_t*)x,
-                     (uint16_t*)dw, (uint16_t*)db, N, K, act, DxJob{}, rg)
+                     (uint16_t*)dw, (uint16_t*)db, N, K, act, DxJob{}, rg, SgdJob{})
   return (int)hipGetLastError();
 }
 
 // The whole backward of a skinny layer in two launches: the data gradient's
 // row splits into ws, then dW / db with the split sum into dx riding along.
-VGPU_API int vgpu_skinny_backward(const void* dy, const void* yout, const void* x, const void* w, void* dx, void* dw,
-                                  void* db, void* ws, int64_t ws_bytes, int B, int N, int K, int act,
-                                  hipStream_t s) {
-  if (!vgpu_skinny_supported(B, N, K) || !al16(x) || !al16(dw) || !al16(w) || !al16(dx) || !al16(ws)) return -1;
+static int skinny_backward(const void* dy, const void* yout, const void* x, const void* w, void* dx, void* dw,
+                           void* db, void* ws, int64_t ws_bytes, int B, int N, int K, int act, const SgdJob& sj,
+                           hipStream_t s) {
+  if (!vgpu_skinny_supported(B, N, K) || !al16(x) || !al16(w) || !al16(dx) || !al16(ws)) return -1;
+  if (sj.p ? !al16(sj.m) : !al16(dw)) return -1;
   if (ws_bytes < vgpu_skinny_dgrad_workspace(B, N, K)) return -1;
   const int splits = (N + kDgRows - 1) / kDgRows;
   const dim3 g1((K / 8 + 63) / 64, splits);
-  VGPU_SKINNY_SWITCH(B, skinny_dgrad_kernel, g1, (const uint16_t*)dy, (const uint16_t*)yout, (const uint16_t*)w,
-                     (float*)ws, N, K, act)
+  if (launch_dgrad(B, g1, dy, yout, w, ws, N, K, act, s)) return -1;
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const int rg = (N + kWgRows - 1) / kWgRows;
   const dim3 g2((K / 8 + kThreads - 1) / kThreads, rg + 1);
   const DxJob job{(const float*)ws, (uint16_t*)dx, (int64_t)B * K / 8, splits};
   VGPU_SKINNY_SWITCH(B, skinny_wgrad_kernel, g2, (const uint16_t*)dy, (const uint16_t*)yout, (const uint16_t*)x,
-                     (uint16_t*)dw, (uint16_t*)db, N, K, act, job, rg)
+                     (uint16_t*)dw, (uint16_t*)db, N, K, act, job, rg, sj)
   return (int)hipGetLastError();
+}
+
+VGPU_API int vgpu_skinny_backward(const void* dy, const void* yout, const void* x, const void* w, void* dx, void* dw,
+                                  void* db, void* ws, int64_t ws_bytes, int B, int N, int K, int act,
+                                  hipStream_t s) {
+  return skinny_backward(dy, yout, x, w, dx, dw, db, ws, ws_bytes, B, N, K, act, SgdJob{}, s);
+}
+
+// The backward with the weight's SGD step fused in (no dW): w and its momentum
+// buffer m are updated in place after the data gradient has read w.  first:
+// m is written from the gradient (PyTorch's first step).  db is still a gradient.
+VGPU_API int vgpu_skinny_backward_sgd(const void* dy, const void* yout, const void* x, void* w, void* dx, void* m,
+                                      void* db, void* ws, int64_t ws_bytes, int B, int N, int K, int act, float lr,
+                                      float momentum, float dampening, float weight_decay, int nesterov, int first,
+                                      hipStream_t s) {
+  if (!w || !m) return -1;
+  const SgdJob sj{(uint16_t*)w, (uint16_t*)m, lr, momentum, first ? 1.0f : 1.0f - dampening, weight_decay,
+                  nesterov, first};
+  return skinny_backward(dy, yout, x, w, dx, nullptr, db, ws, ws_bytes, B, N, K, act, sj, s);
 }

@@ -78,3 +78,61 @@ def test_cross_entropy_matches_torch(gpu_build, dtype, rows, c):
     torch.testing.assert_close(loss, lr, atol=1e-4, rtol=1e-4)
     tol = dict(atol=2e-3, rtol=2e-2) if dtype == torch.bfloat16 else dict(atol=1e-6, rtol=1e-4)
     torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
+
+
+def _mlp(device, seed=0):
+    torch.manual_seed(seed)
+    m = torch.nn.Sequential(torch.nn.Linear(1032, 512), torch.nn.Linear(512, 200))
+    return m.to(device)
+
+
+def test_fuse_into_backward_registers_linear_weights_cpu():
+    """fp32 CPU: the registered weights never take the skinny kernels, so the
+    step is PyTorch's SGD exactly (gradients stay ordinary)."""
+    a, b = _mlp("cpu"), _mlp("cpu")
+    oa = SGD(a.parameters(), lr=0.1, momentum=0.9)
+    assert oa.fuse_into_backward(a) == 2
+    ob = torch.optim.SGD(b.parameters(), lr=0.1, momentum=0.9)
+    x = torch.randn(2, 1032)
+    for _ in range(3):
+        for m, o in ((a, oa), (b, ob)):
+            o.zero_grad(set_to_none=True)
+            m(x).square().sum().backward()
+            o.step()
+    for p, q in zip(a.parameters(), b.parameters()):
+        assert torch.equal(p, q)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [dict(lr=0.1, momentum=0.9), dict(lr=0.05, momentum=0.9, weight_decay=1e-2),
+                                dict(lr=0.05, momentum=0.8, nesterov=True),
+                                dict(lr=0.1, momentum=0.9, dampening=0.3)])
+def test_sgd_in_skinny_backward_bit_exact(gpu_build, kw):
+    """native/kernels/skinny.hip SgdJob: the FC weights stepped inside their
+    backward give the same bf16 weights, momentum buffers and input gradient
+    as the unfused native SGD over a materialised dW, over four steps (the
+    first initialises the buffers), and the fused weights' .grad stays None."""
+    from vgpu.ops.linear import linear_act
+    nets = [_mlp("cuda").to(torch.bfloat16) for _ in range(2)]
+    opts = [SGD(n.parameters(), **kw) for n in nets]
+    assert opts[1].fuse_into_backward(nets[1]) == 2
+    torch.manual_seed(1)
+    xs = [torch.randn(2, 1032, device="cuda", dtype=torch.bfloat16) for _ in range(4)]
+    dys = [torch.randn(2, 200, device="cuda", dtype=torch.bfloat16) for _ in range(4)]
+    for net, opt in zip(nets, opts):
+        net.dx = []
+        for x, dy in zip(xs, dys):
+            opt.zero_grad(set_to_none=True)
+            xi = x.clone().requires_grad_()
+            y = linear_act(linear_act(xi, net[0], "relu"), net[1])
+            y.backward(dy)
+            net.dx.append(xi.grad)
+            if opt is opts[1]:
+                assert net[0].weight.grad is None and net[1].weight.grad is None
+                assert net[0].bias.grad is not None
+            opt.step()
+    for (pa, pb) in zip(nets[0].parameters(), nets[1].parameters()):
+        assert torch.equal(pa, pb)
+        assert torch.equal(opts[0].state[pa]["momentum_buffer"], opts[1].state[pb]["momentum_buffer"])
+    for da, db in zip(nets[0].dx, nets[1].dx):
+        assert torch.equal(da, db)

@@ -57,6 +57,8 @@ def build(args):
         else:
             from vgpu.ops.optim import SGD
             opt = SGD(model.parameters(), lr=1e-3, momentum=0.9)
+            if which != "unfused":  # FC weights stepped inside their backward (VGPU_FUSED_SGD=unfused: A/B)
+                opt.fuse_into_backward(model)
         ncls = 21 if w.name == "deeplab" else (2 if w.name == "lstm" else 1000)
         if w.name == "deeplab":
             target = torch.randint(0, ncls, (w.batch, *w.shape[1:]), device=dev)

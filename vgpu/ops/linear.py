@@ -34,6 +34,9 @@ def _lib():
         lib.vgpu_skinny_wgrad.restype = ci
         lib.vgpu_skinny_backward.argtypes = [vp] * 8 + [ctypes.c_int64] + [ci] * 4 + [vp]
         lib.vgpu_skinny_backward.restype = ci
+        lib.vgpu_skinny_backward_sgd.argtypes = ([vp] * 8 + [ctypes.c_int64] + [ci] * 4 + [ctypes.c_float] * 4
+                                                 + [ci] * 2 + [vp])
+        lib.vgpu_skinny_backward_sgd.restype = ci
         _BOUND = True
     return lib
 
@@ -60,6 +63,8 @@ class _SkinnyLinearFn(torch.autograd.Function):
         _check(_lib().vgpu_skinny_fwd(_p(x), _p(w), _p(b), _p(y), bsz, n, k, act, _stream()), "vgpu_skinny_fwd")
         ctx.save_for_backward(x, w, y)
         ctx.act, ctx.has_b = act, b is not None
+        ctx.sgd = getattr(w, "_vgpu_sgd", None)  # vgpu.ops.optim.SGD.fuse_into_backward
+        ctx.param = w if ctx.sgd is not None else None
         return y
 
     @staticmethod
@@ -71,6 +76,10 @@ class _SkinnyLinearFn(torch.autograd.Function):
         lib = _lib()
         yo = y if ctx.act else None
         dx = dw = db = None
+        if ctx.sgd is not None and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]:
+            done = _backward_sgd(ctx, dy, x, yo, bsz, n, k)
+            if done is not None:
+                return done
         if ctx.needs_input_grad[0] and ctx.needs_input_grad[1]:  # both: two launches in all
             need = lib.vgpu_skinny_dgrad_workspace(bsz, n, k)
             ws = torch.empty(need // 4, dtype=torch.float32, device=x.device)
@@ -91,6 +100,38 @@ class _SkinnyLinearFn(torch.autograd.Function):
             _check(lib.vgpu_skinny_wgrad(_p(dy), _p(yo), _p(x), _p(dw), _p(db), bsz, n, k, ctx.act, _stream()),
                    "vgpu_skinny_wgrad")
         return dx, dw, db, None
+
+
+def _backward_sgd(ctx, dy, x, yo, bsz, n, k):
+    """The weight's SGD step inside its backward (no dW in memory): the
+    weight and its momentum buffer are updated in place once the data
+    gradient has read the weight; the weight's .grad stays None, so the
+    optimizer's own step skips it.  None when the group's settings need the
+    unfused path."""
+    opt, group = ctx.sgd
+    p = ctx.param
+    if group["momentum"] == 0 or group["maximize"] or p.numel() % 8:
+        return None
+    state = opt.state[p]
+    buf = state.get("momentum_buffer")
+    first = buf is None
+    if first:
+        buf = torch.empty_like(p)
+    if buf.stride() != p.stride() or buf.dtype != p.dtype:
+        return None
+    lib = _lib()
+    need = lib.vgpu_skinny_dgrad_workspace(bsz, n, k)
+    ws = torch.empty(need // 4, dtype=torch.float32, device=x.device)
+    dx = torch.empty_like(x)
+    db = torch.empty(n, dtype=p.dtype, device=p.device) if ctx.has_b else None
+    _check(lib.vgpu_skinny_backward_sgd(_p(dy), _p(yo), _p(x), _p(p), _p(dx), _p(buf), _p(db), _p(ws), need, bsz, n,
+                                        k, ctx.act, group["lr"], group["momentum"], group["dampening"],
+                                        group["weight_decay"], int(group["nesterov"]), int(first), _stream()),
+           "vgpu_skinny_backward_sgd")
+    if first:
+        state["momentum_buffer"] = buf
+    p.grad = None
+    return dx, None, db, None
 
 
 def eligible(x: torch.Tensor, lin: nn.Linear) -> bool:

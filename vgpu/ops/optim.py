@@ -78,6 +78,24 @@ class SGD(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, momentum=momentum, dampening=dampening,
                                       weight_decay=weight_decay, nesterov=nesterov, maximize=maximize))
 
+    def fuse_into_backward(self, module: torch.nn.Module) -> int:
+        """Optimizer-in-backward for the module's fully connected weights: a
+        registered weight that goes through the skinny kernels
+        (vgpu.ops.linear, batch ≤ 8) is updated inside its own backward and its
+        gradient never reaches memory (VGG-16 at batch 2: 2 x 247 MB of dW
+        traffic less per step).  Only for weights used once per step and no
+        gradient accumulation across backward passes.  A registered weight that
+        takes any other path keeps an ordinary gradient and is stepped here.
+        Returns the number of weights registered."""
+        count = 0
+        for group in self.param_groups:
+            ids = {id(p) for p in group["params"]}
+            for m in module.modules():
+                if isinstance(m, torch.nn.Linear) and id(m.weight) in ids:
+                    m.weight._vgpu_sgd = (self, group)
+                    count += 1
+        return count
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
