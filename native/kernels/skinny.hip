@@ -126,12 +126,37 @@ __global__ void __launch_bounds__(kThreads) skinny_fwd_kernel(const uint16_t* __
 // 4 waves split the block's rows; thread = 8 consecutive k.  g for the block's
 // rows is formed into LDS first.  Partials of the NS row splits go to ws and
 // skinny_dgrad_reduce sums them in order.
+// Optimizer-in-backward (skinny_dgrad_kernel<..., SGD = true>): the weight gradient never reaches memory.
+// Each bf16-rounded dW element updates p and its momentum buffer m exactly as
+// sgd_bf16_kernel (native/kernels/optim.hip) would, saving the dW write and
+// its read back (2 x 205 MB for VGG-16's fc1).
+struct SgdJob {
+  uint16_t* p;
+  uint16_t* m;
+  float lr, mom, damp1, wd;
+  int nesterov, first;
+};
+
 constexpr int kDgRows = 256;  // rows per block (64 per wave); 128 rows or 16 loads in flight ran no faster
-template <int B, int kDgRows, int RU>
+// bf16(gg) -> SGD on one weight element (sgd_bf16_kernel's math)
+__device__ __forceinline__ void sgd_elem(const SgdJob& sj, float gg, float& p, float& m) {
+  gg = fmaf(sj.wd, p, gg);
+  m = sj.first ? gg : fmaf(sj.mom, m, sj.damp1 * gg);
+  const float d = sj.nesterov ? fmaf(sj.mom, m, gg) : m;
+  p = fmaf(-sj.lr, d, p);
+}
+
+// SGD = true: the block also takes the SGD step of the weights it streams (the
+// weight gradient of its rows x its 64 chunks needs only x and g): the weight is
+// read once for both, dx from its value before the step; db from grid column 0.
+template <int B, int kDgRows, int RU, bool SGD = false>
 __global__ void __launch_bounds__(kThreads) skinny_dgrad_kernel(const uint16_t* __restrict__ dy,
                                                                 const uint16_t* __restrict__ yout,
                                                                 const uint16_t* __restrict__ w,
-                                                                float* __restrict__ ws, int N, int K, int act) {
+                                                                float* __restrict__ ws, int N, int K, int act,
+                                                                const uint16_t* __restrict__ x = nullptr,
+                                                                uint16_t* __restrict__ db = nullptr,
+                                                                const SgdJob sj = SgdJob{}) {
   __shared__ float sg[B][kDgRows];
   __shared__ float red[3][B][64][9];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -148,6 +173,18 @@ __global__ void __launch_bounds__(kThreads) skinny_dgrad_kernel(const uint16_t* 
     sg[b][r] = g;
   }
   __syncthreads();
+  float xf[SGD ? B : 1][8];
+  if (SGD) {
+    if (db && blockIdx.x == 0 && nb + t < N && t < kDgRows) {
+      float sb = 0.0f;
+#pragma unroll
+      for (int b = 0; b < B; ++b) sb += sg[b][t];
+      db[nb + t] = f2bf(sb);
+    }
+    if (c < kv)
+#pragma unroll
+      for (int b = 0; b < (SGD ? B : 1); ++b) unpack8(reinterpret_cast<const u32x4*>(x)[(int64_t)b * kv + c], xf[b]);
+  }
   float acc[B][8];
 #pragma unroll
   for (int b = 0; b < B; ++b)
@@ -157,11 +194,14 @@ __global__ void __launch_bounds__(kThreads) skinny_dgrad_kernel(const uint16_t* 
     const int r0 = wave * (kDgRows / 4);
     const u32x4* W = reinterpret_cast<const u32x4*>(w) + c;
     for (int r = r0; r < r0 + kDgRows / 4; r += RU) {
-      u32x4 wv[RU];
+      u32x4 wv[RU], mv[SGD ? RU : 1];
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
         const int n = nb + r + u;
-        wv[u] = n < N ? W[(int64_t)n * kv] : u32x4{0u, 0u, 0u, 0u};
+        wv[u] = n < N ? (SGD ? __builtin_nontemporal_load(W + (int64_t)n * kv) : W[(int64_t)n * kv])
+                      : u32x4{0u, 0u, 0u, 0u};
+        if (SGD && n < N && !sj.first)
+          mv[SGD ? u : 0] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sj.m) + c + (int64_t)n * kv);
       }
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
@@ -172,6 +212,24 @@ __global__ void __launch_bounds__(kThreads) skinny_dgrad_kernel(const uint16_t* 
           const float g = sg[b][r + u];
 #pragma unroll
           for (int j = 0; j < 8; ++j) acc[b][j] = fmaf(g, wf[j], acc[b][j]);
+        }
+        if (SGD && nb + r + u < N) {
+          float mf[8] = {};
+          if (!sj.first) unpack8(mv[SGD ? u : 0], mf);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float o = 0.0f;
+#pragma unroll
+            for (int b = 0; b < (SGD ? B : 1); ++b) o = fmaf(sg[b][r + u], xf[b][j], o);
+            sgd_elem(sj, bf2f(f2bf(o)), wf[j], mf[j]);  // the gradient as bf16, as unfused
+          }
+          const int64_t at = c + (int64_t)(nb + r + u) * kv;
+          __builtin_nontemporal_store(
+              u32x4{pack2(wf[0], wf[1]), pack2(wf[2], wf[3]), pack2(wf[4], wf[5]), pack2(wf[6], wf[7])},
+              reinterpret_cast<u32x4*>(sj.p) + at);
+          __builtin_nontemporal_store(
+              u32x4{pack2(mf[0], mf[1]), pack2(mf[2], mf[3]), pack2(mf[4], mf[5]), pack2(mf[6], mf[7])},
+              reinterpret_cast<u32x4*>(sj.m) + at);
         }
       }
     }
@@ -229,24 +287,13 @@ struct DxJob {
   int splits;
 };
 
-// Optimizer-in-backward: with p set, the weight gradient never reaches memory.
-// Each bf16-rounded dW element updates p and its momentum buffer m exactly as
-// sgd_bf16_kernel (native/kernels/optim.hip) would, saving the dW write and
-// its read back (2 x 205 MB for VGG-16's fc1).
-struct SgdJob {
-  uint16_t* p;
-  uint16_t* m;
-  float lr, mom, damp1, wd;
-  int nesterov, first;
-};
-
 template <int B>
 __global__ void __launch_bounds__(kThreads) skinny_wgrad_kernel(const uint16_t* __restrict__ dy,
                                                                 const uint16_t* __restrict__ yout,
                                                                 const uint16_t* __restrict__ x,
                                                                 uint16_t* __restrict__ dw, uint16_t* __restrict__ db,
                                                                 int N, int K, int act, const DxJob job,
-                                                                int row_groups, const SgdJob sj) {
+                                                                int row_groups) {
   if ((int)blockIdx.y >= row_groups) {  // block-uniform: the dx reduce job
     for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < job.total8;
          i += (int64_t)gridDim.x * kThreads) {
@@ -303,26 +350,6 @@ __global__ void __launch_bounds__(kThreads) skinny_wgrad_kernel(const uint16_t* 
       for (int b = 0; b < B; ++b) s = fmaf(g[r][b], xf[b][j], s);
       o[j] = s;
     }
-    if (sj.p) {
-      const int64_t at = (int64_t)(n0 + r) * kv + c;
-      u32x4* P = reinterpret_cast<u32x4*>(sj.p) + at;
-      u32x4* M = reinterpret_cast<u32x4*>(sj.m) + at;
-      float pf[8], mf[8] = {};
-      unpack8(__builtin_nontemporal_load(P), pf);
-      if (!sj.first) unpack8(__builtin_nontemporal_load(M), mf);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float gg = fmaf(sj.wd, pf[j], bf2f(f2bf(o[j])));  // the gradient as bf16, as unfused
-        mf[j] = sj.first ? gg : fmaf(sj.mom, mf[j], sj.damp1 * gg);
-        const float d = sj.nesterov ? fmaf(sj.mom, mf[j], gg) : mf[j];
-        pf[j] = fmaf(-sj.lr, d, pf[j]);
-      }
-      __builtin_nontemporal_store(
-          u32x4{pack2(pf[0], pf[1]), pack2(pf[2], pf[3]), pack2(pf[4], pf[5]), pack2(pf[6], pf[7])}, P);
-      __builtin_nontemporal_store(
-          u32x4{pack2(mf[0], mf[1]), pack2(mf[2], mf[3]), pack2(mf[4], mf[5]), pack2(mf[6], mf[7])}, M);
-      continue;
-    }
     // nontemporal: dW (205 MB for fc1) would otherwise push W out of the MALL
     // between this layer's data gradient and the optimizer
     __builtin_nontemporal_store(u32x4{pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7])},
@@ -341,6 +368,16 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
     case 3: hipLaunchKernelGGL((KERNEL<3, P, Q>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break;        \
     case 4: hipLaunchKernelGGL((KERNEL<4, P, Q>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break;        \
     case 8: hipLaunchKernelGGL((KERNEL<8, P, Q>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break;        \
+    default: return -1;                                                                                   \
+  }
+
+#define VGPU_SKINNY_SWITCH_SGD(B, GRID, ...)                                                              \
+  switch (B) {                                                                                            \
+    case 1: hipLaunchKernelGGL((skinny_dgrad_kernel<1, kDgRows, 8, true>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break; \
+    case 2: hipLaunchKernelGGL((skinny_dgrad_kernel<2, kDgRows, 8, true>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break; \
+    case 3: hipLaunchKernelGGL((skinny_dgrad_kernel<3, kDgRows, 8, true>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break; \
+    case 4: hipLaunchKernelGGL((skinny_dgrad_kernel<4, kDgRows, 8, true>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break; \
+    case 8: hipLaunchKernelGGL((skinny_dgrad_kernel<8, kDgRows, 8, true>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break; \
     default: return -1;                                                                                   \
   }
 
@@ -403,17 +440,16 @@ VGPU_API int vgpu_skinny_wgrad(const void* dy, const void* yout, const void* x, 
   const int rg = (N + kWgRows - 1) / kWgRows;
   const dim3 grid((K / 8 + kThreads - 1) / kThreads, rg);
   VGPU_SKINNY_SWITCH(B, skinny_wgrad_kernel, grid, (const uint16_t*)dy, (const uint16_t*)yout, (const uint16_t*)x,
-                     (uint16_t*)dw, (uint16_t*)db, N, K, act, DxJob{}, rg, SgdJob{})
+                     (uint16_t*)dw, (uint16_t*)db, N, K, act, DxJob{}, rg)
   return (int)hipGetLastError();
 }
 
 // The whole backward of a skinny layer in two launches: the data gradient's
 // row splits into ws, then dW / db with the split sum into dx riding along.
-static int skinny_backward(const void* dy, const void* yout, const void* x, const void* w, void* dx, void* dw,
-                           void* db, void* ws, int64_t ws_bytes, int B, int N, int K, int act, const SgdJob& sj,
-                           hipStream_t s) {
-  if (!vgpu_skinny_supported(B, N, K) || !al16(x) || !al16(w) || !al16(dx) || !al16(ws)) return -1;
-  if (sj.p ? !al16(sj.m) : !al16(dw)) return -1;
+VGPU_API int vgpu_skinny_backward(const void* dy, const void* yout, const void* x, const void* w, void* dx, void* dw,
+                                  void* db, void* ws, int64_t ws_bytes, int B, int N, int K, int act,
+                                  hipStream_t s) {
+  if (!vgpu_skinny_supported(B, N, K) || !al16(x) || !al16(dw) || !al16(w) || !al16(dx) || !al16(ws)) return -1;
   if (ws_bytes < vgpu_skinny_dgrad_workspace(B, N, K)) return -1;
   const int splits = (N + kDgRows - 1) / kDgRows;
   const dim3 g1((K / 8 + 63) / 64, splits);
@@ -424,14 +460,8 @@ static int skinny_backward(const void* dy, const void* yout, const void* x, cons
   const dim3 g2((K / 8 + kThreads - 1) / kThreads, rg + 1);
   const DxJob job{(const float*)ws, (uint16_t*)dx, (int64_t)B * K / 8, splits};
   VGPU_SKINNY_SWITCH(B, skinny_wgrad_kernel, g2, (const uint16_t*)dy, (const uint16_t*)yout, (const uint16_t*)x,
-                     (uint16_t*)dw, (uint16_t*)db, N, K, act, job, rg, sj)
+                     (uint16_t*)dw, (uint16_t*)db, N, K, act, job, rg)
   return (int)hipGetLastError();
-}
-
-VGPU_API int vgpu_skinny_backward(const void* dy, const void* yout, const void* x, const void* w, void* dx, void* dw,
-                                  void* db, void* ws, int64_t ws_bytes, int B, int N, int K, int act,
-                                  hipStream_t s) {
-  return skinny_backward(dy, yout, x, w, dx, dw, db, ws, ws_bytes, B, N, K, act, SgdJob{}, s);
 }
 
 // The backward with the weight's SGD step fused in (no dW): w and its momentum
@@ -441,8 +471,19 @@ VGPU_API int vgpu_skinny_backward_sgd(const void* dy, const void* yout, const vo
                                       void* db, void* ws, int64_t ws_bytes, int B, int N, int K, int act, float lr,
                                       float momentum, float dampening, float weight_decay, int nesterov, int first,
                                       hipStream_t s) {
-  if (!w || !m) return -1;
+  if (!w || !m || !vgpu_skinny_supported(B, N, K) || !al16(x) || !al16(w) || !al16(m) || !al16(dx) || !al16(ws))
+    return -1;
+  if (ws_bytes < vgpu_skinny_dgrad_workspace(B, N, K)) return -1;
   const SgdJob sj{(uint16_t*)w, (uint16_t*)m, lr, momentum, first ? 1.0f : 1.0f - dampening, weight_decay,
                   nesterov, first};
-  return skinny_backward(dy, yout, x, w, dx, nullptr, db, ws, ws_bytes, B, N, K, act, sj, s);
+  const int splits = (N + kDgRows - 1) / kDgRows;
+  const dim3 grid((K / 8 + 63) / 64, splits);
+  VGPU_SKINNY_SWITCH_SGD(B, grid, (const uint16_t*)dy, (const uint16_t*)yout, (const uint16_t*)w, (float*)ws, N, K,
+                         act, (const uint16_t*)x, (uint16_t*)db, sj)
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const int64_t total8 = (int64_t)B * K / 8;
+  hipLaunchKernelGGL(skinny_dgrad_reduce_kernel, dim3((unsigned)((total8 + kThreads - 1) / kThreads)), dim3(kThreads),
+                     0, s, (const float*)ws, (uint16_t*)dx, total8, splits);
+  return (int)hipGetLastError();
 }
