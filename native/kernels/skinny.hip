@@ -138,6 +138,10 @@ struct SgdJob {
 };
 
 constexpr int kDgRows = 256;  // rows per block (64 per wave); 128 rows or 16 loads in flight ran no faster
+// The SGD form writes as much as it reads: 128 rows x 4 loads in flight ran VGG-16 b=2 at
+// 1 591-1 610 images/s against 1 563-1 572 for 256 x 8 / 256 x 4, 1 600-1 604 for 128 x 8, 1 581-1 588 for
+// 128 x 2, 1 588-1 601 for 64 x 8 / 64 x 4 and 1 554 for 32 x 4 (profiles/r5/train).
+constexpr int kSgdRows = 128;
 // bf16(gg) -> SGD on one weight element (sgd_bf16_kernel's math)
 __device__ __forceinline__ void sgd_elem(const SgdJob& sj, float gg, float& p, float& m) {
   gg = fmaf(sj.wd, p, gg);
@@ -371,13 +375,13 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
     default: return -1;                                                                                   \
   }
 
-#define VGPU_SKINNY_SWITCH_SGD(B, GRID, ...)                                                              \
+#define VGPU_SKINNY_SGD_CASE(ROWS, RU, GRID, ...)                                                          \
   switch (B) {                                                                                            \
-    case 1: hipLaunchKernelGGL((skinny_dgrad_kernel<1, kDgRows, 8, true>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break; \
-    case 2: hipLaunchKernelGGL((skinny_dgrad_kernel<2, kDgRows, 8, true>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break; \
-    case 3: hipLaunchKernelGGL((skinny_dgrad_kernel<3, kDgRows, 8, true>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break; \
-    case 4: hipLaunchKernelGGL((skinny_dgrad_kernel<4, kDgRows, 8, true>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break; \
-    case 8: hipLaunchKernelGGL((skinny_dgrad_kernel<8, kDgRows, 8, true>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break; \
+    case 1: hipLaunchKernelGGL((skinny_dgrad_kernel<1, ROWS, RU, true>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break; \
+    case 2: hipLaunchKernelGGL((skinny_dgrad_kernel<2, ROWS, RU, true>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break; \
+    case 3: hipLaunchKernelGGL((skinny_dgrad_kernel<3, ROWS, RU, true>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break; \
+    case 4: hipLaunchKernelGGL((skinny_dgrad_kernel<4, ROWS, RU, true>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break; \
+    case 8: hipLaunchKernelGGL((skinny_dgrad_kernel<8, ROWS, RU, true>), GRID, dim3(kThreads), 0, s, __VA_ARGS__); break; \
     default: return -1;                                                                                   \
   }
 
@@ -414,7 +418,7 @@ VGPU_API int vgpu_skinny_fwd(const void* x, const void* w, const void* bias, voi
 
 // Workspace (bytes) of vgpu_skinny_dgrad: fp32 partials of the row splits.
 VGPU_API int64_t vgpu_skinny_dgrad_workspace(int B, int N, int K) {
-  return (int64_t)((N + kDgRows - 1) / kDgRows) * B * K * 4;
+  return (int64_t)((N + kSgdRows - 1) / kSgdRows) * B * K * 4;  // the SGD form's row split
 }
 
 // dx [B][K] = (dy·act'(y)) [B][N] · W [N][K]; yout = the layer's output (null: no activation).
@@ -476,10 +480,10 @@ VGPU_API int vgpu_skinny_backward_sgd(const void* dy, const void* yout, const vo
   if (ws_bytes < vgpu_skinny_dgrad_workspace(B, N, K)) return -1;
   const SgdJob sj{(uint16_t*)w, (uint16_t*)m, lr, momentum, first ? 1.0f : 1.0f - dampening, weight_decay,
                   nesterov, first};
-  const int splits = (N + kDgRows - 1) / kDgRows;
+  const int splits = (N + kSgdRows - 1) / kSgdRows;
   const dim3 grid((K / 8 + 63) / 64, splits);
-  VGPU_SKINNY_SWITCH_SGD(B, grid, (const uint16_t*)dy, (const uint16_t*)yout, (const uint16_t*)w, (float*)ws, N, K,
-                         act, (const uint16_t*)x, (uint16_t*)db, sj)
+  VGPU_SKINNY_SGD_CASE(kSgdRows, 4, grid, (const uint16_t*)dy, (const uint16_t*)yout, (const uint16_t*)w, (float*)ws,
+                       N, K, act, (const uint16_t*)x, (uint16_t*)db, sj)
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const int64_t total8 = (int64_t)B * K / 8;
