@@ -86,7 +86,12 @@ class SGD(torch.optim.Optimizer):
         traffic less per step).  Only for weights used once per step and no
         gradient accumulation across backward passes.  A registered weight that
         takes any other path keeps an ordinary gradient and is stepped here.
-        Returns the number of weights registered."""
+        Not under data parallelism: the gradient that a collective would
+        average never exists (refused when a process group of more than one
+        rank is up).  Returns the number of weights registered."""
+        if torch.distributed.is_available() and torch.distributed.is_initialized() \
+                and torch.distributed.get_world_size() > 1:
+            raise ValueError("fuse_into_backward: the gradients of a data-parallel step must reach the collectives")
         count = 0
         for group in self.param_groups:
             ids = {id(p) for p in group["params"]}
