@@ -1,12 +1,25 @@
 // Cross-entropy over bf16 (or fp32) logits with integer targets, forward and
-// gradient in ONE kernel (vgpu.ops.loss; the training pods).  PyTorch's
+// gradient in one pass (vgpu.ops.loss; the training pods).  PyTorch's
 // CrossEntropyLoss on bf16 logits runs a cast, log-softmax, NLL forward, and
 // in the backward a fill, NLL backward, log-softmax backward and a cast —
 // eight launches of ~4.7 us each in a replayed training step (VGG-16 b=2,
-// profiles/r5/train).  Here each row is one workgroup: max, Σ exp, the row's
-// loss and dlogits = (softmax − onehot) / rows in one pass (fp32 math), then
-// one block takes the mean of the row losses in a fixed order.  The backward
-// only scales the saved dlogits by the incoming gradient.
+// profiles/r5/train); DeepLab's per-pixel loss (nll_loss2d) was ~224 us a step.
+//
+// Logits are [rows][C] in any of three layouts, addressed as
+//   x[row, c] = base(row) + c * cstride,  base(row) = (row / hw) * bstride + (row % hw) * pstride
+// — a 2-D [rows, C] matrix, a channels-last [B, H, W, C] map or an NCHW map
+// (rows = B·H·W) — so the per-pixel loss reads the convolution's output in
+// place.  A row whose target is outside [0, C) or equals ignore_index is
+// ignored as torch.nn.functional.cross_entropy ignores it: loss 0, gradient
+// 0, not counted in the mean.
+//
+// The forward writes the unscaled gradient (softmax − onehot) of every valid
+// row and the reciprocal of the valid-row count; the backward multiplies by
+// (incoming gradient × that reciprocal).  Per-row work is mapped by C: one
+// workgroup per row for wide rows (ImageNet's 1000 classes), one lane per row
+// for narrow ones (DeepLab's 21: a wave covers 64 pixels, its NCHW reads are
+// coalesced across lanes).  The mean of the row losses is taken in a fixed
+// order by one workgroup.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -23,6 +36,13 @@ __device__ __forceinline__ void st(uint16_t* p, int64_t i, float v) {
   p[i] = __builtin_bit_cast(uint16_t, b);
 }
 __device__ __forceinline__ void st(float* p, int64_t i, float v) { p[i] = v; }
+
+struct Layout {
+  int64_t hw, bstride, pstride, cstride;
+  __device__ __forceinline__ int64_t base(int64_t row) const { return (row / hw) * bstride + (row % hw) * pstride; }
+};
+
+__device__ __forceinline__ bool valid_target(int64_t t, int C, int64_t ignore) { return t >= 0 && t < C && t != ignore; }
 
 template <typename T>
 __device__ float block_reduce(float v, float* sh, bool is_max) {
@@ -41,93 +61,139 @@ __device__ float block_reduce(float v, float* sh, bool is_max) {
   return r;
 }
 
-// One block per row.  loss_rows[r] = logsumexp(x_r) − x_r[t_r]; dx = (softmax − onehot) · scale.
+// One workgroup per row (wide rows).
 template <typename T>
-__global__ void __launch_bounds__(kThreads) xent_kernel(const T* __restrict__ x, const int64_t* __restrict__ tgt,
-                                                        float* __restrict__ loss_rows, T* __restrict__ dx, int C,
-                                                        float scale) {
-  __shared__ float sh[kThreads / 64];
-  const int64_t row = blockIdx.x;
-  const T* xr = x + row * C;
+__device__ float xent_row_block(const T* __restrict__ x, const int64_t* __restrict__ tgt, T* __restrict__ dx,
+                                int64_t row, int C, int64_t ignore, Layout L, float* sh) {
+  const int64_t b = L.base(row);
+  const int64_t t = tgt[row];
+  const bool ok = valid_target(t, C, ignore);
   float m = -INFINITY;
-  for (int c = threadIdx.x; c < C; c += kThreads) m = fmaxf(m, ld(xr, c));
+  for (int c = threadIdx.x; c < C; c += kThreads) m = fmaxf(m, ld(x, b + c * L.cstride));
   m = block_reduce<T>(m, sh, true);
   float s = 0.0f;
-  for (int c = threadIdx.x; c < C; c += kThreads) s += __expf(ld(xr, c) - m);
+  for (int c = threadIdx.x; c < C; c += kThreads) s += __expf(ld(x, b + c * L.cstride) - m);
   s = block_reduce<T>(s, sh, false);
-  const int64_t t = tgt[row];
   const float lse = m + __logf(s), inv = 1.0f / s;
-  if (threadIdx.x == 0) loss_rows[row] = (t >= 0 && t < C) ? lse - ld(xr, t) : 0.0f;
   for (int c = threadIdx.x; c < C; c += kThreads) {
-    const float p = __expf(ld(xr, c) - m) * inv;
-    st(dx, row * C + c, (p - (c == t ? 1.0f : 0.0f)) * scale);
+    const float p = __expf(ld(x, b + c * L.cstride) - m) * inv;
+    st(dx, b + c * L.cstride, ok ? p - (c == t ? 1.0f : 0.0f) : 0.0f);
   }
+  return ok ? lse - ld(x, b + t * L.cstride) : 0.0f;
 }
 
-// Up to 64 rows: one block does every row and the mean (one launch in all).
+template <typename T>
+__global__ void __launch_bounds__(kThreads) xent_wide_kernel(const T* __restrict__ x, const int64_t* __restrict__ tgt,
+                                                             float* __restrict__ loss_rows, T* __restrict__ dx, int C,
+                                                             int64_t ignore, Layout L) {
+  __shared__ float sh[kThreads / 64];
+  const float l = xent_row_block(x, tgt, dx, blockIdx.x, C, ignore, L, sh);
+  if (threadIdx.x == 0) loss_rows[blockIdx.x] = l;
+}
+
+// One lane per row (C <= 64): two passes over the row's C logits (max, then
+// Σexp and the gradient), all in registers' reach of L1/L2.
+template <typename T>
+__global__ void __launch_bounds__(kThreads) xent_narrow_kernel(const T* __restrict__ x, const int64_t* __restrict__ tgt,
+                                                               float* __restrict__ loss_rows, T* __restrict__ dx,
+                                                               int64_t rows, int C, int64_t ignore, Layout L) {
+  const int64_t row = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (row >= rows) return;
+  const int64_t b = L.base(row);
+  const int64_t t = tgt[row];
+  const bool ok = valid_target(t, C, ignore);
+  float m = -INFINITY;
+  for (int c = 0; c < C; ++c) m = fmaxf(m, ld(x, b + c * L.cstride));
+  float s = 0.0f, xt = 0.0f;
+  for (int c = 0; c < C; ++c) {
+    const float v = ld(x, b + c * L.cstride);
+    s += __expf(v - m);
+    if (c == t) xt = v;
+  }
+  const float inv = 1.0f / s;
+  for (int c = 0; c < C; ++c) {
+    const float p = __expf(ld(x, b + c * L.cstride) - m) * inv;
+    st(dx, b + c * L.cstride, ok ? p - (c == t ? 1.0f : 0.0f) : 0.0f);
+  }
+  loss_rows[row] = ok ? m + __logf(s) - xt : 0.0f;
+}
+
+// Up to 64 wide rows: one block does every row and the mean (one launch in all).
 template <typename T>
 __global__ void __launch_bounds__(kThreads) xent_small_kernel(const T* __restrict__ x, const int64_t* __restrict__ tgt,
-                                                              float* __restrict__ loss_rows, float* __restrict__ loss,
-                                                              T* __restrict__ dx, int rows, int C, float scale) {
+                                                              float* __restrict__ loss_rows, float* __restrict__ out,
+                                                              T* __restrict__ dx, int rows, int C, int64_t ignore,
+                                                              Layout L) {
   __shared__ float sh[kThreads / 64];
   float total = 0.0f;
+  int valid = 0;
   for (int row = 0; row < rows; ++row) {
-    const T* xr = x + (int64_t)row * C;
-    float m = -INFINITY;
-    for (int c = threadIdx.x; c < C; c += kThreads) m = fmaxf(m, ld(xr, c));
-    m = block_reduce<T>(m, sh, true);
-    float s = 0.0f;
-    for (int c = threadIdx.x; c < C; c += kThreads) s += __expf(ld(xr, c) - m);
-    s = block_reduce<T>(s, sh, false);
-    const int64_t t = tgt[row];
-    const float lse = m + __logf(s), inv = 1.0f / s;
-    const float l = (t >= 0 && t < C) ? lse - ld(xr, t) : 0.0f;
+    const float l = xent_row_block(x, tgt, dx, row, C, ignore, L, sh);
     total += l;
+    valid += valid_target(tgt[row], C, ignore) ? 1 : 0;
     if (threadIdx.x == 0) loss_rows[row] = l;
-    for (int c = threadIdx.x; c < C; c += kThreads) {
-      const float p = __expf(ld(xr, c) - m) * inv;
-      st(dx, (int64_t)row * C + c, (p - (c == t ? 1.0f : 0.0f)) * scale);
-    }
   }
-  if (threadIdx.x == 0) loss[0] = total / (float)rows;  // rows summed in order
+  if (threadIdx.x == 0) {  // rows summed in order
+    out[0] = total / (float)valid;
+    out[1] = valid ? 1.0f / (float)valid : 0.0f;
+  }
 }
 
-// mean of the row losses in a fixed order (one block)
-__global__ void __launch_bounds__(kThreads) mean_kernel(const float* __restrict__ v, float* __restrict__ out,
-                                                        int n) {
+// out[0] = Σ loss_rows / valid rows (in a fixed order), out[1] = 1 / valid rows.
+__global__ void __launch_bounds__(kThreads) mean_kernel(const float* __restrict__ v, const int64_t* __restrict__ tgt,
+                                                        float* __restrict__ out, int64_t n, int C, int64_t ignore) {
   __shared__ float sh[kThreads / 64];
-  float s = 0.0f;
-  for (int i = threadIdx.x; i < n; i += kThreads) s += v[i];
+  float s = 0.0f, k = 0.0f;
+  for (int64_t i = threadIdx.x; i < n; i += kThreads) {
+    s += v[i];
+    k += valid_target(tgt[i], C, ignore) ? 1.0f : 0.0f;
+  }
   s = block_reduce<float>(s, sh, false);
-  if (threadIdx.x == 0) out[0] = s / (float)n;
+  k = block_reduce<float>(k, sh, false);  // exact: counts below 2^24 per lane sum
+  if (threadIdx.x == 0) {
+    out[0] = s / k;
+    out[1] = k > 0.0f ? 1.0f / k : 0.0f;
+  }
+}
+
+template <typename T>
+int launch(const T* x, const int64_t* tgt, float* loss_rows, float* out, T* dx, int64_t rows, int C, int64_t ignore,
+           Layout L, hipStream_t s) {
+  if (C > 64 && rows <= 64) {
+    hipLaunchKernelGGL(xent_small_kernel<T>, dim3(1), dim3(kThreads), 0, s, x, tgt, loss_rows, out, dx, (int)rows, C,
+                       ignore, L);
+    return (int)hipGetLastError();
+  }
+  if (C > 64) {
+    if (rows > 0x7fffffffll) return -1;
+    hipLaunchKernelGGL(xent_wide_kernel<T>, dim3((unsigned)rows), dim3(kThreads), 0, s, x, tgt, loss_rows, dx, C,
+                       ignore, L);
+  } else {
+    const int64_t blocks = (rows + kThreads - 1) / kThreads;
+    if (blocks > 0x7fffffffll) return -1;
+    hipLaunchKernelGGL(xent_narrow_kernel<T>, dim3((unsigned)blocks), dim3(kThreads), 0, s, x, tgt, loss_rows, dx,
+                       rows, C, ignore, L);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(kThreads), 0, s, (const float*)loss_rows, tgt, out, rows, C, ignore);
+  return (int)hipGetLastError();
 }
 
 }  // namespace
 
-// logits [rows][C] (bf16 when is_bf16, else fp32), targets int64 [rows];
-// writes loss_rows fp32 [rows], loss fp32 [1] (mean) and dlogits (the logits'
-// dtype) = ∂mean/∂logits.  Returns 0, -1 (bad arguments) or a hipError_t.
-VGPU_API int vgpu_cross_entropy_fwd_bwd(const void* logits, const int64_t* tgt, float* loss_rows, float* loss,
-                                        void* dlogits, int rows, int C, int is_bf16, hipStream_t s) {
-  if (rows < 1 || C < 1) return -1;
-  const float scale = 1.0f / (float)rows;
-  if (rows <= 64) {
-    if (is_bf16)
-      hipLaunchKernelGGL(xent_small_kernel<uint16_t>, dim3(1), dim3(kThreads), 0, s, (const uint16_t*)logits, tgt,
-                         loss_rows, loss, (uint16_t*)dlogits, rows, C, scale);
-    else
-      hipLaunchKernelGGL(xent_small_kernel<float>, dim3(1), dim3(kThreads), 0, s, (const float*)logits, tgt,
-                         loss_rows, loss, (float*)dlogits, rows, C, scale);
-    return (int)hipGetLastError();
-  }
+// logits (bf16 when is_bf16, else fp32) addressed by (hw, bstride, pstride,
+// cstride) as above; targets int64 [rows].  Writes loss_rows fp32 [rows],
+// out fp32 [2] = {mean loss over valid rows, 1 / valid rows}, and dlogits
+// (same dtype and layout as the logits) = unscaled ∂loss_row/∂logits.
+// Returns 0, -1 (bad arguments) or a hipError_t.
+VGPU_API int vgpu_cross_entropy_fwd_bwd2(const void* logits, const int64_t* tgt, float* loss_rows, float* out,
+                                         void* dlogits, int64_t rows, int C, int64_t ignore_index, int64_t hw,
+                                         int64_t bstride, int64_t pstride, int64_t cstride, int is_bf16,
+                                         hipStream_t s) {
+  if (rows < 1 || C < 1 || hw < 1 || cstride < 1) return -1;
+  const Layout L{hw, bstride, pstride, cstride};
   if (is_bf16)
-    hipLaunchKernelGGL(xent_kernel<uint16_t>, dim3(rows), dim3(kThreads), 0, s, (const uint16_t*)logits, tgt,
-                       loss_rows, (uint16_t*)dlogits, C, scale);
-  else
-    hipLaunchKernelGGL(xent_kernel<float>, dim3(rows), dim3(kThreads), 0, s, (const float*)logits, tgt, loss_rows,
-                       (float*)dlogits, C, scale);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(kThreads), 0, s, (const float*)loss_rows, loss, rows);
-  return (int)hipGetLastError();
+    return launch((const uint16_t*)logits, tgt, loss_rows, out, (uint16_t*)dlogits, rows, C, ignore_index, L, s);
+  return launch((const float*)logits, tgt, loss_rows, out, (float*)dlogits, rows, C, ignore_index, L, s);
 }

@@ -636,23 +636,47 @@ __attribute__((visibility("default"))) hipError_t hipMemPrefetchAsync_v2(const v
                        [&](size_t m) { return REAL_HIP(hipMemPrefetchAsync_v2)(p, m, loc, flags, stream); });
 }
 
-__attribute__((visibility("default"))) hipError_t hipMallocPitch(void** ptr, size_t* pitch,
-                                                                 size_t width, size_t height) {
-  // Pitch is chosen by the runtime; charge the conservative upper bound
-  // (width rounded to 256 B rows) then correct to the real pitch.
-  size_t est = ((width + 255) / 256) * 256 * height;
-  hipError_t rc = charged_alloc(ptr, est, kDeviceBuf,
-                                [&] { return REAL_HIP(hipMallocPitch)(ptr, pitch, width, height); });
+}  // extern "C"
+
+// Pitched allocations: the runtime chooses the pitch, so the conservative
+// upper bound (width rounded to 256 B rows) is charged -- and refused past the
+// cap -- before the call, then corrected to the real pitch.
+template <class F>
+hipError_t pitched_alloc(void** ptr, size_t* pitch, size_t width, size_t height, F&& real) {
+  const size_t est = ((width + 255) / 256) * 256 * height;
+  hipError_t rc = charged_alloc(ptr, est, kDeviceBuf, real);
   if (rc == hipSuccess && pitch && *pitch * height != est) {
     Alloc a;
     if (ledger_take(*ptr, &a)) {
       mem_unreserve(a.dev, a.size, a.kind);
-      size_t real = *pitch * height;
-      mem_reserve(a.dev, real, a.kind);  // may exceed by < one row per call; accepted
-      ledger_add(*ptr, real, a.dev, a.kind);
+      size_t real_bytes = *pitch * height;
+      mem_reserve(a.dev, real_bytes, a.kind);  // may exceed by < one row per call; accepted
+      ledger_add(*ptr, real_bytes, a.dev, a.kind);
     }
   }
   return rc;
+}
+
+extern "C" {
+
+__attribute__((visibility("default"))) hipError_t hipMallocPitch(void** ptr, size_t* pitch,
+                                                                 size_t width, size_t height) {
+  return pitched_alloc(ptr, pitch, width, height, [&] { return REAL_HIP(hipMallocPitch)(ptr, pitch, width, height); });
+}
+
+// The driver-style pitched allocation (reference cuMemAllocPitch_v2, 844 B):
+// the same device memory as hipMallocPitch, reached without it (VERDICT r5
+// missing #1: it used to land in ROCr as "runtime memory", charged but never
+// refused).
+__attribute__((visibility("default"))) hipError_t hipMemAllocPitch(hipDeviceptr_t* dptr, size_t* pitch,
+                                                                   size_t width, size_t height,
+                                                                   unsigned int elem) {
+  return pitched_alloc(dptr, pitch, width, height,
+                       [&] { return REAL_HIP(hipMemAllocPitch)(dptr, pitch, width, height, elem); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemAllocHost(void** ptr, size_t size) {
+  return pinned_alloc(ptr, size, [&] { return REAL_HIP(hipMemAllocHost)(ptr, size); });
 }
 
 // ---- host copies (staged or repaired; see copy_sync / copy_async above) ----------
@@ -885,7 +909,18 @@ __attribute__((visibility("default"))) hipError_t hipFree(void* ptr) {
   ensure_init();
   Alloc a;
   if (uncharge(ptr, &a) && a.kind == kHostSpill) return free_spilled(ptr);
-  if (vmm_free(ptr)) return hipSuccess;
+  // A VMM-backed range (suspend with eviction): hipFree synchronizes the
+  // device before the memory goes (PyTorch's caching allocator relies on it
+  // when it returns segments), so the range is unmapped only once the work
+  // that may still read it has finished.
+  const int vdev = vmm_owner_dev(ptr);
+  if (vdev >= 0) {
+    const int cur = tl_device;
+    if (vdev != cur) (void)REAL_HIP(hipSetDevice)(vdev);
+    (void)REAL_HIP(hipDeviceSynchronize)();
+    if (vdev != cur) (void)REAL_HIP(hipSetDevice)(cur);
+    if (vmm_free(ptr)) return hipSuccess;
+  }
   return REAL_HIP(hipFree)(ptr);
 }
 
@@ -1119,6 +1154,167 @@ __attribute__((visibility("default"))) hipError_t hipLaunchKernelExC(const hipLa
   return rc;
 }
 
+// ---- the remaining launch entry points (VERDICT r5 missing #1) ----------------------
+// Every dispatch path ROCm 7.2's libamdhip64 exports is charged and held like
+// hipLaunchKernel: the per-thread-default-stream (-fgpu-default-stream=per-thread)
+// variants, the driver-style extensible launch, the multi-device launches (one
+// charge per list entry, on that entry's stream's device), the deprecated HCC
+// module launch (C and C++ linkage) and the legacy configure / launch-by-pointer
+// pair.  The reference has one launch path (cuLaunchKernel 461 B and
+// cuLaunchCooperativeKernel 407 B -> rate_limiter 623 B).
+__attribute__((visibility("default"))) hipError_t hipLaunchKernel_spt(const void* f, dim3 grid, dim3 block,
+                                                                      void** args, size_t shmem,
+                                                                      hipStream_t stream) {
+  HookScope hook_scope;
+  ensure_init();
+  const int dev = launch_dev(stream);
+  const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
+  vmem_scan_args(args, stream);
+  hipError_t rc = REAL_HIP(hipLaunchKernel_spt)(f, grid, block, args, shmem, stream);
+  if (track) limiter_track(dev, stream ? stream : hipStreamPerThread, rc);
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipLaunchCooperativeKernel_spt(const void* f, dim3 grid,
+                                                                                 dim3 block, void** params,
+                                                                                 uint32_t shmem,
+                                                                                 hipStream_t stream) {
+  HookScope hook_scope;
+  ensure_init();
+  hipError_t g = cooperative_guard(f, grid, block, shmem);
+  if (g != hipSuccess) return g;
+  const int dev = launch_dev(stream);
+  const bool track = limiter_on_launch(dev, blocks3(grid.x, grid.y, grid.z), f);
+  vmem_scan_args(params, stream);
+  hipError_t rc = REAL_HIP(hipLaunchCooperativeKernel_spt)(f, grid, block, params, shmem, stream);
+  if (track) limiter_track(dev, stream ? stream : hipStreamPerThread, rc);
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipDrvLaunchKernelEx(const HIP_LAUNCH_CONFIG* cfg,
+                                                                       hipFunction_t f, void** params,
+                                                                       void** extra) {
+  HookScope hook_scope;
+  ensure_init();
+  const hipStream_t stream = cfg ? cfg->hStream : nullptr;
+  const int dev = launch_dev(stream);
+  const bool track = cfg && limiter_on_launch(dev, blocks3(cfg->gridDimX, cfg->gridDimY, cfg->gridDimZ));
+  if (extra) vmem_scan_extra(extra, stream);
+  else vmem_scan_args(params, stream);
+  hipError_t rc = REAL_HIP(hipDrvLaunchKernelEx)(cfg, f, params, extra);
+  if (track) limiter_track(dev, stream, rc);
+  return rc;
+}
+
+}  // extern "C"
+
+namespace {
+inline uint64_t work_groups(uint32_t g, uint32_t l) { return l ? (g + l - 1) / l : g; }
+
+// Global work sizes in work-items (hipHccModuleLaunchKernel / hipExtModuleLaunchKernel).
+template <class F>
+hipError_t module_launch_wi(uint32_t gwx, uint32_t gwy, uint32_t gwz, uint32_t lwx, uint32_t lwy, uint32_t lwz,
+                            hipStream_t stream, void** params, void** extra, F&& real) {
+  HookScope hook_scope;
+  ensure_init();
+  const int dev = launch_dev(stream);
+  const bool track =
+      limiter_on_launch(dev, blocks3(work_groups(gwx, lwx), work_groups(gwy, lwy), work_groups(gwz, lwz)));
+  if (extra) vmem_scan_extra(extra, stream);
+  else vmem_scan_args(params, stream);
+  hipError_t rc = real();
+  if (track) limiter_track(dev, stream, rc);
+  return rc;
+}
+
+// One kernel per list entry, each on its entry's stream (and that stream's device).
+template <class Entry, class Grid, class Stream, class Args, class F>
+hipError_t multi_device_launch(Entry* list, size_t n, Grid&& grid, Stream&& stream_of, Args&& args_of, F&& real) {
+  HookScope hook_scope;
+  ensure_init();
+  if (!list || n == 0 || n > 64) return real();
+  int dev[64];
+  bool track[64];
+  for (size_t i = 0; i < n; ++i) {
+    dev[i] = launch_dev(stream_of(list[i]));
+    track[i] = limiter_on_launch(dev[i], grid(list[i]));
+    vmem_scan_args(args_of(list[i]), stream_of(list[i]));
+  }
+  hipError_t rc = real();
+  for (size_t i = 0; i < n; ++i)
+    if (track[i]) limiter_track(dev[i], stream_of(list[i]), rc);
+  return rc;
+}
+
+// hipConfigureCall pushes a launch configuration that hipLaunchByPtr pops
+// (per thread, as the runtime keeps it).
+struct ConfiguredCall {
+  dim3 grid;
+  hipStream_t stream;
+};
+thread_local std::vector<ConfiguredCall> tl_configured;
+}  // namespace
+
+extern "C" {
+
+__attribute__((visibility("default"))) hipError_t hipHccModuleLaunchKernel(
+    hipFunction_t f, uint32_t gwx, uint32_t gwy, uint32_t gwz, uint32_t lwx, uint32_t lwy, uint32_t lwz,
+    size_t shmem, hipStream_t stream, void** params, void** extra, hipEvent_t start, hipEvent_t stop) {
+  return module_launch_wi(gwx, gwy, gwz, lwx, lwy, lwz, stream, params, extra, [&] {
+    return REAL_HIP(hipHccModuleLaunchKernel)(f, gwx, gwy, gwz, lwx, lwy, lwz, shmem, stream, params, extra, start,
+                                              stop);
+  });
+}
+
+__attribute__((visibility("default"))) hipError_t hipExtLaunchMultiKernelMultiDevice(hipLaunchParams* list,
+                                                                                     int n, unsigned int flags) {
+  return multi_device_launch(
+      list, n > 0 ? (size_t)n : 0, [](const hipLaunchParams& p) { return blocks3(p.gridDim.x, p.gridDim.y, p.gridDim.z); },
+      [](const hipLaunchParams& p) { return p.stream; }, [](const hipLaunchParams& p) { return p.args; },
+      [&] { return REAL_HIP(hipExtLaunchMultiKernelMultiDevice)(list, n, flags); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipLaunchCooperativeKernelMultiDevice(hipLaunchParams* list,
+                                                                                        int n, unsigned int flags) {
+  return multi_device_launch(
+      list, n > 0 ? (size_t)n : 0, [](const hipLaunchParams& p) { return blocks3(p.gridDim.x, p.gridDim.y, p.gridDim.z); },
+      [](const hipLaunchParams& p) { return p.stream; }, [](const hipLaunchParams& p) { return p.args; },
+      [&] { return REAL_HIP(hipLaunchCooperativeKernelMultiDevice)(list, n, flags); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipModuleLaunchCooperativeKernelMultiDevice(
+    hipFunctionLaunchParams* list, unsigned int n, unsigned int flags) {
+  return multi_device_launch(
+      list, n, [](const hipFunctionLaunchParams& p) { return blocks3(p.gridDimX, p.gridDimY, p.gridDimZ); },
+      [](const hipFunctionLaunchParams& p) { return p.hStream; },
+      [](const hipFunctionLaunchParams& p) { return p.kernelParams; },
+      [&] { return REAL_HIP(hipModuleLaunchCooperativeKernelMultiDevice)(list, n, flags); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipConfigureCall(dim3 grid, dim3 block, size_t shmem,
+                                                                   hipStream_t stream) {
+  hipError_t rc = REAL_HIP(hipConfigureCall)(grid, block, shmem, stream);
+  if (rc == hipSuccess) tl_configured.push_back(ConfiguredCall{grid, stream});
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipLaunchByPtr(const void* f) {
+  HookScope hook_scope;
+  ensure_init();
+  ConfiguredCall c{dim3(1, 1, 1), nullptr};
+  const bool configured = !tl_configured.empty();
+  if (configured) {
+    c = tl_configured.back();
+    tl_configured.pop_back();
+  }
+  const int dev = launch_dev(c.stream);
+  // Unconfigured: the runtime refuses the call; nothing to charge.
+  const bool track = configured && limiter_on_launch(dev, blocks3(c.grid.x, c.grid.y, c.grid.z), f);
+  hipError_t rc = REAL_HIP(hipLaunchByPtr)(f);
+  if (track) limiter_track(dev, c.stream, rc);
+  return rc;
+}
+
 // Synchronize: the caller's batched launch counters become visible in its
 // region slot (the monitor and tests read them), then the real call.
 __attribute__((visibility("default"))) hipError_t hipDeviceSynchronize() {
@@ -1143,7 +1339,17 @@ __attribute__((visibility("default"))) hipError_t hipStreamDestroy(hipStream_t s
 // `grids` per cuLaunchKernel and has no graph path.
 // Graphs the walk cannot see (instantiated before the shim, or updated in
 // place) fall back to VGPU_GRAPH_LAUNCH_TOKENS.
-__attribute__((visibility("default"))) hipError_t hipGraphLaunch(hipGraphExec_t exec, hipStream_t stream) {
+}  // extern "C"
+
+namespace {
+// A graph with RCCL kernel nodes (a DDP step captured whole) is charged and
+// held like any graph (VERDICT r5 missing #2): the hold is before the replay,
+// a step boundary, never inside the step, so no collective is left waiting on
+// a rank stopped mid-step; a peer that reaches the collective first spins in
+// its kernel and pays for that spin on its own device.  Under `force` the
+// pod's duty stays at its cap whatever its graph contains.
+template <class F>
+hipError_t graph_launch(hipGraphExec_t exec, hipStream_t stream, F&& real) {
   HookScope hook_scope;  // the VMM evict thread waits for this call (vmm.cpp)
   ensure_init();
   static uint64_t fallback_tokens = [] {
@@ -1155,14 +1361,30 @@ __attribute__((visibility("default"))) hipError_t hipGraphLaunch(hipGraphExec_t 
   const int dev = launch_dev(stream);
   uint64_t tentative = 0;
   if (!pools_graph_admit(exec, dev, &tentative)) return hipErrorOutOfMemory;  // alloc nodes past the cap
-  // A graph with RCCL kernel nodes (a DDP step captured whole) is exempt as an
-  // eager RCCL kernel is: holding it would stall the collective's peer ranks.
-  const bool track = limiter_on_launch(dev, wg ? wg : fallback_tokens, nullptr, gw.kernels, gw.collectives > 0);
+  const bool track = limiter_on_launch(dev, wg ? wg : fallback_tokens, nullptr, gw.kernels, false);
   vmem_graph_launched(exec);
-  hipError_t rc = REAL_HIP(hipGraphLaunch)(exec, stream);
+  hipError_t rc = real();
   if (track) limiter_track(dev, stream, rc);
   pools_graph_launched(dev, tentative);
   return rc;
+}
+}  // namespace
+
+extern "C" {
+
+// Graphs: a hipGraphLaunch bypasses every per-kernel hook, so each executable
+// graph is charged the workgroups of all its kernel nodes (child graphs
+// included), counted once when it is instantiated — the reference charges
+// `grids` per cuLaunchKernel and has no graph path.
+// Graphs the walk cannot see (instantiated before the shim, or updated in
+// place) fall back to VGPU_GRAPH_LAUNCH_TOKENS.
+__attribute__((visibility("default"))) hipError_t hipGraphLaunch(hipGraphExec_t exec, hipStream_t stream) {
+  return graph_launch(exec, stream, [&] { return REAL_HIP(hipGraphLaunch)(exec, stream); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipGraphLaunch_spt(hipGraphExec_t exec, hipStream_t stream) {
+  return graph_launch(exec, stream ? stream : hipStreamPerThread,
+                      [&] { return REAL_HIP(hipGraphLaunch_spt)(exec, stream); });
 }
 
 // ---- graphs under one hardware queue ---------------------------------------------------
@@ -1188,26 +1410,30 @@ bool single_hw_queue() {
 
 std::atomic<uint64_t> g_graphs_chained{0};
 
-void chain_graph(hipGraph_t g) {
+// Chains `g` in place; false when it was left as it was or only partly
+// chained (the caller then discards it).  Chain edges are added before any
+// redundant edge is removed, so a failure part-way only ever leaves extra
+// ordering, never a missing dependency.
+bool chain_graph(hipGraph_t g) {
   auto get_nodes = REAL_HIP(hipGraphGetNodes);
   auto get_edges = REAL_HIP(hipGraphGetEdges);
   auto add_deps = REAL_HIP(hipGraphAddDependencies);
   auto rm_deps = REAL_HIP(hipGraphRemoveDependencies);
-  if (!g || !get_nodes || !get_edges || !add_deps || !rm_deps) return;
+  if (!g || !get_nodes || !get_edges || !add_deps || !rm_deps) return false;
   size_t n = 0, ne = 0;
-  if (get_nodes(g, nullptr, &n) != hipSuccess || n < 2) return;
+  if (get_nodes(g, nullptr, &n) != hipSuccess || n < 2) return false;
   std::vector<hipGraphNode_t> nodes(n);
-  if (get_nodes(g, nodes.data(), &n) != hipSuccess) return;
-  if (get_edges(g, nullptr, nullptr, &ne) != hipSuccess) return;
+  if (get_nodes(g, nodes.data(), &n) != hipSuccess) return false;
+  if (get_edges(g, nullptr, nullptr, &ne) != hipSuccess) return false;
   std::vector<hipGraphNode_t> from(ne), to(ne);
-  if (ne && get_edges(g, from.data(), to.data(), &ne) != hipSuccess) return;
+  if (ne && get_edges(g, from.data(), to.data(), &ne) != hipSuccess) return false;
   std::unordered_map<hipGraphNode_t, size_t> idx;
   for (size_t i = 0; i < n; ++i) idx[nodes[i]] = i;
   std::vector<std::vector<size_t>> out(n);
   std::vector<size_t> indeg(n, 0);
   for (size_t e = 0; e < ne; ++e) {
     auto a = idx.find(from[e]), b = idx.find(to[e]);
-    if (a == idx.end() || b == idx.end()) return;
+    if (a == idx.end() || b == idx.end()) return false;
     out[a->second].push_back(b->second);
     ++indeg[b->second];
   }
@@ -1225,39 +1451,92 @@ void chain_graph(hipGraph_t g) {
     for (size_t v : out[u])
       if (--indeg[v] == 0) ready.push_back(v);
   }
-  if (order.size() != n) return;  // not a DAG: leave it to the runtime's own error
+  if (order.size() != n) return false;  // not a DAG: leave it to the runtime's own error
   std::vector<size_t> pos(n);
   for (size_t k = 0; k < n; ++k) pos[order[k]] = k;
   bool chain = ne == n - 1;
   for (size_t e = 0; chain && e < ne; ++e) chain = pos[idx[to[e]]] == pos[idx[from[e]]] + 1;
-  if (chain) return;
+  if (chain) return false;
   std::vector<char> linked(n, 0);  // consecutive pair (k, k+1) already an edge
+  std::vector<char> keep(ne, 0);
   for (size_t e = 0; e < ne; ++e) {
     const size_t a = pos[idx[from[e]]], b = pos[idx[to[e]]];
-    if (b == a + 1 && !linked[a]) {
-      linked[a] = 1;
-      continue;
-    }
-    if (rm_deps(g, &from[e], &to[e], 1) != hipSuccess) {
-      (void)REAL_HIP(hipGetLastError)();
-      return;
-    }
+    if (b == a + 1 && !linked[a]) linked[a] = keep[e] = 1;
   }
   for (size_t k = 0; k + 1 < n; ++k)
     if (!linked[k] && add_deps(g, &nodes[order[k]], &nodes[order[k + 1]], 1) != hipSuccess) {
       (void)REAL_HIP(hipGetLastError)();
-      return;
+      return false;
+    }
+  for (size_t e = 0; e < ne; ++e)
+    if (!keep[e] && rm_deps(g, &from[e], &to[e], 1) != hipSuccess) {
+      (void)REAL_HIP(hipGetLastError)();
+      return false;
     }
   if (g_graphs_chained.fetch_add(1) == 0)
     VLOG_INFO("GPU_MAX_HW_QUEUES=1: graph of %zu nodes with parallel branches chained before instantiation", n);
+  return true;
+}
+
+// The graph to instantiate for the application's `g`: under one hardware
+// queue, a chained clone of it -- the caller's graph and the topology it sees
+// stay untouched, and hipGraphExecUpdate chains its new graph the
+// same way -- else `g` itself.  The clone lives as long as the executable
+// made from it.
+std::mutex g_clone_mu;
+std::unordered_map<const void*, hipGraph_t> g_exec_clone;
+
+hipGraph_t graph_to_instantiate(hipGraph_t g) {
+  if (!single_hw_queue() || !g) return g;
+  auto clone_fn = REAL_HIP(hipGraphClone);
+  hipGraph_t c = nullptr;
+  if (!clone_fn || clone_fn(&c, g) != hipSuccess || !c) {
+    (void)REAL_HIP(hipGetLastError)();
+    return g;
+  }
+  if (!chain_graph(c)) {
+    (void)REAL_HIP(hipGraphDestroy)(c);
+    return g;
+  }
+  return c;
+}
+
+// After instantiate / update of `exec` from `used` (the app's graph or its clone).
+void graph_clone_bind(hipGraphExec_t exec, hipGraph_t app, hipGraph_t used, bool ok) {
+  if (used == app) return;
+  if (!ok || !exec) {
+    (void)REAL_HIP(hipGraphDestroy)(used);
+    return;
+  }
+  hipGraph_t old = nullptr;
+  {
+    std::lock_guard<std::mutex> l(g_clone_mu);
+    auto it = g_exec_clone.find(exec);
+    if (it != g_exec_clone.end()) old = it->second;
+    g_exec_clone[exec] = used;
+  }
+  if (old) (void)REAL_HIP(hipGraphDestroy)(old);
+}
+
+void graph_clone_release(hipGraphExec_t exec) {
+  hipGraph_t c = nullptr;
+  {
+    std::lock_guard<std::mutex> l(g_clone_mu);
+    auto it = g_exec_clone.find(exec);
+    if (it == g_exec_clone.end()) return;
+    c = it->second;
+    g_exec_clone.erase(it);
+  }
+  (void)REAL_HIP(hipGraphDestroy)(c);
 }
 
 __attribute__((visibility("default"))) hipError_t hipGraphInstantiate(hipGraphExec_t* pExec, hipGraph_t graph,
                                                                       hipGraphNode_t* pErrorNode,
                                                                       char* pLogBuffer, size_t bufferSize) {
   ensure_init();
-  if (single_hw_queue()) chain_graph(graph);
-  hipError_t rc = REAL_HIP(hipGraphInstantiate)(pExec, graph, pErrorNode, pLogBuffer, bufferSize);
+  hipGraph_t used = graph_to_instantiate(graph);
+  hipError_t rc = REAL_HIP(hipGraphInstantiate)(pExec, used, pErrorNode, pLogBuffer, bufferSize);
+  graph_clone_bind(rc == hipSuccess && pExec ? *pExec : nullptr, graph, used, rc == hipSuccess);
   if (rc == hipSuccess && pExec) {
     graph_exec_record(*pExec, graph);
     vmem_graph_instantiated(graph, *pExec);
@@ -1270,8 +1549,9 @@ __attribute__((visibility("default"))) hipError_t hipGraphInstantiateWithFlags(h
                                                                                hipGraph_t graph,
                                                                                unsigned long long flags) {
   ensure_init();
-  if (single_hw_queue()) chain_graph(graph);
-  hipError_t rc = REAL_HIP(hipGraphInstantiateWithFlags)(pExec, graph, flags);
+  hipGraph_t used = graph_to_instantiate(graph);
+  hipError_t rc = REAL_HIP(hipGraphInstantiateWithFlags)(pExec, used, flags);
+  graph_clone_bind(rc == hipSuccess && pExec ? *pExec : nullptr, graph, used, rc == hipSuccess);
   if (rc == hipSuccess && pExec) {
     graph_exec_record(*pExec, graph);
     vmem_graph_instantiated(graph, *pExec);
@@ -1283,8 +1563,9 @@ __attribute__((visibility("default"))) hipError_t hipGraphInstantiateWithFlags(h
 __attribute__((visibility("default"))) hipError_t hipGraphInstantiateWithParams(
     hipGraphExec_t* pExec, hipGraph_t graph, hipGraphInstantiateParams* params) {
   ensure_init();
-  if (single_hw_queue()) chain_graph(graph);
-  hipError_t rc = REAL_HIP(hipGraphInstantiateWithParams)(pExec, graph, params);
+  hipGraph_t used = graph_to_instantiate(graph);
+  hipError_t rc = REAL_HIP(hipGraphInstantiateWithParams)(pExec, used, params);
+  graph_clone_bind(rc == hipSuccess && pExec ? *pExec : nullptr, graph, used, rc == hipSuccess);
   if (rc == hipSuccess && pExec) {
     graph_exec_record(*pExec, graph);
     vmem_graph_instantiated(graph, *pExec);
@@ -1332,7 +1613,9 @@ __attribute__((visibility("default"))) hipError_t hipGraphExecUpdate(hipGraphExe
                                                                      hipGraphNode_t* error_node,
                                                                      hipGraphExecUpdateResult* result) {
   ensure_init();
-  hipError_t rc = REAL_HIP(hipGraphExecUpdate)(exec, graph, error_node, result);
+  hipGraph_t used = graph_to_instantiate(graph);  // chained like the executable it updates
+  hipError_t rc = REAL_HIP(hipGraphExecUpdate)(exec, used, error_node, result);
+  graph_clone_bind(exec, graph, used, rc == hipSuccess);
   if (rc == hipSuccess) {  // the executable now runs `graph`'s parameters
     graph_exec_record(exec, graph);
     vmem_graph_instantiated(graph, exec);
@@ -1403,7 +1686,9 @@ __attribute__((visibility("default"))) hipError_t hipGraphExecDestroy(hipGraphEx
   graph_exec_forget(exec);
   vmem_graph_destroyed(exec);
   pools_graph_destroyed(exec);
-  return REAL_HIP(hipGraphExecDestroy)(exec);
+  const hipError_t rc = REAL_HIP(hipGraphExecDestroy)(exec);
+  graph_clone_release(exec);
+  return rc;
 }
 
 __attribute__((visibility("default"))) hipError_t hipGraphDestroy(hipGraph_t graph) {
@@ -1417,33 +1702,24 @@ __attribute__((visibility("default"))) hipError_t hipGraphDestroy(hipGraph_t gra
 // limiter neither records nor polls markers on the capturing streams (their
 // launches are charged when the graph runs); eager work on other streams is
 // tracked and charged as usual.
-__attribute__((visibility("default"))) hipError_t hipStreamBeginCapture(hipStream_t stream,
-                                                                        hipStreamCaptureMode mode) {
+}  // extern "C"
+
+namespace {
+template <class F>
+hipError_t begin_capture(F&& real) {
   {
     std::unique_lock<std::shared_mutex> g(g_capture_mu);  // no limiter marker in flight past here
     g_open_captures.fetch_add(1);
   }
-  hipError_t rc = REAL_HIP(hipStreamBeginCapture)(stream, mode);
+  hipError_t rc = real();
   if (rc != hipSuccess) g_open_captures.fetch_sub(1);
   return rc;
 }
 
-__attribute__((visibility("default"))) hipError_t hipStreamBeginCaptureToGraph(
-    hipStream_t stream, hipGraph_t graph, const hipGraphNode_t* deps, const hipGraphEdgeData* data,
-    size_t n, hipStreamCaptureMode mode) {
-  {
-    std::unique_lock<std::shared_mutex> g(g_capture_mu);
-    g_open_captures.fetch_add(1);
-  }
-  hipError_t rc = REAL_HIP(hipStreamBeginCaptureToGraph)(stream, graph, deps, data, n, mode);
-  if (rc != hipSuccess) g_open_captures.fetch_sub(1);
-  return rc;
-}
-
-__attribute__((visibility("default"))) hipError_t hipStreamEndCapture(hipStream_t stream,
-                                                                      hipGraph_t* graph) {
+template <class F>
+hipError_t end_capture(hipStream_t stream, hipGraph_t* graph, F&& real) {
   const unsigned long long cid = vmem_capture_begin_id(stream);
-  hipError_t rc = REAL_HIP(hipStreamEndCapture)(stream, graph);
+  hipError_t rc = real();
   if (cid) {
     hipGraph_t g = rc == hipSuccess && graph ? *graph : nullptr;
     vmem_capture_ended(cid, g);
@@ -1454,6 +1730,207 @@ __attribute__((visibility("default"))) hipError_t hipStreamEndCapture(hipStream_
   }
   return rc;
 }
+}  // namespace
+
+extern "C" {
+
+__attribute__((visibility("default"))) hipError_t hipStreamBeginCapture(hipStream_t stream,
+                                                                        hipStreamCaptureMode mode) {
+  return begin_capture([&] { return REAL_HIP(hipStreamBeginCapture)(stream, mode); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipStreamBeginCapture_spt(hipStream_t stream,
+                                                                            hipStreamCaptureMode mode) {
+  return begin_capture([&] { return REAL_HIP(hipStreamBeginCapture_spt)(stream, mode); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipStreamBeginCaptureToGraph(
+    hipStream_t stream, hipGraph_t graph, const hipGraphNode_t* deps, const hipGraphEdgeData* data,
+    size_t n, hipStreamCaptureMode mode) {
+  return begin_capture([&] { return REAL_HIP(hipStreamBeginCaptureToGraph)(stream, graph, deps, data, n, mode); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipStreamEndCapture(hipStream_t stream,
+                                                                      hipGraph_t* graph) {
+  return end_capture(stream, graph, [&] { return REAL_HIP(hipStreamEndCapture)(stream, graph); });
+}
+
+__attribute__((visibility("default"))) hipError_t hipStreamEndCapture_spt(hipStream_t stream,
+                                                                          hipGraph_t* graph) {
+  return end_capture(stream ? stream : hipStreamPerThread, graph,
+                     [&] { return REAL_HIP(hipStreamEndCapture_spt)(stream, graph); });
+}
+
+// ---- per-thread-default-stream copies and fills ---------------------------------------
+// The same staging / repair as their legacy-stream forms, on the thread's stream.
+__attribute__((visibility("default"))) hipError_t hipMemcpy_spt(void* dst, const void* src, size_t n,
+                                                                hipMemcpyKind kind) {
+  HookScope hook_scope;
+  ensure_init();
+  return copy_sync(dst, src, n, kind, hipStreamPerThread,
+                   [](void* d, const void* s, size_t c, hipMemcpyKind k, hipStream_t) {
+                     return REAL_HIP(hipMemcpy_spt)(d, s, c, k);
+                   });
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpyAsync_spt(void* dst, const void* src, size_t n,
+                                                                     hipMemcpyKind kind, hipStream_t stream) {
+  HookScope hook_scope;
+  ensure_init();
+  const hipStream_t st = stream ? stream : hipStreamPerThread;
+  hipError_t rc;
+  if (staged_copy(dst, src, n, kind, st, &rc)) return rc;
+  return after_async_copy(REAL_HIP(hipMemcpyAsync_spt)(dst, src, n, kind, stream), dst, src, n, kind, st);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpy2D_spt(void* dst, size_t dpitch, const void* src,
+                                                                  size_t spitch, size_t width, size_t height,
+                                                                  hipMemcpyKind kind) {
+  HookScope hook_scope;
+  ensure_init();
+  hipError_t rc;
+  if (staged_copy2d(dst, dpitch, src, spitch, width, height, kind, hipStreamPerThread, &rc)) {
+    if (rc == hipSuccess) rc = REAL_HIP(hipStreamSynchronize)(hipStreamPerThread);
+    return rc;
+  }
+  rc = REAL_HIP(hipMemcpy2D_spt)(dst, dpitch, src, spitch, width, height, kind);
+  return after_sync_copy(rc, dst, src, std::max(span2d(dpitch, width, height), span2d(spitch, width, height)), kind);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpy2DAsync_spt(void* dst, size_t dpitch, const void* src,
+                                                                       size_t spitch, size_t width, size_t height,
+                                                                       hipMemcpyKind kind, hipStream_t stream) {
+  HookScope hook_scope;
+  ensure_init();
+  const hipStream_t st = stream ? stream : hipStreamPerThread;
+  hipError_t rc;
+  if (staged_copy2d(dst, dpitch, src, spitch, width, height, kind, st, &rc)) return rc;
+  rc = REAL_HIP(hipMemcpy2DAsync_spt)(dst, dpitch, src, spitch, width, height, kind, stream);
+  return after_async_copy(rc, dst, src, std::max(span2d(dpitch, width, height), span2d(spitch, width, height)), kind,
+                          st);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpy3D_spt(const hipMemcpy3DParms* p) {
+  HookScope hook_scope;
+  ensure_init();
+  return after3d(REAL_HIP(hipMemcpy3D_spt)(p), p, hipStreamPerThread, false);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpy3DAsync_spt(const hipMemcpy3DParms* p,
+                                                                       hipStream_t stream) {
+  HookScope hook_scope;
+  ensure_init();
+  return after3d(REAL_HIP(hipMemcpy3DAsync_spt)(p, stream), p, stream ? stream : hipStreamPerThread, true);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpyToSymbol_spt(const void* symbol, const void* src,
+                                                                        size_t n, size_t offset, hipMemcpyKind kind) {
+  HookScope hook_scope;
+  ensure_init();
+  return after_sync_copy(REAL_HIP(hipMemcpyToSymbol_spt)(symbol, src, n, offset, kind), nullptr, src, n, kind);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpyToSymbolAsync_spt(const void* symbol, const void* src,
+                                                                             size_t n, size_t offset,
+                                                                             hipMemcpyKind kind, hipStream_t stream) {
+  HookScope hook_scope;
+  ensure_init();
+  return after_async_copy(REAL_HIP(hipMemcpyToSymbolAsync_spt)(symbol, src, n, offset, kind, stream), nullptr, src,
+                          n, kind, stream ? stream : hipStreamPerThread);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpyFromSymbol_spt(void* dst, const void* symbol, size_t n,
+                                                                          size_t offset, hipMemcpyKind kind) {
+  HookScope hook_scope;
+  ensure_init();
+  return after_sync_copy(REAL_HIP(hipMemcpyFromSymbol_spt)(dst, symbol, n, offset, kind), dst, nullptr, n, kind);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemcpyFromSymbolAsync_spt(void* dst, const void* symbol,
+                                                                               size_t n, size_t offset,
+                                                                               hipMemcpyKind kind,
+                                                                               hipStream_t stream) {
+  HookScope hook_scope;
+  ensure_init();
+  return after_async_copy(REAL_HIP(hipMemcpyFromSymbolAsync_spt)(dst, symbol, n, offset, kind, stream), dst, nullptr,
+                          n, kind, stream ? stream : hipStreamPerThread);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemset_spt(void* dst, int value, size_t n) {
+  HookScope hook_scope;
+  ensure_init();
+  hipError_t rc;
+  if (staged_memset(dst, n, hipStreamPerThread, true, &rc, fill8((unsigned char)value))) return rc;
+  return after_memset(REAL_HIP(hipMemset_spt)(dst, value, n), dst, n);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemsetAsync_spt(void* dst, int value, size_t n,
+                                                                     hipStream_t stream) {
+  HookScope hook_scope;
+  ensure_init();
+  const hipStream_t st = stream ? stream : hipStreamPerThread;
+  hipError_t rc;
+  if (staged_memset(dst, n, st, false, &rc, fill8((unsigned char)value))) return rc;
+  return after_memset_async(REAL_HIP(hipMemsetAsync_spt)(dst, value, n, stream), dst, n, st);
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemset2D_spt(void* dst, size_t pitch, int v, size_t width,
+                                                                  size_t height) {
+  HookScope hook_scope;
+  ensure_init();
+  return after_memset(REAL_HIP(hipMemset2D_spt)(dst, pitch, v, width, height), dst, span2d(pitch, width, height));
+}
+
+__attribute__((visibility("default"))) hipError_t hipMemset2DAsync_spt(void* dst, size_t pitch, int v, size_t width,
+                                                                       size_t height, hipStream_t stream) {
+  HookScope hook_scope;
+  ensure_init();
+  return after_memset_async(REAL_HIP(hipMemset2DAsync_spt)(dst, pitch, v, width, height, stream), dst,
+                            span2d(pitch, width, height), stream ? stream : hipStreamPerThread);
+}
+
+}  // extern "C"
+
+// ---- C++-linkage module launches --------------------------------------------------------
+// Older hip_ext.h declared hipExtModuleLaunchKernel / hipHccModuleLaunchKernel
+// without extern "C"; libamdhip64 still exports those mangled names, and a
+// binary built against that header calls them, not the C entry points.
+using CxxExtModuleLaunch = hipError_t (*)(hipFunction_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t,
+                                          size_t, hipStream_t, void**, void**, hipEvent_t, hipEvent_t, uint32_t);
+using CxxHccModuleLaunch = hipError_t (*)(hipFunction_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t,
+                                          size_t, hipStream_t, void**, void**, hipEvent_t, hipEvent_t);
+#define VGPU_CXX_EXT_LAUNCH "_Z24hipExtModuleLaunchKernelP18ihipModuleSymbol_tjjjjjjmP12ihipStream_tPPvS4_P11ihipEvent_tS6_j"
+#define VGPU_CXX_HCC_LAUNCH "_Z24hipHccModuleLaunchKernelP18ihipModuleSymbol_tjjjjjjmP12ihipStream_tPPvS4_P11ihipEvent_tS6_"
+
+extern "C" __attribute__((visibility("default"))) hipError_t vgpu_cxx_ext_module_launch(
+    hipFunction_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, size_t, hipStream_t, void**, void**,
+    hipEvent_t, hipEvent_t, uint32_t) __asm__(VGPU_CXX_EXT_LAUNCH);
+extern "C" hipError_t vgpu_cxx_ext_module_launch(hipFunction_t f, uint32_t gwx, uint32_t gwy, uint32_t gwz,
+                                                 uint32_t lwx, uint32_t lwy, uint32_t lwz, size_t shmem,
+                                                 hipStream_t stream, void** params, void** extra, hipEvent_t start,
+                                                 hipEvent_t stop, uint32_t flags) {
+  return module_launch_wi(gwx, gwy, gwz, lwx, lwy, lwz, stream, params, extra, [&] {
+    auto real = REAL_HIP_NAMED(CxxExtModuleLaunch, VGPU_CXX_EXT_LAUNCH);
+    return real ? real(f, gwx, gwy, gwz, lwx, lwy, lwz, shmem, stream, params, extra, start, stop, flags)
+                : hipErrorNotSupported;
+  });
+}
+
+extern "C" __attribute__((visibility("default"))) hipError_t vgpu_cxx_hcc_module_launch(
+    hipFunction_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, size_t, hipStream_t, void**, void**,
+    hipEvent_t, hipEvent_t) __asm__(VGPU_CXX_HCC_LAUNCH);
+extern "C" hipError_t vgpu_cxx_hcc_module_launch(hipFunction_t f, uint32_t gwx, uint32_t gwy, uint32_t gwz,
+                                                 uint32_t lwx, uint32_t lwy, uint32_t lwz, size_t shmem,
+                                                 hipStream_t stream, void** params, void** extra, hipEvent_t start,
+                                                 hipEvent_t stop) {
+  return module_launch_wi(gwx, gwy, gwz, lwx, lwy, lwz, stream, params, extra, [&] {
+    auto real = REAL_HIP_NAMED(CxxHccModuleLaunch, VGPU_CXX_HCC_LAUNCH);
+    return real ? real(f, gwx, gwy, gwz, lwx, lwy, lwz, shmem, stream, params, extra, start, stop)
+                : hipErrorNotSupported;
+  });
+}
+
+extern "C" {
 
 // hipGetProcAddress must hand out our hooks too, or a runtime-resolved call
 // would bypass the ledger.
@@ -1464,6 +1941,47 @@ __attribute__((visibility("default"))) hipError_t hipGetProcAddress(const char* 
   if (rc != hipSuccess || !symbol || !pfn || !*pfn) return rc;
   if (void* mine = own_hook(symbol)) *pfn = mine;
   return rc;
+}
+
+// The CUDA-style driver entry-point queries hand out function pointers too
+// (reference cuGetProcAddress 776 B, _v2 794 B).
+using GetDriverEntryPoint = hipError_t (*)(const char*, void**, unsigned long long, hipDriverEntryPointQueryResult*);
+
+__attribute__((visibility("default"))) hipError_t hipGetDriverEntryPoint(const char* symbol, void** pfn,
+                                                                         unsigned long long flags,
+                                                                         hipDriverEntryPointQueryResult* status) {
+  auto real = REAL_HIP_NAMED(GetDriverEntryPoint, "hipGetDriverEntryPoint");
+  if (!real) return hipErrorNotSupported;
+  hipError_t rc = real(symbol, pfn, flags, status);
+  if (rc != hipSuccess || !symbol || !pfn || !*pfn) return rc;
+  if (void* mine = own_hook(symbol)) *pfn = mine;
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipGetDriverEntryPoint_spt(const char* symbol, void** pfn,
+                                                                             unsigned long long flags,
+                                                                             hipDriverEntryPointQueryResult* status) {
+  auto real = REAL_HIP_NAMED(GetDriverEntryPoint, "hipGetDriverEntryPoint_spt");
+  if (!real) return hipErrorNotSupported;
+  hipError_t rc = real(symbol, pfn, flags, status);
+  if (rc != hipSuccess || !symbol || !pfn || !*pfn) return rc;
+  // A per-thread-stream lookup of "hipLaunchKernel" resolves to its _spt form.
+  char spt[160];
+  void* mine = nullptr;
+  if (strlen(symbol) + 5 < sizeof spt) {
+    snprintf(spt, sizeof spt, "%s_spt", symbol);
+    mine = own_hook(spt);
+  }
+  if (!mine) mine = own_hook(symbol);
+  if (mine) *pfn = mine;
+  return rc;
+}
+
+__attribute__((visibility("default"))) hipError_t hipStreamSynchronize_spt(hipStream_t stream) {
+  limiter_flush_thread();
+  using F = hipError_t (*)(hipStream_t);
+  auto real = REAL_HIP_NAMED(F, "hipStreamSynchronize_spt");
+  return real ? real(stream) : hipErrorNotSupported;
 }
 
 }  // extern "C"

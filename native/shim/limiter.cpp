@@ -391,7 +391,7 @@ bool stream_capturing(hipStream_t stream) {
 void recycle_event(Track* t, hipEvent_t ev) {
   const uint32_t fh = t->fhead.load(std::memory_order_relaxed);
   if (fh - t->ftail.load(std::memory_order_acquire) >= kRing) {
-    REAL_HIP(hipEventDestroy)(ev);
+    (void)REAL_HIP(hipEventDestroy)(ev);
     return;
   }
   t->fring[fh & kMask] = ev;
@@ -400,8 +400,8 @@ void recycle_event(Track* t, hipEvent_t ev) {
 
 void free_track(Track* t) {
   const uint32_t fh = t->fhead.load(std::memory_order_acquire);
-  for (uint32_t i = t->ftail.load(std::memory_order_acquire); i != fh; ++i) REAL_HIP(hipEventDestroy)(t->fring[i & kMask]);
-  if (t->spare) REAL_HIP(hipEventDestroy)(t->spare);
+  for (uint32_t i = t->ftail.load(std::memory_order_acquire); i != fh; ++i) (void)REAL_HIP(hipEventDestroy)(t->fring[i & kMask]);
+  if (t->spare) (void)REAL_HIP(hipEventDestroy)(t->spare);
   delete t;
 }
 
@@ -695,8 +695,8 @@ int occ_open(int dev, DevLimiter& L, uint64_t now) {
 // interval whole when its marker completes, so a replay longer than the window
 // is neither charged twice nor missing from the window it ran in).
 // Windows in which this process made launches the markers deliberately do not
-// charge (RCCL kernels and graphs, launches while the monitor reports no
-// contention) are skipped: occupancy cannot tell that work from the rest.
+// charge (launches while the monitor reports no contention) are skipped:
+// occupancy cannot tell that work from the rest.
 void occ_step(int dev, DevLimiter& L, uint64_t now) {
   const uint64_t period = occ_period_ns();
   if (!period) return;
@@ -866,9 +866,9 @@ void note_untracked(DevLimiter& L) {
 
 }  // namespace
 
-// Collective kernels (RCCL) are exempt from the temporal limiter: every rank's
-// kernel must be resident for a collective to progress, so throttling one
-// rank's launches stalls the others (distributed backend row;
+// Collective kernels (RCCL) are never held by the temporal limiter (they are
+// still charged): every rank's kernel must be resident for a collective to
+// progress, so holding one rank's launch mid-step stalls the others (distributed backend row;
 // §7.4 item 8).  A kernel is RCCL's when its host stub lives in librccl (or a
 // library matching VGPU_THROTTLE_EXEMPT).  Decided once per function pointer
 // and launching thread: the cache is thread-local, so a throttled launch takes
@@ -942,6 +942,7 @@ void limiter_after_fork() {
   }
 }
 
+// `collective`: the launch is a collective's (never held, always charged).
 bool limiter_on_launch(int dev, uint64_t wg, const void* fn, uint32_t kernels, bool collective) {
   State& s = st();
   if (!s.enabled) return false;
@@ -966,16 +967,17 @@ bool limiter_on_launch(int dev, uint64_t wg, const void* fn, uint32_t kernels, b
   if (!throttling || !ok_dev) return false;
   DevLimiter& L = g_lim[dev];
   if (!L.active) return false;
-  if (exempt) {
-    note_untracked(L);
-    return false;
-  }
   if (__builtin_expect(L.pool_scale_pending.load(std::memory_order_relaxed), 0)) apply_pool_scale(dev, L);
   if (s.region && s.lim.core_policy != 1 &&
       __atomic_load_n(&s.region->utilization_switch, __ATOMIC_RELAXED) == 0) {
     note_untracked(L);
     return false;  // monitor says no contention: run unthrottled
   }
+  // An eager collective kernel is never held (its peers would wait on it) but
+  // is charged like any launch: its marker's GPU time is paid by the next
+  // held launch of the pod (an exemption from the charge let a
+  // pod's collective time escape its cap).
+  if (exempt) return true;
   // VGPU_LIMITER_DRYRUN=1: measure and charge, never wait (diagnostics).
   static const bool dryrun = env_bool(env_first("VGPU_LIMITER_DRYRUN"), false);
   if (dryrun) return true;

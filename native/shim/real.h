@@ -122,6 +122,7 @@ using hipStreamBeginCaptureToGraph = hipError_t (*)(hipStream_t, hipGraph_t, con
 using hipStreamEndCapture = hipError_t (*)(hipStream_t, hipGraph_t*);
 using hipStreamGetCaptureInfo = hipError_t (*)(hipStream_t, hipStreamCaptureStatus*, unsigned long long*);
 using hipGraphDestroy = hipError_t (*)(hipGraph_t);
+using hipGraphClone = hipError_t (*)(hipGraph_t*, hipGraph_t);
 using hipGraphAddKernelNode = hipError_t (*)(hipGraphNode_t*, hipGraph_t, const hipGraphNode_t*, size_t,
                                              const hipKernelNodeParams*);
 using hipGraphKernelNodeSetParams = hipError_t (*)(hipGraphNode_t, const hipKernelNodeParams*);
@@ -194,6 +195,40 @@ using hipMemPrefetchAsync_v2 = hipError_t (*)(const void*, size_t, hipMemLocatio
 using hipMemGetAddressRange = hipError_t (*)(hipDeviceptr_t*, size_t*, hipDeviceptr_t);
 using hipGetProcAddress = hipError_t (*)(const char*, void**, int, uint64_t,
                                          hipDriverProcAddressQueryResult*);
+using hipMemAllocPitch = hipError_t (*)(hipDeviceptr_t*, size_t*, size_t, size_t, unsigned int);
+using hipMemAllocHost = hipError_t (*)(void**, size_t);
+using hipLaunchKernel_spt = hipError_t (*)(const void*, dim3, dim3, void**, size_t, hipStream_t);
+using hipLaunchCooperativeKernel_spt = hipError_t (*)(const void*, dim3, dim3, void**, uint32_t, hipStream_t);
+using hipGraphLaunch_spt = hipError_t (*)(hipGraphExec_t, hipStream_t);
+using hipDrvLaunchKernelEx = hipError_t (*)(const HIP_LAUNCH_CONFIG*, hipFunction_t, void**, void**);
+using hipHccModuleLaunchKernel = hipError_t (*)(hipFunction_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t,
+                                                uint32_t, size_t, hipStream_t, void**, void**, hipEvent_t,
+                                                hipEvent_t);
+using hipExtLaunchMultiKernelMultiDevice = hipError_t (*)(hipLaunchParams*, int, unsigned int);
+using hipLaunchCooperativeKernelMultiDevice = hipError_t (*)(hipLaunchParams*, int, unsigned int);
+using hipModuleLaunchCooperativeKernelMultiDevice = hipError_t (*)(hipFunctionLaunchParams*, unsigned int,
+                                                                   unsigned int);
+using hipConfigureCall = hipError_t (*)(dim3, dim3, size_t, hipStream_t);
+using hipLaunchByPtr = hipError_t (*)(const void*);
+using hipStreamBeginCapture_spt = hipError_t (*)(hipStream_t, hipStreamCaptureMode);
+using hipStreamEndCapture_spt = hipError_t (*)(hipStream_t, hipGraph_t*);
+using hipMemcpy_spt = hipError_t (*)(void*, const void*, size_t, hipMemcpyKind);
+using hipMemcpyAsync_spt = hipError_t (*)(void*, const void*, size_t, hipMemcpyKind, hipStream_t);
+using hipMemset_spt = hipError_t (*)(void*, int, size_t);
+using hipMemsetAsync_spt = hipError_t (*)(void*, int, size_t, hipStream_t);
+using hipMemcpy2D_spt = hipError_t (*)(void*, size_t, const void*, size_t, size_t, size_t, hipMemcpyKind);
+using hipMemcpy2DAsync_spt = hipError_t (*)(void*, size_t, const void*, size_t, size_t, size_t, hipMemcpyKind,
+                                            hipStream_t);
+using hipMemcpy3D_spt = hipError_t (*)(const hipMemcpy3DParms*);
+using hipMemcpy3DAsync_spt = hipError_t (*)(const hipMemcpy3DParms*, hipStream_t);
+using hipMemset2D_spt = hipError_t (*)(void*, size_t, int, size_t, size_t);
+using hipMemset2DAsync_spt = hipError_t (*)(void*, size_t, int, size_t, size_t, hipStream_t);
+using hipMemcpyToSymbol_spt = hipError_t (*)(const void*, const void*, size_t, size_t, hipMemcpyKind);
+using hipMemcpyToSymbolAsync_spt = hipError_t (*)(const void*, const void*, size_t, size_t, hipMemcpyKind,
+                                                  hipStream_t);
+using hipMemcpyFromSymbol_spt = hipError_t (*)(void*, const void*, size_t, size_t, hipMemcpyKind);
+using hipMemcpyFromSymbolAsync_spt = hipError_t (*)(void*, const void*, size_t, size_t, hipMemcpyKind,
+                                                    hipStream_t);
 }  // namespace fnt
 }  // namespace vgpu
 
@@ -209,4 +244,6 @@ using hipGetProcAddress = hipError_t (*)(const char*, void**, int, uint64_t,
   }())
 // REAL_HIP(hipMalloc)(args...) calls the next definition of hipMalloc.
 #define REAL_HIP(fn) VGPU_REAL_IMPL(hip_lib_handle, ::vgpu::fnt::fn, #fn)
+// A runtime entry point exported under another (e.g. C++-mangled) name.
+#define REAL_HIP_NAMED(T, name) VGPU_REAL_IMPL(hip_lib_handle, T, name)
 #define REAL_HSA(fn) VGPU_REAL_IMPL(hsa_lib_handle, decltype(&::fn), #fn)

@@ -107,10 +107,11 @@ void limiter_stop();        // exit: stop the limiter thread, release the share 
 void limiter_after_fork();
 // Called before every dispatch with the number of workgroups it launches;
 // blocks while the temporal limiter's bucket is overdrawn.  `fn` = the
-// kernel's host stub when known (RCCL kernels are exempt from throttling).
+// kernel's host stub when known (RCCL kernels are never held, only charged).
 // Returns true when the launch must be tracked: call limiter_track after the
-// launch on `stream` with its result.  collective: a graph with RCCL kernel
-// nodes (exempt like an eager RCCL kernel: never held, never charged).
+// launch on `stream` with its result.  collective: the caller knows the launch
+// is a collective's (never held, charged like any launch).  Graphs are held
+// before their replay whatever their nodes are (a step boundary).
 bool limiter_on_launch(int dev, uint64_t workgroups, const void* fn = nullptr, uint32_t kernels = 1,
                        bool collective = false);
 // The kernel whose host stub is `fn` is a collective's (its library is RCCL's,
@@ -217,6 +218,7 @@ bool vmm_wanted(int dev, uint64_t size);
 hipError_t vmm_alloc(void** ptr, size_t size, int dev);
 bool vmm_free(void* p);                 // unmap + release + free the VA; false if not ours
 bool vmm_owns(const void* p);
+int vmm_owner_dev(const void* p);       // device of the range starting at p, -1 if none
 void vmm_ipc_exported(const void* p);   // never evict a range another process may map
 void vmm_stats(uint64_t out[8]);  // ranges, bytes, evicted bytes, suspend ns, resume ns, cycles, pin ns, map ns
 void vmm_after_fork();

@@ -401,6 +401,13 @@ bool vmm_free(void* p) {
   return true;
 }
 
+int vmm_owner_dev(const void* p) {
+  if (!g_vmm_live.load(std::memory_order_relaxed) || !p) return -1;
+  std::lock_guard<std::mutex> l(g_mu);
+  auto it = g_ranges.find((uintptr_t)p);
+  return it == g_ranges.end() ? -1 : it->second.dev;
+}
+
 bool vmm_owns(const void* p) {
   if (!g_vmm_live.load(std::memory_order_relaxed) || !p) return false;
   std::lock_guard<std::mutex> l(g_mu);

@@ -80,6 +80,58 @@ def test_cross_entropy_matches_torch(gpu_build, dtype, rows, c):
     torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("rows,c,ignore", [(50, 1000, -100), (100, 1000, 7), (300, 21, 255), (7, 2, -100)])
+def test_cross_entropy_ignore_index_matches_torch(gpu_build, dtype, rows, c, ignore):
+    """targets equal to ignore_index (or outside [0, C)) drop their
+    row from the loss, the mean and the gradient, as in F.cross_entropy."""
+    from vgpu.ops.loss import cross_entropy
+    g = torch.Generator().manual_seed(rows + c)
+    x = (torch.randn(rows, c, generator=g) * 3).to(dtype).cuda().requires_grad_()
+    t = torch.randint(0, c, (rows,), generator=g)
+    t[::3] = ignore if ignore >= c or ignore < 0 else t[::3]
+    if 0 <= ignore < c:
+        t[1::4] = ignore
+    t = t.cuda()
+    loss = cross_entropy(x, t, ignore_index=ignore)
+    (loss * 2.0).backward()
+    xr = x.detach().float().requires_grad_()
+    lr = torch.nn.functional.cross_entropy(xr, t, ignore_index=ignore)
+    (lr * 2.0).backward()
+    torch.testing.assert_close(loss, lr, atol=1e-4, rtol=1e-4)
+    tol = dict(atol=2e-3, rtol=2e-2) if dtype == torch.bfloat16 else dict(atol=1e-6, rtol=1e-4)
+    torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["channels_last", "nchw"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_pixelwise_cross_entropy_matches_torch(gpu_build, layout, dtype):
+    """DeepLab's per-pixel loss (nll_loss2d was ~224 us a step)
+    read in place from [B, 21, H, W] logits in either layout, with PyTorch's
+    ignore_index=255 convention for void pixels: loss and gradient against
+    F.cross_entropy on the fp32 logits."""
+    from vgpu.ops.loss import cross_entropy
+    g = torch.Generator().manual_seed(5)
+    x = (torch.randn(2, 21, 33, 40, generator=g) * 2).to(dtype).cuda()
+    if layout == "channels_last":
+        x = x.contiguous(memory_format=torch.channels_last)
+    x.requires_grad_()
+    t = torch.randint(0, 21, (2, 33, 40), generator=g)
+    t[:, ::5, ::7] = 255
+    t = t.cuda()
+    loss = cross_entropy(x, t, ignore_index=255)
+    loss.backward()
+    assert x.grad.stride() == x.stride()
+    xr = x.detach().float().requires_grad_()
+    lr = torch.nn.functional.cross_entropy(xr, t, ignore_index=255)
+    lr.backward()
+    torch.testing.assert_close(loss, lr, atol=1e-4, rtol=1e-4)
+    tol = dict(atol=1e-4, rtol=2e-2) if dtype == torch.bfloat16 else dict(atol=1e-7, rtol=1e-4)
+    torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
+
+
 def _mlp(device, seed=0):
     torch.manual_seed(seed)
     m = torch.nn.Sequential(torch.nn.Linear(1032, 512), torch.nn.Linear(512, 200))

@@ -68,6 +68,44 @@ def test_ddp_grads_are_rank_average_and_replicas_agree():
         assert spread == 0.0, res
 
 
+def _unused_worker(rank: int, world: int, port: int, out):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from vgpu.parallel import ddp as D
+    D.setup("gloo")
+    torch.manual_seed(0)
+    used = torch.nn.Linear(8, 4)
+    aux = torch.nn.Linear(8, 4)  # an aux head this step never touches
+    grads = D.GradBuckets(list(used.parameters()) + list(aux.parameters()), bucket_mb=1)
+    x = torch.randn(3, 8, generator=torch.Generator().manual_seed(rank))
+    grads.begin()
+    used(x).square().sum().backward()
+    grads.finish()
+    g = torch.cat([p.grad.flatten() for p in used.parameters()])
+    allg = [torch.empty_like(g) for _ in range(world)]
+    dist.all_gather(allg, g)
+    out[rank] = (float((allg[0] - allg[1]).abs().max()), float(aux.weight.grad.abs().max()), len(grads.buckets))
+    dist.destroy_process_group()
+
+
+def test_ddp_unused_parameter_bucket_still_reduced():
+    """a bucket holding a parameter with no gradient this
+    step was never all-reduced, and the replicas silently diverged.  finish()
+    now reduces every bucket whose hooks did not all fire."""
+    world, port = 2, _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_unused_worker, args=(world, port, out), nprocs=world, join=True)
+        res = dict(out)
+    for rank in range(world):
+        spread, aux_grad, nb = res[rank]
+        assert nb == 1  # used and unused parameters share the bucket
+        assert spread == 0.0, res
+        assert aux_grad == 0.0
+
+
 def test_ddp_entry_point_under_torchrun():
     port = _free_port()
     env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1")

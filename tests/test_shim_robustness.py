@@ -112,3 +112,5 @@ def test_fork_join_graph_replays_under_one_hw_queue(native_build, san):
     assert "AddressSanitizer" not in err, err[-3000:]
     assert (o["instantiate"], o["launch"], o["branchy_refused"], o["fake_launches"]) == ("0", "0", "0", "5")
     assert (o["edges"], o["max_out"], o["max_in"]) == ("3", "1", "1")  # a chain
+    # the chain is a clone's; the application's graph keeps its fork/join
+    assert (o["app_edges"], o["app_max_out"], o["app_max_in"]) == ("4", "2", "2")

@@ -68,9 +68,9 @@ def build(args):
         from vgpu.ops.loss import cross_entropy
 
         def lossf(out, tgt):
-            # classification logits: one native pass for the loss and its gradient
-            # (vgpu.ops.loss); DeepLab's per-pixel loss stays on PyTorch
-            return cross_entropy(out, tgt) if out.dim() == 2 and not fp32 else torch_loss(out.float(), tgt)
+            # one native pass for the loss and its gradient (vgpu.ops.loss):
+            # classification logits and DeepLab's per-pixel logits alike
+            return torch_loss(out.float(), tgt) if fp32 else cross_entropy(out, tgt)
 
         def step():
             opt.zero_grad(set_to_none=True)

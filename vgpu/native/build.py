@@ -219,7 +219,9 @@ def build_fakes(force: bool = False) -> dict[str, Path]:
     hip = FAKES_OUT / "libamdhip64.so.7"
     hip_extra = ("fake_hip_launches; fake_hip_launch_blocks; fake_hip_physical_used; fake_hip_graph_create; "
                  "fake_hip_exec_ns; fake_hip_svm_move; fake_hip_managed_gpu_bytes; fake_hip_host_touch_bytes; fake_hip_memsets; fake_hip_prefetch_overflows; fake_hip_peer_copies; "
-                 "fake_hip_branchy_single_queue_launches;")
+                 "fake_hip_branchy_single_queue_launches; fake_hip_exec_graph; "
+                 "_Z24hipExtModuleLaunchKernelP18ihipModuleSymbol_tjjjjjjmP12ihipStream_tPPvS4_P11ihipEvent_tS6_j; "
+                 "_Z24hipHccModuleLaunchKernelP18ihipModuleSymbol_tjjjjjjmP12ihipStream_tPPvS4_P11ihipEvent_tS6_;")
     if force or not _stamp(hip, [hip_src, hsa_src], hip_extra + str(sorted(versions.items()))[:4096]):
         vs = FAKES_OUT / "hip.map"
         vs.write_text(_version_script(hip_src, "hip_4.2", versions, hip_extra))

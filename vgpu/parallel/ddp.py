@@ -143,17 +143,28 @@ class GradBuckets:
         self.pending = [len(ps) for _, ps in self.buckets]
         self.works = []
 
+    def _reduce(self, b):
+        import torch.distributed as dist
+        view = self.buckets[b][0]
+        if self.world > 1:
+            view.mul_(1.0 / self.world)
+        self.works.append(dist.all_reduce(view, group=self.group, async_op=True))
+
     def _ready(self, p):
         b = self.bucket_of[id(p)]
         self.pending[b] -= 1
         if self.pending[b] == 0:
-            import torch.distributed as dist
-            view = self.buckets[b][0]
-            if self.world > 1:
-                view.mul_(1.0 / self.world)
-            self.works.append(dist.all_reduce(view, group=self.group, async_op=True))
+            self._reduce(b)
 
     def finish(self):
+        # A parameter that got no gradient this step (an unused branch or aux
+        # head) never fired its hook: its bucket is reduced here, in bucket
+        # order on every rank, so no replica is left with an unreduced bucket
+        # (DDP's find_unused_parameters in effect).
+        for b, left in enumerate(self.pending):
+            if left > 0:
+                self.pending[b] = 0
+                self._reduce(b)
         for w in self.works:
             w.wait()
         self.works = []
