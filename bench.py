@@ -15,7 +15,8 @@ own, and keep the faster (vgpu/deviceplugin/custate.py).  `mask` gives every pod
 an XCD-balanced CU mask; `temporal` only time-shares.
 
 Launch: ``python bench.py --gpus N --steps K --warmup W`` (N>1 under
-torch.distributed.run, one rank per GPU).  Each rank spawns its pods BEFORE
+torch.distributed.run, one rank per GPU; started without one, bench.py starts
+it as a child process and refuses to run on fewer than N visible GPUs).  Each rank spawns its pods BEFORE
 touching the GPU itself (it never does), runs W untimed warmup steps in every
 pod, then a cross-rank barrier, then exactly K timed steps in every pod
 concurrently (each pod synchronizes its device before reporting ready and after
@@ -284,8 +285,48 @@ def rccl_check(pg, rank: int, world: int, pod, log) -> dict | None:
     return out
 
 
+def visible_gpu_count(cpu_smoke: bool) -> int | None:
+    """GPUs this process may use, without initialising the GPU runtime: the
+    visible-device list if one is set, else the driver's device count (not an
+    initialisation on this image).  None in a CPU rehearsal with no list."""
+    for var in ("VGPU_BENCH_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None and v.strip():
+            return len({s.strip() for s in v.split(",") if s.strip()})
+    if cpu_smoke:
+        return None
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_ranks(argv: list[str], n: int, cpu_smoke: bool) -> int:
+    """`python bench.py --gpus N` without an outer torch.distributed.run
+    (VERDICT r5 missing #3): start one rank per GPU as a child
+    `torch.distributed.run --nproc-per-node N bench.py ...` -- this process
+    never touches a GPU -- relay its output (rank 0's one JSON line) and exit
+    with its code.  Refuse when fewer than N distinct GPUs are visible rather
+    than measure fewer."""
+    import socket
+    import subprocess
+    have = visible_gpu_count(cpu_smoke)
+    if have is not None and have < n:
+        log(f"--gpus {n}: only {have} distinct GPU(s) visible; refusing to report fewer")
+        return 3
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    log(f"--gpus {n}: one rank per GPU: {' '.join(cmd[2:])}")
+    return subprocess.run(cmd, cwd=os.path.dirname(os.path.abspath(__file__))).returncode
+
+
 def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     args = make_parser().parse_args(argv)
+    if args.gpus > 1 and args.pod_gpus == 0 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(argv, args.gpus, args.cpu_smoke)
     if args.cpu_smoke:
         os.environ["VGPU_BENCH_CPU"] = "1"
         args.no_shim = True
@@ -297,8 +338,9 @@ def main(argv=None) -> int:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        log(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}")
+    if world != args.gpus:
+        log(f"WORLD_SIZE={world} but --gpus={args.gpus}: refusing to measure a different GPU count")
+        return 3
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from vgpu.native import ensure_built
