@@ -165,6 +165,33 @@ VGPU_API int vgpu_busy(float* sink, uint32_t blocks, uint32_t iters, void* strea
   return (int)hipGetLastError();
 }
 
+// The same busy kernel launched through another runtime entry point (GPU
+// tests of the enforcement library's hooks): 1 = hipLaunchKernel_spt (what
+// -fgpu-default-stream=per-thread code calls), 2 = a one-entry
+// hipExtLaunchMultiKernelMultiDevice.
+VGPU_API int vgpu_busy_via(float* sink, uint32_t blocks, uint32_t iters, void* stream, int path) {
+  if (!sink || blocks == 0) return (int)hipErrorInvalidValue;
+  void* args[] = {&sink, &iters};
+  if (path == 1)
+    return (int)hipLaunchKernel_spt((const void*)busy_kernel, dim3(blocks), dim3(kThreads), args, 0,
+                                    (hipStream_t)stream);
+  if (path == 2) {
+    // the multi-device launch wants a real stream per entry (not the null stream)
+    static hipStream_t own = nullptr;
+    if (!stream && !own && hipStreamCreateWithFlags(&own, hipStreamNonBlocking) != hipSuccess) return -1;
+    if (!stream) stream = own;
+    hipLaunchParams p{};
+    p.func = (void*)busy_kernel;
+    p.gridDim = dim3(blocks);
+    p.blockDim = dim3(kThreads);
+    p.args = args;
+    p.sharedMem = 0;
+    p.stream = (hipStream_t)stream;
+    return (int)hipExtLaunchMultiKernelMultiDevice(&p, 1, 0);
+  }
+  return (int)hipLaunchKernel((const void*)busy_kernel, dim3(blocks), dim3(kThreads), args, 0, (hipStream_t)stream);
+}
+
 VGPU_API int vgpu_gather_pages(void* dst, const void* src, const int64_t* idx, uint64_t page_bytes,
                                uint64_t npages, void* stream) {
   if (page_bytes % 16 || !dst || !src || !idx) return (int)hipErrorInvalidValue;

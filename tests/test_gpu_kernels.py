@@ -62,12 +62,16 @@ def test_census_reports_valid_ids(K):
     assert bool((ticks >= 1000).all())
 
 
-@pytest.mark.parametrize("b,t,e,layers", [(37, 64, 300, 2), (100, 48, 128, 1)])
-def test_fused_lstm_matches_fp32(gpu_build, b, t, e, layers):
+@pytest.mark.parametrize("wave", ["1", "0"])
+@pytest.mark.parametrize("b,t,e,layers", [(37, 64, 300, 2), (100, 48, 128, 1), (140, 33, 300, 2)])
+def test_fused_lstm_matches_fp32(gpu_build, monkeypatch, wave, b, t, e, layers):
     """native/kernels/lstm.hip (+ input-projection GEMM) against torch.nn.LSTM in
     fp32 on the same bf16-rounded weights and inputs; B = 37 leaves a partial
-    16-row slice."""
+    16-row slice, B = 140 spans two wavefront placement groups (9 row blocks).
+    wave=1: a 2-layer stack as one wavefront launch (layer 2 a few steps behind
+    layer 1, its input projection inside the kernel); wave=0: layer by layer."""
     import torch
+    monkeypatch.setenv("VGPU_LSTM_WAVE", wave)
     from vgpu.ops import lstm as fused
     torch.manual_seed(0)
     ref = torch.nn.LSTM(e, 128, num_layers=layers, batch_first=True).cuda()
@@ -81,11 +85,14 @@ def test_fused_lstm_matches_fp32(gpu_build, b, t, e, layers):
     torch.testing.assert_close(got, want, atol=3e-2, rtol=3e-2)
 
 
-def test_fused_lstm_training_grads_match_fp32(gpu_build):
-    """Forward + backward-through-time kernels (LSTMLayerFn) against
-    torch.nn.LSTM in fp32 on the same bf16-rounded weights: the loss, every
-    weight / bias gradient, and the input gradient of a 2-layer stack."""
+@pytest.mark.parametrize("wave", ["1", "0"])
+def test_fused_lstm_training_grads_match_fp32(gpu_build, monkeypatch, wave):
+    """Forward + backward-through-time kernels (LSTM2Fn wavefront, or
+    LSTMLayerFn per layer) against torch.nn.LSTM in fp32 on the same
+    bf16-rounded weights: every weight / bias gradient, and the input gradient
+    of a 2-layer stack."""
     import torch
+    monkeypatch.setenv("VGPU_LSTM_WAVE", wave)
     from vgpu.ops import lstm as fused
     torch.manual_seed(1)
     b, t, e = 10, 40, 300

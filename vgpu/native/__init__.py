@@ -51,6 +51,7 @@ def load_kernels() -> ctypes.CDLL:
     vp, u32, u64, i64p = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p
     lib.vgpu_census.argtypes = [vp, u32, u64, vp, vp]
     lib.vgpu_busy.argtypes = [vp, u32, u32, vp]
+    lib.vgpu_busy_via.argtypes = [vp, u32, u32, vp, ctypes.c_int]
     lib.vgpu_gather_pages.argtypes = [vp, vp, i64p, u64, u64, vp]
     lib.vgpu_scatter_pages.argtypes = [vp, vp, i64p, u64, u64, vp]
     lib.vgpu_fill_pattern.argtypes = [vp, u64, u32, vp]
@@ -98,6 +99,17 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_lstm_forward_train.restype = ci
     lib.vgpu_lstm_backward.argtypes = [vp] * 5 + [ci, ci, ci, vp]
     lib.vgpu_lstm_backward.restype = ci
+    i64 = ctypes.c_int64
+    lib.vgpu_lstm_recurrence_window.argtypes = [vp, vp, vp, i64, i64, vp, vp, ci, vp, vp, ci, ci, ci, vp, vp]
+    lib.vgpu_lstm_recurrence_window.restype = ci
+    lib.vgpu_lstm_backward_window.argtypes = [vp, vp, vp, i64, i64, vp, vp, vp, vp, ci, ci, ci, ci, vp]
+    lib.vgpu_lstm_backward_window.restype = ci
+    lib.vgpu_lstm2_forward.argtypes = [vp] * 14 + [ci, ci, ci, vp]
+    lib.vgpu_lstm2_forward.restype = ci
+    lib.vgpu_lstm2_backward.argtypes = [vp] * 12 + [ci, ci, ci, vp]
+    lib.vgpu_lstm2_backward.restype = ci
+    lib.vgpu_lstm2_flags_error.argtypes = [vp, ci]
+    lib.vgpu_lstm2_flags_error.restype = ci
     lib.vgpu_scale_shift_relu_mean_nhwc.argtypes = [vp, vp, vp, vp, ci, ci, ci, vp]
     i64, cf = ctypes.c_int64, ctypes.c_float
     lib.vgpu_bn_workspace.argtypes = [i64, ci]
@@ -134,7 +146,7 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_wt_flip_batched.argtypes = [vp, ci, ci, vp]
     lib.vgpu_wt_flip_batched.restype = ci
     lib.vgpu_wt_desc_size.restype = ci
-    for f in ("vgpu_bn_act_fwd_train", "vgpu_bn_act_bwd","vgpu_census", "vgpu_busy", "vgpu_gather_pages", "vgpu_scatter_pages",
+    for f in ("vgpu_bn_act_fwd_train", "vgpu_bn_act_bwd","vgpu_census", "vgpu_busy", "vgpu_busy_via", "vgpu_gather_pages", "vgpu_scatter_pages",
               "vgpu_fill_pattern", "vgpu_verify_pattern", "vgpu_kernels_abi_version",
               "vgpu_bias_act_nhwc", "vgpu_scale_shift_act_nhwc", "vgpu_add_scale_shift_act_nhwc",
               "vgpu_conv2d_nhwc", "vgpu_maxpool_nhwc", "vgpu_stem_pool_nhwc",

@@ -44,6 +44,13 @@ def busy(blocks: int, iters: int) -> None:
     _check(load_kernels().vgpu_busy(sink.data_ptr(), blocks, iters, _stream()), "vgpu_busy")
 
 
+def busy_via(blocks: int, iters: int, path: int) -> None:
+    """busy() launched through hipLaunchKernel_spt (path 1) or a one-entry
+    hipExtLaunchMultiKernelMultiDevice (path 2); 0 = hipLaunchKernel."""
+    sink = torch.empty(256, dtype=torch.float32, device="cuda")
+    _check(load_kernels().vgpu_busy_via(sink.data_ptr(), blocks, iters, _stream(), path), "vgpu_busy_via")
+
+
 def gather_pages(dst: torch.Tensor, src: torch.Tensor, idx: torch.Tensor, page_bytes: int) -> None:
     """dst[k] = src[idx[k]] for pages of `page_bytes` (dst packed, src scattered)."""
     assert idx.dtype == torch.int64 and idx.is_cuda

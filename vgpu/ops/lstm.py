@@ -1,6 +1,9 @@
 """Fused LSTM: one input-projection GEMM per layer (hipBLASLt) plus one
 persistent recurrence kernel per layer (native/kernels/lstm.hip), instead of
-MIOpen's per-timestep kernel sequence.  Inference (`lstm_last_hidden`) and
+MIOpen's per-timestep kernel sequence.  A 2-layer stack (the ai-benchmark
+shape) runs both layers as one wavefront launch -- layer 2 a few steps behind
+layer 1, its input projection computed inside the kernel -- in the forward and,
+in time-reverse order, in the backward (VGPU_LSTM_WAVE=0: layer by layer).  Inference (`lstm_last_hidden`) and
 training (`LSTMLayerFn`: forward keeps the activated gates and cells, backward is
 one backward-through-time kernel plus three GEMMs for the weight and input
 gradients).  Hidden size 128 (the ai-benchmark LSTM-Sentiment shape)."""
@@ -18,6 +21,19 @@ def supported(lstm: torch.nn.LSTM, x: torch.Tensor, training: bool = False) -> b
             and not lstm.bidirectional and lstm.proj_size == 0 and lstm.bias and lstm.dropout == 0)
 
 
+def _wave(lstm: torch.nn.LSTM) -> bool:
+    """Two-layer stacks run as one wavefront launch (lstm2_forward_kernel); VGPU_LSTM_WAVE=0: layer by layer."""
+    return lstm.num_layers == 2 and os.environ.get("VGPU_LSTM_WAVE", "1") != "0"
+
+
+def _flags(b: int, device) -> torch.Tensor:
+    return torch.empty(2 * ((b + 15) // 16) + 1, dtype=torch.int32, device=device)
+
+
+def _p(t):
+    return t.data_ptr() if t is not None else None
+
+
 def lstm_last_hidden(lstm: torch.nn.LSTM, x: torch.Tensor) -> torch.Tensor:
     """h_T of the last layer, [B, H] — what LSTMSentiment reads (y[:, -1])."""
     from vgpu.native import load_kernels
@@ -25,6 +41,19 @@ def lstm_last_hidden(lstm: torch.nn.LSTM, x: torch.Tensor) -> torch.Tensor:
     b, t, _ = x.shape
     h = lstm.hidden_size
     stream = torch.cuda.current_stream().cuda_stream
+    if _wave(lstm):
+        w_ih1, w_hh1 = lstm.weight_ih_l0, lstm.weight_hh_l0.contiguous()
+        xp1 = torch.addmm(lstm.bias_ih_l0 + lstm.bias_hh_l0, x.transpose(0, 1).reshape(t * b, -1),
+                          w_ih1.t()).view(t, b, 4 * h)
+        b2 = (lstm.bias_ih_l1 + lstm.bias_hh_l1).contiguous()
+        y1t = torch.empty(t, b, h, dtype=x.dtype, device=x.device)
+        xp2 = torch.empty(t, b, 4 * h, dtype=x.dtype, device=x.device)
+        hlast = torch.empty(b, h, dtype=x.dtype, device=x.device)
+        rc = lib.vgpu_lstm2_forward(_p(xp1), _p(w_hh1), _p(lstm.weight_ih_l1.contiguous()), _p(b2),
+                                    _p(lstm.weight_hh_l1.contiguous()), _p(y1t), _p(xp2), _p(_flags(b, x.device)),
+                                    _p(hlast), None, None, None, None, None, b, t, h, stream)
+        _check(rc, "vgpu_lstm2_forward")
+        return hlast
     inp = x
     hlast = torch.empty(b, h, dtype=x.dtype, device=x.device)
     for layer in range(lstm.num_layers):
@@ -91,8 +120,68 @@ class LSTMLayerFn(torch.autograd.Function):
         return dx, dw_ih, dw_hh, db, db
 
 
+class LSTM2Fn(torch.autograd.Function):
+    """Both layers of a 2-layer stack, batch_first x [B, T, E] -> y2 [B, T, H]
+    (zero initial state), forward and backward each one wavefront launch
+    (lstm2_forward_kernel / lstm2_backward_kernel) plus the GEMMs around them:
+    layer 1's input projection, and the weight / input gradients."""
+
+    @staticmethod
+    def forward(ctx, x, w_ih1, w_hh1, b_ih1, b_hh1, w_ih2, w_hh2, b_ih2, b_hh2):
+        from vgpu.native import load_kernels
+        lib = load_kernels()
+        b, t, _ = x.shape
+        h = w_hh1.shape[1]
+        dev, dt = x.device, x.dtype
+        xt = x.transpose(0, 1).reshape(t * b, -1)  # [T*B, E], timestep-major
+        xp1 = torch.addmm(b_ih1 + b_hh1, xt, w_ih1.t()).view(t, b, 4 * h)
+        w_hh1, w_ih2, w_hh2 = w_hh1.contiguous(), w_ih2.contiguous(), w_hh2.contiguous()
+        y1t = torch.empty(t, b, h, dtype=dt, device=dev)
+        y2t = torch.empty(t, b, h, dtype=dt, device=dev)
+        xp2 = torch.empty(t, b, 4 * h, dtype=dt, device=dev)
+        gates1 = torch.empty(t, b, 4 * h, dtype=dt, device=dev)
+        gates2 = torch.empty_like(gates1)
+        cells1 = torch.empty(t, b, h, dtype=torch.float32, device=dev)
+        cells2 = torch.empty_like(cells1)
+        rc = lib.vgpu_lstm2_forward(_p(xp1), _p(w_hh1), _p(w_ih2), _p((b_ih2 + b_hh2).contiguous()), _p(w_hh2),
+                                    _p(y1t), _p(xp2), _p(_flags(b, dev)), None, _p(y2t), _p(gates1), _p(gates2),
+                                    _p(cells1), _p(cells2), b, t, h, torch.cuda.current_stream().cuda_stream)
+        _check(rc, "vgpu_lstm2_forward")
+        ctx.save_for_backward(xt, w_ih1, w_hh1, w_ih2, w_hh2, y1t, y2t, gates1, gates2, cells1, cells2)
+        return y2t.transpose(0, 1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from vgpu.native import load_kernels
+        lib = load_kernels()
+        xt, w_ih1, w_hh1, w_ih2, w_hh2, y1t, y2t, gates1, gates2, cells1, cells2 = ctx.saved_tensors
+        t, b, h = y1t.shape
+        dy = dy.to(y1t.dtype).contiguous()
+        dgates1 = torch.empty_like(gates1)
+        dgates2 = torch.empty_like(gates2)
+        dy1 = torch.empty_like(y1t)
+        _check(lib.vgpu_lstm2_backward(_p(gates1), _p(cells1), _p(gates2), _p(cells2), _p(dy), _p(w_hh1), _p(w_hh2),
+                                       _p(w_ih2), _p(dgates1), _p(dgates2), _p(dy1), _p(_flags(b, y1t.device)), b, t,
+                                       h, torch.cuda.current_stream().cuda_stream), "vgpu_lstm2_backward")
+
+        def grads(dgates, hs, inp):
+            # dW_hh = Σ_t dgates_tᵀ h_{t-1} (h_{-1} = 0), dW_ih = dgatesᵀ · input, db = Σ dgates
+            dg = dgates.view(t * b, 4 * h)
+            dw_hh = dgates[1:].reshape((t - 1) * b, 4 * h).t() @ hs[:-1].reshape((t - 1) * b, h) if t > 1 \
+                else torch.zeros(4 * h, h, dtype=dg.dtype, device=dg.device)
+            return dg, dg.t() @ inp, dw_hh, dg.float().sum(0).to(dg.dtype)
+
+        dg2, dw_ih2, dw_hh2, db2 = grads(dgates2, y2t, y1t.view(t * b, h))
+        dg1, dw_ih1, dw_hh1, db1 = grads(dgates1, y1t, xt)
+        dx = (dg1 @ w_ih1).view(t, b, -1).transpose(0, 1) if ctx.needs_input_grad[0] else None
+        return dx, dw_ih1, dw_hh1, db1, db1, dw_ih2, dw_hh2, db2, db2
+
+
 def lstm_forward_train(lstm: torch.nn.LSTM, x: torch.Tensor) -> torch.Tensor:
     """Output of the last layer [B, T, H], differentiable w.r.t. the LSTM weights."""
+    if _wave(lstm):
+        return LSTM2Fn.apply(x, lstm.weight_ih_l0, lstm.weight_hh_l0, lstm.bias_ih_l0, lstm.bias_hh_l0,
+                             lstm.weight_ih_l1, lstm.weight_hh_l1, lstm.bias_ih_l1, lstm.bias_hh_l1)
     y = x
     for layer in range(lstm.num_layers):
         y = LSTMLayerFn.apply(y, getattr(lstm, f"weight_ih_l{layer}"), getattr(lstm, f"weight_hh_l{layer}"),
