@@ -75,45 +75,54 @@ struct FwdArgs {
 
 __device__ bool wait_flag(const int* flag, int need, int* error);
 
-__device__ void recurrence_body(const FwdArgs& a, int blk, uint16_t* sh, float* sg) {
-  const int t_ = threadIdx.x, lane = t_ & 63, w = t_ >> 6;  // wave w owns gate block w
+// Layout of a step (profiles/r6/lstm): wave w owns hidden
+// units [32w, 32w+32) of ALL four gates — its 8 MFMA tiles are (gate q, half h)
+// = gate columns q·128 + 32w + 16h + 0..15 — and multiplies W·hᵀ (operands
+// swapped), so lane (fr, fk) of tile (q, h) holds the pre-activations of batch
+// row fr, units 32w + 16h + 4fk + 0..3 for gate q.  A lane therefore has i, f,
+// g, o of the same 8 cells: the cell update runs in registers straight after
+// the MFMAs (no gate round trip through LDS), h_t goes to the other half of a
+// ping-pong LDS buffer (one barrier per step), and the step's Xp is 8
+// contiguous bytes per tile.
+__device__ void recurrence_body(const FwdArgs& a, int blk, uint16_t* sh) {
+  const int t_ = threadIdx.x, lane = t_ & 63, w = t_ >> 6;
   const int fr = lane & 15, fk = lane >> 4;
   const int b0 = blk * kRows;
   const int B = a.B, T = a.T;
   const bool prof = a.prof && blk == 0 && t_ == 0;
   unsigned long long ph[kPhases] = {0, 0, 0, 0, 0};
+  const int row = b0 + fr;              // this lane's batch row
+  const bool live = row < B;
+  const int xrow = live ? row : 0;      // loads stay unconditional (no branch around them)
 
-  // W_hh slice of gate block w as B fragments: tile jn (16 gate columns) x k step kk (32 hidden).
+  // gate column of tile jn = (gate q = jn >> 1, half h = jn & 1), element i: col(jn) + 4fk + i
+  auto col = [&](int jn) { return (jn >> 1) * kH + w * 32 + (jn & 1) * 16; };
+  // W_hh rows of this wave's tiles as A fragments: row col(jn) + fr, k = 32kk + 8fk .. +7
   bf16x8_t wf[8][4];
 #pragma unroll
   for (int jn = 0; jn < 8; ++jn)
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
-      wf[jn][kk] = *reinterpret_cast<const bf16x8_t*>(a.whh + (size_t)(w * kH + jn * 16 + fr) * kH + kk * 32 + fk * 8);
+      wf[jn][kk] = *reinterpret_cast<const bf16x8_t*>(a.whh + (size_t)(col(jn) + fr) * kH + kk * 32 + fk * 8);
 
-  const int cm = t_ >> 4, cn = (t_ & 15) * 8;  // this thread's 8 cells: row cm, units cn..cn+7
-  const int row = b0 + cm;
-  const bool live = row < B;
-  // h_{-1}, c_{-1}: the carried state (zero without one)
-  for (int i = t_; i < kRows * kHStride; i += 256) sh[i] = 0;
+  // h_{-1}: the carried state (zero without one); c: this lane's 8 cells
+  for (int i = t_; i < 2 * kRows * kHStride; i += 256) sh[i] = 0;
   __syncthreads();
-  if (a.h0 && live)
-    *reinterpret_cast<u32x4*>(sh + cm * kHStride + cn) = *reinterpret_cast<const u32x4*>(a.h0 + (size_t)row * kH + cn);
-  float c[8];
+  if (a.h0 && t_ < 256) {
+    const int r = t_ >> 4, u = (t_ & 15) * 8;
+    if (b0 + r < B)
+      *reinterpret_cast<u32x4*>(sh + r * kHStride + u) = *reinterpret_cast<const u32x4*>(a.h0 + (size_t)(b0 + r) * kH + u);
+  }
+  float c[8];  // cells (half h, element i) at c[4h + i]: unit 32w + 16h + 4fk + i
 #pragma unroll
-  for (int q = 0; q < 8; ++q) c[q] = (a.c0 && live) ? a.c0[(size_t)row * kH + cn + q] : 0.0f;
+  for (int q = 0; q < 8; ++q)
+    c[q] = (a.c0 && live) ? a.c0[(size_t)row * kH + w * 32 + (q >> 2) * 16 + fk * 4 + (q & 3)] : 0.0f;
 
-  // Xp of one step in accumulator layout: tile jn, row 4*fk+e, column w*128 + 16*jn + fr.
-  uint16_t xn[8][4];
+  uint2 xn[8];  // Xp of the next step: tile jn, 4 bf16
   auto load_xp = [&](int t) {
+    const uint16_t* p = a.xp + ((size_t)t * B + xrow) * (4 * kH) + fk * 4;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int r = b0 + fk * 4 + e;
-      const bool ok = r < B;
-      const uint16_t* p = a.xp + ((size_t)t * B + (ok ? r : 0)) * (4 * kH) + w * kH + fr;
-#pragma unroll
-      for (int jn = 0; jn < 8; ++jn) xn[jn][e] = ok ? p[jn * 16] : (uint16_t)0;
-    }
+    for (int jn = 0; jn < 8; ++jn) xn[jn] = *reinterpret_cast<const uint2*>(p + col(jn));
   };
   if (a.wait) wait_flag(a.wait, 0, a.error);
   load_xp(0);
@@ -124,82 +133,81 @@ __device__ void recurrence_body(const FwdArgs& a, int blk, uint16_t* sh, float* 
     f32x4_t acc[8];
 #pragma unroll
     for (int jn = 0; jn < 8; ++jn)
-      acc[jn] = f32x4_t{bf2f(xn[jn][0]), bf2f(xn[jn][1]), bf2f(xn[jn][2]), bf2f(xn[jn][3])};
+      acc[jn] = f32x4_t{bf2f((uint16_t)(xn[jn].x & 0xffff)), bf2f((uint16_t)(xn[jn].x >> 16)),
+                        bf2f((uint16_t)(xn[jn].y & 0xffff)), bf2f((uint16_t)(xn[jn].y >> 16))};
     if (t + 1 < T) {
       if (a.wait) wait_flag(a.wait, t + 1, a.error);
       load_xp(t + 1);  // lands while this step computes
     }
-    bf16x8_t hf[4];
+    bf16x8_t hf[4];  // B operand: h_{t-1}[batch fr][k = 32kk + 8fk .. +7]
+    const uint16_t* hcur = sh + (t & 1) * kRows * kHStride;
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
-      hf[kk] = *reinterpret_cast<const bf16x8_t*>(sh + fr * kHStride + kk * 32 + fk * 8);
+      hf[kk] = *reinterpret_cast<const bf16x8_t*>(hcur + fr * kHStride + kk * 32 + fk * 8);
     if (prof) { t1 = __builtin_amdgcn_s_memtime(); ph[0] += t1 - t0; t0 = t1; }
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
       for (int jn = 0; jn < 8; ++jn)
-        acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[kk], wf[jn][kk], acc[jn], 0, 0, 0);
-    // activations: sigmoid for i, f, o; tanh for g (block 2)
+        acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[jn][kk], hf[kk], acc[jn], 0, 0, 0);
+    // activations and the cell update, in registers: tiles 2q + h hold gate q
+    float gi[8], gf[8], gg[8], go[8];
 #pragma unroll
-    for (int jn = 0; jn < 8; ++jn)
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float v = acc[jn][e];
-        sg[(w * kRows + fk * 4 + e) * kH + jn * 16 + fr] = (w == 2) ? tanh_f(v) : sigm(v);
+      for (int i = 0; i < 4; ++i) {
+        gi[4 * h + i] = sigm(acc[0 + h][i]);
+        gf[4 * h + i] = sigm(acc[2 + h][i]);
+        gg[4 * h + i] = tanh_f(acc[4 + h][i]);
+        go[4 * h + i] = sigm(acc[6 + h][i]);
       }
-    if (prof) { t1 = __builtin_amdgcn_s_memtime(); ph[1] += t1 - t0; t0 = t1; }
-    __syncthreads();  // gates complete; every wave's reads of h_{t-1} done
-    if (prof) { t1 = __builtin_amdgcn_s_memtime(); ph[2] += t1 - t0; t0 = t1; }
-    const float* gi = sg + (0 * kRows + cm) * kH + cn;
-    const float* gf = sg + (1 * kRows + cm) * kH + cn;
-    const float* gg = sg + (2 * kRows + cm) * kH + cn;
-    const float* go = sg + (3 * kRows + cm) * kH + cn;
     uint16_t hv[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       c[q] = gf[q] * c[q] + gi[q] * gg[q];
       hv[q] = f2bf(go[q] * tanh_f(c[q]));
     }
-    const u32x4 packed{(uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16),
-                       (uint32_t)hv[4] | ((uint32_t)hv[5] << 16), (uint32_t)hv[6] | ((uint32_t)hv[7] << 16)};
-    *reinterpret_cast<u32x4*>(sh + cm * kHStride + cn) = packed;
-    if (live && a.gates_out) {
-      const float* gsrc[4] = {gi, gf, gg, go};
+    if (prof) { t1 = __builtin_amdgcn_s_memtime(); ph[1] += t1 - t0; t0 = t1; }
+    uint16_t* hnext = sh + ((t + 1) & 1) * kRows * kHStride;  // ping-pong: step t reads the other buffer
+    const uint2 hp[2] = {uint2{(uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16)},
+                         uint2{(uint32_t)hv[4] | ((uint32_t)hv[5] << 16), (uint32_t)hv[6] | ((uint32_t)hv[7] << 16)}};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        uint32_t pk[4];
+    for (int h = 0; h < 2; ++h) {
+      const int u = w * 32 + h * 16 + fk * 4;
+      *reinterpret_cast<uint2*>(hnext + fr * kHStride + u) = hp[h];
+      if (live) {
+        if (a.y) *reinterpret_cast<uint2*>(a.y + row * a.ys_row + t * a.ys_t + u) = hp[h];
+        if (a.hlast && t == T - 1) *reinterpret_cast<uint2*>(a.hlast + (size_t)row * kH + u) = hp[h];
+        if (a.gates_out) {
+          const float* gsrc[4] = {gi, gf, gg, go};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) pk[q] = (uint32_t)f2bf(gsrc[k][2 * q]) | ((uint32_t)f2bf(gsrc[k][2 * q + 1]) << 16);
-        *reinterpret_cast<u32x4*>(a.gates_out + ((size_t)t * B + row) * (4 * kH) + k * kH + cn) =
-            u32x4{pk[0], pk[1], pk[2], pk[3]};
+          for (int q = 0; q < 4; ++q) {
+            const float* v = gsrc[q] + 4 * h;
+            *reinterpret_cast<uint2*>(a.gates_out + ((size_t)t * B + row) * (4 * kH) + q * kH + u) =
+                uint2{(uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                      (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16)};
+          }
+          *reinterpret_cast<float4*>(a.cells_out + ((size_t)t * B + row) * kH + u) =
+              float4{c[4 * h], c[4 * h + 1], c[4 * h + 2], c[4 * h + 3]};
+        }
       }
-      float* cd = a.cells_out + ((size_t)t * B + row) * kH + cn;
-      *reinterpret_cast<float4*>(cd) = float4{c[0], c[1], c[2], c[3]};
-      *reinterpret_cast<float4*>(cd + 4) = float4{c[4], c[5], c[6], c[7]};
-    }
-    if (live) {
-      if (a.y) *reinterpret_cast<u32x4*>(a.y + row * a.ys_row + t * a.ys_t + cn) = packed;
-      if (a.hlast && t == T - 1) *reinterpret_cast<u32x4*>(a.hlast + (size_t)row * kH + cn) = packed;
     }
     if (a.publish) __threadfence();  // y_t visible device-wide before the count moves
     if (prof) { t1 = __builtin_amdgcn_s_memtime(); ph[3] += t1 - t0; t0 = t1; }
-    __syncthreads();  // h_t published; gate buffer free
+    __syncthreads();  // h_t published; every read of h_{t-1} done (its buffer is written at t + 1)
     if (a.publish && t_ == 0) __hip_atomic_store(a.publish, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     if (prof) { t1 = __builtin_amdgcn_s_memtime(); ph[4] += t1 - t0; }
   }
-  if (live && a.c_last) {
-    float* cl = a.c_last + (size_t)row * kH + cn;
+  if (live && a.c_last)
 #pragma unroll
-    for (int q = 0; q < 8; ++q) cl[q] = c[q];
-  }
+    for (int q = 0; q < 8; ++q) a.c_last[(size_t)row * kH + w * 32 + (q >> 2) * 16 + fk * 4 + (q & 3)] = c[q];
   if (prof)
     for (int i = 0; i < kPhases; ++i) a.prof[i] = ph[i];
 }
 
 __global__ void __launch_bounds__(256, 1) lstm_recurrence_kernel(const FwdArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t sh[kRows * kHStride];   // h_{t-1}, bf16
-  __shared__ __attribute__((aligned(16))) float sg[4 * kRows * kH];          // activated gates
-  recurrence_body(a, blockIdx.x, sh, sg);
+  __shared__ __attribute__((aligned(16))) uint16_t sh[2 * kRows * kHStride];   // h ping-pong, bf16
+  recurrence_body(a, blockIdx.x, sh);
 }
 
 // Backward through time of one layer.  dgates_t (pre-activation) from the saved
@@ -227,12 +235,21 @@ struct BwdArgs {
   int B, T, has_prev;
 };
 
-__device__ void backward_body(const BwdArgs& a, int blk, uint16_t* sdg, float* sdh) {
+// Same ownership as the forward: wave w owns hidden units [32w, 32w+32), lane
+// (fr, fk) the 8 cells of batch row fr, units 32w + 16h + 4fk + 0..3.  dh_next =
+// W_hhᵀ·dgatesᵀ (operands swapped) lands in exactly those lanes, so it never
+// leaves registers; dgates_t goes through a ping-pong LDS buffer (the MFMA's
+// B operand needs whole rows), one barrier per step.  The saved gates, cells
+// and dY of step t-1 are loaded while step t computes.
+__device__ void backward_body(const BwdArgs& a, int blk, uint16_t* sdg) {
   const int t_ = threadIdx.x, lane = t_ & 63, w = t_ >> 6;
   const int fr = lane & 15, fk = lane >> 4;
   const int b0 = blk * kRows;
   const int B = a.B, T = a.T;
-  // B operand: B[k][n] = W_hh[k][n], k = gate row (0..511), n = hidden column of this wave's tiles.
+  const int row = b0 + fr;
+  const bool live = row < B;
+  const int xrow = live ? row : 0;
+  // A operand: W_hhᵀ rows = hidden units 32w + 16jn + fr, k = gate row 32ks + 8fk .. +7
   bf16x8_t wf[2][16];
 #pragma unroll
   for (int jn = 0; jn < 2; ++jn)
@@ -246,81 +263,99 @@ __device__ void backward_body(const BwdArgs& a, int blk, uint16_t* sdg, float* s
                                                        (uint32_t)v[4] | ((uint32_t)v[5] << 16),
                                                        (uint32_t)v[6] | ((uint32_t)v[7] << 16)});
     }
-  const int cm = t_ >> 4, cn = (t_ & 15) * 8;  // this thread's 8 cells
-  const int row = b0 + cm;
-  const bool live = row < B;
-  for (int i = t_; i < kRows * kH; i += 256) sdh[i] = 0.0f;
-  __syncthreads();
-  if (a.dh && live)
-    for (int q = 0; q < 8; ++q) sdh[cm * kH + cn + q] = a.dh[(size_t)row * kH + cn + q];
-  float dcn[8];
+  auto unit = [&](int h) { return w * 32 + h * 16 + fk * 4; };
+  f32x4_t dh[2], dcn[2];  // carried dh_next / dc_next of this lane's cells (half h)
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dcn[q] = (a.dc && live) ? a.dc[(size_t)row * kH + cn + q] : 0.0f;
-  __syncthreads();
+  for (int h = 0; h < 2; ++h) {
+    dh[h] = (a.dh && live) ? *reinterpret_cast<const f32x4_t*>(a.dh + (size_t)row * kH + unit(h)) : f32x4_t{0, 0, 0, 0};
+    dcn[h] = (a.dc && live) ? *reinterpret_cast<const f32x4_t*>(a.dc + (size_t)row * kH + unit(h)) : f32x4_t{0, 0, 0, 0};
+  }
+  // saved values of one step for this lane's cells (prefetched a step ahead)
+  uint2 ng[2][4], ndy[2];
+  float4 nc[2], ncp[2];
+  auto load_step = [&](int t) {
+    if (a.wait) wait_flag(a.wait, T - t - 1, a.error);
+    const bool prev = t > 0 || a.has_prev;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int u = unit(h);
+      const uint16_t* gp = a.gates + ((size_t)t * B + xrow) * (4 * kH) + u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ng[h][q] = *reinterpret_cast<const uint2*>(gp + q * kH);
+      nc[h] = *reinterpret_cast<const float4*>(a.cells + ((size_t)t * B + xrow) * kH + u);
+      ncp[h] = prev ? *reinterpret_cast<const float4*>(a.cells + ((int64_t)(t - 1) * B + xrow) * kH + u)
+                    : float4{0.f, 0.f, 0.f, 0.f};
+      ndy[h] = a.dy ? *reinterpret_cast<const uint2*>(a.dy + xrow * a.ds_row + t * a.ds_t + u) : uint2{0u, 0u};
+    }
+  };
+  load_step(T - 1);
 
   for (int t = T - 1; t >= 0; --t) {
-    float dg_i[8], dg_f[8], dg_g[8], dg_o[8];
-    if (a.wait) wait_flag(a.wait, T - t - 1, a.error);
-    if (live) {
-      const uint16_t* gp = a.gates + ((size_t)t * B + row) * (4 * kH) + cn;
-      const float* cp = a.cells + ((size_t)t * B + row) * kH + cn;
-      const bool prev = t > 0 || a.has_prev;
-      const float* cpp = a.cells + ((int64_t)(t - 1) * B + row) * kH + cn;
-      const uint16_t* dyp = a.dy ? a.dy + row * a.ds_row + t * a.ds_t + cn : nullptr;
+    uint2 cg[2][4], cdy[2];
+    float4 cc[2], ccp[2];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float i = bf2f(gp[q]), f = bf2f(gp[kH + q]), g = bf2f(gp[2 * kH + q]), o = bf2f(gp[3 * kH + q]);
-        const float c = cp[q], cprev = prev ? cpp[q] : 0.0f;
-        const float dh = (dyp ? bf2f(dyp[q]) : 0.0f) + sdh[cm * kH + cn + q];
-        const float tc = tanh_f(c);
-        const float dc = dh * o * (1.0f - tc * tc) + dcn[q];
-        dg_o[q] = dh * tc * o * (1.0f - o);
-        dg_i[q] = dc * g * i * (1.0f - i);
-        dg_g[q] = dc * i * (1.0f - g * g);
-        dg_f[q] = dc * cprev * f * (1.0f - f);
-        dcn[q] = dc * f;
-      }
-    } else {
+    for (int h = 0; h < 2; ++h) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) dg_i[q] = dg_f[q] = dg_g[q] = dg_o[q] = 0.0f;
+      for (int q = 0; q < 4; ++q) cg[h][q] = ng[h][q];
+      cc[h] = nc[h], ccp[h] = ncp[h], cdy[h] = ndy[h];
     }
-    const float* dsrc[4] = {dg_i, dg_f, dg_g, dg_o};
+    if (t > 0) load_step(t - 1);
+    uint16_t* buf = sdg + (t & 1) * kRows * kGStride;  // ping-pong
+    uint2 dgp[2][4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      uint32_t pk[4];
+    for (int h = 0; h < 2; ++h) {
+      float dgv[4][4];
+      const float cv[4] = {cc[h].x, cc[h].y, cc[h].z, cc[h].w}, cpv[4] = {ccp[h].x, ccp[h].y, ccp[h].z, ccp[h].w};
+      const float dyv[4] = {bf2f((uint16_t)(cdy[h].x & 0xffff)), bf2f((uint16_t)(cdy[h].x >> 16)),
+                            bf2f((uint16_t)(cdy[h].y & 0xffff)), bf2f((uint16_t)(cdy[h].y >> 16))};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) pk[q] = (uint32_t)f2bf(dsrc[k][2 * q]) | ((uint32_t)f2bf(dsrc[k][2 * q + 1]) << 16);
-      const u32x4 v{pk[0], pk[1], pk[2], pk[3]};
-      *reinterpret_cast<u32x4*>(sdg + cm * kGStride + k * kH + cn) = v;
-      if (live) *reinterpret_cast<u32x4*>(a.dgates + ((size_t)t * B + row) * (4 * kH) + k * kH + cn) = v;
+      for (int e = 0; e < 4; ++e) {
+        auto gate = [&](int q) {
+          const uint32_t v = (e >> 1) ? cg[h][q].y : cg[h][q].x;
+          return bf2f((uint16_t)((e & 1) ? (v >> 16) : (v & 0xffff)));
+        };
+        const float i = gate(0), f = gate(1), g = gate(2), o = gate(3);
+        const float dhv = live ? dyv[e] + dh[h][e] : 0.0f;
+        const float tc = tanh_f(cv[e]);
+        const float dc = dhv * o * (1.0f - tc * tc) + dcn[h][e];
+        dgv[3][e] = dhv * tc * o * (1.0f - o);
+        dgv[0][e] = dc * g * i * (1.0f - i);
+        dgv[2][e] = dc * i * (1.0f - g * g);
+        dgv[1][e] = dc * cpv[e] * f * (1.0f - f);
+        dcn[h][e] = live ? dc * f : 0.0f;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        dgp[h][q] = uint2{(uint32_t)f2bf(dgv[q][0]) | ((uint32_t)f2bf(dgv[q][1]) << 16),
+                          (uint32_t)f2bf(dgv[q][2]) | ((uint32_t)f2bf(dgv[q][3]) << 16)};
+        *reinterpret_cast<uint2*>(buf + fr * kGStride + q * kH + unit(h)) = dgp[h][q];
+        if (live) *reinterpret_cast<uint2*>(a.dgates + ((size_t)t * B + row) * (4 * kH) + q * kH + unit(h)) = dgp[h][q];
+      }
     }
     if (a.publish) __threadfence();  // dgates_t visible device-wide before the count moves
-    __syncthreads();  // dgates_t complete; every read of dh_next done
+    __syncthreads();  // dgates_t complete in LDS (its other buffer was last read a step ago)
     if (a.publish && t_ == 0) __hip_atomic_store(a.publish, T - t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) {
-      const bf16x8_t av = *reinterpret_cast<const bf16x8_t*>(sdg + fr * kGStride + ks * 32 + fk * 8);
+      const bf16x8_t bv = *reinterpret_cast<const bf16x8_t*>(buf + fr * kGStride + ks * 32 + fk * 8);
 #pragma unroll
-      for (int jn = 0; jn < 2; ++jn) acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, wf[jn][ks], acc[jn], 0, 0, 0);
+      for (int jn = 0; jn < 2; ++jn) acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[jn][ks], bv, acc[jn], 0, 0, 0);
     }
-#pragma unroll
-    for (int jn = 0; jn < 2; ++jn)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) sdh[(fk * 4 + e) * kH + w * 32 + jn * 16 + fr] = acc[jn][e];
-    __syncthreads();  // dh_next published; dgates buffer free
+    dh[0] = acc[0], dh[1] = acc[1];
   }
   // carry (dh_next, dc_next) of the window's first step to the window before it
-  if (live && a.dh)
-    for (int q = 0; q < 8; ++q) a.dh[(size_t)row * kH + cn + q] = sdh[cm * kH + cn + q];
-  if (live && a.dc)
-    for (int q = 0; q < 8; ++q) a.dc[(size_t)row * kH + cn + q] = dcn[q];
+  if (live)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (a.dh) *reinterpret_cast<f32x4_t*>(a.dh + (size_t)row * kH + unit(h)) = dh[h];
+      if (a.dc) *reinterpret_cast<f32x4_t*>(a.dc + (size_t)row * kH + unit(h)) = dcn[h];
+    }
 }
 
 __global__ void __launch_bounds__(256, 1) lstm_backward_kernel(const BwdArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t sdg[kRows * kGStride];  // dgates_t, bf16
-  __shared__ __attribute__((aligned(16))) float sdh[kRows * kH];            // dh_next, fp32
-  backward_body(a, blockIdx.x, sdg, sdh);
+  __shared__ __attribute__((aligned(16))) uint16_t sdg[2 * kRows * kGStride];  // dgates ping-pong, bf16
+  backward_body(a, blockIdx.x, sdg);
 }
 
 // ---- two layers as one wavefront ------------------------------
@@ -377,7 +412,9 @@ int triple_grid(int nblk) { return 24 * ((nblk + 7) / 8); }
 __device__ void project_fwd_body(const uint16_t* __restrict__ y1, const uint16_t* __restrict__ wih2,
                                  const uint16_t* __restrict__ b2, uint16_t* __restrict__ xp2, const int* wait,
                                  int* publish, int* error, int blk, int B, int T) {
-  const int t_ = threadIdx.x, lane = t_ & 63, g = t_ >> 6;  // wave g owns gate block g
+  // wave g owns gate block g; W_ih2·hᵀ (operands swapped): lane (fr, fk) of tile jn
+  // holds batch row fr, gate columns 128g + 16jn + 4fk + 0..3 -> 8-byte stores
+  const int t_ = threadIdx.x, lane = t_ & 63, g = t_ >> 6;
   const int fr = lane & 15, fk = lane >> 4;
   const int b0 = blk * kRows;
   bf16x8_t wf[8][4];
@@ -386,17 +423,22 @@ __device__ void project_fwd_body(const uint16_t* __restrict__ y1, const uint16_t
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
       wf[jn][kk] = *reinterpret_cast<const bf16x8_t*>(wih2 + (size_t)(g * kH + jn * 16 + fr) * kH + kk * 32 + fk * 8);
-  float bias[8];
+  f32x4_t bias[8];
 #pragma unroll
-  for (int jn = 0; jn < 8; ++jn) bias[jn] = bf2f(b2[g * kH + jn * 16 + fr]);
-  const bool rok = b0 + fr < B;
+  for (int jn = 0; jn < 8; ++jn) {
+    const uint2 bv = *reinterpret_cast<const uint2*>(b2 + g * kH + jn * 16 + fk * 4);
+    bias[jn] = f32x4_t{bf2f((uint16_t)(bv.x & 0xffff)), bf2f((uint16_t)(bv.x >> 16)), bf2f((uint16_t)(bv.y & 0xffff)),
+                       bf2f((uint16_t)(bv.y >> 16))};
+  }
+  const int row = b0 + fr;
+  const bool live = row < B;
+  const int xrow = live ? row : 0;
   bf16x8_t hn[4];
-  auto load_h = [&](int t) {  // A fragments of h1_t: row fr, k = 32kk + 8fk .. +7
+  auto load_h = [&](int t) {  // B fragments of h1_t: batch row fr, k = 32kk + 8fk .. +7
     wait_flag(wait, t, error);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
-      hn[kk] = rok ? *reinterpret_cast<const bf16x8_t*>(y1 + ((size_t)t * B + b0 + fr) * kH + kk * 32 + fk * 8)
-                   : bf16x8_t{};
+      hn[kk] = *reinterpret_cast<const bf16x8_t*>(y1 + ((size_t)t * B + xrow) * kH + kk * 32 + fk * 8);
   };
   load_h(0);
   for (int t = 0; t < T; ++t) {
@@ -404,20 +446,18 @@ __device__ void project_fwd_body(const uint16_t* __restrict__ y1, const uint16_t
     if (t + 1 < T) load_h(t + 1);
     f32x4_t acc[8];
 #pragma unroll
-    for (int jn = 0; jn < 8; ++jn) acc[jn] = f32x4_t{bias[jn], bias[jn], bias[jn], bias[jn]};
+    for (int jn = 0; jn < 8; ++jn) acc[jn] = bias[jn];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
       for (int jn = 0; jn < 8; ++jn)
-        acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[kk], wf[jn][kk], acc[jn], 0, 0, 0);
+        acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[jn][kk], hf[kk], acc[jn], 0, 0, 0);
+    if (live) {
+      uint16_t* p = xp2 + ((size_t)t * B + row) * (4 * kH) + g * kH + fk * 4;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int rr = b0 + fk * 4 + e;
-      if (rr < B) {
-        uint16_t* p = xp2 + ((size_t)t * B + rr) * (4 * kH) + g * kH + fr;
-#pragma unroll
-        for (int jn = 0; jn < 8; ++jn) p[jn * 16] = f2bf(acc[jn][e]);
-      }
+      for (int jn = 0; jn < 8; ++jn)
+        *reinterpret_cast<uint2*>(p + jn * 16) = uint2{(uint32_t)f2bf(acc[jn][0]) | ((uint32_t)f2bf(acc[jn][1]) << 16),
+                                                       (uint32_t)f2bf(acc[jn][2]) | ((uint32_t)f2bf(acc[jn][3]) << 16)};
     }
     __threadfence();
     __syncthreads();
@@ -431,7 +471,9 @@ __device__ void project_fwd_body(const uint16_t* __restrict__ y1, const uint16_t
 __device__ void project_bwd_body(const uint16_t* __restrict__ dgates2, const uint16_t* __restrict__ wih2,
                                  uint16_t* __restrict__ dy1, const int* wait, int* publish, int* error, int blk,
                                  int B, int T) {
-  const int t_ = threadIdx.x, lane = t_ & 63, q = t_ >> 6;  // wave q owns hidden columns [32q, 32q+32)
+  // wave q owns hidden units [32q, 32q+32); W_ih2ᵀ·dgatesᵀ (operands swapped): lane
+  // (fr, fk) of tile jn holds batch row fr, units 32q + 16jn + 4fk + 0..3
+  const int t_ = threadIdx.x, lane = t_ & 63, q = t_ >> 6;
   const int fr = lane & 15, fk = lane >> 4;
   const int b0 = blk * kRows;
   bf16x8_t wf[2][16];
@@ -447,14 +489,15 @@ __device__ void project_bwd_body(const uint16_t* __restrict__ dgates2, const uin
                                                        (uint32_t)v[4] | ((uint32_t)v[5] << 16),
                                                        (uint32_t)v[6] | ((uint32_t)v[7] << 16)});
     }
-  const bool rok = b0 + fr < B;
+  const int row = b0 + fr;
+  const bool live = row < B;
+  const int xrow = live ? row : 0;
   bf16x8_t an[16];
-  auto load_dg = [&](int t) {  // A fragments of dgates2_t: row fr, k = 32ks + 8fk .. +7
+  auto load_dg = [&](int t) {  // B fragments of dgates2_t: batch row fr, k = 32ks + 8fk .. +7
     wait_flag(wait, T - t - 1, error);
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks)
-      an[ks] = rok ? *reinterpret_cast<const bf16x8_t*>(dgates2 + ((size_t)t * B + b0 + fr) * (4 * kH) + ks * 32 + fk * 8)
-                   : bf16x8_t{};
+      an[ks] = *reinterpret_cast<const bf16x8_t*>(dgates2 + ((size_t)t * B + xrow) * (4 * kH) + ks * 32 + fk * 8);
   };
   load_dg(T - 1);
   for (int t = T - 1; t >= 0; --t) {
@@ -466,15 +509,13 @@ __device__ void project_bwd_body(const uint16_t* __restrict__ dgates2, const uin
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks)
 #pragma unroll
-      for (int jn = 0; jn < 2; ++jn) acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[ks], wf[jn][ks], acc[jn], 0, 0, 0);
+      for (int jn = 0; jn < 2; ++jn) acc[jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[jn][ks], av[ks], acc[jn], 0, 0, 0);
+    if (live) {
+      uint16_t* p = dy1 + ((size_t)t * B + row) * kH + q * 32 + fk * 4;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int rr = b0 + fk * 4 + e;
-      if (rr < B) {
-        uint16_t* p = dy1 + ((size_t)t * B + rr) * kH + q * 32 + fr;
-#pragma unroll
-        for (int jn = 0; jn < 2; ++jn) p[jn * 16] = f2bf(acc[jn][e]);
-      }
+      for (int jn = 0; jn < 2; ++jn)
+        *reinterpret_cast<uint2*>(p + jn * 16) = uint2{(uint32_t)f2bf(acc[jn][0]) | ((uint32_t)f2bf(acc[jn][1]) << 16),
+                                                       (uint32_t)f2bf(acc[jn][2]) | ((uint32_t)f2bf(acc[jn][3]) << 16)};
     }
     __threadfence();
     __syncthreads();
@@ -492,8 +533,7 @@ struct Wave2Args {
 };
 
 __global__ void __launch_bounds__(256, 1) lstm2_forward_kernel(const Wave2Args a) {
-  __shared__ __attribute__((aligned(16))) uint16_t sh[kRows * kHStride];
-  __shared__ __attribute__((aligned(16))) float sg[4 * kRows * kH];
+  __shared__ __attribute__((aligned(16))) uint16_t sh[2 * kRows * kHStride];
   int r, role;
   if (!wave_role(blockIdx.x, a.nblk, &r, &role)) return;  // the whole workgroup
   int* err = a.flags + 2 * a.nblk;
@@ -501,14 +541,14 @@ __global__ void __launch_bounds__(256, 1) lstm2_forward_kernel(const Wave2Args a
     FwdArgs l1 = a.l1;
     l1.publish = a.flags + r;
     l1.error = err;
-    recurrence_body(l1, r, sh, sg);
+    recurrence_body(l1, r, sh);
   } else if (role == 1) {
     project_fwd_body(a.l1.y, a.wih2, a.b2, a.xp2, a.flags + r, a.flags + a.nblk + r, err, r, a.l1.B, a.l1.T);
   } else {
     FwdArgs l2 = a.l2;
     l2.wait = a.flags + a.nblk + r;
     l2.error = err;
-    recurrence_body(l2, r, sh, sg);
+    recurrence_body(l2, r, sh);
   }
 }
 
@@ -521,8 +561,7 @@ struct Wave2BwdArgs {
 };
 
 __global__ void __launch_bounds__(256, 1) lstm2_backward_kernel(const Wave2BwdArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t sdg[kRows * kGStride];
-  __shared__ __attribute__((aligned(16))) float sdh[kRows * kH];
+  __shared__ __attribute__((aligned(16))) uint16_t sdg[2 * kRows * kGStride];
   int r, role;
   if (!wave_role(blockIdx.x, a.nblk, &r, &role)) return;
   int* err = a.flags + 2 * a.nblk;
@@ -530,14 +569,14 @@ __global__ void __launch_bounds__(256, 1) lstm2_backward_kernel(const Wave2BwdAr
     BwdArgs l2 = a.l2;
     l2.publish = a.flags + r;
     l2.error = err;
-    backward_body(l2, r, sdg, sdh);
+    backward_body(l2, r, sdg);
   } else if (role == 1) {
     project_bwd_body(a.l2.dgates, a.wih2, a.dy1, a.flags + r, a.flags + a.nblk + r, err, r, a.l2.B, a.l2.T);
   } else {
     BwdArgs l1 = a.l1;
     l1.wait = a.flags + a.nblk + r;
     l1.error = err;
-    backward_body(l1, r, sdg, sdh);
+    backward_body(l1, r, sdg);
   }
 }
 

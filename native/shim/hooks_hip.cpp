@@ -1240,9 +1240,10 @@ hipError_t multi_device_launch(Entry* list, size_t n, Grid&& grid, Stream&& stre
     track[i] = limiter_on_launch(dev[i], grid(list[i]));
     vmem_scan_args(args_of(list[i]), stream_of(list[i]));
   }
+  const uint64_t t0 = mono_ns();  // the runtime may return only once the kernels ran
   hipError_t rc = real();
   for (size_t i = 0; i < n; ++i)
-    if (track[i]) limiter_track(dev[i], stream_of(list[i]), rc);
+    if (track[i]) limiter_track(dev[i], stream_of(list[i]), rc, t0);
   return rc;
 }
 

@@ -1036,7 +1036,7 @@ bool limiter_on_launch(int dev, uint64_t wg, const void* fn, uint32_t kernels, b
 // After a tracked launch: record a marker on its stream and push it onto this
 // thread's ring.  Lock-free; the only shared write is a wake-up of the limiter
 // thread when it has gone idle.
-void limiter_track(int dev, hipStream_t stream, hipError_t launch_rc) {
+void limiter_track(int dev, hipStream_t stream, hipError_t launch_rc, uint64_t submit_ns) {
   if (dev < 0 || dev >= VGPU_MAX_DEVICES) return;
   DevLimiter& L = g_lim[dev];
   // Not tracked: the launch failed, or it was captured into a graph (it runs
@@ -1074,7 +1074,7 @@ void limiter_track(int dev, hipStream_t stream, hipError_t launch_rc) {
     t->spare = ev;
     return untracked();
   }
-  t->ring[h & kMask] = Marker{ev, mono_ns(), stream, 1};
+  t->ring[h & kMask] = Marker{ev, submit_ns ? submit_ns : mono_ns(), stream, 1};
   t->launches.store(t->launches.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
   t->head.store(h + 1, std::memory_order_release);
   // Wake the limiter thread if it went idle (see reap: it re-checks the rings

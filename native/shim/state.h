@@ -117,7 +117,10 @@ bool limiter_on_launch(int dev, uint64_t workgroups, const void* fn = nullptr, u
 // The kernel whose host stub is `fn` is a collective's (its library is RCCL's,
 // or matches VGPU_THROTTLE_EXEMPT).
 bool exempt_kernel(const void* fn);
-void limiter_track(int dev, hipStream_t stream, hipError_t launch_rc);
+// submit_ns: when the launch was submitted (0 = now); a launch call that may
+// return only after its kernel ran (the multi-device launches) passes the time
+// before the call, so the marker's interval still covers the kernel.
+void limiter_track(int dev, hipStream_t stream, hipError_t launch_rc, uint64_t submit_ns = 0);
 void limiter_flush_thread();  // publish this thread's batched slot counters
 // Stream captures in progress anywhere in the process: while one is open the
 // limiter records and polls markers only on streams that are not capturing (an

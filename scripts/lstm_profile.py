@@ -4,9 +4,8 @@ two-layer wavefront buys.
 
 1. Phase profile: one layer's recurrence (B rows, T steps) with s_memtime
    stamps in workgroup 0 (native/kernels/lstm.hip, FwdArgs::prof): cycles per
-   step in (0) A-operand / Xp wait, (1) MFMA + gate activations to LDS,
-   (2) the first barrier, (3) cell update + h / output stores, (4) the second
-   barrier.  The stamps themselves serialise the wave a little; the plain
+   step in (0) Xp wait + h read, (1) MFMA + gate activations + cell update
+   (in registers), (3) h / output stores, (4) the step's barrier.  The stamps themselves serialise the wave a little; the plain
    kernel's time per step is reported next to it.
 2. 5.1 / 5.2 shapes end to end: layer by layer (VGPU_LSTM_WAVE=0) against the
    wavefront launch, inference (B=100) and a training step (B=10).
@@ -58,7 +57,7 @@ def phase_profile(b=100, t=1024, h=128):
     prof_ms = timed(lambda: run(prof.data_ptr()), reps=3, warm=1)
     cyc = prof[:5].double().cpu() / t
     total = float(cyc.sum())
-    names = ["xp_wait_and_h_read", "mfma_and_activations", "barrier_1", "cell_update_and_stores", "barrier_2"]
+    names = ["xp_wait_and_h_read", "mfma_activations_and_cell_update", "unused", "h_and_output_stores", "barrier"]
     return {"B": b, "T": t, "plain_us_per_step": round(plain_ms * 1e3 / t, 3),
             "profiled_us_per_step": round(prof_ms * 1e3 / t, 3),
             "cycles_per_step": round(total, 1),
