@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(kThreads) dw_dgrad_kernel(const u32x4* __restr
   }
 }
 
-// Block = one slab of pb output pixels (pb = kWgPix · (256 / cv)): thread t owns
+// Block = one slab of pb output pixels (pb = k · (256 / cv), k <= kWgPix): thread t owns
 // channel group t % cv and pixels p0 + t / cv + k · (256 / cv), two pixels'
 // loads in flight.  Its 9 x 8 sums are merged across the block one tap at a
 // time with every thread taking part: P = 256 / C threads per channel each
@@ -253,8 +253,16 @@ int grid_for(int64_t total) {
   return (int)(b < 65536 ? (b > 0 ? b : 1) : 65536);
 }
 
-// Pixels per weight-gradient block: kWgPix per thread whatever C.
-int wgrad_pb(const Shape& s) { return kWgPix * (kThreads / (s.C / 8)); }
+// Pixels per weight-gradient block: up to kWgPix per thread, fewer when that
+// would leave the grid under 512 blocks (DeepLab's 48x48 / 24x24 layers ran 30-80
+// slabs -- 30-80 of 256 CUs, ~48 us per layer, profiles/r5/train/prof_4_2_after.md).
+int wgrad_pb(const Shape& s) {
+  const int nsub = kThreads / (s.C / 8);
+  const int64_t P = (int64_t)s.N * s.OH * s.OW;
+  int64_t k = P / (512ll * nsub);
+  k = k < 1 ? 1 : (k > kWgPix ? kWgPix : k);
+  return (int)k * nsub;
+}
 
 int wgrad_slabs(const Shape& s) {
   const int64_t P = (int64_t)s.N * s.OH * s.OW;

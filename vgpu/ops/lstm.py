@@ -3,8 +3,8 @@ persistent recurrence kernel per layer (native/kernels/lstm.hip), instead of
 MIOpen's per-timestep kernel sequence.  A 2-layer stack (the ai-benchmark
 shape) runs both layers as one wavefront launch -- layer 2 a few steps behind
 layer 1, its input projection computed inside the kernel -- in the forward and,
-in time-reverse order, in the backward (VGPU_LSTM_WAVE=0: layer by layer).  Inference (`lstm_last_hidden`) and
-training (`LSTMLayerFn`: forward keeps the activated gates and cells, backward is
+in time-reverse order, in the backward (VGPU_LSTM_WAVE=0: layer by layer).
+Inference (`lstm_last_hidden`) and training (`LSTMLayerFn`: forward keeps the activated gates and cells, backward is
 one backward-through-time kernel plus three GEMMs for the weight and input
 gradients).  Hidden size 128 (the ai-benchmark LSTM-Sentiment shape)."""
 from __future__ import annotations
@@ -49,8 +49,9 @@ def lstm_last_hidden(lstm: torch.nn.LSTM, x: torch.Tensor) -> torch.Tensor:
         y1t = torch.empty(t, b, h, dtype=x.dtype, device=x.device)
         xp2 = torch.empty(t, b, 4 * h, dtype=x.dtype, device=x.device)
         hlast = torch.empty(b, h, dtype=x.dtype, device=x.device)
-        rc = lib.vgpu_lstm2_forward(_p(xp1), _p(w_hh1), _p(lstm.weight_ih_l1.contiguous()), _p(b2),
-                                    _p(lstm.weight_hh_l1.contiguous()), _p(y1t), _p(xp2), _p(_flags(b, x.device)),
+        w_ih2, w_hh2 = lstm.weight_ih_l1.contiguous(), lstm.weight_hh_l1.contiguous()
+        flags = _flags(b, x.device)
+        rc = lib.vgpu_lstm2_forward(_p(xp1), _p(w_hh1), _p(w_ih2), _p(b2), _p(w_hh2), _p(y1t), _p(xp2), _p(flags),
                                     _p(hlast), None, None, None, None, None, b, t, h, stream)
         _check(rc, "vgpu_lstm2_forward")
         return hlast
@@ -143,9 +144,13 @@ class LSTM2Fn(torch.autograd.Function):
         gates2 = torch.empty_like(gates1)
         cells1 = torch.empty(t, b, h, dtype=torch.float32, device=dev)
         cells2 = torch.empty_like(cells1)
-        rc = lib.vgpu_lstm2_forward(_p(xp1), _p(w_hh1), _p(w_ih2), _p((b_ih2 + b_hh2).contiguous()), _p(w_hh2),
-                                    _p(y1t), _p(xp2), _p(_flags(b, dev)), None, _p(y2t), _p(gates1), _p(gates2),
-                                    _p(cells1), _p(cells2), b, t, h, torch.cuda.current_stream().cuda_stream)
+        # every buffer the kernel touches is held in a local until the launch returns
+        # (a temporary freed mid-argument-list can be handed out again to the next one)
+        b2 = (b_ih2 + b_hh2).contiguous()
+        flags = _flags(b, dev)
+        rc = lib.vgpu_lstm2_forward(_p(xp1), _p(w_hh1), _p(w_ih2), _p(b2), _p(w_hh2), _p(y1t), _p(xp2), _p(flags),
+                                    None, _p(y2t), _p(gates1), _p(gates2), _p(cells1), _p(cells2), b, t, h,
+                                    torch.cuda.current_stream().cuda_stream)
         _check(rc, "vgpu_lstm2_forward")
         ctx.save_for_backward(xt, w_ih1, w_hh1, w_ih2, w_hh2, y1t, y2t, gates1, gates2, cells1, cells2)
         return y2t.transpose(0, 1)
@@ -160,9 +165,10 @@ class LSTM2Fn(torch.autograd.Function):
         dgates1 = torch.empty_like(gates1)
         dgates2 = torch.empty_like(gates2)
         dy1 = torch.empty_like(y1t)
+        flags = _flags(b, y1t.device)
         _check(lib.vgpu_lstm2_backward(_p(gates1), _p(cells1), _p(gates2), _p(cells2), _p(dy), _p(w_hh1), _p(w_hh2),
-                                       _p(w_ih2), _p(dgates1), _p(dgates2), _p(dy1), _p(_flags(b, y1t.device)), b, t,
-                                       h, torch.cuda.current_stream().cuda_stream), "vgpu_lstm2_backward")
+                                       _p(w_ih2), _p(dgates1), _p(dgates2), _p(dy1), _p(flags), b, t, h,
+                                       torch.cuda.current_stream().cuda_stream), "vgpu_lstm2_backward")
 
         def grads(dgates, hs, inp):
             # dW_hh = Σ_t dgates_tᵀ h_{t-1} (h_{-1} = 0), dW_ih = dgatesᵀ · input, db = Σ dgates
