@@ -74,6 +74,21 @@ struct FwdArgs {
 };
 
 __device__ bool wait_flag(const int* flag, int need, int* error);
+constexpr int kPubEvery = 8;  // wavefront hand-offs are published (fence + count) every 8 steps
+
+// A wait that remembers the last count it saw: only a step past it polls L2.
+struct Waiter {
+  const int* flag;
+  int* error;
+  int seen;
+  __device__ void until(int need) {  // until *flag > need
+    if (!flag || need < seen) return;
+    wait_flag(flag, need, error);
+    seen = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+};
+// publish after step index `done` (0-based count of finished steps - 1) of `total`?
+__device__ __forceinline__ bool pub_step(int done, int total) { return (done + 1) % kPubEvery == 0 || done + 1 == total; }
 
 // Layout of a step (profiles/r6/lstm): wave w owns hidden
 // units [32w, 32w+32) of ALL four gates — its 8 MFMA tiles are (gate q, half h)
@@ -124,7 +139,8 @@ __device__ void recurrence_body(const FwdArgs& a, int blk, uint16_t* sh) {
 #pragma unroll
     for (int jn = 0; jn < 8; ++jn) xn[jn] = *reinterpret_cast<const uint2*>(p + col(jn));
   };
-  if (a.wait) wait_flag(a.wait, 0, a.error);
+  Waiter wt{a.wait, a.error, 0};
+  wt.until(0);
   load_xp(0);
   __syncthreads();
 
@@ -136,7 +152,7 @@ __device__ void recurrence_body(const FwdArgs& a, int blk, uint16_t* sh) {
       acc[jn] = f32x4_t{bf2f((uint16_t)(xn[jn].x & 0xffff)), bf2f((uint16_t)(xn[jn].x >> 16)),
                         bf2f((uint16_t)(xn[jn].y & 0xffff)), bf2f((uint16_t)(xn[jn].y >> 16))};
     if (t + 1 < T) {
-      if (a.wait) wait_flag(a.wait, t + 1, a.error);
+      wt.until(t + 1);
       load_xp(t + 1);  // lands while this step computes
     }
     bf16x8_t hf[4];  // B operand: h_{t-1}[batch fr][k = 32kk + 8fk .. +7]
@@ -192,10 +208,11 @@ __device__ void recurrence_body(const FwdArgs& a, int blk, uint16_t* sh) {
         }
       }
     }
-    if (a.publish) __threadfence();  // y_t visible device-wide before the count moves
+    const bool pub = a.publish && pub_step(t, T);
+    if (pub) __threadfence();  // y up to t visible device-wide before the count moves
     if (prof) { t1 = __builtin_amdgcn_s_memtime(); ph[3] += t1 - t0; t0 = t1; }
     __syncthreads();  // h_t published; every read of h_{t-1} done (its buffer is written at t + 1)
-    if (a.publish && t_ == 0) __hip_atomic_store(a.publish, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (pub && t_ == 0) __hip_atomic_store(a.publish, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     if (prof) { t1 = __builtin_amdgcn_s_memtime(); ph[4] += t1 - t0; }
   }
   if (live && a.c_last)
@@ -273,8 +290,9 @@ __device__ void backward_body(const BwdArgs& a, int blk, uint16_t* sdg) {
   // saved values of one step for this lane's cells (prefetched a step ahead)
   uint2 ng[2][4], ndy[2];
   float4 nc[2], ncp[2];
+  Waiter wt{a.wait, a.error, 0};
   auto load_step = [&](int t) {
-    if (a.wait) wait_flag(a.wait, T - t - 1, a.error);
+    wt.until(T - t - 1);
     const bool prev = t > 0 || a.has_prev;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -332,9 +350,10 @@ __device__ void backward_body(const BwdArgs& a, int blk, uint16_t* sdg) {
         if (live) *reinterpret_cast<uint2*>(a.dgates + ((size_t)t * B + row) * (4 * kH) + q * kH + unit(h)) = dgp[h][q];
       }
     }
-    if (a.publish) __threadfence();  // dgates_t visible device-wide before the count moves
+    const bool pub = a.publish && pub_step(T - 1 - t, T);
+    if (pub) __threadfence();  // dgates down to t visible device-wide before the count moves
     __syncthreads();  // dgates_t complete in LDS (its other buffer was last read a step ago)
-    if (a.publish && t_ == 0) __hip_atomic_store(a.publish, T - t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (pub && t_ == 0) __hip_atomic_store(a.publish, T - t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) {
@@ -369,8 +388,9 @@ __global__ void __launch_bounds__(256, 1) lstm_backward_kernel(const BwdArgs a) 
 //   consumer   layer 2's recurrence (forward) / layer 1's backward through time,
 //              reading what the projection published.
 // Each hand-off is a per-block step counter, released at agent scope after the
-// data's stores and acquired before its loads; the consumer runs a few steps
-// behind the producer, so the two layers' 1024 steps overlap instead of running
+// data's stores every kPubEvery steps (the fence and the poll are paid once per
+// 8 steps, not per step) and acquired before its loads; the consumer runs a few
+// steps behind the producer, so the two layers' 1024 steps overlap instead of running
 // back to back and layer 2's input projection is no separate GEMM.
 //
 // Placement: block b of the grid is (group b/24, slot b%24); slots 0-7, 8-15 and
@@ -434,8 +454,9 @@ __device__ void project_fwd_body(const uint16_t* __restrict__ y1, const uint16_t
   const bool live = row < B;
   const int xrow = live ? row : 0;
   bf16x8_t hn[4];
+  Waiter wt{wait, error, 0};
   auto load_h = [&](int t) {  // B fragments of h1_t: batch row fr, k = 32kk + 8fk .. +7
-    wait_flag(wait, t, error);
+    wt.until(t);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
       hn[kk] = *reinterpret_cast<const bf16x8_t*>(y1 + ((size_t)t * B + xrow) * kH + kk * 32 + fk * 8);
@@ -459,9 +480,10 @@ __device__ void project_fwd_body(const uint16_t* __restrict__ y1, const uint16_t
         *reinterpret_cast<uint2*>(p + jn * 16) = uint2{(uint32_t)f2bf(acc[jn][0]) | ((uint32_t)f2bf(acc[jn][1]) << 16),
                                                        (uint32_t)f2bf(acc[jn][2]) | ((uint32_t)f2bf(acc[jn][3]) << 16)};
     }
-    __threadfence();
+    const bool pub = pub_step(t, T);
+    if (pub) __threadfence();
     __syncthreads();
-    if (t_ == 0) __hip_atomic_store(publish, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (pub && t_ == 0) __hip_atomic_store(publish, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -493,8 +515,9 @@ __device__ void project_bwd_body(const uint16_t* __restrict__ dgates2, const uin
   const bool live = row < B;
   const int xrow = live ? row : 0;
   bf16x8_t an[16];
+  Waiter wt{wait, error, 0};
   auto load_dg = [&](int t) {  // B fragments of dgates2_t: batch row fr, k = 32ks + 8fk .. +7
-    wait_flag(wait, T - t - 1, error);
+    wt.until(T - t - 1);
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks)
       an[ks] = *reinterpret_cast<const bf16x8_t*>(dgates2 + ((size_t)t * B + xrow) * (4 * kH) + ks * 32 + fk * 8);
@@ -517,9 +540,10 @@ __device__ void project_bwd_body(const uint16_t* __restrict__ dgates2, const uin
         *reinterpret_cast<uint2*>(p + jn * 16) = uint2{(uint32_t)f2bf(acc[jn][0]) | ((uint32_t)f2bf(acc[jn][1]) << 16),
                                                        (uint32_t)f2bf(acc[jn][2]) | ((uint32_t)f2bf(acc[jn][3]) << 16)};
     }
-    __threadfence();
+    const bool pub = pub_step(T - 1 - t, T);
+    if (pub) __threadfence();
     __syncthreads();
-    if (t_ == 0) __hip_atomic_store(publish, T - t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (pub && t_ == 0) __hip_atomic_store(publish, T - t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
