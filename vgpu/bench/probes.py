@@ -585,7 +585,11 @@ def asynccap(cap_mib: int = 8192, graph_mib: int = 1024) -> dict:
     selfpid = ctypes.CDLL(None).vgpu_self_host_pid  # int vgpu_self_host_pid(int* src)
     src = ctypes.c_int(0)
     hp = selfpid(ctypes.byref(src)) or os.getpid()
-    kfd_files = glob.glob(f"/sys/class/kfd/kfd/proc/{hp}/vram_*")
+    kfd_files = glob.glob(f"/sys/class/kfd/kfd/proc/{hp}/vram_*") or \
+        glob.glob(f"/sys/class/kfd/kfd/proc/{os.getpid()}/vram_*")
+    kfd_procs = sorted(os.listdir("/sys/class/kfd/kfd/proc")) if os.path.isdir("/sys/class/kfd/kfd/proc") else None
+    kfd_diag = {"host_pid": hp, "host_pid_src": src.value, "pid": os.getpid(),
+                "kfd_proc_entries": None if kfd_procs is None else len(kfd_procs)}
     kfd_peak = 0
 
     def kfd_vram() -> int:
@@ -662,7 +666,7 @@ def asynccap(cap_mib: int = 8192, graph_mib: int = 1024) -> dict:
         del g
         sample()
     return {"cap": cap_mib * MiB, "baseline": baseline, "peak_over_baseline": peak, "samples": samples,
-            "kfd_vram_peak": kfd_peak, "kfd_files": kfd_files,
+            "kfd_vram_peak": kfd_peak, "kfd_files": kfd_files, "kfd_diag": kfd_diag,
             "max_live_reached": reached, "ooms": ooms, "graphs_replayed": graph_ok, "y": float(y),
             "backend": os.environ.get("PYTORCH_HIP_ALLOC_CONF", ""), "phases": phases}
 
