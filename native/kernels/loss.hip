@@ -18,8 +18,9 @@
 // (incoming gradient × that reciprocal).  Per-row work is mapped by C: one
 // workgroup per row for wide rows (ImageNet's 1000 classes), one lane per row
 // for narrow ones (DeepLab's 21: a wave covers 64 pixels, its NCHW reads are
-// coalesced across lanes).  The mean of the row losses is taken in a fixed
-// order by one workgroup.
+// coalesced across lanes).  The mean is taken in a fixed order: by one
+// workgroup over the row losses (wide rows), or over per-workgroup partials
+// the narrow kernel writes (no atomics: the result is deterministic).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -93,12 +94,17 @@ __global__ void __launch_bounds__(kThreads) xent_wide_kernel(const T* __restrict
 
 // One lane per row (C <= 64): two passes over the row's C logits (max, then
 // Σexp and the gradient), all in registers' reach of L1/L2.
+// Also writes the block's (Σ loss, valid rows) to part[blockIdx.x] for mean_part_kernel
+// (a single-block mean over DeepLab's 147k pixel rows took 158 us).
 template <typename T>
 __global__ void __launch_bounds__(kThreads) xent_narrow_kernel(const T* __restrict__ x, const int64_t* __restrict__ tgt,
                                                                float* __restrict__ loss_rows, T* __restrict__ dx,
-                                                               int64_t rows, int C, int64_t ignore, Layout L) {
-  const int64_t row = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (row >= rows) return;
+                                                               int64_t rows, int C, int64_t ignore, Layout L,
+                                                               float2* __restrict__ part) {
+  __shared__ float sh[kThreads / 64];
+  const int64_t row0 = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const bool in = row0 < rows;
+  const int64_t row = in ? row0 : rows - 1;  // every lane takes part in the block sums
   const int64_t b = L.base(row);
   const int64_t t = tgt[row];
   const bool ok = valid_target(t, C, ignore);
@@ -111,11 +117,33 @@ __global__ void __launch_bounds__(kThreads) xent_narrow_kernel(const T* __restri
     if (c == t) xt = v;
   }
   const float inv = 1.0f / s;
-  for (int c = 0; c < C; ++c) {
-    const float p = __expf(ld(x, b + c * L.cstride) - m) * inv;
-    st(dx, b + c * L.cstride, ok ? p - (c == t ? 1.0f : 0.0f) : 0.0f);
+  if (in)
+    for (int c = 0; c < C; ++c) {
+      const float p = __expf(ld(x, b + c * L.cstride) - m) * inv;
+      st(dx, b + c * L.cstride, ok ? p - (c == t ? 1.0f : 0.0f) : 0.0f);
+    }
+  const float l = (in && ok) ? m + __logf(s) - xt : 0.0f;
+  if (in) loss_rows[row] = l;
+  const float bl = block_reduce<float>(l, sh, false);
+  const float bn = block_reduce<float>((in && ok) ? 1.0f : 0.0f, sh, false);
+  if (threadIdx.x == 0) part[blockIdx.x] = float2{bl, bn};
+}
+
+// out[0] = Σ part.x / Σ part.y, out[1] = 1 / Σ part.y (block partials summed in order).
+__global__ void __launch_bounds__(kThreads) mean_part_kernel(const float2* __restrict__ part, float* __restrict__ out,
+                                                             int n) {
+  __shared__ float sh[kThreads / 64];
+  float s = 0.0f, k = 0.0f;
+  for (int i = threadIdx.x; i < n; i += kThreads) {
+    s += part[i].x;
+    k += part[i].y;
   }
-  loss_rows[row] = ok ? m + __logf(s) - xt : 0.0f;
+  s = block_reduce<float>(s, sh, false);
+  k = block_reduce<float>(k, sh, false);
+  if (threadIdx.x == 0) {
+    out[0] = s / k;
+    out[1] = k > 0.0f ? 1.0f / k : 0.0f;
+  }
 }
 
 // Up to 64 wide rows: one block does every row and the mean (one launch in all).
@@ -169,10 +197,16 @@ int launch(const T* x, const int64_t* tgt, float* loss_rows, float* out, T* dx, 
     hipLaunchKernelGGL(xent_wide_kernel<T>, dim3((unsigned)rows), dim3(kThreads), 0, s, x, tgt, loss_rows, dx, C,
                        ignore, L);
   } else {
+    // block partials live behind the row losses (the caller sizes loss_rows for both)
     const int64_t blocks = (rows + kThreads - 1) / kThreads;
     if (blocks > 0x7fffffffll) return -1;
+    float2* part = reinterpret_cast<float2*>(loss_rows + ((rows + 1) & ~int64_t(1)));
     hipLaunchKernelGGL(xent_narrow_kernel<T>, dim3((unsigned)blocks), dim3(kThreads), 0, s, x, tgt, loss_rows, dx,
-                       rows, C, ignore, L);
+                       rows, C, ignore, L, part);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(mean_part_kernel, dim3(1), dim3(kThreads), 0, s, (const float2*)part, out, (int)blocks);
+    return (int)hipGetLastError();
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
@@ -182,10 +216,18 @@ int launch(const T* x, const int64_t* tgt, float* loss_rows, float* out, T* dx, 
 
 }  // namespace
 
+// fp32 elements loss_rows must hold for vgpu_cross_entropy_fwd_bwd2 (row losses,
+// and for narrow rows the per-block partials behind them).
+VGPU_API int64_t vgpu_cross_entropy_rows_workspace(int64_t rows, int C) {
+  if (rows < 1 || C < 1) return -1;
+  return C > 64 ? rows : ((rows + 1) & ~int64_t(1)) + 2 * ((rows + kThreads - 1) / kThreads);
+}
+
 // logits (bf16 when is_bf16, else fp32) addressed by (hw, bstride, pstride,
 // cstride) as above; targets int64 [rows].  Writes loss_rows fp32 [rows],
 // out fp32 [2] = {mean loss over valid rows, 1 / valid rows}, and dlogits
 // (same dtype and layout as the logits) = unscaled ∂loss_row/∂logits.
+// loss_rows holds vgpu_cross_entropy_rows_workspace(rows, C) floats.
 // Returns 0, -1 (bad arguments) or a hipError_t.
 VGPU_API int vgpu_cross_entropy_fwd_bwd2(const void* logits, const int64_t* tgt, float* loss_rows, float* out,
                                          void* dlogits, int64_t rows, int C, int64_t ignore_index, int64_t hw,

@@ -56,3 +56,49 @@ def test_batched_step_counters_match_per_layer_updates():
         assert all(int(m.num_batches_tracked) == 0 for m in mods)  # deferred
     assert [int(m.num_batches_tracked) for m in mods] == [2, 1, 1]
     assert getattr(B._counters, "pending", None) is None
+
+
+def test_deeplab_channel_padding_is_exact():
+    """DeepLab's MobileNet-V2 stores its channel dims padded to multiples of 64
+    (so every 1x1 conv runs on the native MFMA kernels).  The padded model with
+    an unpadded model's weights computes the same output and loss, gives every
+    real parameter the same gradient, gives the padding exactly zero gradient,
+    and keeps the padding at zero through SGD steps (fp32, CPU)."""
+    import torch
+    import torch.nn.functional as F
+    from vgpu.models.vision import DeepLabV3
+    torch.manual_seed(0)
+    ref = DeepLabV3(num_classes=5, pad_channels=1).train()
+    pad = DeepLabV3(num_classes=5).train()
+    pad.load_unpadded(ref)
+    x = torch.randn(2, 3, 64, 64)
+    tgt = torch.randint(0, 5, (2, 64, 64))
+    opt_r = torch.optim.SGD(ref.parameters(), lr=0.01, momentum=0.9)
+    opt_p = torch.optim.SGD(pad.parameters(), lr=0.01, momentum=0.9)
+    for step in range(3):
+        for o in (opt_r, opt_p):
+            o.zero_grad()
+        lr_, lp = F.cross_entropy(ref(x), tgt), F.cross_entropy(pad(x), tgt)
+        torch.testing.assert_close(lp, lr_, rtol=1e-3 if step else 1e-5, atol=1e-6)
+        lr_.backward()
+        lp.backward()
+        pp = dict(pad.named_parameters())
+        for name, p in ref.named_parameters():
+            q = pp[name]
+            sl = tuple(slice(0, n) for n in p.shape)
+            if step == 0:
+                # (later steps are not compared: the 1e-7 summation-order differences of
+                # the padded convs, amplified by 50 batch-norms over 4x4 maps, reach ~1e-2)
+                torch.testing.assert_close(q.grad[sl], p.grad, rtol=1e-4, atol=1e-6, msg=f"{step} {name}")
+            if q.shape != p.shape:
+                mask = torch.ones_like(q, dtype=torch.bool)
+                mask[sl] = False
+                assert float(q.grad[mask].abs().max()) == 0.0, (step, name)
+        opt_r.step()
+        opt_p.step()
+    for name, p in ref.named_parameters():
+        q = pp[name]
+        if q.shape != p.shape:
+            mask = torch.ones_like(q, dtype=torch.bool)
+            mask[tuple(slice(0, n) for n in p.shape)] = False
+            assert float(q.detach()[mask].abs().max()) == 0.0, name

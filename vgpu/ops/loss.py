@@ -31,6 +31,8 @@ def _lib():
         vp, ci, cl = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
         lib.vgpu_cross_entropy_fwd_bwd2.argtypes = [vp] * 5 + [cl, ci, cl, cl, cl, cl, cl, ci, vp]
         lib.vgpu_cross_entropy_fwd_bwd2.restype = ci
+        lib.vgpu_cross_entropy_rows_workspace.argtypes = [cl, ci]
+        lib.vgpu_cross_entropy_rows_workspace.restype = cl
         _BOUND = True
     return lib
 
@@ -57,11 +59,13 @@ class _CrossEntropyFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target, ignore_index, lay):
         rows, c, hw, bs, ps, cs = lay
-        loss_rows = torch.empty(rows, dtype=torch.float32, device=logits.device)
+        lib = _lib()
+        loss_rows = torch.empty(lib.vgpu_cross_entropy_rows_workspace(rows, c), dtype=torch.float32,
+                                device=logits.device)
         out = torch.empty(2, dtype=torch.float32, device=logits.device)
         dlogits = torch.empty_like(logits)  # same layout as the logits
         p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-        rc = _lib().vgpu_cross_entropy_fwd_bwd2(p(logits), p(target), p(loss_rows), p(out), p(dlogits), rows, c,
+        rc = lib.vgpu_cross_entropy_fwd_bwd2(p(logits), p(target), p(loss_rows), p(out), p(dlogits), rows, c,
                                                 int(ignore_index), hw, bs, ps, cs,
                                                 int(logits.dtype == torch.bfloat16),
                                                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
