@@ -147,7 +147,11 @@ def test_deeplab_native_training_step_matches_torch(gpu_build):
     """DeepLab-v3 (MobileNet-V2 + ASPP) training step: depthwise and 1x1 convs
     on the native kernels against the same bf16 model on MIOpen / PyTorch (51
     batch-norms on 4x4 maps amplify bf16 rounding, so an fp32 model is no
-    reference at this depth)."""
+    reference at this depth; see the fp32 test below).  The two bf16 steps'
+    depthwise gradients measured 0.946-0.995 cosine on different boxes (MIOpen
+    picks its algorithms per box: other rounding, amplified the same way), so
+    the bound is 0.9 -- a wiring error gives ~0; each kernel is held to fp32
+    tightly in its own test."""
     from vgpu.models.vision import DeepLabV3
     from vgpu.ops import dwconv as D
     torch.manual_seed(0)
@@ -172,7 +176,52 @@ def test_deeplab_native_training_step_matches_torch(gpu_build):
         g = m.backbone.features[i].body[-2][0].weight.grad
         gt = mt.backbone.features[i].body[-2][0].weight.grad
         print("deeplab block", i, "dw grad cos", round(_cos(g, gt), 4), "rel", round(_rel(g, gt), 4))
-        assert _cos(g, gt) > 0.95, i
+        assert _cos(g, gt) > 0.9, i
+
+
+def test_deeplab_native_step_loss_and_grads_vs_fp32(gpu_build):
+    """The whole 4.2 training step as the pod runs it (channel-padded bf16 model:
+    native convs / depthwise / BN / cross-entropy) against the same weights in
+    fp32 on PyTorch, and against PyTorch's own bf16 step.
+
+    Measured (scripts/deeplab_grad_check.py, profiles/r6/deeplab_grads.md): at
+    random init the early-layer gradients of ANY bf16 step are far from fp32's
+    (cosine 0.1-0.5 for PyTorch/MIOpen bf16 as for the native path: 17 train-mode
+    BatchNorms over few pixels cancel most of the gradient), while the loss and
+    the head gradient agree.  So the fp32 bounds are: loss and head gradient
+    tight; stem and depthwise gradients no further from fp32 than PyTorch's
+    bf16 step is (margin 0.1), and close to that step."""
+    from vgpu.models.vision import DeepLabV3
+    from vgpu.ops.loss import cross_entropy
+    torch.manual_seed(0)
+    m = DeepLabV3(num_classes=21).cuda().train()
+    ref = copy.deepcopy(m).float()
+    m = m.to(torch.bfloat16).to(memory_format=CL)
+    mt = copy.deepcopy(m)
+    x = _x((4, 3, 128, 128), 21)
+    tgt = torch.randint(0, 21, (4, 128, 128), device="cuda")
+    loss = cross_entropy(m(x), tgt)
+    loss.backward()
+    loss_r = _torch_path(lambda: torch.nn.functional.cross_entropy(ref(x.float()), tgt))
+    loss_r.backward()
+    loss_t = _torch_path(lambda: torch.nn.functional.cross_entropy(mt(x).float(), tgt))
+    _torch_path(loss_t.backward)
+
+    def grads(mod):
+        g = {"stem": mod.backbone.features[0][0].weight.grad, "head": mod.head.weight.grad}
+        g.update({f"dw{i}": mod.backbone.features[i].body[-2][0].weight.grad for i in (1, 5, 12, 16)})
+        return g
+    gn, gr, gt = grads(m), grads(ref), grads(mt)
+    print("deeplab loss native", loss.item(), "torch bf16", loss_t.item(), "fp32", loss_r.item())
+    for k in gn:
+        print(k, "cos native/fp32", round(_cos(gn[k], gr[k]), 4), "torch bf16/fp32", round(_cos(gt[k], gr[k]), 4),
+              "native/torch bf16", round(_cos(gn[k], gt[k]), 4))
+    assert abs(loss.item() - loss_r.item()) < 2e-3 * loss_r.item()
+    assert _cos(gn["head"], gr["head"]) > 0.99
+    for k in gn:
+        assert _cos(gn[k], gr[k]) > _cos(gt[k], gr[k]) - 0.1, k
+        assert _cos(gn[k], gt[k]) > 0.8, k  # measured 0.91-0.94 (see the test above)
+    assert not gn["stem"][32:].any()  # the padding carried no gradient
 
 
 def test_resize_bilinear_backward_matches_pytorch(gpu_build):
