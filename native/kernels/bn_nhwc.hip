@@ -342,11 +342,15 @@ __device__ __forceinline__ void merge_chunk(const float2* __restrict__ partial, 
   __syncthreads();
 }
 
+// shift: the reduction's shift row (x row 0; the plain path's bn_reduce_kernel
+// sums x - x0), null for the conv epilogues' unshifted sums.  coef (s, t at
+// [0, C) and [C, 2C)), mean and invstd outputs are each nullable.
 template <int kAct, typename P>
 __global__ void __launch_bounds__(kFuseT) bn_fwd_fused_kernel(
     const float2* __restrict__ partial, int64_t G, const bf16x8* __restrict__ x, bf16x8* __restrict__ y,
     const P* __restrict__ gamma, const P* __restrict__ beta, P* __restrict__ run_mean, P* __restrict__ run_var,
-    float* __restrict__ coef, int64_t M, int C, float eps, float momentum, int64_t rows_per) {
+    float* __restrict__ coef, float* __restrict__ mean_out, float* __restrict__ invstd_out,
+    const uint16_t* __restrict__ shift, int64_t M, int C, float eps, float momentum, int64_t rows_per) {
   __shared__ double r1[kFuseQ][kFuseC], r2[kFuseQ][kFuseC];
   __shared__ float sS[kFuseC], sT[kFuseC];
   const int c0 = blockIdx.x * kFuseC;
@@ -359,18 +363,21 @@ __global__ void __launch_bounds__(kFuseT) bn_fwd_fused_kernel(
       s1 += r1[q][threadIdx.x];
       s2 += r2[q][threadIdx.x];
     }
-    const double n = (double)M, mu = s1 / n;
-    double var = s2 / n - mu * mu;
+    const double n = (double)M, m1 = s1 / n;
+    double var = s2 / n - m1 * m1;
     if (var < 0.0) var = 0.0;
+    const double mu = (shift ? (double)bf2f(shift[c]) : 0.0) + m1;
     const float is = (float)(1.0 / sqrt(var + (double)eps));
     const float sc = ldp(gamma, c, 1.0f) * is, sh = ldp(beta, c, 0.0f) - (float)mu * sc;
     sS[threadIdx.x] = sc;
     sT[threadIdx.x] = sh;
     if (blockIdx.y == 0) {
-      coef[c] = sc;
-      coef[C + c] = sh;
-      coef[2 * C + c] = (float)mu;
-      coef[3 * C + c] = is;
+      if (coef) {
+        coef[c] = sc;
+        coef[C + c] = sh;
+      }
+      if (mean_out) mean_out[c] = (float)mu;
+      if (invstd_out) invstd_out[c] = is;
       if (run_mean) {
         const float unbiased = (float)(M > 1 ? var * n / (n - 1.0) : var);
         stp(run_mean, c, (1.0f - momentum) * ldp(run_mean, c, 0.0f) + momentum * (float)mu);
@@ -397,15 +404,17 @@ __global__ void __launch_bounds__(kFuseT) bn_fwd_fused_kernel(
   }
 }
 
-// dz already carries act' (the data-gradient epilogue applied it): dx = s·dz + cc·x + b (+ add).
-template <bool kAdd, typename P>
+// kAct == 0: dz already carries act' (the data-gradient epilogue applied it);
+// else dz = dy·act'(x·s + t) here (the plain path's reduction partials).
+// dx = s·dz + cc·x + b (+ add).
+template <int kAct, bool kAdd, typename P>
 __global__ void __launch_bounds__(kFuseT) bn_bwd_fused_kernel(
     const float2* __restrict__ partial, int64_t G, const bf16x8* __restrict__ dz, const bf16x8* __restrict__ x,
-    bf16x8* __restrict__ dx, const bf16x8* __restrict__ add, const P* __restrict__ gamma,
+    bf16x8* __restrict__ dx, const bf16x8* __restrict__ add, const P* __restrict__ gamma, const P* __restrict__ beta,
     const float* __restrict__ mean, const float* __restrict__ invstd, P* __restrict__ dgamma, P* __restrict__ dbeta,
     int64_t M, int C, int64_t rows_per) {
   __shared__ double r1[kFuseQ][kFuseC], r2[kFuseQ][kFuseC];
-  __shared__ float sS[kFuseC], sC[kFuseC], sB[kFuseC];
+  __shared__ float sS[kFuseC], sC[kFuseC], sB[kFuseC], sT[kFuseC];
   const int c0 = blockIdx.x * kFuseC;
   merge_chunk(partial, G, C, c0, r1, r2);
   if (threadIdx.x < kFuseC) {
@@ -428,15 +437,17 @@ __global__ void __launch_bounds__(kFuseT) bn_bwd_fused_kernel(
     sS[threadIdx.x] = sc;
     sC[threadIdx.x] = cc;
     sB[threadIdx.x] = -sc * db * inv_m - mu * cc;
+    sT[threadIdx.x] = ldp(beta, c, 0.0f) - mu * sc;
   }
   __syncthreads();
   const int cg = threadIdx.x & 7, ro = threadIdx.x >> 3;
-  float sc[8], cc[8], bb[8];
+  float sc[8], cc[8], bb[8], tt[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     sc[j] = sS[cg * 8 + j];
     cc[j] = sC[cg * 8 + j];
     bb[j] = sB[cg * 8 + j];
+    tt[j] = sT[cg * 8 + j];
   }
   const int cvec = C >> 3, cv = (c0 >> 3) + cg;
   const int64_t r_end = (int64_t)(blockIdx.y + 1) * rows_per < M ? (int64_t)(blockIdx.y + 1) * rows_per : M;
@@ -448,7 +459,211 @@ __global__ void __launch_bounds__(kFuseT) bn_bwd_fused_kernel(
     bf16x8 o;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float d = fmaf(sc[k], bf2f(g.v[k]), fmaf(cc[k], bf2f(v.v[k]), bb[k]));
+      const float xf = bf2f(v.v[k]);
+      float gz = bf2f(g.v[k]);
+      if constexpr (kAct != 0) gz *= act_grad<kAct>(fmaf(xf, sc[k], tt[k]));
+      float d = fmaf(sc[k], gz, fmaf(cc[k], xf, bb[k]));
+      if constexpr (kAdd) d += bf2f(rr.v[k]);
+      o.v[k] = f2bf(d);
+    }
+    dx[i] = o;
+  }
+}
+
+// ---- one launch per BatchNorm direction for small layers --------------------------
+// DeepLab-v3 4.2 (b=1, 384²) runs 46 of its 56 BatchNorms on 24² / 48² maps
+// (576 / 2304 rows): there a reduce, a finalize and an apply were three ~4.7 us
+// launches for well under a microsecond of memory traffic each, 1/3 of the
+// step's dispatches (profiles/r6/train).  Here one 1024-thread workgroup owns a
+// 64-channel chunk and ALL its rows: it reduces (shifted sums as
+// bn_reduce_kernel, fp32 per thread, 8-row wave shuffles, fp64 across the 16
+// waves), finalizes, and applies from the same registers: a thread loads its
+// kSmallR rows once, all in flight together (a first version re-read them in
+// a row loop: 8.5 / 15.7 us forward / backward at 576 rows, latency-bound,
+// profiles/r6/train).  Rows <= kSmallMaxM (640: DeepLab's 24² maps).
+constexpr int kSmallR = 5;
+constexpr int64_t kSmallMaxM = (int64_t)kSmallR * (kFuseT / 8);  // 640
+// The backward holds x and dy: 512 threads (a 256-VGPR budget), 10 rows each.
+constexpr int kSmallBT = 512, kSmallBR = 10;
+static_assert((int64_t)kSmallBR * (kSmallBT / 8) == kSmallMaxM, "backward covers the same rows");
+
+__device__ __forceinline__ void wave_rows_reduce(float (&a1)[8], float (&a2)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) {  // lanes cg + 8·row: xor over the row bits
+      a1[j] += __shfl_xor(a1[j], o, 64);
+      a2[j] += __shfl_xor(a2[j], o, 64);
+    }
+}
+
+template <int kAct, typename P>
+__global__ void __launch_bounds__(kFuseT) bn_fwd_small_kernel(
+    const bf16x8* __restrict__ x, bf16x8* __restrict__ y, const P* __restrict__ gamma, const P* __restrict__ beta,
+    P* __restrict__ run_mean, P* __restrict__ run_var, float* __restrict__ mean, float* __restrict__ invstd,
+    float* __restrict__ coef, int64_t M, int C, float eps, float momentum) {
+  __shared__ float2 red[kFuseT / 64][kFuseC];
+  __shared__ float sS[kFuseC], sT[kFuseC];
+  const int cg = threadIdx.x & 7, ro = threadIdx.x >> 3, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * kFuseC;
+  const int cvec = C >> 3, cv = (c0 >> 3) + cg;
+  float k0[8], a1[8], a2[8];
+  bf16x8 v[kSmallR];
+#pragma unroll
+  for (int u = 0; u < kSmallR; ++u) {  // rows past M read row 0: shifted, they add 0
+    const int64_t r = ro + u * (kFuseT / 8);
+    v[u] = x[(r < M ? r : 0) * cvec + cv];
+  }
+  const bf16x8 v0 = x[cv];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    k0[j] = bf2f(v0.v[j]);
+    a1[j] = a2[j] = 0.0f;
+  }
+#pragma unroll
+  for (int u = 0; u < kSmallR; ++u)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = bf2f(v[u].v[j]) - k0[j];
+      a1[j] += d;
+      a2[j] = fmaf(d, d, a2[j]);
+    }
+  wave_rows_reduce(a1, a2);
+  if (lane < 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = make_float2(a1[j], a2[j]);
+  __syncthreads();
+  if (threadIdx.x < kFuseC) {
+    const int c = c0 + threadIdx.x;
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int w = 0; w < kFuseT / 64; ++w) {
+      s1 += red[w][threadIdx.x].x;
+      s2 += red[w][threadIdx.x].y;
+    }
+    const double n = (double)M, m1 = s1 / n;
+    double var = s2 / n - m1 * m1;
+    if (var < 0.0) var = 0.0;
+    const double mu = (double)bf2f(reinterpret_cast<const uint16_t*>(x)[c]) + m1;
+    const float is = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = ldp(gamma, c, 1.0f) * is, sh = ldp(beta, c, 0.0f) - (float)mu * sc;
+    sS[threadIdx.x] = sc;
+    sT[threadIdx.x] = sh;
+    mean[c] = (float)mu;
+    invstd[c] = is;
+    if (coef) {
+      coef[c] = sc;
+      coef[C + c] = sh;
+    }
+    if (run_mean) {
+      const float unbiased = (float)(M > 1 ? var * n / (n - 1.0) : var);
+      stp(run_mean, c, (1.0f - momentum) * ldp(run_mean, c, 0.0f) + momentum * (float)mu);
+      stp(run_var, c, (1.0f - momentum) * ldp(run_var, c, 0.0f) + momentum * unbiased);
+    }
+  }
+  __syncthreads();
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = sS[cg * 8 + j];
+    sh[j] = sT[cg * 8 + j];
+  }
+#pragma unroll
+  for (int u = 0; u < kSmallR; ++u) {
+    const int64_t r = ro + u * (kFuseT / 8);
+    if (r >= M) break;
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.v[k] = f2bf(act_fwd<kAct>(fmaf(bf2f(v[u].v[k]), sc[k], sh[k])));
+    y[r * cvec + cv] = o;
+  }
+}
+
+// Σ dz, Σ dz·x̂ (dz = dy·act'(x·s + t)), dγ / dβ, then dx = s·dz + cc·x + b (+ add):
+// bn_reduce_kernel<1> + bn_bwd_finalize_kernel + bn_bwd_apply_kernel in one launch.
+template <int kAct, bool kAdd, typename P>
+__global__ void __launch_bounds__(kSmallBT) bn_bwd_small_kernel(
+    const bf16x8* __restrict__ dy, const bf16x8* __restrict__ x, bf16x8* __restrict__ dx,
+    const bf16x8* __restrict__ add, const P* __restrict__ gamma, const P* __restrict__ beta,
+    const float* __restrict__ mean, const float* __restrict__ invstd, P* __restrict__ dgamma,
+    P* __restrict__ dbeta, int64_t M, int C) {
+  __shared__ float2 red[kSmallBT / 64][kFuseC];
+  __shared__ float sC[kFuseC], sB[kFuseC];
+  const int cg = threadIdx.x & 7, ro = threadIdx.x >> 3, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * kFuseC;
+  const int cvec = C >> 3, cv = (c0 >> 3) + cg;
+  float sc[8], sh[8], mu[8], is[8], a1[8], a2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + cg * 8 + j;
+    is[j] = invstd[c];
+    mu[j] = mean[c];
+    sc[j] = ldp(gamma, c, 1.0f) * is[j];
+    sh[j] = ldp(beta, c, 0.0f) - mu[j] * sc[j];
+    a1[j] = a2[j] = 0.0f;
+  }
+  bf16x8 v[kSmallBR], g[kSmallBR];
+#pragma unroll
+  for (int u = 0; u < kSmallBR; ++u) {
+    const int64_t r = ro + u * (kSmallBT / 8);
+    const int64_t i = (r < M ? r : 0) * cvec + cv;
+    v[u] = x[i];
+    g[u] = dy[i];
+  }
+#pragma unroll
+  for (int u = 0; u < kSmallBR; ++u) {
+    const float ok = ro + u * (kSmallBT / 8) < M ? 1.0f : 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xf = bf2f(v[u].v[j]);
+      const float dz = bf2f(g[u].v[j]) * act_grad<kAct>(fmaf(xf, sc[j], sh[j])) * ok;
+      a1[j] += dz;
+      a2[j] = fmaf(dz, (xf - mu[j]) * is[j], a2[j]);
+    }
+  }
+  wave_rows_reduce(a1, a2);
+  if (lane < 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = make_float2(a1[j], a2[j]);
+  __syncthreads();
+  if (threadIdx.x < kFuseC) {
+    const int c = c0 + threadIdx.x;
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int w = 0; w < kSmallBT / 64; ++w) {
+      s1 += red[w][threadIdx.x].x;
+      s2 += red[w][threadIdx.x].y;
+    }
+    const float db = (float)s1, dg = (float)s2;
+    if (dgamma) stp(dgamma, c, dg);
+    if (dbeta) stp(dbeta, c, db);
+    const float isc = invstd[c];
+    const float s_ = ldp(gamma, c, 1.0f) * isc;
+    const float inv_m = (float)(1.0 / (double)M);
+    const float cc = -s_ * isc * dg * inv_m;
+    sC[threadIdx.x] = cc;
+    sB[threadIdx.x] = -s_ * db * inv_m - mean[c] * cc;
+  }
+  __syncthreads();
+  float cc[8], bb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    cc[j] = sC[cg * 8 + j];
+    bb[j] = sB[cg * 8 + j];
+  }
+#pragma unroll
+  for (int u = 0; u < kSmallBR; ++u) {
+    const int64_t r = ro + u * (kSmallBT / 8);
+    if (r >= M) break;
+    const int64_t i = r * cvec + cv;
+    bf16x8 rr;
+    if constexpr (kAdd) rr = add[i];
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float xf = bf2f(v[u].v[k]);
+      const float dz = bf2f(g[u].v[k]) * act_grad<kAct>(fmaf(xf, sc[k], sh[k]));
+      float d = fmaf(sc[k], dz, fmaf(cc[k], xf, bb[k]));
       if constexpr (kAdd) d += bf2f(rr.v[k]);
       o.v[k] = f2bf(d);
     }
@@ -470,12 +685,23 @@ inline dim3 fused_grid(int64_t M, int C, int64_t& rows_per) {
 }
 
 int g_fuse_small = -1;  // VGPU_BN_FUSE_SMALL=0 / vgpu_bn_set_fuse_small: separate finalize launches
-inline bool fused_ok(int64_t G, int C) {
+inline bool fuse_on();
+inline bool fused_ok(int64_t G, int C) { return fuse_on() && G <= kFuseMaxG && C % kFuseC == 0; }
+
+// The plain path (statistics reduced here): kind 0 = reduce / finalize / apply
+// (three launches), 1 = reduce + finalize-and-apply (bn_*_fused_kernel over the
+// reduction's <= 128 partials, two launches), 2 = one bn_*_small_kernel launch.
+inline bool fuse_on() {
   if (g_fuse_small < 0) {
     const char* v = getenv("VGPU_BN_FUSE_SMALL");
     g_fuse_small = (v && v[0] == '0') ? 0 : 1;
   }
-  return g_fuse_small == 1 && G <= kFuseMaxG && C % kFuseC == 0;
+  return g_fuse_small == 1;
+}
+
+inline int plain_kind(int64_t M, int C) {
+  if (!fuse_on() || C % kFuseC) return 0;
+  return M <= kSmallMaxM ? 2 : 1;
 }
 
 struct Plan {
@@ -488,7 +714,8 @@ Plan make_plan(int64_t M, int C) {
   p.chunk = C <= kMaxChunk ? C : kMaxChunk;
   p.nchunks = (C + p.chunk - 1) / p.chunk;
   p.rpb = kThreads / (p.chunk / 8);
-  int64_t target = g_target_blocks / p.nchunks;
+  const int tb = plain_kind(M, C) == 1 ? 128 : g_target_blocks;  // kind 1: G <= 128 <= kFuseMaxG
+  int64_t target = tb / p.nchunks;
   if (target < 1) target = 1;
   int64_t iters = (M + p.rpb * target - 1) / (p.rpb * target);
   iters = (iters + g_unroll - 1) / g_unroll * g_unroll;
@@ -512,22 +739,48 @@ template <typename P>
 int fwd_train(const void* x, void* y, const void* gamma, const void* beta, void* run_mean, void* run_var,
               float* mean, float* invstd, float* ws, int64_t M, int C, float eps, float momentum, int act,
               hipStream_t s, float* coef_out = nullptr) {
+  const int kind = plain_kind(M, C);
+  const auto* xv = static_cast<const bf16x8*>(x);
+  auto* yv = static_cast<bf16x8*>(y);
+  const auto* g_ = static_cast<const P*>(gamma);
+  const auto* b_ = static_cast<const P*>(beta);
+  auto* rm = static_cast<P*>(run_mean);
+  auto* rv = static_cast<P*>(run_var);
+  if (kind == 2) {
+    const dim3 grid((unsigned)(C / kFuseC));
+    switch (act) {
+      case 0: hipLaunchKernelGGL((bn_fwd_small_kernel<0, P>), grid, dim3(kFuseT), 0, s, xv, yv, g_, b_, rm, rv, mean, invstd, coef_out, M, C, eps, momentum); break;
+      case 1: hipLaunchKernelGGL((bn_fwd_small_kernel<1, P>), grid, dim3(kFuseT), 0, s, xv, yv, g_, b_, rm, rv, mean, invstd, coef_out, M, C, eps, momentum); break;
+      case 2: hipLaunchKernelGGL((bn_fwd_small_kernel<2, P>), grid, dim3(kFuseT), 0, s, xv, yv, g_, b_, rm, rv, mean, invstd, coef_out, M, C, eps, momentum); break;
+      default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+  }
   const Plan p = make_plan(M, C);
   auto* partial = reinterpret_cast<float2*>(ws);
   float* coef = coef_out ? coef_out : ws + 2 * p.G * C;  // s, t
-  const auto* xv = static_cast<const bf16x8*>(x);
   if (g_unroll == 8)
     hipLaunchKernelGGL((bn_reduce_kernel<0, 0, P, 8>), dim3((unsigned)p.G, p.nchunks), dim3(kThreads), 0, s, xv,
                        nullptr, nullptr, nullptr, nullptr, nullptr, partial, M, C, p.chunk, p.rows_per_block);
   else
     hipLaunchKernelGGL((bn_reduce_kernel<0, 0, P>), dim3((unsigned)p.G, p.nchunks), dim3(kThreads), 0, s, xv,
                        nullptr, nullptr, nullptr, nullptr, nullptr, partial, M, C, p.chunk, p.rows_per_block);
+  if (kind == 1) {
+    int64_t rows_per;
+    const dim3 grid = fused_grid(M, C, rows_per);
+    const auto* xs = static_cast<const uint16_t*>(x);
+    switch (act) {
+      case 0: hipLaunchKernelGGL((bn_fwd_fused_kernel<0, P>), grid, dim3(kFuseT), 0, s, partial, p.G, xv, yv, g_, b_, rm, rv, coef, mean, invstd, xs, M, C, eps, momentum, rows_per); break;
+      case 1: hipLaunchKernelGGL((bn_fwd_fused_kernel<1, P>), grid, dim3(kFuseT), 0, s, partial, p.G, xv, yv, g_, b_, rm, rv, coef, mean, invstd, xs, M, C, eps, momentum, rows_per); break;
+      case 2: hipLaunchKernelGGL((bn_fwd_fused_kernel<2, P>), grid, dim3(kFuseT), 0, s, partial, p.G, xv, yv, g_, b_, rm, rv, coef, mean, invstd, xs, M, C, eps, momentum, rows_per); break;
+      default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL((bn_fwd_finalize_kernel<P>), dim3((C + kFinC - 1) / kFinC), dim3(kFinC * kFinG), 0, s,
-                     partial, p.G, static_cast<const uint16_t*>(x), static_cast<const P*>(gamma),
-                     static_cast<const P*>(beta), static_cast<P*>(run_mean), static_cast<P*>(run_var), mean,
-                     invstd, coef, M, C, eps, momentum);
+                     partial, p.G, static_cast<const uint16_t*>(x), g_, b_, rm, rv, mean, invstd, coef, M, C, eps,
+                     momentum);
   const uint64_t nvec = (uint64_t)M * (C / 8);
-  auto* yv = static_cast<bf16x8*>(y);
   switch (act) {
     case 0: hipLaunchKernelGGL(bn_apply_kernel<0>, dim3(grid_for(nvec)), dim3(kThreads), 0, s, xv, yv, coef, nvec, C / 8); break;
     case 1: hipLaunchKernelGGL(bn_apply_kernel<1>, dim3(grid_for(nvec)), dim3(kThreads), 0, s, xv, yv, coef, nvec, C / 8); break;
@@ -541,6 +794,17 @@ template <int kAct, typename P>
 void bwd_launch(const bf16x8* dyv, const bf16x8* xv, bf16x8* dxv, const P* gamma, const P* beta,
                 const float* mean, const float* invstd, P* dgamma, P* dbeta, float* ws, int64_t M, int C,
                 const bf16x8* addv, hipStream_t s) {
+  const int kind = plain_kind(M, C);
+  if (kind == 2) {
+    const dim3 grid((unsigned)(C / kFuseC));
+    if (addv)
+      hipLaunchKernelGGL((bn_bwd_small_kernel<kAct, true, P>), grid, dim3(kSmallBT), 0, s, dyv, xv, dxv, addv, gamma,
+                         beta, mean, invstd, dgamma, dbeta, M, C);
+    else
+      hipLaunchKernelGGL((bn_bwd_small_kernel<kAct, false, P>), grid, dim3(kSmallBT), 0, s, dyv, xv, dxv, addv, gamma,
+                         beta, mean, invstd, dgamma, dbeta, M, C);
+    return;
+  }
   const Plan p = make_plan(M, C);
   auto* partial = reinterpret_cast<float2*>(ws);
   float* coef = ws + 2 * p.G * C;
@@ -550,6 +814,17 @@ void bwd_launch(const bf16x8* dyv, const bf16x8* xv, bf16x8* dxv, const P* gamma
   else
     hipLaunchKernelGGL((bn_reduce_kernel<1, kAct, P>), dim3((unsigned)p.G, p.nchunks), dim3(kThreads), 0, s,
                        xv, dyv, gamma, beta, mean, invstd, partial, M, C, p.chunk, p.rows_per_block);
+  if (kind == 1) {
+    int64_t rows_per;
+    const dim3 grid = fused_grid(M, C, rows_per);
+    if (addv)
+      hipLaunchKernelGGL((bn_bwd_fused_kernel<kAct, true, P>), grid, dim3(kFuseT), 0, s, partial, p.G, dyv, xv, dxv,
+                         addv, gamma, beta, mean, invstd, dgamma, dbeta, M, C, rows_per);
+    else
+      hipLaunchKernelGGL((bn_bwd_fused_kernel<kAct, false, P>), grid, dim3(kFuseT), 0, s, partial, p.G, dyv, xv,
+                         dxv, addv, gamma, beta, mean, invstd, dgamma, dbeta, M, C, rows_per);
+    return;
+  }
   hipLaunchKernelGGL((bn_bwd_finalize_kernel<P>), dim3((C + kFinC - 1) / kFinC), dim3(kFinC * kFinG), 0, s,
                      partial, p.G, gamma, beta, mean, invstd, dgamma, dbeta, coef, M, C);
   const uint64_t nvec = (uint64_t)M * (C / 8);
@@ -654,7 +929,7 @@ VGPU_API int vgpu_bn_act_fwd_partials(const float* partial, int64_t G, const voi
 #define VGPU_BN_FWD_FUSED(A, P_)                                                                                   \
   hipLaunchKernelGGL((bn_fwd_fused_kernel<A, P_>), grid, dim3(kFuseT), 0, s, pp, G, xv, yv,                      \
                      static_cast<const P_*>(gamma), static_cast<const P_*>(beta), static_cast<P_*>(run_mean),      \
-                     static_cast<P_*>(run_var), coef, M, C, eps, momentum, rows_per)
+                     static_cast<P_*>(run_var), coef, mean, invstd, nullptr, M, C, eps, momentum, rows_per)
     if (param_bf16) {
       if (act == 0) VGPU_BN_FWD_FUSED(0, uint16_t); else if (act == 1) VGPU_BN_FWD_FUSED(1, uint16_t); else VGPU_BN_FWD_FUSED(2, uint16_t);
     } else {
@@ -721,9 +996,9 @@ VGPU_API int vgpu_bn_bwd_partials(const float* partial, int64_t G, const void* d
     auto* dxv = static_cast<bf16x8*>(dx);
     const auto* addv = static_cast<const bf16x8*>(add);
 #define VGPU_BN_BWD_FUSED(K, P_)                                                                                   \
-  hipLaunchKernelGGL((bn_bwd_fused_kernel<K, P_>), grid, dim3(kFuseT), 0, s, pp, G, dzv, xv, dxv, addv,          \
-                     static_cast<const P_*>(gamma), mean, invstd, static_cast<P_*>(dgamma), static_cast<P_*>(dbeta), \
-                     M, C, rows_per)
+  hipLaunchKernelGGL((bn_bwd_fused_kernel<0, K, P_>), grid, dim3(kFuseT), 0, s, pp, G, dzv, xv, dxv, addv,       \
+                     static_cast<const P_*>(gamma), static_cast<const P_*>(beta), mean, invstd,                     \
+                     static_cast<P_*>(dgamma), static_cast<P_*>(dbeta), M, C, rows_per)
     if (param_bf16) {
       if (addv) VGPU_BN_BWD_FUSED(true, uint16_t); else VGPU_BN_BWD_FUSED(false, uint16_t);
     } else {

@@ -517,8 +517,10 @@ int64_t wgrad_splits(int N, int H, int W, int C, int Cout, int KS, int stride, i
   double best = 1e30;
   for (int64_t sp = 1; sp <= 1024 && sp <= (steps_total + 3) / 4; sp *= 2) {
     const double waves = (double)((tiles * sp + (int64_t)slots - 1) / (int64_t)slots);
+    // (+ 4 us for the reduce's own launch when split: a dispatch inside a
+    // replayed graph costs ~4.7 us however small, profiles/r6/train)
     const double est = waves * (t_step * (double)((steps_total + sp - 1) / sp) + 3.0) +
-                       (sp > 1 ? 2.0 * sp * tile_bytes / 4.0e6 : tile_bytes / 8.0e6);
+                       (sp > 1 ? 2.0 * sp * tile_bytes / 4.0e6 + 4.0 : tile_bytes / 8.0e6);
     if (est < best) { best = est; splits = sp; }
   }
   return splits;

@@ -18,6 +18,13 @@
 //     each thread its own slab: 64k partial rows whose one-thread-per-element
 //     reduce cost 59 µs a layer, profiles/r5/train/prof_4_2_after.md.)
 // fp32 accumulation, one bf16 rounding per output (forward / data gradient).
+//
+// Weights: fp32 [9][C] (the inference path's BN-folded filter), or the
+// module's own bf16 [C][9] ([C,1,3,3] as stored) -- a thread's 8 channels x 9
+// taps are then one contiguous 144-byte run, nine 16-byte loads; the weight
+// gradient is written in that layout too.  (Converting the filter to fp32
+// [9][C] and back per layer and step was 4 launches per depthwise layer, 68 a
+// DeepLab step: profiles/r6/train.)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -53,13 +60,44 @@ __device__ __forceinline__ void load_w8(const float* __restrict__ w, int C, int 
   f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
 }
 
+// A thread's 8 channels x 9 taps of a bf16 [C][9] filter (w + c8 * 9: 144-B
+// aligned, since c8 is a multiple of 8).
+struct W72 {
+  u32x4 q[9];
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ w, int c8) {
+    const u32x4* p = reinterpret_cast<const u32x4*>(w + (int64_t)c8 * 9);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) q[i] = p[i];
+  }
+  // channel j, tap k (compile-time after unrolling)
+  __device__ __forceinline__ float at(int j, int k) const {
+    const int e = j * 9 + k;
+    const u32x4 v = q[e >> 3];
+    const int wd = (e & 7) >> 1;
+    const uint32_t u = wd == 0 ? v.x : (wd == 1 ? v.y : (wd == 2 ? v.z : v.w));
+    return __uint_as_float((e & 1) ? (u & 0xffff0000u) : (u << 16));
+  }
+};
+
+template <bool kC9>
+__device__ __forceinline__ void tap_w8(const void* __restrict__ w, const W72& wc, int C, int tap, int c8,
+                                       float (&f)[8]) {
+  if constexpr (kC9) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = wc.at(j, tap);
+  } else {
+    load_w8(static_cast<const float*>(w), C, tap, c8, f);
+  }
+}
+
 struct Shape {
   int N, H, W, C, OH, OW, stride, dil;
 };
 
 // bias (fp32 [C], optional) and act (0 none, 1 ReLU, 2 ReLU6): a folded
 // BatchNorm + activation in inference (vgpu.models.vision DeepLab fusion).
-__global__ void __launch_bounds__(kThreads) dw_fwd_kernel(const u32x4* __restrict__ x, const float* __restrict__ w,
+template <bool kC9>
+__global__ void __launch_bounds__(kThreads) dw_fwd_kernel(const u32x4* __restrict__ x, const void* __restrict__ w,
                                                           const float* __restrict__ bias, int act,
                                                           u32x4* __restrict__ y, const Shape s, int64_t total) {
   const int cv = s.C / 8;
@@ -72,6 +110,8 @@ __global__ void __launch_bounds__(kThreads) dw_fwd_kernel(const u32x4* __restric
     const int n = (int)(r / s.OH);
     const int h0 = oh * s.stride - s.dil, w0 = ow * s.stride - s.dil;
     const u32x4* xn = x + (int64_t)n * s.H * s.W * cv + cg;
+    W72 wc;
+    if constexpr (kC9) wc.load(static_cast<const uint16_t*>(w), cg * 8);
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
@@ -83,7 +123,7 @@ __global__ void __launch_bounds__(kThreads) dw_fwd_kernel(const u32x4* __restric
         if ((unsigned)iw >= (unsigned)s.W) continue;
         float xv[8], wv[8];
         unpack8(xn[((int64_t)ih * s.W + iw) * cv], xv);
-        load_w8(w, s.C, kh * 3 + kw, cg * 8, wv);
+        tap_w8<kC9>(w, wc, s.C, kh * 3 + kw, cg * 8, wv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] = fmaf(xv[j], wv[j], acc[j]);
       }
@@ -103,7 +143,8 @@ __global__ void __launch_bounds__(kThreads) dw_fwd_kernel(const u32x4* __restric
   }
 }
 
-__global__ void __launch_bounds__(kThreads) dw_dgrad_kernel(const u32x4* __restrict__ dy, const float* __restrict__ w,
+template <bool kC9>
+__global__ void __launch_bounds__(kThreads) dw_dgrad_kernel(const u32x4* __restrict__ dy, const void* __restrict__ w,
                                                             u32x4* __restrict__ dx, const Shape s, int64_t total) {
   const int cv = s.C / 8;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < total; i += (int64_t)gridDim.x * kThreads) {
@@ -114,6 +155,8 @@ __global__ void __launch_bounds__(kThreads) dw_dgrad_kernel(const u32x4* __restr
     const int ih = (int)(r % s.H);
     const int n = (int)(r / s.H);
     const u32x4* dyn = dy + (int64_t)n * s.OH * s.OW * cv + cg;
+    W72 wc;
+    if constexpr (kC9) wc.load(static_cast<const uint16_t*>(w), cg * 8);
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
@@ -130,7 +173,7 @@ __global__ void __launch_bounds__(kThreads) dw_dgrad_kernel(const u32x4* __restr
         if (ow >= s.OW) continue;
         float gv[8], wv[8];
         unpack8(dyn[((int64_t)oh * s.OW + ow) * cv], gv);
-        load_w8(w, s.C, kh * 3 + kw, cg * 8, wv);
+        tap_w8<kC9>(w, wc, s.C, kh * 3 + kw, cg * 8, wv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] = fmaf(gv[j], wv[j], acc[j]);
       }
@@ -218,8 +261,10 @@ __global__ void __launch_bounds__(kThreads) dw_wgrad_kernel(const u32x4* __restr
 
 // dw[i] = Σ_slab part[slab][i] for i < 9C: 16 threads per element (slab
 // residues mod 16, four accumulators each), merged in a fixed order.
+// c9: write bf16 [C][9] (the module's weight layout) instead of fp32 [9][C].
 __global__ void __launch_bounds__(kThreads) dw_wgrad_reduce_kernel(const float* __restrict__ part,
-                                                                   float* __restrict__ dw, int n9c, int slabs) {
+                                                                   void* __restrict__ dw, int n9c, int slabs,
+                                                                   int c9) {
   __shared__ float red[16][17];
   const int el = threadIdx.x % 16, q = threadIdx.x / 16, i = blockIdx.x * 16 + el;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
@@ -238,8 +283,104 @@ __global__ void __launch_bounds__(kThreads) dw_wgrad_reduce_kernel(const float* 
   if (q == 0 && i < n9c) {
     float a = 0.f;
     for (int r = 0; r < 16; ++r) a += red[r][el];
-    dw[i] = a;
+    if (c9) {
+      const int C = n9c / 9, k = i / C, c = i - k * C;
+      __bf16 b = (__bf16)a;
+      static_cast<uint16_t*>(dw)[c * 9 + k] = __builtin_bit_cast(uint16_t, b);
+    } else {
+      static_cast<float*>(dw)[i] = a;
+    }
   }
+}
+
+// Weight gradient, round 6: a workgroup owns ONE channel group (8 channels)
+// and a slab of 256·ppt output pixels, a thread one pixel in 256 of the slab
+// (ppt of them, all nine taps' loads in flight per pixel); the 72 sums fold
+// across the wave by shuffles and across the 4 waves in LDS, in a fixed order.
+// With one slab (P <= kWgDirectP) the block writes the gradient itself -- no
+// partial rows, no reduce launch.  (The kernel above gave a 24² DeepLab layer
+// 2-pixel slabs: 288 partial rows of 9·C floats and 18-42 us per layer, plus a
+// ~5 us reduce: 430 us a 4.2 step, profiles/r6/train.)
+constexpr int kWgDirectP = 2304;  // 48²: 9 pixels a thread
+__global__ void __launch_bounds__(kThreads) dw_wgrad2_kernel(const u32x4* __restrict__ dy,
+                                                             const u32x4* __restrict__ x, float* __restrict__ part,
+                                                             void* __restrict__ out, int out_fmt, const Shape s,
+                                                             int ppt) {
+  __shared__ float red[kThreads / 64][72];
+  const int cv = s.C / 8, cg = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t P = (int64_t)s.N * s.OH * s.OW;
+  const int64_t p0 = (int64_t)blockIdx.y * kThreads * ppt;
+  float acc[9][8];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
+  for (int i = 0; i < ppt; ++i) {
+    const int64_t p = p0 + (int64_t)i * kThreads + t;
+    if (p >= P) break;
+    const int ow = (int)(p % s.OW);
+    const int64_t r = p / s.OW;
+    const int oh = (int)(r % s.OH);
+    const int n = (int)(r / s.OH);
+    const int h0 = oh * s.stride - s.dil, w0 = ow * s.stride - s.dil;
+    const u32x4* xn = x + (int64_t)n * s.H * s.W * cv + cg;
+    const u32x4 gv = dy[p * cv + cg];
+    u32x4 xv[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int ih = h0 + (k / 3) * s.dil, iw = w0 + (k % 3) * s.dil;
+      const bool ok = (unsigned)ih < (unsigned)s.H && (unsigned)iw < (unsigned)s.W;
+      xv[k] = ok ? xn[((int64_t)ih * s.W + iw) * cv] : u32x4{0u, 0u, 0u, 0u};
+    }
+    float g[8];
+    unpack8(gv, g);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      float xf[8];
+      unpack8(xv[k], xf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[k][j] = fmaf(g[j], xf[j], acc[k][j]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = acc[k][j];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == 0) red[wave][k * 8 + j] = v;
+    }
+  __syncthreads();
+  if (t < 72) {
+    const float v = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+    const int k = t >> 3, c = cg * 8 + (t & 7);
+    if (part) {
+      part[(int64_t)blockIdx.y * 9 * s.C + (int64_t)k * s.C + c] = v;
+    } else if (out_fmt) {
+      __bf16 b = (__bf16)v;
+      static_cast<uint16_t*>(out)[c * 9 + k] = __builtin_bit_cast(uint16_t, b);
+    } else {
+      static_cast<float*>(out)[k * s.C + c] = v;
+    }
+  }
+}
+
+// (pixels per thread, slabs) of dw_wgrad2_kernel
+void wgrad2_plan(const Shape& s, int& ppt, int& slabs) {
+  const int64_t P = (int64_t)s.N * s.OH * s.OW;
+  if (P <= kWgDirectP) {
+    ppt = (int)((P + kThreads - 1) / kThreads);
+    slabs = 1;
+    return;
+  }
+  ppt = 4;
+  int64_t sl = (P + kThreads * 4 - 1) / (kThreads * 4);
+  while (sl * (s.C / 8) > 2048 && ppt < 64) {  // bound the partial rows
+    ppt *= 2;
+    sl = (P + (int64_t)kThreads * ppt - 1) / ((int64_t)kThreads * ppt);
+  }
+  slabs = (int)sl;
 }
 
 bool make_shape(Shape& s, int N, int H, int W, int C, int stride, int dil) {
@@ -272,43 +413,82 @@ int wgrad_slabs(const Shape& s) {
 
 }  // namespace
 
-VGPU_API int vgpu_dwconv3_fwd_nhwc(const void* x, const float* w9c, const float* bias, int act, void* y, int N,
-                                   int H, int W, int C, int stride, int dil, hipStream_t st) {
+// w: fp32 [9][C] (wfmt 0) or bf16 [C][9] (wfmt 1, 16-B aligned).
+VGPU_API int vgpu_dwconv3_fwd_nhwc(const void* x, const void* w, int wfmt, const float* bias, int act, void* y,
+                                   int N, int H, int W, int C, int stride, int dil, hipStream_t st) {
   Shape s;
-  if (!make_shape(s, N, H, W, C, stride, dil) || act < 0 || act > 2) return -1;
+  if (!make_shape(s, N, H, W, C, stride, dil) || act < 0 || act > 2 || wfmt < 0 || wfmt > 1 ||
+      (wfmt == 1 && ((uintptr_t)w & 15u)))
+    return -1;
   const int64_t total = (int64_t)N * s.OH * s.OW * (C / 8);
-  hipLaunchKernelGGL(dw_fwd_kernel, dim3(grid_for(total)), dim3(kThreads), 0, st, (const u32x4*)x, w9c, bias, act,
-                     (u32x4*)y, s, total);
+  if (wfmt)
+    hipLaunchKernelGGL(dw_fwd_kernel<true>, dim3(grid_for(total)), dim3(kThreads), 0, st, (const u32x4*)x, w, bias,
+                       act, (u32x4*)y, s, total);
+  else
+    hipLaunchKernelGGL(dw_fwd_kernel<false>, dim3(grid_for(total)), dim3(kThreads), 0, st, (const u32x4*)x, w, bias,
+                       act, (u32x4*)y, s, total);
   return (int)hipGetLastError();
 }
 
-VGPU_API int vgpu_dwconv3_dgrad_nhwc(const void* dy, const float* w9c, void* dx, int N, int H, int W, int C,
+VGPU_API int vgpu_dwconv3_dgrad_nhwc(const void* dy, const void* w, int wfmt, void* dx, int N, int H, int W, int C,
                                      int stride, int dil, hipStream_t st) {
   Shape s;
-  if (!make_shape(s, N, H, W, C, stride, dil)) return -1;
+  if (!make_shape(s, N, H, W, C, stride, dil) || wfmt < 0 || wfmt > 1 || (wfmt == 1 && ((uintptr_t)w & 15u)))
+    return -1;
   const int64_t total = (int64_t)N * H * W * (C / 8);
-  hipLaunchKernelGGL(dw_dgrad_kernel, dim3(grid_for(total)), dim3(kThreads), 0, st, (const u32x4*)dy, w9c,
-                     (u32x4*)dx, s, total);
+  if (wfmt)
+    hipLaunchKernelGGL(dw_dgrad_kernel<true>, dim3(grid_for(total)), dim3(kThreads), 0, st, (const u32x4*)dy, w,
+                       (u32x4*)dx, s, total);
+  else
+    hipLaunchKernelGGL(dw_dgrad_kernel<false>, dim3(grid_for(total)), dim3(kThreads), 0, st, (const u32x4*)dy, w,
+                       (u32x4*)dx, s, total);
   return (int)hipGetLastError();
+}
+
+static int g_wgrad_v1 = -1;  // VGPU_DW_WGRAD=1: the round-5 slab kernel (A/B)
+static bool wgrad_v1() {
+  if (g_wgrad_v1 < 0) {
+    const char* v = getenv("VGPU_DW_WGRAD");
+    g_wgrad_v1 = (v && v[0] == '1') ? 1 : 0;
+  }
+  return g_wgrad_v1 == 1;
 }
 
 VGPU_API int64_t vgpu_dwconv3_wgrad_workspace(int N, int H, int W, int C, int stride, int dil) {
   Shape s;
   if (!make_shape(s, N, H, W, C, stride, dil) || C / 8 > kThreads) return -1;
+  if (!wgrad_v1()) {
+    int ppt, slabs;
+    wgrad2_plan(s, ppt, slabs);
+    return slabs == 1 ? 0 : (int64_t)slabs * 9 * C * 4;
+  }
   return (int64_t)wgrad_slabs(s) * 9 * C * 4;
 }
 
-// dw9c: fp32 [9][C].  ws: vgpu_dwconv3_wgrad_workspace bytes.
-VGPU_API int vgpu_dwconv3_wgrad_nhwc(const void* dy, const void* x, float* dw9c, void* ws, int64_t ws_bytes, int N,
-                                     int H, int W, int C, int stride, int dil, hipStream_t st) {
+// dw: fp32 [9][C] (dfmt 0) or bf16 [C][9] (dfmt 1).  ws: vgpu_dwconv3_wgrad_workspace bytes.
+VGPU_API int vgpu_dwconv3_wgrad_nhwc(const void* dy, const void* x, void* dw, int dfmt, void* ws, int64_t ws_bytes,
+                                     int N, int H, int W, int C, int stride, int dil, hipStream_t st) {
   Shape s;
-  if (!make_shape(s, N, H, W, C, stride, dil) || C / 8 > kThreads) return -1;
+  if (!make_shape(s, N, H, W, C, stride, dil) || C / 8 > kThreads || dfmt < 0 || dfmt > 1) return -1;
+  if (!wgrad_v1()) {
+    int ppt, sl;
+    wgrad2_plan(s, ppt, sl);
+    if (sl > 1 && ws_bytes < (int64_t)sl * 9 * C * 4) return -2;
+    hipLaunchKernelGGL(dw_wgrad2_kernel, dim3(C / 8, sl), dim3(kThreads), 0, st, (const u32x4*)dy,
+                       (const u32x4*)x, sl > 1 ? (float*)ws : nullptr, dw, dfmt, s, ppt);
+    if (sl > 1) {
+      const int n9c = 9 * C;
+      hipLaunchKernelGGL(dw_wgrad_reduce_kernel, dim3((n9c + 15) / 16), dim3(kThreads), 0, st, (const float*)ws, dw,
+                         n9c, sl, dfmt);
+    }
+    return (int)hipGetLastError();
+  }
   const int slabs = wgrad_slabs(s);
   if (ws_bytes < (int64_t)slabs * 9 * C * 4) return -2;
   hipLaunchKernelGGL(dw_wgrad_kernel, dim3(slabs), dim3(kThreads), 0, st, (const u32x4*)dy, (const u32x4*)x,
                      (float*)ws, s, wgrad_pb(s));
   const int n9c = 9 * C;
-  hipLaunchKernelGGL(dw_wgrad_reduce_kernel, dim3((n9c + 15) / 16), dim3(kThreads), 0, st, (const float*)ws, dw9c,
-                     n9c, slabs);
+  hipLaunchKernelGGL(dw_wgrad_reduce_kernel, dim3((n9c + 15) / 16), dim3(kThreads), 0, st, (const float*)ws, dw,
+                     n9c, slabs, dfmt);
   return (int)hipGetLastError();
 }

@@ -31,7 +31,8 @@ def family(name: str) -> str:
                      ("add_scale_shift", "vgpu add+BN+ReLU"), ("bias_act", "vgpu bias+act"),
                      ("scale_shift_act", "vgpu BN+act"), ("igemm", "MIOpen igemm conv"),
                      ("kernel_grouped_conv", "MIOpen CK grouped conv"), ("Cijk", "hipBLASLt/Tensile GEMM"),
-                     ("max_pool", "torch maxpool"), ("reduce_kernel", "torch reduce")):
+                     ("max_pool", "torch maxpool"), ("wgrad_reduce", "vgpu wgrad reduce"),
+                     ("splitk_reduce", "vgpu split-K reduce"), ("at::native::reduce_kernel", "torch reduce")):
         if key in name:
             return fam
     return name[:60]

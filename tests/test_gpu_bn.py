@@ -38,6 +38,15 @@ CASES = [
     (2, 96, 7, 7, "relu6", torch.bfloat16, 0.0),      # threads-per-row not a power of two
     (20, 64, 87, 87, "relu", torch.float32, 0.0),     # ResNet-V2-50 b=20 stage-1 size
     (8, 128, 33, 33, "relu", torch.float32, 50.0),    # large mean: shifted-sum variance
+    # round 6 plain-path plans (bn_nhwc.hip plain_kind): one-launch small layers
+    # (rows <= 4096, C % 64 == 0) and reduce + fused finalize/apply above that
+    (1, 320, 24, 24, "relu6", torch.bfloat16, 0.0),   # DeepLab 4.2's 24² maps: one launch
+    # (1, 192, 25, 25) would be the natural one-launch case, but PyTorch's own fp32
+    # channels_last batch_norm (the reference) segfaults on it on MI355X
+    # (scripts/bn_case_check.py ref 1 192 25 25 30, rc 139)
+    (2, 192, 16, 19, "relu6", torch.float32, 30.0),   # one launch, 608 rows (<= 640), shifted sums
+    (2, 192, 40, 40, "relu6", torch.float32, 30.0),   # reduce + fused apply, shifted sums
+    (1, 64, 192, 192, "relu6", torch.bfloat16, 0.0),  # DeepLab's stem BN: reduce + fused apply
 ]
 
 
@@ -77,6 +86,31 @@ def test_bn_act_train_matches_fp32_reference(B, n, c, h, w, act, pdt, off):
         assert got.dtype == pdt
         tol = (2e-2 if pdt == torch.bfloat16 else 2e-3) * ref.abs().max().item() + 1e-3
         torch.testing.assert_close(got.float(), ref, atol=tol, rtol=2e-2)
+
+
+@pytest.mark.parametrize("shape", [(1, 128, 24, 24), (1, 64, 96, 96), (1, 192, 48, 48)])
+def test_bn_plain_plans_agree_with_three_pass(B, shape):
+    """The one-launch (small) and two-launch (fused finalize) plain plans give
+    the three-pass path's values (VGPU_BN_FUSE_SMALL=0) up to summation order."""
+    from vgpu.native import load_kernels
+    lib = load_kernels()
+    n, c, h, w = shape
+    res = []
+    for on in (1, 0):
+        lib.vgpu_bn_set_fuse_small(on)
+        try:
+            x = _x(shape, 5, 3.0).requires_grad_()
+            g = torch.Generator(device="cpu").manual_seed(6)
+            wt = (torch.rand(c, generator=g) + 0.5).cuda().requires_grad_()
+            bs = (torch.rand(c, generator=g) - 0.5).cuda().requires_grad_()
+            rm, rv = torch.zeros(c, device="cuda"), torch.ones(c, device="cuda")
+            y = B._BNActFn.apply(x, wt, bs, rm, rv, 0.1, 1e-5, B.ACT["relu6"])
+            y.backward(_x(shape, 7))
+            res.append([y.float(), x.grad.float(), wt.grad, bs.grad, rm, rv])
+        finally:
+            lib.vgpu_bn_set_fuse_small(-1)
+    for a, b in zip(*res):
+        torch.testing.assert_close(a, b, atol=2e-2, rtol=1e-2)
 
 
 def test_bn_act_module_entry_updates_counters(B):

@@ -115,6 +115,8 @@ DW_CASES = [  # n, c, h, w, stride, dilation
     (1, 144, 16, 16, 1, 2),
     (2, 960, 9, 11, 1, 2),
     (1, 64, 7, 5, 2, 1),
+    (1, 64, 100, 100, 1, 1),   # > 2304 output pixels: slab partials + the reduce launch
+    (1, 192, 96, 96, 2, 1),    # 48² output: the largest one-launch weight gradient
 ]
 
 
@@ -141,6 +143,14 @@ def test_dwconv3_matches_fp32(gpu_build, n, c, h, w, stride, dil):
     # deterministic weight gradient
     w1 = D.dwconv3_wgrad(dy, x.detach(), stride, dil)
     assert torch.equal(w1, D.dwconv3_wgrad(dy, x.detach(), stride, dil))
+    # the module-layout variant (bf16 [C, 1, 3, 3], what training uses): the same sums
+    wm = D.dwconv3_wgrad(dy, x.detach(), stride, dil, "module")
+    assert torch.equal(wm, w1.t().reshape(c, 1, 3, 3).to(torch.bfloat16))
+    # forward / data gradient from the fp32 [9, C] filter agree with the bf16 module filter
+    w9c = conv.weight.detach().float().reshape(c, 9).t().contiguous()
+    assert torch.equal(D.dwconv3(x.detach(), w9c, stride, dil), D.dwconv3(x.detach(), conv.weight.detach(), stride, dil))
+    assert torch.equal(D.dwconv3_dgrad(dy, w9c, (h, w), stride, dil),
+                       D.dwconv3_dgrad(dy, conv.weight.detach(), (h, w), stride, dil))
 
 
 def test_deeplab_native_training_step_matches_torch(gpu_build):

@@ -378,10 +378,13 @@ def test_temporal_limiter_throttles_when_forced(native_build, tmp_path):
 def test_rccl_kernels_exempt_from_temporal_limiter(native_build, tmp_path):
     """Collective kernels must not be throttled (every rank's kernel has to be
     resident for a collective to progress): a kernel stub from an rccl library
-    launches at the unthrottled rate while ordinary kernels are cut."""
+    launches at the unthrottled rate while ordinary kernels are cut.  At a 10 %
+    cap (25 % left the ratio at 2.7-3.6x: the charged-but-not-held collective
+    path's host rate varies with the machine's load) ordinary launches drop to
+    ~0.5M/s, collective ones stay at several M/s."""
     util = tmp_path / "util"
     util.write_text("0 100\n")
-    base = {"VGPU_DEVICE_CU_LIMIT_0": "25", "VGPU_FAKE_UTIL_FILE": str(util),
+    base = {"VGPU_DEVICE_CU_LIMIT_0": "10", "VGPU_FAKE_UTIL_FILE": str(util),
             "GPU_CORE_UTILIZATION_POLICY": "force", "VGPU_LIMITER_TICK_MS": "5"}
     thr = run("throttle", 1.0, 64, env=base)
     rccl = run("throttle_rccl", 1.0, 64, env=base)

@@ -305,6 +305,14 @@ class DeepLabV3(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         h, w = x.shape[-2:]
+        if self.training and torch.is_grad_enabled() and x.is_cuda:
+            from vgpu.ops.conv import DgradFilters, native_train_enabled
+            if native_train_enabled():
+                # every 1x1 conv's transposed data-gradient filter in one launch per
+                # step (a transpose copy per conv otherwise: 40 a step at 4.2)
+                if getattr(self, "_dgrad", None) is None:
+                    self._dgrad = DgradFilters([m for m in self.modules() if isinstance(m, nn.Conv2d)])
+                self._dgrad.refresh()
         with batched_step_counters():
             y = self.head(self.aspp(self.backbone(x)))
         return resize_bilinear(y, (h, w))

@@ -376,8 +376,12 @@ def _wgrad_native(dy: torch.Tensor, ks: int, stride: int, c: int = 0) -> bool:
     # 3 / 4 26.6 / 41.8 vs 62 / 53, ResNet-V2-50 stage 4 (2.4k pixels) 59 vs 82
     # (profiles/r5/train/vgg_small_ab*.log: MIOpen's kernel plus its zero-fill
     # and cast passes).
+    # Round 6: 1x1 at any size.  DeepLab-v3 4.2 (b=1) has 40 1x1 layers on
+    # 576-pixel maps; MIOpen's weight gradient there is its kernel plus a
+    # zero-fill and a cast pass (3 dispatches of ~5 us inside a replayed step,
+    # 180 of the step's 790, profiles/r6/train), the native one 1-2.
     if ks == 1:
-        return pixels >= 1024
+        return pixels >= 1
     return ks == 3
 
 

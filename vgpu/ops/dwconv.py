@@ -21,13 +21,13 @@ def _lib():
     lib = load_kernels()
     if not _BOUND:
         vp, ci = ctypes.c_void_p, ctypes.c_int
-        lib.vgpu_dwconv3_fwd_nhwc.argtypes = [vp, vp, vp, ci, vp] + [ci] * 6 + [vp]
+        lib.vgpu_dwconv3_fwd_nhwc.argtypes = [vp, vp, ci, vp, ci, vp] + [ci] * 6 + [vp]
         lib.vgpu_dwconv3_fwd_nhwc.restype = ci
-        lib.vgpu_dwconv3_dgrad_nhwc.argtypes = [vp, vp, vp] + [ci] * 6 + [vp]
+        lib.vgpu_dwconv3_dgrad_nhwc.argtypes = [vp, vp, ci, vp] + [ci] * 6 + [vp]
         lib.vgpu_dwconv3_dgrad_nhwc.restype = ci
         lib.vgpu_dwconv3_wgrad_workspace.argtypes = [ci] * 6
         lib.vgpu_dwconv3_wgrad_workspace.restype = ctypes.c_int64
-        lib.vgpu_dwconv3_wgrad_nhwc.argtypes = [vp, vp, vp, vp, ctypes.c_int64] + [ci] * 6 + [vp]
+        lib.vgpu_dwconv3_wgrad_nhwc.argtypes = [vp, vp, vp, ci, vp, ctypes.c_int64] + [ci] * 6 + [vp]
         lib.vgpu_dwconv3_wgrad_nhwc.restype = ci
         _BOUND = True
     return lib
@@ -48,70 +48,82 @@ def out_hw(h: int, w: int, stride: int) -> tuple[int, int]:
 _ACTS = {"none": 0, "relu": 1, "relu6": 2}
 
 
-def dwconv3(x: torch.Tensor, w9c: torch.Tensor, stride: int, dil: int, bias: torch.Tensor | None = None,
+def _wfmt(w: torch.Tensor) -> int:
+    """0: fp32 [9, C] (tap-major); 1: the module's bf16 [C, 1, 3, 3] as stored."""
+    if w.dtype == torch.float32 and w.dim() == 2 and w.shape[0] == 9 and w.is_contiguous():
+        return 0
+    if w.dtype == torch.bfloat16 and w.dim() == 4 and tuple(w.shape[1:]) == (1, 3, 3) and w.is_contiguous():
+        return 1
+    raise ValueError(f"depthwise filter must be fp32 [9, C] or contiguous bf16 [C, 1, 3, 3], got "
+                     f"{w.dtype} {tuple(w.shape)}")
+
+
+def dwconv3(x: torch.Tensor, w: torch.Tensor, stride: int, dil: int, bias: torch.Tensor | None = None,
             act: str = "none") -> torch.Tensor:
-    """x [N,C,H,W] bf16 channels_last, w9c fp32 [9, C] (tap-major), optional
-    fp32 bias [C] and activation -> y."""
-    n, c, h, w = x.shape
-    oh, ow = out_hw(h, w, stride)
+    """x [N,C,H,W] bf16 channels_last, w fp32 [9, C] (tap-major) or bf16
+    [C, 1, 3, 3], optional fp32 bias [C] and activation -> y."""
+    n, c, h, wd = x.shape
+    oh, ow = out_hw(h, wd, stride)
     y = torch.empty((n, c, oh, ow), dtype=x.dtype, device=x.device, memory_format=_CL)
-    rc = _lib().vgpu_dwconv3_fwd_nhwc(_p(x), _p(w9c), None if bias is None else _p(bias), _ACTS[act], _p(y), n, h, w,
-                                      c, stride, dil, _stream())
+    rc = _lib().vgpu_dwconv3_fwd_nhwc(_p(x), _p(w), _wfmt(w), None if bias is None else _p(bias), _ACTS[act], _p(y),
+                                      n, h, wd, c, stride, dil, _stream())
     if rc != 0:
         raise RuntimeError(f"vgpu_dwconv3_fwd_nhwc: error {rc}")
     return y
 
 
-def dwconv3_dgrad(dy: torch.Tensor, w9c: torch.Tensor, hw: tuple[int, int], stride: int, dil: int) -> torch.Tensor:
+def dwconv3_dgrad(dy: torch.Tensor, w: torch.Tensor, hw: tuple[int, int], stride: int, dil: int) -> torch.Tensor:
     n, c = dy.shape[:2]
     dx = torch.empty((n, c, *hw), dtype=dy.dtype, device=dy.device, memory_format=_CL)
-    rc = _lib().vgpu_dwconv3_dgrad_nhwc(_p(dy), _p(w9c), _p(dx), n, hw[0], hw[1], c, stride, dil, _stream())
+    rc = _lib().vgpu_dwconv3_dgrad_nhwc(_p(dy), _p(w), _wfmt(w), _p(dx), n, hw[0], hw[1], c, stride, dil, _stream())
     if rc != 0:
         raise RuntimeError(f"vgpu_dwconv3_dgrad_nhwc: error {rc}")
     return dx
 
 
-def dwconv3_wgrad(dy: torch.Tensor, x: torch.Tensor, stride: int, dil: int) -> torch.Tensor:
-    """fp32 [9, C] weight gradient (deterministic slab reduction)."""
+def dwconv3_wgrad(dy: torch.Tensor, x: torch.Tensor, stride: int, dil: int, layout: str = "9c") -> torch.Tensor:
+    """Weight gradient (deterministic slab reduction): fp32 [9, C] ("9c"), or
+    bf16 [C, 1, 3, 3] ("module", the weight's own layout and dtype)."""
     n, c, h, w = x.shape
     lib = _lib()
     need = lib.vgpu_dwconv3_wgrad_workspace(n, h, w, c, stride, dil)
     if need < 0:
         raise ValueError("unsupported depthwise shape")
     ws = torch.empty(max(need // 4, 1), dtype=torch.float32, device=x.device)
-    dw = torch.empty((9, c), dtype=torch.float32, device=x.device)
-    rc = lib.vgpu_dwconv3_wgrad_nhwc(_p(dy), _p(x), _p(dw), _p(ws), need, n, h, w, c, stride, dil, _stream())
+    c9 = layout == "module"
+    dw = (torch.empty((c, 1, 3, 3), dtype=torch.bfloat16, device=x.device) if c9 else
+          torch.empty((9, c), dtype=torch.float32, device=x.device))
+    rc = lib.vgpu_dwconv3_wgrad_nhwc(_p(dy), _p(x), _p(dw), int(c9), _p(ws), need, n, h, w, c, stride, dil,
+                                     _stream())
     if rc != 0:
         raise RuntimeError(f"vgpu_dwconv3_wgrad_nhwc: error {rc}")
     return dw
 
 
 class _DWConvFn(torch.autograd.Function):
+    """Forward, data and weight gradient straight from / into the module's bf16
+    [C, 1, 3, 3] filter (no per-step transposes or casts)."""
+
     @staticmethod
     def forward(ctx, x, w, stride: int, dil: int):
-        c = x.shape[1]
-        w9c = w.detach().float().reshape(c, 9).t().contiguous()
-        ctx.save_for_backward(x, w9c)
-        ctx.cfg = (stride, dil, w.dtype, tuple(x.shape[2:]))
-        return dwconv3(x, w9c, stride, dil)
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (stride, dil, tuple(x.shape[2:]))
+        return dwconv3(x, w, stride, dil)
 
     @staticmethod
     def backward(ctx, dy):
-        x, w9c = ctx.saved_tensors
-        stride, dil, wdt, hw = ctx.cfg
+        x, w = ctx.saved_tensors
+        stride, dil, hw = ctx.cfg
         dy = dy.contiguous(memory_format=_CL)
-        dx = dwconv3_dgrad(dy, w9c, hw, stride, dil) if ctx.needs_input_grad[0] else None
-        dw = None
-        if ctx.needs_input_grad[1]:
-            c = x.shape[1]
-            dw = dwconv3_wgrad(dy, x, stride, dil).t().reshape(c, 1, 3, 3).to(wdt).contiguous(memory_format=_CL)
+        dx = dwconv3_dgrad(dy, w, hw, stride, dil) if ctx.needs_input_grad[0] else None
+        dw = dwconv3_wgrad(dy, x, stride, dil, "module") if ctx.needs_input_grad[1] else None
         return dx, dw, None, None
 
 
 def eligible(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     c = conv.in_channels
     return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.is_contiguous(memory_format=_CL)
-            and conv.weight.dtype == torch.bfloat16 and conv.bias is None
+            and conv.weight.dtype == torch.bfloat16 and conv.weight.is_contiguous() and conv.bias is None
             and conv.groups == c == conv.out_channels and c % 8 == 0
             and conv.kernel_size == (3, 3) and conv.stride[0] == conv.stride[1]
             and conv.dilation[0] == conv.dilation[1] and conv.padding == conv.dilation
