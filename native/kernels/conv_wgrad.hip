@@ -492,6 +492,16 @@ bool wgrad3_eligible(int KS, int stride, int pad, int64_t P) {
   return g_wgrad3 == 1 && KS == 3 && pad == 1 && (stride == 1 || stride == 2) && P >= 65536;
 }
 
+double g_launch_us = -1.0;
+double launch_us() {
+  if (g_launch_us < 0.0) {
+    const char* v = getenv("VGPU_WGRAD_LAUNCH_US");
+    g_launch_us = v ? atof(v) : 4.0;
+    if (g_launch_us < 0.0) g_launch_us = 0.0;
+  }
+  return g_launch_us;
+}
+
 // Split-K factor for a shape; -1 = unsupported.
 int64_t wgrad_splits(int N, int H, int W, int C, int Cout, int KS, int stride, int pad) {
   const int OH = (H + 2 * pad - KS) / stride + 1, OW = (W + 2 * pad - KS) / stride + 1;
@@ -517,10 +527,10 @@ int64_t wgrad_splits(int N, int H, int W, int C, int Cout, int KS, int stride, i
   double best = 1e30;
   for (int64_t sp = 1; sp <= 1024 && sp <= (steps_total + 3) / 4; sp *= 2) {
     const double waves = (double)((tiles * sp + (int64_t)slots - 1) / (int64_t)slots);
-    // (+ 4 us for the reduce's own launch when split: a dispatch inside a
-    // replayed graph costs ~4.7 us however small, profiles/r6/train)
+    // (+ the reduce's own launch when split: a dispatch inside a replayed
+    // graph costs ~4.7 us however small, profiles/r6/train; VGPU_WGRAD_LAUNCH_US)
     const double est = waves * (t_step * (double)((steps_total + sp - 1) / sp) + 3.0) +
-                       (sp > 1 ? 2.0 * sp * tile_bytes / 4.0e6 + 4.0 : tile_bytes / 8.0e6);
+                       (sp > 1 ? 2.0 * sp * tile_bytes / 4.0e6 + launch_us() : tile_bytes / 8.0e6);
     if (est < best) { best = est; splits = sp; }
   }
   return splits;

@@ -306,8 +306,9 @@ __global__ void __launch_bounds__(kThreads) dw_wgrad2_kernel(const u32x4* __rest
                                                              const u32x4* __restrict__ x, float* __restrict__ part,
                                                              void* __restrict__ out, int out_fmt, const Shape s,
                                                              int ppt) {
-  __shared__ float red[kThreads / 64][72];
-  const int cv = s.C / 8, cg = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  __shared__ float tr[72][kThreads + 1];  // +1: a thread's 72 stores hit 72 banks apart
+  __shared__ float red[4][72];
+  const int cv = s.C / 8, cg = blockIdx.x, t = threadIdx.x;
   const int64_t P = (int64_t)s.N * s.OH * s.OW;
   const int64_t p0 = (int64_t)blockIdx.y * kThreads * ppt;
   float acc[9][8];
@@ -342,15 +343,28 @@ __global__ void __launch_bounds__(kThreads) dw_wgrad2_kernel(const u32x4* __rest
       for (int j = 0; j < 8; ++j) acc[k][j] = fmaf(g[j], xf[j], acc[k][j]);
     }
   }
+  // 72 sums x 256 threads through LDS: every thread stores its row, then 288
+  // threads-tasks each add a 64-thread column run, then 72 threads merge the 4
+  // runs in order.  (Wave shuffles took 432 cross-lane ops a thread: ~22 us
+  // per call whatever the layer size.)
 #pragma unroll
   for (int k = 0; k < 9; ++k)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = acc[k][j];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-      if (lane == 0) red[wave][k * 8 + j] = v;
+    for (int j = 0; j < 8; ++j) tr[k * 8 + j][t] = acc[k][j];
+  __syncthreads();
+  for (int task = t; task < 72 * 4; task += kThreads) {
+    const int q = task / 72, o = task - q * 72;  // a wave's lanes: consecutive rows, distinct banks
+    const float* row = &tr[o][q * 64];
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll 4
+    for (int i = 0; i < 64; i += 4) {
+      a0 += row[i];
+      a1 += row[i + 1];
+      a2 += row[i + 2];
+      a3 += row[i + 3];
     }
+    red[q][o] = (a0 + a1) + (a2 + a3);
+  }
   __syncthreads();
   if (t < 72) {
     const float v = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);

@@ -19,4 +19,7 @@ run pktcap0 DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 || exit 1
 run pktcap1 DEBUG_CLR_GRAPH_PACKET_CAPTURE=1 || exit 1
 run batch8 DEBUG_HIP_GRAPH_BATCH_SIZE=8 || exit 1
 run batch64 DEBUG_HIP_GRAPH_BATCH_SIZE=64 || exit 1
+run wgrad_launch12 VGPU_WGRAD_LAUNCH_US=12 || exit 1
+run wgrad_launch30 VGPU_WGRAD_LAUNCH_US=30 || exit 1
+run dw_wgrad_v1 VGPU_DW_WGRAD=1 || exit 1
 run base2 VGPU_AB=0 || exit 1

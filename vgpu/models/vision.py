@@ -181,20 +181,28 @@ class ConvBNAct(nn.Sequential):
         y = F.conv2d(x, w, b.to(x.dtype), conv.stride, conv.padding, conv.dilation, conv.groups)
         return F.hardtanh_(y, 0.0, 6.0) if act == "relu6" else y
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, res_out: bool = False):
+        """act(bn(conv(x))); res_out (1x1 / dense convs): also return x as an
+        identity shortcut whose gradient the conv's data-gradient kernel sums in
+        (vgpu.ops.conv.conv_train)."""
         conv = self[0]
         if not self.training and getattr(self, "_fused", None) is not None:
-            return self._forward_fused(x)
+            y = self._forward_fused(x)
+            return (y, x) if res_out else y
+        xs = x
         if x.is_cuda:
             from vgpu.ops import dwconv
             if dwconv.eligible(x, conv):
                 y = dwconv.dwconv_train(x, conv)
             else:
                 from vgpu.ops.conv import conv_train
-                y = conv_train(x, conv)
+                y = conv_train(x, conv, res_out=res_out)
+                if res_out:
+                    y, xs = y
         else:
             y = conv(x)
-        return bn_act(y, self[1], "relu6" if len(self) > 2 else "none")
+        y = bn_act(y, self[1], "relu6" if len(self) > 2 else "none")
+        return (y, xs) if res_out else y
 
 
 def _padc(c: int, pad: int) -> int:
@@ -240,8 +248,13 @@ class InvertedResidual(nn.Module):
         self.body = nn.Sequential(*layers)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        y = self.body(x)
-        return x + y if self.use_res else y
+        if not self.use_res:
+            return self.body(x)
+        # the shortcut's gradient joins the first conv's data gradient in its epilogue
+        y, xs = self.body[0](x, res_out=True)
+        for m in self.body[1:]:
+            y = m(y)
+        return xs + y
 
 
 class MobileNetV2Backbone(nn.Module):

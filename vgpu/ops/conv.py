@@ -468,28 +468,39 @@ class _ConvTrainFn(torch.autograd.Function):
     Per-layer timings that motivated the split: profiles/convtrain_r1.md."""
 
     @staticmethod
-    def forward(ctx, x, w, residual, stride: int, padding: int):
+    def forward(ctx, x, w, residual, stride: int, padding: int, res_out: bool = False):
         y = conv2d(x, w, stride=stride, padding=padding, residual=residual)
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.padding = stride, padding
         ctx.has_res = residual is not None
+        ctx.set_materialize_grads(False)
+        if res_out:
+            # x again as an output: the gradient it receives (an identity
+            # shortcut's) is added by the data-gradient kernel's epilogue instead
+            # of an autograd accumulation pass over x
+            return y, x.view_as(x)
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dxres=None):
         x, w = ctx.saved_tensors
+        if dy is None:  # only the shortcut output was used
+            return dxres, None, None, None, None, None
         dy = dy.contiguous(memory_format=_CL)
-        dx, dw = conv_backward(dy, x, w, ctx.stride, ctx.padding, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        dx, dw = conv_backward(dy, x, w, ctx.stride, ctx.padding, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                               dx_add=dxres)
         dres = dy if ctx.has_res and ctx.needs_input_grad[2] else None
-        return dx, dw, dres, None, None
+        return dx, dw, dres, None, None, None
 
 
 def conv_backward(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, p: int, need_dx: bool,
-                  need_dw: bool, *, skip_dx: bool = False,
-                  db_job: tuple | None = None) -> tuple[torch.Tensor | None, torch.Tensor | None]:
+                  need_dw: bool, *, skip_dx: bool = False, db_job: tuple | None = None,
+                  dx_add: torch.Tensor | None = None) -> tuple[torch.Tensor | None, torch.Tensor | None]:
     """(dx, dw) of y = conv(x, w, stride s, padding p): dx on the MFMA kernel for
     stride 1 (MIOpen otherwise), dw per _wgrad_native.  skip_dx: the caller
-    computed a stride-1 dx itself (vgpu.ops.bnconv's fused data gradient)."""
+    computed a stride-1 dx itself (vgpu.ops.bnconv's fused data gradient).
+    dx_add: a second gradient of x, summed into dx (in the kernel's epilogue
+    for stride 1)."""
     common = ([0], [s, s], [p, p], [1, 1], False, [0, 0], 1)
     bw = torch.ops.aten.convolution_backward
     dx = dw = None
@@ -497,9 +508,13 @@ def conv_backward(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, p:
     if s == 1:
         if need_dx and not skip_dx:
             ks = w.shape[2]
-            dx = conv2d(dy, _dgrad_filter(w), stride=1, padding=ks - 1 - p)
+            add = dx_add.contiguous(memory_format=_CL) if dx_add is not None else None
+            dx = conv2d(dy, _dgrad_filter(w), stride=1, padding=ks - 1 - p, residual=add)
+            dx_add = None
     elif need_dx:
         dx, dw, _ = bw(dy, x, w, *common, [True, need_dw and not native_dw, False])
+    if dx_add is not None and dx is not None:
+        dx = dx + dx_add
     if native_dw:
         dw = conv2d_wgrad(dy, x, w.shape[2], stride=s, padding=p, db_job=db_job)
         db_job = None
@@ -529,13 +544,17 @@ def train_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
             and conv.kernel_size[0] in (1, 3))
 
 
-def conv_train(x: torch.Tensor, conv: torch.nn.Conv2d, residual: torch.Tensor | None = None) -> torch.Tensor:
+def conv_train(x: torch.Tensor, conv: torch.nn.Conv2d, residual: torch.Tensor | None = None,
+               res_out: bool = False):
     """conv(x) (+ residual) with the module's semantics; bf16 channels_last CUDA
-    tensors of supported shapes run natively, anything else through the module."""
+    tensors of supported shapes run natively, anything else through the module.
+    res_out: return (y, x') where x' is x for use as an identity shortcut, whose
+    gradient the data-gradient kernel then sums into dx."""
     if not train_eligible(x, conv) or (residual is not None and not residual.is_contiguous(memory_format=_CL)):
         y = conv(x)
-        return y if residual is None else y + residual
-    return _ConvTrainFn.apply(x, conv.weight, residual, conv.stride[0], conv.padding[0])
+        y = y if residual is None else y + residual
+        return (y, x) if res_out else y
+    return _ConvTrainFn.apply(x, conv.weight, residual, conv.stride[0], conv.padding[0], res_out)
 
 
 class _ConvBiasReLUTrainFn(torch.autograd.Function):
