@@ -297,11 +297,11 @@ __global__ void __launch_bounds__(kThreads) dw_wgrad_reduce_kernel(const float* 
 // and a slab of 256·ppt output pixels, a thread one pixel in 256 of the slab
 // (ppt of them, all nine taps' loads in flight per pixel); the 72 sums fold
 // across the wave by shuffles and across the 4 waves in LDS, in a fixed order.
-// With one slab (P <= kWgDirectP) the block writes the gradient itself -- no
-// partial rows, no reduce launch.  (The kernel above gave a 24² DeepLab layer
+// With one slab the block writes the gradient itself -- no partial rows, no
+// reduce launch.  (A mapping with 8 channel groups x 32 pixel lanes per
+// workgroup coalesced the loads but cut the threads 8x: 25 us at 24², worse.)  (The kernel above gave a 24² DeepLab layer
 // 2-pixel slabs: 288 partial rows of 9·C floats and 18-42 us per layer, plus a
 // ~5 us reduce: 430 us a 4.2 step, profiles/r6/train.)
-constexpr int kWgDirectP = 2304;  // 48²: 9 pixels a thread
 __global__ void __launch_bounds__(kThreads) dw_wgrad2_kernel(const u32x4* __restrict__ dy,
                                                              const u32x4* __restrict__ x, float* __restrict__ part,
                                                              void* __restrict__ out, int out_fmt, const Shape s,
@@ -316,23 +316,26 @@ __global__ void __launch_bounds__(kThreads) dw_wgrad2_kernel(const u32x4* __rest
   for (int k = 0; k < 9; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
-  for (int i = 0; i < ppt; ++i) {
-    const int64_t p = p0 + (int64_t)i * kThreads + t;
-    if (p >= P) break;
-    const int ow = (int)(p % s.OW);
-    const int64_t r = p / s.OW;
-    const int oh = (int)(r % s.OH);
-    const int n = (int)(r / s.OH);
+  // pixel i + 1's ten loads are issued before pixel i's FMAs (32-bit index
+  // math: the host keeps P < 2^31)
+  const int Pi = (int)P;
+  auto load = [&](int i, u32x4& gv, u32x4 (&xv)[9]) {
+    const int p = (int)p0 + i * kThreads + t;
+    const bool in = p < Pi;
+    const int pp = in ? p : 0;
+    const int ow = pp % s.OW, r = pp / s.OW;
+    const int oh = r % s.OH, n = r / s.OH;
     const int h0 = oh * s.stride - s.dil, w0 = ow * s.stride - s.dil;
     const u32x4* xn = x + (int64_t)n * s.H * s.W * cv + cg;
-    const u32x4 gv = dy[p * cv + cg];
-    u32x4 xv[9];
+    gv = in ? dy[(int64_t)pp * cv + cg] : u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
       const int ih = h0 + (k / 3) * s.dil, iw = w0 + (k % 3) * s.dil;
-      const bool ok = (unsigned)ih < (unsigned)s.H && (unsigned)iw < (unsigned)s.W;
+      const bool ok = in && (unsigned)ih < (unsigned)s.H && (unsigned)iw < (unsigned)s.W;
       xv[k] = ok ? xn[((int64_t)ih * s.W + iw) * cv] : u32x4{0u, 0u, 0u, 0u};
     }
+  };
+  auto fma9 = [&](const u32x4& gv, const u32x4 (&xv)[9]) {
     float g[8];
     unpack8(gv, g);
 #pragma unroll
@@ -342,6 +345,17 @@ __global__ void __launch_bounds__(kThreads) dw_wgrad2_kernel(const u32x4* __rest
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[k][j] = fmaf(g[j], xf[j], acc[k][j]);
     }
+  };
+  int n_pix = (int)((P - p0 + kThreads - 1) / kThreads);  // iterations with any live lane
+  if (n_pix > ppt) n_pix = ppt;
+  u32x4 ga, gb, xa[9], xb[9];
+  if (n_pix > 0) load(0, ga, xa);
+  for (int i = 0; i < n_pix; i += 2) {
+    if (i + 1 < n_pix) load(i + 1, gb, xb);
+    fma9(ga, xa);  // out-of-range pixels loaded zeros: they add nothing
+    if (i + 1 >= n_pix) break;
+    if (i + 2 < n_pix) load(i + 2, ga, xa);
+    fma9(gb, xb);
   }
   // 72 sums x 256 threads through LDS: every thread stores its row, then 288
   // threads-tasks each add a 64-thread column run, then 72 threads merge the 4
@@ -380,10 +394,14 @@ __global__ void __launch_bounds__(kThreads) dw_wgrad2_kernel(const u32x4* __rest
   }
 }
 
-// (pixels per thread, slabs) of dw_wgrad2_kernel
+// (pixels per thread, slabs) of dw_wgrad2_kernel.  Its lanes read a pixel's
+// 16 bytes each (uncoalesced, 10 loads in flight per pixel), so the layer's
+// loads in flight scale with its thread count: up to 3 pixels a thread in one
+// slab (DeepLab's 24² layers, ~10 us), else slabs of 4 pixels a thread plus
+// the reduce launch (a 48² layer in one slab of 24 workgroups took 20-29 us).
 void wgrad2_plan(const Shape& s, int& ppt, int& slabs) {
   const int64_t P = (int64_t)s.N * s.OH * s.OW;
-  if (P <= kWgDirectP) {
+  if (P <= 3 * kThreads) {
     ppt = (int)((P + kThreads - 1) / kThreads);
     slabs = 1;
     return;
@@ -488,6 +506,7 @@ VGPU_API int vgpu_dwconv3_wgrad_nhwc(const void* dy, const void* x, void* dw, in
     int ppt, sl;
     wgrad2_plan(s, ppt, sl);
     if (sl > 1 && ws_bytes < (int64_t)sl * 9 * C * 4) return -2;
+    if ((int64_t)N * s.OH * s.OW + (int64_t)kThreads * ppt >= ((int64_t)1 << 31)) return -1;
     hipLaunchKernelGGL(dw_wgrad2_kernel, dim3(C / 8, sl), dim3(kThreads), 0, st, (const u32x4*)dy,
                        (const u32x4*)x, sl > 1 ? (float*)ws : nullptr, dw, dfmt, s, ppt);
     if (sl > 1) {

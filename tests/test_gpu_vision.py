@@ -115,8 +115,9 @@ DW_CASES = [  # n, c, h, w, stride, dilation
     (1, 144, 16, 16, 1, 2),
     (2, 960, 9, 11, 1, 2),
     (1, 64, 7, 5, 2, 1),
-    (1, 64, 100, 100, 1, 1),   # > 2304 output pixels: slab partials + the reduce launch
-    (1, 192, 96, 96, 2, 1),    # 48² output: the largest one-launch weight gradient
+    (1, 64, 100, 100, 1, 1),   # many slabs: partial rows + the reduce launch
+    (1, 192, 96, 96, 2, 1),    # 48² output (DeepLab's stride-2 layer)
+    (1, 384, 24, 24, 1, 2),    # 576 pixels: the largest one-slab (one-launch) weight gradient
 ]
 
 
