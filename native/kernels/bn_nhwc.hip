@@ -480,18 +480,22 @@ __global__ void __launch_bounds__(kFuseT) bn_bwd_fused_kernel(
 // waves), finalizes, and applies from the same registers: a thread loads its
 // kSmallR rows once, all in flight together (a first version re-read them in
 // a row loop: 8.5 / 15.7 us forward / backward at 576 rows, latency-bound,
-// profiles/r6/train).  Rows <= kSmallMaxM (640: DeepLab's 24² maps).
-constexpr int kSmallR = 5;
-constexpr int64_t kSmallMaxM = (int64_t)kSmallR * (kFuseT / 8);  // 640
-// The backward holds x and dy: 512 threads (a 256-VGPR budget), 10 rows each.
-constexpr int kSmallBT = 512, kSmallBR = 10;
-static_assert((int64_t)kSmallBR * (kSmallBT / 8) == kSmallMaxM, "backward covers the same rows");
+// profiles/r6/train).  32-channel chunks (4 lanes a row, 64-byte runs): twice
+// the workgroups of 64-channel ones, half the rows' latency chain each (the
+// 64-channel backward took 10.4 us at 576 rows).  Rows <= kSmallMaxM (768:
+// DeepLab's 24² maps).
+constexpr int kSC = 32, kSL = kSC / 8;  // channels per workgroup, lanes per row
+constexpr int kSmallR = 3;
+constexpr int64_t kSmallMaxM = (int64_t)kSmallR * (kFuseT / kSL);  // 768
+// The backward holds x and dy: 512 threads (a 256-VGPR budget), 6 rows each.
+constexpr int kSmallBT = 512, kSmallBR = 6;
+static_assert((int64_t)kSmallBR * (kSmallBT / kSL) == kSmallMaxM, "backward covers the same rows");
 
 __device__ __forceinline__ void wave_rows_reduce(float (&a1)[8], float (&a2)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j)
 #pragma unroll
-    for (int o = 8; o < 64; o <<= 1) {  // lanes cg + 8·row: xor over the row bits
+    for (int o = kSL; o < 64; o <<= 1) {  // lanes cg + kSL·row: xor over the row bits
       a1[j] += __shfl_xor(a1[j], o, 64);
       a2[j] += __shfl_xor(a2[j], o, 64);
     }
@@ -502,16 +506,16 @@ __global__ void __launch_bounds__(kFuseT) bn_fwd_small_kernel(
     const bf16x8* __restrict__ x, bf16x8* __restrict__ y, const P* __restrict__ gamma, const P* __restrict__ beta,
     P* __restrict__ run_mean, P* __restrict__ run_var, float* __restrict__ mean, float* __restrict__ invstd,
     float* __restrict__ coef, int64_t M, int C, float eps, float momentum) {
-  __shared__ float2 red[kFuseT / 64][kFuseC];
-  __shared__ float sS[kFuseC], sT[kFuseC];
-  const int cg = threadIdx.x & 7, ro = threadIdx.x >> 3, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c0 = blockIdx.x * kFuseC;
+  __shared__ float2 red[kFuseT / 64][kSC];
+  __shared__ float sS[kSC], sT[kSC];
+  const int cg = threadIdx.x % kSL, ro = threadIdx.x / kSL, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * kSC;
   const int cvec = C >> 3, cv = (c0 >> 3) + cg;
   float k0[8], a1[8], a2[8];
   bf16x8 v[kSmallR];
 #pragma unroll
   for (int u = 0; u < kSmallR; ++u) {  // rows past M read row 0: shifted, they add 0
-    const int64_t r = ro + u * (kFuseT / 8);
+    const int64_t r = ro + u * (kFuseT / kSL);
     v[u] = x[(r < M ? r : 0) * cvec + cv];
   }
   const bf16x8 v0 = x[cv];
@@ -529,11 +533,11 @@ __global__ void __launch_bounds__(kFuseT) bn_fwd_small_kernel(
       a2[j] = fmaf(d, d, a2[j]);
     }
   wave_rows_reduce(a1, a2);
-  if (lane < 8)
+  if (lane < kSL)
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = make_float2(a1[j], a2[j]);
   __syncthreads();
-  if (threadIdx.x < kFuseC) {
+  if (threadIdx.x < kSC) {
     const int c = c0 + threadIdx.x;
     double s1 = 0.0, s2 = 0.0;
 #pragma unroll
@@ -570,7 +574,7 @@ __global__ void __launch_bounds__(kFuseT) bn_fwd_small_kernel(
   }
 #pragma unroll
   for (int u = 0; u < kSmallR; ++u) {
-    const int64_t r = ro + u * (kFuseT / 8);
+    const int64_t r = ro + u * (kFuseT / kSL);
     if (r >= M) break;
     bf16x8 o;
 #pragma unroll
@@ -587,10 +591,10 @@ __global__ void __launch_bounds__(kSmallBT) bn_bwd_small_kernel(
     const bf16x8* __restrict__ add, const P* __restrict__ gamma, const P* __restrict__ beta,
     const float* __restrict__ mean, const float* __restrict__ invstd, P* __restrict__ dgamma,
     P* __restrict__ dbeta, int64_t M, int C) {
-  __shared__ float2 red[kSmallBT / 64][kFuseC];
-  __shared__ float sC[kFuseC], sB[kFuseC];
-  const int cg = threadIdx.x & 7, ro = threadIdx.x >> 3, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c0 = blockIdx.x * kFuseC;
+  __shared__ float2 red[kSmallBT / 64][kSC];
+  __shared__ float sC[kSC], sB[kSC];
+  const int cg = threadIdx.x % kSL, ro = threadIdx.x / kSL, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * kSC;
   const int cvec = C >> 3, cv = (c0 >> 3) + cg;
   float sc[8], sh[8], mu[8], is[8], a1[8], a2[8];
 #pragma unroll
@@ -605,14 +609,14 @@ __global__ void __launch_bounds__(kSmallBT) bn_bwd_small_kernel(
   bf16x8 v[kSmallBR], g[kSmallBR];
 #pragma unroll
   for (int u = 0; u < kSmallBR; ++u) {
-    const int64_t r = ro + u * (kSmallBT / 8);
+    const int64_t r = ro + u * (kSmallBT / kSL);
     const int64_t i = (r < M ? r : 0) * cvec + cv;
     v[u] = x[i];
     g[u] = dy[i];
   }
 #pragma unroll
   for (int u = 0; u < kSmallBR; ++u) {
-    const float ok = ro + u * (kSmallBT / 8) < M ? 1.0f : 0.0f;
+    const float ok = ro + u * (kSmallBT / kSL) < M ? 1.0f : 0.0f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float xf = bf2f(v[u].v[j]);
@@ -622,11 +626,11 @@ __global__ void __launch_bounds__(kSmallBT) bn_bwd_small_kernel(
     }
   }
   wave_rows_reduce(a1, a2);
-  if (lane < 8)
+  if (lane < kSL)
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = make_float2(a1[j], a2[j]);
   __syncthreads();
-  if (threadIdx.x < kFuseC) {
+  if (threadIdx.x < kSC) {
     const int c = c0 + threadIdx.x;
     double s1 = 0.0, s2 = 0.0;
 #pragma unroll
@@ -653,7 +657,7 @@ __global__ void __launch_bounds__(kSmallBT) bn_bwd_small_kernel(
   }
 #pragma unroll
   for (int u = 0; u < kSmallBR; ++u) {
-    const int64_t r = ro + u * (kSmallBT / 8);
+    const int64_t r = ro + u * (kSmallBT / kSL);
     if (r >= M) break;
     const int64_t i = r * cvec + cv;
     bf16x8 rr;
@@ -747,7 +751,7 @@ int fwd_train(const void* x, void* y, const void* gamma, const void* beta, void*
   auto* rm = static_cast<P*>(run_mean);
   auto* rv = static_cast<P*>(run_var);
   if (kind == 2) {
-    const dim3 grid((unsigned)(C / kFuseC));
+    const dim3 grid((unsigned)(C / kSC));
     switch (act) {
       case 0: hipLaunchKernelGGL((bn_fwd_small_kernel<0, P>), grid, dim3(kFuseT), 0, s, xv, yv, g_, b_, rm, rv, mean, invstd, coef_out, M, C, eps, momentum); break;
       case 1: hipLaunchKernelGGL((bn_fwd_small_kernel<1, P>), grid, dim3(kFuseT), 0, s, xv, yv, g_, b_, rm, rv, mean, invstd, coef_out, M, C, eps, momentum); break;
@@ -796,7 +800,7 @@ void bwd_launch(const bf16x8* dyv, const bf16x8* xv, bf16x8* dxv, const P* gamma
                 const bf16x8* addv, hipStream_t s) {
   const int kind = plain_kind(M, C);
   if (kind == 2) {
-    const dim3 grid((unsigned)(C / kFuseC));
+    const dim3 grid((unsigned)(C / kSC));
     if (addv)
       hipLaunchKernelGGL((bn_bwd_small_kernel<kAct, true, P>), grid, dim3(kSmallBT), 0, s, dyv, xv, dxv, addv, gamma,
                          beta, mean, invstd, dgamma, dbeta, M, C);

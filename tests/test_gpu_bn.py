@@ -44,7 +44,7 @@ CASES = [
     # (1, 192, 25, 25) would be the natural one-launch case, but PyTorch's own fp32
     # channels_last batch_norm (the reference) segfaults on it on MI355X
     # (scripts/bn_case_check.py ref 1 192 25 25 30, rc 139)
-    (2, 192, 16, 19, "relu6", torch.float32, 30.0),   # one launch, 608 rows (<= 640), shifted sums
+    (2, 192, 16, 19, "relu6", torch.float32, 30.0),   # one launch, 608 rows (<= 768), shifted sums
     (2, 192, 40, 40, "relu6", torch.float32, 30.0),   # reduce + fused apply, shifted sums
     (1, 64, 192, 192, "relu6", torch.bfloat16, 0.0),  # DeepLab's stem BN: reduce + fused apply
 ]
