@@ -346,8 +346,11 @@ def test_vmem_host_copies_keep_managed_ranges_in_hbm(gpu_build):
         assert res[k] > 1000, (k, res)
     # a managed range still reads at HBM speed after hipMemcpy2D and hipMemset
     assert res["memcpy2d_rc"] == 0 and res["memset_rc"] == 0 and res["memset_zeroed"], res
+    # (against the same run's fresh-range speed: an absolute 4000 GB/s missed at
+    # 3948 on one box whose fresh range read 4223; pages moved to system memory
+    # read at host-link speed, ~50x slower)
     for k in ("after_memcpy2d_GBps", "after_memset_GBps"):
-        assert res[k] > 4000, (k, res)
+        assert res[k] > 0.8 * res["fresh_GBps"], (k, res)
 
 
 def test_rocr_cu_mask_env_matches_shim_masks(gpu_build):
