@@ -136,6 +136,16 @@ RECIPES: dict[str, tuple[list, list, int]] = {
         ("2.2", {}, ["--workload", "2.2"]),
         ("3.2", {}, ["--workload", "3.2"]),
     ], 300),
+    # cost of the ROCr tools-lib intercept (HSA_TOOLS_LIB=libvgpu.so,
+    # intercept queues on) on the flagship and on 1.2 training (profiles/r6/toolslib).
+    "tools-lib": (["--steps", "30", "--warmup", "10"], [
+        ("flag_base", {}, []),
+        ("flag_tools", {"VGPU_HSA_TOOLS_INTERCEPT": "1"}, []),
+        ("t12_base", {}, EXCL + ["--workload", "1.2", "--steps", "20", "--warmup", "5"]),
+        ("t12_tools", {"VGPU_HSA_TOOLS_INTERCEPT": "1"}, EXCL + ["--workload", "1.2", "--steps", "20", "--warmup", "5"]),
+        ("flag_base_again", {}, []),
+        ("flag_tools_again", {"VGPU_HSA_TOOLS_INTERCEPT": "1"}, []),
+    ], 400),
     # Virtual device memory column of the reference's chart, one workload.
     "vmem": (["--steps", "20", "--warmup", "5"], [
         ("vgpu", {}, ["--pods", "2", "--gpucores", "50", "--gpumem", "144000"]),

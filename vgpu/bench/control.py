@@ -82,7 +82,9 @@ def admit_pods(specs: list, device_index: int, workdir: str, *, policy: str = "t
     cfg = DevicePluginConfig(node_name=NODE, device_split_count=max(10, len(specs)), config_file="",
                              host_lib_dir=str(host_lib), host_lock_dir=str(lock), cu_share=policy,
                              max_mask_slots=max_mask_slots, device_memory_scaling=memory_scaling,
-                             pool_concurrency=pool_concurrency, suspend_evict=suspend_evict)
+                             pool_concurrency=pool_concurrency, suspend_evict=suspend_evict,
+                             # A/B of the ROCr tools-lib intercept (scripts/bench_ab.py tools-lib)
+                             hsa_tools_intercept=os.environ.get("VGPU_HSA_TOOLS_INTERCEPT", "") in ("1", "true"))
     dev = device or Device(uuid=f"GPU-bench-{device_index}", index=device_index,
                            render_minor=128 + device_index, card=device_index)
     srv = FakeApiServer()

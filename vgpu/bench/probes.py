@@ -819,13 +819,71 @@ def evictee(gib: int = 64, block_gib: int = 4) -> dict:
     return res
 
 
+def _ipc_child(q_in, q_out) -> None:
+    """ipcshare's consumer process: sum the shared tensor, write element 0."""
+    import torch
+    try:
+        t = q_in.get(timeout=120)
+        s = int(t.sum().item())
+        t[0] = -1
+        torch.cuda.synchronize()
+        q_out.put({"sum": s})
+        del t
+    except Exception as e:  # report, never hang the parent
+        q_out.put({"error": repr(e)[:400]})
+
+
+def ipcshare(mib: int = 64) -> dict:
+    """share a CUDA tensor with another process of the container
+    (torch.multiprocessing, CUDA IPC) while allocations of >= 32 MiB are VMM
+    mappings (VGPU_SUSPEND_EVICT).  Reports whether the export worked, what the
+    consumer read, whether its write is visible here, and the shim's VMM /
+    IPC state of the range."""
+    import ctypes
+
+    import torch
+    import torch.multiprocessing as mp
+    lib = ctypes.CDLL(None)
+    n = (mib << 20) // 4
+    x = torch.arange(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    m = (ctypes.c_uint64 * 8)()
+    if hasattr(lib, "vgpu_self_vmm_stats"):
+        lib.vgpu_self_vmm_stats(m)
+    out = {"vmm_ranges": int(m[0]), "vmm_bytes": int(m[1]), "expected_sum": n * (n - 1) // 2}
+    ctx = mp.get_context("spawn")
+    q_in, q_out = ctx.Queue(), ctx.Queue()
+    p = ctx.Process(target=_ipc_child, args=(q_in, q_out))
+    p.start()
+    try:
+        try:
+            q_in.put(x)
+            out["exported"] = True
+        except Exception as e:
+            out["exported"] = False
+            out["export_error"] = repr(e)[:400]
+            q_in.put(torch.zeros(1))  # let the child finish
+        r = q_out.get(timeout=180)
+        out.update({"child_" + k: v for k, v in r.items()})
+        p.join(60)
+        out["child_rc"] = p.exitcode
+    finally:
+        if p.is_alive():
+            p.kill()
+    torch.cuda.synchronize()
+    out["parent_sees_write"] = bool(int(x[0].item()) == -1)
+    out["child_sum_ok"] = out.get("child_sum") == out["expected_sum"]
+    return out
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     cmd = argv.pop(0) if argv else "census"
     nums = [int(a) for a in argv]
     out = {"census": census, "busy": busy, "cap": cap, "smi": smi, "graph": graph, "arrays": arrays,
            "progress": progress, "forkjoin": forkjoin, "vmem": vmem, "vmemcopy": vmemcopy, "capheld": capheld, "asynccap": asynccap, "rcclloop": rcclloop,
-           "vmemfull": vmemfull, "evictee": evictee, "busyvia": busyvia, "pitch": pitch}[cmd](*nums)
+           "vmemfull": vmemfull, "evictee": evictee, "busyvia": busyvia, "pitch": pitch,
+           "ipcshare": ipcshare}[cmd](*nums)
     out["shim"] = shim_stats()
     print("PROBE " + json.dumps(out), flush=True)
     return 0
