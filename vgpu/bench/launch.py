@@ -161,6 +161,8 @@ def launch_pods(specs: list[PodSpec], device: str, *, steps: int, warmup: int, s
             env["GPU_MAX_HW_QUEUES"] = str(hw_queues)
         if shim:
             env.update(cenv)
+            if "HSA_TOOLS_LIB" in env:  # the container path of the library -> this host's build
+                env["HSA_TOOLS_LIB"] = str(shim_path())
             env = preload_env(env)
         env.update(sp.extra_env)
         cmd = [sys.executable, "-u", "-m", "vgpu.bench.pod", "--workload", sp.workload,
