@@ -261,11 +261,24 @@ __attribute__((visibility("default"))) hipError_t hipModuleUnload(hipModule_t m)
 // a device allocation: the runtime cannot export it.  Say so instead of the
 // runtime's bare invalid-value (PyTorch CUDA-IPC tensors / RCCL P2P buffers
 // of an oversubscribed pod: docs/config.md, virtual device memory).
+// Likewise a VMM-backed range (--suspend-evict: allocations >= 32 MiB are
+// hipMemCreate handles mapped at a reserved VA): ROCm's legacy IPC cannot
+// export it -- the runtime answers invalid-value, and PyTorch's CUDA-IPC
+// sharing then fails in the queue's feeder thread with the consumer waiting
+// forever (measured on MI355X, profiles/r6/ipc).  Refuse it up front with the
+// remedy instead.
 __attribute__((visibility("default"))) hipError_t hipIpcGetMemHandle(hipIpcMemHandle_t* handle, void* dev_ptr) {
   ensure_init();
   if (st().enabled && dev_ptr && vmem_contains(dev_ptr)) {
     VLOG_WARN("hipIpcGetMemHandle(%p): a virtual-device-memory (managed) range cannot be exported over IPC; "
               "set VGPU_VMEM_MANAGED_MIN_MB=-1 for pods that share device buffers between processes",
+              dev_ptr);
+    return hipErrorNotSupported;
+  }
+  if (st().enabled && dev_ptr && vmm_owns(dev_ptr)) {
+    VLOG_WARN("hipIpcGetMemHandle(%p): a suspend-evict (VMM) range cannot be exported over legacy IPC; "
+              "set VGPU_VMEM_MANAGED_MIN_MB=-1 for pods that share device buffers between processes "
+              "(their buffers then stay resident across a suspend)",
               dev_ptr);
     return hipErrorNotSupported;
   }

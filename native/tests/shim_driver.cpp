@@ -940,6 +940,24 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (sc == "vmm_ipc") {
+    // legacy IPC of a VMM-backed range (VGPU_SUSPEND_EVICT) is
+    // refused up front (hipErrorNotSupported); a small plain buffer exports.
+    void* p = nullptr;
+    void* small = nullptr;
+    const int ra = hipMalloc(&p, 96ull << 20), rs = hipMalloc(&small, 8ull << 20);
+    auto stats = sym<void (*)(uint64_t*)>("vgpu_self_vmm_stats");
+    uint64_t v[8] = {};
+    if (stats) stats(v);
+    hipIpcMemHandle_t h;
+    printf("alloc=%d\nsmall=%d\nranges=%llu\n", ra, rs, (unsigned long long)v[0]);
+    const int i1 = (int)hipIpcGetMemHandle(&h, p);
+    const int i2 = (int)hipIpcGetMemHandle(&h, (char*)p + 4096);
+    const int i3 = (int)hipIpcGetMemHandle(&h, small);
+    printf("ipc_vmm=%d\nipc_vmm_offset=%d\nipc_small=%d\n", i1, i2, i3);
+    return 0;
+  }
+
   if (sc == "suspend_vmm") {
     // VGPU_SUSPEND_EVICT, VMM vehicle (vmm.cpp): a large allocation is a VMM
     // mapping, a small one stays plain.  SIGUSR2 copies the mapping out and

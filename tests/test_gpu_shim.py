@@ -353,6 +353,26 @@ def test_vmem_host_copies_keep_managed_ranges_in_hbm(gpu_build):
         assert res[k] > 0.8 * res["fresh_GBps"], (k, res)
 
 
+def test_cuda_ipc_tensor_sharing_under_suspend_evict(gpu_build):
+    """a tensor shared with another process (torch.multiprocessing,
+    CUDA IPC) in a --suspend-evict pod.  A 64 MiB tensor is a VMM mapping there,
+    which ROCm's legacy IPC cannot export: the shim refuses the export cleanly
+    (an error in the producer, no hung consumer).  With the documented remedy
+    (VGPU_VMEM_MANAGED_MIN_MB=-1: no VMM ranges) the tensor is shared both ways;
+    without suspend-evict it is shared as usual."""
+    base = {"VGPU_DEVICE_MEMORY_LIMIT_0": "64g"}
+    plain = probe(["ipcshare", 64], base, timeout=400)
+    assert plain["exported"] and plain["child_sum_ok"] and plain["parent_sees_write"], plain
+    evict = probe(["ipcshare", 64], {**base, "VGPU_SUSPEND_EVICT": "true"}, timeout=400)
+    assert evict["vmm_ranges"] == 1, evict
+    assert not evict["exported"] and "not supported" in evict["export_error"].lower(), evict
+    assert evict["child_rc"] == 0, evict
+    fixed = probe(["ipcshare", 64], {**base, "VGPU_SUSPEND_EVICT": "true", "VGPU_VMEM_MANAGED_MIN_MB": "-1"},
+                  timeout=400)
+    assert fixed["vmm_ranges"] == 0, fixed
+    assert fixed["exported"] and fixed["child_sum_ok"] and fixed["parent_sees_write"], fixed
+
+
 def test_rocr_cu_mask_env_matches_shim_masks(gpu_build):
     """Allocate also sets HSA_CU_MASK so ROCr masks the
     queues the shim never sees (its internal blit queue).  Same logical bits:

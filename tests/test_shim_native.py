@@ -1079,6 +1079,26 @@ def test_vmm_free_waits_for_running_kernels(native_build):
     assert float(o["free_ms"]) >= 280, o
 
 
+def test_vmm_range_refuses_legacy_ipc(native_build):
+    """with --suspend-evict, allocations >= 32 MiB are VMM
+    mappings, which ROCm's legacy IPC cannot export (the runtime answered
+    invalid-value on MI355X and PyTorch's sharing hung the consumer,
+    profiles/r6/ipc).  The shim refuses such an export with
+    hipErrorNotSupported and the remedy (VGPU_VMEM_MANAGED_MIN_MB=-1); a plain
+    (small) buffer still exports."""
+    o = run("vmm_ipc", env={"VGPU_FAKE_MEM": str(16 * GiB), "VGPU_DEVICE_MEMORY_LIMIT_0": "12g",
+                            "VGPU_SUSPEND_EVICT": "true"})
+    not_supported = str(801)  # hipErrorNotSupported
+    assert (o["alloc"], o["small"], o["ranges"]) == ("0", "0", "1"), o
+    assert o["ipc_vmm"] == not_supported and o["ipc_vmm_offset"] == not_supported, o
+    assert o["ipc_small"] == "0", o
+    assert "VGPU_VMEM_MANAGED_MIN_MB=-1" in o["_stderr"]
+    # the remedy: no VMM ranges, the large buffer exports
+    o2 = run("vmm_ipc", env={"VGPU_FAKE_MEM": str(16 * GiB), "VGPU_DEVICE_MEMORY_LIMIT_0": "12g",
+                             "VGPU_SUSPEND_EVICT": "true", "VGPU_VMEM_MANAGED_MIN_MB": "-1"})
+    assert o2["ranges"] == "0" and o2["ipc_vmm"] == "0", o2
+
+
 def test_launch_charged_to_the_streams_device(native_build):
     """a launch onto device 3's stream while device 0 is
     current is charged to device 3's limiter, not to the thread's current device."""

@@ -857,12 +857,16 @@ def ipcshare(mib: int = 64) -> dict:
     p.start()
     try:
         try:
+            # pickle here, not in the queue's feeder thread, so an export error
+            # surfaces in this thread (and the child still gets something)
+            from multiprocessing.reduction import ForkingPickler
+            ForkingPickler.dumps(x)
             q_in.put(x)
             out["exported"] = True
         except Exception as e:
             out["exported"] = False
             out["export_error"] = repr(e)[:400]
-            q_in.put(torch.zeros(1))  # let the child finish
+            q_in.put(torch.zeros(1, device="cuda"))  # let the child finish
         r = q_out.get(timeout=180)
         out.update({"child_" + k: v for k, v in r.items()})
         p.join(60)
