@@ -235,6 +235,36 @@ def test_deeplab_native_step_loss_and_grads_vs_fp32(gpu_build):
     assert not gn["stem"][32:].any()  # the padding carried no gradient
 
 
+@pytest.mark.parametrize("case", [(1, 320, 256, 24, 6), (1, 320, 256, 24, 18), (2, 320, 256, 32, 12)])
+def test_atrous_conv_space_to_batch_matches_fp32(gpu_build, case):
+    """DeepLab's ASPP branches (3x3, dilation = padding = d) as a plain 3x3 on the
+    space-to-batch sub-images (vgpu.models.vision._atrous_conv): forward, data
+    and weight gradients on the native kernels against fp32 F.conv2d with
+    dilation; the folded inference form (bias + ReLU6 epilogue) too."""
+    from vgpu.models.vision import _atrous_conv, _atrous_ok
+    n, c, cout, hw, d = case
+    conv = torch.nn.Conv2d(c, cout, 3, padding=d, dilation=d, bias=False).cuda().to(torch.bfloat16)
+    conv = conv.to(memory_format=CL)
+    x = _x((n, c, hw, hw), 31).requires_grad_()
+    assert _atrous_ok(x, conv)
+    y = _atrous_conv(x, conv)
+    xr = x.detach().float().requires_grad_()
+    wr = conv.weight.detach().float().requires_grad_()
+    yr = torch.nn.functional.conv2d(xr, wr, padding=d, dilation=d)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=CL)
+    assert _rel(y, yr) < 1e-2
+    dy = _x(tuple(y.shape), 32)
+    y.backward(dy)
+    yr.backward(dy.float())
+    assert _rel(x.grad, xr.grad) < 1e-2
+    assert _rel(conv.weight.grad, wr.grad) < 1e-2
+    b = torch.randn(cout, device="cuda")
+    with torch.inference_mode():
+        yi = _atrous_conv(x.detach(), conv, conv.weight.detach().contiguous(memory_format=CL), b, "relu6")
+    ri = (yr.detach() + b.view(1, -1, 1, 1)).clamp(0, 6)
+    assert _rel(yi, ri) < 2e-2
+
+
 def test_resize_bilinear_backward_matches_pytorch(gpu_build):
     """The GEMM backward of the bilinear resize (vgpu.ops.interp) against
     PyTorch's atomic scatter, DeepLab's two shapes, fp32."""

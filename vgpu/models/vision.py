@@ -9,6 +9,8 @@ equivalent (parity unpinned); all weights are random-init.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 import torch.nn.functional as F
@@ -142,6 +144,60 @@ class NativeVGG16Inference(nn.Module):
         return self.classifier(torch.flatten(x, 1))
 
 
+_ATROUS = os.environ.get("VGPU_ATROUS", "1") != "0"  # VGPU_ATROUS=0: dilated convs on MIOpen (A/B)
+
+
+def _atrous_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    """A dilated dense 3x3 conv (DeepLab's ASPP branches) that can run as a
+    plain 3x3 on the space-to-batch sub-images (bf16 channels_last CUDA, C and
+    Cout multiples of 64)."""
+    d = conv.dilation[0]
+    return (_ATROUS and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and conv.groups == 1 and d > 1
+            and conv.dilation == (d, d) and conv.kernel_size == (3, 3) and conv.stride == (1, 1)
+            and conv.padding == (d, d) and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0)
+
+
+def _space_to_batch(x: torch.Tensor, d: int) -> torch.Tensor:
+    """[N, C, H, W] -> [d·d·N, C, ⌈H/d⌉, ⌈W/d⌉]: sub-image (a, b) holds the
+    pixels (a + d·i, b + d·j) (zero rows / columns past H, W), so a 3x3 conv
+    with dilation d and padding d is a plain 3x3 / padding 1 conv on each
+    sub-image (TF's atrous convolution)."""
+    n, c, h, w = x.shape
+    hb, wb = -(-h // d), -(-w // d)
+    if hb * d != h or wb * d != w:
+        x = F.pad(x, (0, wb * d - w, 0, hb * d - h))
+    x = x.reshape(n, c, hb, d, wb, d).permute(3, 5, 0, 1, 2, 4).reshape(d * d * n, c, hb, wb)
+    return x.contiguous(memory_format=torch.channels_last)
+
+
+def _batch_to_space(y: torch.Tensor, d: int, n: int, h: int, w: int) -> torch.Tensor:
+    c, hb, wb = y.shape[1:]
+    y = y.reshape(d, d, n, c, hb, wb).permute(2, 3, 4, 0, 5, 1).reshape(n, c, hb * d, wb * d)
+    if hb * d != h or wb * d != w:
+        y = y[:, :, :h, :w]
+    return y.contiguous(memory_format=torch.channels_last)
+
+
+def _atrous_conv(x: torch.Tensor, conv: nn.Conv2d, w: torch.Tensor | None = None,
+                 b: torch.Tensor | None = None, act: str = "none") -> torch.Tensor:
+    """conv(x) for a dilated 3x3 (see _atrous_ok) on the native MFMA kernels
+    via space-to-batch: training through vgpu.ops.conv's autograd conv (native
+    data / weight gradients), or with a folded (w, b, act).  Training uses it
+    (4.2: 367-373 -> 377 images/s, MIOpen's weight gradient alone was ~35 us a
+    branch); the BN-folded inference keeps MIOpen's one forward kernel, which
+    measured faster than the two copies + conv (4.1: 2 994 vs 2 925 images/s,
+    scripts/pod_ab.sh)."""
+    from vgpu.ops import conv as C
+    d = conv.dilation[0]
+    n, _, h, wd = x.shape
+    xs = _space_to_batch(x, d)
+    if w is None:
+        y = C._ConvTrainFn.apply(xs, conv.weight, None, 1, 1)
+    else:
+        y = C.conv2d(xs, w, b, stride=1, padding=1, act=act)
+    return _batch_to_space(y, d, n, h, wd)
+
+
 class ConvBNAct(nn.Sequential):
     """conv → BatchNorm → (ReLU6); the BN + activation pair runs as one native
     training kernel pair (vgpu.ops.bn) on bf16 channels_last tensors.  On CUDA
@@ -192,8 +248,11 @@ class ConvBNAct(nn.Sequential):
         xs = x
         if x.is_cuda:
             from vgpu.ops import dwconv
+            from vgpu.ops.conv import native_train_enabled
             if dwconv.eligible(x, conv):
                 y = dwconv.dwconv_train(x, conv)
+            elif native_train_enabled() and conv.bias is None and _atrous_ok(x, conv):
+                y = _atrous_conv(x.contiguous(memory_format=torch.channels_last), conv)
             else:
                 from vgpu.ops.conv import conv_train
                 y = conv_train(x, conv, res_out=res_out)
@@ -274,7 +333,10 @@ class MobileNetV2Backbone(nn.Module):
     def __init__(self, pad: int = 1):
         super().__init__()
         self.pad = pad
-        layers: list[nn.Module] = [_conv_bn(3, _padc(32, pad), 3, 2, real=(3, 32))]
+        # the stem reads the image zero-padded to 64 channels too: a native conv
+        # and weight gradient (~21x the MACs of 3 channels, still ~2 us) instead
+        # of MIOpen's forward + weight gradient + helpers (~70 us a 4.2 step)
+        layers: list[nn.Module] = [_conv_bn(_padc(3, pad), _padc(32, pad), 3, 2, real=(3, 32))]
         cin = 32
         dilation = 1
         for i, (t, c, n, s) in enumerate(self.settings):
@@ -287,6 +349,13 @@ class MobileNetV2Backbone(nn.Module):
         self.out_channels = _padc(cin, pad)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        cin = self.features[0][0].in_channels
+        if x.shape[1] < cin:  # an RGB image into the channel-padded stem
+            if x.is_cuda and x.dtype == torch.bfloat16:
+                from vgpu.ops.conv import pad_channels
+                x = pad_channels(x.contiguous(memory_format=torch.channels_last), cin)
+            else:
+                x = F.pad(x, (0, 0, 0, 0, 0, cin - x.shape[1]))
         return self.features(x)
 
 
