@@ -350,7 +350,8 @@ __global__ void __launch_bounds__(kFuseT) bn_fwd_fused_kernel(
     const float2* __restrict__ partial, int64_t G, const bf16x8* __restrict__ x, bf16x8* __restrict__ y,
     const P* __restrict__ gamma, const P* __restrict__ beta, P* __restrict__ run_mean, P* __restrict__ run_var,
     float* __restrict__ coef, float* __restrict__ mean_out, float* __restrict__ invstd_out,
-    const uint16_t* __restrict__ shift, int64_t M, int C, float eps, float momentum, int64_t rows_per) {
+    const uint16_t* __restrict__ shift, int64_t M, int C, float eps, float momentum, int64_t rows_per,
+    const bf16x8* __restrict__ add = nullptr) {
   __shared__ double r1[kFuseQ][kFuseC], r2[kFuseQ][kFuseC];
   __shared__ float sS[kFuseC], sT[kFuseC];
   const int c0 = blockIdx.x * kFuseC;
@@ -398,8 +399,14 @@ __global__ void __launch_bounds__(kFuseT) bn_fwd_fused_kernel(
   for (int64_t r = (int64_t)blockIdx.y * rows_per + ro; r < r_end; r += kFuseT / 8) {
     const bf16x8 v = x[r * cvec + cv];
     bf16x8 o;
+    if (add) {
+      const bf16x8 a = add[r * cvec + cv];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o.v[k] = f2bf(act_fwd<kAct>(fmaf(bf2f(v.v[k]), sc[k], sh[k])));
+      for (int k = 0; k < 8; ++k) o.v[k] = f2bf(act_fwd<kAct>(fmaf(bf2f(v.v[k]), sc[k], sh[k])) + bf2f(a.v[k]));
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o.v[k] = f2bf(act_fwd<kAct>(fmaf(bf2f(v.v[k]), sc[k], sh[k])));
+    }
     y[r * cvec + cv] = o;
   }
 }
@@ -501,11 +508,13 @@ __device__ __forceinline__ void wave_rows_reduce(float (&a1)[8], float (&a2)[8])
     }
 }
 
+// add (nullable): y = act(bn(x)) + add, an identity shortcut summed in the
+// same pass (MobileNet-V2's project BN + residual; its gradient is dy itself).
 template <int kAct, typename P>
 __global__ void __launch_bounds__(kFuseT) bn_fwd_small_kernel(
     const bf16x8* __restrict__ x, bf16x8* __restrict__ y, const P* __restrict__ gamma, const P* __restrict__ beta,
     P* __restrict__ run_mean, P* __restrict__ run_var, float* __restrict__ mean, float* __restrict__ invstd,
-    float* __restrict__ coef, int64_t M, int C, float eps, float momentum) {
+    float* __restrict__ coef, int64_t M, int C, float eps, float momentum, const bf16x8* __restrict__ add) {
   __shared__ float2 red[kFuseT / 64][kSC];
   __shared__ float sS[kSC], sT[kSC];
   const int cg = threadIdx.x % kSL, ro = threadIdx.x / kSL, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -577,8 +586,14 @@ __global__ void __launch_bounds__(kFuseT) bn_fwd_small_kernel(
     const int64_t r = ro + u * (kFuseT / kSL);
     if (r >= M) break;
     bf16x8 o;
+    if (add) {
+      const bf16x8 a = add[r * cvec + cv];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o.v[k] = f2bf(act_fwd<kAct>(fmaf(bf2f(v[u].v[k]), sc[k], sh[k])));
+      for (int k = 0; k < 8; ++k) o.v[k] = f2bf(act_fwd<kAct>(fmaf(bf2f(v[u].v[k]), sc[k], sh[k])) + bf2f(a.v[k]));
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o.v[k] = f2bf(act_fwd<kAct>(fmaf(bf2f(v[u].v[k]), sc[k], sh[k])));
+    }
     y[r * cvec + cv] = o;
   }
 }
@@ -742,8 +757,10 @@ inline bool shape_ok(int64_t M, int C) { return M >= 1 && C >= 8 && C % 8 == 0 &
 template <typename P>
 int fwd_train(const void* x, void* y, const void* gamma, const void* beta, void* run_mean, void* run_var,
               float* mean, float* invstd, float* ws, int64_t M, int C, float eps, float momentum, int act,
-              hipStream_t s, float* coef_out = nullptr) {
+              hipStream_t s, float* coef_out = nullptr, const void* add = nullptr) {
   const int kind = plain_kind(M, C);
+  if (add && kind == 0) return -2;  // the three-pass plan has no add: the caller adds
+  const auto* addv = static_cast<const bf16x8*>(add);
   const auto* xv = static_cast<const bf16x8*>(x);
   auto* yv = static_cast<bf16x8*>(y);
   const auto* g_ = static_cast<const P*>(gamma);
@@ -753,9 +770,9 @@ int fwd_train(const void* x, void* y, const void* gamma, const void* beta, void*
   if (kind == 2) {
     const dim3 grid((unsigned)(C / kSC));
     switch (act) {
-      case 0: hipLaunchKernelGGL((bn_fwd_small_kernel<0, P>), grid, dim3(kFuseT), 0, s, xv, yv, g_, b_, rm, rv, mean, invstd, coef_out, M, C, eps, momentum); break;
-      case 1: hipLaunchKernelGGL((bn_fwd_small_kernel<1, P>), grid, dim3(kFuseT), 0, s, xv, yv, g_, b_, rm, rv, mean, invstd, coef_out, M, C, eps, momentum); break;
-      case 2: hipLaunchKernelGGL((bn_fwd_small_kernel<2, P>), grid, dim3(kFuseT), 0, s, xv, yv, g_, b_, rm, rv, mean, invstd, coef_out, M, C, eps, momentum); break;
+      case 0: hipLaunchKernelGGL((bn_fwd_small_kernel<0, P>), grid, dim3(kFuseT), 0, s, xv, yv, g_, b_, rm, rv, mean, invstd, coef_out, M, C, eps, momentum, addv); break;
+      case 1: hipLaunchKernelGGL((bn_fwd_small_kernel<1, P>), grid, dim3(kFuseT), 0, s, xv, yv, g_, b_, rm, rv, mean, invstd, coef_out, M, C, eps, momentum, addv); break;
+      case 2: hipLaunchKernelGGL((bn_fwd_small_kernel<2, P>), grid, dim3(kFuseT), 0, s, xv, yv, g_, b_, rm, rv, mean, invstd, coef_out, M, C, eps, momentum, addv); break;
       default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
@@ -774,9 +791,9 @@ int fwd_train(const void* x, void* y, const void* gamma, const void* beta, void*
     const dim3 grid = fused_grid(M, C, rows_per);
     const auto* xs = static_cast<const uint16_t*>(x);
     switch (act) {
-      case 0: hipLaunchKernelGGL((bn_fwd_fused_kernel<0, P>), grid, dim3(kFuseT), 0, s, partial, p.G, xv, yv, g_, b_, rm, rv, coef, mean, invstd, xs, M, C, eps, momentum, rows_per); break;
-      case 1: hipLaunchKernelGGL((bn_fwd_fused_kernel<1, P>), grid, dim3(kFuseT), 0, s, partial, p.G, xv, yv, g_, b_, rm, rv, coef, mean, invstd, xs, M, C, eps, momentum, rows_per); break;
-      case 2: hipLaunchKernelGGL((bn_fwd_fused_kernel<2, P>), grid, dim3(kFuseT), 0, s, partial, p.G, xv, yv, g_, b_, rm, rv, coef, mean, invstd, xs, M, C, eps, momentum, rows_per); break;
+      case 0: hipLaunchKernelGGL((bn_fwd_fused_kernel<0, P>), grid, dim3(kFuseT), 0, s, partial, p.G, xv, yv, g_, b_, rm, rv, coef, mean, invstd, xs, M, C, eps, momentum, rows_per, addv); break;
+      case 1: hipLaunchKernelGGL((bn_fwd_fused_kernel<1, P>), grid, dim3(kFuseT), 0, s, partial, p.G, xv, yv, g_, b_, rm, rv, coef, mean, invstd, xs, M, C, eps, momentum, rows_per, addv); break;
+      case 2: hipLaunchKernelGGL((bn_fwd_fused_kernel<2, P>), grid, dim3(kFuseT), 0, s, partial, p.G, xv, yv, g_, b_, rm, rv, coef, mean, invstd, xs, M, C, eps, momentum, rows_per, addv); break;
       default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
@@ -884,6 +901,24 @@ VGPU_API int vgpu_bn_act_fwd_train(const void* x, void* y, const void* gamma, co
   if (param_bf16)
     return fwd_train<uint16_t>(x, y, gamma, beta, run_mean, run_var, mean, invstd, ws, M, C, eps, momentum, act, s);
   return fwd_train<float>(x, y, gamma, beta, run_mean, run_var, mean, invstd, ws, M, C, eps, momentum, act, s);
+}
+
+// y = act(batchnorm_train(x)) + add (add: bf16 like y, same layout).  -2
+// when this shape's plan has no add form (the three-pass path: C % 64 != 0 or
+// VGPU_BN_FUSE_SMALL=0); nothing was launched then.
+VGPU_API int vgpu_bn_act_fwd_train_add(const void* x, void* y, const void* gamma, const void* beta, void* run_mean,
+                                       void* run_var, float* mean, float* invstd, float* ws, int64_t M, int C,
+                                       float eps, float momentum, int act, int param_bf16, const void* add,
+                                       void* stream) {
+  if (!shape_ok(M, C) || !aligned16(x) || !aligned16(y) || !aligned16(ws) || !mean || !invstd ||
+      (!run_mean) != (!run_var) || !add || !aligned16(add))
+    return (int)hipErrorInvalidValue;
+  auto s = (hipStream_t)stream;
+  if (param_bf16)
+    return fwd_train<uint16_t>(x, y, gamma, beta, run_mean, run_var, mean, invstd, ws, M, C, eps, momentum, act, s,
+                               nullptr, add);
+  return fwd_train<float>(x, y, gamma, beta, run_mean, run_var, mean, invstd, ws, M, C, eps, momentum, act, s, nullptr,
+                          add);
 }
 
 // dx, dgamma, dbeta of y = act(batchnorm_train(x)) given dy and the saved

@@ -113,6 +113,27 @@ def test_bn_plain_plans_agree_with_three_pass(B, shape):
         torch.testing.assert_close(a, b, atol=2e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("shape", [(1, 192, 24, 24), (1, 64, 96, 96), (2, 96, 7, 7)])
+def test_bn_act_with_shortcut_add_matches_unfused(B, shape):
+    """bn_act(x, bn, add=r): the identity shortcut summed in the BatchNorm's own
+    pass (one-launch and fused plans; the three-pass plan at C=96 adds after)
+    gives the unfused act(bn(x)) + r, and r's gradient is dy."""
+    n, c, h, w = shape
+    res = []
+    for fused in (True, False):
+        torch.manual_seed(0)
+        bn = torch.nn.BatchNorm2d(c).cuda().train()
+        x = _x(shape, 41, 1.0).requires_grad_()
+        r = _x(shape, 42).requires_grad_()
+        y = B.bn_act(x, bn, "none", add=r) if fused else B.bn_act(x, bn, "none") + r
+        dy = _x(shape, 43)
+        y.backward(dy)
+        res.append([y.float(), x.grad.float(), r.grad.float(), bn.weight.grad, bn.running_mean.clone()])
+    for a, b in zip(*res):
+        torch.testing.assert_close(a, b, atol=2e-2, rtol=1e-2)
+    assert torch.equal(res[0][2], _x(shape, 43).float())
+
+
 def test_bn_act_module_entry_updates_counters(B):
     bn = torch.nn.BatchNorm2d(64).cuda().train()
     x = _x((2, 64, 8, 8), 4)

@@ -231,7 +231,11 @@ def test_deeplab_native_step_loss_and_grads_vs_fp32(gpu_build):
     assert _cos(gn["head"], gr["head"]) > 0.99
     for k in gn:
         assert _cos(gn[k], gr[k]) > _cos(gt[k], gr[k]) - 0.1, k
-        assert _cos(gn[k], gt[k]) > 0.8, k  # measured 0.91-0.94 (see the test above)
+        # sanity (a wiring error gives ~0): the two bf16 steps' noise-dominated
+        # early gradients agree at 0.77-0.94 depending on rounding order (0.91-0.94
+        # before the stem / shortcut-add changes, 0.77-0.86 after; MIOpen's own
+        # bf16 path also moves by ~0.01 run to run)
+        assert _cos(gn[k], gt[k]) > 0.6, k
     assert not gn["stem"][32:].any()  # the padding carried no gradient
 
 

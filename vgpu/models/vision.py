@@ -237,13 +237,15 @@ class ConvBNAct(nn.Sequential):
         y = F.conv2d(x, w, b.to(x.dtype), conv.stride, conv.padding, conv.dilation, conv.groups)
         return F.hardtanh_(y, 0.0, 6.0) if act == "relu6" else y
 
-    def forward(self, x: torch.Tensor, res_out: bool = False):
-        """act(bn(conv(x))); res_out (1x1 / dense convs): also return x as an
-        identity shortcut whose gradient the conv's data-gradient kernel sums in
-        (vgpu.ops.conv.conv_train)."""
+    def forward(self, x: torch.Tensor, res_out: bool = False, add: torch.Tensor | None = None):
+        """act(bn(conv(x))) (+ add); res_out (1x1 / dense convs): also return x
+        as an identity shortcut whose gradient the conv's data-gradient kernel
+        sums in (vgpu.ops.conv.conv_train); add: a shortcut summed in the
+        BatchNorm's own pass (vgpu.ops.bn.bn_act)."""
         conv = self[0]
         if not self.training and getattr(self, "_fused", None) is not None:
             y = self._forward_fused(x)
+            y = y if add is None else y + add
             return (y, x) if res_out else y
         xs = x
         if x.is_cuda:
@@ -260,7 +262,7 @@ class ConvBNAct(nn.Sequential):
                     y, xs = y
         else:
             y = conv(x)
-        y = bn_act(y, self[1], "relu6" if len(self) > 2 else "none")
+        y = bn_act(y, self[1], "relu6" if len(self) > 2 else "none", add=add)
         return (y, xs) if res_out else y
 
 
@@ -309,11 +311,12 @@ class InvertedResidual(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if not self.use_res:
             return self.body(x)
-        # the shortcut's gradient joins the first conv's data gradient in its epilogue
+        # the shortcut's gradient joins the first conv's data gradient in its
+        # epilogue; the shortcut itself is added in the last BatchNorm's pass
         y, xs = self.body[0](x, res_out=True)
-        for m in self.body[1:]:
+        for m in self.body[1:-1]:
             y = m(y)
-        return xs + y
+        return self.body[-1](y, add=xs)
 
 
 class MobileNetV2Backbone(nn.Module):

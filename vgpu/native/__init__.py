@@ -115,6 +115,7 @@ def load_kernels() -> ctypes.CDLL:
     lib.vgpu_bn_workspace.argtypes = [i64, ci]
     lib.vgpu_bn_workspace.restype = i64
     lib.vgpu_bn_act_fwd_train.argtypes = [vp] * 9 + [i64, ci, cf, cf, ci, ci, vp]
+    lib.vgpu_bn_act_fwd_train_add.argtypes = [vp] * 9 + [i64, ci, cf, cf, ci, ci, vp, vp]
     lib.vgpu_bn_act_bwd.argtypes = [vp] * 10 + [i64, ci, ci, ci, vp]
     lib.vgpu_bn_act_bwd_add.argtypes = [vp] * 10 + [i64, ci, ci, ci, vp, vp]
     lib.vgpu_bn_act_bwd_add.restype = ci

@@ -62,7 +62,7 @@ def _workspace(lib, m: int, c: int, device) -> torch.Tensor:
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum: float, eps: float, act: int,
-                res_out: bool = False):
+                res_out: bool = False, add: torch.Tensor | None = None):
         lib = load_kernels()
         n, c, h, w = x.shape
         m = n * h * w
@@ -70,15 +70,25 @@ class _BNActFn(torch.autograd.Function):
         mean = torch.empty(c, dtype=torch.float32, device=x.device)
         invstd = torch.empty_like(mean)
         pb = _param_bf16(weight, bias, running_mean, running_var)
-        rc = lib.vgpu_bn_act_fwd_train(
-            _ptr(x), _ptr(y), _ptr(weight), _ptr(bias), _ptr(running_mean), _ptr(running_var),
-            _ptr(mean), _ptr(invstd), _ptr(_workspace(lib, m, c, x.device)), m, c, float(eps),
-            float(momentum), act, pb, _stream())
+        ws = _workspace(lib, m, c, x.device)
+        rc = -2
+        if add is not None:  # y = act(bn(x)) + add in the same pass when the plan has that form
+            rc = lib.vgpu_bn_act_fwd_train_add(
+                _ptr(x), _ptr(y), _ptr(weight), _ptr(bias), _ptr(running_mean), _ptr(running_var),
+                _ptr(mean), _ptr(invstd), _ptr(ws), m, c, float(eps), float(momentum), act, pb, _ptr(add),
+                _stream())
+        if rc == -2:
+            rc = lib.vgpu_bn_act_fwd_train(
+                _ptr(x), _ptr(y), _ptr(weight), _ptr(bias), _ptr(running_mean), _ptr(running_var),
+                _ptr(mean), _ptr(invstd), _ptr(ws), m, c, float(eps), float(momentum), act, pb, _stream())
+            if rc == 0 and add is not None:
+                y.add_(add)
         if rc != 0:
             raise RuntimeError(f"vgpu_bn_act_fwd_train: hipError {rc}")
         ctx.save_for_backward(x, weight, bias, mean, invstd)
         ctx.act = act
         ctx.pb = pb
+        ctx.has_add = add is not None
         if res_out:
             # x again, as an output of this node: the gradient it receives (an
             # identity shortcut's) is summed into dx by the backward kernel
@@ -104,7 +114,8 @@ class _BNActFn(torch.autograd.Function):
             _stream())
         if rc != 0:
             raise RuntimeError(f"vgpu_bn_act_bwd: hipError {rc}")
-        return dx, dw, db, None, None, None, None, None, None
+        dadd = dy if ctx.has_add and ctx.needs_input_grad[9] else None  # the shortcut's gradient is dy itself
+        return dx, dw, db, None, None, None, None, None, None, dadd
 
 
 def native_eligible(x: torch.Tensor, bn: nn.BatchNorm2d) -> bool:
@@ -145,13 +156,18 @@ def batched_step_counters():
                 torch._foreach_add_(pend, 1)
 
 
-def bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, act: str = "relu") -> torch.Tensor:
-    """act(bn(x)) with the module's own semantics (training statistics and
-    running-stat update in train mode, running stats in eval mode)."""
+def bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, act: str = "relu",
+           add: torch.Tensor | None = None) -> torch.Tensor:
+    """act(bn(x)) (+ add) with the module's own semantics (training statistics
+    and running-stat update in train mode, running stats in eval mode).  add:
+    an identity shortcut summed in the BN's own pass where the kernel plan
+    allows (one launch fewer per residual block)."""
     if act not in ACT:
         raise ValueError(act)
-    if not native_eligible(x, bn):
-        return _act(bn(x), act)
+    if not native_eligible(x, bn) or (add is not None and (add.shape != x.shape or add.dtype != x.dtype
+                                                           or not add.is_contiguous(memory_format=_CL))):
+        y = _act(bn(x), act)
+        return y if add is None else y + add
     track = bn.track_running_stats and bn.running_mean is not None
     if track:
         pend = getattr(_counters, "pending", None)
@@ -161,7 +177,7 @@ def bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, act: str = "relu") -> torch.Tens
             bn.num_batches_tracked.add_(1)
     return _BNActFn.apply(x, bn.weight, bn.bias, bn.running_mean if track else None,
                           bn.running_var if track else None, bn.momentum if track else 0.0,
-                          bn.eps, ACT[act])
+                          bn.eps, ACT[act], False, add)
 
 
 def bn_act_res(x: torch.Tensor, bn: nn.BatchNorm2d, act: str = "relu") -> tuple[torch.Tensor, torch.Tensor]:
