@@ -50,8 +50,12 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(uint16_t, b);
 }
-__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + __expf(-x)); }
-__device__ __forceinline__ float tanh_f(float x) { return 2.0f / (1.0f + __expf(-2.0f * x)) - 1.0f; }
+// v_exp_f32 + v_rcp_f32 (1 ulp): an IEEE division here is a ~10-instruction
+// div_scale / div_fmas / div_fixup sequence, and a step evaluates 40 of these
+// per lane on the recurrence's critical path.  Saturates correctly: exp -> inf
+// gives rcp -> 0.
+__device__ __forceinline__ float sigm(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ __forceinline__ float tanh_f(float x) { return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f; }
 
 struct FwdArgs {
   const uint16_t* xp;    // [T][B][4H] bf16 of this window (biases folded in)
