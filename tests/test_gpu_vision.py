@@ -315,14 +315,20 @@ def test_deeplab_fused_inference_matches_unfused(gpu_build):
         if isinstance(mod, torch.nn.BatchNorm2d):
             mod.running_mean.uniform_(-0.2, 0.2)
             mod.running_var.uniform_(0.5, 1.5)
+    m32 = copy.deepcopy(m).eval()
     m = m.to(torch.bfloat16).eval()
     x = _x((2, 3, 128, 128), 11)
     with torch.inference_mode():
         ref = m(x)
         m.fuse_for_inference()
         got = m(x)
-    print("deeplab fused rel", _rel(got, ref), "cos", _cos(got, ref))
+        # also against the fp32 model (eval-mode BN: running
+        # statistics, no batch-statistic amplification)
+        r32 = _torch_path(lambda: m32(x.float()))
+    print("deeplab fused rel", _rel(got, ref), "cos", _cos(got, ref), "vs fp32 rel", _rel(got, r32),
+          "cos", _cos(got, r32), "unfused bf16 vs fp32 rel", _rel(ref, r32))
     assert _cos(got, ref) > 0.999 and _rel(got, ref) < 0.05
+    assert _cos(got, r32) > 0.999 and _rel(got, r32) < 0.05
 
 
 def test_conv_relu6_epilogue_matches_fp32(gpu_build):
