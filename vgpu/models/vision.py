@@ -161,21 +161,24 @@ def _space_to_batch(x: torch.Tensor, d: int) -> torch.Tensor:
     """[N, C, H, W] -> [d·d·N, C, ⌈H/d⌉, ⌈W/d⌉]: sub-image (a, b) holds the
     pixels (a + d·i, b + d·j) (zero rows / columns past H, W), so a 3x3 conv
     with dilation d and padding d is a plain 3x3 / padding 1 conv on each
-    sub-image (TF's atrous convolution)."""
+    sub-image (TF's atrous convolution).  Channels-last in and out, one copy:
+    the permutation is taken on the NHWC storage itself."""
     n, c, h, w = x.shape
     hb, wb = -(-h // d), -(-w // d)
     if hb * d != h or wb * d != w:
         x = F.pad(x, (0, wb * d - w, 0, hb * d - h))
-    x = x.reshape(n, c, hb, d, wb, d).permute(3, 5, 0, 1, 2, 4).reshape(d * d * n, c, hb, wb)
-    return x.contiguous(memory_format=torch.channels_last)
+    xs = x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)  # NHWC view
+    xs = xs.reshape(n, hb, d, wb, d, c).permute(2, 4, 0, 1, 3, 5).contiguous()
+    return xs.view(d * d * n, hb, wb, c).permute(0, 3, 1, 2)
 
 
 def _batch_to_space(y: torch.Tensor, d: int, n: int, h: int, w: int) -> torch.Tensor:
     c, hb, wb = y.shape[1:]
-    y = y.reshape(d, d, n, c, hb, wb).permute(2, 3, 4, 0, 5, 1).reshape(n, c, hb * d, wb * d)
+    yp = y.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)  # NHWC view
+    yp = yp.reshape(d, d, n, hb, wb, c).permute(2, 3, 0, 4, 1, 5).contiguous().view(n, hb * d, wb * d, c)
     if hb * d != h or wb * d != w:
-        y = y[:, :, :h, :w]
-    return y.contiguous(memory_format=torch.channels_last)
+        yp = yp[:, :h, :w, :].contiguous()
+    return yp.permute(0, 3, 1, 2)
 
 
 def _atrous_conv(x: torch.Tensor, conv: nn.Conv2d, w: torch.Tensor | None = None,
