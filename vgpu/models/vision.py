@@ -145,6 +145,7 @@ class NativeVGG16Inference(nn.Module):
 
 
 _ATROUS = os.environ.get("VGPU_ATROUS", "1") != "0"  # VGPU_ATROUS=0: dilated convs on MIOpen (A/B)
+_ATROUS_INFER = os.environ.get("VGPU_ATROUS_INFER", "0") == "1"  # the BN-folded inference path too (A/B)
 
 
 def _atrous_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -232,6 +233,8 @@ class ConvBNAct(nn.Sequential):
         cl = x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)
         if cl and w9c is not None and dwconv.eligible(x, conv):
             return dwconv.dwconv3(x, w9c, conv.stride[0], conv.dilation[0], b, act)
+        if cl and _ATROUS_INFER and _atrous_ok(x, conv):
+            return _atrous_conv(x, conv, w, b, act)
         if (cl and conv.groups == 1 and conv.dilation == (1, 1) and conv.kernel_size[0] == conv.kernel_size[1]
                 and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
                 and C.supported(conv.in_channels, conv.out_channels, conv.kernel_size[0])
