@@ -91,10 +91,6 @@ def build_shim(sanitize: str | None = None, force: bool = False) -> Path:
 def build_smi(force: bool = False) -> Path:
     OUT.mkdir(parents=True, exist_ok=True)
     target = OUT / "libvgpu_smi.so"
-    if not (NATIVE / "smi" / "vgpu_smi.cpp").exists() and target.exists():
-        # a tree shipped without this source (the GPU pool's snapshot leaves it
-        # out, .gpurunignore): keep the library built beside it
-        return target
     srcs = sorted((NATIVE / "smi").glob("*.cpp"))
     inputs = srcs + sorted((NATIVE / "smi").glob("*.h")) + _headers()
     if not force and _stamp(target, inputs):
