@@ -269,6 +269,23 @@ def test_atrous_conv_space_to_batch_matches_fp32(gpu_build, case):
     assert _rel(yi, ri) < 2e-2
 
 
+@pytest.mark.parametrize("case", [(2, 21, 32, 32, 512, 512), (1, 256, 1, 1, 24, 24), (2, 64, 7, 9, 20, 30),
+                                  (1, 5, 24, 24, 384, 384), (1, 16, 40, 40, 13, 17)])
+def test_resize_bilinear_native_forward_matches_fp32(gpu_build, case):
+    """native/kernels/resize.hip (bf16 channels-last) against fp32
+    F.interpolate(bilinear, align_corners=False) of the same values: within
+    one bf16 rounding; and against PyTorch's own bf16 kernel."""
+    from vgpu.ops.interp import _forward
+    n, c, ih, iw, oh, ow = case
+    x = _x((n, c, ih, iw), 51)
+    y = _forward(x, (oh, ow))
+    assert y.is_contiguous(memory_format=CL) and y.shape == (n, c, oh, ow)
+    ref = torch.nn.functional.interpolate(x.float(), size=(oh, ow), mode="bilinear", align_corners=False)
+    torch.testing.assert_close(y.float(), ref, atol=1e-2, rtol=8e-3)
+    pt = torch.nn.functional.interpolate(x, size=(oh, ow), mode="bilinear", align_corners=False)
+    assert (y.float() - pt.float()).abs().max().item() <= 2 * 2 ** -7 * max(1.0, ref.abs().max().item())
+
+
 def test_resize_bilinear_backward_matches_pytorch(gpu_build):
     """The GEMM backward of the bilinear resize (vgpu.ops.interp) against
     PyTorch's atomic scatter, DeepLab's two shapes, fp32."""

@@ -8,14 +8,45 @@ the 4.2 training step (profiles/r5/train/prof_4_2_before.md).  The resize is
 separable and linear, y = A_h · x · A_wᵀ per (n, c), with A_h [OH, IH] and A_w
 [OW, IW] holding PyTorch's two interpolation weights per row, so
 dx = A_hᵀ · dy · A_w: two batched fp32 GEMMs (hipBLASLt), no atomics,
-deterministic.  The forward stays PyTorch's gather kernel.
+deterministic.  The forward of bf16 channels-last tensors runs on
+native/kernels/resize.hip (one thread per output pixel; PyTorch's NHWC kernel
+took 26 us per 4.1 logit upsample), PyTorch's kernel otherwise.
 """
 from __future__ import annotations
+
+import ctypes
+import os
 
 import torch
 import torch.nn.functional as F
 
 _MATS: dict[tuple, torch.Tensor] = {}
+_NATIVE = os.environ.get("VGPU_NATIVE_RESIZE", "1") != "0"  # =0: PyTorch's forward (A/B)
+_BOUND = False
+
+
+def _forward(x: torch.Tensor, size) -> torch.Tensor:
+    """F.interpolate(x, size, bilinear, align_corners=False); native for bf16
+    channels-last CUDA tensors."""
+    if not (_NATIVE and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last)):
+        return F.interpolate(x, size=size, mode="bilinear", align_corners=False)
+    global _BOUND
+    from vgpu.native import load_kernels
+    lib = load_kernels()
+    if not _BOUND:
+        vp, ci = ctypes.c_void_p, ctypes.c_int
+        lib.vgpu_resize_bilinear_nhwc.argtypes = [vp, vp] + [ci] * 6 + [vp]
+        lib.vgpu_resize_bilinear_nhwc.restype = ci
+        _BOUND = True
+    n, c, ih, iw = x.shape
+    oh, ow = size
+    y = torch.empty((n, c, oh, ow), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    rc = lib.vgpu_resize_bilinear_nhwc(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()), n, ih, iw, c,
+                                       oh, ow, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    if rc != 0:
+        raise RuntimeError(f"vgpu_resize_bilinear_nhwc: error {rc}")
+    return y
 
 
 def interp_matrix(out: int, inp: int, device) -> torch.Tensor:
@@ -43,7 +74,7 @@ class _ResizeFn(torch.autograd.Function):
     def forward(ctx, x, size):
         ctx.in_hw = tuple(x.shape[-2:])
         ctx.cl = x.is_contiguous(memory_format=torch.channels_last)
-        return F.interpolate(x, size=size, mode="bilinear", align_corners=False)
+        return _forward(x, size)
 
     @staticmethod
     def backward(ctx, dy):
@@ -60,5 +91,6 @@ def resize_bilinear(x: torch.Tensor, size) -> torch.Tensor:
     GEMM backward on CUDA tensors that need a gradient; PyTorch's otherwise."""
     size = tuple(int(s) for s in size)
     if not (x.is_cuda and x.requires_grad and torch.is_grad_enabled() and x.dim() == 4):
-        return F.interpolate(x, size=size, mode="bilinear", align_corners=False)
+        return _forward(x, size) if x.dim() == 4 else F.interpolate(x, size=size, mode="bilinear",
+                                                                     align_corners=False)
     return _ResizeFn.apply(x, size)
