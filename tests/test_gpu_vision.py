@@ -278,7 +278,7 @@ def test_resize_bilinear_native_forward_matches_fp32(gpu_build, case):
     from vgpu.ops.interp import _forward
     n, c, ih, iw, oh, ow = case
     x = _x((n, c, ih, iw), 51)
-    y = _forward(x, (oh, ow))
+    y = _forward(x, (oh, ow), native=True)
     assert y.is_contiguous(memory_format=CL) and y.shape == (n, c, oh, ow)
     ref = torch.nn.functional.interpolate(x.float(), size=(oh, ow), mode="bilinear", align_corners=False)
     torch.testing.assert_close(y.float(), ref, atol=1e-2, rtol=8e-3)

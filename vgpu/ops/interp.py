@@ -8,9 +8,10 @@ the 4.2 training step (profiles/r5/train/prof_4_2_before.md).  The resize is
 separable and linear, y = A_h · x · A_wᵀ per (n, c), with A_h [OH, IH] and A_w
 [OW, IW] holding PyTorch's two interpolation weights per row, so
 dx = A_hᵀ · dy · A_w: two batched fp32 GEMMs (hipBLASLt), no atomics,
-deterministic.  The forward of bf16 channels-last tensors runs on
-native/kernels/resize.hip (one thread per output pixel; PyTorch's NHWC kernel
-took 26 us per 4.1 logit upsample), PyTorch's kernel otherwise.
+deterministic.  The forward is PyTorch's gather kernel; with
+VGPU_NATIVE_RESIZE=1 bf16 channels-last tensors run on
+native/kernels/resize.hip instead (one thread per output pixel; PyTorch's NHWC
+kernel took 26 us per 4.1 logit upsample).
 """
 from __future__ import annotations
 
@@ -21,14 +22,15 @@ import torch
 import torch.nn.functional as F
 
 _MATS: dict[tuple, torch.Tensor] = {}
-_NATIVE = os.environ.get("VGPU_NATIVE_RESIZE", "1") != "0"  # =0: PyTorch's forward (A/B)
+# VGPU_NATIVE_RESIZE=1: the native forward (not yet measured on MI355X end to end, so off by default)
+_NATIVE = os.environ.get("VGPU_NATIVE_RESIZE", "0") == "1"
 _BOUND = False
 
 
-def _forward(x: torch.Tensor, size) -> torch.Tensor:
+def _forward(x: torch.Tensor, size, native: bool | None = None) -> torch.Tensor:
     """F.interpolate(x, size, bilinear, align_corners=False); native for bf16
-    channels-last CUDA tensors."""
-    if not (_NATIVE and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+    channels-last CUDA tensors when enabled (native=None: VGPU_NATIVE_RESIZE)."""
+    if not ((_NATIVE if native is None else native) and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
             and x.is_contiguous(memory_format=torch.channels_last)):
         return F.interpolate(x, size=size, mode="bilinear", align_corners=False)
     global _BOUND
