@@ -104,3 +104,26 @@ def test_deeplab_channel_padding_is_exact():
             mask = torch.ones_like(q, dtype=torch.bool)
             mask[tuple(slice(0, n) for n in p.shape)] = False
             assert float(q.detach()[mask].abs().max()) == 0.0, name
+
+
+def test_space_to_batch_dilated_conv_identity():
+    """DeepLab's ASPP training path (vgpu.models.vision._atrous_conv): a 3x3
+    conv with dilation = padding = d equals a plain 3x3 / padding 1 conv on the
+    d x d space-to-batch sub-images, for maps that d divides and maps it does
+    not (zero-padded up), channels-last in and out (fp32, CPU)."""
+    import torch
+    import torch.nn.functional as F
+    from vgpu.models.vision import _batch_to_space, _space_to_batch
+    g = torch.Generator().manual_seed(0)
+    for n, c, h, w, d in [(1, 8, 24, 24, 6), (2, 8, 24, 24, 12), (1, 8, 24, 24, 18), (2, 4, 32, 30, 18),
+                          (1, 4, 7, 9, 2)]:
+        x = torch.randn(n, c, h, w, generator=g).contiguous(memory_format=torch.channels_last)
+        wt = torch.randn(5, c, 3, 3, generator=g)
+        ref = F.conv2d(x, wt, padding=d, dilation=d)
+        xs = _space_to_batch(x, d)
+        assert xs.is_contiguous(memory_format=torch.channels_last)
+        assert xs.shape == (d * d * n, c, -(-h // d), -(-w // d))
+        y = F.conv2d(xs, wt, padding=1).contiguous(memory_format=torch.channels_last)
+        got = _batch_to_space(y, d, n, h, w)
+        assert got.is_contiguous(memory_format=torch.channels_last)
+        torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
